@@ -1,0 +1,129 @@
+// Shared device helpers for the gfx950 (CDNA4) kernel library.
+//
+// Conventions used by every kernel in csrc/kernels:
+//   * wave64 everywhere: lane = threadIdx.x & 63, reductions over 64 lanes.
+//   * bf16 is carried as raw `uint16_t` bits; all global traffic is
+//     vectorised to 16 B per lane (8 bf16) -- hipcc does not auto-vectorise
+//     bf16 scalar loads (cdna_hip_programming.md Guideline 13).
+//   * every launch entry point is `extern "C"` with raw pointers and a
+//     hipStream_t so Python can bind it with ctypes without pulling in torch
+//     headers, and so the launches are hipGraph-capturable (no malloc/sync).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#define KCA_API extern "C" __attribute__((visibility("default")))
+
+typedef uint16_t bf16_t;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+struct alignas(16) U16x8 { uint16_t v[8]; };
+struct alignas(8) U16x4 { uint16_t v[4]; };
+
+__device__ __forceinline__ float bf2f(uint16_t b) {
+  return __uint_as_float(((uint32_t)b) << 16);
+}
+
+// Round-to-nearest-even; plain cast lowers to v_cvt_pk_bf16_f32 on gfx950 and
+// keeps NaN a NaN (MI355X_MICROARCH.md "Correctness boundaries").
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  __bf16 h = (__bf16)f;
+  return __builtin_bit_cast(uint16_t, h);
+}
+
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+__device__ __forceinline__ void load8(const bf16_t* p, float (&x)[8]) {
+  U16x8 u = *reinterpret_cast<const U16x8*>(p);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) x[i] = bf2f(u.v[i]);
+}
+
+__device__ __forceinline__ void store8(bf16_t* p, const float (&x)[8]) {
+  U16x8 u;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) u.v[i] = f2bf(x[i]);
+  *reinterpret_cast<U16x8*>(p) = u;
+}
+
+__device__ __forceinline__ void load8f(const float* p, float (&x)[8]) {
+  float4 a = *reinterpret_cast<const float4*>(p);
+  float4 b = *reinterpret_cast<const float4*>(p + 4);
+  x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
+  x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+}
+
+__device__ __forceinline__ void store8f(float* p, const float (&x)[8]) {
+  *reinterpret_cast<float4*>(p) = make_float4(x[0], x[1], x[2], x[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(x[4], x[5], x[6], x[7]);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x a multiple of 64 (<= 1024). `red` must hold
+// blockDim.x/64 floats. Result broadcast to every thread.
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nw = blockDim.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < nw; ++i) t += red[i];
+  return t;
+}
+
+__device__ __forceinline__ float block_max(float v, float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nw = blockDim.x >> 6;
+  v = wave_max(v);
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float t = -INFINITY;
+  for (int i = 0; i < nw; ++i) t = fmaxf(t, red[i]);
+  return t;
+}
+
+// Grid size for memory-bound grid-stride kernels: enough blocks to fill 256 CUs
+// several times over, capped (cdna_hip_programming.md Guideline 11).
+static inline int kca_grid(long long work_items, int per_block, int cap = 2048) {
+  long long g = (work_items + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  float u = k0 * (x + k1 * x * x * x);
+  return 0.5f * x * (1.f + tanhf(u));
+}
+
+__device__ __forceinline__ float gelu_tanh_grad(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  float x2 = x * x;
+  float u = k0 * (x + k1 * x2 * x);
+  float t = tanhf(u);
+  float du = k0 * (1.f + 3.f * k1 * x2);
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * du;
+}

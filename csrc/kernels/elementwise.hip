@@ -1,0 +1,252 @@
+// Memory-bound elementwise kernels (K3 RoPE, K5 GELU, grad accumulation,
+// casts). All bf16 traffic is 16 B per lane; grids are grid-stride, capped at
+// ~2048 workgroups of 256 threads (cdna_hip_programming.md Guideline 11/13).
+#include "common.h"
+
+// ---------------------------------------------------------------- GELU
+// y = gelu(u), tanh approximation ("gelu_new"/"gelu_fast": GPT-J, GPT-2,
+// NeoX-20B, BLOOM) or exact erf ("gelu": Pythia). The bias add is fused into
+// the producing hipBLASLt GEMM epilogue (addmm), so the activation kernel only
+// needs the pre-activation.
+__device__ __forceinline__ float gelu_erf(float x) {
+  return 0.5f * x * (1.f + erff(x * 0.7071067811865476f));
+}
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+  const float cdf = 0.5f * (1.f + erff(x * 0.7071067811865476f));
+  const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+template <bool TANH>
+__global__ void gelu_fwd_kernel(const bf16_t* __restrict__ u,
+                                bf16_t* __restrict__ y, long long n8) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8;
+       i += (long long)gridDim.x * blockDim.x) {
+    float v[8];
+    load8(u + i * 8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = TANH ? gelu_tanh(v[j]) : gelu_erf(v[j]);
+    store8(y + i * 8, v);
+  }
+}
+
+template <bool TANH>
+__global__ void gelu_bwd_kernel(const bf16_t* __restrict__ dy,
+                                const bf16_t* __restrict__ u,
+                                bf16_t* __restrict__ du, long long n8) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8;
+       i += (long long)gridDim.x * blockDim.x) {
+    float g[8], v[8];
+    load8(dy + i * 8, g);
+    load8(u + i * 8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      v[j] = g[j] * (TANH ? gelu_tanh_grad(v[j]) : gelu_erf_grad(v[j]));
+    store8(du + i * 8, v);
+  }
+}
+
+KCA_API int kca_gelu_fwd(const void* u, void* y, long long n, int approx_tanh,
+                         hipStream_t stream) {
+  if (n % 8) return 1;
+  const long long n8 = n / 8;
+  if (approx_tanh)
+    hipLaunchKernelGGL(gelu_fwd_kernel<true>, dim3(kca_grid(n8, 256)), dim3(256), 0,
+                       stream, (const bf16_t*)u, (bf16_t*)y, n8);
+  else
+    hipLaunchKernelGGL(gelu_fwd_kernel<false>, dim3(kca_grid(n8, 256)), dim3(256), 0,
+                       stream, (const bf16_t*)u, (bf16_t*)y, n8);
+  return 0;
+}
+
+KCA_API int kca_gelu_bwd(const void* dy, const void* u, void* du, long long n,
+                         int approx_tanh, hipStream_t stream) {
+  if (n % 8) return 1;
+  const long long n8 = n / 8;
+  if (approx_tanh)
+    hipLaunchKernelGGL(gelu_bwd_kernel<true>, dim3(kca_grid(n8, 256)), dim3(256), 0,
+                       stream, (const bf16_t*)dy, (const bf16_t*)u, (bf16_t*)du, n8);
+  else
+    hipLaunchKernelGGL(gelu_bwd_kernel<false>, dim3(kca_grid(n8, 256)), dim3(256), 0,
+                       stream, (const bf16_t*)dy, (const bf16_t*)u, (bf16_t*)du, n8);
+  return 0;
+}
+
+// ---------------------------------------------------------------- RoPE
+// In-place rotary embedding on the first `rot` dims of every head of a
+// [tokens, heads, head_dim] view with arbitrary token/head strides (so it runs
+// directly on the fused QKV GEMM output). cos/sin tables are precomputed on the
+// host, [max_pos, rot/2] fp32 (Appendix B "trig-heavy ops": no device trig).
+//   interleaved=1 : GPT-J "rotate_every_two", pairs (2i, 2i+1)
+//   interleaved=0 : GPT-NeoX/Pythia "rotate_half", pairs (i, i + rot/2)
+// sign=+1 forward rotation, sign=-1 the transpose (used by the backward).
+// Each thread rotates 4 pairs (8 elements).
+__global__ void rope_kernel(bf16_t* __restrict__ q, bf16_t* __restrict__ k,
+                            int nh_q, int nh_k, long long tokens, int seq,
+                            long long tok_stride_q, long long head_stride_q,
+                            long long tok_stride_k, long long head_stride_k,
+                            int rot, int interleaved,
+                            const float* __restrict__ cos_t,
+                            const float* __restrict__ sin_t,
+                            const int* __restrict__ pos_ids, float sign) {
+  const int half = rot >> 1;
+  const int groups = half >> 2;  // 4 pairs per thread
+  const int nh = nh_q + nh_k;
+  const long long total = tokens * nh * groups;
+  for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+       idx < total; idx += (long long)gridDim.x * blockDim.x) {
+    const int g = idx % groups;
+    const long long th = idx / groups;
+    const int hh = th % nh;
+    const long long t = th / nh;
+    const int pos = pos_ids ? pos_ids[t] : (int)(t % seq);
+    bf16_t* base = hh < nh_q ? q + t * tok_stride_q + hh * head_stride_q
+                             : k + t * tok_stride_k + (hh - nh_q) * head_stride_k;
+    const float* ct = cos_t + (size_t)pos * half + g * 4;
+    const float* st = sin_t + (size_t)pos * half + g * 4;
+    float c[4], s[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { c[j] = ct[j]; s[j] = sign * st[j]; }
+    if (interleaved) {
+      float x[8];
+      load8(base + g * 8, x);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float a = x[2 * j], b = x[2 * j + 1];
+        x[2 * j] = a * c[j] - b * s[j];
+        x[2 * j + 1] = b * c[j] + a * s[j];
+      }
+      store8(base + g * 8, x);
+    } else {
+      U16x4 ua = *reinterpret_cast<const U16x4*>(base + g * 4);
+      U16x4 ub = *reinterpret_cast<const U16x4*>(base + half + g * 4);
+      U16x4 oa, ob;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float a = bf2f(ua.v[j]), b = bf2f(ub.v[j]);
+        oa.v[j] = f2bf(a * c[j] - b * s[j]);
+        ob.v[j] = f2bf(b * c[j] + a * s[j]);
+      }
+      *reinterpret_cast<U16x4*>(base + g * 4) = oa;
+      *reinterpret_cast<U16x4*>(base + half + g * 4) = ob;
+    }
+  }
+}
+
+// One pair per thread: rot/2 not a multiple of 4 (Pythia-2.8B: rot = 20).
+__global__ void rope_scalar_kernel(bf16_t* __restrict__ q,
+                                   bf16_t* __restrict__ k, int nh_q, int nh_k,
+                                   long long tokens, int seq,
+                                   long long tok_stride_q,
+                                   long long head_stride_q,
+                                   long long tok_stride_k,
+                                   long long head_stride_k, int rot,
+                                   int interleaved,
+                                   const float* __restrict__ cos_t,
+                                   const float* __restrict__ sin_t,
+                                   const int* __restrict__ pos_ids,
+                                   float sign) {
+  const int half = rot >> 1;
+  const int nh = nh_q + nh_k;
+  const long long total = tokens * nh * half;
+  for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+       idx < total; idx += (long long)gridDim.x * blockDim.x) {
+    const int i = idx % half;
+    const long long th = idx / half;
+    const int hh = th % nh;
+    const long long t = th / nh;
+    const int pos = pos_ids ? pos_ids[t] : (int)(t % seq);
+    bf16_t* base = hh < nh_q ? q + t * tok_stride_q + hh * head_stride_q
+                             : k + t * tok_stride_k + (hh - nh_q) * head_stride_k;
+    const float c = cos_t[(size_t)pos * half + i];
+    const float s = sign * sin_t[(size_t)pos * half + i];
+    const int ia = interleaved ? 2 * i : i;
+    const int ib = interleaved ? 2 * i + 1 : i + half;
+    const float a = bf2f(base[ia]), b = bf2f(base[ib]);
+    base[ia] = f2bf(a * c - b * s);
+    base[ib] = f2bf(b * c + a * s);
+  }
+}
+
+KCA_API int kca_rope(void* q, void* k, int nh_q, int nh_k, long long tokens,
+                     int seq, long long tok_stride_q, long long head_stride_q,
+                     long long tok_stride_k, long long head_stride_k, int rot,
+                     int interleaved, const float* cos_t, const float* sin_t,
+                     const int* pos_ids, float sign, hipStream_t stream) {
+  if (rot % 2) return 1;
+  if (rot % 8) {
+    const long long total = tokens * (nh_q + nh_k) * (rot / 2);
+    hipLaunchKernelGGL(rope_scalar_kernel, dim3(kca_grid(total, 256)),
+                       dim3(256), 0, stream, (bf16_t*)q, (bf16_t*)k, nh_q,
+                       nh_k, tokens, seq, tok_stride_q, head_stride_q,
+                       tok_stride_k, head_stride_k, rot, interleaved, cos_t,
+                       sin_t, pos_ids, sign);
+    return 0;
+  }
+  const long long total = tokens * (nh_q + nh_k) * (rot / 8);
+  hipLaunchKernelGGL(rope_kernel, dim3(kca_grid(total, 256)), dim3(256), 0,
+                     stream, (bf16_t*)q, (bf16_t*)k, nh_q, nh_k, tokens, seq,
+                     tok_stride_q, head_stride_q, tok_stride_k, head_stride_k,
+                     rot, interleaved, cos_t, sin_t, pos_ids, sign);
+  return 0;
+}
+
+// ---------------------------------------------------------------- grads
+// main_grad (fp32) += grad (bf16) * scale   -- fp32 gradient accumulation across
+// micro-batches (DeepSpeed/Megatron keep grads in fp32 for bf16 training).
+__global__ void accum_grad_kernel(float* __restrict__ acc,
+                                  const bf16_t* __restrict__ g, float scale,
+                                  int overwrite, long long n8) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8;
+       i += (long long)gridDim.x * blockDim.x) {
+    float v[8], a[8];
+    load8(g + i * 8, v);
+    if (overwrite) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] = v[j] * scale;
+    } else {
+      load8f(acc + i * 8, a);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] += v[j] * scale;
+    }
+    store8f(acc + i * 8, a);
+  }
+}
+
+__global__ void accum_grad_tail_kernel(float* acc, const bf16_t* g, float scale,
+                                       int overwrite, long long start,
+                                       long long n) {
+  long long i = start + blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (i < n) acc[i] = (overwrite ? 0.f : acc[i]) + bf2f(g[i]) * scale;
+}
+
+KCA_API int kca_accum_grad(float* acc, const void* g, float scale,
+                           int overwrite, long long n, hipStream_t stream) {
+  const long long n8 = n / 8;
+  if (n8)
+    hipLaunchKernelGGL(accum_grad_kernel, dim3(kca_grid(n8, 256)), dim3(256),
+                       0, stream, acc, (const bf16_t*)g, scale, overwrite, n8);
+  if (n % 8)
+    hipLaunchKernelGGL(accum_grad_tail_kernel, dim3(1), dim3(64), 0, stream,
+                       acc, (const bf16_t*)g, scale, overwrite, n8 * 8, n);
+  return 0;
+}
+
+// fp32 -> bf16 cast (master -> model copy, ZeRO all-gather staging).
+__global__ void cast_f32_bf16_kernel(const float* __restrict__ x,
+                                     bf16_t* __restrict__ y, long long n8) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8;
+       i += (long long)gridDim.x * blockDim.x) {
+    float v[8];
+    load8f(x + i * 8, v);
+    store8(y + i * 8, v);
+  }
+}
+
+KCA_API int kca_cast_f32_bf16(const float* x, void* y, long long n,
+                              hipStream_t stream) {
+  if (n % 8) return 1;
+  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(kca_grid(n / 8, 256)),
+                     dim3(256), 0, stream, x, (bf16_t*)y, n / 8);
+  return 0;
+}

@@ -1,0 +1,133 @@
+"""ctypes binding of the in-tree gfx950 kernel library (``_lib/libkca_kernels.so``).
+
+The library is a plain C-ABI shared object built by ``tools/build_ext.py``
+(``hipcc --offload-arch=gfx950``). It is loaded *after* ``import torch`` so the
+kernels register with the HIP runtime torch already mapped; every launch takes
+the current torch stream, so launches are ordered with torch's own work and
+are captured by ``torch.cuda.graphs`` like any other kernel.
+
+Policy: GPU tensors always go through the native kernels. If the library is
+missing on a machine with a GPU the ops raise (``require()``) instead of
+silently falling back to eager PyTorch -- CPU tensors use the reference
+implementations in each op module (that is what the CPU test-suite runs).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(os.path.dirname(_HERE), "_lib")
+KERNEL_LIB = os.path.join(LIB_DIR, "libkca_kernels.so")
+
+_lock = threading.Lock()
+_lib = None
+_err: str | None = None
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+LL = ctypes.c_longlong
+F = ctypes.c_float
+
+# name -> argtypes (restype is always int status, 0 == ok)
+_SIGS = {
+    "kca_layernorm_fwd": [P, P, P, P, P, P, P, P, P, I, I, F, P],
+    "kca_layernorm_bwd_parts": [I],
+    "kca_layernorm_bwd": [P, P, P, P, P, P, P, P, P, I, P, I, I, P],
+    "kca_gelu_fwd": [P, P, LL, I, P],
+    "kca_gelu_bwd": [P, P, P, LL, I, P],
+    "kca_rope": [P, P, I, I, LL, I, LL, LL, LL, LL, I, I, P, P, P, F, P],
+    "kca_accum_grad": [P, P, F, I, LL, P],
+    "kca_cast_f32_bf16": [P, P, LL, P],
+    "kca_cross_entropy_fwd": [P, LL, P, I, I, I, P, P, P],
+    "kca_cross_entropy_bwd": [P, LL, P, P, P, F, I, I, I, P, LL, P],
+    "kca_adamw": [P, P, P, P, P, LL, LL, F, F, F, F, F, F, F, P, P, P],
+    "kca_sumsq": [P, LL, P, P, P],
+    "kca_clip_coef": [P, F, F, P, P, P, P],
+    "kca_attn_fwd": [P] * 5 + [LL] * 12 + [I] * 7 + [F, P, P, I, P],
+    "kca_attn_bwd_preprocess": [P, P, P, LL, LL, LL, LL, LL, LL, I, I, I, I, P],
+    "kca_attn_bwd": [P] * 10 + [LL] * 21 + [I] * 7 + [F, P, P, P],
+    "kca_groupnorm_fwd": [P, P, P, P, P, P, I, I, I, I, F, I, P],
+    "kca_groupnorm_bwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P],
+    "kca_sample_logits": [P, LL, I, I, P, P, P, P, P, P, P, P, P, I, P],
+    "kca_decode_attn": [P] * 6 + [LL] * 8 + [I] * 7 + [F, P, P],
+}
+
+
+def _load():
+    global _lib, _err
+    if _lib is not None or _err is not None:
+        return _lib
+    with _lock:
+        if _lib is not None or _err is not None:
+            return _lib
+        if not os.path.exists(KERNEL_LIB):
+            _err = f"{KERNEL_LIB} not built (run `python tools/build_ext.py`)"
+            return None
+        try:
+            lib = ctypes.CDLL(KERNEL_LIB, mode=ctypes.RTLD_GLOBAL)
+        except OSError as e:  # pragma: no cover - depends on the box
+            _err = f"failed to load {KERNEL_LIB}: {e}"
+            return None
+        for name, argtypes in _SIGS.items():
+            fn = getattr(lib, name, None)
+            if fn is None:
+                continue
+            fn.argtypes = argtypes
+            fn.restype = ctypes.c_int
+        _lib = lib
+        return _lib
+
+
+def available() -> bool:
+    return _load() is not None
+
+
+def require():
+    lib = _load()
+    if lib is None:
+        raise RuntimeError(
+            "kubernetes_cloud_amd native kernels unavailable: " + str(_err)
+            + " -- refusing to fall back to eager PyTorch on a GPU tensor")
+    return lib
+
+
+def has(name: str) -> bool:
+    lib = _load()
+    return lib is not None and hasattr(lib, name)
+
+
+def call(name: str, *args):
+    lib = require()
+    fn = getattr(lib, name)
+    rc = fn(*args)
+    if rc != 0:
+        raise RuntimeError(f"{name} returned status {rc} (unsupported shape/arguments)")
+    return rc
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def use_native(*tensors: torch.Tensor | None) -> bool:
+    """True when the op must run on the native HIP path.
+
+    Native kernels are bf16; a GPU tensor of another dtype (fp32 debugging runs)
+    uses the reference math. bf16 GPU tensors never fall back: a missing
+    library raises in ``call``.
+    """
+    on_gpu = False
+    for t in tensors:
+        if t is not None and t.is_cuda:
+            on_gpu = True
+            if t.dtype != torch.bfloat16:
+                return False
+    return on_gpu

@@ -1,0 +1,46 @@
+"""Activation ops: tanh-GELU (GPT-J/NeoX/BLOOM/GPT-2 "gelu_new") and GEGLU."""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+
+
+class _GeluFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, u, approx):
+        u = u.contiguous()
+        y = torch.empty_like(u)
+        _lib.call("kca_gelu_fwd", u.data_ptr(), y.data_ptr(), u.numel(), int(approx), _lib.stream())
+        ctx.save_for_backward(u)
+        ctx.approx = approx
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (u,) = ctx.saved_tensors
+        du = torch.empty_like(u)
+        _lib.call("kca_gelu_bwd", dy.contiguous().data_ptr(), u.data_ptr(), du.data_ptr(),
+                  u.numel(), int(ctx.approx), _lib.stream())
+        return du, None
+
+
+def gelu(u: torch.Tensor, approximate: str = "tanh") -> torch.Tensor:
+    """GELU of the pre-activation ``u`` (bias already added by the GEMM
+    epilogue); ``approximate`` is "tanh" (gelu_new / gelu_fast) or "none" (erf)."""
+    approx = approximate == "tanh"
+    if _lib.use_native(u) and u.numel() % 8 == 0:
+        return _GeluFn.apply(u, approx)
+    return F.gelu(u.float(), approximate="tanh" if approx else "none").to(u.dtype)
+
+
+def quick_gelu(x: torch.Tensor) -> torch.Tensor:
+    """CLIP's x * sigmoid(1.702 x)."""
+    return x * torch.sigmoid(1.702 * x)
+
+
+def geglu(x: torch.Tensor) -> torch.Tensor:
+    """diffusers GEGLU: split the projection in half, value * gelu(gate) (exact erf)."""
+    a, g = x.chunk(2, dim=-1)
+    return a * F.gelu(g.float()).to(a.dtype)

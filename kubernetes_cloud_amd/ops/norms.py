@@ -1,0 +1,132 @@
+"""LayerNorm (+ fused residual adds) and GroupNorm(+SiLU) autograd ops.
+
+GPU tensors run ``csrc/kernels/layernorm.hip`` / ``groupnorm.hip``; CPU tensors
+run the fp32 PyTorch reference below (the numerics the kernel tests compare
+against).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+
+
+def _ln_ref(h: torch.Tensor, w, b, eps):
+    return F.layer_norm(h.float(), (h.shape[-1],), w.float() if w is not None else None,
+                        b.float() if b is not None else None, eps).to(h.dtype)
+
+
+class _LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps, r1, r2):
+        d = x.shape[-1]
+        rows = x.numel() // d
+        x2 = x.contiguous()
+        has_res = r1 is not None
+        h = torch.empty_like(x2) if has_res else None
+        y = torch.empty_like(x2)
+        mean = torch.empty(rows, device=x.device, dtype=torch.float32)
+        rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
+        _lib.call("kca_layernorm_fwd", x2.data_ptr(), _lib.ptr(r1.contiguous() if r1 is not None else None),
+                  _lib.ptr(r2.contiguous() if r2 is not None else None), _lib.ptr(h),
+                  weight.data_ptr(), _lib.ptr(bias), y.data_ptr(), mean.data_ptr(),
+                  rstd.data_ptr(), rows, d, float(eps), _lib.stream())
+        ctx.save_for_backward(h if has_res else x2, weight, mean, rstd)
+        ctx.has_bias = bias is not None
+        ctx.has_res = has_res
+        ctx.n_res = (r1 is not None) + (r2 is not None)
+        if has_res:
+            return y, h
+        return y, None
+
+    @staticmethod
+    def backward(ctx, dy, dh):
+        h, weight, mean, rstd = ctx.saved_tensors
+        d = h.shape[-1]
+        rows = h.numel() // d
+        dy = dy.contiguous()
+        dx = torch.empty_like(h)
+        parts = _lib.require().kca_layernorm_bwd_parts(rows)
+        ws = torch.empty(2 * parts * d, device=h.device, dtype=torch.float32)
+        dw = torch.empty_like(weight)
+        db = torch.empty_like(weight) if ctx.has_bias else None
+        dres = dh.contiguous() if (ctx.has_res and dh is not None) else None
+        _lib.call("kca_layernorm_bwd", dy.data_ptr(), h.data_ptr(), mean.data_ptr(),
+                  rstd.data_ptr(), weight.data_ptr(), _lib.ptr(dres), dx.data_ptr(),
+                  dw.data_ptr(), _lib.ptr(db), int(weight.dtype == torch.float32),
+                  ws.data_ptr(), rows, d, _lib.stream())
+        g1 = dx if ctx.n_res >= 1 else None
+        g2 = dx if ctx.n_res >= 2 else None
+        return dx, dw, db, None, g1, g2
+
+
+def layer_norm(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None,
+               eps: float = 1e-5, residual: tuple = ()):
+    """LayerNorm over the last dim, optionally of ``x + sum(residual)``.
+
+    Returns ``y`` when ``residual`` is empty, else ``(y, h)`` with
+    ``h = x + sum(residual)`` (the new residual stream, stored once).
+    """
+    r1 = residual[0] if len(residual) > 0 else None
+    r2 = residual[1] if len(residual) > 1 else None
+    if len(residual) > 2:
+        raise ValueError("at most two fused residual adds")
+    if _lib.use_native(x):
+        y, h = _LayerNormFn.apply(x, weight, bias, eps, r1, r2)
+        return (y, h) if residual else y
+    h = x
+    for r in residual:
+        h = h + r
+    y = _ln_ref(h, weight, bias, eps)
+    return (y, h) if residual else y
+
+
+# ------------------------------------------------------------------ GroupNorm
+class _GroupNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, groups, eps, silu):
+        # x: [N, C, *spatial] contiguous (NCHW) bf16
+        x = x.contiguous()
+        n, c = x.shape[0], x.shape[1]
+        hw = x.numel() // (n * c)
+        y = torch.empty_like(x)
+        mean = torch.empty(n * groups, device=x.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        _lib.call("kca_groupnorm_fwd", x.data_ptr(), weight.data_ptr(), _lib.ptr(bias),
+                  y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), n, c, hw, groups,
+                  float(eps), int(silu), _lib.stream())
+        ctx.save_for_backward(x, weight, bias, mean, rstd)
+        ctx.groups, ctx.silu = groups, silu
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, bias, mean, rstd = ctx.saved_tensors
+        n, c = x.shape[0], x.shape[1]
+        hw = x.numel() // (n * c)
+        dy = dy.contiguous()
+        dx = torch.empty_like(x)
+        dw = torch.empty_like(weight)
+        db = torch.empty_like(weight)
+        ws = torch.empty(2 * n * c, device=x.device, dtype=torch.float32)
+        _lib.call("kca_groupnorm_bwd", dy.data_ptr(), x.data_ptr(), weight.data_ptr(),
+                  _lib.ptr(bias), mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(),
+                  dw.data_ptr(), db.data_ptr(), ws.data_ptr(), n, c, hw, ctx.groups,
+                  int(ctx.silu), _lib.stream())
+        return dx, dw, (db if bias is not None else None), None, None, None
+
+
+def group_norm(x: torch.Tensor, groups: int, weight: torch.Tensor, bias: torch.Tensor | None,
+               eps: float = 1e-5, silu: bool = False) -> torch.Tensor:
+    """GroupNorm over NC* tensors, optionally fused with SiLU (UNet/VAE ResNet blocks)."""
+    if _lib.use_native(x) and x.dtype == torch.bfloat16 and _lib.has("kca_groupnorm_fwd"):
+        return _GroupNormFn.apply(x, weight, bias, groups, eps, silu)
+    if _lib.use_native(x) and x.dtype == torch.bfloat16:
+        _lib.require()
+        raise RuntimeError("kca_groupnorm_fwd missing from the kernel library")
+    y = F.group_norm(x.float(), groups, weight.float() if weight is not None else None,
+                     bias.float() if bias is not None else None, eps)
+    if silu:
+        y = F.silu(y)
+    return y.to(x.dtype)

@@ -1,0 +1,171 @@
+"""Flat-buffer AdamW (K7), LR schedules (K8) and dynamic loss scaling (K9).
+
+Mirrors the optimizer semantics the reference configures through DeepSpeed /
+HF (finetuner-workflow/finetuner/ds_config.json:10-26: AdamW, WarmupLR;
+finetuner.py:987-1027: weight_decay, warmup_ratio, linear decay) and the SD
+trainer (sd-finetuner/finetuner.py:680-686, 751: AdamW + get_scheduler), but
+runs as ONE fused HIP launch over contiguous fp32 buffers:
+
+    master  fp32 [n]   (the ZeRO shard of a rank is a slice of it)
+    grad    fp32 [n]   (micro-batch grads accumulated here in fp32)
+    exp_avg, exp_avg_sq fp32 [n]
+    model_bf16  bf16 [n] (optional: written in the same pass)
+
+The global grad-norm clip and the 1/loss_scale unscale are a device scalar the
+kernel reads, so the step never synchronises with the host.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ..ops import _lib
+
+
+class FlatAdamW:
+    def __init__(self, master: torch.Tensor, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 0.0, n_decay: int | None = None,
+                 model_bf16: torch.Tensor | None = None, grad: torch.Tensor | None = None):
+        assert master.dtype == torch.float32 and master.dim() == 1
+        self.master = master
+        self.grad = grad if grad is not None else torch.zeros_like(master)
+        self.exp_avg = torch.zeros_like(master)
+        self.exp_avg_sq = torch.zeros_like(master)
+        self.model_bf16 = model_bf16
+        self.lr = lr
+        self.betas = betas
+        self.eps = eps
+        self.weight_decay = weight_decay
+        self.n_decay = master.numel() if n_decay is None else n_decay
+        self.step_count = 0
+        dev = master.device
+        self._coef = torch.ones(1, device=dev, dtype=torch.float32)
+        self._sumsq = torch.zeros(1, device=dev, dtype=torch.float32)
+        self._norm = torch.zeros(1, device=dev, dtype=torch.float32)
+        self._skip = torch.zeros(1, device=dev, dtype=torch.int32)
+        self._ws = torch.empty(1024, device=dev, dtype=torch.float32)
+        self.native = master.is_cuda
+        if self.native:
+            assert master.numel() % 4 == 0, "pad flat buffers to a multiple of 4"
+            _lib.require()
+
+    # -- grad norm -------------------------------------------------------
+    def local_sumsq(self) -> torch.Tensor:
+        """Sum of squares of this rank's grad slice (device scalar, no sync)."""
+        if self.native:
+            _lib.call("kca_sumsq", self.grad.data_ptr(), self.grad.numel(), self._ws.data_ptr(),
+                      self._sumsq.data_ptr(), _lib.stream())
+        else:
+            self._sumsq.copy_(self.grad.float().pow(2).sum().view(1))
+        return self._sumsq
+
+    def set_clip(self, sumsq: torch.Tensor, max_norm: float, inv_loss_scale: float = 1.0):
+        """coef = min(1, max_norm/||g||) / loss_scale; skip if non-finite."""
+        if self.native:
+            _lib.call("kca_clip_coef", sumsq.data_ptr(), float(max_norm), float(inv_loss_scale),
+                      self._coef.data_ptr(), self._norm.data_ptr(), self._skip.data_ptr(),
+                      _lib.stream())
+        else:
+            nrm = sumsq.sqrt() * inv_loss_scale
+            c = torch.full_like(nrm, inv_loss_scale)
+            if max_norm > 0:
+                c = torch.where(nrm > max_norm, c * max_norm / (nrm + 1e-6), c)
+            self._coef.copy_(c)
+            self._norm.copy_(nrm)
+            self._skip.copy_((~torch.isfinite(sumsq)).int())
+
+    @property
+    def grad_norm(self) -> torch.Tensor:
+        return self._norm
+
+    @property
+    def skipped(self) -> torch.Tensor:
+        return self._skip
+
+    # -- update ------------------------------------------------------------
+    def step(self, lr: float | None = None, use_clip: bool = False):
+        if lr is not None:
+            self.lr = lr
+        self.step_count += 1
+        b1, b2 = self.betas
+        bc1 = 1.0 - b1 ** self.step_count
+        bc2 = 1.0 - b2 ** self.step_count
+        if self.native:
+            _lib.call("kca_adamw", self.master.data_ptr(), self.grad.data_ptr(), self.exp_avg.data_ptr(),
+                      self.exp_avg_sq.data_ptr(), _lib.ptr(self.model_bf16), self.master.numel(),
+                      self.n_decay, float(self.lr), float(b1), float(b2), float(self.eps),
+                      float(self.weight_decay), float(bc1), float(bc2),
+                      self._coef.data_ptr() if use_clip else None,
+                      self._skip.data_ptr() if use_clip else None, _lib.stream())
+            return
+        if use_clip and bool(self._skip.item()):
+            return
+        g = self.grad * (self._coef if use_clip else 1.0)
+        self.exp_avg.mul_(b1).add_(g, alpha=1 - b1)
+        self.exp_avg_sq.mul_(b2).addcmul_(g, g, value=1 - b2)
+        denom = (self.exp_avg_sq.sqrt() / math.sqrt(bc2)).add_(self.eps)
+        if self.weight_decay and self.n_decay:
+            self.master[: self.n_decay].mul_(1 - self.lr * self.weight_decay)
+        self.master.addcdiv_(self.exp_avg, denom, value=-self.lr / bc1)
+        if self.model_bf16 is not None:
+            self.model_bf16.copy_(self.master)
+
+    def state_dict(self):
+        return {"exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq, "step": self.step_count,
+                "lr": self.lr, "betas": list(self.betas), "eps": self.eps,
+                "weight_decay": self.weight_decay}
+
+    def load_state_dict(self, sd):
+        self.exp_avg.copy_(sd["exp_avg"])
+        self.exp_avg_sq.copy_(sd["exp_avg_sq"])
+        self.step_count = int(sd["step"])
+        self.lr = sd.get("lr", self.lr)
+
+
+# ----------------------------------------------------------------- schedules
+def lr_at(step: int, base_lr: float, total_steps: int, warmup_steps: int, kind: str = "linear",
+          min_lr: float = 0.0) -> float:
+    """HF-style schedules: warmup then linear / cosine / constant decay.
+
+    ``kind='warmup'`` reproduces DeepSpeed WarmupLR (ds_config.json:19-26):
+    linear warmup to ``base_lr`` then constant.
+    """
+    if warmup_steps > 0 and step < warmup_steps:
+        return base_lr * float(step) / float(max(1, warmup_steps))
+    if kind in ("constant", "warmup", "constant_with_warmup"):
+        return base_lr
+    progress = float(step - warmup_steps) / float(max(1, total_steps - warmup_steps))
+    progress = min(max(progress, 0.0), 1.0)
+    if kind == "cosine":
+        return min_lr + (base_lr - min_lr) * 0.5 * (1.0 + math.cos(math.pi * progress))
+    return max(0.0, base_lr * (1.0 - progress))
+
+
+class DynamicLossScaler:
+    """fp16 dynamic loss scale (ds_config.json:2-9: initial 2^16, window 1000,
+    hysteresis 2, min 1)."""
+
+    def __init__(self, init_scale: float = 2.0 ** 16, window: int = 1000, hysteresis: int = 2,
+                 min_scale: float = 1.0, enabled: bool = True):
+        self.scale = init_scale if enabled else 1.0
+        self.window = window
+        self.hysteresis = hysteresis
+        self._hyst = hysteresis
+        self.min_scale = min_scale
+        self.enabled = enabled
+        self._good = 0
+
+    def update(self, overflow: bool):
+        if not self.enabled:
+            return
+        if overflow:
+            self._hyst -= 1
+            if self._hyst <= 0:
+                self.scale = max(self.min_scale, self.scale / 2.0)
+                self._hyst = self.hysteresis
+            self._good = 0
+        else:
+            self._good += 1
+            if self._good % self.window == 0:
+                self.scale *= 2.0

@@ -1,0 +1,172 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference of the same op."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from kubernetes_cloud_amd import ops
+from kubernetes_cloud_amd.ops import _lib
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def test_native_library_loaded():
+    assert _lib.available(), _lib._err
+
+
+@pytest.mark.parametrize("d", [768, 2560, 4096, 14336])
+@pytest.mark.parametrize("nres", [0, 2])
+def test_layernorm(d, nres):
+    torch.manual_seed(0)
+    rows = 257
+    x = torch.randn(rows, d, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    res = [torch.randn(rows, d, device=DEV, dtype=torch.bfloat16, requires_grad=True) for _ in range(nres)]
+    w = (1 + 0.1 * torch.randn(d, device=DEV)).bfloat16().requires_grad_()
+    b = (0.1 * torch.randn(d, device=DEV)).bfloat16().requires_grad_()
+    out = ops.layer_norm(x, w, b, 1e-5, residual=tuple(res))
+    y, h = (out if nres else (out, None))
+    # reference
+    xr = x.detach().float().requires_grad_()
+    rr = [r.detach().float().requires_grad_() for r in res]
+    wr, br = w.detach().float().requires_grad_(), b.detach().float().requires_grad_()
+    hr = xr
+    for r in rr:
+        hr = hr + r
+    yr = F.layer_norm(hr.bfloat16().float() if nres else hr, (d,), wr, br, 1e-5)
+    assert _rel(y, yr) < 1e-2
+    gy = torch.randn_like(y)
+    if nres:
+        gh = torch.randn_like(h)
+        torch.autograd.backward([y, h], [gy, gh])
+        torch.autograd.backward([yr, hr], [gy.float(), gh.float()])
+    else:
+        y.backward(gy)
+        yr.backward(gy.float())
+    assert _rel(x.grad, xr.grad) < 2e-2
+    assert _rel(w.grad, wr.grad) < 2e-2
+    assert _rel(b.grad, br.grad) < 2e-2
+    for r, rref in zip(res, rr):
+        assert _rel(r.grad, rref.grad) < 2e-2
+
+
+def test_gelu():
+    u = torch.randn(4096, 1024, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    y = ops.gelu(u)
+    ur = u.detach().float().requires_grad_()
+    yr = F.gelu(ur, approximate="tanh")
+    assert _rel(y, yr) < 1e-2
+    g = torch.randn_like(y)
+    y.backward(g)
+    yr.backward(g.float())
+    assert _rel(u.grad, ur.grad) < 1e-2
+
+
+@pytest.mark.parametrize("interleaved,D,rot", [(True, 256, 64), (False, 80, 20), (False, 96, 24), (False, 128, 128)])
+def test_rope(interleaved, D, rot):
+    B, S, H = 2, 64, 4
+    x = torch.randn(B, S, 3, H, D, device=DEV, dtype=torch.bfloat16)
+    ref_q = ops.rotary_reference(x[:, :, 0].float(), rot, interleaved)
+    ref_k = ops.rotary_reference(x[:, :, 1].float(), rot, interleaved)
+    y = x.clone()
+    q, k = y[:, :, 0], y[:, :, 1]
+    ops.apply_rotary_(q, k, rot, S, interleaved)
+    assert _rel(q, ref_q) < 1e-2 and _rel(k, ref_k) < 1e-2
+    assert torch.equal(y[:, :, 2], x[:, :, 2])
+    ops.apply_rotary_(q, k, rot, S, interleaved, sign=-1.0)
+    assert _rel(y, x) < 2e-2
+
+
+@pytest.mark.parametrize("V", [50400, 50257, 1000])
+def test_cross_entropy(V):
+    n = 300
+    logits = (3 * torch.randn(n, V, device=DEV)).bfloat16().requires_grad_()
+    labels = torch.randint(0, V, (n,), device=DEV)
+    labels[::7] = -100
+    loss = ops.cross_entropy(logits, labels, inplace_grad=False)
+    lr = logits.detach().float().requires_grad_()
+    ref = F.cross_entropy(lr, labels, ignore_index=-100)
+    assert abs(loss.item() - ref.item()) < 1e-2 * max(1.0, abs(ref.item()))
+    loss.backward()
+    ref.backward()
+    assert _rel(logits.grad, lr.grad) < 2e-2
+
+
+def test_adamw_flat():
+    from kubernetes_cloud_amd.train.optim import FlatAdamW
+    torch.manual_seed(0)
+    n = 10000
+    p32 = torch.randn(n, device=DEV)
+    g = torch.randn(n, device=DEV)
+    ref = p32.clone().requires_grad_()
+    topt = torch.optim.AdamW([ref], lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01)
+    opt = FlatAdamW(p32.clone(), lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01,
+                    n_decay=n)
+    for _ in range(3):
+        ref.grad = g.clone()
+        topt.step()
+        opt.grad.copy_(g)
+        opt.step()
+    assert _rel(opt.master, ref.detach()) < 1e-5
+
+
+def _attn_case(B, Sq, Sk, H, Hkv, D, causal, kv_len=None, alibi=False, check_bwd=True):
+    torch.manual_seed(1)
+    q = torch.randn(B, Sq, H, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(B, Sk, Hkv, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(B, Sk, Hkv, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    kvl = torch.tensor(kv_len, device=DEV, dtype=torch.int32) if kv_len is not None else None
+    slopes = (torch.rand(H, device=DEV) * 0.5) if alibi else None
+    o = ops.flash_attention(q, k, v, causal=causal, kv_len=kvl, alibi=slopes)
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    orf, _ = ops.attention_reference(qr, kr, vr, causal, None, kvl, slopes)
+    # rows fully masked by kv_len=0 are zero in both
+    assert _rel(o, orf) < 2e-2, _rel(o, orf)
+    if not check_bwd:
+        return
+    g = torch.randn_like(o)
+    o.backward(g)
+    orf.backward(g.float())
+    assert _rel(q.grad, qr.grad) < 3e-2, ("dq", _rel(q.grad, qr.grad))
+    assert _rel(k.grad, kr.grad) < 3e-2, ("dk", _rel(k.grad, kr.grad))
+    assert _rel(v.grad, vr.grad) < 3e-2, ("dv", _rel(v.grad, vr.grad))
+
+
+@pytest.mark.parametrize("D", [64, 80, 96, 128, 160, 256, 40])
+@pytest.mark.parametrize("causal", [True, False])
+def test_attention_head_dims(D, causal):
+    _attn_case(2, 200, 200, 4, 4, D, causal)
+
+
+def test_attention_gqa_kvlen_alibi():
+    _attn_case(2, 130, 130, 8, 2, 128, True, kv_len=[130, 97], alibi=True)
+    _attn_case(3, 77, 77, 4, 4, 64, False, kv_len=[77, 10, 50])
+
+
+def test_attention_cross_and_decode_shapes():
+    _attn_case(2, 256, 77, 8, 8, 40, False)        # SD cross-attention (K/V len 77)
+    _attn_case(2, 1, 300, 4, 4, 128, True)          # decode: 1 query vs cache
+    _attn_case(1, 37, 300, 4, 4, 256, True)         # chunked prefill with offset
+
+
+def test_qkv_rope_attention_matches_reference():
+    torch.manual_seed(0)
+    B, S, H, D, rot = 2, 96, 4, 256, 64
+    qkv = torch.randn(B, S, 3 * H * D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    out = ops.qkv_rope_attention(qkv.clone(), H, D, rot, True)
+    ref = ops.qkv_rope_attention(qkv.detach().float().cpu(), H, D, rot, True)
+    assert _rel(out.cpu(), ref) < 2e-2
+    qkv2 = qkv.detach().clone().requires_grad_()
+    o2 = ops.qkv_rope_attention(qkv2 * 1.0, H, D, rot, True)
+    g = torch.randn_like(o2)
+    o2.backward(g)
+    qr = qkv.detach().float().cpu().requires_grad_()
+    ref = ops.qkv_rope_attention(qr, H, D, rot, True)
+    ref.backward(g.float().cpu())
+    assert _rel(qkv2.grad.cpu(), qr.grad) < 3e-2
