@@ -1,0 +1,138 @@
+#!/usr/bin/env python3
+"""Headline benchmark: GPT-J-6B causal-LM finetune throughput (tokens/s), bf16.
+
+Metric / config from BASELINE.json ("GPT-J-6B finetune tokens/sec ... at
+1/2/4/8 MI355X"): tokens/s = world_samples_per_second x context (2048), the
+reference's own formula (finetuner-workflow/finetuner/finetuner.py:516-522).
+Random-init GPT-J-6B (28 x 4096, 16 heads x 256, rotary 64, vocab 50400) on
+synthetic uniform token ids -- no network for checkpoints or datasets.
+
+One timed step = one optimizer step = GAS micro-batches (forward + backward
+through the native kernels) + bucketed RCCL reduce-scatter (N>1) + fused
+AdamW + bf16 all-gather. Weak scaling: per-GPU work is fixed as N grows.
+
+    python bench.py --gpus N --steps K --warmup W
+    (N>1 under: python -m torch.distributed.run --nproc-per-node N ... bench.py ...)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--model", default="gpt-j-6b")
+    ap.add_argument("--micro-batch", type=int, default=8)
+    ap.add_argument("--gas", type=int, default=4)
+    ap.add_argument("--seq", type=int, default=2048)
+    ap.add_argument("--zero-stage", type=int, default=1)
+    ap.add_argument("--ckpt", action="store_true", help="activation checkpointing")
+    ap.add_argument("--bucket", type=float, default=2e8)
+    ap.add_argument("--profile-steps", type=int, default=0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from kubernetes_cloud_amd.models.causal_lm import build_model
+    from kubernetes_cloud_amd.models.config import preset
+    from kubernetes_cloud_amd.parallel.dist import init_distributed
+    from kubernetes_cloud_amd.train.engine import TrainEngine
+    from kubernetes_cloud_amd.ops import _lib
+
+    info = init_distributed()
+    world = info.world_size
+    if world != args.gpus and info.is_main:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    _lib.require()
+    torch.manual_seed(1234 + info.rank)
+
+    cfg = preset(args.model)
+    model = build_model(cfg, device=dev, dtype=torch.bfloat16, seed=0)
+    model.gradient_checkpointing_enable(args.ckpt)
+    model.train()
+    eng = TrainEngine(model, lr=5e-5, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01,
+                      max_grad_norm=1.0, zero_stage=args.zero_stage, grad_accum=args.gas,
+                      bucket_elems=int(args.bucket))
+    B, S = args.micro_batch, args.seq
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(17 + info.rank)
+    batches = [torch.randint(0, cfg.vocab_size, (B, S), device=dev, generator=gen)
+               for _ in range(args.gas)]
+
+    def loss_fn(ids):
+        return model(ids, labels=ids)
+
+    def one_step():
+        return eng.train_batch(batches, loss_fn, lr=5e-5)
+
+    for i in range(args.warmup):
+        loss = one_step()
+        if info.is_main:
+            print(f"[bench] warmup {i} loss={loss.item():.4f} mem={torch.cuda.max_memory_allocated()/2**30:.1f}GiB",
+                  file=sys.stderr, flush=True)
+    if dist.is_initialized():
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = one_step()
+    if dist.is_initialized():
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if dist.is_initialized():
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    global_batch = B * args.gas * world
+    tokens = args.steps * global_batch * S
+    tps = tokens / dt
+    ms = dt / args.steps * 1e3
+    flops_tok = cfg.flops_per_token(S)
+    mfu = tps * flops_tok / (world * 2.5e15)
+    if info.is_main:
+        print(f"[bench] loss={loss.item():.4f} step={ms:.1f}ms tokens/s={tps:.0f} "
+              f"tokens/s/gpu={tps/world:.0f} MFU(2.5PF dense)={mfu*100:.1f}% "
+              f"peak_mem={torch.cuda.max_memory_allocated()/2**30:.1f}GiB", file=sys.stderr, flush=True)
+        rec = {
+            "metric": "GPT-J-6B finetune tokens/sec",
+            "value": round(tps, 1),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (uniform random token ids; random-init weights)",
+            "config": {
+                "model": args.model,
+                "global_batch": global_batch,
+                "micro_batch": B,
+                "grad_accum": args.gas,
+                "seq_len": S,
+                "parallelism": f"dp{world}" + (f"-zero{args.zero_stage}" if world > 1 else ""),
+                "activation_checkpointing": bool(args.ckpt),
+                "mfu_2p5pf": round(mfu, 4),
+            },
+        }
+        print(json.dumps(rec), flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -4,8 +4,9 @@
 // exp_avg, exp_avg_sq) laid out in the same order as the model's flat bf16
 // parameter buffer, so one launch updates every parameter (no multi-tensor
 // pointer lists) and the ZeRO-1/2 shard of a rank is just a [lo, hi) slice.
-// Elements [0, n_decay) get weight decay, the rest (biases, norms) do not --
-// the HF Trainer grouping the reference relies on
+// Weight decay is selected per 64-element block by a byte mask (every parameter
+// starts on a 64-element boundary of the flat buffer), so biases / norms are
+// excluded exactly as in the HF Trainer grouping the reference relies on
 // (finetuner-workflow/finetuner/finetuner.py:987-1027 -> TrainingArguments).
 //
 // The clip coefficient / loss-scale is read from device memory, so the
@@ -19,7 +20,7 @@ struct AdamWArgs {
 __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
                              float* __restrict__ m, float* __restrict__ v,
                              bf16_t* __restrict__ p_bf, long long n4,
-                             long long n_decay, AdamWArgs a,
+                             const uint8_t* __restrict__ wd_mask, AdamWArgs a,
                              const float* __restrict__ gscale,
                              const int* __restrict__ skip) {
   if (skip && *skip) return;
@@ -36,14 +37,14 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
     float ga[4] = {gg.x, gg.y, gg.z, gg.w};
     float ma[4] = {mm.x, mm.y, mm.z, mm.w};
     float va[4] = {vv.x, vv.y, vv.z, vv.w};
+    const bool dec = a.wd != 0.f && (wd_mask == nullptr || wd_mask[i >> 4]);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const long long e = i * 4 + j;
       const float gr = ga[j] * gs;
       ma[j] = a.beta1 * ma[j] + (1.f - a.beta1) * gr;
       va[j] = a.beta2 * va[j] + (1.f - a.beta2) * gr * gr;
       const float denom = sqrtf(va[j]) * inv_sqrt_bc2 + a.eps;
-      if (e < n_decay) pa[j] *= (1.f - a.lr * a.wd);
+      if (dec) pa[j] *= (1.f - a.lr * a.wd);
       pa[j] -= step_size * ma[j] / denom;
     }
     reinterpret_cast<float4*>(p)[i] = make_float4(pa[0], pa[1], pa[2], pa[3]);
@@ -59,14 +60,14 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
 }
 
 KCA_API int kca_adamw(float* p, const float* g, float* m, float* v, void* p_bf,
-                      long long n, long long n_decay, float lr, float beta1,
+                      long long n, const uint8_t* wd_mask, float lr, float beta1,
                       float beta2, float eps, float wd, float bc1, float bc2,
                       const float* gscale, const int* skip,
                       hipStream_t stream) {
   if (n % 4) return 1;
   AdamWArgs a{lr, beta1, beta2, eps, wd, bc1, bc2};
   hipLaunchKernelGGL(adamw_kernel, dim3(kca_grid(n / 4, 256)), dim3(256), 0,
-                     stream, p, g, m, v, (bf16_t*)p_bf, n / 4, n_decay, a,
+                     stream, p, g, m, v, (bf16_t*)p_bf, n / 4, wd_mask, a,
                      gscale, skip);
   return 0;
 }

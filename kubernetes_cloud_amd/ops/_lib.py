@@ -44,7 +44,7 @@ _SIGS = {
     "kca_cast_f32_bf16": [P, P, LL, P],
     "kca_cross_entropy_fwd": [P, LL, P, I, I, I, P, P, P],
     "kca_cross_entropy_bwd": [P, LL, P, P, P, F, I, I, I, P, LL, P],
-    "kca_adamw": [P, P, P, P, P, LL, LL, F, F, F, F, F, F, F, P, P, P],
+    "kca_adamw": [P, P, P, P, P, LL, P, F, F, F, F, F, F, F, P, P, P],
     "kca_sumsq": [P, LL, P, P, P],
     "kca_clip_coef": [P, F, F, P, P, P, P],
     "kca_attn_fwd": [P] * 5 + [LL] * 12 + [I] * 7 + [F, P, P, I, P],

@@ -25,7 +25,7 @@ from ..ops import _lib
 
 class FlatAdamW:
     def __init__(self, master: torch.Tensor, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
-                 weight_decay: float = 0.0, n_decay: int | None = None,
+                 weight_decay: float = 0.0, wd_mask: torch.Tensor | None = None,
                  model_bf16: torch.Tensor | None = None, grad: torch.Tensor | None = None):
         assert master.dtype == torch.float32 and master.dim() == 1
         self.master = master
@@ -37,7 +37,7 @@ class FlatAdamW:
         self.betas = betas
         self.eps = eps
         self.weight_decay = weight_decay
-        self.n_decay = master.numel() if n_decay is None else n_decay
+        self.wd_mask = wd_mask  # uint8 [n/64]: 1 = apply weight decay to that 64-block
         self.step_count = 0
         dev = master.device
         self._coef = torch.ones(1, device=dev, dtype=torch.float32)
@@ -94,7 +94,7 @@ class FlatAdamW:
         if self.native:
             _lib.call("kca_adamw", self.master.data_ptr(), self.grad.data_ptr(), self.exp_avg.data_ptr(),
                       self.exp_avg_sq.data_ptr(), _lib.ptr(self.model_bf16), self.master.numel(),
-                      self.n_decay, float(self.lr), float(b1), float(b2), float(self.eps),
+                      _lib.ptr(self.wd_mask), float(self.lr), float(b1), float(b2), float(self.eps),
                       float(self.weight_decay), float(bc1), float(bc2),
                       self._coef.data_ptr() if use_clip else None,
                       self._skip.data_ptr() if use_clip else None, _lib.stream())
@@ -105,8 +105,12 @@ class FlatAdamW:
         self.exp_avg.mul_(b1).add_(g, alpha=1 - b1)
         self.exp_avg_sq.mul_(b2).addcmul_(g, g, value=1 - b2)
         denom = (self.exp_avg_sq.sqrt() / math.sqrt(bc2)).add_(self.eps)
-        if self.weight_decay and self.n_decay:
-            self.master[: self.n_decay].mul_(1 - self.lr * self.weight_decay)
+        if self.weight_decay:
+            if self.wd_mask is None:
+                self.master.mul_(1 - self.lr * self.weight_decay)
+            else:
+                m = self.wd_mask.to(self.master.device).bool().repeat_interleave(64)[: self.master.numel()]
+                self.master.mul_(torch.where(m, 1 - self.lr * self.weight_decay, 1.0))
         self.master.addcdiv_(self.exp_avg, denom, value=-self.lr / bc1)
         if self.model_bf16 is not None:
             self.model_bf16.copy_(self.master)

@@ -106,8 +106,7 @@ def test_adamw_flat():
     g = torch.randn(n, device=DEV)
     ref = p32.clone().requires_grad_()
     topt = torch.optim.AdamW([ref], lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01)
-    opt = FlatAdamW(p32.clone(), lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01,
-                    n_decay=n)
+    opt = FlatAdamW(p32.clone(), lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01)
     for _ in range(3):
         ref.grad = g.clone()
         topt.step()
