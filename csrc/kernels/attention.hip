@@ -108,8 +108,9 @@ template <int D> struct FwdLds {
 template <int D> struct BwdLds {
   static constexpr int STR = D + 16;  // 2D+32 bytes = 32 B x odd
 };
-
 // Stage rows [r0, r0+ROWS) of a [S, D] head slice into registers (16 B chunks).
+// `full` (workgroup-uniform): every row in range and d_real == D -> no guards,
+// so interior tiles compile to straight global_load_dwordx4 streams.
 template <int D, int ROWS, int NT>
 struct Stager {
   static constexpr int NC = D / 8;
@@ -117,7 +118,17 @@ struct Stager {
   static constexpr int CPT = (TOTAL + NT - 1) / NT;
   uint4 r[CPT];
   __device__ __forceinline__ void load(const bf16_t* base, long long st, int r0,
-                                       int nrows, int d_real) {
+                                       int nrows, int d_real, bool full) {
+    if (full) {
+#pragma unroll
+      for (int i = 0; i < CPT; ++i) {
+        const int idx = threadIdx.x + i * NT;
+        const int row = idx / NC, ch = idx % NC;
+        if (TOTAL % NT == 0 || idx < TOTAL)
+          r[i] = *reinterpret_cast<const uint4*>(base + (long long)(r0 + row) * st + ch * 8);
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
       const int idx = threadIdx.x + i * NT;
@@ -132,7 +143,7 @@ struct Stager {
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
       const int idx = threadIdx.x + i * NT;
-      if (idx < TOTAL) {
+      if (TOTAL % NT == 0 || idx < TOTAL) {
         const int row = idx / NC, ch = idx % NC;
         *reinterpret_cast<uint4*>(lds + row * stride + ch * 8) = r[i];
       }
@@ -140,13 +151,17 @@ struct Stager {
   }
 };
 
+// Deferred-rescale threshold (log2 units): O / l are rescaled only when a row's
+// running max grows by more than this, so P <= 2^8 between rescales (T13).
+#define RESCALE_THR 8.0f
+
 // ============================================================== forward
 template <int D, bool CAUSAL>
-__global__ void __launch_bounds__(256, 1) attn_fwd_kernel(AttnParams p) {
+__global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_kernel(AttnParams p) {
   using L = FwdLds<D>;
   constexpr int BM = 128, BN = 32;
-  __shared__ __attribute__((aligned(16))) bf16_t Ks[BN * L::KSTR];
-  __shared__ __attribute__((aligned(16))) bf16_t Vs[BN * L::VSTR];
+  constexpr int KSZ = BN * L::KSTR, VSZ = BN * L::VSTR;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * (KSZ + VSZ)];
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int l32 = lane & 31, hh = lane >> 5;
@@ -163,6 +178,7 @@ __global__ void __launch_bounds__(256, 1) attn_fwd_kernel(AttnParams p) {
   int kv_hi = kv_end;
   if (CAUSAL) kv_hi = min(kv_hi, qb * BM + BM - 1 + off + 1);
   const int ntiles = kv_hi > 0 ? (kv_hi + BN - 1) / BN : 0;
+  const bool dfull = p.d_real == D;
 
   const float sl2 = p.scale * LOG2E;
   const float slope = p.alibi ? p.alibi[h] * LOG2E : 0.f;
@@ -187,18 +203,24 @@ __global__ void __launch_bounds__(256, 1) attn_fwd_kernel(AttnParams p) {
 
   Stager<D, BN, 256> sk, sv;
   if (ntiles > 0) {
-    sk.load(kp, p.k_st, 0, p.Sk, p.d_real);
-    sv.load(vp, p.v_st, 0, p.Sk, p.d_real);
-    sk.store(Ks, L::KSTR);
-    sv.store(Vs, L::VSTR);
+    const bool full = dfull && BN <= p.Sk;
+    sk.load(kp, p.k_st, 0, p.Sk, p.d_real, full);
+    sv.load(vp, p.v_st, 0, p.Sk, p.d_real, full);
+    sk.store(smem, L::KSTR);
+    sv.store(smem + KSZ, L::VSTR);
   }
   __syncthreads();
 
+  const int gi = lane & 15;
+  const int dcol = 16 * ((lane >> 4) & 1) + 4 * (gi & 3);
   for (int t = 0; t < ntiles; ++t) {
     const int k0 = t * BN;
-    if (t + 1 < ntiles) {  // T14: issue next tile's loads before this tile's MFMAs
-      sk.load(kp, p.k_st, k0 + BN, p.Sk, p.d_real);
-      sv.load(vp, p.v_st, k0 + BN, p.Sk, p.d_real);
+    const bf16_t* Ks = smem + (t & 1) * (KSZ + VSZ);
+    const bf16_t* Vs = Ks + KSZ;
+    if (t + 1 < ntiles) {  // T14: next tile's loads in flight under this tile's MFMAs
+      const bool full = dfull && (k0 + 2 * BN <= p.Sk);
+      sk.load(kp, p.k_st, k0 + BN, p.Sk, p.d_real, full);
+      sv.load(vp, p.v_st, k0 + BN, p.Sk, p.d_real, full);
     }
     const bool active = !CAUSAL || (k0 <= q0 + BN - 1 + off);
     if (active) {
@@ -210,39 +232,47 @@ __global__ void __launch_bounds__(256, 1) attn_fwd_kernel(AttnParams p) {
         bf16x8 a = ld_bf16x8(Ks + l32 * L::KSTR + 16 * s + 8 * hh);
         sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s], sacc, 0, 0, 0);
       }
+      const bool need_mask = (CAUSAL && (k0 + BN - 1 > q0 + off)) || (k0 + BN > kv_end);
       float x[16];
       float mt = -INFINITY;
+      if (need_mask || p.alibi) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = k0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        bool valid = key < kv_end;
-        if (CAUSAL) valid = valid && (key <= qrow + off);
-        float v = sacc[r] * sl2;
-        if (p.alibi) v += slope * (float)(key - qrow - off);
-        x[r] = valid ? v : -INFINITY;
-        mt = fmaxf(mt, x[r]);
+        for (int r = 0; r < 16; ++r) {
+          const int key = k0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          bool valid = key < kv_end;
+          if (CAUSAL) valid = valid && (key <= qrow + off);
+          float v = sacc[r] * sl2;
+          if (p.alibi) v += slope * (float)(key - qrow - off);
+          x[r] = valid ? v : -INFINITY;
+          mt = fmaxf(mt, x[r]);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          x[r] = sacc[r] * sl2;
+          mt = fmaxf(mt, x[r]);
+        }
       }
       mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-      const float mnew = fmaxf(m, mt);
-      const float msub = (mnew == -INFINITY) ? 0.f : mnew;
-      const float alpha = exp2f(m - msub);
+      if (!__all(mt <= m + RESCALE_THR)) {
+        const float mnew = fmaxf(m, mt);
+        const float alpha = (mnew == -INFINITY) ? 1.f : exp2f(m - mnew);
+        lsum *= alpha;
+#pragma unroll
+        for (int i = 0; i < D / 32; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) oacc[i][r] *= alpha;
+        m = mnew;
+      }
+      const float msub = (m == -INFINITY) ? 0.f : m;
       float ps = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         x[r] = exp2f(x[r] - msub);
         ps += x[r];
       }
-      lsum = lsum * alpha + ps;
-      m = mnew;
-      if (!__all(alpha == 1.f)) {
-#pragma unroll
-        for (int i = 0; i < D / 32; ++i)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) oacc[i][r] *= alpha;
-      }
+      lsum += ps;
       const bf16x8 pf0 = to_bf16x8(x), pf1 = to_bf16x8(x + 8);
-      const int gi = lane & 15;
-      const int dcol = 16 * ((lane >> 4) & 1) + 4 * (gi & 3);
 #pragma unroll
       for (int db = 0; db < D / 32; ++db) {
 #pragma unroll
@@ -254,10 +284,10 @@ __global__ void __launch_bounds__(256, 1) attn_fwd_kernel(AttnParams p) {
         }
       }
     }
-    __syncthreads();
-    if (t + 1 < ntiles) {
-      sk.store(Ks, L::KSTR);
-      sv.store(Vs, L::VSTR);
+    if (t + 1 < ntiles) {  // other buffer: last read in tile t-1, fenced by its barrier
+      bf16_t* Kn = smem + ((t + 1) & 1) * (KSZ + VSZ);
+      sk.store(Kn, L::KSTR);
+      sv.store(Kn + KSZ, L::VSTR);
     }
     __syncthreads();
   }
@@ -318,14 +348,14 @@ __global__ void attn_bwd_preprocess_kernel(const bf16_t* __restrict__ o,
   if (row < rows && sub == 0) delta[row] = s;
 }
 
+
 template <int D, bool CAUSAL>
-__global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_kernel(AttnBwdParams p) {
+__global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_bwd_dkdv_kernel(AttnBwdParams p) {
   using L = BwdLds<D>;
   constexpr int BK = 64, BQ = 32;
-  __shared__ __attribute__((aligned(16))) bf16_t Qs[BQ * L::STR];
-  __shared__ __attribute__((aligned(16))) bf16_t Ds[BQ * L::STR];
-  __shared__ float lse_s[BQ];
-  __shared__ float dl_s[BQ];
+  constexpr int TSZ = BQ * L::STR;
+  constexpr int BUF = 2 * TSZ + 2 * BQ * 2;  // Q, dO tiles + lse, delta (as floats)
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * BUF];
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int G = lane >> 4, gi = lane & 15;
@@ -338,6 +368,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_kernel(AttnBwdParams p) 
   const int kw = kb * BK + wave * 16;
   const int key = kw + gi;
   const float sl2 = p.scale * LOG2E;
+  const bool dfull = p.d_real == D;
 
   const bf16_t* kp = p.k + b * p.k_sb + hk * p.k_sh;
   const bf16_t* vp = p.v + b * p.v_sb + hk * p.v_sh;
@@ -361,22 +392,28 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_kernel(AttnBwdParams p) 
   const int total = (kb * BK < kv_end) ? nqt * grp : 0;
 
   Stager<D, BQ, 256> sq, sd;
+  float lse_r = INFINITY, dl_r = 0.f;
   auto load_tile = [&](int it) {
     const int hq = hk * grp + it / nqt;
     const int qt = q_lo + (it % nqt) * BQ;
-    sq.load(p.q + b * p.q_sb + hq * p.q_sh, p.q_st, qt, p.Sq, p.d_real);
-    sd.load(p.dout + b * p.do_sb + hq * p.do_sh, p.do_st, qt, p.Sq, p.d_real);
-  };
-  auto store_tile = [&](int it) {
-    const int hq = hk * grp + it / nqt;
-    const int qt = q_lo + (it % nqt) * BQ;
-    sq.store(Qs, L::STR);
-    sd.store(Ds, L::STR);
+    const bool full = dfull && (qt + BQ <= p.Sq);
+    sq.load(p.q + b * p.q_sb + hq * p.q_sh, p.q_st, qt, p.Sq, p.d_real, full);
+    sd.load(p.dout + b * p.do_sb + hq * p.do_sh, p.do_st, qt, p.Sq, p.d_real, full);
     if (threadIdx.x < BQ) {
       const int q = qt + threadIdx.x;
       const long long li = ((long long)b * p.H + hq) * p.Sq + q;
-      lse_s[threadIdx.x] = q < p.Sq ? p.lse[li] : INFINITY;
-      dl_s[threadIdx.x] = q < p.Sq ? p.delta[li] : 0.f;
+      lse_r = q < p.Sq ? p.lse[li] : INFINITY;
+      dl_r = q < p.Sq ? p.delta[li] : 0.f;
+    }
+  };
+  auto store_tile = [&](int buf) {
+    bf16_t* base = smem + buf * BUF;
+    sq.store(base, L::STR);
+    sd.store(base + TSZ, L::STR);
+    float* f = reinterpret_cast<float*>(base + 2 * TSZ);
+    if (threadIdx.x < BQ) {
+      f[threadIdx.x] = lse_r;
+      f[BQ + threadIdx.x] = dl_r;
     }
   };
   if (total > 0) {
@@ -384,9 +421,15 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_kernel(AttnBwdParams p) 
     store_tile(0);
   }
   __syncthreads();
+  const int trow = 4 * G + (gi >> 2);
+  const int tcol = 4 * (gi & 3);
   for (int it = 0; it < total; ++it) {
     const int hq = hk * grp + it / nqt;
     const int qt = q_lo + (it % nqt) * BQ;
+    const bf16_t* Qs = smem + (it & 1) * BUF;
+    const bf16_t* Ds = Qs + TSZ;
+    const float* lse_s = reinterpret_cast<const float*>(Qs + 2 * TSZ);
+    const float* dl_s = lse_s + BQ;
     if (it + 1 < total) load_tile(it + 1);
     const bool active = !CAUSAL || (kw <= qt + BQ - 1 + off);
     if (active) {
@@ -404,6 +447,8 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_kernel(AttnBwdParams p) 
           dpacc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld_bf16x8(Ds + off_l), vf[s], dpacc[j], 0, 0, 0);
         }
       }
+      const bool need_mask = (CAUSAL && (kw + 15 > qt + off)) || (kw + 16 > kv_end) ||
+                             (qt + BQ > p.Sq);
       const float slope = p.alibi ? p.alibi[hq] * LOG2E : 0.f;
       float pv[8], dsv[8];
 #pragma unroll
@@ -412,18 +457,19 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_kernel(AttnBwdParams p) 
         for (int r = 0; r < 4; ++r) {
           const int ql = j * 16 + 4 * G + r;
           const int q = qt + ql;
-          bool valid = q < p.Sq && key < kv_end;
-          if (CAUSAL) valid = valid && (key <= q + off);
           float x = sacc[j][r] * sl2 - lse_s[ql] * LOG2E;
           if (p.alibi) x += slope * (float)(key - q - off);
-          const float pr = valid ? exp2f(x) : 0.f;
+          float pr = exp2f(x);
+          if (need_mask) {
+            bool valid = q < p.Sq && key < kv_end;
+            if (CAUSAL) valid = valid && (key <= q + off);
+            pr = valid ? pr : 0.f;
+          }
           pv[j * 4 + r] = pr;
           dsv[j * 4 + r] = pr * (dpacc[j][r] - dl_s[ql]);
         }
       }
       const bf16x8 pb = to_bf16x8(pv), dsb = to_bf16x8(dsv);
-      const int trow = 4 * G + (gi >> 2);
-      const int tcol = 4 * (gi & 3);
 #pragma unroll
       for (int db = 0; db < D / 16; ++db) {
         const bf16_t* dob = Ds + trow * L::STR + db * 16 + tcol;
@@ -434,8 +480,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_kernel(AttnBwdParams p) 
         dk[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq, dsb, dk[db], 0, 0, 0);
       }
     }
-    __syncthreads();
-    if (it + 1 < total) store_tile(it + 1);
+    if (it + 1 < total) store_tile((it + 1) & 1);
     __syncthreads();
   }
   if (key < p.Sk) {
@@ -458,11 +503,11 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_kernel(AttnBwdParams p) 
 }
 
 template <int D, bool CAUSAL>
-__global__ void __launch_bounds__(256, 1) attn_bwd_dq_kernel(AttnBwdParams p) {
+__global__ void __launch_bounds__(256, (D <= 160 ? 2 : 1)) attn_bwd_dq_kernel(AttnBwdParams p) {
   using L = BwdLds<D>;
   constexpr int BQ = 64, BN = 32;
-  __shared__ __attribute__((aligned(16))) bf16_t Ks[BN * L::STR];
-  __shared__ __attribute__((aligned(16))) bf16_t Vs[BN * L::STR];
+  constexpr int TSZ = BN * L::STR;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TSZ];
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int G = lane >> 4, gi = lane & 15;
@@ -478,6 +523,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq_kernel(AttnBwdParams p) {
   const int q = qw + gi;
   const float sl2 = p.scale * LOG2E;
   const float slope = p.alibi ? p.alibi[h] * LOG2E : 0.f;
+  const bool dfull = p.d_real == D;
 
   const bf16_t* qp = p.q + b * p.q_sb + h * p.q_sh;
   const bf16_t* gp = p.dout + b * p.do_sb + h * p.do_sh;
@@ -505,17 +551,23 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq_kernel(AttnBwdParams p) {
   const bf16_t* vp = p.v + b * p.v_sb + hk * p.v_sh;
   Stager<D, BN, 256> sk, sv;
   if (ntiles > 0) {
-    sk.load(kp, p.k_st, 0, p.Sk, p.d_real);
-    sv.load(vp, p.v_st, 0, p.Sk, p.d_real);
-    sk.store(Ks, L::STR);
-    sv.store(Vs, L::STR);
+    const bool full = dfull && BN <= p.Sk;
+    sk.load(kp, p.k_st, 0, p.Sk, p.d_real, full);
+    sv.load(vp, p.v_st, 0, p.Sk, p.d_real, full);
+    sk.store(smem, L::STR);
+    sv.store(smem + TSZ, L::STR);
   }
   __syncthreads();
+  const int trow = 4 * G + (gi >> 2);
+  const int tcol = 4 * (gi & 3);
   for (int t = 0; t < ntiles; ++t) {
     const int k0 = t * BN;
+    const bf16_t* Ks = smem + (t & 1) * 2 * TSZ;
+    const bf16_t* Vs = Ks + TSZ;
     if (t + 1 < ntiles) {
-      sk.load(kp, p.k_st, k0 + BN, p.Sk, p.d_real);
-      sv.load(vp, p.v_st, k0 + BN, p.Sk, p.d_real);
+      const bool full = dfull && (k0 + 2 * BN <= p.Sk);
+      sk.load(kp, p.k_st, k0 + BN, p.Sk, p.d_real, full);
+      sv.load(vp, p.v_st, k0 + BN, p.Sk, p.d_real, full);
     }
     const bool active = !CAUSAL || (k0 <= qw + 15 + off);
     if (active) {
@@ -533,23 +585,26 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq_kernel(AttnBwdParams p) {
           dpt[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld_bf16x8(Vs + off_l), gf[s], dpt[j], 0, 0, 0);
         }
       }
+      const bool need_mask = (CAUSAL && (k0 + BN - 1 > qw + off)) || (k0 + BN > kv_end) ||
+                             (qw + 16 > p.Sq);
       float dsv[8];
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int key = k0 + j * 16 + 4 * G + r;
-          bool valid = q < p.Sq && key < kv_end;
-          if (CAUSAL) valid = valid && (key <= q + off);
           float x = st[j][r] * sl2 - lse_q;
           if (p.alibi) x += slope * (float)(key - q - off);
-          const float pr = valid ? exp2f(x) : 0.f;
+          float pr = exp2f(x);
+          if (need_mask) {
+            bool valid = q < p.Sq && key < kv_end;
+            if (CAUSAL) valid = valid && (key <= q + off);
+            pr = valid ? pr : 0.f;
+          }
           dsv[j * 4 + r] = pr * (dpt[j][r] - dl_q);
         }
       }
       const bf16x8 dsb = to_bf16x8(dsv);
-      const int trow = 4 * G + (gi >> 2);
-      const int tcol = 4 * (gi & 3);
 #pragma unroll
       for (int db = 0; db < D / 16; ++db) {
         const bf16_t* kb_ = Ks + trow * L::STR + db * 16 + tcol;
@@ -557,10 +612,10 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq_kernel(AttnBwdParams p) {
         dq[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, dsb, dq[db], 0, 0, 0);
       }
     }
-    __syncthreads();
     if (t + 1 < ntiles) {
-      sk.store(Ks, L::STR);
-      sv.store(Vs, L::STR);
+      bf16_t* Kn = smem + ((t + 1) & 1) * 2 * TSZ;
+      sk.store(Kn, L::STR);
+      sv.store(Kn + TSZ, L::STR);
     }
     __syncthreads();
   }
