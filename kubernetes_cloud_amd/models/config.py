@@ -96,13 +96,16 @@ class LMConfig:
         if mt == "gpt_neox":
             d = cfg["hidden_size"]
             hd = d // cfg["num_attention_heads"]
+            rp = cfg.get("rope_parameters") or {}
+            rot_pct = cfg.get("rotary_pct", rp.get("partial_rotary_factor", 0.25))
+            rot_base = cfg.get("rotary_emb_base", rp.get("rope_theta", cfg.get("rope_theta", 10000)))
             act = cfg.get("hidden_act", "gelu")
             return cls(arch="gpt_neox", vocab_size=cfg["vocab_size"], hidden=d,
                        n_layers=cfg["num_hidden_layers"], n_heads=cfg["num_attention_heads"],
                        ffn=cfg.get("intermediate_size", 4 * d),
                        max_pos=cfg.get("max_position_embeddings", 2048),
-                       rotary_dim=int(hd * cfg.get("rotary_pct", 0.25)), rotary_interleaved=False,
-                       rotary_base=cfg.get("rotary_emb_base", 10000),
+                       rotary_dim=int(hd * rot_pct), rotary_interleaved=False,
+                       rotary_base=rot_base,
                        parallel_residual=cfg.get("use_parallel_residual", True), qkv_bias=True,
                        out_bias=True, mlp_bias=True,
                        gelu_approx="none" if act == "gelu" else "tanh",
