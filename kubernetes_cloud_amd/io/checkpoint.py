@@ -1,0 +1,133 @@
+"""HF-Trainer-style checkpoint directories + the ``.ready.txt`` sentinel.
+
+Layout written under ``{output_path}/results-{run_name}/``
+(finetuner-workflow/finetuner/finetuner.py:345-347, 1016-1018, 1055-1062):
+
+    checkpoint-{step}/
+        config.json, model.safetensors[.index.json + shards]   (HF names)
+        trainer_state.json          global_step, epoch, log_history, schedule
+        training_args.json          the CLI namespace
+        optimizer/rank-{r:05d}.safetensors   fp32 master/exp_avg/exp_avg_sq shard
+        optimizer/meta.json         world size, layout size, ZeRO stage
+        rng_state_{r}.pth           torch / cuda / numpy / python RNG (own file)
+    final/  model + tokenizer + .ready.txt
+
+Resume picks the largest numeric ``checkpoint-N`` and *skips* entries without
+a numeric suffix (the reference's scan silently disabled resume when e.g.
+``final/`` existed: finetuner.py:350-357 -- SURVEY §7.6).
+"""
+from __future__ import annotations
+
+import json
+import os
+import random
+import re
+import time
+
+import numpy as np
+import torch
+
+_CKPT = re.compile(r"^checkpoint-(\d+)$")
+
+
+def find_last_checkpoint(output_dir: str) -> str | None:
+    try:
+        names = os.listdir(output_dir)
+    except FileNotFoundError:
+        return None
+    best = None
+    for n in names:
+        m = _CKPT.match(n)
+        if m and os.path.isdir(os.path.join(output_dir, n)):
+            step = int(m.group(1))
+            if best is None or step > best[0]:
+                best = (step, n)
+    return os.path.join(output_dir, best[1]) if best else None
+
+
+def write_ready(path: str):
+    os.makedirs(path, exist_ok=True)
+    open(os.path.join(path, ".ready.txt"), "a").close()
+
+
+def wait_ready(path: str, timeout_s: float = 3600, poll_s: float = 5.0) -> bool:
+    """Poll for ``.ready.txt`` like the BLOOM / DALL-E predictors
+    (online-inference/bloom-176b/model/bloom.py:79-90)."""
+    t0 = time.time()
+    f = os.path.join(path, ".ready.txt")
+    while not os.path.exists(f):
+        if time.time() - t0 > timeout_s:
+            return False
+        time.sleep(poll_s)
+    return True
+
+
+def _rng_state():
+    st = {"torch": torch.get_rng_state(), "numpy": np.random.get_state()[1].astype(np.int64),
+          "python": random.getstate()[1]}
+    if torch.cuda.is_available():
+        st["cuda"] = torch.cuda.get_rng_state()
+    return st
+
+
+def save_checkpoint(ckpt_dir: str, model, engine, trainer_state: dict, args_dict: dict | None = None,
+                    tokenizer=None, rank: int = 0, world: int = 1, barrier=None):
+    from safetensors.torch import save_file
+
+    from .hf import save_pretrained
+
+    os.makedirs(os.path.join(ckpt_dir, "optimizer"), exist_ok=True)
+    if rank == 0:
+        save_pretrained(model, ckpt_dir)
+        if tokenizer is not None:
+            tokenizer.save_pretrained(ckpt_dir)
+        with open(os.path.join(ckpt_dir, "trainer_state.json"), "w") as f:
+            json.dump(trainer_state, f, indent=2, default=str)
+        if args_dict is not None:
+            with open(os.path.join(ckpt_dir, "training_args.json"), "w") as f:
+                json.dump(args_dict, f, indent=2, default=str)
+    if engine is not None:
+        st = engine.optimizer_state()
+        tensors = {"master": st["master"].detach().cpu(), "exp_avg": st["exp_avg"].detach().cpu(),
+                   "exp_avg_sq": st["exp_avg_sq"].detach().cpu()}
+        save_file(tensors, os.path.join(ckpt_dir, "optimizer", f"rank-{rank:05d}.safetensors"))
+        if rank == 0:
+            with open(os.path.join(ckpt_dir, "optimizer", "meta.json"), "w") as f:
+                json.dump({"world": st["world"], "total": st["total"], "step": st["step"],
+                           "zero_stage": st["zero_stage"], "lr": st["lr"]}, f)
+    rs = _rng_state()
+    torch.save({k: (torch.as_tensor(v) if not isinstance(v, torch.Tensor) else v) for k, v in rs.items()},
+               os.path.join(ckpt_dir, f"rng_state_{rank}.pth"))
+    if barrier is not None:
+        barrier()
+
+
+def load_checkpoint(ckpt_dir: str, model, engine, rank: int = 0) -> dict:
+    from safetensors.torch import load_file
+
+    from ..models.hf_convert import hf_to_native
+    from .hf import read_hf_state_dict
+
+    sd = hf_to_native(read_hf_state_dict(ckpt_dir), model.cfg)
+    with torch.no_grad():
+        own = model.state_dict()
+        for k, v in sd.items():
+            if k in own:
+                own[k].copy_(v.to(own[k].dtype))
+    if engine is not None:
+        with open(os.path.join(ckpt_dir, "optimizer", "meta.json")) as f:
+            meta = json.load(f)
+        t = load_file(os.path.join(ckpt_dir, "optimizer", f"rank-{rank:05d}.safetensors"))
+        dev = engine.opt.master.device
+        engine.load_optimizer_state({"master": t["master"].to(dev), "exp_avg": t["exp_avg"].to(dev),
+                                     "exp_avg_sq": t["exp_avg_sq"].to(dev), "step": meta["step"],
+                                     "lr": meta.get("lr"), "world": meta["world"],
+                                     "total": meta["total"]})
+    p = os.path.join(ckpt_dir, f"rng_state_{rank}.pth")
+    if os.path.exists(p):
+        rs = torch.load(p, weights_only=True)
+        torch.set_rng_state(rs["torch"])
+        if "cuda" in rs and torch.cuda.is_available():
+            torch.cuda.set_rng_state(rs["cuda"])
+    with open(os.path.join(ckpt_dir, "trainer_state.json")) as f:
+        return json.load(f)
