@@ -1,0 +1,60 @@
+"""ctypes binding of the host-side native runtime ``_lib/libkca_host.so``
+(weight streamer, host AdamW, BPE tokenizer / packer). Built by
+``tools/build_ext.py`` with g++ (+ the HIP runtime for the device streamer)."""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+HOST_LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib", "libkca_host.so")
+
+_lock = threading.Lock()
+_lib = None
+_err = None
+
+P, I, LL, F, D = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_float, ctypes.c_double
+_SIGS = {
+    "kca_read_ranges": (I, [ctypes.c_char_p, I, P, P, P, I, LL, P]),
+    "kca_stream_to_device": (I, [ctypes.c_char_p, I, P, P, P, I, I, LL, I, P]),
+    "kca_host_simd_level": (I, []),
+    "kca_host_adamw": (I, [P, P, P, P, P, P, LL, F, F, F, F, F, F, F, F, I]),
+    "kca_bpe_new": (P, [P, I, P, P, P]),
+    "kca_bpe_free": (None, [P]),
+    "kca_bpe_encode": (LL, [P, ctypes.c_char_p, LL, P, LL]),
+    "kca_packer_new": (P, [I, I, I, I, I, D]),
+    "kca_packer_add": (None, [P, P, LL]),
+    "kca_packer_write": (I, [P, ctypes.c_char_p, P]),
+    "kca_packer_free": (None, [P]),
+}
+
+
+def load():
+    global _lib, _err
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        try:
+            import torch  # noqa: F401  (HIP runtime first: one libamdhip64 in the process)
+        except Exception:  # pragma: no cover
+            pass
+        if not os.path.exists(HOST_LIB):
+            _err = f"{HOST_LIB} not built (python tools/build_ext.py)"
+            raise RuntimeError(_err)
+        lib = ctypes.CDLL(HOST_LIB)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def available() -> bool:
+    try:
+        load()
+        return True
+    except Exception:
+        return False
