@@ -634,6 +634,311 @@ __global__ void __launch_bounds__(256, (D <= 160 ? 2 : 1)) attn_bwd_dq_kernel(At
   }
 }
 
+// ====================================================== backward, D >= 128
+// 32x32x16 variants for head_dim 128 / 256 (GPT-J, BLOOM shards): a wave owns
+// 32 keys (dK/dV kernel) or 32 queries (dQ kernel), halving LDS bytes per
+// MFMA versus the 16-wide kernels above (each operand fragment feeds a 32-wide
+// MFMA). Q/dO/K tiles are read both by rows (ds_read_b128) and transposed
+// (ds_read_b64_tr_b16), so they use an XOR-swizzled image with unpadded rows:
+// 16-B chunk c of row r lives at chunk c ^ (((r&3)<<2) | ((r>>2)&3)), which is
+// conflict free for both access kinds (rows are 16-chunk multiples).
+template <int D>
+__device__ __forceinline__ int swz_off(int row, int ch) {
+  return row * D + ((ch ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 3);
+}
+
+template <int D, int ROWS, int NT>
+__device__ __forceinline__ void store_swz(const Stager<D, ROWS, NT>& s, bf16_t* lds) {
+#pragma unroll
+  for (int i = 0; i < Stager<D, ROWS, NT>::CPT; ++i) {
+    const int idx = threadIdx.x + i * NT;
+    if (Stager<D, ROWS, NT>::TOTAL % NT == 0 || idx < Stager<D, ROWS, NT>::TOTAL) {
+      const int row = idx / (D / 8), ch = idx % (D / 8);
+      *reinterpret_cast<uint4*>(lds + swz_off<D>(row, ch)) = s.r[i];
+    }
+  }
+}
+
+// transposed read of the 32x32x16 A operand (rows r0.., 32 columns at c0)
+template <int D>
+__device__ __forceinline__ bf16x8 tr_a32(const bf16_t* base, int s, int hh, int lane, int db) {
+  const int gi = lane & 15;
+  const int row = 16 * s + 4 * hh + (gi >> 2);
+  const int col = db * 32 + 16 * ((lane >> 4) & 1) + 4 * (gi & 3);
+  const int ch = col >> 3, in = col & 7;
+  return cat44(tr_read(base + swz_off<D>(row, ch) + in), tr_read(base + swz_off<D>(row + 8, ch) + in));
+}
+
+template <int D, bool CAUSAL>
+__global__ void __launch_bounds__(256, 1) attn_bwd_dkdv32_kernel(AttnBwdParams p) {
+  constexpr int BK = 128, BQ = 32;
+  constexpr int TSZ = BQ * D;
+  constexpr int BUF = 2 * TSZ + 2 * BQ * 2;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * BUF];
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int kb = blockIdx.x, bh = blockIdx.y;
+  const int b = bh / p.Hkv, hk = bh % p.Hkv;
+  const int grp = p.H / p.Hkv;
+  const int off = p.Sk - p.Sq;
+  int kv_end = p.Sk;
+  if (p.kv_len) kv_end = min(kv_end, p.kv_len[b]);
+  const int kw = kb * BK + wave * 32;
+  const int key = kw + l32;
+  const float sl2 = p.scale * LOG2E;
+  const bool dfull = p.d_real == D;
+
+  const bf16_t* kp = p.k + b * p.k_sb + hk * p.k_sh;
+  const bf16_t* vp = p.v + b * p.v_sb + hk * p.v_sh;
+  bf16x8 kf[D / 16], vf[D / 16];
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    const int d0 = 16 * s + 8 * hh;
+    const bool ok = key < p.Sk && d0 < p.d_real;
+    kf[s] = ok ? ld_bf16x8(kp + (long long)key * p.k_st + d0) : zero_bf16x8();
+    vf[s] = ok ? ld_bf16x8(vp + (long long)key * p.v_st + d0) : zero_bf16x8();
+  }
+  f32x16 dk[D / 32], dv[D / 32];
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { dk[i][r] = 0.f; dv[i][r] = 0.f; }
+
+  int q_lo = 0;
+  if (CAUSAL) q_lo = max(0, kb * BK - off) & ~(BQ - 1);
+  const int nqt = p.Sq > q_lo ? (p.Sq - q_lo + BQ - 1) / BQ : 0;
+  const int total = (kb * BK < kv_end) ? nqt * grp : 0;
+
+  Stager<D, BQ, 256> sq, sd;
+  float lse_r = INFINITY, dl_r = 0.f;
+  auto load_tile = [&](int it) {
+    const int hq = hk * grp + it / nqt;
+    const int qt = q_lo + (it % nqt) * BQ;
+    const bool full = dfull && (qt + BQ <= p.Sq);
+    sq.load(p.q + b * p.q_sb + hq * p.q_sh, p.q_st, qt, p.Sq, p.d_real, full);
+    sd.load(p.dout + b * p.do_sb + hq * p.do_sh, p.do_st, qt, p.Sq, p.d_real, full);
+    if (threadIdx.x < BQ) {
+      const int q = qt + threadIdx.x;
+      const long long li = ((long long)b * p.H + hq) * p.Sq + q;
+      lse_r = q < p.Sq ? p.lse[li] : INFINITY;
+      dl_r = q < p.Sq ? p.delta[li] : 0.f;
+    }
+  };
+  auto store_tile = [&](int buf) {
+    bf16_t* base = smem + buf * BUF;
+    store_swz(sq, base);
+    store_swz(sd, base + TSZ);
+    float* f = reinterpret_cast<float*>(base + 2 * TSZ);
+    if (threadIdx.x < BQ) {
+      f[threadIdx.x] = lse_r;
+      f[BQ + threadIdx.x] = dl_r;
+    }
+  };
+  if (total > 0) {
+    load_tile(0);
+    store_tile(0);
+  }
+  __syncthreads();
+  for (int it = 0; it < total; ++it) {
+    const int hq = hk * grp + it / nqt;
+    const int qt = q_lo + (it % nqt) * BQ;
+    const bf16_t* Qs = smem + (it & 1) * BUF;
+    const bf16_t* Ds = Qs + TSZ;
+    const float* lse_s = reinterpret_cast<const float*>(Qs + 2 * TSZ);
+    const float* dl_s = lse_s + BQ;
+    if (it + 1 < total) load_tile(it + 1);
+    const bool active = !CAUSAL || (kw <= qt + BQ - 1 + off);
+    if (active) {
+      f32x16 sacc, dpacc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { sacc[r] = 0.f; dpacc[r] = 0.f; }
+#pragma unroll
+      for (int s = 0; s < D / 16; ++s) {
+        const int o = swz_off<D>(l32, 2 * s + hh);
+        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld_bf16x8(Qs + o), kf[s], sacc, 0, 0, 0);
+        dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld_bf16x8(Ds + o), vf[s], dpacc, 0, 0, 0);
+      }
+      const bool need_mask = (CAUSAL && (kw + 31 > qt + off)) || (kw + 32 > kv_end) || (qt + BQ > p.Sq);
+      const float slope = p.alibi ? p.alibi[hq] * LOG2E : 0.f;
+      float pv[16], dsv[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ql = (r & 3) + 8 * (r >> 2) + 4 * hh;
+        const int q = qt + ql;
+        float x = sacc[r] * sl2 - lse_s[ql] * LOG2E;
+        if (p.alibi) x += slope * (float)(key - q - off);
+        float pr = exp2f(x);
+        if (need_mask) {
+          bool valid = q < p.Sq && key < kv_end;
+          if (CAUSAL) valid = valid && (key <= q + off);
+          pr = valid ? pr : 0.f;
+        }
+        pv[r] = pr;
+        dsv[r] = pr * (dpacc[r] - dl_s[ql]);
+      }
+      const bf16x8 pb0 = to_bf16x8(pv), pb1 = to_bf16x8(pv + 8);
+      const bf16x8 db0 = to_bf16x8(dsv), db1 = to_bf16x8(dsv + 8);
+#pragma unroll
+      for (int db = 0; db < D / 32; ++db) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          dv[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_a32<D>(Ds, s, hh, lane, db), s ? pb1 : pb0,
+                                                           dv[db], 0, 0, 0);
+          dk[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_a32<D>(Qs, s, hh, lane, db), s ? db1 : db0,
+                                                           dk[db], 0, 0, 0);
+        }
+      }
+    }
+    if (it + 1 < total) store_tile((it + 1) & 1);
+    __syncthreads();
+  }
+  if (key < p.Sk) {
+    bf16_t* dkp = p.dk + b * p.dk_sb + hk * p.dk_sh + (long long)key * p.dk_st;
+    bf16_t* dvp = p.dv + b * p.dv_sb + hk * p.dv_sh + (long long)key * p.dv_st;
+#pragma unroll
+    for (int db = 0; db < D / 32; ++db) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = db * 32 + 8 * g + 4 * hh;
+        if (d < p.d_real) {
+          uint2 w;
+          w.x = pack_bf16x2(dk[db][4 * g] * p.scale, dk[db][4 * g + 1] * p.scale);
+          w.y = pack_bf16x2(dk[db][4 * g + 2] * p.scale, dk[db][4 * g + 3] * p.scale);
+          *reinterpret_cast<uint2*>(dkp + d) = w;
+          w.x = pack_bf16x2(dv[db][4 * g], dv[db][4 * g + 1]);
+          w.y = pack_bf16x2(dv[db][4 * g + 2], dv[db][4 * g + 3]);
+          *reinterpret_cast<uint2*>(dvp + d) = w;
+        }
+      }
+    }
+  }
+}
+
+template <int D, bool CAUSAL>
+__global__ void __launch_bounds__(256, 1) attn_bwd_dq32_kernel(AttnBwdParams p) {
+  constexpr int BQ = 128, BN = 32;
+  constexpr int TSZ = BN * D;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TSZ];
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int nqb = gridDim.x;
+  const int qb = CAUSAL ? (nqb - 1 - (int)blockIdx.x) : (int)blockIdx.x;
+  const int bh = blockIdx.y;
+  const int b = bh / p.H, h = bh % p.H;
+  const int hk = h / (p.H / p.Hkv);
+  const int off = p.Sk - p.Sq;
+  int kv_end = p.Sk;
+  if (p.kv_len) kv_end = min(kv_end, p.kv_len[b]);
+  const int qw = qb * BQ + wave * 32;
+  const int q = qw + l32;
+  const float sl2 = p.scale * LOG2E;
+  const float slope = p.alibi ? p.alibi[h] * LOG2E : 0.f;
+  const bool dfull = p.d_real == D;
+
+  const bf16_t* qp = p.q + b * p.q_sb + h * p.q_sh;
+  const bf16_t* gp = p.dout + b * p.do_sb + h * p.do_sh;
+  bf16x8 qf[D / 16], gf[D / 16];
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    const int d0 = 16 * s + 8 * hh;
+    const bool ok = q < p.Sq && d0 < p.d_real;
+    qf[s] = ok ? ld_bf16x8(qp + (long long)q * p.q_st + d0) : zero_bf16x8();
+    gf[s] = ok ? ld_bf16x8(gp + (long long)q * p.do_st + d0) : zero_bf16x8();
+  }
+  const long long li = ((long long)b * p.H + h) * p.Sq + q;
+  const float lse_q = q < p.Sq ? p.lse[li] * LOG2E : INFINITY;
+  const float dl_q = q < p.Sq ? p.delta[li] : 0.f;
+  f32x16 dq[D / 32];
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dq[i][r] = 0.f;
+
+  int kv_hi = kv_end;
+  if (CAUSAL) kv_hi = min(kv_hi, qb * BQ + BQ - 1 + off + 1);
+  const int ntiles = kv_hi > 0 ? (kv_hi + BN - 1) / BN : 0;
+  const bf16_t* kp = p.k + b * p.k_sb + hk * p.k_sh;
+  const bf16_t* vp = p.v + b * p.v_sb + hk * p.v_sh;
+  Stager<D, BN, 256> sk, sv;
+  if (ntiles > 0) {
+    const bool full = dfull && BN <= p.Sk;
+    sk.load(kp, p.k_st, 0, p.Sk, p.d_real, full);
+    sv.load(vp, p.v_st, 0, p.Sk, p.d_real, full);
+    store_swz(sk, smem);
+    store_swz(sv, smem + TSZ);
+  }
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const int k0 = t * BN;
+    const bf16_t* Ks = smem + (t & 1) * 2 * TSZ;
+    const bf16_t* Vs = Ks + TSZ;
+    if (t + 1 < ntiles) {
+      const bool full = dfull && (k0 + 2 * BN <= p.Sk);
+      sk.load(kp, p.k_st, k0 + BN, p.Sk, p.d_real, full);
+      sv.load(vp, p.v_st, k0 + BN, p.Sk, p.d_real, full);
+    }
+    const bool active = !CAUSAL || (k0 <= qw + 31 + off);
+    if (active) {
+      f32x16 st, dpt;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { st[r] = 0.f; dpt[r] = 0.f; }
+#pragma unroll
+      for (int s = 0; s < D / 16; ++s) {
+        const int o = swz_off<D>(l32, 2 * s + hh);
+        st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld_bf16x8(Ks + o), qf[s], st, 0, 0, 0);
+        dpt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld_bf16x8(Vs + o), gf[s], dpt, 0, 0, 0);
+      }
+      const bool need_mask = (CAUSAL && (k0 + BN - 1 > qw + off)) || (k0 + BN > kv_end) || (qw + 32 > p.Sq);
+      float dsv[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = k0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        float x = st[r] * sl2 - lse_q;
+        if (p.alibi) x += slope * (float)(key - q - off);
+        float pr = exp2f(x);
+        if (need_mask) {
+          bool valid = q < p.Sq && key < kv_end;
+          if (CAUSAL) valid = valid && (key <= q + off);
+          pr = valid ? pr : 0.f;
+        }
+        dsv[r] = pr * (dpt[r] - dl_q);
+      }
+      const bf16x8 d0 = to_bf16x8(dsv), d1 = to_bf16x8(dsv + 8);
+#pragma unroll
+      for (int db = 0; db < D / 32; ++db) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+          dq[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_a32<D>(Ks, s, hh, lane, db), s ? d1 : d0,
+                                                           dq[db], 0, 0, 0);
+      }
+    }
+    if (t + 1 < ntiles) {
+      bf16_t* Kn = smem + ((t + 1) & 1) * 2 * TSZ;
+      store_swz(sk, Kn);
+      store_swz(sv, Kn + TSZ);
+    }
+    __syncthreads();
+  }
+  if (q < p.Sq) {
+    bf16_t* dqp = p.dq + b * p.dq_sb + h * p.dq_sh + (long long)q * p.dq_st;
+#pragma unroll
+    for (int db = 0; db < D / 32; ++db) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = db * 32 + 8 * g + 4 * hh;
+        if (d < p.d_real) {
+          uint2 w;
+          w.x = pack_bf16x2(dq[db][4 * g] * p.scale, dq[db][4 * g + 1] * p.scale);
+          w.y = pack_bf16x2(dq[db][4 * g + 2] * p.scale, dq[db][4 * g + 3] * p.scale);
+          *reinterpret_cast<uint2*>(dqp + d) = w;
+        }
+      }
+    }
+  }
+}
+
 // ============================================================== host API
 static int pick_d(int d) {
   if (d <= 64) return 64;
@@ -718,6 +1023,31 @@ KCA_API int kca_attn_bwd(const void* q, const void* k, const void* v,
                   do_sb, do_st, do_sh, dq_sb, dq_st, dq_sh, dk_sb, dk_st, dk_sh,
                   dv_sb, dv_st, dv_sh,
                   B, Sq, Sk, H, Hkv, d_real, causal, scale, alibi, kv_len};
+  if (D == 128 || D == 256) {  // 32-wide MFMA kernels (see above)
+    dim3 h1((Sk + 127) / 128, B * Hkv);
+    dim3 h2((Sq + 127) / 128, B * H);
+    dim3 g1w((Sk + 63) / 64, B * Hkv);
+    if (D == 128) {
+      if (causal) {
+        hipLaunchKernelGGL((attn_bwd_dkdv32_kernel<128, true>), h1, dim3(256), 0, stream, p);
+        hipLaunchKernelGGL((attn_bwd_dq32_kernel<128, true>), h2, dim3(256), 0, stream, p);
+      } else {
+        hipLaunchKernelGGL((attn_bwd_dkdv32_kernel<128, false>), h1, dim3(256), 0, stream, p);
+        hipLaunchKernelGGL((attn_bwd_dq32_kernel<128, false>), h2, dim3(256), 0, stream, p);
+      }
+    } else {
+      // D = 256: K, V, dK^T, dV^T of 32 keys exceed the 512-register file, so
+      // the dK/dV pass keeps 16 keys per wave; dQ uses the 32-wide kernel.
+      if (causal) {
+        hipLaunchKernelGGL((attn_bwd_dkdv_kernel<256, true>), g1w, dim3(256), 0, stream, p);
+        hipLaunchKernelGGL((attn_bwd_dq32_kernel<256, true>), h2, dim3(256), 0, stream, p);
+      } else {
+        hipLaunchKernelGGL((attn_bwd_dkdv_kernel<256, false>), g1w, dim3(256), 0, stream, p);
+        hipLaunchKernelGGL((attn_bwd_dq32_kernel<256, false>), h2, dim3(256), 0, stream, p);
+      }
+    }
+    return 0;
+  }
   dim3 g1((Sk + 63) / 64, B * Hkv);
   dim3 g2((Sq + 63) / 64, B * H);
   ATTN_D_DISPATCH(D, {
