@@ -50,7 +50,7 @@ _SIGS = {
     "kca_attn_fwd": [P] * 5 + [LL] * 12 + [I] * 7 + [F, P, P, I, P],
     "kca_attn_bwd_preprocess": [P, P, P, LL, LL, LL, LL, LL, LL, I, I, I, I, P],
     "kca_attn_bwd": [P] * 10 + [LL] * 21 + [I] * 7 + [F, P, P, P],
-    "kca_groupnorm_fwd": [P, P, P, P, P, P, I, I, I, I, F, I, P],
+    "kca_groupnorm_fwd": [P, P, P, P, P, P, P, I, I, I, I, F, I, P],
     "kca_groupnorm_bwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P],
     "kca_sample_logits": [P, LL, I, I, P, P, P, P, P, P, P, P, P, I, P],
     "kca_decode_attn": [P] * 6 + [LL] * 8 + [I] * 7 + [F, P, P],

@@ -93,8 +93,9 @@ class _GroupNormFn(torch.autograd.Function):
         y = torch.empty_like(x)
         mean = torch.empty(n * groups, device=x.device, dtype=torch.float32)
         rstd = torch.empty_like(mean)
+        part = torch.empty(2 * n * c, device=x.device, dtype=torch.float32)
         _lib.call("kca_groupnorm_fwd", x.data_ptr(), weight.data_ptr(), _lib.ptr(bias),
-                  y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), n, c, hw, groups,
+                  y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), part.data_ptr(), n, c, hw, groups,
                   float(eps), int(silu), _lib.stream())
         ctx.save_for_backward(x, weight, bias, mean, rstd)
         ctx.groups, ctx.silu = groups, silu
@@ -109,7 +110,7 @@ class _GroupNormFn(torch.autograd.Function):
         dx = torch.empty_like(x)
         dw = torch.empty_like(weight)
         db = torch.empty_like(weight)
-        ws = torch.empty(2 * n * c, device=x.device, dtype=torch.float32)
+        ws = torch.empty(4 * n * c, device=x.device, dtype=torch.float32)
         _lib.call("kca_groupnorm_bwd", dy.data_ptr(), x.data_ptr(), weight.data_ptr(),
                   _lib.ptr(bias), mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(),
                   dw.data_ptr(), db.data_ptr(), ws.data_ptr(), n, c, hw, ctx.groups,

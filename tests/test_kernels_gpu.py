@@ -169,3 +169,24 @@ def test_qkv_rope_attention_matches_reference():
     ref = ops.qkv_rope_attention(qr, H, D, rot, True)
     ref.backward(g.float().cpu())
     assert _rel(qkv2.grad.cpu(), qr.grad) < 3e-2
+
+
+@pytest.mark.parametrize("N,C,H,W,G,silu", [(2, 320, 16, 16, 32, True), (1, 128, 64, 64, 32, False),
+                                            (2, 1280, 8, 8, 32, True), (1, 40, 5, 7, 8, True)])
+def test_groupnorm(N, C, H, W, G, silu):
+    torch.manual_seed(0)
+    x = (torch.randn(N, C, H, W, device=DEV) * 2 + 3).bfloat16().requires_grad_()
+    w = (1 + 0.1 * torch.randn(C, device=DEV)).bfloat16().requires_grad_()
+    b = (0.1 * torch.randn(C, device=DEV)).bfloat16().requires_grad_()
+    y = ops.group_norm(x, G, w, b, 1e-5, silu=silu)
+    xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, b))
+    yr = F.group_norm(xr, G, wr, br, 1e-5)
+    if silu:
+        yr = F.silu(yr)
+    assert _rel(y, yr) < 1e-2
+    g = torch.randn_like(y)
+    y.backward(g)
+    yr.backward(g.float())
+    assert _rel(x.grad, xr.grad) < 2e-2
+    assert _rel(w.grad, wr.grad) < 2e-2
+    assert _rel(b.grad, br.grad) < 2e-2
