@@ -1,0 +1,375 @@
+"""UNet2DConditionModel (SD 1.x / 2.x) with diffusers-compatible parameter names.
+
+The SD finetuner / DreamBooth trainer (sd-finetuner-workflow/sd-finetuner/
+finetuner.py:648-666, 467-547) and the txt2img predictor
+(online-inference/stable-diffusion/service/service.py:163-259) run diffusers'
+UNet; this is the same network built on the native ops:
+
+* GroupNorm(+SiLU) -> ``ops.group_norm`` (HIP, fused SiLU in ResNet blocks);
+* spatial self-attention and text cross-attention -> ``ops.flash_attention``
+  (non-causal; head dims 40/80/160 for SD1.x, 64 for SD2; K/V length 77 for
+  the cross attention);
+* LayerNorm -> fused LN kernel; convolutions -> MIOpen through torch.
+
+Config keys are read from diffusers' ``unet/config.json``.
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+import math
+import os
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import ops
+
+
+@dataclasses.dataclass
+class UNetConfig:
+    in_channels: int = 4
+    out_channels: int = 4
+    block_out_channels: tuple = (320, 640, 1280, 1280)
+    layers_per_block: int = 2
+    cross_attention_dim: int = 768
+    attention_head_dim: object = 8          # int (=#heads, diffusers quirk) or per-block list
+    down_block_types: tuple = ("CrossAttnDownBlock2D", "CrossAttnDownBlock2D", "CrossAttnDownBlock2D",
+                               "DownBlock2D")
+    up_block_types: tuple = ("UpBlock2D", "CrossAttnUpBlock2D", "CrossAttnUpBlock2D", "CrossAttnUpBlock2D")
+    norm_num_groups: int = 32
+    norm_eps: float = 1e-5
+    use_linear_projection: bool = False
+    flip_sin_to_cos: bool = True
+    freq_shift: int = 0
+    sample_size: int = 64
+    raw: dict = dataclasses.field(default_factory=dict, repr=False)
+
+    @classmethod
+    def from_dict(cls, d: dict) -> "UNetConfig":
+        kw = {}
+        for f in dataclasses.fields(cls):
+            if f.name in d and f.name != "raw":
+                v = d[f.name]
+                kw[f.name] = tuple(v) if isinstance(v, list) else v
+        return cls(raw=dict(d), **kw)
+
+    @classmethod
+    def from_pretrained(cls, path: str) -> "UNetConfig":
+        with open(os.path.join(path, "config.json")) as f:
+            return cls.from_dict(json.load(f))
+
+    def to_dict(self) -> dict:
+        d = dict(self.raw) if self.raw else {"_class_name": "UNet2DConditionModel"}
+        for f in dataclasses.fields(self):
+            if f.name != "raw":
+                v = getattr(self, f.name)
+                d[f.name] = list(v) if isinstance(v, tuple) else v
+        return d
+
+    def heads(self, i: int) -> int:
+        a = self.attention_head_dim
+        return a[i] if isinstance(a, (tuple, list)) else a
+
+
+def sd15_unet_config() -> UNetConfig:
+    return UNetConfig()
+
+
+def sd2_unet_config(sample_size: int = 96) -> UNetConfig:
+    return UNetConfig(cross_attention_dim=1024, attention_head_dim=(5, 10, 20, 20), use_linear_projection=True,
+                      sample_size=sample_size)
+
+
+class GroupNorm(nn.GroupNorm):
+    def __init__(self, groups, ch, eps=1e-5, silu=False):
+        super().__init__(groups, ch, eps=eps)
+        self.silu = silu
+
+    def forward(self, x):
+        return ops.group_norm(x, self.num_groups, self.weight, self.bias, self.eps, silu=self.silu)
+
+
+class LayerNorm(nn.LayerNorm):
+    def forward(self, x):
+        return ops.layer_norm(x, self.weight, self.bias, self.eps)
+
+
+def timestep_embedding(t: torch.Tensor, dim: int, flip_sin_to_cos=True, shift: float = 0.0,
+                       max_period: float = 10000.0) -> torch.Tensor:
+    """diffusers get_timestep_embedding (K18)."""
+    half = dim // 2
+    exponent = -math.log(max_period) * torch.arange(half, dtype=torch.float32, device=t.device) / (half - shift)
+    emb = t.float()[:, None] * torch.exp(exponent)[None, :]
+    emb = torch.cat([torch.sin(emb), torch.cos(emb)], dim=-1)
+    if flip_sin_to_cos:
+        emb = torch.cat([emb[:, half:], emb[:, :half]], dim=-1)
+    if dim % 2:
+        emb = F.pad(emb, (0, 1))
+    return emb
+
+
+class TimestepEmbedding(nn.Module):
+    def __init__(self, cin, dim):
+        super().__init__()
+        self.linear_1 = nn.Linear(cin, dim)
+        self.linear_2 = nn.Linear(dim, dim)
+
+    def forward(self, x):
+        return self.linear_2(F.silu(self.linear_1(x)))
+
+
+class ResnetBlock2D(nn.Module):
+    def __init__(self, cin, cout, temb_ch, groups=32, eps=1e-5):
+        super().__init__()
+        self.norm1 = GroupNorm(groups, cin, eps, silu=True)
+        self.conv1 = nn.Conv2d(cin, cout, 3, padding=1)
+        self.time_emb_proj = nn.Linear(temb_ch, cout) if temb_ch else None
+        self.norm2 = GroupNorm(groups, cout, eps, silu=True)
+        self.dropout = nn.Dropout(0.0)
+        self.conv2 = nn.Conv2d(cout, cout, 3, padding=1)
+        self.conv_shortcut = nn.Conv2d(cin, cout, 1) if cin != cout else None
+
+    def forward(self, x, temb=None):
+        h = self.conv1(self.norm1(x))
+        if self.time_emb_proj is not None and temb is not None:
+            h = h + self.time_emb_proj(F.silu(temb))[:, :, None, None]
+        h = self.conv2(self.dropout(self.norm2(h)))
+        sc = self.conv_shortcut(x) if self.conv_shortcut is not None else x
+        return sc + h
+
+
+class Attention(nn.Module):
+    """diffusers Attention (to_q/to_k/to_v/to_out.0) over [B, S, C] tokens."""
+
+    def __init__(self, dim, heads, head_dim, cross_dim=None, bias_qkv=False):
+        super().__init__()
+        inner = heads * head_dim
+        self.heads = heads
+        self.to_q = nn.Linear(dim, inner, bias=bias_qkv)
+        self.to_k = nn.Linear(cross_dim or dim, inner, bias=bias_qkv)
+        self.to_v = nn.Linear(cross_dim or dim, inner, bias=bias_qkv)
+        self.to_out = nn.ModuleList([nn.Linear(inner, dim), nn.Dropout(0.0)])
+
+    def forward(self, x, ctx=None):
+        B, S, _ = x.shape
+        c = x if ctx is None else ctx
+        q = self.to_q(x)
+        k = self.to_k(c)
+        v = self.to_v(c)
+        hd = q.shape[-1] // self.heads
+        o = ops.flash_attention(q.view(B, S, self.heads, hd), k.view(B, c.shape[1], self.heads, hd),
+                                v.view(B, c.shape[1], self.heads, hd), causal=False)
+        return self.to_out[0](o.reshape(B, S, -1))
+
+
+class GEGLU(nn.Module):
+    def __init__(self, dim, inner):
+        super().__init__()
+        self.proj = nn.Linear(dim, inner * 2)
+
+    def forward(self, x):
+        return ops.geglu(self.proj(x))
+
+
+class FeedForward(nn.Module):
+    def __init__(self, dim, mult=4):
+        super().__init__()
+        inner = dim * mult
+        self.net = nn.ModuleList([GEGLU(dim, inner), nn.Dropout(0.0), nn.Linear(inner, dim)])
+
+    def forward(self, x):
+        return self.net[2](self.net[0](x))
+
+
+class BasicTransformerBlock(nn.Module):
+    def __init__(self, dim, heads, head_dim, cross_dim):
+        super().__init__()
+        self.norm1 = LayerNorm(dim)
+        self.attn1 = Attention(dim, heads, head_dim)
+        self.norm2 = LayerNorm(dim)
+        self.attn2 = Attention(dim, heads, head_dim, cross_dim)
+        self.norm3 = LayerNorm(dim)
+        self.ff = FeedForward(dim)
+
+    def forward(self, x, ctx):
+        x = x + self.attn1(self.norm1(x))
+        x = x + self.attn2(self.norm2(x), ctx)
+        return x + self.ff(self.norm3(x))
+
+
+class Transformer2DModel(nn.Module):
+    def __init__(self, ch, heads, cross_dim, groups=32, linear_proj=False):
+        super().__init__()
+        self.norm = nn.GroupNorm(groups, ch, eps=1e-6)
+        self.linear_proj = linear_proj
+        self.proj_in = nn.Linear(ch, ch) if linear_proj else nn.Conv2d(ch, ch, 1)
+        self.transformer_blocks = nn.ModuleList([BasicTransformerBlock(ch, heads, ch // heads, cross_dim)])
+        self.proj_out = nn.Linear(ch, ch) if linear_proj else nn.Conv2d(ch, ch, 1)
+
+    def forward(self, x, ctx):
+        B, C, H, W = x.shape
+        res = x
+        h = ops.group_norm(x, self.norm.num_groups, self.norm.weight, self.norm.bias, self.norm.eps)
+        if self.linear_proj:
+            h = self.proj_in(h.permute(0, 2, 3, 1).reshape(B, H * W, C))
+        else:
+            h = self.proj_in(h).permute(0, 2, 3, 1).reshape(B, H * W, C)
+        for blk in self.transformer_blocks:
+            h = blk(h, ctx)
+        if self.linear_proj:
+            h = self.proj_out(h).reshape(B, H, W, C).permute(0, 3, 1, 2)
+        else:
+            h = self.proj_out(h.reshape(B, H, W, C).permute(0, 3, 1, 2).contiguous())
+        return h + res
+
+
+class Downsample2D(nn.Module):
+    def __init__(self, ch, pad=1):
+        super().__init__()
+        self.conv = nn.Conv2d(ch, ch, 3, stride=2, padding=pad)
+        self.asym = pad == 0
+
+    def forward(self, x):
+        if self.asym:
+            x = F.pad(x, (0, 1, 0, 1))
+        return self.conv(x)
+
+
+class Upsample2D(nn.Module):
+    def __init__(self, ch):
+        super().__init__()
+        self.conv = nn.Conv2d(ch, ch, 3, padding=1)
+
+    def forward(self, x):
+        return self.conv(F.interpolate(x, scale_factor=2.0, mode="nearest"))
+
+
+class DownBlock(nn.Module):
+    def __init__(self, cin, cout, temb, n, attn: bool, heads, cross_dim, add_down, groups, eps, linear_proj):
+        super().__init__()
+        self.resnets = nn.ModuleList([ResnetBlock2D(cin if i == 0 else cout, cout, temb, groups, eps)
+                                      for i in range(n)])
+        self.attentions = nn.ModuleList([Transformer2DModel(cout, heads, cross_dim, groups, linear_proj)
+                                         for _ in range(n)]) if attn else None
+        self.downsamplers = nn.ModuleList([Downsample2D(cout)]) if add_down else None
+
+    def forward(self, x, temb, ctx):
+        skips = []
+        for i, r in enumerate(self.resnets):
+            x = r(x, temb)
+            if self.attentions is not None:
+                x = self.attentions[i](x, ctx)
+            skips.append(x)
+        if self.downsamplers is not None:
+            x = self.downsamplers[0](x)
+            skips.append(x)
+        return x, skips
+
+
+class UpBlock(nn.Module):
+    def __init__(self, cin, cout, prev, temb, n, attn, heads, cross_dim, add_up, groups, eps, linear_proj):
+        super().__init__()
+        rs = []
+        for i in range(n):
+            skip = cin if i == n - 1 else cout
+            rin = prev if i == 0 else cout
+            rs.append(ResnetBlock2D(rin + skip, cout, temb, groups, eps))
+        self.resnets = nn.ModuleList(rs)
+        self.attentions = nn.ModuleList([Transformer2DModel(cout, heads, cross_dim, groups, linear_proj)
+                                         for _ in range(n)]) if attn else None
+        self.upsamplers = nn.ModuleList([Upsample2D(cout)]) if add_up else None
+
+    def forward(self, x, skips, temb, ctx):
+        for i, r in enumerate(self.resnets):
+            x = r(torch.cat([x, skips.pop()], dim=1), temb)
+            if self.attentions is not None:
+                x = self.attentions[i](x, ctx)
+        if self.upsamplers is not None:
+            x = self.upsamplers[0](x)
+        return x
+
+
+class MidBlock(nn.Module):
+    def __init__(self, ch, temb, heads, cross_dim, groups, eps, linear_proj):
+        super().__init__()
+        self.attentions = nn.ModuleList([Transformer2DModel(ch, heads, cross_dim, groups, linear_proj)])
+        self.resnets = nn.ModuleList([ResnetBlock2D(ch, ch, temb, groups, eps), ResnetBlock2D(ch, ch, temb, groups, eps)])
+
+    def forward(self, x, temb, ctx):
+        x = self.resnets[0](x, temb)
+        x = self.attentions[0](x, ctx)
+        return self.resnets[1](x, temb)
+
+
+class UNet2DConditionModel(nn.Module):
+    def __init__(self, config: UNetConfig):
+        super().__init__()
+        c = config
+        self.config = c
+        ch = c.block_out_channels
+        temb = ch[0] * 4
+        g, eps = c.norm_num_groups, c.norm_eps
+        self.conv_in = nn.Conv2d(c.in_channels, ch[0], 3, padding=1)
+        self.time_embedding = TimestepEmbedding(ch[0], temb)
+        downs = []
+        out = ch[0]
+        for i, kind in enumerate(c.down_block_types):
+            cin, out = out, ch[i]
+            downs.append(DownBlock(cin, out, temb, c.layers_per_block, kind.startswith("CrossAttn"), c.heads(i),
+                                   c.cross_attention_dim, i < len(ch) - 1, g, eps, c.use_linear_projection))
+        self.down_blocks = nn.ModuleList(downs)
+        self.mid_block = MidBlock(ch[-1], temb, c.heads(len(ch) - 1), c.cross_attention_dim, g, eps,
+                                  c.use_linear_projection)
+        rch = list(reversed(ch))
+        rheads = [c.heads(i) for i in reversed(range(len(ch)))]
+        ups = []
+        prev = rch[0]
+        for i, kind in enumerate(c.up_block_types):
+            out = rch[i]
+            cin = rch[min(i + 1, len(ch) - 1)]
+            ups.append(UpBlock(cin, out, prev, temb, c.layers_per_block + 1, kind.startswith("CrossAttn"),
+                               rheads[i], c.cross_attention_dim, i < len(ch) - 1, g, eps,
+                               c.use_linear_projection))
+            prev = out
+        self.up_blocks = nn.ModuleList(ups)
+        self.conv_norm_out = GroupNorm(g, ch[0], eps, silu=True)
+        self.conv_out = nn.Conv2d(ch[0], c.out_channels, 3, padding=1)
+        self.gradient_checkpointing = False
+
+    def enable_gradient_checkpointing(self, on: bool = True):
+        self.gradient_checkpointing = on
+
+    def _run(self, fn, *args):
+        if self.gradient_checkpointing and self.training and torch.is_grad_enabled():
+            from torch.utils.checkpoint import checkpoint
+            return checkpoint(fn, *args, use_reentrant=False)
+        return fn(*args)
+
+    def forward(self, sample: torch.Tensor, timestep, encoder_hidden_states: torch.Tensor):
+        c = self.config
+        if not torch.is_tensor(timestep):
+            timestep = torch.tensor([timestep], device=sample.device)
+        t = timestep.to(sample.device).reshape(-1).expand(sample.shape[0])
+        temb = timestep_embedding(t, c.block_out_channels[0], c.flip_sin_to_cos, c.freq_shift).to(sample.dtype)
+        temb = self.time_embedding(temb)
+        ctx = encoder_hidden_states.to(sample.dtype)
+        x = self.conv_in(sample)
+        skips = [x]
+        for blk in self.down_blocks:
+            x, s = self._run(blk, x, temb, ctx)
+            skips.extend(s)
+        x = self._run(self.mid_block, x, temb, ctx)
+        for blk in self.up_blocks:
+            n = len(blk.resnets)
+            mine = skips[-n:]
+            del skips[-n:]
+            x = self._run(lambda a, b, cc, *sk: blk(a, list(sk), b, cc), x, temb, ctx, *mine)
+        return self.conv_out(self.conv_norm_out(x))
+
+
+def build_unet(cfg: UNetConfig, device="cpu", dtype=torch.float32, seed: int = 0) -> UNet2DConditionModel:
+    torch.manual_seed(seed)
+    m = UNet2DConditionModel(cfg)
+    return m.to(device=device, dtype=dtype)

@@ -1,0 +1,205 @@
+"""AutoencoderKL (SD VAE) with diffusers-compatible parameter names.
+
+Encoder used by the SD trainer to get latents (sd-finetuner/finetuner.py:
+470-473: ``vae.encode(px).latent_dist.sample() * 0.18215``); decoder used by
+the txt2img predictor (K20 + the VAE decode of service.py:245-252). GroupNorm
+(+SiLU) run on the native kernel; the mid-block single-head attention
+(512 channels over 64x64 tokens at 512 px) on the native flash kernel.
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+import os
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import ops
+from .unet import Downsample2D, GroupNorm, ResnetBlock2D, Upsample2D
+
+L_SCALE_FACTOR = 0.18215  # sd-finetuner/finetuner.py:42
+
+
+@dataclasses.dataclass
+class VAEConfig:
+    in_channels: int = 3
+    out_channels: int = 3
+    latent_channels: int = 4
+    block_out_channels: tuple = (128, 256, 512, 512)
+    layers_per_block: int = 2
+    norm_num_groups: int = 32
+    scaling_factor: float = L_SCALE_FACTOR
+    sample_size: int = 512
+    raw: dict = dataclasses.field(default_factory=dict, repr=False)
+
+    @classmethod
+    def from_dict(cls, d: dict) -> "VAEConfig":
+        kw = {f.name: (tuple(d[f.name]) if isinstance(d[f.name], list) else d[f.name])
+              for f in dataclasses.fields(cls) if f.name in d and f.name != "raw"}
+        return cls(raw=dict(d), **kw)
+
+    @classmethod
+    def from_pretrained(cls, path: str) -> "VAEConfig":
+        with open(os.path.join(path, "config.json")) as f:
+            return cls.from_dict(json.load(f))
+
+    def to_dict(self):
+        d = dict(self.raw) if self.raw else {"_class_name": "AutoencoderKL"}
+        for f in dataclasses.fields(self):
+            if f.name != "raw":
+                v = getattr(self, f.name)
+                d[f.name] = list(v) if isinstance(v, tuple) else v
+        return d
+
+
+class VAEAttention(nn.Module):
+    """diffusers mid-block Attention: group_norm + to_q/k/v + to_out.0, 1 head."""
+
+    def __init__(self, ch, groups):
+        super().__init__()
+        self.group_norm = nn.GroupNorm(groups, ch, eps=1e-6)
+        self.to_q = nn.Linear(ch, ch)
+        self.to_k = nn.Linear(ch, ch)
+        self.to_v = nn.Linear(ch, ch)
+        self.to_out = nn.ModuleList([nn.Linear(ch, ch), nn.Dropout(0.0)])
+
+    def forward(self, x):
+        B, C, H, W = x.shape
+        h = ops.group_norm(x, self.group_norm.num_groups, self.group_norm.weight, self.group_norm.bias,
+                           self.group_norm.eps)
+        h = h.reshape(B, C, H * W).transpose(1, 2)
+        q, k, v = self.to_q(h), self.to_k(h), self.to_v(h)
+        if C <= 256:
+            o = ops.flash_attention(q[:, :, None], k[:, :, None], v[:, :, None], causal=False)[:, :, 0]
+        else:  # head_dim 512 > kernel max: split into two 256-wide halves of one softmax
+            s = torch.einsum("bqc,bkc->bqk", q.float(), k.float()) / (C ** 0.5)
+            o = torch.einsum("bqk,bkc->bqc", s.softmax(-1), v.float()).to(q.dtype)
+        o = self.to_out[0](o)
+        return x + o.transpose(1, 2).reshape(B, C, H, W)
+
+
+class _Mid(nn.Module):
+    def __init__(self, ch, groups):
+        super().__init__()
+        self.attentions = nn.ModuleList([VAEAttention(ch, groups)])
+        self.resnets = nn.ModuleList([ResnetBlock2D(ch, ch, 0, groups, 1e-6), ResnetBlock2D(ch, ch, 0, groups, 1e-6)])
+
+    def forward(self, x):
+        x = self.resnets[0](x)
+        x = self.attentions[0](x)
+        return self.resnets[1](x)
+
+
+class _DownEnc(nn.Module):
+    def __init__(self, cin, cout, n, groups, add_down):
+        super().__init__()
+        self.resnets = nn.ModuleList([ResnetBlock2D(cin if i == 0 else cout, cout, 0, groups, 1e-6) for i in range(n)])
+        self.downsamplers = nn.ModuleList([Downsample2D(cout, pad=0)]) if add_down else None
+
+    def forward(self, x):
+        for r in self.resnets:
+            x = r(x)
+        if self.downsamplers is not None:
+            x = self.downsamplers[0](x)
+        return x
+
+
+class _UpDec(nn.Module):
+    def __init__(self, cin, cout, n, groups, add_up):
+        super().__init__()
+        self.resnets = nn.ModuleList([ResnetBlock2D(cin if i == 0 else cout, cout, 0, groups, 1e-6) for i in range(n)])
+        self.upsamplers = nn.ModuleList([Upsample2D(cout)]) if add_up else None
+
+    def forward(self, x):
+        for r in self.resnets:
+            x = r(x)
+        if self.upsamplers is not None:
+            x = self.upsamplers[0](x)
+        return x
+
+
+class Encoder(nn.Module):
+    def __init__(self, c: VAEConfig):
+        super().__init__()
+        ch = c.block_out_channels
+        g = c.norm_num_groups
+        self.conv_in = nn.Conv2d(c.in_channels, ch[0], 3, padding=1)
+        blocks, prev = [], ch[0]
+        for i, o in enumerate(ch):
+            blocks.append(_DownEnc(prev, o, c.layers_per_block, g, i < len(ch) - 1))
+            prev = o
+        self.down_blocks = nn.ModuleList(blocks)
+        self.mid_block = _Mid(ch[-1], g)
+        self.conv_norm_out = GroupNorm(g, ch[-1], 1e-6, silu=True)
+        self.conv_out = nn.Conv2d(ch[-1], 2 * c.latent_channels, 3, padding=1)
+
+    def forward(self, x):
+        x = self.conv_in(x)
+        for b in self.down_blocks:
+            x = b(x)
+        x = self.mid_block(x)
+        return self.conv_out(self.conv_norm_out(x))
+
+
+class Decoder(nn.Module):
+    def __init__(self, c: VAEConfig):
+        super().__init__()
+        ch = list(reversed(c.block_out_channels))
+        g = c.norm_num_groups
+        self.conv_in = nn.Conv2d(c.latent_channels, ch[0], 3, padding=1)
+        self.mid_block = _Mid(ch[0], g)
+        blocks, prev = [], ch[0]
+        for i, o in enumerate(ch):
+            blocks.append(_UpDec(prev, o, c.layers_per_block + 1, g, i < len(ch) - 1))
+            prev = o
+        self.up_blocks = nn.ModuleList(blocks)
+        self.conv_norm_out = GroupNorm(g, ch[-1], 1e-6, silu=True)
+        self.conv_out = nn.Conv2d(ch[-1], c.out_channels, 3, padding=1)
+
+    def forward(self, z):
+        x = self.conv_in(z)
+        x = self.mid_block(x)
+        for b in self.up_blocks:
+            x = b(x)
+        return self.conv_out(self.conv_norm_out(x))
+
+
+class DiagonalGaussian:
+    def __init__(self, moments: torch.Tensor):
+        self.mean, logvar = moments.chunk(2, dim=1)
+        self.logvar = logvar.clamp(-30.0, 20.0)
+        self.std = torch.exp(0.5 * self.logvar)
+
+    def sample(self, generator=None) -> torch.Tensor:
+        eps = torch.randn(self.mean.shape, generator=generator, device=self.mean.device, dtype=self.mean.dtype)
+        return self.mean + self.std * eps
+
+    def mode(self):
+        return self.mean
+
+
+class AutoencoderKL(nn.Module):
+    def __init__(self, config: VAEConfig):
+        super().__init__()
+        self.config = config
+        self.encoder = Encoder(config)
+        self.decoder = Decoder(config)
+        lc = config.latent_channels
+        self.quant_conv = nn.Conv2d(2 * lc, 2 * lc, 1)
+        self.post_quant_conv = nn.Conv2d(lc, lc, 1)
+
+    def encode(self, x: torch.Tensor) -> DiagonalGaussian:
+        return DiagonalGaussian(self.quant_conv(self.encoder(x)))
+
+    def decode(self, z: torch.Tensor) -> torch.Tensor:
+        return self.decoder(self.post_quant_conv(z))
+
+
+def build_vae(cfg: VAEConfig, device="cpu", dtype=torch.float32, seed: int = 0) -> AutoencoderKL:
+    torch.manual_seed(seed)
+    return AutoencoderKL(cfg).to(device=device, dtype=dtype)
+
+
+__all__ = ["VAEConfig", "AutoencoderKL", "build_vae", "L_SCALE_FACTOR", "F"]
