@@ -1,0 +1,140 @@
+#!/usr/bin/env python3
+"""SD-1.5 benchmarks (BASELINE.json configs 3 and 5) on random-init weights.
+
+  --mode train : DreamBooth UNet finetune step (instance + class batch, frozen
+                 VAE encode + CLIP encode, UNet fwd/bwd, prior-preservation MSE,
+                 fused AdamW) -> samples/s (the reference's
+                 perf/world_samples_per_second definition, sd-finetuner/
+                 finetuner.py:563-568, counting instance+class images)
+  --mode infer : txt2img batch 8, 512x512, 50 steps, CFG 7.0, incl. VAE decode,
+                 excl. PNG encode -> images/s
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch
+
+
+def build(dev, dtype):
+    from kubernetes_cloud_amd.models.clip_text import CLIPTextConfig, build_clip_text
+    from kubernetes_cloud_amd.models.unet import UNetConfig, build_unet
+    from kubernetes_cloud_amd.models.vae import VAEConfig, build_vae
+    unet = build_unet(UNetConfig(), device=dev, dtype=dtype)
+    vae = build_vae(VAEConfig(), device=dev, dtype=dtype)
+    te = build_clip_text(CLIPTextConfig(), device=dev, dtype=dtype)
+    return unet, vae, te
+
+
+def bench_train(args, dev):
+    from kubernetes_cloud_amd.models.schedulers import DDPMScheduler, sd_scheduler_config
+    from kubernetes_cloud_amd.ops import mse_loss
+    from kubernetes_cloud_amd.train.engine import TrainEngine
+    unet, vae, te = build(dev, torch.bfloat16)
+    vae.requires_grad_(False)
+    te.requires_grad_(False)
+    if args.ckpt:
+        unet.enable_gradient_checkpointing()
+    unet.train()
+    eng = TrainEngine(unet, lr=5e-6, weight_decay=1e-2, max_grad_norm=1.0, zero_stage=0)
+    sch = DDPMScheduler.from_config(sd_scheduler_config())
+    B = args.batch  # instance images per step; class images double it
+    px = torch.randn(2 * B, 3, args.res, args.res, device=dev, dtype=torch.bfloat16)
+    ids = torch.randint(0, 49408, (2 * B, 77), device=dev)
+
+    def step():
+        with torch.no_grad():
+            lat = vae.encode(px).sample() * 0.18215
+            ctx = te(ids)
+        noise = torch.randn_like(lat)
+        t = torch.randint(0, 1000, (lat.shape[0],), device=dev)
+        pred = unet(sch.add_noise(lat, noise, t), t, ctx)
+        pi, pc = pred.chunk(2)
+        ni, nc = noise.chunk(2)
+        loss = mse_loss(pi, ni) + mse_loss(pc, nc)
+        eng.backward(loss)
+        eng.step(5e-6)
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    sps = args.steps * 2 * B / dt
+    return {"metric": "SD-1.5 DreamBooth UNet finetune samples/sec", "value": round(sps, 2),
+            "unit": "samples/s", "ms_per_step": round(dt / args.steps * 1e3, 2), "loss": float(loss.item()),
+            "config": {"instance_batch": B, "class_batch": B, "resolution": args.res, "dtype": "bf16",
+                       "grad_ckpt": args.ckpt, "peak_mem_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1)}}
+
+
+def bench_infer(args, dev):
+    from kubernetes_cloud_amd.models.schedulers import load_scheduler, sd_scheduler_config
+    unet, vae, te = build(dev, torch.bfloat16)
+    for m in (unet, vae, te):
+        m.eval()
+    sch = load_scheduler(sd_scheduler_config(), args.scheduler)
+    B, steps, g = args.batch, args.infer_steps, 7.0
+    ids = torch.randint(0, 49408, (2 * B, 77), device=dev)
+
+    @torch.no_grad()
+    def run():
+        ctx = te(ids)
+        sch.set_timesteps(steps, device=dev)
+        x = torch.randn(B, 4, args.res // 8, args.res // 8, device=dev) * sch.init_noise_sigma
+        for t in sch.timesteps:
+            xin = sch.scale_model_input(torch.cat([x, x]), t).to(torch.bfloat16)
+            eps = unet(xin, torch.full((2 * B,), float(t), device=dev), ctx).float()
+            eu, ec = eps.chunk(2)
+            x = sch.step(eu + g * (ec - eu), t, x).float()
+        return vae.decode((x / 0.18215).to(torch.bfloat16))
+
+    for _ in range(args.warmup):
+        run()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        img = run()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    ips = args.steps * B / dt
+    return {"metric": "SD-1.5 txt2img images/sec", "value": round(ips, 3), "unit": "images/s",
+            "ms_per_batch": round(dt / args.steps * 1e3, 1),
+            "config": {"batch": B, "resolution": args.res, "steps": steps, "cfg": g, "scheduler": args.scheduler,
+                       "dtype": "bf16", "out_shape": list(img.shape)}}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mode", choices=["train", "infer", "both"], default="both")
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--res", type=int, default=512)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--infer-steps", type=int, default=50)
+    ap.add_argument("--scheduler", default="LMSDiscreteScheduler")
+    ap.add_argument("--ckpt", action="store_true")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    from kubernetes_cloud_amd.ops import _lib
+    _lib.require()
+    if args.mode in ("train", "both"):
+        print(json.dumps(bench_train(args, dev)), flush=True)
+        torch.cuda.empty_cache()
+    if args.mode in ("infer", "both"):
+        a2 = argparse.Namespace(**vars(args))
+        a2.steps, a2.warmup = max(1, args.steps // 2), 1
+        print(json.dumps(bench_infer(a2, dev)), flush=True)
+
+
+if __name__ == "__main__":
+    main()

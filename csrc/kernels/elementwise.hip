@@ -232,6 +232,27 @@ KCA_API int kca_accum_grad(float* acc, const void* g, float scale,
   return 0;
 }
 
+// EMA (K21): shadow <- shadow + (1 - decay) * (param - shadow), flat fp32.
+__global__ void ema_kernel(float* __restrict__ shadow, const float* __restrict__ p, float w, long long n4) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4;
+       i += (long long)gridDim.x * blockDim.x) {
+    float4 s = reinterpret_cast<float4*>(shadow)[i];
+    const float4 v = reinterpret_cast<const float4*>(p)[i];
+    s.x += w * (v.x - s.x);
+    s.y += w * (v.y - s.y);
+    s.z += w * (v.z - s.z);
+    s.w += w * (v.w - s.w);
+    reinterpret_cast<float4*>(shadow)[i] = s;
+  }
+}
+
+KCA_API int kca_ema(float* shadow, const float* p, float decay, long long n, hipStream_t stream) {
+  if (n % 4) return 1;
+  hipLaunchKernelGGL(ema_kernel, dim3(kca_grid(n / 4, 256)), dim3(256), 0, stream, shadow, p,
+                     1.f - decay, n / 4);
+  return 0;
+}
+
 // fp32 -> bf16 cast (master -> model copy, ZeRO all-gather staging).
 __global__ void cast_f32_bf16_kernel(const float* __restrict__ x,
                                      bf16_t* __restrict__ y, long long n8) {

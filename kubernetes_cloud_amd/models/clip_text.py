@@ -164,10 +164,19 @@ class CLIPTextModel(nn.Module):
         with torch.device("meta"):
             m = cls(cfg)
         m = m.to_empty(device=device).to(dtype)
-        sd = read_hf_state_dict(path)
-        sd = {k: v for k, v in sd.items() if not k.endswith("position_ids")}
-        m.load_state_dict({k: v.to(dtype) for k, v in sd.items()}, strict=True)
+        m.load_hf(read_hf_state_dict(path))
         return m
+
+    def load_hf(self, sd: dict):
+        """Load a transformers CLIPTextModel state dict (with or without the
+        ``text_model.`` prefix; transformers 5 drops it in memory)."""
+        out = {}
+        for k, v in sd.items():
+            if k.endswith("position_ids"):
+                continue
+            out[k if k.startswith("text_model.") else "text_model." + k] = v
+        dt = next(self.parameters()).dtype
+        self.load_state_dict({k: v.to(dt) for k, v in out.items()}, strict=True)
 
     def save_pretrained(self, path: str):
         from safetensors.torch import save_file

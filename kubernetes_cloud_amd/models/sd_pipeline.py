@@ -1,0 +1,223 @@
+"""Stable Diffusion txt2img pipeline + diffusers-layout I/O (S1/S2/T8 support).
+
+Loads the layouts the reference produces and serves:
+* a diffusers directory (``model_index.json`` + ``unet/ vae/ text_encoder/
+  tokenizer/ scheduler/``) -- what the SD finetuner saves
+  (sd-finetuner/finetuner.py:413-434) and the predictor loads
+  (stable-diffusion/service/service.py:163-171);
+* the tensorized layout (``{encoder,vae,unet}.tensors`` + ``*-config.json`` +
+  tokenizer/scheduler; serializer/serialize.py:35-50, service.py:173-198).
+
+Batched, classifier-free-guided denoise loop: one UNet call on the
+[uncond; cond] 2B batch per step, guidance combine and sampler update in fp32,
+VAE decode at the end. BASELINE config 5 runs it at batch 8, 512x512, 50
+steps, CFG 7.0 (the reference serves batch 1 with containerConcurrency 1).
+"""
+from __future__ import annotations
+
+import json
+import os
+
+import torch
+
+from .clip_text import CLIPTextConfig, CLIPTextModel
+from .schedulers import load_scheduler, sd_scheduler_config
+from .unet import UNet2DConditionModel, UNetConfig
+from .vae import L_SCALE_FACTOR, AutoencoderKL, VAEConfig
+
+
+def _read_cfg(path):
+    with open(path) as f:
+        return json.load(f)
+
+
+def _load_module(cls, cfg, weights_dir, device, dtype, names=("diffusion_pytorch_model", "model")):
+    from safetensors.torch import load_file
+    with torch.device("meta"):
+        m = cls(cfg)
+    m = m.to_empty(device=device).to(dtype)
+    sd = None
+    for n in names:
+        p = os.path.join(weights_dir, n + ".safetensors")
+        if os.path.exists(p):
+            sd = load_file(p)
+            break
+        p = os.path.join(weights_dir, n + ".bin")
+        if os.path.exists(p):
+            sd = torch.load(p, map_location="cpu", weights_only=True)
+            break
+    if sd is None:
+        raise FileNotFoundError(f"no weights in {weights_dir}")
+    if isinstance(m, CLIPTextModel):
+        m.load_hf(sd)
+    else:
+        m.load_state_dict({k: v.to(dtype) for k, v in _map_legacy_vae(sd).items()}, strict=True)
+    return m
+
+
+def _map_legacy_vae(sd: dict) -> dict:
+    """Older diffusers VAE checkpoints name the mid attention query/key/value/
+    proj_attn; map them to to_q/to_k/to_v/to_out.0 (and squeeze 1x1 conv kernels)."""
+    ren = {"query": "to_q", "key": "to_k", "value": "to_v", "proj_attn": "to_out.0"}
+    out = {}
+    for k, v in sd.items():
+        parts = k.split(".")
+        if "attentions" in parts and parts[-2] in ren:
+            k = ".".join(parts[:-2] + [ren[parts[-2]], parts[-1]])
+            if v.dim() == 4:
+                v = v[:, :, 0, 0]
+        out[k] = v
+    return out
+
+
+class StableDiffusionPipeline:
+    def __init__(self, unet: UNet2DConditionModel, vae: AutoencoderKL, text_encoder: CLIPTextModel,
+                 tokenizer, scheduler, scaling_factor: float = L_SCALE_FACTOR):
+        self.unet, self.vae, self.text_encoder = unet, vae, text_encoder
+        self.tokenizer, self.scheduler = tokenizer, scheduler
+        self.scaling_factor = scaling_factor
+
+    @property
+    def device(self):
+        return next(self.unet.parameters()).device
+
+    @property
+    def dtype(self):
+        return next(self.unet.parameters()).dtype
+
+    def to(self, device=None, dtype=None):
+        for m in (self.unet, self.vae, self.text_encoder):
+            m.to(device=device, dtype=dtype)
+        return self
+
+    # ------------------------------------------------------------------ I/O
+    @classmethod
+    def from_pretrained(cls, path: str, device="cpu", dtype=torch.float32, scheduler: str | None = None):
+        from transformers import AutoTokenizer
+        unet = _load_module(UNet2DConditionModel, UNetConfig.from_pretrained(os.path.join(path, "unet")),
+                            os.path.join(path, "unet"), device, dtype)
+        vae = _load_module(AutoencoderKL, VAEConfig.from_pretrained(os.path.join(path, "vae")),
+                           os.path.join(path, "vae"), device, dtype)
+        te = _load_module(CLIPTextModel, CLIPTextConfig.from_pretrained(os.path.join(path, "text_encoder")),
+                          os.path.join(path, "text_encoder"), device, dtype, names=("model", "pytorch_model"))
+        tok = AutoTokenizer.from_pretrained(os.path.join(path, "tokenizer"))
+        sch = load_scheduler(os.path.join(path, "scheduler"), scheduler)
+        return cls(unet, vae, te, tok, sch, vae.config.scaling_factor)
+
+    @classmethod
+    def from_tensorized(cls, path: str, device="cpu", dtype=torch.float32, scheduler: str | None = None):
+        """``{encoder,vae,unet}.tensors`` + ``{encoder,vae,unet}-config.json`` layout."""
+        from transformers import AutoTokenizer
+        from ..io.tensors import load_into_module
+        stats = {}
+        mods = {}
+        for prefix, mcls, ccls in (("encoder", CLIPTextModel, CLIPTextConfig), ("vae", AutoencoderKL, VAEConfig),
+                                   ("unet", UNet2DConditionModel, UNetConfig)):
+            cfg = ccls.from_dict(_read_cfg(os.path.join(path, f"{prefix}-config.json")))
+            with torch.device("meta"):
+                m = mcls(cfg)
+            m = m.to_empty(device=device).to(dtype)
+            stats[prefix] = load_into_module(m, os.path.join(path, f"{prefix}.tensors"), device=device)
+            mods[prefix] = m
+        tdir = os.path.join(path, "tokenizer") if os.path.isdir(os.path.join(path, "tokenizer")) else path
+        tok = AutoTokenizer.from_pretrained(tdir)
+        sdir = os.path.join(path, "scheduler")
+        sch = load_scheduler(sdir if os.path.isdir(sdir) else sd_scheduler_config(), scheduler or "LMSDiscreteScheduler")
+        pipe = cls(mods["unet"], mods["vae"], mods["encoder"], tok, sch, mods["vae"].config.scaling_factor)
+        pipe.load_stats = stats
+        return pipe
+
+    def save_pretrained(self, path: str):
+        """diffusers layout (safety_checker / feature_extractor recorded as null:
+        the CompVis checker weights are not available offline)."""
+        from safetensors.torch import save_file
+        os.makedirs(path, exist_ok=True)
+        for name, m, cfg, fn in (("unet", self.unet, self.unet.config.to_dict(), "diffusion_pytorch_model"),
+                                 ("vae", self.vae, self.vae.config.to_dict(), "diffusion_pytorch_model")):
+            d = os.path.join(path, name)
+            os.makedirs(d, exist_ok=True)
+            with open(os.path.join(d, "config.json"), "w") as f:
+                json.dump(cfg, f, indent=2)
+            save_file({k: v.detach().contiguous().cpu() for k, v in m.state_dict().items()},
+                      os.path.join(d, fn + ".safetensors"), metadata={"format": "pt"})
+        self.text_encoder.save_pretrained(os.path.join(path, "text_encoder"))
+        self.tokenizer.save_pretrained(os.path.join(path, "tokenizer"))
+        self.scheduler.save_pretrained(os.path.join(path, "scheduler"))
+        idx = {"_class_name": "StableDiffusionPipeline", "_diffusers_version": "0.14.0",
+               "unet": ["diffusers", "UNet2DConditionModel"], "vae": ["diffusers", "AutoencoderKL"],
+               "text_encoder": ["transformers", "CLIPTextModel"], "tokenizer": ["transformers", "CLIPTokenizer"],
+               "scheduler": ["diffusers", type(self.scheduler).__name__],
+               "safety_checker": [None, None], "feature_extractor": [None, None],
+               "requires_safety_checker": False}
+        with open(os.path.join(path, "model_index.json"), "w") as f:
+            json.dump(idx, f, indent=2)
+
+    # -------------------------------------------------------------- encode
+    @torch.no_grad()
+    def encode_prompt(self, prompts: list[str]) -> torch.Tensor:
+        ml = getattr(self.tokenizer, "model_max_length", 77)
+        if ml > 1024:
+            ml = 77
+        tok = self.tokenizer(prompts, padding="max_length", max_length=ml, truncation=True, return_tensors="pt")
+        ids = tok.input_ids.to(self.device)
+        return self.text_encoder(ids)
+
+    # --------------------------------------------------------------- sample
+    @torch.no_grad()
+    def __call__(self, prompt, height: int = 512, width: int = 512, num_inference_steps: int = 50,
+                 guidance_scale: float = 7.0, negative_prompt=None, generator: torch.Generator | None = None,
+                 latents: torch.Tensor | None = None, output_type: str = "pil"):
+        prompts = [prompt] if isinstance(prompt, str) else list(prompt)
+        B = len(prompts)
+        dev, dt = self.device, self.dtype
+        cond = self.encode_prompt(prompts)
+        cfg = guidance_scale > 1.0
+        if cfg:
+            neg = negative_prompt or [""] * B
+            neg = [neg] * B if isinstance(neg, str) else neg
+            ctx = torch.cat([self.encode_prompt(neg), cond])
+        else:
+            ctx = cond
+        sch = self.scheduler
+        sch.set_timesteps(num_inference_steps, device=dev)
+        f = 2 ** (len(self.vae.config.block_out_channels) - 1)  # 8 for the SD VAE
+        shape = (B, self.unet.config.in_channels, height // f, width // f)
+        if latents is None:
+            latents = torch.randn(shape, generator=generator, device=generator.device if generator else dev,
+                                  dtype=torch.float32).to(dev)
+        x = latents.float() * sch.init_noise_sigma
+        for t in sch.timesteps:
+            xin = torch.cat([x, x]) if cfg else x
+            xin = sch.scale_model_input(xin, t).to(dt)
+            tt = torch.full((xin.shape[0],), float(t), device=dev)
+            eps = self.unet(xin, tt, ctx).float()
+            if cfg:
+                eu, ec = eps.chunk(2)
+                eps = eu + guidance_scale * (ec - eu)
+            x = sch.step(eps, t, x).float()
+        if output_type == "latent":
+            return x
+        img = self.vae.decode((x / self.scaling_factor).to(dt)).float()
+        if output_type == "tensor":
+            return img
+        from ..data.images import to_pil
+        return to_pil(img)
+
+
+def serialize_pipeline(pipe: StableDiffusionPipeline, out_dir: str, dtype: torch.dtype | None = None):
+    """Write the tensorized layout (serializer/serialize.py:13-50): encoder/vae/unet
+    ``.tensors`` + ``*-config.json`` + tokenizer + scheduler (self-contained:
+    the reference relied on writing into an existing diffusers dir)."""
+    from ..io.tensors import serialize
+    os.makedirs(out_dir, exist_ok=True)
+    stats = {}
+    for prefix, m, cfg in (("encoder", pipe.text_encoder, pipe.text_encoder.config.to_dict()),
+                           ("vae", pipe.vae, pipe.vae.config.to_dict()),
+                           ("unet", pipe.unet, pipe.unet.config.to_dict())):
+        stats[prefix] = serialize(m, os.path.join(out_dir, f"{prefix}.tensors"), dtype=dtype)
+        with open(os.path.join(out_dir, f"{prefix}-config.json"), "w") as f:
+            json.dump(cfg, f, indent=2)
+    pipe.tokenizer.save_pretrained(out_dir)
+    pipe.tokenizer.save_pretrained(os.path.join(out_dir, "tokenizer"))
+    pipe.scheduler.save_pretrained(os.path.join(out_dir, "scheduler"))
+    return stats

@@ -365,7 +365,7 @@ class UNet2DConditionModel(nn.Module):
             n = len(blk.resnets)
             mine = skips[-n:]
             del skips[-n:]
-            x = self._run(lambda a, b, cc, *sk: blk(a, list(sk), b, cc), x, temb, ctx, *mine)
+            x = self._run(lambda a, b, cc, *sk, _blk=blk: _blk(a, list(sk), b, cc), x, temb, ctx, *mine)
         return self.conv_out(self.conv_norm_out(x))
 
 

@@ -42,6 +42,7 @@ _SIGS = {
     "kca_rope": [P, P, I, I, LL, I, LL, LL, LL, LL, I, I, P, P, P, F, P],
     "kca_accum_grad": [P, P, F, I, LL, P],
     "kca_cast_f32_bf16": [P, P, LL, P],
+    "kca_ema": [P, P, F, LL, P],
     "kca_cross_entropy_fwd": [P, LL, P, I, I, I, P, P, P],
     "kca_cross_entropy_bwd": [P, LL, P, P, P, F, I, I, I, P, LL, P],
     "kca_adamw": [P, P, P, P, P, LL, P, F, F, F, F, F, F, F, P, P, P],

@@ -302,6 +302,19 @@ class TrainEngine:
         else:
             self.flat.copy_(self.opt.master)
 
+    def publish(self, master_like: torch.Tensor):
+        """Write bf16 model params from an fp32 tensor laid out like the
+        optimizer master (the shard when ZeRO>=1), e.g. EMA weights for export."""
+        if self.sharded:
+            self.shard_bf16.copy_(master_like)
+            for bk in self.buckets:
+                piece = bk.size // self.world
+                dist.all_gather_into_tensor(self.flat[bk.start:bk.start + bk.size],
+                                            self.shard_bf16[bk.shard_off:bk.shard_off + piece],
+                                            group=self.group)
+        else:
+            self.flat.copy_(master_like)
+
     def remove_hooks(self):
         for h in self._hooks:
             h.remove()

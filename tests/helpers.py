@@ -59,3 +59,41 @@ def make_tokens(path: str, n_ctx: int, ctx: int, vocab: int = 300, seed: int = 0
 def read_jsonl(path):
     with open(path) as f:
         return [json.loads(x) for x in f if x.strip()]
+
+
+def make_sd_dir(path: str, res: int = 32, prediction_type: str = "epsilon"):
+    """Tiny SD pipeline in the diffusers layout (random weights)."""
+    import torch
+    from kubernetes_cloud_amd.models.clip_text import CLIPTextConfig, build_clip_text
+    from kubernetes_cloud_amd.models.schedulers import PNDMScheduler, sd_scheduler_config
+    from kubernetes_cloud_amd.models.sd_pipeline import StableDiffusionPipeline
+    from kubernetes_cloud_amd.models.unet import UNetConfig, build_unet
+    from kubernetes_cloud_amd.models.vae import VAEConfig, build_vae
+    tok = make_tokenizer(os.path.join(path, "_tok"), vocab_size=300)
+    tok.pad_token = tok.eos_token
+    tok.model_max_length = 16
+    te = build_clip_text(CLIPTextConfig(vocab_size=len(tok), hidden_size=32, intermediate_size=64,
+                                        num_hidden_layers=2, num_attention_heads=2, max_position_embeddings=16,
+                                        eos_token_id=tok.eos_token_id))
+    unet = build_unet(UNetConfig(block_out_channels=(32, 64, 64, 64), cross_attention_dim=32,
+                                 attention_head_dim=4, norm_num_groups=8, sample_size=res // 8))
+    vae = build_vae(VAEConfig(block_out_channels=(16, 32), layers_per_block=1, norm_num_groups=8,
+                              sample_size=res))
+    sch = PNDMScheduler.from_config(sd_scheduler_config(prediction_type))
+    pipe = StableDiffusionPipeline(unet, vae, te, tok, sch)
+    pipe.save_pretrained(path)
+    return path
+
+
+def make_images(path: str, n: int, size: int = 40, captions: bool = True):
+    from PIL import Image
+    import numpy as np
+    os.makedirs(path, exist_ok=True)
+    rng = np.random.default_rng(0)
+    for i in range(n):
+        a = (rng.random((size, size + 8, 3)) * 255).astype("uint8")
+        Image.fromarray(a).save(os.path.join(path, f"img{i}.png"))
+        if captions:
+            with open(os.path.join(path, f"img{i}.txt"), "w") as f:
+                f.write(f"a photo of the quick fox number {i}\n")
+    return path

@@ -1,0 +1,125 @@
+"""SD stack on CPU: CLIP text parity vs transformers, UNet/VAE parameter counts
+(SD-1.5 exact), schedulers, pipeline sampling + diffusers-layout round trip,
+tensorized serializer round trip, and the SD finetuner / DreamBooth CLI."""
+import json
+import os
+
+import pytest
+import torch
+
+from kubernetes_cloud_amd.models.clip_text import CLIPTextConfig, CLIPTextModel
+from kubernetes_cloud_amd.models.schedulers import (DDIMScheduler, DDPMScheduler, EulerDiscreteScheduler,
+                                                    LMSDiscreteScheduler, PNDMScheduler, sd_scheduler_config)
+from kubernetes_cloud_amd.models.unet import UNetConfig, build_unet
+from kubernetes_cloud_amd.models.vae import VAEConfig, build_vae
+
+from .helpers import make_images, make_sd_dir
+
+
+def test_clip_text_matches_transformers():
+    from transformers import CLIPTextConfig as HC, CLIPTextModel as HM
+    torch.manual_seed(0)
+    hc = HC(vocab_size=100, hidden_size=64, intermediate_size=128, num_hidden_layers=2, num_attention_heads=4,
+            max_position_embeddings=16, bos_token_id=0, eos_token_id=1, pad_token_id=1)
+    hm = HM(hc).eval()
+    cm = CLIPTextModel(CLIPTextConfig.from_dict(hc.to_dict()))
+    cm.load_hf(dict(hm.state_dict()))
+    ids = torch.randint(0, 100, (2, 16))
+    with torch.no_grad():
+        assert (hm(ids).last_hidden_state - cm(ids)).abs().max() < 1e-4
+
+
+def test_sd15_parameter_counts():
+    u = build_unet(UNetConfig())
+    assert sum(p.numel() for p in u.parameters()) == 859_520_964
+    v = build_vae(VAEConfig())
+    assert sum(p.numel() for p in v.parameters()) == 83_653_863
+    keys = set(u.state_dict())
+    for k in ("down_blocks.0.attentions.0.transformer_blocks.0.attn2.to_k.weight",
+              "up_blocks.3.resnets.2.conv_shortcut.weight", "mid_block.attentions.0.proj_in.weight",
+              "time_embedding.linear_1.weight", "down_blocks.0.downsamplers.0.conv.weight"):
+        assert k in keys, k
+
+
+def test_unet_train_step_small():
+    u = build_unet(UNetConfig(block_out_channels=(32, 64, 64, 64), cross_attention_dim=32, attention_head_dim=4,
+                              norm_num_groups=8))
+    x = torch.randn(2, 4, 16, 16, requires_grad=False)
+    y = u(x, torch.tensor([10, 500]), torch.randn(2, 7, 32))
+    assert y.shape == x.shape
+    y.float().pow(2).mean().backward()
+    assert u.conv_in.weight.grad is not None
+    u.enable_gradient_checkpointing()
+    y2 = u(x, torch.tensor([10, 500]), torch.randn(2, 7, 32))
+    y2.mean().backward()
+
+
+def test_scheduler_math():
+    s = DDPMScheduler.from_config(sd_scheduler_config())
+    x0, n = torch.randn(3, 4, 8, 8), torch.randn(3, 4, 8, 8)
+    t = torch.tensor([0, 500, 999])
+    xt = s.add_noise(x0, n, t)
+    a = s.alphas_cumprod[t].float().view(3, 1, 1, 1)
+    assert torch.allclose(xt, a.sqrt() * x0 + (1 - a).sqrt() * n, atol=1e-6)
+    v = s.get_velocity(x0, n, t)
+    assert torch.allclose(v, a.sqrt() * n - (1 - a).sqrt() * x0, atol=1e-6)
+    for cls in (PNDMScheduler, DDIMScheduler, LMSDiscreteScheduler, EulerDiscreteScheduler):
+        sch = cls.from_config(sd_scheduler_config())
+        sch.set_timesteps(10)
+        x = torch.randn(1, 4, 8, 8) * sch.init_noise_sigma
+        for tt in sch.timesteps:
+            x = sch.step(torch.zeros_like(x), tt, sch.scale_model_input(x, tt))
+        assert torch.isfinite(x).all()
+    p = PNDMScheduler.from_config(sd_scheduler_config())
+    p.set_timesteps(50)
+    assert len(p.timesteps) == 51 and int(p.timesteps[0]) == 981
+
+
+def test_pipeline_sample_and_roundtrip(tmp_path):
+    from kubernetes_cloud_amd.models.sd_pipeline import StableDiffusionPipeline, serialize_pipeline
+    d = make_sd_dir(str(tmp_path / "sd"))
+    idx = json.load(open(tmp_path / "sd" / "model_index.json"))
+    assert idx["unet"] == ["diffusers", "UNet2DConditionModel"]
+    pipe = StableDiffusionPipeline.from_pretrained(d)
+    g = torch.Generator().manual_seed(0)
+    imgs = pipe(["a fox", "a dog"], height=32, width=32, num_inference_steps=3, guidance_scale=7.0, generator=g)
+    assert len(imgs) == 2 and imgs[0].size == (32, 32)
+    lat1 = pipe("a fox", 32, 32, 3, 7.0, generator=torch.Generator().manual_seed(1), output_type="latent")
+    # tensorized layout round trip gives identical results
+    out = str(tmp_path / "tz")
+    serialize_pipeline(pipe, out)
+    for f in ("encoder.tensors", "vae.tensors", "unet.tensors", "unet-config.json", "encoder-config.json"):
+        assert os.path.exists(os.path.join(out, f)), f
+    p2 = StableDiffusionPipeline.from_tensorized(out, scheduler="PNDMScheduler")
+    lat2 = p2("a fox", 32, 32, 3, 7.0, generator=torch.Generator().manual_seed(1), output_type="latent")
+    assert torch.allclose(lat1, lat2)
+
+
+def test_sd_finetuner_vanilla_and_dreambooth(tmp_path):
+    from kubernetes_cloud_amd.train.sd_finetuner import main
+    d = make_sd_dir(str(tmp_path / "sd"))
+    data = make_images(str(tmp_path / "data"), 3)
+    out = str(tmp_path / "out")
+    r = main(["--model", d, "--run_name", "sdt", "--dataset", data, "--resolution", "32", "--batch_size", "2",
+              "--epochs", "2", "--lr", "1e-4", "--save_steps", "2", "--output_path", out, "--image_log_steps", "0",
+              "--use_ema", "True", "--resize", "true", "--center_crop", "False"])
+    assert r["steps"] == 4
+    assert os.path.exists(os.path.join(out, "unet", "diffusion_pytorch_model.safetensors"))
+    assert os.path.exists(os.path.join(out, "model_index.json"))
+    # DreamBooth: 1 instance image, class images generated by the pipeline
+    inst = make_images(str(tmp_path / "inst"), 1, captions=False)
+    cls_dir = str(tmp_path / "cls")
+    r = main(["--model", d, "--run_name", "db", "--instance_dataset", inst, "--instance_prompt", "a sks fox",
+              "--class_dataset", cls_dir, "--class_prompt", "a fox", "--num_class_images", "2",
+              "--resolution", "32", "--batch_size", "1", "--epochs", "1", "--output_path", str(tmp_path / "dbo"),
+              "--image_log_steps", "0", "--gradient_checkpointing", "True"])
+    assert r["steps"] == 2
+    assert len([f for f in os.listdir(cls_dir) if f.endswith(".jpg")]) == 2
+
+
+def test_sd_parser_rejects_partial_dreambooth():
+    from kubernetes_cloud_amd.train.sd_finetuner import parse_args
+    with pytest.raises(SystemExit):
+        parse_args(["--instance_dataset", "x"])
+    with pytest.raises(SystemExit):
+        parse_args([])
