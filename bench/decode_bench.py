@@ -1,0 +1,74 @@
+#!/usr/bin/env python3
+"""Decode-engine benchmark (FasterTransformer-equivalent path).
+
+GPT-J-6B (random init, bf16) through ``LLMEngine`` with HIP-graph decode:
+prefill ms, decode ms/step and generated tokens/s at several batch sizes
+(FT config: request_output_len 64; download-weights-job-gptj.yml). One JSON
+line per batch size.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="gpt-j-6b")
+    ap.add_argument("--batches", default="1,8,32,64")
+    ap.add_argument("--prompt-len", type=int, default=512)
+    ap.add_argument("--new-tokens", type=int, default=64)
+    ap.add_argument("--layers", type=int, default=0, help="override layer count (smoke runs only)")
+    ap.add_argument("--no-graphs", action="store_true")
+    args = ap.parse_args()
+    from kubernetes_cloud_amd.engine.llm_engine import LLMEngine, SamplingParams
+    from kubernetes_cloud_amd.models.causal_lm import build_model
+    from kubernetes_cloud_amd.models.config import preset
+    from kubernetes_cloud_amd.ops import _lib
+    _lib.require()
+    dev = torch.device("cuda", 0)
+    cfg = preset(args.model)
+    if args.layers:
+        cfg.n_layers = args.layers
+    m = build_model(cfg, device=dev, dtype=torch.bfloat16, seed=0)
+    batches = [int(b) for b in args.batches.split(",")]
+    eng = LLMEngine(m, max_slots=max(batches), max_len=args.prompt_len + args.new_tokens + 8,
+                    use_graphs=not args.no_graphs)
+    g = torch.Generator().manual_seed(0)
+    for B in batches:
+        prompts = [torch.randint(0, cfg.vocab_size, (args.prompt_len,), generator=g).tolist() for _ in range(B)]
+        sp = SamplingParams(max_new_tokens=args.new_tokens, temperature=1.0, top_k=50, top_p=0.95, seed=1)
+        eng.generate(prompts, SamplingParams(max_new_tokens=args.new_tokens, do_sample=False))  # warm/capture
+        torch.cuda.synchronize()
+        # prefill alone
+        t0 = time.perf_counter()
+        for p in prompts:
+            eng.runner.prefill(torch.tensor([p]), [0])
+        torch.cuda.synchronize()
+        prefill_ms = (time.perf_counter() - t0) / B * 1e3
+        reqs = [eng.add_request(p, sp) for p in prompts]
+        eng.step()  # admit + first decode
+        torch.cuda.synchronize()
+        steps0, t0 = eng.stats["steps"], time.perf_counter()
+        eng.run_until_done(reqs)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        nsteps = eng.stats["steps"] - steps0
+        gen = sum(len(r.output) for r in reqs) - 2 * B
+        print(json.dumps({"metric": f"{args.model} decode", "batch": B, "prompt_len": args.prompt_len,
+                          "new_tokens": args.new_tokens, "prefill_ms_per_seq": round(prefill_ms, 2),
+                          "decode_ms_per_step": round(dt / max(nsteps, 1) * 1e3, 3),
+                          "decode_tokens_per_s": round(gen / dt, 1), "graphs": not args.no_graphs,
+                          "kv_cache_gib": round(eng.runner.cache.nbytes() / 2**30, 2),
+                          "layers": cfg.n_layers}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

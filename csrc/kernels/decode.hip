@@ -1,0 +1,650 @@
+// Decode-path kernels for the serving engine:
+//
+//   kca_decode_prep     RoPE on the new token's Q/K (GPT-J interleaved or NeoX
+//                       rotate-half, any rot) + append K/V into the slot cache
+//   kca_decode_attn     split-K ("flash-decoding") attention of one query token
+//                       per sequence over its cached K/V, ALiBi optional,
+//                       GQA groups share one K/V read, + combine kernel
+//   kca_sample_logits   fused repetition penalty + bans + temperature + top-k
+//                       (radix select) + top-p (mass radix select) + Philox
+//                       multinomial + log-prob, one workgroup per row
+//
+// Reference behaviour these replace: FasterTransformer's masked MHA / sampling
+// layers behind online-inference/fastertransformer (runtime_top_k, runtime_top_p,
+// temperature, repetition_penalty, bad_words_list, is_return_log_probs:
+// download-weights-job-gptj.yml:101-204) and HF generate() sampling used by
+// finetuner.py:861-875 / evaluator.py:201-213 / bloom.py:68-77.
+//
+// KV cache layout is head-major per slot: [slot][kv_head][pos][D] (strides
+// passed in), so a (sequence, head) chunk of the cache is one contiguous
+// stream of chunk*D*2 bytes -- decode is HBM-bound and reads exactly K+V once.
+#include "common.h"
+
+// ------------------------------------------------------------------ prep
+// One wave per (b, head-row) of the fused QKV GEMM output [B, (H+2Hkv)*D];
+// lane owns dims lane, lane+64, ... Partner elements of the rotation live in the
+// same wave, and every lane loads before any lane stores.
+__global__ __launch_bounds__(256) void decode_prep_kernel(
+    bf16_t* __restrict__ qkv, long long ld, int B, int H, int Hkv, int D, int rot,
+    int interleaved, const float* __restrict__ cos_t, const float* __restrict__ sin_t,
+    const int* __restrict__ pos, const int* __restrict__ slots, bf16_t* __restrict__ kc,
+    bf16_t* __restrict__ vc, long long cs_slot, long long cs_head, long long cs_pos) {
+  const int rows_per_b = H + 2 * Hkv;
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= (long long)B * rows_per_b) return;
+  const int lane = threadIdx.x & 63;
+  const int b = (int)(row / rows_per_b), j = (int)(row % rows_per_b);
+  bf16_t* src = qkv + b * ld + (long long)j * D;
+  const int p = pos[b];
+  float x[4], y[4];
+  const int half = rot >> 1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int d = lane + 64 * i;
+    x[i] = 0.f;
+    y[i] = 0.f;
+    if (d < D) {
+      x[i] = bf2f(src[d]);
+      y[i] = x[i];
+      if (j < H + Hkv && d < rot) {
+        int partner, fi;
+        float sgn;
+        if (interleaved) {
+          partner = d ^ 1;
+          fi = d >> 1;
+          sgn = (d & 1) ? 1.f : -1.f;
+        } else {
+          partner = d < half ? d + half : d - half;
+          fi = d < half ? d : d - half;
+          sgn = d < half ? -1.f : 1.f;
+        }
+        const float xp = bf2f(src[partner]);
+        const float c = cos_t[(long long)p * half + fi], s = sin_t[(long long)p * half + fi];
+        y[i] = x[i] * c + sgn * xp * s;
+      }
+    }
+  }
+  if (j < H) {  // query: rotate in place (only if rotary)
+    if (rot > 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int d = lane + 64 * i;
+        if (d < D && d < rot) src[d] = f2bf(y[i]);
+      }
+    }
+    return;
+  }
+  const bool is_k = j < H + Hkv;
+  const int hk = is_k ? j - H : j - H - Hkv;
+  bf16_t* dst = (is_k ? kc : vc) + slots[b] * cs_slot + hk * cs_head + (long long)p * cs_pos;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int d = lane + 64 * i;
+    if (d < D) dst[d] = f2bf(y[i]);
+  }
+}
+
+KCA_API int kca_decode_prep(void* qkv, long long ld, int B, int H, int Hkv, int D, int rot,
+                            int interleaved, const float* cos_t, const float* sin_t,
+                            const int* pos, const int* slots, void* kc, void* vc,
+                            long long cs_slot, long long cs_head, long long cs_pos,
+                            hipStream_t stream) {
+  if (D > 256 || rot > D || (rot & 1) || B <= 0) return 1;
+  const long long rows = (long long)B * (H + 2 * Hkv);
+  hipLaunchKernelGGL(decode_prep_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, stream,
+                     (bf16_t*)qkv, ld, B, H, Hkv, D, rot, interleaved, cos_t, sin_t, pos, slots,
+                     (bf16_t*)kc, (bf16_t*)vc, cs_slot, cs_head, cs_pos);
+  return 0;
+}
+
+// ------------------------------------------------------------- attention
+struct DecodeParams {
+  const bf16_t* q;
+  long long q_bs;  // q[b*q_bs + h*D + d]
+  const bf16_t* kc;
+  const bf16_t* vc;
+  long long cs_slot, cs_head, cs_pos;
+  const int* slots;
+  const int* kv_lens;
+  bf16_t* out;
+  long long o_bs;
+  float* ws_o;   // [B*H, nsplit, D]
+  float* ws_ml;  // [B*H, nsplit, 2]
+  const float* alibi;
+  int H, Hkv, D, chunk;
+  float scale;
+};
+
+// LPT lanes cooperate on one token row (8 dims per lane); TPW = 64/LPT tokens per
+// wave step; G query heads share each K/V row (GQA group).
+template <int LPT, int G>
+__global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
+  constexpr int TPW = 64 / LPT;
+  constexpr int TPB = 4 * TPW;
+  constexpr int U = 4;  // independent row loads in flight per lane
+  extern __shared__ float smem[];
+  __shared__ float red_s[8];
+  const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
+  const int nsplit = gridDim.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int D = p.D, ND = D >> 3;
+  const int L = p.kv_lens[b];
+  const int c0 = split * p.chunk;
+  const int c1 = min(c0 + p.chunk, L);
+  const long long bh0 = (long long)b * p.H + hk * G;
+  if (c0 >= L) {
+    if (nsplit > 1 && tid < G) {
+      p.ws_ml[((bh0 + tid) * nsplit + split) * 2] = -INFINITY;
+      p.ws_ml[((bh0 + tid) * nsplit + split) * 2 + 1] = 0.f;
+    }
+    return;
+  }
+  const int dslot = lane % LPT, tsub = lane / LPT;
+  const bool dact = dslot < ND;
+  float* sc = smem;                 // [G][chunk]
+  float* red = smem + G * p.chunk;  // [4][G][D]
+  const long long kvoff = p.slots[b] * p.cs_slot + hk * p.cs_head + dslot * 8;
+  const bf16_t* kb = p.kc + kvoff;
+  const bf16_t* vb = p.vc + kvoff;
+
+  float q[G][8];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    if (dact) {
+      load8(p.q + b * p.q_bs + (long long)(hk * G + g) * D + dslot * 8, q[g]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) q[g][j] *= p.scale;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) q[g][j] = 0.f;
+    }
+  }
+  float slope[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) slope[g] = p.alibi ? p.alibi[hk * G + g] : 0.f;
+
+  // ---- scores
+  for (int t0 = c0 + wid * TPW + tsub; t0 < c1; t0 += TPB * U) {
+    float kr[U][8];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int t = t0 + u * TPB;
+      if (t < c1 && dact) {
+        load8(kb + (long long)t * p.cs_pos, kr[u]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) kr[u][j] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int t = t0 + u * TPB;
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s = fmaf(q[g][j], kr[u][j], s);
+#pragma unroll
+        for (int o = 1; o < LPT; o <<= 1) s += __shfl_xor(s, o, 64);
+        if (dslot == 0 && t < c1) sc[g * p.chunk + (t - c0)] = s + slope[g] * (float)(t - (L - 1));
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- softmax over this chunk
+  const int n = c1 - c0;
+  float mg[G], lg[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    float m = -INFINITY;
+    for (int i = tid; i < n; i += 256) m = fmaxf(m, sc[g * p.chunk + i]);
+    m = block_max(m, red_s);
+    float l = 0.f;
+    for (int i = tid; i < n; i += 256) {
+      const float e = __expf(sc[g * p.chunk + i] - m);
+      sc[g * p.chunk + i] = e;
+      l += e;
+    }
+    l = block_sum(l, red_s);
+    mg[g] = m;
+    lg[g] = l;
+  }
+  __syncthreads();
+
+  // ---- P.V
+  float acc[G][8];
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
+  for (int t0 = c0 + wid * TPW + tsub; t0 < c1; t0 += TPB * U) {
+    float vr[U][8];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int t = t0 + u * TPB;
+      if (t < c1 && dact) {
+        load8(vb + (long long)t * p.cs_pos, vr[u]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) vr[u][j] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int t = t0 + u * TPB;
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const float pg = t < c1 ? sc[g * p.chunk + (t - c0)] : 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[g][j] = fmaf(pg, vr[u][j], acc[g][j]);
+      }
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int o = LPT; o < 64; o <<= 1) acc[g][j] += __shfl_xor(acc[g][j], o, 64);
+  if (tsub == 0 && dact) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) store8f(red + (wid * G + g) * D + dslot * 8, acc[g]);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    for (int d = tid; d < D; d += 256) {
+      const float s = red[(0 * G + g) * D + d] + red[(1 * G + g) * D + d] +
+                      red[(2 * G + g) * D + d] + red[(3 * G + g) * D + d];
+      if (nsplit == 1) {
+        p.out[b * p.o_bs + (long long)(hk * G + g) * D + d] = f2bf(lg[g] > 0.f ? s / lg[g] : 0.f);
+      } else {
+        p.ws_o[((bh0 + g) * nsplit + split) * D + d] = s;
+      }
+    }
+    if (nsplit > 1 && tid == 0) {
+      p.ws_ml[((bh0 + g) * nsplit + split) * 2] = mg[g];
+      p.ws_ml[((bh0 + g) * nsplit + split) * 2 + 1] = lg[g];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void decode_combine_kernel(const float* __restrict__ ws_o,
+                                                             const float* __restrict__ ws_ml,
+                                                             bf16_t* __restrict__ out, long long o_bs,
+                                                             int H, int D, int nsplit) {
+  const long long bh = blockIdx.x;
+  const int b = (int)(bh / H), h = (int)(bh % H);
+  const float* ml = ws_ml + bh * nsplit * 2;
+  float M = -INFINITY;
+  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, ml[2 * s]);
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    float Lsum = 0.f, acc = 0.f;
+    for (int s = 0; s < nsplit; ++s) {
+      const float m = ml[2 * s];
+      if (m == -INFINITY) continue;
+      const float w = __expf(m - M);
+      Lsum += w * ml[2 * s + 1];
+      acc += w * ws_o[(bh * nsplit + s) * D + d];
+    }
+    out[b * o_bs + (long long)h * D + d] = f2bf(Lsum > 0.f ? acc / Lsum : 0.f);
+  }
+}
+
+// Split size: enough (sequence, kv-head, split) workgroups to put >= ~2 on each
+// of the 256 CUs, chunks of 64..1024 tokens.
+KCA_API int kca_decode_chunk(int B, int Hkv, int max_kv) {
+  long long work = (long long)B * Hkv;
+  long long want = (512 + work - 1) / work;
+  long long c = (max_kv + want - 1) / want;
+  c = (c + 63) / 64 * 64;
+  if (c < 64) c = 64;
+  if (c > 1024) c = 1024;
+  return (int)c;
+}
+
+KCA_API long long kca_decode_ws_floats(int B, int H, int D, int max_kv, int chunk) {
+  const long long ns = (max_kv + chunk - 1) / chunk;
+  return ns > 1 ? (long long)B * H * ns * (D + 2) : 0;
+}
+
+template <int LPT, int G>
+static void launch_decode(const DecodeParams& p, int B, int nsplit, hipStream_t stream) {
+  const size_t lds = (size_t)(G * p.chunk + 4 * G * p.D) * sizeof(float);
+  hipLaunchKernelGGL((decode_attn_kernel<LPT, G>), dim3(nsplit, p.Hkv, B), dim3(256), lds, stream, p);
+}
+
+template <int LPT>
+static int launch_decode_g(const DecodeParams& p, int G, int B, int nsplit, hipStream_t s) {
+  switch (G) {
+    case 1: launch_decode<LPT, 1>(p, B, nsplit, s); return 0;
+    case 2: launch_decode<LPT, 2>(p, B, nsplit, s); return 0;
+    case 4: launch_decode<LPT, 4>(p, B, nsplit, s); return 0;
+    case 8: launch_decode<LPT, 8>(p, B, nsplit, s); return 0;
+  }
+  return 3;
+}
+
+KCA_API int kca_decode_attn(const void* q, long long q_bs, const void* kc, const void* vc,
+                            long long cs_slot, long long cs_head, long long cs_pos,
+                            const int* slots, const int* kv_lens, void* out, long long o_bs,
+                            float* ws, long long ws_floats, int B, int H, int Hkv, int D,
+                            int max_kv, int chunk, float scale, const float* alibi,
+                            hipStream_t stream) {
+  if (D % 8 || D > 256 || H % Hkv || B <= 0 || max_kv <= 0) return 1;
+  if (chunk <= 0) chunk = kca_decode_chunk(B, Hkv, max_kv);
+  const int G = H / Hkv;
+  if (G * chunk > 8192) return 2;
+  const int nsplit = (max_kv + chunk - 1) / chunk;
+  DecodeParams p{(const bf16_t*)q, q_bs, (const bf16_t*)kc, (const bf16_t*)vc, cs_slot, cs_head,
+                 cs_pos, slots, kv_lens, (bf16_t*)out, o_bs, nullptr, nullptr, alibi,
+                 H, Hkv, D, chunk, scale};
+  if (nsplit > 1) {
+    const long long need = (long long)B * H * nsplit * (D + 2);
+    if (!ws || ws_floats < need) return 4;
+    p.ws_o = ws;
+    p.ws_ml = ws + (long long)B * H * nsplit * D;
+  }
+  const int nd = D / 8;
+  int rc;
+  if (nd <= 8) rc = launch_decode_g<8>(p, G, B, nsplit, stream);
+  else if (nd <= 16) rc = launch_decode_g<16>(p, G, B, nsplit, stream);
+  else rc = launch_decode_g<32>(p, G, B, nsplit, stream);
+  if (rc) return rc;
+  if (nsplit > 1)
+    hipLaunchKernelGGL(decode_combine_kernel, dim3(B * H), dim3(256), 0, stream, p.ws_o, p.ws_ml,
+                       (bf16_t*)out, o_bs, H, D, nsplit);
+  return 0;
+}
+
+// --------------------------------------------------------------- sampling
+__device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c[0]), lo0 = 0xD2511F53u * c[0];
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c[2]), lo1 = 0xCD9E8D57u * c[2];
+    const uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+    c[0] = n0;
+    c[1] = lo1;
+    c[2] = n2;
+    c[3] = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+
+__device__ __forceinline__ uint32_t fkey(float f) {  // order-preserving float -> uint
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+constexpr int SAMPLE_THREADS = 1024;
+
+// Wave 0 scans the 256-bin histogram from the top bin down and finds the bin in
+// which the running total first reaches `target` (excl < target <= incl).
+// Writes bin/excl to sh[0..1]; bin = -1 if not reached.
+__device__ void find_bin_desc(const float* hist, float target, float* sh_excl, int* sh_bin) {
+  const int lane = threadIdx.x & 63;
+  if (threadIdx.x < 64) {
+    float v[4], loc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[i] = hist[255 - 4 * lane - i];
+      loc += v[i];
+    }
+    float incl = loc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const float t = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += t;
+    }
+    float excl = incl - loc;
+    if (lane == 0) *sh_bin = -1;
+    // the (unique) lane whose range contains the crossing
+    const bool mine = excl < target && target <= incl;
+    const unsigned long long bal = __ballot(mine);
+    const int first = bal ? __ffsll((long long)bal) - 1 : -1;
+    if (lane == first) {
+      float run = excl;
+      int bin = 255 - 4 * lane - 3;
+      for (int i = 0; i < 4; ++i) {
+        if (run + v[i] >= target && v[i] > 0.f) {
+          bin = 255 - 4 * lane - i;
+          break;
+        }
+        run += v[i];
+      }
+      *sh_bin = bin;
+      *sh_excl = run;
+    }
+  }
+  __syncthreads();
+}
+
+// One workgroup per row. ws: fp32 scratch [B, V] (processed logits).
+__global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(
+    const void* __restrict__ logits, long long ld, int is_bf16, int V,
+    const float* __restrict__ temperature, const int* __restrict__ top_k,
+    const float* __restrict__ top_p, const float* __restrict__ rep_pen, uint8_t* __restrict__ seen,
+    const int* __restrict__ slots, const int* __restrict__ ban_ids, int n_ban,
+    const unsigned long long* __restrict__ seeds, long long step, float* __restrict__ ws,
+    long long* __restrict__ out_ids, float* __restrict__ out_lp, int* __restrict__ out_kept) {
+  __shared__ float hist[256];
+  __shared__ float red[SAMPLE_THREADS / 64];
+  __shared__ float sh_excl;
+  __shared__ int sh_bin;
+  __shared__ float scan[SAMPLE_THREADS / 64];
+  __shared__ int sh_idx;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const float T = temperature ? temperature[b] : 1.f;
+  const float rp = rep_pen ? rep_pen[b] : 1.f;
+  const int slot = slots ? slots[b] : b;
+  const uint8_t* sn = seen ? seen + (long long)slot * V : nullptr;
+  float* x = ws + (long long)b * V;
+  const bool greedy = !(T > 0.f);
+  const float inv_t = (greedy || T == 1.f) ? 1.f : 1.f / T;
+
+  // pass 1: penalties + temperature -> ws
+  for (int i = tid; i < V; i += SAMPLE_THREADS) {
+    float v = is_bf16 ? bf2f(((const bf16_t*)logits)[b * ld + i]) : ((const float*)logits)[b * ld + i];
+    if (rp != 1.f && sn && sn[i]) v = v < 0.f ? v * rp : v / rp;
+    x[i] = v * inv_t;
+  }
+  __syncthreads();
+  if (ban_ids)
+    for (int j = tid; j < n_ban; j += SAMPLE_THREADS) {
+      const int id = ban_ids[(long long)b * n_ban + j];
+      if (id >= 0 && id < V) x[id] = -INFINITY;
+    }
+  __syncthreads();
+
+  // pass 2: max (+ argmax) and softmax normaliser
+  float m = -INFINITY, s = 0.f;
+  int am = 0x7fffffff;
+  for (int i = tid; i < V; i += SAMPLE_THREADS) {
+    const float v = x[i];
+    if (v > m) {
+      s = s * __expf(m - v) + 1.f;
+      m = v;
+      am = i;
+    } else if (v != -INFINITY) {
+      s += __expf(v - m);
+    }
+  }
+  const float M = block_max(m, red);
+  s = (m == -INFINITY) ? 0.f : s * __expf(m - M);
+  const float Z = block_sum(s, red);
+  const float lZ = M + __logf(Z);
+  if (greedy) {
+    int cand = (m == M) ? am : 0x7fffffff;
+    // first occurrence: block min of candidate indices
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cand = min(cand, __shfl_xor(cand, o, 64));
+    __syncthreads();
+    if ((tid & 63) == 0) red[tid >> 6] = __int_as_float(cand);
+    __syncthreads();
+    if (tid == 0) {
+      int best = 0x7fffffff;
+      for (int w = 0; w < SAMPLE_THREADS / 64; ++w) best = min(best, __float_as_int(red[w]));
+      out_ids[b] = best;
+      if (out_lp) out_lp[b] = x[best] - lZ;
+      if (seen) seen[(long long)slot * V + best] = 1;
+      if (out_kept) out_kept[b] = 1;
+    }
+    return;
+  }
+
+  // top-k: radix select of the k-th largest key (ties at the threshold kept, as
+  // HF's `logits < topk(...)[-1]` mask does)
+  uint32_t thr = 0;
+  const int k = top_k ? top_k[b] : 0;
+  if (k > 0 && k < V) {
+    uint32_t prefix = 0, mask = 0;
+    float remaining = (float)k;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+      for (int i = tid; i < 256; i += SAMPLE_THREADS) hist[i] = 0.f;
+      __syncthreads();
+      for (int i = tid; i < V; i += SAMPLE_THREADS) {
+        const uint32_t key = fkey(x[i]);
+        if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1.f);
+      }
+      __syncthreads();
+      find_bin_desc(hist, remaining, &sh_excl, &sh_bin);
+      const int bin = sh_bin;
+      if (bin < 0) break;
+      prefix |= (uint32_t)bin << shift;
+      mask |= 255u << shift;
+      remaining -= sh_excl;
+      __syncthreads();
+    }
+    thr = prefix;
+  }
+  // top-p: smallest key whose inclusive descending mass reaches p (HF keeps the
+  // tokens whose ascending cumulative probability exceeds 1-p)
+  const float pp = top_p ? top_p[b] : 1.f;
+  if (pp < 1.f) {
+    uint32_t prefix = 0, mask = 0;
+    float above = 0.f, target = 0.f;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+      for (int i = tid; i < 256; i += SAMPLE_THREADS) hist[i] = 0.f;
+      __syncthreads();
+      for (int i = tid; i < V; i += SAMPLE_THREADS) {
+        const float v = x[i];
+        const uint32_t key = fkey(v);
+        if (key >= thr && (key & mask) == prefix && v != -INFINITY)
+          atomicAdd(&hist[(key >> shift) & 255], __expf(v - M));
+      }
+      __syncthreads();
+      if (shift == 24) {  // total kept mass after top-k
+        float t = 0.f;
+        for (int i = tid; i < 256; i += SAMPLE_THREADS) t += hist[i];
+        target = pp * block_sum(t, red);
+      }
+      find_bin_desc(hist, target - above, &sh_excl, &sh_bin);
+      const int bin = sh_bin;
+      if (bin < 0) {  // rounding: target not reached -> keep everything so far
+        prefix = 0;
+        mask = 0;
+        break;
+      }
+      prefix |= (uint32_t)bin << shift;
+      mask |= 255u << shift;
+      above += sh_excl;
+      __syncthreads();
+    }
+    if (mask == 0xffffffffu && prefix > thr) thr = prefix;
+  }
+
+  // multinomial over kept tokens in index order: segment sums + block scan
+  const int seg = (V + SAMPLE_THREADS - 1) / SAMPLE_THREADS;
+  const int lo = min(V, tid * seg), hi = min(V, lo + seg);
+  float ssum = 0.f;
+  int kept = 0;
+  for (int i = lo; i < hi; ++i) {
+    const float v = x[i];
+    if (v != -INFINITY && fkey(v) >= thr) {
+      ssum += __expf(v - M);
+      ++kept;
+    }
+  }
+  // inclusive scan of ssum across the block
+  const int lane = tid & 63, wid = tid >> 6;
+  float incl = ssum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  __syncthreads();
+  if (lane == 63) scan[wid] = incl;
+  __syncthreads();
+  float woff = 0.f, total = 0.f;
+  for (int w = 0; w < SAMPLE_THREADS / 64; ++w) {
+    if (w < wid) woff += scan[w];
+    total += scan[w];
+  }
+  incl += woff;
+  const float excl = incl - ssum;
+  int kept_tot = kept;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) kept_tot += __shfl_xor(kept_tot, o, 64);
+  __syncthreads();
+  if (lane == 0) red[wid] = __int_as_float(kept_tot);
+  if (tid == 0) sh_idx = -1;
+  __syncthreads();
+  // counter = (row if no per-row seeds, step); per-row seeds make a request's
+  // stream independent of the batch row it happens to occupy
+  uint32_t c[4] = {seeds ? 0u : (uint32_t)b, (uint32_t)step,
+                   (uint32_t)((unsigned long long)step >> 32), 0x5eedu};
+  const unsigned long long sd = seeds ? seeds[b] : 0ull;
+  philox4x32_10(c, (uint32_t)sd, (uint32_t)(sd >> 32));
+  const float r = ((c[0] >> 8) + 1) * (1.0f / 16777216.0f);  // (0, 1]
+  const float u = r * total;
+  if (ssum > 0.f && excl < u && u <= incl) {
+    float run = excl;
+    int pick = -1;
+    for (int i = lo; i < hi; ++i) {
+      const float v = x[i];
+      if (v != -INFINITY && fkey(v) >= thr) {
+        pick = i;
+        run += __expf(v - M);
+        if (run >= u) break;
+      }
+    }
+    atomicMax(&sh_idx, pick);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int id = sh_idx;
+    if (id < 0) {  // float rounding at the very top of the range: last kept token
+      for (int i = V - 1; i >= 0; --i)
+        if (x[i] != -INFINITY && fkey(x[i]) >= thr) {
+          id = i;
+          break;
+        }
+      if (id < 0) id = 0;
+    }
+    out_ids[b] = id;
+    if (out_lp) out_lp[b] = x[id] - lZ;
+    if (seen) seen[(long long)slot * V + id] = 1;
+    if (out_kept) {
+      int kt = 0;
+      for (int w = 0; w < SAMPLE_THREADS / 64; ++w) kt += __float_as_int(red[w]);
+      out_kept[b] = kt;
+    }
+  }
+}
+
+KCA_API int kca_sample_logits(const void* logits, long long ld, int is_bf16, int B, int V,
+                              const float* temperature, const int* top_k, const float* top_p,
+                              const float* rep_pen, void* seen, const int* slots,
+                              const int* ban_ids, int n_ban, const unsigned long long* seeds,
+                              long long step, float* ws, long long* out_ids, float* out_lp,
+                              int* out_kept, hipStream_t stream) {
+  if (B <= 0 || V <= 0 || !ws || !out_ids) return 1;
+  hipLaunchKernelGGL(sample_kernel, dim3(B), dim3(SAMPLE_THREADS), 0, stream, logits, ld, is_bf16,
+                     V, temperature, top_k, top_p, rep_pen, (uint8_t*)seen, slots, ban_ids, n_ban,
+                     seeds, step, ws, out_ids, out_lp, out_kept);
+  return 0;
+}

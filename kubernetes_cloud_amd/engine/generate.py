@@ -1,11 +1,9 @@
-"""Autoregressive generation over the native KV cache.
+"""Batch generation API on the continuous-batching engine.
 
-Serves the finetuner's periodic sampler (finetuner.py:538-630, 835-881), the
-evaluator CLI (evaluator.py:175-219), the completion server (inference.py
-80-96) and the KServe predictors (bloom.py:57-77, kserve_api.py:47-72).
-Prefill runs the whole prompt through the flash-attention kernel in one pass;
-each decode step appends one token per sequence to the cache (bottom-right
-aligned causal attention over [0, start+1)).
+Serves the finetuner's periodic sampler (finetuner.py:538-630, 835-881) and
+the evaluator CLI (evaluator.py:175-219) -- HF ``generate`` semantics
+(num_return_sequences, bad_words_ids, min length, repetition penalty, top-k/p)
+over ``LLMEngine`` with a KV cache sized for this call.
 """
 from __future__ import annotations
 
@@ -13,7 +11,7 @@ import dataclasses
 
 import torch
 
-from .sampling import sample_next
+from .llm_engine import LLMEngine, SamplingParams
 
 
 @dataclasses.dataclass
@@ -33,71 +31,45 @@ class GenerationConfig:
     seed: int | None = None
     return_logprobs: bool = False
 
+    def sampling_params(self, seed: int | None = None) -> SamplingParams:
+        return SamplingParams(max_new_tokens=self.max_new_tokens, min_new_tokens=self.min_new_tokens,
+                              do_sample=self.do_sample, temperature=self.temperature, top_k=self.top_k,
+                              top_p=self.top_p, repetition_penalty=self.repetition_penalty, seed=seed,
+                              eos_token_id=self.eos_token_id, stop_sequences=self.stop_sequences,
+                              bad_words_ids=self.bad_words_ids, logprobs=self.return_logprobs)
+
 
 @dataclasses.dataclass
 class GenerationResult:
-    sequences: torch.Tensor        # [N, prompt + new] (padded with pad id after EOS)
+    sequences: torch.Tensor        # [N, prompt + new] (padded with pad id after stop)
     lengths: torch.Tensor          # [N] total valid length
     logprobs: torch.Tensor | None  # [N, new]
     prompt_len: int
 
 
 @torch.no_grad()
-def generate(model, input_ids: torch.Tensor, cfg: GenerationConfig) -> GenerationResult:
-    """``input_ids``: [B, T] prompts of equal length (one request's samples)."""
-    model.eval()
-    dev = next(model.parameters()).device
-    ids = input_ids.to(dev)
-    if cfg.num_return_sequences > 1:
-        ids = ids.repeat_interleave(cfg.num_return_sequences, 0)
-    N, T = ids.shape
-    total = T + cfg.max_new_tokens
-    cache = model.new_cache(N, total)
-    gen = None
-    if cfg.seed is not None:
-        gen = torch.Generator(device=dev)
-        gen.manual_seed(cfg.seed)
-    out = torch.empty(N, total, dtype=torch.long, device=dev)
-    out[:, :T] = ids
-    lps = torch.zeros(N, cfg.max_new_tokens, device=dev) if cfg.return_logprobs else None
-    done = torch.zeros(N, dtype=torch.bool, device=dev)
-    lengths = torch.full((N,), total, dtype=torch.long, device=dev)
+def generate(model, input_ids: torch.Tensor, cfg: GenerationConfig, use_graphs: bool = False) -> GenerationResult:
+    """``input_ids``: [B, T] prompts (one request's samples); sequences come back
+    in input order, ``num_return_sequences`` consecutive rows per prompt."""
+    ids = input_ids.tolist()
+    prompts = [p for p in ids for _ in range(cfg.num_return_sequences)]
+    N, T = len(prompts), input_ids.shape[1]
+    eng = LLMEngine(model, max_slots=N, max_len=min(T + cfg.max_new_tokens, max(model.cfg.max_pos, T + 1)),
+                    use_graphs=use_graphs)
+    params = [cfg.sampling_params(None if cfg.seed is None else cfg.seed + i) for i in range(N)]
+    reqs = eng.generate(prompts, params)
     pad = cfg.pad_token_id if cfg.pad_token_id is not None else (cfg.eos_token_id or 0)
-    logits = model.forward_cached(ids, cache, 0)
-    for i in range(cfg.max_new_tokens):
-        bad = cfg.bad_words_ids
-        if cfg.eos_token_id is not None and i < cfg.min_new_tokens:
-            bad = list(bad or []) + [[cfg.eos_token_id]]
-        res = sample_next(logits, seen=out[:, :T + i], do_sample=cfg.do_sample,
-                          temperature=cfg.temperature, top_k=cfg.top_k, top_p=cfg.top_p,
-                          repetition_penalty=cfg.repetition_penalty, bad_words_ids=bad,
-                          generator=gen, return_logprobs=cfg.return_logprobs)
-        nxt, lp = (res if cfg.return_logprobs else (res, None))
-        nxt = torch.where(done, torch.full_like(nxt, pad), nxt)
-        out[:, T + i] = nxt
-        if lp is not None:
-            lps[:, i] = torch.where(done, torch.zeros_like(lp), lp)
-        newly = ~done & _stopped(out, T + i + 1, nxt, cfg)
-        lengths = torch.where(newly, torch.full_like(lengths, T + i + 1), lengths)
-        done = done | newly
-        if i + 1 == cfg.max_new_tokens or bool(done.all()):
-            if bool(done.all()):
-                out = out[:, :T + i + 1]
-                if lps is not None:
-                    lps = lps[:, :i + 1]
-            break
-        logits = model.forward_cached(nxt[:, None], cache, T + i)
-    lengths = lengths.clamp(max=out.shape[1])
-    return GenerationResult(out, lengths, lps, T)
+    width = T + max(len(r.output) for r in reqs)
+    seqs = torch.full((N, width), pad, dtype=torch.long)
+    lps = torch.zeros(N, width - T) if cfg.return_logprobs else None
+    lens = torch.empty(N, dtype=torch.long)
+    for i, r in enumerate(reqs):
+        toks = r.prompt + r.output
+        seqs[i, :len(toks)] = torch.tensor(toks)
+        lens[i] = len(toks)
+        if lps is not None and r.logprobs:
+            lps[i, :len(r.logprobs)] = torch.tensor(r.logprobs)
+    return GenerationResult(seqs, lens, lps, T)
 
 
-def _stopped(out, upto, nxt, cfg: GenerationConfig):
-    stop = torch.zeros_like(nxt, dtype=torch.bool)
-    if cfg.eos_token_id is not None:
-        stop |= nxt == cfg.eos_token_id
-    for seq in cfg.stop_sequences or []:
-        L = len(seq)
-        if L and upto >= L:
-            tgt = torch.tensor(seq, device=out.device)
-            stop |= (out[:, upto - L:upto] == tgt).all(-1)
-    return stop
+__all__ = ["GenerationConfig", "GenerationResult", "generate"]

@@ -1,0 +1,250 @@
+"""Continuous-batching LLM engine over ``ModelRunner``.
+
+Replaces what the reference delegates to FasterTransformer-on-Triton
+(online-inference/fastertransformer), DeepSpeed-Inference
+(bloom-176b-deepspeed) and HF ``pipeline``/``generate`` (inference.py:67-96,
+bloom.py:57-77, kserve_api.py:47-72): requests join and leave the running batch
+every step (iteration-level scheduling), each request owns one KV-cache slot,
+sampling parameters are per request (FT's per-request runtime_top_k / top_p /
+temperature / repetition_penalty / random_seed / bad_words / stop_words /
+output log-probs).
+
+``step()`` = admit waiting requests (prefill + first token) while slots are
+free, then one fused decode step for every running request. ``start()`` runs
+the loop on a background thread for the HTTP servers; ``generate()`` is the
+synchronous batch API used by the finetuner sampler and the evaluator.
+"""
+from __future__ import annotations
+
+import dataclasses
+import itertools
+import random
+import threading
+import time
+from concurrent.futures import Future
+
+import torch
+
+from .runner import ModelRunner, mix_seed
+
+
+@dataclasses.dataclass
+class SamplingParams:
+    max_new_tokens: int = 50
+    min_new_tokens: int = 0
+    do_sample: bool = True
+    temperature: float = 1.0
+    top_k: int = 0
+    top_p: float = 1.0
+    repetition_penalty: float = 1.0
+    seed: int | None = None
+    eos_token_id: int | None = None
+    stop_sequences: list | None = None   # list of token-id lists (FT stop_words_list)
+    bad_words_ids: list | None = None    # list of token-id lists (FT bad_words_list / HF bad_words_ids)
+    logprobs: bool = False
+
+
+@dataclasses.dataclass
+class Request:
+    rid: int
+    prompt: list
+    params: SamplingParams
+    output: list = dataclasses.field(default_factory=list)
+    logprobs: list = dataclasses.field(default_factory=list)
+    finish_reason: str | None = None
+    slot: int = -1
+    seed: int = 0
+    t_arrive: float = 0.0
+    t_first: float = 0.0
+    t_done: float = 0.0
+    future: Future | None = None
+
+    @property
+    def done(self) -> bool:
+        return self.finish_reason is not None
+
+    @property
+    def tokens(self) -> list:
+        return self.prompt + self.output
+
+
+class LLMEngine:
+    def __init__(self, model, max_slots: int = 32, max_len: int | None = None, use_graphs: bool | None = None,
+                 max_prefill_tokens: int = 16384):
+        self.runner = ModelRunner(model, max_slots=max_slots, max_len=max_len, use_graphs=use_graphs)
+        self.max_len = self.runner.max_len
+        self.free = list(range(max_slots))[::-1]
+        self.waiting: list[Request] = []
+        self.running: list[Request] = []
+        self._ids = itertools.count()
+        self._lock = threading.Lock()
+        self._wake = threading.Event()
+        self._thread = None
+        self._stop = False
+        self.max_prefill_tokens = max_prefill_tokens
+        self.stats = {"steps": 0, "decode_tokens": 0, "prefill_tokens": 0, "finished": 0}
+
+    # ------------------------------------------------------------ requests
+    def add_request(self, prompt: list, params: SamplingParams, future: Future | None = None) -> Request:
+        prompt = [int(t) for t in prompt]
+        if not prompt:
+            raise ValueError("empty prompt")
+        if len(prompt) >= self.max_len:
+            prompt = prompt[-(self.max_len - 1):]
+        seed = params.seed if params.seed is not None else random.getrandbits(63)
+        r = Request(next(self._ids), prompt, params, seed=seed, t_arrive=time.perf_counter(), future=future)
+        if params.max_new_tokens <= 0:
+            r.finish_reason = "length"
+            r.t_done = r.t_arrive
+            if future is not None:
+                future.set_result(r)
+            return r
+        with self._lock:
+            self.waiting.append(r)
+        self._wake.set()
+        return r
+
+    def has_work(self) -> bool:
+        return bool(self.waiting or self.running)
+
+    def _row(self, r: Request, token: int | None = None) -> dict:
+        p = r.params
+        n_gen = len(r.output)
+        greedy = (not p.do_sample) or p.temperature <= 0
+        bans = []
+        for w in p.bad_words_ids or ():
+            if len(w) == 1:
+                bans.append(int(w[0]))
+            elif len(w) > 1 and r.tokens[-(len(w) - 1):] == list(w[:-1]):
+                bans.append(int(w[-1]))
+        if p.eos_token_id is not None and n_gen < p.min_new_tokens:
+            bans.append(int(p.eos_token_id))
+        return {"token": token if token is not None else r.tokens[-1], "pos": len(r.tokens) - 1,
+                "slot": r.slot, "temperature": 0.0 if greedy else float(p.temperature),
+                "top_k": int(p.top_k or 0), "top_p": float(p.top_p if p.top_p is not None else 1.0),
+                "rep": float(p.repetition_penalty or 1.0), "seed": mix_seed(r.seed, n_gen), "bans": bans}
+
+    def _append(self, r: Request, tok: int, lp: float):
+        r.output.append(int(tok))
+        if r.params.logprobs:
+            r.logprobs.append(float(lp))
+        p = r.params
+        if len(r.output) == 1:
+            r.t_first = time.perf_counter()
+        if p.eos_token_id is not None and tok == p.eos_token_id and len(r.output) > p.min_new_tokens:
+            r.finish_reason = "stop"
+        elif any(s and r.output[-len(s):] == list(s) for s in (p.stop_sequences or ())):
+            r.finish_reason = "stop"
+        elif len(r.output) >= p.max_new_tokens or len(r.tokens) >= self.max_len:
+            r.finish_reason = "length"
+
+    def _finish(self, r: Request):
+        r.t_done = time.perf_counter()
+        if r.slot >= 0:
+            self.free.append(r.slot)
+            r.slot = -1
+        self.stats["finished"] += 1
+        if r.future is not None and not r.future.done():
+            r.future.set_result(r)
+
+    # ---------------------------------------------------------------- step
+    def step(self) -> list[Request]:
+        """Admit + one decode step. Returns the requests that finished."""
+        finished = []
+        with self._lock:
+            admit = []
+            budget = self.max_prefill_tokens
+            while self.waiting and self.free and (not admit or budget >= len(self.waiting[0].prompt)):
+                r = self.waiting.pop(0)
+                r.slot = self.free.pop()
+                budget -= len(r.prompt)
+                admit.append(r)
+        # prefill: same-length prompts share one batched pass
+        by_len: dict = {}
+        for r in admit:
+            by_len.setdefault(len(r.prompt), []).append(r)
+        for T, group in by_len.items():
+            ids = torch.tensor([r.prompt for r in group], dtype=torch.long)
+            logits = self.runner.prefill(ids, [r.slot for r in group])
+            toks, lps = self.runner.sample_first(logits, [self._row(r, 0) for r in group])
+            self.stats["prefill_tokens"] += T * len(group)
+            for r, t, lp in zip(group, toks, lps):
+                self._append(r, t, lp)
+                if r.done:
+                    self._finish(r)
+                    finished.append(r)
+                else:
+                    self.running.append(r)
+        # decode one token for everything already running (incl. just admitted)
+        if self.running:
+            rows = [self._row(r) for r in self.running]
+            toks, lps = self.runner.decode(rows)
+            self.stats["decode_tokens"] += len(rows)
+            still = []
+            for r, t, lp in zip(self.running, toks, lps):
+                self._append(r, t, lp)
+                if r.done:
+                    self._finish(r)
+                    finished.append(r)
+                else:
+                    still.append(r)
+            self.running = still
+        self.stats["steps"] += 1
+        return finished
+
+    def run_until_done(self, reqs: list[Request] | None = None):
+        while self.has_work() and (reqs is None or not all(r.done for r in reqs)):
+            self.step()
+
+    def generate(self, prompts: list[list[int]], params: SamplingParams | list[SamplingParams]) -> list[Request]:
+        ps = params if isinstance(params, list) else [params] * len(prompts)
+        reqs = [self.add_request(p, sp) for p, sp in zip(prompts, ps)]
+        self.run_until_done(reqs)
+        return reqs
+
+    # ------------------------------------------------------ background loop
+    def submit(self, prompt: list, params: SamplingParams) -> Future:
+        if self._thread is None:
+            self.start()
+        fut: Future = Future()
+        self.add_request(prompt, params, fut)
+        return fut
+
+    def start(self):
+        if self._thread is not None:
+            return
+        self._stop = False
+        self._thread = threading.Thread(target=self._loop, name="llm-engine", daemon=True)
+        self._thread.start()
+
+    def stop(self):
+        self._stop = True
+        self._wake.set()
+        if self._thread is not None:
+            self._thread.join()
+            self._thread = None
+
+    def _loop(self):
+        dev = self.runner.device
+        if dev.type == "cuda":
+            torch.cuda.set_device(dev)
+        while not self._stop:
+            if not self.has_work():
+                self._wake.wait(0.05)
+                self._wake.clear()
+                continue
+            try:
+                self.step()
+            except Exception as e:  # fail every in-flight request, keep serving
+                with self._lock:
+                    victims = self.running + self.waiting
+                    self.running, self.waiting = [], []
+                for r in victims:
+                    if r.slot >= 0:
+                        self.free.append(r.slot)
+                        r.slot = -1
+                    if r.future is not None and not r.future.done():
+                        r.future.set_exception(e)
+
+
+__all__ = ["LLMEngine", "SamplingParams", "Request"]

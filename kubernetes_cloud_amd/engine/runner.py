@@ -1,0 +1,319 @@
+"""Model runner for serving: slot KV cache, prefill, fused decode step, HIP graphs.
+
+The FT-equivalent decode loop for every causal LM in
+``models.causal_lm`` (GPT-2, GPT-J, GPT-NeoX/Pythia, GPT-Neo, BLOOM):
+
+* ``KVCache``: one [slots+1, Hkv, max_len, D] K and V tensor per layer (head-major
+  so each (sequence, head) is a contiguous HBM stream; the extra slot is scratch
+  for padding rows of a graph bucket). 288 GB of HBM holds e.g. 64 GPT-J
+  sequences x 2048 tokens (60 GB) next to the 12 GB of weights.
+* ``prefill``: the prompt through the flash-attention kernel, K/V (post-RoPE)
+  written into the request's slot.
+* ``decode``: one token per running sequence -- fused QKV GEMM ->
+  ``kca_decode_prep`` (RoPE + cache append) -> ``kca_decode_attn`` (split-K) ->
+  out-proj, residual adds fused into the next LayerNorm -> LM head ->
+  ``kca_sample_logits``. On GPU the whole step (all layers + sampling) is
+  captured once per (batch bucket, kv bucket) into a HIP graph and replayed, so
+  a GPT-J step is one graph launch + one 8-byte/row D2H copy.
+
+Host inputs of a step (tokens, positions, slots, sampling params, bans, seeds)
+travel in ONE packed pinned buffer -> one H2D copy.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .. import ops
+from ..ops import decode as dops
+
+
+def _next_pow2(n: int, lo: int = 1) -> int:
+    p = lo
+    while p < n:
+        p *= 2
+    return p
+
+
+class KVCache:
+    def __init__(self, n_layers: int, slots: int, kv_heads: int, max_len: int, head_dim: int,
+                 device, dtype=torch.bfloat16):
+        shape = (slots + 1, kv_heads, max_len, head_dim)
+        self.k = [torch.zeros(shape, device=device, dtype=dtype) for _ in range(n_layers)]
+        self.v = [torch.zeros(shape, device=device, dtype=dtype) for _ in range(n_layers)]
+        self.slots, self.max_len, self.scratch = slots, max_len, slots
+
+    def nbytes(self) -> int:
+        return sum(t.numel() * t.element_size() for t in self.k + self.v)
+
+
+class _Packed:
+    """Several small typed arrays in one byte buffer (pinned host + device twin)."""
+
+    def __init__(self, fields, device):
+        self.off, self.fields = {}, fields
+        o = 0
+        for name, (dt, n) in fields.items():
+            o = (o + 7) // 8 * 8
+            self.off[name] = o
+            o += n * torch.empty(0, dtype=dt).element_size()
+        self.nbytes = (o + 7) // 8 * 8
+        pin = device.type == "cuda"
+        self.host = torch.zeros(self.nbytes, dtype=torch.uint8, pin_memory=pin)
+        self.dev = torch.zeros(self.nbytes, dtype=torch.uint8, device=device)
+
+    def _view(self, buf, name):
+        dt, n = self.fields[name]
+        o = self.off[name]
+        es = torch.empty(0, dtype=dt).element_size()
+        return buf[o:o + n * es].view(dt)
+
+    def h(self, name):
+        return self._view(self.host, name)
+
+    def d(self, name):
+        return self._view(self.dev, name)
+
+    def upload(self):
+        self.dev.copy_(self.host, non_blocking=True)
+
+
+class ModelRunner:
+    def __init__(self, model, max_slots: int = 32, max_len: int | None = None, use_graphs: bool | None = None,
+                 max_bans: int = 16):
+        self.model = model.eval()
+        cfg = model.cfg
+        self.cfg = cfg
+        p = next(model.parameters())
+        self.device, self.dtype = p.device, p.dtype
+        self.max_len = max_len or cfg.max_pos
+        self.H, self.Hkv, self.D = cfg.n_heads, cfg.kv_heads, cfg.head_dim
+        self.V = cfg.vocab_size
+        self.cache = KVCache(cfg.n_layers, max_slots, self.Hkv, self.max_len, self.D, self.device, self.dtype)
+        self.max_slots = max_slots
+        self.rot = cfg.rotary_dim
+        if self.rot > 0:
+            self.cos, self.sin = ops.rope_tables(self.rot, self.max_len, cfg.rotary_base, self.device)
+        else:
+            self.cos = self.sin = None
+        self.seen = torch.zeros(max_slots + 1, self.V, dtype=torch.uint8, device=self.device)
+        self.max_bans = max_bans
+        on_gpu = self.device.type == "cuda"
+        self.use_graphs = on_gpu if use_graphs is None else (use_graphs and on_gpu)
+        self._graphs: dict = {}
+        self._pool = None
+        self._static: dict = {}
+        self._windowed = any(getattr(b.attn, "window", 0) for b in model.h)
+
+    # ------------------------------------------------------------- prefill
+    @torch.no_grad()
+    def prefill(self, ids: torch.Tensor, slots: list[int]) -> torch.Tensor:
+        """ids [n, T] (same length prompts) -> last-position logits [n, V]. Writes
+        K/V of positions [0, T) into each slot and marks the prompt as seen."""
+        m, cfg = self.model, self.cfg
+        ids = ids.to(self.device)
+        n, T = ids.shape
+        assert T <= self.max_len
+        sl = torch.tensor(slots, device=self.device, dtype=torch.long)
+        self.seen[sl] = 0
+        self.seen[sl[:, None].expand(n, T), ids] = 1
+        h = m.wte(ids)
+        if m.wpe is not None:
+            h = h + m.wpe(torch.arange(T, device=self.device))
+        if m.emb_ln is not None:
+            h = m.emb_ln(h)
+        pending = ()
+        for li, blk in enumerate(m.h):
+            x, h = blk.ln_1(h, residual=pending) if pending else (blk.ln_1(h), h)
+            at = blk.attn
+            qkv = at.qkv(x).view(n, T, 3, self.H, self.D)
+            q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+            if self.rot > 0:
+                ops.apply_rotary_(q, k, self.rot, T, cfg.rotary_interleaved, cfg.rotary_base,
+                                  max_pos=self.max_len)
+            self.cache.k[li][sl, :, :T] = k.transpose(1, 2)
+            self.cache.v[li][sl, :, :T] = v.transpose(1, 2)
+            if at.window:
+                o = self._windowed_prefill(q, k, v, at)
+            else:
+                o = ops.flash_attention(q, k, v, causal=True, scale=at.scale, alibi=at.alibi)
+            a = at.out(o.reshape(n, T, -1))
+            if cfg.parallel_residual:
+                x2 = x if blk.ln_2 is None else blk.ln_2(h)
+                pending = (a, blk.mlp(x2))
+            else:
+                x2, h = blk.ln_2(h, residual=(a,))
+                pending = (blk.mlp(x2),)
+        y, _ = m.ln_f(h[:, -1:], residual=tuple(p_[:, -1:] for p_ in pending))
+        return m.logits_from_hidden(y)[:, -1]
+
+    @staticmethod
+    def _windowed_prefill(q, k, v, at):
+        T = q.shape[1]
+        s = torch.einsum("bqhd,bkhd->bhqk", q.float(), k.float()) * at.scale
+        qi = torch.arange(T, device=q.device)[:, None]
+        ki = torch.arange(T, device=q.device)[None, :]
+        s = s.masked_fill((ki > qi) | (ki <= qi - at.window), float("-inf"))
+        return torch.einsum("bhqk,bkhd->bqhd", s.softmax(-1), v.float()).to(q.dtype)
+
+    # -------------------------------------------------------------- decode
+    def _layers_decode(self, tokens, pos, slots, kv_lens, max_kv, ws, obuf):
+        m, cfg = self.model, self.cfg
+        h = m.wte(tokens)
+        if m.wpe is not None:
+            h = h + m.wpe(pos.long())
+        if m.emb_ln is not None:
+            h = m.emb_ln(h)
+        pending = ()
+        for li, blk in enumerate(m.h):
+            x, h = blk.ln_1(h, residual=pending) if pending else (blk.ln_1(h), h)
+            at = blk.attn
+            qkv = at.qkv(x)
+            kc, vc = self.cache.k[li], self.cache.v[li]
+            dops.decode_prep(qkv, self.H, self.Hkv, self.D, self.rot, cfg.rotary_interleaved, self.cos,
+                             self.sin, pos, slots, kc, vc)
+            if at.window:
+                o = self._windowed_decode(qkv, kc, vc, slots, kv_lens, at)
+            else:
+                o = dops.decode_attention(qkv, kc, vc, slots, kv_lens, self.H, max_kv, at.scale, at.alibi,
+                                          out=obuf, ws=ws)
+            a = at.out(o)
+            if cfg.parallel_residual:
+                x2 = x if blk.ln_2 is None else blk.ln_2(h)
+                pending = (a, blk.mlp(x2))
+            else:
+                x2, h = blk.ln_2(h, residual=(a,))
+                pending = (blk.mlp(x2),)
+        y, _ = m.ln_f(h, residual=pending)
+        return m.logits_from_hidden(y)
+
+    def _windowed_decode(self, qkv, kc, vc, slots, kv_lens, at):
+        B = qkv.shape[0]
+        out = torch.empty(B, self.H * self.D, device=qkv.device, dtype=qkv.dtype)
+        for b in range(B):
+            L = int(kv_lens[b])
+            lo = max(0, L - at.window)
+            s = int(slots[b])
+            sub_len = torch.tensor([L - lo], dtype=torch.int32)
+            dops.decode_attention_reference(qkv[b:b + 1], kc[s:s + 1, :, lo:L], vc[s:s + 1, :, lo:L],
+                                            torch.zeros(1, dtype=torch.int32), sub_len, self.H, at.scale,
+                                            None, out[b:b + 1])
+        return out
+
+    def _static_for(self, Bb: int, Kb: int):
+        key = (Bb, Kb)
+        st = self._static.get(key)
+        if st is not None:
+            return st
+        NB = self.max_bans
+        pk = _Packed({"tokens": (torch.int64, Bb), "seeds": (torch.int64, Bb), "pos": (torch.int32, Bb),
+                      "slots": (torch.int32, Bb), "kv_lens": (torch.int32, Bb), "top_k": (torch.int32, Bb),
+                      "temperature": (torch.float32, Bb), "top_p": (torch.float32, Bb),
+                      "rep": (torch.float32, Bb), "bans": (torch.int32, Bb * NB)}, self.device)
+        ws_n = dops.decode_ws_floats(Bb, self.H, self.Hkv, self.D, Kb)
+        st = {
+            "pk": pk,
+            "ws": torch.empty(max(ws_n, 1), device=self.device, dtype=torch.float32),
+            "obuf": torch.empty(Bb, self.H * self.D, device=self.device, dtype=self.dtype),
+            "sws": torch.empty(Bb * self.V, device=self.device, dtype=torch.float32),
+            "ids": torch.empty(Bb, device=self.device, dtype=torch.int64),
+            "lps": torch.empty(Bb, device=self.device, dtype=torch.float32),
+        }
+        self._static[key] = st
+        return st
+
+    def _step_body(self, st, Bb, Kb):
+        pk = st["pk"]
+        logits = self._layers_decode(pk.d("tokens"), pk.d("pos"), pk.d("slots"), pk.d("kv_lens"), Kb,
+                                     st["ws"], st["obuf"])
+        dops.sample_logits(logits, temperature=pk.d("temperature"), top_k=pk.d("top_k"), top_p=pk.d("top_p"),
+                           rep_penalty=pk.d("rep"), seen=self.seen, slots=pk.d("slots"),
+                           ban_ids=pk.d("bans").view(Bb, self.max_bans), seeds=pk.d("seeds"), step=0,
+                           ws=st["sws"], out_ids=st["ids"], out_logprobs=st["lps"])
+
+    @torch.no_grad()
+    def decode(self, rows: list[dict]):
+        """rows: [{token, pos, slot, temperature, top_k, top_p, rep, seed, bans}]
+        -> (ids list[int], logprobs list[float]) of the next token per row."""
+        n = len(rows)
+        Bb = _next_pow2(n)
+        max_kv = max(r["pos"] for r in rows) + 1
+        Kb = min(_next_pow2(max_kv, 256), self.max_len)
+        if self._windowed or self.device.type != "cuda":
+            Bb = n  # GPU eager keeps the graph buckets so both paths run identical shapes
+        st = self._static_for(Bb, Kb)
+        pk = st["pk"]
+        NB = self.max_bans
+        tok, sd, pos, sl, kl = pk.h("tokens"), pk.h("seeds"), pk.h("pos"), pk.h("slots"), pk.h("kv_lens")
+        tk, te, tp, rp, bans = pk.h("top_k"), pk.h("temperature"), pk.h("top_p"), pk.h("rep"), pk.h("bans")
+        bans.fill_(-1)
+        for i in range(Bb):
+            if i < n:
+                r = rows[i]
+                tok[i], pos[i], sl[i], kl[i] = r["token"], r["pos"], r["slot"], r["pos"] + 1
+                te[i], tk[i], tp[i], rp[i] = r["temperature"], r["top_k"], r["top_p"], r["rep"]
+                sd[i] = r["seed"]
+                b = r.get("bans") or ()
+                if len(b) > NB:
+                    raise ValueError(f"{len(b)} banned ids > max_bans={NB}")
+                for j, t in enumerate(b):
+                    bans[i * NB + j] = t
+            else:  # padding row -> scratch slot
+                tok[i], pos[i], sl[i], kl[i] = 0, 0, self.cache.scratch, 1
+                te[i], tk[i], tp[i], rp[i], sd[i] = 0.0, 0, 1.0, 1.0, 0
+        pk.upload()
+        if self.use_graphs and not self._windowed:
+            g = self._graphs.get((Bb, Kb))
+            if g is None:
+                g = self._capture(st, Bb, Kb)
+            g.replay()
+        else:
+            self._step_body(st, Bb, Kb)
+        ids = st["ids"][:n].tolist()
+        lps = st["lps"][:n].tolist()
+        return ids, lps
+
+    def _capture(self, st, Bb, Kb):
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):  # warm up (allocator, hipBLASLt heuristics)
+                self._step_body(st, Bb, Kb)
+        torch.cuda.current_stream().wait_stream(s)
+        if self._pool is None:
+            self._pool = torch.cuda.graph_pool_handle()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, pool=self._pool):
+            self._step_body(st, Bb, Kb)
+        self._graphs[(Bb, Kb)] = g
+        return g
+
+    @torch.no_grad()
+    def sample_first(self, logits: torch.Tensor, rows: list[dict]):
+        """Sample from prefill logits [n, V] (row params as in ``decode``)."""
+        n = logits.shape[0]
+        dev = self.device
+        NB = self.max_bans
+        bans = torch.full((n, NB), -1, dtype=torch.int32)
+        for i, r in enumerate(rows):
+            for j, t in enumerate((r.get("bans") or ())[:NB]):
+                bans[i, j] = t
+        f = lambda k, dt: torch.tensor([r[k] for r in rows], dtype=dt, device=dev)  # noqa: E731
+        ids, lps = dops.sample_logits(
+            logits.contiguous(), temperature=f("temperature", torch.float32), top_k=f("top_k", torch.int32),
+            top_p=f("top_p", torch.float32), rep_penalty=f("rep", torch.float32), seen=self.seen,
+            slots=f("slot", torch.int32), ban_ids=bans.to(dev), seeds=f("seed", torch.int64), step=0)
+        return ids.tolist(), lps.tolist()
+
+
+def mix_seed(seed: int, step: int) -> int:
+    """Per-(request, token) 64-bit Philox key as a signed int64."""
+    x = (seed * 0x9E3779B97F4A7C15 + (step + 1) * 0xBF58476D1CE4E5B9) & ((1 << 64) - 1)
+    x ^= x >> 31
+    x = (x * 0x94D049BB133111EB) & ((1 << 64) - 1)
+    x ^= x >> 29
+    return x - (1 << 64) if x >= (1 << 63) else x
+
+
+__all__ = ["KVCache", "ModelRunner", "mix_seed", "math"]

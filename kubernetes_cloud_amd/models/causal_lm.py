@@ -71,35 +71,6 @@ class Attention(nn.Module):
         else:
             self.alibi = None
 
-    def forward_cached(self, x: torch.Tensor, cache_k: torch.Tensor, cache_v: torch.Tensor,
-                       start: int, pos_ids: torch.Tensor | None = None) -> torch.Tensor:
-        """Incremental attention for generation: appends this chunk's K/V to the
-        per-layer cache [B, max_len, H, D] and attends over [0, start+T)."""
-        B, T, _ = x.shape
-        cfg = self.cfg
-        qkv = self.qkv(x).view(B, T, 3, self.n_heads, self.head_dim)
-        q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
-        if cfg.rotary_dim > 0:
-            if pos_ids is None:
-                pos_ids = torch.arange(start, start + T, device=x.device).repeat(B)
-            ops.apply_rotary_(q, k, cfg.rotary_dim, T, cfg.rotary_interleaved, cfg.rotary_base,
-                              pos_ids=pos_ids, max_pos=max(cfg.max_pos, start + T))
-        cache_k[:, start:start + T] = k
-        cache_v[:, start:start + T] = v
-        L = start + T
-        if self.window:
-            qf = q.float()
-            kf, vf = cache_k[:, :L].float(), cache_v[:, :L].float()
-            s = torch.einsum("bqhd,bkhd->bhqk", qf, kf) * self.scale
-            qi = torch.arange(start, L, device=x.device)[:, None]
-            ki = torch.arange(L, device=x.device)[None, :]
-            s = s.masked_fill((ki > qi) | (ki <= qi - self.window), float("-inf"))
-            o = torch.einsum("bhqk,bkhd->bqhd", s.softmax(-1), vf).to(x.dtype)
-        else:
-            o = ops.flash_attention(q, cache_k[:, :L], cache_v[:, :L], causal=True, scale=self.scale,
-                                    alibi=self.alibi)
-        return self.out(o.reshape(B, T, -1))
-
     def forward(self, x: torch.Tensor, kv_len: torch.Tensor | None = None) -> torch.Tensor:
         B, S, _ = x.shape
         qkv = self.qkv(x)
@@ -263,38 +234,6 @@ class CausalLM(nn.Module):
 
     def num_parameters(self) -> int:
         return sum(p.numel() for p in self.parameters())
-
-    # ------------------------------------------------------------ generation
-    def new_cache(self, batch: int, max_len: int, device=None, dtype=None):
-        cfg = self.cfg
-        p = next(self.parameters())
-        shape = (batch, max_len, cfg.kv_heads, cfg.head_dim)
-        return [(torch.empty(shape, device=device or p.device, dtype=dtype or p.dtype),
-                 torch.empty(shape, device=device or p.device, dtype=dtype or p.dtype))
-                for _ in range(cfg.n_layers)]
-
-    @torch.no_grad()
-    def forward_cached(self, input_ids: torch.Tensor, cache, start: int) -> torch.Tensor:
-        """Logits of the LAST position after appending ``input_ids`` [B, T]."""
-        B, T = input_ids.shape
-        h = self.wte(input_ids)
-        if self.wpe is not None:
-            h = h + self.wpe(torch.arange(start, start + T, device=input_ids.device))
-        if self.emb_ln is not None:
-            h = self.emb_ln(h)
-        pos = torch.arange(start, start + T, device=input_ids.device).repeat(B).to(torch.int32)
-        pending = ()
-        for blk, (ck, cv) in zip(self.h, cache):
-            x, h = blk.ln_1(h, residual=pending) if pending else (blk.ln_1(h), h)
-            a = blk.attn.forward_cached(x, ck, cv, start, pos)
-            if self.cfg.parallel_residual:
-                x2 = x if blk.ln_2 is None else blk.ln_2(h)
-                pending = (a, blk.mlp(x2))
-            else:
-                x2, h = blk.ln_2(h, residual=(a,))
-                pending = (blk.mlp(x2),)
-        y, _ = self.ln_f(h[:, -1:], residual=tuple(p[:, -1:] for p in pending))
-        return self.logits_from_hidden(y)[:, -1]
 
 
 def build_model(cfg: LMConfig, device="cpu", dtype=torch.bfloat16, seed: int | None = 0) -> CausalLM:

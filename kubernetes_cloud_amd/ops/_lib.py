@@ -53,8 +53,10 @@ _SIGS = {
     "kca_attn_bwd": [P] * 10 + [LL] * 21 + [I] * 7 + [F, P, P, P],
     "kca_groupnorm_fwd": [P, P, P, P, P, P, P, I, I, I, I, F, I, P],
     "kca_groupnorm_bwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P],
-    "kca_sample_logits": [P, LL, I, I, P, P, P, P, P, P, P, P, P, I, P],
-    "kca_decode_attn": [P] * 6 + [LL] * 8 + [I] * 7 + [F, P, P],
+    "kca_decode_prep": [P, LL, I, I, I, I, I, I, P, P, P, P, P, P, LL, LL, LL, P],
+    "kca_decode_chunk": [I, I, I],
+    "kca_decode_attn": [P, LL, P, P, LL, LL, LL, P, P, P, LL, P, LL, I, I, I, I, I, I, F, P, P],
+    "kca_sample_logits": [P, LL, I, I, I, P, P, P, P, P, P, P, I, P, LL, P, P, P, P, P],
 }
 
 

@@ -1,0 +1,226 @@
+"""Decode-path ops (K11/K12/K13/K31/K32) for the serving engine.
+
+* ``decode_prep``       RoPE on the step's Q/K + append K/V into the slot cache
+* ``decode_attention``  split-K flash-decoding over the head-major slot cache
+* ``sample_logits``     fused penalty/bans/temperature/top-k/top-p/multinomial
+
+bf16 GPU tensors run ``csrc/kernels/decode.hip``; CPU tensors run the fp32
+references below (same semantics; used by the CPU test-suite and to pin the
+kernels in ``tests/test_decode_gpu.py``).
+
+Cache layout: ``k_cache``/``v_cache`` are [slots, Hkv, max_len, D] (one per
+layer); a request owns one slot for its lifetime.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import _lib
+
+
+# ------------------------------------------------------------------- prep
+def decode_prep(qkv: torch.Tensor, n_heads: int, kv_heads: int, head_dim: int, rot: int,
+                interleaved: bool, cos: torch.Tensor | None, sin: torch.Tensor | None,
+                pos: torch.Tensor, slots: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor):
+    """qkv: [B, (H+2Hkv)*D] (row-strided). Rotates Q in place, writes rotated K and
+    V of each row b into cache[slots[b], :, pos[b]]."""
+    B = qkv.shape[0]
+    H, Hkv, D = n_heads, kv_heads, head_dim
+    if _lib.use_native(qkv, k_cache):
+        assert qkv.stride(-1) == 1 and k_cache.stride(-1) == 1 and k_cache.stride() == v_cache.stride()
+        assert pos.dtype == torch.int32 and slots.dtype == torch.int32
+        _lib.call("kca_decode_prep", qkv.data_ptr(), qkv.stride(0), B, H, Hkv, D, rot, int(interleaved),
+                  _lib.ptr(cos), _lib.ptr(sin), pos.data_ptr(), slots.data_ptr(), k_cache.data_ptr(),
+                  v_cache.data_ptr(), k_cache.stride(0), k_cache.stride(1), k_cache.stride(2), _lib.stream())
+        return
+    rows = qkv.view(B, H + 2 * Hkv, D)
+    x = rows.to(torch.float32, copy=True)  # never alias: K rows of qkv stay unrotated
+    if rot > 0:
+        half = rot // 2
+        p = pos.long()
+        c, s = cos[p][:, None, :], sin[p][:, None, :]  # [B, 1, rot/2]
+        xr = x[:, :H + Hkv, :rot]
+        if interleaved:
+            a, b = xr[..., 0::2], xr[..., 1::2]
+            out = torch.stack((a * c - b * s, b * c + a * s), dim=-1).flatten(-2)
+        else:
+            a, b = xr[..., :half], xr[..., half:]
+            out = torch.cat((a * c - b * s, b * c + a * s), dim=-1)
+        x[:, :H + Hkv, :rot] = out
+        rows[:, :H, :rot] = x[:, :H, :rot].to(rows.dtype)
+    sl, p = slots.long(), pos.long()
+    k_cache[sl, :, p] = x[:, H:H + Hkv].to(k_cache.dtype)
+    v_cache[sl, :, p] = x[:, H + Hkv:].to(v_cache.dtype)
+
+
+# -------------------------------------------------------------- attention
+def decode_ws_floats(B: int, H: int, Hkv: int, D: int, max_kv: int, chunk: int = 0) -> int:
+    if chunk <= 0:
+        chunk = decode_chunk(B, Hkv, max_kv)
+    ns = -(-max_kv // chunk)
+    return B * H * ns * (D + 2) if ns > 1 else 0
+
+
+def decode_chunk(B: int, Hkv: int, max_kv: int) -> int:
+    """Mirror of kca_decode_chunk: >= ~512 (seq, head, split) workgroups."""
+    work = B * Hkv
+    want = -(-512 // work)
+    c = -(-max_kv // want)
+    c = -(-c // 64) * 64
+    return max(64, min(1024, c))
+
+
+def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slots: torch.Tensor,
+                     kv_lens: torch.Tensor, n_heads: int, max_kv: int, scale: float | None = None,
+                     alibi: torch.Tensor | None = None, out: torch.Tensor | None = None,
+                     ws: torch.Tensor | None = None, chunk: int = 0) -> torch.Tensor:
+    """q: [B, >=H*D] (row-strided; e.g. the Q slice of the fused QKV buffer).
+    Attends row b over cache[slots[b], :, :kv_lens[b]]. Returns [B, H*D]."""
+    B = q.shape[0]
+    _, Hkv, L, D = k_cache.shape
+    H = n_heads
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if out is None:
+        out = torch.empty(B, H * D, device=q.device, dtype=q.dtype)
+    if _lib.use_native(q, k_cache):
+        assert q.stride(-1) == 1 and out.stride(-1) == 1 and k_cache.stride() == v_cache.stride()
+        assert max_kv <= L
+        if chunk <= 0:
+            chunk = decode_chunk(B, Hkv, max_kv)
+        need = decode_ws_floats(B, H, Hkv, D, max_kv, chunk)
+        if need and (ws is None or ws.numel() < need):
+            ws = torch.empty(need, device=q.device, dtype=torch.float32)
+        _lib.call("kca_decode_attn", q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+                  k_cache.stride(0), k_cache.stride(1), k_cache.stride(2), slots.data_ptr(),
+                  kv_lens.data_ptr(), out.data_ptr(), out.stride(0), _lib.ptr(ws),
+                  ws.numel() if ws is not None else 0, B, H, Hkv, D, max_kv, chunk, float(scale),
+                  _lib.ptr(alibi), _lib.stream())
+        return out
+    return decode_attention_reference(q, k_cache, v_cache, slots, kv_lens, H, scale, alibi, out)
+
+
+def decode_attention_reference(q, k_cache, v_cache, slots, kv_lens, n_heads, scale, alibi=None, out=None):
+    B = q.shape[0]
+    _, Hkv, L, D = k_cache.shape
+    H = n_heads
+    if out is None:
+        out = torch.empty(B, H * D, device=q.device, dtype=q.dtype)
+    for b in range(B):
+        n = int(kv_lens[b])
+        s_ = int(slots[b])
+        qb = q[b, :H * D].float().view(H, D)
+        kb = k_cache[s_, :, :n].float().repeat_interleave(H // Hkv, 0)  # [H, n, D]
+        vb = v_cache[s_, :, :n].float().repeat_interleave(H // Hkv, 0)
+        sc = torch.einsum("hd,hnd->hn", qb, kb) * scale
+        if alibi is not None:
+            sc = sc + alibi.float()[:, None] * (torch.arange(n, device=q.device) - (n - 1)).float()[None]
+        o = torch.einsum("hn,hnd->hd", sc.softmax(-1), vb)
+        out[b] = o.reshape(-1).to(out.dtype)
+    return out
+
+
+# --------------------------------------------------------------- sampling
+def sample_logits(logits: torch.Tensor, *, temperature: torch.Tensor, top_k: torch.Tensor,
+                  top_p: torch.Tensor, rep_penalty: torch.Tensor | None = None,
+                  seen: torch.Tensor | None = None, slots: torch.Tensor | None = None,
+                  ban_ids: torch.Tensor | None = None, seeds: torch.Tensor | None = None, step: int = 0,
+                  ws: torch.Tensor | None = None, out_ids: torch.Tensor | None = None,
+                  out_logprobs: torch.Tensor | None = None, out_kept: torch.Tensor | None = None):
+    """Per-row parameters (all [B]): temperature (<= 0 -> greedy), top_k (0 = off),
+    top_p (1 = off), rep_penalty. ``seen`` is a [slots, V] uint8 mask of tokens
+    already in each sequence (repetition penalty; the chosen id is marked).
+    ``ban_ids`` [B, n] (-1 padded) get -inf. Returns (ids int64 [B], logprob [B])
+    where logprob is under the penalised, temperature-scaled distribution."""
+    B, V = logits.shape
+    dev = logits.device
+    if out_ids is None:
+        out_ids = torch.empty(B, dtype=torch.int64, device=dev)
+    if out_logprobs is None:
+        out_logprobs = torch.empty(B, dtype=torch.float32, device=dev)
+    if logits.is_cuda and logits.dtype in (torch.bfloat16, torch.float32):
+        if ws is None or ws.numel() < B * V:
+            ws = torch.empty(B * V, device=dev, dtype=torch.float32)
+        assert logits.stride(-1) == 1
+        n_ban = ban_ids.shape[1] if ban_ids is not None else 0
+        _lib.call("kca_sample_logits", logits.data_ptr(), logits.stride(0),
+                  int(logits.dtype == torch.bfloat16), B, V, temperature.data_ptr(), top_k.data_ptr(),
+                  top_p.data_ptr(), _lib.ptr(rep_penalty), _lib.ptr(seen), _lib.ptr(slots),
+                  _lib.ptr(ban_ids), n_ban, _lib.ptr(seeds), int(step), ws.data_ptr(),
+                  out_ids.data_ptr(), out_logprobs.data_ptr(), _lib.ptr(out_kept), _lib.stream())
+        return out_ids, out_logprobs
+    return sample_logits_reference(logits, temperature, top_k, top_p, rep_penalty, seen, slots, ban_ids,
+                                   seeds, step, out_ids, out_logprobs, out_kept)
+
+
+def processed_logits_reference(logits, temperature, rep_penalty, seen, slots, ban_ids):
+    x = logits.float().clone()
+    B, V = x.shape
+    for b in range(B):
+        slot = int(slots[b]) if slots is not None else b
+        rp = float(rep_penalty[b]) if rep_penalty is not None else 1.0
+        if rp != 1.0 and seen is not None:
+            m = seen[slot].bool()
+            v = x[b, m]
+            x[b, m] = torch.where(v < 0, v * rp, v / rp)
+        if ban_ids is not None:
+            ids = ban_ids[b][(ban_ids[b] >= 0) & (ban_ids[b] < V)].long()
+            x[b, ids] = float("-inf")
+        t = float(temperature[b])
+        if t > 0 and t != 1.0:
+            x[b] = x[b] / t
+    return x
+
+
+def keep_mask_reference(x: torch.Tensor, top_k: int, top_p: float) -> torch.Tensor:
+    """HF TopK then TopP warper keep-mask for one row of processed logits."""
+    keep = torch.isfinite(x)
+    V = x.shape[0]
+    if 0 < top_k < V:
+        kth = torch.topk(x, top_k).values[-1]
+        keep &= x >= kth
+    if top_p < 1.0:
+        xm = x.masked_fill(~keep, float("-inf"))
+        srt, idx = torch.sort(xm, descending=False)
+        cum = srt.softmax(-1).cumsum(-1)
+        remove = cum <= (1 - top_p)
+        remove[-1:] = False
+        rm = torch.zeros_like(keep)
+        rm[idx] = remove
+        keep &= ~rm
+    return keep
+
+
+def sample_logits_reference(logits, temperature, top_k, top_p, rep_penalty=None, seen=None, slots=None,
+                            ban_ids=None, seeds=None, step=0, out_ids=None, out_logprobs=None,
+                            out_kept=None):
+    B, V = logits.shape
+    x = processed_logits_reference(logits, temperature, rep_penalty, seen, slots, ban_ids)
+    lsm = torch.log_softmax(x, -1)
+    ids = torch.empty(B, dtype=torch.int64, device=logits.device) if out_ids is None else out_ids
+    lps = torch.empty(B, device=logits.device) if out_logprobs is None else out_logprobs
+    for b in range(B):
+        t = float(temperature[b])
+        if not t > 0:
+            i = int(torch.argmax(x[b]))
+            kept = 1
+        else:
+            keep = keep_mask_reference(x[b], int(top_k[b]), float(top_p[b]))
+            probs = torch.softmax(x[b].masked_fill(~keep, float("-inf")), -1)
+            g = torch.Generator(device="cpu")
+            g.manual_seed(((int(seeds[b]) if seeds is not None else b) * 1000003 + int(step)) % (1 << 63))
+            i = int(torch.multinomial(probs.cpu(), 1, generator=g))
+            kept = int(keep.sum())
+        ids[b] = i
+        lps[b] = lsm[b, i]
+        if out_kept is not None:
+            out_kept[b] = kept
+        if seen is not None:
+            seen[int(slots[b]) if slots is not None else b, i] = 1
+    return ids, lps
+
+
+__all__ = ["decode_prep", "decode_attention", "decode_attention_reference", "decode_chunk",
+           "decode_ws_floats", "sample_logits", "sample_logits_reference", "keep_mask_reference",
+           "processed_logits_reference"]

@@ -1,0 +1,157 @@
+"""Decode kernels (kca_decode_prep / kca_decode_attn / kca_sample_logits) vs
+fp32 PyTorch references, and the engine's graph-captured decode on MI355X."""
+import math
+
+import pytest
+import torch
+
+from kubernetes_cloud_amd.ops import _lib
+from kubernetes_cloud_amd.ops import decode as dops
+from kubernetes_cloud_amd.ops.rope import rope_tables
+
+pytestmark = pytest.mark.gpu
+dev = torch.device("cuda", 0)
+
+
+@pytest.mark.parametrize("D,rot,inter", [(256, 64, True), (96, 24, False), (80, 20, False), (64, 0, False),
+                                         (128, 128, False)])
+def test_decode_prep(D, rot, inter):
+    torch.manual_seed(0)
+    B, H, Hkv, S, L = 5, 4, 4, 7, 64
+    qkv = torch.randn(B, (H + 2 * Hkv) * D, device=dev).to(torch.bfloat16)
+    pos = torch.tensor([0, 3, 63, 17, 5], device=dev, dtype=torch.int32)
+    slots = torch.tensor([6, 0, 2, 3, 1], device=dev, dtype=torch.int32)
+    cos, sin = rope_tables(rot, L, 10000.0, dev) if rot else (None, None)
+    kc = torch.zeros(S, Hkv, L, D, device=dev, dtype=torch.bfloat16)
+    vc = torch.zeros_like(kc)
+    q2, kc2, vc2 = qkv.cpu().float(), kc.cpu().float(), vc.cpu().float()
+    dops.decode_prep(qkv, H, Hkv, D, rot, inter, cos, sin, pos, slots, kc, vc)
+    dops.decode_prep(q2, H, Hkv, D, rot, inter, cos.cpu() if rot else None, sin.cpu() if rot else None,
+                     pos.cpu(), slots.cpu(), kc2, vc2)
+    torch.cuda.synchronize()
+    assert (qkv.cpu().float() - q2).abs().max() < 2e-2
+    assert (kc.cpu().float() - kc2).abs().max() < 2e-2
+    assert torch.equal(vc.cpu().float(), vc2)
+
+
+@pytest.mark.parametrize("D", [64, 80, 96, 128, 256])
+@pytest.mark.parametrize("G", [1, 4])
+def test_decode_attention(D, G):
+    torch.manual_seed(D + G)
+    B, Hkv, L = 6, 4, 2048
+    H = Hkv * G
+    kc = torch.randn(B + 1, Hkv, L, D, device=dev).to(torch.bfloat16)
+    vc = torch.randn_like(kc)
+    q = torch.randn(B, (H + 2 * Hkv) * D, device=dev).to(torch.bfloat16)
+    slots = torch.tensor([3, 0, 6, 1, 2, 5], device=dev, dtype=torch.int32)
+    lens = torch.tensor([1, 2048, 700, 65, 1500, 129], device=dev, dtype=torch.int32)
+    alibi = None
+    for max_kv, chunk in ((2048, 0), (2048, 64), (2048, 1024)):
+        o = dops.decode_attention(q, kc, vc, slots, lens, H, max_kv, chunk=chunk)
+        ref = dops.decode_attention_reference(q.float(), kc.float(), vc.float(), slots, lens, H,
+                                              1 / math.sqrt(D), alibi, torch.empty(B, H * D, device=dev))
+        assert (o.float() - ref).abs().max() < 2e-2, (max_kv, chunk)
+
+
+def test_decode_attention_alibi():
+    torch.manual_seed(1)
+    B, H, D, L = 3, 8, 128, 512
+    from kubernetes_cloud_amd.models.causal_lm import alibi_slopes
+    al = alibi_slopes(H).to(dev)
+    kc = torch.randn(B, H, L, D, device=dev).to(torch.bfloat16)
+    vc = torch.randn_like(kc)
+    q = torch.randn(B, 3 * H * D, device=dev).to(torch.bfloat16)
+    slots = torch.arange(B, device=dev, dtype=torch.int32)
+    lens = torch.tensor([512, 100, 301], device=dev, dtype=torch.int32)
+    o = dops.decode_attention(q, kc, vc, slots, lens, H, 512, alibi=al)
+    ref = dops.decode_attention_reference(q.float(), kc.float(), vc.float(), slots, lens, H, 1 / math.sqrt(D),
+                                          al, torch.empty(B, H * D, device=dev))
+    assert (o.float() - ref).abs().max() < 2e-2
+
+
+def _params(B, t, k, p, r=1.0):
+    f = lambda v, dt: torch.full((B,), v, dtype=dt, device=dev)  # noqa: E731
+    return dict(temperature=f(t, torch.float32), top_k=f(k, torch.int32), top_p=f(p, torch.float32),
+                rep_penalty=f(r, torch.float32))
+
+
+@pytest.mark.parametrize("V", [50400, 250880, 1000])
+def test_sample_greedy_and_masks(V):
+    torch.manual_seed(0)
+    B = 8
+    logits = (torch.randn(B, V, device=dev) * 4).to(torch.bfloat16)
+    ids, lp = dops.sample_logits(logits, **_params(B, 0.0, 0, 1.0))
+    ref = logits.float().argmax(-1)
+    assert torch.equal(ids, ref)
+    assert torch.allclose(lp, torch.log_softmax(logits.float(), -1).gather(1, ref[:, None])[:, 0], atol=1e-3)
+    # kept-set sizes of the top-k / top-p radix selects == HF warper masks
+    for (t, k, p) in ((1.0, 50, 1.0), (0.7, 0, 0.9), (1.3, 40, 0.8), (1.0, 1, 1.0), (1.0, 0, 0.5)):
+        kept = torch.empty(B, dtype=torch.int32, device=dev)
+        ids, _ = dops.sample_logits(logits, **_params(B, t, k, p), seeds=torch.arange(B, device=dev),
+                                    out_kept=kept)
+        x = logits.float() / t
+        for b in range(B):
+            keep = dops.keep_mask_reference(x[b], k, p)
+            assert abs(int(kept[b]) - int(keep.sum())) <= max(1, int(keep.sum()) // 100), (t, k, p, b)
+            assert bool(keep[ids[b]]), (t, k, p, b)
+
+
+def test_sample_penalty_bans_distribution():
+    torch.manual_seed(0)
+    V = 64
+    base = torch.randn(V, device=dev)
+    B = 4096
+    logits = base[None].expand(B, V).contiguous()
+    seeds = torch.randint(0, 2**62, (B,), device=dev)
+    ids, _ = dops.sample_logits(logits, **_params(B, 1.0, 0, 1.0), seeds=seeds)
+    freq = torch.bincount(ids, minlength=V).float() / B
+    probs = base.softmax(-1)
+    assert (freq - probs).abs().max() < 0.03
+    # repetition penalty through the seen mask + bans
+    seen = torch.zeros(2, V, dtype=torch.uint8, device=dev)
+    top = int(base.argmax())
+    seen[0, top] = 1
+    slots = torch.tensor([0, 1], dtype=torch.int32, device=dev)
+    bans = torch.tensor([[-1], [top]], dtype=torch.int32, device=dev)
+    x = base[None].expand(2, V).contiguous()
+    ref = dops.sample_logits_reference(x.cpu(), *(v.cpu() for v in _params(2, 0.0, 0, 1.0, 50.0).values()),
+                                       seen=seen.cpu().clone(), slots=slots.cpu(), ban_ids=bans.cpu())[0]
+    ids, _ = dops.sample_logits(x, **_params(2, 0.0, 0, 1.0, 50.0), seen=seen, slots=slots, ban_ids=bans)
+    assert ids.tolist() == ref.tolist() and top not in ids.tolist()
+    assert int(seen[1, ids[1]]) == 1  # chosen token is marked seen
+
+
+@pytest.mark.parametrize("preset", ["gpt-j-6b", "bloom-560m", "gpt2"])
+def test_engine_gpu_graphs_match_eager_and_recompute(preset):
+    from kubernetes_cloud_amd.engine.llm_engine import LLMEngine, SamplingParams
+    from kubernetes_cloud_amd.models.causal_lm import build_model
+    from kubernetes_cloud_amd.models.config import PRESETS_HF, LMConfig
+    small = {"gpt-j-6b": dict(n_embd=1024, n_layer=2, n_head=4, rotary_dim=64, n_positions=512),
+             "bloom-560m": dict(hidden_size=512, n_layer=2, n_head=4),
+             "gpt2": dict(n_embd=512, n_layer=2, n_head=8, n_positions=512)}[preset]
+    cfg = dict(PRESETS_HF[preset])
+    cfg.update(small)
+    m = build_model(LMConfig.from_hf(cfg), device=dev, dtype=torch.bfloat16, seed=0)
+    prompts = [[int(x) for x in torch.randint(0, 1000, (n,))] for n in (5, 33, 5, 100)]
+    sp = SamplingParams(max_new_tokens=12, do_sample=False)
+    outs = []
+    for graphs in (False, True):
+        eng = LLMEngine(m, max_slots=8, max_len=256, use_graphs=graphs)
+        outs.append([r.output for r in eng.generate(prompts, sp)])
+    assert outs[0] == outs[1]
+    # every generated token is the argmax of a full forward (except near-ties)
+    for p, o in zip(prompts, outs[1]):
+        with torch.no_grad():
+            lg = m(torch.tensor([p + o], device=dev))[0].float()
+        for i, t in enumerate(o):
+            row = lg[len(p) - 1 + i]
+            top2 = row.topk(2).values
+            if float(top2[0] - top2[1]) > 0.1:
+                assert int(row.argmax()) == t, (preset, i)
+    # seeded sampling is reproducible under graphs
+    eng = LLMEngine(m, max_slots=8, max_len=256, use_graphs=True)
+    sp2 = SamplingParams(max_new_tokens=16, temperature=0.9, top_k=40, top_p=0.95, seed=7)
+    a = [r.output for r in eng.generate(prompts, sp2)]
+    b = [r.output for r in eng.generate(prompts, sp2)]
+    assert a == b
+    assert _lib.has("kca_decode_attn")
