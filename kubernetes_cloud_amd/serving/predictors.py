@@ -1,0 +1,252 @@
+"""KServe predictors of the reference, on the native engine.
+
+* ``BloomPredictor``      -- online-inference/bloom-176b/model/bloom.py:11-97 (env
+  options MODEL_ID / MODEL_PATH / MODEL_TYPE / MODEL_DOWNLOAD_TIMEOUT and
+  sampling defaults MIN_LENGTH / MAX_LENGTH / TEMPERATURE / TOP_K / TOP_P /
+  REPETITION_PENALTY, case-insensitive per-request ``parameters`` override,
+  ``.ready.txt`` gate). On a multi-GPU launch (WORLD_SIZE > 1) the model is
+  tensor-parallel over RCCL instead of accelerate's layer split.
+* ``GPTJPredictor``       -- tensorizer-isvc kserve_api.py:11-78 (model "gptj",
+  ``MODEL_LOAD_TYPE=tensorizer|hf``, instances -> 50 sampled tokens) and the
+  Flask variant flask_api.py:49-63 (``GET /``, ``GET /predict/<text>``).
+* ``AITextGenPredictor``  -- custom-pytorch-aitextgen model.py:6-26 (``{"text",
+  "length"}`` -> ``{"prediction"}``; GPT-2 1.5B).
+* ``GPT2Transformer`` / ``GPT2Predictor`` -- gpt-2/transformer/transformer.py:9-20
+  (BPE pre/post-processing around a token-id predictor, V1 ``signature_name``).
+"""
+from __future__ import annotations
+
+import logging
+import os
+import re
+import time
+
+from .server import InvalidInput, Model, ModelServer
+from .text import TextGenerator, load_lm
+
+log = logging.getLogger("kca.serving")
+
+
+# ---------------------------------------------------------------- BLOOM
+def bloom_options(env=None) -> tuple[dict, dict]:
+    env = os.environ if env is None else env
+    model_id = env.get("MODEL_ID", "bigscience/bloom")
+    options = {
+        "MODEL_PATH": env.get("MODEL_PATH", "/mnt/pvc/bloom"),
+        "MODEL_NAME": re.sub(r"[^\w-]", "-", model_id).lower(),
+        "MODEL_TYPE": env.get("MODEL_TYPE", "text-generation"),
+        "MODEL_DOWNLOAD_TIMEOUT": int(env.get("MODEL_DOWNLOAD_TIMEOUT", 300)),
+    }
+    params = {
+        "MIN_LENGTH": int(env.get("MIN_LENGTH", 1)),
+        "MAX_LENGTH": int(env.get("MAX_LENGTH", 40)),
+        "TEMPERATURE": float(env.get("TEMPERATURE", 1.0)),
+        "TOP_K": int(env.get("TOP_K", 50)),
+        "TOP_P": float(env.get("TOP_P", 1.0)),
+        "REPETITION_PENALTY": float(env.get("REPETITION_PENALTY", 1.0)),
+    }
+    return options, params
+
+
+def wait_for_ready_file(path: str, timeout_s: int, interval_s: float = 10.0):
+    """bloom.py:79-90: poll ``{path}/.ready.txt`` (written by the downloader)."""
+    ready = os.path.join(path, ".ready.txt")
+    deadline = time.time() + timeout_s
+    while True:
+        if os.path.exists(ready):
+            return True
+        if time.time() >= deadline:
+            raise TimeoutError(f"Download timeout {timeout_s}!")
+        time.sleep(min(interval_s, max(0.0, deadline - time.time())))
+
+
+class BloomPredictor(Model):
+    def __init__(self, name: str | None = None, options: dict | None = None, params: dict | None = None,
+                 generator: TextGenerator | None = None):
+        o, p = bloom_options()
+        self.options = options or o
+        self.params = params or p
+        super().__init__(name or self.options["MODEL_NAME"])
+        self.generator = generator
+        if generator is not None:
+            self.ready = True
+
+    def load(self):
+        if self.options["MODEL_TYPE"] != "text-generation":
+            raise ValueError(f"unsupported MODEL_TYPE {self.options['MODEL_TYPE']}")
+        model, tok = load_lm(self.options["MODEL_PATH"])
+        self.generator = TextGenerator(model, tok)
+        self.ready = True
+
+    def request_params(self, request: dict) -> dict:
+        rp = dict(self.params)
+        for k, v in (request.get("parameters") or {}).items():
+            if k.upper() in rp:
+                rp[k.upper()] = v
+        return rp
+
+    def predict(self, request: dict, headers=None) -> dict:
+        if "instances" not in request:
+            raise InvalidInput("request must contain 'instances'")
+        rp = self.request_params(request)
+        return {"predictions": self.generator(
+            request["instances"], min_length=rp["MIN_LENGTH"], max_length=rp["MAX_LENGTH"],
+            temperature=rp["TEMPERATURE"], top_k=rp["TOP_K"], top_p=rp["TOP_P"],
+            repetition_penalty=rp["REPETITION_PENALTY"])}
+
+
+# ----------------------------------------------------------------- GPT-J
+class GPTJPredictor(Model):
+    """Model "gptj"; weights from ``{MODEL_PATH}/gptj.tensors`` (tensorizer) or
+    the HF files in MODEL_PATH (hf)."""
+
+    def __init__(self, name: str = "gptj", model_path: str | None = None, load_type: str | None = None,
+                 generator: TextGenerator | None = None, seed: int = 100):
+        super().__init__(name)
+        self.model_path = model_path or os.getenv("MODEL_PATH", "/mnt/pvc")
+        self.load_type = load_type or os.getenv("MODEL_LOAD_TYPE") or "tensorizer"
+        self.generator = generator
+        self.seed = seed
+        self.load_seconds = None
+        if generator is not None:
+            self.ready = True
+
+    def load(self):
+        if self.load_type not in ("tensorizer", "hf"):
+            raise ValueError(f'model_load_type must be either "tensorizer" or "hf"; got {self.load_type}')
+        t0 = time.perf_counter()
+        tf = os.path.join(self.model_path, "gptj.tensors") if self.load_type == "tensorizer" else None
+        model, tok = load_lm(self.model_path, tensors_file=tf)
+        self.load_seconds = time.perf_counter() - t0
+        log.info("Deserialized model in %.2fs using %s", self.load_seconds, self.load_type)
+        self.generator = TextGenerator(model, tok)
+        self.ready = True
+
+    def complete(self, text: str, idx: int = 0) -> str:
+        g = self.generator
+        r = g.generate_ids([g.tokenizer.encode(text)], [g.sampling_params(
+            0, max_new_tokens=50, do_sample=True, seed=self.seed + idx)])[0]
+        return g.tokenizer.decode(r.prompt + r.output, skip_special_tokens=True)
+
+    def predict(self, payload: dict, headers=None) -> dict:
+        if not isinstance(payload, dict):
+            raise InvalidInput("Expected payload to be a dict")
+        inputs = payload.get("instances") or ["Please input some text"]
+        g = self.generator
+        prompts = [g.tokenizer.encode(t) for t in inputs]
+        params = [g.sampling_params(0, max_new_tokens=50, do_sample=True, seed=self.seed + i)
+                  for i in range(len(prompts))]
+        reqs = g.generate_ids(prompts, params)
+        return {"predictions": [g.tokenizer.decode(r.prompt + r.output, skip_special_tokens=True) for r in reqs]}
+
+
+def create_gptj_text_app(predictor: GPTJPredictor):
+    """Flask-API equivalent (flask_api.py:49-63): ``GET /`` and ``GET /predict/<text>``."""
+    from fastapi import FastAPI
+    from fastapi.responses import PlainTextResponse, Response
+    app = FastAPI()
+
+    @app.get("/")
+    def index():
+        return Response(status_code=200)
+
+    @app.get("/predict/{text:path}")
+    def predict(text: str):
+        return PlainTextResponse(predictor.complete(text))
+
+    return app
+
+
+# -------------------------------------------------------------- GPT-2s
+class AITextGenPredictor(Model):
+    def __init__(self, name: str = "aitextgen", generator: TextGenerator | None = None):
+        super().__init__(name)
+        self.generator = generator
+        if generator is not None:
+            self.ready = True
+
+    def load(self, model_path: str | None = None):
+        path = model_path or os.getenv("MODEL_PATH", "/mnt/models/gpt2-xl")
+        model, tok = load_lm(path, random_init=not os.path.isdir(path))
+        self.generator = TextGenerator(model, tok)
+        self.ready = True
+
+    def predict(self, request: dict, headers=None) -> dict:
+        if "text" not in request:
+            raise InvalidInput("request must contain 'text'")
+        out = self.generator(request["text"], max_length=int(request.get("length", 64)), do_sample=True,
+                             temperature=0.7, top_k=0)
+        return {"prediction": out[0]["generated_text"]}
+
+
+class GPT2Predictor(Model):
+    """Token-id predictor behind the GPT-2 transformer (the TF-Serving SavedModel
+    role of gpt-2/service-*/gpt-s3-inferenceservice.yaml): instances of token
+    ids -> predictions of continuation ids."""
+
+    def __init__(self, name: str = "model", generator: TextGenerator | None = None, length: int = 40):
+        super().__init__(name)
+        self.generator, self.length = generator, length
+        if generator is not None:
+            self.ready = True
+
+    def predict(self, request: dict, headers=None) -> dict:
+        g = self.generator
+        prompts = [list(map(int, ids)) for ids in request["instances"]]
+        params = [g.sampling_params(len(p), max_new_tokens=self.length, do_sample=True, top_k=40)
+                  for p in prompts]
+        return {"predictions": [r.output for r in g.generate_ids(prompts, params)]}
+
+
+class GPT2Transformer(Model):
+    """KServe transformer: text <-> BPE ids around a predictor (transformer.py:9-20)."""
+
+    def __init__(self, name: str, predictor_host: str | None, tokenizer, predictor: Model | None = None):
+        super().__init__(name, predictor_host)
+        self.tokenizer = tokenizer
+        self.local = predictor
+        self.ready = True
+
+    def preprocess(self, inputs: dict, headers=None) -> dict:
+        return {"signature_name": "predict",
+                "instances": [self.tokenizer.encode(i) for i in inputs["instances"]]}
+
+    def predict(self, payload, headers=None):
+        if self.local is not None:
+            return self.local.predict(payload)
+        return super().predict(payload, headers)
+
+    def postprocess(self, outputs: dict, headers=None) -> dict:
+        return {"predictions": [self.tokenizer.decode(p) for p in outputs["predictions"]]}
+
+
+# ------------------------------------------------------------------ CLIs
+def bloom_main(argv=None):
+    options, _ = bloom_options()
+    wait_for_ready_file(options["MODEL_PATH"], options["MODEL_DOWNLOAD_TIMEOUT"])
+    m = BloomPredictor()
+    m.load()
+    ModelServer(argv=argv).start([m])
+
+
+def gptj_main(argv=None):
+    m = GPTJPredictor()
+    m.load()
+    ModelServer(argv=argv).start([m])
+
+
+def gptj_text_main(argv=None):
+    import uvicorn
+    m = GPTJPredictor()
+    m.load()
+    uvicorn.run(create_gptj_text_app(m), host="0.0.0.0", port=int(os.getenv("PORT", 8000)))
+
+
+def aitextgen_main(argv=None):
+    m = AITextGenPredictor()
+    m.load()
+    ModelServer(workers=1, argv=argv).start([m])
+
+
+__all__ = ["BloomPredictor", "GPTJPredictor", "AITextGenPredictor", "GPT2Predictor", "GPT2Transformer",
+           "bloom_options", "wait_for_ready_file", "create_gptj_text_app"]

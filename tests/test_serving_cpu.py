@@ -1,0 +1,189 @@
+"""Serving layer on CPU: KServe V1/V2 server, completion server (T4),
+BLOOM/GPT-J/aitextgen/GPT-2 predictors, FasterTransformer-compatible Triton
+endpoint over the binary tensor protocol, SD predictor (PNG bytes, micro-
+batching), evaluator CLI (T3)."""
+import io
+import os
+import threading
+
+import numpy as np
+import pytest
+import torch
+from fastapi.testclient import TestClient
+
+from kubernetes_cloud_amd.serving import v2
+from kubernetes_cloud_amd.serving.server import ModelServer
+from kubernetes_cloud_amd.serving.text import TextGenerator, load_lm
+
+from .helpers import make_model_dir, make_sd_dir
+
+
+@pytest.fixture(scope="module")
+def gptj_dir(tmp_path_factory):
+    return make_model_dir(str(tmp_path_factory.mktemp("gptj")), "gpt-j-6b")
+
+
+@pytest.fixture(scope="module")
+def gen(gptj_dir):
+    m, tok = load_lm(gptj_dir, device="cpu")
+    g = TextGenerator(m, tok, max_slots=8)
+    yield g
+    g.close()
+
+
+def test_completion_server(gen):
+    from kubernetes_cloud_amd.serving.completion_server import build_parser, create_app
+    c = TestClient(create_app(gen))
+    assert c.get("/").json() == "OK"
+    r = c.post("/completion", json={"prompt": "the quick brown", "max_new_tokens": 5, "num_return_sequences": 2,
+                                    "top_k": 10})
+    out = r.json()
+    assert len(out) == 2 and all(o["generated_text"].startswith("the quick brown") for o in out)
+    r = c.post("/completion", json={"prompt": "fox", "do_sample": False, "max_new_tokens": 4,
+                                    "bad_words": ["the"]})
+    assert "generated_text" in r.json()[0]
+    a = build_parser().parse_args(["--model", "x", "--device_id", "-1", "--port", "8080"])
+    assert a.device_id == -1 and a.port == 8080
+
+
+def test_kserve_v1_bloom_predictor(tmp_path):
+    from kubernetes_cloud_amd.serving.predictors import BloomPredictor, bloom_options, wait_for_ready_file
+    d = make_model_dir(str(tmp_path / "bloom"), "bloom-560m", hidden_size=64, n_layer=2, n_head=4)
+    m, tok = load_lm(d, device="cpu")
+    opts, params = bloom_options({"MODEL_ID": "bigscience/bloom", "MODEL_PATH": d, "MAX_LENGTH": "12"})
+    assert opts["MODEL_NAME"] == "bigscience-bloom" and params["MAX_LENGTH"] == 12
+    pred = BloomPredictor(opts["MODEL_NAME"], opts, params, generator=TextGenerator(m, tok, background=False))
+    app = ModelServer(http_port=1).create_app([pred])
+    c = TestClient(app)
+    assert c.get("/v1/models").json() == {"models": ["bigscience-bloom"]}
+    assert c.get("/v1/models/bigscience-bloom").json()["ready"] is True
+    r = c.post("/v1/models/bigscience-bloom:predict",
+               json={"instances": ["the quick", "a fox"], "parameters": {"max_length": 8, "Top_K": 5}})
+    preds = r.json()["predictions"]
+    assert len(preds) == 2 and preds[0][0]["generated_text"].startswith("the quick")
+    assert c.post("/v1/models/nope:predict", json={}).status_code == 404
+    assert c.post("/v1/models/bigscience-bloom:predict", json={"x": 1}).status_code == 400
+    assert "request_count" in c.get("/metrics").text
+    with pytest.raises(TimeoutError):
+        wait_for_ready_file(str(tmp_path), 0, 0.01)
+    open(os.path.join(d, ".ready.txt"), "w").close()
+    assert wait_for_ready_file(d, 1, 0.01)
+
+
+def test_gptj_predictor_tensorized_and_text_app(gptj_dir, tmp_path):
+    from kubernetes_cloud_amd.io.tensors import serialize
+    from kubernetes_cloud_amd.serving.predictors import GPTJPredictor, create_gptj_text_app
+    m, _ = load_lm(gptj_dir, device="cpu")
+    serialize(m, os.path.join(gptj_dir, "gptj.tensors"))
+    p = GPTJPredictor(model_path=gptj_dir, load_type="tensorizer")
+    p.load()
+    assert p.ready and p.load_seconds is not None
+    c = TestClient(ModelServer(http_port=1).create_app([p]))
+    r = c.post("/v1/models/gptj:predict", json={"instances": ["hello there", "kubernetes"]}).json()
+    assert len(r["predictions"]) == 2 and r["predictions"][0].startswith("hello there")
+    r = c.post("/v1/models/gptj:predict", json={}).json()
+    assert r["predictions"][0].startswith("Please input some text")
+    t = TestClient(create_gptj_text_app(p))
+    assert t.get("/").status_code == 200
+    assert t.get("/predict/the quick fox").text.startswith("the quick fox")
+    p.generator.close()
+    with pytest.raises(ValueError):
+        GPTJPredictor(model_path=gptj_dir, load_type="bogus").load()
+
+
+def test_triton_ft_endpoint_binary_protocol(gptj_dir, tmp_path):
+    from kubernetes_cloud_amd.serving.triton_ft import (FasterTransformerModel, parse_config_pbtxt,
+                                                        parse_word_list, write_model_store)
+    store = str(tmp_path / "triton-model-store")
+    write_model_store(gptj_dir, store, data_type="fp32")
+    cfg = parse_config_pbtxt(open(os.path.join(store, "fastertransformer", "config.pbtxt")).read())
+    assert cfg["max_batch_size"] == 1024 and cfg["parameters"]["model_type"] == "GPT-J"
+    ft = FasterTransformerModel(store_dir=store)
+    ft.load()
+    c = TestClient(ModelServer(http_port=1).create_app([ft]))
+    assert c.get("/v2/health/ready").status_code == 200
+    meta = c.get("/v2/models/fastertransformer").json()
+    assert {i["name"] for i in meta["inputs"]} >= {"input_ids", "runtime_top_k", "stop_words_list"}
+    ids = np.array([[5, 6, 7, 8], [9, 10, 0, 0]], dtype=np.int32)
+    inputs = {"input_ids": ids, "input_lengths": np.array([[4], [2]], dtype=np.int32),
+              "request_output_len": np.array([[6], [6]], dtype=np.int32),
+              "runtime_top_k": np.array([[0], [0]], dtype=np.int32),
+              "runtime_top_p": np.array([[0.0], [0.0]], dtype=np.float32),
+              "random_seed": np.array([[0], [0]], dtype=np.uint64),
+              "is_return_log_probs": np.array([[True], [True]]),
+              "stop_words_list": np.array([[[0], [-1]], [[0], [-1]]], dtype=np.int32)}
+    body, hdr = v2.encode_request(inputs)
+    r = c.post("/v2/models/fastertransformer/infer", content=body, headers=hdr)
+    assert r.status_code == 200, r.text
+    out = v2.decode_response(r.content, int(r.headers[v2.HEADER]))
+    assert out["output_ids"].shape == (2, 1, 10)
+    assert out["output_ids"][0, 0, :4].tolist() == [5, 6, 7, 8]
+    assert out["output_ids"][1, 0, :2].tolist() == [9, 10]
+    assert out["sequence_length"][:, 0].tolist() == [10, 8]
+    assert out["output_log_probs"].shape == (2, 1, 6) and (out["cum_log_probs"] <= 0).all()
+    # greedy == engine greedy; JSON (non-binary) protocol works too
+    body, hdr = v2.encode_request({k: v[:1] for k, v in inputs.items()}, binary=False, binary_output=False)
+    r2 = c.post("/v2/models/fastertransformer/infer", content=body, headers=hdr)
+    o2 = v2.decode_response(r2.content, None)
+    assert o2["output_ids"][0].tolist() == out["output_ids"][0, :, :10].tolist()
+    assert parse_word_list(np.array([[[1, 2, 3, 4], [1, 4, -1, -1]]])) == [[[1], [2, 3, 4]]]
+    bad = dict(inputs, beam_width=np.array([[2], [2]], dtype=np.int32))
+    body, hdr = v2.encode_request(bad)
+    assert c.post("/v2/models/fastertransformer/infer", content=body, headers=hdr).status_code == 400
+    ft.generator.close()
+
+
+def test_gpt2_transformer_chain_and_aitextgen(gen):
+    from kubernetes_cloud_amd.serving.predictors import AITextGenPredictor, GPT2Predictor, GPT2Transformer
+    pred = GPT2Predictor("model", gen, length=5)
+    tr = GPT2Transformer("model", None, gen.tokenizer, predictor=pred)
+    c = TestClient(ModelServer(http_port=1).create_app([tr]))
+    r = c.post("/v1/models/model:predict", json={"instances": ["the quick", "lazy dog"]}).json()
+    assert len(r["predictions"]) == 2 and all(isinstance(p, str) for p in r["predictions"])
+    ai = AITextGenPredictor(generator=gen)
+    r = TestClient(ModelServer(http_port=1).create_app([ai])).post(
+        "/v1/models/aitextgen:predict", json={"text": "a finetuner", "length": 12}).json()
+    assert r["prediction"].startswith("a finetuner")
+
+
+def test_sd_predictor_png_and_batching(tmp_path):
+    from kubernetes_cloud_amd.models.sd_pipeline import StableDiffusionPipeline
+    from kubernetes_cloud_amd.serving.sd_service import SDPredictor, get_args, serialize_main
+    d = make_sd_dir(str(tmp_path / "sd"))
+    a = get_args(["--model-id", d, "--tensorized", "--num-inference-steps", "3", "--width", "32", "--height", "32"])
+    assert a.model_name == "sd" and a.tensorized
+    serialize_main(["--model-id", d, "--save-path", str(tmp_path / "tz")])
+    p = SDPredictor(model_name="sd", model_id=str(tmp_path / "tz"), tensorized=True, num_inference_steps=3,
+                    width=32, height=32, max_batch=4, batch_window_ms=50)
+    p.load()
+    c = TestClient(ModelServer(http_port=1).create_app([p]))
+    r = c.post("/v1/models/sd:predict", json={"prompt": "a fox", "parameters": {"SEED": 3, "guidance_scale": 5}})
+    assert r.status_code == 200 and r.content[:8] == b"\x89PNG\r\n\x1a\n"
+    assert r.headers["content-type"] == "image/png"
+    from PIL import Image
+    assert Image.open(io.BytesIO(r.content)).size == (32, 32)
+    # concurrent requests get batched; identical seeds -> identical images
+    res = [None] * 3
+
+    def go(i):
+        res[i] = p.predict({"prompt": "a fox", "parameters": {"seed": 3, "guidance_scale": 5}})
+    th = [threading.Thread(target=go, args=(i,)) for i in range(3)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    assert res[0] == res[1] == res[2] == r.content
+    assert isinstance(StableDiffusionPipeline, type)
+
+
+def test_evaluator_cli(gptj_dir, tmp_path):
+    from kubernetes_cloud_amd.train.evaluator import main
+    pf = tmp_path / "prompts.txt"
+    pf.write_text("the quick\\nbrown\n\nkubernetes cloud\n")
+    buf = io.StringIO()
+    res = main(["--model", gptj_dir, "--prompt-file", str(pf), "--prompt-tokens", "4", "--prompt-samples", "2",
+                "--seed", "1"], out=buf)
+    assert list(res) == ["the quick\nbrown", "kubernetes cloud"]
+    assert all(len(v) == 2 for v in res.values())
+    assert "RESPONSE:" in buf.getvalue() and "Loaded model in" in buf.getvalue()
+    with pytest.raises(SystemExit):
+        main(["--model", gptj_dir], out=buf)
+    assert torch.is_tensor(torch.zeros(1))
