@@ -70,8 +70,10 @@ class Request:
 
 class LLMEngine:
     def __init__(self, model, max_slots: int = 32, max_len: int | None = None, use_graphs: bool | None = None,
-                 max_prefill_tokens: int = 16384):
-        self.runner = ModelRunner(model, max_slots=max_slots, max_len=max_len, use_graphs=use_graphs)
+                 max_prefill_tokens: int = 16384, runner=None):
+        # ``runner``: e.g. a tp_driver.CollectiveRunner that mirrors every call to TP follower ranks
+        self.runner = runner or ModelRunner(model, max_slots=max_slots, max_len=max_len, use_graphs=use_graphs)
+        max_slots = self.runner.max_slots
         self.max_len = self.runner.max_len
         self.free = list(range(max_slots))[::-1]
         self.waiting: list[Request] = []

@@ -88,7 +88,10 @@ class ModelRunner:
         p = next(model.parameters())
         self.device, self.dtype = p.device, p.dtype
         self.max_len = max_len or cfg.max_pos
-        self.H, self.Hkv, self.D = cfg.n_heads, cfg.kv_heads, cfg.head_dim
+        # local heads: a tensor-parallel shard holds H/tp of them (parallel.tensor_parallel)
+        self.H = model.h[0].attn.n_heads
+        self.Hkv = self.H * cfg.kv_heads // cfg.n_heads
+        self.D = cfg.head_dim
         self.V = cfg.vocab_size
         self.cache = KVCache(cfg.n_layers, max_slots, self.Hkv, self.max_len, self.D, self.device, self.dtype)
         self.max_slots = max_slots

@@ -32,110 +32,127 @@ def _native_qkv_to_neox(w: torch.Tensor, H: int, D: int) -> torch.Tensor:
     return w.view(3, H, D, *shp[1:]).transpose(0, 1).reshape(shp)
 
 
-def hf_to_native(sd: dict, cfg: LMConfig) -> dict:
-    """Map an HF state dict onto CausalLM parameter names."""
-    out = {}
+def hf_to_native_plan(cfg: LMConfig, get, sd_keys=()) -> dict:
+    """native name -> zero-arg producer of that tensor. ``get(k)`` reads HF key
+    ``k`` (prefix-free). Lazy so tensor-parallel loading can materialise one
+    tensor at a time and keep only its shard (BLOOM-176B does not fit in host
+    memory per rank)."""
     H, D = cfg.n_heads, cfg.head_dim
     a = cfg.arch
-    # strip common prefixes
+    plan = {}
+
+    def put(nk, fn):
+        plan[nk] = fn
+
+    def direct(nk, hk):
+        plan[nk] = lambda hk=hk: get(hk)
+
+    def cat3(nk, fmt):
+        plan[nk] = lambda fmt=fmt: torch.cat([get(fmt.format(n)) for n in ("q", "k", "v")], 0)
+
+    def tr(nk, hk):
+        plan[nk] = lambda hk=hk: get(hk).t().contiguous()
+
+    def neox(nk, hk):
+        plan[nk] = lambda hk=hk: _neox_qkv_to_native(get(hk), H, D)
+
+    if a in ("gptj", "gpt2", "gpt_neo"):
+        direct("wte.weight", "wte.weight")
+        if cfg.learned_pos:
+            direct("wpe.weight", "wpe.weight")
+        for i in range(cfg.n_layers):
+            p = f"h.{i}."
+            for ln in ("ln_1",) + (() if cfg.shared_ln else ("ln_2",)):
+                direct(p + ln + ".weight", p + ln + ".weight")
+                direct(p + ln + ".bias", p + ln + ".bias")
+            if a == "gptj":
+                cat3(p + "attn.qkv.weight", p + "attn.{}_proj.weight")
+                direct(p + "attn.out.weight", p + "attn.out_proj.weight")
+                for n in ("fc_in", "fc_out"):
+                    direct(p + f"mlp.{n}.weight", p + f"mlp.{n}.weight")
+                    direct(p + f"mlp.{n}.bias", p + f"mlp.{n}.bias")
+            elif a == "gpt2":
+                tr(p + "attn.qkv.weight", p + "attn.c_attn.weight")
+                direct(p + "attn.qkv.bias", p + "attn.c_attn.bias")
+                tr(p + "attn.out.weight", p + "attn.c_proj.weight")
+                direct(p + "attn.out.bias", p + "attn.c_proj.bias")
+                tr(p + "mlp.fc_in.weight", p + "mlp.c_fc.weight")
+                direct(p + "mlp.fc_in.bias", p + "mlp.c_fc.bias")
+                tr(p + "mlp.fc_out.weight", p + "mlp.c_proj.weight")
+                direct(p + "mlp.fc_out.bias", p + "mlp.c_proj.bias")
+            else:  # gpt_neo
+                cat3(p + "attn.qkv.weight", p + "attn.attention.{}_proj.weight")
+                direct(p + "attn.out.weight", p + "attn.attention.out_proj.weight")
+                direct(p + "attn.out.bias", p + "attn.attention.out_proj.bias")
+                direct(p + "mlp.fc_in.weight", p + "mlp.c_fc.weight")
+                direct(p + "mlp.fc_in.bias", p + "mlp.c_fc.bias")
+                direct(p + "mlp.fc_out.weight", p + "mlp.c_proj.weight")
+                direct(p + "mlp.fc_out.bias", p + "mlp.c_proj.bias")
+        direct("ln_f.weight", "ln_f.weight")
+        direct("ln_f.bias", "ln_f.bias")
+        if not cfg.tie_embeddings:
+            direct("lm_head.weight", "lm_head.weight")
+            if cfg.lm_head_bias and "lm_head.bias" in sd_keys:
+                direct("lm_head.bias", "lm_head.bias")
+        return plan
+
+    if a == "gpt_neox":
+        direct("wte.weight", "embed_in.weight")
+        for i in range(cfg.n_layers):
+            s, p = f"layers.{i}.", f"h.{i}."
+            for nn_, hn in (("ln_1", "input_layernorm"), ("ln_2", "post_attention_layernorm")):
+                direct(p + nn_ + ".weight", s + hn + ".weight")
+                direct(p + nn_ + ".bias", s + hn + ".bias")
+            neox(p + "attn.qkv.weight", s + "attention.query_key_value.weight")
+            neox(p + "attn.qkv.bias", s + "attention.query_key_value.bias")
+            for nn_, hn in (("attn.out", "attention.dense"), ("mlp.fc_in", "mlp.dense_h_to_4h"),
+                            ("mlp.fc_out", "mlp.dense_4h_to_h")):
+                direct(p + nn_ + ".weight", s + hn + ".weight")
+                direct(p + nn_ + ".bias", s + hn + ".bias")
+        direct("ln_f.weight", "final_layer_norm.weight")
+        direct("ln_f.bias", "final_layer_norm.bias")
+        if not cfg.tie_embeddings:
+            direct("lm_head.weight", "embed_out.weight" if "embed_out.weight" in sd_keys else "lm_head.weight")
+        return plan
+
+    if a == "bloom":
+        direct("wte.weight", "word_embeddings.weight")
+        direct("emb_ln.weight", "word_embeddings_layernorm.weight")
+        direct("emb_ln.bias", "word_embeddings_layernorm.bias")
+        for i in range(cfg.n_layers):
+            p = f"h.{i}."
+            for nn_, hn in (("ln_1", "input_layernorm"), ("ln_2", "post_attention_layernorm")):
+                direct(p + nn_ + ".weight", p + hn + ".weight")
+                direct(p + nn_ + ".bias", p + hn + ".bias")
+            neox(p + "attn.qkv.weight", p + "self_attention.query_key_value.weight")
+            neox(p + "attn.qkv.bias", p + "self_attention.query_key_value.bias")
+            for nn_, hn in (("attn.out", "self_attention.dense"), ("mlp.fc_in", "mlp.dense_h_to_4h"),
+                            ("mlp.fc_out", "mlp.dense_4h_to_h")):
+                direct(p + nn_ + ".weight", p + hn + ".weight")
+                direct(p + nn_ + ".bias", p + hn + ".bias")
+        direct("ln_f.weight", "ln_f.weight")
+        direct("ln_f.bias", "ln_f.bias")
+        return plan
+    raise ValueError(a)
+
+
+_PREFIXES = ("", "transformer.", "gpt_neox.", "model.")
+
+
+def prefixed_getter(sd):
+    """``get(k)`` over a mapping whose keys may carry an HF model prefix."""
     def get(k):
-        for pre in ("", "transformer.", "gpt_neox.", "model."):
+        for pre in _PREFIXES:
             if pre + k in sd:
                 return sd[pre + k]
         raise KeyError(k)
+    return get
 
-    def has(k):
-        return any((pre + k) in sd for pre in ("", "transformer.", "gpt_neox.", "model."))
 
-    if a in ("gptj", "gpt2", "gpt_neo"):
-        out["wte.weight"] = get("wte.weight")
-        if cfg.learned_pos:
-            out["wpe.weight"] = get("wpe.weight")
-        for i in range(cfg.n_layers):
-            p = f"h.{i}."
-            out[p + "ln_1.weight"] = get(p + "ln_1.weight")
-            out[p + "ln_1.bias"] = get(p + "ln_1.bias")
-            if not cfg.shared_ln:
-                out[p + "ln_2.weight"] = get(p + "ln_2.weight")
-                out[p + "ln_2.bias"] = get(p + "ln_2.bias")
-            if a == "gptj":
-                out[p + "attn.qkv.weight"] = torch.cat(
-                    [get(p + f"attn.{n}_proj.weight") for n in ("q", "k", "v")], 0)
-                out[p + "attn.out.weight"] = get(p + "attn.out_proj.weight")
-                out[p + "mlp.fc_in.weight"] = get(p + "mlp.fc_in.weight")
-                out[p + "mlp.fc_in.bias"] = get(p + "mlp.fc_in.bias")
-                out[p + "mlp.fc_out.weight"] = get(p + "mlp.fc_out.weight")
-                out[p + "mlp.fc_out.bias"] = get(p + "mlp.fc_out.bias")
-            elif a == "gpt2":
-                out[p + "attn.qkv.weight"] = get(p + "attn.c_attn.weight").t().contiguous()
-                out[p + "attn.qkv.bias"] = get(p + "attn.c_attn.bias")
-                out[p + "attn.out.weight"] = get(p + "attn.c_proj.weight").t().contiguous()
-                out[p + "attn.out.bias"] = get(p + "attn.c_proj.bias")
-                out[p + "mlp.fc_in.weight"] = get(p + "mlp.c_fc.weight").t().contiguous()
-                out[p + "mlp.fc_in.bias"] = get(p + "mlp.c_fc.bias")
-                out[p + "mlp.fc_out.weight"] = get(p + "mlp.c_proj.weight").t().contiguous()
-                out[p + "mlp.fc_out.bias"] = get(p + "mlp.c_proj.bias")
-            else:  # gpt_neo
-                out[p + "attn.qkv.weight"] = torch.cat(
-                    [get(p + f"attn.attention.{n}_proj.weight") for n in ("q", "k", "v")], 0)
-                out[p + "attn.out.weight"] = get(p + "attn.attention.out_proj.weight")
-                out[p + "attn.out.bias"] = get(p + "attn.attention.out_proj.bias")
-                out[p + "mlp.fc_in.weight"] = get(p + "mlp.c_fc.weight")
-                out[p + "mlp.fc_in.bias"] = get(p + "mlp.c_fc.bias")
-                out[p + "mlp.fc_out.weight"] = get(p + "mlp.c_proj.weight")
-                out[p + "mlp.fc_out.bias"] = get(p + "mlp.c_proj.bias")
-        out["ln_f.weight"] = get("ln_f.weight")
-        out["ln_f.bias"] = get("ln_f.bias")
-        if not cfg.tie_embeddings:
-            out["lm_head.weight"] = sd["lm_head.weight"]
-            if cfg.lm_head_bias and "lm_head.bias" in sd:
-                out["lm_head.bias"] = sd["lm_head.bias"]
-        return out
-
-    if a == "gpt_neox":
-        out["wte.weight"] = get("embed_in.weight")
-        for i in range(cfg.n_layers):
-            s, p = f"layers.{i}.", f"h.{i}."
-            out[p + "ln_1.weight"] = get(s + "input_layernorm.weight")
-            out[p + "ln_1.bias"] = get(s + "input_layernorm.bias")
-            out[p + "ln_2.weight"] = get(s + "post_attention_layernorm.weight")
-            out[p + "ln_2.bias"] = get(s + "post_attention_layernorm.bias")
-            out[p + "attn.qkv.weight"] = _neox_qkv_to_native(get(s + "attention.query_key_value.weight"), H, D)
-            out[p + "attn.qkv.bias"] = _neox_qkv_to_native(get(s + "attention.query_key_value.bias"), H, D)
-            out[p + "attn.out.weight"] = get(s + "attention.dense.weight")
-            out[p + "attn.out.bias"] = get(s + "attention.dense.bias")
-            out[p + "mlp.fc_in.weight"] = get(s + "mlp.dense_h_to_4h.weight")
-            out[p + "mlp.fc_in.bias"] = get(s + "mlp.dense_h_to_4h.bias")
-            out[p + "mlp.fc_out.weight"] = get(s + "mlp.dense_4h_to_h.weight")
-            out[p + "mlp.fc_out.bias"] = get(s + "mlp.dense_4h_to_h.bias")
-        out["ln_f.weight"] = get("final_layer_norm.weight")
-        out["ln_f.bias"] = get("final_layer_norm.bias")
-        if not cfg.tie_embeddings:
-            out["lm_head.weight"] = sd["embed_out.weight"] if "embed_out.weight" in sd else sd["lm_head.weight"]
-        return out
-
-    if a == "bloom":
-        out["wte.weight"] = get("word_embeddings.weight")
-        out["emb_ln.weight"] = get("word_embeddings_layernorm.weight")
-        out["emb_ln.bias"] = get("word_embeddings_layernorm.bias")
-        for i in range(cfg.n_layers):
-            p = f"h.{i}."
-            out[p + "ln_1.weight"] = get(p + "input_layernorm.weight")
-            out[p + "ln_1.bias"] = get(p + "input_layernorm.bias")
-            out[p + "ln_2.weight"] = get(p + "post_attention_layernorm.weight")
-            out[p + "ln_2.bias"] = get(p + "post_attention_layernorm.bias")
-            out[p + "attn.qkv.weight"] = _neox_qkv_to_native(get(p + "self_attention.query_key_value.weight"), H, D)
-            out[p + "attn.qkv.bias"] = _neox_qkv_to_native(get(p + "self_attention.query_key_value.bias"), H, D)
-            out[p + "attn.out.weight"] = get(p + "self_attention.dense.weight")
-            out[p + "attn.out.bias"] = get(p + "self_attention.dense.bias")
-            out[p + "mlp.fc_in.weight"] = get(p + "mlp.dense_h_to_4h.weight")
-            out[p + "mlp.fc_in.bias"] = get(p + "mlp.dense_h_to_4h.bias")
-            out[p + "mlp.fc_out.weight"] = get(p + "mlp.dense_4h_to_h.weight")
-            out[p + "mlp.fc_out.bias"] = get(p + "mlp.dense_4h_to_h.bias")
-        out["ln_f.weight"] = get("ln_f.weight")
-        out["ln_f.bias"] = get("ln_f.bias")
-        return out
-    raise ValueError(a)
+def hf_to_native(sd: dict, cfg: LMConfig) -> dict:
+    """Map an HF state dict onto CausalLM parameter names."""
+    plan = hf_to_native_plan(cfg, prefixed_getter(sd), tuple(sd.keys()))
+    return {k: f() for k, f in plan.items()}
 
 
 def native_to_hf(sd: dict, cfg: LMConfig) -> dict:

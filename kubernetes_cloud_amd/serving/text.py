@@ -70,10 +70,10 @@ def load_lm(path: str, device=None, dtype=torch.bfloat16, tensors_file: str | No
 
 class TextGenerator:
     def __init__(self, model, tokenizer, max_slots: int = 32, use_graphs: bool | None = None,
-                 background: bool = True, max_len: int | None = None):
+                 background: bool = True, max_len: int | None = None, runner=None):
         self.model, self.tokenizer = model, tokenizer
         self.engine = LLMEngine(model, max_slots=max_slots, max_len=max_len or model.cfg.max_pos,
-                                use_graphs=use_graphs)
+                                use_graphs=use_graphs, runner=runner)
         self.background = background
         if background:
             self.engine.start()
