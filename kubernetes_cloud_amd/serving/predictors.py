@@ -250,3 +250,21 @@ def aitextgen_main(argv=None):
 
 __all__ = ["BloomPredictor", "GPTJPredictor", "AITextGenPredictor", "GPT2Predictor", "GPT2Transformer",
            "bloom_options", "wait_for_ready_file", "create_gptj_text_app"]
+
+
+def gpt2_predictor_main(argv=None):
+    path = os.getenv("MODEL_PATH", "/mnt/pvc/gpt2")
+    model, tok = load_lm(path, random_init=not os.path.isdir(path))
+    ModelServer(argv=argv).start([GPT2Predictor(os.getenv("MODEL_NAME", "gpt-2"), TextGenerator(model, tok))])
+
+
+def gpt2_transformer_main(argv=None):
+    import argparse
+
+    from ..io.hf import load_tokenizer
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model_name", default="model")
+    ap.add_argument("--predictor_host", default=os.getenv("PREDICTOR_HOST"))
+    a, rest = ap.parse_known_args(argv)
+    tok = load_tokenizer(os.getenv("TOKENIZER_PATH", "/mnt/pvc/gpt2"))
+    ModelServer(argv=rest).start([GPT2Transformer(a.model_name, a.predictor_host, tok)])

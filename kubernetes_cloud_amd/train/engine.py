@@ -228,6 +228,44 @@ class TrainEngine:
         loss.backward()
         self._micro += 1
 
+    def backward_from(self, tensors, grads):
+        """Backward of one micro-batch from an intermediate output (pipeline
+        stages: ``tensors`` = this stage's output, ``grads`` = dL/d(output)
+        received from the next stage; ``grads=None`` for a loss)."""
+        torch.autograd.backward(tensors, grads)
+        self._micro += 1
+
+    def add_pre_step(self, fn):
+        """``fn(engine)`` runs after the gradient reduction, before clipping/AdamW."""
+        if not hasattr(self, "_pre_step"):
+            self._pre_step = []
+        self._pre_step.append(fn)
+
+    def set_model_parallel(self, norm_group, replicated, copies: int = 1):
+        """Tensor/pipeline parallel runs: the clip norm sums over ``norm_group``
+        (all model-parallel shards of one replica). ``replicated``: names of
+        params present ``copies`` times in that group (counted once), or a dict
+        name -> copies (copies 0 = another rank counts it, e.g. the last
+        stage's copy of a tied embedding)."""
+        if not isinstance(replicated, dict):
+            replicated = {n: copies for n in replicated}
+        self._norm_group, self._replicated = norm_group, dict(replicated)
+
+    def _mp_sumsq(self, sumsq):
+        grp = getattr(self, "_norm_group", None)
+        if grp is None:
+            return sumsq
+        if self.sharded:
+            raise NotImplementedError("model-parallel clipping with ZeRO sharding: use zero_stage=0 (plain DP)")
+        adj = sumsq.clone()
+        for sl in self.slots:
+            c = self._replicated.get(sl.name)
+            if c is not None and c != 1:
+                w = 1.0 if c == 0 else (1.0 - 1.0 / c)
+                adj -= w * self.grad[sl.offset:sl.offset + sl.numel].float().pow(2).sum()
+        dist.all_reduce(adj, group=grp)
+        return adj
+
     def step(self, lr: float | None = None) -> None:
         # grads of params that got no gradient this step are zero
         for s in self.slots:
@@ -240,12 +278,15 @@ class TrainEngine:
                 w.wait()
                 if out is not None:
                     out.copy_(out_c)
+        for fn in getattr(self, "_pre_step", ()):
+            fn(self)
         inv = 1.0 / self.world
         if self.loss_scaler is not None and self.loss_scaler.enabled:
             inv /= self.loss_scaler.scale
         sumsq = self.opt.local_sumsq()
         if self.sharded:
             dist.all_reduce(sumsq, group=self.group)
+        sumsq = self._mp_sumsq(sumsq)
         self.opt.set_clip(sumsq, self.max_grad_norm, inv)
         self.opt.step(lr, use_clip=True)
         if self.sharded:

@@ -1,0 +1,284 @@
+"""ResNet-50 ImageNet data-parallel trainer (T13).
+
+CLI = the union of resnet50_pytorch.py:28-70 and resnet50_horovod.py:18-62
+(``--batch-size`` 64, ``--epochs`` 10, ``--lr`` 0.01 (x world size),
+``--momentum`` .9, ``--no-cuda``, ``--seed``, ``--log-interval``, ``--log-dir``,
+``--data-dir`` (train/ + val/ ImageFolder), ``--model-dir``, ``--interpolation``,
+``--val-resize-size`` 256, ``--val-crop-size``/``--train-crop-size`` 224,
+``-j/--workers``, ``--wandb-project``/``--wandb-run``, ``--backend``; Horovod's
+``--fp16-allreduce``, ``--use-mixed-precision``, ``--gradient-predivide-factor``;
+``--use-adasum`` is accepted and falls back to averaging).
+
+MI355X choices: DDP over RCCL with 100 MB buckets (fewer, larger ring
+all-reduces over the point-to-point xGMI links), gradient all-reduce
+overlapped with backward, channels_last + bf16 autocast (no loss scaler
+needed), ``--fp16-allreduce`` = bf16-compressed gradient buckets, rank-0
+checkpoint ``resnet50_imagenet.pt`` (resnet50_pytorch.py:143-145), top-1/top-5
+accuracy (util.py:150-166). ``--synthetic N`` trains on random tensors (bench /
+tests; no dataset offline).
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import os
+import shutil
+import time
+from pathlib import Path
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+import torch.nn.functional as F
+
+MEAN = (0.485, 0.456, 0.406)
+STD = (0.229, 0.224, 0.225)
+IMG_EXT = (".jpg", ".jpeg", ".png", ".bmp", ".JPEG")
+
+
+def build_parser():
+    p = argparse.ArgumentParser(description="ResNet-50 ImageNet (MI355X DDP)")
+    p.add_argument("--batch-size", type=int, default=64)
+    p.add_argument("--epochs", type=int, default=10)
+    p.add_argument("--lr", type=float, default=0.01)
+    p.add_argument("--momentum", type=float, default=0.9)
+    p.add_argument("--no-cuda", action="store_true", default=False)
+    p.add_argument("--seed", type=int, default=1)
+    p.add_argument("--log-interval", type=int, default=10)
+    p.add_argument("--log-dir", type=Path, default=Path("./logs"))
+    p.add_argument("--data-dir", type=Path, default=Path("./data"))
+    p.add_argument("--model-dir", type=Path, default=None)
+    p.add_argument("--interpolation", default="bilinear", type=str)
+    p.add_argument("--val-resize-size", default=256, type=int)
+    p.add_argument("--val-crop-size", default=224, type=int)
+    p.add_argument("--train-crop-size", default=224, type=int)
+    p.add_argument("-j", "--workers", default=16, type=int)
+    p.add_argument("--wandb-project", type=str, default=None)
+    p.add_argument("--wandb-run", type=str, default=None)
+    p.add_argument("--backend", type=str, default=None, help="nccl (RCCL) on GPUs, gloo on CPU")
+    p.add_argument("--fp16-allreduce", action="store_true", default=False)
+    p.add_argument("--use-mixed-precision", action="store_true", default=False)
+    p.add_argument("--use-adasum", action="store_true", default=False)
+    p.add_argument("--gradient-predivide-factor", type=float, default=1.0)
+    p.add_argument("--bucket-mb", type=int, default=100)
+    p.add_argument("--synthetic", type=int, default=0, help="N synthetic samples per epoch instead of data-dir")
+    p.add_argument("--num-classes", type=int, default=1000)
+    p.add_argument("--max-steps", type=int, default=0)
+    p.add_argument("--prepare-val", action="store_true", help="sort val images into class folders and exit")
+    p.add_argument("--val-labels", type=Path, default=None)
+    p.add_argument("--local_rank", "--local-rank", type=int, default=-1)
+    return p
+
+
+# ------------------------------------------------------------------ data
+class ImageFolder(torch.utils.data.Dataset):
+    def __init__(self, root: Path, train: bool, args):
+        root = Path(root)
+        self.classes = sorted(d.name for d in root.iterdir() if d.is_dir())
+        self.items = []
+        for i, c in enumerate(self.classes):
+            for f in sorted((root / c).iterdir()):
+                if f.suffix in IMG_EXT:
+                    self.items.append((f, i))
+        self.train, self.args = train, args
+
+    def __len__(self):
+        return len(self.items)
+
+    def __getitem__(self, i):
+        from PIL import Image
+        import random
+        path, y = self.items[i]
+        img = Image.open(path).convert("RGB")
+        a = self.args
+        interp = {"bilinear": Image.BILINEAR, "bicubic": Image.BICUBIC, "nearest": Image.NEAREST}.get(
+            a.interpolation, Image.BILINEAR)
+        if self.train:  # RandomResizedCrop(scale .08-1, ratio 3/4-4/3) + horizontal flip
+            W, H = img.size
+            for _ in range(10):
+                area = W * H * random.uniform(0.08, 1.0)
+                ar = random.uniform(3 / 4, 4 / 3)
+                w, h = int(round((area * ar) ** 0.5)), int(round((area / ar) ** 0.5))
+                if 0 < w <= W and 0 < h <= H:
+                    x0, y0 = random.randint(0, W - w), random.randint(0, H - h)
+                    break
+            else:
+                w, h = min(W, H), min(W, H)
+                x0, y0 = (W - w) // 2, (H - h) // 2
+            img = img.crop((x0, y0, x0 + w, y0 + h)).resize((a.train_crop_size,) * 2, interp)
+            if random.random() < 0.5:
+                img = img.transpose(Image.FLIP_LEFT_RIGHT)
+        else:
+            W, H = img.size
+            s = a.val_resize_size / min(W, H)
+            img = img.resize((max(1, round(W * s)), max(1, round(H * s))), interp)
+            W, H = img.size
+            c = a.val_crop_size
+            img = img.crop(((W - c) // 2, (H - c) // 2, (W - c) // 2 + c, (H - c) // 2 + c))
+        import numpy as np
+        x = torch.from_numpy(np.asarray(img, dtype=np.float32) / 255.0).permute(2, 0, 1)
+        x = (x - torch.tensor(MEAN)[:, None, None]) / torch.tensor(STD)[:, None, None]
+        return x, y
+
+
+class Synthetic(torch.utils.data.Dataset):
+    def __init__(self, n, size, classes):
+        self.n, self.size, self.classes = n, size, classes
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, i):
+        g = torch.Generator().manual_seed(i)
+        return torch.randn(3, self.size, self.size, generator=g), int(torch.randint(0, self.classes, (1,),
+                                                                                      generator=g))
+
+
+def prepare_val(data_dir: Path, labels_csv: Path):
+    """LOC_val_solution.csv (ImageId, 'nXXXX x y ...') -> val/<wnid>/<img>."""
+    val = Path(data_dir) / "val"
+    with open(labels_csv) as f:
+        for row in csv.DictReader(f):
+            wnid = row["PredictionString"].split()[0]
+            src = val / f"{row['ImageId']}.JPEG"
+            if src.exists():
+                (val / wnid).mkdir(exist_ok=True)
+                shutil.move(str(src), str(val / wnid / src.name))
+
+
+def accuracy(output, target, topk=(1, 5)):
+    maxk = min(max(topk), output.shape[1])
+    _, pred = output.topk(maxk, 1, True, True)
+    correct = pred.t().eq(target.view(1, -1))
+    return [correct[:min(k, maxk)].reshape(-1).float().sum() for k in topk]
+
+
+# ----------------------------------------------------------------- train
+def main(argv=None):
+    from ..models.resnet import resnet50
+    from ..obs.metrics import MetricsSink
+    args = build_parser().parse_args(argv)
+    if args.prepare_val:
+        prepare_val(args.data_dir, args.val_labels)
+        return {}
+    use_cuda = torch.cuda.is_available() and not args.no_cuda
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", max(args.local_rank, 0)))
+    if use_cuda:
+        torch.cuda.set_device(local % torch.cuda.device_count())
+    dev = torch.device("cuda", torch.cuda.current_device()) if use_cuda else torch.device("cpu")
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group(backend=args.backend or ("nccl" if use_cuda else "gloo"))
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    torch.manual_seed(args.seed)
+    if args.synthetic:
+        train_ds = Synthetic(args.synthetic, args.train_crop_size, args.num_classes)
+        val_ds = Synthetic(max(args.synthetic // 4, 1), args.val_crop_size, args.num_classes)
+    else:
+        train_ds = ImageFolder(args.data_dir / "train", True, args)
+        val_ds = ImageFolder(args.data_dir / "val", False, args)
+    from torch.utils.data import DataLoader, DistributedSampler
+    tr_s = DistributedSampler(train_ds, num_replicas=world, rank=rank, shuffle=True, seed=args.seed)
+    va_s = DistributedSampler(val_ds, num_replicas=world, rank=rank, shuffle=False)
+    tl = DataLoader(train_ds, batch_size=args.batch_size, sampler=tr_s, num_workers=args.workers,
+                    pin_memory=use_cuda, drop_last=True, persistent_workers=args.workers > 0)
+    vl = DataLoader(val_ds, batch_size=args.batch_size, sampler=va_s, num_workers=args.workers, pin_memory=use_cuda)
+    model = resnet50(args.num_classes).to(dev)
+    if use_cuda:
+        model = model.to(memory_format=torch.channels_last)
+    if world > 1:
+        model = nn.parallel.DistributedDataParallel(model, device_ids=[dev.index] if use_cuda else None,
+                                                    bucket_cap_mb=args.bucket_mb, gradient_as_bucket_view=True)
+        if args.fp16_allreduce or args.gradient_predivide_factor != 1.0:
+            model.register_comm_hook(state=(dist.group.WORLD, args.fp16_allreduce, args.gradient_predivide_factor),
+                                     hook=_compressed_allreduce_hook)
+    opt = torch.optim.SGD(model.parameters(), lr=args.lr * world, momentum=args.momentum)
+    sink = MetricsSink(str(args.log_dir), args.wandb_run or "resnet50",
+                       project=args.wandb_project or "resnet50-imagenet", enabled=rank == 0)
+    amp = args.use_mixed_precision and use_cuda
+    step, t_start = 0, time.perf_counter()
+    last = {}
+    for epoch in range(1, args.epochs + 1):
+        model.train()
+        tr_s.set_epoch(epoch)
+        for bi, (x, y) in enumerate(tl):
+            t0 = time.perf_counter()
+            x = x.to(dev, non_blocking=True)
+            y = y.to(dev, non_blocking=True)
+            if use_cuda:
+                x = x.contiguous(memory_format=torch.channels_last)
+            opt.zero_grad(set_to_none=True)
+            with torch.autocast(dev.type, dtype=torch.bfloat16, enabled=amp):
+                out = model(x)
+                loss = F.cross_entropy(out.float(), y)
+            loss.backward()
+            opt.step()
+            step += 1
+            if bi % args.log_interval == 0:
+                lv = float(loss)
+                dt = time.perf_counter() - t0
+                if rank == 0:
+                    print(f"Train Epoch: {epoch} [{bi * len(x)}/{len(tr_s)} ({100. * bi / max(len(tl), 1):.0f}%)]"
+                          f"\tLoss: {lv:.6f}", flush=True)
+                    sink.log({"train/loss": lv, "train/epoch": epoch, "train/step": step,
+                              "train/samples_seen": step * len(x) * world,
+                              "perf/rank_samples_per_second": len(x) / dt}, step=step)
+            if args.max_steps and step >= args.max_steps:
+                break
+        last = evaluate(model, vl, va_s, dev, world, amp)
+        if rank == 0:
+            print(f"Test Epoch: {epoch}\tloss={last['loss']:.4f}\tAcc@1={last['acc1']:.3f}\tAcc@5={last['acc5']:.3f}",
+                  flush=True)
+            sink.log({"test/loss": last["loss"], "test/epoch": epoch, "test/acc1": last["acc1"],
+                      "test/acc5": last["acc5"]}, step=step)
+        if args.max_steps and step >= args.max_steps:
+            break
+    if rank == 0:
+        print(f"Training time: {time.perf_counter() - t_start:0.3f}s")
+        if args.model_dir:
+            args.model_dir.mkdir(parents=True, exist_ok=True)
+            sd = (model.module if hasattr(model, "module") else model).state_dict()
+            torch.save(sd, args.model_dir / "resnet50_imagenet.pt")
+        sink.close()
+    if dist.is_initialized():
+        dist.barrier()
+    return {"steps": step, **last}
+
+
+@torch.no_grad()
+def evaluate(model, loader, sampler, dev, world, amp):
+    model.eval()
+    tot = torch.zeros(4, device=dev, dtype=torch.float64)  # loss sum, acc1, acc5, n
+    for x, y in loader:
+        x, y = x.to(dev), y.to(dev)
+        with torch.autocast(dev.type, dtype=torch.bfloat16, enabled=amp):
+            out = model(x).float()
+        a1, a5 = accuracy(out, y)
+        tot += torch.stack([F.cross_entropy(out, y, reduction="sum"), a1, a5,
+                            torch.tensor(float(len(y)), device=dev)]).double()
+    if world > 1:
+        dist.all_reduce(tot)
+    n = max(float(tot[3]), 1.0)
+    return {"loss": float(tot[0]) / n, "acc1": 100.0 * float(tot[1]) / n, "acc5": 100.0 * float(tot[2]) / n}
+
+
+def _compressed_allreduce_hook(state, bucket):
+    """Horovod's fp16 compression / predivide factor as a DDP comm hook: bf16
+    wire format on MI355X (same bytes as fp16, no overflow), mean over ranks."""
+    group, compress, predivide = state
+    world = dist.get_world_size(group)
+    buf = bucket.buffer()
+    t = buf.to(torch.bfloat16) if compress else buf.clone()
+    t.div_(predivide)
+    fut = dist.all_reduce(t, group=group, async_op=True).get_future()
+
+    def done(f):
+        r = f.value()[0]
+        buf.copy_(r.to(buf.dtype).mul_(predivide / world))
+        return buf
+    return fut.then(done)
+
+
+if __name__ == "__main__":
+    main()
