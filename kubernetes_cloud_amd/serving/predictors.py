@@ -268,3 +268,70 @@ def gpt2_transformer_main(argv=None):
     a, rest = ap.parse_known_args(argv)
     tok = load_tokenizer(os.getenv("TOKENIZER_PATH", "/mnt/pvc/gpt2"))
     ModelServer(argv=rest).start([GPT2Transformer(a.model_name, a.predictor_host, tok)])
+
+
+# ------------------------------------------------------ image classifier
+class ImageClassifier(Model):
+    """S11: ``{"instances": [{"b64": ...} | {"url": ...}]}`` -> ``{"predictions":
+    [{"class", "score"}]}`` (image-classifier/transformer/transformer.py:25-48),
+    served by our ResNet-50 directly instead of a TF-Serving Inception behind
+    a transformer. Labels from ``LABELS_PATH`` (one per line) or ``class_<i>``."""
+
+    def __init__(self, name: str = "classifier", model=None, labels: list | None = None, size: int = 224):
+        super().__init__(name)
+        self.model, self.labels, self.size = model, labels, size
+        if model is not None:
+            self.ready = True
+
+    def load(self, weights: str | None = None):
+        import torch
+
+        from ..models.resnet import resnet50
+        m = resnet50()
+        w = weights or os.getenv("MODEL_PATH", "/mnt/models/resnet50_imagenet.pt")
+        if os.path.exists(w):
+            m.load_state_dict(torch.load(w, map_location="cpu", weights_only=True))
+        dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
+        self.model = m.to(dev).eval()
+        lp = os.getenv("LABELS_PATH", "")
+        if lp and os.path.exists(lp):
+            with open(lp) as f:
+                self.labels = [ln.rstrip("\n") for ln in f]
+        self.ready = True
+
+    def _image(self, inst: dict):
+        import base64
+        import io
+
+        import numpy as np
+        import torch
+        from PIL import Image
+        if "b64" in inst:
+            raw = base64.b64decode(inst["b64"])
+        elif "url" in inst:
+            import httpx
+            raw = httpx.get(inst["url"], timeout=30.0).content
+        else:
+            raise InvalidInput("instance needs 'b64' or 'url'")
+        img = Image.open(io.BytesIO(raw)).convert("RGB")
+        W, H = img.size
+        s = 256 / min(W, H)
+        img = img.resize((max(1, round(W * s)), max(1, round(H * s))), Image.BILINEAR)
+        W, H = img.size
+        c = self.size
+        img = img.crop(((W - c) // 2, (H - c) // 2, (W - c) // 2 + c, (H - c) // 2 + c))
+        x = torch.from_numpy(np.asarray(img, dtype=np.float32) / 255.0).permute(2, 0, 1)
+        mean = torch.tensor((0.485, 0.456, 0.406))[:, None, None]
+        std = torch.tensor((0.229, 0.224, 0.225))[:, None, None]
+        return (x - mean) / std
+
+    def predict(self, request: dict, headers=None) -> dict:
+        import torch
+        xs = torch.stack([self._image(i) for i in request["instances"]])
+        p = next(self.model.parameters())
+        with torch.no_grad():
+            probs = self.model(xs.to(p.device, p.dtype)).float().softmax(-1)
+        sc, ix = probs.max(-1)
+        lab = self.labels
+        return {"predictions": [{"class": lab[int(i)] if lab and int(i) < len(lab) else f"class_{int(i)}",
+                                 "score": float(s)} for s, i in zip(sc, ix)]}

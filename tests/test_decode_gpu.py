@@ -92,7 +92,10 @@ def test_sample_greedy_and_masks(V):
         x = logits.float() / t
         for b in range(B):
             keep = dops.keep_mask_reference(x[b], k, p)
-            assert abs(int(kept[b]) - int(keep.sum())) <= max(1, int(keep.sum()) // 100), (t, k, p, b)
+            # the kernel keeps every token tied with the threshold value (bf16 logits tie often);
+            # HF's sort keeps an arbitrary subset of a tie group at the top-p cut
+            expect = int((x[b] >= x[b][keep].min()).sum())
+            assert int(keep.sum()) <= int(kept[b]) <= expect + max(1, expect // 100), (t, k, p, b)
             assert bool(keep[ids[b]]), (t, k, p, b)
 
 

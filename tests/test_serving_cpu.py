@@ -187,3 +187,42 @@ def test_evaluator_cli(gptj_dir, tmp_path):
     with pytest.raises(SystemExit):
         main(["--model", gptj_dir], out=buf)
     assert torch.is_tensor(torch.zeros(1))
+
+
+def test_classifier_and_loadgen(gptj_dir):
+    import base64
+    import socket
+
+    import uvicorn
+    from PIL import Image
+
+    from kubernetes_cloud_amd.models.resnet import resnet50
+    from kubernetes_cloud_amd.serving.loadgen import benchmark
+    from kubernetes_cloud_amd.serving.predictors import GPTJPredictor, ImageClassifier
+    buf = io.BytesIO()
+    Image.new("RGB", (300, 260), (120, 30, 200)).save(buf, format="PNG")
+    clf = ImageClassifier(model=resnet50(10).eval(), labels=[f"l{i}" for i in range(10)])
+    c = TestClient(ModelServer(http_port=1).create_app([clf]))
+    r = c.post("/v1/models/classifier:predict",
+               json={"instances": [{"b64": base64.b64encode(buf.getvalue()).decode()}]}).json()
+    assert r["predictions"][0]["class"].startswith("l") and 0 < r["predictions"][0]["score"] <= 1
+    # load generator against a real uvicorn server (kserve protocol, async, bounded concurrency)
+    m, tok = load_lm(gptj_dir, device="cpu")
+    p = GPTJPredictor(generator=TextGenerator(m, tok, max_slots=4))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    server = uvicorn.Server(uvicorn.Config(ModelServer(http_port=port).create_app([p]), host="127.0.0.1",
+                                           port=port, log_level="error"))
+    th = threading.Thread(target=server.run, daemon=True)
+    th.start()
+    import time
+    for _ in range(100):
+        if server.started:
+            break
+        time.sleep(0.05)
+    res = benchmark(f"http://127.0.0.1:{port}", "kserve", 6, True, 3)
+    server.should_exit = True
+    th.join(timeout=10)
+    p.generator.close()
+    assert res["successes"] == 6 and res["p99_s"] >= res["p50_s"] > 0
