@@ -27,6 +27,7 @@ import torch
 
 from .. import ops
 from ..ops import decode as dops
+from ..ops.gemv import skinny_linear
 
 
 def _next_pow2(n: int, lo: int = 1) -> int:
@@ -135,8 +136,9 @@ class ModelRunner:
             if self.rot > 0:
                 ops.apply_rotary_(q, k, self.rot, T, cfg.rotary_interleaved, cfg.rotary_base,
                                   max_pos=self.max_len)
-            self.cache.k[li][sl, :, :T] = k.transpose(1, 2)
-            self.cache.v[li][sl, :, :T] = v.transpose(1, 2)
+            for i, s_ in enumerate(slots):  # strided copies (advanced-index scatter is ~4x slower)
+                self.cache.k[li][s_, :, :T].copy_(k[i].transpose(0, 1))
+                self.cache.v[li][s_, :, :T].copy_(v[i].transpose(0, 1))
             if at.window:
                 o = self._windowed_prefill(q, k, v, at)
             else:
@@ -172,7 +174,7 @@ class ModelRunner:
         for li, blk in enumerate(m.h):
             x, h = blk.ln_1(h, residual=pending) if pending else (blk.ln_1(h), h)
             at = blk.attn
-            qkv = at.qkv(x)
+            qkv = self._lin(at.qkv, x)
             kc, vc = self.cache.k[li], self.cache.v[li]
             dops.decode_prep(qkv, self.H, self.Hkv, self.D, self.rot, cfg.rotary_interleaved, self.cos,
                              self.sin, pos, slots, kc, vc)
@@ -181,15 +183,38 @@ class ModelRunner:
             else:
                 o = dops.decode_attention(qkv, kc, vc, slots, kv_lens, self.H, max_kv, at.scale, at.alibi,
                                           out=obuf, ws=ws)
-            a = at.out(o)
+            a = self._lin(at.out, o)
             if cfg.parallel_residual:
                 x2 = x if blk.ln_2 is None else blk.ln_2(h)
-                pending = (a, blk.mlp(x2))
+                pending = (a, self._mlp(blk.mlp, x2))
             else:
                 x2, h = blk.ln_2(h, residual=(a,))
-                pending = (blk.mlp(x2),)
+                pending = (self._mlp(blk.mlp, x2),)
         y, _ = m.ln_f(h, residual=pending)
-        return m.logits_from_hidden(y)
+        return self._head(y)
+
+    # decode linears: skinny GEMM (W streamed once, bias/GELU fused) for <= 16 rows
+    def _lin(self, mod, x, act: int = 0):
+        from ..parallel.tensor_parallel import ParallelLMHead, RowParallelLinear, gather_last_dim, reduce_from_tp
+        if isinstance(mod, RowParallelLinear):
+            y = reduce_from_tp(skinny_linear(x, mod.weight, None), mod.group)
+            return y + mod.bias if mod.bias is not None else y
+        if isinstance(mod, ParallelLMHead):
+            return gather_last_dim(skinny_linear(x, mod.local_weight(), mod.bias), mod.group)
+        return skinny_linear(x, mod.weight, mod.bias, act)
+
+    def _mlp(self, mlp, x):
+        act = 1 if mlp.approx in ("tanh", True) else 2
+        from ..parallel.tensor_parallel import RowParallelLinear
+        if isinstance(mlp.fc_in, RowParallelLinear):  # never: fc_in is column-parallel
+            raise AssertionError
+        return self._lin(mlp.fc_out, self._lin(mlp.fc_in, x, act))
+
+    def _head(self, y):
+        m = self.model
+        if m.lm_head is None:
+            return skinny_linear(y, m.wte.weight)
+        return self._lin(m.lm_head, y)
 
     def _windowed_decode(self, qkv, kc, vc, slots, kv_lens, at):
         B = qkv.shape[0]

@@ -21,7 +21,8 @@ class _GeluFn(torch.autograd.Function):
     def backward(ctx, dy):
         (u,) = ctx.saved_tensors
         du = torch.empty_like(u)
-        _lib.call("kca_gelu_bwd", dy.contiguous().data_ptr(), u.data_ptr(), du.data_ptr(),
+        dy = dy.contiguous()
+        _lib.call("kca_gelu_bwd", dy.data_ptr(), u.data_ptr(), du.data_ptr(),
                   u.numel(), int(ctx.approx), _lib.stream())
         return du, None
 

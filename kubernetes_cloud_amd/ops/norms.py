@@ -28,8 +28,11 @@ class _LayerNormFn(torch.autograd.Function):
         y = torch.empty_like(x2)
         mean = torch.empty(rows, device=x.device, dtype=torch.float32)
         rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
-        _lib.call("kca_layernorm_fwd", x2.data_ptr(), _lib.ptr(r1.contiguous() if r1 is not None else None),
-                  _lib.ptr(r2.contiguous() if r2 is not None else None), _lib.ptr(h),
+        # keep the contiguous copies alive until the launch: a temporary freed
+        # inside the argument list is recycled by the next allocation (r2's copy)
+        r1c = r1.contiguous() if r1 is not None else None
+        r2c = r2.contiguous() if r2 is not None else None
+        _lib.call("kca_layernorm_fwd", x2.data_ptr(), _lib.ptr(r1c), _lib.ptr(r2c), _lib.ptr(h),
                   weight.data_ptr(), _lib.ptr(bias), y.data_ptr(), mean.data_ptr(),
                   rstd.data_ptr(), rows, d, float(eps), _lib.stream())
         ctx.save_for_backward(h if has_res else x2, weight, mean, rstd)

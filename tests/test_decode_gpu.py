@@ -158,3 +158,19 @@ def test_engine_gpu_graphs_match_eager_and_recompute(preset):
     b = [r.output for r in eng.generate(prompts, sp2)]
     assert a == b
     assert _lib.has("kca_decode_attn")
+
+
+@pytest.mark.parametrize("M", [1, 3, 8, 16])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (12288, 4096), (4096, 16384), (5376, 14336), (14336, 1792)])
+def test_skinny_gemm(M, N, K):
+    from kubernetes_cloud_amd.ops.gemv import skinny_linear
+    torch.manual_seed(M + N + K)
+    x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+    b = torch.randn(N, device=dev).to(torch.bfloat16)
+    ref = x.float() @ w.float().t() + b.float()
+    for act, fn in ((0, lambda t: t), (1, lambda t: torch.nn.functional.gelu(t, approximate="tanh")),
+                    (2, torch.nn.functional.gelu)):
+        y = skinny_linear(x, w, b, act)
+        assert y.shape == (M, N)
+        assert (y.float() - fn(ref)).abs().max() < 0.05, act
