@@ -80,6 +80,7 @@ class LLMEngine:
         self.running: list[Request] = []
         self._ids = itertools.count()
         self._lock = threading.Lock()
+        self._step_lock = threading.Lock()
         self._wake = threading.Event()
         self._thread = None
         self._stop = False
@@ -150,8 +151,31 @@ class LLMEngine:
             r.future.set_result(r)
 
     # ---------------------------------------------------------------- step
+    def beam_generate(self, prompt: list, num_beams: int, max_new_tokens: int, eos_token_id: int | None = None,
+                      len_penalty: float = 1.0, diversity_rate: float = 0.0, n_return: int = 1):
+        """Beam search for one prompt on ``num_beams`` slots of this engine's cache
+        (mutually exclusive with ``step``; FT beam_width > 1 requests)."""
+        from .beam import beam_search
+        if hasattr(self.runner, "_send"):
+            raise NotImplementedError("beam search with a tensor-parallel runner")
+        with self._step_lock:
+            with self._lock:
+                if len(self.free) < num_beams:
+                    raise RuntimeError(f"need {num_beams} free cache slots, have {len(self.free)}")
+                slots = [self.free.pop() for _ in range(num_beams)]
+            try:
+                return beam_search(self.runner, [int(t) for t in prompt], slots, max_new_tokens, eos_token_id,
+                                   len_penalty, diversity_rate, n_return)
+            finally:
+                with self._lock:
+                    self.free.extend(slots)
+
     def step(self) -> list[Request]:
         """Admit + one decode step. Returns the requests that finished."""
+        with self._step_lock:
+            return self._step()
+
+    def _step(self) -> list[Request]:
         finished = []
         with self._lock:
             admit = []

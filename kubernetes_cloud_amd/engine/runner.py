@@ -260,6 +260,33 @@ class ModelRunner:
                            ban_ids=pk.d("bans").view(Bb, self.max_bans), seeds=pk.d("seeds"), step=0,
                            ws=st["sws"], out_ids=st["ids"], out_logprobs=st["lps"])
 
+    # ----------------------------------------------------------- beam search
+    @torch.no_grad()
+    def decode_topk(self, tokens: list[int], positions: list[int], slots: list[int], k: int):
+        """Eager decode step returning the top-k next-token log-probs per row
+        (beam search; K30). -> (logprobs [n, k] fp32, ids [n, k] int64) on device."""
+        dev = self.device
+        tok = torch.tensor(tokens, device=dev, dtype=torch.long)
+        pos = torch.tensor(positions, device=dev, dtype=torch.int32)
+        sl = torch.tensor(slots, device=dev, dtype=torch.int32)
+        kl = pos + 1
+        max_kv = max(positions) + 1
+        logits = self._layers_decode(tok, pos, sl, kl, max_kv, None, None)
+        lp = torch.log_softmax(logits.float(), dim=-1)
+        return lp.topk(k, dim=-1)
+
+    @torch.no_grad()
+    def copy_slots(self, dst: list[int], src: list[int], upto: int):
+        """KV cache (and seen mask) of ``src`` slots -> ``dst`` slots, positions [0, upto)."""
+        if not dst:
+            return
+        d = torch.tensor(dst, device=self.device, dtype=torch.long)
+        s = torch.tensor(src, device=self.device, dtype=torch.long)
+        for k, v in zip(self.cache.k, self.cache.v):
+            k[d, :, :upto] = k[s, :, :upto]  # RHS gathered first: overlapping permutations are safe
+            v[d, :, :upto] = v[s, :, :upto]
+        self.seen[d] = self.seen[s]
+
     @torch.no_grad()
     def decode(self, rows: list[dict]):
         """rows: [{token, pos, slot, temperature, top_k, top_p, rep, seed, bans}]

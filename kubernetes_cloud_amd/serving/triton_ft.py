@@ -215,8 +215,10 @@ class FasterTransformerModel(Model):
             bad = bad * B
         if stop and len(stop) == 1 and B > 1:
             stop = stop * B
+        lpen = _col(inputs, "len_penalty", B, 1.0, float)
+        div = _col(inputs, "beam_search_diversity_rate", B, 0.0, float)
         if any(b > 1 for b in beam):
-            raise InvalidInput("beam_width > 1 is not supported by this engine build (use sampling)")
+            return self._beam_infer(ids, lens, out_len, end_id, beam, lpen, div, want_lp)
         prompts, params = [], []
         for b in range(B):
             p = ids[b, :lens[b]].tolist()
@@ -245,6 +247,28 @@ class FasterTransformerModel(Model):
         if want_lp:
             out["cum_log_probs"] = cum
             out["output_log_probs"] = olp
+        return out
+
+
+    def _beam_infer(self, ids, lens, out_len, end_id, beam, lpen, div, want_lp):
+        B, W = ids.shape[0], max(beam)
+        max_total = max(lens[b] + out_len[b] for b in range(B))
+        out_ids = np.zeros((B, W, max_total), dtype=np.int32)
+        seq_len = np.zeros((B, W), dtype=np.int32)
+        cum = np.zeros((B, W), dtype=np.float32)
+        for b in range(B):
+            p = ids[b, :lens[b]].tolist()
+            res = self.generator.engine.beam_generate(p, beam[b], out_len[b], end_id[b], lpen[b], div[b],
+                                                      n_return=beam[b])
+            for j, (toks, c) in enumerate(zip(res.sequences, res.cum_logprobs)):
+                full = p + toks
+                out_ids[b, j, :] = end_id[b]
+                out_ids[b, j, :len(full)] = full
+                seq_len[b, j] = len(full)
+                cum[b, j] = c
+        out = {"output_ids": out_ids, "sequence_length": seq_len}
+        if want_lp:
+            out["cum_log_probs"] = cum
         return out
 
 

@@ -117,3 +117,24 @@ def test_decode_reference_ops():
         ref = torch.einsum("hn,hnd->hd", (torch.einsum("hd,hnd->hn", qb, kb) / D ** 0.5).softmax(-1),
                            vc[s, :, :n].repeat_interleave(2, 0))
         assert torch.allclose(o[b].view(H, D), ref, atol=1e-5)
+
+
+def test_beam_search_matches_exhaustive():
+    """W=vocab beams over 2 steps == exhaustive best 2-token continuation."""
+    import itertools
+    m = tiny("gpt2", vocab=11)
+    eng = LLMEngine(m, max_slots=24, max_len=32)
+    prompt = [1, 2, 3]
+    res = eng.beam_generate(prompt, 11, 2, eos_token_id=None, len_penalty=0.0)
+    best, best_s = None, -1e9
+    with torch.no_grad():
+        for a, b in itertools.product(range(11), range(11)):
+            lp = torch.log_softmax(m(torch.tensor([prompt + [a]]))[0, -2:].float(), -1)
+            s = float(lp[0, a] + lp[1, b])
+            if s > best_s:
+                best, best_s = [a, b], s
+    assert res.sequences[0] == best and abs(res.cum_logprobs[0] - best_s) < 1e-4
+    # W=1 beam == greedy; slots are returned
+    g = eng.generate([prompt], SamplingParams(max_new_tokens=5, do_sample=False))[0].output
+    assert eng.beam_generate(prompt, 1, 5).sequences[0] == g
+    assert len(eng.free) == 24

