@@ -70,8 +70,8 @@ def _sources(sub, exts):
 
 
 def build_kernels(jobs: int = 8, verbose: bool = False) -> str:
-    srcs = _sources("kernels", (".hip",))
-    hdrs = _sources("kernels", (".h",))
+    srcs = _sources("kernels", (".hip",)) + _sources("comm", (".hip",))
+    hdrs = _sources("kernels", (".h",)) + _sources("comm", (".h",))
     obj_dir = os.path.join(BUILD, "kernels")
     os.makedirs(obj_dir, exist_ok=True)
     os.makedirs(OUT_DIR, exist_ok=True)
