@@ -56,6 +56,9 @@ def main():
     torch.cuda.synchronize()
     load_s = time.perf_counter() - t0
     batches = [int(b) for b in args.batches.split(",")]
+    if world > 1:  # one-shot xGMI all-reduce for the decode-size TP reductions
+        from kubernetes_cloud_amd.parallel.custom_ar import register
+        register(None)
     runner = ModelRunner(model, max_slots=max(batches), max_len=args.prompt_len + args.new_tokens + 8)
     if rank != 0:
         follower_loop(runner, ctrl)

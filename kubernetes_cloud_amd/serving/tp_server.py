@@ -60,6 +60,9 @@ def main(argv=None):
         wait_for_ready_file(args.model_path, opts["MODEL_DOWNLOAD_TIMEOUT"])
     dist.barrier(group=ctrl)
     model, tok = build_tp_engine_model(args, rank, world, None)
+    if world > 1:  # one-shot xGMI all-reduce for the decode-size TP reductions
+        from ..parallel.custom_ar import register
+        register(None)
     runner = ModelRunner(model, max_slots=args.max_batch, max_len=args.max_len)
     if rank != 0:
         follower_loop(runner, ctrl)
