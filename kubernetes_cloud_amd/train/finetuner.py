@@ -197,6 +197,7 @@ def main(argv=None):
 
     # ds_config subset
     zero_stage, betas, eps, wd, clip = args.zero_stage, (0.9, 0.999), 1e-8, 0.01, 1.0
+    bucket, comm_dtype, sched_kind = int(2e8), torch.float32, "linear"
     if args.ds_config:
         with open(args.ds_config) as f:
             ds = json.load(f)
@@ -209,11 +210,22 @@ def main(argv=None):
             wd = float(opt["weight_decay"])
         if isinstance(ds.get("gradient_clipping"), (int, float)):
             clip = float(ds["gradient_clipping"])
+        zo = ds.get("zero_optimization") or {}
+        if isinstance(zo.get("reduce_bucket_size"), (int, float)):
+            bucket = int(zo["reduce_bucket_size"])
+        if (ds.get("communication_data_type") or "").lower() in ("bf16", "bfloat16", "fp16"):
+            comm_dtype = torch.bfloat16
+        sched = ds.get("scheduler") or {}
+        if sched.get("type") == "WarmupLR":
+            sched_kind = "warmup"  # linear warmup then constant (ds_config.json:19-26)
+        if (zo.get("offload_optimizer") or {}).get("device") == "cpu" and main_proc:
+            log.info("ds_config offload_optimizer=cpu: optimizer state stays in HBM (288 GB); offload not needed")
     if zero_stage == 3 and main_proc:
         log.info("ZeRO-3 requested: parameters stay replicated (288 GB HBM), optimizer state sharded")
 
     engine = TrainEngine(model, lr=args.lr, betas=betas, eps=eps, weight_decay=wd, max_grad_norm=clip,
-                         zero_stage=zero_stage, grad_accum=args.gradients)
+                         zero_stage=zero_stage, grad_accum=args.gradients, bucket_elems=bucket,
+                         comm_dtype=comm_dtype)
     bs = args.bs if args.bs != -1 else estimate_batch_size(model, args.context_size, args.bs_divisor, dev)
     gas = args.gradients
     per_step = bs * gas * world
@@ -277,7 +289,7 @@ def main(argv=None):
             if step >= total_steps:
                 break
             base = s * per_step
-            lr = lr_at(step, args.lr, total_steps, warmup, "linear")
+            lr = lr_at(step, args.lr, total_steps, warmup, sched_kind)
             timer.start()
             loss_acc = None
             for g in range(gas):
