@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--new-tokens", type=int, default=64)
     ap.add_argument("--layers", type=int, default=0, help="override layer count (smoke runs only)")
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--decode-only", type=int, default=0,
+                    help="profile mode: prefill B prompts once, then time N pure decode steps")
     args = ap.parse_args()
     from kubernetes_cloud_amd.engine.llm_engine import LLMEngine, SamplingParams
     from kubernetes_cloud_amd.models.causal_lm import build_model
@@ -42,6 +44,22 @@ def main():
     eng = LLMEngine(m, max_slots=max(batches), max_len=args.prompt_len + args.new_tokens + 8,
                     use_graphs=not args.no_graphs)
     g = torch.Generator().manual_seed(0)
+    if args.decode_only:
+        B = batches[0]
+        prompts = [torch.randint(0, cfg.vocab_size, (args.prompt_len,), generator=g).tolist() for _ in range(B)]
+        sp = SamplingParams(max_new_tokens=args.decode_only + 8, do_sample=False)
+        reqs = [eng.add_request(p, sp) for p in prompts]
+        for _ in range(4):
+            eng.step()  # admit + warm the graph bucket
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.decode_only):
+            eng.step()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / args.decode_only
+        print(json.dumps({"metric": f"{args.model} decode-only", "batch": B, "decode_ms_per_step": round(dt * 1e3, 3),
+                          "decode_tokens_per_s": round(B / dt, 1)}), flush=True)
+        return
     for B in batches:
         prompts = [torch.randint(0, cfg.vocab_size, (args.prompt_len,), generator=g).tolist() for _ in range(B)]
         sp = SamplingParams(max_new_tokens=args.new_tokens, temperature=1.0, top_k=50, top_p=0.95, seed=1)

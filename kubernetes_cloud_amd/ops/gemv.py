@@ -28,7 +28,11 @@ def skinny_linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | No
     """x [M, K] (row stride multiple of 8), weight [N, K] contiguous."""
     M, K = x.shape
     N = weight.shape[0]
-    if (_lib.use_native(x, weight) and M <= 16 and K % 8 == 0 and x.stride(1) == 1 and x.stride(0) % 8 == 0
+    # measured on MI355X (profiles/gemv_bench_r1.jsonl): the skinny kernel wins for M <= 2 everywhere and
+    # up to M = 4 on small weights (hipBLASLt under-fills the chip there); MFMA GEMMs win beyond
+    small = N * K <= (64 << 20)
+    if (_lib.use_native(x, weight) and (M <= 2 or (M <= 4 and small)) and K % 8 == 0 and x.stride(1) == 1
+            and x.stride(0) % 8 == 0
             and weight.is_contiguous() and x.data_ptr() % 16 == 0 and weight.data_ptr() % 16 == 0
             and (bias is None or bias.dtype == torch.bfloat16)):
         if out is None:
