@@ -282,12 +282,18 @@ def main(argv=None):
     step = state["global_step"]
     start_epoch = step // steps_per_epoch
     micro = 0
+    fault_step = int(os.environ.get("KCA_FAULT_STEP", "-1"))
+    fault_ranks = {int(r) for r in os.environ.get("KCA_FAULT_RANKS", "0").split(",") if r.strip()}
     for epoch in range(start_epoch, args.epochs):
         idx = order(epoch)
         first = (step % steps_per_epoch) if epoch == start_epoch else 0
         for s in range(first, steps_per_epoch):
             if step >= total_steps:
                 break
+            if fault_step >= 0 and step == fault_step and rank in fault_ranks:
+                # fault injection: die hard mid-run, like a lost node
+                log.error(f"KCA_FAULT_STEP={fault_step}: rank {rank} exiting")
+                os._exit(17)
             base = s * per_step
             lr = lr_at(step, args.lr, total_steps, warmup, sched_kind)
             timer.start()

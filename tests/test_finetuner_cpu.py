@@ -151,3 +151,33 @@ def test_gpt2_small_124m_cpu_step(tmp_path):
                str(tmp_path / "l"), "--save-steps", "2", "--max-steps", "2", "--zero-stage", "3"])
     assert st["global_step"] == 2
     assert (tmp_path / "o" / "results-g" / "final" / ".ready.txt").exists()
+
+
+def test_fault_injection_and_deterministic_resume(tmp_path):
+    """kill the trainer at step 3 (KCA_FAULT_STEP), restart, and the
+    resumed run from checkpoint-2 must end bit-identical to an uninterrupted run."""
+    import subprocess
+    import sys
+    from safetensors.torch import load_file
+    model = make_model_dir(str(tmp_path / "model"))
+    data = make_tokens(str(tmp_path / "d.tokens"), n_ctx=24, ctx=32)
+
+    def args(out):
+        return ["--run-name", "f", "--model", model, "--dataset", data, "--context-size", "32", "--bs", "2",
+                "--gradients", "2", "--output-path", str(out), "--logs", str(out / "logs"), "--save-steps", "2",
+                "--zero-stage", "0", "--lr", "1e-3", "--max-steps", "5"]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "kubernetes_cloud_amd.train.finetuner"]
+    env = dict(os.environ, KCA_FAULT_STEP="3", PYTHONPATH=root)
+    r = subprocess.run(cmd + args(tmp_path / "a"), env=env, cwd=root, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 17, r.stderr[-2000:]
+    rd = tmp_path / "a" / "results-f"
+    assert (rd / "checkpoint-2").exists() and not (rd / "final").exists()
+    env.pop("KCA_FAULT_STEP")
+    r = subprocess.run(cmd + args(tmp_path / "a"), env=env, cwd=root, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    r = subprocess.run(cmd + args(tmp_path / "b"), env=env, cwd=root, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    a = load_file(str(rd / "final" / "model.safetensors"))
+    b = load_file(str(tmp_path / "b" / "results-f" / "final" / "model.safetensors"))
+    assert max(float((a[k].float() - b[k].float()).abs().max()) for k in a) == 0.0
