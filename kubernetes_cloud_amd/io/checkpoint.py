@@ -38,7 +38,8 @@ def find_last_checkpoint(output_dir: str) -> str | None:
     best = None
     for n in names:
         m = _CKPT.match(n)
-        if m and os.path.isdir(os.path.join(output_dir, n)):
+        if m and os.path.isdir(os.path.join(output_dir, n)) and \
+                not os.path.exists(os.path.join(output_dir, n, ".incomplete")):
             step = int(m.group(1))
             if best is None or step > best[0]:
                 best = (step, n)
@@ -100,6 +101,114 @@ def save_checkpoint(ckpt_dir: str, model, engine, trainer_state: dict, args_dict
                os.path.join(ckpt_dir, f"rng_state_{rank}.pth"))
     if barrier is not None:
         barrier()
+
+
+class _Snapshot:
+    """Host copy of a model/engine, reusing pinned buffers between saves."""
+
+    def __init__(self):
+        self.bufs: dict = {}
+
+    def take(self, name: str, t: torch.Tensor) -> torch.Tensor:
+        b = self.bufs.get(name)
+        if b is None or b.shape != t.shape or b.dtype != t.dtype:
+            b = torch.empty(t.shape, dtype=t.dtype, pin_memory=t.is_cuda)
+            self.bufs[name] = b
+        b.copy_(t.detach(), non_blocking=True)
+        return b
+
+
+class AsyncCheckpointWriter:
+    """checkpoint I/O off the training critical path.
+
+    ``save`` snapshots parameters, optimizer shard and RNG into reused pinned
+    host buffers (a D2H copy at ~50 GB/s, then one sync), and a background
+    thread serialises them to ``checkpoint-N/`` (safetensors + JSON) while
+    training continues; the next ``save`` (or ``wait``) joins the previous
+    writer first, so at most one snapshot is in flight."""
+
+    def __init__(self, rank: int = 0):
+        self._snap = _Snapshot()  # one set of pinned buffers: the previous writer is joined first
+        self._thread = None
+        self._err = None
+        self._pending = None
+        self.rank = rank
+
+    def wait(self, barrier=None):
+        """Join this rank's writer; with ``barrier`` (all ranks) mark the pending
+        checkpoint complete (rank 0 removes its ``.incomplete`` sentinel)."""
+        if self._thread is not None:
+            self._thread.join()
+            self._thread = None
+        if self._err is not None:
+            e, self._err = self._err, None
+            raise e
+        if self._pending is not None:
+            if barrier is not None:
+                barrier()
+            if self.rank == 0:
+                try:
+                    os.remove(os.path.join(self._pending, ".incomplete"))
+                except FileNotFoundError:
+                    pass
+            self._pending = None
+
+    def save(self, ckpt_dir: str, model, engine, trainer_state: dict, args_dict: dict | None = None,
+             tokenizer=None, rank: int = 0, world: int = 1, barrier=None):
+        import copy
+        import threading
+        self.rank = rank
+        self.wait(barrier)
+        snap = self._snap
+        params = {k: snap.take("p." + k, v) for k, v in model.state_dict().items()}
+        opt = None
+        if engine is not None:
+            st = engine.optimizer_state()
+            opt = ({k: snap.take("o." + k, st[k]) for k in ("master", "exp_avg", "exp_avg_sq")},
+                   {k: st[k] for k in ("world", "total", "step", "zero_stage", "lr")})
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        rng = _rng_state()
+        state = copy.deepcopy(trainer_state)
+        os.makedirs(os.path.join(ckpt_dir, "optimizer"), exist_ok=True)
+        if rank == 0:
+            open(os.path.join(ckpt_dir, ".incomplete"), "w").close()  # resume skips it until all ranks wrote
+            if tokenizer is not None:
+                tokenizer.save_pretrained(ckpt_dir)
+        self._pending = ckpt_dir
+
+        def write():
+            try:
+                _write_checkpoint(ckpt_dir, model.cfg, params, opt, state, args_dict, rng, rank)
+            except Exception as e:  # noqa: BLE001 -- surfaced on the next wait()/save()
+                self._err = e
+        self._thread = threading.Thread(target=write, name="ckpt-writer", daemon=False)
+        self._thread.start()
+
+
+def _write_checkpoint(ckpt_dir, cfg, params, opt, trainer_state, args_dict, rng, rank):
+    from safetensors.torch import save_file
+
+    from ..models.hf_convert import native_to_hf
+    if rank == 0:
+        hf = native_to_hf({k: v for k, v in params.items() if not k.endswith("alibi")}, cfg)
+        save_file({k: v.contiguous() for k, v in hf.items()}, os.path.join(ckpt_dir, "model.safetensors"),
+                  metadata={"format": "pt"})
+        with open(os.path.join(ckpt_dir, "config.json"), "w") as f:
+            json.dump(cfg.to_hf(), f, indent=2)
+        with open(os.path.join(ckpt_dir, "trainer_state.json"), "w") as f:
+            json.dump(trainer_state, f, indent=2, default=str)
+        if args_dict is not None:
+            with open(os.path.join(ckpt_dir, "training_args.json"), "w") as f:
+                json.dump(args_dict, f, indent=2, default=str)
+    if opt is not None:
+        tensors, meta = opt
+        save_file(tensors, os.path.join(ckpt_dir, "optimizer", f"rank-{rank:05d}.safetensors"))
+        if rank == 0:
+            with open(os.path.join(ckpt_dir, "optimizer", "meta.json"), "w") as f:
+                json.dump(meta, f)
+    torch.save({k: (torch.as_tensor(v) if not isinstance(v, torch.Tensor) else v) for k, v in rng.items()},
+               os.path.join(ckpt_dir, f"rng_state_{rank}.pth"))
 
 
 def load_checkpoint(ckpt_dir: str, model, engine, rank: int = 0) -> dict:

@@ -282,6 +282,8 @@ def main(argv=None):
     step = state["global_step"]
     start_epoch = step // steps_per_epoch
     micro = 0
+    from ..io.checkpoint import AsyncCheckpointWriter
+    ckpt_writer = AsyncCheckpointWriter(rank)
     fault_step = int(os.environ.get("KCA_FAULT_STEP", "-1"))
     fault_ranks = {int(r) for r in os.environ.get("KCA_FAULT_RANKS", "0").split(",") if r.strip()}
     for epoch in range(start_epoch, args.epochs):
@@ -325,13 +327,14 @@ def main(argv=None):
             state.update(global_step=step, epoch=epoch)
             if args.save_steps and step % args.save_steps == 0:
                 ck = os.path.join(output_dir, f"checkpoint-{step}")
-                save_checkpoint(ck, model, engine, state, {k: str(v) for k, v in vars(args).items()},
-                                tokenizer, rank, world, barrier)
+                ckpt_writer.save(ck, model, engine, state, {k: str(v) for k, v in vars(args).items()},
+                                 tokenizer, rank, world, barrier)
                 if main_proc:
                     log.info(f"saved {ck}")
         if step >= total_steps:
             break
 
+    ckpt_writer.wait(barrier)
     barrier()
     if main_proc:
         final = os.path.join(output_dir, "final")
