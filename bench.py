@@ -39,6 +39,9 @@ def main():
     ap.add_argument("--ckpt", action="store_true", help="activation checkpointing")
     ap.add_argument("--bucket", type=float, default=2e8)
     ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--tunableop", choices=["auto", "use", "tune", "off"], default="auto",
+                    help="hipBLASLt/rocBLAS solution selection via PyTorch TunableOp: 'tune' measures during "
+                         "warmup and writes tuning/tunableop_results.csv; 'auto' uses that file when present")
     args = ap.parse_args()
 
     import torch
@@ -56,6 +59,21 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
     _lib.require()
     torch.manual_seed(1234 + info.rank)
+
+    tfile = os.path.join(ROOT, "tuning", "tunableop_results.csv")
+    mode = args.tunableop
+    if mode == "auto":
+        mode = "use" if os.path.exists(tfile) else "off"
+    if mode != "off":
+        import torch.cuda.tunable as tunable
+        os.makedirs(os.path.dirname(tfile), exist_ok=True)
+        tunable.enable(True)
+        tunable.set_filename(tfile, insert_device_ordinal=False)
+        tunable.tuning_enable(mode == "tune")
+        if mode == "use":
+            tunable.read_file(tfile)
+        if mode == "tune":
+            tunable.set_max_tuning_duration(40)
 
     cfg = preset(args.model)
     model = build_model(cfg, device=dev, dtype=torch.bfloat16, seed=0)
@@ -78,6 +96,11 @@ def main():
 
     for i in range(args.warmup):
         loss = one_step()
+    if mode == "tune":
+        torch.cuda.synchronize()
+        tunable.tuning_enable(False)
+        if info.rank == 0:
+            tunable.write_file()
         if info.is_main:
             print(f"[bench] warmup {i} loss={loss.item():.4f} mem={torch.cuda.max_memory_allocated()/2**30:.1f}GiB",
                   file=sys.stderr, flush=True)
