@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--tunableop", choices=["auto", "use", "tune", "off"], default="auto",
                     help="hipBLASLt/rocBLAS solution selection via PyTorch TunableOp: 'tune' measures during "
                          "warmup and writes tuning/tunableop_results.csv; 'auto' uses that file when present")
+    ap.add_argument("--tunableop-file", default=os.path.join(ROOT, "tuning", "tunableop_results.csv"))
     args = ap.parse_args()
 
     import torch
@@ -60,7 +61,7 @@ def main():
     _lib.require()
     torch.manual_seed(1234 + info.rank)
 
-    tfile = os.path.join(ROOT, "tuning", "tunableop_results.csv")
+    tfile = args.tunableop_file
     mode = args.tunableop
     if mode == "auto":
         mode = "use" if os.path.exists(tfile) else "off"
