@@ -97,11 +97,9 @@ def main():
 
     for i in range(args.warmup):
         loss = one_step()
-    if mode == "tune":
+    if mode == "tune":  # results are written to the file at interpreter exit
         torch.cuda.synchronize()
         tunable.tuning_enable(False)
-        if info.rank == 0:
-            tunable.write_file()
         if info.is_main:
             print(f"[bench] warmup {i} loss={loss.item():.4f} mem={torch.cuda.max_memory_allocated()/2**30:.1f}GiB",
                   file=sys.stderr, flush=True)
