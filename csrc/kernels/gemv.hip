@@ -11,12 +11,83 @@
 // FT / DS-Inference decoders (SURVEY K1/K5 decode shapes).
 #include "common.h"
 
-template <int M, int R>
+struct LnArgs {
+  const bf16_t* r1;     // residual adds (nullable): h = x (+ r1) (+ r2)
+  const bf16_t* r2;
+  bf16_t* h_out;        // updated residual stream, written by workgroup 0 (nullable)
+  long long ldh;        // row stride of r1 / r2 / h_out
+  const bf16_t* gamma;  // [K]
+  const bf16_t* beta;   // [K] (nullable)
+  float eps;
+};
+
+// LayerNorm prologue: every workgroup normalises the M activation rows itself
+// (K*M*2 B of L2-resident reads, ~1 us) straight into the LDS tile the GEMM
+// consumes, so the decode step needs no separate LN launch nor the HBM round
+// trip of the normalised row. Statistics match ln_fwd_kernel (two-pass, fp32,
+// over the bf16-rounded residual sum).
+template <int M>
+__device__ __forceinline__ void ln_prologue(const bf16_t* __restrict__ x, long long ldx, const LnArgs& a,
+                                            bf16_t* xs, int K, int mv, float* red) {
+  const int tid = threadIdx.x;
+  for (int m = 0; m < M; ++m) {
+    bf16_t* row = xs + m * K;
+    if (m >= mv) {
+      for (int k = tid * 8; k < K; k += 256 * 8) *reinterpret_cast<uint4*>(row + k) = make_uint4(0u, 0u, 0u, 0u);
+      continue;
+    }
+    float s = 0.f;
+    for (int k = tid * 8; k < K; k += 256 * 8) {
+      float v[8], t[8];
+      load8(x + m * ldx + k, v);
+      if (a.r1) {
+        load8(a.r1 + m * a.ldh + k, t);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] += t[j];
+      }
+      if (a.r2) {
+        load8(a.r2 + m * a.ldh + k, t);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] += t[j];
+      }
+      store8(row + k, v);  // bf16-rounded residual sum
+      if (a.h_out && blockIdx.x == 0) store8(a.h_out + m * a.ldh + k, v);
+      load8(row + k, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[j];
+    }
+    const float mean = block_sum(s, red) / K;
+    float q = 0.f;
+    for (int k = tid * 8; k < K; k += 256 * 8) {
+      float v[8];
+      load8(row + k, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) q += (v[j] - mean) * (v[j] - mean);
+    }
+    const float rstd = rsqrtf(block_sum(q, red + 8) / K + a.eps);
+    for (int k = tid * 8; k < K; k += 256 * 8) {
+      float v[8], g[8], b[8];
+      load8(row + k, v);
+      load8(a.gamma + k, g);
+      if (a.beta) load8(a.beta + k, b);
+      else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) b[j] = 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (v[j] - mean) * rstd * g[j] + b[j];
+      store8(row + k, v);
+    }
+  }
+}
+
+template <int M, int R, bool LN>
 __global__ __launch_bounds__(256) void skinny_gemm_kernel(
     const bf16_t* __restrict__ x, long long ldx, const bf16_t* __restrict__ w,
     const bf16_t* __restrict__ bias, bf16_t* __restrict__ y, long long ldy, int N, int K,
-    int kc, int act, int mv) {
+    int kc, int act, int mv, LnArgs ln) {
   extern __shared__ __attribute__((aligned(16))) bf16_t xs[];  // [M][kc]
+  __shared__ float red[16];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int n0 = (blockIdx.x * 4 + wid) * R;
   float acc[R][M];
@@ -34,11 +105,15 @@ __global__ __launch_bounds__(256) void skinny_gemm_kernel(
   for (int k0 = 0; k0 < K; k0 += kc) {
     const int kn = min(kc, K - k0);
     __syncthreads();
-    for (int i = tid * 8; i < M * kn; i += 256 * 8) {
-      const int m = i / kn, kk = i % kn;
-      uint4 v = make_uint4(0u, 0u, 0u, 0u);  // rows >= mv (padding of M) stay zero
-      if (m < mv) v = *reinterpret_cast<const uint4*>(x + m * ldx + k0 + kk);
-      *reinterpret_cast<uint4*>(xs + m * kc + kk) = v;
+    if constexpr (LN) {
+      ln_prologue<M>(x, ldx, ln, xs, K, mv, red);  // kc == K: one chunk
+    } else {
+      for (int i = tid * 8; i < M * kn; i += 256 * 8) {
+        const int m = i / kn, kk = i % kn;
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);  // rows >= mv (padding of M) stay zero
+        if (m < mv) v = *reinterpret_cast<const uint4*>(x + m * ldx + k0 + kk);
+        *reinterpret_cast<uint4*>(xs + m * kc + kk) = v;
+      }
     }
     __syncthreads();
     // 4 K-steps of 512 elements per iteration: R*4 independent 16 B loads per lane
@@ -96,17 +171,18 @@ __global__ __launch_bounds__(256) void skinny_gemm_kernel(
   }
 }
 
-template <int M>
+template <int M, bool LN = false>
 static void launch_skinny(const bf16_t* x, long long ldx, const bf16_t* w, const bf16_t* bias,
-                          bf16_t* y, long long ldy, int mv, int N, int K, int act, hipStream_t s) {
+                          bf16_t* y, long long ldy, int mv, int N, int K, int act, hipStream_t s,
+                          const LnArgs& ln = LnArgs{}) {
   constexpr int R = (M <= 4) ? 4 : 2;
   int kc = (32768 / M) / 512 * 512;  // M*kc*2 B <= 64 KB of LDS
   if (kc < 512) kc = 512;
-  if (kc > K) kc = (K + 7) / 8 * 8;
+  if (kc > K || LN) kc = (K + 7) / 8 * 8;
   const int rows_per_block = 4 * R;
   const dim3 grid((N + rows_per_block - 1) / rows_per_block);
-  hipLaunchKernelGGL((skinny_gemm_kernel<M, R>), grid, dim3(256), (size_t)M * kc * sizeof(bf16_t), s,
-                     x, ldx, w, bias, y, ldy, N, K, kc, act, mv);
+  hipLaunchKernelGGL((skinny_gemm_kernel<M, R, LN>), grid, dim3(256), (size_t)M * kc * sizeof(bf16_t), s,
+                     x, ldx, w, bias, y, ldy, N, K, kc, act, mv, ln);
 }
 
 KCA_API int kca_skinny_gemm(const void* x, long long ldx, const void* w, const void* bias, void* y,
@@ -123,5 +199,29 @@ KCA_API int kca_skinny_gemm(const void* x, long long ldx, const void* w, const v
   else if (M <= 4) launch_skinny<4>(xp, ldx, wp, bp, yp, ldy, M, N, K, act, stream);
   else if (M <= 8) launch_skinny<8>(xp, ldx, wp, bp, yp, ldy, M, N, K, act, stream);
   else launch_skinny<16>(xp, ldx, wp, bp, yp, ldy, M, N, K, act, stream);
+  return 0;
+}
+
+// y = act(LayerNorm(x (+ r1) (+ r2)) . W^T + b); h_out (nullable) receives the
+// bf16 residual sum. Needs the whole normalised rows in LDS: M*K <= 32768.
+KCA_API int kca_ln_skinny_gemm(const void* x, long long ldx, const void* r1, const void* r2, void* h_out,
+                               long long ldh, const void* gamma, const void* beta, float eps, const void* w,
+                               const void* bias, void* y, long long ldy, int M, int N, int K, int act,
+                               hipStream_t stream) {
+  if (M < 1 || M > 8 || K % 8 || ldx % 8 || ldh % 8 || N < 1) return 1;
+  const int Mp = M == 1 ? 1 : M == 2 ? 2 : M <= 4 ? 4 : 8;
+  if ((long long)Mp * K > 32768) return 1;
+  if (((uintptr_t)x | (uintptr_t)w | (uintptr_t)r1 | (uintptr_t)r2 | (uintptr_t)h_out | (uintptr_t)gamma |
+       (uintptr_t)beta) & 15) return 2;
+  LnArgs a{(const bf16_t*)r1, (const bf16_t*)r2, (bf16_t*)h_out, ldh, (const bf16_t*)gamma,
+           (const bf16_t*)beta, eps};
+  const bf16_t* xp = (const bf16_t*)x;
+  const bf16_t* wp = (const bf16_t*)w;
+  const bf16_t* bp = (const bf16_t*)bias;
+  bf16_t* yp = (bf16_t*)y;
+  if (Mp == 1) launch_skinny<1, true>(xp, ldx, wp, bp, yp, ldy, M, N, K, act, stream, a);
+  else if (Mp == 2) launch_skinny<2, true>(xp, ldx, wp, bp, yp, ldy, M, N, K, act, stream, a);
+  else if (Mp == 4) launch_skinny<4, true>(xp, ldx, wp, bp, yp, ldy, M, N, K, act, stream, a);
+  else launch_skinny<8, true>(xp, ldx, wp, bp, yp, ldy, M, N, K, act, stream, a);
   return 0;
 }

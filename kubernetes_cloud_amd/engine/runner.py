@@ -27,7 +27,7 @@ import torch
 
 from .. import ops
 from ..ops import decode as dops
-from ..ops.gemv import skinny_linear
+from ..ops.gemv import ln_skinny_linear, skinny_linear
 
 
 def _next_pow2(n: int, lo: int = 1) -> int:
@@ -172,9 +172,9 @@ class ModelRunner:
             h = m.emb_ln(h)
         pending = ()
         for li, blk in enumerate(m.h):
-            x, h = blk.ln_1(h, residual=pending) if pending else (blk.ln_1(h), h)
+            # every LayerNorm (+ pending residual adds) runs as the prologue of the GEMM that consumes it
             at = blk.attn
-            qkv = self._lin(at.qkv, x)
+            qkv, h = self._ln_lin(blk.ln_1, h, pending, at.qkv)
             kc, vc = self.cache.k[li], self.cache.v[li]
             dops.decode_prep(qkv, self.H, self.Hkv, self.D, self.rot, cfg.rotary_interleaved, self.cos,
                              self.sin, pos, slots, kc, vc)
@@ -184,14 +184,27 @@ class ModelRunner:
                 o = dops.decode_attention(qkv, kc, vc, slots, kv_lens, self.H, max_kv, at.scale, at.alibi,
                                           out=obuf, ws=ws)
             a = self._lin(at.out, o)
+            mlp = blk.mlp
+            act = 1 if mlp.approx in ("tanh", True) else 2
             if cfg.parallel_residual:
-                x2 = x if blk.ln_2 is None else blk.ln_2(h)
-                pending = (a, self._mlp(blk.mlp, x2))
+                f, _ = self._ln_lin(blk.ln_1 if blk.ln_2 is None else blk.ln_2, h, (), mlp.fc_in, act)
+                pending = (a, self._lin(mlp.fc_out, f))
             else:
-                x2, h = blk.ln_2(h, residual=(a,))
-                pending = (self._mlp(blk.mlp, x2),)
-        y, _ = m.ln_f(h, residual=pending)
-        return self._head(y)
+                f, h = self._ln_lin(blk.ln_2, h, (a,), mlp.fc_in, act)
+                pending = (self._lin(mlp.fc_out, f),)
+        if m.lm_head is None:
+            return self._ln_lin(m.ln_f, h, pending, None, weight=m.wte.weight)[0]
+        return self._ln_lin(m.ln_f, h, pending, m.lm_head)[0]
+
+    def _ln_lin(self, ln, h, res, mod, act: int = 0, weight=None):
+        """LayerNorm(h + sum(res)) -> column-parallel / LM-head linear, fused (decode)."""
+        from ..parallel.tensor_parallel import ParallelLMHead, RowParallelLinear, gather_last_dim
+        assert not isinstance(mod, RowParallelLinear)
+        if isinstance(mod, ParallelLMHead):
+            y, h = ln_skinny_linear(h, ln.weight, ln.bias, ln.eps, mod.local_weight(), mod.bias, res, act)
+            return gather_last_dim(y, mod.group), h
+        return ln_skinny_linear(h, ln.weight, ln.bias, ln.eps, mod.weight if weight is None else weight,
+                                None if mod is None else mod.bias, res, act)
 
     # decode linears: skinny GEMM (W streamed once, bias/GELU fused) for <= 16 rows
     def _lin(self, mod, x, act: int = 0):
@@ -202,19 +215,6 @@ class ModelRunner:
         if isinstance(mod, ParallelLMHead):
             return gather_last_dim(skinny_linear(x, mod.local_weight(), mod.bias), mod.group)
         return skinny_linear(x, mod.weight, mod.bias, act)
-
-    def _mlp(self, mlp, x):
-        act = 1 if mlp.approx in ("tanh", True) else 2
-        from ..parallel.tensor_parallel import RowParallelLinear
-        if isinstance(mlp.fc_in, RowParallelLinear):  # never: fc_in is column-parallel
-            raise AssertionError
-        return self._lin(mlp.fc_out, self._lin(mlp.fc_in, x, act))
-
-    def _head(self, y):
-        m = self.model
-        if m.lm_head is None:
-            return skinny_linear(y, m.wte.weight)
-        return self._lin(m.lm_head, y)
 
     def _windowed_decode(self, qkv, kc, vc, slots, kv_lens, at):
         B = qkv.shape[0]

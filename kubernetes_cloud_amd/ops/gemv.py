@@ -47,4 +47,42 @@ def skinny_linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | No
     return y
 
 
-__all__ = ["skinny_linear", "ACT"]
+def _ln_ok(x, M, K, weight, residuals, gamma, beta, bias):
+    Mp = 1 if M == 1 else 2 if M == 2 else 4 if M <= 4 else 8
+    ts = [x, weight, gamma, *residuals] + ([beta] if beta is not None else [])
+    return (M <= 2 or (M <= 4 and weight.shape[0] * K <= (64 << 20))) and Mp * K <= 32768 and K % 8 == 0 \
+        and all(t.data_ptr() % 16 == 0 for t in ts) and x.stride(1) == 1 and x.stride(0) % 8 == 0 \
+        and all(r.is_contiguous() and r.shape == x.shape for r in residuals) and weight.is_contiguous() \
+        and gamma.is_contiguous() and (beta is None or beta.is_contiguous()) \
+        and (bias is None or bias.dtype == torch.bfloat16)
+
+
+def ln_skinny_linear(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor | None, eps: float,
+                     weight: torch.Tensor, bias: torch.Tensor | None = None, residuals=(), act: int = 0,
+                     want_h: bool = False):
+    """``act(LayerNorm(x + sum(residuals)) W^T + b)`` in one launch (decode).
+
+    Returns ``(y, h)`` with ``h`` the updated residual stream (``x`` itself when
+    no residuals are added). Falls back to the LN kernel + ``skinny_linear``
+    when the rows do not fit the LDS tile or the batch is too wide."""
+    M, K = x.shape
+    residuals = tuple(r for r in residuals if r is not None)
+    if _lib.use_native(x, weight) and _ln_ok(x, M, K, weight, residuals, gamma, beta, bias):
+        h = torch.empty(M, K, device=x.device, dtype=x.dtype) if residuals else x
+        y = torch.empty(M, weight.shape[0], device=x.device, dtype=x.dtype)
+        r1 = residuals[0] if residuals else None
+        r2 = residuals[1] if len(residuals) > 1 else None
+        _lib.call("kca_ln_skinny_gemm", x.data_ptr(), x.stride(0), _lib.ptr(r1), _lib.ptr(r2),
+                  h.data_ptr() if residuals else None, h.stride(0) if residuals else K, gamma.data_ptr(),
+                  _lib.ptr(beta), float(eps), weight.data_ptr(), _lib.ptr(bias), y.data_ptr(), y.stride(0),
+                  M, weight.shape[0], K, int(act), _lib.stream())
+        return y, h
+    from .norms import layer_norm
+    if residuals:
+        xn, h = layer_norm(x, gamma, beta, eps, residual=residuals)
+    else:
+        xn, h = layer_norm(x, gamma, beta, eps), x
+    return skinny_linear(xn, weight, bias, act), h
+
+
+__all__ = ["skinny_linear", "ln_skinny_linear", "ACT"]

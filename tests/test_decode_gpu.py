@@ -174,3 +174,28 @@ def test_skinny_gemm(M, N, K):
         y = skinny_linear(x, w, b, act)
         assert y.shape == (M, N)
         assert (y.float() - fn(ref)).abs().max() < 0.05, act
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 12288, 4096), (2, 16384, 4096), (4, 4096, 4096), (1, 5376, 14336),
+                                   (2, 7168, 14336), (3, 8192, 4096)])
+@pytest.mark.parametrize("nres", [0, 1, 2])
+def test_ln_skinny_gemm(M, N, K, nres):
+    from kubernetes_cloud_amd.ops import gemv
+    torch.manual_seed(M * 7 + N + K + nres)
+    x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    res = tuple(torch.randn(M, K, device=dev).to(torch.bfloat16) for _ in range(nres))
+    g = (1 + 0.1 * torch.randn(K, device=dev)).to(torch.bfloat16)
+    be = (0.1 * torch.randn(K, device=dev)).to(torch.bfloat16) if nres != 1 else None
+    w = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+    b = torch.randn(N, device=dev).to(torch.bfloat16)
+    assert gemv._ln_ok(x, M, K, w, res, g, be, b)  # the fused kernel, not the fallback, is under test
+    hs = x.float()
+    for r in res:
+        hs = hs + r.float()
+    h_ref = hs.to(torch.bfloat16)
+    xn = torch.nn.functional.layer_norm(h_ref.float(), (K,), g.float(), None if be is None else be.float(), 1e-5)
+    ref = xn.to(torch.bfloat16).float() @ w.float().t() + b.float()
+    y, h = gemv.ln_skinny_linear(x, g, be, 1e-5, w, b, res, act=1)
+    torch.cuda.synchronize()
+    assert torch.equal(h, h_ref)
+    assert (y.float() - torch.nn.functional.gelu(ref, approximate="tanh")).abs().max() < 0.06
