@@ -165,9 +165,11 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_kernel(AttnP
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int l32 = lane & 31, hh = lane >> 5;
-  const int nqb = gridDim.x;
-  const int qb = CAUSAL ? (nqb - 1 - (int)blockIdx.x) : (int)blockIdx.x;
-  const int bh = blockIdx.y;
+  const int nqb = (p.Sq + BM - 1) / BM;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int qi = lid % nqb;
+  const int qb = CAUSAL ? (nqb - 1 - qi) : qi;
+  const int bh = lid / nqb;
   const int b = bh / p.H, h = bh % p.H;
   const int hk = h / (p.H / p.Hkv);
   const int off = p.Sk - p.Sq;
@@ -359,7 +361,9 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_bwd_dkdv_kernel(
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int G = lane >> 4, gi = lane & 15;
-  const int kb = blockIdx.x, bh = blockIdx.y;
+  const int nkb = (p.Sk + BK - 1) / BK;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int kb = lid % nkb, bh = lid / nkb;
   const int b = bh / p.Hkv, hk = bh % p.Hkv;
   const int grp = p.H / p.Hkv;
   const int off = p.Sk - p.Sq;
@@ -511,9 +515,11 @@ __global__ void __launch_bounds__(256, (D <= 160 ? 2 : 1)) attn_bwd_dq_kernel(At
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int G = lane >> 4, gi = lane & 15;
-  const int nqb = gridDim.x;
-  const int qb = CAUSAL ? (nqb - 1 - (int)blockIdx.x) : (int)blockIdx.x;
-  const int bh = blockIdx.y;
+  const int nqb = (p.Sq + BQ - 1) / BQ;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int qi = lid % nqb;
+  const int qb = CAUSAL ? (nqb - 1 - qi) : qi;
+  const int bh = lid / nqb;
   const int b = bh / p.H, h = bh % p.H;
   const int hk = h / (p.H / p.Hkv);
   const int off = p.Sk - p.Sq;
@@ -678,7 +684,9 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv32_kernel(AttnBwdParams p
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int l32 = lane & 31, hh = lane >> 5;
-  const int kb = blockIdx.x, bh = blockIdx.y;
+  const int nkb = (p.Sk + BK - 1) / BK;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int kb = lid % nkb, bh = lid / nkb;
   const int b = bh / p.Hkv, hk = bh % p.Hkv;
   const int grp = p.H / p.Hkv;
   const int off = p.Sk - p.Sq;
@@ -823,9 +831,11 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq32_kernel(AttnBwdParams p) 
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int l32 = lane & 31, hh = lane >> 5;
-  const int nqb = gridDim.x;
-  const int qb = CAUSAL ? (nqb - 1 - (int)blockIdx.x) : (int)blockIdx.x;
-  const int bh = blockIdx.y;
+  const int nqb = (p.Sq + BQ - 1) / BQ;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int qi = lid % nqb;
+  const int qb = CAUSAL ? (nqb - 1 - qi) : qi;
+  const int bh = lid / nqb;
   const int b = bh / p.H, h = bh % p.H;
   const int hk = h / (p.H / p.Hkv);
   const int off = p.Sk - p.Sq;
@@ -974,7 +984,7 @@ KCA_API int kca_attn_fwd(const void* q, const void* k, const void* v, void* o,
   AttnParams p{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, lse,
                q_sb, q_st, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh, o_sb, o_st, o_sh,
                B, Sq, Sk, H, Hkv, d_real, causal, scale, alibi, kv_len};
-  dim3 grid((Sq + 127) / 128, B * H);
+  dim3 grid(((Sq + 127) / 128) * B * H);
   ATTN_D_DISPATCH(D, {
     if (causal)
       hipLaunchKernelGGL((attn_fwd_kernel<DD, true>), grid, dim3(256), 0, stream, p);
@@ -1024,9 +1034,9 @@ KCA_API int kca_attn_bwd(const void* q, const void* k, const void* v,
                   dv_sb, dv_st, dv_sh,
                   B, Sq, Sk, H, Hkv, d_real, causal, scale, alibi, kv_len};
   if (D == 256) {  // dQ on the 32-wide kernel (D=128 measured faster on the 16-wide pair: occupancy)
-    dim3 h1((Sk + 127) / 128, B * Hkv);
-    dim3 h2((Sq + 127) / 128, B * H);
-    dim3 g1w((Sk + 63) / 64, B * Hkv);
+    dim3 h1(((Sk + 127) / 128) * B * Hkv);
+    dim3 h2(((Sq + 127) / 128) * B * H);
+    dim3 g1w(((Sk + 63) / 64) * B * Hkv);
     if (D == 128) {
       if (causal) {
         hipLaunchKernelGGL((attn_bwd_dkdv32_kernel<128, true>), h1, dim3(256), 0, stream, p);
@@ -1048,8 +1058,8 @@ KCA_API int kca_attn_bwd(const void* q, const void* k, const void* v,
     }
     return 0;
   }
-  dim3 g1((Sk + 63) / 64, B * Hkv);
-  dim3 g2((Sq + 63) / 64, B * H);
+  dim3 g1(((Sk + 63) / 64) * B * Hkv);
+  dim3 g2(((Sq + 63) / 64) * B * H);
   ATTN_D_DISPATCH(D, {
     if (causal) {
       hipLaunchKernelGGL((attn_bwd_dkdv_kernel<DD, true>), g1, dim3(256), 0, stream, p);

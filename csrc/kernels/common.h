@@ -127,3 +127,15 @@ __device__ __forceinline__ float gelu_tanh_grad(float x) {
   float du = k0 * (1.f + 3.f * k1 * x2);
   return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * du;
 }
+
+// XCD-aware workgroup remap (cdna_hip_programming.md §5.5 T1). The dispatcher
+// hands linear workgroup id i to XCD i % 8, and each XCD has its own 4 MiB L2.
+// Kernels whose neighbouring logical tiles share operands (the q-blocks of one
+// attention head share its K/V) call this so that logical ids
+// [x*n/8, (x+1)*n/8) all run on XCD x: the shared stream is fetched into one
+// L2 instead of eight. Ids past the last multiple of 8 map to themselves.
+__device__ __forceinline__ int xcd_remap(int bid, int n) {
+  const int full = n & ~7;
+  if (bid >= full) return bid;
+  return (bid & 7) * (full >> 3) + (bid >> 3);
+}
