@@ -969,6 +969,15 @@ static int pick_d(int d) {
     default: return 2;                                             \
   }
 
+KCA_API int kca_attn_fwd_tiled(const void* q, const void* k, const void* v, void* o, float* lse,
+                               long long q_sb, long long q_st, long long q_sh, long long k_sb,
+                               long long k_st, long long k_sh, long long v_sb, long long v_st,
+                               long long v_sh, long long o_sb, long long o_st, long long o_sh,
+                               int B, int Sq, int Sk, int H, int Hkv, int d, int causal,
+                               float scale, hipStream_t stream);
+
+// path: 0 = auto (full-tile fast path of attention_tiled.hip when the shape
+// allows, else the generic kernel), 1 = generic kernel only.
 KCA_API int kca_attn_fwd(const void* q, const void* k, const void* v, void* o,
                          float* lse, long long q_sb, long long q_st,
                          long long q_sh, long long k_sb, long long k_st,
@@ -976,10 +985,13 @@ KCA_API int kca_attn_fwd(const void* q, const void* k, const void* v, void* o,
                          long long v_sh, long long o_sb, long long o_st,
                          long long o_sh, int B, int Sq, int Sk, int H, int Hkv,
                          int d_real, int causal, float scale,
-                         const float* alibi, const int* kv_len, int reserved,
+                         const float* alibi, const int* kv_len, int path,
                          hipStream_t stream) {
-  (void)reserved;
   if (d_real % 8 || H % Hkv) return 1;
+  if (path == 0 && !alibi && !kv_len &&
+      kca_attn_fwd_tiled(q, k, v, o, lse, q_sb, q_st, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh,
+                         o_sb, o_st, o_sh, B, Sq, Sk, H, Hkv, d_real, causal, scale, stream) == 0)
+    return 0;
   const int D = pick_d(d_real);
   AttnParams p{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, lse,
                q_sb, q_st, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh, o_sb, o_st, o_sh,

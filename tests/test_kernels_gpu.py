@@ -143,6 +143,33 @@ def test_attention_head_dims(D, causal):
     _attn_case(2, 200, 200, 4, 4, D, causal)
 
 
+@pytest.mark.parametrize("D", [128, 256])
+@pytest.mark.parametrize("causal", [True, False])
+def test_attention_tiled_fast_path(D, causal):
+    # Sq % 128 == 0, Sk % 32 == 0, no ALiBi / kv_len: attention_tiled.hip
+    _attn_case(2, 256, 256, 4, 4, D, causal)
+    _attn_case(1, 128, 384, 4, 2, D, causal)   # GQA, bottom-right causal offset 256
+
+
+@pytest.mark.parametrize("D", [128, 256])
+def test_attention_deferred_rescale_branch(D):
+    """Scores whose row max keeps growing tile after tile (ramped key norms and
+    a hot key per tile), so the deferred-rescale branch of the forward fires
+    repeatedly at data-dependent points (cdna_hip_programming.md §5.4 rule 26)."""
+    torch.manual_seed(3)
+    B, S, H = 1, 512, 2
+    q = torch.randn(B, S, H, D, device=DEV) * 0.5
+    ramp = torch.linspace(0.2, 6.0, S, device=DEV).view(1, S, 1, 1)
+    k = torch.randn(B, S, H, D, device=DEV) * ramp
+    k[:, ::37] += q.mean(1, keepdim=True) * 8.0
+    v = torch.randn(B, S, H, D, device=DEV)
+    q, k, v = (t.bfloat16() for t in (q, k, v))
+    for causal in (True, False):
+        o = ops.flash_attention(q, k, v, causal=causal)
+        orf, _ = ops.attention_reference(q.float(), k.float(), v.float(), causal)
+        assert _rel(o, orf) < 2e-2, (causal, _rel(o, orf))
+
+
 def test_attention_gqa_kvlen_alibi():
     _attn_case(2, 130, 130, 8, 2, 128, True, kv_len=[130, 97], alibi=True)
     _attn_case(3, 77, 77, 4, 4, 64, False, kv_len=[77, 10, 50])
