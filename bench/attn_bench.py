@@ -99,7 +99,11 @@ def main():
     ap.add_argument("--shapes", default=",".join(SHAPES))
     ap.add_argument("--no-sdpa", action="store_true")
     ap.add_argument("--fwd-only", action="store_true")
+    ap.add_argument("--generic", action="store_true", help="disable the full-tile fast kernels")
     a = ap.parse_args()
+    if a.generic:
+        from kubernetes_cloud_amd.ops.attention import set_tiled_path
+        set_tiled_path(False)
     for n in a.shapes.split(","):
         r = run(n, *SHAPES[n], sdpa=not a.no_sdpa, bwd=not a.fwd_only)
         print(json.dumps(r), flush=True)

@@ -969,6 +969,14 @@ static int pick_d(int d) {
     default: return 2;                                             \
   }
 
+// Process-wide switch for the full-tile fast paths (A/B measurement and
+// tests): 1 = use them where the shape allows (default), 0 = generic only.
+static int g_attn_tiled = 1;
+KCA_API int kca_attn_set_tiled(int enable) {
+  g_attn_tiled = enable;
+  return 0;
+}
+
 KCA_API int kca_attn_fwd_tiled(const void* q, const void* k, const void* v, void* o, float* lse,
                                long long q_sb, long long q_st, long long q_sh, long long k_sb,
                                long long k_st, long long k_sh, long long v_sb, long long v_st,
@@ -988,7 +996,7 @@ KCA_API int kca_attn_fwd(const void* q, const void* k, const void* v, void* o,
                          const float* alibi, const int* kv_len, int path,
                          hipStream_t stream) {
   if (d_real % 8 || H % Hkv) return 1;
-  if (path == 0 && !alibi && !kv_len &&
+  if (path == 0 && g_attn_tiled && !alibi && !kv_len &&
       kca_attn_fwd_tiled(q, k, v, o, lse, q_sb, q_st, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh,
                          o_sb, o_st, o_sh, B, Sq, Sk, H, Hkv, d_real, causal, scale, stream) == 0)
     return 0;
@@ -1024,6 +1032,16 @@ KCA_API int kca_attn_bwd_preprocess(const void* o, const void* dout,
   return 0;
 }
 
+KCA_API int kca_attn_bwd_tiled(const void* q, const void* k, const void* v, const void* dout,
+                               void* dq, void* dk, void* dv, const float* lse, const float* delta,
+                               long long q_sb, long long q_st, long long q_sh, long long k_sb,
+                               long long k_st, long long k_sh, long long v_sb, long long v_st,
+                               long long v_sh, long long do_sb, long long do_st, long long do_sh,
+                               long long dq_sb, long long dq_st, long long dq_sh, long long dk_sb,
+                               long long dk_st, long long dk_sh, long long dv_sb, long long dv_st,
+                               long long dv_sh, int B, int Sq, int Sk, int H, int Hkv, int d,
+                               int causal, float scale, hipStream_t stream);
+
 KCA_API int kca_attn_bwd(const void* q, const void* k, const void* v,
                          const void* o, const void* dout, void* dq, void* dk,
                          void* dv, const float* lse, const float* delta,
@@ -1038,6 +1056,12 @@ KCA_API int kca_attn_bwd(const void* q, const void* k, const void* v,
                          int causal, float scale, const float* alibi,
                          const int* kv_len, hipStream_t stream) {
   if (d_real % 8 || H % Hkv) return 1;
+  if (g_attn_tiled && !alibi && !kv_len &&
+      kca_attn_bwd_tiled(q, k, v, dout, dq, dk, dv, lse, delta, q_sb, q_st, q_sh, k_sb, k_st, k_sh,
+                         v_sb, v_st, v_sh, do_sb, do_st, do_sh, dq_sb, dq_st, dq_sh, dk_sb, dk_st,
+                         dk_sh, dv_sb, dv_st, dv_sh, B, Sq, Sk, H, Hkv, d_real, causal, scale,
+                         stream) == 0)
+    return 0;
   const int D = pick_d(d_real);
   AttnBwdParams p{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)o,
                   (const bf16_t*)dout, (bf16_t*)dq, (bf16_t*)dk, (bf16_t*)dv, lse, delta,

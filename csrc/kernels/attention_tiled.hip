@@ -161,8 +161,8 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel
     // of the MFMAs: without the fences the compiler merges the two `t + 1 <
     // ntiles` blocks and stores each load to LDS right after it (vmcnt(0)).
     asm volatile("" ::: "memory");
-    const bool active = !CAUSAL || (k0 <= q0 + 31 + off);
-    if (active) {
+    {  // causal tiles wholly above this wave's rows are masked, not skipped
+       // (a skip puts the O accumulators in a conditional region: spills)
       f32x16 sacc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
@@ -241,6 +241,299 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel
   }
 }
 
+
+// ====================================================================== backward
+// Same image and fragment conventions as the forward. Two kernels, no float
+// atomics, deterministic:
+//   dQ kernel  : wave = 32 queries; Q, dO fragments resident, dQ^T in AGPRs;
+//                sweeps 32-key K/V tiles (double-buffered images).
+//                S^T = K.Q^T, dP^T = V.dO^T (keys on registers, query on the
+//                lane), dS^T = P^T (dP^T - delta), dQ^T += K^T.dS^T with K^T
+//                from the K image by transposed reads.
+//   dK/dV kernel: wave = 32 keys; K fragments resident, the workgroup's V rows
+//                in one LDS image, dK^T / dV^T in AGPRs; sweeps 32-row Q/dO
+//                tiles (and the query heads of its KV head for GQA).
+//                S = Q.K^T, dP = dO.V^T (key on the lane), dV^T += dO^T.P,
+//                dK^T += Q^T.dS with dO^T, Q^T by transposed reads.
+struct FastBwdParams {
+  const bf16_t* q; const bf16_t* k; const bf16_t* v; const bf16_t* dout;
+  bf16_t* dq; bf16_t* dk; bf16_t* dv;
+  const float* lse; const float* delta;
+  long long q_sb, q_st, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh, do_sb, do_st, do_sh;
+  long long dq_sb, dq_st, dq_sh, dk_sb, dk_st, dk_sh, dv_sb, dv_st, dv_sh;
+  int B, Sq, Sk, H, Hkv;
+  float scale;
+};
+
+// A operand (32 rows x 16 k) read by rows from an image: lane (row l32, half hh)
+// takes chunk 2s+hh of its row. Returns the two per-lane bases (s even / odd).
+template <int D>
+__device__ __forceinline__ void row_bases(int l32, int hh, int& e, int& o) {
+  const int xr = (l32 >> 2) & 3;
+  e = (l32 >> 3) * 16 * D + 64 * (l32 & 7) + 16 * (hh ^ xr);
+  o = (l32 >> 3) * 16 * D + 64 * (l32 & 7) + 16 * ((2 + hh) ^ xr);
+}
+// transposed A operand (32 columns x 16 permuted rows) from an image
+template <int D>
+__device__ __forceinline__ void tr_bases(int lane, int& b1, int& b2) {
+  const int hh = lane >> 5, gi = lane & 15;
+  const int c3 = 2 * ((lane >> 4) & 1) + ((gi & 3) >> 1);
+  b1 = 64 * (4 * hh + (gi >> 2)) + 16 * (c3 ^ hh) + 8 * (gi & 1);
+  b2 = 16 * D + 64 * (4 * hh + (gi >> 2)) + 16 * (c3 ^ hh ^ 2) + 8 * (gi & 1);
+}
+template <int D>
+__device__ __forceinline__ bf16x8 tr_frag(const char* img, int b1, int b2, int s, int db) {
+  return cat8(lds_tr4(img, b1 + 2 * s * 16 * D + 512 * db), lds_tr4(img, b2 + 2 * s * 16 * D + 512 * db));
+}
+template <int D>
+__device__ __forceinline__ bf16x8 row_frag(const char* img, int be, int bo, int s) {
+  return lds_b128(img, ((s & 1) ? bo : be) + 512 * (s >> 1));
+}
+
+// store a D/32 x f32x16 transposed accumulator (row d, column = lane token) as
+// bf16 row `tok` of a [.., D] tensor, times `mul`
+template <int D>
+__device__ __forceinline__ void store_acc_t(bf16_t* rowp, const f32x16 (&acc)[D / 32], int hh, float mul) {
+#pragma unroll
+  for (int db = 0; db < D / 32; ++db) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      uint2 w;
+      w.x = pk_bf16(acc[db][4 * g] * mul, acc[db][4 * g + 1] * mul);
+      w.y = pk_bf16(acc[db][4 * g + 2] * mul, acc[db][4 * g + 3] * mul);
+      *reinterpret_cast<uint2*>(rowp + db * 32 + 8 * g + 4 * hh) = w;
+    }
+  }
+}
+
+template <int D, bool CAUSAL>
+__global__ void __launch_bounds__(256, 1) attn_bwd_dq_tiled_kernel(FastBwdParams p) {
+  constexpr int BM = 128, BN = 32;
+  constexpr int TILE = BN * D * 2;
+  constexpr int NCH = D / 8, CPT = BN * NCH / 256, RPI = 256 / NCH;
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int nqb = p.Sq / BM;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int qi = lid % nqb;
+  const int qb = CAUSAL ? (nqb - 1 - qi) : qi;
+  const int bh = lid / nqb;
+  const int b = bh / p.H, h = bh % p.H;
+  const int hk = h / (p.H / p.Hkv);
+  const int off = p.Sk - p.Sq;
+  const int q0 = qb * BM + wave * 32;
+  const int qrow = q0 + l32;
+  int kv_hi = p.Sk;
+  if (CAUSAL) kv_hi = min(kv_hi, qb * BM + BM + off);
+  const int ntiles = (kv_hi + BN - 1) / BN;
+  const float sl2 = p.scale * kLog2e;
+
+  const bf16_t* qp = p.q + b * p.q_sb + h * p.q_sh + (long long)qrow * p.q_st;
+  const bf16_t* gp = p.dout + b * p.do_sb + h * p.do_sh + (long long)qrow * p.do_st;
+  bf16x8 qf[D / 16], gf[D / 16];
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    qf[s] = *reinterpret_cast<const bf16x8*>(qp + 16 * s + 8 * hh);
+    gf[s] = *reinterpret_cast<const bf16x8*>(gp + 16 * s + 8 * hh);
+  }
+  const long long li = ((long long)b * p.H + h) * p.Sq + qrow;
+  const float nlse = -p.lse[li] * kLog2e;
+  const float dl = p.delta[li];
+  f32x16 dq[D / 32];
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dq[i][r] = 0.f;
+
+  const int st_row = tid / NCH, st_ch = tid % NCH;
+  const bf16_t* kst = p.k + b * p.k_sb + hk * p.k_sh + (long long)st_row * p.k_st + st_ch * 8;
+  const bf16_t* vst = p.v + b * p.v_sb + hk * p.v_sh + (long long)st_row * p.v_st + st_ch * 8;
+  u32x4 sk[CPT], sv[CPT];
+  int be, bo, b1, b2;
+  row_bases<D>(l32, hh, be, bo);
+  tr_bases<D>(lane, b1, b2);
+
+  stage_load<CPT, RPI>(sk, sv, kst, vst, 0, p.k_st, p.v_st);
+  stage_store<CPT, RPI, D>(sk, sv, smem, st_row, st_ch);
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const int k0 = t * BN;
+    const char* Ks = smem + (t & 1) * 2 * TILE;
+    const char* Vs = Ks + TILE;
+    stage_load<CPT, RPI>(sk, sv, kst, vst, min(k0 + BN, (ntiles - 1) * BN), p.k_st, p.v_st);
+    asm volatile("" ::: "memory");
+    {  // tiles wholly above this wave's rows (causal) are masked, not skipped:
+       // see the dK/dV kernel
+      f32x16 st, dpt;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { st[r] = 0.f; dpt[r] = 0.f; }
+#pragma unroll
+      for (int s = 0; s < D / 16; ++s) {
+        st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(Ks, be, bo, s), qf[s], st, 0, 0, 0);
+        dpt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(Vs, be, bo, s), gf[s], dpt, 0, 0, 0);
+      }
+      const bool diag = CAUSAL && (k0 + 31 > q0 + off);
+      bf16x8 d0, d1;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        float p0 = __builtin_amdgcn_exp2f(fmaf(st[r], sl2, nlse));
+        float p1 = __builtin_amdgcn_exp2f(fmaf(st[r + 8], sl2, nlse));
+        if (diag) {
+          const int key0 = k0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          if (key0 > qrow + off) p0 = 0.f;
+          if (key0 + 16 > qrow + off) p1 = 0.f;
+        }
+        d0[r] = (__bf16)(p0 * (dpt[r] - dl));
+        d1[r] = (__bf16)(p1 * (dpt[r + 8] - dl));
+      }
+#pragma unroll
+      for (int db = 0; db < D / 32; ++db) {
+        dq[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(Ks, b1, b2, 0, db), d0, dq[db], 0, 0, 0);
+        dq[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(Ks, b1, b2, 1, db), d1, dq[db], 0, 0, 0);
+      }
+    }
+    asm volatile("" ::: "memory");
+    if (t + 1 < ntiles) stage_store<CPT, RPI, D>(sk, sv, smem + ((t + 1) & 1) * 2 * TILE, st_row, st_ch);
+    __syncthreads();
+  }
+  store_acc_t<D>(p.dq + b * p.dq_sb + h * p.dq_sh + (long long)qrow * p.dq_st, dq, hh, p.scale);
+}
+
+template <int D, bool CAUSAL>
+__global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_tiled_kernel(FastBwdParams p) {
+  constexpr int BK = 128, BQ = 32;
+  constexpr int TILE = BQ * D * 2;                  // one 32-row image
+  constexpr int NCH = D / 8, CPT = BQ * NCH / 256, RPI = 256 / NCH;
+  constexpr int VOFF = 4 * TILE;                    // V images of the 4 waves
+  constexpr int LOFF = VOFF + 4 * TILE;             // lse/delta: [buf][64] floats
+  __shared__ __attribute__((aligned(16))) char smem[LOFF + 2 * 64 * 4];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int nkb = p.Sk / BK;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int kb = lid % nkb, bh = lid / nkb;
+  const int b = bh / p.Hkv, hk = bh % p.Hkv;
+  const int grp = p.H / p.Hkv;
+  const int off = p.Sk - p.Sq;
+  const int kw = kb * BK + wave * 32;
+  const int key = kw + l32;
+  const float sl2 = p.scale * kLog2e;
+
+  const bf16_t* kp = p.k + b * p.k_sb + hk * p.k_sh;
+  const bf16_t* vp = p.v + b * p.v_sb + hk * p.v_sh;
+  bf16x8 kf[D / 16];
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s)
+    kf[s] = *reinterpret_cast<const bf16x8*>(kp + (long long)key * p.k_st + 16 * s + 8 * hh);
+  // this wave's 32 V rows -> its own image (read back by rows for dP)
+  char* vimg = smem + VOFF + wave * TILE;
+#pragma unroll
+  for (int i = 0; i < 32 * NCH / 64; ++i) {
+    const int idx = lane + 64 * i, row = idx / NCH, ch = idx % NCH;
+    *reinterpret_cast<u32x4*>(vimg + img_off<D>(row, ch)) =
+        *reinterpret_cast<const u32x4*>(vp + (long long)(kw + row) * p.v_st + ch * 8);
+  }
+  f32x16 dk[D / 32], dv[D / 32];
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { dk[i][r] = 0.f; dv[i][r] = 0.f; }
+
+  int q_lo = 0;
+  if (CAUSAL) q_lo = max(0, kb * BK - off) & ~(BQ - 1);
+  const int nqt = (p.Sq - q_lo) / BQ;
+  const int total = nqt * grp;
+
+  const int st_row = tid / NCH, st_ch = tid % NCH;
+  const long long q_row_off = (long long)st_row * p.q_st + st_ch * 8;
+  const long long g_row_off = (long long)st_row * p.do_st + st_ch * 8;
+  u32x4 sq[CPT], sg[CPT];
+  float lreg = 0.f;
+  int be, bo, b1, b2;
+  row_bases<D>(l32, hh, be, bo);
+  tr_bases<D>(lane, b1, b2);
+
+#define KCA_DKDV_LOAD(it_)                                                                     \
+  {                                                                                            \
+    const int hq_ = hk * grp + (it_) / nqt, qt_ = q_lo + ((it_) % nqt) * BQ;                   \
+    stage_load<CPT, RPI>(sq, sg, p.q + b * p.q_sb + hq_ * p.q_sh + q_row_off,                  \
+                         p.dout + b * p.do_sb + hq_ * p.do_sh + g_row_off, qt_, p.q_st, p.do_st); \
+    if (tid < 64) {                                                                            \
+      const long long li_ = ((long long)b * p.H + hq_) * p.Sq + qt_ + (tid & 31);              \
+      lreg = tid < 32 ? p.lse[li_] * kLog2e : p.delta[li_];                                    \
+    }                                                                                          \
+  }
+#define KCA_DKDV_STORE(buf_)                                                                   \
+  {                                                                                            \
+    stage_store<CPT, RPI, D>(sq, sg, smem + (buf_) * 2 * TILE, st_row, st_ch);                 \
+    if (tid < 64) reinterpret_cast<float*>(smem + LOFF)[(buf_) * 64 + tid] = lreg;             \
+  }
+
+  if (total > 0) {
+    KCA_DKDV_LOAD(0);
+    KCA_DKDV_STORE(0);
+  }
+  __syncthreads();
+  for (int it = 0; it < total; ++it) {
+    const int qt = q_lo + (it % nqt) * BQ;
+    const char* Qs = smem + (it & 1) * 2 * TILE;
+    const char* Gs = Qs + TILE;
+    const float* ls = reinterpret_cast<const float*>(smem + LOFF) + (it & 1) * 64;
+    const int nx = min(it + 1, total - 1);
+    KCA_DKDV_LOAD(nx);
+    asm volatile("" ::: "memory");
+    // No skip of the (at most 3 per head) q tiles that lie wholly above this
+    // wave's keys: they are masked to P = 0 like the diagonal, which costs
+    // ~4 % extra MFMAs under a causal mask but keeps the 256 dK/dV accumulator
+    // registers out of a conditional region (the skip made hipcc spill).
+    {
+      f32x16 sacc, dpacc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { sacc[r] = 0.f; dpacc[r] = 0.f; }
+#pragma unroll
+      for (int s = 0; s < D / 16; ++s) {
+        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(Qs, be, bo, s), kf[s], sacc, 0, 0, 0);
+        dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(Gs, be, bo, s),
+                                                        row_frag<D>(vimg, be, bo, s), dpacc, 0, 0, 0);
+      }
+      // rows q = qt + 8g + 4hh + j (g = r>>2, j = r&3): lse / delta as float4
+      const bool diag = CAUSAL && (kw + 31 > qt + off);
+      bf16x8 p0, p1, s0, s1;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 lq = *reinterpret_cast<const f32x4*>(ls + 8 * g + 4 * hh);
+        const f32x4 dq4 = *reinterpret_cast<const f32x4*>(ls + 32 + 8 * g + 4 * hh);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = 4 * g + j;
+          float pr = __builtin_amdgcn_exp2f(fmaf(sacc[r], sl2, -lq[j]));
+          if (diag && key > qt + 8 * g + 4 * hh + j + off) pr = 0.f;
+          const float ds = pr * (dpacc[r] - dq4[j]);
+          if (r < 8) { p0[r] = (__bf16)pr; s0[r] = (__bf16)ds; }
+          else { p1[r - 8] = (__bf16)pr; s1[r - 8] = (__bf16)ds; }
+        }
+      }
+#pragma unroll
+      for (int db = 0; db < D / 32; ++db) {
+        dv[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(Gs, b1, b2, 0, db), p0, dv[db], 0, 0, 0);
+        dv[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(Gs, b1, b2, 1, db), p1, dv[db], 0, 0, 0);
+        dk[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(Qs, b1, b2, 0, db), s0, dk[db], 0, 0, 0);
+        dk[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(Qs, b1, b2, 1, db), s1, dk[db], 0, 0, 0);
+      }
+    }
+    asm volatile("" ::: "memory");
+    if (it + 1 < total) KCA_DKDV_STORE((it + 1) & 1);
+    __syncthreads();
+  }
+#undef KCA_DKDV_LOAD
+#undef KCA_DKDV_STORE
+  store_acc_t<D>(p.dk + b * p.dk_sb + hk * p.dk_sh + (long long)key * p.dk_st, dk, hh, p.scale);
+  store_acc_t<D>(p.dv + b * p.dv_sb + hk * p.dv_sh + (long long)key * p.dv_st, dv, hh, 1.f);
+}
+
 }  // namespace
 
 // Returns 0 when launched, 1 when the shape is outside the fast path (the
@@ -263,6 +556,43 @@ KCA_API int kca_attn_fwd_tiled(const void* q, const void* k, const void* v, void
   } else {
     if (causal) hipLaunchKernelGGL((attn_fwd_tiled_kernel<128, true>), grid, dim3(256), 0, stream, p);
     else hipLaunchKernelGGL((attn_fwd_tiled_kernel<128, false>), grid, dim3(256), 0, stream, p);
+  }
+  return 0;
+}
+
+KCA_API int kca_attn_bwd_tiled(const void* q, const void* k, const void* v, const void* dout,
+                               void* dq, void* dk, void* dv, const float* lse, const float* delta,
+                               long long q_sb, long long q_st, long long q_sh, long long k_sb,
+                               long long k_st, long long k_sh, long long v_sb, long long v_st,
+                               long long v_sh, long long do_sb, long long do_st, long long do_sh,
+                               long long dq_sb, long long dq_st, long long dq_sh, long long dk_sb,
+                               long long dk_st, long long dk_sh, long long dv_sb, long long dv_st,
+                               long long dv_sh, int B, int Sq, int Sk, int H, int Hkv, int d,
+                               int causal, float scale, hipStream_t stream) {
+  if ((d != 128 && d != 256) || Sq % 128 || Sk % 128 || Sq <= 0 || H % Hkv) return 1;
+  if (causal && Sk < Sq) return 1;
+  FastBwdParams p{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout,
+                  (bf16_t*)dq, (bf16_t*)dk, (bf16_t*)dv, lse, delta,
+                  q_sb, q_st, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh, do_sb, do_st, do_sh,
+                  dq_sb, dq_st, dq_sh, dk_sb, dk_st, dk_sh, dv_sb, dv_st, dv_sh,
+                  B, Sq, Sk, H, Hkv, scale};
+  dim3 g1((Sk / 128) * B * Hkv), g2((Sq / 128) * B * H);
+  if (d == 256) {
+    if (causal) {
+      hipLaunchKernelGGL((attn_bwd_dkdv_tiled_kernel<256, true>), g1, dim3(256), 0, stream, p);
+      hipLaunchKernelGGL((attn_bwd_dq_tiled_kernel<256, true>), g2, dim3(256), 0, stream, p);
+    } else {
+      hipLaunchKernelGGL((attn_bwd_dkdv_tiled_kernel<256, false>), g1, dim3(256), 0, stream, p);
+      hipLaunchKernelGGL((attn_bwd_dq_tiled_kernel<256, false>), g2, dim3(256), 0, stream, p);
+    }
+  } else {
+    if (causal) {
+      hipLaunchKernelGGL((attn_bwd_dkdv_tiled_kernel<128, true>), g1, dim3(256), 0, stream, p);
+      hipLaunchKernelGGL((attn_bwd_dq_tiled_kernel<128, true>), g2, dim3(256), 0, stream, p);
+    } else {
+      hipLaunchKernelGGL((attn_bwd_dkdv_tiled_kernel<128, false>), g1, dim3(256), 0, stream, p);
+      hipLaunchKernelGGL((attn_bwd_dq_tiled_kernel<128, false>), g2, dim3(256), 0, stream, p);
+    }
   }
   return 0;
 }

@@ -51,6 +51,14 @@ def attention_reference(q, k, v, causal: bool, scale: float | None = None,
     return o.to(q.dtype), lse
 
 
+def set_tiled_path(enable: bool) -> None:
+    """Toggle the full-tile fast kernels (csrc/kernels/attention_tiled.hip) used
+    for head_dim 128/256 when Sq % 128 == 0 and Sk % 32 (fwd) / 128 (bwd) == 0
+    and there is no ALiBi / key-length mask. On by default; off forces the
+    generic kernels (A/B measurement, tests)."""
+    _lib.call("kca_attn_set_tiled", int(bool(enable)))
+
+
 def _strides(t):
     return t.stride(0), t.stride(1), t.stride(2)
 

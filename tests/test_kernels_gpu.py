@@ -149,6 +149,29 @@ def test_attention_tiled_fast_path(D, causal):
     # Sq % 128 == 0, Sk % 32 == 0, no ALiBi / kv_len: attention_tiled.hip
     _attn_case(2, 256, 256, 4, 4, D, causal)
     _attn_case(1, 128, 384, 4, 2, D, causal)   # GQA, bottom-right causal offset 256
+    _attn_case(1, 256, 288, 2, 2, D, causal, check_bwd=False)  # fwd tiled, bwd generic (Sk % 128)
+
+
+@pytest.mark.parametrize("D", [128, 256])
+def test_attention_tiled_matches_generic(D):
+    """Fast and generic kernels agree (fwd output and all three grads)."""
+    from kubernetes_cloud_amd.ops.attention import set_tiled_path
+    torch.manual_seed(5)
+    B, S, H = 2, 384, 2
+    q, k, v = (torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16) for _ in range(3))
+    g = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16)
+    outs = []
+    for tiled in (True, False):
+        set_tiled_path(tiled)
+        try:
+            qq, kk, vv = (t.clone().requires_grad_() for t in (q, k, v))
+            o = ops.flash_attention(qq, kk, vv, causal=True)
+            o.backward(g)
+            outs.append((o.float(), qq.grad.float(), kk.grad.float(), vv.grad.float()))
+        finally:
+            set_tiled_path(True)
+    for a, b in zip(*outs):
+        assert _rel(a, b) < 1e-2, _rel(a, b)
 
 
 @pytest.mark.parametrize("D", [128, 256])
