@@ -47,6 +47,7 @@ _SIGS = {
     "kca_cross_entropy_bwd": [P, LL, P, P, P, F, I, I, I, P, LL, P],
     "kca_adamw": [P, P, P, P, P, LL, P, F, F, F, F, F, F, F, P, P, P],
     "kca_sumsq": [P, LL, P, P, P],
+    "kca_adamw8bit": [P, P, P, P, P, P, P, LL, P, F, F, F, F, F, F, F, P, P, P],
     "kca_clip_coef": [P, F, F, P, P, P, P],
     "kca_attn_fwd": [P] * 5 + [LL] * 12 + [I] * 7 + [F, P, P, I, P],
     "kca_attn_bwd_preprocess": [P, P, P, LL, LL, LL, LL, LL, LL, I, I, I, I, P],
@@ -106,12 +107,24 @@ def has(name: str) -> bool:
     return lib is not None and hasattr(lib, name)
 
 
+# KCA_SYNC_LAUNCH=1: synchronise after every native launch so an asynchronous
+# GPU fault (out-of-bounds access, illegal instruction) is reported at the op
+# that caused it, by name -- the HIP_LAUNCH_BLOCKING-style debug mode of
+# SURVEY §5.2. Off by default (it serialises the stream).
+SYNC_LAUNCH = os.environ.get("KCA_SYNC_LAUNCH", "0") in ("1", "true")
+
+
 def call(name: str, *args):
     lib = require()
     fn = getattr(lib, name)
     rc = fn(*args)
     if rc != 0:
         raise RuntimeError(f"{name} returned status {rc} (unsupported shape/arguments)")
+    if SYNC_LAUNCH and torch.cuda.is_available():
+        try:
+            torch.cuda.synchronize()
+        except RuntimeError as e:  # pragma: no cover - needs a faulting kernel
+            raise RuntimeError(f"GPU fault after native launch {name}: {e}") from e
     return rc
 
 

@@ -41,7 +41,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..ops import _lib
-from .optim import FlatAdamW
+from .optim import FlatAdamW, FlatAdamW8bit
 
 ALIGN = 64
 
@@ -82,8 +82,9 @@ class TrainEngine:
     def __init__(self, model: nn.Module, lr: float = 5e-5, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 0.0, max_grad_norm: float = 1.0, zero_stage: int = 0,
                  grad_accum: int = 1, bucket_elems: int = int(2e8), group=None,
-                 comm_dtype: torch.dtype = torch.float32, loss_scaler=None):
+                 comm_dtype: torch.dtype = torch.float32, loss_scaler=None, optim_bits: int = 32):
         self.model = model
+        opt_cls = FlatAdamW8bit if optim_bits == 8 else FlatAdamW
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
@@ -157,12 +158,12 @@ class TrainEngine:
                 master[so:so + piece].copy_(self.flat[lo:lo + piece].float())
                 mask[so // ALIGN:(so + piece) // ALIGN] = full_mask[lo // ALIGN:(lo + piece) // ALIGN]
                 so += piece
-            self.opt = FlatAdamW(master, lr, betas, eps, weight_decay, mask.to(dev),
-                                 model_bf16=self.shard_bf16, grad=self.shard_grad)
+            self.opt = opt_cls(master, lr, betas, eps, weight_decay, mask.to(dev),
+                               model_bf16=self.shard_bf16, grad=self.shard_grad)
         else:
             master = self.flat.float()
-            self.opt = FlatAdamW(master, lr, betas, eps, weight_decay, full_mask.to(dev),
-                                 model_bf16=self.flat, grad=self.grad)
+            self.opt = opt_cls(master, lr, betas, eps, weight_decay, full_mask.to(dev),
+                               model_bf16=self.flat, grad=self.grad)
 
         # ---- hooks
         self._micro = 0

@@ -286,6 +286,12 @@ def main(argv=None):
     ckpt_writer = AsyncCheckpointWriter(rank)
     fault_step = int(os.environ.get("KCA_FAULT_STEP", "-1"))
     fault_ranks = {int(r) for r in os.environ.get("KCA_FAULT_RANKS", "0").split(",") if r.strip()}
+    hang_step = int(os.environ.get("KCA_FAULT_HANG_STEP", "-1"))
+    from ..obs.trace import trace_range
+    from ..utils.watchdog import StepWatchdog
+    watchdog = StepWatchdog.from_env(rank, report_dir=output_dir)
+    if watchdog is not None:
+        watchdog.start()
     for epoch in range(start_epoch, args.epochs):
         idx = order(epoch)
         first = (step % steps_per_epoch) if epoch == start_epoch else 0
@@ -296,6 +302,12 @@ def main(argv=None):
                 # fault injection: die hard mid-run, like a lost node
                 log.error(f"KCA_FAULT_STEP={fault_step}: rank {rank} exiting")
                 os._exit(17)
+            if hang_step >= 0 and step == hang_step and rank in fault_ranks:
+                # hang injection: a rank that stops making progress (stuck
+                # collective / wedged device) -- the watchdog must catch it
+                log.error(f"KCA_FAULT_HANG_STEP={hang_step}: rank {rank} hanging")
+                while True:
+                    time.sleep(1.0)
             base = s * per_step
             lr = lr_at(step, args.lr, total_steps, warmup, sched_kind)
             timer.start()
@@ -306,16 +318,21 @@ def main(argv=None):
                 ids = batch["input_ids"].to(dev, non_blocking=True)
                 mask = batch["attention_mask"].to(dev, non_blocking=True)
                 labels = batch["labels"].to(dev, non_blocking=True)
-                loss = model(ids, attention_mask=mask, labels=labels)
-                engine.backward(loss)
+                with trace_range("forward"):
+                    loss = model(ids, attention_mask=mask, labels=labels)
+                with trace_range("backward"):
+                    engine.backward(loss)
                 d = loss.detach().float()
                 loss_acc = d if loss_acc is None else loss_acc + d
                 micro += 1
                 if micro % (2 * gas) == 0 and main_proc:
                     print(f"\nLOSS: {d.item():.3f} {MemoryUsage.now()}", file=sys.stderr, flush=True)
             timer.gas_done()
-            engine.step(lr)
+            with trace_range("optimizer"):
+                engine.step(lr)
             step += 1
+            if watchdog is not None:
+                watchdog.beat(step)
             perf = timer.stop(bs * gas, world, args.context_size, flops_tok)
             rec = {"loss": (loss_acc / gas).item(), "learning_rate": lr, "epoch": epoch, **perf}
             if step % 10 == 0 or step == 1:
@@ -336,6 +353,8 @@ def main(argv=None):
 
     ckpt_writer.wait(barrier)
     barrier()
+    if watchdog is not None:
+        watchdog.stop()
     if main_proc:
         final = os.path.join(output_dir, "final")
         save_pretrained(model, final)

@@ -127,6 +127,102 @@ class FlatAdamW:
         self.lr = sd.get("lr", self.lr)
 
 
+class FlatAdamW8bit(FlatAdamW):
+    """Block-wise 8-bit AdamW (csrc/kernels/adamw8bit.hip): the bitsandbytes
+    AdamW8bit that ``--use_8bit_adam`` selects in the reference SD trainer
+    (sd-finetuner-workflow/sd-finetuner/finetuner.py:669-678).
+
+    exp_avg -> int8 codes + fp32 absmax per 2048-element block, exp_avg_sq ->
+    uint8 codes + absmax, companded (m = a*sign*(|c|/127)^2, v = a*(c/255)^4)
+    so small moments keep their precision: 2 B/param of state instead of 8.
+    Master params stay fp32. The CPU path implements the same math in torch.
+    """
+
+    BLOCK = 2048
+
+    def __init__(self, master: torch.Tensor, *args, **kw):
+        super().__init__(master, *args, **kw)
+        n = master.numel()
+        nb = (n + self.BLOCK - 1) // self.BLOCK
+        dev = master.device
+        del self.exp_avg, self.exp_avg_sq
+        self.m_codes = torch.zeros(n, device=dev, dtype=torch.int8)
+        self.v_codes = torch.zeros(n, device=dev, dtype=torch.uint8)
+        self.m_absmax = torch.zeros(nb, device=dev, dtype=torch.float32)
+        self.v_absmax = torch.zeros(nb, device=dev, dtype=torch.float32)
+
+    # -- (de)quantisation, torch reference -------------------------------------
+    def _blocks(self, x):
+        n = x.numel()
+        pad = (-n) % self.BLOCK
+        return torch.nn.functional.pad(x, (0, pad)).view(-1, self.BLOCK), n
+
+    def dequant(self):
+        mb, n = self._blocks(self.m_codes.float())
+        vb, _ = self._blocks(self.v_codes.float())
+        m = torch.sign(mb) * (mb.abs() / 127.0) ** 2 * self.m_absmax[:, None]
+        v = (vb / 255.0) ** 4 * self.v_absmax[:, None]
+        return m.reshape(-1)[:n], v.reshape(-1)[:n]
+
+    def _quant(self, m, v):
+        mb, n = self._blocks(m)
+        vb, _ = self._blocks(v.clamp_min(0))
+        am = mb.abs().amax(1)
+        av = vb.amax(1)
+        im = torch.where(am > 0, 1.0 / am, torch.zeros_like(am))[:, None]
+        iv = torch.where(av > 0, 1.0 / av, torch.zeros_like(av))[:, None]
+        mc = torch.round(127.0 * (mb.abs() * im).clamp(max=1).sqrt()) * torch.sign(mb)
+        vc = torch.round(255.0 * (vb * iv).clamp(max=1).sqrt().sqrt())
+        self.m_codes.copy_(mc.reshape(-1)[:n].to(torch.int8))
+        self.v_codes.copy_(vc.reshape(-1)[:n].to(torch.uint8))
+        self.m_absmax.copy_(am)
+        self.v_absmax.copy_(av)
+
+    def step(self, lr: float | None = None, use_clip: bool = False):
+        if lr is not None:
+            self.lr = lr
+        self.step_count += 1
+        b1, b2 = self.betas
+        bc1 = 1.0 - b1 ** self.step_count
+        bc2 = 1.0 - b2 ** self.step_count
+        if self.native:
+            _lib.call("kca_adamw8bit", self.master.data_ptr(), self.grad.data_ptr(), self.m_codes.data_ptr(),
+                      self.m_absmax.data_ptr(), self.v_codes.data_ptr(), self.v_absmax.data_ptr(),
+                      _lib.ptr(self.model_bf16), self.master.numel(), _lib.ptr(self.wd_mask), float(self.lr),
+                      float(b1), float(b2), float(self.eps), float(self.weight_decay), float(bc1), float(bc2),
+                      self._coef.data_ptr() if use_clip else None,
+                      self._skip.data_ptr() if use_clip else None, _lib.stream())
+            return
+        if use_clip and bool(self._skip.item()):
+            return
+        g = self.grad * (self._coef if use_clip else 1.0)
+        m, v = self.dequant()
+        m = b1 * m + (1 - b1) * g
+        v = b2 * v + (1 - b2) * g * g
+        denom = v.sqrt() / math.sqrt(bc2) + self.eps
+        if self.weight_decay:
+            if self.wd_mask is None:
+                self.master.mul_(1 - self.lr * self.weight_decay)
+            else:
+                mk = self.wd_mask.to(self.master.device).bool().repeat_interleave(64)[: self.master.numel()]
+                self.master.mul_(torch.where(mk, 1 - self.lr * self.weight_decay, 1.0))
+        self.master.add_(-self.lr / bc1 * m / denom)
+        self._quant(m, v)
+        if self.model_bf16 is not None:
+            self.model_bf16.copy_(self.master)
+
+    def state_dict(self):
+        return {"m_codes": self.m_codes, "v_codes": self.v_codes, "m_absmax": self.m_absmax,
+                "v_absmax": self.v_absmax, "step": self.step_count, "lr": self.lr, "betas": list(self.betas),
+                "eps": self.eps, "weight_decay": self.weight_decay, "bits": 8}
+
+    def load_state_dict(self, sd):
+        for k in ("m_codes", "v_codes", "m_absmax", "v_absmax"):
+            getattr(self, k).copy_(sd[k])
+        self.step_count = int(sd["step"])
+        self.lr = sd.get("lr", self.lr)
+
+
 # ----------------------------------------------------------------- schedules
 def lr_at(step: int, base_lr: float, total_steps: int, warmup_steps: int, kind: str = "linear",
           min_lr: float = 0.0) -> float:

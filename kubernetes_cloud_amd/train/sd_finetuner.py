@@ -184,11 +184,12 @@ def main(argv=None):
                                      sampler=sampler, collate_fn=ds.get_collate_fn(), num_workers=2,
                                      drop_last=world > 1)
     if args.use_8bit_adam and info.is_main:
-        print("--use_8bit_adam: using the fused fp32-state AdamW (the reference's own fallback)", file=sys.stderr)
+        print("--use_8bit_adam: block-wise 8-bit AdamW states (kca_adamw8bit)", file=sys.stderr)
     unet.train()
     eng = TrainEngine(unet, lr=args.lr, betas=(args.adam_beta1, args.adam_beta2), eps=args.adam_epsilon,
                       weight_decay=args.adam_weight_decay, max_grad_norm=1.0,
-                      zero_stage=args.zero_stage if world > 1 else 0, grad_accum=1)
+                      zero_stage=args.zero_stage if world > 1 else 0, grad_accum=1,
+                      optim_bits=8 if args.use_8bit_adam else 32)
     ema = FlatEMA(eng.opt.master) if args.use_ema else None
     total = args.epochs * len(dl)
     if args.max_steps > 0:

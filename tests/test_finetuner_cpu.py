@@ -181,3 +181,31 @@ def test_fault_injection_and_deterministic_resume(tmp_path):
     a = load_file(str(rd / "final" / "model.safetensors"))
     b = load_file(str(tmp_path / "b" / "results-f" / "final" / "model.safetensors"))
     assert max(float((a[k].float() - b[k].float()).abs().max()) for k in a) == 0.0
+
+
+def test_watchdog_catches_hung_rank_and_resume_completes(tmp_path):
+    """SURVEY §5.3 failure detection: a rank that stops making progress at step 3
+    (KCA_FAULT_HANG_STEP) is caught by the step watchdog (KCA_WATCHDOG_TIMEOUT),
+    which writes a stack report and exits 124 so the pod restarts; the restart
+    resumes from checkpoint-2 and finishes."""
+    import json
+    import subprocess
+    import sys
+    model = make_model_dir(str(tmp_path / "model"))
+    data = make_tokens(str(tmp_path / "d.tokens"), n_ctx=24, ctx=32)
+    out = tmp_path / "a"
+    argv = ["--run-name", "h", "--model", model, "--dataset", data, "--context-size", "32", "--bs", "2",
+            "--gradients", "1", "--output-path", str(out), "--logs", str(out / "logs"), "--save-steps", "2",
+            "--zero-stage", "0", "--max-steps", "4"]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "kubernetes_cloud_amd.train.finetuner"]
+    env = dict(os.environ, KCA_FAULT_HANG_STEP="3", KCA_WATCHDOG_TIMEOUT="4", PYTHONPATH=root)
+    r = subprocess.run(cmd + argv, env=env, cwd=root, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 124, r.stderr[-2000:]
+    rd = out / "results-h"
+    rep = json.loads((rd / "watchdog-rank0.json").read_text())
+    assert rep["last_step"] == 3 and rep["seconds_since_beat"] > 4 and "Thread" in rep["stacks"]
+    env.pop("KCA_FAULT_HANG_STEP")
+    r = subprocess.run(cmd + argv, env=env, cwd=root, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert (rd / "final" / ".ready.txt").exists()

@@ -240,3 +240,30 @@ def test_groupnorm(N, C, H, W, G, silu):
     assert _rel(x.grad, xr.grad) < 2e-2
     assert _rel(w.grad, wr.grad) < 2e-2
     assert _rel(b.grad, br.grad) < 2e-2
+
+
+def test_adamw8bit_matches_reference_math():
+    """kca_adamw8bit vs the torch implementation of the same block-wise 8-bit
+    AdamW (FlatAdamW8bit with native=False) over several steps, ragged tail."""
+    from kubernetes_cloud_amd.train.optim import FlatAdamW8bit
+    torch.manual_seed(0)
+    n = 2048 * 5 + 1028  # last block partial
+    p0 = torch.randn(n, device=DEV)
+    mask = (torch.arange((n + 63) // 64, device=DEV) % 3 != 0).to(torch.uint8)
+    opts = []
+    for native in (True, False):
+        o = FlatAdamW8bit(p0.clone(), lr=1e-2, weight_decay=0.1, wd_mask=mask,
+                          model_bf16=torch.empty(n, device=DEV, dtype=torch.bfloat16))
+        o.native = native
+        opts.append(o)
+    for it in range(5):
+        g = torch.randn(n, device=DEV) * (1.0 + it)
+        for o in opts:
+            o.grad.copy_(g)
+            o.step()
+    a, b = opts
+    assert _rel(a.master, b.master) < 1e-4
+    assert (a.m_codes.int() - b.m_codes.int()).abs().max() <= 1
+    assert (a.v_codes.int() - b.v_codes.int()).abs().max() <= 1
+    assert _rel(a.m_absmax, b.m_absmax) < 1e-4 and _rel(a.v_absmax, b.v_absmax) < 1e-4
+    assert _rel(a.model_bf16.float(), a.master) < 1e-2
