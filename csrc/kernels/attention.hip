@@ -52,6 +52,7 @@ struct AttnParams {
   float scale;
   const float* alibi;  // [H] slopes or null
   const int* kv_len;   // [B] or null
+  const int* fix_flags;  // fixup mode: run only blocks whose tiled-path wave flags are set
 };
 
 struct AttnBwdParams {
@@ -167,6 +168,10 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_kernel(AttnP
   const int l32 = lane & 31, hh = lane >> 5;
   const int nqb = (p.Sq + BM - 1) / BM;
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  if (p.fix_flags) {  // same grid / lid mapping as attn_fwd_tiled_kernel
+    const int4 f = reinterpret_cast<const int4*>(p.fix_flags)[lid];
+    if (!(f.x | f.y | f.z | f.w)) return;
+  }
   const int qi = lid % nqb;
   const int qb = CAUSAL ? (nqb - 1 - qi) : qi;
   const int bh = lid / nqb;
@@ -982,10 +987,10 @@ KCA_API int kca_attn_fwd_tiled(const void* q, const void* k, const void* v, void
                                long long k_st, long long k_sh, long long v_sb, long long v_st,
                                long long v_sh, long long o_sb, long long o_st, long long o_sh,
                                int B, int Sq, int Sk, int H, int Hkv, int d, int causal,
-                               float scale, hipStream_t stream);
+                               float scale, int* flags, hipStream_t stream);
 
-// path: 0 = auto (full-tile fast path of attention_tiled.hip when the shape
-// allows, else the generic kernel), 1 = generic kernel only.
+// workspace: >= 4 * ceil(Sq/128) * B * H ints for the full-tile fast path of
+// attention_tiled.hip (its overflow flags), or null for the generic kernel.
 KCA_API int kca_attn_fwd(const void* q, const void* k, const void* v, void* o,
                          float* lse, long long q_sb, long long q_st,
                          long long q_sh, long long k_sb, long long k_st,
@@ -993,17 +998,18 @@ KCA_API int kca_attn_fwd(const void* q, const void* k, const void* v, void* o,
                          long long v_sh, long long o_sb, long long o_st,
                          long long o_sh, int B, int Sq, int Sk, int H, int Hkv,
                          int d_real, int causal, float scale,
-                         const float* alibi, const int* kv_len, int path,
+                         const float* alibi, const int* kv_len, int* workspace,
                          hipStream_t stream) {
   if (d_real % 8 || H % Hkv) return 1;
-  if (path == 0 && g_attn_tiled && !alibi && !kv_len &&
-      kca_attn_fwd_tiled(q, k, v, o, lse, q_sb, q_st, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh,
-                         o_sb, o_st, o_sh, B, Sq, Sk, H, Hkv, d_real, causal, scale, stream) == 0)
-    return 0;
   const int D = pick_d(d_real);
   AttnParams p{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, lse,
                q_sb, q_st, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh, o_sb, o_st, o_sh,
-               B, Sq, Sk, H, Hkv, d_real, causal, scale, alibi, kv_len};
+               B, Sq, Sk, H, Hkv, d_real, causal, scale, alibi, kv_len, nullptr};
+  if (g_attn_tiled && workspace && !alibi && !kv_len &&
+      kca_attn_fwd_tiled(q, k, v, o, lse, q_sb, q_st, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh,
+                         o_sb, o_st, o_sh, B, Sq, Sk, H, Hkv, d_real, causal, scale, workspace,
+                         stream) == 0)
+    p.fix_flags = workspace;  // fixup launch below: only flagged blocks do work
   dim3 grid(((Sq + 127) / 128) * B * H);
   ATTN_D_DISPATCH(D, {
     if (causal)

@@ -31,6 +31,7 @@ constexpr float kRescaleThr = 8.0f;
 struct FastFwdParams {
   const bf16_t* q; const bf16_t* k; const bf16_t* v;
   bf16_t* o; float* lse;
+  int* flags;  // [grid * 4]: 1 = this wave's rows overflowed -> fixup kernel
   long long q_sb, q_st, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh;
   long long o_sb, o_st, o_sh;
   int B, Sq, Sk, H, Hkv;
@@ -128,7 +129,7 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel
   for (int i = 0; i < D / 32; ++i)
 #pragma unroll
     for (int r = 0; r < 16; ++r) oacc[i][r] = 0.f;
-  float m = -INFINITY, lsum = 0.f;
+  float m = 0.f, lsum = 0.f;  // m: reference max (log2 units), set by tile 0
 
   // staging: thread handles chunks idx = tid + i*256 -> row = tid/NCH + i*RPI,
   // ch = tid % NCH (256 % NCH == 0)
@@ -179,24 +180,22 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel
           if (key > qrow + off) sacc[r] = -INFINITY;
         }
       }
-      float mt = sacc[0];
+      // No running max and no O rescale: the reference max m is the row max of
+      // the first tile and stays fixed. Floating point is scale invariant, so
+      // P = 2^(s - m) only needs to stay finite -- it can exceed 1 when a later
+      // key scores higher. Overflow (a later score ~2^100 times the first
+      // tile's best) is detected once, from the final row sum, and those rows
+      // are recomputed by the generic kernel (kca_attn_fwd_tiled's fixup
+      // launch). Keeping every rescale out of the loop keeps the O^T
+      // accumulators in AGPRs, touched only by MFMAs (a conditional rescale
+      // made hipcc copy all of O to VGPRs and back every tile).
+      if (t == 0) {
+        float mt = sacc[0];
 #pragma unroll
-      for (int r = 1; r < 16; ++r) mt = fmaxf(mt, sacc[r]);
-      mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * sl2;
-      if (!__all(mt <= m + kRescaleThr)) {
-        const float mnew = fmaxf(m, mt);
-        const float alpha = (m == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m - mnew);
-        lsum *= alpha;
-        // one 32x32 tile at a time: the accumulators live in AGPRs and a
-        // whole-O rescale in flight would need D*4/64 extra VGPRs
-#pragma unroll
-        for (int i = 0; i < D / 32; ++i) {
-          oacc[i] *= alpha;
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        m = mnew;
+        for (int r = 1; r < 16; ++r) mt = fmaxf(mt, sacc[r]);
+        m = fmaxf(mt, __shfl_xor(mt, 32, 64)) * sl2;
       }
-      const float nm = (m == -INFINITY) ? 0.f : -m;
+      const float nm = -m;
       float ps = 0.f;
       bf16x8 pf0, pf1;
 #pragma unroll
@@ -225,6 +224,11 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel
   }
 
   const float ltot = lsum + __shfl_xor(lsum, 32, 64);
+  // row sums past 2^100 (or inf / NaN) mean P may have overflowed: flag the
+  // wave for the generic-kernel fixup (which then rewrites O and lse)
+  const bool bad = !(ltot < 1.2676506e30f);
+  const int any_bad = __any(bad);
+  if (lane == 0) p.flags[lid * 4 + wave] = any_bad;
   const float inv = ltot > 0.f ? 1.f / ltot : 0.f;
   if (hh == 0 && p.lse)
     p.lse[((long long)b * p.H + h) * p.Sq + qrow] = ltot > 0.f ? (m + log2f(ltot)) * kLn2 : INFINITY;
@@ -543,13 +547,14 @@ KCA_API int kca_attn_fwd_tiled(const void* q, const void* k, const void* v, void
                                long long k_st, long long k_sh, long long v_sb, long long v_st,
                                long long v_sh, long long o_sb, long long o_st, long long o_sh,
                                int B, int Sq, int Sk, int H, int Hkv, int d, int causal,
-                               float scale, hipStream_t stream) {
-  if ((d != 128 && d != 256) || Sq % 128 || Sk % 32 || Sq <= 0 || H % Hkv) return 1;
+                               float scale, int* flags, hipStream_t stream) {
+  if ((d != 128 && d != 256) || Sq % 128 || Sk % 32 || Sq <= 0 || H % Hkv || !flags) return 1;
   if (causal && Sk < Sq) return 1;
-  FastFwdParams p{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, lse,
+  FastFwdParams p{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, lse, flags,
                   q_sb, q_st, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh, o_sb, o_st, o_sh,
                   B, Sq, Sk, H, Hkv, scale};
   dim3 grid((Sq / 128) * B * H);
+  (void)hipGetLastError();
   if (d == 256) {
     if (causal) hipLaunchKernelGGL((attn_fwd_tiled_kernel<256, true>), grid, dim3(256), 0, stream, p);
     else hipLaunchKernelGGL((attn_fwd_tiled_kernel<256, false>), grid, dim3(256), 0, stream, p);
@@ -557,7 +562,9 @@ KCA_API int kca_attn_fwd_tiled(const void* q, const void* k, const void* v, void
     if (causal) hipLaunchKernelGGL((attn_fwd_tiled_kernel<128, true>), grid, dim3(256), 0, stream, p);
     else hipLaunchKernelGGL((attn_fwd_tiled_kernel<128, false>), grid, dim3(256), 0, stream, p);
   }
-  return 0;
+  // a failed launch leaves the flags unwritten: report it so the caller runs
+  // the generic kernel on every block instead of trusting stale flags
+  return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
 KCA_API int kca_attn_bwd_tiled(const void* q, const void* k, const void* v, const void* dout,

@@ -68,10 +68,12 @@ def _fwd(q, k, v, causal, scale, kv_len, alibi, out=None):
     Sk, Hkv = k.shape[1], k.shape[2]
     o = out if out is not None else torch.empty(B, Sq, H, D, device=q.device, dtype=q.dtype)
     lse = torch.empty(B, H, Sq, device=q.device, dtype=torch.float32)
+    # overflow flags of the full-tile fast path (4 per 128-row block)
+    flags = torch.empty(4 * ((Sq + 127) // 128) * B * H, device=q.device, dtype=torch.int32)
     _lib.call("kca_attn_fwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr(),
               *_strides(q), *_strides(k), *_strides(v), *_strides(o),
-              B, Sq, Sk, H, Hkv, D, int(causal), float(scale), _lib.ptr(alibi), _lib.ptr(kv_len), 0,
-              _lib.stream())
+              B, Sq, Sk, H, Hkv, D, int(causal), float(scale), _lib.ptr(alibi), _lib.ptr(kv_len),
+              flags.data_ptr(), _lib.stream())
     return o, lse
 
 

@@ -193,6 +193,25 @@ def test_attention_deferred_rescale_branch(D):
         assert _rel(o, orf) < 2e-2, (causal, _rel(o, orf))
 
 
+@pytest.mark.parametrize("D", [128, 256])
+def test_attention_tiled_overflow_fixup(D):
+    """A key far past the first tile scores ~2^900 times higher than anything in
+    tile 0: the fixed-reference-max fast path overflows, flags the rows, and the
+    generic-kernel fixup launch must rewrite them (and only them) exactly."""
+    torch.manual_seed(4)
+    B, S, H = 1, 256, 2
+    q = torch.randn(B, S, H, D, device=DEV) * 0.3
+    k = torch.randn(B, S, H, D, device=DEV) * 0.3
+    v = torch.randn(B, S, H, D, device=DEV)
+    k[:, 200] = q[:, 220] * 40.0  # rows near 220 see one enormous score at key 200
+    q, k, v = (t.bfloat16() for t in (q, k, v))
+    for causal in (True, False):
+        o = ops.flash_attention(q, k, v, causal=causal)
+        orf, _ = ops.attention_reference(q.float(), k.float(), v.float(), causal)
+        assert torch.isfinite(o.float()).all()
+        assert _rel(o, orf) < 2e-2, (causal, _rel(o, orf))
+
+
 def test_attention_gqa_kvlen_alibi():
     _attn_case(2, 130, 130, 8, 2, 128, True, kv_len=[130, 97], alibi=True)
     _attn_case(3, 77, 77, 4, 4, 64, False, kv_len=[77, 10, 50])
