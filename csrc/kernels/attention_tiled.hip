@@ -22,6 +22,8 @@
 // scale folded into one FMA, deferred rescale (T13, threshold 8).
 #include "common.h"
 
+#include <type_traits>
+
 namespace {
 
 constexpr float kLog2e = 1.4426950408889634f;
@@ -94,7 +96,7 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel
   constexpr int TILE = BN * D * 2;           // bytes per K or V tile
   constexpr int NCH = D / 8;                 // 16-B chunks per row
   constexpr int CPT = BN * NCH / 256;        // chunks per thread per tile
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // [buf][K|V]
+  __shared__ __attribute__((aligned(16))) char smem[3 * 2 * TILE];  // [buf 0..2][K|V]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, hh = lane >> 5, gi = lane & 15;
@@ -148,80 +150,99 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel
   const int vb_2 = 16 * D + 64 * (4 * hh + (gi >> 2)) + 16 * (c3 ^ hh ^ 2) + 8 * (gi & 1);
 
   // ntiles >= 1 on this path (Sk >= 32; causal: Sk >= Sq)
+  // Software pipeline over 32-key tiles, three LDS buffers: while the softmax
+  // of tile t runs on the VALU, the S^T MFMAs of tile t+1 run on the matrix
+  // pipe (independent instructions the scheduler interleaves, T15), then
+  // O^T += V_t^T P_t^T; the global loads of tile t+2 are in flight throughout
+  // and land in the buffer tile t-1 vacated (T14).
+  auto qk = [&](const char* Ks) {
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s) {
+      const bf16x8 a = lds_b128(Ks, ((s & 1) ? kb_o : kb_e) + 512 * (s >> 1));
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s], acc, 0, 0, 0);
+    }
+    return acc;
+  };
+  // causal: keys past this lane's query -> -inf. sacc[r] holds key
+  // k0 + (r&3) + 8(r>>2) + 4hh of query qrow. Tiles wholly above a wave's rows
+  // are masked, not skipped (a skip puts O in a conditional region: spills).
+  auto mask = [&](f32x16& acc, int k0) {
+    const int lim = qrow + off - k0 - 4 * hh;
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      if ((r & 3) + 8 * (r >> 2) > lim) acc[r] = -INFINITY;
+  };
+
   stage_load<CPT, RPI>(sk, sv, kst, vst, 0, p.k_st, p.v_st);
   stage_store<CPT, RPI, D>(sk, sv, smem, st_row, st_ch);
+  stage_load<CPT, RPI>(sk, sv, kst, vst, min(BN, (ntiles - 1) * BN), p.k_st, p.v_st);
+  stage_store<CPT, RPI, D>(sk, sv, smem + 2 * TILE, st_row, st_ch);
   __syncthreads();
 
-  for (int t = 0; t < ntiles; ++t) {
-    const int k0 = t * BN;
-    const char* Ks = smem + (t & 1) * 2 * TILE;
-    const char* Vs = Ks + TILE;
-    // the last iteration re-loads its own tile (in bounds, never stored)
-    stage_load<CPT, RPI>(sk, sv, kst, vst, min(k0 + BN, (ntiles - 1) * BN), p.k_st, p.v_st);
-    // Keep the staging loads above and the LDS stores below on their own sides
-    // of the MFMAs: without the fences the compiler merges the two `t + 1 <
-    // ntiles` blocks and stores each load to LDS right after it (vmcnt(0)).
+  const int nfree = CAUSAL ? ntiles - 4 : ntiles;  // tiles no wave needs masked
+  f32x16 sa = qk(smem);
+  if (CAUSAL && nfree <= 0) mask(sa, 0);
+  {
+    // No running max and no O rescale: the reference max m is the row max of
+    // the first tile and stays fixed. Floating point is scale invariant, so
+    // P = 2^(s - m) only needs to stay finite -- it can exceed 1 when a later
+    // key scores higher. Overflow (a later score ~2^100 times the first
+    // tile's best) is detected once, from the final row sum, and those rows
+    // are recomputed by the generic kernel (kca_attn_fwd_tiled's fixup
+    // launch). Keeping every rescale out of the loop keeps the O^T
+    // accumulators in AGPRs, touched only by MFMAs (a conditional rescale
+    // made hipcc copy all of O to VGPRs and back every tile).
+    float mt = sa[0];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) mt = fmaxf(mt, sa[r]);
+    m = fmaxf(mt, __shfl_xor(mt, 32, 64)) * sl2;
+  }
+  const float nm = -m;
+
+  auto tile_step = [&](int t, auto masked) {
+    constexpr bool MASKED = decltype(masked)::value;
+    const char* Vs = smem + (t % 3) * 2 * TILE + TILE;
+    const char* Kn = smem + ((t + 1) % 3) * 2 * TILE;
+    // the loads of tile t+2 (clamped: the last iterations re-load a tile that
+    // is never stored)
+    stage_load<CPT, RPI>(sk, sv, kst, vst, min((t + 2) * BN, (ntiles - 1) * BN), p.k_st, p.v_st);
+    // keep the staging loads above and the LDS stores below on their own
+    // sides of the MFMAs (without the fences hipcc stores each load right
+    // after it, behind a vmcnt(0))
     asm volatile("" ::: "memory");
-    {  // causal tiles wholly above this wave's rows are masked, not skipped
-       // (a skip puts the O accumulators in a conditional region: spills)
-      f32x16 sacc;
+    f32x16 sb = qk(Kn);  // S of tile t+1 (stale buffer on the last tile: unused)
+    if constexpr (MASKED) mask(sa, t * BN);
+    float ps = 0.f;
+    bf16x8 pf0, pf1;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
+    for (int r = 0; r < 8; ++r) {
+      const float e0 = __builtin_amdgcn_exp2f(fmaf(sa[r], sl2, nm));
+      const float e1 = __builtin_amdgcn_exp2f(fmaf(sa[r + 8], sl2, nm));
+      ps += e0 + e1;
+      pf0[r] = (__bf16)e0;
+      pf1[r] = (__bf16)e1;
+    }
+    lsum += ps;
 #pragma unroll
-      for (int s = 0; s < D / 16; ++s) {
-        const bf16x8 a = lds_b128(Ks, ((s & 1) ? kb_o : kb_e) + 512 * (s >> 1));
-        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s], sacc, 0, 0, 0);
-      }
-      // sacc[r] = S[key = k0 + (r&3) + 8(r>>2) + 4hh][q = qrow] (raw dot products)
-      if (CAUSAL && (k0 + 31 > q0 + off)) {
+    for (int db = 0; db < D / 32; ++db) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = k0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          if (key > qrow + off) sacc[r] = -INFINITY;
-        }
-      }
-      // No running max and no O rescale: the reference max m is the row max of
-      // the first tile and stays fixed. Floating point is scale invariant, so
-      // P = 2^(s - m) only needs to stay finite -- it can exceed 1 when a later
-      // key scores higher. Overflow (a later score ~2^100 times the first
-      // tile's best) is detected once, from the final row sum, and those rows
-      // are recomputed by the generic kernel (kca_attn_fwd_tiled's fixup
-      // launch). Keeping every rescale out of the loop keeps the O^T
-      // accumulators in AGPRs, touched only by MFMAs (a conditional rescale
-      // made hipcc copy all of O to VGPRs and back every tile).
-      if (t == 0) {
-        float mt = sacc[0];
-#pragma unroll
-        for (int r = 1; r < 16; ++r) mt = fmaxf(mt, sacc[r]);
-        m = fmaxf(mt, __shfl_xor(mt, 32, 64)) * sl2;
-      }
-      const float nm = -m;
-      float ps = 0.f;
-      bf16x8 pf0, pf1;
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const float e0 = __builtin_amdgcn_exp2f(fmaf(sacc[r], sl2, nm));
-        const float e1 = __builtin_amdgcn_exp2f(fmaf(sacc[r + 8], sl2, nm));
-        ps += e0 + e1;
-        pf0[r] = (__bf16)e0;
-        pf1[r] = (__bf16)e1;
-      }
-      lsum += ps;
-#pragma unroll
-      for (int db = 0; db < D / 32; ++db) {
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const int o1 = vb_1 + 2 * s * 16 * D + 512 * db;
-          const int o2 = vb_2 + 2 * s * 16 * D + 512 * db;
-          const bf16x8 a = cat8(lds_tr4(Vs, o1), lds_tr4(Vs, o2));
-          oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, s ? pf1 : pf0, oacc[db], 0, 0, 0);
-        }
+      for (int s = 0; s < 2; ++s) {
+        const int o1 = vb_1 + 2 * s * 16 * D + 512 * db;
+        const int o2 = vb_2 + 2 * s * 16 * D + 512 * db;
+        const bf16x8 a = cat8(lds_tr4(Vs, o1), lds_tr4(Vs, o2));
+        oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, s ? pf1 : pf0, oacc[db], 0, 0, 0);
       }
     }
+    sa = sb;
     asm volatile("" ::: "memory");
-    if (t + 1 < ntiles) stage_store<CPT, RPI, D>(sk, sv, smem + ((t + 1) & 1) * 2 * TILE, st_row, st_ch);
+    if (t + 2 < ntiles) stage_store<CPT, RPI, D>(sk, sv, smem + ((t + 2) % 3) * 2 * TILE, st_row, st_ch);
     __syncthreads();
-  }
+  };
+  for (int t = 0; t < nfree; ++t) tile_step(t, std::false_type{});
+  for (int t = max(nfree, 0); t < ntiles; ++t) tile_step(t, std::true_type{});
 
   const float ltot = lsum + __shfl_xor(lsum, 32, 64);
   // row sums past 2^100 (or inf / NaN) mean P may have overflowed: flag the
@@ -362,46 +383,48 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq_tiled_kernel(FastBwdParams
   stage_load<CPT, RPI>(sk, sv, kst, vst, 0, p.k_st, p.v_st);
   stage_store<CPT, RPI, D>(sk, sv, smem, st_row, st_ch);
   __syncthreads();
-  for (int t = 0; t < ntiles; ++t) {
+  // the last 4 tiles hold the four waves' diagonals; earlier tiles run the
+  // mask-free body. Tiles wholly above a wave's rows are masked, not skipped.
+  auto tile_step = [&](int t, auto masked) {
+    constexpr bool MASKED = decltype(masked)::value;
     const int k0 = t * BN;
     const char* Ks = smem + (t & 1) * 2 * TILE;
     const char* Vs = Ks + TILE;
     stage_load<CPT, RPI>(sk, sv, kst, vst, min(k0 + BN, (ntiles - 1) * BN), p.k_st, p.v_st);
     asm volatile("" ::: "memory");
-    {  // tiles wholly above this wave's rows (causal) are masked, not skipped:
-       // see the dK/dV kernel
-      f32x16 st, dpt;
+    f32x16 st, dpt;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) { st[r] = 0.f; dpt[r] = 0.f; }
+    for (int r = 0; r < 16; ++r) { st[r] = 0.f; dpt[r] = 0.f; }
 #pragma unroll
-      for (int s = 0; s < D / 16; ++s) {
-        st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(Ks, be, bo, s), qf[s], st, 0, 0, 0);
-        dpt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(Vs, be, bo, s), gf[s], dpt, 0, 0, 0);
+    for (int s = 0; s < D / 16; ++s) {
+      st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(Ks, be, bo, s), qf[s], st, 0, 0, 0);
+      dpt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(Vs, be, bo, s), gf[s], dpt, 0, 0, 0);
+    }
+    const int lim = qrow + off - k0 - 4 * hh;  // visible key offsets (r&3)+8(r>>2) <= lim
+    bf16x8 d0, d1;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      float p0 = __builtin_amdgcn_exp2f(fmaf(st[r], sl2, nlse));
+      float p1 = __builtin_amdgcn_exp2f(fmaf(st[r + 8], sl2, nlse));
+      if constexpr (MASKED) {
+        if ((r & 3) + 8 * (r >> 2) > lim) p0 = 0.f;
+        if ((r & 3) + 8 * (r >> 2) + 16 > lim) p1 = 0.f;
       }
-      const bool diag = CAUSAL && (k0 + 31 > q0 + off);
-      bf16x8 d0, d1;
+      d0[r] = (__bf16)(p0 * (dpt[r] - dl));
+      d1[r] = (__bf16)(p1 * (dpt[r + 8] - dl));
+    }
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        float p0 = __builtin_amdgcn_exp2f(fmaf(st[r], sl2, nlse));
-        float p1 = __builtin_amdgcn_exp2f(fmaf(st[r + 8], sl2, nlse));
-        if (diag) {
-          const int key0 = k0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          if (key0 > qrow + off) p0 = 0.f;
-          if (key0 + 16 > qrow + off) p1 = 0.f;
-        }
-        d0[r] = (__bf16)(p0 * (dpt[r] - dl));
-        d1[r] = (__bf16)(p1 * (dpt[r + 8] - dl));
-      }
-#pragma unroll
-      for (int db = 0; db < D / 32; ++db) {
-        dq[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(Ks, b1, b2, 0, db), d0, dq[db], 0, 0, 0);
-        dq[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(Ks, b1, b2, 1, db), d1, dq[db], 0, 0, 0);
-      }
+    for (int db = 0; db < D / 32; ++db) {
+      dq[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(Ks, b1, b2, 0, db), d0, dq[db], 0, 0, 0);
+      dq[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(Ks, b1, b2, 1, db), d1, dq[db], 0, 0, 0);
     }
     asm volatile("" ::: "memory");
     if (t + 1 < ntiles) stage_store<CPT, RPI, D>(sk, sv, smem + ((t + 1) & 1) * 2 * TILE, st_row, st_ch);
     __syncthreads();
-  }
+  };
+  const int nfree = CAUSAL ? ntiles - 4 : ntiles;
+  for (int t = 0; t < nfree; ++t) tile_step(t, std::false_type{});
+  for (int t = max(nfree, 0); t < ntiles; ++t) tile_step(t, std::true_type{});
   store_acc_t<D>(p.dq + b * p.dq_sb + h * p.dq_sh + (long long)qrow * p.dq_st, dq, hh, p.scale);
 }
 
@@ -481,7 +504,8 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_tiled_kernel(FastBwdPara
     KCA_DKDV_STORE(0);
   }
   __syncthreads();
-  for (int it = 0; it < total; ++it) {
+  auto tile_step = [&](int it, auto masked) {
+    constexpr bool MASKED = decltype(masked)::value;
     const int qt = q_lo + (it % nqt) * BQ;
     const char* Qs = smem + (it & 1) * 2 * TILE;
     const char* Gs = Qs + TILE;
@@ -493,45 +517,50 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_tiled_kernel(FastBwdPara
     // wave's keys: they are masked to P = 0 like the diagonal, which costs
     // ~4 % extra MFMAs under a causal mask but keeps the 256 dK/dV accumulator
     // registers out of a conditional region (the skip made hipcc spill).
-    {
-      f32x16 sacc, dpacc;
+    f32x16 sacc, dpacc;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) { sacc[r] = 0.f; dpacc[r] = 0.f; }
+    for (int r = 0; r < 16; ++r) { sacc[r] = 0.f; dpacc[r] = 0.f; }
 #pragma unroll
-      for (int s = 0; s < D / 16; ++s) {
-        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(Qs, be, bo, s), kf[s], sacc, 0, 0, 0);
-        dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(Gs, be, bo, s),
-                                                        row_frag<D>(vimg, be, bo, s), dpacc, 0, 0, 0);
-      }
-      // rows q = qt + 8g + 4hh + j (g = r>>2, j = r&3): lse / delta as float4
-      const bool diag = CAUSAL && (kw + 31 > qt + off);
-      bf16x8 p0, p1, s0, s1;
+    for (int s = 0; s < D / 16; ++s) {
+      sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(Qs, be, bo, s), kf[s], sacc, 0, 0, 0);
+      dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(Gs, be, bo, s),
+                                                      row_frag<D>(vimg, be, bo, s), dpacc, 0, 0, 0);
+    }
+    // rows q = qt + 8g + 4hh + j (g = r>>2, j = r&3): lse / delta as float4;
+    // visible iff key <= q + off, i.e. 8g + j >= key - qt - off - 4hh
+    const int lim = key - qt - off - 4 * hh;
+    bf16x8 p0, p1, s0, s1;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const f32x4 lq = *reinterpret_cast<const f32x4*>(ls + 8 * g + 4 * hh);
-        const f32x4 dq4 = *reinterpret_cast<const f32x4*>(ls + 32 + 8 * g + 4 * hh);
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 lq = *reinterpret_cast<const f32x4*>(ls + 8 * g + 4 * hh);
+      const f32x4 dq4 = *reinterpret_cast<const f32x4*>(ls + 32 + 8 * g + 4 * hh);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int r = 4 * g + j;
-          float pr = __builtin_amdgcn_exp2f(fmaf(sacc[r], sl2, -lq[j]));
-          if (diag && key > qt + 8 * g + 4 * hh + j + off) pr = 0.f;
-          const float ds = pr * (dpacc[r] - dq4[j]);
-          if (r < 8) { p0[r] = (__bf16)pr; s0[r] = (__bf16)ds; }
-          else { p1[r - 8] = (__bf16)pr; s1[r - 8] = (__bf16)ds; }
+      for (int j = 0; j < 4; ++j) {
+        const int r = 4 * g + j;
+        float pr = __builtin_amdgcn_exp2f(fmaf(sacc[r], sl2, -lq[j]));
+        if constexpr (MASKED) {
+          if (8 * g + j < lim) pr = 0.f;
         }
+        const float ds = pr * (dpacc[r] - dq4[j]);
+        if (r < 8) { p0[r] = (__bf16)pr; s0[r] = (__bf16)ds; }
+        else { p1[r - 8] = (__bf16)pr; s1[r - 8] = (__bf16)ds; }
       }
+    }
 #pragma unroll
-      for (int db = 0; db < D / 32; ++db) {
-        dv[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(Gs, b1, b2, 0, db), p0, dv[db], 0, 0, 0);
-        dv[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(Gs, b1, b2, 1, db), p1, dv[db], 0, 0, 0);
-        dk[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(Qs, b1, b2, 0, db), s0, dk[db], 0, 0, 0);
-        dk[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(Qs, b1, b2, 1, db), s1, dk[db], 0, 0, 0);
-      }
+    for (int db = 0; db < D / 32; ++db) {
+      dv[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(Gs, b1, b2, 0, db), p0, dv[db], 0, 0, 0);
+      dv[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(Gs, b1, b2, 1, db), p1, dv[db], 0, 0, 0);
+      dk[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(Qs, b1, b2, 0, db), s0, dk[db], 0, 0, 0);
+      dk[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(Qs, b1, b2, 1, db), s1, dk[db], 0, 0, 0);
     }
     asm volatile("" ::: "memory");
     if (it + 1 < total) KCA_DKDV_STORE((it + 1) & 1);
     __syncthreads();
-  }
+  };
+  // One flat loop with the (cheap, select-only) causal mask on every tile:
+  // splitting into masked / mask-free bodies -- by a per-tile branch or by
+  // two loops per head -- pushed the 256 dK/dV accumulators into spills.
+  for (int it = 0; it < total; ++it) tile_step(it, std::integral_constant<bool, CAUSAL>{});
 #undef KCA_DKDV_LOAD
 #undef KCA_DKDV_STORE
   store_acc_t<D>(p.dk + b * p.dk_sb + hk * p.dk_sh + (long long)key * p.dk_st, dk, hh, p.scale);
