@@ -292,14 +292,16 @@ __global__ __launch_bounds__(256) void decode_combine_kernel(const float* __rest
   }
 }
 
-// Split size: enough (sequence, kv-head, split) workgroups to put >= ~2 on each
-// of the 256 CUs, chunks of 64..1024 tokens.
+// Split size: enough (sequence, kv-head, split) workgroups for ~8 per CU on
+// the 256 CUs (each split streams its K rows, then its V rows, a few 16-B
+// loads per lane in flight: the pass is HBM-latency bound per workgroup, so
+// bandwidth comes from workgroup count), chunks of 32..1024 tokens.
 KCA_API int kca_decode_chunk(int B, int Hkv, int max_kv) {
   long long work = (long long)B * Hkv;
-  long long want = (512 + work - 1) / work;
+  long long want = (2048 + work - 1) / work;
   long long c = (max_kv + want - 1) / want;
-  c = (c + 63) / 64 * 64;
-  if (c < 64) c = 64;
+  c = (c + 31) / 32 * 32;
+  if (c < 32) c = 32;
   if (c > 1024) c = 1024;
   return (int)c;
 }

@@ -63,6 +63,9 @@ class _Packed:
         pin = device.type == "cuda"
         self.host = torch.zeros(self.nbytes, dtype=torch.uint8, pin_memory=pin)
         self.dev = torch.zeros(self.nbytes, dtype=torch.uint8, device=device)
+        # numpy views of the pinned host buffer: per-row scalar writes cost
+        # ~0.1 us instead of a torch indexing op (~5 us) each
+        self.np = {name: self._view(self.host, name).numpy() for name in fields}
 
     def _view(self, buf, name):
         dt, n = self.fields[name]
@@ -300,9 +303,10 @@ class ModelRunner:
         st = self._static_for(Bb, Kb)
         pk = st["pk"]
         NB = self.max_bans
-        tok, sd, pos, sl, kl = pk.h("tokens"), pk.h("seeds"), pk.h("pos"), pk.h("slots"), pk.h("kv_lens")
-        tk, te, tp, rp, bans = pk.h("top_k"), pk.h("temperature"), pk.h("top_p"), pk.h("rep"), pk.h("bans")
-        bans.fill_(-1)
+        a = pk.np
+        tok, sd, pos, sl, kl = a["tokens"], a["seeds"], a["pos"], a["slots"], a["kv_lens"]
+        tk, te, tp, rp, bans = a["top_k"], a["temperature"], a["top_p"], a["rep"], a["bans"]
+        bans.fill(-1)
         for i in range(Bb):
             if i < n:
                 r = rows[i]

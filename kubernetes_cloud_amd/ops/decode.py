@@ -64,12 +64,14 @@ def decode_ws_floats(B: int, H: int, Hkv: int, D: int, max_kv: int, chunk: int =
 
 
 def decode_chunk(B: int, Hkv: int, max_kv: int) -> int:
-    """Mirror of kca_decode_chunk: >= ~512 (seq, head, split) workgroups."""
+    """Mirror of kca_decode_chunk: ~2048 (seq, head, split) workgroups (8 per
+    CU: each split's K then V stream is latency bound, so bandwidth comes
+    from workgroup count), chunks of 32..1024 tokens."""
     work = B * Hkv
-    want = -(-512 // work)
+    want = -(-2048 // work)
     c = -(-max_kv // want)
-    c = -(-c // 64) * 64
-    return max(64, min(1024, c))
+    c = -(-c // 32) * 32
+    return max(32, min(1024, c))
 
 
 def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slots: torch.Tensor,
