@@ -231,9 +231,13 @@ class ModelServer:
 
         return app
 
-    def start(self, models: list):
+    def start(self, models: list, extra_routes=None):
+        """``extra_routes(app)`` registers additional (non-KServe) routes, e.g.
+        the bloom-inference-server API of ``serving.bloom_server``."""
         import uvicorn
         app = self.create_app(models)
+        if extra_routes is not None:
+            extra_routes(app)
         log.info("serving %s on %s:%d", list(self.models), self.host, self.http_port)
         uvicorn.run(app, host=self.host, port=self.http_port, workers=1, log_level="info")
 

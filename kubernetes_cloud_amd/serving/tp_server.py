@@ -50,7 +50,12 @@ def main(argv=None):
     ap.add_argument("--max-len", type=int, default=2048)
     ap.add_argument("--random-init", default=None, help="preset name: random weights (benchmarks)")
     ap.add_argument("--layers", type=int, default=0)
+    ap.add_argument("--model-name", default=os.getenv("MODEL_NAME", ""),
+                    help="org/repo resolved in the read-only HF hub cache (bloom-176b-deepspeed layout)")
     args = ap.parse_args(argv)
+    if args.model_name and not args.random_init:
+        from .bloom_server import resolve_hf_cache_path
+        args.model_path = resolve_hf_cache_path(args.model_name)
     info = init_distributed()
     rank, world = info.rank, info.world_size
     ctrl = dist.new_group(backend="gloo")
@@ -72,8 +77,11 @@ def main(argv=None):
     from .text import TextGenerator
     gen = TextGenerator(model, tok, runner=CollectiveRunner(runner, ctrl))
     pred = BloomPredictor(generator=gen)
+    from .bloom_server import add_routes
     try:
-        ModelServer(http_port=args.port).start([pred])
+        # KServe V1 (bloom.py contract) and the bloom-inference-server routes
+        # (/generate/, /tokenize/, /query_id/) on the same port
+        ModelServer(http_port=args.port).start([pred], extra_routes=lambda app: add_routes(app, gen))
     finally:
         gen.close()
         gen.engine.runner.shutdown()

@@ -70,6 +70,35 @@ def test_kserve_v1_bloom_predictor(tmp_path):
     assert wait_for_ready_file(d, 1, 0.01)
 
 
+def test_bloom_inference_server_routes_and_hf_cache(tmp_path):
+    """S5: /generate/ + /tokenize/ + /query_id/ of transformers-bloom-inference
+    (text, num_generated_tokens, remove_input_from_output) and the read-only HF
+    hub cache resolution of files/isvc-patch.txt."""
+    from kubernetes_cloud_amd.serving.bloom_server import add_routes, resolve_hf_cache_path
+    d = make_model_dir(str(tmp_path / "bloom"), "bloom-560m", hidden_size=64, n_layer=2, n_head=4)
+    m, tok = load_lm(d, device="cpu")
+    gen = TextGenerator(m, tok, background=False)
+    app = ModelServer(http_port=1).create_app([])
+    add_routes(app, gen)
+    c = TestClient(app)
+    r = c.post("/generate/", json={"text": ["the quick", "a fox"], "max_new_tokens": 5, "do_sample": False,
+                                   "remove_input_from_output": True}).json()
+    assert r["num_generated_tokens"] == [5, 5] and len(r["text"]) == 2 and r["query_id"] == 0
+    r2 = c.post("/generate/", json={"text": "the quick", "max_new_tokens": 5, "do_sample": False}).json()
+    assert r2["text"][0].startswith("the quick") and r2["text"][0].endswith(r["text"][0])
+    t = c.post("/tokenize/", json={"text": ["the quick"]}).json()
+    assert t["token_ids"][0] == tok.encode("the quick")
+    assert c.get("/query_id/").json()["query_id"] == 3
+    assert c.post("/generate/", json={"text": 5}).status_code == 400
+    # HF hub cache layout: models--org--repo/refs/main -> snapshots/<sha>
+    root = tmp_path / "hub" / "models--microsoft--bloom-deepspeed-inference-fp16"
+    (root / "refs").mkdir(parents=True)
+    (root / "snapshots" / "abc123").mkdir(parents=True)
+    (root / "refs" / "main").write_text("abc123\n")
+    got = resolve_hf_cache_path("microsoft/bloom-deepspeed-inference-fp16", str(tmp_path / "hub"))
+    assert got.endswith("snapshots/abc123")
+
+
 def test_gptj_predictor_tensorized_and_text_app(gptj_dir, tmp_path):
     from kubernetes_cloud_amd.io.tensors import serialize
     from kubernetes_cloud_amd.serving.predictors import GPTJPredictor, create_gptj_text_app
