@@ -153,12 +153,20 @@ class CausalLM(nn.Module):
     @torch.no_grad()
     def init_weights(self, std: float = 0.02, seed: int | None = None):
         g = torch.Generator(device="cpu")
+        gd = None
         if seed is not None:
             g.manual_seed(seed)
         for name, p in self.named_parameters():
             if p.dim() >= 2:
                 if p.is_cuda:
-                    p.normal_(0.0, std)
+                    # seeded device generator: every DP rank builds identical weights
+                    if gd is None:
+                        gd = torch.Generator(device=p.device)
+                        if seed is not None:
+                            gd.manual_seed(seed)
+                        else:
+                            gd.seed()
+                    p.normal_(0.0, std, generator=gd)
                 else:
                     p.copy_(torch.randn(p.shape, generator=g) * std)
             elif name.endswith("weight"):

@@ -41,7 +41,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..ops import _lib
-from .optim import FlatAdamW, FlatAdamW8bit
+from .optim import FlatAdamW, FlatAdamW8bit, HostOffloadAdamW
 
 ALIGN = 64
 
@@ -82,9 +82,10 @@ class TrainEngine:
     def __init__(self, model: nn.Module, lr: float = 5e-5, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 0.0, max_grad_norm: float = 1.0, zero_stage: int = 0,
                  grad_accum: int = 1, bucket_elems: int = int(2e8), group=None,
-                 comm_dtype: torch.dtype = torch.float32, loss_scaler=None, optim_bits: int = 32):
+                 comm_dtype: torch.dtype = torch.float32, loss_scaler=None, optim_bits: int = 32,
+                 offload_optimizer: bool = False):
         self.model = model
-        opt_cls = FlatAdamW8bit if optim_bits == 8 else FlatAdamW
+        opt_cls = HostOffloadAdamW if offload_optimizer else (FlatAdamW8bit if optim_bits == 8 else FlatAdamW)
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0

@@ -198,6 +198,7 @@ def main(argv=None):
     # ds_config subset
     zero_stage, betas, eps, wd, clip = args.zero_stage, (0.9, 0.999), 1e-8, 0.01, 1.0
     bucket, comm_dtype, sched_kind = int(2e8), torch.float32, "linear"
+    want_offload = False
     if args.ds_config:
         with open(args.ds_config) as f:
             ds = json.load(f)
@@ -218,14 +219,28 @@ def main(argv=None):
         sched = ds.get("scheduler") or {}
         if sched.get("type") == "WarmupLR":
             sched_kind = "warmup"  # linear warmup then constant (ds_config.json:19-26)
-        if (zo.get("offload_optimizer") or {}).get("device") == "cpu" and main_proc:
-            log.info("ds_config offload_optimizer=cpu: optimizer state stays in HBM (288 GB); offload not needed")
+        want_offload = (zo.get("offload_optimizer") or {}).get("device") == "cpu"
     if zero_stage == 3 and main_proc:
         log.info("ZeRO-3 requested: parameters stay replicated (288 GB HBM), optimizer state sharded")
+    # ds_config offload_optimizer=cpu is honoured when the sharded fp32 optimizer
+    # state would not fit next to the bf16 params + fp32 grads in HBM (or when
+    # forced with KCA_OFFLOAD_OPTIMIZER=1; =0 disables it)
+    offload = False
+    force = os.environ.get("KCA_OFFLOAD_OPTIMIZER")
+    if force is not None:
+        offload = force not in ("0", "false", "no")
+    elif want_offload:
+        n_par = sum(p.numel() for p in model.parameters() if p.requires_grad)
+        shard = world if zero_stage >= 1 else 1
+        need = n_par * 6 + n_par * 12 / shard
+        total = torch.cuda.get_device_properties(dev).total_memory if dev.type == "cuda" else float("inf")
+        offload = need > 0.85 * total
+    if main_proc:
+        log.info("optimizer state: %s", "host (offload_optimizer=cpu, host AdamW)" if offload else "HBM")
 
     engine = TrainEngine(model, lr=args.lr, betas=betas, eps=eps, weight_decay=wd, max_grad_norm=clip,
                          zero_stage=zero_stage, grad_accum=args.gradients, bucket_elems=bucket,
-                         comm_dtype=comm_dtype)
+                         comm_dtype=comm_dtype, offload_optimizer=offload)
     bs = args.bs if args.bs != -1 else estimate_batch_size(model, args.context_size, args.bs_divisor, dev)
     gas = args.gradients
     per_step = bs * gas * world

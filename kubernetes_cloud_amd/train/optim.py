@@ -223,6 +223,111 @@ class FlatAdamW8bit(FlatAdamW):
         self.lr = sd.get("lr", self.lr)
 
 
+class HostOffloadAdamW(FlatAdamW):
+    """ZeRO-Offload style optimizer (N2 + PAR-3's ``offload_optimizer: cpu``,
+    finetuner-workflow/finetuner/ds_config.json:35-37): fp32 master, exp_avg
+    and exp_avg_sq of this rank's shard live in pinned HOST memory and are
+    updated by the AVX-512/AVX2 host AdamW (csrc/cpu/adamw_host.cpp, OpenMP).
+
+    Per step: the grad-norm clip coefficient is computed on the device (no extra
+    traffic), the fp32 grad shard streams D2H in chunks on a copy stream while
+    the host updates the previous chunk, and the bf16 result streams back H2D
+    into the device parameters. Used only when the optimizer state would not
+    fit in HBM (288 GB holds it for every model the
+    reference trains on one node), or when forced for testing.
+    """
+
+    CHUNK = 1 << 24  # elements per D2H / host-update / H2D pipeline stage (64 MB fp32)
+
+    def __init__(self, master: torch.Tensor, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 0.0, wd_mask: torch.Tensor | None = None,
+                 model_bf16: torch.Tensor | None = None, grad: torch.Tensor | None = None):
+        dev = master.device
+        pin = dev.type == "cuda"
+        host_master = torch.empty(master.numel(), dtype=torch.float32, pin_memory=pin)
+        host_master.copy_(master)
+        super().__init__(host_master, lr, betas, eps, weight_decay, None, model_bf16, grad)
+        # the base class put grad / clip scalars on the master's (host) device: keep
+        # the grad where the engine accumulates it and the clip math on that device
+        self.grad = grad if grad is not None else torch.zeros(master.numel(), device=dev)
+        self.device = dev
+        self._coef = torch.ones(1, device=dev, dtype=torch.float32)
+        self._sumsq = torch.zeros(1, device=dev, dtype=torch.float32)
+        self._norm = torch.zeros(1, device=dev, dtype=torch.float32)
+        self._skip = torch.zeros(1, device=dev, dtype=torch.int32)
+        self._ws = torch.empty(1024, device=dev, dtype=torch.float32)
+        self.native = dev.type == "cuda"
+        self.exp_avg = torch.zeros(master.numel(), dtype=torch.float32, pin_memory=pin)
+        self.exp_avg_sq = torch.zeros(master.numel(), dtype=torch.float32, pin_memory=pin)
+        self.wd_mask_host = wd_mask.cpu() if wd_mask is not None else None
+        n = master.numel()
+        c = min(self.CHUNK, n)
+        self._g_host = [torch.empty(c, dtype=torch.float32, pin_memory=pin) for _ in range(2)]
+        self._b_host = [torch.empty(c, dtype=torch.bfloat16, pin_memory=pin) for _ in range(2)]
+        self._scal_host = torch.empty(2, dtype=torch.float32, pin_memory=pin)
+        self._copy = torch.cuda.Stream(device=dev) if pin else None
+
+    def step(self, lr: float | None = None, use_clip: bool = False):
+        from ..io import native
+        lib = native.load()
+        if lr is not None:
+            self.lr = lr
+        self.step_count += 1
+        b1, b2 = self.betas
+        bc1 = 1.0 - b1 ** self.step_count
+        bc2 = 1.0 - b2 ** self.step_count
+        if use_clip:
+            if bool(self._skip.item()):
+                return
+            gs = float(self._coef.item())
+        else:
+            gs = 1.0
+        n = self.master.numel()
+        mask = self.wd_mask_host
+        cuda = self.device.type == "cuda"
+        if cuda:
+            cur = torch.cuda.current_stream(self.device)
+            self._copy.wait_stream(cur)
+        chunks = [(lo, min(n, lo + self.CHUNK)) for lo in range(0, n, self.CHUNK)]
+        ev_in = [None, None]
+
+        def fetch(i):
+            lo, hi = chunks[i]
+            buf = self._g_host[i & 1][: hi - lo]
+            if cuda:
+                with torch.cuda.stream(self._copy):
+                    buf.copy_(self.grad[lo:hi], non_blocking=True)
+                    ev_in[i & 1] = torch.cuda.Event()
+                    ev_in[i & 1].record(self._copy)
+            else:
+                buf.copy_(self.grad[lo:hi])
+            return buf
+
+        pending = fetch(0) if chunks else None
+        for i, (lo, hi) in enumerate(chunks):
+            g = pending
+            if cuda:
+                ev_in[i & 1].synchronize()
+            if i + 1 < len(chunks):
+                pending = fetch(i + 1)
+            pb = self._b_host[i & 1][: hi - lo]
+            mk = mask[lo // 64:(hi + 63) // 64] if mask is not None else None
+            lib.kca_host_adamw(self.master[lo:hi].data_ptr(), g.data_ptr(), self.exp_avg[lo:hi].data_ptr(),
+                               self.exp_avg_sq[lo:hi].data_ptr(), pb.data_ptr(),
+                               mk.data_ptr() if mk is not None else None, hi - lo, float(self.lr), float(b1),
+                               float(b2), float(self.eps), float(self.weight_decay), float(bc1), float(bc2),
+                               float(gs), 0)
+            if self.model_bf16 is not None:
+                if self.model_bf16.dtype != torch.bfloat16:  # fp32 model (CPU runs): exact copy
+                    self.model_bf16[lo:hi].copy_(self.master[lo:hi])
+                elif cuda:
+                    self.model_bf16[lo:hi].copy_(pb, non_blocking=True)
+                    # the host buffer is reused two chunks later: fence its upload
+                    torch.cuda.current_stream(self.device).synchronize()
+                else:
+                    self.model_bf16[lo:hi].copy_(pb)
+
+
 # ----------------------------------------------------------------- schedules
 def lr_at(step: int, base_lr: float, total_steps: int, warmup_steps: int, kind: str = "linear",
           min_lr: float = 0.0) -> float:

@@ -209,3 +209,24 @@ def test_watchdog_catches_hung_rank_and_resume_completes(tmp_path):
     r = subprocess.run(cmd + argv, env=env, cwd=root, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
     assert (rd / "final" / ".ready.txt").exists()
+
+
+def test_finetuner_optimizer_offload_matches_hbm(tmp_path, monkeypatch):
+    """ds_config offload_optimizer=cpu (forced with KCA_OFFLOAD_OPTIMIZER=1) runs the
+    host AdamW path and lands on the same weights as the in-HBM optimizer."""
+    import json
+    from safetensors.torch import load_file
+    model = make_model_dir(str(tmp_path / "model"))
+    data = make_tokens(str(tmp_path / "d.tokens"), n_ctx=16, ctx=32)
+    ds = tmp_path / "ds.json"
+    ds.write_text(json.dumps({"zero_optimization": {"stage": 2, "offload_optimizer": {"device": "cpu"}}}))
+    finals = []
+    for name, force in (("a", "1"), ("b", "0")):
+        monkeypatch.setenv("KCA_OFFLOAD_OPTIMIZER", force)
+        out = tmp_path / name
+        _run(["--run-name", "o", "--model", model, "--dataset", data, "--context-size", "32", "--bs", "2",
+              "--gradients", "1", "--output-path", str(out), "--logs", str(out / "l"), "--save-steps", "0",
+              "--zero-stage", "2", "--lr", "1e-3", "--max-steps", "3", "--ds-config", str(ds)])
+        finals.append(load_file(str(out / "results-o" / "final" / "model.safetensors")))
+    a, b = finals
+    assert max(float((a[k].float() - b[k].float()).abs().max()) for k in a) < 1e-5

@@ -286,3 +286,27 @@ def test_adamw8bit_matches_reference_math():
     assert (a.v_codes.int() - b.v_codes.int()).abs().max() <= 1
     assert _rel(a.m_absmax, b.m_absmax) < 1e-4 and _rel(a.v_absmax, b.v_absmax) < 1e-4
     assert _rel(a.model_bf16.float(), a.master) < 1e-2
+
+
+def test_engine_host_offload_matches_hbm_optimizer():
+    """TrainEngine(offload_optimizer=True): grads stream D2H in chunks, host AdamW
+    updates pinned state, bf16 params stream back -- same weights as the fused
+    device AdamW up to bf16 rounding of the final cast."""
+    from kubernetes_cloud_amd.models.causal_lm import build_model
+    from kubernetes_cloud_amd.models.config import LMConfig, PRESETS_HF
+    from kubernetes_cloud_amd.train.engine import TrainEngine
+    from kubernetes_cloud_amd.train.optim import HostOffloadAdamW
+    cfg = dict(PRESETS_HF["gpt-j-6b"])
+    cfg.update(n_embd=256, n_layer=2, n_head=4, rotary_dim=32, vocab_size=1024)
+    ids = torch.randint(0, 1024, (2, 128), device=DEV)
+    out = []
+    for off in (False, True):
+        m = build_model(LMConfig.from_hf(cfg), device=DEV, dtype=torch.bfloat16, seed=0)
+        HostOffloadAdamW.CHUNK = 1 << 16
+        eng = TrainEngine(m, lr=1e-3, weight_decay=0.01, grad_accum=1, offload_optimizer=off)
+        assert isinstance(eng.opt, HostOffloadAdamW) == off
+        for _ in range(3):
+            eng.train_batch([ids], lambda b: m(b, labels=b))
+        torch.cuda.synchronize()
+        out.append(eng.flat.float().clone())
+    assert _rel(out[0], out[1]) < 2e-3

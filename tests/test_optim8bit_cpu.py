@@ -49,3 +49,30 @@ def test_state_dict_roundtrip():
     o2 = FlatAdamW8bit(o.master.clone(), lr=1e-3)
     o2.load_state_dict(sd)
     assert torch.equal(o2.m_codes, o.m_codes) and o2.step_count == 1
+
+
+def test_host_offload_adamw_matches_device_math():
+    """HostOffloadAdamW (pinned host state + AVX host AdamW, N2) == FlatAdamW."""
+    from kubernetes_cloud_amd.io import native
+    from kubernetes_cloud_amd.train.optim import HostOffloadAdamW
+    if not native.available():
+        import pytest
+        pytest.skip("libkca_host.so not built")
+    torch.manual_seed(2)
+    n = 64 * 300
+    p0 = torch.randn(n)
+    mask = (torch.arange(n // 64) % 2).to(torch.uint8)
+    bf = [torch.empty(n, dtype=torch.bfloat16) for _ in range(2)]
+    a = FlatAdamW(p0.clone(), lr=1e-2, weight_decay=0.1, wd_mask=mask, model_bf16=bf[0])
+    HostOffloadAdamW.CHUNK = 64 * 70  # several pipeline chunks, ragged tail
+    b = HostOffloadAdamW(p0.clone(), lr=1e-2, weight_decay=0.1, wd_mask=mask, model_bf16=bf[1])
+    for it in range(4):
+        g = torch.randn(n)
+        a.grad.copy_(g)
+        b.grad.copy_(g)
+        for o in (a, b):
+            o.set_clip(o.local_sumsq(), 1.0)
+            o.step(use_clip=True)
+    assert torch.allclose(a.master, b.master, atol=1e-6, rtol=1e-5)
+    assert torch.allclose(a.exp_avg_sq, b.exp_avg_sq, atol=1e-7, rtol=1e-5)
+    assert torch.equal(bf[1], b.master.bfloat16())
