@@ -26,6 +26,7 @@ import torch.nn.functional as F
 from torch.utils.checkpoint import checkpoint
 
 from .. import ops
+from ..ops.linear import TLinear
 from .config import LMConfig
 
 
@@ -60,8 +61,8 @@ class Attention(nn.Module):
         self.cfg = cfg
         self.n_heads = cfg.n_heads
         self.head_dim = cfg.head_dim
-        self.qkv = nn.Linear(d, 3 * d, bias=cfg.qkv_bias)
-        self.out = nn.Linear(d, d, bias=cfg.out_bias)
+        self.qkv = TLinear(d, 3 * d, bias=cfg.qkv_bias)
+        self.out = TLinear(d, d, bias=cfg.out_bias)
         self.window = 0
         if cfg.attention_layers and cfg.attention_layers[layer_idx] == "local":
             self.window = cfg.local_window
@@ -100,8 +101,8 @@ class Attention(nn.Module):
 class MLP(nn.Module):
     def __init__(self, cfg: LMConfig):
         super().__init__()
-        self.fc_in = nn.Linear(cfg.hidden, cfg.ffn_dim, bias=cfg.mlp_bias)
-        self.fc_out = nn.Linear(cfg.ffn_dim, cfg.hidden, bias=cfg.mlp_bias)
+        self.fc_in = TLinear(cfg.hidden, cfg.ffn_dim, bias=cfg.mlp_bias)
+        self.fc_out = TLinear(cfg.ffn_dim, cfg.hidden, bias=cfg.mlp_bias)
         self.approx = cfg.gelu_approx
 
     def forward(self, x):
@@ -174,6 +175,20 @@ class CausalLM(nn.Module):
             else:
                 p.zero_()
         return self
+
+    def enable_tn_grads(self, on: bool = True):
+        """TN-layout backward GEMMs for the block linears (ops/linear.py): keeps a
+        transposed bf16 copy of each block weight (+1x the block weights in HBM)."""
+        for m in self.modules():
+            if isinstance(m, TLinear):
+                m.enable_tn(on)
+
+    @torch.no_grad()
+    def refresh_transposed_weights(self):
+        """Re-derive the transposed weight copies after the weights changed."""
+        for m in self.modules():
+            if isinstance(m, TLinear):
+                m.refresh_transposed()
 
     def gradient_checkpointing_enable(self, on: bool = True):
         self.gradient_checkpointing = on

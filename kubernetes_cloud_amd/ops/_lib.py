@@ -53,6 +53,7 @@ _SIGS = {
     "kca_attn_bwd_preprocess": [P, P, P, LL, LL, LL, LL, LL, LL, I, I, I, I, P],
     "kca_attn_bwd": [P] * 10 + [LL] * 21 + [I] * 7 + [F, P, P, P],
     "kca_attn_set_tiled": [I],
+    "kca_transpose_bf16": [P, LL, P, LL, I, I, P],
     "kca_groupnorm_fwd": [P, P, P, P, P, P, P, I, I, I, I, F, I, P],
     "kca_groupnorm_bwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P],
     "kca_skinny_gemm": [P, LL, P, P, P, LL, I, I, I, I, P],

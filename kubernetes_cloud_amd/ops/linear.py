@@ -1,0 +1,97 @@
+"""Linear layers whose backward runs both GEMMs in the K-contiguous ("TN") layout.
+
+PyTorch's Linear backward issues dX = dY W as an NN GEMM and dW = dY^T X as an
+NT GEMM; on MI355X (hipBLASLt, GPT-J shapes, profiles/gemm_layout_gptj_r1.jsonl)
+those run at 1.21-1.31 and 1.10-1.15 PFLOP/s, against 1.43-1.54 for the same
+math with both operands K-contiguous. ``TLinear`` keeps a transposed copy of
+its weight (refreshed after every optimizer step: ~4.5 ms for GPT-J-6B) for
+dX = F.linear(dY, W^T), and transposes dY and X with ``kca_transpose_bf16``
+(HBM-speed, csrc/kernels/transpose.hip) so that dW = F.linear(dY^T, X^T).
+CPU tensors and inference use plain ``F.linear``.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib
+
+
+def transpose(x: torch.Tensor) -> torch.Tensor:
+    """[R, C] -> contiguous [C, R]; native for bf16 GPU tensors with R, C % 64 == 0."""
+    R, C = x.shape
+    if (_lib.use_native(x) and R % 64 == 0 and C % 64 == 0 and x.stride(1) == 1 and x.stride(0) % 8 == 0
+            and x.data_ptr() % 16 == 0):
+        out = torch.empty(C, R, device=x.device, dtype=x.dtype)
+        _lib.call("kca_transpose_bf16", x.data_ptr(), x.stride(0), out.data_ptr(), R, R, C, _lib.stream())
+        return out
+    return x.t().contiguous()
+
+
+def _tn_ok(t: torch.Tensor) -> bool:
+    return t.shape[0] % 64 == 0 and t.shape[1] % 64 == 0
+
+
+class _LinearTN(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, layer):
+        y = F.linear(x, weight, bias)
+        ctx.save_for_backward(x, weight)
+        ctx.layer = layer
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        K, N = x.shape[-1], dy.shape[-1]
+        x2 = x.reshape(-1, K)
+        dy2 = dy.reshape(-1, N).contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            wt = ctx.layer.weight_t
+            dx = (F.linear(dy2, wt) if wt is not None else dy2 @ weight).view(x.shape)
+        if ctx.needs_input_grad[1]:
+            if _tn_ok(dy2) and _tn_ok(x2):
+                dw = F.linear(transpose(dy2), transpose(x2))
+            else:
+                dw = dy2.t() @ x2
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = dy2.sum(0)
+        return dx, dw, db, None
+
+
+class TLinear(nn.Linear):
+    """nn.Linear (same parameters / state dict) with the TN backward above when
+    ``enable_tn(True)`` was called and the input is a bf16 GPU tensor."""
+
+    weight_t: torch.Tensor | None
+
+    def __init__(self, *a, **kw):
+        super().__init__(*a, **kw)
+        self.weight_t = None
+        self._tn = False
+
+    def enable_tn(self, on: bool = True):
+        self._tn = bool(on) and self.weight.is_cuda and self.weight.dtype == torch.bfloat16 \
+            and self.weight.shape[0] % 64 == 0 and self.weight.shape[1] % 64 == 0
+        self.weight_t = torch.empty(self.weight.shape[1], self.weight.shape[0], device=self.weight.device,
+                                    dtype=self.weight.dtype) if self._tn else None
+        self.refresh_transposed()
+
+    @torch.no_grad()
+    def refresh_transposed(self):
+        if self.weight_t is not None:
+            w = self.weight.detach()
+            _lib.call("kca_transpose_bf16", w.data_ptr(), w.stride(0), self.weight_t.data_ptr(), w.shape[0],
+                      w.shape[0], w.shape[1], _lib.stream())
+
+    def forward(self, x):
+        if self._tn and torch.is_grad_enabled() and (x.requires_grad or self.weight.requires_grad) \
+                and x.is_cuda and x.dtype == torch.bfloat16:
+            return _LinearTN.apply(x, self.weight, self.bias, self)
+        return F.linear(x, self.weight, self.bias)
+
+
+__all__ = ["TLinear", "transpose"]

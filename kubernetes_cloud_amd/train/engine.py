@@ -174,6 +174,11 @@ class TrainEngine:
         self._touched = set()
         self._hooks = [s.param.register_post_accumulate_grad_hook(self._hook) for s in slots]
         self.native = dev.type == "cuda"
+        # TN-layout backward GEMMs (ops/linear.py) for models that support them
+        import os
+        if self.native and os.environ.get("KCA_TN_GRADS", "1") not in ("0", "false") \
+                and hasattr(model, "enable_tn_grads"):
+            model.enable_tn_grads(True)
 
     # ------------------------------------------------------------------ hooks
     def _hook(self, p: torch.Tensor):
@@ -303,6 +308,7 @@ class TrainEngine:
                 w.wait()
         if self.loss_scaler is not None and self.loss_scaler.enabled:
             self.loss_scaler.update(bool(self.opt.skipped.item()))
+        self._refresh_derived()
         self._micro = 0
         self._works = []
         self._bucket_done = [0] * len(self.buckets)
@@ -344,6 +350,13 @@ class TrainEngine:
                                             group=self.group)
         else:
             self.flat.copy_(self.opt.master)
+        self._refresh_derived()
+
+    def _refresh_derived(self):
+        """Weights changed: re-derive per-model caches (transposed weight copies)."""
+        fn = getattr(self.model, "refresh_transposed_weights", None)
+        if fn is not None:
+            fn()
 
     def publish(self, master_like: torch.Tensor):
         """Write bf16 model params from an fp32 tensor laid out like the
@@ -357,6 +370,7 @@ class TrainEngine:
                                             group=self.group)
         else:
             self.flat.copy_(master_like)
+        self._refresh_derived()
 
     def remove_hooks(self):
         for h in self._hooks:

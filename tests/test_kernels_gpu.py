@@ -310,3 +310,64 @@ def test_engine_host_offload_matches_hbm_optimizer():
         torch.cuda.synchronize()
         out.append(eng.flat.float().clone())
     assert _rel(out[0], out[1]) < 2e-3
+
+
+@pytest.mark.parametrize("R,C,ld", [(64, 64, 64), (128, 4096, 4096), (4096, 192, 256), (16384, 640, 640)])
+def test_transpose_bf16(R, C, ld):
+    from kubernetes_cloud_amd.ops.linear import transpose
+    base = torch.randn(R, ld, device=DEV).bfloat16()
+    x = base[:, :C]
+    assert torch.equal(transpose(x), x.t().contiguous())
+
+
+def test_tlinear_tn_backward_matches_reference():
+    """TN-layout backward (transposed weight copy for dX, transposed dY / X for
+    dW) equals the plain Linear backward math."""
+    from kubernetes_cloud_amd.ops.linear import TLinear
+    torch.manual_seed(0)
+    lin = TLinear(256, 768, bias=True).to(DEV).bfloat16()
+    lin.enable_tn(True)
+    assert lin.weight_t is not None and torch.equal(lin.weight_t, lin.weight.t().contiguous())
+    x = torch.randn(4, 64, 256, device=DEV).bfloat16().requires_grad_()
+    y = lin(x)
+    g = torch.randn_like(y)
+    y.backward(g)
+    xr = x.detach().float().requires_grad_()
+    wr = lin.weight.detach().float().requires_grad_()
+    br = lin.bias.detach().float().requires_grad_()
+    yr = torch.nn.functional.linear(xr, wr, br)
+    yr.backward(g.float())
+    assert _rel(y, yr) < 1e-2
+    assert _rel(x.grad, xr.grad) < 1e-2
+    assert _rel(lin.weight.grad, wr.grad) < 1e-2
+    assert _rel(lin.bias.grad, br.grad) < 1e-2
+    # weights changed -> refresh
+    with torch.no_grad():
+        lin.weight.add_(1.0)
+    lin.refresh_transposed()
+    assert torch.equal(lin.weight_t, lin.weight.t().contiguous())
+
+
+def test_engine_tn_grads_match_default_backward(monkeypatch):
+    """Training a tiny GPT-J through the engine with and without the TN backward
+    (KCA_TN_GRADS) lands on the same weights up to bf16 rounding."""
+    from kubernetes_cloud_amd.models.causal_lm import build_model
+    from kubernetes_cloud_amd.models.config import LMConfig, PRESETS_HF
+    from kubernetes_cloud_amd.train.engine import TrainEngine
+    cfg = dict(PRESETS_HF["gpt-j-6b"])
+    cfg.update(n_embd=256, n_layer=2, n_head=4, rotary_dim=32, vocab_size=1024)
+    ids = torch.randint(0, 1024, (2, 128), device=DEV)
+    out = []
+    for tn in ("1", "0"):
+        monkeypatch.setenv("KCA_TN_GRADS", tn)
+        m = build_model(LMConfig.from_hf(cfg), device=DEV, dtype=torch.bfloat16, seed=0)
+        eng = TrainEngine(m, lr=1e-3, weight_decay=0.01, grad_accum=1)
+        assert (m.h[0].attn.qkv.weight_t is not None) == (tn == "1")
+        for _ in range(3):
+            eng.train_batch([ids], lambda b: m(b, labels=b))
+        torch.cuda.synchronize()
+        if tn == "1":
+            w = m.h[0].mlp.fc_in
+            assert torch.equal(w.weight_t, w.weight.t().contiguous())  # refreshed after the step
+        out.append(eng.flat.float().clone())
+    assert _rel(out[0], out[1]) < 5e-3
