@@ -113,17 +113,25 @@ static inline int kca_grid(long long work_items, int per_block, int cap = 2048) 
   return (int)g;
 }
 
+// tanh(u) = 1 - 2 / (exp(2u) + 1) on v_exp_f32 + v_rcp_f32: ~1e-7 absolute
+// error, saturates correctly (exp -> inf gives 1, exp -> 0 gives -1), and a
+// fraction of libm tanhf's instructions and registers -- the activation kernels
+// stay memory-bound at full occupancy.
+__device__ __forceinline__ float fast_tanh(float u) {
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(__expf(2.f * u) + 1.f);
+}
+
 __device__ __forceinline__ float gelu_tanh(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
   float u = k0 * (x + k1 * x * x * x);
-  return 0.5f * x * (1.f + tanhf(u));
+  return 0.5f * x * (1.f + fast_tanh(u));
 }
 
 __device__ __forceinline__ float gelu_tanh_grad(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
   float x2 = x * x;
   float u = k0 * (x + k1 * x2 * x);
-  float t = tanhf(u);
+  float t = fast_tanh(u);
   float du = k0 * (1.f + 3.f * k1 * x2);
   return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * du;
 }

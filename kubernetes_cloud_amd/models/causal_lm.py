@@ -117,12 +117,16 @@ class Block(nn.Module):
         self.attn = Attention(cfg, layer_idx)
         self.ln_2 = None if cfg.shared_ln else LayerNorm(cfg.hidden, cfg.ln_eps)
         self.mlp = MLP(cfg)
+        self.fused = None  # ops.fused_block.FusedParallelBlock (GPT-J training path)
 
     def forward(self, h, kv_len, *pending):
         if pending:
             x, h = self.ln_1(h, residual=pending)
         else:
             x = self.ln_1(h)
+        if self.fused is not None and torch.is_grad_enabled() and self.fused.applies(x):
+            a, m = self.fused(x, kv_len)
+            return h, a, m
         if self.cfg.parallel_residual:
             a = self.attn(x, kv_len)
             x2 = x if self.ln_2 is None else self.ln_2(h)
@@ -178,17 +182,34 @@ class CausalLM(nn.Module):
 
     def enable_tn_grads(self, on: bool = True):
         """TN-layout backward GEMMs for the block linears (ops/linear.py): keeps a
-        transposed bf16 copy of each block weight (+1x the block weights in HBM)."""
+        transposed bf16 copy of each block weight (+1x the block weights in HBM).
+        GPT-J-shaped blocks additionally run their training forward/backward
+        through ops/fused_block.py (GELU, bias grads and operand transposes
+        folded into single passes; KCA_FUSED_BLOCK=0 keeps the per-module
+        autograd path)."""
+        import os
+
+        from ..ops import fused_block
+        fuse = (on and os.environ.get("KCA_FUSED_BLOCK", "1") not in ("0", "false")
+                and fused_block.eligible(self.cfg))
+        for blk in self.h:
+            w = blk.attn.qkv.weight
+            blk.fused = None
+            if fuse and w.is_cuda and w.dtype == torch.bfloat16:
+                blk.fused = fused_block.FusedParallelBlock(blk)
         for m in self.modules():
             if isinstance(m, TLinear):
                 m.enable_tn(on)
 
     @torch.no_grad()
     def refresh_transposed_weights(self):
-        """Re-derive the transposed weight copies after the weights changed."""
+        """Re-derive the transposed / concatenated weight copies after the weights changed."""
         for m in self.modules():
             if isinstance(m, TLinear):
                 m.refresh_transposed()
+        for blk in self.h:
+            if blk.fused is not None:
+                blk.fused.refresh()
 
     def gradient_checkpointing_enable(self, on: bool = True):
         self.gradient_checkpointing = on

@@ -54,6 +54,11 @@ _SIGS = {
     "kca_attn_bwd": [P] * 10 + [LL] * 21 + [I] * 7 + [F, P, P, P],
     "kca_attn_set_tiled": [I],
     "kca_transpose_bf16": [P, LL, P, LL, I, I, P],
+    "kca_gelu_fwd_t": [P, LL, P, LL, P, LL, I, I, I, P],
+    "kca_gelu_bwd_t": [P, LL, P, LL, P, LL, P, LL, P, I, I, I, P],
+    "kca_transpose_colsum": [P, LL, P, LL, P, I, I, P],
+    "kca_col_reduce_f32": [P, I, I, P, P, P],
+    "kca_accum_grad_2d": [P, P, LL, I, I, F, I, P],
     "kca_groupnorm_fwd": [P, P, P, P, P, P, P, I, I, I, I, F, I, P],
     "kca_groupnorm_bwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P],
     "kca_skinny_gemm": [P, LL, P, P, P, LL, I, I, I, I, P],

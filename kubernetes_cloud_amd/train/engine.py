@@ -40,7 +40,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
-from ..ops import _lib
+from ..ops import _lib, grad_sink
 from .optim import FlatAdamW, FlatAdamW8bit, HostOffloadAdamW
 
 ALIGN = 64
@@ -173,6 +173,8 @@ class TrainEngine:
         self._bucket_launched = [False] * len(buckets)
         self._touched = set()
         self._hooks = [s.param.register_post_accumulate_grad_hook(self._hook) for s in slots]
+        for s in slots:
+            grad_sink.register(s.param, self._accum)
         self.native = dev.type == "cuda"
         # TN-layout backward GEMMs (ops/linear.py) for models that support them
         import os
@@ -182,21 +184,34 @@ class TrainEngine:
 
     # ------------------------------------------------------------------ hooks
     def _hook(self, p: torch.Tensor):
-        s = self._by_param[id(p)]
         g = p.grad
+        if g is None:  # the op handed this gradient to the sink (autograd still fires the hook)
+            return
+        p.grad = None
+        self._accum(p, g)
+
+    def _accum(self, p: torch.Tensor, g: torch.Tensor):
+        """Add one micro-batch gradient of ``p`` into the fp32 flat buffer and
+        launch its bucket's collective once the bucket is complete. Also the
+        gradient sink (ops/grad_sink.py) that fused ops (ops/fused_block.py) call
+        directly with row-strided column slices of a concatenated-weight dW."""
+        s = self._by_param[id(p)]
         dst = self.grad[s.offset:s.offset + s.numel]
         first = id(p) not in self._touched
         scale = 1.0 / self.grad_accum
         if self.native and g.dtype == torch.bfloat16 and g.is_contiguous():
             _lib.call("kca_accum_grad", dst.data_ptr(), g.data_ptr(), scale, int(first), s.numel,
                       _lib.stream())
+        elif (self.native and g.dtype == torch.bfloat16 and g.dim() == 2 and g.stride(1) == 1
+              and g.shape[1] % 8 == 0 and g.stride(0) % 8 == 0 and g.data_ptr() % 16 == 0):
+            _lib.call("kca_accum_grad_2d", dst.data_ptr(), g.data_ptr(), g.stride(0), g.shape[0], g.shape[1],
+                      scale, int(first), _lib.stream())
         else:
             if first:
                 dst.copy_(g.reshape(-1).float() * scale)
             else:
                 dst.add_(g.reshape(-1).float(), alpha=scale)
         self._touched.add(id(p))
-        p.grad = None
         if self._last_micro and self.world > 1:
             self._bucket_done[s.bucket] += 1
             if self._bucket_done[s.bucket] == len(self.buckets[s.bucket].slots):
@@ -376,6 +391,8 @@ class TrainEngine:
         for h in self._hooks:
             h.remove()
         self._hooks = []
+        for s in self.slots:
+            grad_sink.unregister(s.param)
 
 
 def count_tokens_flops(cfg, seq: int) -> float:

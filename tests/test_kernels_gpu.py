@@ -358,6 +358,7 @@ def test_engine_tn_grads_match_default_backward(monkeypatch):
     cfg.update(n_embd=256, n_layer=2, n_head=4, rotary_dim=32, vocab_size=1024)
     ids = torch.randint(0, 1024, (2, 128), device=DEV)
     out = []
+    monkeypatch.setenv("KCA_FUSED_BLOCK", "0")
     for tn in ("1", "0"):
         monkeypatch.setenv("KCA_TN_GRADS", tn)
         m = build_model(LMConfig.from_hf(cfg), device=DEV, dtype=torch.bfloat16, seed=0)
@@ -370,4 +371,106 @@ def test_engine_tn_grads_match_default_backward(monkeypatch):
             w = m.h[0].mlp.fc_in
             assert torch.equal(w.weight_t, w.weight.t().contiguous())  # refreshed after the step
         out.append(eng.flat.float().clone())
+    assert _rel(out[0], out[1]) < 5e-3
+
+
+@pytest.mark.parametrize("tanh", [True, False])
+def test_block_fusion_tile_kernels(tanh):
+    """gelu_fwd_t / gelu_bwd_t / transpose_colsum / col_reduce / accum_grad_2d
+    against fp32 PyTorch on strided views (csrc/kernels/block_fusion.hip)."""
+    torch.manual_seed(0)
+    st = _lib.stream()
+    R, C, ld = 512, 768, 1024
+    approx = "tanh" if tanh else "none"
+    hb = torch.randn(R, ld, device=DEV).bfloat16()
+    h = hb[:, 128:128 + C]
+    g = torch.empty(R, ld, device=DEV, dtype=torch.bfloat16)[:, :C]
+    gt = torch.empty(C, R, device=DEV, dtype=torch.bfloat16)
+    _lib.call("kca_gelu_fwd_t", h.data_ptr(), ld, g.data_ptr(), ld, gt.data_ptr(), R, R, C, int(tanh), st)
+    ref = F.gelu(h.float(), approximate=approx)
+    assert _rel(g, ref) < 5e-3
+    assert torch.equal(gt, g.t().contiguous())
+    dg = torch.randn(R, C, device=DEV).bfloat16()
+    dh = torch.empty(R, ld, device=DEV, dtype=torch.bfloat16)[:, 64:64 + C]
+    dht = torch.empty(C, R, device=DEV, dtype=torch.bfloat16)
+    part = torch.empty(R // 64, C, device=DEV)
+    _lib.call("kca_gelu_bwd_t", dg.data_ptr(), C, h.data_ptr(), ld, dh.data_ptr(), ld, dht.data_ptr(), R,
+              part.data_ptr(), R, C, int(tanh), st)
+    hr = h.float().requires_grad_()
+    F.gelu(hr, approximate=approx).backward(dg.float())
+    assert _rel(dh, hr.grad) < 5e-3
+    assert torch.equal(dht, dh.t().contiguous())
+    db = torch.empty(C, device=DEV, dtype=torch.bfloat16)
+    _lib.call("kca_col_reduce_f32", part.data_ptr(), R // 64, C, db.data_ptr(), None, st)
+    assert _rel(db, hr.grad.sum(0)) < 1e-2
+    x = torch.randn(R, C, device=DEV).bfloat16()
+    xt = torch.empty(C, R, device=DEV, dtype=torch.bfloat16)
+    _lib.call("kca_transpose_colsum", x.data_ptr(), C, xt.data_ptr(), R, part.data_ptr(), R, C, st)
+    assert torch.equal(xt, x.t().contiguous())
+    cs = torch.empty(C, device=DEV)
+    _lib.call("kca_col_reduce_f32", part.data_ptr(), R // 64, C, None, cs.data_ptr(), st)
+    assert _rel(cs, x.float().sum(0)) < 1e-5
+    acc = torch.randn(R, 256, device=DEV)
+    a0 = acc.clone()
+    src = x[:, 128:384]
+    _lib.call("kca_accum_grad_2d", acc.data_ptr(), src.data_ptr(), C, R, 256, 0.5, 0, st)
+    assert torch.allclose(acc, a0 + 0.5 * src.float(), atol=1e-6)
+    _lib.call("kca_accum_grad_2d", acc.data_ptr(), src.data_ptr(), C, R, 256, 0.25, 1, st)
+    assert torch.allclose(acc, 0.25 * src.float(), atol=1e-6)
+
+
+def _tiny_gptj(n_embd, n_head, rot, layers=2):
+    from kubernetes_cloud_amd.models.config import LMConfig, PRESETS_HF
+    cfg = dict(PRESETS_HF["gpt-j-6b"])
+    cfg.update(n_embd=n_embd, n_layer=layers, n_head=n_head, rotary_dim=rot, vocab_size=1024)
+    return LMConfig.from_hf(cfg)
+
+
+@pytest.mark.parametrize("n_embd,n_head,S", [(256, 4, 128), (1024, 4, 256)])
+def test_fused_block_matches_module_path(n_embd, n_head, S):
+    """The fused GPT-J block (ops/fused_block.py) gives the loss and gradients
+    of the per-module path (head_dim 64 generic / 256 tiled attention)."""
+    from kubernetes_cloud_amd.models.causal_lm import build_model
+    torch.manual_seed(0)
+    m = build_model(_tiny_gptj(n_embd, n_head, 32), device=DEV, dtype=torch.bfloat16, seed=0)
+    ids = torch.randint(0, 1024, (2, S), device=DEV)
+    res = []
+    for fused in (True, False):
+        m.zero_grad(set_to_none=True)
+        m.enable_tn_grads(True)
+        if not fused:
+            for blk in m.h:
+                blk.fused = None
+        else:
+            assert all(blk.fused is not None for blk in m.h)
+        loss = m(ids, labels=ids)
+        loss.backward()
+        res.append((loss.item(), {n: p.grad.float().clone() for n, p in m.named_parameters()}))
+    (l0, g0), (l1, g1) = res
+    assert abs(l0 - l1) < 2e-2 * abs(l1)
+    for n in g1:
+        assert _rel(g0[n], g1[n]) < 3e-2, n
+
+
+def test_engine_fused_block_matches_unfused(monkeypatch):
+    """Engine training (GAS 2: first-write + accumulate through the gradient
+    sinks) with and without the fused block lands on the same weights up to
+    bf16 rounding; transposed weight copies follow the weights."""
+    from kubernetes_cloud_amd.models.causal_lm import build_model
+    from kubernetes_cloud_amd.train.engine import TrainEngine
+    ids = [torch.randint(0, 1024, (2, 128), device=DEV) for _ in range(2)]
+    out = []
+    for fb in ("1", "0"):
+        monkeypatch.setenv("KCA_FUSED_BLOCK", fb)
+        m = build_model(_tiny_gptj(256, 4, 32), device=DEV, dtype=torch.bfloat16, seed=0)
+        eng = TrainEngine(m, lr=1e-3, weight_decay=0.01, grad_accum=2)
+        assert (m.h[0].fused is not None) == (fb == "1")
+        for _ in range(3):
+            eng.train_batch(ids, lambda b: m(b, labels=b))
+        torch.cuda.synchronize()
+        if fb == "1":
+            w = m.h[1].mlp.fc_out
+            assert torch.equal(w.weight_t, w.weight.t().contiguous())  # refreshed after the step
+        out.append(eng.flat.float().clone())
+        eng.remove_hooks()
     assert _rel(out[0], out[1]) < 5e-3
