@@ -21,14 +21,22 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch
 
+from kubernetes_cloud_amd.utils import miopen as _miopen  # noqa: E402
+
+_miopen.configure()
+
 
 def build(dev, dtype):
     from kubernetes_cloud_amd.models.clip_text import CLIPTextConfig, build_clip_text
     from kubernetes_cloud_amd.models.unet import UNetConfig, build_unet
     from kubernetes_cloud_amd.models.vae import VAEConfig, build_vae
+    from kubernetes_cloud_amd.models.unet import to_channels_last
     unet = build_unet(UNetConfig(), device=dev, dtype=dtype)
     vae = build_vae(VAEConfig(), device=dev, dtype=dtype)
     te = build_clip_text(CLIPTextConfig(), device=dev, dtype=dtype)
+    if os.environ.get("KCA_SD_CHANNELS_LAST", "1") not in ("0", "false"):
+        to_channels_last(unet)
+        to_channels_last(vae)
     return unet, vae, te
 
 
@@ -62,8 +70,11 @@ def bench_train(args, dev):
         eng.step(5e-6)
         return loss
 
-    for _ in range(args.warmup):
+    for i in range(args.warmup):
+        tw = time.perf_counter()
         step()
+        torch.cuda.synchronize()
+        print(f"[sd_bench] train warmup {i}: {time.perf_counter() - tw:.1f}s", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -98,8 +109,11 @@ def bench_infer(args, dev):
             x = sch.step(eu + g * (ec - eu), t, x).float()
         return vae.decode((x / 0.18215).to(torch.bfloat16))
 
-    for _ in range(args.warmup):
+    for i in range(args.warmup):
+        tw = time.perf_counter()
         run()
+        torch.cuda.synchronize()
+        print(f"[sd_bench] infer warmup {i}: {time.perf_counter() - tw:.1f}s", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):

@@ -22,7 +22,7 @@ import torch
 
 from .clip_text import CLIPTextConfig, CLIPTextModel
 from .schedulers import load_scheduler, sd_scheduler_config
-from .unet import UNet2DConditionModel, UNetConfig
+from .unet import UNet2DConditionModel, UNetConfig, to_channels_last
 from .vae import L_SCALE_FACTOR, AutoencoderKL, VAEConfig
 
 
@@ -76,6 +76,14 @@ class StableDiffusionPipeline:
         self.unet, self.vae, self.text_encoder = unet, vae, text_encoder
         self.tokenizer, self.scheduler = tokenizer, scheduler
         self.scaling_factor = scaling_factor
+        self._layout()
+
+    def _layout(self):
+        """On the GPU the UNet and VAE run channels-last end to end (NHWC MIOpen
+        convolutions + NHWC GroupNorm kernels; models/unet.py:to_channels_last)."""
+        if next(self.unet.parameters()).is_cuda:
+            to_channels_last(self.unet)
+            to_channels_last(self.vae)
 
     @property
     def device(self):
@@ -88,6 +96,7 @@ class StableDiffusionPipeline:
     def to(self, device=None, dtype=None):
         for m in (self.unet, self.vae, self.text_encoder):
             m.to(device=device, dtype=dtype)
+        self._layout()
         return self
 
     # ------------------------------------------------------------------ I/O

@@ -212,6 +212,15 @@ class Transformer2DModel(nn.Module):
         B, C, H, W = x.shape
         res = x
         h = ops.group_norm(x, self.norm.num_groups, self.norm.weight, self.norm.bias, self.norm.eps)
+        if _is_cl(h):
+            # channels-last: the [B, HW, C] token view is free and the 1x1 proj
+            # convs are plain GEMMs on it
+            t = h.permute(0, 2, 3, 1).reshape(B, H * W, C)
+            t = _proj(self.proj_in, t)
+            for blk in self.transformer_blocks:
+                t = blk(t, ctx)
+            t = _proj(self.proj_out, t)
+            return t.view(B, H, W, C).permute(0, 3, 1, 2) + res
         if self.linear_proj:
             h = self.proj_in(h.permute(0, 2, 3, 1).reshape(B, H * W, C))
         else:
@@ -225,6 +234,31 @@ class Transformer2DModel(nn.Module):
         return h + res
 
 
+def _is_cl(x: torch.Tensor) -> bool:
+    return x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last) and not x.is_contiguous()
+
+
+def _proj(m: nn.Module, t: torch.Tensor) -> torch.Tensor:
+    """nn.Linear, or a 1x1 nn.Conv2d applied as the same GEMM on a token view."""
+    if isinstance(m, nn.Linear):
+        return m(t)
+    return F.linear(t, m.weight.reshape(m.weight.shape[0], m.weight.shape[1]), m.bias)
+
+
+def to_channels_last(model: nn.Module, weights: bool = True) -> nn.Module:
+    """Run a UNet / VAE channels-last end to end on MI355X: NHWC activations
+    (MIOpen's NHWC convolutions without per-call layout transposes, NHWC
+    GroupNorm kernels, free token views for attention). ``weights`` also
+    converts the conv weights (inference); a training engine that owns the
+    weights in a flat buffer keeps them NCHW."""
+    from ..utils import miopen
+    miopen.configure()
+    model.channels_last = True
+    if weights:
+        model.to(memory_format=torch.channels_last)
+    return model
+
+
 class Downsample2D(nn.Module):
     def __init__(self, ch, pad=1):
         super().__init__()
@@ -233,7 +267,10 @@ class Downsample2D(nn.Module):
 
     def forward(self, x):
         if self.asym:
+            cl = _is_cl(x)
             x = F.pad(x, (0, 1, 0, 1))
+            if cl:
+                x = x.contiguous(memory_format=torch.channels_last)
         return self.conv(x)
 
 
@@ -337,6 +374,7 @@ class UNet2DConditionModel(nn.Module):
         self.conv_norm_out = GroupNorm(g, ch[0], eps, silu=True)
         self.conv_out = nn.Conv2d(ch[0], c.out_channels, 3, padding=1)
         self.gradient_checkpointing = False
+        self.channels_last = False
 
     def enable_gradient_checkpointing(self, on: bool = True):
         self.gradient_checkpointing = on
@@ -355,6 +393,8 @@ class UNet2DConditionModel(nn.Module):
         temb = timestep_embedding(t, c.block_out_channels[0], c.flip_sin_to_cos, c.freq_shift).to(sample.dtype)
         temb = self.time_embedding(temb)
         ctx = encoder_hidden_states.to(sample.dtype)
+        if self.channels_last:
+            sample = sample.contiguous(memory_format=torch.channels_last)
         x = self.conv_in(sample)
         skips = [x]
         for blk in self.down_blocks:
@@ -366,7 +406,7 @@ class UNet2DConditionModel(nn.Module):
             mine = skips[-n:]
             del skips[-n:]
             x = self._run(lambda a, b, cc, *sk, _blk=blk: _blk(a, list(sk), b, cc), x, temb, ctx, *mine)
-        return self.conv_out(self.conv_norm_out(x))
+        return self.conv_out(self.conv_norm_out(x)).contiguous()
 
 
 def build_unet(cfg: UNetConfig, device="cpu", dtype=torch.float32, seed: int = 0) -> UNet2DConditionModel:

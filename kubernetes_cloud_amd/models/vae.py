@@ -189,12 +189,16 @@ class AutoencoderKL(nn.Module):
         lc = config.latent_channels
         self.quant_conv = nn.Conv2d(2 * lc, 2 * lc, 1)
         self.post_quant_conv = nn.Conv2d(lc, lc, 1)
+        self.channels_last = False  # unet.to_channels_last
+
+    def _in(self, x):
+        return x.contiguous(memory_format=torch.channels_last) if self.channels_last else x
 
     def encode(self, x: torch.Tensor) -> DiagonalGaussian:
-        return DiagonalGaussian(self.quant_conv(self.encoder(x)))
+        return DiagonalGaussian(self.quant_conv(self.encoder(self._in(x))).contiguous())
 
     def decode(self, z: torch.Tensor) -> torch.Tensor:
-        return self.decoder(self.post_quant_conv(z))
+        return self.decoder(self.post_quant_conv(self._in(z))).contiguous()
 
 
 def build_vae(cfg: VAEConfig, device="cpu", dtype=torch.float32, seed: int = 0) -> AutoencoderKL:

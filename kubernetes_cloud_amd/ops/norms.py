@@ -121,9 +121,52 @@ class _GroupNormFn(torch.autograd.Function):
         return dx, dw, (db if bias is not None else None), None, None, None
 
 
+class _GroupNormNHWCFn(torch.autograd.Function):
+    """Channels-last [N, C, H, W] (memory NHWC): csrc/kernels/groupnorm_nhwc.hip."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, groups, eps, silu):
+        n, c = x.shape[0], x.shape[1]
+        p = x.numel() // (n * c)
+        y = torch.empty_like(x)
+        mean = torch.empty(n * groups, device=x.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        ws = torch.empty(_lib.require().kca_groupnorm_nhwc_ws(n, p, c), device=x.device, dtype=torch.float32)
+        _lib.call("kca_groupnorm_nhwc_fwd", x.data_ptr(), weight.data_ptr(), _lib.ptr(bias), y.data_ptr(),
+                  mean.data_ptr(), rstd.data_ptr(), ws.data_ptr(), n, p, c, groups, float(eps), int(silu),
+                  _lib.stream())
+        ctx.save_for_backward(x, weight, bias, mean, rstd)
+        ctx.groups, ctx.silu = groups, silu
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, bias, mean, rstd = ctx.saved_tensors
+        n, c = x.shape[0], x.shape[1]
+        p = x.numel() // (n * c)
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = torch.empty_like(x)
+        dw = torch.empty_like(weight)
+        db = torch.empty_like(weight) if bias is not None else None
+        ws = torch.empty(_lib.require().kca_groupnorm_nhwc_ws(n, p, c) + 2 * n * ctx.groups, device=x.device,
+                         dtype=torch.float32)
+        _lib.call("kca_groupnorm_nhwc_bwd", dy.data_ptr(), x.data_ptr(), weight.data_ptr(), _lib.ptr(bias),
+                  mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(), dw.data_ptr(), _lib.ptr(db), ws.data_ptr(),
+                  n, p, c, ctx.groups, int(ctx.silu), _lib.stream())
+        return dx, dw, db, None, None, None
+
+
+def _channels_last(x: torch.Tensor) -> bool:
+    return x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last) and not x.is_contiguous()
+
+
 def group_norm(x: torch.Tensor, groups: int, weight: torch.Tensor, bias: torch.Tensor | None,
                eps: float = 1e-5, silu: bool = False) -> torch.Tensor:
-    """GroupNorm over NC* tensors, optionally fused with SiLU (UNet/VAE ResNet blocks)."""
+    """GroupNorm over NC* tensors, optionally fused with SiLU (UNet/VAE ResNet blocks).
+    Channels-last 4-D inputs stay channels-last (NHWC kernels)."""
+    if (_lib.use_native(x) and x.dtype == torch.bfloat16 and _channels_last(x) and x.shape[1] % 8 == 0
+            and weight is not None and _lib.has("kca_groupnorm_nhwc_fwd")):
+        return _GroupNormNHWCFn.apply(x, weight, bias, groups, eps, silu)
     if _lib.use_native(x) and x.dtype == torch.bfloat16 and _lib.has("kca_groupnorm_fwd"):
         return _GroupNormFn.apply(x, weight, bias, groups, eps, silu)
     if _lib.use_native(x) and x.dtype == torch.bfloat16:

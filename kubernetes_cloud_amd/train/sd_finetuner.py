@@ -186,6 +186,11 @@ def main(argv=None):
     if args.use_8bit_adam and info.is_main:
         print("--use_8bit_adam: block-wise 8-bit AdamW states (kca_adamw8bit)", file=sys.stderr)
     unet.train()
+    if next(unet.parameters()).is_cuda:
+        from ..models.unet import to_channels_last
+        # NHWC activations end to end; the engine owns the (NCHW) weights in its flat buffer
+        to_channels_last(unet, weights=False)
+        to_channels_last(vae)
     eng = TrainEngine(unet, lr=args.lr, betas=(args.adam_beta1, args.adam_beta2), eps=args.adam_epsilon,
                       weight_decay=args.adam_weight_decay, max_grad_norm=1.0,
                       zero_stage=args.zero_stage if world > 1 else 0, grad_accum=1,

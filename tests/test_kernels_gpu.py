@@ -261,6 +261,55 @@ def test_groupnorm(N, C, H, W, G, silu):
     assert _rel(b.grad, br.grad) < 2e-2
 
 
+@pytest.mark.parametrize("N,C,H,W,G,silu", [(2, 320, 16, 16, 32, True), (1, 128, 64, 64, 32, False),
+                                            (2, 1280, 8, 8, 32, True), (1, 40, 5, 7, 8, True),
+                                            (2, 640, 72, 72, 32, False), (2, 2560, 16, 16, 32, True)])
+def test_groupnorm_nhwc(N, C, H, W, G, silu):
+    """Channels-last GroupNorm(+SiLU) (csrc/kernels/groupnorm_nhwc.hip): cg = 10
+    straddles 16-B vectors, odd pixel counts, > 64 chunks of 64 pixels."""
+    torch.manual_seed(0)
+    x0 = torch.randn(N, C, H, W, device=DEV) * 2 + 3
+    x = x0.bfloat16().contiguous(memory_format=torch.channels_last).requires_grad_()
+    w = (1 + 0.1 * torch.randn(C, device=DEV)).bfloat16().requires_grad_()
+    b = (0.1 * torch.randn(C, device=DEV)).bfloat16().requires_grad_()
+    y = ops.group_norm(x, G, w, b, 1e-5, silu=silu)
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, b))
+    yr = F.group_norm(xr, G, wr, br, 1e-5)
+    if silu:
+        yr = F.silu(yr)
+    assert _rel(y, yr) < 1e-2
+    g = torch.randn_like(y)
+    y.backward(g)
+    yr.backward(g.float())
+    assert _rel(x.grad, xr.grad) < 2e-2
+    assert _rel(w.grad, wr.grad) < 2e-2
+    assert _rel(b.grad, br.grad) < 2e-2
+
+
+def test_unet_channels_last_matches_nchw_on_gpu():
+    """bf16 SD-shaped UNet slice: channels-last forward+backward == NCHW within bf16 noise."""
+    from kubernetes_cloud_amd.models.unet import UNetConfig, build_unet, to_channels_last
+    torch.manual_seed(0)
+    cfg = UNetConfig(block_out_channels=(320, 640, 640, 640), cross_attention_dim=64, sample_size=16)
+    u = build_unet(cfg, device=DEV, dtype=torch.bfloat16)
+    x = torch.randn(2, 4, 16, 16, device=DEV).bfloat16()
+    ctx = torch.randn(2, 7, 64, device=DEV).bfloat16()
+    t = torch.tensor([10, 500], device=DEV)
+    out = []
+    for cl in (False, True):
+        if cl:
+            to_channels_last(u)
+        u.zero_grad(set_to_none=True)
+        y = u(x, t, ctx)
+        y.float().square().mean().backward()
+        out.append((y.float(), u.conv_in.weight.grad.float().clone(), u.up_blocks[1].resnets[0].norm1.weight.grad.float().clone()))
+    # output to bf16 noise; weight grads after ~30 bf16 layers of backward through
+    # different MIOpen conv algorithms (NHWC vs NCHW solvers) drift a few percent
+    for a, b, tol in zip(out[0], out[1], (3e-2, 8e-2, 8e-2)):
+        assert _rel(b, a) < tol
+
+
 def test_adamw8bit_matches_reference_math():
     """kca_adamw8bit vs the torch implementation of the same block-wise 8-bit
     AdamW (FlatAdamW8bit with native=False) over several steps, ragged tail."""

@@ -123,3 +123,28 @@ def test_sd_parser_rejects_partial_dreambooth():
         parse_args(["--instance_dataset", "x"])
     with pytest.raises(SystemExit):
         parse_args([])
+
+
+def test_unet_vae_channels_last_match_nchw():
+    """Channels-last UNet / VAE (the MI355X layout: NHWC convs, NHWC GroupNorm,
+    1x1 projections as token GEMMs) compute the same function as NCHW."""
+    from kubernetes_cloud_amd.models.unet import to_channels_last
+    torch.manual_seed(0)
+    u = build_unet(UNetConfig(block_out_channels=(32, 64, 64, 64), cross_attention_dim=32, attention_head_dim=4,
+                              norm_num_groups=8, sample_size=16))
+    v = build_vae(VAEConfig(block_out_channels=(16, 32), layers_per_block=1, norm_num_groups=8, sample_size=32))
+    x = torch.randn(2, 4, 16, 16)
+    ctx = torch.randn(2, 7, 32)
+    img = torch.randn(2, 3, 32, 32)
+    with torch.no_grad():
+        ref = u(x, torch.tensor([10, 500]), ctx)
+        ref_d = v.decode(x[:, :, :8, :8])
+        ref_e = v.encode(img).mean
+        to_channels_last(u)
+        to_channels_last(v)
+        out = u(x, torch.tensor([10, 500]), ctx)
+        out_d = v.decode(x[:, :, :8, :8])
+        out_e = v.encode(img).mean
+    assert out.is_contiguous() and out_d.is_contiguous()
+    for a, b in ((out, ref), (out_d, ref_d), (out_e, ref_e)):
+        assert torch.allclose(a, b, atol=1e-4, rtol=1e-4), (a - b).abs().max()
