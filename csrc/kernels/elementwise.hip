@@ -271,3 +271,63 @@ KCA_API int kca_cast_f32_bf16(const float* x, void* y, long long n,
                      dim3(256), 0, stream, x, (bf16_t*)y, n / 8);
   return 0;
 }
+
+// GEGLU (K17, diffusers FeedForward in every UNet transformer block):
+// x = [a | g] per row (2*I wide, the GEMM output), y = a * gelu_erf(g).
+// One pass over x instead of chunk + fp32 cast + GELU + cast + multiply.
+// Backward writes dx = [dy * gelu(g) | dy * a * gelu'(g)].
+__global__ void geglu_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int i8, long long n8) {
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < n8;
+       t += (long long)gridDim.x * blockDim.x) {
+    const long long row = t / i8;
+    const int c = (int)(t - row * i8) * 8;
+    const bf16_t* xr = x + row * (16LL * i8);
+    float a[8], g[8];
+    load8(xr + c, a);
+    load8(xr + 8LL * i8 + c, g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] *= gelu_erf(g[j]);
+    store8(y + t * 8, a);
+  }
+}
+
+__global__ void geglu_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                 bf16_t* __restrict__ dx, int i8, long long n8) {
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < n8;
+       t += (long long)gridDim.x * blockDim.x) {
+    const long long row = t / i8;
+    const int c = (int)(t - row * i8) * 8;
+    const long long ro = row * (16LL * i8);
+    float a[8], g[8], d[8];
+    load8(x + ro + c, a);
+    load8(x + ro + 8LL * i8 + c, g);
+    load8(dy + t * 8, d);
+    float da[8], dg[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      da[j] = d[j] * gelu_erf(g[j]);
+      dg[j] = d[j] * a[j] * gelu_erf_grad(g[j]);
+    }
+    store8(dx + ro + c, da);
+    store8(dx + ro + 8LL * i8 + c, dg);
+  }
+}
+
+// x: [rows, 2*inner], y/dy: [rows, inner]; inner % 8 == 0
+KCA_API int kca_geglu_fwd(const void* x, void* y, long long rows, int inner, hipStream_t stream) {
+  if (inner % 8) return 1;
+  const long long n8 = rows * (inner / 8);
+  if (n8 == 0) return 0;
+  hipLaunchKernelGGL(geglu_fwd_kernel, dim3(kca_grid(n8, 256, 8192)), dim3(256), 0, stream, (const bf16_t*)x,
+                     (bf16_t*)y, inner / 8, n8);
+  return 0;
+}
+
+KCA_API int kca_geglu_bwd(const void* dy, const void* x, void* dx, long long rows, int inner, hipStream_t stream) {
+  if (inner % 8) return 1;
+  const long long n8 = rows * (inner / 8);
+  if (n8 == 0) return 0;
+  hipLaunchKernelGGL(geglu_bwd_kernel, dim3(kca_grid(n8, 256, 8192)), dim3(256), 0, stream, (const bf16_t*)dy,
+                     (const bf16_t*)x, (bf16_t*)dx, inner / 8, n8);
+  return 0;
+}

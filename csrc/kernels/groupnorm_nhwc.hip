@@ -61,6 +61,7 @@ __global__ void __launch_bounds__(256) nhwc_chunk_stats(const bf16_t* __restrict
 #pragma unroll
   for (int j = 0; j < 8; ++j) mean[j] = m2[j] = 0.f;
   const bf16_t* base = x + ((long long)n * P) * C + cv * 8;
+#pragma unroll 4
   for (int p = p0 + r; live && p < p1; p += R) {
     float v[8];
     load8(base + (long long)p * C, v);
@@ -98,7 +99,8 @@ __global__ void __launch_bounds__(256) nhwc_chunk_stats(const bf16_t* __restrict
 // grid N*G, block 256: merge (chunk, channel) partials of one group
 __global__ void __launch_bounds__(256) nhwc_group_stats(const float* __restrict__ part, int P, int C, int G,
                                                         int nchunks, float eps, float* __restrict__ mean_out,
-                                                        float* __restrict__ rstd_out) {
+                                                        float* __restrict__ rstd_out, const bf16_t* __restrict__ w,
+                                                        const bf16_t* __restrict__ b, float* __restrict__ ss) {
   __shared__ float red[3 * 256];
   const int ng = blockIdx.x, n = ng / G, g = ng % G, cg = C / G;
   const int items = nchunks * cg, CH = chunk_of(P);
@@ -123,27 +125,35 @@ __global__ void __launch_bounds__(256) nhwc_group_stats(const float* __restrict_
     }
     __syncthreads();
   }
+  const float mu_g = red[256], rs_g = rsqrtf(red[512] / red[0] + eps);
   if (threadIdx.x == 0) {
-    mean_out[ng] = red[256];
-    rstd_out[ng] = rsqrtf(red[512] / red[0] + eps);
+    mean_out[ng] = mu_g;
+    rstd_out[ng] = rs_g;
+  }
+  // per-(n, c) affine of the apply pass: y = x * scale + shift
+  for (int j = threadIdx.x; j < cg; j += blockDim.x) {
+    const int c = g * cg + j;
+    const float sc = rs_g * bf2f(w[c]);
+    ss[((long long)n * 2) * C + c] = sc;
+    ss[((long long)n * 2 + 1) * C + c] = (b ? bf2f(b[c]) : 0.f) - mu_g * sc;
   }
 }
 
-__global__ void __launch_bounds__(256) nhwc_apply(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
-                                                  const bf16_t* __restrict__ b, const float* __restrict__ mean,
-                                                  const float* __restrict__ rstd, bf16_t* __restrict__ y, int P,
-                                                  int C, int G, int silu, int nvec) {
-  const int cg = C / G, cv8 = C / 8;
+// y = x * scale[n, c] + shift[n, c] (+ SiLU); ss = [N][2][C] fp32
+__global__ void __launch_bounds__(256) nhwc_apply(const bf16_t* __restrict__ x, const float* __restrict__ ss,
+                                                  bf16_t* __restrict__ y, int P, int C, int silu, int nvec) {
+  const int cv8 = C / 8;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += gridDim.x * blockDim.x) {
     const int pix = i / cv8;
     const int c0 = (i - pix * cv8) * 8;
     const int n = pix / P;
-    float v[8];
+    float v[8], sc[8], sh[8];
     load8(x + (long long)i * 8, v);
+    load8f(ss + (long long)n * 2 * C + c0, sc);
+    load8f(ss + ((long long)n * 2 + 1) * C + c0, sh);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int c = c0 + j, ng = n * G + c / cg;
-      float z = (v[j] - mean[ng]) * rstd[ng] * bf2f(w[c]) + (b ? bf2f(b[c]) : 0.f);
+      const float z = v[j] * sc[j] + sh[j];
       v[j] = silu ? silu_of(z) : z;
     }
     store8(y + (long long)i * 8, v);
@@ -308,7 +318,7 @@ bool geometry(int C, int G, dim3& block, int& slabs) {
 
 KCA_API int kca_groupnorm_nhwc_ws(int N, int P, int C) {  // fp32 workspace floats needed
   const int nchunks = (P + chunk_of(P) - 1) / chunk_of(P);
-  return 2 * N * nchunks * C;
+  return 2 * N * nchunks * C + 2 * N * C;
 }
 
 // x, y: [N, P, C] bf16; mean/rstd: [N*G] fp32 out; ws: kca_groupnorm_nhwc_ws floats
@@ -321,10 +331,12 @@ KCA_API int kca_groupnorm_nhwc_fwd(const void* x, const void* w, const void* b, 
   const int nchunks = (P + chunk_of(P) - 1) / chunk_of(P);
   const size_t smem = (2 * block.y * block.x * 8 + block.y) * sizeof(float);
   hipLaunchKernelGGL(nhwc_chunk_stats, dim3(nchunks, N, slabs), block, smem, stream, (const bf16_t*)x, P, C, ws);
-  hipLaunchKernelGGL(nhwc_group_stats, dim3(N * G), dim3(256), 0, stream, ws, P, C, G, nchunks, eps, mean, rstd);
+  float* ss = ws + 2LL * N * nchunks * C;
+  hipLaunchKernelGGL(nhwc_group_stats, dim3(N * G), dim3(256), 0, stream, ws, P, C, G, nchunks, eps, mean, rstd,
+                     (const bf16_t*)w, (const bf16_t*)b, ss);
   const int nvec = (int)((long long)N * P * C / 8);
-  hipLaunchKernelGGL(nhwc_apply, dim3(kca_grid(nvec, 256, 8192)), dim3(256), 0, stream, (const bf16_t*)x,
-                     (const bf16_t*)w, (const bf16_t*)b, mean, rstd, (bf16_t*)y, P, C, G, silu, nvec);
+  hipLaunchKernelGGL(nhwc_apply, dim3(kca_grid(nvec, 256, 8192)), dim3(256), 0, stream, (const bf16_t*)x, ss,
+                     (bf16_t*)y, P, C, silu, nvec);
   return 0;
 }
 

@@ -39,6 +39,8 @@ _SIGS = {
     "kca_layernorm_bwd": [P, P, P, P, P, P, P, P, P, I, P, I, I, P],
     "kca_gelu_fwd": [P, P, LL, I, P],
     "kca_gelu_bwd": [P, P, P, LL, I, P],
+    "kca_geglu_fwd": [P, P, LL, I, P],
+    "kca_geglu_bwd": [P, P, P, LL, I, P],
     "kca_rope": [P, P, I, I, LL, I, LL, LL, LL, LL, I, I, P, P, P, F, P],
     "kca_accum_grad": [P, P, F, I, LL, P],
     "kca_cast_f32_bf16": [P, P, LL, P],

@@ -41,7 +41,31 @@ def quick_gelu(x: torch.Tensor) -> torch.Tensor:
     return x * torch.sigmoid(1.702 * x)
 
 
+class _GegluFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = x.contiguous()
+        inner = x.shape[-1] // 2
+        rows = x.numel() // x.shape[-1]
+        y = torch.empty(*x.shape[:-1], inner, device=x.device, dtype=x.dtype)
+        _lib.call("kca_geglu_fwd", x.data_ptr(), y.data_ptr(), rows, inner, _lib.stream())
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = torch.empty_like(x)
+        _lib.call("kca_geglu_bwd", dy.data_ptr(), x.data_ptr(), dx.data_ptr(), x.numel() // x.shape[-1],
+                  x.shape[-1] // 2, _lib.stream())
+        return dx
+
+
 def geglu(x: torch.Tensor) -> torch.Tensor:
-    """diffusers GEGLU: split the projection in half, value * gelu(gate) (exact erf)."""
+    """diffusers GEGLU: split the projection in half, value * gelu(gate) (exact erf).
+    GPU: one fused pass (kca_geglu_fwd / _bwd)."""
+    if _lib.use_native(x) and (x.shape[-1] // 2) % 8 == 0 and x.shape[-1] % 2 == 0:
+        return _GegluFn.apply(x)
     a, g = x.chunk(2, dim=-1)
     return a * F.gelu(g.float()).to(a.dtype)

@@ -287,6 +287,21 @@ def test_groupnorm_nhwc(N, C, H, W, G, silu):
     assert _rel(b.grad, br.grad) < 2e-2
 
 
+@pytest.mark.parametrize("rows,inner", [(4096, 1280), (77, 2560), (3, 8)])
+def test_geglu(rows, inner):
+    torch.manual_seed(0)
+    x = torch.randn(rows, 2 * inner, device=DEV).bfloat16().requires_grad_()
+    y = ops.geglu(x)
+    xr = x.detach().float().requires_grad_()
+    a, g = xr.chunk(2, -1)
+    yr = a * F.gelu(g)
+    assert _rel(y, yr) < 1e-2
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    yr.backward(dy.float())
+    assert _rel(x.grad, xr.grad) < 2e-2
+
+
 def test_unet_channels_last_matches_nchw_on_gpu():
     """bf16 SD-shaped UNet slice: channels-last forward+backward == NCHW within bf16 noise."""
     from kubernetes_cloud_amd.models.unet import UNetConfig, build_unet, to_channels_last
