@@ -43,6 +43,8 @@ def main():
                     help="hipBLASLt/rocBLAS solution selection via PyTorch TunableOp: 'tune' measures during "
                          "warmup and writes tuning/tunableop_results.csv; 'auto' uses that file when present")
     ap.add_argument("--tunableop-file", default=os.path.join(ROOT, "tuning", "tunableop_results.csv"))
+    ap.add_argument("--sd", type=int, default=1, help="also measure the SD-1.5 txt2img half of the BASELINE metric "
+                    "(batch 8, 512 px, 50 LMS steps, CFG 7; one rank-local replica per GPU) after the GPT-J steps")
     args = ap.parse_args()
 
     import torch
@@ -118,6 +120,13 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     global_batch = B * args.gas * world
+    peak_gib = torch.cuda.max_memory_allocated() / 2**30
+    sd = None
+    if args.sd:
+        eng.remove_hooks()  # drops the gradient-sink references to the engine
+        del eng, model, batches
+        torch.cuda.empty_cache()
+        sd = _sd_txt2img(dev, world, info.is_main)
     tokens = args.steps * global_batch * S
     tps = tokens / dt
     ms = dt / args.steps * 1e3
@@ -126,7 +135,7 @@ def main():
     if info.is_main:
         print(f"[bench] loss={loss.item():.4f} step={ms:.1f}ms tokens/s={tps:.0f} "
               f"tokens/s/gpu={tps/world:.0f} MFU(2.5PF dense)={mfu*100:.1f}% "
-              f"peak_mem={torch.cuda.max_memory_allocated()/2**30:.1f}GiB", file=sys.stderr, flush=True)
+              f"peak_mem={peak_gib:.1f}GiB", file=sys.stderr, flush=True)
         rec = {
             "metric": "GPT-J-6B finetune tokens/sec",
             "value": round(tps, 1),
@@ -150,10 +159,42 @@ def main():
                 "activation_checkpointing": bool(args.ckpt),
                 "mfu_2p5pf": round(mfu, 4),
             },
+            "secondary": sd,
         }
         print(json.dumps(rec), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
+
+
+def _sd_txt2img(dev, world, is_main):
+    """SD-1.5 txt2img images/s (BASELINE.json metric, second half; BASELINE.md
+    protocol: batch 8, 512x512, 50 steps, CFG 7.0, incl. VAE decode, excl. PNG
+    encode), random-init weights, one replica per rank (weak scaling): total
+    images / max-over-ranks time of one timed batch after one warmup batch."""
+    import importlib.util
+
+    import torch
+    import torch.distributed as dist
+    spec = importlib.util.spec_from_file_location("kca_sd_bench", os.path.join(ROOT, "bench", "sd_bench.py"))
+    sdb = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(sdb)
+    a = argparse.Namespace(batch=8, res=512, steps=1, warmup=1, infer_steps=50, scheduler="LMSDiscreteScheduler",
+                           ckpt=False)
+    try:
+        if dist.is_initialized():
+            dist.barrier()
+        r = sdb.bench_infer(a, dev)
+        dt = torch.tensor([r["ms_per_batch"]], dtype=torch.float64, device=dev)
+        if dist.is_initialized():
+            dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+        ms = float(dt.item())
+        return {"metric": "SD-1.5 txt2img images/sec", "value": round(world * a.batch / (ms / 1e3), 3),
+                "unit": "images/s", "ms_per_batch": round(ms, 1), "n_gpus": world,
+                "config": dict(r["config"], replicas=world)}
+    except Exception as e:  # noqa: BLE001 - the headline line must still print
+        if is_main:
+            print(f"[bench] SD txt2img measurement failed: {e!r}", file=sys.stderr, flush=True)
+        return None
 
 
 if __name__ == "__main__":
