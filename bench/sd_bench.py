@@ -96,6 +96,8 @@ def bench_infer(args, dev):
     sch = load_scheduler(sd_scheduler_config(), args.scheduler)
     B, steps, g = args.batch, args.infer_steps, 7.0
     ids = torch.randint(0, 49408, (2 * B, 77), device=dev)
+    from kubernetes_cloud_amd.models.sd_pipeline import unet_runner
+    run_unet = unet_runner(unet)
 
     @torch.no_grad()
     def run():
@@ -104,7 +106,7 @@ def bench_infer(args, dev):
         x = torch.randn(B, 4, args.res // 8, args.res // 8, device=dev) * sch.init_noise_sigma
         for t in sch.timesteps:
             xin = sch.scale_model_input(torch.cat([x, x]), t).to(torch.bfloat16)
-            eps = unet(xin, torch.full((2 * B,), float(t), device=dev), ctx).float()
+            eps = run_unet(xin, torch.full((2 * B,), float(t), device=dev), ctx).float()
             eu, ec = eps.chunk(2)
             x = sch.step(eu + g * (ec - eu), t, x).float()
         return vae.decode((x / 0.18215).to(torch.bfloat16))
@@ -124,7 +126,8 @@ def bench_infer(args, dev):
     return {"metric": "SD-1.5 txt2img images/sec", "value": round(ips, 3), "unit": "images/s",
             "ms_per_batch": round(dt / args.steps * 1e3, 1),
             "config": {"batch": B, "resolution": args.res, "steps": steps, "cfg": g, "scheduler": args.scheduler,
-                       "dtype": "bf16", "out_shape": list(img.shape)}}
+                       "dtype": "bf16", "out_shape": list(img.shape),
+                       "hip_graph": type(run_unet).__name__ == "UNetGraph"}}
 
 
 def main():

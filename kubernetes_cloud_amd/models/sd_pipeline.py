@@ -70,6 +70,61 @@ def _map_legacy_vae(sd: dict) -> dict:
     return out
 
 
+class UNetGraph:
+    """The UNet denoising forward replayed as a HIP graph (one per input
+    shape): SD-1.5 at 512 px is ~1000 kernel launches per step, and the host
+    cannot issue them as fast as MI355X retires them at batch 8 + CFG. Inputs
+    are copied into the graph's static buffers; the returned tensor is the
+    graph's static output (consume it before the next call). Capture failures
+    fall back to eager for that shape. ``KCA_SD_GRAPH=0`` disables."""
+
+    def __init__(self, unet):
+        self.unet = unet
+        self.graphs: dict = {}
+
+    def __call__(self, x, t, ctx):
+        key = (tuple(x.shape), x.dtype, tuple(t.shape), tuple(ctx.shape), ctx.dtype)
+        g = self.graphs.get(key)
+        if g is None:
+            g = self.graphs[key] = self._capture(x, t, ctx)
+        if g is False:
+            return self.unet(x, t, ctx)
+        graph, sx, st, sc, out = g
+        sx.copy_(x)
+        st.copy_(t)
+        sc.copy_(ctx)
+        graph.replay()
+        return out
+
+    @torch.no_grad()
+    def _capture(self, x, t, ctx):
+        sx, st, sc = x.clone(), t.clone(), ctx.clone()
+        try:
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):  # warm up: solver search, workspaces, allocator
+                for _ in range(2):
+                    self.unet(sx, st, sc)
+            torch.cuda.current_stream().wait_stream(side)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                out = self.unet(sx, st, sc)
+            return graph, sx, st, sc, out
+        except Exception as e:  # noqa: BLE001 - eager is always correct
+            import sys
+            print(f"[sd] HIP graph capture failed ({e!r}); running the UNet eagerly", file=sys.stderr)
+            torch.cuda.synchronize()
+            return False
+
+
+def unet_runner(unet):
+    """Graph-replaying runner on the GPU (eval only), the module itself otherwise."""
+    if (next(unet.parameters()).is_cuda and not unet.training
+            and os.environ.get("KCA_SD_GRAPH", "1") not in ("0", "false")):
+        return UNetGraph(unet)
+    return unet
+
+
 class StableDiffusionPipeline:
     def __init__(self, unet: UNet2DConditionModel, vae: AutoencoderKL, text_encoder: CLIPTextModel,
                  tokenizer, scheduler, scaling_factor: float = L_SCALE_FACTOR):
@@ -77,6 +132,12 @@ class StableDiffusionPipeline:
         self.tokenizer, self.scheduler = tokenizer, scheduler
         self.scaling_factor = scaling_factor
         self._layout()
+
+    def _runner(self):
+        r = getattr(self, "_unet_runner", None)
+        if r is None or getattr(r, "unet", r) is not self.unet or self.unet.training:
+            r = self._unet_runner = unet_runner(self.unet)
+        return r
 
     def _layout(self):
         """On the GPU the UNet and VAE run channels-last end to end (NHWC MIOpen
@@ -195,11 +256,12 @@ class StableDiffusionPipeline:
             latents = torch.randn(shape, generator=generator, device=generator.device if generator else dev,
                                   dtype=torch.float32).to(dev)
         x = latents.float() * sch.init_noise_sigma
+        run = self._runner()
         for t in sch.timesteps:
             xin = torch.cat([x, x]) if cfg else x
             xin = sch.scale_model_input(xin, t).to(dt)
             tt = torch.full((xin.shape[0],), float(t), device=dev)
-            eps = self.unet(xin, tt, ctx).float()
+            eps = run(xin, tt, ctx).float()
             if cfg:
                 eu, ec = eps.chunk(2)
                 eps = eu + guidance_scale * (ec - eu)

@@ -325,6 +325,29 @@ def test_unet_channels_last_matches_nchw_on_gpu():
         assert _rel(b, a) < tol
 
 
+def test_unet_hip_graph_replay_matches_eager():
+    """The HIP-graph UNet runner (models/sd_pipeline.py:UNetGraph) replays the
+    eager forward and follows new inputs (not bit-exact: library GEMM/conv
+    solver choices under stream capture may differ from eager)."""
+    from kubernetes_cloud_amd.models.sd_pipeline import UNetGraph
+    from kubernetes_cloud_amd.models.unet import UNetConfig, build_unet, to_channels_last
+    torch.manual_seed(0)
+    u = build_unet(UNetConfig(block_out_channels=(320, 640, 640, 640), cross_attention_dim=64, sample_size=16),
+                   device=DEV, dtype=torch.bfloat16).eval()
+    to_channels_last(u)
+    r = UNetGraph(u)
+    with torch.no_grad():
+        for seed in (1, 2):
+            g = torch.Generator(device=DEV).manual_seed(seed)
+            x = torch.randn(2, 4, 16, 16, device=DEV, generator=g).bfloat16()
+            ctx = torch.randn(2, 7, 64, device=DEV, generator=g).bfloat16()
+            t = torch.tensor([10.0 * seed, 500.0], device=DEV)
+            out = r(x, t, ctx).clone()
+            ref = u(x, t, ctx)
+            assert r.graphs and next(iter(r.graphs.values())) is not False
+            assert _rel(out, ref) < 2e-2
+
+
 def test_adamw8bit_matches_reference_math():
     """kca_adamw8bit vs the torch implementation of the same block-wise 8-bit
     AdamW (FlatAdamW8bit with native=False) over several steps, ragged tail."""
