@@ -186,6 +186,8 @@ def main(argv=None):
     vl = DataLoader(val_ds, batch_size=args.batch_size, sampler=va_s, num_workers=args.workers, pin_memory=use_cuda)
     model = resnet50(args.num_classes).to(dev)
     if use_cuda:
+        from ..utils import miopen
+        miopen.configure()  # keep MIOpen's naive NHWC solvers out of the conv search
         model = model.to(memory_format=torch.channels_last)
     if world > 1:
         model = nn.parallel.DistributedDataParallel(model, device_ids=[dev.index] if use_cuda else None,
