@@ -171,6 +171,115 @@ __global__ __launch_bounds__(256) void skinny_gemm_kernel(
   }
 }
 
+// Split-K form for M == 1 (single-sequence decode, the latency case):
+// a workgroup owns R rows and its 4 waves interleave over K in 512-element
+// slabs (wave w: slabs w, w+4, ...), each lane keeping R*4 16-B weight loads
+// in flight; the 4 partial dot products meet in LDS. Against the row-per-wave
+// form above this quadruples the workgroups (4/CU for a 4096-row output, 16
+// resident waves per CU) and cuts each wave's serial K chain to a quarter --
+// in context (weights never L2/MALL-resident across a 28-layer step) the
+// row-per-wave form streamed at 3.5-3.9 TB/s. (At M = 4 the LN prologue and
+// the 4x larger LDS tile, repeated in 4x the workgroups, made it a loss: GPT-J
+// B=4 decode 5.9 -> 9.3 ms/step, so M > 1 keeps the row-per-wave kernel.)
+template <int M, int R, bool LN>
+__global__ __launch_bounds__(256) void skinny_gemm_sk_kernel(
+    const bf16_t* __restrict__ x, long long ldx, const bf16_t* __restrict__ w,
+    const bf16_t* __restrict__ bias, bf16_t* __restrict__ y, long long ldy, int N, int K,
+    int kc, int act, int mv, LnArgs ln) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t xs[];  // [M][kc]
+  __shared__ float red[16];
+  __shared__ float part[4][R * M];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int n0 = blockIdx.x * R;
+  float acc[R][M];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int m = 0; m < M; ++m) acc[r][m] = 0.f;
+  const bf16_t* wr[R];
+  bool rv[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    rv[r] = n0 + r < N;
+    wr[r] = w + (long long)(rv[r] ? n0 + r : 0) * K;
+  }
+  for (int k0 = 0; k0 < K; k0 += kc) {
+    const int kn = min(kc, K - k0);
+    __syncthreads();
+    if constexpr (LN) {
+      ln_prologue<M>(x, ldx, ln, xs, K, mv, red);  // kc == K: one chunk
+    } else {
+      for (int i = tid * 8; i < M * kn; i += 256 * 8) {
+        const int m = i / kn, kk = i % kn;
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (m < mv) v = *reinterpret_cast<const uint4*>(x + m * ldx + k0 + kk);
+        *reinterpret_cast<uint4*>(xs + m * kc + kk) = v;
+      }
+    }
+    __syncthreads();
+    for (int kb = wid * 512 + lane * 8; kb < kn; kb += 4 * 2048) {
+      uint4 wv[4][R];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = kb + u * 2048;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          wv[u][r] = make_uint4(0u, 0u, 0u, 0u);
+          if (k < kn && rv[r]) wv[u][r] = *reinterpret_cast<const uint4*>(wr[r] + k0 + k);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = kb + u * 2048;
+        if (k < kn) {
+#pragma unroll
+          for (int m = 0; m < M; ++m) {
+            float xv[8];
+            load8(xs + m * kc + k, xv);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+              const uint32_t q[4] = {wv[u][r].x, wv[u][r].y, wv[u][r].z, wv[u][r].w};
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                acc[r][m] = fmaf(__uint_as_float(q[j] << 16), xv[2 * j], acc[r][m]);
+                acc[r][m] = fmaf(__uint_as_float(q[j] & 0xffff0000u), xv[2 * j + 1], acc[r][m]);
+              }
+            }
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int m = 0; m < M; ++m) acc[r][m] = wave_sum(acc[r][m]);
+  if (lane == 0) {
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int m = 0; m < M; ++m) part[wid][r * M + m] = acc[r][m];
+  }
+  __syncthreads();
+  if (tid < R * M) {
+    const int r = tid / M, m = tid % M;
+    if (rv[0] && n0 + r < N && m < mv) {
+      float v = part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid];
+      v += bias ? bf2f(bias[n0 + r]) : 0.f;
+      if (act == 1) v = gelu_tanh(v);
+      else if (act == 2) v = 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
+      y[m * ldy + n0 + r] = f2bf(v);
+    }
+  }
+}
+
+// 1 = split-K kernel for M == 1 (default), 0 = row-per-wave kernel (A/B)
+static int g_skinny_sk = 1;
+KCA_API int kca_skinny_set_splitk(int on) {
+  g_skinny_sk = on ? 1 : 0;
+  return 0;
+}
+
 template <int M, bool LN = false>
 static void launch_skinny(const bf16_t* x, long long ldx, const bf16_t* w, const bf16_t* bias,
                           bf16_t* y, long long ldy, int mv, int N, int K, int act, hipStream_t s,
@@ -179,6 +288,12 @@ static void launch_skinny(const bf16_t* x, long long ldx, const bf16_t* w, const
   int kc = (32768 / M) / 512 * 512;  // M*kc*2 B <= 64 KB of LDS
   if (kc < 512) kc = 512;
   if (kc > K || LN) kc = (K + 7) / 8 * 8;
+  if constexpr (M == 1) if (g_skinny_sk) {
+    const dim3 grid((N + R - 1) / R);
+    hipLaunchKernelGGL((skinny_gemm_sk_kernel<M, R, LN>), grid, dim3(256), (size_t)M * kc * sizeof(bf16_t), s,
+                       x, ldx, w, bias, y, ldy, N, K, kc, act, mv, ln);
+    return;
+  }
   const int rows_per_block = 4 * R;
   const dim3 grid((N + rows_per_block - 1) / rows_per_block);
   hipLaunchKernelGGL((skinny_gemm_kernel<M, R, LN>), grid, dim3(256), (size_t)M * kc * sizeof(bf16_t), s,

@@ -7,6 +7,8 @@ hipBLASLt through ``F.linear``.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -23,18 +25,33 @@ def _act_ref(y, act):
     return y
 
 
+_MODE_SET = False
+
+
+def _set_mode():
+    """KCA_SKINNY_SPLITK=0 selects the row-per-wave kernel (A/B runs)."""
+    global _MODE_SET
+    if not _MODE_SET:
+        _MODE_SET = True
+        if os.environ.get("KCA_SKINNY_SPLITK", "1") in ("0", "false") and _lib.has("kca_skinny_set_splitk"):
+            _lib.call("kca_skinny_set_splitk", 0)
+
+
 def skinny_linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None, act: int = 0,
                   out: torch.Tensor | None = None) -> torch.Tensor:
     """x [M, K] (row stride multiple of 8), weight [N, K] contiguous."""
     M, K = x.shape
     N = weight.shape[0]
-    # measured on MI355X (profiles/gemv_bench_r1.jsonl): the skinny kernel wins for M <= 2 everywhere and
-    # up to M = 4 on small weights (hipBLASLt under-fills the chip there); MFMA GEMMs win beyond
-    small = N * K <= (64 << 20)
-    if (_lib.use_native(x, weight) and (M <= 2 or (M <= 4 and small)) and K % 8 == 0 and x.stride(1) == 1
+    # measured on MI355X (profiles/gemv_bench_r1.jsonl, decode_bench in context): the skinny kernel wins
+    # at M = 1 and for 2 <= M <= 4 only on the small out-projection (hipBLASLt under-fills the chip there:
+    # 12.4 vs 18.4 us); on the QKV / MLP weights hipBLASLt is faster from M = 2 (GPT-J decode B=2 4.69 ms
+    # with the skinny kernel vs 4.54 ms at B=4 through hipBLASLt); MFMA GEMMs beyond
+    small = N * K <= (16 << 20)
+    if (_lib.use_native(x, weight) and (M == 1 or (M <= 4 and small)) and K % 8 == 0 and x.stride(1) == 1
             and x.stride(0) % 8 == 0
             and weight.is_contiguous() and x.data_ptr() % 16 == 0 and weight.data_ptr() % 16 == 0
             and (bias is None or bias.dtype == torch.bfloat16)):
+        _set_mode()
         if out is None:
             out = torch.empty(M, N, device=x.device, dtype=x.dtype)
         _lib.call("kca_skinny_gemm", x.data_ptr(), x.stride(0), weight.data_ptr(), _lib.ptr(bias), out.data_ptr(),
@@ -50,7 +67,7 @@ def skinny_linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | No
 def _ln_ok(x, M, K, weight, residuals, gamma, beta, bias):
     Mp = 1 if M == 1 else 2 if M == 2 else 4 if M <= 4 else 8
     ts = [x, weight, gamma, *residuals] + ([beta] if beta is not None else [])
-    return (M <= 2 or (M <= 4 and weight.shape[0] * K <= (64 << 20))) and Mp * K <= 32768 and K % 8 == 0 \
+    return (M == 1 or (M <= 4 and weight.shape[0] * K <= (16 << 20))) and Mp * K <= 32768 and K % 8 == 0 \
         and all(t.data_ptr() % 16 == 0 for t in ts) and x.stride(1) == 1 and x.stride(0) % 8 == 0 \
         and all(r.is_contiguous() and r.shape == x.shape for r in residuals) and weight.is_contiguous() \
         and gamma.is_contiguous() and (beta is None or beta.is_contiguous()) \
@@ -72,6 +89,7 @@ def ln_skinny_linear(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor | 
         y = torch.empty(M, weight.shape[0], device=x.device, dtype=x.dtype)
         r1 = residuals[0] if residuals else None
         r2 = residuals[1] if len(residuals) > 1 else None
+        _set_mode()
         _lib.call("kca_ln_skinny_gemm", x.data_ptr(), x.stride(0), _lib.ptr(r1), _lib.ptr(r2),
                   h.data_ptr() if residuals else None, h.stride(0) if residuals else K, gamma.data_ptr(),
                   _lib.ptr(beta), float(eps), weight.data_ptr(), _lib.ptr(bias), y.data_ptr(), y.stride(0),

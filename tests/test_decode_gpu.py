@@ -176,8 +176,25 @@ def test_skinny_gemm(M, N, K):
         assert (y.float() - fn(ref)).abs().max() < 0.05, act
 
 
-@pytest.mark.parametrize("M,N,K", [(1, 12288, 4096), (2, 16384, 4096), (4, 4096, 4096), (1, 5376, 14336),
-                                   (2, 7168, 14336), (3, 8192, 4096)])
+@pytest.mark.parametrize("M", [1, 2, 4])
+def test_skinny_gemm_row_per_wave_kernel(M):
+    """The row-per-wave skinny kernel (A/B alternative to the split-K default)."""
+    from kubernetes_cloud_amd.ops.gemv import skinny_linear
+    torch.manual_seed(M)
+    x = torch.randn(M, 4096, device=dev).to(torch.bfloat16)
+    w = (torch.randn(2048, 4096, device=dev) * 0.02).to(torch.bfloat16)  # small: skinny for every M <= 4
+    ref = x.float() @ w.float().t()
+    _lib.call("kca_skinny_set_splitk", 0)
+    try:
+        y = skinny_linear(x, w)
+    finally:
+        _lib.call("kca_skinny_set_splitk", 1)
+    assert (y.float() - ref).abs().max() < 0.05
+    assert (skinny_linear(x, w).float() - ref).abs().max() < 0.05
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 12288, 4096), (2, 4096, 4096), (4, 4096, 4096), (1, 5376, 14336),
+                                   (2, 1024, 14336), (3, 4096, 4096)])
 @pytest.mark.parametrize("nres", [0, 1, 2])
 def test_ln_skinny_gemm(M, N, K, nres):
     from kubernetes_cloud_amd.ops import gemv
