@@ -19,6 +19,8 @@ struct LnArgs {
   const bf16_t* gamma;  // [K]
   const bf16_t* beta;   // [K] (nullable)
   float eps;
+  bf16_t* xn_out;       // normalised rows [M][K], written by workgroup 0 (nullable): GPT-J's shared LN
+                        // feeds the fc_in GEMV too, which then skips its own prologue
 };
 
 // LayerNorm prologue: every workgroup normalises the M activation rows itself
@@ -77,6 +79,7 @@ __device__ __forceinline__ void ln_prologue(const bf16_t* __restrict__ x, long l
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = (v[j] - mean) * rstd * g[j] + b[j];
       store8(row + k, v);
+      if (a.xn_out && blockIdx.x == 0) store8(a.xn_out + m * K + k, v);
     }
   }
 }
@@ -322,14 +325,14 @@ KCA_API int kca_skinny_gemm(const void* x, long long ldx, const void* w, const v
 KCA_API int kca_ln_skinny_gemm(const void* x, long long ldx, const void* r1, const void* r2, void* h_out,
                                long long ldh, const void* gamma, const void* beta, float eps, const void* w,
                                const void* bias, void* y, long long ldy, int M, int N, int K, int act,
-                               hipStream_t stream) {
+                               void* xn_out, hipStream_t stream) {
   if (M < 1 || M > 8 || K % 8 || ldx % 8 || ldh % 8 || N < 1) return 1;
   const int Mp = M == 1 ? 1 : M == 2 ? 2 : M <= 4 ? 4 : 8;
   if ((long long)Mp * K > 32768) return 1;
   if (((uintptr_t)x | (uintptr_t)w | (uintptr_t)r1 | (uintptr_t)r2 | (uintptr_t)h_out | (uintptr_t)gamma |
-       (uintptr_t)beta) & 15) return 2;
+       (uintptr_t)beta | (uintptr_t)xn_out) & 15) return 2;
   LnArgs a{(const bf16_t*)r1, (const bf16_t*)r2, (bf16_t*)h_out, ldh, (const bf16_t*)gamma,
-           (const bf16_t*)beta, eps};
+           (const bf16_t*)beta, eps, (bf16_t*)xn_out};
   const bf16_t* xp = (const bf16_t*)x;
   const bf16_t* wp = (const bf16_t*)w;
   const bf16_t* bp = (const bf16_t*)bias;

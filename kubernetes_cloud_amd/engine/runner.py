@@ -177,7 +177,11 @@ class ModelRunner:
         for li, blk in enumerate(m.h):
             # every LayerNorm (+ pending residual adds) runs as the prologue of the GEMM that consumes it
             at = blk.attn
-            qkv, h = self._ln_lin(blk.ln_1, h, pending, at.qkv)
+            shared = cfg.parallel_residual and blk.ln_2 is None  # GPT-J: one LN feeds qkv and fc_in
+            if shared:
+                qkv, h, xn = self._ln_lin(blk.ln_1, h, pending, at.qkv, want_xn=True)
+            else:
+                qkv, h = self._ln_lin(blk.ln_1, h, pending, at.qkv)
             kc, vc = self.cache.k[li], self.cache.v[li]
             dops.decode_prep(qkv, self.H, self.Hkv, self.D, self.rot, cfg.rotary_interleaved, self.cos,
                              self.sin, pos, slots, kc, vc)
@@ -189,8 +193,10 @@ class ModelRunner:
             a = self._lin(at.out, o)
             mlp = blk.mlp
             act = 1 if mlp.approx in ("tanh", True) else 2
-            if cfg.parallel_residual:
-                f, _ = self._ln_lin(blk.ln_1 if blk.ln_2 is None else blk.ln_2, h, (), mlp.fc_in, act)
+            if shared:
+                pending = (a, self._lin(mlp.fc_out, self._lin(mlp.fc_in, xn, act)))
+            elif cfg.parallel_residual:
+                f, _ = self._ln_lin(blk.ln_2, h, (), mlp.fc_in, act)
                 pending = (a, self._lin(mlp.fc_out, f))
             else:
                 f, h = self._ln_lin(blk.ln_2, h, (a,), mlp.fc_in, act)
@@ -199,7 +205,7 @@ class ModelRunner:
             return self._ln_lin(m.ln_f, h, pending, None, weight=m.wte.weight)[0]
         return self._ln_lin(m.ln_f, h, pending, m.lm_head)[0]
 
-    def _ln_lin(self, ln, h, res, mod, act: int = 0, weight=None):
+    def _ln_lin(self, ln, h, res, mod, act: int = 0, weight=None, want_xn: bool = False):
         """LayerNorm(h + sum(res)) -> column-parallel / LM-head linear, fused (decode)."""
         from ..parallel.tensor_parallel import ParallelLMHead, RowParallelLinear, gather_last_dim
         assert not isinstance(mod, RowParallelLinear)
@@ -207,7 +213,7 @@ class ModelRunner:
             y, h = ln_skinny_linear(h, ln.weight, ln.bias, ln.eps, mod.local_weight(), mod.bias, res, act)
             return gather_last_dim(y, mod.group), h
         return ln_skinny_linear(h, ln.weight, ln.bias, ln.eps, mod.weight if weight is None else weight,
-                                None if mod is None else mod.bias, res, act)
+                                None if mod is None else mod.bias, res, act, want_xn=want_xn)
 
     # decode linears: skinny GEMM (W streamed once, bias/GELU fused) for <= 16 rows
     def _lin(self, mod, x, act: int = 0):

@@ -76,31 +76,35 @@ def _ln_ok(x, M, K, weight, residuals, gamma, beta, bias):
 
 def ln_skinny_linear(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor | None, eps: float,
                      weight: torch.Tensor, bias: torch.Tensor | None = None, residuals=(), act: int = 0,
-                     want_h: bool = False):
+                     want_h: bool = False, want_xn: bool = False):
     """``act(LayerNorm(x + sum(residuals)) W^T + b)`` in one launch (decode).
 
     Returns ``(y, h)`` with ``h`` the updated residual stream (``x`` itself when
-    no residuals are added). Falls back to the LN kernel + ``skinny_linear``
-    when the rows do not fit the LDS tile or the batch is too wide."""
+    no residuals are added), plus the normalised rows ``xn`` when ``want_xn``
+    (GPT-J's shared LayerNorm feeds a second GEMM). Falls back to the LN
+    kernel + ``skinny_linear`` when the rows do not fit the LDS tile or the
+    batch is too wide."""
     M, K = x.shape
     residuals = tuple(r for r in residuals if r is not None)
     if _lib.use_native(x, weight) and _ln_ok(x, M, K, weight, residuals, gamma, beta, bias):
         h = torch.empty(M, K, device=x.device, dtype=x.dtype) if residuals else x
         y = torch.empty(M, weight.shape[0], device=x.device, dtype=x.dtype)
+        xn = torch.empty(M, K, device=x.device, dtype=x.dtype) if want_xn else None
         r1 = residuals[0] if residuals else None
         r2 = residuals[1] if len(residuals) > 1 else None
         _set_mode()
         _lib.call("kca_ln_skinny_gemm", x.data_ptr(), x.stride(0), _lib.ptr(r1), _lib.ptr(r2),
                   h.data_ptr() if residuals else None, h.stride(0) if residuals else K, gamma.data_ptr(),
                   _lib.ptr(beta), float(eps), weight.data_ptr(), _lib.ptr(bias), y.data_ptr(), y.stride(0),
-                  M, weight.shape[0], K, int(act), _lib.stream())
-        return y, h
+                  M, weight.shape[0], K, int(act), _lib.ptr(xn), _lib.stream())
+        return (y, h, xn) if want_xn else (y, h)
     from .norms import layer_norm
     if residuals:
         xn, h = layer_norm(x, gamma, beta, eps, residual=residuals)
     else:
         xn, h = layer_norm(x, gamma, beta, eps), x
-    return skinny_linear(xn, weight, bias, act), h
+    y = skinny_linear(xn, weight, bias, act)
+    return (y, h, xn) if want_xn else (y, h)
 
 
 __all__ = ["skinny_linear", "ln_skinny_linear", "ACT"]

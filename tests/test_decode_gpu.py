@@ -212,7 +212,8 @@ def test_ln_skinny_gemm(M, N, K, nres):
     h_ref = hs.to(torch.bfloat16)
     xn = torch.nn.functional.layer_norm(h_ref.float(), (K,), g.float(), None if be is None else be.float(), 1e-5)
     ref = xn.to(torch.bfloat16).float() @ w.float().t() + b.float()
-    y, h = gemv.ln_skinny_linear(x, g, be, 1e-5, w, b, res, act=1)
+    y, h, xo = gemv.ln_skinny_linear(x, g, be, 1e-5, w, b, res, act=1, want_xn=True)
     torch.cuda.synchronize()
     assert torch.equal(h, h_ref)
+    assert (xo.float() - xn).abs().max() < 0.05  # normalised rows (GPT-J shared-LN output)
     assert (y.float() - torch.nn.functional.gelu(ref, approximate="tanh")).abs().max() < 0.06
