@@ -183,6 +183,25 @@ def aitextgen() -> dict:
                                  cpu=4, memory="32Gi")])}
 
 
+def dalle_mini() -> dict:
+    """online-inference/dalle-mini: PVC, downloader job (.ready.txt), InferenceService with the
+    generation defaults as env (02-inference-service.yaml:33-47); PyTorch-ROCm predictor."""
+    model = "dalle-mini/dalle-mega"
+    env = [{"name": "MODEL_ID", "value": model}, {"name": "MODEL_CACHE", "value": "/mnt/models"},
+           {"name": "STORAGE_URI", "value": "pvc://dalle-mini-model-cache/"},
+           {"name": "TOP_K", "value": "50"}, {"name": "TOP_P", "value": "1.0"},
+           {"name": "TEMPERATURE", "value": "1.0"}, {"name": "CONDITION_SCALE", "value": "10.0"}]
+    return {
+        "00-model-pvc.yaml": pvc("dalle-mini-model-cache", "100Gi"),
+        "01-model-download-job.yaml": _job(
+            "dalle-mini-download", ["python3", "-m", "kubernetes_cloud_amd.data.downloader"],
+            ["-model", model, "-dest", f"/mnt/models/{model}"], "dalle-mini-model-cache", cpu=4, memory="16Gi"),
+        "02-inference-service.yaml": _isvc(
+            "dalle-mega", [_container(["python3", "-m", "kubernetes_cloud_amd.serving.dalle_service"], env=env,
+                                      cpu=6, memory="48Gi")], min_replicas=1, concurrency=1),
+    }
+
+
 def custom_predictor() -> dict:
     """S13/S14 pattern: bring-your-own predictor subclassing serving.server.Model."""
     return {"custom-inferenceservice.yaml": _isvc(

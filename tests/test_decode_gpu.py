@@ -217,3 +217,20 @@ def test_ln_skinny_gemm(M, N, K, nres):
     assert torch.equal(h, h_ref)
     assert (xo.float() - xn).abs().max() < 0.05  # normalised rows (GPT-J shared-LN output)
     assert (y.float() - torch.nn.functional.gelu(ref, approximate="tanh")).abs().max() < 0.06
+
+
+def test_dalle_mini_predictor_on_gpu():
+    """S12 on the MI355X path (bf16, flash attention, NHWC VQGAN decoder): PNG out,
+    deterministic per seed."""
+    import io as _io
+
+    from tests.test_serving_cpu import _tiny_dalle_cfgs
+    from kubernetes_cloud_amd.serving.dalle_service import DalleMiniPredictor, options
+    c, v = _tiny_dalle_cfgs()
+    p = DalleMiniPredictor("dalle-mini", None, options({}), device=torch.device("cuda", 0), config=c, vq_config=v)
+    p.load()
+    a = p.predict({"prompt": "a red fox", "parameters": {"seed": 3, "top_k": 8}})
+    b = p.predict({"prompt": "a red fox", "parameters": {"seed": 3, "top_k": 8}})
+    from PIL import Image
+    assert a[:8] == b"\x89PNG\r\n\x1a\n" and a == b
+    assert Image.open(_io.BytesIO(a)).size == (8, 8)

@@ -258,3 +258,46 @@ def test_classifier_and_loadgen(gptj_dir):
     th.join(timeout=10)
     p.generator.close()
     assert res["successes"] == 6 and res["p99_s"] >= res["p50_s"] > 0
+
+
+def _tiny_dalle_cfgs():
+    from kubernetes_cloud_amd.models.dalle_mini import DalleBartConfig, VQGANConfig
+    c = DalleBartConfig(encoder_vocab_size=300, image_vocab_size=64, d_model=64, encoder_layers=2, decoder_layers=2,
+                        encoder_attention_heads=4, decoder_attention_heads=4, encoder_ffn_dim=96, decoder_ffn_dim=96,
+                        max_text_length=16, image_length=16)
+    v = VQGANConfig(n_embed=64, embed_dim=16, z_channels=32, ch=32, ch_mult=(1, 2), num_res_blocks=1,
+                    attn_resolutions=(4,), resolution=8)
+    return c, v
+
+
+def test_dalle_mini_predictor_png_params_and_kv_cache(tmp_path):
+    """S12: DALL·E mini service contract (service.py:111-158) on the PyTorch model:
+    case-insensitive parameter overrides, PNG bytes, deterministic per seed; the
+    KV-cached token-by-token decode equals the full-sequence decoder."""
+    from kubernetes_cloud_amd.serving.dalle_service import DalleMiniPredictor, options, wait_ready
+    c, v = _tiny_dalle_cfgs()
+    o = options({"TOP_K": "7", "CONDITION_SCALE": "3.0"})
+    assert o["TOP_K"] == 7 and o["CONDITION_SCALE"] == 3.0 and o["MODEL_ID"] == "dalle-mini/dalle-mini"
+    p = DalleMiniPredictor("dalle-mini", None, o, device=torch.device("cpu"), config=c, vq_config=v)
+    p.load()
+    prm = p.configure_request({"prompt": "x", "parameters": {"temperature": 0.5, "Top_P": 0.9, "other": 1}})
+    assert prm == {"TOP_K": 7, "TOP_P": 0.9, "TEMPERATURE": 0.5, "CONDITION_SCALE": 3.0}
+    c2 = TestClient(ModelServer(http_port=1).create_app([p]))
+    r = c2.post("/v1/models/dalle-mini:predict", json={"prompt": "a red fox", "parameters": {"seed": 11}})
+    assert r.status_code == 200 and r.headers["content-type"] == "image/png"
+    from PIL import Image
+    assert Image.open(io.BytesIO(r.content)).size == (8, 8)
+    assert p.predict({"prompt": "a red fox", "parameters": {"seed": 11}}) == r.content
+    m = p.model
+    ids = p.tok(["a red fox"])
+    codes = m.generate(ids, p.tok([""]), top_k=5, generator=torch.Generator().manual_seed(0))
+    assert codes.shape == (1, 16) and int(codes.max()) < c.image_vocab_size
+    with torch.no_grad():
+        enc = m.encode(ids)
+        tok = torch.cat([torch.full((1, 1), c.bos_token_id), codes[:, :-1]], 1)
+        full = m.decode(tok, enc)
+        caches = [{"self": {}, "cross": {}} for _ in m.decoder_layers]
+        step = torch.cat([m.decode(tok[:, t:t + 1], enc, start=t, caches=caches) for t in range(16)], 1)
+    assert torch.allclose(full, step, atol=1e-4)
+    (tmp_path / ".ready.txt").write_text("ok")
+    wait_ready(str(tmp_path), 1, interval=0.01)
