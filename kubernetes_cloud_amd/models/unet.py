@@ -249,8 +249,8 @@ def to_channels_last(model: nn.Module, weights: bool = True) -> nn.Module:
     """Run a UNet / VAE channels-last end to end on MI355X: NHWC activations
     (MIOpen's NHWC convolutions without per-call layout transposes, NHWC
     GroupNorm kernels, free token views for attention). ``weights`` also
-    converts the conv weights (inference); a training engine that owns the
-    weights in a flat buffer keeps them NCHW."""
+    converts the conv weights; the training engine keeps that order in its
+    flat buffer (train/engine.py)."""
     from ..utils import miopen
     miopen.configure()
     model.channels_last = True

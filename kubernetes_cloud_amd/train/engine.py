@@ -74,6 +74,10 @@ def _no_decay_names(model: nn.Module) -> set:
     return out
 
 
+def _is_cl(t: torch.Tensor) -> bool:
+    return t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last) and not t.is_contiguous()
+
+
 def _round_up(x: int, m: int) -> int:
     return (x + m - 1) // m * m
 
@@ -132,8 +136,16 @@ class TrainEngine:
         with torch.no_grad():
             for s in slots:
                 view = self.flat[s.offset:s.offset + s.numel]
-                view.copy_(s.param.detach().reshape(-1))
-                s.param.data = view.view(s.param.shape)
+                p = s.param.detach()
+                if _is_cl(p):
+                    # channels-last conv weight (SD UNet on MI355X): keep the NHWC memory order in the
+                    # flat buffer so MIOpen's NHWC kernels read it without a per-call layout copy
+                    O, I, kh, kw = p.shape
+                    view.copy_(p.permute(0, 2, 3, 1).reshape(-1))
+                    s.param.data = view.view(O, kh, kw, I).permute(0, 3, 1, 2)
+                else:
+                    view.copy_(p.reshape(-1))
+                    s.param.data = view.view(s.param.shape)
         self.grad = torch.zeros(self.total, device=dev, dtype=torch.float32)
 
         # ---- decay mask per 64-block (full layout)
@@ -199,6 +211,9 @@ class TrainEngine:
         dst = self.grad[s.offset:s.offset + s.numel]
         first = id(p) not in self._touched
         scale = 1.0 / self.grad_accum
+        if g.dim() == 4 and _is_cl(p):  # flat slot holds the NHWC order
+            g = g.permute(0, 2, 3, 1)
+            g = g.reshape(-1) if g.is_contiguous() else g.contiguous().reshape(-1)
         if self.native and g.dtype == torch.bfloat16 and g.is_contiguous():
             _lib.call("kca_accum_grad", dst.data_ptr(), g.data_ptr(), scale, int(first), s.numel,
                       _lib.stream())

@@ -188,8 +188,8 @@ def main(argv=None):
     unet.train()
     if next(unet.parameters()).is_cuda:
         from ..models.unet import to_channels_last
-        # NHWC activations end to end; the engine owns the (NCHW) weights in its flat buffer
-        to_channels_last(unet, weights=False)
+        # NHWC activations and conv weights end to end (the engine keeps the NHWC order in its flat buffer)
+        to_channels_last(unet)
         to_channels_last(vae)
     eng = TrainEngine(unet, lr=args.lr, betas=(args.adam_beta1, args.adam_beta2), eps=args.adam_epsilon,
                       weight_decay=args.adam_weight_decay, max_grad_norm=1.0,

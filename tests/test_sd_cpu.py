@@ -148,3 +148,30 @@ def test_unet_vae_channels_last_match_nchw():
     assert out.is_contiguous() and out_d.is_contiguous()
     for a, b in ((out, ref), (out_d, ref_d), (out_e, ref_e)):
         assert torch.allclose(a, b, atol=1e-4, rtol=1e-4), (a - b).abs().max()
+
+
+def test_engine_keeps_channels_last_conv_weights():
+    """TrainEngine stores channels-last conv weights in NHWC order inside its flat
+    buffer (no per-call NCHW->NHWC weight copy before MIOpen) and trains them to
+    the same values as the NCHW layout (GAS 2: first write + accumulate)."""
+    import torch.nn as nn
+
+    from kubernetes_cloud_amd.train.engine import TrainEngine
+
+    def run(cl):
+        torch.manual_seed(0)
+        m = nn.Sequential(nn.Conv2d(8, 16, 3, padding=1), nn.ReLU(), nn.Conv2d(16, 8, 1))
+        if cl:
+            m = m.to(memory_format=torch.channels_last)
+        eng = TrainEngine(m, lr=1e-2, weight_decay=0.01, grad_accum=2)
+        x = torch.randn(2, 8, 6, 6)
+        if cl:
+            x = x.contiguous(memory_format=torch.channels_last)
+        for _ in range(3):
+            eng.train_batch([x, x * 0.5], lambda b: m(b).square().mean())
+        return m
+    a, b = run(False), run(True)
+    assert b[0].weight.is_contiguous(memory_format=torch.channels_last)
+    assert b[0].weight.data_ptr() >= 0 and not b[0].weight.is_contiguous()
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        assert torch.allclose(pa, pb, atol=1e-6)
