@@ -292,13 +292,13 @@ __global__ __launch_bounds__(256) void decode_combine_kernel(const float* __rest
   }
 }
 
-// Split size: enough (sequence, kv-head, split) workgroups for ~8 per CU on
+// Split size: enough (sequence, kv-head, split) workgroups for ~4 per CU on
 // the 256 CUs (each split streams its K rows, then its V rows, a few 16-B
 // loads per lane in flight: the pass is HBM-latency bound per workgroup, so
 // bandwidth comes from workgroup count), chunks of 32..1024 tokens.
 KCA_API int kca_decode_chunk(int B, int Hkv, int max_kv) {
   long long work = (long long)B * Hkv;
-  long long want = (2048 + work - 1) / work;
+  long long want = (1024 + work - 1) / work;
   long long c = (max_kv + want - 1) / want;
   c = (c + 31) / 32 * 32;
   if (c < 32) c = 32;

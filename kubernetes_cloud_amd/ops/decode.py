@@ -13,6 +13,8 @@ layer); a request owns one slot for its lifetime.
 """
 from __future__ import annotations
 
+import os
+
 import math
 
 import torch
@@ -63,12 +65,16 @@ def decode_ws_floats(B: int, H: int, Hkv: int, D: int, max_kv: int, chunk: int =
     return B * H * ns * (D + 2) if ns > 1 else 0
 
 
+_DECODE_WGS = int(os.environ.get("KCA_DECODE_WGS", "1024"))  # split-K workgroup target (A/B knob)
+
+
 def decode_chunk(B: int, Hkv: int, max_kv: int) -> int:
-    """Mirror of kca_decode_chunk: ~2048 (seq, head, split) workgroups (8 per
-    CU: each split's K then V stream is latency bound, so bandwidth comes
-    from workgroup count), chunks of 32..1024 tokens."""
+    """Mirror of kca_decode_chunk: ~1024 (seq, head, split) workgroups, 4 per
+    CU (each split's K then V stream is latency bound, so bandwidth comes from
+    workgroup count; swept 256..2048 on MI355X, GPT-J B=8/32 best at 1024),
+    chunks of 32..1024 tokens."""
     work = B * Hkv
-    want = -(-2048 // work)
+    want = -(-_DECODE_WGS // work)
     c = -(-max_kv // want)
     c = -(-c // 32) * 32
     return max(32, min(1024, c))
