@@ -291,7 +291,9 @@ static void launch_skinny(const bf16_t* x, long long ldx, const bf16_t* w, const
   int kc = (32768 / M) / 512 * 512;  // M*kc*2 B <= 64 KB of LDS
   if (kc < 512) kc = 512;
   if (kc > K || LN) kc = (K + 7) / 8 * 8;
-  if constexpr (M == 1) if (g_skinny_sk) {
+  // the LN prologue is redone by every workgroup: at BLOOM's K = 14336 the 4x workgroup count of the
+  // split-K form costs more than it saves (B=1 8.75 -> 9.47 ms/token), so wide LN rows stay row-per-wave
+  if constexpr (M == 1) if (g_skinny_sk && !(LN && K > 8192)) {
     const dim3 grid((N + R - 1) / R);
     hipLaunchKernelGGL((skinny_gemm_sk_kernel<M, R, LN>), grid, dim3(256), (size_t)M * kc * sizeof(bf16_t), s,
                        x, ldx, w, bias, y, ldy, N, K, kc, act, mv, ln);
