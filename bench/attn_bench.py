@@ -27,6 +27,7 @@ SHAPES = {
     "gpt2": (16, 1024, 1024, 12, 64, True),
     "bloom_tp8": (4, 2048, 2048, 14, 128, True),
     "sd_64": (16, 4096, 4096, 8, 40, False),
+    "sd_64_pad64": (16, 4096, 4096, 8, 64, False),  # SD heads zero-padded 40 -> 64 (UNet inference path)
     "sd_32": (16, 1024, 1024, 8, 80, False),
     "sd_cross": (16, 4096, 77, 8, 40, False),
 }

@@ -1,4 +1,5 @@
-// Flash attention forward, full-tile fast path for head_dim 128 / 256 (K2).
+// Flash attention forward, full-tile fast path for head_dim 64 / 128 / 256 (K2);
+// backward for 128 / 256.
 //
 // The generic kernels in attention.hip handle every shape (ALiBi, per-batch
 // key lengths, ragged tiles, padded head dims). This file holds the path the
@@ -577,7 +578,7 @@ KCA_API int kca_attn_fwd_tiled(const void* q, const void* k, const void* v, void
                                long long v_sh, long long o_sb, long long o_st, long long o_sh,
                                int B, int Sq, int Sk, int H, int Hkv, int d, int causal,
                                float scale, int* flags, hipStream_t stream) {
-  if ((d != 128 && d != 256) || Sq % 128 || Sk % 32 || Sq <= 0 || H % Hkv || !flags) return 1;
+  if ((d != 64 && d != 128 && d != 256) || Sq % 128 || Sk % 32 || Sq <= 0 || H % Hkv || !flags) return 1;
   if (causal && Sk < Sq) return 1;
   FastFwdParams p{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, lse, flags,
                   q_sb, q_st, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh, o_sb, o_st, o_sh,
@@ -587,9 +588,12 @@ KCA_API int kca_attn_fwd_tiled(const void* q, const void* k, const void* v, void
   if (d == 256) {
     if (causal) hipLaunchKernelGGL((attn_fwd_tiled_kernel<256, true>), grid, dim3(256), 0, stream, p);
     else hipLaunchKernelGGL((attn_fwd_tiled_kernel<256, false>), grid, dim3(256), 0, stream, p);
-  } else {
+  } else if (d == 128) {
     if (causal) hipLaunchKernelGGL((attn_fwd_tiled_kernel<128, true>), grid, dim3(256), 0, stream, p);
     else hipLaunchKernelGGL((attn_fwd_tiled_kernel<128, false>), grid, dim3(256), 0, stream, p);
+  } else {  // 64: GPT-2 / CLIP heads, SD-1.5 heads (40) zero-padded by the UNet inference path
+    if (causal) hipLaunchKernelGGL((attn_fwd_tiled_kernel<64, true>), grid, dim3(256), 0, stream, p);
+    else hipLaunchKernelGGL((attn_fwd_tiled_kernel<64, false>), grid, dim3(256), 0, stream, p);
   }
   // a failed launch leaves the flags unwritten: report it so the caller runs
   // the generic kernel on every block instead of trusting stale flags

@@ -81,8 +81,12 @@ class UNetGraph:
     def __init__(self, unet):
         self.unet = unet
         self.graphs: dict = {}
+        self.pad_gen = -1
 
     def __call__(self, x, t, ctx):
+        from .unet import pad_generation
+        if self.graphs and pad_generation() != self.pad_gen:
+            self.graphs.clear()  # padded attention weights were rebuilt: the graphs hold stale copies
         key = (tuple(x.shape), x.dtype, tuple(t.shape), tuple(ctx.shape), ctx.dtype)
         g = self.graphs.get(key)
         if g is None:
@@ -109,6 +113,8 @@ class UNetGraph:
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
                 out = self.unet(sx, st, sc)
+            from .unet import pad_generation
+            self.pad_gen = pad_generation()
             return graph, sx, st, sc, out
         except Exception as e:  # noqa: BLE001 - eager is always correct
             import sys

@@ -140,6 +140,18 @@ class ResnetBlock2D(nn.Module):
         return sc + h
 
 
+# Inference-only head padding for the self-attention (see Attention.forward);
+# KCA_SD_PAD_HEADS=0 disables. _PAD_GEN counts padded-weight rebuilds so a HIP
+# graph captured over the old buffers knows to re-capture (sd_pipeline.UNetGraph).
+PAD_HEAD_DIM = 64
+_PAD_HEADS = os.environ.get("KCA_SD_PAD_HEADS", "1") not in ("0", "false")
+_PAD_GEN = 0
+
+
+def pad_generation() -> int:
+    return _PAD_GEN
+
+
 class Attention(nn.Module):
     """diffusers Attention (to_q/to_k/to_v/to_out.0) over [B, S, C] tokens."""
 
@@ -151,9 +163,49 @@ class Attention(nn.Module):
         self.to_k = nn.Linear(cross_dim or dim, inner, bias=bias_qkv)
         self.to_v = nn.Linear(cross_dim or dim, inner, bias=bias_qkv)
         self.to_out = nn.ModuleList([nn.Linear(inner, dim), nn.Dropout(0.0)])
+        self._padded = None
+
+    def train(self, mode: bool = True):
+        self._padded = None  # weights may change while training: rebuild on the next inference call
+        return super().train(mode)
+
+    def _padded_weights(self, hd: int):
+        """One fused QKV weight with each head zero-padded to PAD_HEAD_DIM rows,
+        and the out-projection with matching zero columns (built once per
+        eval phase; ``train()`` drops it)."""
+        p = getattr(self, "_padded", None)
+        if p is None:
+            global _PAD_GEN
+            H, dp = self.heads, PAD_HEAD_DIM
+            C = self.to_q.weight.shape[1]
+            w = self.to_q.weight.new_zeros(3, H, dp, C)
+            b = self.to_q.weight.new_zeros(3, H, dp)
+            for i, lin in enumerate((self.to_q, self.to_k, self.to_v)):
+                w[i, :, :hd] = lin.weight.view(H, hd, C)
+                if lin.bias is not None:
+                    b[i, :, :hd] = lin.bias.view(H, hd)
+            has_b = any(lin.bias is not None for lin in (self.to_q, self.to_k, self.to_v))
+            wo = self.to_out[0].weight
+            wo_p = wo.new_zeros(wo.shape[0], H, dp)
+            wo_p[:, :, :hd] = wo.view(wo.shape[0], H, hd)
+            p = self._padded = (w.view(3 * H * dp, C), b.view(-1) if has_b else None, wo_p.view(wo.shape[0], H * dp))
+            _PAD_GEN += 1
+        return p
 
     def forward(self, x, ctx=None):
         B, S, _ = x.shape
+        hd = self.to_q.weight.shape[0] // self.heads
+        if (ctx is None and not torch.is_grad_enabled() and x.is_cuda and hd < PAD_HEAD_DIM and hd % 8 == 0
+                and S % 128 == 0 and _PAD_HEADS):
+            # inference self-attention on the full-tile D=64 kernel (attention_tiled.hip):
+            # zero q/k columns leave Q.K^T unchanged, zero v columns give zero outputs that
+            # meet zero out-projection columns. SD-1.5 64x64-latent self-attention (B16 H8
+            # S4096 d40) 1.04 -> 0.71 ms on MI355X (profiles/attn_bench_r1_v7_d64.jsonl).
+            w, b, wo = self._padded_weights(hd)
+            qkv = F.linear(x, w, b).view(B, S, 3, self.heads, PAD_HEAD_DIM)
+            o = ops.flash_attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], causal=False,
+                                    scale=1.0 / math.sqrt(hd))
+            return F.linear(o.reshape(B, S, -1), wo, self.to_out[0].bias)
         c = x if ctx is None else ctx
         q = self.to_q(x)
         k = self.to_k(c)

@@ -152,8 +152,9 @@ def test_attention_tiled_fast_path(D, causal):
     _attn_case(1, 256, 288, 2, 2, D, causal, check_bwd=False)  # fwd tiled, bwd generic (Sk % 128)
 
 
-@pytest.mark.parametrize("D", [128, 256])
-def test_attention_tiled_matches_generic(D):
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("D", [64, 128, 256])
+def test_attention_tiled_matches_generic(D, causal):
     """Fast and generic kernels agree (fwd output and all three grads)."""
     from kubernetes_cloud_amd.ops.attention import set_tiled_path
     torch.manual_seed(5)
@@ -165,7 +166,7 @@ def test_attention_tiled_matches_generic(D):
         set_tiled_path(tiled)
         try:
             qq, kk, vv = (t.clone().requires_grad_() for t in (q, k, v))
-            o = ops.flash_attention(qq, kk, vv, causal=True)
+            o = ops.flash_attention(qq, kk, vv, causal=causal)
             o.backward(g)
             outs.append((o.float(), qq.grad.float(), kk.grad.float(), vv.grad.float()))
         finally:
@@ -174,7 +175,7 @@ def test_attention_tiled_matches_generic(D):
         assert _rel(a, b) < 1e-2, _rel(a, b)
 
 
-@pytest.mark.parametrize("D", [128, 256])
+@pytest.mark.parametrize("D", [64, 128, 256])
 def test_attention_deferred_rescale_branch(D):
     """Scores whose row max keeps growing tile after tile (ramped key norms and
     a hot key per tile), so the deferred-rescale branch of the forward fires
@@ -193,7 +194,7 @@ def test_attention_deferred_rescale_branch(D):
         assert _rel(o, orf) < 2e-2, (causal, _rel(o, orf))
 
 
-@pytest.mark.parametrize("D", [128, 256])
+@pytest.mark.parametrize("D", [64, 128, 256])
 def test_attention_tiled_overflow_fixup(D):
     """A key far past the first tile scores ~2^900 times higher than anything in
     tile 0: the fixed-reference-max fast path overflows, flags the rows, and the
@@ -561,3 +562,26 @@ def test_engine_fused_block_matches_unfused(monkeypatch):
         out.append(eng.flat.float().clone())
         eng.remove_hooks()
     assert _rel(out[0], out[1]) < 5e-3
+
+
+def test_unet_padded_head_self_attention():
+    """Inference self-attention with 40-wide heads zero-padded to 64 (fused
+    padded QKV GEMM + D=64 full-tile kernel, models/unet.py Attention.forward)
+    matches the unpadded path, and a weight change is picked up after
+    train()/eval() (the padded copies are rebuilt, UNetGraph re-captures)."""
+    from kubernetes_cloud_amd.models import unet as unet_mod
+    torch.manual_seed(0)
+    a = unet_mod.Attention(320, 8, 40).to(DEV, torch.bfloat16).eval()
+    x = torch.randn(2, 256, 320, device=DEV, dtype=torch.bfloat16)
+    ref = a(x)  # grad enabled: standard unpadded path
+    gen0 = unet_mod.pad_generation()
+    with torch.no_grad():
+        out = a(x)
+        assert a._padded is not None and unet_mod.pad_generation() == gen0 + 1
+        assert _rel(out, ref) < 2e-2, _rel(out, ref)
+        a.to_v.weight.data.mul_(-1.0)  # in-place update without a version bump (native optimizers)
+        a.train()
+        a.eval()
+        out2 = a(x)
+    assert unet_mod.pad_generation() == gen0 + 2
+    assert _rel(out2, a(x)) < 2e-2

@@ -20,6 +20,7 @@ import torch  # noqa: E402
 def timed(fn, iters):
     fn()
     torch.cuda.synchronize()
+    time.sleep(1.0)  # idle gap: marks the start of the steady-state dispatches in a kernel trace
     t = time.perf_counter()
     for _ in range(iters):
         fn()
