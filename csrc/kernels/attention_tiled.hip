@@ -1,5 +1,4 @@
-// Flash attention forward, full-tile fast path for head_dim 64 / 128 / 256 (K2);
-// backward for 128 / 256.
+// Flash attention forward + backward, full-tile fast path for head_dim 64 / 128 / 256 (K2).
 //
 // The generic kernels in attention.hip handle every shape (ALiBi, per-batch
 // key lengths, ragged tiles, padded head dims). This file holds the path the
@@ -609,7 +608,7 @@ KCA_API int kca_attn_bwd_tiled(const void* q, const void* k, const void* v, cons
                                long long dk_st, long long dk_sh, long long dv_sb, long long dv_st,
                                long long dv_sh, int B, int Sq, int Sk, int H, int Hkv, int d,
                                int causal, float scale, hipStream_t stream) {
-  if ((d != 128 && d != 256) || Sq % 128 || Sk % 128 || Sq <= 0 || H % Hkv) return 1;
+  if ((d != 64 && d != 128 && d != 256) || Sq % 128 || Sk % 128 || Sq <= 0 || H % Hkv) return 1;
   if (causal && Sk < Sq) return 1;
   FastBwdParams p{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout,
                   (bf16_t*)dq, (bf16_t*)dk, (bf16_t*)dv, lse, delta,
@@ -625,13 +624,21 @@ KCA_API int kca_attn_bwd_tiled(const void* q, const void* k, const void* v, cons
       hipLaunchKernelGGL((attn_bwd_dkdv_tiled_kernel<256, false>), g1, dim3(256), 0, stream, p);
       hipLaunchKernelGGL((attn_bwd_dq_tiled_kernel<256, false>), g2, dim3(256), 0, stream, p);
     }
-  } else {
+  } else if (d == 128) {
     if (causal) {
       hipLaunchKernelGGL((attn_bwd_dkdv_tiled_kernel<128, true>), g1, dim3(256), 0, stream, p);
       hipLaunchKernelGGL((attn_bwd_dq_tiled_kernel<128, true>), g2, dim3(256), 0, stream, p);
     } else {
       hipLaunchKernelGGL((attn_bwd_dkdv_tiled_kernel<128, false>), g1, dim3(256), 0, stream, p);
       hipLaunchKernelGGL((attn_bwd_dq_tiled_kernel<128, false>), g2, dim3(256), 0, stream, p);
+    }
+  } else {
+    if (causal) {
+      hipLaunchKernelGGL((attn_bwd_dkdv_tiled_kernel<64, true>), g1, dim3(256), 0, stream, p);
+      hipLaunchKernelGGL((attn_bwd_dq_tiled_kernel<64, true>), g2, dim3(256), 0, stream, p);
+    } else {
+      hipLaunchKernelGGL((attn_bwd_dkdv_tiled_kernel<64, false>), g1, dim3(256), 0, stream, p);
+      hipLaunchKernelGGL((attn_bwd_dq_tiled_kernel<64, false>), g2, dim3(256), 0, stream, p);
     }
   }
   return 0;

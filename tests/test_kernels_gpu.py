@@ -585,3 +585,27 @@ def test_unet_padded_head_self_attention():
         out2 = a(x)
     assert unet_mod.pad_generation() == gen0 + 2
     assert _rel(out2, a(x)) < 2e-2
+
+
+def test_unet_padded_head_self_attention_training_grads():
+    """Training self-attention with 40-wide heads padded to 64 (activation pad,
+    D=64 full-tile fwd/bwd kernels) gives the same output and parameter
+    gradients as the unpadded generic path (KCA_SD_PAD_HEADS_TRAIN opt-in)."""
+    from kubernetes_cloud_amd.models import unet as unet_mod
+    torch.manual_seed(1)
+    a = unet_mod.Attention(320, 8, 40).to(DEV, torch.bfloat16).train()
+    x = torch.randn(2, 256, 320, device=DEV, dtype=torch.bfloat16)
+    g = torch.randn(2, 256, 320, device=DEV, dtype=torch.bfloat16)
+    res = []
+    for padded in (True, False):
+        unet_mod._PAD_HEADS = unet_mod._PAD_TRAIN = padded
+        try:
+            a.zero_grad(set_to_none=True)
+            xx = x.clone().requires_grad_()
+            y = a(xx)
+            y.backward(g)
+            res.append((y.float(), xx.grad.float(), a.to_q.weight.grad.float(), a.to_v.weight.grad.float()))
+        finally:
+            unet_mod._PAD_HEADS, unet_mod._PAD_TRAIN = True, False
+    for p_, u_ in zip(*res):
+        assert _rel(p_, u_) < 2e-2, _rel(p_, u_)
