@@ -100,7 +100,8 @@ __global__ void __launch_bounds__(256) nhwc_chunk_stats(const bf16_t* __restrict
 __global__ void __launch_bounds__(256) nhwc_group_stats(const float* __restrict__ part, int P, int C, int G,
                                                         int nchunks, float eps, float* __restrict__ mean_out,
                                                         float* __restrict__ rstd_out, const bf16_t* __restrict__ w,
-                                                        const bf16_t* __restrict__ b, float* __restrict__ ss) {
+                                                        const bf16_t* __restrict__ b, float* __restrict__ ss,
+                                                        const float* __restrict__ add) {
   __shared__ float red[3 * 256];
   const int ng = blockIdx.x, n = ng / G, g = ng % G, cg = C / G;
   const int items = nchunks * cg, CH = chunk_of(P);
@@ -109,7 +110,8 @@ __global__ void __launch_bounds__(256) nhwc_group_stats(const float* __restrict_
     const int ch = i / cg, c = g * cg + i % cg;
     const float cn = (float)(min(P, (ch + 1) * CH) - ch * CH);
     const float* s = part + (((long long)n * nchunks + ch) * C + c) * 2;
-    chan_merge(cnt, mu, q, cn, s[0], s[1]);
+    // a per-(n, c) pre-add shifts that channel's mean and leaves its M2 unchanged
+    chan_merge(cnt, mu, q, cn, s[0] + (add ? add[(long long)n * C + c] : 0.f), s[1]);
   }
   red[threadIdx.x] = cnt;
   red[256 + threadIdx.x] = mu;
@@ -134,8 +136,9 @@ __global__ void __launch_bounds__(256) nhwc_group_stats(const float* __restrict_
   for (int j = threadIdx.x; j < cg; j += blockDim.x) {
     const int c = g * cg + j;
     const float sc = rs_g * bf2f(w[c]);
+    const float t = add ? add[(long long)n * C + c] : 0.f;  // y = (x + t - mu) * sc + b
     ss[((long long)n * 2) * C + c] = sc;
-    ss[((long long)n * 2 + 1) * C + c] = (b ? bf2f(b[c]) : 0.f) - mu_g * sc;
+    ss[((long long)n * 2 + 1) * C + c] = (b ? bf2f(b[c]) : 0.f) + (t - mu_g) * sc;
   }
 }
 
@@ -321,9 +324,13 @@ KCA_API int kca_groupnorm_nhwc_ws(int N, int P, int C) {  // fp32 workspace floa
   return 2 * N * nchunks * C + 2 * N * C;
 }
 
-// x, y: [N, P, C] bf16; mean/rstd: [N*G] fp32 out; ws: kca_groupnorm_nhwc_ws floats
-KCA_API int kca_groupnorm_nhwc_fwd(const void* x, const void* w, const void* b, void* y, float* mean, float* rstd,
-                                   float* ws, int N, int P, int C, int G, float eps, int silu, hipStream_t stream) {
+// x, y: [N, P, C] bf16; mean/rstd: [N*G] fp32 out; ws: kca_groupnorm_nhwc_ws floats;
+// add: optional fp32 [N, C] added to x before the norm (the ResNet block's time
+// embedding, folded into the statistics and the apply pass's shift: no extra
+// pass over x and no materialised x + temb)
+KCA_API int kca_groupnorm_nhwc_fwd_add(const void* x, const void* w, const void* b, const float* add, void* y,
+                                       float* mean, float* rstd, float* ws, int N, int P, int C, int G, float eps,
+                                       int silu, hipStream_t stream) {
   dim3 block;
   int slabs;
   if (!geometry(C, G, block, slabs) || N <= 0 || P <= 0) return 1;
@@ -333,11 +340,16 @@ KCA_API int kca_groupnorm_nhwc_fwd(const void* x, const void* w, const void* b, 
   hipLaunchKernelGGL(nhwc_chunk_stats, dim3(nchunks, N, slabs), block, smem, stream, (const bf16_t*)x, P, C, ws);
   float* ss = ws + 2LL * N * nchunks * C;
   hipLaunchKernelGGL(nhwc_group_stats, dim3(N * G), dim3(256), 0, stream, ws, P, C, G, nchunks, eps, mean, rstd,
-                     (const bf16_t*)w, (const bf16_t*)b, ss);
+                     (const bf16_t*)w, (const bf16_t*)b, ss, add);
   const int nvec = (int)((long long)N * P * C / 8);
   hipLaunchKernelGGL(nhwc_apply, dim3(kca_grid(nvec, 256, 8192)), dim3(256), 0, stream, (const bf16_t*)x, ss,
                      (bf16_t*)y, P, C, silu, nvec);
   return 0;
+}
+
+KCA_API int kca_groupnorm_nhwc_fwd(const void* x, const void* w, const void* b, void* y, float* mean, float* rstd,
+                                   float* ws, int N, int P, int C, int G, float eps, int silu, hipStream_t stream) {
+  return kca_groupnorm_nhwc_fwd_add(x, w, b, nullptr, y, mean, rstd, ws, N, P, C, G, eps, silu, stream);
 }
 
 // ws: kca_groupnorm_nhwc_ws floats + 2*N*G floats

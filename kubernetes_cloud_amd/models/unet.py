@@ -87,8 +87,8 @@ class GroupNorm(nn.GroupNorm):
         super().__init__(groups, ch, eps=eps)
         self.silu = silu
 
-    def forward(self, x):
-        return ops.group_norm(x, self.num_groups, self.weight, self.bias, self.eps, silu=self.silu)
+    def forward(self, x, add=None):
+        return ops.group_norm(x, self.num_groups, self.weight, self.bias, self.eps, silu=self.silu, add=add)
 
 
 class LayerNorm(nn.LayerNorm):
@@ -135,19 +135,20 @@ class ResnetBlock2D(nn.Module):
 
     def forward(self, x, temb=None):
         h = self.conv1(self.norm1(x))
+        t = None
         if self.time_emb_proj is not None and temb is not None:
-            h = h + self.time_emb_proj(F.silu(temb))[:, :, None, None]
-        h = self.conv2(self.dropout(self.norm2(h)))
+            t = self.time_emb_proj(F.silu(temb))  # added to h inside norm2 (fused at inference)
+        h = self.conv2(self.dropout(self.norm2(h, add=t)))
         sc = self.conv_shortcut(x) if self.conv_shortcut is not None else x
         return sc + h
 
 
-# Inference-only head padding for the self-attention (see Attention.forward);
-# KCA_SD_PAD_HEADS=0 disables. _PAD_GEN counts padded-weight rebuilds so a HIP
+# Head padding for the self-attention (see Attention.forward); KCA_SD_PAD_HEADS=0
+# disables it, KCA_SD_PAD_HEADS_TRAIN=0 only in training. _PAD_GEN counts padded-weight rebuilds so a HIP
 # graph captured over the old buffers knows to re-capture (sd_pipeline.UNetGraph).
 PAD_HEAD_DIM = 64
 _PAD_HEADS = os.environ.get("KCA_SD_PAD_HEADS", "1") not in ("0", "false")
-_PAD_TRAIN = os.environ.get("KCA_SD_PAD_HEADS_TRAIN", "0") not in ("0", "false")
+_PAD_TRAIN = os.environ.get("KCA_SD_PAD_HEADS_TRAIN", "1") not in ("0", "false")
 _PAD_GEN = 0
 
 
@@ -202,14 +203,15 @@ class Attention(nn.Module):
         if pad and torch.is_grad_enabled() and _PAD_TRAIN:
             # training: pad the q/k/v activations instead (F.pad's backward slices the
             # gradients back) so the backward also runs the full-tile D=64 kernels.
-            # Off by default: the attention itself gets faster (fwd+bwd 4.50 -> 3.31 ms)
-            # but the pad/slice copies cost more, DreamBooth 96.1 -> 93.6 samples/s.
+            # Attention fwd+bwd 4.50 -> 3.31 ms; DreamBooth 93.4 -> 96.4 samples/s
+            # (same-box A/B, profiles/sd_bench_r1_v11_gn_add_padtrain.jsonl);
+            # KCA_SD_PAD_HEADS_TRAIN=0 disables.
             dp = PAD_HEAD_DIM - hd
             q, k, v = (F.pad(lin(x).view(B, S, self.heads, hd), (0, dp))
                        for lin in (self.to_q, self.to_k, self.to_v))
             o = ops.flash_attention(q, k, v, causal=False, scale=1.0 / math.sqrt(hd))
             return self.to_out[0](o[..., :hd].reshape(B, S, -1))
-        if pad:
+        if pad and not torch.is_grad_enabled():
             # inference self-attention on the full-tile D=64 kernel (attention_tiled.hip):
             # zero q/k columns leave Q.K^T unchanged, zero v columns give zero outputs that
             # meet zero out-projection columns. SD-1.5 64x64-latent self-attention (B16 H8

@@ -65,6 +65,7 @@ _SIGS = {
     "kca_groupnorm_bwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P],
     "kca_groupnorm_nhwc_ws": [I, I, I],
     "kca_groupnorm_nhwc_fwd": [P, P, P, P, P, P, P, I, I, I, I, F, I, P],
+    "kca_groupnorm_nhwc_fwd_add": [P, P, P, P, P, P, P, P, I, I, I, I, F, I, P],
     "kca_groupnorm_nhwc_bwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P],
     "kca_skinny_gemm": [P, LL, P, P, P, LL, I, I, I, I, P],
     "kca_skinny_set_splitk": [I],

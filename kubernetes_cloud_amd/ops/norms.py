@@ -160,12 +160,35 @@ def _channels_last(x: torch.Tensor) -> bool:
     return x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last) and not x.is_contiguous()
 
 
+def _group_norm_nhwc_add(x, add, weight, bias, groups, eps, silu):
+    """Inference GroupNorm of ``x + add[:, :, None, None]`` without forming the sum."""
+    n, c = x.shape[0], x.shape[1]
+    p = x.numel() // (n * c)
+    add = add.to(torch.float32).contiguous()
+    y = torch.empty_like(x)
+    mean = torch.empty(n * groups, device=x.device, dtype=torch.float32)
+    rstd = torch.empty_like(mean)
+    ws = torch.empty(_lib.require().kca_groupnorm_nhwc_ws(n, p, c), device=x.device, dtype=torch.float32)
+    _lib.call("kca_groupnorm_nhwc_fwd_add", x.data_ptr(), weight.data_ptr(), _lib.ptr(bias), add.data_ptr(),
+              y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), ws.data_ptr(), n, p, c, groups, float(eps),
+              int(silu), _lib.stream())
+    return y
+
+
 def group_norm(x: torch.Tensor, groups: int, weight: torch.Tensor, bias: torch.Tensor | None,
-               eps: float = 1e-5, silu: bool = False) -> torch.Tensor:
+               eps: float = 1e-5, silu: bool = False, add: torch.Tensor | None = None) -> torch.Tensor:
     """GroupNorm over NC* tensors, optionally fused with SiLU (UNet/VAE ResNet blocks).
-    Channels-last 4-D inputs stay channels-last (NHWC kernels)."""
-    if (_lib.use_native(x) and x.dtype == torch.bfloat16 and _channels_last(x) and x.shape[1] % 8 == 0
-            and weight is not None and _lib.has("kca_groupnorm_nhwc_fwd")):
+    Channels-last 4-D inputs stay channels-last (NHWC kernels). ``add`` ([N, C]):
+    normalise ``x + add[:, :, None, None]`` (the ResNet block's time embedding);
+    fused into the statistics and the apply pass when no gradient is needed."""
+    nhwc = (_lib.use_native(x) and x.dtype == torch.bfloat16 and _channels_last(x) and x.shape[1] % 8 == 0
+            and weight is not None and _lib.has("kca_groupnorm_nhwc_fwd"))
+    if add is not None:
+        if (nhwc and not torch.is_grad_enabled() and add.shape == x.shape[:2]
+                and _lib.has("kca_groupnorm_nhwc_fwd_add")):
+            return _group_norm_nhwc_add(x, add, weight, bias, groups, eps, silu)
+        x = x + add[:, :, None, None]
+    if nhwc:
         return _GroupNormNHWCFn.apply(x, weight, bias, groups, eps, silu)
     if _lib.use_native(x) and x.dtype == torch.bfloat16 and _lib.has("kca_groupnorm_fwd"):
         return _GroupNormFn.apply(x, weight, bias, groups, eps, silu)

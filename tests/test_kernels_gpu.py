@@ -590,7 +590,7 @@ def test_unet_padded_head_self_attention():
 def test_unet_padded_head_self_attention_training_grads():
     """Training self-attention with 40-wide heads padded to 64 (activation pad,
     D=64 full-tile fwd/bwd kernels) gives the same output and parameter
-    gradients as the unpadded generic path (KCA_SD_PAD_HEADS_TRAIN opt-in)."""
+    gradients as the unpadded generic path (KCA_SD_PAD_HEADS_TRAIN=0)."""
     from kubernetes_cloud_amd.models import unet as unet_mod
     torch.manual_seed(1)
     a = unet_mod.Attention(320, 8, 40).to(DEV, torch.bfloat16).train()
@@ -606,6 +606,26 @@ def test_unet_padded_head_self_attention_training_grads():
             y.backward(g)
             res.append((y.float(), xx.grad.float(), a.to_q.weight.grad.float(), a.to_v.weight.grad.float()))
         finally:
-            unet_mod._PAD_HEADS, unet_mod._PAD_TRAIN = True, False
+            unet_mod._PAD_HEADS, unet_mod._PAD_TRAIN = True, True
     for p_, u_ in zip(*res):
         assert _rel(p_, u_) < 2e-2, _rel(p_, u_)
+
+
+@pytest.mark.parametrize("silu", [False, True])
+def test_groupnorm_nhwc_fused_add(silu):
+    """Inference GroupNorm of x + t[:, :, None, None] with the per-(n, c) add
+    folded into the statistics and the apply shift (kca_groupnorm_nhwc_fwd_add)
+    vs the fp32 reference of the materialised sum."""
+    torch.manual_seed(2)
+    N, C, H, W, G = 3, 320, 16, 24, 32
+    x = torch.randn(N, C, H, W, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
+    t = (torch.randn(N, C, device=DEV) * 3.0).bfloat16()
+    w = torch.randn(C, device=DEV).bfloat16()
+    b = torch.randn(C, device=DEV).bfloat16()
+    with torch.no_grad():
+        y = ops.group_norm(x, G, w, b, 1e-5, silu=silu, add=t)
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    yr = F.group_norm(x.float() + t.float()[:, :, None, None], G, w.float(), b.float(), 1e-5)
+    if silu:
+        yr = F.silu(yr)
+    assert _rel(y, yr) < 1e-2, _rel(y, yr)
