@@ -67,3 +67,56 @@ def test_kubeconfig_parsing(tmp_path):
     api = K8sREST.from_kubeconfig(str(p))
     assert str(api.http.base_url).startswith("https://api.example:6443")
     assert api.http.headers["Authorization"] == "Bearer abc"
+
+
+def test_workstation_bootstrap_offline_mirror(tmp_path, monkeypatch):
+    """P6 (getting-started/k8ctl_setup.ps1): plan per OS/arch, install the
+    three CLIs from a file:// mirror (helm out of its archive), import the
+    kubeconfig, uninstall."""
+    import io
+    import json
+    import tarfile
+    import zipfile
+
+    from kubernetes_cloud_amd.platform import workstation as ws
+
+    assert ws.host_target("Windows", "AMD64") == ("windows", "amd64")
+    assert ws.host_target("Linux", "aarch64") == ("linux", "arm64")
+    p = {e["tool"]: e for e in ws.plan("windows", "amd64", ws.PINNED)}
+    assert p["kubectl"]["url"].endswith("/bin/windows/amd64/kubectl.exe")
+    assert p["helm"]["url"].endswith(".zip") and p["helm"]["member"] == "windows-amd64/helm.exe"
+    assert p["virtctl"]["binary"] == "virtctl.exe"
+
+    mirror = tmp_path / "mirror"
+    for e in ws.plan("linux", "amd64", ws.PINNED, f"file://{mirror}"):
+        f = mirror / e["tool"] / e["version"]
+        f.mkdir(parents=True)
+        asset = e["url"].rsplit("/", 1)[1]
+        if e["member"]:
+            with tarfile.open(f / asset, "w:gz") as t:
+                data = b"#!/bin/sh\necho helm\n"
+                info = tarfile.TarInfo(e["member"])
+                info.size = len(data)
+                t.addfile(info, io.BytesIO(data))
+        else:
+            (f / asset).write_bytes(b"#!/bin/sh\necho " + e["tool"].encode() + b"\n")
+    monkeypatch.setenv("HOME", str(tmp_path / "home"))
+    monkeypatch.setattr(ws.shutil, "which", lambda name: None)
+    kc = tmp_path / "cw-kubeconfig"
+    kc.write_text("apiVersion: v1\nkind: Config\n")
+    dest = tmp_path / "k8s"
+    rc = ws.main(["--dest", str(dest), "--os", "linux", "--arch", "amd64", "--mirror", f"file://{mirror}",
+                  "--kubeconfig", str(kc)])
+    assert rc == 0
+    for b in ("kubectl", "virtctl", "helm"):
+        assert (dest / b).exists() and (dest / b).stat().st_mode & 0o111
+    assert (tmp_path / "home" / ".kube" / "config").read_text().startswith("apiVersion")
+    assert ws.main(["--dest", str(dest), "--uninstall"]) == 0 and not dest.exists()
+    # the zip layout used on Windows
+    z = tmp_path / "h.zip"
+    with zipfile.ZipFile(z, "w") as zz:
+        zz.writestr("windows-amd64/helm.exe", b"MZ")
+    ent = [{"tool": "helm", "version": "v0", "url": f"file://{z}", "member": "windows-amd64/helm.exe",
+            "binary": "helm.exe"}]
+    assert ws.install(ent, str(tmp_path / "w"))[0].endswith("helm.exe")
+    assert json.loads(json.dumps(ws.plan("darwin", "arm64", ws.PINNED)))[2]["url"].endswith("darwin-arm64.tar.gz")
