@@ -9,9 +9,9 @@
 // per channel).
 //
 //   fwd  1) chunk_stats : workgroup = (n, pixel chunk), thread tile =
-//                         (8-channel vector, pixel row); per-channel Welford
-//                         over the thread's pixels, merged over the rows in
-//                         LDS -> (mean, M2) per (n, chunk, c)
+//                         (8-channel vector, pixel row); per-channel sums
+//                         shifted by the chunk's first pixel, added over the
+//                         rows in LDS -> (mean, M2) per (n, chunk, c)
 //        2) group_stats : workgroup per (n, g): Chan-merges chunks x cg
 //                         partials -> mean, rstd (exact parallel Welford, no
 //                         E[x^2] - E[x]^2 cancellation)
@@ -20,7 +20,8 @@
 //                         (dz = dy * silu'(z) when SiLU is fused)
 //        2) group_grads : per (n, g) the gamma-weighted means m1, m2
 //        3) chan_grads  : dgamma / dbeta per channel over (n, chunk)
-//        4) dx          : rstd * (dz*gamma - m1 - xhat*m2)
+//        4) dx          : rstd * (dz*gamma - m1 - xhat*m2), from per-(n, c)
+//                         coefficients written by group_grads
 // No atomics anywhere (deterministic).
 #include "common.h"
 
@@ -51,48 +52,58 @@ __device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, flo
 // concat takes two)
 __global__ void __launch_bounds__(256) nhwc_chunk_stats(const bf16_t* __restrict__ x, int P, int C,
                                                         float* __restrict__ part) {
-  extern __shared__ float sm[];  // [R][W] mean, [R][W] m2, [R] count; W = slab width in channels
-  const int lv = threadIdx.x, r = threadIdx.y, R = blockDim.y, W = blockDim.x * 8;
-  const int cv = blockIdx.z * blockDim.x + lv;
+  // Shifted sums: every thread accumulates sum(v - K) and sum((v - K)^2) with
+  // K = the chunk's first pixel of that channel (one data point, so |mean - K|
+  // is O(std) and the final M2 = S2 - S1^2/N does not cancel), as independent
+  // FMAs per pixel -- no per-pixel division and no serial Welford chain, so
+  // the unrolled loads stay in flight. Rows of the workgroup share K, so
+  // their partials merge by plain addition.
+  extern __shared__ float sm[];  // [8][R][bw] s1, then [8][R][bw] s2 (lane-contiguous: conflict free)
+  const int lv = threadIdx.x, r = threadIdx.y, R = blockDim.y, bw = blockDim.x;
+  const int tid = r * bw + lv, nthr = R * bw;
+  const int cv = blockIdx.z * bw + lv;
   const bool live = cv * 8 < C;
   const int n = blockIdx.y, chunk = blockIdx.x, nchunks = gridDim.x, CH = chunk_of(P);
   const int p0 = chunk * CH, p1 = min(P, p0 + CH);
-  float mean[8], m2[8], cnt = 0.f;
+  const bf16_t* base = x + ((long long)n * P) * C;
+  float k[8], s1[8], s2[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) mean[j] = m2[j] = 0.f;
-  const bf16_t* base = x + ((long long)n * P) * C + cv * 8;
+  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
+  if (live) {
+    load8(base + (long long)p0 * C + cv * 8, k);
 #pragma unroll 4
-  for (int p = p0 + r; live && p < p1; p += R) {
-    float v[8];
-    load8(base + (long long)p * C, v);
-    cnt += 1.f;
-    const float inv = 1.f / cnt;
+    for (int p = p0 + r; p < p1; p += R) {
+      float v[8];
+      load8(base + (long long)p * C + cv * 8, v);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float d = v[j] - mean[j];
-      mean[j] += d * inv;
-      m2[j] += d * (v[j] - mean[j]);
+      for (int j = 0; j < 8; ++j) {
+        const float d = v[j] - k[j];
+        s1[j] += d;
+        s2[j] = fmaf(d, d, s2[j]);
+      }
     }
   }
-  float* smean = sm;
-  float* sm2 = sm + R * W;
-  float* scnt = sm + 2 * R * W;
+  float* a1 = sm;
+  float* a2 = sm + 8 * R * bw;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    smean[r * W + lv * 8 + j] = mean[j];
-    sm2[r * W + lv * 8 + j] = m2[j];
+    a1[(j * R + r) * bw + lv] = s1[j];
+    a2[(j * R + r) * bw + lv] = s2[j];
   }
-  if (lv == 0) scnt[r] = (float)((p1 - p0 - r + R - 1) / R);
   __syncthreads();
-  if (r == 0 && live) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float nn = scnt[0], mu = smean[lv * 8 + j], q = sm2[lv * 8 + j];
-      for (int rr = 1; rr < R; ++rr) chan_merge(nn, mu, q, scnt[rr], smean[rr * W + lv * 8 + j], sm2[rr * W + lv * 8 + j]);
-      float* dst = part + (((long long)n * nchunks + chunk) * C + cv * 8 + j) * 2;
-      dst[0] = mu;
-      dst[1] = q;
+  const float nn = (float)(p1 - p0), inv = 1.f / nn;
+  for (int i = tid; i < 8 * bw; i += nthr) {  // i = j * bw + lane
+    const int j = i / bw, l = i % bw, c = (blockIdx.z * bw + l) * 8 + j;
+    if (c >= C) continue;
+    float t1 = 0.f, t2 = 0.f;
+    for (int rr = 0; rr < R; ++rr) {
+      t1 += a1[(j * R + rr) * bw + l];
+      t2 += a2[(j * R + rr) * bw + l];
     }
+    const float kk = bf2f(base[(long long)p0 * C + c]);
+    float* dst = part + (((long long)n * nchunks + chunk) * C + c) * 2;
+    dst[0] = kk + t1 * inv;
+    dst[1] = fmaxf(t2 - t1 * t1 * inv, 0.f);
   }
 }
 
@@ -170,7 +181,7 @@ __global__ void __launch_bounds__(256) nhwc_chunk_grads(const bf16_t* __restrict
                                                         const float* __restrict__ rstd, int P, int C, int G, int silu,
                                                         float* __restrict__ part) {
   extern __shared__ float sm[];  // [R][W] s1, [R][W] s2
-  const int lv = threadIdx.x, r = threadIdx.y, R = blockDim.y, W = blockDim.x * 8;
+  const int lv = threadIdx.x, r = threadIdx.y, R = blockDim.y;
   const int cv = blockIdx.z * blockDim.x + lv;
   const bool live = cv * 8 < C;
   const int n = blockIdx.y, chunk = blockIdx.x, nchunks = gridDim.x, CH = chunk_of(P);
@@ -187,6 +198,7 @@ __global__ void __launch_bounds__(256) nhwc_chunk_grads(const bf16_t* __restrict
     s1[j] = s2[j] = 0.f;
   }
   const long long off = ((long long)n * P) * C + cv * 8;
+#pragma unroll 2
   for (int p = p0 + r; live && p < p1; p += R) {
     float v[8], g[8];
     load8(x + off + (long long)p * C, v);
@@ -199,33 +211,37 @@ __global__ void __launch_bounds__(256) nhwc_chunk_grads(const bf16_t* __restrict
       s2[j] += dz * xh;
     }
   }
+  // [8][R][bw] layout (lane-contiguous, conflict free); every thread of the
+  // workgroup then reduces one channel column over the R rows
+  const int bw = blockDim.x, tid = r * bw + lv, nthr = R * bw;
   float* a1 = sm;
-  float* a2 = sm + R * W;
+  float* a2 = sm + 8 * R * bw;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    a1[r * W + lv * 8 + j] = s1[j];
-    a2[r * W + lv * 8 + j] = s2[j];
+    a1[(j * R + r) * bw + lv] = s1[j];
+    a2[(j * R + r) * bw + lv] = s2[j];
   }
   __syncthreads();
-  if (r == 0 && live) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float t1 = 0.f, t2 = 0.f;
-      for (int rr = 0; rr < R; ++rr) {
-        t1 += a1[rr * W + lv * 8 + j];
-        t2 += a2[rr * W + lv * 8 + j];
-      }
-      float* dst = part + (((long long)n * nchunks + chunk) * C + cv * 8 + j) * 2;
-      dst[0] = t1;
-      dst[1] = t2;
+  for (int i = tid; i < 8 * bw; i += nthr) {  // i = j * bw + lane
+    const int j = i / bw, l = i % bw, c = (blockIdx.z * bw + l) * 8 + j;
+    if (c >= C) continue;
+    float t1 = 0.f, t2 = 0.f;
+    for (int rr = 0; rr < R; ++rr) {
+      t1 += a1[(j * R + rr) * bw + l];
+      t2 += a2[(j * R + rr) * bw + l];
     }
+    float* dst = part + (((long long)n * nchunks + chunk) * C + c) * 2;
+    dst[0] = t1;
+    dst[1] = t2;
   }
 }
 
 // per (n, g): m1 = sum_c gamma_c s1 / cnt, m2 = sum_c gamma_c s2 / cnt
 __global__ void __launch_bounds__(256) nhwc_group_grads(const float* __restrict__ part, const bf16_t* __restrict__ w,
-                                                        int P, int C, int G, int nchunks, float* __restrict__ m1,
-                                                        float* __restrict__ m2) {
+                                                        const bf16_t* __restrict__ b, const float* __restrict__ mean,
+                                                        const float* __restrict__ rstd, int P, int C, int G,
+                                                        int nchunks, float* __restrict__ m1, float* __restrict__ m2,
+                                                        float* __restrict__ coef) {
   __shared__ float red[2 * 256];
   const int ng = blockIdx.x, n = ng / G, g = ng % G, cg = C / G;
   float a = 0.f, b2 = 0.f;
@@ -246,63 +262,96 @@ __global__ void __launch_bounds__(256) nhwc_group_grads(const float* __restrict_
     }
     __syncthreads();
   }
+  const float inv = 1.f / ((float)P * cg);
+  const float gm1 = red[0] * inv, gm2 = red[256] * inv;
   if (threadIdx.x == 0) {
-    const float inv = 1.f / ((float)P * cg);
-    m1[ng] = red[0] * inv;
-    m2[ng] = red[256] * inv;
+    m1[ng] = gm1;
+    m2[ng] = gm2;
+  }
+  // dx = sc * dz + B * x + Cc with z = x * sc + sh (the forward's pre-SiLU value):
+  // sc = rstd*gamma, sh = beta - mean*sc, B = -rstd^2*m2, Cc = rstd*(rstd*m2*mean - m1)
+  const float mu = mean[ng], rs = rstd[ng];
+  for (int j = threadIdx.x; j < cg; j += blockDim.x) {
+    const int c = g * cg + j;
+    const float sc = rs * bf2f(w[c]);
+    float* cf = coef + (long long)n * 4 * C + c;
+    cf[0] = sc;
+    cf[C] = (b ? bf2f(b[c]) : 0.f) - mu * sc;
+    cf[2 * C] = -rs * rs * gm2;
+    cf[3 * C] = rs * (rs * gm2 * mu - gm1);
   }
 }
 
-// dgamma[c] = sum s2, dbeta[c] = sum s1 over the (n, chunk) rows; workgroup =
-// 64 channels x 4 row groups, LDS combine
+// grid ceil(C/16), block 256 = 16 channels x 16 row groups: dgamma / dbeta
+// per channel over the (n, chunk) rows. 16 row groups with 4 independent
+// accumulators each keep ~64 loads in flight per channel column (the earlier
+// 64-channel x 4-group shape left 5 workgroups on the chip for C = 320, each
+// thread walking 128+ rows serially: 33 us for 1.3 MB of partials).
 __global__ void __launch_bounds__(256) nhwc_chan_grads(const float* __restrict__ part, int rows, int C,
                                                        bf16_t* __restrict__ dw, bf16_t* __restrict__ db) {
-  __shared__ float red[2][4][64];
-  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
-  float a = 0.f, b2 = 0.f;
+  __shared__ float red[2][16][17];
+  const int cl = threadIdx.x & 15, rg = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
+  float a[4] = {0.f, 0.f, 0.f, 0.f}, q[4] = {0.f, 0.f, 0.f, 0.f};
   if (c < C) {
-    for (int r = rg; r < rows; r += 4) {
-      const float* s = part + ((long long)r * C + c) * 2;
-      a += s[0];
-      b2 += s[1];
+    int r = rg;
+    for (; r + 48 < rows; r += 64) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float2 s2 = *reinterpret_cast<const float2*>(part + ((long long)(r + 16 * u) * C + c) * 2);
+        a[u] += s2.x;
+        q[u] += s2.y;
+      }
+    }
+    for (; r < rows; r += 16) {
+      const float2 s2 = *reinterpret_cast<const float2*>(part + ((long long)r * C + c) * 2);
+      a[0] += s2.x;
+      q[0] += s2.y;
     }
   }
-  red[0][rg][cl] = a;
-  red[1][rg][cl] = b2;
+  red[0][rg][cl] = (a[0] + a[1]) + (a[2] + a[3]);
+  red[1][rg][cl] = (q[0] + q[1]) + (q[2] + q[3]);
   __syncthreads();
   if (rg == 0 && c < C) {
-    for (int k = 1; k < 4; ++k) {
-      a += red[0][k][cl];
-      b2 += red[1][k][cl];
+    float ta = 0.f, tq = 0.f;
+    for (int k = 0; k < 16; ++k) {
+      ta += red[0][k][cl];
+      tq += red[1][k][cl];
     }
-    dw[c] = f2bf(b2);
-    if (db) db[c] = f2bf(a);
+    dw[c] = f2bf(tq);
+    if (db) db[c] = f2bf(ta);
   }
 }
 
+// grid (chunks, N, channel slabs), block (slab vectors, R) as chunk_grads:
+// each thread keeps its 8 channels' coefficients in registers and streams
+// dy / x of its pixels (16-B vectors) -> dx
 __global__ void __launch_bounds__(256) nhwc_dx(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
-                                               const bf16_t* __restrict__ w, const bf16_t* __restrict__ b,
-                                               const float* __restrict__ mean, const float* __restrict__ rstd,
-                                               const float* __restrict__ m1, const float* __restrict__ m2,
-                                               bf16_t* __restrict__ dx, int P, int C, int G, int silu, int nvec) {
-  const int cg = C / G, cv8 = C / 8;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += gridDim.x * blockDim.x) {
-    const int pix = i / cv8;
-    const int c0 = (i - pix * cv8) * 8;
-    const int n = pix / P;
+                                               const float* __restrict__ coef, bf16_t* __restrict__ dx, int P,
+                                               int C, int silu) {
+  const int lv = threadIdx.x, r = threadIdx.y, R = blockDim.y;
+  const int cv = blockIdx.z * blockDim.x + lv;
+  if (cv * 8 >= C) return;
+  const int n = blockIdx.y, CH = chunk_of(P);
+  const int p0 = blockIdx.x * CH, p1 = min(P, p0 + CH);
+  float sc[8], sh[8], cb[8], cc[8];
+  const float* cf = coef + (long long)n * 4 * C + cv * 8;
+  load8f(cf, sc);
+  load8f(cf + C, sh);
+  load8f(cf + 2 * C, cb);
+  load8f(cf + 3 * C, cc);
+  const long long off = ((long long)n * P) * C + cv * 8;
+#pragma unroll 2
+  for (int p = p0 + r; p < p1; p += R) {
     float v[8], g[8];
-    load8(x + (long long)i * 8, v);
-    load8(dy + (long long)i * 8, g);
+    load8(x + off + (long long)p * C, v);
+    load8(dy + off + (long long)p * C, g);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int c = c0 + j, ng = n * G + c / cg;
-      const float gw = bf2f(w[c]);
-      const float xh = (v[j] - mean[ng]) * rstd[ng];
-      const float dz = silu ? g[j] * silu_d(xh * gw + (b ? bf2f(b[c]) : 0.f)) : g[j];
-      v[j] = rstd[ng] * (dz * gw - m1[ng] - xh * m2[ng]);
+      const float dz = silu ? g[j] * silu_d(fmaf(v[j], sc[j], sh[j])) : g[j];
+      v[j] = fmaf(sc[j], dz, fmaf(cb[j], v[j], cc[j]));
     }
-    store8(dx + (long long)i * 8, v);
+    store8(dx + off + (long long)p * C, v);
   }
 }
 
@@ -321,7 +370,8 @@ bool geometry(int C, int G, dim3& block, int& slabs) {
 
 KCA_API int kca_groupnorm_nhwc_ws(int N, int P, int C) {  // fp32 workspace floats needed
   const int nchunks = (P + chunk_of(P) - 1) / chunk_of(P);
-  return 2 * N * nchunks * C + 2 * N * C;
+  // fwd: partials + [N][2][C] scale/shift; bwd: + [N][4][C] dx coefs (+4: 16-B alignment slack)
+  return 2 * N * nchunks * C + 4 * N * C + 4;
 }
 
 // x, y: [N, P, C] bf16; mean/rstd: [N*G] fp32 out; ws: kca_groupnorm_nhwc_ws floats;
@@ -336,7 +386,7 @@ KCA_API int kca_groupnorm_nhwc_fwd_add(const void* x, const void* w, const void*
   if (!geometry(C, G, block, slabs) || N <= 0 || P <= 0) return 1;
   if ((long long)N * P * C / 8 >= (1LL << 31)) return 2;
   const int nchunks = (P + chunk_of(P) - 1) / chunk_of(P);
-  const size_t smem = (2 * block.y * block.x * 8 + block.y) * sizeof(float);
+  const size_t smem = 2 * block.y * block.x * 8 * sizeof(float);
   hipLaunchKernelGGL(nhwc_chunk_stats, dim3(nchunks, N, slabs), block, smem, stream, (const bf16_t*)x, P, C, ws);
   float* ss = ws + 2LL * N * nchunks * C;
   hipLaunchKernelGGL(nhwc_group_stats, dim3(N * G), dim3(256), 0, stream, ws, P, C, G, nchunks, eps, mean, rstd,
@@ -352,7 +402,7 @@ KCA_API int kca_groupnorm_nhwc_fwd(const void* x, const void* w, const void* b, 
   return kca_groupnorm_nhwc_fwd_add(x, w, b, nullptr, y, mean, rstd, ws, N, P, C, G, eps, silu, stream);
 }
 
-// ws: kca_groupnorm_nhwc_ws floats + 2*N*G floats
+// ws: kca_groupnorm_nhwc_ws floats + 2*N*G floats (partials, m1, m2, dx coefficients)
 KCA_API int kca_groupnorm_nhwc_bwd(const void* dy, const void* x, const void* w, const void* b, const float* mean,
                                    const float* rstd, void* dx, void* dw, void* db, float* ws, int N, int P, int C,
                                    int G, int silu, hipStream_t stream) {
@@ -364,16 +414,15 @@ KCA_API int kca_groupnorm_nhwc_bwd(const void* dy, const void* x, const void* w,
   float* part = ws;
   float* m1 = ws + 2LL * N * nchunks * C;
   float* m2 = m1 + N * G;
+  float* coef = m1 + ((2 * N * G + 3) & ~3);  // [N][4][C], 16-B aligned for the float4 loads
   const size_t smem = 2 * block.y * block.x * 8 * sizeof(float);
   hipLaunchKernelGGL(nhwc_chunk_grads, dim3(nchunks, N, slabs), block, smem, stream, (const bf16_t*)dy, (const bf16_t*)x,
                      (const bf16_t*)w, (const bf16_t*)b, mean, rstd, P, C, G, silu, part);
-  hipLaunchKernelGGL(nhwc_group_grads, dim3(N * G), dim3(256), 0, stream, part, (const bf16_t*)w, P, C, G, nchunks,
-                     m1, m2);
-  hipLaunchKernelGGL(nhwc_chan_grads, dim3((C + 63) / 64), dim3(256), 0, stream, part, N * nchunks, C,
+  hipLaunchKernelGGL(nhwc_group_grads, dim3(N * G), dim3(256), 0, stream, part, (const bf16_t*)w, (const bf16_t*)b,
+                     mean, rstd, P, C, G, nchunks, m1, m2, coef);
+  hipLaunchKernelGGL(nhwc_chan_grads, dim3((C + 15) / 16), dim3(256), 0, stream, part, N * nchunks, C,
                      (bf16_t*)dw, (bf16_t*)db);
-  const int nvec = (int)((long long)N * P * C / 8);
-  hipLaunchKernelGGL(nhwc_dx, dim3(kca_grid(nvec, 256, 8192)), dim3(256), 0, stream, (const bf16_t*)dy,
-                     (const bf16_t*)x, (const bf16_t*)w, (const bf16_t*)b, mean, rstd, m1, m2, (bf16_t*)dx,
-                     P, C, G, silu, nvec);
+  hipLaunchKernelGGL(nhwc_dx, dim3(nchunks, N, slabs), block, 0, stream, (const bf16_t*)dy, (const bf16_t*)x,
+                     coef, (bf16_t*)dx, P, C, silu);
   return 0;
 }

@@ -629,3 +629,19 @@ def test_groupnorm_nhwc_fused_add(silu):
     if silu:
         yr = F.silu(yr)
     assert _rel(y, yr) < 1e-2, _rel(y, yr)
+
+
+def test_groupnorm_nhwc_offset_input_stats():
+    """Shifted-sum statistics (chunk_stats) on data whose mean is several
+    standard deviations from zero and differs per chunk: variance must not
+    cancel. Reference: fp32 GroupNorm of the same bf16 input."""
+    torch.manual_seed(7)
+    N, C, H, W, G = 2, 640, 32, 32, 32
+    ramp = torch.linspace(-4.0, 6.0, H * W, device=DEV).view(1, 1, H, W)
+    x = (ramp + 8.0 + 0.3 * torch.randn(N, C, H, W, device=DEV)).bfloat16()
+    x = x.contiguous(memory_format=torch.channels_last)
+    w = torch.randn(C, device=DEV).bfloat16()
+    b = torch.randn(C, device=DEV).bfloat16()
+    y = ops.group_norm(x, G, w, b, 1e-6)
+    yr = F.group_norm(x.float(), G, w.float(), b.float(), 1e-6)
+    assert _rel(y, yr) < 1e-2, _rel(y, yr)
