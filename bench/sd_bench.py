@@ -140,10 +140,18 @@ def main():
     ap.add_argument("--infer-steps", type=int, default=50)
     ap.add_argument("--scheduler", default="LMSDiscreteScheduler")
     ap.add_argument("--ckpt", action="store_true")
+    ap.add_argument("--tunableop", choices=["auto", "use", "tune", "off"], default="auto",
+                    help="hipBLASLt solution choices from tuning/tunableop_sd.csv (utils/tunable.py)")
+    ap.add_argument("--tunableop-file", default=None)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     from kubernetes_cloud_amd.ops import _lib
+    from kubernetes_cloud_amd.utils import tunable
     _lib.require()
+    if args.tunableop == "off":
+        os.environ["KCA_TUNABLEOP"] = "off"  # also keeps models/unet.py:to_channels_last from enabling it
+    tmode = tunable.configure(args.tunableop_file or tunable.SD_FILE, args.tunableop)
+    print(f"[sd_bench] tunableop: {tmode}", file=sys.stderr, flush=True)
     if args.mode in ("train", "both"):
         print(json.dumps(bench_train(args, dev)), flush=True)
         torch.cuda.empty_cache()

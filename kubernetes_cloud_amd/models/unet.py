@@ -319,8 +319,10 @@ def to_channels_last(model: nn.Module, weights: bool = True) -> nn.Module:
     GroupNorm kernels, free token views for attention). ``weights`` also
     converts the conv weights; the training engine keeps that order in its
     flat buffer (train/engine.py)."""
-    from ..utils import miopen
+    from ..utils import miopen, tunable
     miopen.configure()
+    if next(model.parameters()).is_cuda:
+        tunable.ensure(tunable.SD_FILE)  # MI355X-tuned hipBLASLt choices for the SD GEMM shapes
     model.channels_last = True
     if weights:
         model.to(memory_format=torch.channels_last)

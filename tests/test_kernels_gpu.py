@@ -645,3 +645,16 @@ def test_groupnorm_nhwc_offset_input_stats():
     y = ops.group_norm(x, G, w, b, 1e-6)
     yr = F.group_norm(x.float(), G, w.float(), b.float(), 1e-6)
     assert _rel(y, yr) < 1e-2, _rel(y, yr)
+
+
+def test_vae_wide_head_attention_bf16_gemms():
+    """VAE mid-block attention (one 512-wide head): bf16 GEMMs with fp32 logits
+    (models/vae.py _wide_head_attention) vs the fp32 reference."""
+    from kubernetes_cloud_amd.models.vae import _wide_head_attention
+    torch.manual_seed(3)
+    q, k, v = (torch.randn(2, 1024, 512, device=DEV) for _ in range(3))
+    o = _wide_head_attention(q.bfloat16(), k.bfloat16(), v.bfloat16(), 512 ** -0.5)
+    qb, kb, vb = (t.bfloat16().float() for t in (q, k, v))
+    ref = torch.softmax(qb @ kb.transpose(1, 2) * 512 ** -0.5, -1) @ vb
+    assert o.dtype == torch.bfloat16
+    assert _rel(o, ref) < 2e-2, _rel(o, ref)
