@@ -32,8 +32,11 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--model", default="gpt-j-6b")
-    ap.add_argument("--micro-batch", type=int, default=8)
-    ap.add_argument("--gas", type=int, default=4)
+    # micro-batch 16 x GAS 2 (global 32): the largest micro-batch that fits 288 GB
+    # (peak 216 GiB), as the reference's auto batch size picks the largest that fits
+    # (finetuner.py:447-466); vs 8 x 4: 32.7k -> 33.5k tok/s (profiles/bench_gptj_r1_v13_mb16.log)
+    ap.add_argument("--micro-batch", type=int, default=16)
+    ap.add_argument("--gas", type=int, default=2)
     ap.add_argument("--seq", type=int, default=2048)
     ap.add_argument("--zero-stage", type=int, default=1)
     ap.add_argument("--ckpt", action="store_true", help="activation checkpointing")
