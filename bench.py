@@ -12,7 +12,12 @@ through the native kernels) + bucketed RCCL reduce-scatter (N>1) + fused
 AdamW + bf16 all-gather. Weak scaling: per-GPU work is fixed as N grows.
 
     python bench.py --gpus N --steps K --warmup W
-    (N>1 under: python -m torch.distributed.run --nproc-per-node N ... bench.py ...)
+    (N>1: either under `python -m torch.distributed.run --nproc-per-node N ...`,
+     or plain -- without WORLD_SIZE in the env the script re-launches itself
+     as N ranks, kubernetes_cloud_amd/launch.py)
+
+Secondary measurements in the same JSON line: SD-1.5 txt2img images/s (one
+replica per GPU) and, when N > 1, BLOOM-176B TP=N decode (BASELINE config 4).
 """
 from __future__ import annotations
 
@@ -48,7 +53,25 @@ def main():
     ap.add_argument("--tunableop-file", default=os.path.join(ROOT, "tuning", "tunableop_results.csv"))
     ap.add_argument("--sd", type=int, default=1, help="also measure the SD-1.5 txt2img half of the BASELINE metric "
                     "(batch 8, 512 px, 50 LMS steps, CFG 7; one rank-local replica per GPU) after the GPT-J steps")
+    ap.add_argument("--bloom-tp", choices=["auto", "on", "off"], default="auto",
+                    help="also measure BLOOM-176B TP=N decode (BASELINE config 4) after the GPT-J steps; "
+                         "'auto' = when N > 1")
+    ap.add_argument("--bloom-layers", type=int, default=0, help="0 = all 70 layers")
+    ap.add_argument("--bloom-timeout", type=float, default=420.0,
+                    help="seconds; if the BLOOM phase overruns, the headline line is printed without it")
     args = ap.parse_args()
+
+    # `python bench.py --gpus N` outside torchrun: re-run this script as N ranks
+    # (torchrun's env contract) before anything touches the GPU, and exit with
+    # their status. Under torchrun WORLD_SIZE is set and this is skipped.
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        from kubernetes_cloud_amd.launch import self_launch_argv, spawn
+        cmds, envs = self_launch_argv(os.path.abspath(__file__), sys.argv[1:], args.gpus)
+        sys.exit(spawn(cmds, envs))
+    if os.environ.get("KCA_BENCH_DRYRUN") == "1":  # CPU test of the launch contract (tests/test_launch_cpu.py)
+        print(f"[bench] dryrun rank {os.environ.get('RANK', '0')} "
+              + json.dumps({"world_size": int(os.environ.get("WORLD_SIZE", "1"))}), flush=True)
+        return
 
     import torch
     import torch.distributed as dist
@@ -61,7 +84,10 @@ def main():
     info = init_distributed()
     world = info.world_size
     if world != args.gpus and info.is_main:
-        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; reporting the real world size",
+              file=sys.stderr)
+    if torch.cuda.device_count() < world:
+        raise SystemExit(f"[bench] {world} ranks but only {torch.cuda.device_count()} visible GPUs")
     dev = torch.device("cuda", torch.cuda.current_device())
     _lib.require()
     torch.manual_seed(1234 + info.rank)
@@ -126,19 +152,18 @@ def main():
         dt = float(t.item())
     global_batch = B * args.gas * world
     peak_gib = torch.cuda.max_memory_allocated() / 2**30
-    sd = None
-    if args.sd:
-        eng.remove_hooks()  # drops the gradient-sink references to the engine
-        del eng, model, batches
-        torch.cuda.empty_cache()
-        sd = _sd_txt2img(dev, world, info.is_main)
     tokens = args.steps * global_batch * S
     tps = tokens / dt
     ms = dt / args.steps * 1e3
     flops_tok = cfg.flops_per_token(S)
     mfu = tps * flops_tok / (world * 2.5e15)
+    loss_v = float(loss.item())
+    eng.remove_hooks()  # drops the gradient-sink references to the engine
+    del eng, model, batches
+    torch.cuda.empty_cache()
+    rec = None
     if info.is_main:
-        print(f"[bench] loss={loss.item():.4f} step={ms:.1f}ms tokens/s={tps:.0f} "
+        print(f"[bench] loss={loss_v:.4f} step={ms:.1f}ms tokens/s={tps:.0f} "
               f"tokens/s/gpu={tps/world:.0f} MFU(2.5PF dense)={mfu*100:.1f}% "
               f"peak_mem={peak_gib:.1f}GiB", file=sys.stderr, flush=True)
         rec = {
@@ -163,12 +188,57 @@ def main():
                 "parallelism": f"dp{world}" + (f"-zero{args.zero_stage}" if world > 1 else ""),
                 "activation_checkpointing": bool(args.ckpt),
                 "mfu_2p5pf": round(mfu, 4),
+                "peak_mem_gib": round(peak_gib, 1),
             },
-            "secondary": sd,
+            "secondary": None,
         }
+    if args.sd:
+        sd = _sd_txt2img(dev, world, info.is_main)
+        if rec is not None:
+            rec["secondary"] = sd
+    if args.bloom_tp == "on" or (args.bloom_tp == "auto" and world > 1):
+        bloom = _bloom_tp(args, info, rec)
+        if rec is not None:
+            rec["bloom_tp"] = bloom
+    if rec is not None:
         print(json.dumps(rec), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
+
+
+def _bloom_tp(args, info, rec):
+    """BLOOM-176B TP=N decode (BASELINE config 4: prefill ms, decode ms/token,
+    tokens/s at batch 1/8/32; bench/bloom_tp_bench.py) on the same ranks. A
+    watchdog bounds the phase: on overrun rank 0 prints the headline record
+    (marked) and every rank exits, so a stuck TP phase can never cost the
+    GPT-J number."""
+    import importlib.util
+    import threading
+
+    def _overrun():
+        if rec is not None:
+            rec["bloom_tp"] = {"error": f"timeout after {args.bloom_timeout:.0f}s"}
+            print(json.dumps(rec), flush=True)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
+
+    timer = threading.Timer(args.bloom_timeout, _overrun)
+    timer.daemon = True
+    timer.start()
+    try:
+        spec = importlib.util.spec_from_file_location("kca_bloom_bench", os.path.join(ROOT, "bench", "bloom_tp_bench.py"))
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        out = mod.run_tp_decode("bloom-176b", layers=args.bloom_layers, batches=(1, 8, 32), prompt_len=128,
+                                new_tokens=32)
+        return out
+    except Exception as e:  # noqa: BLE001 - the headline line must still print
+        if info.is_main:
+            print(f"[bench] BLOOM TP measurement failed: {e!r}", file=sys.stderr, flush=True)
+        return {"error": repr(e)[:300]}
+    finally:
+        timer.cancel()
 
 
 def _sd_txt2img(dev, world, is_main):

@@ -1,25 +1,35 @@
-// One-shot all-reduce over xGMI peer memory for small (latency-bound) messages
-// (BLOOM TP=8 decode runs ~140 all-reduces of
-// B x 14336 bf16 per token; RCCL's ring latency dominates at that size).
+// Custom all-reduce over xGMI peer memory.
 //
-// Each rank owns, in device-uncached memory shared with its peers through
-// hipIpc handles:
-//   * two staging buffers (double-buffered by call parity), and
-//   * a signal block: per workgroup a monotonically increasing call counter
-//     and one arrival slot per peer.
-// One kernel launch per all-reduce; workgroup b:
-//   1. copies its slice of the input into its own staging[parity] buffer;
-//   2. system-scope fence, then stores the new call count into slot[b][rank]
-//      of EVERY peer's signal block (remote stores over xGMI);
-//   3. spins (bounded) until all peers' counts arrived in its own slots;
-//   4. reads its slice from all W peers' staging[parity] (uncached, straight
-//      over the links -- 7 links in parallel on an 8-GPU mesh), sums in fp32
-//      and writes the output.
-// Double buffering removes the exit barrier: a peer can only overwrite
-// staging[parity] two calls later, after it saw this rank arrive at the next
-// call, i.e. after this rank finished reading. Counters live in device memory
-// so the kernel is HIP-graph capturable (no host-side sequence numbers).
-// A bounded spin sets an error word instead of hanging the GPU.
+// BLOOM TP=8 decode runs ~140 all-reduces of B x 14336 bf16 per token and TP
+// prefill / NeoX TP training run MB-sized ones; RCCL's ring pays 2(W-1) link
+// latencies per call. On an 8-GPU xGMI mesh every GPU has a direct link to
+// every peer, so a kernel can read all 7 peers' buffers concurrently:
+//
+//   * one-shot  (small, latency-bound): every rank reads the WHOLE message
+//     from all W staging buffers and sums -> 1 sync round, (W-1)*n bytes over
+//     the links per rank;
+//   * two-shot  (medium/large, bandwidth-bound): reduce-scatter then
+//     all-gather through peer memory -> 2 sync rounds, 2(W-1)/W*n bytes per
+//     rank, all 7 links busy in both phases.
+//
+// Memory: per rank, two staging buffers (double-buffered by call parity) and a
+// signal block (per-block arrival flags written by peers) in device-uncached
+// memory shared through hipIpc handles, plus a local control block (call
+// sequence number, finished-block counter, sticky error word).
+//
+// Ordering/race argument (this replaces round 1's per-block counters, whose
+// parities drifted apart when the block count or slice map changed between
+// calls): the call number is ONE per-rank sequence word, read by every block
+// at kernel start and advanced by the last block to finish. Flags compare
+// `>= call`, so blocks that sat out intermediate calls are still correct.
+// Call k+2 reuses call k's parity; before ANY block of call k+1 on rank X
+// finished, it observed every peer Y arriving at call k+1, and Y's call-(k+1)
+// kernel can only start after Y's call-k kernel completed (same stream) --
+// so no peer is still reading X's call-k staging when X's call k+2 writes it,
+// whatever the slice->block mapping of the three calls.
+//
+// A bounded spin sets the sticky error word and poisons the output with NaN
+// (never a plausible wrong sum); the host wrapper raises on it.
 #include <hip/hip_runtime.h>
 
 #include <cstring>
@@ -29,12 +39,17 @@
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int AR_MAX_RANKS = 8;
-constexpr int AR_MAX_BLOCKS = 64;
+constexpr int AR_MAX_BLOCKS = 128;
 
-struct ARSignal {
-  uint32_t slot[AR_MAX_BLOCKS][AR_MAX_RANKS];  // written by peers
-  uint32_t count[AR_MAX_BLOCKS];               // this rank's call counter per block
-  uint32_t error;
+struct ARSignal {  // uncached, IPC-shared: written by peers
+  uint32_t flag[2][AR_MAX_BLOCKS][AR_MAX_RANKS];  // [phase][block][peer] = last call the peer reached
+};
+
+struct ARCtl {  // local (cached) control words, touched only by this rank's kernels
+  uint32_t seq;    // calls completed
+  uint32_t done;   // blocks finished in the running call
+  uint32_t error;  // sticky: 1 = spin timeout
+  uint32_t pad;
 };
 
 struct ARPeers {
@@ -49,60 +64,164 @@ __device__ __forceinline__ uint32_t ld_sys(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-template <int W>
-__global__ __launch_bounds__(512) void ar_one_shot_kernel(ARPeers peers, int rank, const bf16_t* __restrict__ in,
-                                                          bf16_t* __restrict__ out, long long n8,
-                                                          long long spin_limit) {
-  const int b = blockIdx.x, nb = gridDim.x, tid = threadIdx.x;
-  ARSignal* me = peers.sig[rank];
+__device__ __forceinline__ uint32_t ar_begin(ARCtl* ctl) {
   __shared__ uint32_t s_call;
-  if (tid == 0) s_call = me->count[b] + 1;
+  if (threadIdx.x == 0) s_call = __hip_atomic_load(&ctl->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) + 1;
   __syncthreads();
-  const uint32_t call = s_call;
-  const int par = call & 1;
-  // slice of 16-byte chunks owned by this block
-  const long long per = (n8 + nb - 1) / nb;
-  const long long lo = b * per, hi = min(n8, lo + per);
-  bf16_t* mine = peers.stage[par][rank];
-  for (long long i = lo + tid; i < hi; i += blockDim.x)
-    reinterpret_cast<uint4*>(mine)[i] = reinterpret_cast<const uint4*>(in)[i];
+  return s_call;
+}
+
+// Last block out advances the sequence word (all blocks have read it by then:
+// the nb-th finisher runs after every block started).
+__device__ __forceinline__ void ar_end(ARCtl* ctl, uint32_t call) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t old = __hip_atomic_fetch_add(&ctl->done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == gridDim.x - 1) {
+      __hip_atomic_store(&ctl->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&ctl->seq, call, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// Publish this block's arrival at (phase, call) to every peer, then wait until
+// every peer's same-index block arrived. Returns false on timeout.
+template <int W>
+__device__ __forceinline__ bool ar_sync(const ARPeers& peers, ARCtl* ctl, int rank, int phase, uint32_t call,
+                                        long long spin_limit) {
+  __shared__ int s_ok;
+  const int b = blockIdx.x, tid = threadIdx.x;
   __threadfence_system();
   __syncthreads();
-  if (tid < W) st_sys(&peers.sig[tid]->slot[b][rank], call);
+  if (tid == 0) s_ok = 1;
+  if (tid < W) st_sys(&peers.sig[tid]->flag[phase][b][rank], call);
+  __syncthreads();
   if (tid < W) {
+    const uint32_t* f = &peers.sig[rank]->flag[phase][b][tid];
     long long spins = 0;
-    while (ld_sys(&me->slot[b][tid]) < call) {
+    while (ld_sys(f) < call) {
       if (++spins > spin_limit) {
-        atomicOr(&me->error, 1u);
+        __hip_atomic_fetch_or(&ctl->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_ok = 0;
         break;
       }
       __builtin_amdgcn_s_sleep(1);
     }
   }
   __syncthreads();
-  for (long long i = lo + tid; i < hi; i += blockDim.x) {
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  return s_ok != 0;
+}
+
+__device__ __forceinline__ void debug_delay(int delay) {
+  for (int i = 0; i < delay; ++i) __builtin_amdgcn_s_sleep(127);
+}
+
+template <int W>
+__device__ __forceinline__ uint4 sum_peers(const ARPeers& peers, int par, long long i) {
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-    for (int r = 0; r < W; ++r) {
-      const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(peers.stage[par][r]) + i);
-      const uint32_t q[4] = {v[0], v[1], v[2], v[3]};
+  for (int r = 0; r < W; ++r) {
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(peers.stage[par][r]) + i);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        acc[2 * j] += __uint_as_float(q[j] << 16);
-        acc[2 * j + 1] += __uint_as_float(q[j] & 0xffff0000u);
-      }
+    for (int j = 0; j < 4; ++j) {
+      acc[2 * j] += __uint_as_float(v[j] << 16);
+      acc[2 * j + 1] += __uint_as_float(v[j] & 0xffff0000u);
     }
-    store8(out + i * 8, acc);
   }
-  if (tid == 0) me->count[b] = call;
+  uint4 o;
+  o.x = pack_bf16x2(acc[0], acc[1]);
+  o.y = pack_bf16x2(acc[2], acc[3]);
+  o.z = pack_bf16x2(acc[4], acc[5]);
+  o.w = pack_bf16x2(acc[6], acc[7]);
+  return o;
+}
+
+__device__ __forceinline__ uint4 nan_bf16x8() {
+  const uint32_t q = 0x7fc07fc0u;
+  return make_uint4(q, q, q, q);
+}
+
+// ---------------------------------------------------------------- one-shot
+template <int W>
+__global__ __launch_bounds__(512) void ar_one_shot_kernel(ARPeers peers, ARCtl* ctl, int rank,
+                                                          const bf16_t* __restrict__ in, bf16_t* __restrict__ out,
+                                                          long long n8, long long spin_limit, int delay) {
+  const int b = blockIdx.x, nb = gridDim.x, tid = threadIdx.x;
+  const uint32_t call = ar_begin(ctl);
+  const int par = call & 1;
+  const long long per = (n8 + nb - 1) / nb;
+  const long long lo = b * per, hi = min(n8, lo + per);
+  uint4* mine = reinterpret_cast<uint4*>(peers.stage[par][rank]);
+  for (long long i = lo + tid; i < hi; i += blockDim.x) mine[i] = reinterpret_cast<const uint4*>(in)[i];
+  const bool ok = ar_sync<W>(peers, ctl, rank, 0, call, spin_limit);
+  debug_delay(delay);
+  for (long long i = lo + tid; i < hi; i += blockDim.x)
+    reinterpret_cast<uint4*>(out)[i] = ok ? sum_peers<W>(peers, par, i) : nan_bf16x8();
+  ar_end(ctl, call);
+}
+
+// ---------------------------------------------------------------- two-shot
+// The message is cut into W partitions; block b owns sub-slice b of every
+// partition on every rank, so phase flags are per block index.
+//   phase A: copy own input into staging; sync
+//   reduce : rank r sums sub-slice b of partition r over all W stagings and
+//            writes the bf16 result in place into its OWN staging (no peer
+//            reads partition r of rank r's staging before phase B); sync
+//   gather : read sub-slice b of partition p from rank p's staging, all p.
+template <int W>
+__global__ __launch_bounds__(512) void ar_two_shot_kernel(ARPeers peers, ARCtl* ctl, int rank,
+                                                          const bf16_t* __restrict__ in, bf16_t* __restrict__ out,
+                                                          long long n8, long long spin_limit, int delay) {
+  const int b = blockIdx.x, nb = gridDim.x, tid = threadIdx.x;
+  const uint32_t call = ar_begin(ctl);
+  const int par = call & 1;
+  const long long part = (n8 + W - 1) / W;
+  const long long sub = (part + nb - 1) / nb;
+  uint4* mine = reinterpret_cast<uint4*>(peers.stage[par][rank]);
+  const uint4* src = reinterpret_cast<const uint4*>(in);
+#pragma unroll
+  for (int p = 0; p < W; ++p) {
+    const long long pend = min(n8, (p + 1) * part);
+    const long long lo = p * part + b * sub, hi = min(pend, lo + sub);
+    for (long long i = lo + tid; i < hi; i += blockDim.x) mine[i] = src[i];
+  }
+  bool ok = ar_sync<W>(peers, ctl, rank, 0, call, spin_limit);
+  debug_delay(delay);
+  {
+    const long long pend = min(n8, (long long)(rank + 1) * part);
+    const long long lo = rank * part + b * sub, hi = min(pend, lo + sub);
+    for (long long i = lo + tid; i < hi; i += blockDim.x) {
+      const uint4 v = sum_peers<W>(peers, par, i);
+      mine[i] = ok ? v : nan_bf16x8();
+    }
+  }
+  ok = ar_sync<W>(peers, ctl, rank, 1, call, spin_limit) && ok;
+  uint4* dst = reinterpret_cast<uint4*>(out);
+#pragma unroll
+  for (int p = 0; p < W; ++p) {
+    const long long pend = min(n8, (p + 1) * part);
+    const long long lo = p * part + b * sub, hi = min(pend, lo + sub);
+    const u32x4* s = reinterpret_cast<const u32x4*>(peers.stage[par][p]);
+    for (long long i = lo + tid; i < hi; i += blockDim.x) {
+      const u32x4 v = __builtin_nontemporal_load(s + i);
+      dst[i] = ok ? make_uint4(v[0], v[1], v[2], v[3]) : nan_bf16x8();
+    }
+  }
+  ar_end(ctl, call);
 }
 
 KCA_API int kca_ar_signal_bytes() { return (int)sizeof(ARSignal); }
+KCA_API int kca_ar_max_blocks() { return AR_MAX_BLOCKS; }
 
 // Uncached device allocation (coherent for peer access over xGMI).
 KCA_API int kca_ar_alloc(long long bytes, void** ptr) {
   if (hipExtMallocWithFlags(ptr, (size_t)bytes, hipDeviceMallocUncached) != hipSuccess) return 1;
   return hipMemset(*ptr, 0, (size_t)bytes) == hipSuccess ? 0 : 2;
+}
+
+KCA_API int kca_ar_ctl_alloc(void** ptr) {
+  if (hipMalloc(ptr, sizeof(ARCtl)) != hipSuccess) return 1;
+  return hipMemset(*ptr, 0, sizeof(ARCtl)) == hipSuccess ? 0 : 2;
 }
 
 KCA_API int kca_ar_free(void* ptr) { return hipFree(ptr) == hipSuccess ? 0 : 1; }
@@ -123,10 +242,14 @@ KCA_API int kca_ipc_open(const void* handle, void** ptr) {
 KCA_API int kca_ipc_close(void* ptr) { return hipIpcCloseMemHandle(ptr) == hipSuccess ? 0 : 1; }
 
 // stage0/stage1/sig: arrays of `world` device pointers (host memory).
-KCA_API int kca_ar_one_shot(void* const* stage0, void* const* stage1, void* const* sig, int rank, int world,
-                            const void* in, void* out, long long n, int blocks, long long spin_limit,
-                            hipStream_t stream) {
-  if (world < 1 || world > AR_MAX_RANKS || n % 8 || blocks < 1 || blocks > AR_MAX_BLOCKS) return 1;
+// algo 0 = one-shot, 1 = two-shot. `n` bf16 elements, multiple of 8, and
+// n*2 must fit the staging buffers (checked by the Python wrapper).
+KCA_API int kca_ar_run(void* const* stage0, void* const* stage1, void* const* sig, void* ctl, int rank, int world,
+                       int algo, const void* in, void* out, long long n, int blocks, long long spin_limit, int delay,
+                       hipStream_t stream) {
+  if (world < 1 || world > AR_MAX_RANKS || rank < 0 || rank >= world || n % 8 || n <= 0 || blocks < 1 ||
+      blocks > AR_MAX_BLOCKS || algo < 0 || algo > 1)
+    return 1;
   if (((uintptr_t)in | (uintptr_t)out) & 15) return 2;
   ARPeers p{};
   for (int r = 0; r < world; ++r) {
@@ -135,11 +258,16 @@ KCA_API int kca_ar_one_shot(void* const* stage0, void* const* stage1, void* cons
     p.sig[r] = (ARSignal*)sig[r];
   }
   const long long n8 = n / 8;
+  ARCtl* c = (ARCtl*)ctl;
   switch (world) {
-#define KCA_AR_CASE(WW)                                                                                   \
-  case WW:                                                                                                \
-    hipLaunchKernelGGL(ar_one_shot_kernel<WW>, dim3(blocks), dim3(512), 0, stream, p, rank,                \
-                       (const bf16_t*)in, (bf16_t*)out, n8, spin_limit);                                  \
+#define KCA_AR_CASE(WW)                                                                                        \
+  case WW:                                                                                                     \
+    if (algo == 0)                                                                                             \
+      hipLaunchKernelGGL(ar_one_shot_kernel<WW>, dim3(blocks), dim3(512), 0, stream, p, c, rank,               \
+                         (const bf16_t*)in, (bf16_t*)out, n8, spin_limit, delay);                              \
+    else                                                                                                       \
+      hipLaunchKernelGGL(ar_two_shot_kernel<WW>, dim3(blocks), dim3(512), 0, stream, p, c, rank,               \
+                         (const bf16_t*)in, (bf16_t*)out, n8, spin_limit, delay);                              \
     break;
     KCA_AR_CASE(1) KCA_AR_CASE(2) KCA_AR_CASE(3) KCA_AR_CASE(4) KCA_AR_CASE(5) KCA_AR_CASE(6)
     KCA_AR_CASE(7) KCA_AR_CASE(8)
@@ -147,12 +275,12 @@ KCA_API int kca_ar_one_shot(void* const* stage0, void* const* stage1, void* cons
     default:
       return 3;
   }
-  return 0;
+  return hipGetLastError() == hipSuccess ? 0 : 4;
 }
 
-KCA_API int kca_ar_error(const void* sig, int* err) {
+KCA_API int kca_ar_error(const void* ctl, int* err) {
   uint32_t e = 0;
-  if (hipMemcpy(&e, (const char*)sig + offsetof(ARSignal, error), 4, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+  if (hipMemcpy(&e, (const char*)ctl + offsetof(ARCtl, error), 4, hipMemcpyDeviceToHost) != hipSuccess) return 1;
   *err = (int)e;
   return 0;
 }

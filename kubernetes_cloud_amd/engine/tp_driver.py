@@ -29,7 +29,9 @@ class CollectiveRunner:
 
     def prefill(self, ids, slots):
         self._send(("prefill", ids.tolist(), list(slots)))
-        return self.runner.prefill(ids, slots)
+        out = self.runner.prefill(ids, slots)
+        _check_ar()
+        return out
 
     def sample_first(self, logits, rows):
         self._send(("sample_first", rows))
@@ -43,6 +45,13 @@ class CollectiveRunner:
         self._send(("stop",))
 
 
+def _check_ar():
+    """A timed-out xGMI all-reduce NaN-poisons its output and flags; surface it
+    as an exception once per prefill (one device sync per request batch)."""
+    from ..parallel.custom_ar import check_all
+    check_all()
+
+
 def follower_loop(runner, ctrl_group=None):
     """Ranks > 0: mirror rank 0's runner calls until it sends ``stop``."""
     last_logits = None
@@ -54,6 +63,7 @@ def follower_loop(runner, ctrl_group=None):
             return
         if op == "prefill":
             last_logits = runner.prefill(torch.tensor(obj[0][1], dtype=torch.long), obj[0][2])
+            _check_ar()
         elif op == "sample_first":
             runner.sample_first(last_logits, obj[0][1])
         elif op == "decode":

@@ -39,6 +39,53 @@ def _count_gpus() -> int:
         return 0
 
 
+def rank_env(i: int, n: int, master_addr: str, port: int, base=None) -> dict:
+    """torchrun's env contract for rank ``i`` of ``n`` on one node."""
+    return dict(os.environ if base is None else base, RANK=str(i), LOCAL_RANK=str(i), WORLD_SIZE=str(n),
+                LOCAL_WORLD_SIZE=str(n), MASTER_ADDR=master_addr, MASTER_PORT=str(port),
+                HSA_ENABLE_IPC_MODE_LEGACY="0")
+
+
+def spawn(cmds, envs) -> int:
+    """Run one child per rank (own process group each) and wait. If a rank
+    fails, the others are terminated; returns the first non-zero exit code."""
+    procs = [subprocess.Popen(c, env=e, start_new_session=True) for c, e in zip(cmds, envs)]
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                r = p.poll()
+                if r is None:
+                    continue
+                procs.remove(p)
+                if r != 0 and rc == 0:
+                    rc = r
+                    for q in procs:
+                        try:
+                            os.killpg(q.pid, signal.SIGTERM)
+                        except ProcessLookupError:
+                            pass
+            time.sleep(0.2)
+    except KeyboardInterrupt:
+        for q in procs:
+            try:
+                os.killpg(q.pid, signal.SIGTERM)
+            except ProcessLookupError:
+                pass
+        rc = 130
+    return rc
+
+
+def self_launch_argv(script: str, argv, n: int, master_addr: str = "127.0.0.1", port: int = 0):
+    """(cmds, envs) to re-run ``script argv`` as ``n`` ranks -- used by entry
+    points (bench.py) invoked with ``--gpus N`` outside torchrun. Must be
+    called before anything initialises the GPU in the parent."""
+    port = port or _free_port()
+    cmds = [[sys.executable, "-u", script] + list(argv) for _ in range(n)]
+    envs = [rank_env(i, n, master_addr, port) for i in range(n)]
+    return cmds, envs
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(description="kubernetes_cloud_amd single-node launcher")
     ap.add_argument("--num_gpus", "--num-gpus", "--num_processes", "--num-processes", "--nproc_per_node",
@@ -69,37 +116,9 @@ def main(argv=None):
     else:
         base = [sys.executable, "-u", rest[0]]
         child_args = rest[1:]
-    a.args = child_args
-    procs = []
-    for i in range(n):
-        env = dict(os.environ, RANK=str(i), LOCAL_RANK=str(i), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR=a.master_addr, MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
-        cmd = base + list(a.args) + ([] if a.no_local_rank else [f"--local_rank={i}"])
-        procs.append(subprocess.Popen(cmd, env=env, start_new_session=True))
-    rc = 0
-    try:
-        while procs:
-            for p in list(procs):
-                r = p.poll()
-                if r is None:
-                    continue
-                procs.remove(p)
-                if r != 0 and rc == 0:
-                    rc = r
-                    for q in procs:
-                        try:
-                            os.killpg(q.pid, signal.SIGTERM)
-                        except ProcessLookupError:
-                            pass
-            time.sleep(0.2)
-    except KeyboardInterrupt:
-        for q in procs:
-            try:
-                os.killpg(q.pid, signal.SIGTERM)
-            except ProcessLookupError:
-                pass
-        rc = 130
-    return rc
+    cmds = [base + list(child_args) + ([] if a.no_local_rank else [f"--local_rank={i}"]) for i in range(n)]
+    envs = [rank_env(i, n, a.master_addr, port) for i in range(n)]
+    return spawn(cmds, envs)
 
 
 if __name__ == "__main__":

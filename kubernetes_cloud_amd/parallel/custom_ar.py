@@ -1,15 +1,22 @@
-"""Custom one-shot all-reduce over xGMI peer memory (csrc/comm/xgmi_allreduce.hip).
+"""Custom all-reduce over xGMI peer memory (csrc/comm/xgmi_allreduce.hip).
 
-For the latency-bound all-reduces of tensor-parallel decode (BLOOM TP=8: two
-per layer, B x 14336 bf16 each) a single kernel that reads the 7 peers'
-buffers directly over the point-to-point links beats RCCL's ring; larger
-messages keep going to RCCL (SURVEY §5.8 algorithm-by-size table).
+On an 8-GPU xGMI mesh every GPU has a direct link to every peer, so one kernel
+that reads the peers' buffers concurrently beats RCCL's ring for the
+tensor-parallel all-reduces (BLOOM TP=8 decode: two per layer of B x 14336
+bf16; TP prefill and NeoX TP training: MB-sized, C12):
+
+* ``one-shot`` up to ``one_shot_max`` bytes: one sync round, each rank reads
+  the whole message from every peer (latency-bound sizes);
+* ``two-shot`` up to ``max_bytes``: reduce-scatter + all-gather through peer
+  memory, 2(W-1)/W of the message per rank over the links;
+* larger messages keep going to RCCL (SURVEY §5.8 algorithm-by-size table).
 
 Setup exchanges hipIpc handles of each rank's uncached staging/signal buffers
 through ``torch.distributed`` (any backend) and maps the peers' buffers.
-``all_reduce_(t)`` reduces a bf16 tensor in place and is graph-capturable.
-``register(group)`` makes ``tensor_parallel.reduce_from_tp`` use it for
-messages up to ``max_bytes``.
+``all_reduce_(t)`` reduces a bf16 tensor in place and is graph-capturable (the
+call sequence number lives on the device). A peer that never arrives makes
+the kernel time out: it poisons the output with NaN and sets a sticky error
+word; ``check()`` raises on it (the TP engine calls it once per request).
 """
 from __future__ import annotations
 
@@ -25,6 +32,8 @@ _REGISTRY: dict = {}
 
 P = ctypes.c_void_p
 
+ONE_SHOT, TWO_SHOT = 0, 1
+
 
 def _fn(name, argtypes):
     lib = _lib.require()
@@ -34,30 +43,62 @@ def _fn(name, argtypes):
     return f
 
 
+def pick(nbytes: int, world: int, one_shot_max: int) -> int:
+    """Algorithm for a message of ``nbytes``: one-shot reads (W-1)*n bytes per
+    rank in one round trip, two-shot 2(W-1)/W*n in two -- one-shot wins while
+    the link latency dominates."""
+    if world <= 2:
+        return ONE_SHOT if nbytes <= 2 * one_shot_max else TWO_SHOT
+    return ONE_SHOT if nbytes <= one_shot_max else TWO_SHOT
+
+
+def blocks_for(n: int, world: int, algo: int, max_blocks: int = 128) -> int:
+    """Workgroups: ~one 512-lane pass of 16-byte chunks per block per
+    partition (two-shot) or of the whole message (one-shot)."""
+    n8 = -(-n // 8)
+    work = n8 if algo == ONE_SHOT else -(-n8 // world)
+    return max(1, min(max_blocks, -(-work // 512)))
+
+
+class AllReduceError(RuntimeError):
+    pass
+
+
 class XGMIAllReduce:
-    def __init__(self, group=None, max_bytes: int = 4 << 20, spin_limit: int = 1 << 26):
+    def __init__(self, group=None, max_bytes: int = 64 << 20, one_shot_max: int = 256 << 10,
+                 spin_limit: int = 1 << 26):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         if self.world > 8:
-            raise ValueError("one-shot all-reduce supports up to 8 ranks (one node)")
+            raise ValueError("xGMI all-reduce supports up to 8 ranks (one node)")
         self.max_bytes = max_bytes
+        self.one_shot_max = one_shot_max
         self.spin_limit = spin_limit
+        self.debug_delay = 0  # tests: spin before the read phase to force rank skew
         alloc = _fn("kca_ar_alloc", [ctypes.c_longlong, ctypes.POINTER(P)])
+        ctl_alloc = _fn("kca_ar_ctl_alloc", [ctypes.POINTER(P)])
         handle = _fn("kca_ipc_handle", [P, P])
         self._open = _fn("kca_ipc_open", [P, ctypes.POINTER(P)])
         self._close = _fn("kca_ipc_close", [P])
         self._free = _fn("kca_ar_free", [P])
-        self._run = _fn("kca_ar_one_shot", [ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(P), ctypes.c_int,
-                                            ctypes.c_int, P, P, ctypes.c_longlong, ctypes.c_int, ctypes.c_longlong,
-                                            P])
-        sig_bytes = _lib.require().kca_ar_signal_bytes()
+        self._run = _fn("kca_ar_run", [ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(P), P, ctypes.c_int,
+                                       ctypes.c_int, ctypes.c_int, P, P, ctypes.c_longlong, ctypes.c_int,
+                                       ctypes.c_longlong, ctypes.c_int, P])
+        self._err = _fn("kca_ar_error", [P, ctypes.POINTER(ctypes.c_int)])
+        lib = _lib.require()
+        self.max_blocks = int(lib.kca_ar_max_blocks())
+        sig_bytes = lib.kca_ar_signal_bytes()
         own = []
         for nbytes in (max_bytes, max_bytes, sig_bytes):
             p = P()
             if alloc(nbytes, ctypes.byref(p)) != 0:
                 raise RuntimeError("kca_ar_alloc failed")
             own.append(p.value)
+        c = P()
+        if ctl_alloc(ctypes.byref(c)) != 0:
+            raise RuntimeError("kca_ar_ctl_alloc failed")
+        self._ctl = c.value
         self._own = own
         hs = []
         for p in own:
@@ -83,37 +124,51 @@ class XGMIAllReduce:
         self._stage0 = arr(*ptrs[0])
         self._stage1 = arr(*ptrs[1])
         self._sig = arr(*ptrs[2])
-        self.sig_own = own[2]
         dist.barrier(group=group)
 
     def eligible(self, t: torch.Tensor) -> bool:
         return (t.is_cuda and t.dtype == torch.bfloat16 and t.is_contiguous() and t.numel() % 8 == 0
-                and t.numel() * 2 <= self.max_bytes and t.data_ptr() % 16 == 0)
+                and 0 < t.numel() * 2 <= self.max_bytes and t.data_ptr() % 16 == 0)
 
-    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+    def all_reduce_(self, t: torch.Tensor, algo: int | None = None) -> torch.Tensor:
         n = t.numel()
-        blocks = max(1, min(64, -(-n // (8 * 256))))
-        rc = self._run(self._stage0, self._stage1, self._sig, self.rank, self.world, t.data_ptr(), t.data_ptr(),
-                       n, blocks, self.spin_limit, _lib.stream())
+        if not self.eligible(t):
+            raise ValueError("tensor not eligible for the xGMI all-reduce (bf16, contiguous, 16B-aligned, "
+                             f"numel % 8 == 0, <= {self.max_bytes} bytes)")
+        if algo is None:
+            algo = pick(2 * n, self.world, self.one_shot_max)
+        blocks = blocks_for(n, self.world, algo, self.max_blocks)
+        rc = self._run(self._stage0, self._stage1, self._sig, P(self._ctl), self.rank, self.world, algo,
+                       t.data_ptr(), t.data_ptr(), n, blocks, self.spin_limit, int(self.debug_delay),
+                       _lib.stream())
         if rc != 0:
-            raise RuntimeError(f"kca_ar_one_shot status {rc}")
+            raise RuntimeError(f"kca_ar_run status {rc}")
         return t
 
     def error(self) -> int:
-        f = _fn("kca_ar_error", [P, ctypes.POINTER(ctypes.c_int)])
         e = ctypes.c_int(0)
-        f(P(self.sig_own), ctypes.byref(e))
+        self._err(P(self._ctl), ctypes.byref(e))
         return e.value
+
+    def check(self):
+        """Raise if any call since setup timed out waiting for a peer (its
+        output was NaN-poisoned). Synchronises the device."""
+        e = self.error()
+        if e:
+            raise AllReduceError(f"xGMI all-reduce: peer did not arrive within the spin limit (error={e}); "
+                                 "outputs of the affected calls are NaN")
 
     def close(self):
         for p in self._opened:
             self._close(P(p))
         for p in self._own:
             self._free(P(p))
-        self._opened, self._own = [], []
+        if self._ctl:
+            self._free(P(self._ctl))
+        self._opened, self._own, self._ctl = [], [], 0
 
 
-def register(group=None, max_bytes: int = 4 << 20) -> XGMIAllReduce | None:
+def register(group=None, max_bytes: int = 64 << 20) -> XGMIAllReduce | None:
     """Enable the custom all-reduce for ``group`` (no-op off GPU or if disabled
     with KCA_CUSTOM_AR=0)."""
     if not torch.cuda.is_available() or os.environ.get("KCA_CUSTOM_AR", "1") == "0":
@@ -127,4 +182,10 @@ def lookup(group):
     return _REGISTRY.get(id(group))
 
 
-__all__ = ["XGMIAllReduce", "register", "lookup"]
+def check_all():
+    """Raise if any registered all-reduce timed out (call per request)."""
+    for ar in _REGISTRY.values():
+        ar.check()
+
+
+__all__ = ["XGMIAllReduce", "AllReduceError", "register", "lookup", "check_all", "pick", "blocks_for"]

@@ -300,7 +300,8 @@ def load_tp_model(path: str, rank: int, world: int, group=None, device=None, dty
     with torch.device("meta"):
         m = CausalLM(cfg)
     tp_convert_(m, rank, world, group)
-    m = m.to_empty(device=device or "cpu").to(dtype)
+    # cast on meta first: materialising fp32 and then casting would peak at 3x the shard
+    m = m.to(dtype).to_empty(device=device or "cpu")
     if cfg.alibi:
         Hl = cfg.n_heads // world
         for blk in m.h:
