@@ -55,10 +55,13 @@ def collate(batch):
     """(input_ids, attention_mask) pairs -> the reference collector's dict
     (finetuner.py:1030-1035); labels == input_ids, masked to -100 where the
     attention mask is False (ModifiedTrainer.compute_loss, :476-477)."""
+    from ..models.causal_lm import mask_to_kv
     ids = torch.stack([b[0] for b in batch])
     mask = torch.stack([b[1] for b in batch])
     labels = ids.masked_fill(~mask, -100)
-    return {"input_ids": ids, "attention_mask": mask, "labels": labels}
+    # the attention kernels' key lengths / per-key mask, classified here on the
+    # host so the model forward needs no device->host sync
+    return {"input_ids": ids, "attention_mask": mask, "labels": labels, "kv_len": mask_to_kv(mask)}
 
 
 def write_tokens(path: str, tokens, context_length: int | None = None, pad_id: int | None = None):

@@ -73,6 +73,7 @@ def _rng_state():
 
 def save_checkpoint(ckpt_dir: str, model, engine, trainer_state: dict, args_dict: dict | None = None,
                     tokenizer=None, rank: int = 0, world: int = 1, barrier=None):
+    """Synchronous save (ZeRO-3 callers wrap it in ``engine.gathered()``)."""
     from safetensors.torch import save_file
 
     from .hf import save_pretrained
@@ -160,7 +161,9 @@ class AsyncCheckpointWriter:
         self.rank = rank
         self.wait(barrier)
         snap = self._snap
-        params = {k: snap.take("p." + k, v) for k, v in model.state_dict().items()}
+        # only rank 0 writes the model files: other ranks snapshot just their optimizer shard + RNG
+        # (8 ranks x a bf16 replica in pinned host memory would be ~96 GB for GPT-J)
+        params = {k: snap.take("p." + k, v) for k, v in model.state_dict().items()} if rank == 0 else None
         opt = None
         if engine is not None:
             st = engine.optimizer_state()
@@ -217,12 +220,14 @@ def load_checkpoint(ckpt_dir: str, model, engine, rank: int = 0) -> dict:
     from ..models.hf_convert import hf_to_native
     from .hf import read_hf_state_dict
 
-    sd = hf_to_native(read_hf_state_dict(ckpt_dir), model.cfg)
-    with torch.no_grad():
-        own = model.state_dict()
-        for k, v in sd.items():
-            if k in own:
-                own[k].copy_(v.to(own[k].dtype))
+    if engine is None or not getattr(engine, "part_params", False):
+        # (ZeRO-3: the params are this rank's bf16 shard, re-derived from the fp32 master below)
+        sd = hf_to_native(read_hf_state_dict(ckpt_dir), model.cfg)
+        with torch.no_grad():
+            own = model.state_dict()
+            for k, v in sd.items():
+                if k in own:
+                    own[k].copy_(v.to(own[k].dtype))
     if engine is not None:
         with open(os.path.join(ckpt_dir, "optimizer", "meta.json")) as f:
             meta = json.load(f)

@@ -43,6 +43,32 @@ def alibi_slopes(n_heads: int) -> torch.Tensor:
     return torch.tensor(s, dtype=torch.float32)
 
 
+def mask_to_kv(mask: torch.Tensor):
+    """HF attention_mask [B, S] (1 = real token) -> what the attention kernels take:
+
+    * ``None``            every token attends (no mask work at all);
+    * int32 [B] lengths   right padding (each row a prefix of ones);
+    * bool [B, S]         a mask with holes, e.g. the interior EOS separators of
+                          the last context of a pad == eos dataset
+                          (finetuner.py:674-691) -- exact HF semantics through
+                          the reference attention path.
+
+    A host mask is classified exactly. A device mask is never read back (no
+    host sync): it is taken as right padding, length = last real token + 1."""
+    if mask.device.type != "cpu":
+        S = mask.shape[-1]
+        pos = torch.arange(1, S + 1, device=mask.device, dtype=torch.int32)
+        return (mask.to(torch.int32) * pos).amax(-1).to(torch.int32)
+    m = mask.bool()
+    if bool(m.all()):
+        return None
+    pos = torch.arange(1, m.shape[-1] + 1, dtype=torch.int64)
+    last = (m.long() * pos).amax(-1)
+    if bool((m.long().sum(-1) == last).all()):
+        return last.to(torch.int32)
+    return m
+
+
 class LayerNorm(nn.Module):
     def __init__(self, d: int, eps: float):
         super().__init__()
@@ -124,7 +150,7 @@ class Block(nn.Module):
             x, h = self.ln_1(h, residual=pending)
         else:
             x = self.ln_1(h)
-        if self.fused is not None and torch.is_grad_enabled() and self.fused.applies(x):
+        if self.fused is not None and torch.is_grad_enabled() and self.fused.applies(x, kv_len):
             a, m = self.fused(x, kv_len)
             return h, a, m
         if self.cfg.parallel_residual:
@@ -239,7 +265,7 @@ class CausalLM(nn.Module):
 
     # --------------------------------------------------------------- forward
     def hidden_states(self, input_ids: torch.Tensor, attention_mask: torch.Tensor | None = None,
-                      position_ids: torch.Tensor | None = None):
+                      position_ids: torch.Tensor | None = None, kv_len: torch.Tensor | None = None):
         B, S = input_ids.shape
         h = self.wte(input_ids)
         if self.wpe is not None:
@@ -247,9 +273,10 @@ class CausalLM(nn.Module):
             h = h + self.wpe(pos)
         if self.emb_ln is not None:
             h = self.emb_ln(h)
-        kv_len = None
-        if attention_mask is not None and not bool(attention_mask.all()):
-            kv_len = attention_mask.sum(-1).to(torch.int32)
+        if kv_len is None and attention_mask is not None:
+            kv_len = mask_to_kv(attention_mask)
+        if kv_len is not None:
+            kv_len = kv_len.to(h.device, non_blocking=True)
         pending = ()
         for blk in self.h:
             if self.gradient_checkpointing and self.training and torch.is_grad_enabled():
@@ -262,12 +289,18 @@ class CausalLM(nn.Module):
 
     def logits_from_hidden(self, y: torch.Tensor) -> torch.Tensor:
         if self.lm_head is None:
+            if getattr(self, "_param_linear", False):  # ZeRO-3 (train/engine.py)
+                from ..ops.linear import param_linear
+                return param_linear(y, self.wte.weight)
             return F.linear(y, self.wte.weight)
         return self.lm_head(y)
 
     def forward(self, input_ids: torch.Tensor, attention_mask: torch.Tensor | None = None,
-                labels: torch.Tensor | None = None, position_ids: torch.Tensor | None = None):
-        y = self.hidden_states(input_ids, attention_mask, position_ids)
+                labels: torch.Tensor | None = None, position_ids: torch.Tensor | None = None,
+                kv_len: torch.Tensor | None = None):
+        """``kv_len``: precomputed ``mask_to_kv(attention_mask)`` (the data
+        collator does it on the host, so the forward never syncs)."""
+        y = self.hidden_states(input_ids, attention_mask, position_ids, kv_len)
         logits = self.logits_from_hidden(y)
         if labels is None:
             return logits

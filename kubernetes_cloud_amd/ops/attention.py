@@ -7,7 +7,9 @@ attention kernels read Q/K/V straight out of the [B, S, 3, H, D] buffer; the
 backward writes dQ/dK/dV into one fused dQKV buffer (so one dgrad GEMM and one
 wgrad GEMM serve all three projections) and un-rotates dQ/dK in place.
 
-CPU tensors use the fp32 reference (``attention_reference``).
+CPU tensors use the fp32 reference (``attention_reference``), and so do the
+rare per-key masks with holes (the last context of a pad == eos dataset,
+data/tokenized.py): the kernels take right-padding key lengths only.
 """
 from __future__ import annotations
 
@@ -21,7 +23,9 @@ from .rope import apply_rotary_
 
 def attention_reference(q, k, v, causal: bool, scale: float | None = None,
                         kv_len: torch.Tensor | None = None, alibi: torch.Tensor | None = None):
-    """fp32 reference. q [B,Sq,H,D], k/v [B,Sk,Hkv,D] -> o [B,Sq,H,D] (q.dtype), lse [B,H,Sq]."""
+    """fp32 reference. q [B,Sq,H,D], k/v [B,Sk,Hkv,D] -> o [B,Sq,H,D] (q.dtype), lse [B,H,Sq].
+    ``kv_len``: int [B] key lengths (right padding), or a bool [B, Sk] per-key
+    mask (True = attend) for masks with holes."""
     B, Sq, H, D = q.shape
     Sk, Hkv = k.shape[1], k.shape[2]
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
@@ -41,7 +45,9 @@ def attention_reference(q, k, v, causal: bool, scale: float | None = None,
     mask = torch.zeros(B, 1, Sq, Sk, dtype=torch.bool, device=q.device)
     if causal:
         mask = mask | (ki > qi + off)
-    if kv_len is not None:
+    if kv_len is not None and kv_len.dtype == torch.bool:  # per-key mask [B, Sk] (True = attend)
+        mask = mask | ~kv_len.to(q.device).view(B, 1, 1, Sk)
+    elif kv_len is not None:
         mask = mask | (ki[None, None] >= kv_len.view(B, 1, 1, 1).to(q.device))
     s = s.masked_fill(mask, float("-inf"))
     lse = torch.logsumexp(s, dim=-1)
@@ -127,11 +133,12 @@ def flash_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: b
                     alibi: torch.Tensor | None = None) -> torch.Tensor:
     """softmax(scale * Q K^T + alibi + mask) V over [B, S, H, D] views."""
     scale = scale if scale is not None else 1.0 / math.sqrt(q.shape[-1])
-    if kv_len is not None:
+    holes = kv_len is not None and kv_len.dtype == torch.bool
+    if kv_len is not None and not holes:
         kv_len = kv_len.to(device=q.device, dtype=torch.int32).contiguous()
     if alibi is not None:
         alibi = alibi.to(device=q.device, dtype=torch.float32).contiguous()
-    if _lib.use_native(q, k, v):
+    if _lib.use_native(q, k, v) and not holes:
         return _FlashAttnFn.apply(q, k, v, causal, scale, kv_len, alibi)
     o, _ = attention_reference(q, k, v, causal, scale, kv_len, alibi)
     return o
@@ -176,9 +183,10 @@ def qkv_rope_attention(qkv: torch.Tensor, n_heads: int, head_dim: int, rot: int,
     """Fused (RoPE + attention) over a [B, S, 3*H*D] QKV buffer -> [B, S, H*D]."""
     B, S, _ = qkv.shape
     scale = scale if scale is not None else 1.0 / math.sqrt(head_dim)
-    if kv_len is not None:
+    holes = kv_len is not None and kv_len.dtype == torch.bool
+    if kv_len is not None and not holes:
         kv_len = kv_len.to(device=qkv.device, dtype=torch.int32).contiguous()
-    if _lib.use_native(qkv):
+    if _lib.use_native(qkv) and not holes:
         return _QKVRopeAttnFn.apply(qkv.contiguous(), n_heads, head_dim, rot, interleaved, base,
                                     causal, scale, kv_len)
     v5 = qkv.view(B, S, 3, n_heads, head_dim)

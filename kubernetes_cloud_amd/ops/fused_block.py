@@ -57,9 +57,9 @@ class FusedParallelBlock:
     def refresh(self):  # the TLinears own the transposed copies
         pass
 
-    def applies(self, x: torch.Tensor) -> bool:
+    def applies(self, x: torch.Tensor, kv_len=None) -> bool:
         a, m = self.blk.attn, self.blk.mlp
-        return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 3 and x.is_contiguous()
+        return ((kv_len is None or kv_len.dtype != torch.bool) and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 3 and x.is_contiguous()
                 and (x.shape[0] * x.shape[1]) % 64 == 0
                 and all(t.weight_t is not None for t in (a.qkv, a.out, m.fc_in, m.fc_out)))
 

@@ -62,6 +62,41 @@ class _LinearTN(torch.autograd.Function):
         return dx, dw, db, None
 
 
+class _ParamLinear(torch.autograd.Function):
+    """y = x W^T + b that saves the Parameter W itself for backward. F.linear
+    saves ``W.t()`` -- a view that pins W's storage at forward time; ZeRO-3
+    (train/engine.py) swaps a released parameter's storage out after forward
+    and back in (re-gathered) before backward, which only works when the
+    autograd graph refers to the Parameter."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return F.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        K, N = x.shape[-1], dy.shape[-1]
+        x2 = x.reshape(-1, K)
+        dy2 = dy.reshape(-1, N)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = (dy2 @ weight).view(x.shape)
+        if ctx.needs_input_grad[1]:
+            dw = dy2.t() @ x2
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = dy2.sum(0)
+        return dx, dw, db
+
+
+def param_linear(x, weight, bias=None):
+    if torch.is_grad_enabled() and (x.requires_grad or weight.requires_grad):
+        return _ParamLinear.apply(x, weight, bias)
+    return F.linear(x, weight, bias)
+
+
 class TLinear(nn.Linear):
     """nn.Linear (same parameters / state dict) with the TN backward above when
     ``enable_tn(True)`` was called and the input is a bf16 GPU tensor."""
@@ -94,4 +129,4 @@ class TLinear(nn.Linear):
         return F.linear(x, self.weight, self.bias)
 
 
-__all__ = ["TLinear", "transpose"]
+__all__ = ["TLinear", "transpose", "param_linear"]

@@ -205,11 +205,13 @@ def tie_embedding_grads(engine, stage: PipelineStage, group):
     p = stage.wte.weight if stage.first else getattr(stage, "head_weight", None)
     if p is None:
         return
-    slot = next(s for s in engine.slots if s.param is p)
+    slot = engine.slot_of(p)
 
     def fn(eng):
+        # on the full local grads, before the DP reduction (sums commute); the
+        # slot's bucket is held back from the overlapped launch until this ran
         dist.all_reduce(eng.grad[slot.offset:slot.offset + slot.numel], group=group)
-    engine.add_pre_step(fn)
+    engine.add_pre_reduce(fn, params=(p,))
 
 
 __all__ = ["PipelineStage", "build_stage", "split_layers", "P2P", "one_f_one_b", "tie_embedding_grads"]

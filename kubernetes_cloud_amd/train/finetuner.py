@@ -198,7 +198,7 @@ def main(argv=None):
     # ds_config subset
     zero_stage, betas, eps, wd, clip = args.zero_stage, (0.9, 0.999), 1e-8, 0.01, 1.0
     bucket, comm_dtype, sched_kind = int(2e8), torch.float32, "linear"
-    want_offload = False
+    want_offload = want_offload_param = False
     if args.ds_config:
         with open(args.ds_config) as f:
             ds = json.load(f)
@@ -211,7 +211,7 @@ def main(argv=None):
             wd = float(opt["weight_decay"])
         if isinstance(ds.get("gradient_clipping"), (int, float)):
             clip = float(ds["gradient_clipping"])
-        zo = ds.get("zero_optimization") or {}
+        zo = ds.get("zero_optimization") or {}  # its "stage" is overridden by --zero-stage (finetuner.py:915-920)
         if isinstance(zo.get("reduce_bucket_size"), (int, float)):
             bucket = int(zo["reduce_bucket_size"])
         if (ds.get("communication_data_type") or "").lower() in ("bf16", "bfloat16", "fp16"):
@@ -220,27 +220,32 @@ def main(argv=None):
         if sched.get("type") == "WarmupLR":
             sched_kind = "warmup"  # linear warmup then constant (ds_config.json:19-26)
         want_offload = (zo.get("offload_optimizer") or {}).get("device") == "cpu"
-    if zero_stage == 3 and main_proc:
-        log.info("ZeRO-3 requested: parameters stay replicated (288 GB HBM), optimizer state sharded")
-    # ds_config offload_optimizer=cpu is honoured when the sharded fp32 optimizer
-    # state would not fit next to the bf16 params + fp32 grads in HBM (or when
-    # forced with KCA_OFFLOAD_OPTIMIZER=1; =0 disables it)
+        want_offload_param = (zo.get("offload_param") or {}).get("device") == "cpu"
+    # ds_config offload_optimizer=cpu (and offload_param=cpu with stage 3) are honoured when
+    # this rank's share of params + grads + fp32 optimizer state would not fit in HBM (or when
+    # forced with KCA_OFFLOAD_OPTIMIZER=1; =0 disables it): 288 GB holds every model the
+    # reference finetunes on one GPU without offload.
     offload = False
     force = os.environ.get("KCA_OFFLOAD_OPTIMIZER")
+    n_par = sum(p.numel() for p in model.parameters() if p.requires_grad)
+    eff = zero_stage if world > 1 else 0
+    need = n_par * (2 / (world if eff >= 3 else 1) + 4 / (world if eff >= 2 else 1)
+                    + 12 / (world if eff >= 1 else 1))
     if force is not None:
         offload = force not in ("0", "false", "no")
     elif want_offload:
-        n_par = sum(p.numel() for p in model.parameters() if p.requires_grad)
-        shard = world if zero_stage >= 1 else 1
-        need = n_par * 6 + n_par * 12 / shard
         total = torch.cuda.get_device_properties(dev).total_memory if dev.type == "cuda" else float("inf")
         offload = need > 0.85 * total
+    offload_param = offload and want_offload_param and eff >= 3
     if main_proc:
-        log.info("optimizer state: %s", "host (offload_optimizer=cpu, host AdamW)" if offload else "HBM")
+        log.info("ZeRO stage %d (effective %d): %.1f GiB/rank of params+grads+optimizer state", zero_stage, eff,
+                 need / 2**30)
+        log.info("optimizer state: %s%s", "host (offload_optimizer=cpu, host AdamW)" if offload else "HBM",
+                 "; bf16 param shard: host (offload_param=cpu)" if offload_param else "")
 
     engine = TrainEngine(model, lr=args.lr, betas=betas, eps=eps, weight_decay=wd, max_grad_norm=clip,
                          zero_stage=zero_stage, grad_accum=args.gradients, bucket_elems=bucket,
-                         comm_dtype=comm_dtype, offload_optimizer=offload)
+                         comm_dtype=comm_dtype, offload_optimizer=offload, offload_param=offload_param)
     bs = args.bs if args.bs != -1 else estimate_batch_size(model, args.context_size, args.bs_divisor, dev)
     gas = args.gradients
     per_step = bs * gas * world
@@ -279,6 +284,10 @@ def main(argv=None):
     def sample(step):
         if tokenizer is None:
             return
+        with engine.gathered():  # ZeRO-3: full weights once, not per generated token
+            _sample(step)
+
+    def _sample(step):
         model.eval()
         for pr in prompts:
             ids = torch.tensor([tokenizer.encode(pr)], device=dev)
@@ -331,10 +340,10 @@ def main(argv=None):
                 lo = base + (g * world + rank) * bs
                 batch = collate([dataset[i] for i in idx[lo:lo + bs]])
                 ids = batch["input_ids"].to(dev, non_blocking=True)
-                mask = batch["attention_mask"].to(dev, non_blocking=True)
                 labels = batch["labels"].to(dev, non_blocking=True)
+                kv = batch["kv_len"]  # host-classified mask: None / key lengths / per-key mask
                 with trace_range("forward"):
-                    loss = model(ids, attention_mask=mask, labels=labels)
+                    loss = model(ids, labels=labels, kv_len=kv.to(dev, non_blocking=True) if kv is not None else None)
                 with trace_range("backward"):
                     engine.backward(loss)
                 d = loss.detach().float()
@@ -359,8 +368,9 @@ def main(argv=None):
             state.update(global_step=step, epoch=epoch)
             if args.save_steps and step % args.save_steps == 0:
                 ck = os.path.join(output_dir, f"checkpoint-{step}")
-                ckpt_writer.save(ck, model, engine, state, {k: str(v) for k, v in vars(args).items()},
-                                 tokenizer, rank, world, barrier)
+                with engine.gathered():  # ZeRO-3: stage3_gather_16bit_weights_on_model_save
+                    ckpt_writer.save(ck, model, engine, state, {k: str(v) for k, v in vars(args).items()},
+                                     tokenizer, rank, world, barrier)
                 if main_proc:
                     log.info(f"saved {ck}")
         if step >= total_steps:
@@ -370,13 +380,14 @@ def main(argv=None):
     barrier()
     if watchdog is not None:
         watchdog.stop()
-    if main_proc:
-        final = os.path.join(output_dir, "final")
-        save_pretrained(model, final)
-        if tokenizer is not None:
-            tokenizer.save_pretrained(final)
-        write_ready(final)
-        log.info(f"FINAL: {final}")
+    with engine.gathered():  # every rank joins the ZeRO-3 gathers; rank 0 writes
+        if main_proc:
+            final = os.path.join(output_dir, "final")
+            save_pretrained(model, final)
+            if tokenizer is not None:
+                tokenizer.save_pretrained(final)
+            write_ready(final)
+            log.info(f"FINAL: {final}")
     sink.close()
     barrier()
     return state

@@ -11,9 +11,11 @@ activation checkpointing: kubeflow/training-operator/gpt-neox/
 Rank layout (tp fastest, then pp, then dp) keeps a TP group on adjacent GPUs
 of one node, i.e. on direct xGMI links, where its 4 all-reduces per layer per
 micro-batch run; pipeline p2p and the once-per-step DP all-reduce tolerate the
-slower paths. Every rank holds only its (stage, TP shard) of the weights; with
-288 GB per MI355X, NeoX-20B at TP2xPP4 is ~2.5B params (~40 GB incl. fp32
-AdamW state) per GPU, so plain DP all-reduce replaces ZeRO-1 sharding.
+slower paths. Every rank holds only its (stage, TP shard) of the weights, and
+the optimizer state is ZeRO-1 sharded over the DP group (``--zero-stage 1``,
+the reference's setting): per-bucket reduce-scatter over DP in the last
+micro-batch's backward, the clip norm summed over DP then over the
+model-parallel group with TP-replicated params counted once.
 
 Checkpoints: ``{output}/checkpoint-{step}/mp_rank_{tp:02d}_{pp:03d}.safetensors``
 (written by dp rank 0 of each shard) + ``meta.json``; ``consolidate`` rebuilds
@@ -47,7 +49,8 @@ def build_parser():
     p.add_argument("--micro-batch", type=int, default=1)
     p.add_argument("--gradients", type=int, default=1, help="micro-batches per optimizer step (GAS)")
     p.add_argument("--seq-len", type=int, default=2048)
-    p.add_argument("--zero-stage", type=int, default=0, help="accepted for CLI parity; model-parallel runs use 0")
+    p.add_argument("--zero-stage", type=int, default=1, choices=(0, 1, 2),
+                   help="ZeRO stage over the data-parallel group (NeoX: 1, 04-finetune-workflow.yaml:236-244)")
     p.add_argument("--gradient-checkpointing", action="store_true")
     p.add_argument("--lr", type=float, default=6e-5)
     p.add_argument("--min-lr", type=float, default=0.0)
@@ -262,7 +265,7 @@ def main(argv=None):
     cfg, stage = build_model_shard(args, topo, dev, dtype)
     stage.train()
     eng = TrainEngine(stage, lr=args.lr, betas=tuple(args.betas), eps=args.eps, weight_decay=args.weight_decay,
-                      max_grad_norm=args.max_grad_norm, zero_stage=0, grad_accum=args.gradients,
+                      max_grad_norm=args.max_grad_norm, zero_stage=args.zero_stage, grad_accum=args.gradients,
                       group=topo.dp_group)
     if topo.world > 1:
         rep = {n: topo.tp for n in replicated_param_names(stage)} if topo.tp > 1 else {}

@@ -1,6 +1,8 @@
-"""Multi-process CPU tests (gloo, world_size 2): the bucketed ZeRO engine must
-produce the same parameters as a single-process run over the same global
-batch, and the launcher must run the finetuner CLI across ranks."""
+"""Multi-process CPU tests (gloo): the bucketed ZeRO engine (stages 0-3, world
+2/4/8) must produce the same parameters as a single-process run over the same
+global batch; stage 3 must hold less per rank than stage 2, which holds less
+than stage 1; the launcher must run the finetuner CLI across ranks (ZeRO-2 and
+ZeRO-3, checkpoint + resume + final save of the gathered weights)."""
 import os
 import socket
 import subprocess
@@ -33,61 +35,119 @@ def _batches(world, gas, bs=2, seq=16, steps=3):
     return [[torch.randint(0, 256, (bs * world, seq), generator=g) for _ in range(gas)] for _ in range(steps)]
 
 
-def _worker(rank, world, port, stage, bucket, out_path):
+def _worker(rank, world, port, stage, bucket, ckpt, out_path):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.set_num_threads(1)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from kubernetes_cloud_amd.train.engine import TrainEngine
     m = _model()
+    m.gradient_checkpointing_enable(ckpt)
+    m.train()
     eng = TrainEngine(m, lr=1e-2, weight_decay=0.01, zero_stage=stage, grad_accum=2, bucket_elems=bucket)
+    mem = eng.memory_report()
     for step in _batches(world, 2):
         mbs = [b[rank * 2:(rank + 1) * 2] for b in step]
         eng.train_batch(mbs, lambda ids: m(ids, labels=ids))
+    if stage == 3:  # released between steps: only this rank's shard is resident
+        assert all(p.numel() == 0 for p in m.parameters()), "ZeRO-3 params not released"
+    with eng.gathered():
+        sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
     if rank == 0:
-        torch.save({k: v.detach().clone() for k, v in m.state_dict().items()}, out_path)
+        torch.save({"sd": sd, "mem": mem}, out_path)
     dist.barrier()
     dist.destroy_process_group()
 
 
-def _reference():
+def _reference(world):
     from kubernetes_cloud_amd.train.engine import TrainEngine
     m = _model()
     eng = TrainEngine(m, lr=1e-2, weight_decay=0.01, zero_stage=0, grad_accum=2)
-    for step in _batches(2, 2):
-        # global batch of 4 per micro-step, same mean as 2 ranks x 2
+    for step in _batches(world, 2):
+        # global batch of 2*world per micro-step, same mean as world ranks x 2
         def lf(ids):
-            return 0.5 * (m(ids[:2], labels=ids[:2]) + m(ids[2:], labels=ids[2:]))
+            return sum(m(ids[2 * r:2 * r + 2], labels=ids[2 * r:2 * r + 2]) for r in range(world)) / world
         eng.train_batch(step, lf)
     return {k: v.detach().clone() for k, v in m.state_dict().items()}
 
 
-@pytest.mark.parametrize("stage,bucket", [(0, 10_000), (1, 10_000), (2, 3_000)])
-def test_engine_dp_matches_single_process(stage, bucket, tmp_path):
+def _run(world, stage, bucket, tmp_path, ckpt=False):
     ctx = mp.get_context("spawn")
     port = _port()
-    out = str(tmp_path / "sd.pt")
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, stage, bucket, out)) for r in range(2)]
+    out = str(tmp_path / f"sd_{world}_{stage}_{int(ckpt)}.pt")
+    ps = [ctx.Process(target=_worker, args=(r, world, port, stage, bucket, ckpt, out)) for r in range(world)]
     for p in ps:
         p.start()
     for p in ps:
         p.join(timeout=300)
         assert p.exitcode == 0
-    got = torch.load(out, weights_only=True)
-    ref = _reference()
+    return torch.load(out, weights_only=True)
+
+
+_REFS: dict = {}
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("stage,bucket", [(0, 10_000), (1, 10_000), (2, 3_000), (3, 0)])
+def test_engine_dp_matches_single_process(world, stage, bucket, tmp_path):
+    got = _run(world, stage, bucket, tmp_path)["sd"]
+    if world not in _REFS:
+        _REFS[world] = _reference(world)
+    ref = _REFS[world]
     for k in ref:
         assert torch.allclose(got[k], ref[k], atol=2e-5, rtol=1e-4), k
 
 
-def test_launcher_runs_finetuner_two_ranks(tmp_path):
+def test_zero3_with_activation_checkpointing_matches(tmp_path):
+    """Recompute inside backward re-enters the blocks' forward hooks: the
+    gathered params must stay resident through the recompute."""
+    got = _run(2, 3, 0, tmp_path, ckpt=True)["sd"]
+    ref = _reference(2)
+    for k in ref:
+        assert torch.allclose(got[k], ref[k], atol=2e-5, rtol=1e-4), k
+
+
+def test_zero_stage_memory_per_rank(tmp_path):
+    """Per-rank resident bytes shrink stage by stage."""
+    def total(world, stage, bucket):
+        mem = _run(world, stage, bucket, tmp_path)["mem"]
+        return mem, sum(v for k, v in mem.items() if k != "zero_stage")
+    m1, t1 = total(4, 1, 3_000)
+    m2, t2 = total(4, 2, 3_000)
+    m3, t3 = total(4, 3, 0)
+    assert (m1["zero_stage"], m2["zero_stage"], m3["zero_stage"]) == (1, 2, 3)
+    assert m2["grads_fp32"] < m1["grads_fp32"] / 2  # no full fp32 gradient buffer at stage 2
+    assert m3["params_bf16"] < m2["params_bf16"] / 2  # only the param shard at stage 3
+    assert t3 < t2 < t1
+
+
+@pytest.mark.parametrize("stage", [2, 3])
+def test_launcher_runs_finetuner_two_ranks(stage, tmp_path):
+    from kubernetes_cloud_amd.io.hf import read_hf_state_dict
+
     from .helpers import make_model_dir, make_tokens
     model = make_model_dir(str(tmp_path / "m"))
     data = make_tokens(str(tmp_path / "d.tokens"), n_ctx=16, ctx=16)
-    cmd = [sys.executable, "-m", "kubernetes_cloud_amd.launch", "--num_gpus", "2", "-m",
-           "kubernetes_cloud_amd.train.finetuner", "--run-name", "dd", "--model", model, "--dataset", data,
-           "--context-size", "16", "--bs", "2", "--gradients", "1", "--output-path", str(tmp_path / "o"),
-           "--logs", str(tmp_path / "l"), "--save-steps", "2", "--max-steps", "2", "--zero-stage", "2"]
-    env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
-    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
-    assert r.returncode == 0, r.stderr[-3000:]
+
+    def run(max_steps):
+        cmd = [sys.executable, "-m", "kubernetes_cloud_amd.launch", "--num_gpus", "2", "-m",
+               "kubernetes_cloud_amd.train.finetuner", "--run-name", "dd", "--model", model, "--dataset", data,
+               "--context-size", "16", "--bs", "2", "--gradients", "1", "--output-path", str(tmp_path / "o"),
+               "--logs", str(tmp_path / "l"), "--save-steps", "2", "--max-steps", str(max_steps),
+               "--zero-stage", str(stage)]
+        env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+        r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
+        assert r.returncode == 0, r.stderr[-3000:]
+        return r
+    run(2)
     rd = tmp_path / "o" / "results-dd"
     assert (rd / "checkpoint-2" / "optimizer" / "rank-00001.safetensors").exists()
     assert (rd / "final" / ".ready.txt").exists()
+    w2 = read_hf_state_dict(str(rd / "checkpoint-2"))
+    fin = read_hf_state_dict(str(rd / "final"))
+    assert all(v.numel() > 0 for v in fin.values())  # gathered, not this rank's empty placeholders
+    for k in w2:
+        assert torch.equal(w2[k], fin[k]), k
+    r = run(4)  # resumes from checkpoint-2 (optimizer shards + master)
+    assert "RESUMED" in r.stderr
+    fin4 = read_hf_state_dict(str(rd / "final"))
+    assert any(not torch.equal(fin4[k], fin[k]) for k in fin)

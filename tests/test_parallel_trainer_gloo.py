@@ -1,7 +1,8 @@
-"""3D-parallel trainer on CPU (gloo): TP=2 x PP=2 (GPT-J, untied) and PP=2
-(GPT-2, tied embedding) must train to the same weights as a single-process
-run over the same micro-batches; sharded checkpoints consolidate back to an
-HF directory."""
+"""3D-parallel trainer on CPU (gloo): TP=2 x PP=2 (GPT-J, untied), PP=2
+(GPT-2, tied embedding) and DP=2 x TP=2 x PP=2 with ZeRO-1 over the DP group
+(the reference's NeoX layout, gpt-neox/04-finetune-workflow.yaml:199-244) must
+train to the same weights as a single-process run over the same global
+micro-batches; sharded checkpoints consolidate back to an HF directory."""
 import os
 import socket
 
@@ -21,55 +22,59 @@ def _port():
         return s.getsockname()[1]
 
 
-def _args(model_dir, out, tp, pp):
-    return ["--model", model_dir, "--tp", str(tp), "--pp", str(pp), "--micro-batch", str(MB), "--gradients",
+def _args(model_dir, out, tp, pp, zero=1):
+    return ["--model", model_dir, "--tp", str(tp), "--pp", str(pp), "--zero-stage", str(zero),
+            "--micro-batch", str(MB), "--gradients",
             str(GAS), "--seq-len", str(SEQ), "--max-steps", str(STEPS), "--lr", "1e-2", "--lr-schedule",
             "constant", "--warmup-ratio", "0", "--output-path", out, "--weight-decay", "0.01"]
 
 
-def _worker(rank, world, port, model_dir, out, tp, pp):
+def _worker(rank, world, port, model_dir, out, tp, pp, zero):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
     from kubernetes_cloud_amd.train.parallel_trainer import main
-    main(_args(model_dir, out, tp, pp))
+    main(_args(model_dir, out, tp, pp, zero))
     dist.destroy_process_group()
 
 
-def _reference(model_dir):
+def _reference(model_dir, dp=1):
     from kubernetes_cloud_amd.io.hf import load_pretrained
     from kubernetes_cloud_amd.models.config import LMConfig
     from kubernetes_cloud_amd.train.engine import TrainEngine
     m = load_pretrained(model_dir, dtype=torch.float32)
     cfg = LMConfig.from_pretrained(model_dir)
     eng = TrainEngine(m, lr=1e-2, betas=(0.9, 0.95), weight_decay=0.01, max_grad_norm=1.0, grad_accum=GAS)
-    g = torch.Generator().manual_seed(42)  # synthetic stream of dp replica 0 (seed + dp_idx)
+    gens = [torch.Generator().manual_seed(42 + d) for d in range(dp)]  # replica d's stream: seed + dp_idx
     for _ in range(STEPS):
-        mbs = [torch.randint(0, cfg.vocab_size, (MB, SEQ), generator=g) for _ in range(GAS)]
-        for ids in mbs:
-            eng.backward(m(ids, labels=ids))
+        mbs = [[torch.randint(0, cfg.vocab_size, (MB, SEQ), generator=g) for _ in range(GAS)] for g in gens]
+        for k in range(GAS):
+            eng.backward(sum(m(mbs[d][k], labels=mbs[d][k]) for d in range(dp)) / dp)
         eng.step(1e-2)
     return m
 
 
-@pytest.mark.parametrize("preset,tp,pp", [("gpt-j-6b", 2, 2), ("gpt2", 1, 2)])
-def test_3d_matches_single_process(preset, tp, pp, tmp_path):
+@pytest.mark.parametrize("preset,tp,pp,dp,zero", [("gpt-j-6b", 2, 2, 1, 0), ("gpt2", 1, 2, 1, 0),
+                                                  ("gpt-j-6b", 2, 2, 2, 1), ("gpt2", 1, 2, 2, 1),
+                                                  ("gpt-j-6b", 2, 1, 2, 2)])
+def test_3d_matches_single_process(preset, tp, pp, dp, zero, tmp_path):
     from kubernetes_cloud_amd.io.hf import load_pretrained
     from kubernetes_cloud_amd.train.parallel_trainer import consolidate
     d = make_model_dir(str(tmp_path / "m"), preset, vocab_size=128, tokenizer=False)
     out = str(tmp_path / "out")
-    world = tp * pp
+    world = tp * pp * dp
     port = _port()
     ctx = mp.get_context("spawn")
-    ps = [ctx.Process(target=_worker, args=(r, world, port, d, out, tp, pp)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, d, out, tp, pp, zero)) for r in range(world)]
     for p in ps:
         p.start()
     for p in ps:
         p.join(timeout=600)
         assert p.exitcode == 0
     ck = os.path.join(out, f"checkpoint-{STEPS}")
-    assert len([f for f in os.listdir(ck) if f.startswith("mp_rank_")]) == world
+    assert len([f for f in os.listdir(ck) if f.startswith("mp_rank_")]) == tp * pp
     merged = consolidate(ck, str(tmp_path / "merged"))
     got = load_pretrained(merged, dtype=torch.float32).state_dict()
-    ref = _reference(d).state_dict()
+    ref = _reference(d, dp).state_dict()
     err = max(float((got[k] - ref[k]).abs().max()) for k in ref if not k.endswith("alibi"))
     assert err < 2e-4, err
