@@ -1,0 +1,121 @@
+#!/usr/bin/env python3
+"""Weight-load benchmark (BASELINE.md "Weight load": GB/s and seconds to ready,
+PVC -> HBM for GPT-J fp16 ~12.1 GB; the reference prints the same numbers from
+tensorizer at tensorizer-isvc/tensorizer_hf_isvc/load_model.py:63-73).
+
+    python bench/weight_load_bench.py [--model gpt-j-6b] [--dir /tmp] [--http]
+
+Writes a random-init GPT-J-6B as fp16 ``.tensors`` (config embedded), then
+measures ``load_tensorized`` -- no-init model construction + native stream
+into preallocated HBM parameters -- from:
+
+* the file with O_DIRECT (storage -> pinned ring -> hipMemcpyAsync; the page
+  cache is bypassed, so this is a cold read of the device),
+* the same file again (steady state),
+* ``--http``: a local HTTP/1.1 Range server (sendfile) through the ranged-GET
+  streamer (16 keep-alive connections) -- the s3:// / https:// code path.
+
+One JSON line per source. Random weights (no checkpoints offline).
+"""
+from __future__ import annotations
+
+import argparse
+import http.server
+import json
+import os
+import sys
+import threading
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch
+
+
+class _SendfileRange(http.server.BaseHTTPRequestHandler):
+    protocol_version = "HTTP/1.1"
+    root = "/tmp"
+
+    def log_message(self, *a):
+        pass
+
+    def do_GET(self):
+        path = os.path.join(self.root, self.path.lstrip("/"))
+        size = os.path.getsize(path)
+        a, b = 0, size - 1
+        rng = self.headers.get("Range")
+        if rng:
+            a, b = (int(x) for x in rng.split("=")[1].split("-"))
+            b = min(b, size - 1)
+        n = b - a + 1
+        self.send_response(206 if rng else 200)
+        self.send_header("Content-Length", str(n))
+        if rng:
+            self.send_header("Content-Range", f"bytes {a}-{b}/{size}")
+        self.end_headers()
+        self.wfile.flush()
+        with open(path, "rb") as f:
+            off = a
+            while off <= b:
+                sent = os.sendfile(self.connection.fileno(), f.fileno(), off, b + 1 - off)
+                if sent <= 0:
+                    break
+                off += sent
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="gpt-j-6b")
+    ap.add_argument("--dir", default=os.environ.get("TMPDIR", "/tmp"))
+    ap.add_argument("--http", action="store_true")
+    ap.add_argument("--threads", type=int, default=8)
+    ap.add_argument("--keep", action="store_true")
+    args = ap.parse_args()
+    from kubernetes_cloud_amd.io.hf import load_tensorized, serialize_causal_lm
+    from kubernetes_cloud_amd.models.causal_lm import build_model
+    from kubernetes_cloud_amd.models.config import preset
+    dev = torch.device("cuda", 0)
+    cfg = preset(args.model)
+    path = os.path.join(args.dir, f"kca_{args.model}.tensors")
+    t0 = time.perf_counter()
+    m = build_model(cfg, device=dev, dtype=torch.float16, seed=0)
+    ref = {k: v.float().abs().sum().item() for k, v in list(m.state_dict().items())[:3]}
+    info = serialize_causal_lm(m, path)
+    del m
+    torch.cuda.empty_cache()
+    print(f"[weight-load] wrote {info['bytes'] / 1e9:.2f} GB to {path} in {time.perf_counter() - t0:.1f}s",
+          file=sys.stderr, flush=True)
+    results = []
+
+    def run(label, uri, **kw):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        model, st = load_tensorized(uri, None, device=dev, dtype=torch.float16, threads=args.threads)
+        torch.cuda.synchronize()
+        ready = time.perf_counter() - t
+        got = {k: v.float().abs().sum().item() for k, v in list(model.state_dict().items())[:3]}
+        assert all(abs(got[k] - ref[k]) <= 1e-3 * max(1.0, ref[k]) for k in ref), (got, ref)
+        rec = {"metric": "weight load", "source": label, "model": args.model, "dtype": "fp16",
+               "bytes": int(st["bytes"]), "stream_s": round(st["seconds"], 3), "gbps": round(st["gbps"], 2),
+               "seconds_to_ready": round(ready, 3), "threads": args.threads, "data": "random-init weights", **kw}
+        print(json.dumps(rec), flush=True)
+        results.append(rec)
+        del model
+        torch.cuda.empty_cache()
+
+    run("file O_DIRECT (cold device read)", path)
+    run("file O_DIRECT (repeat)", path)
+    if args.http:
+        class H(_SendfileRange):
+            root = args.dir
+        srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), H)
+        threading.Thread(target=srv.serve_forever, daemon=True).start()
+        url = f"http://127.0.0.1:{srv.server_address[1]}/{os.path.basename(path)}"
+        run("http://localhost ranged GET (page-cache warm server)", url)
+        srv.shutdown()
+    if not args.keep:
+        os.remove(path)
+
+
+if __name__ == "__main__":
+    main()

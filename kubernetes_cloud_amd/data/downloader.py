@@ -53,23 +53,18 @@ def download(model: str, dest: str, tokenizer_only: bool = False, kind: str = ""
 def tensorize(dest: str, filename: str, dtype: str = "float16") -> str:
     import torch
 
-    from ..io.hf import load_pretrained
-    from ..io.tensors import serialize
+    from ..io.hf import load_pretrained, serialize_causal_lm
     dt = getattr(torch, dtype)
     model = load_pretrained(dest, device="cpu", dtype=dt)
     out = os.path.join(dest, filename)
-    serialize(model, out)
+    serialize_causal_lm(model, out)  # config embedded: the URI alone rebuilds the model
     return out
 
 
 def check_tensorized(model: str, base_url: str | None = None, timeout: float = 10.0) -> bool:
-    base = base_url or os.getenv("TENSORIZED_BASE_URL", "https://accel-object.ord1.coreweave.com/tensorized")
-    try:
-        import requests
-        r = requests.head(f"{base}/{model}/model.tensors", timeout=timeout, allow_redirects=True)
-        return r.status_code == 200
-    except Exception:  # noqa: BLE001 -- offline / DNS failure == not available
-        return False
+    from ..io.remote import PUBLIC_TENSORIZED, exists
+    base = base_url or os.getenv("TENSORIZED_BASE_URL") or os.getenv("KCA_TENSORIZED_BASE", PUBLIC_TENSORIZED)
+    return exists(f"{base.rstrip('/')}/{model}/model.tensors", timeout)  # offline / DNS failure == False
 
 
 def main(argv=None):

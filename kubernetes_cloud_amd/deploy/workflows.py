@@ -98,11 +98,19 @@ def finetune_workflow() -> dict:
     main = {"name": "main", "steps": [
         [{"name": "check-model", "template": "check-model", "arguments": _args(["model"]),
           "when": "'{{workflow.parameters.tensorizer_uri}}' == ''"}],
+        # weights come from the PVC unless they stream from a tensorized URI (the finetuner's
+        # --tensorizer-uri, or its probe of the public bucket when check-model found the model);
+        # config + tokenizer always land on the PVC (the finetuner and the tokenizer step read them)
         [{"name": "model-downloader", "template": "model-downloader",
           "arguments": {"parameters": [{"name": "model", "value": wp("model")},
                                        {"name": "dest", "value": "/" + wp("pvc") + "/models/" + wp("model")},
                                        {"name": "tokenizer_only", "value": "{{steps.check-model.outputs.result}}"}]},
-          "when": "'{{workflow.parameters.tensorizer_uri}}' == ''"}],
+          "when": "'{{workflow.parameters.tensorizer_uri}}' == ''"},
+         {"name": "model-downloader-tokenizer", "template": "model-downloader",
+          "arguments": {"parameters": [{"name": "model", "value": wp("model")},
+                                       {"name": "dest", "value": "/" + wp("pvc") + "/models/" + wp("model")},
+                                       {"name": "tokenizer_only", "value": "true"}]},
+          "when": "'{{workflow.parameters.tensorizer_uri}}' != ''"}],
         [{"name": "dataset-downloader", "template": "dataset-downloader",
           "arguments": {"parameters": [{"name": "output", "value": "/" + wp("pvc") + "/" + wp("dataset")}]},
           "when": "{{workflow.parameters.inference_only}} == false && {{workflow.parameters.download_dataset}} == true"}],

@@ -67,6 +67,43 @@ def load_pretrained(path: str, device="cpu", dtype=torch.bfloat16, random_init_i
     return model
 
 
+def load_tensorized(uri: str, config_dir: str | None = None, device="cpu", dtype=torch.bfloat16,
+                    threads: int = 8) -> tuple[CausalLM, dict]:
+    """Build the model with no init and stream its weights from a ``.tensors``
+    file or ``http(s)://`` / ``s3://`` URI straight into the (preallocated)
+    parameters -- the reference's ``no_init_or_tensor`` + ``TensorDeserializer``
+    path (finetuner.py:802-815, tensorizer-isvc load_model.py:46-59). The
+    config comes from ``config_dir/config.json`` when present, else from the
+    file's own metadata (written by ``serialize_causal_lm``). -> (model, stats)."""
+    from ..models.causal_lm import alibi_slopes
+    from .tensors import load_into_module, metadata
+    if config_dir and os.path.exists(os.path.join(config_dir, "config.json")):
+        cfg = LMConfig.from_pretrained(config_dir)
+    else:
+        meta = metadata(uri)
+        if "config" not in meta:
+            raise FileNotFoundError(f"{uri}: no config.json given and no config in the file metadata")
+        cfg = LMConfig.from_hf(meta["config"])
+    with torch.device("meta"):
+        model = CausalLM(cfg)
+    model = model.to(dtype).to_empty(device=device)  # cast on meta: no fp32 materialisation
+    stats = load_into_module(model, uri, device=device, threads=threads)
+    if cfg.alibi:
+        for blk in model.h:
+            blk.attn.alibi = alibi_slopes(cfg.n_heads).to(device)
+    return model, stats
+
+
+def serialize_causal_lm(model: CausalLM, path: str, dtype: torch.dtype | None = None) -> dict:
+    """``.tensors`` of a causal LM with its HF config embedded (so a URI alone
+    is enough to rebuild it), e.g. ``model.tensors`` / ``gptj.tensors``."""
+    from .tensors import serialize
+    hf_cfg = model.cfg.to_hf()
+    hf_cfg["vocab_size"] = model.cfg.vocab_size
+    sd = {k: v for k, v in model.state_dict().items() if not k.endswith("alibi")}
+    return serialize(sd, path, dtype=dtype, metadata={"config": hf_cfg, "kind": "causal_lm"})
+
+
 def save_pretrained(model: CausalLM, path: str, max_shard_bytes: int = 10 << 30):
     """Write config.json + (sharded) safetensors in HF naming."""
     from safetensors.torch import save_file
@@ -128,5 +165,6 @@ def load_tokenizer(path: str, eot: str = "", pad: str = ""):
     return tok
 
 
-__all__ = ["read_hf_state_dict", "load_pretrained", "save_pretrained", "load_tokenizer",
+__all__ = ["read_hf_state_dict", "load_pretrained", "save_pretrained", "load_tokenizer", "load_tensorized",
+           "serialize_causal_lm",
            "is_ignorable_hf_key"]

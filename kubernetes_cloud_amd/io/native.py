@@ -1,5 +1,5 @@
 """ctypes binding of the host-side native runtime ``_lib/libkca_host.so``
-(weight streamer, host AdamW, BPE tokenizer / packer). Built by
+(file and HTTP(S)/S3 weight streamers, host AdamW, BPE tokenizer / packer). Built by
 ``tools/build_ext.py`` with g++ (+ the HIP runtime for the device streamer)."""
 from __future__ import annotations
 
@@ -17,6 +17,9 @@ P, I, LL, F, D = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_floa
 _SIGS = {
     "kca_read_ranges": (I, [ctypes.c_char_p, I, P, P, P, I, LL, P]),
     "kca_stream_to_device": (I, [ctypes.c_char_p, I, P, P, P, I, I, LL, I, P]),
+    "kca_http_get_range": (I, [ctypes.c_char_p, I, I, I, ctypes.c_char_p, ctypes.c_char_p, LL, LL, P, P, D]),
+    "kca_http_stream": (I, [ctypes.c_char_p, I, I, I, ctypes.c_char_p, ctypes.c_char_p, I, P, P, P, I, I, LL, D,
+                            P]),
     "kca_host_simd_level": (I, []),
     "kca_host_adamw": (I, [P, P, P, P, P, P, LL, F, F, F, F, F, F, F, F, I]),
     "kca_bpe_new": (P, [P, I, P, P, P]),

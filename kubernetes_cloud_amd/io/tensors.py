@@ -128,13 +128,23 @@ def _python_read(path, offs, lens, tensors):
     return float(sum(lens)), time.perf_counter() - t0
 
 
+def _header_any(path: str):
+    from . import remote
+    if remote.is_remote(path):
+        return remote.read_header(path)
+    hdr, start = read_header(path)
+    return hdr, start, None
+
+
 def load_into_module(module: torch.nn.Module, path: str, device=None, strict: bool = True,
                      threads: int = 8, chunk: int = 64 << 20, odirect: bool = True) -> dict:
-    """Stream a ``.tensors`` file into an existing module's parameters/buffers.
+    """Stream a ``.tensors`` file -- a local path, or an ``http(s)://`` /
+    ``s3://`` URI (io/remote.py) -- into an existing module's parameters/buffers.
 
     Same-dtype tensors stream straight into the parameter storage; others go
     through a staging tensor and a cast. Returns {bytes, seconds, gbps}."""
-    hdr, data_start = read_header(path)
+    t_begin = time.perf_counter()
+    hdr, data_start, rem = _header_any(path)
     own = dict(module.state_dict(keep_vars=True))
     dev = torch.device(device) if device is not None else next(module.parameters()).device
     offs, lens, ptrs, targets, casts = [], [], [], [], []
@@ -165,7 +175,11 @@ def load_into_module(module: torch.nn.Module, path: str, device=None, strict: bo
         if missing:
             raise KeyError(f"missing in {path}: {missing[:8]}")
     from . import native
-    if native.available():
+    if rem is not None:
+        from . import remote
+        nbytes, secs = remote.stream(rem, offs, lens, ptrs, dev, threads=max(threads, 16),
+                                     chunk=min(chunk, 16 << 20))
+    elif native.available():
         nbytes, secs = _stream(path, offs, lens, ptrs, dev, threads, chunk, odirect)
     else:
         if dev.type == "cuda":
@@ -176,11 +190,12 @@ def load_into_module(module: torch.nn.Module, path: str, device=None, strict: bo
             dst.copy_(buf)
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
-    return {"bytes": nbytes, "seconds": secs, "gbps": nbytes / max(secs, 1e-9) / 1e9}
+    return {"bytes": nbytes, "seconds": secs, "gbps": nbytes / max(secs, 1e-9) / 1e9,
+            "seconds_total": time.perf_counter() - t_begin, "source": "http" if rem is not None else "file"}
 
 
 def load_state_dict(path: str, device="cpu", threads: int = 8) -> dict:
-    hdr, data_start = read_header(path)
+    hdr, data_start, rem = _header_any(path)
     dev = torch.device(device)
     out, offs, lens, ptrs, ts = {}, [], [], [], []
     for e in hdr["tensors"]:
@@ -192,7 +207,10 @@ def load_state_dict(path: str, device="cpu", threads: int = 8) -> dict:
             ptrs.append(t.data_ptr())
             ts.append(t)
     from . import native
-    if native.available():
+    if rem is not None:
+        from . import remote
+        remote.stream(rem, offs, lens, ptrs, dev, threads=max(threads, 16))
+    elif native.available():
         _stream(path, offs, lens, ptrs, dev, threads, 64 << 20, True)
     else:
         _python_read(path, offs, lens, ts)
@@ -200,4 +218,4 @@ def load_state_dict(path: str, device="cpu", threads: int = 8) -> dict:
 
 
 def metadata(path: str) -> dict:
-    return read_header(path)[0].get("metadata", {})
+    return _header_any(path)[0].get("metadata", {})

@@ -28,31 +28,28 @@ def load_lm(path: str, device=None, dtype=torch.bfloat16, tensors_file: str | No
             random_init: bool = False):
     """-> (model, tokenizer). ``path``: HF-layout directory (config.json +
     safetensors/bin + tokenizer) or a preset name with ``random_init``.
-    ``tensors_file``: stream weights from our ``.tensors`` file straight into
-    HBM (the tensorizer path, load_model.py:46-73) instead of safetensors."""
+    ``tensors_file``: stream weights from our ``.tensors`` file -- or an
+    ``http(s)://`` / ``s3://`` URI -- straight into HBM (the tensorizer path,
+    load_model.py:46-73) instead of safetensors."""
     from ..io.hf import load_pretrained, load_tokenizer
     from ..models.causal_lm import build_model
-    from ..models.config import PRESETS_HF, LMConfig, preset
+    from ..models.config import PRESETS_HF, preset
     dev = torch.device(device) if device is not None else (
         torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu"))
     if dev.type == "cpu" and dtype == torch.bfloat16:
         dtype = torch.float32
     t0 = time.perf_counter()
     tok = None
-    if os.path.isdir(path):
-        cfg = LMConfig.from_pretrained(path)
+    if tensors_file and not os.path.isdir(path):
+        # URI-only load (s3:// / https:// / a file): config from the file's metadata
+        from ..io.hf import load_tensorized
+        model, stats = load_tensorized(tensors_file, None, device=dev, dtype=dtype)
+        log.info("tensorized load: %s", stats)
+    elif os.path.isdir(path):
         if tensors_file:
-            from ..io.tensors import load_into_module
-            with torch.device("meta"):
-                from ..models.causal_lm import CausalLM
-                model = CausalLM(cfg)
-            model = model.to_empty(device=dev).to(dtype)
-            stats = load_into_module(model, tensors_file, device=dev)
+            from ..io.hf import load_tensorized
+            model, stats = load_tensorized(tensors_file, path, device=dev, dtype=dtype)
             log.info("tensorized load: %s", stats)
-            if cfg.alibi:
-                from ..models.causal_lm import alibi_slopes
-                for blk in model.h:
-                    blk.attn.alibi = alibi_slopes(cfg.n_heads).to(dev)
         else:
             model = load_pretrained(path, device=dev, dtype=dtype, random_init_if_missing=random_init)
         try:

@@ -168,7 +168,21 @@ def main(argv=None):
         tokenizer = load_tokenizer(args.model, args.eot, args.pad)
     except Exception as e:  # noqa: BLE001
         log.warning(f"no tokenizer loaded from {args.model}: {e}")
-    cfg = LMConfig.from_pretrained(args.model)
+    # weights from a tensorized file/URI: explicit --tensorizer-uri, else the reference's probe of
+    # the public `tensorized` bucket for this model id (finetuner.py:395-410; 5 s timeout)
+    tz_uri = args.tensorizer_uri
+    if not tz_uri:
+        from ..io.remote import public_tensorized_uri
+        tz_uri = public_tensorized_uri(args.model, fp16=args.fp16) or ""
+        if tz_uri and main_proc:
+            log.info(f"{args.model} is publicly tensorized: streaming {tz_uri}")
+    if tz_uri and os.path.exists(os.path.join(args.model, "config.json")):
+        cfg = LMConfig.from_pretrained(args.model)
+    elif tz_uri:
+        from ..io.tensors import metadata
+        cfg = LMConfig.from_hf(metadata(tz_uri)["config"])
+    else:
+        cfg = LMConfig.from_pretrained(args.model)
     eos_id = tokenizer.eos_token_id if tokenizer is not None else cfg.eos_token_id
     pad_id = tokenizer.pad_token_id if tokenizer is not None else (cfg.pad_token_id if cfg.pad_token_id is not None else eos_id)
 
@@ -188,7 +202,14 @@ def main(argv=None):
     dtype = torch.bfloat16 if (dev.type == "cuda") else torch.float32
     if args.fp16 and dev.type == "cuda":
         log.info("--fp16: 16-bit mixed precision runs as bf16 on MI355X")
-    model = load_pretrained(args.model, device=dev, dtype=dtype, random_init_if_missing=args.random_init)
+    if tz_uri:
+        from ..io.hf import load_tensorized
+        model, ld = load_tensorized(tz_uri, args.model, device=dev, dtype=dtype)
+        if main_proc:
+            log.info(f"TENSORIZED LOAD: {tz_uri} {ld['bytes'] / 1e9:.2f} GB in {ld['seconds']:.2f}s "
+                     f"({ld['gbps']:.2f} GB/s)")
+    else:
+        model = load_pretrained(args.model, device=dev, dtype=dtype, random_init_if_missing=args.random_init)
     if tokenizer is not None and len(tokenizer) > model.cfg.vocab_size:
         model.resize_token_embeddings((len(tokenizer) + 63) // 64 * 64)
     model.gradient_checkpointing_enable(args.gradient_checkpointing)

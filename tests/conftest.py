@@ -6,6 +6,8 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
+# the finetuner probes the public tensorized bucket (finetuner.py:395-410); tests opt in explicitly
+os.environ.setdefault("KCA_TENSORIZED_PROBE", "0")
 
 
 def pytest_configure(config):

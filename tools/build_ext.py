@@ -106,7 +106,7 @@ def build_host(jobs: int = 8, verbose: bool = False) -> str | None:
         objs = list(ex.map(lambda s: _compile([cxx], s, hdrs, obj_dir, flags), srcs))
     out = os.path.join(OUT_DIR, "libkca_host.so")
     cmd = [cxx, "-shared", "-fPIC", "-fopenmp", "-o", out + ".tmp"] + objs + [
-        f"-L{ROCM}/lib", "-lamdhip64", "-lpthread"]
+        f"-L{ROCM}/lib", "-lamdhip64", "-lssl", "-lcrypto", "-lpthread"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stderr}")
