@@ -58,6 +58,7 @@ class Request:
     t_first: float = 0.0
     t_done: float = 0.0
     future: Future | None = None
+    on_token: object = None  # callable(request) after every generated token (streaming front ends)
 
     @property
     def done(self) -> bool:
@@ -88,14 +89,16 @@ class LLMEngine:
         self.stats = {"steps": 0, "decode_tokens": 0, "prefill_tokens": 0, "finished": 0}
 
     # ------------------------------------------------------------ requests
-    def add_request(self, prompt: list, params: SamplingParams, future: Future | None = None) -> Request:
+    def add_request(self, prompt: list, params: SamplingParams, future: Future | None = None,
+                    on_token=None) -> Request:
         prompt = [int(t) for t in prompt]
         if not prompt:
             raise ValueError("empty prompt")
         if len(prompt) >= self.max_len:
             prompt = prompt[-(self.max_len - 1):]
         seed = params.seed if params.seed is not None else random.getrandbits(63)
-        r = Request(next(self._ids), prompt, params, seed=seed, t_arrive=time.perf_counter(), future=future)
+        r = Request(next(self._ids), prompt, params, seed=seed, t_arrive=time.perf_counter(), future=future,
+                    on_token=on_token)
         if params.max_new_tokens <= 0:
             r.finish_reason = "length"
             r.t_done = r.t_arrive
@@ -140,6 +143,11 @@ class LLMEngine:
             r.finish_reason = "stop"
         elif len(r.output) >= p.max_new_tokens or len(r.tokens) >= self.max_len:
             r.finish_reason = "length"
+        if r.on_token is not None:
+            try:
+                r.on_token(r)
+            except Exception:  # noqa: BLE001 -- a broken stream consumer must not stall the batch
+                r.on_token = None
 
     def _finish(self, r: Request):
         r.t_done = time.perf_counter()
@@ -229,11 +237,11 @@ class LLMEngine:
         return reqs
 
     # ------------------------------------------------------ background loop
-    def submit(self, prompt: list, params: SamplingParams) -> Future:
+    def submit(self, prompt: list, params: SamplingParams, on_token=None) -> Future:
         if self._thread is None:
             self.start()
         fut: Future = Future()
-        self.add_request(prompt, params, fut)
+        self.add_request(prompt, params, fut, on_token=on_token)
         return fut
 
     def start(self):

@@ -15,7 +15,9 @@ the same contract natively:
   ``POST /v1/models/<m>:predict``; ``GET /v2``, ``/v2/health/{live,ready}``,
   ``GET /v2/models/<m>[/versions/<v>][/ready]``, ``POST .../infer`` (JSON and
   the binary-tensor extension); Prometheus ``/metrics``. CLI flags as kserve's
-  (``--http_port``, ``--workers``); default port 8080.
+  (``--http_port``, ``--grpc_port``, ``--workers``); default ports 8080 / 8081.
+* the V2 gRPC service (``serving.grpc_v2``: ``GRPCInferenceService`` incl. the
+  bidirectional ``ModelStreamInfer``) on ``--grpc_port`` for the same models.
 """
 from __future__ import annotations
 
@@ -100,6 +102,7 @@ class ModelServer:
     def __init__(self, http_port: int | None = None, workers: int = 1, host: str | None = None,
                  argv: list | None = None):
         a = parse_server_args(argv)
+        self.grpc_port = a.grpc_port
         self.http_port = http_port or a.http_port
         self.workers = workers or a.workers
         self.host = host or a.host
@@ -238,8 +241,17 @@ class ModelServer:
         app = self.create_app(models)
         if extra_routes is not None:
             extra_routes(app)
+        self.grpc_server = None
+        if self.grpc_port and self.grpc_port > 0 and os.getenv("KCA_GRPC", "1") != "0":
+            # KServe V2 / Triton GRPCInferenceService (incl. ModelStreamInfer) on the same models
+            from .grpc_v2 import serve
+            self.grpc_server = serve(self.models, self.grpc_port, self.host)
         log.info("serving %s on %s:%d", list(self.models), self.host, self.http_port)
-        uvicorn.run(app, host=self.host, port=self.http_port, workers=1, log_level="info")
+        try:
+            uvicorn.run(app, host=self.host, port=self.http_port, workers=1, log_level="info")
+        finally:
+            if self.grpc_server is not None:
+                self.grpc_server.stop(grace=2)
 
 
 __all__ = ["Model", "ModelServer", "InvalidInput", "parse_server_args"]

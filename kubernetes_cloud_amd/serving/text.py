@@ -113,11 +113,17 @@ class TextGenerator:
             seed=seed, eos_token_id=eos, stop_sequences=stops, bad_words_ids=bw or None, logprobs=logprobs)
 
     # -------------------------------------------------------------- run
-    def generate_ids(self, prompts: list[list[int]], params: list[SamplingParams]):
+    def generate_ids(self, prompts: list[list[int]], params: list[SamplingParams], on_token=None):
+        """``on_token(index, request)`` is called from the engine thread after
+        every generated token of request ``index`` (streaming responses)."""
+        cbs = [None] * len(prompts) if on_token is None else \
+            [(lambda r, i=i: on_token(i, r)) for i in range(len(prompts))]
         if self.background:
-            futs = [self.engine.submit(p, sp) for p, sp in zip(prompts, params)]
+            futs = [self.engine.submit(p, sp, on_token=cb) for p, sp, cb in zip(prompts, params, cbs)]
             return [f.result() for f in futs]
-        return self.engine.generate(prompts, params)
+        reqs = [self.engine.add_request(p, sp, on_token=cb) for p, sp, cb in zip(prompts, params, cbs)]
+        self.engine.run_until_done(reqs)
+        return reqs
 
     def __call__(self, text_inputs, return_full_text: bool = True, num_return_sequences: int = 1, **kw):
         single = isinstance(text_inputs, str)

@@ -191,7 +191,7 @@ class FasterTransformerModel(Model):
                 "outputs": [{"name": n, "datatype": m[d], "shape": [-1] + json.loads(s.replace(" ", ""))}
                             for n, d, s in FT_OUTPUTS]}
 
-    def infer(self, inputs: dict, request: dict, headers=None) -> dict:
+    def _prepare(self, inputs: dict):
         from ..engine.llm_engine import SamplingParams
         if "input_ids" not in inputs or "request_output_len" not in inputs:
             raise InvalidInput("input_ids and request_output_len are required")
@@ -217,8 +217,6 @@ class FasterTransformerModel(Model):
             stop = stop * B
         lpen = _col(inputs, "len_penalty", B, 1.0, float)
         div = _col(inputs, "beam_search_diversity_rate", B, 0.0, float)
-        if any(b > 1 for b in beam):
-            return self._beam_infer(ids, lens, out_len, end_id, beam, lpen, div, want_lp)
         prompts, params = [], []
         for b in range(B):
             p = ids[b, :lens[b]].tolist()
@@ -230,25 +228,86 @@ class FasterTransformerModel(Model):
                 eos_token_id=end_id[b], stop_sequences=stop[b] if stop else None,
                 bad_words_ids=bad[b] if bad else None, logprobs=True))
             prompts.append(p)
-        reqs = self.generator.generate_ids(prompts, params)
+        meta = dict(ids=ids, B=B, lens=lens, out_len=out_len, end_id=end_id, beam=beam, want_lp=want_lp, lpen=lpen,
+                    div=div)
+        return prompts, params, meta
+
+    @staticmethod
+    def _assemble(views, meta) -> dict:
+        """``views``: per row (prompt, output, logprobs) -> FT output tensors."""
+        B, lens, out_len, end_id = meta["B"], meta["lens"], meta["out_len"], meta["end_id"]
         max_total = max(lens[b] + out_len[b] for b in range(B))
         out_ids = np.full((B, 1, max_total), 0, dtype=np.int32)
         seq_len = np.zeros((B, 1), dtype=np.int32)
         cum = np.zeros((B, 1), dtype=np.float32)
         olp = np.zeros((B, 1, max(out_len)), dtype=np.float32)
-        for b, r in enumerate(reqs):
-            toks = r.prompt + r.output
+        for b, (prompt, output, lps) in enumerate(views):
+            toks = list(prompt) + list(output)
             out_ids[b, 0, :] = end_id[b]
             out_ids[b, 0, :len(toks)] = toks
             seq_len[b, 0] = len(toks)
-            cum[b, 0] = float(np.sum(r.logprobs)) if r.logprobs else 0.0
-            olp[b, 0, :len(r.logprobs)] = r.logprobs
+            cum[b, 0] = float(np.sum(lps)) if lps else 0.0
+            olp[b, 0, :len(lps)] = lps
         out = {"output_ids": out_ids, "sequence_length": seq_len}
-        if want_lp:
+        if meta["want_lp"]:
             out["cum_log_probs"] = cum
             out["output_log_probs"] = olp
         return out
 
+    def infer(self, inputs: dict, request: dict, headers=None) -> dict:
+        prompts, params, meta = self._prepare(inputs)
+        if any(b > 1 for b in meta["beam"]):
+            return self._beam_infer(meta["ids"], meta["lens"], meta["out_len"], meta["end_id"], meta["beam"],
+                                    meta["lpen"], meta["div"], meta["want_lp"])
+        reqs = self.generator.generate_ids(prompts, params)
+        return self._assemble([(r.prompt, r.output, r.logprobs) for r in reqs], meta)
+
+    def infer_stream(self, inputs: dict, request: dict, headers=None):
+        """Decoupled (token-streaming) inference, FT's ``decoupled: True`` mode
+        behind ``ModelStreamInfer``: yields the FT output tensors after every
+        generation step (all rows padded to the same shapes), the last one
+        complete. Beam search answers once."""
+        import queue
+        import threading
+        prompts, params, meta = self._prepare(inputs)
+        if any(b > 1 for b in meta["beam"]):
+            yield self.infer(inputs, request, headers)
+            return
+        q: queue.Queue = queue.Queue()
+        state = [(p, [], []) for p in prompts]
+        lock = threading.Lock()
+
+        def on_token(i, r):
+            with lock:
+                state[i] = (r.prompt, list(r.output), list(r.logprobs))
+                q.put(("tok", [(a, list(b), list(c)) for a, b, c in state]))
+
+        def run():
+            try:
+                reqs = self.generator.generate_ids(prompts, params, on_token=on_token)
+                q.put(("done", [(r.prompt, r.output, r.logprobs) for r in reqs]))
+            except Exception as e:  # noqa: BLE001 -- surfaced to the stream
+                q.put(("error", e))
+        threading.Thread(target=run, daemon=True).start()
+        while True:
+            kind, val = q.get()
+            if kind == "error":
+                raise val
+            if kind == "done":
+                yield self._assemble(val, meta)
+                return
+            while not q.empty():  # coalesce tokens that arrived while the consumer was busy
+                nxt = q.get()
+                if nxt[0] != "tok":
+                    kind, val = nxt
+                    break
+                val = nxt[1]
+            if kind == "error":
+                raise val
+            if kind == "done":
+                yield self._assemble(val, meta)
+                return
+            yield self._assemble(val, meta)
 
     def _beam_infer(self, ids, lens, out_len, end_id, beam, lpen, div, want_lp):
         B, W = ids.shape[0], max(beam)
