@@ -38,8 +38,12 @@ def bytes_to_unicode() -> dict:
 
 
 def load_bpe_tables(path: str):
-    """-> (vocab dict, merges list[(a, b)], special tokens dict)."""
-    tj = os.path.join(path, "tokenizer.json")
+    """-> (vocab dict, merges list[(a, b)], added tokens dict, normalizer name).
+
+    ``path``: a directory with ``tokenizer.json`` (HF fast BPE, e.g. the NeoX
+    ``20B_tokenizer.json`` layout) or ``vocab.json`` + ``merges.txt`` (GPT-2),
+    or a ``tokenizer.json`` file itself."""
+    tj = path if path.endswith(".json") and os.path.isfile(path) else os.path.join(path, "tokenizer.json")
     if os.path.exists(tj):
         with open(tj, encoding="utf-8") as f:
             t = json.load(f)
@@ -48,13 +52,16 @@ def load_bpe_tables(path: str):
             raise ValueError(f"{tj}: model type {m.get('type')} is not BPE")
         merges = [tuple(x.split(" ", 1)) if isinstance(x, str) else tuple(x) for x in m["merges"]]
         specials = {a["content"]: a["id"] for a in t.get("added_tokens", [])}
-        return m["vocab"], merges, specials
+        norm = (t.get("normalizer") or {}).get("type") or ""
+        return m["vocab"], merges, specials, norm
     with open(os.path.join(path, "vocab.json"), encoding="utf-8") as f:
         vocab = json.load(f)
     with open(os.path.join(path, "merges.txt"), encoding="utf-8") as f:
         lines = [ln.rstrip("\n") for ln in f if ln.strip() and not ln.startswith("#version")]
     merges = [tuple(ln.split(" ", 1)) for ln in lines]
-    return vocab, merges, {}
+    # GPT-2's end-of-text token is special (matched whole in text) in every HF tokenizer of it
+    specials = {t: vocab[t] for t in ("<|endoftext|>",) if t in vocab}
+    return vocab, merges, specials, ""
 
 
 class NativeBPE:
@@ -62,13 +69,19 @@ class NativeBPE:
 
     def __init__(self, path: str):
         from ..io import native
-        self.vocab, merges, self.specials = load_bpe_tables(path)
+        self.vocab, merges, self.specials, self.normalizer = load_bpe_tables(path)
+        if self.normalizer not in ("", "NFC", "NFKC", "NFD", "NFKD"):
+            raise ValueError(f"unsupported normalizer {self.normalizer!r}")
+        # added tokens split the text first, leftmost-longest (HF tokenizers' AddedVocabulary)
+        self._split = re.compile("(" + "|".join(re.escape(t) for t in sorted(self.specials, key=len, reverse=True))
+                                 + ")") if self.specials else None
         self.inv = {v: k for k, v in self.vocab.items()}
         for k, v in self.specials.items():
             self.inv.setdefault(v, k)
         b2u = bytes_to_unicode()
         self.u2b = {v: k for k, v in b2u.items()}
-        byte_ids = (ctypes.c_int32 * 256)(*[self.vocab[b2u[b]] for b in range(256)])
+        # bytes that never occur in UTF-8 (0xC0, 0xC1, 0xF5-0xFF) may be absent (NeoX vocab): id -1
+        byte_ids = (ctypes.c_int32 * 256)(*[self.vocab.get(b2u[b], -1) for b in range(256)])
         L, R, M = [], [], []
         for a, b in merges:
             if a in self.vocab and b in self.vocab and (a + b) in self.vocab:
@@ -90,12 +103,28 @@ class NativeBPE:
             return self.specials[tok]
         return self.vocab.get(tok)
 
-    def encode(self, text: str) -> np.ndarray:
+    def _encode_plain(self, text: str) -> np.ndarray:
+        if self.normalizer:
+            import unicodedata
+            text = unicodedata.normalize(self.normalizer, text)
         raw = text.encode("utf-8")
         cap = len(raw) + 16
         buf = (ctypes.c_int32 * cap)()
         n = self._lib.kca_bpe_encode(self._h, raw, len(raw), buf, cap)
         return np.frombuffer(buf, dtype=np.int32, count=n).copy()
+
+    def encode(self, text: str) -> np.ndarray:
+        if self._split is None:
+            return self._encode_plain(text)
+        parts = []
+        for i, seg in enumerate(self._split.split(text)):
+            if not seg:
+                continue
+            if i % 2:  # captured added token
+                parts.append(np.array([self.specials[seg]], dtype=np.int32))
+            else:
+                parts.append(self._encode_plain(seg))
+        return np.concatenate(parts) if parts else np.zeros(0, dtype=np.int32)
 
     def decode(self, ids) -> str:
         out = bytearray()
