@@ -179,6 +179,7 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_kernel(AttnP
   const int hk = h / (p.H / p.Hkv);
   const int off = p.Sk - p.Sq;
   int kv_end = p.Sk;
+  KCA_DASSERT(!p.kv_len || (p.kv_len[b] >= 0 && p.kv_len[b] <= p.Sk));
   if (p.kv_len) kv_end = min(kv_end, p.kv_len[b]);
   const int q0 = qb * BM + wave * BN;
   const int qrow = q0 + l32;
@@ -373,6 +374,7 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_bwd_dkdv_kernel(
   const int grp = p.H / p.Hkv;
   const int off = p.Sk - p.Sq;
   int kv_end = p.Sk;
+  KCA_DASSERT(!p.kv_len || (p.kv_len[b] >= 0 && p.kv_len[b] <= p.Sk));
   if (p.kv_len) kv_end = min(kv_end, p.kv_len[b]);
   const int kw = kb * BK + wave * 16;
   const int key = kw + gi;
@@ -529,6 +531,7 @@ __global__ void __launch_bounds__(256, (D <= 160 ? 2 : 1)) attn_bwd_dq_kernel(At
   const int hk = h / (p.H / p.Hkv);
   const int off = p.Sk - p.Sq;
   int kv_end = p.Sk;
+  KCA_DASSERT(!p.kv_len || (p.kv_len[b] >= 0 && p.kv_len[b] <= p.Sk));
   if (p.kv_len) kv_end = min(kv_end, p.kv_len[b]);
   const int qw = qb * BQ + wave * 16;
   const int q = qw + gi;
@@ -696,6 +699,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv32_kernel(AttnBwdParams p
   const int grp = p.H / p.Hkv;
   const int off = p.Sk - p.Sq;
   int kv_end = p.Sk;
+  KCA_DASSERT(!p.kv_len || (p.kv_len[b] >= 0 && p.kv_len[b] <= p.Sk));
   if (p.kv_len) kv_end = min(kv_end, p.kv_len[b]);
   const int kw = kb * BK + wave * 32;
   const int key = kw + l32;
@@ -845,6 +849,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq32_kernel(AttnBwdParams p) 
   const int hk = h / (p.H / p.Hkv);
   const int off = p.Sk - p.Sq;
   int kv_end = p.Sk;
+  KCA_DASSERT(!p.kv_len || (p.kv_len[b] >= 0 && p.kv_len[b] <= p.Sk));
   if (p.kv_len) kv_end = min(kv_end, p.kv_len[b]);
   const int qw = qb * BQ + wave * 32;
   const int q = qw + l32;

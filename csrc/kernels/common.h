@@ -23,6 +23,24 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
+// Bounds/invariant checks of the debug kernel library (tools/build_ext.py
+// --debug -> libkca_kernels_debug.so, loaded when KCA_DEBUG=1):
+// a violated check prints the site and the offending block/thread and traps,
+// so the fault is reported at the kernel that caused it. Compiled out of the
+// release library.
+#ifdef KCA_DEBUG
+#define KCA_DASSERT(cond)                                                                                  \
+  do {                                                                                                     \
+    if (!(cond)) {                                                                                         \
+      printf("KCA_DASSERT failed %s:%d: %s (block %d,%d,%d thread %d)\n", __FILE__, __LINE__, #cond,         \
+             (int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z, (int)threadIdx.x);                         \
+      __builtin_trap();                                                                                    \
+    }                                                                                                      \
+  } while (0)
+#else
+#define KCA_DASSERT(cond) ((void)0)
+#endif
+
 struct alignas(16) U16x8 { uint16_t v[8]; };
 struct alignas(8) U16x4 { uint16_t v[4]; };
 

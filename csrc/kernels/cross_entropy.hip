@@ -48,6 +48,7 @@ __global__ void __launch_bounds__(256) ce_fwd_kernel(
   if (threadIdx.x == 0) {
     const float lse = gm + __logf(gs);
     const long long lab = labels[row];
+    KCA_DASSERT(lab == ignore_index || (lab >= 0 && lab < V));  // a label outside the vocab is a data bug
     lse_out[row] = lse;
     loss[row] = (lab == ignore_index || lab < 0 || lab >= V)
                     ? 0.f

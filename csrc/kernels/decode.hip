@@ -36,6 +36,7 @@ __global__ __launch_bounds__(256) void decode_prep_kernel(
   const int b = (int)(row / rows_per_b), j = (int)(row % rows_per_b);
   bf16_t* src = qkv + b * ld + (long long)j * D;
   const int p = pos[b];
+  KCA_DASSERT(p >= 0 && (long long)p * cs_pos < cs_head);  // position inside the slot's KV capacity
   float x[4], y[4];
   const int half = rot >> 1;
 #pragma unroll
@@ -143,6 +144,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
   const bool dact = dslot < ND;
   float* sc = smem;                 // [G][chunk]
   float* red = smem + G * p.chunk;  // [4][G][D]
+  KCA_DASSERT(p.slots[b] >= 0);
   const long long kvoff = p.slots[b] * p.cs_slot + hk * p.cs_head + dslot * 8;
   const bf16_t* kb = p.kc + kvoff;
   const bf16_t* vb = p.vc + kvoff;

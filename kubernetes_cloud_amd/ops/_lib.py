@@ -21,7 +21,9 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(os.path.dirname(_HERE), "_lib")
-KERNEL_LIB = os.path.join(LIB_DIR, "libkca_kernels.so")
+# KCA_DEBUG=1: the debug build (KCA_DASSERT bounds/invariant checks in the kernels)
+DEBUG = os.environ.get("KCA_DEBUG", "0") in ("1", "true")
+KERNEL_LIB = os.path.join(LIB_DIR, "libkca_kernels_debug.so" if DEBUG else "libkca_kernels.so")
 
 _lock = threading.Lock()
 _lib = None

@@ -22,7 +22,13 @@ wedges one process keeps the pod "Running" until the job deadline.
 
 Configuration from the environment (so manifests can set it without new CLI
 flags): ``KCA_WATCHDOG_TIMEOUT`` seconds (0/unset = off), ``KCA_WATCHDOG_ABORT``
-(default 1), ``KCA_WATCHDOG_DIR``.
+(default 1), ``KCA_WATCHDOG_DIR``, ``KCA_WATCHDOG_FACTOR`` (default 0 = off).
+
+Adaptive deadline: with ``factor > 0`` the deadline is ``max(timeout_s, factor
+x the slowest step seen so far)``, so a loaded node or a long first step
+(graph capture, tuning, checkpoint write) never trips it while a step that
+takes ``factor`` times longer than any before does; until the first beat the
+deadline is ``max(timeout_s, startup_s)`` (``KCA_WATCHDOG_STARTUP``).
 """
 from __future__ import annotations
 
@@ -44,8 +50,13 @@ def enable_rccl_async_errors() -> None:
 
 class StepWatchdog:
     def __init__(self, timeout_s: float, rank: int = 0, report_dir: str | None = None,
-                 abort: bool = True, poll_s: float | None = None, on_timeout=None):
+                 abort: bool = True, poll_s: float | None = None, on_timeout=None, factor: float = 0.0,
+                 startup_s: float = 0.0):
         self.timeout_s = float(timeout_s)
+        self.factor = float(factor)
+        self.startup_s = float(startup_s)
+        self._max_step_s = 0.0
+        self._beats = 0
         self.rank = rank
         self.report_dir = report_dir or tempfile.gettempdir()
         self.abort = abort
@@ -63,7 +74,9 @@ class StepWatchdog:
         if t <= 0:
             return None
         abort = os.environ.get("KCA_WATCHDOG_ABORT", "1") not in ("0", "false", "no")
-        return cls(t, rank=rank, report_dir=os.environ.get("KCA_WATCHDOG_DIR", report_dir), abort=abort)
+        return cls(t, rank=rank, report_dir=os.environ.get("KCA_WATCHDOG_DIR", report_dir), abort=abort,
+                   factor=float(os.environ.get("KCA_WATCHDOG_FACTOR", "0") or 0),
+                   startup_s=float(os.environ.get("KCA_WATCHDOG_STARTUP", "0") or 0))
 
     def start(self) -> "StepWatchdog":
         enable_rccl_async_errors()
@@ -73,9 +86,22 @@ class StepWatchdog:
         return self
 
     def beat(self, step: int | None = None) -> None:
-        self._last = time.monotonic()
+        now = time.monotonic()
+        if self._beats:  # the first interval includes startup work: not a step time
+            self._max_step_s = max(self._max_step_s, now - self._last)
+        self._beats += 1
+        self._last = now
         if step is not None:
             self._step = step
+
+    @property
+    def deadline_s(self) -> float:
+        """Current allowed age of the last beat."""
+        if self._beats == 0:
+            return max(self.timeout_s, self.startup_s)
+        if self.factor > 0 and self._beats >= 2:
+            return max(self.timeout_s, self.factor * self._max_step_s)
+        return max(self.timeout_s, self.startup_s) if self.factor > 0 else self.timeout_s
 
     def stop(self) -> None:
         self._stop.set()
@@ -105,7 +131,8 @@ class StepWatchdog:
         path = os.path.join(self.report_dir, f"watchdog-rank{self.rank}.json")
         rec = {"rank": self.rank, "host": socket.gethostname(), "pid": os.getpid(),
                "last_step": self._step, "seconds_since_beat": round(age, 3),
-               "timeout_s": self.timeout_s, "time": time.time(), "stacks": self._stacks()}
+               "timeout_s": self.timeout_s, "deadline_s": round(self.deadline_s, 3),
+               "max_step_s": round(self._max_step_s, 3), "time": time.time(), "stacks": self._stacks()}
         with open(path, "w") as f:
             json.dump(rec, f, indent=1)
         return path
@@ -113,11 +140,12 @@ class StepWatchdog:
     def _run(self):
         while not self._stop.wait(self.poll_s):
             age = time.monotonic() - self._last
-            if age <= self.timeout_s:
+            limit = self.deadline_s
+            if age <= limit:
                 continue
             self.fired = True
             path = self.report(age)
-            print(f"[watchdog] rank {self.rank}: no step for {age:.1f}s (> {self.timeout_s}s) after step "
+            print(f"[watchdog] rank {self.rank}: no step for {age:.1f}s (> {limit:.1f}s) after step "
                   f"{self._step}; report {path}", file=sys.stderr, flush=True)
             if self.on_timeout is not None:
                 self.on_timeout(self)

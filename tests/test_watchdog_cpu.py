@@ -56,3 +56,23 @@ def test_trace_ranges_are_safe_without_a_profiler():
     with trace_range("outer"):
         with trace_range("inner"):
             mark("point")
+
+
+def test_watchdog_adaptive_deadline(tmp_path):
+    """factor x slowest step (after 2 beats); startup grace before the first beat."""
+    import time as _t
+    wd = StepWatchdog(0.1, report_dir=str(tmp_path), abort=False, poll_s=0.02, factor=4, startup_s=5)
+    assert wd.deadline_s == 5  # no beat yet: startup grace
+    wd.start()
+    _t.sleep(0.3)  # a slow first step (startup) does not trip it
+    assert not wd.fired
+    wd.beat(1)
+    _t.sleep(0.15)
+    wd.beat(2)  # slowest step so far: 0.15 s -> deadline 0.6 s
+    assert 0.55 < wd.deadline_s < 0.8
+    _t.sleep(0.4)
+    assert not wd.fired
+    wd.beat(3)  # slowest step now ~0.4 s -> deadline ~1.6 s
+    _t.sleep(2.5)  # a step 4x+ longer than any before -> fires
+    assert wd.fired
+    wd.stop()

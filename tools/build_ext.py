@@ -69,15 +69,18 @@ def _sources(sub, exts):
     return sorted(os.path.join(d, f) for f in os.listdir(d) if f.endswith(exts))
 
 
-def build_kernels(jobs: int = 8, verbose: bool = False) -> str:
+def build_kernels(jobs: int = 8, verbose: bool = False, debug: bool = False) -> str:
+    """``debug``: libkca_kernels_debug.so with the KCA_DASSERT bounds checks
+    compiled in (csrc/kernels/common.h), loaded by ops/_lib.py when KCA_DEBUG=1."""
     srcs = _sources("kernels", (".hip",)) + _sources("comm", (".hip",))
     hdrs = _sources("kernels", (".h",)) + _sources("comm", (".h",))
-    obj_dir = os.path.join(BUILD, "kernels")
+    obj_dir = os.path.join(BUILD, "kernels_debug" if debug else "kernels")
     os.makedirs(obj_dir, exist_ok=True)
     os.makedirs(OUT_DIR, exist_ok=True)
+    flags = HIP_FLAGS + (["-DKCA_DEBUG", "-g"] if debug else [])
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        objs = list(ex.map(lambda s: _compile([HIPCC], s, hdrs, obj_dir, HIP_FLAGS), srcs))
-    out = os.path.join(OUT_DIR, "libkca_kernels.so")
+        objs = list(ex.map(lambda s: _compile([HIPCC], s, hdrs, obj_dir, flags), srcs))
+    out = os.path.join(OUT_DIR, "libkca_kernels_debug.so" if debug else "libkca_kernels.so")
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp"] + objs
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
@@ -116,15 +119,50 @@ def build_host(jobs: int = 8, verbose: bool = False) -> str | None:
     return out
 
 
+SANITIZE_FLAGS = ["-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-fno-omit-frame-pointer", "-g", "-O1",
+                  "-std=c++17", "-fopenmp", "-Wall", "-Wno-unused-function"]
+
+
+def build_sanitize(verbose: bool = False) -> str:
+    """ASan + UBSan executable of the host runtime (csrc/{cpu,io,tokenize}) and
+    its harness csrc/tests/host_sanitize_main.cpp: the code that
+    parses untrusted files / network bytes, instrumented as a standalone binary
+    so no sanitizer runtime has to be preloaded into Python."""
+    srcs = []
+    for sub in ("cpu", "io", "tokenize", "tests"):
+        srcs += _sources(sub, (".cpp",))
+    out_dir = os.path.join(BUILD, "sanitize")
+    os.makedirs(out_dir, exist_ok=True)
+    out = os.path.join(out_dir, "kca_host_sanitize")
+    cxx = shutil.which("g++") or "g++"
+    cmd = [cxx] + SANITIZE_FLAGS + [f"-I{ROCM}/include", "-D__HIP_PLATFORM_AMD__", "-o", out] + srcs + [
+        f"-L{ROCM}/lib", f"-Wl,-rpath,{ROCM}/lib", "-lamdhip64", "-lssl", "-lcrypto", "-lpthread"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"sanitize build failed: {' '.join(cmd)}\n{r.stderr}")
+    if verbose:
+        print(f"built {out}")
+    return out
+
+
 def build_all(jobs: int = 8, verbose: bool = False):
-    return build_kernels(jobs, verbose), build_host(jobs, verbose)
+    return build_kernels(jobs, verbose), build_host(jobs, verbose), build_kernels(jobs, verbose, debug=True)
 
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 1))
     ap.add_argument("--kernels-only", action="store_true")
+    ap.add_argument("--debug", action="store_true", help="only the KCA_DASSERT debug kernel library")
+    ap.add_argument("--sanitize", action="store_true", help="build + run the ASan/UBSan host harness")
     a = ap.parse_args()
+    if a.sanitize:
+        exe = build_sanitize(True)
+        sys.exit(subprocess.run([exe], env=dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1",
+                                                UBSAN_OPTIONS="print_stacktrace=1")).returncode)
+    if a.debug:
+        build_kernels(a.jobs, True, debug=True)
+        sys.exit(0)
     if a.kernels_only:
         build_kernels(a.jobs, True)
     else:
