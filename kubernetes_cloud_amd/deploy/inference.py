@@ -73,7 +73,19 @@ HF_TOKEN_ENV = [{"name": "HUGGING_FACE_HUB_TOKEN", "valueFrom": {"secretKeyRef":
 
 def stable_diffusion() -> dict:
     model = "runwayml/stable-diffusion-v1-5"
+    s3 = lambda n, k: {"apiVersion": "v1", "kind": "Secret", "type": "Opaque", "metadata": {"name": n},  # noqa: E731
+                       "data": {k: "<base64-encoded-value>"}}
+    upload = _job("stable-diffusion-uploader", ["python3", "-m", "kubernetes_cloud_amd.io.s3_upload"],
+                  ["--src", f"/mnt/models/{model}", "--dest", "s3://<BUCKET>/", "--acl-public"],
+                  "stable-diffusion-models", cpu=1, memory="2Gi",
+                  env=[{"name": "AWS_KEY", "valueFrom": {"secretKeyRef": {"name": "s3-access-key", "key": "access_key"}}},
+                       {"name": "AWS_SECRET", "valueFrom": {"secretKeyRef": {"name": "s3-secret-key",
+                                                                              "key": "secret_key"}}},
+                       {"name": "AWS_HOST", "valueFrom": {"secretKeyRef": {"name": "s3-host-url", "key": "url"}}}])
     return {
+        "01-optional-s3-secret.yaml": [s3("s3-access-key", "access_key"), s3("s3-secret-key", "secret_key"),
+                                       s3("s3-host-url", "url")],
+        "03-optional-s3-upload-job.yaml": upload,
         "00-model-pvc.yaml": pvc("stable-diffusion-models", "100Gi"),
         "02-model-download-job.yaml": _job(
             "stable-diffusion-download", ["python3", "-m", "kubernetes_cloud_amd.data.downloader"],
@@ -119,6 +131,28 @@ def bloom_176b() -> dict:
     }
 
 
+def bloom_176b_deepspeed() -> dict:
+    """online-inference/bloom-176b-deepspeed (S5): the pre-sharded
+    microsoft/bloom-deepspeed-inference-fp16 checkpoint downloaded into the HF
+    hub cache on a PVC (01-download-job.yaml: download.py --model-id --revision,
+    HF_HOME=/mnt/models), served TP=8 on one MI355X node on port 5000 with the
+    bloom-inference-server routes (02-inference-service.yaml:22-45)."""
+    repo = "microsoft/bloom-deepspeed-inference-fp16"
+    name = "microsoft-bloom-deepspeed-inference-fp16"
+    dl = _job(f"{name}-download", ["python3", "-m", "kubernetes_cloud_amd.data.hf_snapshot"],
+              [f"--model-id={repo}", "--revision=main"], name, mount="/mnt/models",
+              env=[{"name": "HF_HOME", "value": "/mnt/models"}] + HF_TOKEN_ENV, cpu=4, memory="16Gi")
+    c = _container(["torchrun", "--standalone", "--nproc-per-node", "8", "-m",
+                    "kubernetes_cloud_amd.serving.tp_server"], ["--model-name", repo, "--port", "5000"],
+                   env=[{"name": "STORAGE_URI", "value": f"pvc://{name}/"}, {"name": "HF_HOME", "value": "/mnt/models"},
+                        {"name": "MODEL_NAME", "value": repo}],
+                   gpus=8, cpu=96, memory="512Gi", port=5000)
+    c["volumeMounts"] = [{"name": "dshm", "mountPath": "/dev/shm"}]
+    isvc = _isvc(name, [c], min_replicas=1, concurrency=1)
+    isvc["spec"]["predictor"]["volumes"] = [{"name": "dshm", "emptyDir": {"medium": "Memory"}}]
+    return {"00-pvc.yaml": pvc(name, "400Gi"), "01-download-job.yaml": dl, "02-inference-service.yaml": isvc}
+
+
 def fastertransformer() -> dict:
     out = {"model-storage-pvc.yml": pvc("ft-model-storage", "200Gi")}
     for name, model, store in (("gptj", "EleutherAI/gpt-j-6B", "gptj-store"),
@@ -162,16 +196,83 @@ def tensorizer_isvc() -> dict:
 
 
 def gpt2() -> dict:
-    pred = _container(["python3", "-c", "from kubernetes_cloud_amd.serving.predictors import gpt2_predictor_main; "
-                                        "gpt2_predictor_main()"],
-                      env=[{"name": "MODEL_PATH", "value": "/mnt/pvc/gpt2"},
-                           {"name": "STORAGE_URI", "value": "pvc://model-storage/"}], cpu=4, memory="16Gi")
-    tr = {"containers": [{"name": "kserve-container", "image": image(),
-                          "command": ["python3", "-c", "from kubernetes_cloud_amd.serving.predictors import "
-                                                       "gpt2_transformer_main; gpt2_transformer_main()"],
-                          "args": ["--model_name", "gpt-2"], "env": [{"name": "TOKENIZER_PATH",
-                                                                       "value": "/mnt/pvc/gpt2"}]}]}
-    return {"gpt-pvc-inferenceservice.yaml": _isvc("gpt-2", [pred], transformer=tr, concurrency=4)}
+    """online-inference/gpt-2: PVC-backed ISVC (124M and the 1558M "huge" model,
+    service-pvc/*.yaml) and the S3-backed one with its credentials secret and
+    service account (service-s3/*.yaml: KServe's storage initializer pulls
+    storageUri with the SA's secret; target concurrency 4), each predictor +
+    BPE transformer."""
+    def pair(name, model_path, storage_uri, sa=None, concurrency=4, max_replicas=2, transformer_par=None):
+        pred = _container(["python3", "-c", "from kubernetes_cloud_amd.serving.predictors import "
+                                            "gpt2_predictor_main; gpt2_predictor_main()"],
+                          env=[{"name": "MODEL_PATH", "value": model_path},
+                               {"name": "STORAGE_URI", "value": storage_uri}], cpu=4, memory="16Gi")
+        tr = {"containers": [{"name": "kserve-container", "image": image(),
+                              "command": ["python3", "-c", "from kubernetes_cloud_amd.serving.predictors import "
+                                                           "gpt2_transformer_main; gpt2_transformer_main()"],
+                              "args": ["--model_name", name], "env": [{"name": "TOKENIZER_PATH",
+                                                                       "value": model_path}]}],
+              "minReplicas": 0, "maxReplicas": transformer_par or 1}
+        isvc = _isvc(name, [pred], transformer=tr, concurrency=concurrency, max_replicas=max_replicas,
+                     annotations={"autoscaling.knative.dev/target": str(concurrency)})
+        if sa:
+            isvc["spec"]["predictor"]["serviceAccountName"] = sa
+        return isvc
+    s3_secret = {"apiVersion": "v1", "kind": "Secret", "type": "Opaque",
+                 "metadata": {"name": "s3-secret", "annotations": {"serving.kserve.io/s3-endpoint": "object.ord1.coreweave.com",
+                                                                   "serving.kserve.io/s3-usehttps": "1"}},
+                 "data": {"AWS_ACCESS_KEY_ID": "<base64-encoded-value>",
+                          "AWS_SECRET_ACCESS_KEY": "<base64-encoded-value>"}}
+    sa = {"apiVersion": "v1", "kind": "ServiceAccount", "metadata": {"name": "s3-sa"},
+          "secrets": [{"name": "s3-secret"}]}
+    return {
+        "gpt-pvc-inferenceservice.yaml": pair("gpt-2", "/mnt/pvc/gpt2", "pvc://model-storage/"),
+        "service-pvc/gpt-pvc-huge-model-inferenceservice.yaml": pair(
+            "gpt-pvc-huge", "/mnt/models", "pvc://model-storage/1558M/", max_replicas=20, transformer_par=2),
+        "service-s3/s3-secret.yaml": s3_secret,
+        "service-s3/s3-serviceaccount.yaml": sa,
+        "service-s3/gpt-s3-inferenceservice.yaml": pair("gpt-s3", "/mnt/models", "s3://coreweave/gpt-2/124M/",
+                                                        sa="s3-sa"),
+    }
+
+
+def image_classifier() -> dict:
+    """online-inference/image-classifier (S11): classifier ISVC + b64/url transformer
+    (service/classifier-inferenceservice.yaml:1-47), PyTorch model on the PVC."""
+    pred = _container(["python3", "-c", "from kubernetes_cloud_amd.serving.predictors import "
+                                        "image_classifier_main; image_classifier_main()"],
+                      env=[{"name": "MODEL_PATH", "value": "/mnt/models/resnet50_imagenet.pt"},
+                           {"name": "MODEL_NAME", "value": "image-classifier"},
+                           {"name": "STORAGE_URI", "value": "pvc://model-storage/classifier/"}], cpu=4, memory="8Gi")
+    return {"service/classifier-inferenceservice.yaml": _isvc("image-classifier", [pred], max_replicas=4,
+                                                              concurrency=8),
+            "model-storage-pvc.yaml": pvc("model-storage", "20Gi")}
+
+
+def custom_sentiment() -> dict:
+    """online-inference/custom-sentiment (S14): PVC-loaded custom predictor
+    (sentiment-inferenceservice.yaml), a sleep Deployment that mounts the PVC
+    for copying the model in (sleep-deployment.yaml), and the image-pull
+    secret patch of the default service account."""
+    c = _container(["python3", "/app/model.py"], env=[{"name": "STORAGE_URI", "value": "pvc://model-storage/sentiment"}],
+                   cpu=3, memory="8Gi")
+    isvc = _isvc("sentiment", [c], max_replicas=10, concurrency=1)
+    isvc["metadata"]["labels"] = {"qos.coreweave.cloud/latency": "low"}
+    sleep = {"apiVersion": "apps/v1", "kind": "Deployment", "metadata": {"name": "sleep"},
+             "spec": {"replicas": 1, "revisionHistoryLimit": 1, "strategy": {"type": "Recreate"},
+                      "selector": {"matchLabels": {"app.kubernetes.io/name": "sleep"}},
+                      "template": {"metadata": {"labels": {"app.kubernetes.io/name": "sleep"}},
+                                   "spec": {"containers": [{
+                                       "name": "sleep", "image": image(), "command": ["sleep"], "args": ["86400d"],
+                                       "imagePullPolicy": "IfNotPresent",
+                                       "resources": {"requests": {"cpu": "50m", "memory": "10Mi"},
+                                                     "limits": {"cpu": 1, "memory": "128Mi"}},
+                                       "volumeMounts": [{"name": "model-storage", "mountPath": "/models"}]}],
+                                       "volumes": [{"name": "model-storage",
+                                                    "persistentVolumeClaim": {"claimName": "model-storage"}}]}}}}
+    patch = {"apiVersion": "v1", "kind": "ServiceAccount", "imagePullSecrets": [{"name": "docker-hub"}]}
+    return {"sentiment-inferenceservice.yaml": isvc, "sleep-deployment.yaml": sleep,
+            "model-storage-pvc.yaml": pvc("model-storage", "20Gi"),
+            "image-secrets-serviceaccount.patch.yaml": patch}
 
 
 def aitextgen() -> dict:
@@ -209,5 +310,5 @@ def custom_predictor() -> dict:
         "model-storage-pvc.yaml": pvc("model-storage", "20Gi")}
 
 
-__all__ = ["stable_diffusion", "bloom_176b", "fastertransformer", "tensorizer_isvc", "gpt2", "aitextgen",
-           "custom_predictor", "GPU_CLASS_LABEL"]
+__all__ = ["stable_diffusion", "bloom_176b", "bloom_176b_deepspeed", "fastertransformer", "tensorizer_isvc", "gpt2",
+           "image_classifier", "custom_sentiment", "aitextgen", "custom_predictor", "GPU_CLASS_LABEL"]

@@ -335,3 +335,11 @@ class ImageClassifier(Model):
         lab = self.labels
         return {"predictions": [{"class": lab[int(i)] if lab and int(i) < len(lab) else f"class_{int(i)}",
                                  "score": float(s)} for s, i in zip(sc, ix)]}
+
+
+def image_classifier_main(argv=None):
+    """ISVC entrypoint of online-inference/image-classifier (deploy: image-classifier)."""
+    from .server import ModelServer
+    m = ImageClassifier(os.getenv("MODEL_NAME", "image-classifier"))
+    m.load()
+    ModelServer(argv=argv).start([m])

@@ -4,7 +4,10 @@
         --model-path /mnt/pvc/bloom [--port 8080] [--random-init bloom-176b]
 
 Every rank loads only its TP shard (``parallel.tensor_parallel.load_tp_model``,
-one tensor at a time from the safetensors checkpoint) into its own GPU; rank 0
+one tensor at a time from the safetensors checkpoint, or
+``parallel.ds_inference_ckpt`` for a pre-sharded DeepSpeed-Inference
+checkpoint such as microsoft/bloom-deepspeed-inference-fp16 resolved from the
+HF cache with ``--model-name``) into its own GPU; rank 0
 runs the KServe V1 server with the BLOOM predictor contract (bloom.py env
 options and request format, ``.ready.txt`` gate) and the continuous-batching
 engine; ranks 1..N-1 mirror its runner calls (``engine.tp_driver``). The
@@ -35,7 +38,13 @@ def build_tp_engine_model(args, rank, world, group):
             cfg.n_layers = args.layers
         return load_tp_model(cfg, rank, world, group, device=dev, dtype=dtype, random_init=True), None
     from ..io.hf import load_tokenizer
-    model = load_tp_model(args.model_path, rank, world, group, device=dev, dtype=dtype)
+    from ..parallel.ds_inference_ckpt import is_ds_inference_dir, load_ds_inference_tp
+    if is_ds_inference_dir(args.model_path):
+        # pre-sharded DeepSpeed-Inference checkpoint (microsoft/bloom-deepspeed-inference-fp16):
+        # each rank reads only the tp_{rank}_* files it needs, re-sharded to this world size
+        model = load_ds_inference_tp(args.model_path, rank, world, group, device=dev, dtype=dtype)
+    else:
+        model = load_tp_model(args.model_path, rank, world, group, device=dev, dtype=dtype)
     return model, load_tokenizer(args.model_path)
 
 

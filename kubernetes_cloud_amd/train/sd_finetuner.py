@@ -158,18 +158,25 @@ def main(argv=None):
     pred_type = noise_sched.prediction_type
 
     def gen_class_images(n: int):
-        if not info.is_main:
-            barrier()
-            return
+        """Prior-preservation class images, data-parallel (PAR-13): prompt batch j
+        runs on rank j % world (the sharding ``accelerator.prepare(sample_dataloader)``
+        gives the reference, sd-finetuner/finetuner.py:612-625); each batch is
+        seeded by its first index, so the images do not depend on the world
+        size. Files are ``{index}-{sha1(image)}.jpg`` as in the reference."""
+        import hashlib
         ds = PromptDataset(args.class_prompt, n)
         os.makedirs(args.class_dataset, exist_ok=True)
         bs = max(1, args.batch_size)
-        for i in range(0, n, bs):
-            items = [ds[j] for j in range(i, min(n, i + bs))]
+        for j, i in enumerate(range(0, n, bs)):
+            if j % world != rank:
+                continue
+            items = [ds[k] for k in range(i, min(n, i + bs))]
             imgs = pipe([it["prompt"] for it in items], height=args.resolution, width=args.resolution,
+                        num_inference_steps=int(os.environ.get("KCA_CLASS_IMAGE_STEPS", "50")),
                         generator=torch.Generator(device=dev).manual_seed(args.seed + i))
             for it, im in zip(items, imgs):
-                im.save(os.path.join(args.class_dataset, f"{it['index']}-{args.seed}.jpg"))
+                h = hashlib.sha1(im.tobytes()).hexdigest()
+                im.save(os.path.join(args.class_dataset, f"{it['index']}-{h}.jpg"))
         barrier()
 
     tf = dict(size=args.resolution, center_crop=args.center_crop, interpolation=args.resize_interp)

@@ -175,3 +175,30 @@ def test_engine_keeps_channels_last_conv_weights():
     assert b[0].weight.data_ptr() >= 0 and not b[0].weight.is_contiguous()
     for pa, pb in zip(a.parameters(), b.parameters()):
         assert torch.allclose(pa, pb, atol=1e-6)
+
+
+def test_dreambooth_class_images_sharded_across_ranks(tmp_path):
+    """PAR-13: two ranks split the class-prompt batches (rank = batch % world) and
+    produce exactly the images a single process produces (same per-batch seeds;
+    file names carry the image hash, as in the reference)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    d = make_sd_dir(str(tmp_path / "sd"))
+    inst = make_images(str(tmp_path / "inst"), 2, captions=False)
+
+    def run(n_proc, cls_dir):
+        argv = ["--model", d, "--run_name", "db", "--instance_dataset", inst, "--instance_prompt", "a sks fox",
+                "--class_dataset", cls_dir, "--class_prompt", "a fox", "--num_class_images", "3",
+                "--resolution", "32", "--batch_size", "1", "--epochs", "1", "--output_path",
+                str(tmp_path / f"o{n_proc}"), "--image_log_steps", "0"]
+        env = dict(os.environ, PYTHONPATH=root, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="",
+                   KCA_CLASS_IMAGE_STEPS="3", OMP_NUM_THREADS="2")
+        cmd = [sys.executable, "-m", "kubernetes_cloud_amd.launch", "--num_processes", str(n_proc), "--no_local_rank",
+               "-m", "kubernetes_cloud_amd.train.sd_finetuner"] + argv
+        r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-3000:]
+        return sorted(f for f in os.listdir(cls_dir) if f.endswith(".jpg"))
+    two = run(2, str(tmp_path / "cls2"))
+    one = run(1, str(tmp_path / "cls1"))
+    assert len(two) == 3 and two == one
