@@ -30,6 +30,22 @@ import torch
 _CKPT = re.compile(r"^checkpoint-(\d+)$")
 
 
+def checkpoint_complete(path: str) -> bool:
+    """A checkpoint dir is complete when it carries no ``.incomplete`` marker,
+    or when every rank named in the marker has written its ``.done-rank{r}``
+    (the async writers finished even if the process died before the next
+    save / the final barrier removed the marker)."""
+    inc = os.path.join(path, ".incomplete")
+    if not os.path.exists(inc):
+        return True
+    try:
+        with open(inc) as f:
+            world = int(f.read().strip() or "0")
+    except (OSError, ValueError):
+        return False
+    return world > 0 and all(os.path.exists(os.path.join(path, f".done-rank{r}")) for r in range(world))
+
+
 def find_last_checkpoint(output_dir: str) -> str | None:
     try:
         names = os.listdir(output_dir)
@@ -38,8 +54,7 @@ def find_last_checkpoint(output_dir: str) -> str | None:
     best = None
     for n in names:
         m = _CKPT.match(n)
-        if m and os.path.isdir(os.path.join(output_dir, n)) and \
-                not os.path.exists(os.path.join(output_dir, n, ".incomplete")):
+        if m and os.path.isdir(os.path.join(output_dir, n)) and checkpoint_complete(os.path.join(output_dir, n)):
             step = int(m.group(1))
             if best is None or step > best[0]:
                 best = (step, n)
@@ -174,15 +189,23 @@ class AsyncCheckpointWriter:
         rng = _rng_state()
         state = copy.deepcopy(trainer_state)
         os.makedirs(os.path.join(ckpt_dir, "optimizer"), exist_ok=True)
-        if rank == 0:
-            open(os.path.join(ckpt_dir, ".incomplete"), "w").close()  # resume skips it until all ranks wrote
-            if tokenizer is not None:
-                tokenizer.save_pretrained(ckpt_dir)
+        # every rank marks the dir incomplete before its writer starts (resume skips it until all
+        # ranks' .done-rank markers exist or the post-save barrier removed the marker)
+        with open(os.path.join(ckpt_dir, ".incomplete"), "w") as f:
+            f.write(str(world))
+        if rank == 0 and tokenizer is not None:
+            tokenizer.save_pretrained(ckpt_dir)
+        try:  # a re-save of the same step starts from no done markers
+            os.remove(os.path.join(ckpt_dir, f".done-rank{rank}"))
+        except FileNotFoundError:
+            pass
         self._pending = ckpt_dir
 
         def write():
             try:
                 _write_checkpoint(ckpt_dir, model.cfg, params, opt, state, args_dict, rng, rank)
+                with open(os.path.join(ckpt_dir, f".done-rank{rank}"), "w") as f:
+                    f.write("ok")
             except Exception as e:  # noqa: BLE001 -- surfaced on the next wait()/save()
                 self._err = e
         self._thread = threading.Thread(target=write, name="ckpt-writer", daemon=False)

@@ -261,7 +261,7 @@ class StableDiffusionPipeline:
         if latents is None:
             latents = torch.randn(shape, generator=generator, device=generator.device if generator else dev,
                                   dtype=torch.float32).to(dev)
-        x = latents.float() * sch.init_noise_sigma
+        x = latents.to(dev).float() * sch.init_noise_sigma
         run = self._runner()
         for t in sch.timesteps:
             xin = torch.cat([x, x]) if cfg else x

@@ -236,3 +236,19 @@ def test_finetuner_optimizer_offload_matches_hbm(tmp_path, monkeypatch):
         finals.append(load_file(str(out / "results-o" / "final" / "model.safetensors")))
     a, b = finals
     assert max(float((a[k].float() - b[k].float()).abs().max()) for k in a) < 1e-5
+
+
+def test_checkpoint_complete_markers(tmp_path):
+    """A process that dies right after an async save (before the next save's
+    barrier removes `.incomplete`) still leaves a resumable checkpoint once every
+    rank's writer wrote its done marker; a missing rank marker keeps it skipped."""
+    from kubernetes_cloud_amd.io.checkpoint import checkpoint_complete, find_last_checkpoint
+    for step, done in ((2, (0, 1)), (4, (0,))):
+        d = tmp_path / f"checkpoint-{step}"
+        d.mkdir()
+        (d / ".incomplete").write_text("2")
+        for r in done:
+            (d / f".done-rank{r}").write_text("ok")
+    assert checkpoint_complete(str(tmp_path / "checkpoint-2"))
+    assert not checkpoint_complete(str(tmp_path / "checkpoint-4"))
+    assert find_last_checkpoint(str(tmp_path)).endswith("checkpoint-2")
