@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--new-tokens", type=int, default=64)
     ap.add_argument("--layers", type=int, default=0, help="override layer count (smoke runs only)")
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--page-size", type=int, default=None, help="KV page size (0 = contiguous slots)")
     ap.add_argument("--decode-only", type=int, default=0,
                     help="profile mode: prefill B prompts once, then time N pure decode steps")
     args = ap.parse_args()
@@ -42,7 +43,7 @@ def main():
     m = build_model(cfg, device=dev, dtype=torch.bfloat16, seed=0)
     batches = [int(b) for b in args.batches.split(",")]
     eng = LLMEngine(m, max_slots=max(batches), max_len=args.prompt_len + args.new_tokens + 8,
-                    use_graphs=not args.no_graphs)
+                    use_graphs=not args.no_graphs, page_size=args.page_size)
     g = torch.Generator().manual_seed(0)
     if args.decode_only:
         B = batches[0]
@@ -58,7 +59,8 @@ def main():
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / args.decode_only
         print(json.dumps({"metric": f"{args.model} decode-only", "batch": B, "decode_ms_per_step": round(dt * 1e3, 3),
-                          "decode_tokens_per_s": round(B / dt, 1)}), flush=True)
+                          "decode_tokens_per_s": round(B / dt, 1), "page_size": eng.runner.cache.page_size}),
+              flush=True)
         return
     for B in batches:
         prompts = [torch.randint(0, cfg.vocab_size, (args.prompt_len,), generator=g).tolist() for _ in range(B)]
@@ -70,6 +72,7 @@ def main():
         for p in prompts:
             eng.runner.prefill(torch.tensor([p]), [0])
         torch.cuda.synchronize()
+        eng.runner.release(0)
         prefill_ms = (time.perf_counter() - t0) / B * 1e3
         reqs = [eng.add_request(p, sp) for p in prompts]
         eng.step()  # admit + first decode
@@ -85,6 +88,7 @@ def main():
                           "decode_ms_per_step": round(dt / max(nsteps, 1) * 1e3, 3),
                           "decode_tokens_per_s": round(gen / dt, 1), "graphs": not args.no_graphs,
                           "kv_cache_gib": round(eng.runner.cache.nbytes() / 2**30, 2),
+                          "page_size": eng.runner.cache.page_size,
                           "layers": cfg.n_layers}), flush=True)
 
 

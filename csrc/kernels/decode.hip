@@ -18,7 +18,20 @@
 // KV cache layout is head-major per slot: [slot][kv_head][pos][D] (strides
 // passed in), so a (sequence, head) chunk of the cache is one contiguous
 // stream of chunk*D*2 bytes -- decode is HBM-bound and reads exactly K+V once.
+// Paged mode (tbl != nullptr): the cache is a pool of pages
+// [page][kv_head][ps][D] (ps = 1 << ps_shift tokens) and token t of sequence
+// `seq` lives in page tbl[seq * tbl_stride + (t >> ps_shift)] -- requests hold
+// only the pages they use, and beams share their prefix pages.
 #include "common.h"
+
+// element offset of token t of sequence `seq` (paged or contiguous)
+__device__ __forceinline__ long long kv_row(const int* __restrict__ tbl, int tbl_stride, int ps_shift, int seq,
+                                            int t, long long cs_slot, long long cs_pos) {
+  if (!tbl) return (long long)seq * cs_slot + (long long)t * cs_pos;
+  const int page = tbl[(long long)seq * tbl_stride + (t >> ps_shift)];
+  KCA_DASSERT(page >= 0);
+  return (long long)page * cs_slot + (long long)(t & ((1 << ps_shift) - 1)) * cs_pos;
+}
 
 // ------------------------------------------------------------------ prep
 // One wave per (b, head-row) of the fused QKV GEMM output [B, (H+2Hkv)*D];
@@ -28,7 +41,8 @@ __global__ __launch_bounds__(256) void decode_prep_kernel(
     bf16_t* __restrict__ qkv, long long ld, int B, int H, int Hkv, int D, int rot,
     int interleaved, const float* __restrict__ cos_t, const float* __restrict__ sin_t,
     const int* __restrict__ pos, const int* __restrict__ slots, bf16_t* __restrict__ kc,
-    bf16_t* __restrict__ vc, long long cs_slot, long long cs_head, long long cs_pos) {
+    bf16_t* __restrict__ vc, long long cs_slot, long long cs_head, long long cs_pos, const int* __restrict__ tbl,
+    int tbl_stride, int ps_shift) {
   const int rows_per_b = H + 2 * Hkv;
   const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= (long long)B * rows_per_b) return;
@@ -36,7 +50,7 @@ __global__ __launch_bounds__(256) void decode_prep_kernel(
   const int b = (int)(row / rows_per_b), j = (int)(row % rows_per_b);
   bf16_t* src = qkv + b * ld + (long long)j * D;
   const int p = pos[b];
-  KCA_DASSERT(p >= 0 && (long long)p * cs_pos < cs_head);  // position inside the slot's KV capacity
+  KCA_DASSERT(p >= 0 && (tbl || (long long)p * cs_pos < cs_head));  // position inside the slot's KV capacity
   float x[4], y[4];
   const int half = rot >> 1;
 #pragma unroll
@@ -77,7 +91,7 @@ __global__ __launch_bounds__(256) void decode_prep_kernel(
   }
   const bool is_k = j < H + Hkv;
   const int hk = is_k ? j - H : j - H - Hkv;
-  bf16_t* dst = (is_k ? kc : vc) + slots[b] * cs_slot + hk * cs_head + (long long)p * cs_pos;
+  bf16_t* dst = (is_k ? kc : vc) + kv_row(tbl, tbl_stride, ps_shift, slots[b], p, cs_slot, cs_pos) + hk * cs_head;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int d = lane + 64 * i;
@@ -88,13 +102,14 @@ __global__ __launch_bounds__(256) void decode_prep_kernel(
 KCA_API int kca_decode_prep(void* qkv, long long ld, int B, int H, int Hkv, int D, int rot,
                             int interleaved, const float* cos_t, const float* sin_t,
                             const int* pos, const int* slots, void* kc, void* vc,
-                            long long cs_slot, long long cs_head, long long cs_pos,
-                            hipStream_t stream) {
+                            long long cs_slot, long long cs_head, long long cs_pos, const int* tbl,
+                            int tbl_stride, int ps_shift, hipStream_t stream) {
   if (D > 256 || rot > D || (rot & 1) || B <= 0) return 1;
+  if (tbl && (ps_shift < 0 || ps_shift > 20 || tbl_stride <= 0)) return 2;
   const long long rows = (long long)B * (H + 2 * Hkv);
   hipLaunchKernelGGL(decode_prep_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, stream,
                      (bf16_t*)qkv, ld, B, H, Hkv, D, rot, interleaved, cos_t, sin_t, pos, slots,
-                     (bf16_t*)kc, (bf16_t*)vc, cs_slot, cs_head, cs_pos);
+                     (bf16_t*)kc, (bf16_t*)vc, cs_slot, cs_head, cs_pos, tbl, tbl_stride, ps_shift);
   return 0;
 }
 
@@ -112,13 +127,15 @@ struct DecodeParams {
   float* ws_o;   // [B*H, nsplit, D]
   float* ws_ml;  // [B*H, nsplit, 2]
   const float* alibi;
+  const int* tbl;  // paged cache: [seq][tbl_stride] page ids (nullptr: contiguous slots)
+  int tbl_stride, ps_shift;
   int H, Hkv, D, chunk;
   float scale;
 };
 
 // LPT lanes cooperate on one token row (8 dims per lane); TPW = 64/LPT tokens per
 // wave step; G query heads share each K/V row (GQA group).
-template <int LPT, int G>
+template <int LPT, int G, bool PAGED>
 __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
   constexpr int TPW = 64 / LPT;
   constexpr int TPB = 4 * TPW;
@@ -145,9 +162,26 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
   float* sc = smem;                 // [G][chunk]
   float* red = smem + G * p.chunk;  // [4][G][D]
   KCA_DASSERT(p.slots[b] >= 0);
-  const long long kvoff = p.slots[b] * p.cs_slot + hk * p.cs_head + dslot * 8;
+  const int seq = p.slots[b];
+  const long long kvoff = (PAGED ? 0 : (long long)seq * p.cs_slot) + hk * p.cs_head + dslot * 8;
   const bf16_t* kb = p.kc + kvoff;
   const bf16_t* vb = p.vc + kvoff;
+  // paged: this split's page ids staged in LDS once (chunk <= 1024 tokens, pages >= 16 tokens), so a
+  // token's address costs an LDS read instead of a dependent global load in front of every K/V load
+  __shared__ int pg[1024 / 16 + 2];
+  const int pg0 = c0 >> p.ps_shift;
+  if constexpr (PAGED) {
+    const int npg = ((c1 - 1) >> p.ps_shift) - pg0 + 1;
+    KCA_DASSERT(npg <= 1024 / 16 + 2);
+    for (int i = tid; i < npg; i += 256) pg[i] = p.tbl[(long long)seq * p.tbl_stride + pg0 + i];
+    __syncthreads();
+  }
+  // offset of token t inside this sequence's storage
+  auto toff = [&](int t) -> long long {
+    if constexpr (PAGED)
+      return (long long)pg[(t >> p.ps_shift) - pg0] * p.cs_slot + (long long)(t & ((1 << p.ps_shift) - 1)) * p.cs_pos;
+    return (long long)t * p.cs_pos;
+  };
 
   float q[G][8];
 #pragma unroll
@@ -165,6 +199,16 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
 #pragma unroll
   for (int g = 0; g < G; ++g) slope[g] = p.alibi ? p.alibi[hk * G + g] : 0.f;
 
+  // V rows of the first P.V iteration, issued together with the K loads: they do not depend on the
+  // scores, so a chunk of <= TPB*U tokens (every B=1 split) costs one HBM round trip, not two
+  const int tv0 = c0 + wid * TPW + tsub;
+  U16x8 vpre[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int t = tv0 + u * TPB;
+    if (t < c1 && dact) vpre[u] = *reinterpret_cast<const U16x8*>(vb + toff(t));
+  }
+
   // ---- scores
   for (int t0 = c0 + wid * TPW + tsub; t0 < c1; t0 += TPB * U) {
     float kr[U][8];
@@ -172,7 +216,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
     for (int u = 0; u < U; ++u) {
       const int t = t0 + u * TPB;
       if (t < c1 && dact) {
-        load8(kb + (long long)t * p.cs_pos, kr[u]);
+        load8(kb + toff(t), kr[u]);
       } else {
 #pragma unroll
         for (int j = 0; j < 8; ++j) kr[u][j] = 0.f;
@@ -220,13 +264,18 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
   for (int g = 0; g < G; ++g)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
-  for (int t0 = c0 + wid * TPW + tsub; t0 < c1; t0 += TPB * U) {
+  for (int t0 = tv0; t0 < c1; t0 += TPB * U) {
     float vr[U][8];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int t = t0 + u * TPB;
       if (t < c1 && dact) {
-        load8(vb + (long long)t * p.cs_pos, vr[u]);
+        if (t0 == tv0) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) vr[u][j] = bf2f(vpre[u].v[j]);
+        } else {
+          load8(vb + toff(t), vr[u]);
+        }
       } else {
 #pragma unroll
         for (int j = 0; j < 8; ++j) vr[u][j] = 0.f;
@@ -272,25 +321,38 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
   }
 }
 
+// One workgroup per (sequence, head): split maxima and weights in one
+// parallel pass into LDS, then every lane owns one output dim and sums the
+// splits with 8 independent loads in flight (the old per-split serial chain
+// of dependent L2 loads cost ~9 us per layer at B=1).
 __global__ __launch_bounds__(256) void decode_combine_kernel(const float* __restrict__ ws_o,
                                                              const float* __restrict__ ws_ml,
                                                              bf16_t* __restrict__ out, long long o_bs,
                                                              int H, int D, int nsplit) {
+  __shared__ float wsp[1024];
+  __shared__ float red[8];
   const long long bh = blockIdx.x;
   const int b = (int)(bh / H), h = (int)(bh % H);
+  const int tid = threadIdx.x;
   const float* ml = ws_ml + bh * nsplit * 2;
-  float M = -INFINITY;
-  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, ml[2 * s]);
-  for (int d = threadIdx.x; d < D; d += blockDim.x) {
-    float Lsum = 0.f, acc = 0.f;
-    for (int s = 0; s < nsplit; ++s) {
-      const float m = ml[2 * s];
-      if (m == -INFINITY) continue;
-      const float w = __expf(m - M);
-      Lsum += w * ml[2 * s + 1];
-      acc += w * ws_o[(bh * nsplit + s) * D + d];
-    }
-    out[b * o_bs + (long long)h * D + d] = f2bf(Lsum > 0.f ? acc / Lsum : 0.f);
+  float m = -INFINITY;
+  for (int s = tid; s < nsplit; s += 256) m = fmaxf(m, ml[2 * s]);
+  const float M = block_max(m, red);
+  float l = 0.f;
+  for (int s = tid; s < nsplit; s += 256) {
+    const float ms = ml[2 * s];
+    const float w = ms == -INFINITY ? 0.f : __expf(ms - M);
+    wsp[s] = w;
+    l += w * ml[2 * s + 1];
+  }
+  const float Lsum = block_sum(l, red + 4);  // block_sum's barriers also publish wsp
+  const float inv = Lsum > 0.f ? 1.f / Lsum : 0.f;
+  const float* o = ws_o + bh * nsplit * D;
+  for (int d = tid; d < D; d += 256) {
+    float acc = 0.f;
+#pragma unroll 8
+    for (int s = 0; s < nsplit; ++s) acc = fmaf(wsp[s], o[(long long)s * D + d], acc);
+    out[b * o_bs + (long long)h * D + d] = f2bf(acc * inv);
   }
 }
 
@@ -316,7 +378,10 @@ KCA_API long long kca_decode_ws_floats(int B, int H, int D, int max_kv, int chun
 template <int LPT, int G>
 static void launch_decode(const DecodeParams& p, int B, int nsplit, hipStream_t stream) {
   const size_t lds = (size_t)(G * p.chunk + 4 * G * p.D) * sizeof(float);
-  hipLaunchKernelGGL((decode_attn_kernel<LPT, G>), dim3(nsplit, p.Hkv, B), dim3(256), lds, stream, p);
+  if (p.tbl)
+    hipLaunchKernelGGL((decode_attn_kernel<LPT, G, true>), dim3(nsplit, p.Hkv, B), dim3(256), lds, stream, p);
+  else
+    hipLaunchKernelGGL((decode_attn_kernel<LPT, G, false>), dim3(nsplit, p.Hkv, B), dim3(256), lds, stream, p);
 }
 
 template <int LPT>
@@ -334,15 +399,18 @@ KCA_API int kca_decode_attn(const void* q, long long q_bs, const void* kc, const
                             long long cs_slot, long long cs_head, long long cs_pos,
                             const int* slots, const int* kv_lens, void* out, long long o_bs,
                             float* ws, long long ws_floats, int B, int H, int Hkv, int D,
-                            int max_kv, int chunk, float scale, const float* alibi,
-                            hipStream_t stream) {
+                            int max_kv, int chunk, float scale, const float* alibi, const int* tbl,
+                            int tbl_stride, int ps_shift, hipStream_t stream) {
   if (D % 8 || D > 256 || H % Hkv || B <= 0 || max_kv <= 0) return 1;
+  if (tbl && (ps_shift < 4 || ps_shift > 20 || tbl_stride <= 0)) return 5;  // pages of >= 16 tokens
   if (chunk <= 0) chunk = kca_decode_chunk(B, Hkv, max_kv);
   const int G = H / Hkv;
   if (G * chunk > 8192) return 2;
+  if (tbl && chunk > 1024) return 6;  // the LDS page-id stage holds 1024 tokens of pages
   const int nsplit = (max_kv + chunk - 1) / chunk;
+  if (nsplit > 1024) return 7;  // combine keeps the split weights in LDS
   DecodeParams p{(const bf16_t*)q, q_bs, (const bf16_t*)kc, (const bf16_t*)vc, cs_slot, cs_head,
-                 cs_pos, slots, kv_lens, (bf16_t*)out, o_bs, nullptr, nullptr, alibi,
+                 cs_pos, slots, kv_lens, (bf16_t*)out, o_bs, nullptr, nullptr, alibi, tbl, tbl_stride, ps_shift,
                  H, Hkv, D, chunk, scale};
   if (nsplit > 1) {
     const long long need = (long long)B * H * nsplit * (D + 2);

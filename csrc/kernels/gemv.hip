@@ -174,31 +174,28 @@ __global__ __launch_bounds__(256) void skinny_gemm_kernel(
   }
 }
 
-// Split-K form for M == 1 (single-sequence decode, the latency case):
-// a workgroup owns R rows and its 4 waves interleave over K in 512-element
-// slabs (wave w: slabs w, w+4, ...), each lane keeping R*4 16-B weight loads
-// in flight; the 4 partial dot products meet in LDS. Against the row-per-wave
-// form above this quadruples the workgroups (4/CU for a 4096-row output, 16
-// resident waves per CU) and cuts each wave's serial K chain to a quarter --
-// in context (weights never L2/MALL-resident across a 28-layer step) the
-// row-per-wave form streamed at 3.5-3.9 TB/s. (At M = 4 the LN prologue and
-// the 4x larger LDS tile, repeated in 4x the workgroups, made it a loss: GPT-J
-// B=4 decode 5.9 -> 9.3 ms/step, so M > 1 keeps the row-per-wave kernel.)
-template <int M, int R, bool LN>
-__global__ __launch_bounds__(256) void skinny_gemm_sk_kernel(
-    const bf16_t* __restrict__ x, long long ldx, const bf16_t* __restrict__ w,
-    const bf16_t* __restrict__ bias, bf16_t* __restrict__ y, long long ldy, int N, int K,
-    int kc, int act, int mv, LnArgs ln) {
-  extern __shared__ __attribute__((aligned(16))) bf16_t xs[];  // [M][kc]
+// Split-K form for M == 1 (single-sequence decode, the latency case): a
+// workgroup owns R weight rows; lane (wave w, lane l) owns K positions
+// i*2048 + w*512 + l*8 (i = 0, 1, ...) of every row, so its slice of the
+// activation row is a handful of 16-B loads straight into registers -- no
+// LDS stage and no barrier in front of the weight stream. Weights for the
+// first U slabs are requested first; with a LayerNorm prologue (K <= 8192,
+// the lane's whole slice in registers) the residual sum, the two block
+// reductions and the normalisation all run while those loads are in flight.
+// Per-lane loads: R*U weights + U activations, 16 B each. The 4 waves' partial
+// dots meet in LDS. (Was: every workgroup staged / normalised the full row
+// into LDS before its first weight load -- the LN form streamed 3.3 TB/s
+// against 5.2 TB/s for the plain one at GPT-J shapes.)
+template <int R, bool LN>
+__global__ __launch_bounds__(256) void gemv1_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+                                                    const bf16_t* __restrict__ bias, bf16_t* __restrict__ y,
+                                                    int N, int K, int act, LnArgs ln) {
+  constexpr int U = 4;
   __shared__ float red[16];
-  __shared__ float part[4][R * M];
+  __shared__ float part[4][R];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int n0 = blockIdx.x * R;
-  float acc[R][M];
-#pragma unroll
-  for (int r = 0; r < R; ++r)
-#pragma unroll
-    for (int m = 0; m < M; ++m) acc[r][m] = 0.f;
+  const int kl = wid * 512 + lane * 8;
   const bf16_t* wr[R];
   bool rv[R];
 #pragma unroll
@@ -206,73 +203,132 @@ __global__ __launch_bounds__(256) void skinny_gemm_sk_kernel(
     rv[r] = n0 + r < N;
     wr[r] = w + (long long)(rv[r] ? n0 + r : 0) * K;
   }
-  for (int k0 = 0; k0 < K; k0 += kc) {
-    const int kn = min(kc, K - k0);
-    __syncthreads();
-    if constexpr (LN) {
-      ln_prologue<M>(x, ldx, ln, xs, K, mv, red);  // kc == K: one chunk
-    } else {
-      for (int i = tid * 8; i < M * kn; i += 256 * 8) {
-        const int m = i / kn, kk = i % kn;
-        uint4 v = make_uint4(0u, 0u, 0u, 0u);
-        if (m < mv) v = *reinterpret_cast<const uint4*>(x + m * ldx + k0 + kk);
-        *reinterpret_cast<uint4*>(xs + m * kc + kk) = v;
+  float acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = 0.f;
+  uint4 wv[U][R];
+  auto load_w = [&](int i0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = (i0 + u) * 2048 + kl;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        wv[u][r] = make_uint4(0u, 0u, 0u, 0u);
+        if (k < K && rv[r]) wv[u][r] = *reinterpret_cast<const uint4*>(wr[r] + k);
       }
     }
-    __syncthreads();
-    for (int kb = wid * 512 + lane * 8; kb < kn; kb += 4 * 2048) {
-      uint4 wv[4][R];
+  };
+  auto fma_w = [&](int i0, const float (&xv)[U][8]) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int k = kb + u * 2048;
+    for (int u = 0; u < U; ++u) {
+      if ((i0 + u) * 2048 + kl >= K) continue;
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-          wv[u][r] = make_uint4(0u, 0u, 0u, 0u);
-          if (k < kn && rv[r]) wv[u][r] = *reinterpret_cast<const uint4*>(wr[r] + k0 + k);
+      for (int r = 0; r < R; ++r) {
+        const uint32_t q[4] = {wv[u][r].x, wv[u][r].y, wv[u][r].z, wv[u][r].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc[r] = fmaf(__uint_as_float(q[j] << 16), xv[u][2 * j], acc[r]);
+          acc[r] = fmaf(__uint_as_float(q[j] & 0xffff0000u), xv[u][2 * j + 1], acc[r]);
         }
       }
+    }
+  };
+  load_w(0);
+  if constexpr (LN) {
+    float xv[U][8];  // K <= 8192 = U * 2048: the lane's whole slice
+    float s = 0.f;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int k = kb + u * 2048;
-        if (k < kn) {
+    for (int u = 0; u < U; ++u) {
+      const int k = u * 2048 + kl;
+      if (k < K) {
+        float t[8];
+        load8(x + k, xv[u]);
+        if (ln.r1) {
+          load8(ln.r1 + k, t);
 #pragma unroll
-          for (int m = 0; m < M; ++m) {
-            float xv[8];
-            load8(xs + m * kc + k, xv);
+          for (int j = 0; j < 8; ++j) xv[u][j] += t[j];
+        }
+        if (ln.r2) {
+          load8(ln.r2 + k, t);
 #pragma unroll
-            for (int r = 0; r < R; ++r) {
-              const uint32_t q[4] = {wv[u][r].x, wv[u][r].y, wv[u][r].z, wv[u][r].w};
+          for (int j = 0; j < 8; ++j) xv[u][j] += t[j];
+        }
 #pragma unroll
-              for (int j = 0; j < 4; ++j) {
-                acc[r][m] = fmaf(__uint_as_float(q[j] << 16), xv[2 * j], acc[r][m]);
-                acc[r][m] = fmaf(__uint_as_float(q[j] & 0xffff0000u), xv[2 * j + 1], acc[r][m]);
-              }
-            }
+        for (int j = 0; j < 8; ++j) {
+          xv[u][j] = bf2f(f2bf(xv[u][j]));  // statistics over the bf16-rounded residual sum
+          s += xv[u][j];
+        }
+        if (ln.h_out && blockIdx.x == 0) store8(ln.h_out + k, xv[u]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xv[u][j] = 0.f;
+      }
+    }
+    const float mean = block_sum(s, red) / K;
+    float q = 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (u * 2048 + kl >= K) continue;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) q += (xv[u][j] - mean) * (xv[u][j] - mean);
+    }
+    const float rstd = rsqrtf(block_sum(q, red + 8) / K + ln.eps);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = u * 2048 + kl;
+      if (k >= K) continue;
+      float g[8], bb[8];
+      load8(ln.gamma + k, g);
+      if (ln.beta) load8(ln.beta + k, bb);
+      else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bb[j] = 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) xv[u][j] = bf2f(f2bf((xv[u][j] - mean) * rstd * g[j] + bb[j]));
+      if (ln.xn_out && blockIdx.x == 0) store8(ln.xn_out + k, xv[u]);
+    }
+    fma_w(0, xv);
+  } else {
+    const int NI = (K + 2047) / 2048;
+    for (int i0 = 0; i0 < NI; i0 += U) {
+      if (i0) load_w(i0);
+      uint4 xr[U];  // raw bf16, widened at use (keeps the kernel at 4 waves/SIMD)
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = (i0 + u) * 2048 + kl;
+        xr[u] = make_uint4(0u, 0u, 0u, 0u);
+        if (k < K) xr[u] = *reinterpret_cast<const uint4*>(x + k);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if ((i0 + u) * 2048 + kl >= K) continue;
+        const uint32_t xq[4] = {xr[u].x, xr[u].y, xr[u].z, xr[u].w};
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const uint32_t q[4] = {wv[u][r].x, wv[u][r].y, wv[u][r].z, wv[u][r].w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            acc[r] = fmaf(__uint_as_float(q[j] << 16), __uint_as_float(xq[j] << 16), acc[r]);
+            acc[r] = fmaf(__uint_as_float(q[j] & 0xffff0000u), __uint_as_float(xq[j] & 0xffff0000u), acc[r]);
           }
         }
       }
     }
   }
 #pragma unroll
-  for (int r = 0; r < R; ++r)
-#pragma unroll
-    for (int m = 0; m < M; ++m) acc[r][m] = wave_sum(acc[r][m]);
+  for (int r = 0; r < R; ++r) acc[r] = wave_sum(acc[r]);
   if (lane == 0) {
 #pragma unroll
-    for (int r = 0; r < R; ++r)
-#pragma unroll
-      for (int m = 0; m < M; ++m) part[wid][r * M + m] = acc[r][m];
+    for (int r = 0; r < R; ++r) part[wid][r] = acc[r];
   }
   __syncthreads();
-  if (tid < R * M) {
-    const int r = tid / M, m = tid % M;
-    if (rv[0] && n0 + r < N && m < mv) {
-      float v = part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid];
-      v += bias ? bf2f(bias[n0 + r]) : 0.f;
-      if (act == 1) v = gelu_tanh(v);
-      else if (act == 2) v = 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
-      y[m * ldy + n0 + r] = f2bf(v);
-    }
+  if (tid < R && n0 + tid < N) {
+    float v = part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid];
+    v += bias ? bf2f(bias[n0 + tid]) : 0.f;
+    if (act == 1) v = gelu_tanh(v);
+    else if (act == 2) v = 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
+    y[n0 + tid] = f2bf(v);
   }
 }
 
@@ -295,8 +351,7 @@ static void launch_skinny(const bf16_t* x, long long ldx, const bf16_t* w, const
   // split-K form costs more than it saves (B=1 8.75 -> 9.47 ms/token), so wide LN rows stay row-per-wave
   if constexpr (M == 1) if (g_skinny_sk && !(LN && K > 8192)) {
     const dim3 grid((N + R - 1) / R);
-    hipLaunchKernelGGL((skinny_gemm_sk_kernel<M, R, LN>), grid, dim3(256), (size_t)M * kc * sizeof(bf16_t), s,
-                       x, ldx, w, bias, y, ldy, N, K, kc, act, mv, ln);
+    hipLaunchKernelGGL((gemv1_kernel<R, LN>), grid, dim3(256), 0, s, x, w, bias, y, N, K, act, ln);
     return;
   }
   const int rows_per_block = 4 * R;

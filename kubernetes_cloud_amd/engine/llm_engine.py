@@ -9,8 +9,13 @@ sampling parameters are per request (FT's per-request runtime_top_k / top_p /
 temperature / repetition_penalty / random_seed / bad_words / stop_words /
 output log-probs).
 
-``step()`` = admit waiting requests (prefill + first token) while slots are
-free, then one fused decode step for every running request. ``start()`` runs
+``step()`` = admit waiting requests (prefill + first token) while slots and
+KV pages are free, then one fused decode step for every running request.
+Admission reserves a request's worst-case page count (prompt + max_new_tokens)
+against the paged cache, so a running request never runs out of pages (no
+preemption needed); pages go back to the pool the step a request finishes.
+Admitted prompts of different lengths prefill together, right-padded into a
+few length-sorted batches (``_prefill_groups``). ``start()`` runs
 the loop on a background thread for the HTTP servers; ``generate()`` is the
 synchronous batch API used by the finetuner sampler and the evaluator.
 """
@@ -71,9 +76,11 @@ class Request:
 
 class LLMEngine:
     def __init__(self, model, max_slots: int = 32, max_len: int | None = None, use_graphs: bool | None = None,
-                 max_prefill_tokens: int = 16384, runner=None):
+                 max_prefill_tokens: int = 16384, runner=None, page_size: int | None = None,
+                 kv_pages: int | None = None):
         # ``runner``: e.g. a tp_driver.CollectiveRunner that mirrors every call to TP follower ranks
-        self.runner = runner or ModelRunner(model, max_slots=max_slots, max_len=max_len, use_graphs=use_graphs)
+        self.runner = runner or ModelRunner(model, max_slots=max_slots, max_len=max_len, use_graphs=use_graphs,
+                                            page_size=page_size, kv_pages=kv_pages)
         max_slots = self.runner.max_slots
         self.max_len = self.runner.max_len
         self.free = list(range(max_slots))[::-1]
@@ -86,7 +93,12 @@ class LLMEngine:
         self._thread = None
         self._stop = False
         self.max_prefill_tokens = max_prefill_tokens
-        self.stats = {"steps": 0, "decode_tokens": 0, "prefill_tokens": 0, "finished": 0}
+        self.stats = {"steps": 0, "decode_tokens": 0, "prefill_tokens": 0, "finished": 0, "prefill_batches": 0,
+                      "prefill_pad_tokens": 0}
+        cache = getattr(self.runner, "cache", None)
+        self._paged = cache is not None and getattr(cache, "paged", False)
+        self._page_budget = cache.n_pages if self._paged else 0
+        self._committed = 0  # worst-case pages promised to admitted requests
 
     # ------------------------------------------------------------ requests
     def add_request(self, prompt: list, params: SamplingParams, future: Future | None = None,
@@ -149,11 +161,21 @@ class LLMEngine:
             except Exception:  # noqa: BLE001 -- a broken stream consumer must not stall the batch
                 r.on_token = None
 
-    def _finish(self, r: Request):
-        r.t_done = time.perf_counter()
+    def _pages_needed(self, r: Request) -> int:
+        if not self._paged:
+            return 0
+        return self.runner.cache.pages_for(min(len(r.prompt) + r.params.max_new_tokens, self.max_len))
+
+    def _free_slot(self, r: Request):
         if r.slot >= 0:
+            self.runner.release(r.slot)
             self.free.append(r.slot)
             r.slot = -1
+            self._committed -= self._pages_needed(r)
+
+    def _finish(self, r: Request):
+        r.t_done = time.perf_counter()
+        self._free_slot(r)
         self.stats["finished"] += 1
         if r.future is not None and not r.future.done():
             r.future.set_result(r)
@@ -164,19 +186,28 @@ class LLMEngine:
         """Beam search for one prompt on ``num_beams`` slots of this engine's cache
         (mutually exclusive with ``step``; FT beam_width > 1 requests)."""
         from .beam import beam_search
-        if hasattr(self.runner, "_send"):
-            raise NotImplementedError("beam search with a tensor-parallel runner")
+        # a tensor-parallel runner (tp_driver.CollectiveRunner) mirrors prefill / decode_topk /
+        # copy_slots / release to its followers, so beams run under TP unchanged
+        need = 0
+        if self._paged:
+            need = num_beams * (self.runner.cache.pages_for(min(len(prompt) + max_new_tokens, self.max_len)) + 1)
         with self._step_lock:
             with self._lock:
                 if len(self.free) < num_beams:
                     raise RuntimeError(f"need {num_beams} free cache slots, have {len(self.free)}")
+                if self._committed + need > self._page_budget and self._paged:
+                    raise RuntimeError(f"need {need} free KV pages, have {self._page_budget - self._committed}")
                 slots = [self.free.pop() for _ in range(num_beams)]
+                self._committed += need
             try:
                 return beam_search(self.runner, [int(t) for t in prompt], slots, max_new_tokens, eos_token_id,
                                    len_penalty, diversity_rate, n_return)
             finally:
                 with self._lock:
+                    for s_ in slots:
+                        self.runner.release(s_)
                     self.free.extend(slots)
+                    self._committed -= need
 
     def step(self) -> list[Request]:
         """Admit + one decode step. Returns the requests that finished."""
@@ -189,19 +220,34 @@ class LLMEngine:
             admit = []
             budget = self.max_prefill_tokens
             while self.waiting and self.free and (not admit or budget >= len(self.waiting[0].prompt)):
+                need = self._pages_needed(self.waiting[0])
+                if self._paged and self._committed + need > self._page_budget:
+                    if need > self._page_budget:  # can never fit: fail it rather than block the queue
+                        r = self.waiting.pop(0)
+                        r.finish_reason = "error"
+                        r.t_done = time.perf_counter()
+                        if r.future is not None and not r.future.done():
+                            r.future.set_exception(RuntimeError(
+                                f"request needs {need} KV pages > cache size {self._page_budget}"))
+                        continue
+                    break
                 r = self.waiting.pop(0)
                 r.slot = self.free.pop()
+                self._committed += need
                 budget -= len(r.prompt)
                 admit.append(r)
-        # prefill: same-length prompts share one batched pass
-        by_len: dict = {}
-        for r in admit:
-            by_len.setdefault(len(r.prompt), []).append(r)
-        for T, group in by_len.items():
-            ids = torch.tensor([r.prompt for r in group], dtype=torch.long)
-            logits = self.runner.prefill(ids, [r.slot for r in group])
+        for group in _prefill_groups(admit):
+            T = max(len(r.prompt) for r in group)
+            lens = [len(r.prompt) for r in group]
+            ids = torch.tensor([r.prompt + [0] * (T - len(r.prompt)) for r in group], dtype=torch.long)
+            if all(L == T for L in lens):
+                logits = self.runner.prefill(ids, [r.slot for r in group])
+            else:
+                logits = self.runner.prefill(ids, [r.slot for r in group], lens)
             toks, lps = self.runner.sample_first(logits, [self._row(r, 0) for r in group])
-            self.stats["prefill_tokens"] += T * len(group)
+            self.stats["prefill_tokens"] += sum(lens)
+            self.stats["prefill_pad_tokens"] += T * len(group) - sum(lens)
+            self.stats["prefill_batches"] += 1
             for r, t, lp in zip(group, toks, lps):
                 self._append(r, t, lp)
                 if r.done:
@@ -274,11 +320,29 @@ class LLMEngine:
                     victims = self.running + self.waiting
                     self.running, self.waiting = [], []
                 for r in victims:
-                    if r.slot >= 0:
-                        self.free.append(r.slot)
+                    try:
+                        self._free_slot(r)
+                    except Exception:  # noqa: BLE001 -- a broken runner must not stop the loop
                         r.slot = -1
                     if r.future is not None and not r.future.done():
                         r.future.set_exception(e)
+
+
+def _prefill_groups(reqs: list[Request], slack: float = 0.25, min_slack: int = 256) -> list[list[Request]]:
+    """Length-sorted batches whose right padding stays within ``slack`` of the
+    real tokens (or ``min_slack`` tokens: short prompts are launch-bound, so
+    they batch freely)."""
+    out, cur, real = [], [], 0
+    for r in sorted(reqs, key=lambda r: len(r.prompt)):
+        L = len(r.prompt)
+        if cur and L * (len(cur) + 1) - (real + L) > max(slack * (real + L), min_slack):
+            out.append(cur)
+            cur, real = [], 0
+        cur.append(r)
+        real += L
+    if cur:
+        out.append(cur)
+    return out
 
 
 __all__ = ["LLMEngine", "SamplingParams", "Request"]

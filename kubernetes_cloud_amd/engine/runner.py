@@ -3,12 +3,14 @@
 The FT-equivalent decode loop for every causal LM in
 ``models.causal_lm`` (GPT-2, GPT-J, GPT-NeoX/Pythia, GPT-Neo, BLOOM):
 
-* ``KVCache``: one [slots+1, Hkv, max_len, D] K and V tensor per layer (head-major
-  so each (sequence, head) is a contiguous HBM stream; the extra slot is scratch
-  for padding rows of a graph bucket). 288 GB of HBM holds e.g. 64 GPT-J
-  sequences x 2048 tokens (60 GB) next to the 12 GB of weights.
-* ``prefill``: the prompt through the flash-attention kernel, K/V (post-RoPE)
-  written into the request's slot.
+* ``KVCache``: paged by default -- per layer a pool of [Hkv, 64, D] pages and a
+  block table per sequence slot (head-major pages, so each (sequence, head,
+  page) is a contiguous HBM stream); ``page_size=0`` gives one contiguous
+  [Hkv, max_len, D] slot per sequence. 288 GB of HBM holds e.g. 64 GPT-J
+  sequences x 2048 tokens (60 GB) next to the 12 GB of weights; with pages, the
+  slot count is no longer tied to that worst case.
+* ``prefill``: prompts (ragged: right-padded in one batch) through the
+  flash-attention kernel, K/V (post-RoPE) written into each sequence's pages.
 * ``decode``: one token per running sequence -- fused QKV GEMM ->
   ``kca_decode_prep`` (RoPE + cache append) -> ``kca_decode_attn`` (split-K) ->
   out-proj, residual adds fused into the next LayerNorm -> LM head ->
@@ -22,6 +24,7 @@ travel in ONE packed pinned buffer -> one H2D copy.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -37,16 +40,190 @@ def _next_pow2(n: int, lo: int = 1) -> int:
     return p
 
 
+class KVCacheFull(RuntimeError):
+    """No free KV page for a sequence (the engine's admission control keeps
+    running requests clear of this)."""
+
+
 class KVCache:
+    """Per-layer K and V storage for the serving engine.
+
+    ``page_size == 0``: contiguous slots [slots+1, Hkv, max_len, D] (a slot is
+    one sequence's whole capacity). ``page_size > 0`` (default): paged pools
+    [pages+1, Hkv, PS, D] plus a block table [slots+1, max_len/PS] (int32,
+    device; host twin ``table_h``) -- a sequence holds only the pages it has
+    filled, finished requests return theirs at once, and beams share their
+    prefix pages (refcounted, ``fork`` copies only a partial tail page). The
+    last page and the last table row are scratch: free table entries point at
+    the scratch page, so a stray read or a graph bucket's padding row touches
+    nothing live. Head-major pages keep each (sequence, head, page) a
+    contiguous PS*D*2-byte stream for the decode kernel (``ops.decode``).
+    """
+
     def __init__(self, n_layers: int, slots: int, kv_heads: int, max_len: int, head_dim: int,
-                 device, dtype=torch.bfloat16):
-        shape = (slots + 1, kv_heads, max_len, head_dim)
-        self.k = [torch.zeros(shape, device=device, dtype=dtype) for _ in range(n_layers)]
-        self.v = [torch.zeros(shape, device=device, dtype=dtype) for _ in range(n_layers)]
+                 device, dtype=torch.bfloat16, page_size: int = 0, n_pages: int | None = None,
+                 layer_devices: list | None = None):
         self.slots, self.max_len, self.scratch = slots, max_len, slots
+        self.page_size = page_size
+        self.device = torch.device(device)
+        # layer-split models (parallel.layer_split): each layer's cache lives on that layer's device
+        self.layer_devices = [torch.device(d) for d in layer_devices] if layer_devices else [self.device] * n_layers
+        self.devices = list(dict.fromkeys([self.device] + self.layer_devices))
+        if page_size:
+            if page_size < 16 or page_size & (page_size - 1):
+                raise ValueError(f"page_size {page_size}: need a power of two >= 16")
+            self.blocks = -(-max_len // page_size)
+            # default: every slot can hold a full-length sequence, plus one page per slot of headroom
+            # for beam forks (a fork copies a partial tail page before the old one is dropped)
+            self.n_pages = int(n_pages or slots * (self.blocks + 1))
+            self.scratch_page = self.n_pages
+            shape = (self.n_pages + 1, kv_heads, page_size, head_dim)
+            self.table_h = torch.full((slots + 1, self.blocks), self.n_pages, dtype=torch.int32)
+            self.tables = {d: self.table_h.to(d) for d in self.devices}
+            self.table = self.tables[self.device]
+            self.free_pages = list(range(self.n_pages - 1, -1, -1))
+            self.ref = [0] * self.n_pages
+            self.pages: list[list[int]] = [[] for _ in range(slots + 1)]
+            self._dirty = False
+        else:
+            self.table = None
+            self.n_pages = 0
+            shape = (slots + 1, kv_heads, max_len, head_dim)
+            self.tables = {}
+        self.k = [torch.zeros(shape, device=d, dtype=dtype) for d in self.layer_devices]
+        self.v = [torch.zeros(shape, device=d, dtype=dtype) for d in self.layer_devices]
 
     def nbytes(self) -> int:
         return sum(t.numel() * t.element_size() for t in self.k + self.v)
+
+    @property
+    def paged(self) -> bool:
+        return self.page_size > 0
+
+    def pages_for(self, n_tokens: int) -> int:
+        return -(-n_tokens // self.page_size) if self.paged else 0
+
+    def free_count(self) -> int:
+        return len(self.free_pages) if self.paged else 0
+
+    # ------------------------------------------------------------ page table
+    def reserve(self, slot: int, n_tokens: int):
+        """Make positions [0, n_tokens) of ``slot`` addressable (allocates pages)."""
+        if not self.paged:
+            return
+        own = self.pages[slot]
+        need = self.pages_for(min(n_tokens, self.max_len)) - len(own)
+        if need <= 0:
+            return
+        if need > len(self.free_pages):
+            raise KVCacheFull(f"slot {slot} needs {need} KV pages, {len(self.free_pages)} free")
+        for _ in range(need):
+            pg = self.free_pages.pop()
+            self.ref[pg] = 1
+            self.table_h[slot, len(own)] = pg
+            own.append(pg)
+        self._dirty = True
+
+    def _drop(self, pages):
+        for pg in pages:
+            self.ref[pg] -= 1
+            if self.ref[pg] == 0:
+                self.free_pages.append(pg)
+
+    def release(self, slot: int):
+        if not self.paged or not self.pages[slot]:
+            return
+        self._drop(self.pages[slot])
+        self.pages[slot] = []
+        self.table_h[slot].fill_(self.scratch_page)
+        self._dirty = True
+
+    def sync(self):
+        """Block-table edits -> device (stream-ordered after the work already queued)."""
+        if self.paged and self._dirty:
+            for t in self.tables.values():
+                t.copy_(self.table_h)
+            self._dirty = False
+
+    def table_on(self, dev):
+        return self.tables.get(torch.device(dev)) if self.paged else None
+
+    def _per_layer(self, idx: list[int]):
+        """``idx`` as a long tensor on every cache device."""
+        t = torch.tensor(idx, dtype=torch.long)
+        return {d: t.to(d) for d in self.devices}
+
+    def fork(self, dst: list[int], src: list[int], upto: int):
+        """Sequence ``src[i]`` positions [0, upto) -> ``dst[i]``. Paged: whole
+        pages are shared (refcount), only a partial last page is copied; a
+        permutation (dst and src overlapping) is safe."""
+        if not dst:
+            return
+        if not self.paged:
+            d, s = self._per_layer(dst), self._per_layer(src)
+            for k, v, dev in zip(self.k, self.v, self.layer_devices):
+                k[d[dev], :, :upto] = k[s[dev], :, :upto]  # RHS gathered first: overlapping permutations are safe
+                v[d[dev], :, :upto] = v[s[dev], :, :upto]
+            return
+        full, part = divmod(upto, self.page_size)
+        new_lists, cp_from, cp_to = [], [], []
+        for d_, s_ in zip(dst, src):
+            shared = self.pages[s_][:full]
+            for pg in shared:
+                self.ref[pg] += 1
+            lst = list(shared)
+            if part:
+                if not self.free_pages:
+                    self._drop([pg for l_ in new_lists for pg in l_] + lst)
+                    raise KVCacheFull("no free KV page for a beam fork")
+                pg = self.free_pages.pop()
+                self.ref[pg] = 1
+                cp_from.append(self.pages[s_][full])
+                cp_to.append(pg)
+                lst.append(pg)
+            new_lists.append(lst)
+        if cp_to:
+            a, b = self._per_layer(cp_from), self._per_layer(cp_to)
+            for k, v, dev in zip(self.k, self.v, self.layer_devices):
+                k[b[dev]] = k[a[dev]]
+                v[b[dev]] = v[a[dev]]
+        for d_, lst in zip(dst, new_lists):  # old dst pages go only after every source was read
+            self._drop(self.pages[d_])
+            self.pages[d_] = lst
+            self.table_h[d_].fill_(self.scratch_page)
+            if lst:
+                self.table_h[d_, :len(lst)] = torch.tensor(lst, dtype=torch.int32)
+        self._dirty = True
+
+    # --------------------------------------------------------------- prefill
+    def plan_write(self, slots: list[int], lens: list[int], T: int):
+        """Index plan for writing prompts (right-padded to T) into the cache."""
+        if not self.paged:
+            return None
+        import numpy as np
+        PS = self.page_size
+        pg, off, src = [], [], []
+        for i, (s_, L) in enumerate(zip(slots, lens)):
+            t = np.arange(L)
+            own = np.asarray(self.pages[s_][:self.pages_for(L)], dtype=np.int64)
+            pg.append(own[t // PS])
+            off.append(t % PS)
+            src.append(i * T + t)
+        host = [torch.from_numpy(np.concatenate(xs)) for xs in (pg, off, src)]
+        return {d: tuple(t.to(d) for t in host) for d in self.devices}
+
+    def write(self, li: int, k: torch.Tensor, v: torch.Tensor, slots: list[int], lens: list[int], plan):
+        """k, v: [n, T, Hkv, D] (strided views of the QKV GEMM output)."""
+        kc, vc = self.k[li], self.v[li]
+        if plan is None:
+            for i, (s_, L) in enumerate(zip(slots, lens)):  # strided copies (index scatter is ~4x slower)
+                kc[s_, :, :L].copy_(k[i, :L].transpose(0, 1))
+                vc[s_, :, :L].copy_(v[i, :L].transpose(0, 1))
+            return
+        pg, off, src = plan[self.layer_devices[li]]
+        n, T, Hkv, D = k.shape
+        kc[pg, :, off] = k.reshape(n * T, Hkv, D)[src]
+        vc[pg, :, off] = v.reshape(n * T, Hkv, D)[src]
 
 
 class _Packed:
@@ -85,7 +262,7 @@ class _Packed:
 
 class ModelRunner:
     def __init__(self, model, max_slots: int = 32, max_len: int | None = None, use_graphs: bool | None = None,
-                 max_bans: int = 16):
+                 max_bans: int = 16, page_size: int | None = None, kv_pages: int | None = None):
         self.model = model.eval()
         cfg = model.cfg
         self.cfg = cfg
@@ -97,17 +274,26 @@ class ModelRunner:
         self.Hkv = self.H * cfg.kv_heads // cfg.n_heads
         self.D = cfg.head_dim
         self.V = cfg.vocab_size
-        self.cache = KVCache(cfg.n_layers, max_slots, self.Hkv, self.max_len, self.D, self.device, self.dtype)
+        if page_size is None:
+            page_size = int(os.environ.get("KCA_KV_PAGE_SIZE", "64"))
+        # layer-split placement (parallel.layer_split): per-layer devices, the head's device
+        self.layer_devs = [blk.ln_1.weight.device for blk in model.h]
+        self.head_dev = model.ln_f.weight.device
+        self.multi_device = len({str(d) for d in self.layer_devs + [self.device, self.head_dev]}) > 1
+        self.cache = KVCache(cfg.n_layers, max_slots, self.Hkv, self.max_len, self.D, self.device, self.dtype,
+                             page_size=page_size, n_pages=kv_pages, layer_devices=self.layer_devs)
         self.max_slots = max_slots
         self.rot = cfg.rotary_dim
-        if self.rot > 0:
-            self.cos, self.sin = ops.rope_tables(self.rot, self.max_len, cfg.rotary_base, self.device)
-        else:
-            self.cos = self.sin = None
+        self._rope = {}
+        for d in self.cache.devices:
+            self._rope[d] = ops.rope_tables(self.rot, self.max_len, cfg.rotary_base, d) if self.rot > 0 else (None, None)
+        self.cos, self.sin = self._rope[self.device]
         self.seen = torch.zeros(max_slots + 1, self.V, dtype=torch.uint8, device=self.device)
         self.max_bans = max_bans
         on_gpu = self.device.type == "cuda"
         self.use_graphs = on_gpu if use_graphs is None else (use_graphs and on_gpu)
+        if self.multi_device:
+            self.use_graphs = False  # one graph cannot span devices; the split path runs eagerly
         self._graphs: dict = {}
         self._pool = None
         self._static: dict = {}
@@ -115,16 +301,31 @@ class ModelRunner:
 
     # ------------------------------------------------------------- prefill
     @torch.no_grad()
-    def prefill(self, ids: torch.Tensor, slots: list[int]) -> torch.Tensor:
-        """ids [n, T] (same length prompts) -> last-position logits [n, V]. Writes
-        K/V of positions [0, T) into each slot and marks the prompt as seen."""
+    def prefill(self, ids: torch.Tensor, slots: list[int], lens: list[int] | None = None) -> torch.Tensor:
+        """ids [n, T] prompts, right-padded to T when ``lens`` (their true
+        lengths) is given -> last-real-position logits [n, V]. Writes K/V of
+        positions [0, lens[i]) into each slot and marks the prompt as seen.
+        Padding needs no mask: with causal attention a real query row never
+        sees a key to its right, so ragged prompts batch into one pass."""
         m, cfg = self.model, self.cfg
         ids = ids.to(self.device)
         n, T = ids.shape
         assert T <= self.max_len
+        lens = [T] * n if lens is None else [int(x) for x in lens]
+        assert len(lens) == n and all(0 < L <= T for L in lens)
+        ragged = any(L != T for L in lens)
+        for s_, L in zip(slots, lens):
+            self.cache.release(s_)  # a reused slot starts empty
+            self.cache.reserve(s_, L)
+        self.cache.sync()
+        plan = self.cache.plan_write(slots, lens, T)
         sl = torch.tensor(slots, device=self.device, dtype=torch.long)
         self.seen[sl] = 0
-        self.seen[sl[:, None].expand(n, T), ids] = 1
+        if ragged:
+            valid = torch.arange(T, device=self.device)[None] < torch.tensor(lens, device=self.device)[:, None]
+            self.seen[sl[:, None].expand(n, T)[valid], ids[valid]] = 1
+        else:
+            self.seen[sl[:, None].expand(n, T), ids] = 1
         h = m.wte(ids)
         if m.wpe is not None:
             h = h + m.wpe(torch.arange(T, device=self.device))
@@ -132,6 +333,8 @@ class ModelRunner:
             h = m.emb_ln(h)
         pending = ()
         for li, blk in enumerate(m.h):
+            if self.multi_device and h.device != self.layer_devs[li]:
+                h, pending = self._hop(self.layer_devs[li], h, pending)
             x, h = blk.ln_1(h, residual=pending) if pending else (blk.ln_1(h), h)
             at = blk.attn
             qkv = at.qkv(x).view(n, T, 3, self.H, self.D)
@@ -139,9 +342,7 @@ class ModelRunner:
             if self.rot > 0:
                 ops.apply_rotary_(q, k, self.rot, T, cfg.rotary_interleaved, cfg.rotary_base,
                                   max_pos=self.max_len)
-            for i, s_ in enumerate(slots):  # strided copies (advanced-index scatter is ~4x slower)
-                self.cache.k[li][s_, :, :T].copy_(k[i].transpose(0, 1))
-                self.cache.v[li][s_, :, :T].copy_(v[i].transpose(0, 1))
+            self.cache.write(li, k, v, slots, lens, plan)
             if at.window:
                 o = self._windowed_prefill(q, k, v, at)
             else:
@@ -153,8 +354,21 @@ class ModelRunner:
             else:
                 x2, h = blk.ln_2(h, residual=(a,))
                 pending = (blk.mlp(x2),)
-        y, _ = m.ln_f(h[:, -1:], residual=tuple(p_[:, -1:] for p_ in pending))
-        return m.logits_from_hidden(y)[:, -1]
+        if self.multi_device and h.device != self.head_dev:
+            h, pending = self._hop(self.head_dev, h, pending)
+        if ragged:
+            rows = torch.arange(n, device=h.device)
+            last = torch.tensor(lens, device=h.device) - 1
+            pick = lambda t: t[rows, last][:, None]  # noqa: E731
+        else:
+            pick = lambda t: t[:, -1:]  # noqa: E731
+        y, _ = m.ln_f(pick(h), residual=tuple(pick(p_) for p_ in pending))
+        return m.logits_from_hidden(y)[:, -1].to(self.device)
+
+    @staticmethod
+    def _hop(dev, h, pending):
+        """Move the residual stream to the next layer-split device."""
+        return h.to(dev), tuple(p_.to(dev) for p_ in pending)
 
     @staticmethod
     def _windowed_prefill(q, k, v, at):
@@ -174,22 +388,31 @@ class ModelRunner:
         if m.emb_ln is not None:
             h = m.emb_ln(h)
         pending = ()
+        per_dev = {self.device: (pos, slots, kv_lens, ws, obuf)}
         for li, blk in enumerate(m.h):
             # every LayerNorm (+ pending residual adds) runs as the prologue of the GEMM that consumes it
             at = blk.attn
+            dev = self.layer_devs[li]
+            if self.multi_device:
+                if h.device != dev:
+                    h, pending = self._hop(dev, h, pending)
+                if dev not in per_dev:
+                    per_dev[dev] = (pos.to(dev), slots.to(dev), kv_lens.to(dev), None, None)
+                pos, slots, kv_lens, ws, obuf = per_dev[dev]
             shared = cfg.parallel_residual and blk.ln_2 is None  # GPT-J: one LN feeds qkv and fc_in
             if shared:
                 qkv, h, xn = self._ln_lin(blk.ln_1, h, pending, at.qkv, want_xn=True)
             else:
                 qkv, h = self._ln_lin(blk.ln_1, h, pending, at.qkv)
-            kc, vc = self.cache.k[li], self.cache.v[li]
-            dops.decode_prep(qkv, self.H, self.Hkv, self.D, self.rot, cfg.rotary_interleaved, self.cos,
-                             self.sin, pos, slots, kc, vc)
+            kc, vc, tbl = self.cache.k[li], self.cache.v[li], self.cache.table_on(dev)
+            cos, sin = self._rope[dev]
+            dops.decode_prep(qkv, self.H, self.Hkv, self.D, self.rot, cfg.rotary_interleaved, cos, sin, pos,
+                             slots, kc, vc, block_table=tbl)
             if at.window:
                 o = self._windowed_decode(qkv, kc, vc, slots, kv_lens, at)
             else:
                 o = dops.decode_attention(qkv, kc, vc, slots, kv_lens, self.H, max_kv, at.scale, at.alibi,
-                                          out=obuf, ws=ws)
+                                          out=obuf, ws=ws, block_table=tbl)
             a = self._lin(at.out, o)
             mlp = blk.mlp
             act = 1 if mlp.approx in ("tanh", True) else 2
@@ -201,9 +424,13 @@ class ModelRunner:
             else:
                 f, h = self._ln_lin(blk.ln_2, h, (a,), mlp.fc_in, act)
                 pending = (self._lin(mlp.fc_out, f),)
+        if self.multi_device and h.device != self.head_dev:
+            h, pending = self._hop(self.head_dev, h, pending)
         if m.lm_head is None:
-            return self._ln_lin(m.ln_f, h, pending, None, weight=m.wte.weight)[0]
-        return self._ln_lin(m.ln_f, h, pending, m.lm_head)[0]
+            y = self._ln_lin(m.ln_f, h, pending, None, weight=m.wte.weight)[0]
+        else:
+            y = self._ln_lin(m.ln_f, h, pending, m.lm_head)[0]
+        return y.to(self.device) if self.multi_device else y
 
     def _ln_lin(self, ln, h, res, mod, act: int = 0, weight=None, want_xn: bool = False):
         """LayerNorm(h + sum(res)) -> column-parallel / LM-head linear, fused (decode)."""
@@ -228,14 +455,16 @@ class ModelRunner:
     def _windowed_decode(self, qkv, kc, vc, slots, kv_lens, at):
         B = qkv.shape[0]
         out = torch.empty(B, self.H * self.D, device=qkv.device, dtype=qkv.dtype)
+        tbl = self.cache.table_on(kc.device)
         for b in range(B):
             L = int(kv_lens[b])
             lo = max(0, L - at.window)
             s = int(slots[b])
             sub_len = torch.tensor([L - lo], dtype=torch.int32)
-            dops.decode_attention_reference(qkv[b:b + 1], kc[s:s + 1, :, lo:L], vc[s:s + 1, :, lo:L],
-                                            torch.zeros(1, dtype=torch.int32), sub_len, self.H, at.scale,
-                                            None, out[b:b + 1])
+            kw = dops.gather_kv(kc, s, L, tbl)[:, lo:][None]
+            vw = dops.gather_kv(vc, s, L, tbl)[:, lo:][None]
+            dops.decode_attention_reference(qkv[b:b + 1], kw, vw, torch.zeros(1, dtype=torch.int32), sub_len,
+                                            self.H, at.scale, None, out[b:b + 1])
         return out
 
     def _static_for(self, Bb: int, Kb: int):
@@ -275,6 +504,9 @@ class ModelRunner:
         """Eager decode step returning the top-k next-token log-probs per row
         (beam search; K30). -> (logprobs [n, k] fp32, ids [n, k] int64) on device."""
         dev = self.device
+        for s_, p_ in zip(slots, positions):
+            self.cache.reserve(s_, p_ + 1)
+        self.cache.sync()
         tok = torch.tensor(tokens, device=dev, dtype=torch.long)
         pos = torch.tensor(positions, device=dev, dtype=torch.int32)
         sl = torch.tensor(slots, device=dev, dtype=torch.int32)
@@ -286,15 +518,19 @@ class ModelRunner:
 
     @torch.no_grad()
     def copy_slots(self, dst: list[int], src: list[int], upto: int):
-        """KV cache (and seen mask) of ``src`` slots -> ``dst`` slots, positions [0, upto)."""
+        """KV cache (and seen mask) of ``src`` slots -> ``dst`` slots, positions
+        [0, upto) (paged: prefix pages shared, see ``KVCache.fork``)."""
         if not dst:
             return
+        self.cache.fork(dst, src, upto)
+        self.cache.sync()
         d = torch.tensor(dst, device=self.device, dtype=torch.long)
         s = torch.tensor(src, device=self.device, dtype=torch.long)
-        for k, v in zip(self.cache.k, self.cache.v):
-            k[d, :, :upto] = k[s, :, :upto]  # RHS gathered first: overlapping permutations are safe
-            v[d, :, :upto] = v[s, :, :upto]
         self.seen[d] = self.seen[s]
+
+    def release(self, slot: int):
+        """A finished sequence's KV pages go back to the pool."""
+        self.cache.release(slot)
 
     @torch.no_grad()
     def decode(self, rows: list[dict]):
@@ -309,6 +545,9 @@ class ModelRunner:
         st = self._static_for(Bb, Kb)
         pk = st["pk"]
         NB = self.max_bans
+        for r in rows:
+            self.cache.reserve(r["slot"], r["pos"] + 1)
+        self.cache.sync()
         a = pk.np
         tok, sd, pos, sl, kl = a["tokens"], a["seeds"], a["pos"], a["slots"], a["kv_lens"]
         tk, te, tp, rp, bans = a["top_k"], a["temperature"], a["top_p"], a["rep"], a["bans"]
@@ -381,4 +620,4 @@ def mix_seed(seed: int, step: int) -> int:
     return x - (1 << 64) if x >= (1 << 63) else x
 
 
-__all__ = ["KVCache", "ModelRunner", "mix_seed", "math"]
+__all__ = ["KVCache", "KVCacheFull", "ModelRunner", "mix_seed", "math"]

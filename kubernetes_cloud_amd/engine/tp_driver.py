@@ -1,7 +1,8 @@
 """Tensor-parallel serving driver: one engine, ``tp`` lock-stepped runners.
 
 Rank 0 owns the scheduler (``LLMEngine``) and the HTTP front end; every call it
-makes on its ``ModelRunner`` (prefill / sample_first / decode) is first
+makes on its ``ModelRunner`` (prefill / sample_first / decode, and for beam
+search decode_topk / copy_slots, and page release) is first
 broadcast on a small CPU (gloo) control group, and follower ranks replay it on
 their own shard (``follower_loop``). The GPU work of each call -- including the
 row-parallel all-reduces and the vocab all-gather -- then runs in lock step
@@ -27,9 +28,9 @@ class CollectiveRunner:
         obj = [msg]
         dist.broadcast_object_list(obj, src=0, group=self.group)
 
-    def prefill(self, ids, slots):
-        self._send(("prefill", ids.tolist(), list(slots)))
-        out = self.runner.prefill(ids, slots)
+    def prefill(self, ids, slots, lens=None):
+        self._send(("prefill", ids.tolist(), list(slots), lens))
+        out = self.runner.prefill(ids, slots, lens)
         _check_ar()
         return out
 
@@ -40,6 +41,19 @@ class CollectiveRunner:
     def decode(self, rows):
         self._send(("decode", rows))
         return self.runner.decode(rows)
+
+    # beam search (engine.beam): scoring pass, cache re-order, and page release in lock step
+    def decode_topk(self, tokens, positions, slots, k):
+        self._send(("decode_topk", list(tokens), list(positions), list(slots), int(k)))
+        return self.runner.decode_topk(tokens, positions, slots, k)
+
+    def copy_slots(self, dst, src, upto):
+        self._send(("copy_slots", list(dst), list(src), int(upto)))
+        return self.runner.copy_slots(dst, src, upto)
+
+    def release(self, slot):
+        self._send(("release", int(slot)))
+        return self.runner.release(slot)
 
     def shutdown(self):
         self._send(("stop",))
@@ -62,12 +76,18 @@ def follower_loop(runner, ctrl_group=None):
         if op == "stop":
             return
         if op == "prefill":
-            last_logits = runner.prefill(torch.tensor(obj[0][1], dtype=torch.long), obj[0][2])
+            last_logits = runner.prefill(torch.tensor(obj[0][1], dtype=torch.long), obj[0][2], obj[0][3])
             _check_ar()
         elif op == "sample_first":
             runner.sample_first(last_logits, obj[0][1])
         elif op == "decode":
             runner.decode(obj[0][1])
+        elif op == "decode_topk":
+            runner.decode_topk(*obj[0][1:])
+        elif op == "copy_slots":
+            runner.copy_slots(*obj[0][1:])
+        elif op == "release":
+            runner.release(obj[0][1])
         else:
             raise RuntimeError(f"unknown op {op}")
 

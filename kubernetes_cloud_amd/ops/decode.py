@@ -9,7 +9,11 @@ references below (same semantics; used by the CPU test-suite and to pin the
 kernels in ``tests/test_decode_gpu.py``).
 
 Cache layout: ``k_cache``/``v_cache`` are [slots, Hkv, max_len, D] (one per
-layer); a request owns one slot for its lifetime.
+layer); a request owns one slot for its lifetime. Paged (``block_table``
+given): they are page pools [pages, Hkv, PS, D] (PS a power of two >= 16) and
+token t of sequence ``slots[b]`` lives in page ``block_table[slots[b], t // PS]``
+at row ``t % PS`` -- a request holds only the pages it has filled, and beams
+share their common prefix pages (``engine.runner.KVCache``).
 """
 from __future__ import annotations
 
@@ -25,17 +29,20 @@ from . import _lib
 # ------------------------------------------------------------------- prep
 def decode_prep(qkv: torch.Tensor, n_heads: int, kv_heads: int, head_dim: int, rot: int,
                 interleaved: bool, cos: torch.Tensor | None, sin: torch.Tensor | None,
-                pos: torch.Tensor, slots: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor):
+                pos: torch.Tensor, slots: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                block_table: torch.Tensor | None = None):
     """qkv: [B, (H+2Hkv)*D] (row-strided). Rotates Q in place, writes rotated K and
-    V of each row b into cache[slots[b], :, pos[b]]."""
+    V of each row b into cache[slots[b], :, pos[b]] (paged: into its page)."""
     B = qkv.shape[0]
     H, Hkv, D = n_heads, kv_heads, head_dim
     if _lib.use_native(qkv, k_cache):
         assert qkv.stride(-1) == 1 and k_cache.stride(-1) == 1 and k_cache.stride() == v_cache.stride()
         assert pos.dtype == torch.int32 and slots.dtype == torch.int32
+        tbl, tstride, shift = _table_args(block_table, k_cache)
         _lib.call("kca_decode_prep", qkv.data_ptr(), qkv.stride(0), B, H, Hkv, D, rot, int(interleaved),
                   _lib.ptr(cos), _lib.ptr(sin), pos.data_ptr(), slots.data_ptr(), k_cache.data_ptr(),
-                  v_cache.data_ptr(), k_cache.stride(0), k_cache.stride(1), k_cache.stride(2), _lib.stream())
+                  v_cache.data_ptr(), k_cache.stride(0), k_cache.stride(1), k_cache.stride(2), tbl, tstride, shift,
+                  _lib.stream())
         return
     rows = qkv.view(B, H + 2 * Hkv, D)
     x = rows.to(torch.float32, copy=True)  # never alias: K rows of qkv stay unrotated
@@ -53,8 +60,31 @@ def decode_prep(qkv: torch.Tensor, n_heads: int, kv_heads: int, head_dim: int, r
         x[:, :H + Hkv, :rot] = out
         rows[:, :H, :rot] = x[:, :H, :rot].to(rows.dtype)
     sl, p = slots.long(), pos.long()
+    if block_table is not None:
+        PS = k_cache.shape[2]
+        sl, p = block_table.long()[sl, p // PS], p % PS
     k_cache[sl, :, p] = x[:, H:H + Hkv].to(k_cache.dtype)
     v_cache[sl, :, p] = x[:, H + Hkv:].to(v_cache.dtype)
+
+
+def _table_args(block_table, k_cache):
+    """(pointer, row stride, log2 page size) of a paged cache's block table."""
+    if block_table is None:
+        return 0, 0, 0
+    PS = k_cache.shape[2]
+    assert PS >= 16 and PS & (PS - 1) == 0, "page size must be a power of two >= 16"
+    assert block_table.dtype == torch.int32 and block_table.is_contiguous()
+    return block_table.data_ptr(), block_table.stride(0), PS.bit_length() - 1
+
+
+def gather_kv(cache: torch.Tensor, seq: int, n: int, block_table: torch.Tensor | None = None) -> torch.Tensor:
+    """Tokens [0, n) of sequence ``seq`` as a [Hkv, n, D] tensor (contiguous or paged cache)."""
+    if block_table is None:
+        return cache[seq, :, :n]
+    PS = cache.shape[2]
+    pages = block_table[seq, :-(-n // PS)].long()
+    Hkv, D = cache.shape[1], cache.shape[3]
+    return cache[pages].transpose(0, 1).reshape(Hkv, -1, D)[:, :n]
 
 
 # -------------------------------------------------------------- attention
@@ -83,9 +113,11 @@ def decode_chunk(B: int, Hkv: int, max_kv: int) -> int:
 def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slots: torch.Tensor,
                      kv_lens: torch.Tensor, n_heads: int, max_kv: int, scale: float | None = None,
                      alibi: torch.Tensor | None = None, out: torch.Tensor | None = None,
-                     ws: torch.Tensor | None = None, chunk: int = 0) -> torch.Tensor:
+                     ws: torch.Tensor | None = None, chunk: int = 0,
+                     block_table: torch.Tensor | None = None) -> torch.Tensor:
     """q: [B, >=H*D] (row-strided; e.g. the Q slice of the fused QKV buffer).
-    Attends row b over cache[slots[b], :, :kv_lens[b]]. Returns [B, H*D]."""
+    Attends row b over cache[slots[b], :, :kv_lens[b]] (paged: over its pages).
+    Returns [B, H*D]."""
     B = q.shape[0]
     _, Hkv, L, D = k_cache.shape
     H = n_heads
@@ -94,7 +126,8 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
         out = torch.empty(B, H * D, device=q.device, dtype=q.dtype)
     if _lib.use_native(q, k_cache):
         assert q.stride(-1) == 1 and out.stride(-1) == 1 and k_cache.stride() == v_cache.stride()
-        assert max_kv <= L
+        tbl, tstride, shift = _table_args(block_table, k_cache)
+        assert max_kv <= (L if block_table is None else block_table.shape[1] * L)
         if chunk <= 0:
             chunk = decode_chunk(B, Hkv, max_kv)
         need = decode_ws_floats(B, H, Hkv, D, max_kv, chunk)
@@ -104,12 +137,13 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
                   k_cache.stride(0), k_cache.stride(1), k_cache.stride(2), slots.data_ptr(),
                   kv_lens.data_ptr(), out.data_ptr(), out.stride(0), _lib.ptr(ws),
                   ws.numel() if ws is not None else 0, B, H, Hkv, D, max_kv, chunk, float(scale),
-                  _lib.ptr(alibi), _lib.stream())
+                  _lib.ptr(alibi), tbl, tstride, shift, _lib.stream())
         return out
-    return decode_attention_reference(q, k_cache, v_cache, slots, kv_lens, H, scale, alibi, out)
+    return decode_attention_reference(q, k_cache, v_cache, slots, kv_lens, H, scale, alibi, out, block_table)
 
 
-def decode_attention_reference(q, k_cache, v_cache, slots, kv_lens, n_heads, scale, alibi=None, out=None):
+def decode_attention_reference(q, k_cache, v_cache, slots, kv_lens, n_heads, scale, alibi=None, out=None,
+                               block_table=None):
     B = q.shape[0]
     _, Hkv, L, D = k_cache.shape
     H = n_heads
@@ -119,8 +153,8 @@ def decode_attention_reference(q, k_cache, v_cache, slots, kv_lens, n_heads, sca
         n = int(kv_lens[b])
         s_ = int(slots[b])
         qb = q[b, :H * D].float().view(H, D)
-        kb = k_cache[s_, :, :n].float().repeat_interleave(H // Hkv, 0)  # [H, n, D]
-        vb = v_cache[s_, :, :n].float().repeat_interleave(H // Hkv, 0)
+        kb = gather_kv(k_cache, s_, n, block_table).float().repeat_interleave(H // Hkv, 0)  # [H, n, D]
+        vb = gather_kv(v_cache, s_, n, block_table).float().repeat_interleave(H // Hkv, 0)
         sc = torch.einsum("hd,hnd->hn", qb, kb) * scale
         if alibi is not None:
             sc = sc + alibi.float()[:, None] * (torch.arange(n, device=q.device) - (n - 1)).float()[None]
@@ -229,6 +263,6 @@ def sample_logits_reference(logits, temperature, top_k, top_p, rep_penalty=None,
     return ids, lps
 
 
-__all__ = ["decode_prep", "decode_attention", "decode_attention_reference", "decode_chunk",
+__all__ = ["decode_prep", "decode_attention", "decode_attention_reference", "decode_chunk", "gather_kv",
            "decode_ws_floats", "sample_logits", "sample_logits_reference", "keep_mask_reference",
            "processed_logits_reference"]

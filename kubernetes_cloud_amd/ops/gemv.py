@@ -74,6 +74,12 @@ def _ln_ok(x, M, K, weight, residuals, gamma, beta, bias):
         and (bias is None or bias.dtype == torch.bfloat16)
 
 
+# M == 1: normalise once (ln_fwd_kernel, one workgroup) and stream the weights with the plain GEMV,
+# instead of every GEMV workgroup re-reading x + residuals + gamma/beta and redoing the reductions
+# (at N = 12288 that per-workgroup prologue moved more L2 bytes than the weights themselves).
+_LN_SPLIT_M1 = os.environ.get("KCA_DECODE_LN_SPLIT", "1") not in ("0", "false")
+
+
 def ln_skinny_linear(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor | None, eps: float,
                      weight: torch.Tensor, bias: torch.Tensor | None = None, residuals=(), act: int = 0,
                      want_h: bool = False, want_xn: bool = False):
@@ -86,7 +92,8 @@ def ln_skinny_linear(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor | 
     batch is too wide."""
     M, K = x.shape
     residuals = tuple(r for r in residuals if r is not None)
-    if _lib.use_native(x, weight) and _ln_ok(x, M, K, weight, residuals, gamma, beta, bias):
+    split = M == 1 and _LN_SPLIT_M1  # one LN launch + the plain GEMV (A/B knob, see _LN_SPLIT_M1)
+    if not split and _lib.use_native(x, weight) and _ln_ok(x, M, K, weight, residuals, gamma, beta, bias):
         h = torch.empty(M, K, device=x.device, dtype=x.dtype) if residuals else x
         y = torch.empty(M, weight.shape[0], device=x.device, dtype=x.dtype)
         xn = torch.empty(M, K, device=x.device, dtype=x.dtype) if want_xn else None

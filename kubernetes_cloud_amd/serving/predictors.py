@@ -36,6 +36,10 @@ def bloom_options(env=None) -> tuple[dict, dict]:
         "MODEL_NAME": re.sub(r"[^\w-]", "-", model_id).lower(),
         "MODEL_TYPE": env.get("MODEL_TYPE", "text-generation"),
         "MODEL_DOWNLOAD_TIMEOUT": int(env.get("MODEL_DOWNLOAD_TIMEOUT", 300)),
+        # layer-split fallback (bloom.py:11,46 device_map="auto" + max_memory): e.g.
+        # DEVICE_MAP=auto MAX_MEMORY="0:71GIB,1:71GIB,2:71GIB,3:71GIB,4:71GIB"
+        "DEVICE_MAP": env.get("DEVICE_MAP", ""),
+        "MAX_MEMORY": env.get("MAX_MEMORY", ""),
     }
     params = {
         "MIN_LENGTH": int(env.get("MIN_LENGTH", 1)),
@@ -46,6 +50,15 @@ def bloom_options(env=None) -> tuple[dict, dict]:
         "REPETITION_PENALTY": float(env.get("REPETITION_PENALTY", 1.0)),
     }
     return options, params
+
+
+def default_max_memory(frac: float = 0.9) -> dict:
+    """Every visible GPU at ``frac`` of its HBM (accelerate's "auto" budget)."""
+    import torch
+    n = torch.cuda.device_count()
+    if n == 0:
+        return {"cpu": 1 << 40}
+    return {i: int(torch.cuda.get_device_properties(i).total_memory * frac) for i in range(n)}
 
 
 def wait_for_ready_file(path: str, timeout_s: int, interval_s: float = 10.0):
@@ -74,7 +87,13 @@ class BloomPredictor(Model):
     def load(self):
         if self.options["MODEL_TYPE"] != "text-generation":
             raise ValueError(f"unsupported MODEL_TYPE {self.options['MODEL_TYPE']}")
-        model, tok = load_lm(self.options["MODEL_PATH"])
+        if self.options.get("DEVICE_MAP"):
+            from ..io.hf import load_tokenizer
+            from ..parallel.layer_split import load_layer_split
+            model = load_layer_split(self.options["MODEL_PATH"], self.options.get("MAX_MEMORY") or default_max_memory())
+            tok = load_tokenizer(self.options["MODEL_PATH"])
+        else:
+            model, tok = load_lm(self.options["MODEL_PATH"])
         self.generator = TextGenerator(model, tok)
         self.ready = True
 

@@ -182,7 +182,7 @@ def main(argv=None):
     tf = dict(size=args.resolution, center_crop=args.center_crop, interpolation=args.resize_interp)
     if args.is_dreambooth:
         ds = DreamBoothDataset(tok, args.instance_dataset, args.instance_prompt, args.class_prompt,
-                               args.class_dataset, args.num_class_images, gen_class_images, **tf)
+                               args.class_dataset, args.num_class_images, gen_class_images, sync=barrier, **tf)
     else:
         ds = LocalBase(tok, args.dataset, ucg=args.ucg, shuffle=args.shuffle, **tf)
     sampler = torch.utils.data.DistributedSampler(ds, world, rank, shuffle=args.shuffle, seed=args.seed) \

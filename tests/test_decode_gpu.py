@@ -234,3 +234,122 @@ def test_dalle_mini_predictor_on_gpu():
     from PIL import Image
     assert a[:8] == b"\x89PNG\r\n\x1a\n" and a == b
     assert Image.open(_io.BytesIO(a)).size == (8, 8)
+
+
+def _paginate(kc, PS, seed=0):
+    """Contiguous [S, Hkv, L, D] -> (shuffled page pool [S*L/PS + 1, Hkv, PS, D], block table [S, L/PS])."""
+    S, Hkv, L, D = kc.shape
+    nb = L // PS
+    perm = torch.randperm(S * nb, generator=torch.Generator().manual_seed(seed))
+    pool = torch.zeros(S * nb + 1, Hkv, PS, D, device=kc.device, dtype=kc.dtype)
+    pages = kc.view(S, Hkv, nb, PS, D).permute(0, 2, 1, 3, 4).reshape(S * nb, Hkv, PS, D)
+    pool[perm.to(kc.device)] = pages
+    return pool, perm.view(S, nb).to(torch.int32).to(kc.device)
+
+
+@pytest.mark.parametrize("D,G,PS", [(256, 1, 64), (128, 4, 16), (80, 1, 256), (64, 2, 32)])
+def test_decode_attention_paged_equals_contiguous(D, G, PS):
+    torch.manual_seed(D + G)
+    B, Hkv, L = 6, 4, 2048
+    H = Hkv * G
+    kc = torch.randn(B + 1, Hkv, L, D, device=dev).to(torch.bfloat16)
+    vc = torch.randn_like(kc)
+    kp, tbl = _paginate(kc, PS, 1)
+    vp, _ = _paginate(vc, PS, 1)
+    q = torch.randn(B, (H + 2 * Hkv) * D, device=dev).to(torch.bfloat16)
+    slots = torch.tensor([3, 0, 6, 1, 2, 5], device=dev, dtype=torch.int32)
+    lens = torch.tensor([1, 2048, 700, 65, 1500, 129], device=dev, dtype=torch.int32)
+    for chunk in (0, 64, 1024):
+        a = dops.decode_attention(q, kc, vc, slots, lens, H, L, chunk=chunk)
+        b = dops.decode_attention(q, kp, vp, slots, lens, H, L, chunk=chunk, block_table=tbl)
+        assert torch.equal(a, b), chunk  # same values, same reduction order
+    ref = dops.decode_attention_reference(q.float(), kp.float(), vp.float(), slots, lens, H, 1 / math.sqrt(D),
+                                          None, torch.empty(B, H * D, device=dev), tbl)
+    assert (b.float() - ref).abs().max() < 2e-2
+
+
+def test_decode_prep_paged_equals_contiguous():
+    torch.manual_seed(0)
+    B, H, Hkv, D, S, L, PS = 5, 4, 4, 256, 7, 256, 64
+    qkv = torch.randn(B, (H + 2 * Hkv) * D, device=dev).to(torch.bfloat16)
+    pos = torch.tensor([0, 3, 255, 64, 130], device=dev, dtype=torch.int32)
+    slots = torch.tensor([6, 0, 2, 3, 1], device=dev, dtype=torch.int32)
+    cos, sin = rope_tables(64, L, 10000.0, dev)
+    kc = torch.zeros(S, Hkv, L, D, device=dev, dtype=torch.bfloat16)
+    vc = torch.zeros_like(kc)
+    kp, tbl = _paginate(kc, PS, 2)
+    vp, _ = _paginate(vc, PS, 2)
+    q1, q2 = qkv.clone(), qkv.clone()
+    dops.decode_prep(q1, H, Hkv, D, 64, True, cos, sin, pos, slots, kc, vc)
+    dops.decode_prep(q2, H, Hkv, D, 64, True, cos, sin, pos, slots, kp, vp, block_table=tbl)
+    assert torch.equal(q1, q2)
+    for s in range(S):
+        assert torch.equal(dops.gather_kv(kp, s, L, tbl), kc[s]) and torch.equal(dops.gather_kv(vp, s, L, tbl), vc[s])
+
+
+def _gpu_model(preset):
+    from kubernetes_cloud_amd.models.causal_lm import build_model
+    from kubernetes_cloud_amd.models.config import PRESETS_HF, LMConfig
+    small = {"gpt-j-6b": dict(n_embd=1024, n_layer=2, n_head=4, rotary_dim=64, n_positions=512),
+             "bloom-560m": dict(hidden_size=512, n_layer=2, n_head=4)}[preset]
+    cfg = dict(PRESETS_HF[preset])
+    cfg.update(small)
+    return build_model(LMConfig.from_hf(cfg), device=dev, dtype=torch.bfloat16, seed=0)
+
+
+@pytest.mark.parametrize("preset", ["gpt-j-6b", "bloom-560m"])
+def test_engine_gpu_paged_and_ragged(preset):
+    """Paged cache == contiguous cache exactly; mixed prompt lengths prefilled in
+    one ragged batch == each prompt run alone (up to bf16 near-ties of the
+    batched vs single-row GEMMs); beam search paged == contiguous."""
+    from kubernetes_cloud_amd.engine.llm_engine import LLMEngine, SamplingParams
+    m = _gpu_model(preset)
+    g = torch.Generator().manual_seed(1)
+    prompts = [[int(x) for x in torch.randint(0, 1000, (n,), generator=g)] for n in (7, 150, 33, 64, 1, 90)]
+    sp = SamplingParams(max_new_tokens=20, do_sample=False)
+    runs = {}
+    for ps in (0, 16, 64):
+        eng = LLMEngine(m, max_slots=8, max_len=256, page_size=ps)
+        runs[ps] = [r.output for r in eng.generate(prompts, sp)]
+        assert eng.stats["prefill_batches"] < len(prompts)
+        if ps:
+            assert eng.runner.cache.free_count() == eng.runner.cache.n_pages
+    assert runs[0] == runs[16] == runs[64]
+    for p, o in zip(prompts, runs[64]):
+        solo = LLMEngine(m, max_slots=1, max_len=256).generate([p], sp)[0].output
+        i = next((j for j, (a, b) in enumerate(zip(o, solo)) if a != b), None)
+        if i is not None:  # allowed only where the two best logits are within bf16 noise
+            with torch.no_grad():
+                row = m(torch.tensor([p + o[:i]], device=dev))[0, -1].float()
+            top2 = row.topk(2).values
+            assert float(top2[0] - top2[1]) < 0.1, (preset, len(p), i)
+    beams = [LLMEngine(m, max_slots=4, max_len=256, page_size=ps).beam_generate(
+        prompts[2], num_beams=4, max_new_tokens=16, n_return=4).sequences for ps in (0, 16)]
+    assert beams[0] == beams[1]
+
+
+def test_layer_split_gpu_cpu_engine(tmp_path):
+    """PAR-9 fallback: a model split over the MI355X and host memory serves
+    through the engine (per-layer KV caches on each layer's device) and its
+    prefill logits match the all-GPU model."""
+    from kubernetes_cloud_amd.engine.llm_engine import LLMEngine, SamplingParams
+    from kubernetes_cloud_amd.io.hf import load_pretrained
+    from kubernetes_cloud_amd.parallel import layer_split as ls
+
+    from .helpers import make_model_dir
+    d = make_model_dir(str(tmp_path / "m"), "gpt-j-6b", n_embd=256, n_layer=4, n_head=4, rotary_dim=32,
+                       vocab_size=512, tokenizer=False)
+    full = load_pretrained(d, device=dev, dtype=torch.bfloat16)
+    meta_blk = ls._nbytes(full.h[0], torch.bfloat16)
+    emb = ls._nbytes(full.wte, torch.bfloat16)
+    m = ls.load_layer_split(d, {0: emb + 2 * meta_blk + 1024, "cpu": 1 << 30}, dtype=torch.bfloat16)
+    assert m.hf_device_map["h.1"].startswith("cuda") and m.hf_device_map["h.2"] == "cpu"
+    eng = LLMEngine(m, max_slots=2, max_len=64)
+    r = eng.runner
+    assert r.multi_device and r.cache.k[0].is_cuda and not r.cache.k[3].is_cuda
+    ids = torch.tensor([[5, 9, 2, 7, 1, 3]])
+    a = r.prefill(ids, [0]).float()
+    b = LLMEngine(full, max_slots=2, max_len=64).runner.prefill(ids, [0]).float()
+    assert (a - b).abs().max() < 0.1 * b.abs().max()
+    out = eng.generate([[5, 9, 2], [1, 2, 3, 4, 5]], SamplingParams(max_new_tokens=6, do_sample=False))
+    assert all(len(x.output) == 6 for x in out)

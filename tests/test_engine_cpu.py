@@ -138,3 +138,113 @@ def test_beam_search_matches_exhaustive():
     g = eng.generate([prompt], SamplingParams(max_new_tokens=5, do_sample=False))[0].output
     assert eng.beam_generate(prompt, 1, 5).sequences[0] == g
     assert len(eng.free) == 24
+
+
+# ------------------------------------------------------ paged KV / ragged prefill
+@pytest.mark.parametrize("preset", ["gpt-j-6b", "bloom-560m"])
+def test_paged_cache_matches_contiguous_and_recompute(preset):
+    m = tiny(preset)
+    prompts = [[5, 6, 7], list(range(1, 20)), [11, 12, 13, 14], [3] * 33]
+    sp = SamplingParams(max_new_tokens=9, do_sample=False)
+    paged = LLMEngine(m, max_slots=4, max_len=64, page_size=16).generate(prompts, sp)
+    contig = LLMEngine(m, max_slots=4, max_len=64, page_size=0).generate(prompts, sp)
+    for p, a, b in zip(prompts, paged, contig):
+        assert a.output == b.output == greedy_recompute(m, p, 9)
+
+
+def test_ragged_prefill_batches_and_matches_solo():
+    m = tiny("gpt-j-6b")
+    prompts = [[1, 2, 3], [4] * 9, [5, 6], list(range(7, 21)), [9] * 5, [2, 9, 4, 1]]
+    sp = SamplingParams(max_new_tokens=5, do_sample=False)
+    eng = LLMEngine(m, max_slots=8, max_len=48, page_size=16)
+    reqs = eng.generate(prompts, sp)
+    assert eng.stats["prefill_batches"] < len(set(map(len, prompts)))  # mixed lengths shared a pass
+    assert eng.stats["prefill_pad_tokens"] > 0
+    for p, r in zip(prompts, reqs):
+        assert r.output == LLMEngine(m, max_slots=1, max_len=48).generate([p], sp)[0].output
+
+
+def test_prefill_groups_bound_padding():
+    from kubernetes_cloud_amd.engine.llm_engine import Request, _prefill_groups
+    reqs = [Request(i, [0] * L, SamplingParams()) for i, L in enumerate([1000, 10, 990, 12, 400, 2000])]
+    groups = _prefill_groups(reqs)
+    assert sorted(r.rid for g in groups for r in g) == list(range(6))
+    for g in groups:
+        T, real = max(len(r.prompt) for r in g), sum(len(r.prompt) for r in g)
+        assert T * len(g) - real <= max(0.25 * real, 256)
+    assert [len(r.prompt) for r in groups[0]] == [10, 12]
+
+
+def test_kv_page_budget_queues_and_returns_pages():
+    m = tiny("gpt2")
+    sp = SamplingParams(max_new_tokens=20, do_sample=False)
+    prompts = [[1, 2, 3], [4, 5], [6, 7, 8, 9], [10], [11, 12]]
+    # 2 pages of 16 tokens per request in the worst case, 4 pages total -> at most 2 requests in flight
+    eng = LLMEngine(m, max_slots=4, max_len=32, page_size=16, kv_pages=4)
+    reqs = [eng.add_request(p, sp) for p in prompts]
+    eng.step()
+    assert len(eng.running) == 2 and len(eng.waiting) == 3
+    eng.run_until_done(reqs)
+    solo = [LLMEngine(m, max_slots=1, max_len=32).generate([p], sp)[0].output for p in prompts]
+    assert [r.output for r in reqs] == solo
+    cache = eng.runner.cache
+    assert cache.free_count() == 4 and eng._committed == 0 and all(x == 0 for x in cache.ref)
+    small = LLMEngine(m, max_slots=2, max_len=32, page_size=16, kv_pages=1)
+    too_big = small.add_request([1] * 20, SamplingParams(max_new_tokens=5))  # 2 pages > the whole cache
+    ok = small.add_request([1] * 4, SamplingParams(max_new_tokens=5))
+    small.run_until_done()
+    assert too_big.finish_reason == "error" and ok.finish_reason == "length"
+
+
+def test_fork_shares_full_pages_and_copies_tail():
+    from kubernetes_cloud_amd.engine.runner import KVCache
+    c = KVCache(1, 3, 2, 64, 4, "cpu", torch.float32, page_size=16)
+    c.reserve(0, 40)  # 3 pages
+    c.k[0][c.pages[0]] = torch.randn(3, 2, 16, 4)
+    c.fork([1, 2], [0, 0], 37)
+    assert c.pages[1][:2] == c.pages[2][:2] == c.pages[0][:2]  # 2 full pages shared
+    assert c.pages[1][2] != c.pages[0][2] != c.pages[2][2]     # partial tail copied
+    for s in (1, 2):
+        assert torch.equal(dops.gather_kv(c.k[0], s, 37, c.table_h), dops.gather_kv(c.k[0], 0, 37, c.table_h))
+    assert c.ref[c.pages[0][0]] == 3
+    c.fork([0, 1], [1, 0], 37)  # permutation
+    c.release(0), c.release(1), c.release(2)
+    assert c.free_count() == c.n_pages and all(x == 0 for x in c.ref)
+
+
+def test_paged_decode_ops_reference_match_contiguous():
+    torch.manual_seed(0)
+    H, Hkv, D, PS, L = 4, 2, 8, 16, 64
+    contig_k, contig_v = torch.randn(3, Hkv, L, D), torch.randn(3, Hkv, L, D)
+    pool_k, pool_v = torch.zeros(13, Hkv, PS, D), torch.zeros(13, Hkv, PS, D)
+    perm = torch.randperm(12).view(3, 4)
+    tbl = perm.to(torch.int32)
+    for s in range(3):
+        for j in range(4):
+            pool_k[perm[s, j]] = contig_k[s, :, j * PS:(j + 1) * PS]
+            pool_v[perm[s, j]] = contig_v[s, :, j * PS:(j + 1) * PS]
+    qkv = torch.randn(3, (H + 2 * Hkv) * D)
+    pos = torch.tensor([5, 40, 63], dtype=torch.int32)
+    slots = torch.tensor([2, 0, 1], dtype=torch.int32)
+    cos, sin = torch.randn(L, 2), torch.randn(L, 2)
+    q1, q2 = qkv.clone(), qkv.clone()
+    dops.decode_prep(q1, H, Hkv, D, 4, False, cos, sin, pos, slots, contig_k, contig_v)
+    dops.decode_prep(q2, H, Hkv, D, 4, False, cos, sin, pos, slots, pool_k, pool_v, block_table=tbl)
+    assert torch.equal(q1, q2)
+    kl = pos + 1
+    a = dops.decode_attention(q1, contig_k, contig_v, slots, kl, H, L)
+    b = dops.decode_attention(q2, pool_k, pool_v, slots, kl, H, L, block_table=tbl)
+    assert torch.allclose(a, b)
+
+
+@pytest.mark.parametrize("page_size", [0, 16])
+def test_beam_search_paged_equals_contiguous(page_size):
+    m = tiny("gpt-j-6b")
+    eng = LLMEngine(m, max_slots=4, max_len=64, page_size=page_size)
+    res = eng.beam_generate([3, 1, 4, 1, 5, 9, 2, 6, 5, 3, 5, 8, 9, 7, 9, 3, 2], num_beams=3, max_new_tokens=12,
+                            n_return=3)
+    ref = LLMEngine(m, max_slots=4, max_len=64, page_size=0).beam_generate(
+        [3, 1, 4, 1, 5, 9, 2, 6, 5, 3, 5, 8, 9, 7, 9, 3, 2], num_beams=3, max_new_tokens=12, n_return=3)
+    assert res.sequences == ref.sequences
+    if page_size:
+        assert eng.runner.cache.free_count() == eng.runner.cache.n_pages

@@ -1,7 +1,7 @@
 """Tensor parallelism on CPU (gloo, world_size 2): sharded forward/backward
 match the unsharded model, the lazy safetensors TP loader matches in-memory
 sharding, and the lock-stepped TP serving engine reproduces single-process
-greedy generation."""
+greedy generation (ragged prefill, paged cache) and beam search."""
 import os
 import socket
 
@@ -71,11 +71,15 @@ def _worker(rank, world, port, preset, model_dir, q):
     if rank == 0:
         eng = LLMEngine(tp, runner=CollectiveRunner(runner, ctrl))
         reqs = eng.generate([[1, 2, 3], [7, 8, 9, 10, 11]], SamplingParams(max_new_tokens=6, do_sample=False))
-        eng.runner.shutdown()
         res["gen"] = [r.output for r in reqs]
+        # beam search under TP: decode_topk / copy_slots / release mirrored to the follower
+        res["beam"] = eng.beam_generate(list(range(1, 18)), num_beams=3, max_new_tokens=8, n_return=3).sequences
+        eng.runner.shutdown()
         ref_eng = LLMEngine(full, max_slots=4, max_len=48)
         res["ref"] = [r.output for r in ref_eng.generate([[1, 2, 3], [7, 8, 9, 10, 11]],
                                                           SamplingParams(max_new_tokens=6, do_sample=False))]
+        res["beam_ref"] = ref_eng.beam_generate(list(range(1, 18)), num_beams=3, max_new_tokens=8,
+                                                n_return=3).sequences
         q.put(res)
     else:
         follower_loop(runner, ctrl)
@@ -106,3 +110,4 @@ def test_tp2_matches_unsharded(preset, tmp_path):
     if model_dir:
         assert res["load"] == 0.0
     assert res["gen"] == res["ref"]
+    assert res["beam"] == res["beam_ref"]
