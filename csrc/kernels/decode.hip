@@ -131,7 +131,40 @@ struct DecodeParams {
   int tbl_stride, ps_shift;
   int H, Hkv, D, chunk;
   float scale;
+  // fused prep (kca_decode_prep_attn): q is the fused QKV row; the kernel applies RoPE to Q itself
+  // and the split holding the new token (position kv_len-1) rotates its K, appends K/V to the cache
+  // and uses them from LDS -- one launch instead of prep + attention
+  int fused, rot, interleaved;
+  const float* cos_t;
+  const float* sin_t;
 };
+
+// RoPE of the 8 dims [d0, d0+8) of a head row at position `pos`, matching
+// decode_prep_kernel (partner values read from the unrotated row; the result is
+// rounded to bf16 as the stored rotation would be).
+__device__ __forceinline__ void rope8(const bf16_t* __restrict__ row, int d0, float (&x)[8], int pos, int rot,
+                                      int interleaved, const float* __restrict__ cos_t,
+                                      const float* __restrict__ sin_t) {
+  const int half = rot >> 1;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int d = d0 + j;
+    if (d >= rot) continue;
+    int partner, fi;
+    float sgn;
+    if (interleaved) {
+      partner = d ^ 1;
+      fi = d >> 1;
+      sgn = (d & 1) ? 1.f : -1.f;
+    } else {
+      partner = d < half ? d + half : d - half;
+      fi = d < half ? d : d - half;
+      sgn = d < half ? -1.f : 1.f;
+    }
+    const float c = cos_t[(long long)pos * half + fi], sn = sin_t[(long long)pos * half + fi];
+    x[j] = bf2f(f2bf(x[j] * c + sgn * bf2f(row[partner]) * sn));
+  }
+}
 
 // LPT lanes cooperate on one token row (8 dims per lane); TPW = 64/LPT tokens per
 // wave step; G query heads share each K/V row (GQA group).
@@ -166,6 +199,26 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
   const long long kvoff = (PAGED ? 0 : (long long)seq * p.cs_slot) + hk * p.cs_head + dslot * 8;
   const bf16_t* kb = p.kc + kvoff;
   const bf16_t* vb = p.vc + kvoff;
+  const int pnew = L - 1;  // the new token's position (fused prep)
+  // Q first: its loads (and RoPE table reads) are in flight while the page ids are staged
+  float q[G][8];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    if (dact) {
+      const bf16_t* qrow = p.q + b * p.q_bs + (long long)(hk * G + g) * D;
+      load8(qrow + dslot * 8, q[g]);
+      if (p.fused && p.rot > 0) rope8(qrow, dslot * 8, q[g], pnew, p.rot, p.interleaved, p.cos_t, p.sin_t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) q[g][j] *= p.scale;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) q[g][j] = 0.f;
+    }
+  }
+  float slope[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) slope[g] = p.alibi ? p.alibi[hk * G + g] : 0.f;
+
   // paged: this split's page ids staged in LDS once (chunk <= 1024 tokens, pages >= 16 tokens), so a
   // token's address costs an LDS read instead of a dependent global load in front of every K/V load
   __shared__ int pg[1024 / 16 + 2];
@@ -183,21 +236,29 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
     return (long long)t * p.cs_pos;
   };
 
-  float q[G][8];
+  // fused prep: the split holding the new token (position L-1) rotates its K, appends K and V to the
+  // cache, and serves that row from LDS (no other split reads position L-1)
+  __shared__ float knew[256], vnew[256];
+  const bool own_new = p.fused && c1 == L;
+  if (own_new) {
+    if (tid < ND) {
+      const bf16_t* krow = p.q + b * p.q_bs + (long long)(p.H + hk) * D;
+      const bf16_t* vrow = p.q + b * p.q_bs + (long long)(p.H + p.Hkv + hk) * D;
+      float kx[8], vx[8];
+      load8(krow + tid * 8, kx);
+      load8(vrow + tid * 8, vx);
+      if (p.rot > 0) rope8(krow, tid * 8, kx, pnew, p.rot, p.interleaved, p.cos_t, p.sin_t);
+      const long long o = toff(pnew) + hk * p.cs_head + tid * 8;  // toff: offset inside the sequence
+      store8(const_cast<bf16_t*>(p.kc) + (PAGED ? 0 : (long long)seq * p.cs_slot) + o, kx);
+      store8(const_cast<bf16_t*>(p.vc) + (PAGED ? 0 : (long long)seq * p.cs_slot) + o, vx);
 #pragma unroll
-  for (int g = 0; g < G; ++g) {
-    if (dact) {
-      load8(p.q + b * p.q_bs + (long long)(hk * G + g) * D + dslot * 8, q[g]);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) q[g][j] *= p.scale;
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) q[g][j] = 0.f;
+      for (int j = 0; j < 8; ++j) {
+        knew[tid * 8 + j] = kx[j];
+        vnew[tid * 8 + j] = vx[j];
+      }
     }
+    __syncthreads();
   }
-  float slope[G];
-#pragma unroll
-  for (int g = 0; g < G; ++g) slope[g] = p.alibi ? p.alibi[hk * G + g] : 0.f;
 
   // V rows of the first P.V iteration, issued together with the K loads: they do not depend on the
   // scores, so a chunk of <= TPB*U tokens (every B=1 split) costs one HBM round trip, not two
@@ -206,7 +267,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int t = tv0 + u * TPB;
-    if (t < c1 && dact) vpre[u] = *reinterpret_cast<const U16x8*>(vb + toff(t));
+    if (t < c1 && dact && !(own_new && t == pnew)) vpre[u] = *reinterpret_cast<const U16x8*>(vb + toff(t));
   }
 
   // ---- scores
@@ -216,7 +277,12 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
     for (int u = 0; u < U; ++u) {
       const int t = t0 + u * TPB;
       if (t < c1 && dact) {
-        load8(kb + toff(t), kr[u]);
+        if (own_new && t == pnew) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) kr[u][j] = knew[dslot * 8 + j];
+        } else {
+          load8(kb + toff(t), kr[u]);
+        }
       } else {
 #pragma unroll
         for (int j = 0; j < 8; ++j) kr[u][j] = 0.f;
@@ -270,7 +336,10 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
     for (int u = 0; u < U; ++u) {
       const int t = t0 + u * TPB;
       if (t < c1 && dact) {
-        if (t0 == tv0) {
+        if (own_new && t == pnew) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) vr[u][j] = vnew[dslot * 8 + j];
+        } else if (t0 == tv0) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) vr[u][j] = bf2f(vpre[u].v[j]);
         } else {
@@ -351,7 +420,10 @@ __global__ __launch_bounds__(256) void decode_combine_kernel(const float* __rest
   for (int d = tid; d < D; d += 256) {
     float acc = 0.f;
 #pragma unroll 8
-    for (int s = 0; s < nsplit; ++s) acc = fmaf(wsp[s], o[(long long)s * D + d], acc);
+    for (int s = 0; s < nsplit; ++s) {
+      const float ov = o[(long long)s * D + d];   // never written for an empty split: may hold NaN
+      acc = wsp[s] > 0.f ? fmaf(wsp[s], ov, acc) : acc;
+    }
     out[b * o_bs + (long long)h * D + d] = f2bf(acc * inv);
   }
 }
@@ -395,12 +467,44 @@ static int launch_decode_g(const DecodeParams& p, int G, int B, int nsplit, hipS
   return 3;
 }
 
+static int decode_attn_launch(DecodeParams p, float* ws, long long ws_floats, int B, int max_kv, int chunk,
+                              hipStream_t stream);
+
 KCA_API int kca_decode_attn(const void* q, long long q_bs, const void* kc, const void* vc,
                             long long cs_slot, long long cs_head, long long cs_pos,
                             const int* slots, const int* kv_lens, void* out, long long o_bs,
                             float* ws, long long ws_floats, int B, int H, int Hkv, int D,
                             int max_kv, int chunk, float scale, const float* alibi, const int* tbl,
                             int tbl_stride, int ps_shift, hipStream_t stream) {
+  DecodeParams p{(const bf16_t*)q, q_bs, (const bf16_t*)kc, (const bf16_t*)vc, cs_slot, cs_head,
+                 cs_pos, slots, kv_lens, (bf16_t*)out, o_bs, nullptr, nullptr, alibi, tbl, tbl_stride, ps_shift,
+                 H, Hkv, D, chunk, scale, 0, 0, 0, nullptr, nullptr};
+  return decode_attn_launch(p, ws, ws_floats, B, max_kv, chunk, stream);
+}
+
+// Fused decode prep + attention: qkv is the fused QKV GEMM output [B, (H+2Hkv)*D]
+// (row stride ld); RoPE (rot dims, GPT-J interleaved or NeoX rotate-half) of the
+// new token at position kv_lens[b]-1, its K/V appended to the cache, then the
+// split-K attention -- replaces kca_decode_prep + kca_decode_attn.
+KCA_API int kca_decode_prep_attn(const void* qkv, long long ld, const void* kc, const void* vc,
+                                 long long cs_slot, long long cs_head, long long cs_pos,
+                                 const int* slots, const int* kv_lens, void* out, long long o_bs,
+                                 float* ws, long long ws_floats, int B, int H, int Hkv, int D,
+                                 int max_kv, int chunk, float scale, const float* alibi, const int* tbl,
+                                 int tbl_stride, int ps_shift, int rot, int interleaved, const float* cos_t,
+                                 const float* sin_t, hipStream_t stream) {
+  if (rot > D || (rot & 1) || (rot > 0 && (!cos_t || !sin_t))) return 8;
+  DecodeParams p{(const bf16_t*)qkv, ld, (const bf16_t*)kc, (const bf16_t*)vc, cs_slot, cs_head,
+                 cs_pos, slots, kv_lens, (bf16_t*)out, o_bs, nullptr, nullptr, alibi, tbl, tbl_stride, ps_shift,
+                 H, Hkv, D, chunk, scale, 1, rot, interleaved, cos_t, sin_t};
+  return decode_attn_launch(p, ws, ws_floats, B, max_kv, chunk, stream);
+}
+
+static int decode_attn_launch(DecodeParams p, float* ws, long long ws_floats, int B, int max_kv, int chunk,
+                              hipStream_t stream) {
+  const int H = p.H, Hkv = p.Hkv, D = p.D;
+  const int* tbl = p.tbl;
+  const int ps_shift = p.ps_shift, tbl_stride = p.tbl_stride;
   if (D % 8 || D > 256 || H % Hkv || B <= 0 || max_kv <= 0) return 1;
   if (tbl && (ps_shift < 4 || ps_shift > 20 || tbl_stride <= 0)) return 5;  // pages of >= 16 tokens
   if (chunk <= 0) chunk = kca_decode_chunk(B, Hkv, max_kv);
@@ -409,9 +513,7 @@ KCA_API int kca_decode_attn(const void* q, long long q_bs, const void* kc, const
   if (tbl && chunk > 1024) return 6;  // the LDS page-id stage holds 1024 tokens of pages
   const int nsplit = (max_kv + chunk - 1) / chunk;
   if (nsplit > 1024) return 7;  // combine keeps the split weights in LDS
-  DecodeParams p{(const bf16_t*)q, q_bs, (const bf16_t*)kc, (const bf16_t*)vc, cs_slot, cs_head,
-                 cs_pos, slots, kv_lens, (bf16_t*)out, o_bs, nullptr, nullptr, alibi, tbl, tbl_stride, ps_shift,
-                 H, Hkv, D, chunk, scale};
+  p.chunk = chunk;
   if (nsplit > 1) {
     const long long need = (long long)B * H * nsplit * (D + 2);
     if (!ws || ws_floats < need) return 4;
@@ -426,7 +528,7 @@ KCA_API int kca_decode_attn(const void* q, long long q_bs, const void* kc, const
   if (rc) return rc;
   if (nsplit > 1)
     hipLaunchKernelGGL(decode_combine_kernel, dim3(B * H), dim3(256), 0, stream, p.ws_o, p.ws_ml,
-                       (bf16_t*)out, o_bs, H, D, nsplit);
+                       p.out, p.o_bs, H, D, nsplit);
   return 0;
 }
 

@@ -332,6 +332,86 @@ __global__ __launch_bounds__(256) void gemv1_kernel(const bf16_t* __restrict__ x
   }
 }
 
+// Decode LayerNorm of a few rows (one workgroup per row, the row in
+// registers): h = x (+ r1) (+ r2) -> h_out (bf16), xn = LN(h) -> xn_out. All
+// five operand streams are requested in one round, then two block
+// reductions -- the M = 1 decode step normalises once here and streams the
+// weights with the plain gemv1 kernel (ops/gemv.py:_LN_SPLIT_M1).
+template <int PER>
+__global__ __launch_bounds__(256) void ln_rows_kernel(const bf16_t* __restrict__ x, long long ldx, LnArgs a,
+                                                      int K) {
+  __shared__ float red[16];
+  const int tid = threadIdx.x, m = blockIdx.x;
+  float v[PER][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int k = (i * 256 + tid) * 8;
+    if (k < K) {
+      float t[8];
+      load8(x + m * ldx + k, v[i]);
+      if (a.r1) {
+        load8(a.r1 + m * a.ldh + k, t);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[i][j] += t[j];
+      }
+      if (a.r2) {
+        load8(a.r2 + m * a.ldh + k, t);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[i][j] += t[j];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        v[i][j] = bf2f(f2bf(v[i][j]));
+        s += v[i][j];
+      }
+      if (a.h_out) store8(a.h_out + m * a.ldh + k, v[i]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
+    }
+  }
+  const float mean = block_sum(s, red) / K;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    if ((i * 256 + tid) * 8 >= K) continue;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) q += (v[i][j] - mean) * (v[i][j] - mean);
+  }
+  const float rstd = rsqrtf(block_sum(q, red + 8) / K + a.eps);
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int k = (i * 256 + tid) * 8;
+    if (k >= K) continue;
+    float g[8], bb[8];
+    load8(a.gamma + k, g);
+    if (a.beta) load8(a.beta + k, bb);
+    else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bb[j] = 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[i][j] = (v[i][j] - mean) * rstd * g[j] + bb[j];
+    store8(a.xn_out + (long long)m * K + k, v[i]);
+  }
+}
+
+KCA_API int kca_ln_rows(const void* x, long long ldx, const void* r1, const void* r2, void* h_out, long long ldh,
+                        const void* gamma, const void* beta, float eps, void* xn_out, int M, int K,
+                        hipStream_t stream) {
+  if (M < 1 || K % 8 || K > 16384 || ldx % 8 || ldh % 8 || !xn_out) return 1;
+  if (((uintptr_t)x | (uintptr_t)r1 | (uintptr_t)r2 | (uintptr_t)h_out | (uintptr_t)gamma | (uintptr_t)beta |
+       (uintptr_t)xn_out) & 15) return 2;
+  LnArgs a{(const bf16_t*)r1, (const bf16_t*)r2, (bf16_t*)h_out, ldh, (const bf16_t*)gamma, (const bf16_t*)beta,
+           eps, (bf16_t*)xn_out};
+  const int per = (K + 2047) / 2048;
+  if (per <= 2) hipLaunchKernelGGL((ln_rows_kernel<2>), dim3(M), dim3(256), 0, stream, (const bf16_t*)x, ldx, a, K);
+  else if (per <= 4) hipLaunchKernelGGL((ln_rows_kernel<4>), dim3(M), dim3(256), 0, stream, (const bf16_t*)x, ldx, a, K);
+  else hipLaunchKernelGGL((ln_rows_kernel<8>), dim3(M), dim3(256), 0, stream, (const bf16_t*)x, ldx, a, K);
+  return 0;
+}
+
 // 1 = split-K kernel for M == 1 (default), 0 = row-per-wave kernel (A/B)
 static int g_skinny_sk = 1;
 KCA_API int kca_skinny_set_splitk(int on) {

@@ -298,6 +298,16 @@ class ModelRunner:
         self._pool = None
         self._static: dict = {}
         self._windowed = any(getattr(b.attn, "window", 0) for b in model.h)
+        # parallel-residual models (GPT-J, NeoX): the MLP branch does not depend on attention, so at
+        # decode its two weight-streaming GEMVs run on a side stream while the latency-bound attention
+        # chain (split-K attention, combine, out-proj) runs on the main one -- both captured into the
+        # step's graph as a fork/join. Not under TP: two concurrent collectives could interleave
+        # differently across ranks.
+        from ..parallel.tensor_parallel import RowParallelLinear
+        tp = any(isinstance(mm, RowParallelLinear) for mm in model.modules())
+        self._par_mlp = (cfg.parallel_residual and on_gpu and not tp and not self.multi_device
+                         and os.environ.get("KCA_DECODE_PAR_MLP", "1") not in ("0", "false"))
+        self._side = torch.cuda.Stream(device=self.device) if self._par_mlp else None
 
     # ------------------------------------------------------------- prefill
     @torch.no_grad()
@@ -404,19 +414,38 @@ class ModelRunner:
                 qkv, h, xn = self._ln_lin(blk.ln_1, h, pending, at.qkv, want_xn=True)
             else:
                 qkv, h = self._ln_lin(blk.ln_1, h, pending, at.qkv)
-            kc, vc, tbl = self.cache.k[li], self.cache.v[li], self.cache.table_on(dev)
-            cos, sin = self._rope[dev]
-            dops.decode_prep(qkv, self.H, self.Hkv, self.D, self.rot, cfg.rotary_interleaved, cos, sin, pos,
-                             slots, kc, vc, block_table=tbl)
-            if at.window:
-                o = self._windowed_decode(qkv, kc, vc, slots, kv_lens, at)
-            else:
-                o = dops.decode_attention(qkv, kc, vc, slots, kv_lens, self.H, max_kv, at.scale, at.alibi,
-                                          out=obuf, ws=ws, block_table=tbl)
-            a = self._lin(at.out, o)
             mlp = blk.mlp
             act = 1 if mlp.approx in ("tanh", True) else 2
-            if shared:
+            side_out = None
+            if self._par_mlp:  # fork: MLP branch on the side stream
+                cur = torch.cuda.current_stream()
+                self._side.wait_stream(cur)
+                with torch.cuda.stream(self._side):
+                    if shared:
+                        xm = xn
+                    else:
+                        xm, _ = self._ln_lin(blk.ln_2, h, (), mlp.fc_in, act)  # NeoX: ln_2 + fc_in fused
+                    side_out = self._lin(mlp.fc_out, self._lin(mlp.fc_in, xm, act) if shared else xm)
+                if not torch.cuda.is_current_stream_capturing():  # eager: keep cross-stream buffers alive
+                    xm.record_stream(self._side)
+                    h.record_stream(self._side)
+            kc, vc, tbl = self.cache.k[li], self.cache.v[li], self.cache.table_on(dev)
+            cos, sin = self._rope[dev]
+            if at.window:
+                dops.decode_prep(qkv, self.H, self.Hkv, self.D, self.rot, cfg.rotary_interleaved, cos, sin, pos,
+                                 slots, kc, vc, block_table=tbl)
+                o = self._windowed_decode(qkv, kc, vc, slots, kv_lens, at)
+            else:  # RoPE + cache append + split-K attention (one launch on the GPU)
+                o = dops.decode_prep_attention(qkv, self.H, self.Hkv, self.D, self.rot, cfg.rotary_interleaved,
+                                               cos, sin, pos, slots, kc, vc, kv_lens, max_kv, at.scale, at.alibi,
+                                               out=obuf, ws=ws, block_table=tbl)
+            a = self._lin(at.out, o)
+            if side_out is not None:  # join
+                cur.wait_stream(self._side)
+                if not torch.cuda.is_current_stream_capturing():
+                    side_out.record_stream(cur)
+                pending = (a, side_out)
+            elif shared:
                 pending = (a, self._lin(mlp.fc_out, self._lin(mlp.fc_in, xn, act)))
             elif cfg.parallel_residual:
                 f, _ = self._ln_lin(blk.ln_2, h, (), mlp.fc_in, act)

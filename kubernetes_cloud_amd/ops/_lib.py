@@ -72,9 +72,12 @@ _SIGS = {
     "kca_skinny_gemm": [P, LL, P, P, P, LL, I, I, I, I, P],
     "kca_skinny_set_splitk": [I],
     "kca_ln_skinny_gemm": [P, LL, P, P, P, LL, P, P, F, P, P, P, LL, I, I, I, I, P, P],
+    "kca_ln_rows": [P, LL, P, P, P, LL, P, P, F, P, I, I, P],
     "kca_decode_prep": [P, LL, I, I, I, I, I, I, P, P, P, P, P, P, LL, LL, LL, P, I, I, P],
     "kca_decode_chunk": [I, I, I],
     "kca_decode_attn": [P, LL, P, P, LL, LL, LL, P, P, P, LL, P, LL, I, I, I, I, I, I, F, P, P, I, I, P],
+    "kca_decode_prep_attn": [P, LL, P, P, LL, LL, LL, P, P, P, LL, P, LL, I, I, I, I, I, I, F, P, P, I, I, I, I, P,
+                             P, P],
     "kca_sample_logits": [P, LL, I, I, I, P, P, P, P, P, P, P, I, P, LL, P, P, P, P, P],
 }
 

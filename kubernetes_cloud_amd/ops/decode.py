@@ -142,6 +142,41 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
     return decode_attention_reference(q, k_cache, v_cache, slots, kv_lens, H, scale, alibi, out, block_table)
 
 
+def decode_prep_attention(qkv: torch.Tensor, n_heads: int, kv_heads: int, head_dim: int, rot: int,
+                          interleaved: bool, cos: torch.Tensor | None, sin: torch.Tensor | None,
+                          pos: torch.Tensor, slots: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                          kv_lens: torch.Tensor, max_kv: int, scale: float | None = None,
+                          alibi: torch.Tensor | None = None, out: torch.Tensor | None = None,
+                          ws: torch.Tensor | None = None, block_table: torch.Tensor | None = None) -> torch.Tensor:
+    """``decode_prep`` + ``decode_attention`` for the decode step (kv_lens = pos + 1).
+    Native: ONE launch (``kca_decode_prep_attn``) that rotates Q itself and lets
+    the split holding the new token rotate and append K/V (the prep kernel's ~5 us
+    per layer at B=1 disappears); bit-identical to the two-kernel path."""
+    B = qkv.shape[0]
+    _, Hkv, L, D = k_cache.shape
+    H = n_heads
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if _lib.use_native(qkv, k_cache) and _lib.has("kca_decode_prep_attn"):
+        assert qkv.stride(-1) == 1 and k_cache.stride() == v_cache.stride()
+        assert kv_lens.dtype == torch.int32 and slots.dtype == torch.int32
+        if out is None:
+            out = torch.empty(B, H * D, device=qkv.device, dtype=qkv.dtype)
+        tbl, tstride, shift = _table_args(block_table, k_cache)
+        chunk = decode_chunk(B, Hkv, max_kv)
+        need = decode_ws_floats(B, H, Hkv, D, max_kv, chunk)
+        if need and (ws is None or ws.numel() < need):
+            ws = torch.empty(need, device=qkv.device, dtype=torch.float32)
+        _lib.call("kca_decode_prep_attn", qkv.data_ptr(), qkv.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+                  k_cache.stride(0), k_cache.stride(1), k_cache.stride(2), slots.data_ptr(), kv_lens.data_ptr(),
+                  out.data_ptr(), out.stride(0), _lib.ptr(ws), ws.numel() if ws is not None else 0, B, H, Hkv, D,
+                  max_kv, chunk, float(scale), _lib.ptr(alibi), tbl, tstride, shift, rot, int(interleaved),
+                  _lib.ptr(cos), _lib.ptr(sin), _lib.stream())
+        return out
+    decode_prep(qkv, H, Hkv, D, rot, interleaved, cos, sin, pos, slots, k_cache, v_cache, block_table)
+    return decode_attention(qkv, k_cache, v_cache, slots, kv_lens, H, max_kv, scale, alibi, out, ws,
+                            block_table=block_table)
+
+
 def decode_attention_reference(q, k_cache, v_cache, slots, kv_lens, n_heads, scale, alibi=None, out=None,
                                block_table=None):
     B = q.shape[0]
@@ -263,6 +298,6 @@ def sample_logits_reference(logits, temperature, top_k, top_p, rep_penalty=None,
     return ids, lps
 
 
-__all__ = ["decode_prep", "decode_attention", "decode_attention_reference", "decode_chunk", "gather_kv",
+__all__ = ["decode_prep", "decode_attention", "decode_prep_attention", "decode_attention_reference", "decode_chunk", "gather_kv",
            "decode_ws_floats", "sample_logits", "sample_logits_reference", "keep_mask_reference",
            "processed_logits_reference"]

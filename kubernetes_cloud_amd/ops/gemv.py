@@ -105,6 +105,18 @@ def ln_skinny_linear(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor | 
                   _lib.ptr(beta), float(eps), weight.data_ptr(), _lib.ptr(bias), y.data_ptr(), y.stride(0),
                   M, weight.shape[0], K, int(act), _lib.ptr(xn), _lib.stream())
         return (y, h, xn) if want_xn else (y, h)
+    if split and _lib.use_native(x, weight) and K % 8 == 0 and K <= 16384 and x.stride(1) == 1 \
+            and x.stride(0) % 8 == 0 and all(r.is_contiguous() and r.shape == x.shape for r in residuals) \
+            and gamma.is_contiguous() and (beta is None or beta.is_contiguous()) and len(residuals) <= 2:
+        h = torch.empty(M, K, device=x.device, dtype=x.dtype) if residuals else x
+        xn = torch.empty(M, K, device=x.device, dtype=x.dtype)
+        r1 = residuals[0] if residuals else None
+        r2 = residuals[1] if len(residuals) > 1 else None
+        _lib.call("kca_ln_rows", x.data_ptr(), x.stride(0), _lib.ptr(r1), _lib.ptr(r2),
+                  h.data_ptr() if residuals else None, h.stride(0) if residuals else K, gamma.data_ptr(),
+                  _lib.ptr(beta), float(eps), xn.data_ptr(), M, K, _lib.stream())
+        y = skinny_linear(xn, weight, bias, act)
+        return (y, h, xn) if want_xn else (y, h)
     from .norms import layer_norm
     if residuals:
         xn, h = layer_norm(x, gamma, beta, eps, residual=residuals)

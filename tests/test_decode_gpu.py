@@ -196,8 +196,14 @@ def test_skinny_gemm_row_per_wave_kernel(M):
 @pytest.mark.parametrize("M,N,K", [(1, 12288, 4096), (2, 4096, 4096), (4, 4096, 4096), (1, 5376, 14336),
                                    (2, 1024, 14336), (3, 4096, 4096)])
 @pytest.mark.parametrize("nres", [0, 1, 2])
-def test_ln_skinny_gemm(M, N, K, nres):
+@pytest.mark.parametrize("split", [False, True])
+def test_ln_skinny_gemm(M, N, K, nres, split, monkeypatch):
+    """split: at M = 1 the LN runs once (kca_ln_rows) before the plain GEMV;
+    otherwise every GEMV workgroup normalises its activation slice itself."""
     from kubernetes_cloud_amd.ops import gemv
+    monkeypatch.setattr(gemv, "_LN_SPLIT_M1", split)
+    if split and M != 1:
+        pytest.skip("the split path is M == 1 only")
     torch.manual_seed(M * 7 + N + K + nres)
     x = torch.randn(M, K, device=dev).to(torch.bfloat16)
     res = tuple(torch.randn(M, K, device=dev).to(torch.bfloat16) for _ in range(nres))
@@ -353,3 +359,33 @@ def test_layer_split_gpu_cpu_engine(tmp_path):
     assert (a - b).abs().max() < 0.1 * b.abs().max()
     out = eng.generate([[5, 9, 2], [1, 2, 3, 4, 5]], SamplingParams(max_new_tokens=6, do_sample=False))
     assert all(len(x.output) == 6 for x in out)
+
+
+@pytest.mark.parametrize("D,rot,inter,G,PS", [(256, 64, True, 1, 64), (256, 64, True, 1, 0), (128, 32, False, 4, 16),
+                                              (80, 20, False, 1, 0), (64, 0, False, 2, 32)])
+def test_decode_prep_attention_fused_equals_two_kernels(D, rot, inter, G, PS):
+    """kca_decode_prep_attn (one launch) == kca_decode_prep + kca_decode_attn, bit for bit:
+    same rotated Q, same appended K/V rows, same attention output."""
+    torch.manual_seed(D + rot + G)
+    B, Hkv, L = 5, 4, 512
+    H = Hkv * G
+    kc = torch.randn(B + 1, Hkv, L, D, device=dev).to(torch.bfloat16)
+    vc = torch.randn_like(kc)
+    tbl = None
+    if PS:
+        kc, tbl = _paginate(kc, PS, 3)
+        vc, _ = _paginate(vc, PS, 3)
+    qkv = torch.randn(B, (H + 2 * Hkv) * D, device=dev).to(torch.bfloat16)
+    slots = torch.tensor([3, 0, 5, 1, 2], device=dev, dtype=torch.int32)
+    pos = torch.tensor([0, 511, 200, 63, 64], device=dev, dtype=torch.int32)
+    kl = pos + 1
+    cos, sin = rope_tables(rot, L, 10000.0, dev) if rot else (None, None)
+    k1, v1, k2, v2 = kc.clone(), vc.clone(), kc.clone(), vc.clone()
+    q1, q2 = qkv.clone(), qkv.clone()
+    dops.decode_prep(q1, H, Hkv, D, rot, inter, cos, sin, pos, slots, k1, v1, block_table=tbl)
+    a = dops.decode_attention(q1, k1, v1, slots, kl, H, L, block_table=tbl)
+    b = dops.decode_prep_attention(q2, H, Hkv, D, rot, inter, cos, sin, pos, slots, k2, v2, kl, L, block_table=tbl)
+    torch.cuda.synchronize()
+    assert torch.equal(k1, k2) and torch.equal(v1, v2)
+    assert torch.equal(a, b)
+    assert torch.equal(q2, qkv)  # the fused kernel leaves the QKV buffer untouched
