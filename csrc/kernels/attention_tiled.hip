@@ -159,10 +159,19 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    // K fragments two k-steps ahead of their MFMA (pinned: hipcc otherwise waits lgkmcnt(1))
+    bf16x8 fa[3];
+    fa[0] = lds_b128(Ks, kb_e);
+    fa[1] = lds_b128(Ks, kb_o);
+    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
 #pragma unroll
     for (int s = 0; s < D / 16; ++s) {
-      const bf16x8 a = lds_b128(Ks, ((s & 1) ? kb_o : kb_e) + 512 * (s >> 1));
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s], acc, 0, 0, 0);
+      if (s + 2 < D / 16) {
+        fa[(s + 2) % 3] = lds_b128(Ks, (((s + 2) & 1) ? kb_o : kb_e) + 512 * ((s + 2) >> 1));
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s % 3], qf[s], acc, 0, 0, 0);
+      __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
     }
     return acc;
   };
@@ -226,14 +235,24 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel
       pf1[r] = (__bf16)e1;
     }
     lsum += ps;
+    {  // O^T += V^T P^T, V^T fragments one d-block ahead of their MFMAs
+      auto vfrag = [&](int db, int s) {
+        return cat8(lds_tr4(Vs, vb_1 + 2 * s * 16 * D + 512 * db), lds_tr4(Vs, vb_2 + 2 * s * 16 * D + 512 * db));
+      };
+      bf16x8 va[2], vb2[2];
+      va[0] = vfrag(0, 0);
+      vb2[0] = vfrag(0, 1);
+      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
 #pragma unroll
-    for (int db = 0; db < D / 32; ++db) {
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int o1 = vb_1 + 2 * s * 16 * D + 512 * db;
-        const int o2 = vb_2 + 2 * s * 16 * D + 512 * db;
-        const bf16x8 a = cat8(lds_tr4(Vs, o1), lds_tr4(Vs, o2));
-        oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, s ? pf1 : pf0, oacc[db], 0, 0, 0);
+      for (int db = 0; db < D / 32; ++db) {
+        if (db + 1 < D / 32) {
+          va[(db + 1) & 1] = vfrag(db + 1, 0);
+          vb2[(db + 1) & 1] = vfrag(db + 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+        }
+        oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va[db & 1], pf0, oacc[db], 0, 0, 0);
+        oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vb2[db & 1], pf1, oacc[db], 0, 0, 0);
+        __builtin_amdgcn_sched_group_barrier(0x8, 2, 0);
       }
     }
     sa = sb;
@@ -395,10 +414,26 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq_tiled_kernel(FastBwdParams
     f32x16 st, dpt;
 #pragma unroll
     for (int r = 0; r < 16; ++r) { st[r] = 0.f; dpt[r] = 0.f; }
+    // K / V row fragments of k-step s+2 requested before the MFMAs of step s (pinned), so no MFMA
+    // waits out an LDS round trip (see the dK/dV kernel)
+    {
+      bf16x8 fk[3], fv[3];
+      fk[0] = row_frag<D>(Ks, be, bo, 0);
+      fv[0] = row_frag<D>(Vs, be, bo, 0);
+      fk[1] = row_frag<D>(Ks, be, bo, 1);
+      fv[1] = row_frag<D>(Vs, be, bo, 1);
+      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
 #pragma unroll
-    for (int s = 0; s < D / 16; ++s) {
-      st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(Ks, be, bo, s), qf[s], st, 0, 0, 0);
-      dpt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(Vs, be, bo, s), gf[s], dpt, 0, 0, 0);
+      for (int s = 0; s < D / 16; ++s) {
+        if (s + 2 < D / 16) {
+          fk[(s + 2) % 3] = row_frag<D>(Ks, be, bo, s + 2);
+          fv[(s + 2) % 3] = row_frag<D>(Vs, be, bo, s + 2);
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        }
+        st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fk[s % 3], qf[s], st, 0, 0, 0);
+        dpt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fv[s % 3], gf[s], dpt, 0, 0, 0);
+        __builtin_amdgcn_sched_group_barrier(0x8, 2, 0);
+      }
     }
     const int lim = qrow + off - k0 - 4 * hh;  // visible key offsets (r&3)+8(r>>2) <= lim
     bf16x8 d0, d1;
@@ -413,10 +448,22 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq_tiled_kernel(FastBwdParams
       d0[r] = (__bf16)(p0 * (dpt[r] - dl));
       d1[r] = (__bf16)(p1 * (dpt[r + 8] - dl));
     }
+    {
+      bf16x8 t0[2], t1[2];
+      t0[0] = tr_frag<D>(Ks, b1, b2, 0, 0);
+      t1[0] = tr_frag<D>(Ks, b1, b2, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
 #pragma unroll
-    for (int db = 0; db < D / 32; ++db) {
-      dq[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(Ks, b1, b2, 0, db), d0, dq[db], 0, 0, 0);
-      dq[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(Ks, b1, b2, 1, db), d1, dq[db], 0, 0, 0);
+      for (int db = 0; db < D / 32; ++db) {
+        if (db + 1 < D / 32) {
+          t0[(db + 1) & 1] = tr_frag<D>(Ks, b1, b2, 0, db + 1);
+          t1[(db + 1) & 1] = tr_frag<D>(Ks, b1, b2, 1, db + 1);
+          __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+        }
+        dq[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(t0[db & 1], d0, dq[db], 0, 0, 0);
+        dq[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(t1[db & 1], d1, dq[db], 0, 0, 0);
+        __builtin_amdgcn_sched_group_barrier(0x8, 2, 0);
+      }
     }
     asm volatile("" ::: "memory");
     if (t + 1 < ntiles) stage_store<CPT, RPI, D>(sk, sv, smem + ((t + 1) & 1) * 2 * TILE, st_row, st_ch);
@@ -520,11 +567,32 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_tiled_kernel(FastBwdPara
     f32x16 sacc, dpacc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) { sacc[r] = 0.f; dpacc[r] = 0.f; }
+    // S = Q.K^T, dP = dO.V^T with the three LDS fragments of k-step s+1 requested before the two
+    // MFMAs of step s (pinned by sched_group_barrier): at ~445 live registers hipcc otherwise
+    // issues each read right before its MFMA behind an lgkmcnt(0) -- 63 of this kernel's 64 MFMAs
+    // waited out a full LDS round trip (20 % MFMA busy, profiles/pmc_kernels_r1.md).
+    {
+      bf16x8 fq0 = row_frag<D>(Qs, be, bo, 0), fg0 = row_frag<D>(Gs, be, bo, 0), fv0 = row_frag<D>(vimg, be, bo, 0);
+      bf16x8 fq1, fg1, fv1;
+      __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
 #pragma unroll
-    for (int s = 0; s < D / 16; ++s) {
-      sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(Qs, be, bo, s), kf[s], sacc, 0, 0, 0);
-      dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(Gs, be, bo, s),
-                                                      row_frag<D>(vimg, be, bo, s), dpacc, 0, 0, 0);
+      for (int s = 0; s < D / 16; ++s) {
+        bf16x8& cq = (s & 1) ? fq1 : fq0;
+        bf16x8& cg = (s & 1) ? fg1 : fg0;
+        bf16x8& cv = (s & 1) ? fv1 : fv0;
+        bf16x8& nq = (s & 1) ? fq0 : fq1;
+        bf16x8& ng = (s & 1) ? fg0 : fg1;
+        bf16x8& nv = (s & 1) ? fv0 : fv1;
+        if (s + 1 < D / 16) {
+          nq = row_frag<D>(Qs, be, bo, s + 1);
+          ng = row_frag<D>(Gs, be, bo, s + 1);
+          nv = row_frag<D>(vimg, be, bo, s + 1);
+          __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+        }
+        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cq, kf[s], sacc, 0, 0, 0);
+        dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cg, cv, dpacc, 0, 0, 0);
+        __builtin_amdgcn_sched_group_barrier(0x8, 2, 0);
+      }
     }
     // rows q = qt + 8g + 4hh + j (g = r>>2, j = r&3): lse / delta as float4;
     // visible iff key <= q + off, i.e. 8g + j >= key - qt - off - 4hh
@@ -546,12 +614,36 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_tiled_kernel(FastBwdPara
         else { p1[r - 8] = (__bf16)pr; s1[r - 8] = (__bf16)ds; }
       }
     }
+    // dV^T += dO^T.P, dK^T += Q^T.dS: the 8 transposed reads of block db+1 in flight under the 4
+    // MFMAs of block db (same pinning)
+    {
+      bf16x8 a0 = tr_frag<D>(Gs, b1, b2, 0, 0), a1 = tr_frag<D>(Gs, b1, b2, 1, 0);
+      bf16x8 a2 = tr_frag<D>(Qs, b1, b2, 0, 0), a3 = tr_frag<D>(Qs, b1, b2, 1, 0);
+      bf16x8 n0, n1, n2, n3;
+      __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
 #pragma unroll
-    for (int db = 0; db < D / 32; ++db) {
-      dv[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(Gs, b1, b2, 0, db), p0, dv[db], 0, 0, 0);
-      dv[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(Gs, b1, b2, 1, db), p1, dv[db], 0, 0, 0);
-      dk[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(Qs, b1, b2, 0, db), s0, dk[db], 0, 0, 0);
-      dk[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(Qs, b1, b2, 1, db), s1, dk[db], 0, 0, 0);
+      for (int db = 0; db < D / 32; ++db) {
+        bf16x8& c0 = (db & 1) ? n0 : a0;
+        bf16x8& c1 = (db & 1) ? n1 : a1;
+        bf16x8& c2 = (db & 1) ? n2 : a2;
+        bf16x8& c3 = (db & 1) ? n3 : a3;
+        bf16x8& x0 = (db & 1) ? a0 : n0;
+        bf16x8& x1 = (db & 1) ? a1 : n1;
+        bf16x8& x2 = (db & 1) ? a2 : n2;
+        bf16x8& x3 = (db & 1) ? a3 : n3;
+        if (db + 1 < D / 32) {
+          x0 = tr_frag<D>(Gs, b1, b2, 0, db + 1);
+          x1 = tr_frag<D>(Gs, b1, b2, 1, db + 1);
+          x2 = tr_frag<D>(Qs, b1, b2, 0, db + 1);
+          x3 = tr_frag<D>(Qs, b1, b2, 1, db + 1);
+          __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+        }
+        dv[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c0, p0, dv[db], 0, 0, 0);
+        dv[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c1, p1, dv[db], 0, 0, 0);
+        dk[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c2, s0, dk[db], 0, 0, 0);
+        dk[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c3, s1, dk[db], 0, 0, 0);
+        __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
+      }
     }
     asm volatile("" ::: "memory");
     if (it + 1 < total) KCA_DKDV_STORE((it + 1) & 1);

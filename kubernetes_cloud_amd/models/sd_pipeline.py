@@ -263,6 +263,62 @@ class StableDiffusionPipeline:
                                   dtype=torch.float32).to(dev)
         x = latents.to(dev).float() * sch.init_noise_sigma
         run = self._runner()
+        if self._fused_sampler_ok(sch, dev):
+            x = self._sample_fused(run, sch, x, ctx, guidance_scale if cfg else None)
+        else:
+            x = self._sample_torch(run, sch, x, ctx, guidance_scale if cfg else None)
+        if output_type == "latent":
+            return x
+        img = self.vae.decode((x / self.scaling_factor).to(dt)).float()
+        if output_type == "tensor":
+            return img
+        from ..data.images import to_pil
+        return to_pil(img)
+
+    @staticmethod
+    def _fused_sampler_ok(sch, dev) -> bool:
+        import os
+
+        from ..ops import _lib
+        from .schedulers import LMSDiscreteScheduler
+        return (dev.type == "cuda" and isinstance(sch, LMSDiscreteScheduler) and _lib.has("kca_sd_lms_step")
+                and os.environ.get("KCA_SD_FUSED_STEP", "1") not in ("0", "false"))
+
+    def _sample_fused(self, run, sch, x, ctx, guidance):
+        """LMS / Euler sampling with one fused kernel per step between UNet replays
+        (ops/sd_step.py): CFG combine + multistep update + the next scaled bf16
+        UNet input, instead of ~15 elementwise launches."""
+        from ..ops.sd_step import lms_step
+        from .schedulers import EulerDiscreteScheduler
+        dev, dt = x.device, self.dtype
+        euler = isinstance(sch, EulerDiscreteScheduler)
+        order = 1 if euler else 4
+        x = x.contiguous(memory_format=torch.channels_last) if x.dim() == 4 else x.contiguous()
+        ring = torch.zeros((order, x.numel()), device=dev, dtype=torch.float32)
+        sig = sch.sigmas.tolist()
+        xin = sch.scale_model_input(torch.cat([x, x]) if guidance is not None else x, sch.timesteps[0]).to(dt)
+        xin = xin.contiguous(memory_format=torch.channels_last) if xin.dim() == 4 else xin
+        n = len(sch.timesteps)
+        for i, t in enumerate(sch.timesteps):
+            tt = torch.full((xin.shape[0],), float(t), device=dev)
+            eps = run(xin, tt, ctx)
+            if eps.dtype != torch.bfloat16:
+                eps = eps.to(torch.bfloat16)
+            if eps.stride()[1:] != x.stride()[1:]:
+                eps = eps.contiguous(memory_format=torch.channels_last) if eps.dim() == 4 else eps.contiguous()
+            o = 1 if euler else min(i + 1, order)
+            coefs = [sig[i + 1] - sig[i]] if euler else [sch._coef(o, i, j) for j in range(o)]
+            last = i + 1 == n
+            nxt = None if last else torch.empty_like(xin)
+            lms_step(eps, x, ring, coefs, i % order, sig[i], guidance, sch.prediction_type,
+                     None if last else 1.0 / (sig[i + 1] ** 2 + 1) ** 0.5, nxt)
+            xin = nxt
+        return x.contiguous()
+
+    def _sample_torch(self, run, sch, x, ctx, guidance):
+        dev, dt = x.device, self.dtype
+        cfg = guidance is not None
+        guidance_scale = guidance
         for t in sch.timesteps:
             xin = torch.cat([x, x]) if cfg else x
             xin = sch.scale_model_input(xin, t).to(dt)
@@ -272,13 +328,7 @@ class StableDiffusionPipeline:
                 eu, ec = eps.chunk(2)
                 eps = eu + guidance_scale * (ec - eu)
             x = sch.step(eps, t, x).float()
-        if output_type == "latent":
-            return x
-        img = self.vae.decode((x / self.scaling_factor).to(dt)).float()
-        if output_type == "tensor":
-            return img
-        from ..data.images import to_pil
-        return to_pil(img)
+        return x
 
 
 def serialize_pipeline(pipe: StableDiffusionPipeline, out_dir: str, dtype: torch.dtype | None = None):

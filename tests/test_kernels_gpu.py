@@ -658,3 +658,34 @@ def test_vae_wide_head_attention_bf16_gemms():
     ref = torch.softmax(qb @ kb.transpose(1, 2) * 512 ** -0.5, -1) @ vb
     assert o.dtype == torch.bfloat16
     assert _rel(o, ref) < 2e-2, _rel(o, ref)
+
+
+@pytest.mark.parametrize("cfg,pred,order", [(True, "epsilon", 4), (False, "epsilon", 1), (True, "v_prediction", 4)])
+def test_sd_fused_lms_step_matches_reference(cfg, pred, order):
+    """kca_sd_lms_step (CFG + LMS/Euler update + next scaled bf16 input) vs the
+    fp32 torch reference over several steps, channels-last latents."""
+    from kubernetes_cloud_amd.ops import _lib
+    from kubernetes_cloud_amd.ops.sd_step import lms_step, lms_step_reference
+    assert _lib.has("kca_sd_lms_step")
+    torch.manual_seed(0)
+    B = 4
+    cl = torch.channels_last
+    x_gpu = torch.randn(B, 4, 64, 64, device="cuda").contiguous(memory_format=cl)
+    x_ref = x_gpu.cpu().contiguous()
+    ring_g = torch.zeros(order, x_gpu.numel(), device="cuda")
+    ring_r = torch.zeros(order, x_ref.numel())
+    sig = [14.6, 9.2, 5.1, 2.7, 1.3, 0.6]
+    for i in range(5):
+        eps = (torch.randn((2 if cfg else 1) * B, 4, 64, 64, device="cuda")).to(torch.bfloat16).contiguous(memory_format=cl)
+        o = min(i + 1, order)
+        coefs = [(sig[i + 1] - sig[i]) / (j + 1) for j in range(o)]
+        xin_g = torch.empty_like(eps)
+        lms_step(eps, x_gpu, ring_g, coefs, i % order, sig[i], 7.5 if cfg else None, pred,
+                 1 / (sig[i + 1] ** 2 + 1) ** 0.5, xin_g)
+        xin_r = torch.empty(eps.shape, dtype=torch.bfloat16)
+        lms_step_reference(eps.cpu().contiguous(), x_ref, ring_r, coefs, i % order, sig[i], 7.5 if cfg else None,
+                           pred, 1 / (sig[i + 1] ** 2 + 1) ** 0.5, xin_r)
+        torch.cuda.synchronize()
+        assert torch.allclose(x_gpu.cpu(), x_ref, atol=1e-3, rtol=1e-4), (i, (x_gpu.cpu() - x_ref).abs().max())
+        # one bf16 ulp: out * in_scale may round to the other side of a bf16 boundary
+        assert torch.allclose(xin_g.cpu().float(), xin_r.float(), rtol=8e-3, atol=1e-3)

@@ -202,3 +202,31 @@ def test_dreambooth_class_images_sharded_across_ranks(tmp_path):
     two = run(2, str(tmp_path / "cls2"))
     one = run(1, str(tmp_path / "cls1"))
     assert len(two) == 3 and two == one
+
+
+@pytest.mark.parametrize("sched_cls,pred", [(LMSDiscreteScheduler, "epsilon"), (EulerDiscreteScheduler, "epsilon"),
+                                            (LMSDiscreteScheduler, "v_prediction")])
+@pytest.mark.parametrize("guidance", [None, 7.5])
+def test_fused_sampler_path_matches_scheduler_steps(sched_cls, pred, guidance):
+    """The fused sampler (ops/sd_step.py: CFG + LMS/Euler update + next scaled input in
+    one pass; its CPU reference here) follows the same trajectory as the
+    per-op pipeline loop around ``scheduler.step``."""
+    from kubernetes_cloud_amd.models.sd_pipeline import StableDiffusionPipeline
+    torch.manual_seed(0)
+    w = torch.randn(4, 4) * 0.3
+
+    def fake_unet(xin, t, ctx):  # deterministic, input- and time-dependent "noise prediction"
+        out = torch.einsum("bchw,cd->bdhw", xin.float(), w) * (1 + t.view(-1, 1, 1, 1) / 1000)
+        return out.to(torch.bfloat16)  # the UNet's output dtype
+
+    x0 = torch.randn(2, 4, 8, 8)
+    out = []
+    for fused in (False, True):
+        sch = sched_cls(prediction_type=pred)
+        sch.set_timesteps(12)
+        x = x0 * sch.init_noise_sigma
+        pipe = StableDiffusionPipeline.__new__(StableDiffusionPipeline)
+        pipe.unet = torch.nn.Linear(1, 1).to(torch.bfloat16)  # dtype/device probe only
+        f = pipe._sample_fused if fused else pipe._sample_torch
+        out.append(f(fake_unet, sch, x.clone(), None, guidance))
+    assert torch.allclose(out[0], out[1], atol=2e-2, rtol=2e-2), (out[0] - out[1]).abs().max()
