@@ -121,6 +121,7 @@ class XGMIAllReduce:
                     ptrs[i][r] = q.value
                     self._opened.append(q.value)
         arr = P * self.world
+        self.calls = 0  # launches so far (tests check the xGMI path really carried the traffic)
         self._stage0 = arr(*ptrs[0])
         self._stage1 = arr(*ptrs[1])
         self._sig = arr(*ptrs[2])
@@ -143,6 +144,7 @@ class XGMIAllReduce:
                        _lib.stream())
         if rc != 0:
             raise RuntimeError(f"kca_ar_run status {rc}")
+        self.calls += 1
         return t
 
     def error(self) -> int:
