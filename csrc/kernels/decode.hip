@@ -404,6 +404,15 @@ __global__ __launch_bounds__(256) void decode_combine_kernel(const float* __rest
   const int b = (int)(bh / H), h = (int)(bh % H);
   const int tid = threadIdx.x;
   const float* ml = ws_ml + bh * nsplit * 2;
+  const float* o = ws_o + bh * nsplit * D;
+  // the first 16 splits' partial outputs of this lane's dim are requested together with the split
+  // maxima (one memory round trip, not two: at B=1 every split count is <= 16..32)
+  constexpr int PRE = 16;
+  float opre[PRE];
+  if (tid < D) {
+#pragma unroll
+    for (int s = 0; s < PRE; ++s) opre[s] = s < nsplit ? o[(long long)s * D + tid] : 0.f;
+  }
   float m = -INFINITY;
   for (int s = tid; s < nsplit; s += 256) m = fmaxf(m, ml[2 * s]);
   const float M = block_max(m, red);
@@ -416,15 +425,17 @@ __global__ __launch_bounds__(256) void decode_combine_kernel(const float* __rest
   }
   const float Lsum = block_sum(l, red + 4);  // block_sum's barriers also publish wsp
   const float inv = Lsum > 0.f ? 1.f / Lsum : 0.f;
-  const float* o = ws_o + bh * nsplit * D;
-  for (int d = tid; d < D; d += 256) {
+  if (tid < D) {  // D <= 256: one output dim per lane
     float acc = 0.f;
+#pragma unroll
+    for (int s = 0; s < PRE; ++s)  // an empty split's partial was never written: may hold NaN
+      acc = (s < nsplit && wsp[s] > 0.f) ? fmaf(wsp[s], opre[s], acc) : acc;
 #pragma unroll 8
-    for (int s = 0; s < nsplit; ++s) {
-      const float ov = o[(long long)s * D + d];   // never written for an empty split: may hold NaN
+    for (int s = PRE; s < nsplit; ++s) {
+      const float ov = o[(long long)s * D + tid];
       acc = wsp[s] > 0.f ? fmaf(wsp[s], ov, acc) : acc;
     }
-    out[b * o_bs + (long long)h * D + d] = f2bf(acc * inv);
+    out[b * o_bs + (long long)h * D + tid] = f2bf(acc * inv);
   }
 }
 
