@@ -44,7 +44,7 @@ def run_tp_decode(model_name="bloom-176b", layers=0, batches=(1, 8, 32), prompt_
         cfg.n_layers = layers
     dev = torch.device("cuda", torch.cuda.current_device())
     t0 = time.perf_counter()
-    if world > 1:
+    if dist.is_initialized():  # TP modules even at world 1: exercises the RCCL collectives in the decode graph
         from kubernetes_cloud_amd.parallel.tensor_parallel import load_tp_model
         model = load_tp_model(cfg, rank, world, None, device=dev, dtype=torch.bfloat16, random_init=True)
     else:
@@ -74,6 +74,7 @@ def run_tp_decode(model_name="bloom-176b", layers=0, batches=(1, 8, 32), prompt_
             run.prefill(torch.tensor(prompts[:1]), [0])
             torch.cuda.synchronize()
             prefill_ms = (time.perf_counter() - t0) * 1e3
+            run.release(0)  # hand the slot's KV pages back before the engine admits the batch
             reqs = [eng.add_request(p, sp) for p in prompts]
             eng.step()
             torch.cuda.synchronize()
@@ -107,9 +108,15 @@ def main():
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--new-tokens", type=int, default=64)
     ap.add_argument("--no-custom-ar", action="store_true", help="TP all-reduces through RCCL only")
+    ap.add_argument("--force-pg", action="store_true",
+                    help="one-rank RCCL process group: TP modules + collectives captured in the decode graph")
     args = ap.parse_args()
     from kubernetes_cloud_amd.parallel.dist import init_distributed
     init_distributed()
+    if args.force_pg and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     recs = run_tp_decode(args.model, args.layers, [int(b) for b in args.batches.split(",")], args.prompt_len,
                          args.new_tokens, custom_ar=not args.no_custom_ar)
     for r in recs or ():

@@ -175,6 +175,8 @@ def register(group=None, max_bytes: int = 64 << 20) -> XGMIAllReduce | None:
     with KCA_CUSTOM_AR=0)."""
     if not torch.cuda.is_available() or os.environ.get("KCA_CUSTOM_AR", "1") == "0":
         return None
+    if dist.get_world_size(group) < 2:  # nothing to exchange
+        return None
     ar = XGMIAllReduce(group, max_bytes)
     _REGISTRY[id(group)] = ar
     return ar
