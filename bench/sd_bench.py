@@ -56,16 +56,29 @@ def bench_train(args, dev):
     px = torch.randn(2 * B, 3, args.res, args.res, device=dev, dtype=torch.bfloat16)
     ids = torch.randint(0, 49408, (2 * B, 77), device=dev)
 
+    from kubernetes_cloud_amd.ops.sd_train import mse_split, noise_prep
+    fused = os.environ.get("KCA_SD_FUSED_TRAIN", "1") not in ("0", "false")
+    acp = sch.alphas_cumprod.to(dev).float()
+    it = [0]
+
     def step():
-        with torch.no_grad():
-            lat = vae.encode(px).sample() * 0.18215
-            ctx = te(ids)
-        noise = torch.randn_like(lat)
-        t = torch.randint(0, 1000, (lat.shape[0],), device=dev)
-        pred = unet(sch.add_noise(lat, noise, t), t, ctx)
-        pi, pc = pred.chunk(2)
-        ni, nc = noise.chunk(2)
-        loss = mse_loss(pi, ni) + mse_loss(pc, nc)
+        t = torch.randint(0, 1000, (px.shape[0],), device=dev)
+        if fused:  # the trainer's fused path (train/sd_finetuner.py): 2 kernels for sample/noise/target/MSE
+            with torch.no_grad():
+                mean, logvar = vae.encode_moments(px).chunk(2, dim=1)
+                ctx = te(ids)
+            noisy, target = noise_prep(mean, logvar, acp[t], 0.18215, False, seed=it[0])
+            it[0] += 1
+            loss = mse_split(unet(noisy, t, ctx), target, 1.0)
+        else:
+            with torch.no_grad():
+                lat = vae.encode(px).sample() * 0.18215
+                ctx = te(ids)
+            noise = torch.randn_like(lat)
+            pred = unet(sch.add_noise(lat, noise, t), t, ctx)
+            pi, pc = pred.chunk(2)
+            ni, nc = noise.chunk(2)
+            loss = mse_loss(pi, ni) + mse_loss(pc, nc)
         eng.backward(loss)
         eng.step(5e-6)
         return loss

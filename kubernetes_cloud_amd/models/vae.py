@@ -217,7 +217,12 @@ class AutoencoderKL(nn.Module):
         return x.contiguous(memory_format=torch.channels_last) if self.channels_last else x
 
     def encode(self, x: torch.Tensor) -> DiagonalGaussian:
-        return DiagonalGaussian(self.quant_conv(self.encoder(self._in(x))).contiguous())
+        return DiagonalGaussian(self.encode_moments(x).contiguous())
+
+    def encode_moments(self, x: torch.Tensor) -> torch.Tensor:
+        """[B, 2C, h, w] mean / logvar moments in the conv layout (the fused
+        training-step noise prep reads them in place: ops/sd_train.py)."""
+        return self.quant_conv(self.encoder(self._in(x)))
 
     def decode(self, z: torch.Tensor) -> torch.Tensor:
         return self.decoder(self.post_quant_conv(self._in(z))).contiguous()

@@ -80,6 +80,28 @@ def _ln_ok(x, M, K, weight, residuals, gamma, beta, bias):
 _LN_SPLIT_M1 = os.environ.get("KCA_DECODE_LN_SPLIT", "1") not in ("0", "false")
 
 
+def ln_rows(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor | None, eps: float, residuals=()):
+    """Decode LayerNorm alone: ``(xn, h)`` with h = x + sum(residuals) (bf16-rounded)
+    and xn = LN(h) -- ``kca_ln_rows`` (one register-resident workgroup per row)."""
+    M, K = x.shape
+    residuals = tuple(r for r in residuals if r is not None)
+    if _lib.use_native(x) and K % 8 == 0 and K <= 16384 and x.stride(1) == 1 and x.stride(0) % 8 == 0 \
+            and all(r.is_contiguous() and r.shape == x.shape for r in residuals) and len(residuals) <= 2 \
+            and gamma.is_contiguous() and (beta is None or beta.is_contiguous()):
+        h = torch.empty(M, K, device=x.device, dtype=x.dtype) if residuals else x
+        xn = torch.empty(M, K, device=x.device, dtype=x.dtype)
+        r1 = residuals[0] if residuals else None
+        r2 = residuals[1] if len(residuals) > 1 else None
+        _lib.call("kca_ln_rows", x.data_ptr(), x.stride(0), _lib.ptr(r1), _lib.ptr(r2),
+                  h.data_ptr() if residuals else None, h.stride(0) if residuals else K, gamma.data_ptr(),
+                  _lib.ptr(beta), float(eps), xn.data_ptr(), M, K, _lib.stream())
+        return xn, h
+    from .norms import layer_norm
+    if residuals:
+        return layer_norm(x, gamma, beta, eps, residual=residuals)
+    return layer_norm(x, gamma, beta, eps), x
+
+
 def ln_skinny_linear(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor | None, eps: float,
                      weight: torch.Tensor, bias: torch.Tensor | None = None, residuals=(), act: int = 0,
                      want_h: bool = False, want_xn: bool = False):
@@ -105,16 +127,8 @@ def ln_skinny_linear(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor | 
                   _lib.ptr(beta), float(eps), weight.data_ptr(), _lib.ptr(bias), y.data_ptr(), y.stride(0),
                   M, weight.shape[0], K, int(act), _lib.ptr(xn), _lib.stream())
         return (y, h, xn) if want_xn else (y, h)
-    if split and _lib.use_native(x, weight) and K % 8 == 0 and K <= 16384 and x.stride(1) == 1 \
-            and x.stride(0) % 8 == 0 and all(r.is_contiguous() and r.shape == x.shape for r in residuals) \
-            and gamma.is_contiguous() and (beta is None or beta.is_contiguous()) and len(residuals) <= 2:
-        h = torch.empty(M, K, device=x.device, dtype=x.dtype) if residuals else x
-        xn = torch.empty(M, K, device=x.device, dtype=x.dtype)
-        r1 = residuals[0] if residuals else None
-        r2 = residuals[1] if len(residuals) > 1 else None
-        _lib.call("kca_ln_rows", x.data_ptr(), x.stride(0), _lib.ptr(r1), _lib.ptr(r2),
-                  h.data_ptr() if residuals else None, h.stride(0) if residuals else K, gamma.data_ptr(),
-                  _lib.ptr(beta), float(eps), xn.data_ptr(), M, K, _lib.stream())
+    if split:
+        xn, h = ln_rows(x, gamma, beta, eps, residuals)
         y = skinny_linear(xn, weight, bias, act)
         return (y, h, xn) if want_xn else (y, h)
     from .norms import layer_norm
@@ -126,4 +140,4 @@ def ln_skinny_linear(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor | 
     return (y, h, xn) if want_xn else (y, h)
 
 
-__all__ = ["skinny_linear", "ln_skinny_linear", "ACT"]
+__all__ = ["skinny_linear", "ln_skinny_linear", "ln_rows", "ACT"]

@@ -209,6 +209,10 @@ def main(argv=None):
     sink = MetricsSink(args.logs or os.path.join(args.output_path, "logs"), args.run_name or "sd", args.project_id,
                        enabled=info.is_main, config={k: v for k, v in vars(args).items() if k != "hf_token"})
     scale = vae.config.scaling_factor or L_SCALE_FACTOR
+    from ..ops.sd_train import mse_split, noise_prep
+    fused_step = (dev.type == "cuda" and dtype == torch.bfloat16
+                  and os.environ.get("KCA_SD_FUSED_TRAIN", "1") not in ("0", "false"))
+    acp_dev = noise_sched.alphas_cumprod.to(dev).float()
 
     def save():
         if ema is not None:  # export the EMA weights, then restore the live ones
@@ -229,20 +233,30 @@ def main(argv=None):
             t0 = time.perf_counter()
             px = batch["pixel_values"].to(dev, dtype)
             ids = batch["input_ids"].to(dev)
-            with torch.no_grad():
-                lat = vae.encode(px).sample() * scale
-                ctx = te(ids)
-            noise = torch.randn_like(lat)
-            ts = torch.randint(0, noise_sched.N, (lat.shape[0],), device=dev)
-            noisy = noise_sched.add_noise(lat, noise, ts)
-            pred = unet(noisy, ts, ctx)
-            target = noise if pred_type == "epsilon" else noise_sched.get_velocity(lat, noise, ts)
-            if args.is_dreambooth:
-                p_i, p_c = pred.chunk(2)
-                t_i, t_c = target.chunk(2)
-                loss = mse_loss(p_i, t_i) + args.prior_loss_weight * mse_loss(p_c, t_c)
+            if fused_step:  # K18/K20 + K19: sample, noise, target and the split MSE as two fused kernels
+                with torch.no_grad():
+                    mean, logvar = vae.encode_moments(px).chunk(2, dim=1)
+                    ctx = te(ids)
+                ts = torch.randint(0, noise_sched.N, (mean.shape[0],), device=dev)
+                noisy, target = noise_prep(mean, logvar, acp_dev[ts], scale, pred_type == "v_prediction",
+                                           seed=(args.seed * 1000003 + step * info.world_size + info.rank))
+                pred = unet(noisy, ts, ctx)
+                loss = mse_split(pred, target, args.prior_loss_weight if args.is_dreambooth else None)
             else:
-                loss = mse_loss(pred, target)
+                with torch.no_grad():
+                    lat = vae.encode(px).sample() * scale
+                    ctx = te(ids)
+                noise = torch.randn_like(lat)
+                ts = torch.randint(0, noise_sched.N, (lat.shape[0],), device=dev)
+                noisy = noise_sched.add_noise(lat, noise, ts)
+                pred = unet(noisy, ts, ctx)
+                target = noise if pred_type == "epsilon" else noise_sched.get_velocity(lat, noise, ts)
+                if args.is_dreambooth:
+                    p_i, p_c = pred.chunk(2)
+                    t_i, t_c = target.chunk(2)
+                    loss = mse_loss(p_i, t_i) + args.prior_loss_weight * mse_loss(p_c, t_c)
+                else:
+                    loss = mse_loss(pred, target)
             lr = sd_lr(step, args.lr, args.lr_scheduler, args.lr_warmup_steps, total)
             eng.backward(loss)
             eng.step(lr)

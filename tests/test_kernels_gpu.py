@@ -689,3 +689,38 @@ def test_sd_fused_lms_step_matches_reference(cfg, pred, order):
         assert torch.allclose(x_gpu.cpu(), x_ref, atol=1e-3, rtol=1e-4), (i, (x_gpu.cpu() - x_ref).abs().max())
         # one bf16 ulp: out * in_scale may round to the other side of a bf16 boundary
         assert torch.allclose(xin_g.cpu().float(), xin_r.float(), rtol=8e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("v_pred", [False, True])
+def test_sd_fused_noise_prep_and_mse_split(v_pred):
+    """kca_sd_noise_prep (channels-last moments) vs the torch reference with the
+    same explicit draws; Philox draws are standard normal; kca_mse_split fwd/bwd
+    vs the chunked fp32 MSE with prior weight."""
+    from kubernetes_cloud_amd.ops import _lib
+    from kubernetes_cloud_amd.ops.sd_train import mse_split, mse_split_reference, noise_prep, noise_prep_reference
+    assert _lib.has("kca_sd_noise_prep") and _lib.has("kca_mse_split_fwd")
+    torch.manual_seed(0)
+    B = 8
+    moments = torch.randn(B, 8, 64, 64, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    mean, logvar = moments.chunk(2, dim=1)
+    acp = torch.rand(B, device="cuda") * 0.98 + 0.01
+    e, n = torch.randn(B, 4, 64, 64, device="cuda"), torch.randn(B, 4, 64, 64, device="cuda")
+    noisy, target = noise_prep(mean, logvar, acp, 0.18215, v_pred, e=e, n=n)
+    rn, rt = noise_prep_reference(mean, logvar, acp, 0.18215, v_pred, e.to(torch.bfloat16), n.to(torch.bfloat16),
+                                  torch.channels_last)
+    assert noisy.is_contiguous(memory_format=torch.channels_last)
+    assert (noisy.float() - rn.float()).abs().max() <= 0.02 and (target.float() - rt.float()).abs().max() <= 0.02
+    # internal Philox draws: the epsilon target is the noise itself -> standard normal
+    _, t2 = noise_prep(mean, logvar, acp, 0.18215, False, seed=1234)
+    assert abs(float(t2.float().mean())) < 0.01 and abs(float(t2.float().std()) - 1) < 0.01
+    _, t3 = noise_prep(mean, logvar, acp, 0.18215, False, seed=1235)
+    assert not torch.equal(t2, t3)
+    # MSE split fwd / bwd
+    pred = torch.randn_like(noisy).requires_grad_()
+    loss = mse_split(pred, target, 0.7)
+    loss.backward()
+    p_ref = pred.detach().float().requires_grad_()
+    l_ref = mse_split_reference(p_ref, target.float(), 0.7)
+    l_ref.backward()
+    assert abs(float(loss) - float(l_ref)) < 1e-3 * float(l_ref)
+    assert torch.allclose(pred.grad.float(), p_ref.grad, rtol=2e-2, atol=1e-7)

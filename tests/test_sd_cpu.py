@@ -230,3 +230,26 @@ def test_fused_sampler_path_matches_scheduler_steps(sched_cls, pred, guidance):
         f = pipe._sample_fused if fused else pipe._sample_torch
         out.append(f(fake_unet, sch, x.clone(), None, guidance))
     assert torch.allclose(out[0], out[1], atol=2e-2, rtol=2e-2), (out[0] - out[1]).abs().max()
+
+
+@pytest.mark.parametrize("v_pred", [False, True])
+def test_fused_noise_prep_reference_matches_scheduler_math(v_pred):
+    """ops/sd_train.py reference == DiagonalGaussian.sample() * scale -> add_noise / get_velocity."""
+    from kubernetes_cloud_amd.models.vae import DiagonalGaussian
+    from kubernetes_cloud_amd.ops.sd_train import mse_split_reference, noise_prep_reference
+    torch.manual_seed(0)
+    sch = DDPMScheduler(prediction_type="v_prediction" if v_pred else "epsilon")
+    moments = torch.randn(4, 8, 6, 6)
+    mean, logvar = moments.chunk(2, dim=1)
+    e, n = torch.randn(4, 4, 6, 6), torch.randn(4, 4, 6, 6)
+    ts = torch.tensor([1, 100, 500, 999])
+    noisy, target = noise_prep_reference(mean, logvar, sch.alphas_cumprod[ts].float(), 0.18215, v_pred, e, n)
+    g = DiagonalGaussian(moments)
+    lat = (g.mean + g.std * e) * 0.18215
+    ref_noisy = sch.add_noise(lat, n, ts)
+    ref_target = sch.get_velocity(lat, n, ts) if v_pred else n
+    assert torch.allclose(noisy, ref_noisy, atol=1e-5) and torch.allclose(target, ref_target, atol=1e-5)
+    p = torch.randn(4, 4, 6, 6)
+    from kubernetes_cloud_amd.ops import mse_loss
+    assert torch.allclose(mse_split_reference(p, target, 0.5),
+                          mse_loss(p[:2], target[:2]) + 0.5 * mse_loss(p[2:], target[2:]))
