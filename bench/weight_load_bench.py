@@ -70,15 +70,21 @@ def main():
     ap.add_argument("--http", action="store_true")
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--keep", action="store_true")
+    ap.add_argument("--tp", type=int, default=0,
+                    help="time rank 0's tensor-parallel shard of --model at this TP degree (BLOOM TP shard load)")
     args = ap.parse_args()
     from kubernetes_cloud_amd.io.hf import load_tensorized, serialize_causal_lm
     from kubernetes_cloud_amd.models.causal_lm import build_model
     from kubernetes_cloud_amd.models.config import preset
     dev = torch.device("cuda", 0)
     cfg = preset(args.model)
-    path = os.path.join(args.dir, f"kca_{args.model}.tensors")
+    path = os.path.join(args.dir, f"kca_{args.model}{f'_tp{args.tp}r0' if args.tp else ''}.tensors")
     t0 = time.perf_counter()
-    m = build_model(cfg, device=dev, dtype=torch.float16, seed=0)
+    if args.tp:  # rank 0's shard, random-init on the device (a 176B shard never touches host memory)
+        from kubernetes_cloud_amd.parallel.tensor_parallel import load_tp_model
+        m = load_tp_model(cfg, 0, args.tp, None, device=dev, dtype=torch.float16, random_init=True)
+    else:
+        m = build_model(cfg, device=dev, dtype=torch.float16, seed=0)
     ref = {k: v.float().abs().sum().item() for k, v in list(m.state_dict().items())[:3]}
     info = serialize_causal_lm(m, path)
     del m
@@ -90,12 +96,23 @@ def main():
     def run(label, uri, **kw):
         torch.cuda.synchronize()
         t = time.perf_counter()
-        model, st = load_tensorized(uri, None, device=dev, dtype=torch.float16, threads=args.threads)
+        if args.tp:
+            from kubernetes_cloud_amd.io.tensors import load_into_module
+            from kubernetes_cloud_amd.models.causal_lm import CausalLM
+            from kubernetes_cloud_amd.parallel.tensor_parallel import tp_convert_
+            with torch.device("meta"):
+                model = CausalLM(cfg)
+            tp_convert_(model, 0, args.tp, None)
+            model = model.to(torch.float16).to_empty(device=dev)
+            st = load_into_module(model, uri, device=dev, threads=args.threads)
+        else:
+            model, st = load_tensorized(uri, None, device=dev, dtype=torch.float16, threads=args.threads)
         torch.cuda.synchronize()
         ready = time.perf_counter() - t
         got = {k: v.float().abs().sum().item() for k, v in list(model.state_dict().items())[:3]}
         assert all(abs(got[k] - ref[k]) <= 1e-3 * max(1.0, ref[k]) for k in ref), (got, ref)
-        rec = {"metric": "weight load", "source": label, "model": args.model, "dtype": "fp16",
+        rec = {"metric": "weight load", "source": label, "model": args.model + (f" TP={args.tp} rank-0 shard" if args.tp else ""),
+               "dtype": "fp16",
                "bytes": int(st["bytes"]), "stream_s": round(st["seconds"], 3), "gbps": round(st["gbps"], 2),
                "seconds_to_ready": round(ready, 3), "threads": args.threads, "data": "random-init weights", **kw}
         print(json.dumps(rec), flush=True)
