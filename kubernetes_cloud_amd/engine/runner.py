@@ -291,6 +291,9 @@ class ModelRunner:
         self.seen = torch.zeros(max_slots + 1, self.V, dtype=torch.uint8, device=self.device)
         self.max_bans = max_bans
         on_gpu = self.device.type == "cuda"
+        if on_gpu:  # MI355X-tuned hipBLASLt/rocBLAS choices for the batched decode GEMMs (utils/tunable.py)
+            from ..utils import tunable
+            tunable.ensure(tunable.DECODE_FILE)
         self.use_graphs = on_gpu if use_graphs is None else (use_graphs and on_gpu)
         if self.multi_device:
             self.use_graphs = False  # one graph cannot span devices; the split path runs eagerly

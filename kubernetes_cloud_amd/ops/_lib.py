@@ -24,6 +24,8 @@ LIB_DIR = os.path.join(os.path.dirname(_HERE), "_lib")
 # KCA_DEBUG=1: the debug build (KCA_DASSERT bounds/invariant checks in the kernels)
 DEBUG = os.environ.get("KCA_DEBUG", "0") in ("1", "true")
 KERNEL_LIB = os.path.join(LIB_DIR, "libkca_kernels_debug.so" if DEBUG else "libkca_kernels.so")
+# KCA_KERNEL_LIB=<path>: load another build of the kernel library (same-box A/B of a kernel change)
+KERNEL_LIB = os.environ.get("KCA_KERNEL_LIB") or KERNEL_LIB
 
 _lock = threading.Lock()
 _lib = None

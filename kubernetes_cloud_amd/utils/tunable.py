@@ -7,7 +7,9 @@ tokens) land on a 64x64 macro tile without split-K -- 25 workgroups on a
 256-CU chip. TunableOp times the candidate solutions once on an MI355X and
 records the winner; ``configure(..., "use")`` replays those choices with no
 search. Files: ``tuning/tunableop_results.csv`` (GPT-J-6B training step) and
-``tuning/tunableop_sd.csv`` (SD-1.5 DreamBooth step + txt2img UNet).
+``tuning/tunableop_sd.csv`` (SD-1.5 DreamBooth step + txt2img UNet),
+``tuning/tunableop_decode.csv`` (serving decode / prefill GEMMs, loaded by
+``engine.runner.ModelRunner`` on the GPU).
 """
 from __future__ import annotations
 
@@ -16,6 +18,9 @@ import os
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 GPTJ_FILE = os.path.join(ROOT, "tuning", "tunableop_results.csv")
 SD_FILE = os.path.join(ROOT, "tuning", "tunableop_sd.csv")
+# serving: the decode-step GEMMs at batch buckets 2..64 (M = batch, K/N = model dims), where
+# hipBLASLt's default heuristic picks long split-free K loops (GPT-J fc_out at M=64: 0.9 TB/s)
+DECODE_FILE = os.path.join(ROOT, "tuning", "tunableop_decode.csv")
 
 
 def configure(path: str, mode: str = "auto", max_tuning_ms: int = 40) -> str:

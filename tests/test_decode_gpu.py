@@ -46,7 +46,7 @@ def test_decode_attention(D, G):
     slots = torch.tensor([3, 0, 6, 1, 2, 5], device=dev, dtype=torch.int32)
     lens = torch.tensor([1, 2048, 700, 65, 1500, 129], device=dev, dtype=torch.int32)
     alibi = None
-    for max_kv, chunk in ((2048, 0), (2048, 64), (2048, 1024)):
+    for max_kv, chunk in ((2048, 0), (2048, 32), (2048, 64), (2048, 1024)):  # short (two-phase) and online
         o = dops.decode_attention(q, kc, vc, slots, lens, H, max_kv, chunk=chunk)
         ref = dops.decode_attention_reference(q.float(), kc.float(), vc.float(), slots, lens, H,
                                               1 / math.sqrt(D), alibi, torch.empty(B, H * D, device=dev))
@@ -265,7 +265,7 @@ def test_decode_attention_paged_equals_contiguous(D, G, PS):
     q = torch.randn(B, (H + 2 * Hkv) * D, device=dev).to(torch.bfloat16)
     slots = torch.tensor([3, 0, 6, 1, 2, 5], device=dev, dtype=torch.int32)
     lens = torch.tensor([1, 2048, 700, 65, 1500, 129], device=dev, dtype=torch.int32)
-    for chunk in (0, 64, 1024):
+    for chunk in (0, 32, 64, 1024):
         a = dops.decode_attention(q, kc, vc, slots, lens, H, L, chunk=chunk)
         b = dops.decode_attention(q, kp, vp, slots, lens, H, L, chunk=chunk, block_table=tbl)
         assert torch.equal(a, b), chunk  # same values, same reduction order
