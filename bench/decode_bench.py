@@ -30,7 +30,14 @@ def main():
     ap.add_argument("--page-size", type=int, default=None, help="KV page size (0 = contiguous slots)")
     ap.add_argument("--decode-only", type=int, default=0,
                     help="profile mode: prefill B prompts once, then time N pure decode steps")
+    ap.add_argument("--tune", default=None,
+                    help="TunableOp: search the GEMM solutions of this run and write them to this file "
+                         "(run with --no-graphs; graphs cannot capture the search)")
     args = ap.parse_args()
+    if args.tune:
+        os.environ["KCA_TUNABLEOP"] = "off"  # no preloaded table: search everything this run touches
+        from kubernetes_cloud_amd.utils import tunable
+        tunable.configure(args.tune, "tune", max_tuning_ms=30)
     from kubernetes_cloud_amd.engine.llm_engine import LLMEngine, SamplingParams
     from kubernetes_cloud_amd.models.causal_lm import build_model
     from kubernetes_cloud_amd.models.config import preset
