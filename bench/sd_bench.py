@@ -153,10 +153,14 @@ def main():
     ap.add_argument("--infer-steps", type=int, default=50)
     ap.add_argument("--scheduler", default="LMSDiscreteScheduler")
     ap.add_argument("--ckpt", action="store_true")
+    ap.add_argument("--deterministic", action="store_true",
+                    help="MIOpen deterministic convolution solvers only (the SD predictor's setting)")
     ap.add_argument("--tunableop", choices=["auto", "use", "tune", "off"], default="auto",
                     help="hipBLASLt solution choices from tuning/tunableop_sd.csv (utils/tunable.py)")
     ap.add_argument("--tunableop-file", default=None)
     args = ap.parse_args()
+    if args.deterministic:
+        torch.backends.cudnn.deterministic = True
     dev = torch.device("cuda", 0)
     from kubernetes_cloud_amd.ops import _lib
     from kubernetes_cloud_amd.utils import tunable

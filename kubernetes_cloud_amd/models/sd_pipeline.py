@@ -263,7 +263,7 @@ class StableDiffusionPipeline:
                                   dtype=torch.float32).to(dev)
         x = latents.to(dev).float() * sch.init_noise_sigma
         run = self._runner()
-        if self._fused_sampler_ok(sch, dev):
+        if self._fused_sampler_ok(sch, dev, dt):
             x = self._sample_fused(run, sch, x, ctx, guidance_scale if cfg else None)
         else:
             x = self._sample_torch(run, sch, x, ctx, guidance_scale if cfg else None)
@@ -276,13 +276,13 @@ class StableDiffusionPipeline:
         return to_pil(img)
 
     @staticmethod
-    def _fused_sampler_ok(sch, dev) -> bool:
+    def _fused_sampler_ok(sch, dev, dtype) -> bool:
         import os
 
         from ..ops import _lib
         from .schedulers import LMSDiscreteScheduler
-        return (dev.type == "cuda" and isinstance(sch, LMSDiscreteScheduler) and _lib.has("kca_sd_lms_step")
-                and os.environ.get("KCA_SD_FUSED_STEP", "1") not in ("0", "false"))
+        return (dev.type == "cuda" and dtype == torch.bfloat16 and isinstance(sch, LMSDiscreteScheduler)
+                and _lib.has("kca_sd_lms_step") and os.environ.get("KCA_SD_FUSED_STEP", "1") not in ("0", "false"))
 
     def _sample_fused(self, run, sch, x, ctx, guidance):
         """LMS / Euler sampling with one fused kernel per step between UNet replays

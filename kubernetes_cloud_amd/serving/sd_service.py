@@ -47,6 +47,8 @@ def get_args(argv=None):
     p.add_argument("--tensorized", default=False, action="store_true")
     p.add_argument("--max-batch", default=int(os.getenv("MAX_BATCH", 8)), type=int)
     p.add_argument("--batch-window-ms", default=float(os.getenv("BATCH_WINDOW_MS", 5.0)), type=float)
+    p.add_argument("--deterministic", default=os.getenv("DETERMINISTIC", "0") in ("1", "true", "True"),
+                   action="store_true", help="bit-identical images per seed (deterministic MIOpen solvers only)")
     args, _ = p.parse_known_args(argv)
     args.model_name = args.model_id.rstrip("/").split("/")[-1]
     return args
@@ -62,13 +64,14 @@ class SDPredictor(Model):
     def __init__(self, model_name: str, model_id: str, precision: str = "float16", guidance_scale: float = 7.0,
                  num_inference_steps: int = 50, seed: int | None = None, width: int = 512, height: int = 512,
                  tensorized: bool = False, max_batch: int = 8, batch_window_ms: float = 5.0, pipeline=None,
-                 device=None, **_):
+                 device=None, deterministic: bool = False, **_):
         super().__init__(model_name)
         self.model_id, self.tensorized = model_id, tensorized
         self.precision = precision
         self.parameters = {"GUIDANCE_SCALE": guidance_scale, "NUM_INFERENCE_STEPS": num_inference_steps,
                            "SEED": seed, "WIDTH": width, "HEIGHT": height}
         self.max_batch, self.window = max_batch, batch_window_ms / 1000.0
+        self.deterministic = deterministic
         self.pipeline = pipeline
         self.device = device
         self._q: queue.Queue = queue.Queue()
@@ -85,6 +88,9 @@ class SDPredictor(Model):
             dt = torch.bfloat16  # MFMA bf16 path; fp16 UNet activations overflow without autocast
         if dev.type == "cpu":
             dt = torch.float32
+        if self.deterministic:  # same seed -> bit-identical PNG (utils/miopen.py: split-K atomics otherwise)
+            from ..utils import miopen
+            miopen.configure(deterministic=True)
         t0 = time.perf_counter()
         if self.tensorized:
             self.pipeline = StableDiffusionPipeline.from_tensorized(self.model_id, device=dev, dtype=dt,

@@ -21,6 +21,19 @@ to MIOpen's normal find, and their results are appended to the same db.
 
 ``configure()`` runs before the first convolution; explicit environment
 settings win.
+
+Determinism: for some configs MIOpen's find picks a split-K igemm kernel that
+accumulates through fp32 atomics (igemm_fwd_gtcx35_nhwc_* after a zero-fill of
+its workspace), so two identical calls can differ in the last bf16 bit
+(measured on the tiny test UNet with ``tools/sd_determinism.py``).
+``configure(deterministic=True)`` switches that solver family off (forward,
+backward-data and weight-gradient GTC NHWC igemm; the CK implicit-GEMM solvers
+that remain write their tiles once) and lets the naive solvers back in as the
+fallback for configs nothing else covers; its find results go to a separate
+user db so the tuned one keeps the fastest solvers. It must run before the
+first convolution of the process. (``torch.backends.cudnn.deterministic``
+itself is no use here: MIOpen then found no solver for the small-channel
+``conv_in`` of the SD UNet.)
 """
 from __future__ import annotations
 
@@ -34,8 +47,26 @@ TUNED_DB = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.
                         "tuning", "miopen")
 
 
-def configure() -> None:
+_GTC = ("MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_FWD_GTC_XDLOPS_NHWC",
+        "MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_BWD_GTC_XDLOPS_NHWC",
+        "MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_WRW_GTC_XDLOPS_NHWC")
+_OURS: set = set()
+
+
+def configure(deterministic: bool = False) -> None:
     for k in _NAIVE:
-        os.environ.setdefault(k, "0")
+        if k not in os.environ:
+            os.environ[k] = "0"
+            _OURS.add(k)
+        if deterministic and k in _OURS:
+            os.environ[k] = "1"
+    if deterministic:
+        for k in _GTC:
+            os.environ.setdefault(k, "0")
+        if os.environ.get("MIOPEN_USER_DB_PATH", TUNED_DB) == TUNED_DB:
+            det = os.path.join(os.path.expanduser("~"), ".cache", "kca_miopen_deterministic")
+            os.makedirs(det, exist_ok=True)
+            os.environ["MIOPEN_USER_DB_PATH"] = det
+        return
     if os.path.isdir(TUNED_DB) and os.access(TUNED_DB, os.W_OK):
         os.environ.setdefault("MIOPEN_USER_DB_PATH", TUNED_DB)
