@@ -137,7 +137,21 @@ struct DecodeParams {
   int fused, rot, interleaved;
   const float* cos_t;
   const float* sin_t;
+  unsigned long long* stamps;  // diagnostic: per-workgroup s_memrealtime stamps (nullptr in normal runs)
 };
+
+// diagnostic stamps (bench/decode_attn_bench.py --stamps): 8 per workgroup, 100 MHz clock
+static unsigned long long* g_decode_stamps = nullptr;
+KCA_API int kca_decode_set_stamps(void* buf) {
+  g_decode_stamps = (unsigned long long*)buf;
+  return 0;
+}
+#define DSTAMP(k)                                                                                     \
+  do {                                                                                                \
+    if (p.stamps && threadIdx.x == 0)                                                                 \
+      p.stamps[(((long long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 8 + (k)] = \
+          __builtin_amdgcn_s_memrealtime();                                                           \
+  } while (0)
 
 // RoPE of the 8 dims [d0, d0+8) of a head row at position `pos`, matching
 // decode_prep_kernel (partner values read from the unrotated row; the result is
@@ -166,6 +180,25 @@ __device__ __forceinline__ void rope8(const bf16_t* __restrict__ row, int d0, fl
   }
 }
 
+// Sum over the LPT lanes of a lane group (LPT = 8/16/32 consecutive lanes), the result in every lane
+// of the group: DPP quad swaps, then half-row / row mirrors, then a 32-lane swizzle -- VALU-latency
+// steps instead of a chain of ds_bpermute round trips through the LDS crossbar. Each step adds the
+// same two partial sums in every lane of a pair, so all lanes agree bit for bit.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int LPT>
+__device__ __forceinline__ float group_sum(float v) {
+  v += dpp_mov<0xB1>(v);                 // quad_perm [1,0,3,2]: lane ^ 1
+  v += dpp_mov<0x4E>(v);                 // quad_perm [2,3,0,1]: lane ^ 2
+  if constexpr (LPT > 4) v += dpp_mov<0x141>(v);  // row_half_mirror: quad <-> quad in 8 lanes
+  if constexpr (LPT > 8) v += dpp_mov<0x140>(v);  // row_mirror: 8 <-> 8 in 16 lanes
+  if constexpr (LPT > 16)                          // ds_swizzle xor 16 within 32 lanes
+    v += __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x401F));
+  return v;
+}
+
 // LPT lanes cooperate on one token row (8 dims per lane); TPW = 64/LPT tokens per
 // wave step; G query heads share each K/V row (GQA group).
 template <int LPT, int G, bool PAGED, bool ONLINE>
@@ -174,14 +207,42 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
   constexpr int TPB = 4 * TPW;
   constexpr int U = 4;  // tokens per lane per iteration: 2U independent 16-B row loads in flight
   extern __shared__ float smem[];
+  DSTAMP(0);
   const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
   const int nsplit = gridDim.x;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int D = p.D, ND = D >> 3;
-  const int L = p.kv_lens[b];
-  const int c0 = split * p.chunk;
-  const int c1 = min(c0 + p.chunk, L);
+  const int dslot = lane % LPT, tsub = lane / LPT;
+  const bool dact = dslot < ND;
   const long long bh0 = (long long)b * p.H + hk * G;
+  const int c0 = split * p.chunk;
+  // every load that does not depend on the sequence length is issued before the length arrives:
+  // the length, the slot, the raw Q rows, the new token's raw K/V rows (fused) and, once the slot
+  // is known, this split's page ids -- so the K/V stream starts after two memory round trips, not four
+  const int L = p.kv_lens[b];
+  const int seq = p.slots[b];
+  U16x8 qraw[G];  // inactive lanes read dims [0, 8) (unused) instead of branching around the load
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+    qraw[g] = *reinterpret_cast<const U16x8*>(p.q + b * p.q_bs + (long long)(hk * G + g) * D + (dact ? dslot : 0) * 8);
+  const bf16_t* krow = p.q + b * p.q_bs + (long long)(p.H + hk) * D;
+  const bf16_t* vrow = p.q + b * p.q_bs + (long long)(p.H + p.Hkv + hk) * D;
+  U16x8 knraw, vnraw;  // the new token's K / V slice of lane tid (< ND), from the fused QKV row
+  if (p.fused && tid < ND) {
+    knraw = *reinterpret_cast<const U16x8*>(krow + tid * 8);
+    vnraw = *reinterpret_cast<const U16x8*>(vrow + tid * 8);
+  }
+  // paged: this split's page ids staged in LDS (chunk <= 1024 tokens, pages >= 16 tokens), so a
+  // token's address costs an LDS read instead of a dependent global load in front of every K/V
+  // load; the whole chunk's range is staged (clipped to the table row), independent of the length
+  __shared__ int pg[1024 / 16 + 2];
+  const int pg0 = c0 >> p.ps_shift;
+  if constexpr (PAGED) {
+    const int npg = min(((c0 + p.chunk - 1) >> p.ps_shift) - pg0 + 1, p.tbl_stride - pg0);
+    KCA_DASSERT(npg <= 1024 / 16 + 2);
+    for (int i = tid; i < npg; i += 256) pg[i] = p.tbl[(long long)seq * p.tbl_stride + pg0 + i];
+  }
+  const int c1 = min(c0 + p.chunk, L);
   if (c0 >= L) {
     if (nsplit > 1 && tid < G) {
       p.ws_ml[((bh0 + tid) * nsplit + split) * 2] = -INFINITY;
@@ -189,22 +250,21 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
     }
     return;
   }
-  const int dslot = lane % LPT, tsub = lane / LPT;
-  const bool dact = dslot < ND;
-  KCA_DASSERT(p.slots[b] >= 0);
-  const int seq = p.slots[b];
+  DSTAMP(1);
+  KCA_DASSERT(seq >= 0);
   const long long kvoff = (PAGED ? 0 : (long long)seq * p.cs_slot) + hk * p.cs_head + dslot * 8;
   const bf16_t* kb = p.kc + kvoff;
   const bf16_t* vb = p.vc + kvoff;
   const int pnew = L - 1;  // the new token's position (fused prep)
-  // Q first: its loads (and RoPE table reads) are in flight while the page ids are staged
   float q[G][8];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     if (dact) {
-      const bf16_t* qrow = p.q + b * p.q_bs + (long long)(hk * G + g) * D;
-      load8(qrow + dslot * 8, q[g]);
-      if (p.fused && p.rot > 0) rope8(qrow, dslot * 8, q[g], pnew, p.rot, p.interleaved, p.cos_t, p.sin_t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) q[g][j] = bf2f(qraw[g].v[j]);
+      if (p.fused && p.rot > 0)
+        rope8(p.q + b * p.q_bs + (long long)(hk * G + g) * D, dslot * 8, q[g], pnew, p.rot, p.interleaved, p.cos_t,
+              p.sin_t);
 #pragma unroll
       for (int j = 0; j < 8; ++j) q[g][j] *= p.scale;
     } else {
@@ -215,17 +275,15 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
   float slope[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) slope[g] = p.alibi ? p.alibi[hk * G + g] : 0.f;
-
-  // paged: this split's page ids staged in LDS once (chunk <= 1024 tokens, pages >= 16 tokens), so a
-  // token's address costs an LDS read instead of a dependent global load in front of every K/V load
-  __shared__ int pg[1024 / 16 + 2];
-  const int pg0 = c0 >> p.ps_shift;
-  if constexpr (PAGED) {
-    const int npg = ((c1 - 1) >> p.ps_shift) - pg0 + 1;
-    KCA_DASSERT(npg <= 1024 / 16 + 2);
-    for (int i = tid; i < npg; i += 256) pg[i] = p.tbl[(long long)seq * p.tbl_stride + pg0 + i];
-    __syncthreads();
+  if (p.stamps && tid == 0) {  // diagnostic: wait for Q (and its RoPE) before stamping
+    float z = 0.f;
+#pragma unroll
+    for (int g = 0; g < G; ++g) z += q[g][0];
+    if (z == 12345.f) p.stamps[0] = 0;
   }
+  DSTAMP(2);
+  if constexpr (PAGED) __syncthreads();  // pg[] published
+  DSTAMP(3);
   // offset of token t inside this sequence's storage
   auto toff = [&](int t) -> long long {
     if constexpr (PAGED)
@@ -233,28 +291,44 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
     return (long long)t * p.cs_pos;
   };
 
-  // fused prep: the split holding the new token (position L-1) rotates its K, appends K and V to the
-  // cache, and serves that row from LDS (no other split reads position L-1)
-  __shared__ float knew[256], vnew[256];
+  // fused prep: the split holding the new token (position L-1) rotates its K and appends K and V to
+  // the cache; no other split reads position L-1. The one-pass path folds the token in after its
+  // loop (registers); the two-phase path serves it from LDS.
   const bool own_new = p.fused && c1 == L;
-  if (own_new) {
-    if (tid < ND) {
-      const bf16_t* krow = p.q + b * p.q_bs + (long long)(p.H + hk) * D;
-      const bf16_t* vrow = p.q + b * p.q_bs + (long long)(p.H + p.Hkv + hk) * D;
-      float kx[8], vx[8];
-      load8(krow + tid * 8, kx);
-      load8(vrow + tid * 8, vx);
-      if (p.rot > 0) rope8(krow, tid * 8, kx, pnew, p.rot, p.interleaved, p.cos_t, p.sin_t);
-      const long long o = toff(pnew) + hk * p.cs_head + tid * 8;  // toff: offset inside the sequence
-      store8(const_cast<bf16_t*>(p.kc) + (PAGED ? 0 : (long long)seq * p.cs_slot) + o, kx);
-      store8(const_cast<bf16_t*>(p.vc) + (PAGED ? 0 : (long long)seq * p.cs_slot) + o, vx);
+  // one-pass path: the split holding the last token (position L-1) folds it in after its loop, in
+  // both modes (fused: the new row from registers; plain: the cached row), so the fused launch
+  // stays bit-identical to prep + attention
+  const bool own_last = ONLINE && c1 == L;
+  float kx[8], vx[8];  // two-phase path: the new row, staged to LDS below
+  if (own_new && tid < ND) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        knew[tid * 8 + j] = kx[j];
-        vnew[tid * 8 + j] = vx[j];
-      }
+    for (int j = 0; j < 8; ++j) {
+      kx[j] = bf2f(knraw.v[j]);
+      vx[j] = bf2f(vnraw.v[j]);
     }
-    __syncthreads();
+    if (p.rot > 0) rope8(krow, tid * 8, kx, pnew, p.rot, p.interleaved, p.cos_t, p.sin_t);
+    const long long o = toff(pnew) + hk * p.cs_head + tid * 8;  // toff: offset inside the sequence
+    store8(const_cast<bf16_t*>(p.kc) + (PAGED ? 0 : (long long)seq * p.cs_slot) + o, kx);
+    store8(const_cast<bf16_t*>(p.vc) + (PAGED ? 0 : (long long)seq * p.cs_slot) + o, vx);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) knraw.v[j] = f2bf(kx[j]);  // exact: the rotation is bf16-rounded
+  } else if (own_last && tid < ND) {
+    const long long o = (PAGED ? 0 : (long long)seq * p.cs_slot) + toff(pnew) + hk * p.cs_head + tid * 8;
+    knraw = *reinterpret_cast<const U16x8*>(p.kc + o);
+    vnraw = *reinterpret_cast<const U16x8*>(p.vc + o);
+  }
+  __shared__ float knew[ONLINE ? 1 : 256], vnew[ONLINE ? 1 : 256];
+  if constexpr (!ONLINE) {
+    if (own_new) {
+      if (tid < ND) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          knew[tid * 8 + j] = kx[j];
+          vnew[tid * 8 + j] = vx[j];
+        }
+      }
+      __syncthreads();
+    }
   }
 
   if constexpr (ONLINE) {
@@ -270,54 +344,81 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
   }
-  for (int t0 = c0 + wid * TPW + tsub; t0 < c1; t0 += TPB * U) {
+  // the tokens [c0, ce); the last one (own_last) is folded in below from registers
+  const int ce = own_last ? c1 - 1 : c1;
+  // inactive lanes (dslot >= ND) and tokens past the split read an in-range row instead of branching
+  // around their loads: no branch in the loop, so all 2U loads of an iteration are in flight together
+  const long long dfix = dact ? 0 : -(long long)dslot * 8;
+  for (int t0 = c0 + wid * TPW + tsub; t0 < ce; t0 += TPB * U) {
+    long long o[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) o[u] = toff(min(t0 + u * TPB, ce - 1)) + dfix;
     U16x8 kr[U], vr[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int t = t0 + u * TPB;
-      if (t < c1 && dact && !(own_new && t == pnew)) {
-        const long long o = toff(t);
-        kr[u] = *reinterpret_cast<const U16x8*>(kb + o);
-        vr[u] = *reinterpret_cast<const U16x8*>(vb + o);
-      }
+      kr[u] = *reinterpret_cast<const U16x8*>(kb + o[u]);
+      vr[u] = *reinterpret_cast<const U16x8*>(vb + o[u]);
     }
+    // the U scores of this iteration are independent (their lane-group sums overlap), then ONE
+    // online-softmax update folds them in: the dependent chain per iteration is one reduction and
+    // one rescale, not U of each. Token t0 (u = 0) is always valid, so the running max is finite.
+    float sv[G][U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int t = t0 + u * TPB;
-      float kf[8], vf[8];
-      if (own_new && t == pnew && dact) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          kf[j] = knew[dslot * 8 + j];
-          vf[j] = vnew[dslot * 8 + j];
-        }
-      } else if (t < c1 && dact) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          kf[j] = bf2f(kr[u].v[j]);
-          vf[j] = bf2f(vr[u].v[j]);
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) kf[j] = vf[j] = 0.f;
-      }
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        float sv = 0.f;
+        float d = 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) sv = fmaf(q[g][j], kf[j], sv);
-#pragma unroll
-        for (int o = 1; o < LPT; o <<= 1) sv += __shfl_xor(sv, o, 64);
-        if (t < c1) {
-          sv += slope[g] * (float)(t - (L - 1));
-          const float mn = fmaxf(m[g], sv);
-          const float cs = __expf(m[g] - mn), pv = __expf(sv - mn);
-          l[g] = l[g] * cs + pv;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) acc[g][j] = fmaf(acc[g][j], cs, pv * vf[j]);
-          m[g] = mn;
-        }
+        for (int j = 0; j < 8; ++j) d = fmaf(q[g][j], bf2f(kr[u].v[j]), d);  // q == 0 on inactive lanes
+        d = group_sum<LPT>(d);
+        sv[g][u] = t < ce ? d + slope[g] * (float)(t - (L - 1)) : -INFINITY;
       }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      float mx = sv[g][0];
+#pragma unroll
+      for (int u = 1; u < U; ++u) mx = fmaxf(mx, sv[g][u]);
+      const float mn = fmaxf(m[g], mx);
+      const float cs = __expf(m[g] - mn);
+      float pu[U], ps = 0.f;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        pu[u] = __expf(sv[g][u] - mn);  // 0 for tokens past the split
+        ps += pu[u];
+      }
+      l[g] = l[g] * cs + ps;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float a = acc[g][j] * cs;
+#pragma unroll
+        for (int u = 0; u < U; ++u) a = fmaf(pu[u], bf2f(vr[u].v[j]), a);
+        acc[g][j] = a;
+      }
+      m[g] = mn;
+    }
+  }
+  DSTAMP(4);
+  // the last token, into lane group (wave 0, tsub 0): its lanes 0..ND-1 are the threads tid < ND
+  // that hold its K / V slices (every LPT >= ND)
+  if (own_last && wid == 0 && tsub == 0) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      float sv = 0.f;
+      if (dact) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sv = fmaf(q[g][j], bf2f(knraw.v[j]), sv);
+      }
+      sv = group_sum<LPT>(sv);
+      const float mn = fmaxf(m[g], sv);
+      const float cs = __expf(m[g] - mn), pv = __expf(sv - mn);
+      l[g] = l[g] * cs + pv;
+      if (dact) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[g][j] = fmaf(acc[g][j], cs, pv * bf2f(vnraw.v[j]));
+      }
+      m[g] = mn;
     }
   }
 
@@ -352,6 +453,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
     for (int g = 0; g < G; ++g) store8f(gacc + (long long)(wid * G + g) * D + dslot * 8, acc[g]);
   }
   __syncthreads();
+  DSTAMP(5);
   for (int idx = tid; idx < G * D; idx += 256) {
     const int g = idx / D, d = idx % D;
     float M = -INFINITY;
@@ -375,6 +477,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
       }
     }
   }
+  DSTAMP(6);
   } else {
     // short splits (one iteration of U tokens per lane group: every B=1 split): scores of the split
     // into LDS, a block-wide softmax, then P.V -- measured faster there than the online form's
@@ -563,17 +666,18 @@ __global__ __launch_bounds__(256) void decode_combine_kernel(const float* __rest
   }
 }
 
-// Split size: enough (sequence, kv-head, split) workgroups for ~4 per CU on
-// the 256 CUs (each split streams its K rows, then its V rows, a few 16-B
-// loads per lane in flight: the pass is HBM-latency bound per workgroup, so
-// bandwidth comes from workgroup count), chunks of 32..1024 tokens.
+// Split size (ops/decode.py:decode_chunk documents the cold-cache sweep behind it):
+// ~256 (sequence, kv-head, split) workgroups of >= 64 tokens, one split for a cache
+// of <= 256 tokens, splits of at most 256 tokens once the cache reaches 2048.
 KCA_API int kca_decode_chunk(int B, int Hkv, int max_kv) {
-  long long work = (long long)B * Hkv;
-  long long want = (1024 + work - 1) / work;
+  if (max_kv <= 256) return max(64, (max_kv + 31) / 32 * 32);
+  const long long work = (long long)B * Hkv;
+  const long long want = (256 + work - 1) / work;
   long long c = (max_kv + want - 1) / want;
   c = (c + 31) / 32 * 32;
-  if (c < 32) c = 32;
-  if (c > 1024) c = 1024;
+  const long long cap = max_kv >= 2048 ? 256 : 1024;
+  if (c > cap) c = cap;
+  if (c < 64) c = 64;
   return (int)c;
 }
 
@@ -619,7 +723,7 @@ KCA_API int kca_decode_attn(const void* q, long long q_bs, const void* kc, const
                             int tbl_stride, int ps_shift, hipStream_t stream) {
   DecodeParams p{(const bf16_t*)q, q_bs, (const bf16_t*)kc, (const bf16_t*)vc, cs_slot, cs_head,
                  cs_pos, slots, kv_lens, (bf16_t*)out, o_bs, nullptr, nullptr, alibi, tbl, tbl_stride, ps_shift,
-                 H, Hkv, D, chunk, scale, 0, 0, 0, nullptr, nullptr};
+                 H, Hkv, D, chunk, scale, 0, 0, 0, nullptr, nullptr, g_decode_stamps};
   return decode_attn_launch(p, ws, ws_floats, B, max_kv, chunk, stream);
 }
 
@@ -637,7 +741,7 @@ KCA_API int kca_decode_prep_attn(const void* qkv, long long ld, const void* kc, 
   if (rot > D || (rot & 1) || (rot > 0 && (!cos_t || !sin_t))) return 8;
   DecodeParams p{(const bf16_t*)qkv, ld, (const bf16_t*)kc, (const bf16_t*)vc, cs_slot, cs_head,
                  cs_pos, slots, kv_lens, (bf16_t*)out, o_bs, nullptr, nullptr, alibi, tbl, tbl_stride, ps_shift,
-                 H, Hkv, D, chunk, scale, 1, rot, interleaved, cos_t, sin_t};
+                 H, Hkv, D, chunk, scale, 1, rot, interleaved, cos_t, sin_t, g_decode_stamps};
   return decode_attn_launch(p, ws, ws_floats, B, max_kv, chunk, stream);
 }
 

@@ -95,19 +95,29 @@ def decode_ws_floats(B: int, H: int, Hkv: int, D: int, max_kv: int, chunk: int =
     return B * H * ns * (D + 2) if ns > 1 else 0
 
 
-_DECODE_WGS = int(os.environ.get("KCA_DECODE_WGS", "1024"))  # split-K workgroup target (A/B knob)
+_DECODE_WGS = int(os.environ.get("KCA_DECODE_WGS", "256"))  # split-K workgroup target (A/B knob)
+_OLD_POLICY = os.environ.get("KCA_DECODE_SPLIT_POLICY", "") == "wgs1024"
 
 
 def decode_chunk(B: int, Hkv: int, max_kv: int) -> int:
-    """Mirror of kca_decode_chunk: ~1024 (seq, head, split) workgroups, 4 per
-    CU (each split's K then V stream is latency bound, so bandwidth comes from
-    workgroup count; swept 256..2048 on MI355X, GPT-J B=8/32 best at 1024),
-    chunks of 32..1024 tokens."""
+    """Mirror of kca_decode_chunk. Measured on MI355X with cold caches (the decode
+    regime: a layer's KV was last touched a full weight stream ago;
+    profiles/decode_attn_cold_sweep_r2.jsonl): a split of the one-pass kernel costs
+    about one HBM round trip per 32 tokens, so ~256 (sequence, head, split)
+    workgroups of >= 64 tokens beat many short splits (B=1, 600 cached tokens: 64-token
+    splits 11.5 us vs 32-token 20.1 us), a cache of <= 256 tokens is one split, and
+    long caches stop at 256-token splits (more workgroups beat longer chains there)."""
+    if _OLD_POLICY:  # A/B: the earlier ~1024-workgroup, 32..1024-token policy
+        want = -(-1024 // (B * Hkv))
+        return max(32, min(1024, -(-(-(-max_kv // want)) // 32) * 32))
+    if max_kv <= 256:
+        return max(64, -(-max_kv // 32) * 32)
     work = B * Hkv
     want = -(-_DECODE_WGS // work)
     c = -(-max_kv // want)
     c = -(-c // 32) * 32
-    return max(32, min(1024, c))
+    cap = 256 if max_kv >= 2048 else 1024
+    return max(64, min(cap, c))
 
 
 def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slots: torch.Tensor,

@@ -363,9 +363,13 @@ def test_layer_split_gpu_cpu_engine(tmp_path):
 
 @pytest.mark.parametrize("D,rot,inter,G,PS", [(256, 64, True, 1, 64), (256, 64, True, 1, 0), (128, 32, False, 4, 16),
                                               (80, 20, False, 1, 0), (64, 0, False, 2, 32)])
-def test_decode_prep_attention_fused_equals_two_kernels(D, rot, inter, G, PS):
+@pytest.mark.parametrize("CH", [0, 128])
+def test_decode_prep_attention_fused_equals_two_kernels(D, rot, inter, G, PS, CH, monkeypatch):
     """kca_decode_prep_attn (one launch) == kca_decode_prep + kca_decode_attn, bit for bit:
-    same rotated Q, same appended K/V rows, same attention output."""
+    same rotated Q, same appended K/V rows, same attention output (CH 128: the one-pass
+    online-softmax kernel, which folds the last token in after its loop in both modes)."""
+    if CH:
+        monkeypatch.setattr(dops, "decode_chunk", lambda *a: CH)
     torch.manual_seed(D + rot + G)
     B, Hkv, L = 5, 4, 512
     H = Hkv * G
@@ -383,7 +387,7 @@ def test_decode_prep_attention_fused_equals_two_kernels(D, rot, inter, G, PS):
     k1, v1, k2, v2 = kc.clone(), vc.clone(), kc.clone(), vc.clone()
     q1, q2 = qkv.clone(), qkv.clone()
     dops.decode_prep(q1, H, Hkv, D, rot, inter, cos, sin, pos, slots, k1, v1, block_table=tbl)
-    a = dops.decode_attention(q1, k1, v1, slots, kl, H, L, block_table=tbl)
+    a = dops.decode_attention(q1, k1, v1, slots, kl, H, L, block_table=tbl, chunk=CH)
     b = dops.decode_prep_attention(q2, H, Hkv, D, rot, inter, cos, sin, pos, slots, k2, v2, kl, L, block_table=tbl)
     torch.cuda.synchronize()
     assert torch.equal(k1, k2) and torch.equal(v1, v2)
