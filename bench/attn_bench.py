@@ -29,6 +29,10 @@ SHAPES = {
     "sd_64": (16, 4096, 4096, 8, 40, False),
     "sd_64_pad64": (16, 4096, 4096, 8, 64, False),  # SD heads zero-padded 40 -> 64 (UNet inference path)
     "sd_32": (16, 1024, 1024, 8, 80, False),
+    "sd_32_pad96": (16, 1024, 1024, 8, 96, False),  # 80 -> 96 (UNet padding onto the D=96 full-tile kernels)
+    "sd_16": (16, 256, 256, 8, 160, False),
+    "d160_1k": (16, 1024, 1024, 8, 160, False),
+    "d160_4k": (4, 4096, 4096, 8, 160, True),  # SD-1.5 1280-channel heads (native D=160 full tiles)
     "sd_cross": (16, 4096, 77, 8, 40, False),
 }
 

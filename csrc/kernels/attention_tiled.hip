@@ -1,4 +1,4 @@
-// Flash attention forward + backward, full-tile fast path for head_dim 64 / 128 / 256 (K2).
+// Flash attention forward + backward, full-tile fast path for head_dim 64 / 96 / 128 / 160 / 256 (K2).
 //
 // The generic kernels in attention.hip handle every shape (ALiBi, per-batch
 // key lengths, ragged tiles, padded head dims). This file holds the path the
@@ -66,36 +66,89 @@ __device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) {
   return pack_bf16x2(lo, hi);
 }
 
-template <int CPT, int RPI>
-__device__ __forceinline__ void stage_load(u32x4 (&sk)[CPT], u32x4 (&sv)[CPT], const bf16_t* kst,
-                                           const bf16_t* vst, int k0, long long k_st, long long v_st) {
-#pragma unroll
-  for (int i = 0; i < CPT; ++i) {
-    sk[i] = *reinterpret_cast<const u32x4*>(kst + (long long)(k0 + i * RPI) * k_st);
-    sv[i] = *reinterpret_cast<const u32x4*>(vst + (long long)(k0 + i * RPI) * v_st);
-  }
-}
+// Staging of a 32-row x D tile by the 256 threads of a workgroup: chunk idx = tid + 256*i is
+// (row idx / NCH, 16-B chunk idx % NCH). D = 96 / 160 serve SD-1.5's 80-wide heads (padded to
+// 96) and its 160-wide heads (native) instead of padding them to 128 / 256.
+template <int D, bool POW2 = (256 % (D / 8)) == 0>
+struct Stager;
 
-// K image at `buf`, V image at buf + tile bytes; chunk i of this thread is
-// (row0 + i*RPI, ch) -- the XOR term depends on the row, so each i gets its
-// own offset (folded by the compiler to a few adds).
-template <int CPT, int RPI, int D>
-__device__ __forceinline__ void stage_store(const u32x4 (&sk)[CPT], const u32x4 (&sv)[CPT], char* buf,
-                                            int row0, int ch) {
-#pragma unroll
-  for (int i = 0; i < CPT; ++i) {
-    const int o = img_off<D>(row0 + i * RPI, ch);
-    *reinterpret_cast<u32x4*>(buf + o) = sk[i];
-    *reinterpret_cast<u32x4*>(buf + 32 * D * 2 + o) = sv[i];
+// D = 64 / 128 / 256: thread tid owns chunk column tid % NCH of rows tid / NCH + i * RPI
+template <int D>
+struct Stager<D, true> {
+  static constexpr int NCH = D / 8, CPT = 32 * NCH / 256, RPI = 256 / NCH;
+  long long ok_, ov_;  // element offset of this thread's first chunk in a K / V tile
+  int row0_, ch_;
+  __device__ __forceinline__ Stager(int tid, long long k_st, long long v_st) {
+    row0_ = tid / NCH;
+    ch_ = tid % NCH;
+    ok_ = (long long)row0_ * k_st + ch_ * 8;
+    ov_ = (long long)row0_ * v_st + ch_ * 8;
   }
-}
+  __device__ __forceinline__ void load(u32x4 (&sk)[CPT], u32x4 (&sv)[CPT], const bf16_t* kb, const bf16_t* vb,
+                                       int k0, long long k_st, long long v_st) const {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      sk[i] = *reinterpret_cast<const u32x4*>(kb + ok_ + (long long)(k0 + i * RPI) * k_st);
+      sv[i] = *reinterpret_cast<const u32x4*>(vb + ov_ + (long long)(k0 + i * RPI) * v_st);
+    }
+  }
+  __device__ __forceinline__ void store(const u32x4 (&sk)[CPT], const u32x4 (&sv)[CPT], char* buf) const {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int o = img_off<D>(row0_ + i * RPI, ch_);
+      *reinterpret_cast<u32x4*>(buf + o) = sk[i];
+      *reinterpret_cast<u32x4*>(buf + 32 * D * 2 + o) = sv[i];
+    }
+  }
+};
+
+// D = 96 / 160 (NCH 12 / 20): 32 * NCH chunks are not a multiple of 256, so the last i covers
+// the first (32 * NCH) % 256 threads (whole waves) and each i has its own (row, chunk), with the
+// element offsets precomputed once, outside the key loop
+template <int D>
+struct Stager<D, false> {
+  static constexpr int NCH = D / 8, TOT = 32 * NCH, CPT = (TOT + 255) / 256;
+  static_assert(D % 32 == 0 && TOT % 64 == 0, "tiled attention: D multiple of 32");
+  long long ok_[CPT], ov_[CPT];
+  int lds_[CPT];
+  bool tail_;  // this thread owns a chunk in the last, partial round
+  __device__ __forceinline__ Stager(int tid, long long k_st, long long v_st) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int idx = min(tid + 256 * i, TOT - 1);
+      const int row = idx / NCH, ch = idx % NCH;
+      ok_[i] = (long long)row * k_st + ch * 8;
+      ov_[i] = (long long)row * v_st + ch * 8;
+      lds_[i] = img_off<D>(row, ch);
+    }
+    tail_ = tid + 256 * (CPT - 1) < TOT;
+  }
+  __device__ __forceinline__ void load(u32x4 (&sk)[CPT], u32x4 (&sv)[CPT], const bf16_t* kb, const bf16_t* vb,
+                                       int k0, long long k_st, long long v_st) const {
+    const bf16_t* kr = kb + (long long)k0 * k_st;
+    const bf16_t* vr = vb + (long long)k0 * v_st;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {  // a clamped tail chunk re-reads a valid chunk (never stored)
+      sk[i] = *reinterpret_cast<const u32x4*>(kr + ok_[i]);
+      sv[i] = *reinterpret_cast<const u32x4*>(vr + ov_[i]);
+    }
+  }
+  __device__ __forceinline__ void store(const u32x4 (&sk)[CPT], const u32x4 (&sv)[CPT], char* buf) const {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      if (i < CPT - 1 || tail_) {
+        *reinterpret_cast<u32x4*>(buf + lds_[i]) = sk[i];
+        *reinterpret_cast<u32x4*>(buf + 32 * D * 2 + lds_[i]) = sv[i];
+      }
+    }
+  }
+};
 
 template <int D, bool CAUSAL>
 __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel(FastFwdParams p) {
   constexpr int BM = 128, BN = 32;
   constexpr int TILE = BN * D * 2;           // bytes per K or V tile
-  constexpr int NCH = D / 8;                 // 16-B chunks per row
-  constexpr int CPT = BN * NCH / 256;        // chunks per thread per tile
+  constexpr int CPT = Stager<D>::CPT;       // 16-B chunks per thread per tile
   __shared__ __attribute__((aligned(16))) char smem[3 * 2 * TILE];  // [buf 0..2][K|V]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -133,12 +186,8 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel
     for (int r = 0; r < 16; ++r) oacc[i][r] = 0.f;
   float m = 0.f, lsum = 0.f;  // m: reference max (log2 units), set by tile 0
 
-  // staging: thread handles chunks idx = tid + i*256 -> row = tid/NCH + i*RPI,
-  // ch = tid % NCH (256 % NCH == 0)
-  constexpr int RPI = 256 / NCH;
-  const int st_row = tid / NCH, st_ch = tid % NCH;
-  const bf16_t* kst = kp + (long long)st_row * p.k_st + st_ch * 8;
-  const bf16_t* vst = vp + (long long)st_row * p.v_st + st_ch * 8;
+  // staging: thread handles chunks idx = tid + i*256 (Stager)
+  const Stager<D> stg(tid, p.k_st, p.v_st);
   u32x4 sk[CPT], sv[CPT];
 
   // per-lane read bases (bytes)
@@ -185,10 +234,10 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel
       if ((r & 3) + 8 * (r >> 2) > lim) acc[r] = -INFINITY;
   };
 
-  stage_load<CPT, RPI>(sk, sv, kst, vst, 0, p.k_st, p.v_st);
-  stage_store<CPT, RPI, D>(sk, sv, smem, st_row, st_ch);
-  stage_load<CPT, RPI>(sk, sv, kst, vst, min(BN, (ntiles - 1) * BN), p.k_st, p.v_st);
-  stage_store<CPT, RPI, D>(sk, sv, smem + 2 * TILE, st_row, st_ch);
+  stg.load(sk, sv, kp, vp, 0, p.k_st, p.v_st);
+  stg.store(sk, sv, smem);
+  stg.load(sk, sv, kp, vp, min(BN, (ntiles - 1) * BN), p.k_st, p.v_st);
+  stg.store(sk, sv, smem + 2 * TILE);
   __syncthreads();
 
   const int nfree = CAUSAL ? ntiles - 4 : ntiles;  // tiles no wave needs masked
@@ -217,7 +266,7 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel
     const char* Kn = smem + ((t + 1) % 3) * 2 * TILE;
     // the loads of tile t+2 (clamped: the last iterations re-load a tile that
     // is never stored)
-    stage_load<CPT, RPI>(sk, sv, kst, vst, min((t + 2) * BN, (ntiles - 1) * BN), p.k_st, p.v_st);
+    stg.load(sk, sv, kp, vp, min((t + 2) * BN, (ntiles - 1) * BN), p.k_st, p.v_st);
     // keep the staging loads above and the LDS stores below on their own
     // sides of the MFMAs (without the fences hipcc stores each load right
     // after it, behind a vmcnt(0))
@@ -257,7 +306,7 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel
     }
     sa = sb;
     asm volatile("" ::: "memory");
-    if (t + 2 < ntiles) stage_store<CPT, RPI, D>(sk, sv, smem + ((t + 2) % 3) * 2 * TILE, st_row, st_ch);
+    if (t + 2 < ntiles) stg.store(sk, sv, smem + ((t + 2) % 3) * 2 * TILE);
     __syncthreads();
   };
   for (int t = 0; t < nfree; ++t) tile_step(t, std::false_type{});
@@ -354,7 +403,7 @@ template <int D, bool CAUSAL>
 __global__ void __launch_bounds__(256, 1) attn_bwd_dq_tiled_kernel(FastBwdParams p) {
   constexpr int BM = 128, BN = 32;
   constexpr int TILE = BN * D * 2;
-  constexpr int NCH = D / 8, CPT = BN * NCH / 256, RPI = 256 / NCH;
+  constexpr int CPT = Stager<D>::CPT;
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -391,16 +440,16 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq_tiled_kernel(FastBwdParams
 #pragma unroll
     for (int r = 0; r < 16; ++r) dq[i][r] = 0.f;
 
-  const int st_row = tid / NCH, st_ch = tid % NCH;
-  const bf16_t* kst = p.k + b * p.k_sb + hk * p.k_sh + (long long)st_row * p.k_st + st_ch * 8;
-  const bf16_t* vst = p.v + b * p.v_sb + hk * p.v_sh + (long long)st_row * p.v_st + st_ch * 8;
+  const bf16_t* kst = p.k + b * p.k_sb + hk * p.k_sh;
+  const bf16_t* vst = p.v + b * p.v_sb + hk * p.v_sh;
+  const Stager<D> stg(tid, p.k_st, p.v_st);
   u32x4 sk[CPT], sv[CPT];
   int be, bo, b1, b2;
   row_bases<D>(l32, hh, be, bo);
   tr_bases<D>(lane, b1, b2);
 
-  stage_load<CPT, RPI>(sk, sv, kst, vst, 0, p.k_st, p.v_st);
-  stage_store<CPT, RPI, D>(sk, sv, smem, st_row, st_ch);
+  stg.load(sk, sv, kst, vst, 0, p.k_st, p.v_st);
+  stg.store(sk, sv, smem);
   __syncthreads();
   // the last 4 tiles hold the four waves' diagonals; earlier tiles run the
   // mask-free body. Tiles wholly above a wave's rows are masked, not skipped.
@@ -409,7 +458,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq_tiled_kernel(FastBwdParams
     const int k0 = t * BN;
     const char* Ks = smem + (t & 1) * 2 * TILE;
     const char* Vs = Ks + TILE;
-    stage_load<CPT, RPI>(sk, sv, kst, vst, min(k0 + BN, (ntiles - 1) * BN), p.k_st, p.v_st);
+    stg.load(sk, sv, kst, vst, min(k0 + BN, (ntiles - 1) * BN), p.k_st, p.v_st);
     asm volatile("" ::: "memory");
     f32x16 st, dpt;
 #pragma unroll
@@ -466,7 +515,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq_tiled_kernel(FastBwdParams
       }
     }
     asm volatile("" ::: "memory");
-    if (t + 1 < ntiles) stage_store<CPT, RPI, D>(sk, sv, smem + ((t + 1) & 1) * 2 * TILE, st_row, st_ch);
+    if (t + 1 < ntiles) stg.store(sk, sv, smem + ((t + 1) & 1) * 2 * TILE);
     __syncthreads();
   };
   const int nfree = CAUSAL ? ntiles - 4 : ntiles;
@@ -479,7 +528,7 @@ template <int D, bool CAUSAL>
 __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_tiled_kernel(FastBwdParams p) {
   constexpr int BK = 128, BQ = 32;
   constexpr int TILE = BQ * D * 2;                  // one 32-row image
-  constexpr int NCH = D / 8, CPT = BQ * NCH / 256, RPI = 256 / NCH;
+  constexpr int NCH = D / 8, CPT = Stager<D>::CPT;
   constexpr int VOFF = 4 * TILE;                    // V images of the 4 waves
   constexpr int LOFF = VOFF + 4 * TILE;             // lse/delta: [buf][64] floats
   __shared__ __attribute__((aligned(16))) char smem[LOFF + 2 * 64 * 4];
@@ -521,9 +570,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_tiled_kernel(FastBwdPara
   const int nqt = (p.Sq - q_lo) / BQ;
   const int total = nqt * grp;
 
-  const int st_row = tid / NCH, st_ch = tid % NCH;
-  const long long q_row_off = (long long)st_row * p.q_st + st_ch * 8;
-  const long long g_row_off = (long long)st_row * p.do_st + st_ch * 8;
+  const Stager<D> stg(tid, p.q_st, p.do_st);
   u32x4 sq[CPT], sg[CPT];
   float lreg = 0.f;
   int be, bo, b1, b2;
@@ -533,8 +580,8 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_tiled_kernel(FastBwdPara
 #define KCA_DKDV_LOAD(it_)                                                                     \
   {                                                                                            \
     const int hq_ = hk * grp + (it_) / nqt, qt_ = q_lo + ((it_) % nqt) * BQ;                   \
-    stage_load<CPT, RPI>(sq, sg, p.q + b * p.q_sb + hq_ * p.q_sh + q_row_off,                  \
-                         p.dout + b * p.do_sb + hq_ * p.do_sh + g_row_off, qt_, p.q_st, p.do_st); \
+    stg.load(sq, sg, p.q + b * p.q_sb + hq_ * p.q_sh, p.dout + b * p.do_sb + hq_ * p.do_sh, qt_,   \
+             p.q_st, p.do_st);                                                                 \
     if (tid < 64) {                                                                            \
       const long long li_ = ((long long)b * p.H + hq_) * p.Sq + qt_ + (tid & 31);              \
       lreg = tid < 32 ? p.lse[li_] * kLog2e : p.delta[li_];                                    \
@@ -542,7 +589,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_tiled_kernel(FastBwdPara
   }
 #define KCA_DKDV_STORE(buf_)                                                                   \
   {                                                                                            \
-    stage_store<CPT, RPI, D>(sq, sg, smem + (buf_) * 2 * TILE, st_row, st_ch);                 \
+    stg.store(sq, sg, smem + (buf_) * 2 * TILE);                                               \
     if (tid < 64) reinterpret_cast<float*>(smem + LOFF)[(buf_) * 64 + tid] = lreg;             \
   }
 
@@ -669,7 +716,9 @@ KCA_API int kca_attn_fwd_tiled(const void* q, const void* k, const void* v, void
                                long long v_sh, long long o_sb, long long o_st, long long o_sh,
                                int B, int Sq, int Sk, int H, int Hkv, int d, int causal,
                                float scale, int* flags, hipStream_t stream) {
-  if ((d != 64 && d != 128 && d != 256) || Sq % 128 || Sk % 32 || Sq <= 0 || H % Hkv || !flags) return 1;
+  if ((d != 64 && d != 96 && d != 128 && d != 160 && d != 256) || Sq % 128 || Sk % 32 || Sq <= 0 || H % Hkv ||
+      !flags)
+    return 1;
   if (causal && Sk < Sq) return 1;
   FastFwdParams p{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, lse, flags,
                   q_sb, q_st, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh, o_sb, o_st, o_sh,
@@ -679,9 +728,15 @@ KCA_API int kca_attn_fwd_tiled(const void* q, const void* k, const void* v, void
   if (d == 256) {
     if (causal) hipLaunchKernelGGL((attn_fwd_tiled_kernel<256, true>), grid, dim3(256), 0, stream, p);
     else hipLaunchKernelGGL((attn_fwd_tiled_kernel<256, false>), grid, dim3(256), 0, stream, p);
+  } else if (d == 160) {  // SD-1.5 1280-channel heads
+    if (causal) hipLaunchKernelGGL((attn_fwd_tiled_kernel<160, true>), grid, dim3(256), 0, stream, p);
+    else hipLaunchKernelGGL((attn_fwd_tiled_kernel<160, false>), grid, dim3(256), 0, stream, p);
   } else if (d == 128) {
     if (causal) hipLaunchKernelGGL((attn_fwd_tiled_kernel<128, true>), grid, dim3(256), 0, stream, p);
     else hipLaunchKernelGGL((attn_fwd_tiled_kernel<128, false>), grid, dim3(256), 0, stream, p);
+  } else if (d == 96) {  // SD-1.5 640-channel heads (80) zero-padded by the UNet
+    if (causal) hipLaunchKernelGGL((attn_fwd_tiled_kernel<96, true>), grid, dim3(256), 0, stream, p);
+    else hipLaunchKernelGGL((attn_fwd_tiled_kernel<96, false>), grid, dim3(256), 0, stream, p);
   } else {  // 64: GPT-2 / CLIP heads, SD-1.5 heads (40) zero-padded by the UNet inference path
     if (causal) hipLaunchKernelGGL((attn_fwd_tiled_kernel<64, true>), grid, dim3(256), 0, stream, p);
     else hipLaunchKernelGGL((attn_fwd_tiled_kernel<64, false>), grid, dim3(256), 0, stream, p);
@@ -700,7 +755,8 @@ KCA_API int kca_attn_bwd_tiled(const void* q, const void* k, const void* v, cons
                                long long dk_st, long long dk_sh, long long dv_sb, long long dv_st,
                                long long dv_sh, int B, int Sq, int Sk, int H, int Hkv, int d,
                                int causal, float scale, hipStream_t stream) {
-  if ((d != 64 && d != 128 && d != 256) || Sq % 128 || Sk % 128 || Sq <= 0 || H % Hkv) return 1;
+  if ((d != 64 && d != 96 && d != 128 && d != 160 && d != 256) || Sq % 128 || Sk % 128 || Sq <= 0 || H % Hkv)
+    return 1;
   if (causal && Sk < Sq) return 1;
   FastBwdParams p{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout,
                   (bf16_t*)dq, (bf16_t*)dk, (bf16_t*)dv, lse, delta,
@@ -715,6 +771,22 @@ KCA_API int kca_attn_bwd_tiled(const void* q, const void* k, const void* v, cons
     } else {
       hipLaunchKernelGGL((attn_bwd_dkdv_tiled_kernel<256, false>), g1, dim3(256), 0, stream, p);
       hipLaunchKernelGGL((attn_bwd_dq_tiled_kernel<256, false>), g2, dim3(256), 0, stream, p);
+    }
+  } else if (d == 160) {
+    if (causal) {
+      hipLaunchKernelGGL((attn_bwd_dkdv_tiled_kernel<160, true>), g1, dim3(256), 0, stream, p);
+      hipLaunchKernelGGL((attn_bwd_dq_tiled_kernel<160, true>), g2, dim3(256), 0, stream, p);
+    } else {
+      hipLaunchKernelGGL((attn_bwd_dkdv_tiled_kernel<160, false>), g1, dim3(256), 0, stream, p);
+      hipLaunchKernelGGL((attn_bwd_dq_tiled_kernel<160, false>), g2, dim3(256), 0, stream, p);
+    }
+  } else if (d == 96) {
+    if (causal) {
+      hipLaunchKernelGGL((attn_bwd_dkdv_tiled_kernel<96, true>), g1, dim3(256), 0, stream, p);
+      hipLaunchKernelGGL((attn_bwd_dq_tiled_kernel<96, true>), g2, dim3(256), 0, stream, p);
+    } else {
+      hipLaunchKernelGGL((attn_bwd_dkdv_tiled_kernel<96, false>), g1, dim3(256), 0, stream, p);
+      hipLaunchKernelGGL((attn_bwd_dq_tiled_kernel<96, false>), g2, dim3(256), 0, stream, p);
     }
   } else if (d == 128) {
     if (causal) {

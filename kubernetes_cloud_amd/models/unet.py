@@ -146,7 +146,14 @@ class ResnetBlock2D(nn.Module):
 # Head padding for the self-attention (see Attention.forward); KCA_SD_PAD_HEADS=0
 # disables it, KCA_SD_PAD_HEADS_TRAIN=0 only in training. _PAD_GEN counts padded-weight rebuilds so a HIP
 # graph captured over the old buffers knows to re-capture (sd_pipeline.UNetGraph).
-PAD_HEAD_DIM = 64
+_TILED_DIMS = (64, 96, 128, 160, 256)  # attention_tiled.hip instantiations
+
+
+def padded_head_dim(hd: int) -> int:
+    """Smallest full-tile head dim >= hd: 40 -> 64, 80 -> 96 (160 runs natively)."""
+    return next((d for d in _TILED_DIMS if d >= hd), hd)
+
+
 _PAD_HEADS = os.environ.get("KCA_SD_PAD_HEADS", "1") not in ("0", "false")
 _PAD_TRAIN = os.environ.get("KCA_SD_PAD_HEADS_TRAIN", "1") not in ("0", "false")
 _PAD_GEN = 0
@@ -173,14 +180,14 @@ class Attention(nn.Module):
         self._padded = None  # weights may change while training: rebuild on the next inference call
         return super().train(mode)
 
-    def _padded_weights(self, hd: int):
-        """One fused QKV weight with each head zero-padded to PAD_HEAD_DIM rows,
-        and the out-projection with matching zero columns (built once per
-        eval phase; ``train()`` drops it)."""
+    def _padded_weights(self, hd: int, dp: int):
+        """One fused QKV weight with each head zero-padded to dp rows, and the
+        out-projection with matching zero columns (built once per eval phase;
+        ``train()`` drops it)."""
         p = getattr(self, "_padded", None)
         if p is None:
             global _PAD_GEN
-            H, dp = self.heads, PAD_HEAD_DIM
+            H = self.heads
             C = self.to_q.weight.shape[1]
             w = self.to_q.weight.new_zeros(3, H, dp, C)
             b = self.to_q.weight.new_zeros(3, H, dp)
@@ -199,25 +206,27 @@ class Attention(nn.Module):
     def forward(self, x, ctx=None):
         B, S, _ = x.shape
         hd = self.to_q.weight.shape[0] // self.heads
-        pad = ctx is None and x.is_cuda and hd < PAD_HEAD_DIM and hd % 8 == 0 and S % 128 == 0 and _PAD_HEADS
+        dpad = padded_head_dim(hd)
+        pad = ctx is None and x.is_cuda and dpad != hd and hd % 8 == 0 and S % 128 == 0 and _PAD_HEADS
         if pad and torch.is_grad_enabled() and _PAD_TRAIN:
             # training: pad the q/k/v activations instead (F.pad's backward slices the
             # gradients back) so the backward also runs the full-tile D=64 kernels.
             # Attention fwd+bwd 4.50 -> 3.31 ms; DreamBooth 93.4 -> 96.4 samples/s
             # (same-box A/B, profiles/sd_bench_r1_v11_gn_add_padtrain.jsonl);
             # KCA_SD_PAD_HEADS_TRAIN=0 disables.
-            dp = PAD_HEAD_DIM - hd
+            dp = dpad - hd
             q, k, v = (F.pad(lin(x).view(B, S, self.heads, hd), (0, dp))
                        for lin in (self.to_q, self.to_k, self.to_v))
             o = ops.flash_attention(q, k, v, causal=False, scale=1.0 / math.sqrt(hd))
             return self.to_out[0](o[..., :hd].reshape(B, S, -1))
         if pad and not torch.is_grad_enabled():
-            # inference self-attention on the full-tile D=64 kernel (attention_tiled.hip):
-            # zero q/k columns leave Q.K^T unchanged, zero v columns give zero outputs that
-            # meet zero out-projection columns. SD-1.5 64x64-latent self-attention (B16 H8
-            # S4096 d40) 1.04 -> 0.71 ms on MI355X (profiles/attn_bench_r1_v7_d64.jsonl).
-            w, b, wo = self._padded_weights(hd)
-            qkv = F.linear(x, w, b).view(B, S, 3, self.heads, PAD_HEAD_DIM)
+            # inference self-attention on the full-tile kernels (attention_tiled.hip, D=64 for
+            # the 40-wide heads, D=96 for the 80-wide ones): zero q/k columns leave Q.K^T
+            # unchanged, zero v columns give zero outputs that meet zero out-projection columns.
+            # SD-1.5 64x64-latent self-attention (B16 H8 S4096 d40) 1.04 -> 0.71 ms on MI355X
+            # (profiles/attn_bench_r1_v7_d64.jsonl).
+            w, b, wo = self._padded_weights(hd, dpad)
+            qkv = F.linear(x, w, b).view(B, S, 3, self.heads, dpad)
             o = ops.flash_attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], causal=False,
                                     scale=1.0 / math.sqrt(hd))
             return F.linear(o.reshape(B, S, -1), wo, self.to_out[0].bias)

@@ -143,7 +143,7 @@ def test_attention_head_dims(D, causal):
     _attn_case(2, 200, 200, 4, 4, D, causal)
 
 
-@pytest.mark.parametrize("D", [128, 256])
+@pytest.mark.parametrize("D", [96, 128, 160, 256])
 @pytest.mark.parametrize("causal", [True, False])
 def test_attention_tiled_fast_path(D, causal):
     # Sq % 128 == 0, Sk % 32 == 0, no ALiBi / kv_len: attention_tiled.hip
@@ -153,7 +153,7 @@ def test_attention_tiled_fast_path(D, causal):
 
 
 @pytest.mark.parametrize("causal", [True, False])
-@pytest.mark.parametrize("D", [64, 128, 256])
+@pytest.mark.parametrize("D", [64, 96, 128, 160, 256])
 def test_attention_tiled_matches_generic(D, causal):
     """Fast and generic kernels agree (fwd output and all three grads)."""
     from kubernetes_cloud_amd.ops.attention import set_tiled_path
@@ -175,7 +175,7 @@ def test_attention_tiled_matches_generic(D, causal):
         assert _rel(a, b) < 1e-2, _rel(a, b)
 
 
-@pytest.mark.parametrize("D", [64, 128, 256])
+@pytest.mark.parametrize("D", [64, 96, 128, 160, 256])
 def test_attention_deferred_rescale_branch(D):
     """Scores whose row max keeps growing tile after tile (ramped key norms and
     a hot key per tile), so the deferred-rescale branch of the forward fires
@@ -194,7 +194,7 @@ def test_attention_deferred_rescale_branch(D):
         assert _rel(o, orf) < 2e-2, (causal, _rel(o, orf))
 
 
-@pytest.mark.parametrize("D", [64, 128, 256])
+@pytest.mark.parametrize("D", [64, 96, 128, 160, 256])
 def test_attention_tiled_overflow_fixup(D):
     """A key far past the first tile scores ~2^900 times higher than anything in
     tile 0: the fixed-reference-max fast path overflows, flags the rows, and the
