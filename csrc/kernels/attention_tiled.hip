@@ -30,6 +30,45 @@ constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
 constexpr float kRescaleThr = 8.0f;
 
+// Diagnostic build only (-DKCA_ATTN_STAMPS, bench/attn_stamps.py): per-wave s_memtime segment
+// sums of the main loops, added into g_attn_stamps once per wave at the end (fwd slots 0..7,
+// dQ 16..23, dK/dV 32..39). The fences around each stamp forbid overlaps the real kernel has: read
+// the shares, not the lengths. In the normal build every ASTAMP is empty.
+#ifdef KCA_ATTN_STAMPS
+__device__ unsigned long long g_attn_stamps[64];
+__device__ __forceinline__ unsigned long long ast_now() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define ASTAMP_DECL                                            \
+  unsigned long long st_acc_[8] = {0, 0, 0, 0, 0, 0, 0, 0}; \
+  unsigned long long st_prev_ = ast_now();
+#define ASTAMP(k)                           \
+  do {                                      \
+    const unsigned long long n_ = ast_now(); \
+    st_acc_[k] += n_ - st_prev_;            \
+    st_prev_ = n_;                          \
+  } while (0)
+#define ASTAMP_FLUSH(base)                                                          \
+  do {                                                                              \
+    st_acc_[7] = 1;                                                                 \
+    if ((threadIdx.x & 63) == 0)                                                    \
+      for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&g_attn_stamps[(base) + i_], st_acc_[i_]); \
+  } while (0)
+#else
+#define ASTAMP_DECL
+#define ASTAMP(k) \
+  do {            \
+  } while (0)
+#define ASTAMP_FLUSH(base) \
+  do {                     \
+  } while (0)
+#endif
+
+
 struct FastFwdParams {
   const bf16_t* q; const bf16_t* k; const bf16_t* v;
   bf16_t* o; float* lse;
@@ -151,6 +190,7 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel
   constexpr int CPT = Stager<D>::CPT;       // 16-B chunks per thread per tile
   __shared__ __attribute__((aligned(16))) char smem[3 * 2 * TILE];  // [buf 0..2][K|V]
 
+  ASTAMP_DECL
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, hh = lane >> 5, gi = lane & 15;
   const int nqb = p.Sq / BM;
@@ -238,6 +278,12 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel
   stg.store(sk, sv, smem);
   stg.load(sk, sv, kp, vp, min(BN, (ntiles - 1) * BN), p.k_st, p.v_st);
   stg.store(sk, sv, smem + 2 * TILE);
+  // D = 256 (one wave per SIMD, no other wave to cover a load): two tiles of K/V loads in flight
+  // in registers; tile 2 goes into set 0 before the loop (stored at the end of iteration 0).
+  // GPT-J fwd 0.563 -> 0.535 ms; at D = 160 it measured 3-4 % slower (profiles/attn_stamps_r2.md)
+  constexpr bool PF2 = D >= 256;
+  u32x4 sk2[CPT], sv2[CPT];
+  if constexpr (PF2) stg.load(sk, sv, kp, vp, min(2 * BN, (ntiles - 1) * BN), p.k_st, p.v_st);
   __syncthreads();
 
   const int nfree = CAUSAL ? ntiles - 4 : ntiles;  // tiles no wave needs masked
@@ -259,14 +305,23 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel
     m = fmaxf(mt, __shfl_xor(mt, 32, 64)) * sl2;
   }
   const float nm = -m;
+  ASTAMP(0);
 
-  auto tile_step = [&](int t, auto masked) {
+  auto tile_step = [&](int t, auto masked, auto par) {
     constexpr bool MASKED = decltype(masked)::value;
     const char* Vs = smem + (t % 3) * 2 * TILE + TILE;
     const char* Kn = smem + ((t + 1) % 3) * 2 * TILE;
-    // the loads of tile t+2 (clamped: the last iterations re-load a tile that
-    // is never stored)
-    stg.load(sk, sv, kp, vp, min((t + 2) * BN, (ntiles - 1) * BN), p.k_st, p.v_st);
+    // PF2: tile t+3 is requested into one register set while the other (tile t+2, requested an
+    // iteration ago) is stored at the end of this iteration; set parity = t & 1 = par.
+    // Otherwise the loads of tile t+2. (Clamped: the last iterations re-load a tile that is never
+    // stored.)
+    constexpr bool ODD = PF2 && decltype(par)::value;
+    u32x4(&ldk)[CPT] = (PF2 && !ODD) ? sk2 : sk;
+    u32x4(&ldv)[CPT] = (PF2 && !ODD) ? sv2 : sv;
+    u32x4(&stk)[CPT] = ODD ? sk2 : sk;
+    u32x4(&stv)[CPT] = ODD ? sv2 : sv;
+    stg.load(ldk, ldv, kp, vp, min((t + (PF2 ? 3 : 2)) * BN, (ntiles - 1) * BN), p.k_st, p.v_st);
+    ASTAMP(1);
     // keep the staging loads above and the LDS stores below on their own
     // sides of the MFMAs (without the fences hipcc stores each load right
     // after it, behind a vmcnt(0))
@@ -284,6 +339,7 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel
       pf1[r] = (__bf16)e1;
     }
     lsum += ps;
+    ASTAMP(2);
     {  // O^T += V^T P^T, V^T fragments one d-block ahead of their MFMAs
       auto vfrag = [&](int db, int s) {
         return cat8(lds_tr4(Vs, vb_1 + 2 * s * 16 * D + 512 * db), lds_tr4(Vs, vb_2 + 2 * s * 16 * D + 512 * db));
@@ -304,13 +360,34 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel
         __builtin_amdgcn_sched_group_barrier(0x8, 2, 0);
       }
     }
+    ASTAMP(3);
     sa = sb;
     asm volatile("" ::: "memory");
-    if (t + 2 < ntiles) stg.store(sk, sv, smem + ((t + 2) % 3) * 2 * TILE);
+    if (t + 2 < ntiles) stg.store(stk, stv, smem + ((t + 2) % 3) * 2 * TILE);
     __syncthreads();
+    ASTAMP(4);
   };
-  for (int t = 0; t < nfree; ++t) tile_step(t, std::false_type{});
-  for (int t = max(nfree, 0); t < ntiles; ++t) tile_step(t, std::true_type{});
+  if constexpr (PF2) {  // register-set parity must follow t: the loops advance two tiles per trip
+  int t = 0;
+  for (; t + 1 < nfree; t += 2) {
+    tile_step(t, std::false_type{}, std::false_type{});
+    tile_step(t + 1, std::false_type{}, std::true_type{});
+  }
+  if (t < nfree) {
+    tile_step(t, std::false_type{}, std::false_type{});
+    ++t;
+    if (t < ntiles) { tile_step(t, std::true_type{}, std::true_type{}); ++t; }
+  }
+  t = max(t, 0);
+  for (; t + 1 < ntiles; t += 2) {
+    tile_step(t, std::true_type{}, std::false_type{});
+    tile_step(t + 1, std::true_type{}, std::true_type{});
+  }
+  if (t < ntiles) tile_step(t, std::true_type{}, std::false_type{});
+  } else {
+  for (int t = 0; t < nfree; ++t) tile_step(t, std::false_type{}, std::false_type{});
+  for (int t = max(nfree, 0); t < ntiles; ++t) tile_step(t, std::true_type{}, std::false_type{});
+  }
 
   const float ltot = lsum + __shfl_xor(lsum, 32, 64);
   // row sums past 2^100 (or inf / NaN) mean P may have overflowed: flag the
@@ -332,6 +409,8 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel
       *reinterpret_cast<uint2*>(op + db * 32 + 8 * g + 4 * hh) = w;
     }
   }
+  ASTAMP(5);
+  ASTAMP_FLUSH(0);
 }
 
 
@@ -405,6 +484,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq_tiled_kernel(FastBwdParams
   constexpr int TILE = BN * D * 2;
   constexpr int CPT = Stager<D>::CPT;
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE];
+  ASTAMP_DECL
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, hh = lane >> 5;
@@ -451,6 +531,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq_tiled_kernel(FastBwdParams
   stg.load(sk, sv, kst, vst, 0, p.k_st, p.v_st);
   stg.store(sk, sv, smem);
   __syncthreads();
+  ASTAMP(0);
   // the last 4 tiles hold the four waves' diagonals; earlier tiles run the
   // mask-free body. Tiles wholly above a wave's rows are masked, not skipped.
   auto tile_step = [&](int t, auto masked) {
@@ -458,8 +539,12 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq_tiled_kernel(FastBwdParams
     const int k0 = t * BN;
     const char* Ks = smem + (t & 1) * 2 * TILE;
     const char* Vs = Ks + TILE;
+    // (a second register set of loads in flight -- as the forward's PF2 -- only moved this kernel's
+    // wait from the LDS store to the load issue: the K/V stream is throughput-bound per CU,
+    // profiles/attn_stamps_r2.md)
     stg.load(sk, sv, kst, vst, min(k0 + BN, (ntiles - 1) * BN), p.k_st, p.v_st);
     asm volatile("" ::: "memory");
+    ASTAMP(1);
     f32x16 st, dpt;
 #pragma unroll
     for (int r = 0; r < 16; ++r) { st[r] = 0.f; dpt[r] = 0.f; }
@@ -484,6 +569,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq_tiled_kernel(FastBwdParams
         __builtin_amdgcn_sched_group_barrier(0x8, 2, 0);
       }
     }
+    ASTAMP(2);
     const int lim = qrow + off - k0 - 4 * hh;  // visible key offsets (r&3)+8(r>>2) <= lim
     bf16x8 d0, d1;
 #pragma unroll
@@ -497,6 +583,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq_tiled_kernel(FastBwdParams
       d0[r] = (__bf16)(p0 * (dpt[r] - dl));
       d1[r] = (__bf16)(p1 * (dpt[r + 8] - dl));
     }
+    ASTAMP(3);
     {
       bf16x8 t0[2], t1[2];
       t0[0] = tr_frag<D>(Ks, b1, b2, 0, 0);
@@ -514,14 +601,18 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq_tiled_kernel(FastBwdParams
         __builtin_amdgcn_sched_group_barrier(0x8, 2, 0);
       }
     }
+    ASTAMP(4);
     asm volatile("" ::: "memory");
     if (t + 1 < ntiles) stg.store(sk, sv, smem + ((t + 1) & 1) * 2 * TILE);
     __syncthreads();
+    ASTAMP(5);
   };
   const int nfree = CAUSAL ? ntiles - 4 : ntiles;
   for (int t = 0; t < nfree; ++t) tile_step(t, std::false_type{});
   for (int t = max(nfree, 0); t < ntiles; ++t) tile_step(t, std::true_type{});
   store_acc_t<D>(p.dq + b * p.dq_sb + h * p.dq_sh + (long long)qrow * p.dq_st, dq, hh, p.scale);
+  ASTAMP(6);
+  ASTAMP_FLUSH(16);
 }
 
 template <int D, bool CAUSAL>
@@ -532,6 +623,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_tiled_kernel(FastBwdPara
   constexpr int VOFF = 4 * TILE;                    // V images of the 4 waves
   constexpr int LOFF = VOFF + 4 * TILE;             // lse/delta: [buf][64] floats
   __shared__ __attribute__((aligned(16))) char smem[LOFF + 2 * 64 * 4];
+  ASTAMP_DECL
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, hh = lane >> 5;
@@ -598,6 +690,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_tiled_kernel(FastBwdPara
     KCA_DKDV_STORE(0);
   }
   __syncthreads();
+  ASTAMP(0);
   auto tile_step = [&](int it, auto masked) {
     constexpr bool MASKED = decltype(masked)::value;
     const int qt = q_lo + (it % nqt) * BQ;
@@ -607,6 +700,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_tiled_kernel(FastBwdPara
     const int nx = min(it + 1, total - 1);
     KCA_DKDV_LOAD(nx);
     asm volatile("" ::: "memory");
+    ASTAMP(1);
     // No skip of the (at most 3 per head) q tiles that lie wholly above this
     // wave's keys: they are masked to P = 0 like the diagonal, which costs
     // ~4 % extra MFMAs under a causal mask but keeps the 256 dK/dV accumulator
@@ -641,6 +735,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_tiled_kernel(FastBwdPara
         __builtin_amdgcn_sched_group_barrier(0x8, 2, 0);
       }
     }
+    ASTAMP(2);
     // rows q = qt + 8g + 4hh + j (g = r>>2, j = r&3): lse / delta as float4;
     // visible iff key <= q + off, i.e. 8g + j >= key - qt - off - 4hh
     const int lim = key - qt - off - 4 * hh;
@@ -661,6 +756,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_tiled_kernel(FastBwdPara
         else { p1[r - 8] = (__bf16)pr; s1[r - 8] = (__bf16)ds; }
       }
     }
+    ASTAMP(3);
     // dV^T += dO^T.P, dK^T += Q^T.dS: the 8 transposed reads of block db+1 in flight under the 4
     // MFMAs of block db (same pinning)
     {
@@ -692,9 +788,11 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_tiled_kernel(FastBwdPara
         __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
       }
     }
+    ASTAMP(4);
     asm volatile("" ::: "memory");
     if (it + 1 < total) KCA_DKDV_STORE((it + 1) & 1);
     __syncthreads();
+    ASTAMP(5);
   };
   // One flat loop with the (cheap, select-only) causal mask on every tile:
   // splitting into masked / mask-free bodies -- by a per-tile branch or by
@@ -704,6 +802,8 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_tiled_kernel(FastBwdPara
 #undef KCA_DKDV_STORE
   store_acc_t<D>(p.dk + b * p.dk_sb + hk * p.dk_sh + (long long)key * p.dk_st, dk, hh, p.scale);
   store_acc_t<D>(p.dv + b * p.dv_sb + hk * p.dv_sh + (long long)key * p.dv_st, dv, hh, 1.f);
+  ASTAMP(6);
+  ASTAMP_FLUSH(32);
 }
 
 }  // namespace
@@ -807,3 +907,15 @@ KCA_API int kca_attn_bwd_tiled(const void* q, const void* k, const void* v, cons
   }
   return 0;
 }
+
+#ifdef KCA_ATTN_STAMPS
+// diagnostic build: copy out (and optionally clear) the 64 segment sums
+KCA_API int kca_attn_stamps(unsigned long long* host, int reset) {
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_attn_stamps), sizeof(unsigned long long) * 64) != hipSuccess) return 1;
+  if (reset) {
+    unsigned long long z[64] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_attn_stamps), z, sizeof(z)) != hipSuccess) return 1;
+  }
+  return 0;
+}
+#endif
