@@ -138,7 +138,17 @@ struct DecodeParams {
   const float* cos_t;
   const float* sin_t;
   unsigned long long* stamps;  // diagnostic: per-workgroup s_memrealtime stamps (nullptr in normal runs)
+  // split-K fan-in (nsplit > 1): one arrival counter per (sequence, kv-head); the last split to
+  // arrive combines the partials in place of the separate decode_combine_kernel (nullptr: that kernel)
+  unsigned int* cnt;
 };
+
+// Partials that another workgroup of the same launch combines: write-through (sc1) stores, so a
+// drain (vmcnt(0)) + barrier + counter add publishes them across XCDs without a release fence
+// (cdna_hip_programming.md Guideline 16, recipe R1).
+__device__ __forceinline__ void st_pub(float* a, float v) {
+  __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // diagnostic stamps (bench/decode_attn_bench.py --stamps): 8 per workgroup, 100 MHz clock
 static unsigned long long* g_decode_stamps = nullptr;
@@ -199,6 +209,62 @@ __device__ __forceinline__ float group_sum(float v) {
   return v;
 }
 
+// Split-K fan-in at the end of every split's workgroup (nsplit > 1): its partials (st_pub) are
+// drained by every storing wave, then one lane adds to the (sequence, kv-head) counter; the
+// workgroup that brings it to nsplit re-arms it, acquires (agent scope: drops this CU's stale
+// lines) and combines the G heads' splits -- what decode_combine_kernel does, minus a launch and
+// its dependency gap on the decode critical path (one per layer).
+template <int G>
+__device__ void fanin_combine(const DecodeParams& p, int b, int hk, int nsplit) {
+  __shared__ float wsp[1024];
+  __shared__ float red[8];
+  __shared__ int s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+  __syncthreads();
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    unsigned int* c = p.cnt + ((long long)b * p.Hkv + hk);
+    const unsigned prev = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == (unsigned)(nsplit - 1);
+    if (last) {
+      __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm for the next call
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    s_last = last;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  const int D = p.D;
+  for (int g = 0; g < G; ++g) {
+    const long long bh = (long long)b * p.H + hk * G + g;
+    const float* ml = p.ws_ml + bh * nsplit * 2;
+    const float* o = p.ws_o + bh * nsplit * D;
+    float m = -INFINITY;
+    for (int s = tid; s < nsplit; s += 256) m = fmaxf(m, ml[2 * s]);
+    const float M = block_max(m, red);
+    float l = 0.f;
+    for (int s = tid; s < nsplit; s += 256) {
+      const float ms = ml[2 * s];
+      const float w = ms == -INFINITY ? 0.f : __expf(ms - M);
+      wsp[s] = w;
+      l += w * ml[2 * s + 1];
+    }
+    const float Lsum = block_sum(l, red + 4);  // block_sum's barriers also publish wsp
+    const float inv = Lsum > 0.f ? 1.f / Lsum : 0.f;
+    if (tid < D) {  // D <= 256: one output dim per lane
+      float acc = 0.f;
+#pragma unroll 8
+      for (int s = 0; s < nsplit; ++s) {  // an empty split's partial was never written: may hold NaN
+        const float ov = o[(long long)s * D + tid];
+        acc = wsp[s] > 0.f ? fmaf(wsp[s], ov, acc) : acc;
+      }
+      p.out[b * p.o_bs + (hk * G + g) * (long long)D + tid] = f2bf(acc * inv);
+    }
+    __syncthreads();  // wsp / red reused by the next head
+  }
+}
+
 // LPT lanes cooperate on one token row (8 dims per lane); TPW = 64/LPT tokens per
 // wave step; G query heads share each K/V row (GQA group).
 template <int LPT, int G, bool PAGED, bool ONLINE>
@@ -245,9 +311,10 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
   const int c1 = min(c0 + p.chunk, L);
   if (c0 >= L) {
     if (nsplit > 1 && tid < G) {
-      p.ws_ml[((bh0 + tid) * nsplit + split) * 2] = -INFINITY;
-      p.ws_ml[((bh0 + tid) * nsplit + split) * 2 + 1] = 0.f;
+      st_pub(&p.ws_ml[((bh0 + tid) * nsplit + split) * 2], -INFINITY);
+      st_pub(&p.ws_ml[((bh0 + tid) * nsplit + split) * 2 + 1], 0.f);
     }
+    if (nsplit > 1 && p.cnt) fanin_combine<G>(p, b, hk, nsplit);
     return;
   }
   DSTAMP(1);
@@ -470,10 +537,10 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
     if (nsplit == 1) {
       p.out[b * p.o_bs + (long long)(hk * G + g) * D + d] = f2bf(Ls > 0.f ? O / Ls : 0.f);
     } else {
-      p.ws_o[((bh0 + g) * nsplit + split) * D + d] = O;
+      st_pub(&p.ws_o[((bh0 + g) * nsplit + split) * D + d], O);
       if (d == 0) {
-        p.ws_ml[((bh0 + g) * nsplit + split) * 2] = M;
-        p.ws_ml[((bh0 + g) * nsplit + split) * 2 + 1] = Ls;
+        st_pub(&p.ws_ml[((bh0 + g) * nsplit + split) * 2], M);
+        st_pub(&p.ws_ml[((bh0 + g) * nsplit + split) * 2 + 1], Ls);
       }
     }
   }
@@ -606,15 +673,16 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
       if (nsplit == 1) {
         p.out[b * p.o_bs + (long long)(hk * G + g) * D + d] = f2bf(lg[g] > 0.f ? s / lg[g] : 0.f);
       } else {
-        p.ws_o[((bh0 + g) * nsplit + split) * D + d] = s;
+        st_pub(&p.ws_o[((bh0 + g) * nsplit + split) * D + d], s);
       }
     }
     if (nsplit > 1 && tid == 0) {
-      p.ws_ml[((bh0 + g) * nsplit + split) * 2] = mg[g];
-      p.ws_ml[((bh0 + g) * nsplit + split) * 2 + 1] = lg[g];
+      st_pub(&p.ws_ml[((bh0 + g) * nsplit + split) * 2], mg[g]);
+      st_pub(&p.ws_ml[((bh0 + g) * nsplit + split) * 2 + 1], lg[g]);
     }
   }
   }
+  if (nsplit > 1 && p.cnt) fanin_combine<G>(p, b, hk, nsplit);
 }
 
 // One workgroup per (sequence, head): split maxima and weights in one
@@ -723,7 +791,7 @@ KCA_API int kca_decode_attn(const void* q, long long q_bs, const void* kc, const
                             int tbl_stride, int ps_shift, hipStream_t stream) {
   DecodeParams p{(const bf16_t*)q, q_bs, (const bf16_t*)kc, (const bf16_t*)vc, cs_slot, cs_head,
                  cs_pos, slots, kv_lens, (bf16_t*)out, o_bs, nullptr, nullptr, alibi, tbl, tbl_stride, ps_shift,
-                 H, Hkv, D, chunk, scale, 0, 0, 0, nullptr, nullptr, g_decode_stamps};
+                 H, Hkv, D, chunk, scale, 0, 0, 0, nullptr, nullptr, g_decode_stamps, nullptr};
   return decode_attn_launch(p, ws, ws_floats, B, max_kv, chunk, stream);
 }
 
@@ -741,8 +809,35 @@ KCA_API int kca_decode_prep_attn(const void* qkv, long long ld, const void* kc, 
   if (rot > D || (rot & 1) || (rot > 0 && (!cos_t || !sin_t))) return 8;
   DecodeParams p{(const bf16_t*)qkv, ld, (const bf16_t*)kc, (const bf16_t*)vc, cs_slot, cs_head,
                  cs_pos, slots, kv_lens, (bf16_t*)out, o_bs, nullptr, nullptr, alibi, tbl, tbl_stride, ps_shift,
-                 H, Hkv, D, chunk, scale, 1, rot, interleaved, cos_t, sin_t, g_decode_stamps};
+                 H, Hkv, D, chunk, scale, 1, rot, interleaved, cos_t, sin_t, g_decode_stamps, nullptr};
   return decode_attn_launch(p, ws, ws_floats, B, max_kv, chunk, stream);
+}
+
+// Fan-in counters: a zero-initialised device array per GPU (module globals load zeroed, and every
+// fan-in re-arms its counter), indexed by (sequence, kv-head). One decode attention launch at a
+// time per device uses them (the engines issue decode attention on one stream); KCA_DECODE_FANIN=0
+// selects the separate combine kernel.
+constexpr int kFaninMax = 65536;
+__device__ unsigned int g_fanin_cnt[kFaninMax];
+static unsigned int* fanin_counters(int n, hipStream_t stream) {
+  static int enabled = -1;
+  if (enabled < 0) {
+    const char* e = getenv("KCA_DECODE_FANIN");
+    enabled = !(e && e[0] == '0');
+  }
+  if (!enabled || n > kFaninMax) return nullptr;
+  static unsigned int* addr[64] = {nullptr};
+  int dev = 0, sdev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  // the symbol address is the current device's: a launch on another device's stream (layer-split
+  // across GPUs) keeps the separate combine kernel
+  if (hipStreamGetDevice(stream, &sdev) != hipSuccess || sdev != dev) return nullptr;
+  if (!addr[dev]) {
+    void* a = nullptr;
+    if (hipGetSymbolAddress(&a, HIP_SYMBOL(g_fanin_cnt)) != hipSuccess) return nullptr;
+    addr[dev] = (unsigned int*)a;
+  }
+  return addr[dev];
 }
 
 static int decode_attn_launch(DecodeParams p, float* ws, long long ws_floats, int B, int max_kv, int chunk,
@@ -764,13 +859,14 @@ static int decode_attn_launch(DecodeParams p, float* ws, long long ws_floats, in
     p.ws_o = ws;
     p.ws_ml = ws + (long long)B * H * nsplit * D;
   }
+  if (nsplit > 1) p.cnt = fanin_counters(B * Hkv, stream);
   const int nd = D / 8;
   int rc;
   if (nd <= 8) rc = launch_decode_g<8>(p, G, B, nsplit, stream);
   else if (nd <= 16) rc = launch_decode_g<16>(p, G, B, nsplit, stream);
   else rc = launch_decode_g<32>(p, G, B, nsplit, stream);
   if (rc) return rc;
-  if (nsplit > 1)
+  if (nsplit > 1 && !p.cnt)
     hipLaunchKernelGGL(decode_combine_kernel, dim3(B * H), dim3(256), 0, stream, p.ws_o, p.ws_ml,
                        p.out, p.o_bs, H, D, nsplit);
   return 0;

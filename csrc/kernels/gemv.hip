@@ -84,6 +84,16 @@ __device__ __forceinline__ void ln_prologue(const bf16_t* __restrict__ x, long l
   }
 }
 
+// Weight stream loads: every weight byte of a decode GEMV is read once, by one workgroup, so
+// they are non-temporal (global_load_dwordx4 ... nt): they do not displace the L2 / MALL lines the
+// latency-bound attention chain and the activations re-read (MI355X_MICROARCH.md, nt-weights:
+// decode layers 5-10 % faster with nt weight streams).
+typedef unsigned int u32x4_nt __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld_w16(const bf16_t* p) {
+  const u32x4_nt v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_nt*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 template <int M, int R, bool LN>
 __global__ __launch_bounds__(256) void skinny_gemm_kernel(
     const bf16_t* __restrict__ x, long long ldx, const bf16_t* __restrict__ w,
@@ -128,7 +138,7 @@ __global__ __launch_bounds__(256) void skinny_gemm_kernel(
 #pragma unroll
         for (int r = 0; r < R; ++r) {
           wv[u][r] = make_uint4(0u, 0u, 0u, 0u);
-          if (k < kn && rv[r]) wv[u][r] = *reinterpret_cast<const uint4*>(wr[r] + k0 + k);
+          if (k < kn && rv[r]) wv[u][r] = ld_w16(wr[r] + k0 + k);
         }
       }
 #pragma unroll
@@ -214,7 +224,7 @@ __global__ __launch_bounds__(256) void gemv1_kernel(const bf16_t* __restrict__ x
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         wv[u][r] = make_uint4(0u, 0u, 0u, 0u);
-        if (k < K && rv[r]) wv[u][r] = *reinterpret_cast<const uint4*>(wr[r] + k);
+        if (k < K && rv[r]) wv[u][r] = ld_w16(wr[r] + k);
       }
     }
   };

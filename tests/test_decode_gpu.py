@@ -393,3 +393,39 @@ def test_decode_prep_attention_fused_equals_two_kernels(D, rot, inter, G, PS, CH
     assert torch.equal(k1, k2) and torch.equal(v1, v2)
     assert torch.equal(a, b)
     assert torch.equal(q2, qkv)  # the fused kernel leaves the QKV buffer untouched
+
+
+_FANIN_CASE = """
+import sys, torch
+from kubernetes_cloud_amd.ops import decode as dops
+torch.manual_seed(7)
+dev = torch.device("cuda", 0)
+B, Hkv, G, D, L = 3, 4, 4, 128, 2048
+kc = torch.randn(B, Hkv, L, D, device=dev).to(torch.bfloat16)
+vc = torch.randn_like(kc)
+q = torch.randn(B, (Hkv * G + 2 * Hkv) * D, device=dev).to(torch.bfloat16)
+slots = torch.tensor([2, 0, 1], device=dev, dtype=torch.int32)
+lens = torch.tensor([2048, 33, 1000], device=dev, dtype=torch.int32)
+outs = [dops.decode_attention(q, kc, vc, slots, lens, Hkv * G, L, chunk=c).cpu() for c in (32, 64, 256, 0)]
+torch.save(outs, sys.argv[1])
+"""
+
+
+def test_decode_split_fanin_matches_combine_kernel(tmp_path):
+    """The split-K fan-in (last split's workgroup combines, csrc/kernels/decode.hip
+    fanin_combine) is bit-identical to the separate combine kernel (KCA_DECODE_FANIN=0)
+    at 64 / 32 / 8 splits and the default split policy."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = {}
+    for f in ("1", "0"):
+        out = str(tmp_path / f"o{f}.pt")
+        env = dict(os.environ, KCA_DECODE_FANIN=f, PYTHONPATH=root)
+        r = subprocess.run([sys.executable, "-c", _FANIN_CASE, out], env=env, capture_output=True, text=True,
+                           timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res[f] = torch.load(out, weights_only=True)
+    for a, b in zip(res["1"], res["0"]):
+        assert torch.equal(a, b)
