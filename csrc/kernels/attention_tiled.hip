@@ -183,6 +183,36 @@ struct Stager<D, false> {
   }
 };
 
+// Epilogue through LDS (cdna_hip_programming.md T21): the wave's 32 x D accumulator tile (row =
+// lane & 31) goes into a wave-private [32][D] bf16 LDS image -- 16-B chunks rotated by the row,
+// so the per-lane 8-B writes and the row-contiguous 16-B reads are both conflict-free -- and every
+// store instruction then writes two whole rows with 16-B stores, instead of 8-B stores that each
+// touch 64 rows. `mul` is the lane's row scale. The LDS must be free (after the loop's barrier).
+template <int D>
+__device__ __forceinline__ void store_tile_lds(bf16_t* row0, long long st, const f32x16 (&acc)[D / 32], int lane,
+                                               float mul, char* lds) {
+  constexpr int NCH = D / 8, RB = D * 2;
+  const int l32 = lane & 31, hh = lane >> 5;
+#pragma unroll
+  for (int db = 0; db < D / 32; ++db) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      uint2 w;
+      w.x = pk_bf16(acc[db][4 * g] * mul, acc[db][4 * g + 1] * mul);
+      w.y = pk_bf16(acc[db][4 * g + 2] * mul, acc[db][4 * g + 3] * mul);
+      *reinterpret_cast<uint2*>(lds + l32 * RB + ((4 * db + g + l32) % NCH) * 16 + hh * 8) = w;
+    }
+  }
+  asm volatile("" ::: "memory");  // the wave's LDS accesses execute in order: reads see its writes
+#pragma unroll
+  for (int j = 0; j < NCH / 2; ++j) {
+    const int idx = j * 64 + lane, r = idx / NCH, c = idx % NCH;
+    const uint4 v = *reinterpret_cast<const uint4*>(lds + r * RB + ((c + r) % NCH) * 16);
+    *reinterpret_cast<uint4*>(row0 + (long long)r * st + c * 8) = v;
+  }
+  asm volatile("" ::: "memory");
+}
+
 template <int D, bool CAUSAL>
 __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel(FastFwdParams p) {
   constexpr int BM = 128, BN = 32;
@@ -398,17 +428,8 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel
   const float inv = ltot > 0.f ? 1.f / ltot : 0.f;
   if (hh == 0 && p.lse)
     p.lse[((long long)b * p.H + h) * p.Sq + qrow] = ltot > 0.f ? (m + log2f(ltot)) * kLn2 : INFINITY;
-  bf16_t* op = p.o + b * p.o_sb + h * p.o_sh + (long long)qrow * p.o_st;
-#pragma unroll
-  for (int db = 0; db < D / 32; ++db) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      uint2 w;
-      w.x = pk_bf16(oacc[db][4 * g] * inv, oacc[db][4 * g + 1] * inv);
-      w.y = pk_bf16(oacc[db][4 * g + 2] * inv, oacc[db][4 * g + 3] * inv);
-      *reinterpret_cast<uint2*>(op + db * 32 + 8 * g + 4 * hh) = w;
-    }
-  }
+  store_tile_lds<D>(p.o + b * p.o_sb + h * p.o_sh + (long long)q0 * p.o_st, p.o_st, oacc, lane, inv,
+                    smem + wave * 32 * D * 2);
   ASTAMP(5);
   ASTAMP_FLUSH(0);
 }
@@ -610,7 +631,8 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq_tiled_kernel(FastBwdParams
   const int nfree = CAUSAL ? ntiles - 4 : ntiles;
   for (int t = 0; t < nfree; ++t) tile_step(t, std::false_type{});
   for (int t = max(nfree, 0); t < ntiles; ++t) tile_step(t, std::true_type{});
-  store_acc_t<D>(p.dq + b * p.dq_sb + h * p.dq_sh + (long long)qrow * p.dq_st, dq, hh, p.scale);
+  store_tile_lds<D>(p.dq + b * p.dq_sb + h * p.dq_sh + (long long)q0 * p.dq_st, p.dq_st, dq, lane, p.scale,
+                    smem + wave * 32 * D * 2);
   ASTAMP(6);
   ASTAMP_FLUSH(16);
 }
@@ -800,8 +822,15 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_tiled_kernel(FastBwdPara
   for (int it = 0; it < total; ++it) tile_step(it, std::integral_constant<bool, CAUSAL>{});
 #undef KCA_DKDV_LOAD
 #undef KCA_DKDV_STORE
-  store_acc_t<D>(p.dk + b * p.dk_sb + hk * p.dk_sh + (long long)key * p.dk_st, dk, hh, p.scale);
-  store_acc_t<D>(p.dv + b * p.dv_sb + hk * p.dv_sh + (long long)key * p.dv_st, dv, hh, 1.f);
+  if constexpr (D == 96) {  // the LDS staging's registers push this one past 256 (2 -> 1 wave per SIMD)
+    store_acc_t<D>(p.dk + b * p.dk_sb + hk * p.dk_sh + (long long)key * p.dk_st, dk, hh, p.scale);
+    store_acc_t<D>(p.dv + b * p.dv_sb + hk * p.dv_sh + (long long)key * p.dv_st, dv, hh, 1.f);
+  } else {
+    store_tile_lds<D>(p.dk + b * p.dk_sb + hk * p.dk_sh + (long long)kw * p.dk_st, p.dk_st, dk, lane, p.scale,
+                      smem + wave * 32 * D * 2);
+    store_tile_lds<D>(p.dv + b * p.dv_sb + hk * p.dv_sh + (long long)kw * p.dv_st, p.dv_st, dv, lane, 1.f,
+                      smem + wave * 32 * D * 2);
+  }
   ASTAMP(6);
   ASTAMP_FLUSH(32);
 }
