@@ -196,13 +196,17 @@ __global__ __launch_bounds__(256) void skinny_gemm_kernel(
 // dots meet in LDS. (Was: every workgroup staged / normalised the full row
 // into LDS before its first weight load -- the LN form streamed 3.3 TB/s
 // against 5.2 TB/s for the plain one at GPT-J shapes.)
-template <int R, bool LN>
+// MR > 1 (decode batch 2..4, no LN prologue): the same K-split structure over MR activation rows
+// held in registers -- W still streamed once, MR FMAs per weight element
+template <int R, bool LN, int MR = 1>
 __global__ __launch_bounds__(256) void gemv1_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
                                                     const bf16_t* __restrict__ bias, bf16_t* __restrict__ y,
-                                                    int N, int K, int act, LnArgs ln) {
+                                                    int N, int K, int act, LnArgs ln, long long ldx = 0,
+                                                    long long ldy = 0, int mv = 1) {
+  static_assert(MR == 1 || !LN, "the LN prologue is single-row");
   constexpr int U = 4;
   __shared__ float red[16];
-  __shared__ float part[4][R];
+  __shared__ float part[4][R * MR];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int n0 = blockIdx.x * R;
   const int kl = wid * 512 + lane * 8;
@@ -213,9 +217,11 @@ __global__ __launch_bounds__(256) void gemv1_kernel(const bf16_t* __restrict__ x
     rv[r] = n0 + r < N;
     wr[r] = w + (long long)(rv[r] ? n0 + r : 0) * K;
   }
-  float acc[R];
+  float acc[MR][R];
 #pragma unroll
-  for (int r = 0; r < R; ++r) acc[r] = 0.f;
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[m][r] = 0.f;
   uint4 wv[U][R];
   auto load_w = [&](int i0) {
 #pragma unroll
@@ -237,8 +243,8 @@ __global__ __launch_bounds__(256) void gemv1_kernel(const bf16_t* __restrict__ x
         const uint32_t q[4] = {wv[u][r].x, wv[u][r].y, wv[u][r].z, wv[u][r].w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          acc[r] = fmaf(__uint_as_float(q[j] << 16), xv[u][2 * j], acc[r]);
-          acc[r] = fmaf(__uint_as_float(q[j] & 0xffff0000u), xv[u][2 * j + 1], acc[r]);
+          acc[0][r] = fmaf(__uint_as_float(q[j] << 16), xv[u][2 * j], acc[0][r]);
+          acc[0][r] = fmaf(__uint_as_float(q[j] & 0xffff0000u), xv[u][2 * j + 1], acc[0][r]);
         }
       }
     }
@@ -303,42 +309,53 @@ __global__ __launch_bounds__(256) void gemv1_kernel(const bf16_t* __restrict__ x
     const int NI = (K + 2047) / 2048;
     for (int i0 = 0; i0 < NI; i0 += U) {
       if (i0) load_w(i0);
-      uint4 xr[U];  // raw bf16, widened at use (keeps the kernel at 4 waves/SIMD)
+      uint4 xr[MR][U];  // raw bf16, widened at use (keeps the MR = 1 kernel at 4 waves/SIMD)
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int k = (i0 + u) * 2048 + kl;
-        xr[u] = make_uint4(0u, 0u, 0u, 0u);
-        if (k < K) xr[u] = *reinterpret_cast<const uint4*>(x + k);
-      }
+      for (int m = 0; m < MR; ++m)
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int k = (i0 + u) * 2048 + kl;
+          xr[m][u] = make_uint4(0u, 0u, 0u, 0u);
+          if (k < K && m < mv) xr[m][u] = *reinterpret_cast<const uint4*>(x + m * ldx + k);
+        }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if ((i0 + u) * 2048 + kl >= K) continue;
-        const uint32_t xq[4] = {xr[u].x, xr[u].y, xr[u].z, xr[u].w};
 #pragma unroll
         for (int r = 0; r < R; ++r) {
           const uint32_t q[4] = {wv[u][r].x, wv[u][r].y, wv[u][r].z, wv[u][r].w};
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            acc[r] = fmaf(__uint_as_float(q[j] << 16), __uint_as_float(xq[j] << 16), acc[r]);
-            acc[r] = fmaf(__uint_as_float(q[j] & 0xffff0000u), __uint_as_float(xq[j] & 0xffff0000u), acc[r]);
+          for (int m = 0; m < MR; ++m) {
+            const uint32_t xq[4] = {xr[m][u].x, xr[m][u].y, xr[m][u].z, xr[m][u].w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              acc[m][r] = fmaf(__uint_as_float(q[j] << 16), __uint_as_float(xq[j] << 16), acc[m][r]);
+              acc[m][r] = fmaf(__uint_as_float(q[j] & 0xffff0000u), __uint_as_float(xq[j] & 0xffff0000u), acc[m][r]);
+            }
           }
         }
       }
     }
   }
 #pragma unroll
-  for (int r = 0; r < R; ++r) acc[r] = wave_sum(acc[r]);
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[m][r] = wave_sum(acc[m][r]);
   if (lane == 0) {
 #pragma unroll
-    for (int r = 0; r < R; ++r) part[wid][r] = acc[r];
+    for (int m = 0; m < MR; ++m)
+#pragma unroll
+      for (int r = 0; r < R; ++r) part[wid][m * R + r] = acc[m][r];
   }
   __syncthreads();
-  if (tid < R && n0 + tid < N) {
-    float v = part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid];
-    v += bias ? bf2f(bias[n0 + tid]) : 0.f;
+  const int m = tid / R, r = tid % R;
+  if (tid < R * MR && m < mv && n0 + r < N) {
+    const int i = m * R + r;
+    float v = part[0][i] + part[1][i] + part[2][i] + part[3][i];
+    v += bias ? bf2f(bias[n0 + r]) : 0.f;
     if (act == 1) v = gelu_tanh(v);
     else if (act == 2) v = 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
-    y[n0 + tid] = f2bf(v);
+    y[m * ldy + n0 + r] = f2bf(v);
   }
 }
 
@@ -446,7 +463,17 @@ static void launch_skinny(const bf16_t* x, long long ldx, const bf16_t* w, const
   // split-K form costs more than it saves (B=1 8.75 -> 9.47 ms/token), so wide LN rows stay row-per-wave
   if constexpr (M == 1) if (g_skinny_sk && !(LN && K > 8192)) {
     const dim3 grid((N + R - 1) / R);
-    hipLaunchKernelGGL((gemv1_kernel<R, LN>), grid, dim3(256), 0, s, x, w, bias, y, N, K, act, ln);
+    hipLaunchKernelGGL((gemv1_kernel<R, LN>), grid, dim3(256), 0, s, x, w, bias, y, N, K, act, ln, 0LL, 0LL, 1);
+    return;
+  }
+  // 2 rows without an LN prologue (decode batch 2): the K-split register-resident form, K <= 8192
+  // (the lanes' x slices stay in registers). GPT-J B=2 decode 3.41-3.50 -> 3.13-3.16 ms/step vs
+  // hipBLASLt; at 4 rows it lost to hipBLASLt (4.1-4.2 vs 3.5-3.6 ms, also with several weight-row
+  // groups per workgroup), so 3-4 rows keep the kernel below (profiles/decode_skinny_ab_r2.txt)
+  if constexpr (M == 2) if (g_skinny_sk && !LN && K <= 8192) {
+    const dim3 grid((N + 3) / 4);
+    hipLaunchKernelGGL((gemv1_kernel<4, false, 2>), grid, dim3(256), 0, s, x, w, bias, y, N, K, act, ln, ldx, ldy,
+                       mv);
     return;
   }
   const int rows_per_block = 4 * R;

@@ -37,6 +37,12 @@ def _set_mode():
             _lib.call("kca_skinny_set_splitk", 0)
 
 
+# rows up to which every weight streams through the skinny kernel (A/B knob): M = 1 and M = 2 run the
+# register-resident K-split GEMV (B=2 GPT-J decode 3.13-3.16 vs 3.41-3.50 ms/step through hipBLASLt);
+# from 3 rows hipBLASLt is faster on the big weights (profiles/decode_skinny_ab_r2.txt)
+_SKINNY_MAX_M = int(os.environ.get("KCA_SKINNY_MAX_M", "2"))
+
+
 def skinny_linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None, act: int = 0,
                   out: torch.Tensor | None = None) -> torch.Tensor:
     """x [M, K] (row stride multiple of 8), weight [N, K] contiguous."""
@@ -47,7 +53,8 @@ def skinny_linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | No
     # 12.4 vs 18.4 us); on the QKV / MLP weights hipBLASLt is faster from M = 2 (GPT-J decode B=2 4.69 ms
     # with the skinny kernel vs 4.54 ms at B=4 through hipBLASLt); MFMA GEMMs beyond
     small = N * K <= (16 << 20)
-    if (_lib.use_native(x, weight) and (M == 1 or (M <= 4 and small)) and K % 8 == 0 and x.stride(1) == 1
+    if (_lib.use_native(x, weight) and (M <= _SKINNY_MAX_M or (M <= 4 and small)) and K % 8 == 0
+            and x.stride(1) == 1
             and x.stride(0) % 8 == 0
             and weight.is_contiguous() and x.data_ptr() % 16 == 0 and weight.data_ptr() % 16 == 0
             and (bias is None or bias.dtype == torch.bfloat16)):

@@ -176,6 +176,27 @@ def test_skinny_gemm(M, N, K):
         assert (y.float() - fn(ref)).abs().max() < 0.05, act
 
 
+@pytest.mark.parametrize("M", [2, 3, 4])
+@pytest.mark.parametrize("N,K", [(12288, 4096), (4098, 4096), (4096, 16384), (1026, 1000)])
+def test_skinny_gemm_multirow_kernel(M, N, K):
+    """kca_skinny_gemm at 2-4 rows (the K-split register-resident kernel for K <= 8192, the
+    row-per-wave kernel beyond), called directly: skinny_linear sends these shapes to hipBLASLt
+    unless KCA_SKINNY_MAX_M says otherwise. Strided x / y rows, ragged N, bias + GELU."""
+    torch.manual_seed(M * 7 + N + K)
+    xs = torch.randn(M, K + 8, device=dev).to(torch.bfloat16)
+    x = xs[:, :K]
+    w = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+    b = torch.randn(N, device=dev).to(torch.bfloat16)
+    ys = torch.full((M, N + 4), float("nan"), device=dev, dtype=torch.bfloat16)
+    y = ys[:, :N]
+    _lib.call("kca_skinny_gemm", x.data_ptr(), x.stride(0), w.data_ptr(), b.data_ptr(), y.data_ptr(), y.stride(0),
+              M, N, K, 1, _lib.stream())
+    torch.cuda.synchronize()
+    ref = torch.nn.functional.gelu(x.float() @ w.float().t() + b.float(), approximate="tanh")
+    assert (y.float() - ref).abs().max() < 0.05
+    assert torch.isnan(ys[:, N:].float()).all()  # nothing written past the row
+
+
 @pytest.mark.parametrize("M", [1, 2, 4])
 def test_skinny_gemm_row_per_wave_kernel(M):
     """The row-per-wave skinny kernel (A/B alternative to the split-K default)."""
