@@ -67,7 +67,7 @@ def run(B, ctx, wgs, H=16, D=256, ps=16, iters=50, chunk=0, mode="fused", paged=
     cos, sin = ang.cos().contiguous(), ang.sin().contiguous()
     out = torch.empty(B, H * D, device=dev, dtype=torch.bfloat16)
     chunk = dops.decode_chunk(B, H, ctx)
-    ws = torch.empty(max(1, dops.decode_ws_floats(B, H, H, D, ctx, chunk)), device=dev)
+    ws = torch.zeros(max(1, dops.decode_ws_floats(B, H, H, D, ctx, chunk)), device=dev)
 
     if not paged:  # contiguous slots [B, H, ctx_max, D]
         kc = torch.randn(B, H, pages * ps, D, device=dev).to(torch.bfloat16)

@@ -749,9 +749,23 @@ KCA_API int kca_decode_chunk(int B, int Hkv, int max_kv) {
   return (int)c;
 }
 
+// Fan-in counters live at the start of the workspace: B*H words (indexed by (sequence, kv-head)),
+// padded to 16 B, that must be zero when the workspace is first used (the callers allocate it
+// zeroed, ops/decode.py) and that every fan-in re-arms -- so concurrent launches on separate
+// workspaces never share a counter. KCA_DECODE_FANIN=0 selects the separate combine kernel.
+static bool fanin_enabled() {
+  static int enabled = -1;
+  if (enabled < 0) {
+    const char* e = getenv("KCA_DECODE_FANIN");
+    enabled = !(e && e[0] == '0');
+  }
+  return enabled;
+}
+static long long fanin_words(int B, int H) { return ((long long)B * H + 3) / 4 * 4; }
+
 KCA_API long long kca_decode_ws_floats(int B, int H, int D, int max_kv, int chunk) {
   const long long ns = (max_kv + chunk - 1) / chunk;
-  return ns > 1 ? (long long)B * H * ns * (D + 2) : 0;
+  return ns > 1 ? fanin_words(B, H) + (long long)B * H * ns * (D + 2) : 0;
 }
 
 template <int LPT, int G>
@@ -813,33 +827,6 @@ KCA_API int kca_decode_prep_attn(const void* qkv, long long ld, const void* kc, 
   return decode_attn_launch(p, ws, ws_floats, B, max_kv, chunk, stream);
 }
 
-// Fan-in counters: a zero-initialised device array per GPU (module globals load zeroed, and every
-// fan-in re-arms its counter), indexed by (sequence, kv-head). One decode attention launch at a
-// time per device uses them (the engines issue decode attention on one stream); KCA_DECODE_FANIN=0
-// selects the separate combine kernel.
-constexpr int kFaninMax = 65536;
-__device__ unsigned int g_fanin_cnt[kFaninMax];
-static unsigned int* fanin_counters(int n, hipStream_t stream) {
-  static int enabled = -1;
-  if (enabled < 0) {
-    const char* e = getenv("KCA_DECODE_FANIN");
-    enabled = !(e && e[0] == '0');
-  }
-  if (!enabled || n > kFaninMax) return nullptr;
-  static unsigned int* addr[64] = {nullptr};
-  int dev = 0, sdev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  // the symbol address is the current device's: a launch on another device's stream (layer-split
-  // across GPUs) keeps the separate combine kernel
-  if (hipStreamGetDevice(stream, &sdev) != hipSuccess || sdev != dev) return nullptr;
-  if (!addr[dev]) {
-    void* a = nullptr;
-    if (hipGetSymbolAddress(&a, HIP_SYMBOL(g_fanin_cnt)) != hipSuccess) return nullptr;
-    addr[dev] = (unsigned int*)a;
-  }
-  return addr[dev];
-}
-
 static int decode_attn_launch(DecodeParams p, float* ws, long long ws_floats, int B, int max_kv, int chunk,
                               hipStream_t stream) {
   const int H = p.H, Hkv = p.Hkv, D = p.D;
@@ -854,12 +841,13 @@ static int decode_attn_launch(DecodeParams p, float* ws, long long ws_floats, in
   if (nsplit > 1024) return 7;  // combine keeps the split weights in LDS
   p.chunk = chunk;
   if (nsplit > 1) {
-    const long long need = (long long)B * H * nsplit * (D + 2);
+    const long long cw = fanin_words(B, H);
+    const long long need = cw + (long long)B * H * nsplit * (D + 2);
     if (!ws || ws_floats < need) return 4;
-    p.ws_o = ws;
-    p.ws_ml = ws + (long long)B * H * nsplit * D;
+    if (fanin_enabled()) p.cnt = reinterpret_cast<unsigned int*>(ws);
+    p.ws_o = ws + cw;
+    p.ws_ml = p.ws_o + (long long)B * H * nsplit * D;
   }
-  if (nsplit > 1) p.cnt = fanin_counters(B * Hkv, stream);
   const int nd = D / 8;
   int rc;
   if (nd <= 8) rc = launch_decode_g<8>(p, G, B, nsplit, stream);

@@ -514,7 +514,7 @@ class ModelRunner:
         ws_n = dops.decode_ws_floats(Bb, self.H, self.Hkv, self.D, Kb)
         st = {
             "pk": pk,
-            "ws": torch.empty(max(ws_n, 1), device=self.device, dtype=torch.float32),
+            "ws": torch.zeros(max(ws_n, 1), device=self.device, dtype=torch.float32),  # zeroed: fan-in counters
             "obuf": torch.empty(Bb, self.H * self.D, device=self.device, dtype=self.dtype),
             "sws": torch.empty(Bb * self.V, device=self.device, dtype=torch.float32),
             "ids": torch.empty(Bb, device=self.device, dtype=torch.int64),

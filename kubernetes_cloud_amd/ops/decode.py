@@ -92,7 +92,9 @@ def decode_ws_floats(B: int, H: int, Hkv: int, D: int, max_kv: int, chunk: int =
     if chunk <= 0:
         chunk = decode_chunk(B, Hkv, max_kv)
     ns = -(-max_kv // chunk)
-    return B * H * ns * (D + 2) if ns > 1 else 0
+    # the first B*H words (padded to 16 B) are the split-K fan-in counters (csrc/kernels/decode.hip):
+    # a workspace must be ZERO-initialised before its first use (the kernel re-arms them after)
+    return -(-(B * H) // 4) * 4 + B * H * ns * (D + 2) if ns > 1 else 0
 
 
 _DECODE_WGS = int(os.environ.get("KCA_DECODE_WGS", "256"))  # split-K workgroup target (A/B knob)
@@ -142,7 +144,7 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
             chunk = decode_chunk(B, Hkv, max_kv)
         need = decode_ws_floats(B, H, Hkv, D, max_kv, chunk)
         if need and (ws is None or ws.numel() < need):
-            ws = torch.empty(need, device=q.device, dtype=torch.float32)
+            ws = torch.zeros(need, device=q.device, dtype=torch.float32)
         _lib.call("kca_decode_attn", q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
                   k_cache.stride(0), k_cache.stride(1), k_cache.stride(2), slots.data_ptr(),
                   kv_lens.data_ptr(), out.data_ptr(), out.stride(0), _lib.ptr(ws),
@@ -175,7 +177,7 @@ def decode_prep_attention(qkv: torch.Tensor, n_heads: int, kv_heads: int, head_d
         chunk = decode_chunk(B, Hkv, max_kv)
         need = decode_ws_floats(B, H, Hkv, D, max_kv, chunk)
         if need and (ws is None or ws.numel() < need):
-            ws = torch.empty(need, device=qkv.device, dtype=torch.float32)
+            ws = torch.zeros(need, device=qkv.device, dtype=torch.float32)
         _lib.call("kca_decode_prep_attn", qkv.data_ptr(), qkv.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
                   k_cache.stride(0), k_cache.stride(1), k_cache.stride(2), slots.data_ptr(), kv_lens.data_ptr(),
                   out.data_ptr(), out.stride(0), _lib.ptr(ws), ws.numel() if ws is not None else 0, B, H, Hkv, D,
