@@ -14,7 +14,7 @@ Tuned solver parameters ship in ``tuning/miopen/``: MIOpen's user perf-db
 (``*.ufdb.txt``) for the SD-1.5 UNet at the bench shapes (txt2img batch 8 + CFG,
 DreamBooth 8 + 8 fwd/bwd/wrw) and the VAE decoder, produced on an MI355X by
 ``MIOPEN_FIND_ENFORCE=3`` runs of ``bench/sd_bench.py --mode train`` and
-``tools/debug/sd_breakdown.py`` (the recipe is ``tools/miopen_tune.sh``).
+``tools/sd_breakdown.py`` (the recipe is ``tools/miopen_tune.sh``).
 Measured with vs without: UNet CFG step 34.7 -> 30.5 ms, VAE decode
 52.3 -> 39.0 ms, DreamBooth 81.5 -> 92.5 samples/s. Other shapes fall back
 to MIOpen's normal find, and their results are appended to the same db.
