@@ -331,3 +331,39 @@ KCA_API int kca_geglu_bwd(const void* dy, const void* x, void* dx, long long row
                      (const bf16_t*)x, (bf16_t*)dx, inner / 8, n8);
   return 0;
 }
+
+// ---------------------------------------------------------------- residual + conv bias (NHWC)
+// out = a + b + bias[c] over channels-last rows of C channels (c = innermost index): the SD ResNet
+// block's `shortcut(x) + conv2(h)` with conv2's (and the 1x1 shortcut conv's) bias folded in, so
+// the convolutions run without their separate broadcast bias-add pass. b may be null.
+__global__ void add_bias_nhwc_kernel(const bf16_t* __restrict__ a, const bf16_t* __restrict__ b,
+                                     const float* __restrict__ bias, bf16_t* __restrict__ out, int c8,
+                                     long long n8) {
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < n8;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(t % c8) * 8;
+    float x[8], y[8];
+    load8(a + t * 8, x);
+    if (b) {
+      load8(b + t * 8, y);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] += y[j];
+    }
+    const float4 b0 = *reinterpret_cast<const float4*>(bias + c);
+    const float4 b1 = *reinterpret_cast<const float4*>(bias + c + 4);
+    x[0] += b0.x; x[1] += b0.y; x[2] += b0.z; x[3] += b0.w;
+    x[4] += b1.x; x[5] += b1.y; x[6] += b1.z; x[7] += b1.w;
+    store8(out + t * 8, x);
+  }
+}
+
+KCA_API int kca_add_bias_nhwc(const void* a, const void* b, const float* bias, void* out, long long n, int C,
+                              hipStream_t stream) {
+  if (C % 8 || n % C || !a || !bias || !out) return 1;
+  if (((uintptr_t)a | (uintptr_t)b | (uintptr_t)out | (uintptr_t)bias) & 15) return 2;
+  const long long n8 = n / 8;
+  if (n8 == 0) return 0;
+  hipLaunchKernelGGL(add_bias_nhwc_kernel, dim3(kca_grid(n8, 256, 8192)), dim3(256), 0, stream, (const bf16_t*)a,
+                     (const bf16_t*)b, bias, (bf16_t*)out, C / 8, n8);
+  return 0;
+}

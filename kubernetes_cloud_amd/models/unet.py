@@ -122,6 +122,10 @@ class TimestepEmbedding(nn.Module):
         return self.linear_2(F.silu(self.linear_1(x)))
 
 
+# KCA_SD_FOLD_BIAS=0 keeps the biased convolutions + separate residual add at inference (A/B knob)
+_FOLD_BIAS = os.environ.get("KCA_SD_FOLD_BIAS", "1") not in ("0", "false")
+
+
 class ResnetBlock2D(nn.Module):
     def __init__(self, cin, cout, temb_ch, groups=32, eps=1e-5):
         super().__init__()
@@ -134,6 +138,9 @@ class ResnetBlock2D(nn.Module):
         self.conv_shortcut = nn.Conv2d(cin, cout, 1) if cin != cout else None
 
     def forward(self, x, temb=None):
+        if _FOLD_BIAS and not torch.is_grad_enabled() and x.is_cuda and x.dtype == torch.bfloat16 \
+                and x.is_contiguous(memory_format=torch.channels_last) and self.conv1.bias is not None:
+            return self._forward_folded(x, temb)
         h = self.conv1(self.norm1(x))
         t = None
         if self.time_emb_proj is not None and temb is not None:
@@ -141,6 +148,25 @@ class ResnetBlock2D(nn.Module):
         h = self.conv2(self.dropout(self.norm2(h, add=t)))
         sc = self.conv_shortcut(x) if self.conv_shortcut is not None else x
         return sc + h
+
+    def _forward_folded(self, x, temb):
+        """Inference: the convolutions run without bias (MIOpen adds a conv bias in a separate
+        broadcast pass over the whole output): conv1's bias joins the time embedding that norm2
+        adds inside its statistics, and conv2's (+ the 1x1 shortcut's) bias joins the residual add
+        -- one full read+write pass fewer per convolution (profiles/sd_unet_add_attribution_r2.txt)."""
+        h = F.conv2d(self.norm1(x), self.conv1.weight, None, padding=1)
+        add = self.conv1.bias.float()[None].expand(x.shape[0], -1)
+        if self.time_emb_proj is not None and temb is not None:
+            add = add + self.time_emb_proj(F.silu(temb)).float()
+        h = F.conv2d(self.norm2(h, add=add), self.conv2.weight, None, padding=1)
+        bias = self.conv2.bias.float()
+        if self.conv_shortcut is not None:
+            sc = F.conv2d(x, self.conv_shortcut.weight, None)
+            if self.conv_shortcut.bias is not None:
+                bias = bias + self.conv_shortcut.bias.float()
+        else:
+            sc = x
+        return ops.add_bias_nhwc(sc, h, bias)
 
 
 # Head padding for the self-attention (see Attention.forward); KCA_SD_PAD_HEADS=0

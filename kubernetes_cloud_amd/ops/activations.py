@@ -69,3 +69,21 @@ def geglu(x: torch.Tensor) -> torch.Tensor:
         return _GegluFn.apply(x)
     a, g = x.chunk(2, dim=-1)
     return a * F.gelu(g.float()).to(a.dtype)
+
+
+def add_bias_nhwc(a: torch.Tensor, b: torch.Tensor | None, bias: torch.Tensor) -> torch.Tensor:
+    """``a + b + bias[None, :, None, None]`` for channels-last [N, C, H, W] bf16 tensors in one
+    pass (``kca_add_bias_nhwc``): the SD ResNet block's residual add with the convolution biases
+    folded in (models/unet.py). Inference helper: no autograd."""
+    ok = (_lib.use_native(a) and a.dtype == torch.bfloat16 and a.dim() == 4 and a.shape[1] % 8 == 0
+          and a.is_contiguous(memory_format=torch.channels_last)
+          and (b is None or (b.shape == a.shape and b.dtype == a.dtype
+                             and b.is_contiguous(memory_format=torch.channels_last))))
+    if not ok:
+        y = a.float() + (b.float() if b is not None else 0.0) + bias.float()[None, :, None, None]
+        return y.to(a.dtype)
+    out = torch.empty_like(a)
+    bf = bias.float().contiguous()
+    _lib.call("kca_add_bias_nhwc", a.data_ptr(), _lib.ptr(b), bf.data_ptr(), out.data_ptr(), a.numel(),
+              a.shape[1], _lib.stream())
+    return out

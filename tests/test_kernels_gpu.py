@@ -724,3 +724,43 @@ def test_sd_fused_noise_prep_and_mse_split(v_pred):
     l_ref.backward()
     assert abs(float(loss) - float(l_ref)) < 1e-3 * float(l_ref)
     assert torch.allclose(pred.grad.float(), p_ref.grad, rtol=2e-2, atol=1e-7)
+
+
+def test_add_bias_nhwc_kernel():
+    """kca_add_bias_nhwc (residual + folded conv biases) vs fp32, with and without the second
+    operand, at an SD UNet shape."""
+    torch.manual_seed(3)
+    a = torch.randn(4, 320, 16, 16, device=DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    b = torch.randn_like(a)
+    bias = torch.randn(320, device=DEV)
+    for bb in (b, None):
+        y = ops.add_bias_nhwc(a, bb, bias)
+        ref = a.float() + (bb.float() if bb is not None else 0) + bias[None, :, None, None]
+        assert y.is_contiguous(memory_format=torch.channels_last)
+        assert (y.float() - ref).abs().max() <= 0.02 * ref.abs().max()
+
+
+@pytest.mark.parametrize("cin,cout", [(320, 320), (320, 640)])
+def test_unet_resnet_block_folded_biases(cin, cout):
+    """Inference ResnetBlock2D with the conv biases folded into norm2's add and the residual add
+    (models/unet.py _forward_folded) == the biased-convolution path within bf16 rounding."""
+    from kubernetes_cloud_amd.models import unet as U
+    torch.manual_seed(cin + cout)
+    blk = U.ResnetBlock2D(cin, cout, 1280).to(DEV).to(torch.bfloat16).eval()
+    with torch.no_grad():
+        for p in blk.parameters():
+            p.normal_(0, 0.05)
+    for m in blk.modules():
+        if isinstance(m, torch.nn.Conv2d):
+            m.to(memory_format=torch.channels_last)
+    x = torch.randn(2, cin, 16, 16, device=DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    temb = torch.randn(2, 1280, device=DEV).to(torch.bfloat16)
+    with torch.no_grad():
+        folded = blk(x, temb)
+        U._FOLD_BIAS = False
+        try:
+            plain = blk(x, temb)
+        finally:
+            U._FOLD_BIAS = True
+    err = (folded.float() - plain.float()).abs().max()
+    assert err <= 0.02 * plain.float().abs().max(), err
