@@ -25,6 +25,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
+from ..ops.linear import SplitKLinear, linear_splitk_wgrad
 
 
 @dataclasses.dataclass
@@ -122,6 +123,10 @@ class TimestepEmbedding(nn.Module):
         return self.linear_2(F.silu(self.linear_1(x)))
 
 
+# token-level linears train with split-K weight gradients (ops/linear.py); KCA_SD_SPLITK_WGRAD=0 -> nn.Linear
+_Linear = SplitKLinear if os.environ.get("KCA_SD_SPLITK_WGRAD", "1") not in ("0", "false") else nn.Linear
+
+
 # KCA_SD_FOLD_BIAS=0 keeps the biased convolutions + separate residual add at inference (A/B knob)
 _FOLD_BIAS = os.environ.get("KCA_SD_FOLD_BIAS", "1") not in ("0", "false")
 
@@ -196,10 +201,10 @@ class Attention(nn.Module):
         super().__init__()
         inner = heads * head_dim
         self.heads = heads
-        self.to_q = nn.Linear(dim, inner, bias=bias_qkv)
-        self.to_k = nn.Linear(cross_dim or dim, inner, bias=bias_qkv)
-        self.to_v = nn.Linear(cross_dim or dim, inner, bias=bias_qkv)
-        self.to_out = nn.ModuleList([nn.Linear(inner, dim), nn.Dropout(0.0)])
+        self.to_q = _Linear(dim, inner, bias=bias_qkv)
+        self.to_k = _Linear(cross_dim or dim, inner, bias=bias_qkv)
+        self.to_v = _Linear(cross_dim or dim, inner, bias=bias_qkv)
+        self.to_out = nn.ModuleList([_Linear(inner, dim), nn.Dropout(0.0)])
         self._padded = None
 
     def train(self, mode: bool = True):
@@ -269,7 +274,7 @@ class Attention(nn.Module):
 class GEGLU(nn.Module):
     def __init__(self, dim, inner):
         super().__init__()
-        self.proj = nn.Linear(dim, inner * 2)
+        self.proj = _Linear(dim, inner * 2)
 
     def forward(self, x):
         return ops.geglu(self.proj(x))
@@ -279,7 +284,7 @@ class FeedForward(nn.Module):
     def __init__(self, dim, mult=4):
         super().__init__()
         inner = dim * mult
-        self.net = nn.ModuleList([GEGLU(dim, inner), nn.Dropout(0.0), nn.Linear(inner, dim)])
+        self.net = nn.ModuleList([GEGLU(dim, inner), nn.Dropout(0.0), _Linear(inner, dim)])
 
     def forward(self, x):
         return self.net[2](self.net[0](x))
@@ -307,9 +312,9 @@ class Transformer2DModel(nn.Module):
         super().__init__()
         self.norm = nn.GroupNorm(groups, ch, eps=1e-6)
         self.linear_proj = linear_proj
-        self.proj_in = nn.Linear(ch, ch) if linear_proj else nn.Conv2d(ch, ch, 1)
+        self.proj_in = _Linear(ch, ch) if linear_proj else nn.Conv2d(ch, ch, 1)
         self.transformer_blocks = nn.ModuleList([BasicTransformerBlock(ch, heads, ch // heads, cross_dim)])
-        self.proj_out = nn.Linear(ch, ch) if linear_proj else nn.Conv2d(ch, ch, 1)
+        self.proj_out = _Linear(ch, ch) if linear_proj else nn.Conv2d(ch, ch, 1)
 
     def forward(self, x, ctx):
         B, C, H, W = x.shape
@@ -345,7 +350,7 @@ def _proj(m: nn.Module, t: torch.Tensor) -> torch.Tensor:
     """nn.Linear, or a 1x1 nn.Conv2d applied as the same GEMM on a token view."""
     if isinstance(m, nn.Linear):
         return m(t)
-    return F.linear(t, m.weight.reshape(m.weight.shape[0], m.weight.shape[1]), m.bias)
+    return linear_splitk_wgrad(t, m.weight.reshape(m.weight.shape[0], m.weight.shape[1]), m.bias)
 
 
 def to_channels_last(model: nn.Module, weights: bool = True) -> nn.Module:

@@ -764,3 +764,24 @@ def test_unet_resnet_block_folded_biases(cin, cout):
             U._FOLD_BIAS = True
     err = (folded.float() - plain.float()).abs().max()
     assert err <= 0.02 * plain.float().abs().max(), err
+
+
+@pytest.mark.parametrize("T,N,K", [(65536, 320, 320), (16384, 640, 2560), (4096, 1280, 1280)])
+def test_linear_splitk_weight_grad(T, N, K):
+    """ops/linear.py split-K weight gradient (token chunks as a batched GEMM + fp32 sum) vs an fp32
+    reference, next to the single-GEMM bf16 gradient's own error."""
+    from kubernetes_cloud_amd.ops.linear import linear_splitk_wgrad
+    torch.manual_seed(T + N)
+    x = torch.randn(T // 64, 64, K, device=DEV).to(torch.bfloat16).requires_grad_()
+    w = (torch.randn(N, K, device=DEV) * 0.05).to(torch.bfloat16).requires_grad_()
+    b = torch.randn(N, device=DEV).to(torch.bfloat16).requires_grad_()
+    y = linear_splitk_wgrad(x, w, b)
+    g = torch.randn_like(y)
+    y.backward(g)
+    ref_w = g.float().reshape(-1, N).t() @ x.detach().float().reshape(-1, K)
+    ref_x = g.float() @ w.detach().float()
+    plain = (g.reshape(-1, N).t() @ x.detach().reshape(-1, K)).float()
+    scale = ref_w.abs().max()
+    assert (w.grad.float() - ref_w).abs().max() <= max(2 * (plain - ref_w).abs().max(), 1e-3 * scale)
+    assert (x.grad.float() - ref_x).abs().max() <= 0.02 * ref_x.abs().max()
+    assert (b.grad.float() - g.float().reshape(-1, N).sum(0)).abs().max() <= 0.02 * g.float().reshape(-1, N).sum(0).abs().max() + 0.5
