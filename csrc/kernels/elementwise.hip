@@ -367,3 +367,42 @@ KCA_API int kca_add_bias_nhwc(const void* a, const void* b, const float* bias, v
                      (const bf16_t*)b, bias, (bf16_t*)out, C / 8, n8);
   return 0;
 }
+
+// ---------------------------------------------------------------- column sums (bias gradients)
+// part[by][c] = sum over rows [by*RB, by*RB + RB) of x[r][c], x [M][N] bf16 row-major (N % 8 == 0):
+// 32 column groups of 8 (16-B loads, coalesced along the row) x 8 row lanes per workgroup, the row
+// lanes folded through LDS; the caller sums the few partial rows (deterministic: no atomics).
+// PyTorch's reduction ran these tall-skinny sums at 0.4-1 TB/s (profiles/sd_train_gemm_attribution_r2.txt).
+__global__ __launch_bounds__(256) void colsum_bf16_kernel(const bf16_t* __restrict__ x, float* __restrict__ part,
+                                                          int M, int N, int RB) {
+  __shared__ float red[8][32 * 8 + 4];
+  const int cg = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  const int c0 = (blockIdx.x * 32 + cg) * 8;
+  const int r0 = blockIdx.y * RB, r1 = min(M, r0 + RB);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c0 < N) {
+    for (int r = r0 + rl; r < r1; r += 8) {
+      float v[8];
+      load8(x + (long long)r * N + c0, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += v[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[rl][cg * 8 + j] = acc[j];
+  __syncthreads();
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c < N) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += red[i][threadIdx.x];
+    part[(long long)blockIdx.y * N + c] = s;
+  }
+}
+
+KCA_API int kca_colsum_bf16(const void* x, float* part, int M, int N, int RB, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || N % 8 || RB <= 0 || ((uintptr_t)x & 15)) return 1;
+  const dim3 grid((N + 255) / 256, (M + RB - 1) / RB);
+  hipLaunchKernelGGL(colsum_bf16_kernel, grid, dim3(256), 0, stream, (const bf16_t*)x, part, M, N, RB);
+  return 0;
+}

@@ -785,3 +785,14 @@ def test_linear_splitk_weight_grad(T, N, K):
     assert (w.grad.float() - ref_w).abs().max() <= max(2 * (plain - ref_w).abs().max(), 1e-3 * scale)
     assert (x.grad.float() - ref_x).abs().max() <= 0.02 * ref_x.abs().max()
     assert (b.grad.float() - g.float().reshape(-1, N).sum(0)).abs().max() <= 0.02 * g.float().reshape(-1, N).sum(0).abs().max() + 0.5
+
+
+@pytest.mark.parametrize("M,N", [(65536, 320), (4096, 10240), (1000, 1288), (7, 8)])
+def test_column_sum_kernel(M, N):
+    from kubernetes_cloud_amd.ops.linear import column_sum
+    torch.manual_seed(M + N)
+    x = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    ref = x.float().sum(0)
+    got = column_sum(x)
+    assert got.dtype == torch.bfloat16 and got.shape == (N,)
+    assert (got.float() - ref).abs().max() <= 0.01 * ref.abs().max() + 0.05

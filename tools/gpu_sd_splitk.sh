@@ -1,12 +1,12 @@
 # SD training: split-K weight gradients -- test, then DreamBooth A/B (KCA_SD_SPLITK_WGRAD=0 / 1)
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -k "splitk or unet" -x -q --timeout 120 --timeout-method thread > gpurun_out/splitk_tests.log 2>&1 || { tail -30 gpurun_out/splitk_tests.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -k "splitk or unet or column_sum" -x -q --timeout 120 --timeout-method thread > gpurun_out/splitk_tests.log 2>&1 || { tail -30 gpurun_out/splitk_tests.log; exit 1; }
 tail -1 gpurun_out/splitk_tests.log
 : > gpurun_out/splitk_ab.log
 for rep in 1 2; do
   for S in 0 1; do
-    KCA_SD_SPLITK_WGRAD=$S timeout -k 10 300 python -u bench/sd_bench.py --mode train --steps 10 > gpurun_out/sk_${S}_$rep.log 2>&1 || exit 1
-    echo "splitk=$S rep=$rep $(grep -h '^{' gpurun_out/sk_${S}_$rep.log | grep -o '"value": [0-9.]*\|"loss": [0-9.]*' | tr '\n' ' ')" | tee -a gpurun_out/splitk_ab.log
+    KCA_COLSUM=$S timeout -k 10 300 python -u bench/sd_bench.py --mode train --steps 10 > gpurun_out/sk_${S}_$rep.log 2>&1 || exit 1
+    echo "colsum=$S rep=$rep $(grep -h '^{' gpurun_out/sk_${S}_$rep.log | grep -o '"value": [0-9.]*\|"loss": [0-9.]*' | tr '\n' ' ')" | tee -a gpurun_out/splitk_ab.log
   done
 done
