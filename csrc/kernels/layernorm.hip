@@ -171,63 +171,77 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(
 
 // Sum fp32 partial rows [nparts, d] -> out[d] (bf16 or fp32). Each thread owns
 // one column; consecutive threads read consecutive columns (coalesced).
-// Narrow rows (d <= 512: SD's 320-wide transformer LayerNorms, GPT-2 small): the block kernel
+// Narrow rows (d <= 1024: SD's 320/640-wide transformer LayerNorms, GPT-2 small): the block kernel
 // above runs one 64-thread workgroup per partial -- 512 waves for the whole chip, each through
 // ~128 dependent rows (1.9 TB/s on [65536, 320]). Here every wave of a 256-thread workgroup takes
 // its own rows (wave-level sums, no barrier per row) and the 4 waves fold their dgamma / dbeta
 // partials through LDS once: the same 512 partial rows, 4x the waves.
+template <int NV>
 __global__ void __launch_bounds__(256) ln_bwd_narrow_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ h,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     const bf16_t* __restrict__ gamma, const bf16_t* __restrict__ dres,
     bf16_t* __restrict__ dx, float* __restrict__ dg_part,
     float* __restrict__ db_part, int rows, int d) {
-  __shared__ float sg[4][512], sb[4][512];
+  __shared__ float sg[4][512 * NV], sb[4][512 * NV];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const bool act = lane < (d >> 3);
-  float g[8], acc_g[8], acc_b[8];
+  float g[NV][8], acc_g[NV][8], acc_b[NV][8];
+  bool act[NV];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) { g[j] = 0.f; acc_g[j] = 0.f; acc_b[j] = 0.f; }
-  if (act) load8(gamma + lane * 8, g);
+  for (int i = 0; i < NV; ++i) {
+    act[i] = lane + 64 * i < (d >> 3);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { g[i][j] = 0.f; acc_g[i][j] = 0.f; acc_b[i][j] = 0.f; }
+    if (act[i]) load8(gamma + (lane + 64 * i) * 8, g[i]);
+  }
   for (int row = blockIdx.x * 4 + wave; row < rows; row += gridDim.x * 4) {
     const size_t base = (size_t)row * d + lane * 8;
     const float mean = mean_in[row], rstd = rstd_in[row];
-    float xh[8], gy[8];
+    float xh[NV][8], gy[NV][8];
     float s1 = 0.f, s2 = 0.f;
-    if (act) {
-      float hv[8], dv[8];
-      load8(h + base, hv);
-      load8(dy + base, dv);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        xh[j] = (hv[j] - mean) * rstd;
-        gy[j] = dv[j] * g[j];
-        s1 += gy[j];
-        s2 += gy[j] * xh[j];
-        acc_g[j] += dv[j] * xh[j];
-        acc_b[j] += dv[j];
+    for (int i = 0; i < NV; ++i) {
+      if (act[i]) {
+        float hv[8], dv[8];
+        load8(h + base + 512 * i, hv);
+        load8(dy + base + 512 * i, dv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xh[i][j] = (hv[j] - mean) * rstd;
+          gy[i][j] = dv[j] * g[i][j];
+          s1 += gy[i][j];
+          s2 += gy[i][j] * xh[i][j];
+          acc_g[i][j] += dv[j] * xh[i][j];
+          acc_b[i][j] += dv[j];
+        }
       }
     }
     const float m1 = wave_sum(s1) / d;
     const float m2 = wave_sum(s2) / d;
-    if (act) {
-      float o[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = rstd * (gy[j] - m1 - xh[j] * m2);
-      if (dres) {
-        float r[8];
-        load8(dres + base, r);
+    for (int i = 0; i < NV; ++i) {
+      if (act[i]) {
+        float o[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] += r[j];
+        for (int j = 0; j < 8; ++j) o[j] = rstd * (gy[i][j] - m1 - xh[i][j] * m2);
+        if (dres) {
+          float r[8];
+          load8(dres + base + 512 * i, r);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += r[j];
+        }
+        store8(dx + base + 512 * i, o);
       }
-      store8(dx + base, o);
     }
   }
-  if (act) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      sg[wave][lane * 8 + j] = acc_g[j];
-      sb[wave][lane * 8 + j] = acc_b[j];
+  for (int i = 0; i < NV; ++i) {
+    if (act[i]) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sg[wave][(lane + 64 * i) * 8 + j] = acc_g[i][j];
+        sb[wave][(lane + 64 * i) * 8 + j] = acc_b[i][j];
+      }
     }
   }
   __syncthreads();
@@ -354,10 +368,15 @@ KCA_API int kca_layernorm_bwd(const void* dy, const void* h, const float* mean,
   const int parts = kca_layernorm_bwd_parts(rows);
   float* dgp = workspace;
   float* dbp = workspace + (size_t)parts * d;
-  if (d <= 512 && !getenv_flag_off("KCA_LN_BWD_NARROW")) {
-    hipLaunchKernelGGL(ln_bwd_narrow_kernel, dim3(parts), dim3(256), 0, stream, (const bf16_t*)dy,
-                       (const bf16_t*)h, mean, rstd, (const bf16_t*)gamma, (const bf16_t*)dres, (bf16_t*)dx,
-                       dgp, dbp, rows, d);
+  if (d <= 1024 && !getenv_flag_off("KCA_LN_BWD_NARROW")) {
+    if (d <= 512)
+      hipLaunchKernelGGL((ln_bwd_narrow_kernel<1>), dim3(parts), dim3(256), 0, stream, (const bf16_t*)dy,
+                         (const bf16_t*)h, mean, rstd, (const bf16_t*)gamma, (const bf16_t*)dres, (bf16_t*)dx,
+                         dgp, dbp, rows, d);
+    else
+      hipLaunchKernelGGL((ln_bwd_narrow_kernel<2>), dim3(parts), dim3(256), 0, stream, (const bf16_t*)dy,
+                         (const bf16_t*)h, mean, rstd, (const bf16_t*)gamma, (const bf16_t*)dres, (bf16_t*)dx,
+                         dgp, dbp, rows, d);
   } else {
   LN_DISPATCH(nv, hipLaunchKernelGGL((ln_bwd_kernel<NV>), dim3(parts),
                                      dim3(threads), 0, stream,

@@ -21,7 +21,7 @@ def test_native_library_loaded():
     assert _lib.available(), _lib._err
 
 
-@pytest.mark.parametrize("d", [64, 320, 512, 768, 2560, 4096, 14336])
+@pytest.mark.parametrize("d", [64, 320, 512, 640, 768, 1024, 1280, 2560, 4096, 14336])
 @pytest.mark.parametrize("nres", [0, 2])
 def test_layernorm(d, nres):
     torch.manual_seed(0)
