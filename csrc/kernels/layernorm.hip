@@ -307,10 +307,13 @@ static void col_reduce(const float* part, int nparts, int d, bf16_t* out_bf, flo
                        out_bf, out_f);
 }
 
-// A/B knob: KCA_LN_BWD_NARROW=0 keeps the block kernel for narrow rows
-static bool getenv_flag_off(const char* name) {
-  const char* e = getenv(name);
-  return e && e[0] == '0';
+// A/B knob: KCA_LN_BWD_NARROW=0 keeps the block kernel for narrow rows (read once)
+static bool narrow_bwd_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("KCA_LN_BWD_NARROW");
+    return !(e && e[0] == '0');
+  }();
+  return on;
 }
 
 static void ln_geometry(int d, int& nv, int& threads) {
@@ -368,7 +371,7 @@ KCA_API int kca_layernorm_bwd(const void* dy, const void* h, const float* mean,
   const int parts = kca_layernorm_bwd_parts(rows);
   float* dgp = workspace;
   float* dbp = workspace + (size_t)parts * d;
-  if (d <= 1024 && !getenv_flag_off("KCA_LN_BWD_NARROW")) {
+  if (d <= 1024 && narrow_bwd_enabled()) {
     if (d <= 512)
       hipLaunchKernelGGL((ln_bwd_narrow_kernel<1>), dim3(parts), dim3(256), 0, stream, (const bf16_t*)dy,
                          (const bf16_t*)h, mean, rstd, (const bf16_t*)gamma, (const bf16_t*)dres, (bf16_t*)dx,
