@@ -16,8 +16,27 @@ AdamW + bf16 all-gather. Weak scaling: per-GPU work is fixed as N grows.
      or plain -- without WORLD_SIZE in the env the script re-launches itself
      as N ranks, kubernetes_cloud_amd/launch.py)
 
-Secondary measurements in the same JSON line: SD-1.5 txt2img images/s (one
-replica per GPU) and, when N > 1, BLOOM-176B TP=N decode (BASELINE config 4).
+Secondary measurements in the same JSON line (each bounded and fenced off, so
+the headline always prints):
+
+* ``secondary``             SD-1.5 txt2img images/s (BASELINE config 5; one
+                            replica per GPU, 3 timed batches);
+* ``bloom_tp``              N > 1: BLOOM-176B TP=N decode, all 70 layers
+                            (BASELINE config 4);
+* N = 1 only (``--extra``):
+  ``secondary_dreambooth``  SD-1.5 DreamBooth samples/s (BASELINE config 3,
+                            the reference formula: instance batch / step time);
+  ``secondary_decode``      GPT-J-6B decode ms/token at batch 1 and 32, prompt
+                            512 (the FasterTransformer GPT-J serving row);
+  ``secondary_bloom_slice`` BLOOM-176B, 8 of 70 layers + embeddings/head, TP
+                            modules under a one-rank RCCL group, batch 1/8/32;
+  ``secondary_weight_load`` GPT-J fp16 ``.tensors`` -> HBM GB/s (file written
+                            in the run, O_DIRECT read).
+
+``KCA_BENCH_SHARED_GPU=1`` (rehearsal only, parallel/shared_gpu.py): N ranks
+share cuda:0 with gloo collectives staged through the host, so the N > 1 paths
+run on a one-GPU box; pair it with ``--layers/--hidden`` shrink flags, which
+make the number a rehearsal, not a measurement (flagged in ``config``).
 """
 from __future__ import annotations
 
@@ -59,6 +78,16 @@ def main():
     ap.add_argument("--bloom-layers", type=int, default=0, help="0 = all 70 layers")
     ap.add_argument("--bloom-timeout", type=float, default=420.0,
                     help="seconds; if the BLOOM phase overruns, the headline line is printed without it")
+    ap.add_argument("--bloom-batches", default="1,8,32")
+    ap.add_argument("--extra", choices=["auto", "on", "off"], default="auto",
+                    help="N=1 secondaries (DreamBooth, GPT-J decode, BLOOM 8-layer slice, weight load); "
+                         "'auto' = when N == 1")
+    ap.add_argument("--extra-timeout", type=float, default=330.0,
+                    help="seconds for all N=1 secondaries together; on overrun the line prints with what finished")
+    # rehearsal shrink flags (tests/test_bench_shared_gpu.py): NOT the BASELINE config
+    ap.add_argument("--layers", type=int, default=0)
+    ap.add_argument("--hidden", type=int, default=0)
+    ap.add_argument("--heads", type=int, default=0)
     args = ap.parse_args()
 
     # `python bench.py --gpus N` outside torchrun: re-run this script as N ranks
@@ -81,12 +110,19 @@ def main():
     from kubernetes_cloud_amd.train.engine import TrainEngine
     from kubernetes_cloud_amd.ops import _lib
 
-    info = init_distributed()
+    from kubernetes_cloud_amd.parallel import shared_gpu
+    shared = shared_gpu.enabled()
+    if shared:  # rehearsal: every rank on cuda:0, gloo collectives staged through the host
+        torch.cuda.set_device(0)
+        info = init_distributed(backend="gloo")
+        shared_gpu.install()
+    else:
+        info = init_distributed()
     world = info.world_size
     if world != args.gpus and info.is_main:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; reporting the real world size",
               file=sys.stderr)
-    if torch.cuda.device_count() < world:
+    if torch.cuda.device_count() < world and not shared:
         raise SystemExit(f"[bench] {world} ranks but only {torch.cuda.device_count()} visible GPUs")
     dev = torch.device("cuda", torch.cuda.current_device())
     _lib.require()
@@ -109,7 +145,8 @@ def main():
         if mode == "tune":
             tunable.set_max_tuning_duration(40)
 
-    cfg = preset(args.model)
+    shrink = {k: v for k, v in (("n_layer", args.layers), ("n_embd", args.hidden), ("n_head", args.heads)) if v}
+    cfg = preset(args.model, **shrink)
     model = build_model(cfg, device=dev, dtype=torch.bfloat16, seed=0)
     model.gradient_checkpointing_enable(args.ckpt)
     model.train()
@@ -192,6 +229,8 @@ def main():
             },
             "secondary": None,
         }
+        if shrink or shared:  # rehearsal runs are never a BASELINE measurement
+            rec["config"]["rehearsal"] = {"shrink": shrink, "shared_gpu": shared}
     if args.sd:
         sd = _sd_txt2img(dev, world, info.is_main)
         if rec is not None:
@@ -200,6 +239,8 @@ def main():
         bloom = _bloom_tp(args, info, rec)
         if rec is not None:
             rec["bloom_tp"] = bloom
+    if args.extra == "on" or (args.extra == "auto" and world == 1):
+        _extras(args, dev, rec)
     if rec is not None:
         print(json.dumps(rec), flush=True)
     if dist.is_initialized():
@@ -230,7 +271,8 @@ def _bloom_tp(args, info, rec):
         spec = importlib.util.spec_from_file_location("kca_bloom_bench", os.path.join(ROOT, "bench", "bloom_tp_bench.py"))
         mod = importlib.util.module_from_spec(spec)
         spec.loader.exec_module(mod)
-        out = mod.run_tp_decode("bloom-176b", layers=args.bloom_layers, batches=(1, 8, 32), prompt_len=128,
+        out = mod.run_tp_decode("bloom-176b", layers=args.bloom_layers,
+                                batches=tuple(int(b) for b in args.bloom_batches.split(",")), prompt_len=128,
                                 new_tokens=32)
         return out
     except Exception as e:  # noqa: BLE001 - the headline line must still print
@@ -245,7 +287,7 @@ def _sd_txt2img(dev, world, is_main):
     """SD-1.5 txt2img images/s (BASELINE.json metric, second half; BASELINE.md
     protocol: batch 8, 512x512, 50 steps, CFG 7.0, incl. VAE decode, excl. PNG
     encode), random-init weights, one replica per rank (weak scaling): total
-    images / max-over-ranks time of one timed batch after one warmup batch."""
+    images / max-over-ranks mean time of three timed batches after one warmup."""
     import importlib.util
 
     import torch
@@ -253,7 +295,7 @@ def _sd_txt2img(dev, world, is_main):
     spec = importlib.util.spec_from_file_location("kca_sd_bench", os.path.join(ROOT, "bench", "sd_bench.py"))
     sdb = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(sdb)
-    a = argparse.Namespace(batch=8, res=512, steps=1, warmup=1, infer_steps=50, scheduler="LMSDiscreteScheduler",
+    a = argparse.Namespace(batch=8, res=512, steps=3, warmup=1, infer_steps=50, scheduler="LMSDiscreteScheduler",
                            ckpt=False)
     try:
         # hipBLASLt solution choices tuned for the SD GEMM shapes (utils/tunable.py;
@@ -274,6 +316,81 @@ def _sd_txt2img(dev, world, is_main):
         if is_main:
             print(f"[bench] SD txt2img measurement failed: {e!r}", file=sys.stderr, flush=True)
         return None
+
+
+def _load_bench(name):
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(f"kca_{name}", os.path.join(ROOT, "bench", f"{name}.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def _extras(args, dev, rec):
+    """N = 1 secondaries: the BASELINE configs a one-GPU run can measure besides
+    the headline and txt2img. Each is fenced (an exception records ``error``);
+    a watchdog bounds them all, printing the line with what finished."""
+    import threading
+
+    import torch
+    deadline = time.perf_counter() + args.extra_timeout
+
+    def _overrun():
+        if rec is not None:
+            rec["extra_error"] = f"N=1 secondaries overran {args.extra_timeout:.0f}s; unfinished ones omitted"
+            print(json.dumps(rec), flush=True)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
+
+    timer = threading.Timer(args.extra_timeout, _overrun)
+    timer.daemon = True
+    timer.start()
+
+    def fenced(key, fn):
+        if time.perf_counter() > deadline:
+            return
+        t0 = time.perf_counter()
+        try:
+            out = fn()
+        except Exception as e:  # noqa: BLE001 - the headline line must still print
+            print(f"[bench] {key} failed: {e!r}", file=sys.stderr, flush=True)
+            out = {"error": repr(e)[:300]}
+        torch.cuda.empty_cache()
+        print(f"[bench] {key}: {time.perf_counter() - t0:.1f}s", file=sys.stderr, flush=True)
+        if rec is not None:
+            rec[key] = out
+
+    def dreambooth():
+        sdb = _load_bench("sd_bench")
+        a = argparse.Namespace(batch=8, res=512, steps=5, warmup=2, ckpt=False)
+        return sdb.bench_train(a, dev)
+
+    def decode():
+        return _load_bench("decode_bench").run_decode("gpt-j-6b", batches=(1, 32), prompt_len=512, new_tokens=64)
+
+    def bloom_slice():
+        import torch.distributed as dist
+        # one-rank RCCL group: TP modules + vocab-parallel head, collectives captured in the decode graph
+        store = dist.HashStore()
+        dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=dev)
+        try:
+            return _load_bench("bloom_tp_bench").run_tp_decode("bloom-176b", layers=8, batches=(1, 8, 32),
+                                                               prompt_len=128, new_tokens=32)
+        finally:
+            dist.destroy_process_group()
+
+    def weight_load():
+        d = os.environ.get("KCA_WEIGHT_LOAD_DIR", os.environ.get("TMPDIR", "/tmp"))
+        return _load_bench("weight_load_bench").run_weight_load("gpt-j-6b", d, threads=8, sources=("cold",))
+
+    try:
+        fenced("secondary_dreambooth", dreambooth)
+        fenced("secondary_decode", decode)
+        fenced("secondary_bloom_slice", bloom_slice)
+        fenced("secondary_weight_load", weight_load)
+    finally:
+        timer.cancel()
 
 
 if __name__ == "__main__":

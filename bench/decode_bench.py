@@ -19,6 +19,46 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 
 
+def run_decode(model="gpt-j-6b", batches=(1, 32), prompt_len=512, new_tokens=64):
+    """bench.py's ``secondary_decode``: per batch size, prefill ms and pure
+    decode ms/token (greedy, HIP graphs, all requests running) -- the FT GPT-J
+    serving row (request_output_len 64)."""
+    from kubernetes_cloud_amd.engine.llm_engine import LLMEngine, SamplingParams
+    from kubernetes_cloud_amd.models.causal_lm import build_model
+    from kubernetes_cloud_amd.models.config import preset
+    dev = torch.device("cuda", torch.cuda.current_device())
+    cfg = preset(model)
+    m = build_model(cfg, device=dev, dtype=torch.bfloat16, seed=0)
+    m.eval()
+    eng = LLMEngine(m, max_slots=max(batches), max_len=prompt_len + new_tokens + 16)
+    g = torch.Generator().manual_seed(0)
+    out = []
+    for B in batches:
+        prompts = [torch.randint(0, cfg.vocab_size, (prompt_len,), generator=g).tolist() for _ in range(B)]
+        sp = SamplingParams(max_new_tokens=new_tokens, do_sample=False)
+        eng.generate(prompts, sp)  # warm-up + graph capture for this bucket
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.runner.prefill(torch.tensor(prompts[:1]), [0])
+        torch.cuda.synchronize()
+        prefill_ms = (time.perf_counter() - t0) * 1e3
+        eng.runner.release(0)
+        reqs = [eng.add_request(p, sp) for p in prompts]
+        eng.step()  # admit (prefill + first token) + first decode
+        torch.cuda.synchronize()
+        s0, t0 = eng.stats["steps"], time.perf_counter()
+        eng.run_until_done(reqs)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        n = eng.stats["steps"] - s0
+        out.append({"metric": f"{model} decode", "batch": B, "prompt_len": prompt_len, "new_tokens": new_tokens,
+                    "prefill_ms_one_seq": round(prefill_ms, 2), "decode_ms_per_token": round(dt / max(n, 1) * 1e3, 3),
+                    "decode_tokens_per_s": round(B * n / dt, 1), "dtype": "bf16", "graphs": eng.runner.use_graphs,
+                    "data": "random-init weights, random prompts"})
+    del eng, m
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="gpt-j-6b")

@@ -3,9 +3,12 @@
 
   --mode train : DreamBooth UNet finetune step (instance + class batch, frozen
                  VAE encode + CLIP encode, UNet fwd/bwd, prior-preservation MSE,
-                 fused AdamW) -> samples/s (the reference's
-                 perf/world_samples_per_second definition, sd-finetuner/
-                 finetuner.py:563-568, counting instance+class images)
+                 fused AdamW) -> samples/s by the reference's
+                 perf/world_samples_per_second definition (sd-finetuner/
+                 finetuner.py:563-568: ``args.batch_size / step_time``, where
+                 batch_size counts INSTANCE examples -- each carries its class
+                 image, datasets.py:122-140); images/s incl. class is reported
+                 alongside
   --mode infer : txt2img batch 8, 512x512, 50 steps, CFG 7.0, incl. VAE decode,
                  excl. PNG encode -> images/s
 """
@@ -94,9 +97,10 @@ def bench_train(args, dev):
         loss = step()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    sps = args.steps * 2 * B / dt
+    sps = args.steps * B / dt  # reference formula: instance batch_size / step time
     return {"metric": "SD-1.5 DreamBooth UNet finetune samples/sec", "value": round(sps, 2),
-            "unit": "samples/s", "ms_per_step": round(dt / args.steps * 1e3, 2), "loss": float(loss.item()),
+            "unit": "samples/s", "images_per_s_incl_class": round(2 * sps, 2),
+            "ms_per_step": round(dt / args.steps * 1e3, 2), "loss": float(loss.item()),
             "config": {"instance_batch": B, "class_batch": B, "resolution": args.res, "dtype": "bf16",
                        "grad_ckpt": args.ckpt, "peak_mem_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1)}}
 

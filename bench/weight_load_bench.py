@@ -63,6 +63,41 @@ class _SendfileRange(http.server.BaseHTTPRequestHandler):
                 off += sent
 
 
+def run_weight_load(model="gpt-j-6b", directory="/tmp", threads=8, sources=("cold", "repeat")):
+    """bench.py's ``secondary_weight_load``: write a random-init fp16 model as
+    ``.tensors``, then time no-init construction + native O_DIRECT stream into
+    HBM. Returns one record per source; the file is removed."""
+    from kubernetes_cloud_amd.io.hf import load_tensorized, serialize_causal_lm
+    from kubernetes_cloud_amd.models.causal_lm import build_model
+    from kubernetes_cloud_amd.models.config import preset
+    dev = torch.device("cuda", torch.cuda.current_device())
+    cfg = preset(model)
+    path = os.path.join(directory, f"kca_bench_{model}_{os.getpid()}.tensors")
+    m = build_model(cfg, device=dev, dtype=torch.float16, seed=0)
+    ref = {k: v.float().abs().sum().item() for k, v in list(m.state_dict().items())[:3]}
+    serialize_causal_lm(m, path)
+    del m
+    torch.cuda.empty_cache()
+    out = []
+    try:
+        for src in sources:
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            model_, st = load_tensorized(path, None, device=dev, dtype=torch.float16, threads=threads)
+            torch.cuda.synchronize()
+            ready = time.perf_counter() - t
+            got = {k: v.float().abs().sum().item() for k, v in list(model_.state_dict().items())[:3]}
+            assert all(abs(got[k] - ref[k]) <= 1e-3 * max(1.0, ref[k]) for k in ref), (got, ref)
+            out.append({"metric": "weight load", "source": f"file O_DIRECT ({src})", "model": model, "dtype": "fp16",
+                        "bytes": int(st["bytes"]), "gbps": round(st["gbps"], 2),
+                        "seconds_to_ready": round(ready, 3), "threads": threads, "data": "random-init weights"})
+            del model_
+            torch.cuda.empty_cache()
+    finally:
+        os.remove(path)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="gpt-j-6b")

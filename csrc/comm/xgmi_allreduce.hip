@@ -210,6 +210,37 @@ __global__ __launch_bounds__(512) void ar_two_shot_kernel(ARPeers peers, ARCtl* 
   ar_end(ctl, call);
 }
 
+// ---------------------------------------------------------------- all-gather
+// Rank r's n8 chunks land at out[r*n8 ...] on every rank (the vocab-parallel
+// LM head's logits): stage own input, one sync round, read every
+// peer's staging. Shares the call sequence (and its race argument) with the
+// all-reduce kernels above, so the two can be interleaved freely.
+template <int W>
+__global__ __launch_bounds__(512) void ag_kernel(ARPeers peers, ARCtl* ctl, int rank,
+                                                 const bf16_t* __restrict__ in, bf16_t* __restrict__ out,
+                                                 long long n8, long long spin_limit, int delay) {
+  const int b = blockIdx.x, nb = gridDim.x, tid = threadIdx.x;
+  const uint32_t call = ar_begin(ctl);
+  const int par = call & 1;
+  const long long per = (n8 + nb - 1) / nb;
+  const long long lo = b * per, hi = min(n8, lo + per);
+  uint4* mine = reinterpret_cast<uint4*>(peers.stage[par][rank]);
+  const uint4* src = reinterpret_cast<const uint4*>(in);
+  for (long long i = lo + tid; i < hi; i += blockDim.x) mine[i] = src[i];
+  const bool ok = ar_sync<W>(peers, ctl, rank, 0, call, spin_limit);
+  debug_delay(delay);
+  uint4* dst = reinterpret_cast<uint4*>(out);
+#pragma unroll
+  for (int p = 0; p < W; ++p) {
+    const u32x4* s = reinterpret_cast<const u32x4*>(peers.stage[par][p]);
+    for (long long i = lo + tid; i < hi; i += blockDim.x) {
+      const u32x4 v = __builtin_nontemporal_load(s + i);
+      dst[p * n8 + i] = ok ? make_uint4(v[0], v[1], v[2], v[3]) : nan_bf16x8();
+    }
+  }
+  ar_end(ctl, call);
+}
+
 KCA_API int kca_ar_signal_bytes() { return (int)sizeof(ARSignal); }
 KCA_API int kca_ar_max_blocks() { return AR_MAX_BLOCKS; }
 
@@ -242,13 +273,14 @@ KCA_API int kca_ipc_open(const void* handle, void** ptr) {
 KCA_API int kca_ipc_close(void* ptr) { return hipIpcCloseMemHandle(ptr) == hipSuccess ? 0 : 1; }
 
 // stage0/stage1/sig: arrays of `world` device pointers (host memory).
-// algo 0 = one-shot, 1 = two-shot. `n` bf16 elements, multiple of 8, and
-// n*2 must fit the staging buffers (checked by the Python wrapper).
+// algo 0 = one-shot, 1 = two-shot all-reduce (in/out: n elements); algo 2 =
+// all-gather (in: n elements, out: world*n). `n` bf16 elements, multiple of 8,
+// and n*2 must fit the staging buffers (checked by the Python wrapper).
 KCA_API int kca_ar_run(void* const* stage0, void* const* stage1, void* const* sig, void* ctl, int rank, int world,
                        int algo, const void* in, void* out, long long n, int blocks, long long spin_limit, int delay,
                        hipStream_t stream) {
   if (world < 1 || world > AR_MAX_RANKS || rank < 0 || rank >= world || n % 8 || n <= 0 || blocks < 1 ||
-      blocks > AR_MAX_BLOCKS || algo < 0 || algo > 1)
+      blocks > AR_MAX_BLOCKS || algo < 0 || algo > 2)
     return 1;
   if (((uintptr_t)in | (uintptr_t)out) & 15) return 2;
   ARPeers p{};
@@ -265,6 +297,9 @@ KCA_API int kca_ar_run(void* const* stage0, void* const* stage1, void* const* si
     if (algo == 0)                                                                                             \
       hipLaunchKernelGGL(ar_one_shot_kernel<WW>, dim3(blocks), dim3(512), 0, stream, p, c, rank,               \
                          (const bf16_t*)in, (bf16_t*)out, n8, spin_limit, delay);                              \
+    else if (algo == 2)                                                                                        \
+      hipLaunchKernelGGL(ag_kernel<WW>, dim3(blocks), dim3(512), 0, stream, p, c, rank, (const bf16_t*)in,     \
+                         (bf16_t*)out, n8, spin_limit, delay);                                                 \
     else                                                                                                       \
       hipLaunchKernelGGL(ar_two_shot_kernel<WW>, dim3(blocks), dim3(512), 0, stream, p, c, rank,               \
                          (const bf16_t*)in, (bf16_t*)out, n8, spin_limit, delay);                              \

@@ -219,7 +219,8 @@ class Conn {
     const int64_t body = std::atoll(cl.c_str());
     const bool keep = lower.find("\r\nconnection: close") == std::string::npos;
     if (status != 206 && !(status == 200 && off == 0 && body == len)) {
-      // drain a small error body so the connection state stays sane, then report
+      // error status: the body is not read; the caller closes this connection
+      // (its state is unknown past the headers) and reports the status
       return status >= 100 ? status : 15;
     }
     if (body != len) return 16;

@@ -111,7 +111,7 @@ def save_checkpoint(ckpt_dir: str, model, engine, trainer_state: dict, args_dict
         if rank == 0:
             with open(os.path.join(ckpt_dir, "optimizer", "meta.json"), "w") as f:
                 json.dump({"world": st["world"], "total": st["total"], "step": st["step"],
-                           "zero_stage": st["zero_stage"], "lr": st["lr"]}, f)
+                           "zero_stage": st["zero_stage"], "lr": st["lr"], "layout": st["layout"]}, f)
     rs = _rng_state()
     torch.save({k: (torch.as_tensor(v) if not isinstance(v, torch.Tensor) else v) for k, v in rs.items()},
                os.path.join(ckpt_dir, f"rng_state_{rank}.pth"))
@@ -183,7 +183,7 @@ class AsyncCheckpointWriter:
         if engine is not None:
             st = engine.optimizer_state()
             opt = ({k: snap.take("o." + k, st[k]) for k in ("master", "exp_avg", "exp_avg_sq")},
-                   {k: st[k] for k in ("world", "total", "step", "zero_stage", "lr")})
+                   {k: st[k] for k in ("world", "total", "step", "zero_stage", "lr", "layout")})
         if torch.cuda.is_available():
             torch.cuda.synchronize()
         rng = _rng_state()
@@ -259,7 +259,8 @@ def load_checkpoint(ckpt_dir: str, model, engine, rank: int = 0) -> dict:
         engine.load_optimizer_state({"master": t["master"].to(dev), "exp_avg": t["exp_avg"].to(dev),
                                      "exp_avg_sq": t["exp_avg_sq"].to(dev), "step": meta["step"],
                                      "lr": meta.get("lr"), "world": meta["world"],
-                                     "total": meta["total"]})
+                                     "total": meta["total"], "zero_stage": meta.get("zero_stage"),
+                                     **({"layout": meta["layout"]} if "layout" in meta else {})})
     p = os.path.join(ckpt_dir, f"rng_state_{rank}.pth")
     if os.path.exists(p):
         rs = torch.load(p, weights_only=True)

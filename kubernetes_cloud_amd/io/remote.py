@@ -13,7 +13,10 @@ this module resolves URIs, signs S3 requests and reads the file header.
   ``S3_ENDPOINT_URL`` / ``AWS_ENDPOINT_URL`` (default CoreWeave's accelerated
   endpoint, the one the reference probes); requests are anonymous unless
   ``AWS_ACCESS_KEY_ID`` / ``AWS_SECRET_ACCESS_KEY`` are set, then SigV4
-  (``UNSIGNED-PAYLOAD``; one signature covers every range GET of the load).
+  (``UNSIGNED-PAYLOAD``). S3 rejects header-signed requests older than 15
+  minutes, so ``stream`` re-signs before every window of at most
+  ``RESIGN_BYTES`` (2 GB: > 2 MB/s keeps a window inside the limit) and
+  re-signs and retries once when a window comes back 403.
 * TLS peers are verified against the system CA store (``KCA_TLS_VERIFY=0``
   disables it, e.g. for a self-signed test server).
 """
@@ -30,6 +33,7 @@ import urllib.parse
 from dataclasses import dataclass
 
 DEFAULT_S3_ENDPOINT = "https://accel-object.ord1.coreweave.com"
+RESIGN_BYTES = 2 << 30
 PUBLIC_TENSORIZED = "https://accel-object.ord1.coreweave.com/tensorized"
 
 
@@ -46,6 +50,11 @@ class Remote:
     headers: str = ""
     verify: bool = True
     timeout_s: float = 30.0
+    signer: object = None  # () -> fresh header block (SigV4), or None for anonymous / static headers
+
+    def resign(self):
+        if self.signer is not None:
+            self.headers = self.signer()
 
     @property
     def url(self) -> str:
@@ -92,9 +101,10 @@ def resolve(uri: str, timeout_s: float = 30.0) -> Remote:
         r = resolve(ep.rstrip("/") + "/" + bucket + "/" + key, timeout_s)
         access, secret = os.environ.get("AWS_ACCESS_KEY_ID"), os.environ.get("AWS_SECRET_ACCESS_KEY")
         if access and secret:
-            r.headers = _sigv4_headers(r.host, r.path, access, secret,
-                                       os.environ.get("AWS_DEFAULT_REGION", os.environ.get("AWS_REGION", "us-east-1")),
-                                       os.environ.get("AWS_SESSION_TOKEN"))
+            region = os.environ.get("AWS_DEFAULT_REGION", os.environ.get("AWS_REGION", "us-east-1"))
+            token = os.environ.get("AWS_SESSION_TOKEN")
+            r.signer = lambda: _sigv4_headers(r.host, r.path, access, secret, region, token)
+            r.resign()
         return r
     u = urllib.parse.urlsplit(uri)
     if scheme not in ("http", "https") or not u.hostname:
@@ -141,8 +151,39 @@ def read_header(uri: str, timeout_s: float = 30.0) -> tuple[dict, int, Remote]:
     return hdr, (16 + hl + ALIGN - 1) // ALIGN * ALIGN, r
 
 
+def _windows(lens, limit: int):
+    """Index ranges [i, j) of consecutive ranges summing to <= ``limit`` bytes
+    (a single larger range gets a window of its own)."""
+    i, acc = 0, 0
+    for j, n in enumerate(lens):
+        if j > i and acc + n > limit:
+            yield i, j
+            i, acc = j, 0
+        acc += n
+    if i < len(lens):
+        yield i, len(lens)
+
+
 def stream(r: Remote, offs, lens, ptrs, device, threads: int = 16, chunk: int = 16 << 20) -> tuple[float, float]:
-    """Ranged GETs into device (``device.type == 'cuda'``) or host pointers."""
+    """Ranged GETs into device (``device.type == 'cuda'``) or host pointers.
+    Signed sources are re-signed per window (and once more on a 403)."""
+    if r.signer is None:
+        return _stream(r, offs, lens, ptrs, device, threads, chunk)
+    tot_b, tot_s = 0.0, 0.0
+    for i, j in _windows(list(lens), RESIGN_BYTES):
+        r.resign()
+        try:
+            b, s = _stream(r, offs[i:j], lens[i:j], ptrs[i:j], device, threads, chunk)
+        except IOError as e:
+            if "HTTP 403" not in str(e):
+                raise
+            r.resign()  # e.g. RequestTimeTooSkewed / expired signature: one fresh attempt
+            b, s = _stream(r, offs[i:j], lens[i:j], ptrs[i:j], device, threads, chunk)
+        tot_b, tot_s = tot_b + b, tot_s + s
+    return tot_b, tot_s
+
+
+def _stream(r: Remote, offs, lens, ptrs, device, threads: int = 16, chunk: int = 16 << 20) -> tuple[float, float]:
     import torch
 
     from . import native

@@ -13,8 +13,10 @@ bf16; TP prefill and NeoX TP training: MB-sized, C12):
 
 Setup exchanges hipIpc handles of each rank's uncached staging/signal buffers
 through ``torch.distributed`` (any backend) and maps the peers' buffers.
-``all_reduce_(t)`` reduces a bf16 tensor in place and is graph-capturable (the
-call sequence number lives on the device). A peer that never arrives makes
+``all_reduce_(t)`` reduces a bf16 tensor in place and ``all_gather(t)``
+concatenates every rank's ``t`` (the vocab-parallel LM head's logits); both are
+graph-capturable (the call sequence number lives on the device), so a TP decode
+graph holds no RCCL call at all. A peer that never arrives makes
 the kernel time out: it poisons the output with NaN and sets a sticky error
 word; ``check()`` raises on it (the TP engine calls it once per request).
 """
@@ -32,7 +34,7 @@ _REGISTRY: dict = {}
 
 P = ctypes.c_void_p
 
-ONE_SHOT, TWO_SHOT = 0, 1
+ONE_SHOT, TWO_SHOT, ALL_GATHER = 0, 1, 2
 
 
 def _fn(name, argtypes):
@@ -146,6 +148,25 @@ class XGMIAllReduce:
             raise RuntimeError(f"kca_ar_run status {rc}")
         self.calls += 1
         return t
+
+    def all_gather(self, t: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """[world * t.numel()] bf16: rank r's ``t`` at ``out[r*n:(r+1)*n]``."""
+        n = t.numel()
+        if not self.eligible(t):
+            raise ValueError("tensor not eligible for the xGMI all-gather (bf16, contiguous, 16B-aligned, "
+                             f"numel % 8 == 0, <= {self.max_bytes} bytes)")
+        if out is None:
+            out = torch.empty(self.world * n, device=t.device, dtype=t.dtype)
+        if out.numel() != self.world * n or not out.is_contiguous() or out.data_ptr() % 16:
+            raise ValueError("all-gather output must be a contiguous 16B-aligned [world * n] tensor")
+        blocks = blocks_for(n, self.world, ONE_SHOT, self.max_blocks)
+        rc = self._run(self._stage0, self._stage1, self._sig, P(self._ctl), self.rank, self.world, ALL_GATHER,
+                       t.data_ptr(), out.data_ptr(), n, blocks, self.spin_limit, int(self.debug_delay),
+                       _lib.stream())
+        if rc != 0:
+            raise RuntimeError(f"kca_ar_run (all-gather) status {rc}")
+        self.calls += 1
+        return out
 
     def error(self) -> int:
         e = ctypes.c_int(0)

@@ -16,8 +16,11 @@ Slice axes (Megatron column/row split, what TP inference engines store):
 ``dense_h_to_4h`` weight/bias by rows, ``self_attention.dense`` and
 ``dense_4h_to_h`` weights by columns; everything else is replicated.
 ``export_ds_inference`` writes the same layout from an HF directory (tests,
-re-sharding). Parity with the published checkpoint itself is unpinned: it is
-not in the tree and there is no network; the layout follows its config schema.
+re-sharding). Rank r's files are found by position in ``checkpoints.tp``
+(DeepSpeed's assignment, not the file names), and ``[tensor, dtype]`` list
+values (how DeepSpeed's TP save stores ``query_key_value``) are unwrapped.
+Parity with the published checkpoint itself is unpinned: it is not in the tree
+and there is no network; the layout follows its config schema.
 """
 from __future__ import annotations
 
@@ -98,9 +101,28 @@ def export_ds_inference(model_or_dir, out_dir: str, tp_size: int, shards_per_ran
     return out_dir
 
 
-def _tp_rank_of(fn: str) -> int:
-    base = os.path.basename(fn)
-    return int(base.split("_")[1])
+def _tp_files_by_rank(files: list, tp_size: int) -> dict:
+    """Checkpoint rank -> its files. DeepSpeed assigns ``checkpoints.tp`` by
+    POSITION: with n = len(files) / tp_size, rank r reads files[r*n:(r+1)*n]
+    (file names carry no contract)."""
+    if not files:
+        return {}
+    if len(files) % tp_size:
+        raise ValueError(f"{len(files)} tp checkpoint files do not split over tp_size {tp_size}")
+    n = len(files) // tp_size
+    return {r: list(files[r * n:(r + 1) * n]) for r in range(tp_size)}
+
+
+def _unwrap(v):
+    """DeepSpeed's TP save stores some entries (query_key_value) as
+    ``[tensor, dtype]`` lists; take the tensor."""
+    while isinstance(v, (list, tuple)):
+        if not v:
+            raise ValueError("empty list value in DS-inference checkpoint")
+        v = v[0]
+    if not isinstance(v, torch.Tensor):
+        raise TypeError(f"unexpected checkpoint value {type(v).__name__}")
+    return v
 
 
 @torch.no_grad()
@@ -131,14 +153,13 @@ def load_ds_inference_tp(path: str, rank: int, world: int, group=None, device=No
         src_ranks, sub, nsub = [rank * T // world], rank % (world // T), world // T
     full: dict = {}
     for fn in ck.get("non_tp", []):
-        full.update({_strip(k): v for k, v in load(fn).items()})
+        full.update({_strip(k): _unwrap(v) for k, v in load(fn).items()})
     slices: dict = {}  # hf key -> {ckpt rank: tensor}
-    for fn in ck.get("tp", []):
-        r = _tp_rank_of(fn)
-        if r not in src_ranks:
-            continue
-        for k, v in load(fn).items():
-            slices.setdefault(_strip(k), {})[r] = v
+    by_rank = _tp_files_by_rank(list(ck.get("tp", [])), T)
+    for r in src_ranks:
+        for fn in by_rank.get(r, ()):
+            for k, v in load(fn).items():
+                slices.setdefault(_strip(k), {})[r] = _unwrap(v)
 
     Hs = H // T  # heads per checkpoint slice
 

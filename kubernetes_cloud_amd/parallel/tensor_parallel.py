@@ -106,6 +106,11 @@ def gather_last_dim(x, group):
 def _gather_nograd(x, group):
     world = dist.get_world_size(group)
     x = x.contiguous()
+    from .custom_ar import lookup
+    ar = lookup(group)
+    if ar is not None and ar.eligible(x):  # decode logits: one sync round over xGMI peer memory, graph-capturable
+        flat = ar.all_gather(x)  # [world, *x.shape] flattened
+        return flat.view(world, *x.shape).movedim(0, -2).reshape(*x.shape[:-1], world * x.shape[-1])
     parts = [torch.empty_like(x) for _ in range(world)]
     dist.all_gather(parts, x, group=group)
     return torch.cat(parts, dim=-1)

@@ -674,14 +674,30 @@ class TrainEngine:
     def grad_norm(self) -> float:
         return float(self.opt.grad_norm.item())
 
+    def layout_tag(self) -> str:
+        """Hash of the flat layout (slot names/offsets, bucket bounds, param
+        partitioning): stage 3 orders slots by gather unit, stages 0-2 by
+        backward buckets, so equal totals do not imply equal layouts."""
+        import hashlib
+        h = hashlib.sha1(f"{int(self.part_params)}|{self.world}|{self.total}".encode())
+        for s in self.slots:
+            h.update(f"{s.name}:{s.offset}:{s.numel};".encode())
+        for b in self.buckets:
+            h.update(f"[{b.start}:{b.size}]".encode())
+        return h.hexdigest()[:16]
+
     def optimizer_state(self) -> dict:
         return {"master": self.opt.master, **self.opt.state_dict(), "rank": self.rank,
                 "world": self.world, "total": self.total, "zero_stage": self.stage,
-                "requested_zero_stage": self.zero_stage}
+                "requested_zero_stage": self.zero_stage, "layout": self.layout_tag()}
 
     def load_optimizer_state(self, sd: dict):
         if sd.get("world", 1) != self.world or sd.get("total") != self.total:
             raise ValueError("optimizer shard layout mismatch (world size or model changed)")
+        if "layout" in sd and sd["layout"] != self.layout_tag():
+            raise ValueError(f"optimizer state was saved with a different flat layout (ZeRO stage "
+                             f"{sd.get('zero_stage')} vs {self.stage}, or bucket size / model changed); "
+                             "resume with the same --zero-stage and bucket size")
         self.opt.master.copy_(sd["master"])
         self.opt.load_state_dict(sd)
         self.publish(self.opt.master)

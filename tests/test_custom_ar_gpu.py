@@ -1,6 +1,7 @@
 """Custom xGMI all-reduce (csrc/comm/xgmi_allreduce.hip): two ranks on the
 box's single GPU exchange hipIpc handles (gloo bootstrap) and must produce the
-exact bf16 sum.
+exact bf16 sum (and, for the all-gather interleaved into the same call
+sequence, the exact concatenation).
 
 The stress case interleaves sizes below and above the one-shot/two-shot switch
 and the block-count cap (so the slice->block map changes from call to call),
@@ -68,6 +69,10 @@ def _worker(rank, world, port, q, mode):
                 ar.all_reduce_(t, algo=algo)
                 outs.append(t)
                 refs.append(sum(x.float() for x in xs))
+                if n * 2 <= (8 << 20) and it % 3 == 0:  # all-gathers share the call sequence
+                    g = xs[rank].cuda() + 1
+                    outs.append(ar.all_gather(g))
+                    refs.append(torch.cat([x.float() + 1 for x in xs]))
         torch.cuda.synchronize()
         errs = [float((o.float().cpu() - r).abs().max()) for o, r in zip(outs, refs)]
         q.put((rank, ar.error() == 0, errs))

@@ -43,6 +43,38 @@ def test_ds_inference_reshard(bloom, world, tmp_path):
             assert torch.equal(got[k], v), (world, rank, k)
 
 
+def test_ds_inference_deepspeed_layout(bloom, tmp_path):
+    """A hand-built checkpoint in DeepSpeed's own save layout: qkv
+    entries as [tensor, dtype] lists, file names that carry no rank, ranks
+    assigned by position in checkpoints.tp."""
+    from kubernetes_cloud_amd.parallel.ds_inference_ckpt import export_ds_inference, load_ds_inference_tp
+    from kubernetes_cloud_amd.parallel.tensor_parallel import shard_model_from_full
+    d, full = bloom
+    src = export_ds_inference(d, str(tmp_path / "ours"), tp_size=2, shards_per_rank=2, dtype=torch.float32)
+    cfgj = json.load(open(os.path.join(src, "ds_inference_config.json")))
+    out = tmp_path / "ds"
+    out.mkdir()
+    names = []
+    for i, fn in enumerate(cfgj["checkpoints"]["tp"]):  # rank-major order, renamed
+        sd = torch.load(os.path.join(src, fn), weights_only=True)
+        sd = {k: ([v, "torch.float32"] if "query_key_value" in k else v) for k, v in sd.items()}
+        name = f"bloom-ds-shard-{chr(ord('a') + i)}.pt"
+        torch.save(sd, str(out / name))
+        names.append(name)
+    nt = torch.load(os.path.join(src, "non-tp.pt"), weights_only=True)
+    torch.save(nt, str(out / "non-tp-weights.pt"))
+    cfgj["checkpoints"] = {"non_tp": ["non-tp-weights.pt"], "tp": names}
+    (out / "ds_inference_config.json").write_text(json.dumps(cfgj))
+    (out / "config.json").write_text(open(os.path.join(src, "config.json")).read())
+    for world in (1, 2):
+        for rank in range(world):
+            got = load_ds_inference_tp(str(out), rank, world, dtype=torch.float32).state_dict()
+            ref = shard_model_from_full(full, rank, world).state_dict()
+            for k, v in ref.items():
+                if not k.endswith("alibi"):
+                    assert torch.equal(got[k], v), (world, rank, k)
+
+
 def test_hf_snapshot_cli_local_mirror(tmp_path, monkeypatch):
     """download.py contract (--model-id/--revision into $HF_HOME's hub cache), served
     here from a local mirror dir: the result resolves through the read-only

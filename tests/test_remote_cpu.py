@@ -119,6 +119,44 @@ def test_s3_path_style_and_sigv4(server, monkeypatch):
     assert H.log and all(a and a.startswith("AWS4-HMAC-SHA256") for _, _, a in H.log)
 
 
+def test_s3_resign_per_window_and_retry_on_403(server, monkeypatch):
+    """S3 rejects header-signed requests older than 15 min: the
+    stream re-signs per byte window, and a window answered 403 (expired
+    signature) is re-signed and retried once."""
+    from kubernetes_cloud_amd.io import remote
+    from kubernetes_cloud_amd.io.hf import serialize_causal_lm
+    from kubernetes_cloud_amd.io.tensors import load_state_dict
+    base, H, root = server
+    _, m = _tiny_lm(root, "gpt2")
+    os.makedirs(root / "bucket", exist_ok=True)
+    serialize_causal_lm(m, str(root / "bucket" / "model.tensors"))
+    monkeypatch.setenv("S3_ENDPOINT_URL", base)
+    monkeypatch.setenv("AWS_ACCESS_KEY_ID", "AKIDEXAMPLE")
+    monkeypatch.setenv("AWS_SECRET_ACCESS_KEY", "secret")
+    monkeypatch.setattr(remote, "RESIGN_BYTES", 64 << 10)
+    calls = {"n": 0, "fail": 1}
+    orig_sign, orig_stream = remote._sigv4_headers, remote._stream
+
+    def sign(*a, **k):
+        calls["n"] += 1
+        return orig_sign(*a, **k)
+
+    def flaky(r, *a, **k):  # the first window's GETs come back 403 once
+        if calls["fail"]:
+            calls["fail"] -= 1
+            raise IOError(f"streaming {r.url} failed: HTTP 403")
+        return orig_stream(r, *a, **k)
+    monkeypatch.setattr(remote, "_sigv4_headers", sign)
+    monkeypatch.setattr(remote, "_stream", flaky)
+    sd = load_state_dict("s3://bucket/model.tensors")
+    assert torch.equal(sd["wte.weight"], m.state_dict()["wte.weight"])
+    windows = list(remote._windows([e.numel() * e.element_size() for e in m.state_dict().values()], 64 << 10))
+    assert len(windows) > 2
+    assert calls["n"] >= len(windows) + 2  # resolve + one per window + the 403 retry
+    assert calls["fail"] == 0
+    assert list(remote._windows([10, 10, 100, 5], 25)) == [(0, 2), (2, 3), (3, 4)]
+
+
 def test_sigv4_matches_aws_reference_vector():
     """AWS's documented S3 SigV4 example (GET /test.txt, Range bytes=0-9,
     examplebucket, 20130524T000000Z): our signer with the same signed headers
