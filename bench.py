@@ -23,6 +23,8 @@ the headline always prints):
                             replica per GPU, 3 timed batches);
 * ``bloom_tp``              N > 1: BLOOM-176B TP=N decode, all 70 layers
                             (BASELINE config 4);
+* ``allreduce_sweep``       N > 1: custom xGMI one-/two-shot vs RCCL
+                            latency by message size (bench/allreduce_bench.py);
 * N = 1 only (``--extra``):
   ``secondary_dreambooth``  SD-1.5 DreamBooth samples/s (BASELINE config 3,
                             the reference formula: instance batch / step time);
@@ -274,6 +276,13 @@ def _bloom_tp(args, info, rec):
         out = mod.run_tp_decode("bloom-176b", layers=args.bloom_layers,
                                 batches=tuple(int(b) for b in args.bloom_batches.split(",")), prompt_len=128,
                                 new_tokens=32)
+        try:  # custom one-/two-shot vs RCCL by message size, on the same ranks (placing the switch points)
+            sweep = _load_bench("allreduce_bench").run_sweep()
+            if rec is not None:
+                rec["allreduce_sweep"] = sweep
+        except Exception as e:  # noqa: BLE001
+            if rec is not None:
+                rec["allreduce_sweep"] = {"error": repr(e)[:300]}
         return out
     except Exception as e:  # noqa: BLE001 - the headline line must still print
         if info.is_main:

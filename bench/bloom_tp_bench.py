@@ -57,11 +57,15 @@ def run_tp_decode(model_name="bloom-176b", layers=0, batches=(1, 8, 32), prompt_
         from kubernetes_cloud_amd.parallel.custom_ar import register
         ar = register(None)
     runner = ModelRunner(model, max_slots=max(batches), max_len=prompt_len + new_tokens + 8)
+    chan = None
+    if world > 1:
+        from kubernetes_cloud_amd.engine.ctrl_channel import open_channel
+        chan = open_channel(ctrl)
     out = None
     if rank != 0:
-        follower_loop(runner, ctrl)
+        follower_loop(runner, chan)
     else:
-        run = CollectiveRunner(runner, ctrl) if world > 1 else runner
+        run = CollectiveRunner(runner, chan) if world > 1 else runner
         eng = LLMEngine(model, runner=run)
         g = torch.Generator().manual_seed(0)
         out = []
@@ -87,13 +91,15 @@ def run_tp_decode(model_name="bloom-176b", layers=0, batches=(1, 8, 32), prompt_
                         "prefill_ms": round(prefill_ms, 2), "decode_ms_per_token": round(dt / max(n, 1) * 1e3, 3),
                         "tokens_per_s": round((sum(len(r.output) for r in reqs) - 2 * B) / dt, 1),
                         "layers": cfg.n_layers, "tp": world, "load_s": round(load_s, 1), "dtype": "bf16",
-                        "custom_allreduce": ar is not None, "data": "random-init weights"})
+                        "custom_allreduce": ar is not None, "ctrl": chan.kind if chan is not None else None,
+                        "data": "random-init weights"})
         if world > 1:
             run.shutdown()
     if ar is not None:
         ar.check()
     if world > 1:
-        dist.barrier()
+        dist.barrier(group=ctrl)
+        chan.close()
         dist.destroy_process_group(ctrl)
     del runner, model
     torch.cuda.empty_cache()

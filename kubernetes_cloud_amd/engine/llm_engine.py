@@ -11,6 +11,12 @@ output log-probs).
 
 ``step()`` = admit waiting requests (prefill + first token) while slots and
 KV pages are free, then one fused decode step for every running request.
+Chunked prefill (``prefill_chunk``): while requests are decoding, a step
+spends at most ``prefill_chunk`` prompt tokens on prefill -- a long prompt is
+prefilled over several steps (``ModelRunner.prefill(..., start=)`` continues
+its slot), each followed by the decode step of the running batch, so a
+2048-token admission no longer stalls every running stream for its whole
+prefill; with nothing decoding a prompt prefills in one pass.
 Admission reserves a request's worst-case page count (prompt + max_new_tokens)
 against the paged cache, so a running request never runs out of pages (no
 preemption needed); pages go back to the pool the step a request finishes.
@@ -64,6 +70,7 @@ class Request:
     t_done: float = 0.0
     future: Future | None = None
     on_token: object = None  # callable(request) after every generated token (streaming front ends)
+    prefilled: int = 0       # chunked prefill: prompt tokens already in the KV cache
 
     @property
     def done(self) -> bool:
@@ -77,7 +84,7 @@ class Request:
 class LLMEngine:
     def __init__(self, model, max_slots: int = 32, max_len: int | None = None, use_graphs: bool | None = None,
                  max_prefill_tokens: int = 16384, runner=None, page_size: int | None = None,
-                 kv_pages: int | None = None):
+                 kv_pages: int | None = None, prefill_chunk: int | None = None):
         # ``runner``: e.g. a tp_driver.CollectiveRunner that mirrors every call to TP follower ranks
         self.runner = runner or ModelRunner(model, max_slots=max_slots, max_len=max_len, use_graphs=use_graphs,
                                             page_size=page_size, kv_pages=kv_pages)
@@ -93,8 +100,11 @@ class LLMEngine:
         self._thread = None
         self._stop = False
         self.max_prefill_tokens = max_prefill_tokens
+        # prompt-token budget of a step while requests are decoding (None/0: whole prompts)
+        self.prefill_chunk = int(prefill_chunk) if prefill_chunk else 0
+        self.prefilling: list[Request] = []  # admitted, prompt partially in the cache (r.prefilled tokens)
         self.stats = {"steps": 0, "decode_tokens": 0, "prefill_tokens": 0, "finished": 0, "prefill_batches": 0,
-                      "prefill_pad_tokens": 0}
+                      "prefill_pad_tokens": 0, "prefill_chunks": 0, "max_step_prefill_tokens": 0}
         cache = getattr(self.runner, "cache", None)
         self._paged = cache is not None and getattr(cache, "paged", False)
         self._page_budget = cache.n_pages if self._paged else 0
@@ -123,7 +133,7 @@ class LLMEngine:
         return r
 
     def has_work(self) -> bool:
-        return bool(self.waiting or self.running)
+        return bool(self.waiting or self.running or self.prefilling)
 
     def _row(self, r: Request, token: int | None = None) -> dict:
         p = r.params
@@ -214,12 +224,43 @@ class LLMEngine:
         with self._step_lock:
             return self._step()
 
+    def _first_token(self, r: Request, logits, finished: list):
+        toks, lps = self.runner.sample_first(logits, [self._row(r, 0)])
+        self._append(r, toks[0], lps[0])
+        if r.done:
+            self._finish(r)
+            finished.append(r)
+        else:
+            self.running.append(r)
+
+    def _chunk_step(self, budget: int, finished: list) -> int:
+        """Advance partially prefilled prompts by up to ``budget`` tokens."""
+        used = 0
+        for r in list(self.prefilling):
+            if used >= budget:
+                break
+            p0 = r.prefilled
+            n = min(budget - used, len(r.prompt) - p0)
+            ids = torch.tensor([r.prompt[p0:p0 + n]], dtype=torch.long)
+            logits = self.runner.prefill(ids, [r.slot], [n], start=[p0])
+            r.prefilled += n
+            used += n
+            self.stats["prefill_tokens"] += n
+            self.stats["prefill_chunks"] += 1
+            if r.prefilled == len(r.prompt):
+                self.prefilling.remove(r)
+                self._first_token(r, logits, finished)
+        return used
+
     def _step(self) -> list[Request]:
         finished = []
+        chunked = self.prefill_chunk > 0 and (self.running or self.prefilling)
+        budget = self.prefill_chunk if chunked else self.max_prefill_tokens
+        used = self._chunk_step(budget, finished) if self.prefilling else 0
+        budget -= used
         with self._lock:
             admit = []
-            budget = self.max_prefill_tokens
-            while self.waiting and self.free and (not admit or budget >= len(self.waiting[0].prompt)):
+            while self.waiting and self.free and budget > 0 and (not admit or budget >= len(self.waiting[0].prompt)):
                 need = self._pages_needed(self.waiting[0])
                 if self._paged and self._committed + need > self._page_budget:
                     if need > self._page_budget:  # can never fit: fail it rather than block the queue
@@ -234,8 +275,14 @@ class LLMEngine:
                 r = self.waiting.pop(0)
                 r.slot = self.free.pop()
                 self._committed += need
+                if chunked and len(r.prompt) > budget:  # prefill this one chunk by chunk
+                    r.prefilled = 0
+                    self.prefilling.append(r)
+                    break
                 budget -= len(r.prompt)
                 admit.append(r)
+        if self.prefilling and budget > 0 and chunked:
+            used += self._chunk_step(budget, finished)
         for group in _prefill_groups(admit):
             T = max(len(r.prompt) for r in group)
             lens = [len(r.prompt) for r in group]
@@ -246,6 +293,7 @@ class LLMEngine:
                 logits = self.runner.prefill(ids, [r.slot for r in group], lens)
             toks, lps = self.runner.sample_first(logits, [self._row(r, 0) for r in group])
             self.stats["prefill_tokens"] += sum(lens)
+            used += sum(lens)
             self.stats["prefill_pad_tokens"] += T * len(group) - sum(lens)
             self.stats["prefill_batches"] += 1
             for r, t, lp in zip(group, toks, lps):
@@ -270,6 +318,7 @@ class LLMEngine:
                     still.append(r)
             self.running = still
         self.stats["steps"] += 1
+        self.stats["max_step_prefill_tokens"] = max(self.stats["max_step_prefill_tokens"], used)
         return finished
 
     def run_until_done(self, reqs: list[Request] | None = None):
@@ -317,8 +366,8 @@ class LLMEngine:
                 self.step()
             except Exception as e:  # fail every in-flight request, keep serving
                 with self._lock:
-                    victims = self.running + self.waiting
-                    self.running, self.waiting = [], []
+                    victims = self.running + self.prefilling + self.waiting
+                    self.running, self.prefilling, self.waiting = [], [], []
                 for r in victims:
                     try:
                         self._free_slot(r)

@@ -196,29 +196,33 @@ class KVCache:
         self._dirty = True
 
     # --------------------------------------------------------------- prefill
-    def plan_write(self, slots: list[int], lens: list[int], T: int):
-        """Index plan for writing prompts (right-padded to T) into the cache."""
+    def plan_write(self, slots: list[int], lens: list[int], T: int, start: list[int] | None = None):
+        """Index plan for writing prompts (right-padded to T) into the cache;
+        ``start``: first position of each row (chunked prefill continues a slot)."""
         if not self.paged:
             return None
         import numpy as np
         PS = self.page_size
+        start = start or [0] * len(slots)
         pg, off, src = [], [], []
-        for i, (s_, L) in enumerate(zip(slots, lens)):
-            t = np.arange(L)
-            own = np.asarray(self.pages[s_][:self.pages_for(L)], dtype=np.int64)
+        for i, (s_, L, p0) in enumerate(zip(slots, lens, start)):
+            t = np.arange(p0, p0 + L)
+            own = np.asarray(self.pages[s_][:self.pages_for(p0 + L)], dtype=np.int64)
             pg.append(own[t // PS])
             off.append(t % PS)
-            src.append(i * T + t)
+            src.append(i * T + t - p0)
         host = [torch.from_numpy(np.concatenate(xs)) for xs in (pg, off, src)]
         return {d: tuple(t.to(d) for t in host) for d in self.devices}
 
-    def write(self, li: int, k: torch.Tensor, v: torch.Tensor, slots: list[int], lens: list[int], plan):
+    def write(self, li: int, k: torch.Tensor, v: torch.Tensor, slots: list[int], lens: list[int], plan,
+              start: list[int] | None = None):
         """k, v: [n, T, Hkv, D] (strided views of the QKV GEMM output)."""
         kc, vc = self.k[li], self.v[li]
         if plan is None:
-            for i, (s_, L) in enumerate(zip(slots, lens)):  # strided copies (index scatter is ~4x slower)
-                kc[s_, :, :L].copy_(k[i, :L].transpose(0, 1))
-                vc[s_, :, :L].copy_(v[i, :L].transpose(0, 1))
+            start = start or [0] * len(slots)
+            for i, (s_, L, p0) in enumerate(zip(slots, lens, start)):  # strided copies (index scatter is ~4x slower)
+                kc[s_, :, p0:p0 + L].copy_(k[i, :L].transpose(0, 1))
+                vc[s_, :, p0:p0 + L].copy_(v[i, :L].transpose(0, 1))
             return
         pg, off, src = plan[self.layer_devices[li]]
         n, T, Hkv, D = k.shape
@@ -314,36 +318,48 @@ class ModelRunner:
 
     # ------------------------------------------------------------- prefill
     @torch.no_grad()
-    def prefill(self, ids: torch.Tensor, slots: list[int], lens: list[int] | None = None) -> torch.Tensor:
+    def prefill(self, ids: torch.Tensor, slots: list[int], lens: list[int] | None = None,
+                start: list[int] | None = None) -> torch.Tensor:
         """ids [n, T] prompts, right-padded to T when ``lens`` (their true
         lengths) is given -> last-real-position logits [n, V]. Writes K/V of
         positions [0, lens[i]) into each slot and marks the prompt as seen.
         Padding needs no mask: with causal attention a real query row never
-        sees a key to its right, so ragged prompts batch into one pass."""
+        sees a key to its right, so ragged prompts batch into one pass.
+
+        ``start`` (chunked prefill): row i continues slot i's sequence at
+        position start[i] -- its K/V land at [start, start + lens[i]) and its
+        queries attend to the cached prefix plus the chunk."""
         m, cfg = self.model, self.cfg
         ids = ids.to(self.device)
         n, T = ids.shape
-        assert T <= self.max_len
         lens = [T] * n if lens is None else [int(x) for x in lens]
-        assert len(lens) == n and all(0 < L <= T for L in lens)
+        start = [0] * n if start is None else [int(x) for x in start]
+        assert len(lens) == n and len(start) == n and all(0 < L <= T for L in lens)
+        assert all(p0 + L <= self.max_len for p0, L in zip(start, lens))
         ragged = any(L != T for L in lens)
-        for s_, L in zip(slots, lens):
-            self.cache.release(s_)  # a reused slot starts empty
-            self.cache.reserve(s_, L)
+        cont = any(start)
+        for s_, L, p0 in zip(slots, lens, start):
+            if p0 == 0:
+                self.cache.release(s_)  # a reused slot starts empty
+            self.cache.reserve(s_, p0 + L)
         self.cache.sync()
-        plan = self.cache.plan_write(slots, lens, T)
+        plan = self.cache.plan_write(slots, lens, T, start)
         sl = torch.tensor(slots, device=self.device, dtype=torch.long)
-        self.seen[sl] = 0
+        fresh = [i for i, p0 in enumerate(start) if p0 == 0]
+        if len(fresh) == n:
+            self.seen[sl] = 0
+        elif fresh:
+            self.seen[sl[fresh]] = 0
         if ragged:
             valid = torch.arange(T, device=self.device)[None] < torch.tensor(lens, device=self.device)[:, None]
             self.seen[sl[:, None].expand(n, T)[valid], ids[valid]] = 1
         else:
             self.seen[sl[:, None].expand(n, T), ids] = 1
-        h = m.wte(ids)
-        if m.wpe is not None:
-            h = h + m.wpe(torch.arange(T, device=self.device))
-        if m.emb_ln is not None:
-            h = m.emb_ln(h)
+        pos_ids = None
+        if cont:
+            pos_ids = (torch.tensor(start, device=self.device)[:, None]
+                       + torch.arange(T, device=self.device)[None]).clamp_(max=self.max_len - 1)
+        h = m.embed(ids, pos_ids if cont else None)
         pending = ()
         for li, blk in enumerate(m.h):
             if self.multi_device and h.device != self.layer_devs[li]:
@@ -354,9 +370,11 @@ class ModelRunner:
             q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
             if self.rot > 0:
                 ops.apply_rotary_(q, k, self.rot, T, cfg.rotary_interleaved, cfg.rotary_base,
-                                  max_pos=self.max_len)
-            self.cache.write(li, k, v, slots, lens, plan)
-            if at.window:
+                                  pos_ids=pos_ids, max_pos=self.max_len)
+            self.cache.write(li, k, v, slots, lens, plan, start)
+            if cont:
+                o = self._continued_attention(li, q, slots, lens, start, at)
+            elif at.window:
                 o = self._windowed_prefill(q, k, v, at)
             else:
                 o = ops.flash_attention(q, k, v, causal=True, scale=at.scale, alibi=at.alibi)
@@ -378,6 +396,25 @@ class ModelRunner:
         y, _ = m.ln_f(pick(h), residual=tuple(pick(p_) for p_ in pending))
         return m.logits_from_hidden(y)[:, -1].to(self.device)
 
+    def _continued_attention(self, li, q, slots, lens, start, at):
+        """Chunk queries [start, start + L) of each row against the slot's cached
+        keys [0, start + L) (just written): bottom-right-aligned causal mask,
+        so query j of the chunk sees keys <= start + j."""
+        n, T = q.shape[0], q.shape[1]
+        o = torch.zeros_like(q)
+        kc, vc, tbl = self.cache.k[li], self.cache.v[li], self.cache.table_on(self.layer_devs[li])
+        for i, (s_, L, p0) in enumerate(zip(slots, lens, start)):
+            kv = p0 + L
+            kw = dops.gather_kv(kc, s_, kv, tbl).transpose(0, 1)[None]
+            vw = dops.gather_kv(vc, s_, kv, tbl).transpose(0, 1)[None]
+            if at.window:
+                lo = max(0, kv - L - at.window + 1)  # oldest key any chunk query can see
+                o[i:i + 1, :L] = self._windowed_prefill(q[i:i + 1, :L], kw[:, lo:], vw[:, lo:], at)
+            else:
+                o[i:i + 1, :L] = ops.flash_attention(q[i:i + 1, :L], kw, vw, causal=True, scale=at.scale,
+                                                     alibi=at.alibi)
+        return o
+
     @staticmethod
     def _hop(dev, h, pending):
         """Move the residual stream to the next layer-split device."""
@@ -385,21 +422,17 @@ class ModelRunner:
 
     @staticmethod
     def _windowed_prefill(q, k, v, at):
-        T = q.shape[1]
+        Tq, Tk = q.shape[1], k.shape[1]
         s = torch.einsum("bqhd,bkhd->bhqk", q.float(), k.float()) * at.scale
-        qi = torch.arange(T, device=q.device)[:, None]
-        ki = torch.arange(T, device=q.device)[None, :]
+        qi = torch.arange(Tq, device=q.device)[:, None] + (Tk - Tq)  # bottom-right aligned
+        ki = torch.arange(Tk, device=q.device)[None, :]
         s = s.masked_fill((ki > qi) | (ki <= qi - at.window), float("-inf"))
         return torch.einsum("bhqk,bkhd->bqhd", s.softmax(-1), v.float()).to(q.dtype)
 
     # -------------------------------------------------------------- decode
     def _layers_decode(self, tokens, pos, slots, kv_lens, max_kv, ws, obuf):
         m, cfg = self.model, self.cfg
-        h = m.wte(tokens)
-        if m.wpe is not None:
-            h = h + m.wpe(pos.long())
-        if m.emb_ln is not None:
-            h = m.emb_ln(h)
+        h = m.embed(tokens, pos.long())
         pending = ()
         per_dev = {self.device: (pos, slots, kv_lens, ws, obuf)}
         for li, blk in enumerate(m.h):

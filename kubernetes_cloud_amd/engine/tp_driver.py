@@ -2,11 +2,13 @@
 
 Rank 0 owns the scheduler (``LLMEngine``) and the HTTP front end; every call it
 makes on its ``ModelRunner`` (prefill / sample_first / decode, and for beam
-search decode_topk / copy_slots, and page release) is first
-broadcast on a small CPU (gloo) control group, and follower ranks replay it on
-their own shard (``follower_loop``). The GPU work of each call -- including the
-row-parallel all-reduces and the vocab all-gather -- then runs in lock step
-over RCCL. Sampling is replicated: identical gathered logits + identical
+search decode_topk / copy_slots, and page release) is first published on a
+control channel (``engine/ctrl_channel.py``: the native shared-memory ring when
+the TP group shares a node -- no collective between decode steps -- else a gloo
+broadcast), and follower ranks replay it on their own shard
+(``follower_loop``). The GPU work of each call -- including the row-parallel
+all-reduces and the vocab all-gather (the custom xGMI kernels for decode-size
+messages, RCCL above) -- then runs in lock step. Sampling is replicated: identical gathered logits + identical
 per-request seeds give identical tokens on every rank, so no token broadcast is
 needed. This is the MI355X replacement for the DeepSpeed-Inference /
 MII deployment of BLOOM-176B (bloom-176b-deepspeed, TP=8).
@@ -14,23 +16,30 @@ MII deployment of BLOOM-176B (bloom-176b-deepspeed, TP=8).
 from __future__ import annotations
 
 import torch
-import torch.distributed as dist
+
+
+def as_channel(ctrl):
+    """A control channel (``send``/``recv``) or a process group (gloo broadcast)."""
+    if getattr(ctrl, "kind", None) in ("shm", "gloo"):  # (a ProcessGroup has send/recv too)
+        return ctrl
+    from .ctrl_channel import GlooChannel
+    return GlooChannel(ctrl)
 
 
 class CollectiveRunner:
-    def __init__(self, runner, ctrl_group=None):
-        self.runner, self.group = runner, ctrl_group
+    def __init__(self, runner, ctrl=None):
+        self.runner = runner
+        self.chan = as_channel(ctrl)
 
     def __getattr__(self, k):
         return getattr(self.runner, k)
 
     def _send(self, msg):
-        obj = [msg]
-        dist.broadcast_object_list(obj, src=0, group=self.group)
+        self.chan.send(msg)
 
-    def prefill(self, ids, slots, lens=None):
-        self._send(("prefill", ids.tolist(), list(slots), lens))
-        out = self.runner.prefill(ids, slots, lens)
+    def prefill(self, ids, slots, lens=None, start=None):
+        self._send(("prefill", ids.to(torch.int32).numpy(), list(slots), lens, start))
+        out = self.runner.prefill(ids, slots, lens, start)
         _check_ar()
         return out
 
@@ -66,17 +75,17 @@ def _check_ar():
     check_all()
 
 
-def follower_loop(runner, ctrl_group=None):
+def follower_loop(runner, ctrl=None):
     """Ranks > 0: mirror rank 0's runner calls until it sends ``stop``."""
+    chan = as_channel(ctrl)
     last_logits = None
     while True:
-        obj = [None]
-        dist.broadcast_object_list(obj, src=0, group=ctrl_group)
+        obj = [chan.recv()]
         op = obj[0][0]
         if op == "stop":
             return
         if op == "prefill":
-            last_logits = runner.prefill(torch.tensor(obj[0][1], dtype=torch.long), obj[0][2], obj[0][3])
+            last_logits = runner.prefill(torch.from_numpy(obj[0][1]).long(), obj[0][2], obj[0][3], obj[0][4])
             _check_ar()
         elif op == "sample_first":
             runner.sample_first(last_logits, obj[0][1])

@@ -1,5 +1,6 @@
 """ctypes binding of the host-side native runtime ``_lib/libkca_host.so``
-(file and HTTP(S)/S3 weight streamers, host AdamW, BPE tokenizer / packer). Built by
+(file and HTTP(S)/S3 weight streamers, host AdamW, BPE tokenizer / packer, the
+TP control-plane shared-memory channel). Built by
 ``tools/build_ext.py`` with g++ (+ the HIP runtime for the device streamer)."""
 from __future__ import annotations
 
@@ -29,6 +30,12 @@ _SIGS = {
     "kca_packer_add": (None, [P, P, LL]),
     "kca_packer_write": (I, [P, ctypes.c_char_p, P]),
     "kca_packer_free": (None, [P]),
+    "kca_chan_create": (P, [ctypes.c_char_p, LL, LL, I]),
+    "kca_chan_open": (P, [ctypes.c_char_p, I]),
+    "kca_chan_send": (I, [P, P, LL, I]),
+    "kca_chan_recv": (LL, [P, I, P, LL, I, ctypes.POINTER(I)]),
+    "kca_chan_slot_bytes": (LL, [P]),
+    "kca_chan_close": (None, [P]),
 }
 
 

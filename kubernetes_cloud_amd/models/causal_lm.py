@@ -1,4 +1,5 @@
-"""Native decoder-only LM covering GPT-2, GPT-Neo(X)/Pythia, GPT-J and BLOOM.
+"""Native decoder-only LM covering GPT-2, GPT-Neo(X)/Pythia, GPT-J, BLOOM and
+XGLM / fairseq-dense (scaled embeddings + fixed sinusoidal positions, pre-LN).
 
 What the reference runs through HF ``AutoModelForCausalLM`` + DeepSpeed
 (finetuner-workflow/finetuner/finetuner.py:789-831 load, 469-493 loss) and the
@@ -67,6 +68,25 @@ def mask_to_kv(mask: torch.Tensor):
     if bool((m.long().sum(-1) == last).all()):
         return last.to(torch.int32)
     return m
+
+
+class SinusoidalPositions(nn.Module):
+    """fairseq / XGLM fixed positions: row p + offset of the tensor2tensor table
+    [sin(p w_i) | cos(p w_i)], w_i = 10000^(-i / (d/2 - 1)). Computed on the fly
+    in fp32 (no parameters, nothing to load or shard)."""
+
+    def __init__(self, d: int, offset: int):
+        super().__init__()
+        self.d, self.offset = d, offset
+
+    def forward(self, pos: torch.Tensor) -> torch.Tensor:
+        half = self.d // 2
+        w = torch.exp(torch.arange(half, device=pos.device, dtype=torch.float32) * -(math.log(10000.0) / (half - 1)))
+        a = (pos.to(torch.float32) + self.offset).unsqueeze(-1) * w
+        e = torch.cat([torch.sin(a), torch.cos(a)], dim=-1)
+        if self.d % 2:
+            e = F.pad(e, (0, 1))
+        return e
 
 
 class LayerNorm(nn.Module):
@@ -170,7 +190,10 @@ class CausalLM(nn.Module):
         self.cfg = cfg
         d = cfg.hidden
         self.wte = nn.Embedding(cfg.vocab_size, d)
-        self.wpe = nn.Embedding(cfg.max_pos, d) if cfg.learned_pos else None
+        if cfg.sinusoidal_pos:
+            self.wpe = SinusoidalPositions(d, cfg.pos_offset)
+        else:
+            self.wpe = nn.Embedding(cfg.max_pos, d) if cfg.learned_pos else None
         self.emb_ln = LayerNorm(d, cfg.ln_eps) if cfg.embed_ln else None
         self.h = nn.ModuleList([Block(cfg, i) for i in range(cfg.n_layers)])
         self.ln_f = LayerNorm(d, cfg.ln_eps)
@@ -264,15 +287,23 @@ class CausalLM(nn.Module):
         self.cfg.vocab_size = n
 
     # --------------------------------------------------------------- forward
-    def hidden_states(self, input_ids: torch.Tensor, attention_mask: torch.Tensor | None = None,
-                      position_ids: torch.Tensor | None = None, kv_len: torch.Tensor | None = None):
-        B, S = input_ids.shape
+    def embed(self, input_ids: torch.Tensor, pos: torch.Tensor | None = None) -> torch.Tensor:
+        """Token (+ position) embeddings (+ BLOOM's embedding LayerNorm); ``pos``
+        defaults to 0..S-1 (the training forward, a fresh prefill)."""
         h = self.wte(input_ids)
+        if self.cfg.embed_scale != 1.0:
+            h = h * self.cfg.embed_scale
         if self.wpe is not None:
-            pos = position_ids if position_ids is not None else torch.arange(S, device=input_ids.device)
-            h = h + self.wpe(pos)
+            if pos is None:
+                pos = torch.arange(input_ids.shape[-1], device=input_ids.device)
+            h = h + self.wpe(pos).to(h.dtype)
         if self.emb_ln is not None:
             h = self.emb_ln(h)
+        return h
+
+    def hidden_states(self, input_ids: torch.Tensor, attention_mask: torch.Tensor | None = None,
+                      position_ids: torch.Tensor | None = None, kv_len: torch.Tensor | None = None):
+        h = self.embed(input_ids, position_ids)
         if kv_len is None and attention_mask is not None:
             kv_len = mask_to_kv(attention_mask)
         if kv_len is not None:

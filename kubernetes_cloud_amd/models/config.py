@@ -2,7 +2,8 @@
 
 The reference finetunes any HF causal LM (GPT-2 / GPT-Neo / GPT-J / GPT-NeoX /
 Pythia; finetuner-workflow/finetuner/finetuner.py:808-822 via
-AutoModelForCausalLM) and serves BLOOM-176B (online-inference/bloom-176b/model/
+AutoModelForCausalLM; the workflow also names Fairseq dense models,
+finetune-workflow.yaml:22-27 -- HF ``model_type`` "xglm") and serves BLOOM-176B (online-inference/bloom-176b/model/
 bloom.py:13). We read the same HF config files so an unchanged model directory
 on the PVC works, and map them onto one native decoder implementation.
 """
@@ -10,12 +11,31 @@ from __future__ import annotations
 
 import dataclasses
 import json
+import math
 import os
+
+
+SUPPORTED_MODEL_TYPES = ("gpt2", "gpt_neo", "gptj", "gpt_neox", "bloom", "xglm")
+
+
+class UnsupportedModel(ValueError):
+    """A ``model_type`` outside the native families. The reference loads any
+    ``AutoModelForCausalLM`` (with ``--trust-remote-code`` for Hub code,
+    finetuner.py:795-822); this framework runs its own kernels, so remote model
+    code is never executed -- the error names what is supported."""
+
+    def __init__(self, model_type: str):
+        super().__init__(
+            f"unsupported model_type {model_type!r}: the MI355X-native model families are "
+            f"{', '.join(SUPPORTED_MODEL_TYPES)} (GPT-2, GPT-Neo, GPT-J, GPT-NeoX/Pythia, BLOOM, XGLM/fairseq-dense). "
+            "--trust-remote-code cannot add an architecture: remote modeling code is not executed; "
+            "convert the checkpoint to one of these families")
+        self.model_type = model_type
 
 
 @dataclasses.dataclass
 class LMConfig:
-    arch: str                      # gptj | gpt2 | gpt_neox | gpt_neo | bloom
+    arch: str                      # gptj | gpt2 | gpt_neox | gpt_neo | bloom | xglm
     vocab_size: int
     hidden: int
     n_layers: int
@@ -40,6 +60,9 @@ class LMConfig:
     ln_eps: float = 1e-5
     attn_scale: float | None = None   # None -> 1/sqrt(head_dim); GPT-Neo uses 1.0
     local_window: int = 0             # GPT-Neo local attention window
+    embed_scale: float = 1.0          # XGLM / fairseq-dense: token embeddings x sqrt(d_model)
+    sinusoidal_pos: bool = False      # XGLM / fairseq-dense: fixed sinusoidal positions
+    pos_offset: int = 0               # ... at position + 2 (fairseq padding_idx convention)
     attention_layers: tuple | None = None
     bos_token_id: int = 50256
     eos_token_id: int = 50256
@@ -135,7 +158,19 @@ class LMConfig:
                        ln_eps=cfg.get("layer_norm_epsilon", 1e-5),
                        bos_token_id=cfg.get("bos_token_id", 1), eos_token_id=cfg.get("eos_token_id", 2),
                        pad_token_id=cfg.get("pad_token_id", 3), hf=cfg)
-        raise ValueError(f"unsupported model_type {mt!r}")
+        if mt == "xglm":  # XGLM and the KoboldAI fairseq-dense conversions
+            d = cfg["d_model"]
+            act = cfg.get("activation_function", "gelu")
+            return cls(arch="xglm", vocab_size=cfg["vocab_size"], hidden=d, n_layers=cfg["num_layers"],
+                       n_heads=cfg["attention_heads"], ffn=cfg.get("ffn_dim", 4 * d),
+                       max_pos=cfg.get("max_position_embeddings", 2048), sinusoidal_pos=True, pos_offset=2,
+                       embed_scale=math.sqrt(d) if cfg.get("scale_embedding", True) else 1.0,
+                       qkv_bias=True, out_bias=True, mlp_bias=True,
+                       tie_embeddings=cfg.get("tie_word_embeddings", True),
+                       gelu_approx="none" if act == "gelu" else "tanh", ln_eps=1e-5,
+                       bos_token_id=cfg.get("bos_token_id", 0), eos_token_id=cfg.get("eos_token_id", 2),
+                       pad_token_id=cfg.get("pad_token_id", 1), hf=cfg)
+        raise UnsupportedModel(mt)
 
     @classmethod
     def from_pretrained(cls, path: str) -> "LMConfig":
@@ -176,6 +211,10 @@ PRESETS_HF: dict = {
     "bloom-176b": {"model_type": "bloom", "vocab_size": 250880, "hidden_size": 14336, "n_layer": 70,
                    "n_head": 112, "layer_norm_epsilon": 1e-5, "bos_token_id": 1, "eos_token_id": 2,
                    "pad_token_id": 3, "architectures": ["BloomForCausalLM"]},
+    "xglm-564m": {"model_type": "xglm", "vocab_size": 256008, "d_model": 1024, "num_layers": 24,
+                  "attention_heads": 16, "ffn_dim": 4096, "max_position_embeddings": 2048,
+                  "activation_function": "gelu", "scale_embedding": True, "bos_token_id": 0, "pad_token_id": 1,
+                  "eos_token_id": 2, "architectures": ["XGLMForCausalLM"]},
     "bloom-560m": {"model_type": "bloom", "vocab_size": 250880, "hidden_size": 1024, "n_layer": 24,
                    "n_head": 16, "layer_norm_epsilon": 1e-5, "bos_token_id": 1, "eos_token_id": 2,
                    "pad_token_id": 3, "architectures": ["BloomForCausalLM"]},

@@ -115,6 +115,24 @@ def hf_to_native_plan(cfg: LMConfig, get, sd_keys=()) -> dict:
             direct("lm_head.weight", "embed_out.weight" if "embed_out.weight" in sd_keys else "lm_head.weight")
         return plan
 
+    if a == "xglm":
+        direct("wte.weight", "embed_tokens.weight")
+        for i in range(cfg.n_layers):
+            s, p = f"layers.{i}.", f"h.{i}."
+            for nn_, hn in (("ln_1", "self_attn_layer_norm"), ("ln_2", "final_layer_norm")):
+                direct(p + nn_ + ".weight", s + hn + ".weight")
+                direct(p + nn_ + ".bias", s + hn + ".bias")
+            cat3(p + "attn.qkv.weight", s + "self_attn.{}_proj.weight")
+            cat3(p + "attn.qkv.bias", s + "self_attn.{}_proj.bias")
+            for nn_, hn in (("attn.out", "self_attn.out_proj"), ("mlp.fc_in", "fc1"), ("mlp.fc_out", "fc2")):
+                direct(p + nn_ + ".weight", s + hn + ".weight")
+                direct(p + nn_ + ".bias", s + hn + ".bias")
+        direct("ln_f.weight", "layer_norm.weight")
+        direct("ln_f.bias", "layer_norm.bias")
+        if not cfg.tie_embeddings:
+            direct("lm_head.weight", "lm_head.weight")
+        return plan
+
     if a == "bloom":
         direct("wte.weight", "word_embeddings.weight")
         direct("emb_ln.weight", "word_embeddings_layernorm.weight")
@@ -225,6 +243,25 @@ def native_to_hf(sd: dict, cfg: LMConfig) -> dict:
         if not cfg.tie_embeddings:
             out["embed_out.weight"] = sd["lm_head.weight"]
         return out
+    if a == "xglm":
+        out["model.embed_tokens.weight"] = sd["wte.weight"]
+        for i in range(cfg.n_layers):
+            p, t = f"h.{i}.", f"model.layers.{i}."
+            out[t + "self_attn_layer_norm.weight"] = sd[p + "ln_1.weight"]
+            out[t + "self_attn_layer_norm.bias"] = sd[p + "ln_1.bias"]
+            out[t + "final_layer_norm.weight"] = sd[p + "ln_2.weight"]
+            out[t + "final_layer_norm.bias"] = sd[p + "ln_2.bias"]
+            for n, w, b in zip(("q", "k", "v"), sd[p + "attn.qkv.weight"].split(d, 0), sd[p + "attn.qkv.bias"].split(d, 0)):
+                out[t + f"self_attn.{n}_proj.weight"] = w.contiguous()
+                out[t + f"self_attn.{n}_proj.bias"] = b.contiguous()
+            for nn_, hn in (("attn.out", "self_attn.out_proj"), ("mlp.fc_in", "fc1"), ("mlp.fc_out", "fc2")):
+                out[t + hn + ".weight"] = sd[p + nn_ + ".weight"]
+                out[t + hn + ".bias"] = sd[p + nn_ + ".bias"]
+        out["model.layer_norm.weight"] = sd["ln_f.weight"]
+        out["model.layer_norm.bias"] = sd["ln_f.bias"]
+        if not cfg.tie_embeddings:
+            out["lm_head.weight"] = sd["lm_head.weight"]
+        return out
     if a == "bloom":
         out["transformer.word_embeddings.weight"] = sd["wte.weight"]
         out["transformer.word_embeddings_layernorm.weight"] = sd["emb_ln.weight"]
@@ -250,7 +287,7 @@ def native_to_hf(sd: dict, cfg: LMConfig) -> dict:
 
 
 _IGNORED = re.compile(r"(\.attn\.bias|\.attn\.masked_bias|rotary_emb\.inv_freq|\.attention\.bias|"
-                      r"\.attention\.masked_bias)$")
+                      r"\.attention\.masked_bias|embed_positions\.weights)$")
 
 
 def is_ignorable_hf_key(k: str) -> bool:

@@ -39,6 +39,7 @@ class PipelineStage(nn.Module):
             self.wte = full.wte
             self.wpe = full.wpe
             self.emb_ln = full.emb_ln
+            self.embed_scale = full.cfg.embed_scale
         self.h = nn.ModuleList(list(full.h)[lo:hi])
         if last:
             self.ln_f = full.ln_f
@@ -49,10 +50,11 @@ class PipelineStage(nn.Module):
 
     def forward(self, x, labels=None):
         if self.first:
-            B, S = x.shape
             h = self.wte(x)
+            if self.embed_scale != 1.0:
+                h = h * self.embed_scale
             if self.wpe is not None:
-                h = h + self.wpe(torch.arange(S, device=x.device))
+                h = h + self.wpe(torch.arange(x.shape[1], device=x.device)).to(h.dtype)
             if self.emb_ln is not None:
                 h = self.emb_ln(h)
         else:

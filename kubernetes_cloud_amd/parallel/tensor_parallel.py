@@ -103,11 +103,14 @@ def gather_last_dim(x, group):
     return _gather_nograd(x, group)
 
 
+_AR_GATHER = os.environ.get("KCA_AR_GATHER", "1") not in ("0", "false")
+
+
 def _gather_nograd(x, group):
     world = dist.get_world_size(group)
     x = x.contiguous()
     from .custom_ar import lookup
-    ar = lookup(group)
+    ar = lookup(group) if _AR_GATHER else None
     if ar is not None and ar.eligible(x):  # decode logits: one sync round over xGMI peer memory, graph-capturable
         flat = ar.all_gather(x)  # [world, *x.shape] flattened
         return flat.view(world, *x.shape).movedim(0, -2).reshape(*x.shape[:-1], world * x.shape[-1])

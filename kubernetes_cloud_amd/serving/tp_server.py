@@ -78,6 +78,8 @@ def main(argv=None):
         from ..parallel.custom_ar import register
         register(None)
     runner = ModelRunner(model, max_slots=args.max_batch, max_len=args.max_len)
+    from ..engine.ctrl_channel import open_channel
+    ctrl = open_channel(ctrl)  # shared-memory ring on one node: no collective between decode steps
     if rank != 0:
         follower_loop(runner, ctrl)
         return

@@ -21,6 +21,7 @@ aligned LM-head/CE kernels), never shrunk.
 """
 from __future__ import annotations
 
+import copy
 import json
 import logging
 import math
@@ -104,6 +105,21 @@ def build_parser() -> DashParser:
     return p
 
 
+def resolve_model_dir(model: str, cache: str | None) -> str:
+    """A local directory as is; an ``org/name`` id from the HF hub cache under
+    ``cache`` (``models--org--name/snapshots/<rev>``, directly or in ``hub/``),
+    else unchanged (the caller's error then names it)."""
+    if os.path.isdir(model) or "/" not in model or model.startswith(("/", ".")):
+        return model
+    from ..serving.bloom_server import resolve_hf_cache_path
+    for root in ([cache, os.path.join(cache, "hub")] if cache else []) + [None]:
+        try:
+            return resolve_hf_cache_path(model, root)
+        except (FileNotFoundError, OSError, ValueError):
+            continue
+    return model
+
+
 def read_prompts(path: str) -> list[str]:
     """Prompt file: JSON list of strings, or one prompt per line."""
     with open(path) as f:
@@ -158,6 +174,12 @@ def main(argv=None):
     if main_proc:
         log.info(f"HOST: {host_info()}")
 
+    # --model: a directory, or an HF id resolved in the --cache hub cache (the reference passes
+    # cache_dir=args.cache to from_pretrained, finetuner.py:432,795)
+    args.model = resolve_model_dir(args.model, args.cache)
+    if args.trust_remote_code and main_proc:
+        log.info("--trust-remote-code: accepted for CLI compatibility; remote modeling code is never executed "
+                 "(models run on the native kernels; unsupported model_types fail with the list of families)")
     output_dir = os.path.abspath(os.path.join(args.output_path, "results-" + args.run_name))
     last = find_last_checkpoint(output_dir) if args.resume else None
     log.info(f"LAST CHECKPOINT: {last}")
@@ -310,10 +332,19 @@ def main(argv=None):
 
     def _sample(step):
         model.eval()
+        # --fp16-full-eval: sampling in 16-bit (bf16 on MI355X -- already the GPU weights' dtype; the fp32
+        # CPU path samples from a bf16 copy)
+        sm = model
+        if args.fp16_full_eval and next(model.parameters()).dtype == torch.float32:
+            sm = copy.deepcopy(model).to(torch.bfloat16)
+        _sample_prompts(step, sm)
+        model.train()
+
+    def _sample_prompts(step, sm):
         for pr in prompts:
             ids = torch.tensor([tokenizer.encode(pr)], device=dev)
             t0 = time.time()
-            res = generate(model, ids, GenerationConfig(
+            res = generate(sm, ids, GenerationConfig(
                 max_new_tokens=args.prompt_tokens, do_sample=True, top_k=args.top_k, top_p=args.top_p,
                 temperature=args.temperature, repetition_penalty=args.repetition_penalty,
                 num_return_sequences=args.prompt_samples, eos_token_id=eos_id, pad_token_id=pad_id,
@@ -322,7 +353,6 @@ def main(argv=None):
                 log.info(f"STEP {step} PROMPT: {pr}  INFERENCE TIME: {time.time() - t0:.2f}s")
                 for s in res.sequences:
                     log.info(f"RESPONSE: {tokenizer.decode(s.tolist(), skip_special_tokens=False)}")
-        model.train()
 
     step = state["global_step"]
     start_epoch = step // steps_per_epoch

@@ -248,3 +248,55 @@ def test_beam_search_paged_equals_contiguous(page_size):
     assert res.sequences == ref.sequences
     if page_size:
         assert eng.runner.cache.free_count() == eng.runner.cache.n_pages
+
+
+@pytest.mark.parametrize("preset,page", [("gpt-j-6b", 16), ("gpt2", 0), ("bloom-560m", 16), ("pythia-2.8b", 16)])
+def test_chunked_prefill_bounds_the_gap_and_matches(preset, page):
+    """a long prompt admitted while a stream decodes is
+    prefilled in chunks of <= prefill_chunk tokens; the running stream gets a
+    token every step throughout, and every output equals the unchunked run."""
+    m = tiny(preset)
+    g = torch.Generator().manual_seed(3)
+    short = torch.randint(0, 97, (5,), generator=g).tolist()
+    long = torch.randint(0, 97, (45,), generator=g).tolist()
+    sp_run = SamplingParams(max_new_tokens=14, do_sample=False)
+    sp_long = SamplingParams(max_new_tokens=6, do_sample=False)
+    eng = LLMEngine(m, max_slots=4, max_len=64, page_size=page, prefill_chunk=8)
+    r1 = eng.add_request(short, sp_run)
+    eng.step()
+    eng.step()
+    r2 = eng.add_request(long, sp_long)
+    counts = []
+    while not r2.output and not r1.done:
+        before = len(r1.output)
+        eng.step()
+        counts.append(len(r1.output) - before)
+    assert len(counts) >= 45 // 8  # the 45-token prompt took several steps
+    assert all(c == 1 for c in counts), counts  # ... and the running stream never skipped a step
+    assert eng.stats["prefill_chunks"] >= 5
+    assert eng.stats["max_step_prefill_tokens"] <= 8 or eng.stats["steps"] <= 1
+    eng.run_until_done([r1, r2])
+    assert r1.output == greedy_recompute(m, short, 14)
+    assert r2.output == greedy_recompute(m, long, 6)
+    ref = LLMEngine(m, max_slots=4, max_len=64, page_size=page).generate([long], sp_long)[0]
+    assert r2.output == ref.output
+
+
+def test_chunked_prefill_window_model():
+    """GPT-Neo local layers: a continued chunk sees only the last `window` keys."""
+    cfg = dict(PRESETS_HF.get("gpt-neo-125m", {}) or {})
+    if not cfg:
+        cfg = {"model_type": "gpt_neo", "vocab_size": 97, "hidden_size": 64, "num_layers": 2, "num_heads": 4,
+               "attention_types": [[["global", "local"], 1]], "window_size": 8, "max_position_embeddings": 64}
+    m = build_model(LMConfig.from_hf(cfg), dtype=torch.float32, seed=0)
+    g = torch.Generator().manual_seed(5)
+    short = torch.randint(0, 97, (4,), generator=g).tolist()
+    long = torch.randint(0, 97, (30,), generator=g).tolist()
+    eng = LLMEngine(m, max_slots=4, max_len=64, prefill_chunk=7)
+    r1 = eng.add_request(short, SamplingParams(max_new_tokens=12, do_sample=False))
+    eng.step()
+    r2 = eng.add_request(long, SamplingParams(max_new_tokens=5, do_sample=False))
+    eng.run_until_done([r1, r2])
+    assert eng.stats["prefill_chunks"] >= 4
+    assert r1.output == greedy_recompute(m, short, 12)
+    assert r2.output == greedy_recompute(m, long, 5)

@@ -252,3 +252,42 @@ def test_checkpoint_complete_markers(tmp_path):
     assert checkpoint_complete(str(tmp_path / "checkpoint-2"))
     assert not checkpoint_complete(str(tmp_path / "checkpoint-4"))
     assert find_last_checkpoint(str(tmp_path)).endswith("checkpoint-2")
+
+
+def test_finetuner_xglm_from_hf_cache_id(tmp_path):
+    """a Fairseq-dense / XGLM model (finetune-workflow.yaml:22-27) given as an HF id,
+    resolved in the --cache hub cache (models--org--name/snapshots/<rev>), finetuned with
+    --fp16-full-eval sampling and --trust-remote-code accepted; the final dir loads in transformers."""
+    from transformers import AutoModelForCausalLM
+    snap = tmp_path / "cache" / "models--KoboldAI--fairseq-dense-tiny" / "snapshots" / "abc123"
+    (tmp_path / "cache" / "models--KoboldAI--fairseq-dense-tiny" / "refs").mkdir(parents=True)
+    (tmp_path / "cache" / "models--KoboldAI--fairseq-dense-tiny" / "refs" / "main").write_text("abc123")
+    make_model_dir(str(snap), preset="xglm-564m", d_model=64, num_layers=2, attention_heads=4, ffn_dim=128,
+                   max_position_embeddings=64)
+    data = make_tokens(str(tmp_path / "d.tokens"), n_ctx=8, ctx=16)
+    prompts = tmp_path / "p.txt"
+    prompts.write_text("the quick\n")
+    st = _run(["--run-name", "xg", "--model", "KoboldAI/fairseq-dense-tiny", "--cache", str(tmp_path / "cache"),
+               "--dataset", data, "--context-size", "16", "--bs", "2", "--gradients", "1",
+               "--output-path", str(tmp_path / "o"), "--logs", str(tmp_path / "l"), "--save-steps", "0",
+               "--max-steps", "2", "--trust-remote-code", "--fp16-full-eval", "--prompt-file", str(prompts),
+               "--prompt-every", "1", "--prompt-tokens", "3", "--prompt-samples", "1"])
+    assert st["global_step"] == 2
+    final = tmp_path / "o" / "results-xg" / "final"
+    hm = AutoModelForCausalLM.from_pretrained(str(final))
+    assert type(hm).__name__ == "XGLMForCausalLM"
+
+
+def test_finetuner_unsupported_model_type_is_explicit(tmp_path):
+    import json as _json
+
+    import pytest as _pytest
+
+    from kubernetes_cloud_amd.models.config import UnsupportedModel
+    d = tmp_path / "llama"
+    d.mkdir()
+    (d / "config.json").write_text(_json.dumps({"model_type": "llama", "hidden_size": 64}))
+    data = make_tokens(str(tmp_path / "d.tokens"), n_ctx=4, ctx=16)
+    with _pytest.raises(UnsupportedModel, match="trust-remote-code"):
+        _run(["--run-name", "x", "--model", str(d), "--dataset", data, "--context-size", "16", "--bs", "2",
+              "--output-path", str(tmp_path / "o"), "--logs", str(tmp_path / "l"), "--trust-remote-code"])

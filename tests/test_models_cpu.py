@@ -14,7 +14,7 @@ transformers = pytest.importorskip("transformers")
 
 def _cases():
     from transformers import (BloomConfig, BloomForCausalLM, GPT2Config, GPT2LMHeadModel, GPTJConfig,
-                              GPTJForCausalLM, GPTNeoXConfig, GPTNeoXForCausalLM)
+                              GPTJForCausalLM, GPTNeoXConfig, GPTNeoXForCausalLM, XGLMConfig, XGLMForCausalLM)
     return [
         ("gptj", GPTJConfig(vocab_size=300, n_embd=64, n_layer=2, n_head=4, rotary_dim=8, n_positions=64,
                             bos_token_id=0, eos_token_id=0), GPTJForCausalLM),
@@ -24,10 +24,14 @@ def _cases():
                                    intermediate_size=128, rotary_pct=0.25, max_position_embeddings=64),
          GPTNeoXForCausalLM),
         ("bloom", BloomConfig(vocab_size=300, hidden_size=64, n_layer=2, n_head=4), BloomForCausalLM),
+        # XGLM / fairseq-dense (finetune-workflow.yaml:22-27 names Fairseq models): scaled embeddings,
+        # sinusoidal positions at +2, pre-LN, exact GELU, tied head
+        ("xglm", XGLMConfig(vocab_size=300, d_model=64, num_layers=2, attention_heads=4, ffn_dim=128,
+                            max_position_embeddings=64, dropout=0.0, attention_dropout=0.0), XGLMForCausalLM),
     ]
 
 
-@pytest.mark.parametrize("idx", range(4))
+@pytest.mark.parametrize("idx", range(5))
 def test_logits_match_hf(idx):
     torch.manual_seed(idx)
     name, hcfg, cls = _cases()[idx]
@@ -107,3 +111,29 @@ def test_sharded_save(tmp_path):
     ids = torch.randint(0, 300, (1, 8))
     with torch.no_grad():
         assert torch.allclose(m(ids), m2(ids))
+
+
+def test_xglm_engine_decode_matches_recompute():
+    """The serving engine (prefill + KV-cache decode at positions 0..n) on an
+    XGLM model equals greedy full recompute: the sinusoidal positions of the
+    decode step line up with the training forward's."""
+    from kubernetes_cloud_amd.engine.llm_engine import LLMEngine, SamplingParams
+    from kubernetes_cloud_amd.models.config import PRESETS_HF
+    cfg = dict(PRESETS_HF["xglm-564m"])
+    cfg.update(vocab_size=97, d_model=64, num_layers=2, attention_heads=4, ffn_dim=128, max_position_embeddings=64)
+    m = build_model(LMConfig.from_hf(cfg), dtype=torch.float32, seed=0)
+    prompt = [5, 9, 17, 3, 44]
+    out = LLMEngine(m, max_slots=2, max_len=48).generate([prompt], SamplingParams(max_new_tokens=8, do_sample=False))
+    ids = list(prompt)
+    for _ in range(8):
+        with torch.no_grad():
+            ids.append(int(m(torch.tensor([ids]))[0, -1].argmax()))
+    assert out[0].output == ids[len(prompt):]
+
+
+def test_unsupported_model_type_names_the_families():
+    from kubernetes_cloud_amd.models.config import UnsupportedModel
+    with pytest.raises(UnsupportedModel) as e:
+        LMConfig.from_hf({"model_type": "llama", "hidden_size": 64})
+    msg = str(e.value)
+    assert "llama" in msg and "gptj" in msg and "xglm" in msg and "trust-remote-code" in msg

@@ -120,7 +120,9 @@ def _close(a, b):
     reduction order agree on all but a few elements; a wrong or missing
     gradient reduction moves a large fraction of them the other way."""
     d = (a - b).abs()
-    return float(d.mean()), float((d > 5e-3).float().mean())
+    # one bf16 ulp is 7.8e-3 at 1.0 (LayerNorm weights): the bound scales with |b|; a wrong
+    # update moves a ~0.02 weight by 2 x lr = 2e-2
+    return float(d.mean()), float((d > 4e-3 + 1e-2 * b.abs()).float().mean())
 
 
 def test_zero_stages_world2_on_gpu_match(tmp_path):

@@ -65,11 +65,20 @@ def _worker(rank, world, port, preset, model_dir, q):
             model_dir, dtype=torch.float32), rank, world)
         res["load"] = max(float((a - b).abs().max()) for a, b in zip(lm.state_dict().values(),
                                                                     ref.state_dict().values()))
-    # lock-stepped TP engine
+    # lock-stepped TP engine; control plane over the shared-memory ring: no gloo call after setup
+    from kubernetes_cloud_amd.engine.ctrl_channel import open_channel
     ctrl = dist.new_group(backend="gloo")
     runner = ModelRunner(tp, max_slots=4, max_len=48)
+    chan = open_channel(ctrl)
+    calls = {"n": 0}
+    orig = dist.broadcast_object_list
+
+    def counting(*a, **k):
+        calls["n"] += 1
+        return orig(*a, **k)
+    dist.broadcast_object_list = counting
     if rank == 0:
-        eng = LLMEngine(tp, runner=CollectiveRunner(runner, ctrl))
+        eng = LLMEngine(tp, runner=CollectiveRunner(runner, chan))
         reqs = eng.generate([[1, 2, 3], [7, 8, 9, 10, 11]], SamplingParams(max_new_tokens=6, do_sample=False))
         res["gen"] = [r.output for r in reqs]
         # beam search under TP: decode_topk / copy_slots / release mirrored to the follower
@@ -80,10 +89,15 @@ def _worker(rank, world, port, preset, model_dir, q):
                                                           SamplingParams(max_new_tokens=6, do_sample=False))]
         res["beam_ref"] = ref_eng.beam_generate(list(range(1, 18)), num_beams=3, max_new_tokens=8,
                                                 n_return=3).sequences
+        res["chan"] = chan.kind
+        res["bcasts0"] = calls["n"]
         q.put(res)
     else:
-        follower_loop(runner, ctrl)
+        follower_loop(runner, chan)
+        q.put({"bcasts1": calls["n"]})
+    dist.broadcast_object_list = orig
     dist.barrier()
+    chan.close()
     dist.destroy_process_group()
 
 
@@ -102,6 +116,7 @@ def test_tp2_matches_unsharded(preset, tmp_path):
     for p in procs:
         p.start()
     res = q.get(timeout=300)
+    res.update(q.get(timeout=120))
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -111,3 +126,4 @@ def test_tp2_matches_unsharded(preset, tmp_path):
         assert res["load"] == 0.0
     assert res["gen"] == res["ref"]
     assert res["beam"] == res["beam_ref"]
+    assert res["chan"] == "shm" and res["bcasts0"] == 0 and res["bcasts1"] == 0, res

@@ -5,7 +5,8 @@
   --offload-arch=gfx950`` (CDNA4 only; no other targets, no hipify step).
 * ``libkca_host.so``    -- host-side C++ runtime pieces (``csrc/cpu``,
   ``csrc/io``, ``csrc/tokenize``): AVX-512/AVX2 AdamW for offload, the
-  ``.tensors`` weight streamer and the BPE tokenizer / context packer.
+  ``.tensors`` weight streamer, the BPE tokenizer / context packer and the
+  shared-memory control channel of the TP serving engine (``csrc/runtime``).
 
 Both are plain C-ABI shared objects loaded with ctypes *after* ``import
 torch`` so that the HIP runtime torch already mapped (soname
@@ -99,12 +100,12 @@ def build_kernels(jobs: int = 8, verbose: bool = False, debug: bool = False, sta
 
 def build_host(jobs: int = 8, verbose: bool = False) -> str | None:
     srcs = []
-    for sub in ("cpu", "io", "tokenize"):
+    for sub in ("cpu", "io", "tokenize", "runtime"):
         srcs += _sources(sub, (".cpp",))
     if not srcs:
         return None
     hdrs = []
-    for sub in ("cpu", "io", "tokenize"):
+    for sub in ("cpu", "io", "tokenize", "runtime"):
         hdrs += _sources(sub, (".h",))
     obj_dir = os.path.join(BUILD, "host")
     os.makedirs(obj_dir, exist_ok=True)
@@ -135,7 +136,7 @@ def build_sanitize(verbose: bool = False) -> str:
     parses untrusted files / network bytes, instrumented as a standalone binary
     so no sanitizer runtime has to be preloaded into Python."""
     srcs = []
-    for sub in ("cpu", "io", "tokenize", "tests"):
+    for sub in ("cpu", "io", "tokenize", "runtime", "tests"):
         srcs += _sources(sub, (".cpp",))
     out_dir = os.path.join(BUILD, "sanitize")
     os.makedirs(out_dir, exist_ok=True)
