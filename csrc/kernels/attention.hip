@@ -35,7 +35,10 @@
 // Layouts: q/k/v/o/do/dq/dk/dv are [B, S, H, D] views with arbitrary batch,
 // token and head strides (so the fused QKV GEMM output is consumed in place);
 // lse / delta are [B, H, Sq] fp32. Supports causal (bottom-right aligned,
-// offset = Sk - Sq), per-batch key lengths (right padding), ALiBi and GQA.
+// offset = Sk - Sq), per-batch key lengths (right padding), ALiBi, GQA, a
+// sliding window (GPT-Neo local layers: tiles left of the band are skipped,
+// not masked) and a per-key bitmap for masks with holes (the interior EOS
+// separators of a pad == eos context, finetuner.py:674-691).
 // Head dims are padded to a compiled D in {64, 96, 128, 160, 256}; the real
 // head dim (a multiple of 8) is masked on load/store.
 #include "common.h"
@@ -53,6 +56,9 @@ struct AttnParams {
   const float* alibi;  // [H] slopes or null
   const int* kv_len;   // [B] or null
   const int* fix_flags;  // fixup mode: run only blocks whose tiled-path wave flags are set
+  int window;                 // > 0: key visible only if key > q + off - window (GPT-Neo local layers)
+  const unsigned* key_mask;   // [B, km_words] bitmap of attended keys (masks with holes) or null
+  int km_words;
 };
 
 struct AttnBwdParams {
@@ -66,6 +72,9 @@ struct AttnBwdParams {
   float scale;
   const float* alibi;
   const int* kv_len;
+  int window;
+  const unsigned* key_mask;
+  int km_words;
 };
 
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
@@ -152,6 +161,11 @@ struct Stager {
   }
 };
 
+// bit `key` of batch row b of the attended-key bitmap (caller guarantees key < Sk)
+__device__ __forceinline__ bool km_bit(const unsigned* km, int words, int b, int key) {
+  return (km[(long long)b * words + (key >> 5)] >> (key & 31)) & 1u;
+}
+
 // Deferred-rescale threshold (log2 units): O / l are rescaled only when a row's
 // running max grows by more than this, so P <= 2^8 between rescales (T13).
 #define RESCALE_THR 8.0f
@@ -186,6 +200,8 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_kernel(AttnP
   int kv_hi = kv_end;
   if (CAUSAL) kv_hi = min(kv_hi, qb * BM + BM - 1 + off + 1);
   const int ntiles = kv_hi > 0 ? (kv_hi + BN - 1) / BN : 0;
+  // sliding window: tiles wholly left of the workgroup's band are never loaded
+  const int t0 = p.window > 0 ? min(ntiles, max(0, qb * BM + off - p.window + 1) / BN) : 0;
   const bool dfull = p.d_real == D;
 
   const float sl2 = p.scale * LOG2E;
@@ -210,18 +226,19 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_kernel(AttnP
   float m = -INFINITY, lsum = 0.f;
 
   Stager<D, BN, 256> sk, sv;
-  if (ntiles > 0) {
-    const bool full = dfull && BN <= p.Sk;
-    sk.load(kp, p.k_st, 0, p.Sk, p.d_real, full);
-    sv.load(vp, p.v_st, 0, p.Sk, p.d_real, full);
-    sk.store(smem, L::KSTR);
-    sv.store(smem + KSZ, L::VSTR);
+  if (ntiles > t0) {
+    const bool full = dfull && (t0 + 1) * BN <= p.Sk;
+    sk.load(kp, p.k_st, t0 * BN, p.Sk, p.d_real, full);
+    sv.load(vp, p.v_st, t0 * BN, p.Sk, p.d_real, full);
+    sk.store(smem + (t0 & 1) * (KSZ + VSZ), L::KSTR);
+    sv.store(smem + (t0 & 1) * (KSZ + VSZ) + KSZ, L::VSTR);
   }
   __syncthreads();
 
   const int gi = lane & 15;
   const int dcol = 16 * ((lane >> 4) & 1) + 4 * (gi & 3);
-  for (int t = 0; t < ntiles; ++t) {
+  const int wlo = q0 + off - p.window + 1;  // window: first key visible to the wave's first row
+  for (int t = t0; t < ntiles; ++t) {
     const int k0 = t * BN;
     const bf16_t* Ks = smem + (t & 1) * (KSZ + VSZ);
     const bf16_t* Vs = Ks + KSZ;
@@ -230,7 +247,7 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_kernel(AttnP
       sk.load(kp, p.k_st, k0 + BN, p.Sk, p.d_real, full);
       sv.load(vp, p.v_st, k0 + BN, p.Sk, p.d_real, full);
     }
-    const bool active = !CAUSAL || (k0 <= q0 + BN - 1 + off);
+    const bool active = (!CAUSAL || (k0 <= q0 + BN - 1 + off)) && (p.window <= 0 || k0 + BN - 1 >= wlo);
     if (active) {
       f32x16 sacc;
 #pragma unroll
@@ -240,7 +257,8 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_kernel(AttnP
         bf16x8 a = ld_bf16x8(Ks + l32 * L::KSTR + 16 * s + 8 * hh);
         sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s], sacc, 0, 0, 0);
       }
-      const bool need_mask = (CAUSAL && (k0 + BN - 1 > q0 + off)) || (k0 + BN > kv_end);
+      const bool need_mask = (CAUSAL && (k0 + BN - 1 > q0 + off)) || (k0 + BN > kv_end) ||
+                             (p.window > 0 && k0 < wlo + BN - 1) || p.key_mask;
       float x[16];
       float mt = -INFINITY;
       if (need_mask || p.alibi) {
@@ -249,6 +267,8 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_kernel(AttnP
           const int key = k0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
           bool valid = key < kv_end;
           if (CAUSAL) valid = valid && (key <= qrow + off);
+          if (p.window > 0) valid = valid && (key > qrow + off - p.window);
+          if (p.key_mask) valid = valid && km_bit(p.key_mask, p.km_words, b, key);
           float v = sacc[r] * sl2;
           if (p.alibi) v += slope * (float)(key - qrow - off);
           x[r] = valid ? v : -INFINITY;
@@ -399,8 +419,11 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_bwd_dkdv_kernel(
 
   int q_lo = 0;
   if (CAUSAL) q_lo = max(0, kb * BK - off) & ~(BQ - 1);
-  const int nqt = p.Sq > q_lo ? (p.Sq - q_lo + BQ - 1) / BQ : 0;
+  // window: queries past the last key's band see none of this block's keys
+  const int q_end = p.window > 0 ? min(p.Sq, kb * BK + BK - 1 - off + p.window) : p.Sq;
+  const int nqt = q_end > q_lo ? (q_end - q_lo + BQ - 1) / BQ : 0;
   const int total = (kb * BK < kv_end) ? nqt * grp : 0;
+  const bool key_ok = key < kv_end && (!p.key_mask || km_bit(p.key_mask, p.km_words, b, key));
 
   Stager<D, BQ, 256> sq, sd;
   float lse_r = INFINITY, dl_r = 0.f;
@@ -459,7 +482,7 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_bwd_dkdv_kernel(
         }
       }
       const bool need_mask = (CAUSAL && (kw + 15 > qt + off)) || (kw + 16 > kv_end) ||
-                             (qt + BQ > p.Sq);
+                             (qt + BQ > p.Sq) || p.window > 0 || p.key_mask;
       const float slope = p.alibi ? p.alibi[hq] * LOG2E : 0.f;
       float pv[8], dsv[8];
 #pragma unroll
@@ -472,8 +495,9 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_bwd_dkdv_kernel(
           if (p.alibi) x += slope * (float)(key - q - off);
           float pr = exp2f(x);
           if (need_mask) {
-            bool valid = q < p.Sq && key < kv_end;
+            bool valid = q < p.Sq && key_ok;
             if (CAUSAL) valid = valid && (key <= q + off);
+            if (p.window > 0) valid = valid && (key > q + off - p.window);
             pr = valid ? pr : 0.f;
           }
           pv[j * 4 + r] = pr;
@@ -561,20 +585,22 @@ __global__ void __launch_bounds__(256, (D <= 160 ? 2 : 1)) attn_bwd_dq_kernel(At
   int kv_hi = kv_end;
   if (CAUSAL) kv_hi = min(kv_hi, qb * BQ + BQ - 1 + off + 1);
   const int ntiles = kv_hi > 0 ? (kv_hi + BN - 1) / BN : 0;
+  const int t0 = p.window > 0 ? min(ntiles, max(0, qb * BQ + off - p.window + 1) / BN) : 0;
+  const int wlo = qw + off - p.window + 1;
   const bf16_t* kp = p.k + b * p.k_sb + hk * p.k_sh;
   const bf16_t* vp = p.v + b * p.v_sb + hk * p.v_sh;
   Stager<D, BN, 256> sk, sv;
-  if (ntiles > 0) {
-    const bool full = dfull && BN <= p.Sk;
-    sk.load(kp, p.k_st, 0, p.Sk, p.d_real, full);
-    sv.load(vp, p.v_st, 0, p.Sk, p.d_real, full);
-    sk.store(smem, L::STR);
-    sv.store(smem + TSZ, L::STR);
+  if (ntiles > t0) {
+    const bool full = dfull && (t0 + 1) * BN <= p.Sk;
+    sk.load(kp, p.k_st, t0 * BN, p.Sk, p.d_real, full);
+    sv.load(vp, p.v_st, t0 * BN, p.Sk, p.d_real, full);
+    sk.store(smem + (t0 & 1) * 2 * TSZ, L::STR);
+    sv.store(smem + (t0 & 1) * 2 * TSZ + TSZ, L::STR);
   }
   __syncthreads();
   const int trow = 4 * G + (gi >> 2);
   const int tcol = 4 * (gi & 3);
-  for (int t = 0; t < ntiles; ++t) {
+  for (int t = t0; t < ntiles; ++t) {
     const int k0 = t * BN;
     const bf16_t* Ks = smem + (t & 1) * 2 * TSZ;
     const bf16_t* Vs = Ks + TSZ;
@@ -583,7 +609,7 @@ __global__ void __launch_bounds__(256, (D <= 160 ? 2 : 1)) attn_bwd_dq_kernel(At
       sk.load(kp, p.k_st, k0 + BN, p.Sk, p.d_real, full);
       sv.load(vp, p.v_st, k0 + BN, p.Sk, p.d_real, full);
     }
-    const bool active = !CAUSAL || (k0 <= qw + 15 + off);
+    const bool active = (!CAUSAL || (k0 <= qw + 15 + off)) && (p.window <= 0 || k0 + BN - 1 >= wlo);
     if (active) {
       f32x4 st[2], dpt[2];
 #pragma unroll
@@ -600,7 +626,7 @@ __global__ void __launch_bounds__(256, (D <= 160 ? 2 : 1)) attn_bwd_dq_kernel(At
         }
       }
       const bool need_mask = (CAUSAL && (k0 + BN - 1 > qw + off)) || (k0 + BN > kv_end) ||
-                             (qw + 16 > p.Sq);
+                             (qw + 16 > p.Sq) || (p.window > 0 && k0 < wlo + 15) || p.key_mask;
       float dsv[8];
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -613,6 +639,8 @@ __global__ void __launch_bounds__(256, (D <= 160 ? 2 : 1)) attn_bwd_dq_kernel(At
           if (need_mask) {
             bool valid = q < p.Sq && key < kv_end;
             if (CAUSAL) valid = valid && (key <= q + off);
+            if (p.window > 0) valid = valid && (key > q + off - p.window);
+            if (p.key_mask) valid = valid && km_bit(p.key_mask, p.km_words, b, key);
             pr = valid ? pr : 0.f;
           }
           dsv[j * 4 + r] = pr * (dpt[j][r] - dl_q);
@@ -724,8 +752,10 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv32_kernel(AttnBwdParams p
 
   int q_lo = 0;
   if (CAUSAL) q_lo = max(0, kb * BK - off) & ~(BQ - 1);
-  const int nqt = p.Sq > q_lo ? (p.Sq - q_lo + BQ - 1) / BQ : 0;
+  const int q_end = p.window > 0 ? min(p.Sq, kb * BK + BK - 1 - off + p.window) : p.Sq;
+  const int nqt = q_end > q_lo ? (q_end - q_lo + BQ - 1) / BQ : 0;
   const int total = (kb * BK < kv_end) ? nqt * grp : 0;
+  const bool key_ok = key < kv_end && (!p.key_mask || km_bit(p.key_mask, p.km_words, b, key));
 
   Stager<D, BQ, 256> sq, sd;
   float lse_r = INFINITY, dl_r = 0.f;
@@ -776,7 +806,8 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv32_kernel(AttnBwdParams p
         sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld_bf16x8(Qs + o), kf[s], sacc, 0, 0, 0);
         dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld_bf16x8(Ds + o), vf[s], dpacc, 0, 0, 0);
       }
-      const bool need_mask = (CAUSAL && (kw + 31 > qt + off)) || (kw + 32 > kv_end) || (qt + BQ > p.Sq);
+      const bool need_mask = (CAUSAL && (kw + 31 > qt + off)) || (kw + 32 > kv_end) || (qt + BQ > p.Sq) ||
+                             p.window > 0 || p.key_mask;
       const float slope = p.alibi ? p.alibi[hq] * LOG2E : 0.f;
       float pv[16], dsv[16];
 #pragma unroll
@@ -787,8 +818,9 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv32_kernel(AttnBwdParams p
         if (p.alibi) x += slope * (float)(key - q - off);
         float pr = exp2f(x);
         if (need_mask) {
-          bool valid = q < p.Sq && key < kv_end;
+          bool valid = q < p.Sq && key_ok;
           if (CAUSAL) valid = valid && (key <= q + off);
+          if (p.window > 0) valid = valid && (key > q + off - p.window);
           pr = valid ? pr : 0.f;
         }
         pv[r] = pr;
@@ -879,18 +911,20 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq32_kernel(AttnBwdParams p) 
   int kv_hi = kv_end;
   if (CAUSAL) kv_hi = min(kv_hi, qb * BQ + BQ - 1 + off + 1);
   const int ntiles = kv_hi > 0 ? (kv_hi + BN - 1) / BN : 0;
+  const int t0 = p.window > 0 ? min(ntiles, max(0, qb * BQ + off - p.window + 1) / BN) : 0;
+  const int wlo = qw + off - p.window + 1;
   const bf16_t* kp = p.k + b * p.k_sb + hk * p.k_sh;
   const bf16_t* vp = p.v + b * p.v_sb + hk * p.v_sh;
   Stager<D, BN, 256> sk, sv;
-  if (ntiles > 0) {
-    const bool full = dfull && BN <= p.Sk;
-    sk.load(kp, p.k_st, 0, p.Sk, p.d_real, full);
-    sv.load(vp, p.v_st, 0, p.Sk, p.d_real, full);
-    store_swz(sk, smem);
-    store_swz(sv, smem + TSZ);
+  if (ntiles > t0) {
+    const bool full = dfull && (t0 + 1) * BN <= p.Sk;
+    sk.load(kp, p.k_st, t0 * BN, p.Sk, p.d_real, full);
+    sv.load(vp, p.v_st, t0 * BN, p.Sk, p.d_real, full);
+    store_swz(sk, smem + (t0 & 1) * 2 * TSZ);
+    store_swz(sv, smem + (t0 & 1) * 2 * TSZ + TSZ);
   }
   __syncthreads();
-  for (int t = 0; t < ntiles; ++t) {
+  for (int t = t0; t < ntiles; ++t) {
     const int k0 = t * BN;
     const bf16_t* Ks = smem + (t & 1) * 2 * TSZ;
     const bf16_t* Vs = Ks + TSZ;
@@ -899,7 +933,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq32_kernel(AttnBwdParams p) 
       sk.load(kp, p.k_st, k0 + BN, p.Sk, p.d_real, full);
       sv.load(vp, p.v_st, k0 + BN, p.Sk, p.d_real, full);
     }
-    const bool active = !CAUSAL || (k0 <= qw + 31 + off);
+    const bool active = (!CAUSAL || (k0 <= qw + 31 + off)) && (p.window <= 0 || k0 + BN - 1 >= wlo);
     if (active) {
       f32x16 st, dpt;
 #pragma unroll
@@ -910,7 +944,8 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq32_kernel(AttnBwdParams p) 
         st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld_bf16x8(Ks + o), qf[s], st, 0, 0, 0);
         dpt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld_bf16x8(Vs + o), gf[s], dpt, 0, 0, 0);
       }
-      const bool need_mask = (CAUSAL && (k0 + BN - 1 > qw + off)) || (k0 + BN > kv_end) || (qw + 32 > p.Sq);
+      const bool need_mask = (CAUSAL && (k0 + BN - 1 > qw + off)) || (k0 + BN > kv_end) || (qw + 32 > p.Sq) ||
+                             (p.window > 0 && k0 < wlo + 31) || p.key_mask;
       float dsv[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -921,6 +956,8 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq32_kernel(AttnBwdParams p) 
         if (need_mask) {
           bool valid = q < p.Sq && key < kv_end;
           if (CAUSAL) valid = valid && (key <= q + off);
+          if (p.window > 0) valid = valid && (key > q + off - p.window);
+          if (p.key_mask) valid = valid && km_bit(p.key_mask, p.km_words, b, key);
           pr = valid ? pr : 0.f;
         }
         dsv[r] = pr * (dpt[r] - dl_q);
@@ -1003,14 +1040,15 @@ KCA_API int kca_attn_fwd(const void* q, const void* k, const void* v, void* o,
                          long long v_sh, long long o_sb, long long o_st,
                          long long o_sh, int B, int Sq, int Sk, int H, int Hkv,
                          int d_real, int causal, float scale,
-                         const float* alibi, const int* kv_len, int* workspace,
-                         hipStream_t stream) {
-  if (d_real % 8 || H % Hkv) return 1;
+                         const float* alibi, const int* kv_len, int window, const unsigned* key_mask,
+                         int* workspace, hipStream_t stream) {
+  if (d_real % 8 || H % Hkv || window < 0) return 1;
   const int D = pick_d(d_real);
   AttnParams p{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, lse,
                q_sb, q_st, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh, o_sb, o_st, o_sh,
-               B, Sq, Sk, H, Hkv, d_real, causal, scale, alibi, kv_len, nullptr};
-  if (g_attn_tiled && workspace && !alibi && !kv_len &&
+               B, Sq, Sk, H, Hkv, d_real, causal, scale, alibi, kv_len, nullptr,
+               window, key_mask, (Sk + 31) / 32};
+  if (g_attn_tiled && workspace && !alibi && !kv_len && !window && !key_mask &&
       kca_attn_fwd_tiled(q, k, v, o, lse, q_sb, q_st, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh,
                          o_sb, o_st, o_sh, B, Sq, Sk, H, Hkv, d_real, causal, scale, workspace,
                          stream) == 0)
@@ -1065,9 +1103,9 @@ KCA_API int kca_attn_bwd(const void* q, const void* k, const void* v,
                          long long dv_sb, long long dv_st, long long dv_sh,
                          int B, int Sq, int Sk, int H, int Hkv, int d_real,
                          int causal, float scale, const float* alibi,
-                         const int* kv_len, hipStream_t stream) {
-  if (d_real % 8 || H % Hkv) return 1;
-  if (g_attn_tiled && !alibi && !kv_len &&
+                         const int* kv_len, int window, const unsigned* key_mask, hipStream_t stream) {
+  if (d_real % 8 || H % Hkv || window < 0) return 1;
+  if (g_attn_tiled && !alibi && !kv_len && !window && !key_mask &&
       kca_attn_bwd_tiled(q, k, v, dout, dq, dk, dv, lse, delta, q_sb, q_st, q_sh, k_sb, k_st, k_sh,
                          v_sb, v_st, v_sh, do_sb, do_st, do_sh, dq_sb, dq_st, dq_sh, dk_sb, dk_st,
                          dk_sh, dv_sb, dv_st, dv_sh, B, Sq, Sk, H, Hkv, d_real, causal, scale,
@@ -1079,7 +1117,7 @@ KCA_API int kca_attn_bwd(const void* q, const void* k, const void* v,
                   q_sb, q_st, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh,
                   do_sb, do_st, do_sh, dq_sb, dq_st, dq_sh, dk_sb, dk_st, dk_sh,
                   dv_sb, dv_st, dv_sh,
-                  B, Sq, Sk, H, Hkv, d_real, causal, scale, alibi, kv_len};
+                  B, Sq, Sk, H, Hkv, d_real, causal, scale, alibi, kv_len, window, key_mask, (Sk + 31) / 32};
   if (D == 256) {  // dQ on the 32-wide kernel (D=128 measured faster on the 16-wide pair: occupancy)
     dim3 h1(((Sk + 127) / 128) * B * Hkv);
     dim3 h2(((Sq + 127) / 128) * B * H);

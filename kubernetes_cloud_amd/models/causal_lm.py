@@ -51,8 +51,8 @@ def mask_to_kv(mask: torch.Tensor):
     * int32 [B] lengths   right padding (each row a prefix of ones);
     * bool [B, S]         a mask with holes, e.g. the interior EOS separators of
                           the last context of a pad == eos dataset
-                          (finetuner.py:674-691) -- exact HF semantics through
-                          the reference attention path.
+                          (finetuner.py:674-691) -- exact HF semantics; the
+                          kernels take it as a packed key bitmap.
 
     A host mask is classified exactly. A device mask is never read back (no
     host sync): it is taken as right padding, length = last real token + 1."""
@@ -122,24 +122,15 @@ class Attention(nn.Module):
         B, S, _ = x.shape
         qkv = self.qkv(x)
         cfg = self.cfg
-        if self.window:
-            # GPT-Neo local layers: banded causal mask (reference math; rare arch)
-            v5 = qkv.view(B, S, 3, self.n_heads, self.head_dim)
-            q, k, v = (v5[:, :, i].float() for i in range(3))
-            s = torch.einsum("bqhd,bkhd->bhqk", q, k) * self.scale
-            qi = torch.arange(S, device=x.device)[:, None]
-            ki = torch.arange(S, device=x.device)[None, :]
-            s = s.masked_fill((ki > qi) | (ki <= qi - self.window), float("-inf"))
-            o = torch.einsum("bhqk,bkhd->bqhd", s.softmax(-1), v).to(x.dtype)
-            o = o.reshape(B, S, -1)
-        elif cfg.rotary_dim > 0:
+        if cfg.rotary_dim > 0:
             o = ops.qkv_rope_attention(qkv, self.n_heads, self.head_dim, cfg.rotary_dim,
                                        cfg.rotary_interleaved, causal=True, base=cfg.rotary_base,
                                        scale=self.scale, kv_len=kv_len)
         else:
+            # (GPT-Neo local layers: the kernels skip the tiles left of the band, ``window``)
             v5 = qkv.view(B, S, 3, self.n_heads, self.head_dim)
             o = ops.flash_attention(v5[:, :, 0], v5[:, :, 1], v5[:, :, 2], causal=True,
-                                    scale=self.scale, kv_len=kv_len, alibi=self.alibi)
+                                    scale=self.scale, kv_len=kv_len, alibi=self.alibi, window=self.window)
             o = o.reshape(B, S, -1)
         return self.out(o)
 

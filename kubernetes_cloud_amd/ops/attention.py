@@ -7,9 +7,11 @@ attention kernels read Q/K/V straight out of the [B, S, 3, H, D] buffer; the
 backward writes dQ/dK/dV into one fused dQKV buffer (so one dgrad GEMM and one
 wgrad GEMM serve all three projections) and un-rotates dQ/dK in place.
 
-CPU tensors use the fp32 reference (``attention_reference``), and so do the
-rare per-key masks with holes (the last context of a pad == eos dataset,
-data/tokenized.py): the kernels take right-padding key lengths only.
+Masks: ``kv_len`` is None, int [B] key lengths (right padding), or a bool
+[B, Sk] per-key mask with holes (the last context of a pad == eos dataset,
+data/tokenized.py; finetuner.py:674-691) which the kernels take as a packed
+bitmap; ``window`` > 0 is GPT-Neo's local band (key > q - window). CPU
+tensors use the fp32 reference (``attention_reference``).
 """
 from __future__ import annotations
 
@@ -22,10 +24,12 @@ from .rope import apply_rotary_
 
 
 def attention_reference(q, k, v, causal: bool, scale: float | None = None,
-                        kv_len: torch.Tensor | None = None, alibi: torch.Tensor | None = None):
+                        kv_len: torch.Tensor | None = None, alibi: torch.Tensor | None = None,
+                        window: int = 0):
     """fp32 reference. q [B,Sq,H,D], k/v [B,Sk,Hkv,D] -> o [B,Sq,H,D] (q.dtype), lse [B,H,Sq].
     ``kv_len``: int [B] key lengths (right padding), or a bool [B, Sk] per-key
-    mask (True = attend) for masks with holes."""
+    mask (True = attend) for masks with holes. ``window``: keys more than
+    window-1 positions left of the (bottom-right aligned) query are masked."""
     B, Sq, H, D = q.shape
     Sk, Hkv = k.shape[1], k.shape[2]
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
@@ -45,6 +49,8 @@ def attention_reference(q, k, v, causal: bool, scale: float | None = None,
     mask = torch.zeros(B, 1, Sq, Sk, dtype=torch.bool, device=q.device)
     if causal:
         mask = mask | (ki > qi + off)
+    if window:
+        mask = mask | (ki <= qi + off - window)
     if kv_len is not None and kv_len.dtype == torch.bool:  # per-key mask [B, Sk] (True = attend)
         mask = mask | ~kv_len.to(q.device).view(B, 1, 1, Sk)
     elif kv_len is not None:
@@ -69,21 +75,41 @@ def _strides(t):
     return t.stride(0), t.stride(1), t.stride(2)
 
 
-def _fwd(q, k, v, causal, scale, kv_len, alibi, out=None):
+def pack_key_mask(mask: torch.Tensor) -> torch.Tensor:
+    """bool [B, Sk] (True = attend) -> int32 [B, ceil(Sk/32)] bitmap, bit k%32
+    of word k//32 = key k (the kernels' ``key_mask``)."""
+    B, Sk = mask.shape
+    W = (Sk + 31) // 32
+    m = torch.zeros(B, W * 32, dtype=torch.int64, device=mask.device)
+    m[:, :Sk] = mask.to(torch.int64)
+    words = (m.view(B, W, 32) << torch.arange(32, device=mask.device, dtype=torch.int64)).sum(-1)
+    words = torch.where(words >= 2 ** 31, words - 2 ** 32, words)
+    return words.to(torch.int32).contiguous()
+
+
+def _masks(kv_len):
+    """Internal mask form -> (lengths int32 [B] or None, bitmap int32 [B, W] or None)."""
+    if kv_len is None:
+        return None, None
+    return (kv_len, None) if kv_len.dim() == 1 else (None, kv_len)
+
+
+def _fwd(q, k, v, causal, scale, kv_len, alibi, out=None, window: int = 0):
     B, Sq, H, D = q.shape
     Sk, Hkv = k.shape[1], k.shape[2]
     o = out if out is not None else torch.empty(B, Sq, H, D, device=q.device, dtype=q.dtype)
     lse = torch.empty(B, H, Sq, device=q.device, dtype=torch.float32)
     # overflow flags of the full-tile fast path (4 per 128-row block)
     flags = torch.empty(4 * ((Sq + 127) // 128) * B * H, device=q.device, dtype=torch.int32)
+    lens, km = _masks(kv_len)
     _lib.call("kca_attn_fwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr(),
               *_strides(q), *_strides(k), *_strides(v), *_strides(o),
-              B, Sq, Sk, H, Hkv, D, int(causal), float(scale), _lib.ptr(alibi), _lib.ptr(kv_len),
-              flags.data_ptr(), _lib.stream())
+              B, Sq, Sk, H, Hkv, D, int(causal), float(scale), _lib.ptr(alibi), _lib.ptr(lens),
+              int(window), _lib.ptr(km), flags.data_ptr(), _lib.stream())
     return o, lse
 
 
-def _bwd(q, k, v, o, do, lse, dq, dk, dv, causal, scale, kv_len, alibi):
+def _bwd(q, k, v, o, do, lse, dq, dk, dv, causal, scale, kv_len, alibi, window: int = 0):
     B, Sq, H, D = q.shape
     Sk, Hkv = k.shape[1], k.shape[2]
     delta = torch.empty(B, H, Sq, device=q.device, dtype=torch.float32)
@@ -93,8 +119,8 @@ def _bwd(q, k, v, o, do, lse, dq, dk, dv, causal, scale, kv_len, alibi):
               dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), lse.data_ptr(), delta.data_ptr(),
               *_strides(q), *_strides(k), *_strides(v), *_strides(do),
               *_strides(dq), *_strides(dk), *_strides(dv),
-              B, Sq, Sk, H, Hkv, D, int(causal), float(scale), _lib.ptr(alibi), _lib.ptr(kv_len),
-              _lib.stream())
+              B, Sq, Sk, H, Hkv, D, int(causal), float(scale), _lib.ptr(alibi), _lib.ptr(_masks(kv_len)[0]),
+              int(window), _lib.ptr(_masks(kv_len)[1]), _lib.stream())
 
 
 def _check(q, k, v):
@@ -110,11 +136,11 @@ def _check(q, k, v):
 
 class _FlashAttnFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q, k, v, causal, scale, kv_len, alibi):
+    def forward(ctx, q, k, v, causal, scale, kv_len, alibi, window):
         _check(q, k, v)
-        o, lse = _fwd(q, k, v, causal, scale, kv_len, alibi)
+        o, lse = _fwd(q, k, v, causal, scale, kv_len, alibi, window=window)
         ctx.save_for_backward(q, k, v, o, lse, kv_len, alibi)
-        ctx.causal, ctx.scale = causal, scale
+        ctx.causal, ctx.scale, ctx.window = causal, scale, window
         return o
 
     @staticmethod
@@ -124,23 +150,30 @@ class _FlashAttnFn(torch.autograd.Function):
         dq = torch.empty(q.shape, device=q.device, dtype=q.dtype)
         dk = torch.empty(k.shape, device=k.device, dtype=k.dtype)
         dv = torch.empty(v.shape, device=v.device, dtype=v.dtype)
-        _bwd(q, k, v, o, do, lse, dq, dk, dv, ctx.causal, ctx.scale, kv_len, alibi)
-        return dq, dk, dv, None, None, None, None
+        _bwd(q, k, v, o, do, lse, dq, dk, dv, ctx.causal, ctx.scale, kv_len, alibi, ctx.window)
+        return dq, dk, dv, None, None, None, None, None
+
+
+def native_mask(kv_len, device):
+    """Public mask form -> the kernels': int32 lengths [B], or the packed
+    bitmap [B, W] of a bool per-key mask."""
+    if kv_len is None:
+        return None
+    if kv_len.dtype == torch.bool:
+        return pack_key_mask(kv_len.to(device))
+    return kv_len.to(device=device, dtype=torch.int32).contiguous()
 
 
 def flash_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool = False,
                     scale: float | None = None, kv_len: torch.Tensor | None = None,
-                    alibi: torch.Tensor | None = None) -> torch.Tensor:
+                    alibi: torch.Tensor | None = None, window: int = 0) -> torch.Tensor:
     """softmax(scale * Q K^T + alibi + mask) V over [B, S, H, D] views."""
     scale = scale if scale is not None else 1.0 / math.sqrt(q.shape[-1])
-    holes = kv_len is not None and kv_len.dtype == torch.bool
-    if kv_len is not None and not holes:
-        kv_len = kv_len.to(device=q.device, dtype=torch.int32).contiguous()
     if alibi is not None:
         alibi = alibi.to(device=q.device, dtype=torch.float32).contiguous()
-    if _lib.use_native(q, k, v) and not holes:
-        return _FlashAttnFn.apply(q, k, v, causal, scale, kv_len, alibi)
-    o, _ = attention_reference(q, k, v, causal, scale, kv_len, alibi)
+    if _lib.use_native(q, k, v):
+        return _FlashAttnFn.apply(q, k, v, causal, scale, native_mask(kv_len, q.device), alibi, int(window))
+    o, _ = attention_reference(q, k, v, causal, scale, kv_len, alibi, window)
     return o
 
 
@@ -183,12 +216,9 @@ def qkv_rope_attention(qkv: torch.Tensor, n_heads: int, head_dim: int, rot: int,
     """Fused (RoPE + attention) over a [B, S, 3*H*D] QKV buffer -> [B, S, H*D]."""
     B, S, _ = qkv.shape
     scale = scale if scale is not None else 1.0 / math.sqrt(head_dim)
-    holes = kv_len is not None and kv_len.dtype == torch.bool
-    if kv_len is not None and not holes:
-        kv_len = kv_len.to(device=qkv.device, dtype=torch.int32).contiguous()
-    if _lib.use_native(qkv) and not holes:
+    if _lib.use_native(qkv):
         return _QKVRopeAttnFn.apply(qkv.contiguous(), n_heads, head_dim, rot, interleaved, base,
-                                    causal, scale, kv_len)
+                                    causal, scale, native_mask(kv_len, qkv.device))
     v5 = qkv.view(B, S, 3, n_heads, head_dim)
     q, k, v = v5[:, :, 0], v5[:, :, 1], v5[:, :, 2]
     if rot > 0:

@@ -35,6 +35,7 @@ import torch.nn.functional as F
 from . import _lib, grad_sink
 from .attention import _bwd as _attn_bwd
 from .attention import _fwd as _attn_fwd
+from .attention import native_mask
 from .linear import transpose
 from .rope import apply_rotary_
 
@@ -59,14 +60,14 @@ class FusedParallelBlock:
 
     def applies(self, x: torch.Tensor, kv_len=None) -> bool:
         a, m = self.blk.attn, self.blk.mlp
-        return ((kv_len is None or kv_len.dtype != torch.bool) and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 3 and x.is_contiguous()
+        return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 3 and x.is_contiguous()
                 and (x.shape[0] * x.shape[1]) % 64 == 0
                 and all(t.weight_t is not None for t in (a.qkv, a.out, m.fc_in, m.fc_out)))
 
     def __call__(self, x: torch.Tensor, kv_len=None):
         attn, mlp = self.blk.attn, self.blk.mlp
         return _FusedBlockFn.apply(x, attn.qkv.weight, attn.out.weight, mlp.fc_in.weight, mlp.fc_in.bias,
-                                   mlp.fc_out.weight, mlp.fc_out.bias, self, kv_len)
+                                   mlp.fc_out.weight, mlp.fc_out.bias, self, native_mask(kv_len, x.device))
 
 
 def _col_sums(part: torch.Tensor, dtype) -> torch.Tensor:
