@@ -141,6 +141,7 @@ struct DecodeParams {
   // split-K fan-in (nsplit > 1): one arrival counter per (sequence, kv-head); the last split to
   // arrive combines the partials in place of the separate decode_combine_kernel (nullptr: that kernel)
   unsigned int* cnt;
+  int window;  // > 0: attend only the last `window` positions (GPT-Neo local layers)
 };
 
 // Partials that another workgroup of the same launch combines: write-through (sc1) stores, so a
@@ -309,7 +310,9 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
     for (int i = tid; i < npg; i += 256) pg[i] = p.tbl[(long long)seq * p.tbl_stride + pg0 + i];
   }
   const int c1 = min(c0 + p.chunk, L);
-  if (c0 >= L) {
+  // sliding window: positions below L - window are never read (splits left of it are empty)
+  const int ca = p.window > 0 ? max(c0, L - p.window) : c0;
+  if (ca >= c1) {
     if (nsplit > 1 && tid < G) {
       st_pub(&p.ws_ml[((bh0 + tid) * nsplit + split) * 2], -INFINITY);
       st_pub(&p.ws_ml[((bh0 + tid) * nsplit + split) * 2 + 1], 0.f);
@@ -416,7 +419,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
   // inactive lanes (dslot >= ND) and tokens past the split read an in-range row instead of branching
   // around their loads: no branch in the loop, so all 2U loads of an iteration are in flight together
   const long long dfix = dact ? 0 : -(long long)dslot * 8;
-  for (int t0 = c0 + wid * TPW + tsub; t0 < ce; t0 += TPB * U) {
+  for (int t0 = ca + wid * TPW + tsub; t0 < ce; t0 += TPB * U) {
     long long o[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) o[u] = toff(min(t0 + u * TPB, ce - 1)) + dfix;
@@ -551,7 +554,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
     // dependent per-token updates (GPT-J B=1 decode 2.71 vs 2.80 ms/token, same box)
   // V rows of the first P.V iteration, issued together with the K loads: they do not depend on the
   // scores, so a chunk of <= TPB*U tokens (every B=1 split) costs one HBM round trip, not two
-  const int tv0 = c0 + wid * TPW + tsub;
+  const int tv0 = ca + wid * TPW + tsub;
   U16x8 vpre[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
@@ -564,7 +567,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
   __shared__ float red_s[8];
 
   // ---- scores
-  for (int t0 = c0 + wid * TPW + tsub; t0 < c1; t0 += TPB * U) {
+  for (int t0 = ca + wid * TPW + tsub; t0 < c1; t0 += TPB * U) {
     float kr[U][8];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -591,14 +594,14 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
         for (int j = 0; j < 8; ++j) s = fmaf(q[g][j], kr[u][j], s);
 #pragma unroll
         for (int o = 1; o < LPT; o <<= 1) s += __shfl_xor(s, o, 64);
-        if (dslot == 0 && t < c1) sc[g * p.chunk + (t - c0)] = s + slope[g] * (float)(t - (L - 1));
+        if (dslot == 0 && t < c1) sc[g * p.chunk + (t - ca)] = s + slope[g] * (float)(t - (L - 1));
       }
     }
   }
   __syncthreads();
 
   // ---- softmax over this chunk
-  const int n = c1 - c0;
+  const int n = c1 - ca;
   float mg[G], lg[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
@@ -648,7 +651,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
       const int t = t0 + u * TPB;
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        const float pg = t < c1 ? sc[g * p.chunk + (t - c0)] : 0.f;
+        const float pg = t < c1 ? sc[g * p.chunk + (t - ca)] : 0.f;
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[g][j] = fmaf(pg, vr[u][j], acc[g][j]);
       }
@@ -802,10 +805,11 @@ KCA_API int kca_decode_attn(const void* q, long long q_bs, const void* kc, const
                             const int* slots, const int* kv_lens, void* out, long long o_bs,
                             float* ws, long long ws_floats, int B, int H, int Hkv, int D,
                             int max_kv, int chunk, float scale, const float* alibi, const int* tbl,
-                            int tbl_stride, int ps_shift, hipStream_t stream) {
+                            int tbl_stride, int ps_shift, int window, hipStream_t stream) {
+  if (window < 0) return 9;
   DecodeParams p{(const bf16_t*)q, q_bs, (const bf16_t*)kc, (const bf16_t*)vc, cs_slot, cs_head,
                  cs_pos, slots, kv_lens, (bf16_t*)out, o_bs, nullptr, nullptr, alibi, tbl, tbl_stride, ps_shift,
-                 H, Hkv, D, chunk, scale, 0, 0, 0, nullptr, nullptr, g_decode_stamps, nullptr};
+                 H, Hkv, D, chunk, scale, 0, 0, 0, nullptr, nullptr, g_decode_stamps, nullptr, window};
   return decode_attn_launch(p, ws, ws_floats, B, max_kv, chunk, stream);
 }
 
@@ -819,11 +823,12 @@ KCA_API int kca_decode_prep_attn(const void* qkv, long long ld, const void* kc, 
                                  float* ws, long long ws_floats, int B, int H, int Hkv, int D,
                                  int max_kv, int chunk, float scale, const float* alibi, const int* tbl,
                                  int tbl_stride, int ps_shift, int rot, int interleaved, const float* cos_t,
-                                 const float* sin_t, hipStream_t stream) {
+                                 const float* sin_t, int window, hipStream_t stream) {
   if (rot > D || (rot & 1) || (rot > 0 && (!cos_t || !sin_t))) return 8;
+  if (window < 0) return 9;
   DecodeParams p{(const bf16_t*)qkv, ld, (const bf16_t*)kc, (const bf16_t*)vc, cs_slot, cs_head,
                  cs_pos, slots, kv_lens, (bf16_t*)out, o_bs, nullptr, nullptr, alibi, tbl, tbl_stride, ps_shift,
-                 H, Hkv, D, chunk, scale, 1, rot, interleaved, cos_t, sin_t, g_decode_stamps, nullptr};
+                 H, Hkv, D, chunk, scale, 1, rot, interleaved, cos_t, sin_t, g_decode_stamps, nullptr, window};
   return decode_attn_launch(p, ws, ws_floats, B, max_kv, chunk, stream);
 }
 

@@ -304,7 +304,6 @@ class ModelRunner:
         self._graphs: dict = {}
         self._pool = None
         self._static: dict = {}
-        self._windowed = any(getattr(b.attn, "window", 0) for b in model.h)
         # parallel-residual models (GPT-J, NeoX): the MLP branch does not depend on attention, so at
         # decode its two weight-streaming GEMVs run on a side stream while the latency-bound attention
         # chain (split-K attention, combine, out-proj) runs on the main one -- both captured into the
@@ -374,10 +373,8 @@ class ModelRunner:
             self.cache.write(li, k, v, slots, lens, plan, start)
             if cont:
                 o = self._continued_attention(li, q, slots, lens, start, at)
-            elif at.window:
-                o = self._windowed_prefill(q, k, v, at)
-            else:
-                o = ops.flash_attention(q, k, v, causal=True, scale=at.scale, alibi=at.alibi)
+            else:  # (GPT-Neo local layers: banded, the kernels skip the tiles left of the band)
+                o = ops.flash_attention(q, k, v, causal=True, scale=at.scale, alibi=at.alibi, window=at.window)
             a = at.out(o.reshape(n, T, -1))
             if cfg.parallel_residual:
                 x2 = x if blk.ln_2 is None else blk.ln_2(h)
@@ -405,29 +402,17 @@ class ModelRunner:
         kc, vc, tbl = self.cache.k[li], self.cache.v[li], self.cache.table_on(self.layer_devs[li])
         for i, (s_, L, p0) in enumerate(zip(slots, lens, start)):
             kv = p0 + L
-            kw = dops.gather_kv(kc, s_, kv, tbl).transpose(0, 1)[None]
-            vw = dops.gather_kv(vc, s_, kv, tbl).transpose(0, 1)[None]
-            if at.window:
-                lo = max(0, kv - L - at.window + 1)  # oldest key any chunk query can see
-                o[i:i + 1, :L] = self._windowed_prefill(q[i:i + 1, :L], kw[:, lo:], vw[:, lo:], at)
-            else:
-                o[i:i + 1, :L] = ops.flash_attention(q[i:i + 1, :L], kw, vw, causal=True, scale=at.scale,
-                                                     alibi=at.alibi)
+            lo = max(0, kv - L - at.window + 1) if at.window else 0  # oldest key any chunk query can see
+            kw = dops.gather_kv(kc, s_, kv, tbl)[:, lo:].transpose(0, 1)[None]
+            vw = dops.gather_kv(vc, s_, kv, tbl)[:, lo:].transpose(0, 1)[None]
+            o[i:i + 1, :L] = ops.flash_attention(q[i:i + 1, :L], kw, vw, causal=True, scale=at.scale,
+                                                 alibi=at.alibi, window=at.window)
         return o
 
     @staticmethod
     def _hop(dev, h, pending):
         """Move the residual stream to the next layer-split device."""
         return h.to(dev), tuple(p_.to(dev) for p_ in pending)
-
-    @staticmethod
-    def _windowed_prefill(q, k, v, at):
-        Tq, Tk = q.shape[1], k.shape[1]
-        s = torch.einsum("bqhd,bkhd->bhqk", q.float(), k.float()) * at.scale
-        qi = torch.arange(Tq, device=q.device)[:, None] + (Tk - Tq)  # bottom-right aligned
-        ki = torch.arange(Tk, device=q.device)[None, :]
-        s = s.masked_fill((ki > qi) | (ki <= qi - at.window), float("-inf"))
-        return torch.einsum("bhqk,bkhd->bqhd", s.softmax(-1), v.float()).to(q.dtype)
 
     # -------------------------------------------------------------- decode
     def _layers_decode(self, tokens, pos, slots, kv_lens, max_kv, ws, obuf):
@@ -469,14 +454,11 @@ class ModelRunner:
                     h.record_stream(self._side)
             kc, vc, tbl = self.cache.k[li], self.cache.v[li], self.cache.table_on(dev)
             cos, sin = self._rope[dev]
-            if at.window:
-                dops.decode_prep(qkv, self.H, self.Hkv, self.D, self.rot, cfg.rotary_interleaved, cos, sin, pos,
-                                 slots, kc, vc, block_table=tbl)
-                o = self._windowed_decode(qkv, kc, vc, slots, kv_lens, at)
-            else:  # RoPE + cache append + split-K attention (one launch on the GPU)
-                o = dops.decode_prep_attention(qkv, self.H, self.Hkv, self.D, self.rot, cfg.rotary_interleaved,
-                                               cos, sin, pos, slots, kc, vc, kv_lens, max_kv, at.scale, at.alibi,
-                                               out=obuf, ws=ws, block_table=tbl)
+            # RoPE + cache append + split-K attention (one launch on the GPU; GPT-Neo local layers read
+            # only the last `window` positions)
+            o = dops.decode_prep_attention(qkv, self.H, self.Hkv, self.D, self.rot, cfg.rotary_interleaved,
+                                           cos, sin, pos, slots, kc, vc, kv_lens, max_kv, at.scale, at.alibi,
+                                           out=obuf, ws=ws, block_table=tbl, window=at.window)
             a = self._lin(at.out, o)
             if side_out is not None:  # join
                 cur.wait_stream(self._side)
@@ -518,21 +500,6 @@ class ModelRunner:
         if isinstance(mod, ParallelLMHead):
             return gather_last_dim(skinny_linear(x, mod.local_weight(), mod.bias), mod.group)
         return skinny_linear(x, mod.weight, mod.bias, act)
-
-    def _windowed_decode(self, qkv, kc, vc, slots, kv_lens, at):
-        B = qkv.shape[0]
-        out = torch.empty(B, self.H * self.D, device=qkv.device, dtype=qkv.dtype)
-        tbl = self.cache.table_on(kc.device)
-        for b in range(B):
-            L = int(kv_lens[b])
-            lo = max(0, L - at.window)
-            s = int(slots[b])
-            sub_len = torch.tensor([L - lo], dtype=torch.int32)
-            kw = dops.gather_kv(kc, s, L, tbl)[:, lo:][None]
-            vw = dops.gather_kv(vc, s, L, tbl)[:, lo:][None]
-            dops.decode_attention_reference(qkv[b:b + 1], kw, vw, torch.zeros(1, dtype=torch.int32), sub_len,
-                                            self.H, at.scale, None, out[b:b + 1])
-        return out
 
     def _static_for(self, Bb: int, Kb: int):
         key = (Bb, Kb)
@@ -607,7 +574,7 @@ class ModelRunner:
         Bb = _next_pow2(n)
         max_kv = max(r["pos"] for r in rows) + 1
         Kb = min(_next_pow2(max_kv, 256), self.max_len)
-        if self._windowed or self.device.type != "cuda":
+        if self.device.type != "cuda":
             Bb = n  # GPU eager keeps the graph buckets so both paths run identical shapes
         st = self._static_for(Bb, Kb)
         pk = st["pk"]
@@ -634,7 +601,7 @@ class ModelRunner:
                 tok[i], pos[i], sl[i], kl[i] = 0, 0, self.cache.scratch, 1
                 te[i], tk[i], tp[i], rp[i], sd[i] = 0.0, 0, 1.0, 1.0, 0
         pk.upload()
-        if self.use_graphs and not self._windowed:
+        if self.use_graphs:
             g = self._graphs.get((Bb, Kb))
             if g is None:
                 g = self._capture(st, Bb, Kb)

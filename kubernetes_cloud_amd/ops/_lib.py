@@ -80,13 +80,13 @@ _SIGS = {
     "kca_decode_prep": [P, LL, I, I, I, I, I, I, P, P, P, P, P, P, LL, LL, LL, P, I, I, P],
     "kca_decode_chunk": [I, I, I],
     "kca_decode_set_stamps": [P],
-    "kca_decode_attn": [P, LL, P, P, LL, LL, LL, P, P, P, LL, P, LL, I, I, I, I, I, I, F, P, P, I, I, P],
+    "kca_decode_attn": [P, LL, P, P, LL, LL, LL, P, P, P, LL, P, LL, I, I, I, I, I, I, F, P, P, I, I, I, P],
     "kca_sd_noise_prep": [P, P, P, P, P, P, P, P, P, I, I, I, I, F, I, ctypes.c_ulonglong, P],
     "kca_mse_split_fwd": [P, P, LL, LL, F, P, I, P, P],
     "kca_mse_split_bwd": [P, P, P, LL, LL, F, P, P],
     "kca_sd_lms_step": [P, P, P, P, LL, P, I, I, I, I, I, F, F, F, P],
     "kca_decode_prep_attn": [P, LL, P, P, LL, LL, LL, P, P, P, LL, P, LL, I, I, I, I, I, I, F, P, P, I, I, I, I, P,
-                             P, P],
+                             P, I, P],
     "kca_sample_logits": [P, LL, I, I, I, P, P, P, P, P, P, P, I, P, LL, P, P, P, P, P],
 }
 

@@ -126,10 +126,10 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
                      kv_lens: torch.Tensor, n_heads: int, max_kv: int, scale: float | None = None,
                      alibi: torch.Tensor | None = None, out: torch.Tensor | None = None,
                      ws: torch.Tensor | None = None, chunk: int = 0,
-                     block_table: torch.Tensor | None = None) -> torch.Tensor:
+                     block_table: torch.Tensor | None = None, window: int = 0) -> torch.Tensor:
     """q: [B, >=H*D] (row-strided; e.g. the Q slice of the fused QKV buffer).
-    Attends row b over cache[slots[b], :, :kv_lens[b]] (paged: over its pages).
-    Returns [B, H*D]."""
+    Attends row b over cache[slots[b], :, :kv_lens[b]] (paged: over its pages),
+    or over its last ``window`` positions (GPT-Neo local layers). Returns [B, H*D]."""
     B = q.shape[0]
     _, Hkv, L, D = k_cache.shape
     H = n_heads
@@ -149,9 +149,10 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
                   k_cache.stride(0), k_cache.stride(1), k_cache.stride(2), slots.data_ptr(),
                   kv_lens.data_ptr(), out.data_ptr(), out.stride(0), _lib.ptr(ws),
                   ws.numel() if ws is not None else 0, B, H, Hkv, D, max_kv, chunk, float(scale),
-                  _lib.ptr(alibi), tbl, tstride, shift, _lib.stream())
+                  _lib.ptr(alibi), tbl, tstride, shift, int(window), _lib.stream())
         return out
-    return decode_attention_reference(q, k_cache, v_cache, slots, kv_lens, H, scale, alibi, out, block_table)
+    return decode_attention_reference(q, k_cache, v_cache, slots, kv_lens, H, scale, alibi, out, block_table,
+                                      window)
 
 
 def decode_prep_attention(qkv: torch.Tensor, n_heads: int, kv_heads: int, head_dim: int, rot: int,
@@ -159,7 +160,8 @@ def decode_prep_attention(qkv: torch.Tensor, n_heads: int, kv_heads: int, head_d
                           pos: torch.Tensor, slots: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
                           kv_lens: torch.Tensor, max_kv: int, scale: float | None = None,
                           alibi: torch.Tensor | None = None, out: torch.Tensor | None = None,
-                          ws: torch.Tensor | None = None, block_table: torch.Tensor | None = None) -> torch.Tensor:
+                          ws: torch.Tensor | None = None, block_table: torch.Tensor | None = None,
+                          window: int = 0) -> torch.Tensor:
     """``decode_prep`` + ``decode_attention`` for the decode step (kv_lens = pos + 1).
     Native: ONE launch (``kca_decode_prep_attn``) that rotates Q itself and lets
     the split holding the new token rotate and append K/V (the prep kernel's ~5 us
@@ -182,15 +184,15 @@ def decode_prep_attention(qkv: torch.Tensor, n_heads: int, kv_heads: int, head_d
                   k_cache.stride(0), k_cache.stride(1), k_cache.stride(2), slots.data_ptr(), kv_lens.data_ptr(),
                   out.data_ptr(), out.stride(0), _lib.ptr(ws), ws.numel() if ws is not None else 0, B, H, Hkv, D,
                   max_kv, chunk, float(scale), _lib.ptr(alibi), tbl, tstride, shift, rot, int(interleaved),
-                  _lib.ptr(cos), _lib.ptr(sin), _lib.stream())
+                  _lib.ptr(cos), _lib.ptr(sin), int(window), _lib.stream())
         return out
     decode_prep(qkv, H, Hkv, D, rot, interleaved, cos, sin, pos, slots, k_cache, v_cache, block_table)
     return decode_attention(qkv, k_cache, v_cache, slots, kv_lens, H, max_kv, scale, alibi, out, ws,
-                            block_table=block_table)
+                            block_table=block_table, window=window)
 
 
 def decode_attention_reference(q, k_cache, v_cache, slots, kv_lens, n_heads, scale, alibi=None, out=None,
-                               block_table=None):
+                               block_table=None, window: int = 0):
     B = q.shape[0]
     _, Hkv, L, D = k_cache.shape
     H = n_heads
@@ -198,13 +200,14 @@ def decode_attention_reference(q, k_cache, v_cache, slots, kv_lens, n_heads, sca
         out = torch.empty(B, H * D, device=q.device, dtype=q.dtype)
     for b in range(B):
         n = int(kv_lens[b])
+        lo = max(0, n - window) if window > 0 else 0
         s_ = int(slots[b])
         qb = q[b, :H * D].float().view(H, D)
-        kb = gather_kv(k_cache, s_, n, block_table).float().repeat_interleave(H // Hkv, 0)  # [H, n, D]
-        vb = gather_kv(v_cache, s_, n, block_table).float().repeat_interleave(H // Hkv, 0)
+        kb = gather_kv(k_cache, s_, n, block_table)[:, lo:].float().repeat_interleave(H // Hkv, 0)  # [H, n, D]
+        vb = gather_kv(v_cache, s_, n, block_table)[:, lo:].float().repeat_interleave(H // Hkv, 0)
         sc = torch.einsum("hd,hnd->hn", qb, kb) * scale
         if alibi is not None:
-            sc = sc + alibi.float()[:, None] * (torch.arange(n, device=q.device) - (n - 1)).float()[None]
+            sc = sc + alibi.float()[:, None] * (torch.arange(lo, n, device=q.device) - (n - 1)).float()[None]
         o = torch.einsum("hn,hnd->hd", sc.softmax(-1), vb)
         out[b] = o.reshape(-1).to(out.dtype)
     return out
