@@ -82,11 +82,11 @@ def run_tp_decode(model_name="bloom-176b", layers=0, batches=(1, 8, 32), prompt_
             reqs = [eng.add_request(p, sp) for p in prompts]
             eng.step()
             torch.cuda.synchronize()
-            s0, t0 = eng.stats["steps"], time.perf_counter()
+            s0, t0 = eng.stats["decode_steps"], time.perf_counter()
             eng.run_until_done(reqs)
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
-            n = eng.stats["steps"] - s0
+            n = eng.stats["decode_steps"] - s0
             out.append({"metric": f"{model_name} TP={world} decode", "batch": B, "prompt_len": prompt_len,
                         "prefill_ms": round(prefill_ms, 2), "decode_ms_per_token": round(dt / max(n, 1) * 1e3, 3),
                         "tokens_per_s": round((sum(len(r.output) for r in reqs) - 2 * B) / dt, 1),

@@ -46,11 +46,11 @@ def run_decode(model="gpt-j-6b", batches=(1, 32), prompt_len=512, new_tokens=64)
         reqs = [eng.add_request(p, sp) for p in prompts]
         eng.step()  # admit (prefill + first token) + first decode
         torch.cuda.synchronize()
-        s0, t0 = eng.stats["steps"], time.perf_counter()
+        s0, t0 = eng.stats["decode_steps"], time.perf_counter()
         eng.run_until_done(reqs)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        n = eng.stats["steps"] - s0
+        n = eng.stats["decode_steps"] - s0
         out.append({"metric": f"{model} decode", "batch": B, "prompt_len": prompt_len, "new_tokens": new_tokens,
                     "prefill_ms_one_seq": round(prefill_ms, 2), "decode_ms_per_token": round(dt / max(n, 1) * 1e3, 3),
                     "decode_tokens_per_s": round(B * n / dt, 1), "dtype": "bf16", "graphs": eng.runner.use_graphs,
@@ -89,7 +89,9 @@ def main():
         cfg.n_layers = args.layers
     m = build_model(cfg, device=dev, dtype=torch.bfloat16, seed=0)
     batches = [int(b) for b in args.batches.split(",")]
-    eng = LLMEngine(m, max_slots=max(batches), max_len=args.prompt_len + args.new_tokens + 8,
+    # (decode-only: room for every timed step -- a request that hit max_len would leave the
+    # remaining steps empty and the average meaningless)
+    eng = LLMEngine(m, max_slots=max(batches), max_len=args.prompt_len + max(args.new_tokens, args.decode_only) + 16,
                     use_graphs=not args.no_graphs, page_size=args.page_size)
     g = torch.Generator().manual_seed(0)
     if args.decode_only:
@@ -104,6 +106,7 @@ def main():
         for _ in range(args.decode_only):
             eng.step()
         torch.cuda.synchronize()
+        assert all(not r.done for r in reqs), "a request finished inside the timed decode-only steps"
         dt = (time.perf_counter() - t0) / args.decode_only
         print(json.dumps({"metric": f"{args.model} decode-only", "batch": B, "decode_ms_per_step": round(dt * 1e3, 3),
                           "decode_tokens_per_s": round(B / dt, 1), "page_size": eng.runner.cache.page_size}),
@@ -124,11 +127,11 @@ def main():
         reqs = [eng.add_request(p, sp) for p in prompts]
         eng.step()  # admit + first decode
         torch.cuda.synchronize()
-        steps0, t0 = eng.stats["steps"], time.perf_counter()
+        steps0, t0 = eng.stats["decode_steps"], time.perf_counter()
         eng.run_until_done(reqs)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        nsteps = eng.stats["steps"] - steps0
+        nsteps = eng.stats["decode_steps"] - steps0
         gen = sum(len(r.output) for r in reqs) - 2 * B
         print(json.dumps({"metric": f"{args.model} decode", "batch": B, "prompt_len": args.prompt_len,
                           "new_tokens": args.new_tokens, "prefill_ms_per_seq": round(prefill_ms, 2),

@@ -11,6 +11,13 @@ output log-probs).
 
 ``step()`` = admit waiting requests (prefill + first token) while slots and
 KV pages are free, then one fused decode step for every running request.
+One-step lookahead (``pipeline``, on with a pipelining runner): a step launches
+the next decode -- its input tokens chained on the device from the step in
+flight (``ModelRunner.decode_async``) -- and only then reads the in-flight
+step's tokens, so stop checks, streaming callbacks and row preparation overlap
+the GPU instead of idling it. A request that stops on a token the host has not
+seen yet gets one discarded extra token computed; length stops are predicted
+and never over-run.
 Chunked prefill (``prefill_chunk``): while requests are decoding, a step
 spends at most ``prefill_chunk`` prompt tokens on prefill -- a long prompt is
 prefilled over several steps (``ModelRunner.prefill(..., start=)`` continues
@@ -84,7 +91,7 @@ class Request:
 class LLMEngine:
     def __init__(self, model, max_slots: int = 32, max_len: int | None = None, use_graphs: bool | None = None,
                  max_prefill_tokens: int = 16384, runner=None, page_size: int | None = None,
-                 kv_pages: int | None = None, prefill_chunk: int | None = None):
+                 kv_pages: int | None = None, prefill_chunk: int | None = None, pipeline: bool | None = None):
         # ``runner``: e.g. a tp_driver.CollectiveRunner that mirrors every call to TP follower ranks
         self.runner = runner or ModelRunner(model, max_slots=max_slots, max_len=max_len, use_graphs=use_graphs,
                                             page_size=page_size, kv_pages=kv_pages)
@@ -103,8 +110,11 @@ class LLMEngine:
         # prompt-token budget of a step while requests are decoding (None/0: whole prompts)
         self.prefill_chunk = int(prefill_chunk) if prefill_chunk else 0
         self.prefilling: list[Request] = []  # admitted, prompt partially in the cache (r.prefilled tokens)
+        self.pipeline = bool(getattr(self.runner, "pipelined", False)) if pipeline is None else pipeline
+        self._inflight = None  # (DecodeHandle, [Request]) of the launched, not yet read decode step
         self.stats = {"steps": 0, "decode_tokens": 0, "prefill_tokens": 0, "finished": 0, "prefill_batches": 0,
-                      "prefill_pad_tokens": 0, "prefill_chunks": 0, "max_step_prefill_tokens": 0}
+                      "prefill_pad_tokens": 0, "prefill_chunks": 0, "max_step_prefill_tokens": 0,
+                      "decode_steps": 0}
         cache = getattr(self.runner, "cache", None)
         self._paged = cache is not None and getattr(cache, "paged", False)
         self._page_budget = cache.n_pages if self._paged else 0
@@ -133,11 +143,13 @@ class LLMEngine:
         return r
 
     def has_work(self) -> bool:
-        return bool(self.waiting or self.running or self.prefilling)
+        return bool(self.waiting or self.running or self.prefilling or self._inflight)
 
-    def _row(self, r: Request, token: int | None = None) -> dict:
+    def _row(self, r: Request, token: int | None = None, ahead: int = 0) -> dict:
+        """Decode-row parameters. ``ahead`` = 1: the row's input token is the
+        in-flight step's (not yet on the host), chained on the device."""
         p = r.params
-        n_gen = len(r.output)
+        n_gen = len(r.output) + ahead
         greedy = (not p.do_sample) or p.temperature <= 0
         bans = []
         for w in p.bad_words_ids or ():
@@ -147,6 +159,11 @@ class LLMEngine:
                 bans.append(int(w[-1]))
         if p.eos_token_id is not None and n_gen < p.min_new_tokens:
             bans.append(int(p.eos_token_id))
+        if ahead:
+            return {"token": None, "pos": len(r.tokens) - 1 + ahead,
+                    "slot": r.slot, "temperature": 0.0 if greedy else float(p.temperature),
+                    "top_k": int(p.top_k or 0), "top_p": float(p.top_p if p.top_p is not None else 1.0),
+                    "rep": float(p.repetition_penalty or 1.0), "seed": mix_seed(r.seed, n_gen), "bans": bans}
         return {"token": token if token is not None else r.tokens[-1], "pos": len(r.tokens) - 1,
                 "slot": r.slot, "temperature": 0.0 if greedy else float(p.temperature),
                 "top_k": int(p.top_k or 0), "top_p": float(p.top_p if p.top_p is not None else 1.0),
@@ -202,6 +219,7 @@ class LLMEngine:
         if self._paged:
             need = num_beams * (self.runner.cache.pages_for(min(len(prompt) + max_new_tokens, self.max_len)) + 1)
         with self._step_lock:
+            self._drain([])  # the in-flight lookahead step finishes before the beams take the runner
             with self._lock:
                 if len(self.free) < num_beams:
                     raise RuntimeError(f"need {num_beams} free cache slots, have {len(self.free)}")
@@ -304,22 +322,75 @@ class LLMEngine:
                 else:
                     self.running.append(r)
         # decode one token for everything already running (incl. just admitted)
-        if self.running:
+        if self.pipeline and self._lookahead_ok():
+            self._decode_lookahead(finished)
+        elif self.running or self._inflight:
+            self._drain(finished)
             rows = [self._row(r) for r in self.running]
-            toks, lps = self.runner.decode(rows)
-            self.stats["decode_tokens"] += len(rows)
-            still = []
-            for r, t, lp in zip(self.running, toks, lps):
-                self._append(r, t, lp)
-                if r.done:
-                    self._finish(r)
-                    finished.append(r)
-                else:
-                    still.append(r)
-            self.running = still
+            if rows:
+                toks, lps = self.runner.decode(rows)
+                self.stats["decode_tokens"] += len(rows)
+                self.stats["decode_steps"] += 1
+                self._take(self.running, toks, lps, finished)
+            self.running = [r for r in self.running if not r.done]
         self.stats["steps"] += 1
         self.stats["max_step_prefill_tokens"] = max(self.stats["max_step_prefill_tokens"], used)
         return finished
+
+    # ------------------------------------------------------------ lookahead
+    def _take(self, reqs, toks, lps, finished):
+        for r, t, lp in zip(reqs, toks, lps):
+            if r.done:  # stopped on the previous token: this one was computed ahead and is dropped
+                continue
+            self._append(r, t, lp)
+            if r.done:
+                self._finish(r)
+                finished.append(r)
+
+    def _drain(self, finished):
+        """Read the in-flight decode step (before a synchronous runner call)."""
+        if self._inflight is not None:
+            h, reqs = self._inflight
+            self._inflight = None
+            toks, lps = h.result()
+            self._take(reqs, toks, lps, finished)
+
+    def _lookahead_ok(self) -> bool:
+        # a multi-token bad word's ban depends on the token still in flight
+        return not any(len(w) > 1 for r in self.running for w in (r.params.bad_words_ids or ()))
+
+    def _last_by_length(self, r: Request, ahead: int) -> bool:
+        return (len(r.output) + ahead >= r.params.max_new_tokens
+                or len(r.tokens) + ahead >= self.max_len)
+
+    def _decode_lookahead(self, finished):
+        """Launch step t+1 (tokens of step t chained on the device), then read step t."""
+        inflight = self._inflight
+        src = {id(r): i for i, r in enumerate(inflight[1])} if inflight else {}
+        rows, reqs = [], []
+        for r in self.running:
+            if r.done:
+                continue
+            j = src.get(id(r))
+            if j is None:
+                rows.append(self._row(r))
+            else:
+                if self._last_by_length(r, 1):  # its in-flight token is its last one
+                    continue
+                row = self._row(r, ahead=1)
+                row["src"] = j
+                rows.append(row)
+            reqs.append(r)
+        h = self.runner.decode_async(rows, prev=inflight[0] if inflight else None) if rows else None
+        if rows:
+            self.stats["decode_tokens"] += len(rows)
+            self.stats["decode_steps"] += 1
+        self._inflight = None
+        if inflight is not None:
+            toks, lps = inflight[0].result()
+            self._take(inflight[1], toks, lps, finished)
+        self._inflight = (h, reqs) if h is not None else None
+        self.running = [r for r in self.running if not r.done]
 
     def run_until_done(self, reqs: list[Request] | None = None):
         while self.has_work() and (reqs is None or not all(r.done for r in reqs)):
@@ -368,6 +439,7 @@ class LLMEngine:
                 with self._lock:
                     victims = self.running + self.prefilling + self.waiting
                     self.running, self.prefilling, self.waiting = [], [], []
+                    self._inflight = None
                 for r in victims:
                     try:
                         self._free_slot(r)

@@ -19,7 +19,10 @@ The FT-equivalent decode loop for every causal LM in
   a GPT-J step is one graph launch + one 8-byte/row D2H copy.
 
 Host inputs of a step (tokens, positions, slots, sampling params, bans, seeds)
-travel in ONE packed pinned buffer -> one H2D copy.
+travel in ONE packed pinned buffer -> one H2D copy. ``decode_async`` launches a
+step without waiting for it and can take each row's input token from the
+previous launch's device output, so the engine launches step t+1 before it
+reads step t's tokens (``LLMEngine``'s one-step lookahead).
 """
 from __future__ import annotations
 
@@ -231,7 +234,9 @@ class KVCache:
 
 
 class _Packed:
-    """Several small typed arrays in one byte buffer (pinned host + device twin)."""
+    """Several small typed arrays in one byte buffer: two pinned host buffers
+    (alternating per launch, so the host fills one while the previous launch's
+    H2D copy may still be pending) + one device twin the decode graph reads."""
 
     def __init__(self, fields, device):
         self.off, self.fields = {}, fields
@@ -242,11 +247,23 @@ class _Packed:
             o += n * torch.empty(0, dtype=dt).element_size()
         self.nbytes = (o + 7) // 8 * 8
         pin = device.type == "cuda"
-        self.host = torch.zeros(self.nbytes, dtype=torch.uint8, pin_memory=pin)
+        self.hosts = [torch.zeros(self.nbytes, dtype=torch.uint8, pin_memory=pin) for _ in range(2)]
         self.dev = torch.zeros(self.nbytes, dtype=torch.uint8, device=device)
-        # numpy views of the pinned host buffer: per-row scalar writes cost
+        # numpy views of the pinned host buffers: per-row scalar writes cost
         # ~0.1 us instead of a torch indexing op (~5 us) each
-        self.np = {name: self._view(self.host, name).numpy() for name in fields}
+        self._nps = [{name: self._view(h, name).numpy() for name in fields} for h in self.hosts]
+        self.cur = 0
+
+    def flip(self):
+        self.cur ^= 1
+
+    @property
+    def host(self):
+        return self.hosts[self.cur]
+
+    @property
+    def np(self):
+        return self._nps[self.cur]
 
     def _view(self, buf, name):
         dt, n = self.fields[name]
@@ -262,6 +279,25 @@ class _Packed:
 
     def upload(self):
         self.dev.copy_(self.host, non_blocking=True)
+
+
+class DecodeHandle:
+    """A launched decode step: its sampled ids / log-probs land in pinned host
+    memory behind an event; ``result()`` waits for them. ``ids_dev`` is the
+    device output the next launch may chain its input tokens from."""
+
+    __slots__ = ("ids_h", "lps_h", "n", "event", "ids_dev", "_res")
+
+    def __init__(self, ids_h, lps_h, n, event, ids_dev):
+        self.ids_h, self.lps_h, self.n, self.event, self.ids_dev = ids_h, lps_h, n, event, ids_dev
+        self._res = None
+
+    def result(self):
+        if self._res is None:
+            if self.event is not None:
+                self.event.synchronize()
+            self._res = (self.ids_h[:self.n].tolist(), self.lps_h[:self.n].tolist())
+        return self._res
 
 
 class ModelRunner:
@@ -519,6 +555,10 @@ class ModelRunner:
             "sws": torch.empty(Bb * self.V, device=self.device, dtype=torch.float32),
             "ids": torch.empty(Bb, device=self.device, dtype=torch.int64),
             "lps": torch.empty(Bb, device=self.device, dtype=torch.float32),
+            # pinned landing buffers of the ids / log-probs D2H copies, one per host pk buffer
+            "ids_h": [torch.empty(Bb, dtype=torch.int64, pin_memory=self.device.type == "cuda") for _ in range(2)],
+            "lps_h": [torch.empty(Bb, dtype=torch.float32, pin_memory=self.device.type == "cuda")
+                      for _ in range(2)],
         }
         self._static[key] = st
         return st
@@ -566,10 +606,21 @@ class ModelRunner:
         """A finished sequence's KV pages go back to the pool."""
         self.cache.release(slot)
 
+    pipelined = True  # supports decode_async (the TP CollectiveRunner does not)
+
     @torch.no_grad()
     def decode(self, rows: list[dict]):
         """rows: [{token, pos, slot, temperature, top_k, top_p, rep, seed, bans}]
         -> (ids list[int], logprobs list[float]) of the next token per row."""
+        return self.decode_async(rows).result()
+
+    @torch.no_grad()
+    def decode_async(self, rows: list[dict], prev: DecodeHandle | None = None) -> DecodeHandle:
+        """Launch one decode step without waiting for it. A row whose
+        ``token`` is None takes its input token from ``prev``'s output row
+        ``src`` on the device (the previous step's sample, not yet seen by the
+        host), so the engine can launch step t+1 before reading step t: the GPU
+        never idles on the host's bookkeeping between steps."""
         n = len(rows)
         Bb = _next_pow2(n)
         max_kv = max(r["pos"] for r in rows) + 1
@@ -578,6 +629,7 @@ class ModelRunner:
             Bb = n  # GPU eager keeps the graph buckets so both paths run identical shapes
         st = self._static_for(Bb, Kb)
         pk = st["pk"]
+        pk.flip()
         NB = self.max_bans
         for r in rows:
             self.cache.reserve(r["slot"], r["pos"] + 1)
@@ -586,10 +638,16 @@ class ModelRunner:
         tok, sd, pos, sl, kl = a["tokens"], a["seeds"], a["pos"], a["slots"], a["kv_lens"]
         tk, te, tp, rp, bans = a["top_k"], a["temperature"], a["top_p"], a["rep"], a["bans"]
         bans.fill(-1)
+        chain_dst, chain_src = [], []
         for i in range(Bb):
             if i < n:
                 r = rows[i]
-                tok[i], pos[i], sl[i], kl[i] = r["token"], r["pos"], r["slot"], r["pos"] + 1
+                t = r["token"]
+                if t is None:
+                    chain_dst.append(i)
+                    chain_src.append(int(r["src"]))
+                    t = 0
+                tok[i], pos[i], sl[i], kl[i] = t, r["pos"], r["slot"], r["pos"] + 1
                 te[i], tk[i], tp[i], rp[i] = r["temperature"], r["top_k"], r["top_p"], r["rep"]
                 sd[i] = r["seed"]
                 b = r.get("bans") or ()
@@ -601,6 +659,17 @@ class ModelRunner:
                 tok[i], pos[i], sl[i], kl[i] = 0, 0, self.cache.scratch, 1
                 te[i], tk[i], tp[i], rp[i], sd[i] = 0.0, 0, 1.0, 1.0, 0
         pk.upload()
+        if chain_dst:
+            if prev is None:
+                raise ValueError("rows chain their token from a previous launch, but prev is None")
+            dst = pk.d("tokens")
+            m = len(chain_dst)
+            if chain_dst == chain_src == list(range(m)):  # the common case: same rows, same order
+                dst[:m].copy_(prev.ids_dev[:m])
+            else:
+                di = torch.tensor(chain_dst, dtype=torch.long).to(self.device, non_blocking=True)
+                si = torch.tensor(chain_src, dtype=torch.long).to(self.device, non_blocking=True)
+                dst.index_copy_(0, di, prev.ids_dev.index_select(0, si))
         if self.use_graphs:
             g = self._graphs.get((Bb, Kb))
             if g is None:
@@ -608,9 +677,18 @@ class ModelRunner:
             g.replay()
         else:
             self._step_body(st, Bb, Kb)
-        ids = st["ids"][:n].tolist()
-        lps = st["lps"][:n].tolist()
-        return ids, lps
+        k = pk.cur
+        ids_h, lps_h = st["ids_h"][k], st["lps_h"][k]
+        if self.device.type == "cuda":
+            ids_h[:n].copy_(st["ids"][:n], non_blocking=True)
+            lps_h[:n].copy_(st["lps"][:n], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        else:
+            ids_h[:n].copy_(st["ids"][:n])
+            lps_h[:n].copy_(st["lps"][:n])
+            ev = None
+        return DecodeHandle(ids_h, lps_h, n, ev, st["ids"])
 
     def _capture(self, st, Bb, Kb):
         s = torch.cuda.Stream()
@@ -654,4 +732,4 @@ def mix_seed(seed: int, step: int) -> int:
     return x - (1 << 64) if x >= (1 << 63) else x
 
 
-__all__ = ["KVCache", "KVCacheFull", "ModelRunner", "mix_seed", "math"]
+__all__ = ["KVCache", "KVCacheFull", "ModelRunner", "DecodeHandle", "mix_seed", "math"]

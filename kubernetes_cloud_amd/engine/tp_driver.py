@@ -27,6 +27,8 @@ def as_channel(ctrl):
 
 
 class CollectiveRunner:
+    pipelined = False  # every call is mirrored to the followers: no decode_async lookahead
+
     def __init__(self, runner, ctrl=None):
         self.runner = runner
         self.chan = as_channel(ctrl)
