@@ -6,8 +6,11 @@ CLI = the union of resnet50_pytorch.py:28-70 and resnet50_horovod.py:18-62
 ``--data-dir`` (train/ + val/ ImageFolder), ``--model-dir``, ``--interpolation``,
 ``--val-resize-size`` 256, ``--val-crop-size``/``--train-crop-size`` 224,
 ``-j/--workers``, ``--wandb-project``/``--wandb-run``, ``--backend``; Horovod's
-``--fp16-allreduce``, ``--use-mixed-precision``, ``--gradient-predivide-factor``;
-``--use-adasum`` is accepted and falls back to averaging).
+``--fp16-allreduce``, ``--use-mixed-precision``, ``--gradient-predivide-factor``,
+``--use-adasum``: Horovod's Adasum combination (resnet50_horovod.py:115-139;
+``adasum_hook``, recursive doubling with per-tensor coefficients, LR not
+scaled by the world size -- the reference's "Adasum doesn't need scaling up
+learning rate").
 
 MI355X choices: DDP over RCCL with 100 MB buckets (fewer, larger ring
 all-reduces over the point-to-point xGMI links), gradient all-reduce
@@ -189,13 +192,20 @@ def main(argv=None):
         from ..utils import miopen
         miopen.configure()  # keep MIOpen's naive NHWC solvers out of the conv search
         model = model.to(memory_format=torch.channels_last)
+    adasum = args.use_adasum and world > 1
+    if adasum and world & (world - 1):
+        print(f"[resnet] --use-adasum needs a power-of-two world size (got {world}); averaging instead", flush=True)
+        adasum = False
     if world > 1:
         model = nn.parallel.DistributedDataParallel(model, device_ids=[dev.index] if use_cuda else None,
                                                     bucket_cap_mb=args.bucket_mb, gradient_as_bucket_view=True)
-        if args.fp16_allreduce or args.gradient_predivide_factor != 1.0:
+        if adasum:
+            model.register_comm_hook(state=AdasumState(dist.group.WORLD, args.fp16_allreduce), hook=adasum_hook)
+        elif args.fp16_allreduce or args.gradient_predivide_factor != 1.0:
             model.register_comm_hook(state=(dist.group.WORLD, args.fp16_allreduce, args.gradient_predivide_factor),
                                      hook=_compressed_allreduce_hook)
-    opt = torch.optim.SGD(model.parameters(), lr=args.lr * world, momentum=args.momentum)
+    # Horovod's LR scaler: x world for averaging, 1 for Adasum (resnet50_horovod.py:115-116)
+    opt = torch.optim.SGD(model.parameters(), lr=args.lr * (1 if adasum else world), momentum=args.momentum)
     sink = MetricsSink(str(args.log_dir), args.wandb_run or "resnet50",
                        project=args.wandb_project or "resnet50-imagenet", enabled=rank == 0)
     amp = args.use_mixed_precision and use_cuda
@@ -280,6 +290,63 @@ def _compressed_allreduce_hook(state, bucket):
         buf.copy_(r.to(buf.dtype).mul_(predivide / world))
         return buf
     return fut.then(done)
+
+
+class AdasumState:
+    def __init__(self, group, compress: bool = False):
+        self.group, self.compress = group, compress
+        self.segments: dict = {}  # bucket index -> (segment ids, n tensors)
+
+
+def adasum_pair(a: torch.Tensor, b: torch.Tensor, seg: torch.Tensor, n: int) -> torch.Tensor:
+    """Adasum of two flat gradient buffers, coefficients per tensor segment
+    (Maleki et al., Horovod's op=hvd.Adasum): (1 - a.b / 2|a|^2) a + (1 - a.b / 2|b|^2) b.
+    Symmetric in (a, b), so both partners of a pair compute the same bits."""
+    af, bf = a.float(), b.float()
+    dot = torch.zeros(n, device=a.device, dtype=torch.float64).index_add_(0, seg, (af * bf).double())
+    na = torch.zeros(n, device=a.device, dtype=torch.float64).index_add_(0, seg, (af * af).double())
+    nb = torch.zeros(n, device=a.device, dtype=torch.float64).index_add_(0, seg, (bf * bf).double())
+    ca = torch.where(na > 0, 1.0 - dot / (2.0 * na), torch.ones_like(na)).float()[seg]
+    cb = torch.where(nb > 0, 1.0 - dot / (2.0 * nb), torch.ones_like(nb)).float()[seg]
+    return (ca * af + cb * bf).to(a.dtype)
+
+
+def adasum_allreduce(buf: torch.Tensor, seg: torch.Tensor, n: int, group=None, compress: bool = False):
+    """In-place Adasum over all ranks of ``group`` (power-of-two size):
+    recursive doubling -- at level l every rank swaps its running result with
+    rank ^ 2^l and both combine the pair -- so after log2(W) exchanges every
+    rank holds Adasum(Adasum(g0, g1), Adasum(g2, g3)) ... in the same bits."""
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    cur = buf.to(torch.bfloat16) if compress else buf.clone()
+    lvl = 1
+    while lvl < world:
+        peer = rank ^ lvl
+        other = torch.empty_like(cur)
+        gpeer = dist.get_global_rank(group, peer) if group is not None and group != dist.group.WORLD else peer
+        ops = [dist.P2POp(dist.isend, cur, gpeer, group), dist.P2POp(dist.irecv, other, gpeer, group)]
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+        # lower rank's buffer first: both partners evaluate the identical expression
+        cur = adasum_pair(cur, other, seg, n) if rank < peer else adasum_pair(other, cur, seg, n)
+        lvl <<= 1
+    buf.copy_(cur.to(buf.dtype))
+    return buf
+
+
+def adasum_hook(state: AdasumState, bucket):
+    """DDP comm hook: the bucket's flat gradient is combined with Adasum, one
+    coefficient pair per parameter tensor of the bucket."""
+    buf = bucket.buffer()
+    key = bucket.index()
+    seg = state.segments.get(key)
+    if seg is None or seg[0].numel() != buf.numel():
+        ids = [torch.full((g.numel(),), i, dtype=torch.long) for i, g in enumerate(bucket.gradients())]
+        seg = (torch.cat(ids).to(buf.device), len(ids))
+        state.segments[key] = seg
+    adasum_allreduce(buf, seg[0], seg[1], state.group, state.compress)
+    fut = torch.futures.Future()
+    fut.set_result(buf)
+    return fut
 
 
 if __name__ == "__main__":
