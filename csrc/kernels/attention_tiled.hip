@@ -213,7 +213,11 @@ __device__ __forceinline__ void store_tile_lds(bf16_t* row0, long long st, const
   asm volatile("" ::: "memory");
 }
 
-template <int D, bool CAUSAL>
+// OC >= 0 ("ones column"): V's zero-padded column OC holds 1.0 for every key (the SD UNet's
+// padded QKV GEMM writes it through its bias), so O^T row OC accumulates the softmax row sum
+// sum_k bf16(P) on the matrix pipe: the per-element f32 adds of the row sum leave the VALU, which
+// bounds this loop at D = 64 (SD-1.5's 40-wide heads, padded).
+template <int D, bool CAUSAL, int OC = -1>
 __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel(FastFwdParams p) {
   constexpr int BM = 128, BN = 32;
   constexpr int TILE = BN * D * 2;           // bytes per K or V tile
@@ -364,11 +368,11 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel
     for (int r = 0; r < 8; ++r) {
       const float e0 = __builtin_amdgcn_exp2f(fmaf(sa[r], sl2, nm));
       const float e1 = __builtin_amdgcn_exp2f(fmaf(sa[r + 8], sl2, nm));
-      ps += e0 + e1;
+      if constexpr (OC < 0) ps += e0 + e1;
       pf0[r] = (__bf16)e0;
       pf1[r] = (__bf16)e1;
     }
-    lsum += ps;
+    if constexpr (OC < 0) lsum += ps;
     ASTAMP(2);
     {  // O^T += V^T P^T, V^T fragments one d-block ahead of their MFMAs
       auto vfrag = [&](int db, int s) {
@@ -419,7 +423,17 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel
   for (int t = max(nfree, 0); t < ntiles; ++t) tile_step(t, std::true_type{}, std::false_type{});
   }
 
-  const float ltot = lsum + __shfl_xor(lsum, 32, 64);
+  float ltot;
+  if constexpr (OC >= 0) {
+    // O^T row OC (d index) of query l32: register r = (OC & 3) + 4 * (OC >> 3) of d-block OC / 32 in
+    // the half hh = (OC >> 2) & 1; the other half reads it across
+    constexpr int ROW = OC % 32, RR = (ROW & 3) + 4 * (ROW >> 3), HH = (ROW >> 2) & 1;
+    const float mine = oacc[OC / 32][RR];
+    const float other = __shfl_xor(mine, 32, 64);
+    ltot = hh == HH ? mine : other;
+  } else {
+    ltot = lsum + __shfl_xor(lsum, 32, 64);
+  }
   // row sums past 2^100 (or inf / NaN) mean P may have overflowed: flag the
   // wave for the generic-kernel fixup (which then rewrites O and lse)
   const bool bad = !(ltot < 1.2676506e30f);
@@ -844,10 +858,11 @@ KCA_API int kca_attn_fwd_tiled(const void* q, const void* k, const void* v, void
                                long long k_st, long long k_sh, long long v_sb, long long v_st,
                                long long v_sh, long long o_sb, long long o_st, long long o_sh,
                                int B, int Sq, int Sk, int H, int Hkv, int d, int causal,
-                               float scale, int* flags, hipStream_t stream) {
+                               float scale, int rowsum_col, int* flags, hipStream_t stream) {
   if ((d != 64 && d != 96 && d != 128 && d != 160 && d != 256) || Sq % 128 || Sk % 32 || Sq <= 0 || H % Hkv ||
       !flags)
     return 1;
+  if (rowsum_col >= 0 && (rowsum_col != 40 || d != 64 || causal)) return 1;  // the one instantiated variant
   if (causal && Sk < Sq) return 1;
   FastFwdParams p{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, lse, flags,
                   q_sb, q_st, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh, o_sb, o_st, o_sh,
@@ -868,6 +883,7 @@ KCA_API int kca_attn_fwd_tiled(const void* q, const void* k, const void* v, void
     else hipLaunchKernelGGL((attn_fwd_tiled_kernel<96, false>), grid, dim3(256), 0, stream, p);
   } else {  // 64: GPT-2 / CLIP heads, SD-1.5 heads (40) zero-padded by the UNet inference path
     if (causal) hipLaunchKernelGGL((attn_fwd_tiled_kernel<64, true>), grid, dim3(256), 0, stream, p);
+    else if (rowsum_col == 40) hipLaunchKernelGGL((attn_fwd_tiled_kernel<64, false, 40>), grid, dim3(256), 0, stream, p);
     else hipLaunchKernelGGL((attn_fwd_tiled_kernel<64, false>), grid, dim3(256), 0, stream, p);
   }
   // a failed launch leaves the flags unwritten: report it so the caller runs

@@ -186,6 +186,8 @@ def padded_head_dim(hd: int) -> int:
 
 
 _PAD_HEADS = os.environ.get("KCA_SD_PAD_HEADS", "1") not in ("0", "false")
+ROWSUM_COL = 40  # SD-1.5's 40-wide heads: padded V column 40 carries ones (softmax row sums on the MFMA)
+_ROWSUM = os.environ.get("KCA_SD_ROWSUM_COL", "1") not in ("0", "false")
 _PAD_TRAIN = os.environ.get("KCA_SD_PAD_HEADS_TRAIN", "1") not in ("0", "false")
 _PAD_GEN = 0
 
@@ -227,6 +229,12 @@ class Attention(nn.Module):
                 if lin.bias is not None:
                     b[i, :, :hd] = lin.bias.view(H, hd)
             has_b = any(lin.bias is not None for lin in (self.to_q, self.to_k, self.to_v))
+            if dp == 64 and hd == ROWSUM_COL:
+                # V column 40 = 1 for every key (zero weights + unit bias): the D=64 attention kernel
+                # reads the softmax row sums off O's column 40 (ops.flash_attention rowsum_col);
+                # the out-projection's zero columns ignore it
+                b[2, :, ROWSUM_COL] = 1.0
+                has_b = True
             wo = self.to_out[0].weight
             wo_p = wo.new_zeros(wo.shape[0], H, dp)
             wo_p[:, :, :hd] = wo.view(wo.shape[0], H, hd)
@@ -259,7 +267,8 @@ class Attention(nn.Module):
             w, b, wo = self._padded_weights(hd, dpad)
             qkv = F.linear(x, w, b).view(B, S, 3, self.heads, dpad)
             o = ops.flash_attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], causal=False,
-                                    scale=1.0 / math.sqrt(hd))
+                                    scale=1.0 / math.sqrt(hd),
+                                    rowsum_col=ROWSUM_COL if (dpad == 64 and hd == ROWSUM_COL and _ROWSUM) else -1)
             return F.linear(o.reshape(B, S, -1), wo, self.to_out[0].bias)
         c = x if ctx is None else ctx
         q = self.to_q(x)

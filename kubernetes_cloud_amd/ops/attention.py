@@ -94,7 +94,7 @@ def _masks(kv_len):
     return (kv_len, None) if kv_len.dim() == 1 else (None, kv_len)
 
 
-def _fwd(q, k, v, causal, scale, kv_len, alibi, out=None, window: int = 0):
+def _fwd(q, k, v, causal, scale, kv_len, alibi, out=None, window: int = 0, rowsum_col: int = -1):
     B, Sq, H, D = q.shape
     Sk, Hkv = k.shape[1], k.shape[2]
     o = out if out is not None else torch.empty(B, Sq, H, D, device=q.device, dtype=q.dtype)
@@ -105,7 +105,7 @@ def _fwd(q, k, v, causal, scale, kv_len, alibi, out=None, window: int = 0):
     _lib.call("kca_attn_fwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr(),
               *_strides(q), *_strides(k), *_strides(v), *_strides(o),
               B, Sq, Sk, H, Hkv, D, int(causal), float(scale), _lib.ptr(alibi), _lib.ptr(lens),
-              int(window), _lib.ptr(km), flags.data_ptr(), _lib.stream())
+              int(window), _lib.ptr(km), int(rowsum_col), flags.data_ptr(), _lib.stream())
     return o, lse
 
 
@@ -166,11 +166,18 @@ def native_mask(kv_len, device):
 
 def flash_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool = False,
                     scale: float | None = None, kv_len: torch.Tensor | None = None,
-                    alibi: torch.Tensor | None = None, window: int = 0) -> torch.Tensor:
-    """softmax(scale * Q K^T + alibi + mask) V over [B, S, H, D] views."""
+                    alibi: torch.Tensor | None = None, window: int = 0, rowsum_col: int = -1) -> torch.Tensor:
+    """softmax(scale * Q K^T + alibi + mask) V over [B, S, H, D] views.
+    ``rowsum_col`` (inference): V's zero-padded column that the caller filled
+    with ones -- the D=64 fast kernel then takes the softmax row sums from the
+    output instead of summing on the VALU (the SD UNet's padded heads)."""
     scale = scale if scale is not None else 1.0 / math.sqrt(q.shape[-1])
     if alibi is not None:
         alibi = alibi.to(device=q.device, dtype=torch.float32).contiguous()
+    if rowsum_col >= 0 and _lib.use_native(q, k, v) and not torch.is_grad_enabled():
+        _check(q, k, v)
+        return _fwd(q, k, v, causal, scale, native_mask(kv_len, q.device), alibi, window=window,
+                    rowsum_col=rowsum_col)[0]
     if _lib.use_native(q, k, v):
         return _FlashAttnFn.apply(q, k, v, causal, scale, native_mask(kv_len, q.device), alibi, int(window))
     o, _ = attention_reference(q, k, v, causal, scale, kv_len, alibi, window)

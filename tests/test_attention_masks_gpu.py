@@ -119,3 +119,38 @@ def test_gpt_neo_engine_graphs_and_training_on_kernels():
     names = [e.name for e in prof.events()]
     assert not any("softmax" in n.lower() for n in names), [n for n in names if "softmax" in n.lower()][:5]
     assert any("attn" in n for n in names)
+
+
+def test_rowsum_column_variant_matches_reference():
+    """SD-1.5 padded heads (40 -> 64): V column 40 = 1 lets the D=64 kernel take
+    the softmax row sums from O; output equals the fp32 reference on the real
+    40 dims and is 1.0 in column 40."""
+    torch.manual_seed(7)
+    B, S, H = 2, 4096, 8
+    q, k, v = (torch.zeros(B, S, H, 64, device=DEV, dtype=torch.bfloat16) for _ in range(3))
+    for t in (q, k, v):
+        t[..., :40] = torch.randn(B, S, H, 40, device=DEV).bfloat16()
+    v[..., 40] = 1.0
+    with torch.no_grad():
+        o = ops.flash_attention(q, k, v, causal=False, scale=40 ** -0.5, rowsum_col=40)
+        o_plain = ops.flash_attention(q, k, v, causal=False, scale=40 ** -0.5)
+    ref, _ = attention_reference(q[..., :40], k[..., :40], v[..., :40], False, 40 ** -0.5)
+    assert _rel(o[..., :40], ref) < 1e-2
+    assert _rel(o_plain[..., :40], ref) < 1e-2
+    assert float((o[..., 40].float() - 1).abs().max()) < 2e-2
+
+
+def test_unet_padded_attention_rowsum_matches_unpadded():
+    from kubernetes_cloud_amd.models.unet import Attention
+    torch.manual_seed(3)
+    att = Attention(320, 8, 40).to(DEV).bfloat16().eval()
+    for p_ in att.parameters():
+        torch.nn.init.normal_(p_, std=0.05)
+    x = torch.randn(2, 4096, 320, device=DEV, dtype=torch.bfloat16)
+    with torch.no_grad():
+        fast = att(x)  # padded heads + rowsum column
+        q, k_, v = att.to_q(x), att.to_k(x), att.to_v(x)
+        ref, _ = attention_reference(q.view(2, 4096, 8, 40), k_.view(2, 4096, 8, 40), v.view(2, 4096, 8, 40),
+                                     False, 40 ** -0.5)
+        ref = att.to_out[0](ref.reshape(2, 4096, 320).to(torch.bfloat16))
+    assert _rel(fast, ref) < 2e-2
