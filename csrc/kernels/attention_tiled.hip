@@ -111,25 +111,71 @@ __device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) {
 template <int D, bool POW2 = (256 % (D / 8)) == 0>
 struct Stager;
 
-// D = 64 / 128 / 256: thread tid owns chunk column tid % NCH of rows tid / NCH + i * RPI
+// D = 64 / 128 / 256: thread tid owns chunk column tid % NCH of rows tid / NCH + i * RPI.
+// Loads go through buffer resources (T8): the per-thread byte offsets are loop constants in
+// VGPRs and the tile's row offset k0 * stride is ONE scalar -- no 64-bit address arithmetic on the
+// VALU per load, which at D = 64 (SD-1.5's padded heads) is VALU-issue-bound.
+// (-DKCA_ATTN_FLAT_LOADS: the flat-pointer form, A/B)
 template <int D>
 struct Stager<D, true> {
   static constexpr int NCH = D / 8, CPT = 32 * NCH / 256, RPI = 256 / NCH;
   long long ok_, ov_;  // element offset of this thread's first chunk in a K / V tile
   int row0_, ch_;
+#ifndef KCA_ATTN_FLAT_LOADS
+  __amdgpu_buffer_rsrc_t rk_, rv_;
+  int vok_[CPT], vov_[CPT];  // byte offsets of this thread's chunks (tile row 0)
+#endif
   __device__ __forceinline__ Stager(int tid, long long k_st, long long v_st) {
     row0_ = tid / NCH;
     ch_ = tid % NCH;
     ok_ = (long long)row0_ * k_st + ch_ * 8;
     ov_ = (long long)row0_ * v_st + ch_ * 8;
   }
+#ifndef KCA_ATTN_FLAT_LOADS
+  // kb / vb: the (batch, kv head) base pointers -- workgroup-uniform (readfirstlane'd so the
+  // descriptor is provably scalar: no waterfall loop, T20). Offsets stay < 2^31 bytes per head slice.
+  __device__ __forceinline__ void bind(const bf16_t* kb, const bf16_t* vb, long long k_st, long long v_st) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      vok_[i] = (int)((ok_ + (long long)i * RPI * k_st) * 2);
+      vov_[i] = (int)((ov_ + (long long)i * RPI * v_st) * 2);
+    }
+    set_base(kb, vb);
+  }
+  static __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const bf16_t* b) {
+    const unsigned long long a = (unsigned long long)b;
+    const unsigned long long au = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(a >> 32)) << 32) |
+                                  (unsigned)__builtin_amdgcn_readfirstlane((unsigned)a);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)au, (short)0, 0x7fffffff, 0x00020000);
+  }
+  // scalar work only: a kernel whose base changes per tile (dK/dV over GQA query heads) rebinds it
+  __device__ __forceinline__ void set_base(const bf16_t* kb, const bf16_t* vb) {
+    rk_ = rsrc(kb);
+    rv_ = rsrc(vb);
+  }
+#else
+  __device__ __forceinline__ void bind(const bf16_t*, const bf16_t*, long long, long long) {}
+  __device__ __forceinline__ void set_base(const bf16_t*, const bf16_t*) {}
+#endif
   __device__ __forceinline__ void load(u32x4 (&sk)[CPT], u32x4 (&sv)[CPT], const bf16_t* kb, const bf16_t* vb,
                                        int k0, long long k_st, long long v_st) const {
+#ifndef KCA_ATTN_FLAT_LOADS
+    const int sok = __builtin_amdgcn_readfirstlane((int)(k0 * k_st * 2));
+    const int sov = __builtin_amdgcn_readfirstlane((int)(k0 * v_st * 2));
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const auto a = __builtin_amdgcn_raw_buffer_load_b128(rk_, vok_[i], sok, 0);
+      const auto b = __builtin_amdgcn_raw_buffer_load_b128(rv_, vov_[i], sov, 0);
+      sk[i] = *reinterpret_cast<const u32x4*>(&a);
+      sv[i] = *reinterpret_cast<const u32x4*>(&b);
+    }
+#else
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
       sk[i] = *reinterpret_cast<const u32x4*>(kb + ok_ + (long long)(k0 + i * RPI) * k_st);
       sv[i] = *reinterpret_cast<const u32x4*>(vb + ov_ + (long long)(k0 + i * RPI) * v_st);
     }
+#endif
   }
   __device__ __forceinline__ void store(const u32x4 (&sk)[CPT], const u32x4 (&sv)[CPT], char* buf) const {
 #pragma unroll
@@ -162,6 +208,8 @@ struct Stager<D, false> {
     }
     tail_ = tid + 256 * (CPT - 1) < TOT;
   }
+  __device__ __forceinline__ void bind(const bf16_t*, const bf16_t*, long long, long long) {}
+  __device__ __forceinline__ void set_base(const bf16_t*, const bf16_t*) {}
   __device__ __forceinline__ void load(u32x4 (&sk)[CPT], u32x4 (&sv)[CPT], const bf16_t* kb, const bf16_t* vb,
                                        int k0, long long k_st, long long v_st) const {
     const bf16_t* kr = kb + (long long)k0 * k_st;
@@ -261,7 +309,8 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel
   float m = 0.f, lsum = 0.f;  // m: reference max (log2 units), set by tile 0
 
   // staging: thread handles chunks idx = tid + i*256 (Stager)
-  const Stager<D> stg(tid, p.k_st, p.v_st);
+  Stager<D> stg(tid, p.k_st, p.v_st);
+  stg.bind(kp, vp, p.k_st, p.v_st);
   u32x4 sk[CPT], sv[CPT];
 
   // per-lane read bases (bytes)
@@ -557,7 +606,8 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq_tiled_kernel(FastBwdParams
 
   const bf16_t* kst = p.k + b * p.k_sb + hk * p.k_sh;
   const bf16_t* vst = p.v + b * p.v_sb + hk * p.v_sh;
-  const Stager<D> stg(tid, p.k_st, p.v_st);
+  Stager<D> stg(tid, p.k_st, p.v_st);
+  stg.bind(kst, vst, p.k_st, p.v_st);
   u32x4 sk[CPT], sv[CPT];
   int be, bo, b1, b2;
   row_bases<D>(l32, hh, be, bo);
@@ -698,7 +748,8 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_tiled_kernel(FastBwdPara
   const int nqt = (p.Sq - q_lo) / BQ;
   const int total = nqt * grp;
 
-  const Stager<D> stg(tid, p.q_st, p.do_st);
+  Stager<D> stg(tid, p.q_st, p.do_st);
+  stg.bind(p.q + b * p.q_sb + hk * grp * p.q_sh, p.dout + b * p.do_sb + hk * grp * p.do_sh, p.q_st, p.do_st);
   u32x4 sq[CPT], sg[CPT];
   float lreg = 0.f;
   int be, bo, b1, b2;
@@ -708,6 +759,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_tiled_kernel(FastBwdPara
 #define KCA_DKDV_LOAD(it_)                                                                     \
   {                                                                                            \
     const int hq_ = hk * grp + (it_) / nqt, qt_ = q_lo + ((it_) % nqt) * BQ;                   \
+    if (grp > 1) stg.set_base(p.q + b * p.q_sb + hq_ * p.q_sh, p.dout + b * p.do_sb + hq_ * p.do_sh); \
     stg.load(sq, sg, p.q + b * p.q_sb + hq_ * p.q_sh, p.dout + b * p.do_sb + hq_ * p.do_sh, qt_,   \
              p.q_st, p.do_st);                                                                 \
     if (tid < 64) {                                                                            \
@@ -849,6 +901,10 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_tiled_kernel(FastBwdPara
   ASTAMP_FLUSH(32);
 }
 
+// the staged K/V (dK/dV: Q/dO) rows are addressed as 32-bit byte offsets from a
+// per-head buffer resource; longer rows fall back to the generic kernel
+inline bool offsets_fit(long long rows, long long stride) { return (rows + 128) * stride * 2 < (1ll << 31); }
+
 }  // namespace
 
 // Returns 0 when launched, 1 when the shape is outside the fast path (the
@@ -864,6 +920,7 @@ KCA_API int kca_attn_fwd_tiled(const void* q, const void* k, const void* v, void
     return 1;
   if (rowsum_col >= 0 && (rowsum_col != 40 || d != 64 || causal)) return 1;  // the one instantiated variant
   if (causal && Sk < Sq) return 1;
+  if (!offsets_fit(Sk, k_st) || !offsets_fit(Sk, v_st)) return 1;  // buffer-load byte offsets are 32-bit
   FastFwdParams p{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, lse, flags,
                   q_sb, q_st, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh, o_sb, o_st, o_sh,
                   B, Sq, Sk, H, Hkv, scale};
@@ -903,6 +960,7 @@ KCA_API int kca_attn_bwd_tiled(const void* q, const void* k, const void* v, cons
   if ((d != 64 && d != 96 && d != 128 && d != 160 && d != 256) || Sq % 128 || Sk % 128 || Sq <= 0 || H % Hkv)
     return 1;
   if (causal && Sk < Sq) return 1;
+  if (!offsets_fit(Sk, k_st) || !offsets_fit(Sk, v_st) || !offsets_fit(Sq, q_st) || !offsets_fit(Sq, do_st)) return 1;
   FastBwdParams p{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout,
                   (bf16_t*)dq, (bf16_t*)dk, (bf16_t*)dv, lse, delta,
                   q_sb, q_st, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh, do_sb, do_st, do_sh,

@@ -70,24 +70,33 @@ def _sources(sub, exts):
     return sorted(os.path.join(d, f) for f in os.listdir(d) if f.endswith(exts))
 
 
-def build_kernels(jobs: int = 8, verbose: bool = False, debug: bool = False, stamps: bool = False) -> str:
+def build_kernels(jobs: int = 8, verbose: bool = False, debug: bool = False, stamps: bool = False,
+                  ab_define: str | None = None) -> str:
     """``debug``: libkca_kernels_debug.so with the KCA_DASSERT bounds checks
     compiled in (csrc/kernels/common.h), loaded by ops/_lib.py when KCA_DEBUG=1.
     ``stamps``: ab/libkca_kernels_stamps.so, the diagnostic build with the
     attention kernels' in-loop s_memtime segment sums (bench/attn_stamps.py,
-    loaded through KCA_KERNEL_LIB); never the library the framework loads."""
+    loaded through KCA_KERNEL_LIB); never the library the framework loads.
+    ``ab_define``: ab/libkca_kernels_<define>.so built with -D<define>, the
+    other arm of a same-box A/B (loaded through KCA_KERNEL_LIB)."""
     srcs = _sources("kernels", (".hip",)) + _sources("comm", (".hip",))
     hdrs = _sources("kernels", (".h",)) + _sources("comm", (".h",))
     obj_dir = os.path.join(BUILD, "kernels_debug" if debug else ("kernels_stamps" if stamps else "kernels"))
+    if ab_define:
+        obj_dir = os.path.join(BUILD, "kernels_" + ab_define.lower())
     os.makedirs(obj_dir, exist_ok=True)
     os.makedirs(OUT_DIR, exist_ok=True)
-    flags = HIP_FLAGS + (["-DKCA_DEBUG", "-g"] if debug else []) + (["-DKCA_ATTN_STAMPS"] if stamps else [])
+    flags = HIP_FLAGS + (["-DKCA_DEBUG", "-g"] if debug else []) + (["-DKCA_ATTN_STAMPS"] if stamps else []) + (
+        [f"-D{ab_define}"] if ab_define else [])
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(lambda s: _compile([HIPCC], s, hdrs, obj_dir, flags), srcs))
     out = os.path.join(OUT_DIR, "libkca_kernels_debug.so" if debug else "libkca_kernels.so")
     if stamps:
         os.makedirs(os.path.join(ROOT, "ab"), exist_ok=True)
         out = os.path.join(ROOT, "ab", "libkca_kernels_stamps.so")
+    if ab_define:
+        os.makedirs(os.path.join(ROOT, "ab"), exist_ok=True)
+        out = os.path.join(ROOT, "ab", f"libkca_kernels_{ab_define.lower()}.so")
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp"] + objs
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
@@ -163,7 +172,11 @@ if __name__ == "__main__":
     ap.add_argument("--debug", action="store_true", help="only the KCA_DASSERT debug kernel library")
     ap.add_argument("--sanitize", action="store_true", help="build + run the ASan/UBSan host harness")
     ap.add_argument("--stamps", action="store_true", help="only the attention stamp diagnostic library (ab/)")
+    ap.add_argument("--ab-define", help="only an A/B kernel library built with -D<this> (ab/)")
     a = ap.parse_args()
+    if a.ab_define:
+        build_kernels(a.jobs, True, ab_define=a.ab_define)
+        sys.exit(0)
     if a.stamps:
         build_kernels(a.jobs, True, stamps=True)
         sys.exit(0)
