@@ -27,7 +27,8 @@ SHAPES = {
     "gpt2": (16, 1024, 1024, 12, 64, True),
     "bloom_tp8": (4, 2048, 2048, 14, 128, True),
     "sd_64": (16, 4096, 4096, 8, 40, False),
-    "sd_64_pad64": (16, 4096, 4096, 8, 64, False),  # SD heads zero-padded 40 -> 64 (UNet inference path)
+    "sd_64_pad64": (16, 4096, 4096, 8, 64, False),  # SD heads zero-padded 40 -> 64 (UNet training path)
+    "sd_64_pad48": (16, 4096, 4096, 8, 48, False),  # 40 -> 48 narrow storage (UNet inference path; fwd only)
     "sd_32": (16, 1024, 1024, 8, 80, False),
     "sd_32_pad96": (16, 1024, 1024, 8, 96, False),  # 80 -> 96 (UNet padding onto the D=96 full-tile kernels)
     "sd_16": (16, 256, 256, 8, 160, False),

@@ -105,6 +105,15 @@ __device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) {
   return pack_bf16x2(lo, hi);
 }
 
+// buffer resource over one (batch, head) slice; the base is workgroup-uniform (readfirstlane'd so
+// the descriptor is provably scalar: no waterfall loop, T20)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t head_rsrc(const bf16_t* b) {
+  const unsigned long long a = (unsigned long long)b;
+  const unsigned long long au = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(a >> 32)) << 32) |
+                                (unsigned)__builtin_amdgcn_readfirstlane((unsigned)a);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)au, (short)0, 0x7fffffff, 0x00020000);
+}
+
 // Staging of a 32-row x D tile by the 256 threads of a workgroup: chunk idx = tid + 256*i is
 // (row idx / NCH, 16-B chunk idx % NCH). D = 96 / 160 serve SD-1.5's 80-wide heads (padded to
 // 96) and its 160-wide heads (native) instead of padding them to 128 / 256.
@@ -142,16 +151,10 @@ struct Stager<D, true> {
     }
     set_base(kb, vb);
   }
-  static __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const bf16_t* b) {
-    const unsigned long long a = (unsigned long long)b;
-    const unsigned long long au = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(a >> 32)) << 32) |
-                                  (unsigned)__builtin_amdgcn_readfirstlane((unsigned)a);
-    return __builtin_amdgcn_make_buffer_rsrc((void*)au, (short)0, 0x7fffffff, 0x00020000);
-  }
   // scalar work only: a kernel whose base changes per tile (dK/dV over GQA query heads) rebinds it
   __device__ __forceinline__ void set_base(const bf16_t* kb, const bf16_t* vb) {
-    rk_ = rsrc(kb);
-    rv_ = rsrc(vb);
+    rk_ = head_rsrc(kb);
+    rv_ = head_rsrc(vb);
   }
 #else
   __device__ __forceinline__ void bind(const bf16_t*, const bf16_t*, long long, long long) {}
@@ -231,15 +234,58 @@ struct Stager<D, false> {
   }
 };
 
+// DS < D ("narrow storage"): heads stored DS wide in memory (SD-1.5's 40-wide heads padded to 48
+// instead of 64: 25 % fewer Q/K/V bytes and QKV-GEMM columns, 3 instead of 4 S MFMAs) staged into
+// the D-wide LDS image; image chunks DS/8 .. D/8-1 are never loaded (the kernel zeroes V's once).
+// 32 * DS/8 chunks per tile: threads below that count own one K and one V chunk, whole waves.
+template <int D, int DS>
+struct StagerNarrow {
+  static constexpr int NCH = DS / 8, TOT = 32 * NCH, CPT = 1;
+  static_assert(TOT <= 256 && TOT % 64 == 0, "narrow stager: one chunk per thread, whole waves");
+  int vok_[1], vov_[1], lds_;
+  bool on_;
+  __amdgpu_buffer_rsrc_t rk_, rv_;
+  __device__ __forceinline__ StagerNarrow(int tid, long long k_st, long long v_st) {
+    const int idx = min(tid, TOT - 1), row = idx / NCH, ch = idx % NCH;
+    vok_[0] = (int)(((long long)row * k_st + ch * 8) * 2);
+    vov_[0] = (int)(((long long)row * v_st + ch * 8) * 2);
+    lds_ = img_off<D>(row, ch);
+    on_ = tid < TOT;
+  }
+  __device__ __forceinline__ void bind(const bf16_t* kb, const bf16_t* vb, long long, long long) { set_base(kb, vb); }
+  __device__ __forceinline__ void set_base(const bf16_t* kb, const bf16_t* vb) {
+    rk_ = head_rsrc(kb);
+    rv_ = head_rsrc(vb);
+  }
+  __device__ __forceinline__ void load(u32x4 (&sk)[1], u32x4 (&sv)[1], const bf16_t*, const bf16_t*, int k0,
+                                       long long k_st, long long v_st) const {
+    const int sok = __builtin_amdgcn_readfirstlane((int)(k0 * k_st * 2));
+    const int sov = __builtin_amdgcn_readfirstlane((int)(k0 * v_st * 2));
+    const auto a = __builtin_amdgcn_raw_buffer_load_b128(rk_, vok_[0], sok, 0);
+    const auto b = __builtin_amdgcn_raw_buffer_load_b128(rv_, vov_[0], sov, 0);
+    sk[0] = *reinterpret_cast<const u32x4*>(&a);
+    sv[0] = *reinterpret_cast<const u32x4*>(&b);
+  }
+  __device__ __forceinline__ void store(const u32x4 (&sk)[1], const u32x4 (&sv)[1], char* buf) const {
+    if (on_) {
+      *reinterpret_cast<u32x4*>(buf + lds_) = sk[0];
+      *reinterpret_cast<u32x4*>(buf + 32 * D * 2 + lds_) = sv[0];
+    }
+  }
+};
+
+template <int D, int DS>
+using StagerFor = std::conditional_t<DS == D, Stager<D>, StagerNarrow<D, DS>>;
+
 // Epilogue through LDS (cdna_hip_programming.md T21): the wave's 32 x D accumulator tile (row =
 // lane & 31) goes into a wave-private [32][D] bf16 LDS image -- 16-B chunks rotated by the row,
 // so the per-lane 8-B writes and the row-contiguous 16-B reads are both conflict-free -- and every
 // store instruction then writes two whole rows with 16-B stores, instead of 8-B stores that each
 // touch 64 rows. `mul` is the lane's row scale. The LDS must be free (after the loop's barrier).
-template <int D>
+template <int D, int DS = D>
 __device__ __forceinline__ void store_tile_lds(bf16_t* row0, long long st, const f32x16 (&acc)[D / 32], int lane,
                                                float mul, char* lds) {
-  constexpr int NCH = D / 8, RB = D * 2;
+  constexpr int NCH = D / 8, RB = D * 2, NCS = DS / 8;  // NCS: stored chunks per row
   const int l32 = lane & 31, hh = lane >> 5;
 #pragma unroll
   for (int db = 0; db < D / 32; ++db) {
@@ -252,9 +298,10 @@ __device__ __forceinline__ void store_tile_lds(bf16_t* row0, long long st, const
     }
   }
   asm volatile("" ::: "memory");  // the wave's LDS accesses execute in order: reads see its writes
+  static_assert((32 * NCS) % 64 == 0, "whole-wave epilogue rounds");
 #pragma unroll
-  for (int j = 0; j < NCH / 2; ++j) {
-    const int idx = j * 64 + lane, r = idx / NCH, c = idx % NCH;
+  for (int j = 0; j < 32 * NCS / 64; ++j) {
+    const int idx = j * 64 + lane, r = idx / NCS, c = idx % NCS;
     const uint4 v = *reinterpret_cast<const uint4*>(lds + r * RB + ((c + r) % NCH) * 16);
     *reinterpret_cast<uint4*>(row0 + (long long)r * st + c * 8) = v;
   }
@@ -265,11 +312,14 @@ __device__ __forceinline__ void store_tile_lds(bf16_t* row0, long long st, const
 // padded QKV GEMM writes it through its bias), so O^T row OC accumulates the softmax row sum
 // sum_k bf16(P) on the matrix pipe: the per-element f32 adds of the row sum leave the VALU, which
 // bounds this loop at D = 64 (SD-1.5's 40-wide heads, padded).
-template <int D, bool CAUSAL, int OC = -1>
+// DS < D: heads stored DS wide (StagerNarrow); the contraction over d runs DS / 16 MFMA steps.
+template <int D, bool CAUSAL, int OC = -1, int DS = D>
 __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel(FastFwdParams p) {
   constexpr int BM = 128, BN = 32;
-  constexpr int TILE = BN * D * 2;           // bytes per K or V tile
-  constexpr int CPT = Stager<D>::CPT;       // 16-B chunks per thread per tile
+  constexpr int TILE = BN * D * 2;           // bytes per K or V tile (LDS image)
+  constexpr int KS = DS / 16;                // S MFMA steps
+  using Stg = StagerFor<D, DS>;
+  constexpr int CPT = Stg::CPT;             // 16-B chunks per thread per tile
   __shared__ __attribute__((aligned(16))) char smem[3 * 2 * TILE];  // [buf 0..2][K|V]
 
   ASTAMP_DECL
@@ -296,9 +346,9 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel
 
   // Q^T fragments (B operand of S^T = K.Q^T): lane (q = l32, half hh) holds
   // Q[q][16s + 8hh .. +7].
-  bf16x8 qf[D / 16];
+  bf16x8 qf[KS];
 #pragma unroll
-  for (int s = 0; s < D / 16; ++s)
+  for (int s = 0; s < KS; ++s)
     qf[s] = *reinterpret_cast<const bf16x8*>(qp + (long long)qrow * p.q_st + 16 * s + 8 * hh);
 
   f32x16 oacc[D / 32];
@@ -309,9 +359,16 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel
   float m = 0.f, lsum = 0.f;  // m: reference max (log2 units), set by tile 0
 
   // staging: thread handles chunks idx = tid + i*256 (Stager)
-  Stager<D> stg(tid, p.k_st, p.v_st);
+  Stg stg(tid, p.k_st, p.v_st);
   stg.bind(kp, vp, p.k_st, p.v_st);
   u32x4 sk[CPT], sv[CPT];
+  if constexpr (DS < D) {  // V image chunks DS/8.. (read by the PV d-blocks, never loaded): zero once
+    constexpr int PC = D / 8 - DS / 8, NZ = 3 * 32 * PC;
+    for (int i = tid; i < NZ; i += 256) {
+      const int buf = i / (32 * PC), row = (i / PC) % 32, ch = DS / 8 + i % PC;
+      *reinterpret_cast<u32x4*>(smem + buf * 2 * TILE + TILE + img_off<D>(row, ch)) = u32x4{0, 0, 0, 0};
+    }
+  }
 
   // per-lane read bases (bytes)
   const int xr = (l32 >> 2) & 3;
@@ -337,8 +394,8 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel
     fa[1] = lds_b128(Ks, kb_o);
     __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
 #pragma unroll
-    for (int s = 0; s < D / 16; ++s) {
-      if (s + 2 < D / 16) {
+    for (int s = 0; s < KS; ++s) {
+      if (s + 2 < KS) {
         fa[(s + 2) % 3] = lds_b128(Ks, (((s + 2) & 1) ? kb_o : kb_e) + 512 * ((s + 2) >> 1));
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       }
@@ -491,8 +548,8 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel
   const float inv = ltot > 0.f ? 1.f / ltot : 0.f;
   if (hh == 0 && p.lse)
     p.lse[((long long)b * p.H + h) * p.Sq + qrow] = ltot > 0.f ? (m + log2f(ltot)) * kLn2 : INFINITY;
-  store_tile_lds<D>(p.o + b * p.o_sb + h * p.o_sh + (long long)q0 * p.o_st, p.o_st, oacc, lane, inv,
-                    smem + wave * 32 * D * 2);
+  store_tile_lds<D, DS>(p.o + b * p.o_sb + h * p.o_sh + (long long)q0 * p.o_st, p.o_st, oacc, lane, inv,
+                        smem + wave * 32 * D * 2);
   ASTAMP(5);
   ASTAMP_FLUSH(0);
 }
@@ -915,10 +972,11 @@ KCA_API int kca_attn_fwd_tiled(const void* q, const void* k, const void* v, void
                                long long v_sh, long long o_sb, long long o_st, long long o_sh,
                                int B, int Sq, int Sk, int H, int Hkv, int d, int causal,
                                float scale, int rowsum_col, int* flags, hipStream_t stream) {
-  if ((d != 64 && d != 96 && d != 128 && d != 160 && d != 256) || Sq % 128 || Sk % 32 || Sq <= 0 || H % Hkv ||
-      !flags)
+  if ((d != 48 && d != 64 && d != 96 && d != 128 && d != 160 && d != 256) || Sq % 128 || Sk % 32 || Sq <= 0 ||
+      H % Hkv || !flags)
     return 1;
-  if (rowsum_col >= 0 && (rowsum_col != 40 || d != 64 || causal)) return 1;  // the one instantiated variant
+  if (d == 48 && causal) return 1;  // narrow storage: SD-1.5's (non-causal) 40-wide heads
+  if (rowsum_col >= 0 && (rowsum_col != 40 || (d != 64 && d != 48) || causal)) return 1;  // instantiated variants
   if (causal && Sk < Sq) return 1;
   if (!offsets_fit(Sk, k_st) || !offsets_fit(Sk, v_st)) return 1;  // buffer-load byte offsets are 32-bit
   FastFwdParams p{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, lse, flags,
@@ -938,7 +996,10 @@ KCA_API int kca_attn_fwd_tiled(const void* q, const void* k, const void* v, void
   } else if (d == 96) {  // SD-1.5 640-channel heads (80) zero-padded by the UNet
     if (causal) hipLaunchKernelGGL((attn_fwd_tiled_kernel<96, true>), grid, dim3(256), 0, stream, p);
     else hipLaunchKernelGGL((attn_fwd_tiled_kernel<96, false>), grid, dim3(256), 0, stream, p);
-  } else {  // 64: GPT-2 / CLIP heads, SD-1.5 heads (40) zero-padded by the UNet inference path
+  } else if (d == 48) {  // SD-1.5 heads (40) zero-padded to 48 by the UNet inference path, D = 64 image
+    if (rowsum_col == 40) hipLaunchKernelGGL((attn_fwd_tiled_kernel<64, false, 40, 48>), grid, dim3(256), 0, stream, p);
+    else hipLaunchKernelGGL((attn_fwd_tiled_kernel<64, false, -1, 48>), grid, dim3(256), 0, stream, p);
+  } else {  // 64: GPT-2 / CLIP heads
     if (causal) hipLaunchKernelGGL((attn_fwd_tiled_kernel<64, true>), grid, dim3(256), 0, stream, p);
     else if (rowsum_col == 40) hipLaunchKernelGGL((attn_fwd_tiled_kernel<64, false, 40>), grid, dim3(256), 0, stream, p);
     else hipLaunchKernelGGL((attn_fwd_tiled_kernel<64, false>), grid, dim3(256), 0, stream, p);

@@ -47,11 +47,38 @@ __device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, flo
   }
 }
 
+// Where the normalised tensor's (n, pixel, channel) lives. SrcPlain: one [N, P, C] tensor.
+// SrcCat: the UNet up-block's channel concat [x1 | x2] read in place (no concatenated copy is
+// made for the norm), x1 optionally still in the sub-pixel phase layout of the upsampler's 2x2
+// conv ([N, H/2+1, W/2+1, 4*C1]: high-res pixel (y, x) is phase (y&1, x&1) of low-res position
+// (y>>1 + (y&1), x>>1 + (x&1)) -- models/unet.py phase_weights). C1 % 8 == 0: no 8-channel
+// vector straddles the two inputs.
+struct SrcPlain {
+  const bf16_t* x;
+  int C, P;
+  __device__ __forceinline__ const bf16_t* ptr(int n, int p, int c) const {
+    return x + ((long long)n * P + p) * C + c;
+  }
+};
+
+struct SrcCat {
+  const bf16_t* x1;
+  const bf16_t* x2;
+  int C1, C2, P, W, phase;
+  __device__ __forceinline__ const bf16_t* ptr(int n, int p, int c) const {
+    if (c >= C1) return x2 + ((long long)n * P + p) * C2 + (c - C1);
+    if (!phase) return x1 + ((long long)n * P + p) * C1 + c;
+    const int y = p / W, xx = p - y * W, a = y & 1, b = xx & 1;
+    const int hs1 = (P / W) / 2 + 1, ws1 = W / 2 + 1;
+    return x1 + (((long long)n * hs1 + (y >> 1) + a) * ws1 + (xx >> 1) + b) * 4 * C1 + (2 * a + b) * C1 + c;
+  }
+};
+
 // grid (chunks, N, channel slabs), block (slab vectors, R); a slab is <= 256
 // 8-channel vectors (C up to 2048 in one slab, the 2560-channel UNet up-block
 // concat takes two)
-__global__ void __launch_bounds__(256) nhwc_chunk_stats(const bf16_t* __restrict__ x, int P, int C,
-                                                        float* __restrict__ part) {
+template <typename Src>
+__global__ void __launch_bounds__(256) nhwc_chunk_stats(const Src src, int P, int C, float* __restrict__ part) {
   // Shifted sums: every thread accumulates sum(v - K) and sum((v - K)^2) with
   // K = the chunk's first pixel of that channel (one data point, so |mean - K|
   // is O(std) and the final M2 = S2 - S1^2/N does not cancel), as independent
@@ -65,16 +92,15 @@ __global__ void __launch_bounds__(256) nhwc_chunk_stats(const bf16_t* __restrict
   const bool live = cv * 8 < C;
   const int n = blockIdx.y, chunk = blockIdx.x, nchunks = gridDim.x, CH = chunk_of(P);
   const int p0 = chunk * CH, p1 = min(P, p0 + CH);
-  const bf16_t* base = x + ((long long)n * P) * C;
   float k[8], s1[8], s2[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
   if (live) {
-    load8(base + (long long)p0 * C + cv * 8, k);
+    load8(src.ptr(n, p0, cv * 8), k);
 #pragma unroll 4
     for (int p = p0 + r; p < p1; p += R) {
       float v[8];
-      load8(base + (long long)p * C + cv * 8, v);
+      load8(src.ptr(n, p, cv * 8), v);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float d = v[j] - k[j];
@@ -100,7 +126,7 @@ __global__ void __launch_bounds__(256) nhwc_chunk_stats(const bf16_t* __restrict
       t1 += a1[(j * R + rr) * bw + l];
       t2 += a2[(j * R + rr) * bw + l];
     }
-    const float kk = bf2f(base[(long long)p0 * C + c]);
+    const float kk = bf2f(*src.ptr(n, p0, c));
     float* dst = part + (((long long)n * nchunks + chunk) * C + c) * 2;
     dst[0] = kk + t1 * inv;
     dst[1] = fmaxf(t2 - t1 * t1 * inv, 0.f);
@@ -153,16 +179,31 @@ __global__ void __launch_bounds__(256) nhwc_group_stats(const float* __restrict_
   }
 }
 
-// y = x * scale[n, c] + shift[n, c] (+ SiLU); ss = [N][2][C] fp32
-__global__ void __launch_bounds__(256) nhwc_apply(const bf16_t* __restrict__ x, const float* __restrict__ ss,
-                                                  bf16_t* __restrict__ y, int P, int C, int silu, int nvec) {
+// y = x * scale[n, c] + shift[n, c] (+ SiLU); ss = [N][2][C] fp32; raw (optional): the input
+// itself, contiguous [N, P, C] (the concat the up-block's 1x1 shortcut conv consumes)
+template <typename Src>
+__global__ void __launch_bounds__(256) nhwc_apply(const Src src, const float* __restrict__ ss,
+                                                  bf16_t* __restrict__ y, bf16_t* __restrict__ raw,
+                                                  const float* __restrict__ radd, int P, int C, int silu, int nvec) {
   const int cv8 = C / 8;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += gridDim.x * blockDim.x) {
     const int pix = i / cv8;
     const int c0 = (i - pix * cv8) * 8;
     const int n = pix / P;
     float v[8], sc[8], sh[8];
-    load8(x + (long long)i * 8, v);
+    const bf16_t* xp = src.ptr(n, pix - n * P, c0);
+    load8(xp, v);
+    if (raw) {
+      if (radd) {  // the per-(n, c) pre-add (the upsampler conv's bias) applies to the copy too
+        float t[8], a[8];
+        load8f(radd + (long long)n * C + c0, a);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) t[j] = v[j] + a[j];
+        store8(raw + (long long)i * 8, t);
+      } else {
+        *reinterpret_cast<uint4*>(raw + (long long)i * 8) = *reinterpret_cast<const uint4*>(xp);
+      }
+    }
     load8f(ss + (long long)n * 2 * C + c0, sc);
     load8f(ss + ((long long)n * 2 + 1) * C + c0, sh);
 #pragma unroll
@@ -387,13 +428,42 @@ KCA_API int kca_groupnorm_nhwc_fwd_add(const void* x, const void* w, const void*
   if ((long long)N * P * C / 8 >= (1LL << 31)) return 2;
   const int nchunks = (P + chunk_of(P) - 1) / chunk_of(P);
   const size_t smem = 2 * block.y * block.x * 8 * sizeof(float);
-  hipLaunchKernelGGL(nhwc_chunk_stats, dim3(nchunks, N, slabs), block, smem, stream, (const bf16_t*)x, P, C, ws);
+  const SrcPlain src{(const bf16_t*)x, C, P};
+  hipLaunchKernelGGL(nhwc_chunk_stats<SrcPlain>, dim3(nchunks, N, slabs), block, smem, stream, src, P, C, ws);
   float* ss = ws + 2LL * N * nchunks * C;
   hipLaunchKernelGGL(nhwc_group_stats, dim3(N * G), dim3(256), 0, stream, ws, P, C, G, nchunks, eps, mean, rstd,
                      (const bf16_t*)w, (const bf16_t*)b, ss, add);
   const int nvec = (int)((long long)N * P * C / 8);
-  hipLaunchKernelGGL(nhwc_apply, dim3(kca_grid(nvec, 256, 8192)), dim3(256), 0, stream, (const bf16_t*)x, ss,
-                     (bf16_t*)y, P, C, silu, nvec);
+  hipLaunchKernelGGL(nhwc_apply<SrcPlain>, dim3(kca_grid(nvec, 256, 8192)), dim3(256), 0, stream, src, ss,
+                     (bf16_t*)y, (bf16_t*)nullptr, (const float*)nullptr, P, C, silu, nvec);
+  return 0;
+}
+
+// Inference GroupNorm(+SiLU) of the channel concat [x1 | x2] ([N, P, C1] and [N, P, C2], or x1 in
+// the upsampler's phase layout when phase_w > 0 = the high-res width W, P = H * W) without
+// materialising the concat for the norm: y = GN([x1 | x2]) ([N, P, C1 + C2]) and, when raw is
+// given, the concat itself (the 1x1 shortcut's input) written by the same apply pass. add
+// (optional, fp32 [N, C1 + C2]): added to the input before both (the upsampler conv's bias).
+KCA_API int kca_groupnorm_nhwc_cat_fwd(const void* x1, const void* x2, const void* w, const void* b,
+                                       const float* add, void* y, void* raw, float* mean, float* rstd, float* ws,
+                                       int N, int P, int C1, int C2, int phase_w, int G, float eps, int silu,
+                                       hipStream_t stream) {
+  const int C = C1 + C2;
+  dim3 block;
+  int slabs;
+  if (!x1 || !x2 || C1 % 8 || C2 % 8 || !geometry(C, G, block, slabs) || N <= 0 || P <= 0) return 1;
+  if (phase_w > 0 && (phase_w % 2 || P % phase_w || (P / phase_w) % 2)) return 1;
+  if ((long long)N * P * C / 8 >= (1LL << 31)) return 2;
+  const int nchunks = (P + chunk_of(P) - 1) / chunk_of(P);
+  const size_t smem = 2 * block.y * block.x * 8 * sizeof(float);
+  const SrcCat src{(const bf16_t*)x1, (const bf16_t*)x2, C1, C2, P, phase_w > 0 ? phase_w : 1, phase_w > 0};
+  hipLaunchKernelGGL(nhwc_chunk_stats<SrcCat>, dim3(nchunks, N, slabs), block, smem, stream, src, P, C, ws);
+  float* ss = ws + 2LL * N * nchunks * C;
+  hipLaunchKernelGGL(nhwc_group_stats, dim3(N * G), dim3(256), 0, stream, ws, P, C, G, nchunks, eps, mean, rstd,
+                     (const bf16_t*)w, (const bf16_t*)b, ss, add);
+  const int nvec = (int)((long long)N * P * C / 8);
+  hipLaunchKernelGGL(nhwc_apply<SrcCat>, dim3(kca_grid(nvec, 256, 8192)), dim3(256), 0, stream, src, ss,
+                     (bf16_t*)y, (bf16_t*)raw, add, P, C, silu, nvec);
   return 0;
 }
 

@@ -25,7 +25,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
-from ..ops.linear import SplitKLinear, linear_splitk_wgrad
+from ..ops.linear import SplitKLinear, linear_residual, linear_splitk_wgrad
 
 
 @dataclasses.dataclass
@@ -154,12 +154,21 @@ class ResnetBlock2D(nn.Module):
         sc = self.conv_shortcut(x) if self.conv_shortcut is not None else x
         return sc + h
 
-    def _forward_folded(self, x, temb):
+    def forward_cat(self, x1, x2, temb):
+        """Inference on the up-block input ``cat([x1, x2])`` (x1 possibly a _Phased upsampler
+        output): norm1 reads both in place and writes the concat once, for the 1x1 shortcut."""
+        ph = isinstance(x1, _Phased)
+        xn, raw = ops.group_norm_cat(x1.t if ph else x1, x2, self.norm1.num_groups, self.norm1.weight,
+                                     self.norm1.bias, self.norm1.eps, silu=True, phase=ph,
+                                     x1_add=x1.bias if ph else None)
+        return self._forward_folded(raw, temb, xn=xn)
+
+    def _forward_folded(self, x, temb, xn=None):
         """Inference: the convolutions run without bias (MIOpen adds a conv bias in a separate
         broadcast pass over the whole output): conv1's bias joins the time embedding that norm2
         adds inside its statistics, and conv2's (+ the 1x1 shortcut's) bias joins the residual add
         -- one full read+write pass fewer per convolution (profiles/sd_unet_add_attribution_r2.txt)."""
-        h = F.conv2d(self.norm1(x), self.conv1.weight, None, padding=1)
+        h = F.conv2d(self.norm1(x) if xn is None else xn, self.conv1.weight, None, padding=1)
         add = self.conv1.bias.float()[None].expand(x.shape[0], -1)
         if self.time_emb_proj is not None and temb is not None:
             add = add + self.time_emb_proj(F.silu(temb)).float()
@@ -177,12 +186,16 @@ class ResnetBlock2D(nn.Module):
 # Head padding for the self-attention (see Attention.forward); KCA_SD_PAD_HEADS=0
 # disables it, KCA_SD_PAD_HEADS_TRAIN=0 only in training. _PAD_GEN counts padded-weight rebuilds so a HIP
 # graph captured over the old buffers knows to re-capture (sd_pipeline.UNetGraph).
-_TILED_DIMS = (64, 96, 128, 160, 256)  # attention_tiled.hip instantiations
+_TILED_DIMS = (64, 96, 128, 160, 256)  # attention_tiled.hip instantiations (fwd + bwd)
+# forward-only narrow storage: heads stored 48 wide, staged into the D=64 LDS image
+# (attention_tiled.hip StagerNarrow); KCA_SD_NARROW_HEADS=0 pads inference heads to 64 as training does
+_NARROW = os.environ.get("KCA_SD_NARROW_HEADS", "1") not in ("0", "false")
 
 
-def padded_head_dim(hd: int) -> int:
-    """Smallest full-tile head dim >= hd: 40 -> 64, 80 -> 96 (160 runs natively)."""
-    return next((d for d in _TILED_DIMS if d >= hd), hd)
+def padded_head_dim(hd: int, infer: bool = False) -> int:
+    """Smallest full-tile head dim >= hd: 40 -> 64 (inference: 48), 80 -> 96 (160 runs natively)."""
+    dims = ((48,) if infer and _NARROW else ()) + _TILED_DIMS
+    return next((d for d in dims if d >= hd), hd)
 
 
 _PAD_HEADS = os.environ.get("KCA_SD_PAD_HEADS", "1") not in ("0", "false")
@@ -190,6 +203,13 @@ ROWSUM_COL = 40  # SD-1.5's 40-wide heads: padded V column 40 carries ones (soft
 _ROWSUM = os.environ.get("KCA_SD_ROWSUM_COL", "1") not in ("0", "false")
 _PAD_TRAIN = os.environ.get("KCA_SD_PAD_HEADS_TRAIN", "1") not in ("0", "false")
 _PAD_GEN = 0
+# inference: residual adds carried by the preceding GEMM's epilogue (ops.linear_residual);
+# KCA_SD_FUSE_RES=0 keeps the separate adds (A/B knob)
+_FUSE_RES = os.environ.get("KCA_SD_FUSE_RES", "1") not in ("0", "false")
+# inference: upsamplers as one 2x2 phase conv of the low-res input (phase_weights), whose output the
+# next up-block's concat GroupNorm reads in place (ops.group_norm_cat): no upsampled activation, no
+# concatenated copy for the norm
+_FUSE_UP = os.environ.get("KCA_SD_FUSE_UP", "0") in ("1", "true")
 
 
 def pad_generation() -> int:
@@ -229,10 +249,10 @@ class Attention(nn.Module):
                 if lin.bias is not None:
                     b[i, :, :hd] = lin.bias.view(H, hd)
             has_b = any(lin.bias is not None for lin in (self.to_q, self.to_k, self.to_v))
-            if dp == 64 and hd == ROWSUM_COL:
-                # V column 40 = 1 for every key (zero weights + unit bias): the D=64 attention kernel
-                # reads the softmax row sums off O's column 40 (ops.flash_attention rowsum_col);
-                # the out-projection's zero columns ignore it
+            if dp in (48, 64) and hd == ROWSUM_COL:
+                # V column 40 = 1 for every key (zero weights + unit bias): the D=64-image attention
+                # kernel reads the softmax row sums off O's column 40 (ops.flash_attention
+                # rowsum_col); the out-projection's zero columns ignore it
                 b[2, :, ROWSUM_COL] = 1.0
                 has_b = True
             wo = self.to_out[0].weight
@@ -245,9 +265,10 @@ class Attention(nn.Module):
     def forward(self, x, ctx=None):
         B, S, _ = x.shape
         hd = self.to_q.weight.shape[0] // self.heads
-        dpad = padded_head_dim(hd)
+        train = torch.is_grad_enabled()
+        dpad = padded_head_dim(hd, infer=not train)
         pad = ctx is None and x.is_cuda and dpad != hd and hd % 8 == 0 and S % 128 == 0 and _PAD_HEADS
-        if pad and torch.is_grad_enabled() and _PAD_TRAIN:
+        if pad and train and _PAD_TRAIN:
             # training: pad the q/k/v activations instead (F.pad's backward slices the
             # gradients back) so the backward also runs the full-tile D=64 kernels.
             # Attention fwd+bwd 4.50 -> 3.31 ms; DreamBooth 93.4 -> 96.4 samples/s
@@ -258,17 +279,18 @@ class Attention(nn.Module):
                        for lin in (self.to_q, self.to_k, self.to_v))
             o = ops.flash_attention(q, k, v, causal=False, scale=1.0 / math.sqrt(hd))
             return self.to_out[0](o[..., :hd].reshape(B, S, -1))
-        if pad and not torch.is_grad_enabled():
-            # inference self-attention on the full-tile kernels (attention_tiled.hip, D=64 for
-            # the 40-wide heads, D=96 for the 80-wide ones): zero q/k columns leave Q.K^T
-            # unchanged, zero v columns give zero outputs that meet zero out-projection columns.
-            # SD-1.5 64x64-latent self-attention (B16 H8 S4096 d40) 1.04 -> 0.71 ms on MI355X
-            # (profiles/attn_bench_r1_v7_d64.jsonl).
+        if pad and not train:
+            # inference self-attention on the full-tile kernels (attention_tiled.hip: the 40-wide
+            # heads stored 48 wide in a D=64 LDS image, the 80-wide ones padded to 96): zero q/k
+            # columns leave Q.K^T unchanged, zero v columns give zero outputs that meet zero
+            # out-projection columns. SD-1.5 64x64-latent self-attention (B16 H8 S4096 d40)
+            # 1.04 -> 0.71 ms on MI355X at 64 wide (profiles/attn_bench_r1_v7_d64.jsonl).
             w, b, wo = self._padded_weights(hd, dpad)
             qkv = F.linear(x, w, b).view(B, S, 3, self.heads, dpad)
             o = ops.flash_attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], causal=False,
                                     scale=1.0 / math.sqrt(hd),
-                                    rowsum_col=ROWSUM_COL if (dpad == 64 and hd == ROWSUM_COL and _ROWSUM) else -1)
+                                    rowsum_col=ROWSUM_COL if (dpad in (48, 64) and hd == ROWSUM_COL and _ROWSUM)
+                                    else -1)
             return F.linear(o.reshape(B, S, -1), wo, self.to_out[0].bias)
         c = x if ctx is None else ctx
         q = self.to_q(x)
@@ -313,6 +335,9 @@ class BasicTransformerBlock(nn.Module):
         # the residual adds after attn1 / attn2 ride in the next LayerNorm kernel
         n2, x = self.norm2(self.attn1(self.norm1(x)), residual=(x,))
         n3, x = self.norm3(self.attn2(n2, ctx), residual=(x,))
+        if _FUSE_RES and not torch.is_grad_enabled():  # FF out-projection + bias + residual: one GEMM
+            out = self.ff.net[2]
+            return linear_residual(self.ff.net[0](n3), out.weight, out.bias, x)
         return x + self.ff(n3)
 
 
@@ -336,6 +361,11 @@ class Transformer2DModel(nn.Module):
             t = _proj(self.proj_in, t)
             for blk in self.transformer_blocks:
                 t = blk(t, ctx)
+            if _FUSE_RES and not torch.is_grad_enabled():  # proj_out + bias + residual: one GEMM
+                w = self.proj_out.weight
+                o = linear_residual(t, w.reshape(w.shape[0], w.shape[1]), self.proj_out.bias,
+                                    res.permute(0, 2, 3, 1))
+                return o.permute(0, 3, 1, 2)
             t = _proj(self.proj_out, t)
             return t.view(B, H, W, C).permute(0, 3, 1, 2) + res
         if self.linear_proj:
@@ -393,13 +423,57 @@ class Downsample2D(nn.Module):
         return self.conv(x)
 
 
+# nearest-x2 then 3x3 conv (padding 1) == per output phase (a, b) a 2x2 conv of the low-resolution
+# input (padding 1, output window offset (a, b)) whose taps sum the 3x3 taps that land on the same
+# input pixel: rows/cols {0} {1,2} for phase 0 and {0,1} {2} for phase 1
+_PHASE_TAPS = (((0,), (1, 2)), ((0, 1), (2,)))
+
+
+def phase_weights(w: torch.Tensor) -> torch.Tensor:
+    """[Cout, Cin, 3, 3] -> [4 * Cout, Cin, 2, 2]: output channel block k = 2a + b holds phase (a, b)."""
+    wf = w.float()
+    out = wf.new_zeros(4, w.shape[0], w.shape[1], 2, 2)
+    for a in range(2):
+        for b in range(2):
+            for s_ in range(2):
+                for t in range(2):
+                    rows, cols = _PHASE_TAPS[a][s_], _PHASE_TAPS[b][t]
+                    out[2 * a + b, :, :, s_, t] = wf[:, :, list(rows)][:, :, :, list(cols)].sum(dim=(2, 3))
+    return out.reshape(4 * w.shape[0], w.shape[1], 2, 2).to(w.dtype)
+
+
 class Upsample2D(nn.Module):
     def __init__(self, ch):
         super().__init__()
         self.conv = nn.Conv2d(ch, ch, 3, padding=1)
 
     def forward(self, x):
+        if (_FUSE_UP and not torch.is_grad_enabled() and x.is_cuda and x.dtype == torch.bfloat16 and _is_cl(x)
+                and x.shape[1] % 8 == 0):
+            cw = self.conv.weight
+            key = (cw.data_ptr(), cw._version)
+            w = getattr(self, "_phase_w", None)
+            if w is None or w[0] != key:  # re-derived when the conv weight is replaced or updated
+                w = self._phase_w = (key, phase_weights(cw).contiguous(memory_format=torch.channels_last))
+            t = F.conv2d(x, w[1], None, padding=1)
+            return _Phased(t, self.conv.bias, (x.shape[2] * 2, x.shape[3] * 2))
         return self.conv(F.interpolate(x, scale_factor=2.0, mode="nearest"))
+
+
+class _Phased:
+    """An upsampler output left in the 2x2 phase-conv layout (inference): ``t`` [N, 4C, H/2+1,
+    W/2+1] channels-last without the conv bias; the next up-block's concat GroupNorm reads it in
+    place. ``dense()`` materialises it (fallback)."""
+
+    def __init__(self, t, bias, hw):
+        self.t, self.bias, self.hw = t, bias, hw
+
+    def dense(self):
+        from ..ops.norms import phase_to_dense
+        d = phase_to_dense(self.t, self.hw)
+        if self.bias is not None:
+            d = d + self.bias.to(d.dtype)[None, :, None, None]
+        return d.contiguous(memory_format=torch.channels_last)
 
 
 class DownBlock(nn.Module):
@@ -439,7 +513,12 @@ class UpBlock(nn.Module):
 
     def forward(self, x, skips, temb, ctx):
         for i, r in enumerate(self.resnets):
-            x = r(torch.cat([x, skips.pop()], dim=1), temb)
+            skip = skips.pop()
+            if (_FUSE_UP and not torch.is_grad_enabled() and skip.is_cuda and _is_cl(skip) and _FOLD_BIAS
+                    and r.conv1.bias is not None):
+                x = r.forward_cat(x, skip, temb)
+            else:
+                x = r(torch.cat([x.dense() if isinstance(x, _Phased) else x, skip], dim=1), temb)
             if self.attentions is not None:
                 x = self.attentions[i](x, ctx)
         if self.upsamplers is not None:
@@ -525,6 +604,8 @@ class UNet2DConditionModel(nn.Module):
             mine = skips[-n:]
             del skips[-n:]
             x = self._run(lambda a, b, cc, *sk, _blk=blk: _blk(a, list(sk), b, cc), x, temb, ctx, *mine)
+        if isinstance(x, _Phased):  # a config whose last up block upsamples
+            x = x.dense()
         return self.conv_out(self.conv_norm_out(x)).contiguous()
 
 

@@ -39,6 +39,7 @@ F = ctypes.c_float
 # name -> argtypes (restype is always int status, 0 == ok)
 _SIGS = {
     "kca_layernorm_fwd": [P, P, P, P, P, P, P, P, P, I, I, F, P],
+    "kca_gemm_lt": [P, LL, P, LL, P, P, LL, P, LL, I, I, I, F, P, LL, P],
     "kca_layernorm_bwd_parts": [I],
     "kca_layernorm_bwd": [P, P, P, P, P, P, P, P, P, I, P, I, I, P],
     "kca_gelu_fwd": [P, P, LL, I, P],
@@ -72,6 +73,7 @@ _SIGS = {
     "kca_groupnorm_nhwc_ws": [I, I, I],
     "kca_groupnorm_nhwc_fwd": [P, P, P, P, P, P, P, I, I, I, I, F, I, P],
     "kca_groupnorm_nhwc_fwd_add": [P, P, P, P, P, P, P, P, I, I, I, I, F, I, P],
+    "kca_groupnorm_nhwc_cat_fwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, I, P],
     "kca_groupnorm_nhwc_bwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P],
     "kca_skinny_gemm": [P, LL, P, P, P, LL, I, I, I, I, P],
     "kca_skinny_set_splitk": [I],

@@ -208,3 +208,39 @@ class SplitKLinear(nn.Linear):
 
     def forward(self, x):
         return linear_splitk_wgrad(x, self.weight, self.bias)
+
+
+_WS: dict[int, torch.Tensor] = {}
+_WS_BYTES = 32 << 20
+
+
+def _workspace(dev: torch.device) -> torch.Tensor | None:
+    """hipBLASLt workspace, allocated once per device outside any graph capture."""
+    ws = _WS.get(dev.index)
+    if ws is None and not torch.cuda.is_current_stream_capturing():
+        ws = _WS[dev.index] = torch.empty(_WS_BYTES, device=dev, dtype=torch.uint8)
+    return ws
+
+
+def linear_residual(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None,
+                    res: torch.Tensor) -> torch.Tensor:
+    """``res + F.linear(x, weight, bias)`` in ONE hipBLASLt GEMM (bias and residual in its epilogue,
+    csrc/kernels/gemm_lt.hip) at inference on the GPU; the two-pass form otherwise (autograd,
+    CPU). ``res`` is any view whose rows are the output rows ([..., N], unit last stride); the
+    result has ``res``'s shape."""
+    N, K = weight.shape
+    if not (not torch.is_grad_enabled() and _lib.use_native(x, weight, res) and (bias is None or bias.is_cuda)
+            and x.shape[-1] == K and res.shape[-1] == N and x.stride(-1) == 1 and res.stride(-1) == 1
+            and weight.stride(1) == 1 and (bias is None or bias.is_contiguous())):
+        return res + F.linear(x, weight, bias).reshape(res.shape)
+    x2 = x.reshape(-1, K)
+    r2 = res.reshape(-1, N)
+    M = x2.shape[0]
+    if r2.shape[0] != M or x2.stride(1) != 1 or r2.stride(1) != 1:
+        return res + F.linear(x, weight, bias).reshape(res.shape)
+    out = torch.empty(M, N, device=x.device, dtype=x.dtype)
+    ws = _workspace(x.device)
+    _lib.call("kca_gemm_lt", x2.data_ptr(), x2.stride(0), weight.data_ptr(), weight.stride(0), _lib.ptr(bias),
+              r2.data_ptr(), r2.stride(0), out.data_ptr(), N, M, N, K, 1.0, _lib.ptr(ws),
+              _WS_BYTES if ws is not None else 0, _lib.stream())
+    return out.view(res.shape)

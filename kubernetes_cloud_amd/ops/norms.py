@@ -175,6 +175,55 @@ def _group_norm_nhwc_add(x, add, weight, bias, groups, eps, silu):
     return y
 
 
+def phase_to_dense(ph: torch.Tensor, hw: tuple) -> torch.Tensor:
+    """The upsampler's sub-pixel phase layout -> the dense upsampled tensor (reference / fallback):
+    ph [N, 4C, H/2+1, W/2+1] holds output phase (a, b) in channel block 2a + b at offset (a, b)."""
+    H, W = hw
+    C = ph.shape[1] // 4
+    out = ph.new_empty(ph.shape[0], C, H, W)
+    for a in range(2):
+        for b in range(2):
+            k = 2 * a + b
+            out[:, :, a::2, b::2] = ph[:, k * C:(k + 1) * C, a:a + H // 2, b:b + W // 2]
+    return out
+
+
+def group_norm_cat(x1: torch.Tensor, x2: torch.Tensor, groups: int, weight: torch.Tensor,
+                   bias: torch.Tensor | None, eps: float = 1e-5, silu: bool = False, phase: bool = False,
+                   x1_add: torch.Tensor | None = None, want_raw: bool = True):
+    """Inference GroupNorm(+SiLU) of the channel concat ``[x1 + x1_add | x2]`` without a
+    concatenated copy for the norm (``kca_groupnorm_nhwc_cat_fwd``): returns ``(y, raw)`` with
+    ``raw`` the concat itself (None unless ``want_raw``), both channels-last [N, C1 + C2, H, W].
+    ``phase``: x1 is still in the upsampler's phase layout (``phase_to_dense``); ``x1_add``: a
+    per-channel [C1] vector (the upsampler conv's bias) added to x1."""
+    N, C2, H, W = x2.shape
+    C1 = x1.shape[1] // (4 if phase else 1)
+    native = (_lib.use_native(x1, x2) and not torch.is_grad_enabled() and x1.dtype == torch.bfloat16
+              and x2.dtype == torch.bfloat16 and _channels_last(x1) and _channels_last(x2) and C1 % 8 == 0
+              and C2 % 8 == 0 and weight is not None and _lib.has("kca_groupnorm_nhwc_cat_fwd")
+              and (not phase or (H % 2 == 0 and W % 2 == 0 and tuple(x1.shape[2:]) == (H // 2 + 1, W // 2 + 1))))
+    if not native:
+        d1 = phase_to_dense(x1, (H, W)) if phase else x1
+        if x1_add is not None:
+            d1 = d1 + x1_add.to(d1.dtype)[None, :, None, None]
+        cat = torch.cat([d1, x2], dim=1)
+        return group_norm(cat, groups, weight, bias, eps, silu=silu), (cat if want_raw else None)
+    C, P = C1 + C2, H * W
+    y = torch.empty(N, H, W, C, device=x2.device, dtype=x2.dtype).permute(0, 3, 1, 2)
+    raw = torch.empty(N, H, W, C, device=x2.device, dtype=x2.dtype).permute(0, 3, 1, 2) if want_raw else None
+    add = None
+    if x1_add is not None:
+        add = torch.zeros(N, C, device=x2.device, dtype=torch.float32)
+        add[:, :C1] = x1_add.float()
+    mean = torch.empty(N * groups, device=x2.device, dtype=torch.float32)
+    rstd = torch.empty_like(mean)
+    ws = torch.empty(_lib.require().kca_groupnorm_nhwc_ws(N, P, C), device=x2.device, dtype=torch.float32)
+    _lib.call("kca_groupnorm_nhwc_cat_fwd", x1.data_ptr(), x2.data_ptr(), weight.data_ptr(), _lib.ptr(bias),
+              _lib.ptr(add), y.data_ptr(), _lib.ptr(raw), mean.data_ptr(), rstd.data_ptr(), ws.data_ptr(), N, P, C1,
+              C2, W if phase else 0, groups, float(eps), int(silu), _lib.stream())
+    return y, raw
+
+
 def group_norm(x: torch.Tensor, groups: int, weight: torch.Tensor, bias: torch.Tensor | None,
                eps: float = 1e-5, silu: bool = False, add: torch.Tensor | None = None) -> torch.Tensor:
     """GroupNorm over NC* tensors, optionally fused with SiLU (UNet/VAE ResNet blocks).

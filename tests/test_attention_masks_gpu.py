@@ -154,3 +154,36 @@ def test_unet_padded_attention_rowsum_matches_unpadded():
                                      False, 40 ** -0.5)
         ref = att.to_out[0](ref.reshape(2, 4096, 320).to(torch.bfloat16))
     assert _rel(fast, ref) < 2e-2
+
+
+@pytest.mark.parametrize("rowsum", [False, True])
+def test_narrow_48_storage_matches_reference(rowsum):
+    """SD-1.5 inference heads stored 48 wide (40 real + 8 zero) in a packed QKV
+    tensor, staged into the D=64 LDS image (StagerNarrow): equals the fp32
+    reference on the 40 real dims, and the narrow tiled kernel is the one that ran."""
+    torch.manual_seed(11)
+    B, S, H = 2, 2048, 8
+    qkv = torch.zeros(B, S, 3, H, 48, device=DEV, dtype=torch.bfloat16)
+    qkv[..., :40] = torch.randn(B, S, 3, H, 40, device=DEV).bfloat16()
+    if rowsum:
+        qkv[:, :, 2, :, 40] = 1.0
+    q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+    with torch.no_grad(), torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CUDA]) as prof:
+        o = ops.flash_attention(q, k, v, causal=False, scale=40 ** -0.5, rowsum_col=40 if rowsum else -1)
+        torch.cuda.synchronize()
+    ref, _ = attention_reference(q[..., :40], k[..., :40], v[..., :40], False, 40 ** -0.5)
+    assert o.shape == (B, S, H, 48)
+    assert _rel(o[..., :40], ref) < 1e-2
+    if rowsum:
+        assert float((o[..., 40].float() - 1).abs().max()) < 2e-2
+    else:
+        assert float(o[..., 40:].float().abs().max()) == 0.0
+    names = [e.name for e in prof.events()]
+    assert any("attn_fwd_tiled" in n and "48" in n for n in names), sorted(set(names))[:8]
+
+
+def test_unet_inference_heads_are_48_wide():
+    from kubernetes_cloud_amd.models import unet
+    assert unet.padded_head_dim(40, infer=True) == 48
+    assert unet.padded_head_dim(40) == 64  # training keeps the fwd+bwd D=64 kernels
+    assert unet.padded_head_dim(80, infer=True) == 96

@@ -97,7 +97,8 @@ def build_kernels(jobs: int = 8, verbose: bool = False, debug: bool = False, sta
     if ab_define:
         os.makedirs(os.path.join(ROOT, "ab"), exist_ok=True)
         out = os.path.join(ROOT, "ab", f"libkca_kernels_{ab_define.lower()}.so")
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp"] + objs
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp"] + objs + [
+        f"-L{ROCM}/lib", "-lhipblaslt"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stderr}")
