@@ -264,6 +264,9 @@ def _bloom_tp(args, info, rec):
             print(json.dumps(rec), flush=True)
         sys.stdout.flush()
         sys.stderr.flush()
+        # exit 0 on every rank, deliberately: rank 0's record above is complete and carries
+        # bloom_tp.error, and a non-zero rank exit makes torch.distributed.run fail the whole job,
+        # which would discard the measured GPT-J number along with the hung secondary
         os._exit(0)
 
     timer = threading.Timer(args.bloom_timeout, _overrun)

@@ -7,7 +7,9 @@ low-resolution input with the four 2x2 phase kernels (one 2x2 conv, 4*C outputs,
 Nearest-x2 followed by a 3x3 conv touches each input pixel through 2x2 distinct weight sums per
 output phase, so the phase form does 16 instead of 36 multiply-adds per (input pixel, Cin, Cout)
 and never materialises the 4x upsampled activation. One JSON line per shape (CFG batch 16,
-channels-last bf16, MIOpen): ms for upsample+conv3x3, conv3x3 alone, and the 2x2 phase conv.
+channels-last bf16, MIOpen): ms for upsample+conv3x3, conv3x3 alone, the 2x2 phase conv through
+MIOpen, and the framework's path (ops/upsample.py: im2col + one hipBLASLt GEMM, phase layout out;
+``phase_gemm_dense_ms`` adds the densifying scatter + bias the VAE decoder needs).
 """
 from __future__ import annotations
 
@@ -37,7 +39,8 @@ def _time(fn, iters=20, warmup=5):
 
 
 def main():
-    from kubernetes_cloud_amd.models.unet import phase_weights
+    from kubernetes_cloud_amd.ops.upsample import (phase_gemm_weights, phase_to_dense, phase_weights,
+                                                   upsample_conv_phase)
     from kubernetes_cloud_amd.utils import miopen
     miopen.configure()
     dev = "cuda"
@@ -51,6 +54,11 @@ def main():
             t_up = _time(lambda: F.conv2d(F.interpolate(x, scale_factor=2.0, mode="nearest"), w, padding=1))
             t_conv = _time(lambda: F.conv2d(up, w, padding=1))
             t_ph = _time(lambda: F.conv2d(x, wp, padding=1))
+            wg = phase_gemm_weights(w)
+            t_gemm = _time(lambda: upsample_conv_phase(x, wg))
+            t_gemm_d = _time(lambda: phase_to_dense(upsample_conv_phase(x, wg), (2 * S, 2 * S)))
+            gd = phase_to_dense(upsample_conv_phase(x, wg), (2 * S, 2 * S)).float()
+            gerr = ((gd - F.conv2d(up.float(), w.float(), padding=1)).abs().max()).item()
             ref = F.conv2d(up.float(), w.float(), padding=1)
             ph = F.conv2d(x, wp, padding=1).float()
             out = torch.empty_like(ref)
@@ -61,7 +69,8 @@ def main():
             err = ((out - ref).abs().max() / ref.abs().max()).item()
         print(json.dumps({"B": B, "C": C, "low_res": S, "upsample_conv3x3_ms": round(t_up, 4),
                           "conv3x3_only_ms": round(t_conv, 4), "phase_conv2x2_ms": round(t_ph, 4),
-                          "phase_rel_err": round(err, 5)}), flush=True)
+                          "phase_gemm_ms": round(t_gemm, 4), "phase_gemm_dense_ms": round(t_gemm_d, 4),
+                          "phase_rel_err": round(err, 5), "phase_gemm_abs_err": round(gerr, 5)}), flush=True)
 
 
 if __name__ == "__main__":

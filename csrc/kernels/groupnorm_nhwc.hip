@@ -138,7 +138,7 @@ __global__ void __launch_bounds__(256) nhwc_group_stats(const float* __restrict_
                                                         int nchunks, float eps, float* __restrict__ mean_out,
                                                         float* __restrict__ rstd_out, const bf16_t* __restrict__ w,
                                                         const bf16_t* __restrict__ b, float* __restrict__ ss,
-                                                        const float* __restrict__ add) {
+                                                        const float* __restrict__ add, long long add_ld) {
   __shared__ float red[3 * 256];
   const int ng = blockIdx.x, n = ng / G, g = ng % G, cg = C / G;
   const int items = nchunks * cg, CH = chunk_of(P);
@@ -148,7 +148,7 @@ __global__ void __launch_bounds__(256) nhwc_group_stats(const float* __restrict_
     const float cn = (float)(min(P, (ch + 1) * CH) - ch * CH);
     const float* s = part + (((long long)n * nchunks + ch) * C + c) * 2;
     // a per-(n, c) pre-add shifts that channel's mean and leaves its M2 unchanged
-    chan_merge(cnt, mu, q, cn, s[0] + (add ? add[(long long)n * C + c] : 0.f), s[1]);
+    chan_merge(cnt, mu, q, cn, s[0] + (add ? add[(long long)n * add_ld + c] : 0.f), s[1]);
   }
   red[threadIdx.x] = cnt;
   red[256 + threadIdx.x] = mu;
@@ -173,7 +173,7 @@ __global__ void __launch_bounds__(256) nhwc_group_stats(const float* __restrict_
   for (int j = threadIdx.x; j < cg; j += blockDim.x) {
     const int c = g * cg + j;
     const float sc = rs_g * bf2f(w[c]);
-    const float t = add ? add[(long long)n * C + c] : 0.f;  // y = (x + t - mu) * sc + b
+    const float t = add ? add[(long long)n * add_ld + c] : 0.f;  // y = (x + t - mu) * sc + b
     ss[((long long)n * 2) * C + c] = sc;
     ss[((long long)n * 2 + 1) * C + c] = (b ? bf2f(b[c]) : 0.f) + (t - mu_g) * sc;
   }
@@ -416,15 +416,16 @@ KCA_API int kca_groupnorm_nhwc_ws(int N, int P, int C) {  // fp32 workspace floa
 }
 
 // x, y: [N, P, C] bf16; mean/rstd: [N*G] fp32 out; ws: kca_groupnorm_nhwc_ws floats;
-// add: optional fp32 [N, C] added to x before the norm (the ResNet block's time
-// embedding, folded into the statistics and the apply pass's shift: no extra
-// pass over x and no materialised x + temb)
-KCA_API int kca_groupnorm_nhwc_fwd_add(const void* x, const void* w, const void* b, const float* add, void* y,
-                                       float* mean, float* rstd, float* ws, int N, int P, int C, int G, float eps,
-                                       int silu, hipStream_t stream) {
+// add: optional fp32 [N, C] (row stride add_ld >= C) added to x before the norm (the ResNet
+// block's time embedding, folded into the statistics and the apply pass's shift: no extra pass
+// over x and no materialised x + temb; add_ld lets every block read its slice of the UNet's one
+// batched time-projection GEMM in place)
+KCA_API int kca_groupnorm_nhwc_fwd_add(const void* x, const void* w, const void* b, const float* add,
+                                       long long add_ld, void* y, float* mean, float* rstd, float* ws, int N, int P,
+                                       int C, int G, float eps, int silu, hipStream_t stream) {
   dim3 block;
   int slabs;
-  if (!geometry(C, G, block, slabs) || N <= 0 || P <= 0) return 1;
+  if (!geometry(C, G, block, slabs) || N <= 0 || P <= 0 || (add && add_ld < C)) return 1;
   if ((long long)N * P * C / 8 >= (1LL << 31)) return 2;
   const int nchunks = (P + chunk_of(P) - 1) / chunk_of(P);
   const size_t smem = 2 * block.y * block.x * 8 * sizeof(float);
@@ -432,7 +433,7 @@ KCA_API int kca_groupnorm_nhwc_fwd_add(const void* x, const void* w, const void*
   hipLaunchKernelGGL(nhwc_chunk_stats<SrcPlain>, dim3(nchunks, N, slabs), block, smem, stream, src, P, C, ws);
   float* ss = ws + 2LL * N * nchunks * C;
   hipLaunchKernelGGL(nhwc_group_stats, dim3(N * G), dim3(256), 0, stream, ws, P, C, G, nchunks, eps, mean, rstd,
-                     (const bf16_t*)w, (const bf16_t*)b, ss, add);
+                     (const bf16_t*)w, (const bf16_t*)b, ss, add, add_ld);
   const int nvec = (int)((long long)N * P * C / 8);
   hipLaunchKernelGGL(nhwc_apply<SrcPlain>, dim3(kca_grid(nvec, 256, 8192)), dim3(256), 0, stream, src, ss,
                      (bf16_t*)y, (bf16_t*)nullptr, (const float*)nullptr, P, C, silu, nvec);
@@ -460,7 +461,7 @@ KCA_API int kca_groupnorm_nhwc_cat_fwd(const void* x1, const void* x2, const voi
   hipLaunchKernelGGL(nhwc_chunk_stats<SrcCat>, dim3(nchunks, N, slabs), block, smem, stream, src, P, C, ws);
   float* ss = ws + 2LL * N * nchunks * C;
   hipLaunchKernelGGL(nhwc_group_stats, dim3(N * G), dim3(256), 0, stream, ws, P, C, G, nchunks, eps, mean, rstd,
-                     (const bf16_t*)w, (const bf16_t*)b, ss, add);
+                     (const bf16_t*)w, (const bf16_t*)b, ss, add, (long long)C);
   const int nvec = (int)((long long)N * P * C / 8);
   hipLaunchKernelGGL(nhwc_apply<SrcCat>, dim3(kca_grid(nvec, 256, 8192)), dim3(256), 0, stream, src, ss,
                      (bf16_t*)y, (bf16_t*)raw, add, P, C, silu, nvec);
@@ -469,7 +470,7 @@ KCA_API int kca_groupnorm_nhwc_cat_fwd(const void* x1, const void* x2, const voi
 
 KCA_API int kca_groupnorm_nhwc_fwd(const void* x, const void* w, const void* b, void* y, float* mean, float* rstd,
                                    float* ws, int N, int P, int C, int G, float eps, int silu, hipStream_t stream) {
-  return kca_groupnorm_nhwc_fwd_add(x, w, b, nullptr, y, mean, rstd, ws, N, P, C, G, eps, silu, stream);
+  return kca_groupnorm_nhwc_fwd_add(x, w, b, nullptr, 0, y, mean, rstd, ws, N, P, C, G, eps, silu, stream);
 }
 
 // ws: kca_groupnorm_nhwc_ws floats + 2*N*G floats (partials, m1, m2, dx coefficients)

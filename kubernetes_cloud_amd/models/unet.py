@@ -26,6 +26,7 @@ import torch.nn.functional as F
 
 from .. import ops
 from ..ops.linear import SplitKLinear, linear_residual, linear_splitk_wgrad
+from ..ops.upsample import phase_gemm_weights, phase_to_dense, phase_weights, upsample_conv_phase, upsample_nearest2x
 
 
 @dataclasses.dataclass
@@ -146,6 +147,8 @@ class ResnetBlock2D(nn.Module):
         if _FOLD_BIAS and not torch.is_grad_enabled() and x.is_cuda and x.dtype == torch.bfloat16 \
                 and x.is_contiguous(memory_format=torch.channels_last) and self.conv1.bias is not None:
             return self._forward_folded(x, temb)
+        if isinstance(temb, _TembAdds):
+            temb = temb.temb
         h = self.conv1(self.norm1(x))
         t = None
         if self.time_emb_proj is not None and temb is not None:
@@ -169,18 +172,46 @@ class ResnetBlock2D(nn.Module):
         adds inside its statistics, and conv2's (+ the 1x1 shortcut's) bias joins the residual add
         -- one full read+write pass fewer per convolution (profiles/sd_unet_add_attribution_r2.txt)."""
         h = F.conv2d(self.norm1(x) if xn is None else xn, self.conv1.weight, None, padding=1)
-        add = self.conv1.bias.float()[None].expand(x.shape[0], -1)
-        if self.time_emb_proj is not None and temb is not None:
-            add = add + self.time_emb_proj(F.silu(temb)).float()
+        add = temb.get(self) if isinstance(temb, _TembAdds) else None  # conv1 bias + time projection, fp32
+        if add is None:
+            if isinstance(temb, _TembAdds):
+                temb = temb.temb
+            b1, _ = self._folded_biases()
+            add = b1[None].expand(x.shape[0], -1)
+            if self.time_emb_proj is not None and temb is not None:
+                add = add + self.time_emb_proj(F.silu(temb)).float()
         h = F.conv2d(self.norm2(h, add=add), self.conv2.weight, None, padding=1)
-        bias = self.conv2.bias.float()
-        if self.conv_shortcut is not None:
-            sc = F.conv2d(x, self.conv_shortcut.weight, None)
-            if self.conv_shortcut.bias is not None:
-                bias = bias + self.conv_shortcut.bias.float()
-        else:
-            sc = x
+        _, bias = self._folded_biases()
+        sc = F.conv2d(x, self.conv_shortcut.weight, None) if self.conv_shortcut is not None else x
         return ops.add_bias_nhwc(sc, h, bias)
+
+    def _folded_biases(self):
+        """fp32 conv1 bias and conv2 (+ shortcut) bias, cached while the parameters are unchanged
+        (one cast/add kernel pair less per block and step)."""
+        ps = [p for p in (self.conv1.bias, self.conv2.bias,
+                          self.conv_shortcut.bias if self.conv_shortcut is not None else None) if p is not None]
+        key = tuple((p.data_ptr(), p._version) for p in ps)
+        c = getattr(self, "_fb_cache", None)
+        if c is None or c[0] != key:
+            b2 = self.conv2.bias.float()
+            if self.conv_shortcut is not None and self.conv_shortcut.bias is not None:
+                b2 = b2 + self.conv_shortcut.bias.float()
+            c = self._fb_cache = (key, self.conv1.bias.float(), b2)
+        return c[1], c[2]
+
+
+class _TembAdds:
+    """Inference: every ResNet block's ``conv1.bias + time_emb_proj(silu(temb))`` (fp32), computed by
+    ONE GEMM over the concatenated projection weights (UNet2DConditionModel._temb_adds) instead of
+    a SiLU + GEMM + two casts + an add per block; each block's GroupNorm reads its [B, cout] slice
+    in place (row stride = the table width)."""
+
+    def __init__(self, temb, table, offsets):
+        self.temb, self.table, self.offsets = temb, table, offsets
+
+    def get(self, blk):
+        o = self.offsets.get(id(blk))
+        return None if o is None else self.table[:, o[0]:o[0] + o[1]]
 
 
 # Head padding for the self-attention (see Attention.forward); KCA_SD_PAD_HEADS=0
@@ -206,10 +237,16 @@ _PAD_GEN = 0
 # inference: residual adds carried by the preceding GEMM's epilogue (ops.linear_residual);
 # KCA_SD_FUSE_RES=0 keeps the separate adds (A/B knob)
 _FUSE_RES = os.environ.get("KCA_SD_FUSE_RES", "1") not in ("0", "false")
-# inference: upsamplers as one 2x2 phase conv of the low-res input (phase_weights), whose output the
-# next up-block's concat GroupNorm reads in place (ops.group_norm_cat): no upsampled activation, no
-# concatenated copy for the norm
-_FUSE_UP = os.environ.get("KCA_SD_FUSE_UP", "0") in ("1", "true")
+# inference: upsamplers as im2col + ONE hipBLASLt GEMM of the low-res input with the four 2x2 phase
+# kernels (ops/upsample.py: 16 instead of 36 MACs per input pixel, no upsampled activation); the UNet's
+# up blocks read that phase layout in place in their concat GroupNorm, the VAE gets it densified.
+# KCA_SD_PHASE_UP=0: nearest-x2 (native NHWC kernel) + the 3x3 conv
+_PHASE_UP = os.environ.get("KCA_SD_PHASE_UP", "1") not in ("0", "false")
+# inference: the up blocks' GroupNorm reads [x | skip] in place and writes the concat once for the
+# 1x1 shortcut (ops.group_norm_cat) instead of torch.cat + GroupNorm; KCA_SD_CAT_GN=0 disables
+_CAT_GN = os.environ.get("KCA_SD_CAT_GN", "1") not in ("0", "false")
+# inference: all ResNet time projections as one GEMM (_TembAdds); KCA_SD_TEMB_BATCH=0 disables
+_TEMB_BATCH = os.environ.get("KCA_SD_TEMB_BATCH", "1") not in ("0", "false")
 
 
 def pad_generation() -> int:
@@ -423,57 +460,44 @@ class Downsample2D(nn.Module):
         return self.conv(x)
 
 
-# nearest-x2 then 3x3 conv (padding 1) == per output phase (a, b) a 2x2 conv of the low-resolution
-# input (padding 1, output window offset (a, b)) whose taps sum the 3x3 taps that land on the same
-# input pixel: rows/cols {0} {1,2} for phase 0 and {0,1} {2} for phase 1
-_PHASE_TAPS = (((0,), (1, 2)), ((0, 1), (2,)))
-
-
-def phase_weights(w: torch.Tensor) -> torch.Tensor:
-    """[Cout, Cin, 3, 3] -> [4 * Cout, Cin, 2, 2]: output channel block k = 2a + b holds phase (a, b)."""
-    wf = w.float()
-    out = wf.new_zeros(4, w.shape[0], w.shape[1], 2, 2)
-    for a in range(2):
-        for b in range(2):
-            for s_ in range(2):
-                for t in range(2):
-                    rows, cols = _PHASE_TAPS[a][s_], _PHASE_TAPS[b][t]
-                    out[2 * a + b, :, :, s_, t] = wf[:, :, list(rows)][:, :, :, list(cols)].sum(dim=(2, 3))
-    return out.reshape(4 * w.shape[0], w.shape[1], 2, 2).to(w.dtype)
-
-
 class Upsample2D(nn.Module):
     def __init__(self, ch):
         super().__init__()
         self.conv = nn.Conv2d(ch, ch, 3, padding=1)
+        self.phase_out = False  # set by the UNet: its up blocks read the phase layout in place
+
+    def _gemm_weights(self):
+        cw = self.conv.weight
+        key = (cw.data_ptr(), cw._version)
+        c = getattr(self, "_phase_cache", None)
+        if c is None or c[0] != key:  # re-derived when the conv weight is replaced or updated
+            c = self._phase_cache = (key, phase_gemm_weights(cw))
+        return c[1]
 
     def forward(self, x):
-        if (_FUSE_UP and not torch.is_grad_enabled() and x.is_cuda and x.dtype == torch.bfloat16 and _is_cl(x)
-                and x.shape[1] % 8 == 0):
-            cw = self.conv.weight
-            key = (cw.data_ptr(), cw._version)
-            w = getattr(self, "_phase_w", None)
-            if w is None or w[0] != key:  # re-derived when the conv weight is replaced or updated
-                w = self._phase_w = (key, phase_weights(cw).contiguous(memory_format=torch.channels_last))
-            t = F.conv2d(x, w[1], None, padding=1)
-            return _Phased(t, self.conv.bias, (x.shape[2] * 2, x.shape[3] * 2))
+        infer = (not torch.is_grad_enabled() and x.is_cuda and x.dtype == torch.bfloat16 and _is_cl(x)
+                 and x.shape[1] % 8 == 0)
+        if infer and _PHASE_UP:
+            t = upsample_conv_phase(x, self._gemm_weights())
+            hw = (x.shape[2] * 2, x.shape[3] * 2)
+            if self.phase_out:
+                return _Phased(t, self.conv.bias, hw)
+            return phase_to_dense(t, hw, self.conv.bias)
+        if infer:
+            return self.conv(upsample_nearest2x(x))
         return self.conv(F.interpolate(x, scale_factor=2.0, mode="nearest"))
 
 
 class _Phased:
-    """An upsampler output left in the 2x2 phase-conv layout (inference): ``t`` [N, 4C, H/2+1,
-    W/2+1] channels-last without the conv bias; the next up-block's concat GroupNorm reads it in
-    place. ``dense()`` materialises it (fallback)."""
+    """An upsampler output left in the 2x2 phase layout (inference): ``t`` [N, 4C, H/2+1, W/2+1]
+    channels-last without the conv bias; the next up-block's concat GroupNorm reads it in place.
+    ``dense()`` materialises it (+ bias) with the native scatter kernel (fallback)."""
 
     def __init__(self, t, bias, hw):
         self.t, self.bias, self.hw = t, bias, hw
 
     def dense(self):
-        from ..ops.norms import phase_to_dense
-        d = phase_to_dense(self.t, self.hw)
-        if self.bias is not None:
-            d = d + self.bias.to(d.dtype)[None, :, None, None]
-        return d.contiguous(memory_format=torch.channels_last)
+        return phase_to_dense(self.t, self.hw, self.bias)
 
 
 class DownBlock(nn.Module):
@@ -514,8 +538,8 @@ class UpBlock(nn.Module):
     def forward(self, x, skips, temb, ctx):
         for i, r in enumerate(self.resnets):
             skip = skips.pop()
-            if (_FUSE_UP and not torch.is_grad_enabled() and skip.is_cuda and _is_cl(skip) and _FOLD_BIAS
-                    and r.conv1.bias is not None):
+            if (_CAT_GN and not torch.is_grad_enabled() and skip.is_cuda and _is_cl(skip) and _FOLD_BIAS
+                    and r.conv1.bias is not None and (isinstance(x, _Phased) or _is_cl(x))):
                 x = r.forward_cat(x, skip, temb)
             else:
                 x = r(torch.cat([x.dense() if isinstance(x, _Phased) else x, skip], dim=1), temb)
@@ -569,6 +593,9 @@ class UNet2DConditionModel(nn.Module):
                                c.use_linear_projection))
             prev = out
         self.up_blocks = nn.ModuleList(ups)
+        for blk in self.up_blocks:  # every up-block upsampler feeds the next block's concat GroupNorm
+            if blk.upsamplers is not None:
+                blk.upsamplers[0].phase_out = True
         self.conv_norm_out = GroupNorm(g, ch[0], eps, silu=True)
         self.conv_out = nn.Conv2d(ch[0], c.out_channels, 3, padding=1)
         self.gradient_checkpointing = False
@@ -576,6 +603,26 @@ class UNet2DConditionModel(nn.Module):
 
     def enable_gradient_checkpointing(self, on: bool = True):
         self.gradient_checkpointing = on
+
+    def _temb_adds(self, temb: torch.Tensor) -> _TembAdds:
+        """One GEMM for every ResNet block's time projection (+ its conv1 bias, fp32): see _TembAdds."""
+        rs = [m for m in self.modules() if isinstance(m, ResnetBlock2D) and m.time_emb_proj is not None
+              and m.conv1.bias is not None]
+        ps = [p for r in rs for p in (r.time_emb_proj.weight, r.time_emb_proj.bias, r.conv1.bias) if p is not None]
+        key = tuple((p.data_ptr(), p._version) for p in ps)
+        c = getattr(self, "_temb_cache", None)
+        if c is None or c[0] != key:
+            w = torch.cat([r.time_emb_proj.weight for r in rs])
+            b = torch.cat([r.conv1.bias.float() + (r.time_emb_proj.bias.float() if r.time_emb_proj.bias is not None
+                                                   else 0.0) for r in rs])
+            offs, o = {}, 0
+            for r in rs:
+                n = r.time_emb_proj.weight.shape[0]
+                offs[id(r)] = (o, n)
+                o += n
+            c = self._temb_cache = (key, w, b, offs)
+        _, w, b, offs = c
+        return _TembAdds(temb, torch.add(b, F.linear(F.silu(temb), w)), offs)
 
     def _run(self, fn, *args):
         if self.gradient_checkpointing and self.training and torch.is_grad_enabled():
@@ -590,6 +637,9 @@ class UNet2DConditionModel(nn.Module):
         t = timestep.to(sample.device).reshape(-1).expand(sample.shape[0])
         temb = timestep_embedding(t, c.block_out_channels[0], c.flip_sin_to_cos, c.freq_shift).to(sample.dtype)
         temb = self.time_embedding(temb)
+        if (_TEMB_BATCH and _FOLD_BIAS and not torch.is_grad_enabled() and self.channels_last and temb.is_cuda
+                and temb.dtype == torch.bfloat16):
+            temb = self._temb_adds(temb)
         ctx = encoder_hidden_states.to(sample.dtype)
         if self.channels_last:
             sample = sample.contiguous(memory_format=torch.channels_last)

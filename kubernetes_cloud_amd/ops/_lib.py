@@ -72,7 +72,7 @@ _SIGS = {
     "kca_groupnorm_bwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P],
     "kca_groupnorm_nhwc_ws": [I, I, I],
     "kca_groupnorm_nhwc_fwd": [P, P, P, P, P, P, P, I, I, I, I, F, I, P],
-    "kca_groupnorm_nhwc_fwd_add": [P, P, P, P, P, P, P, P, I, I, I, I, F, I, P],
+    "kca_groupnorm_nhwc_fwd_add": [P, P, P, P, LL, P, P, P, P, I, I, I, I, F, I, P],
     "kca_groupnorm_nhwc_cat_fwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, I, P],
     "kca_groupnorm_nhwc_bwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P],
     "kca_skinny_gemm": [P, LL, P, P, P, LL, I, I, I, I, P],
@@ -89,6 +89,9 @@ _SIGS = {
     "kca_sd_lms_step": [P, P, P, P, LL, P, I, I, I, I, I, F, F, F, P],
     "kca_decode_prep_attn": [P, LL, P, P, LL, LL, LL, P, P, P, LL, P, LL, I, I, I, I, I, I, F, P, P, I, I, I, I, P,
                              P, I, P],
+    "kca_im2col2x2_nhwc": [P, P, I, I, I, I, P],
+    "kca_phase_to_dense_nhwc": [P, P, P, I, I, I, I, P],
+    "kca_upsample2x_nhwc": [P, P, I, I, I, I, P],
     "kca_sample_logits": [P, LL, I, I, I, P, P, P, P, P, P, P, I, P, LL, P, P, P, P, P],
 }
 

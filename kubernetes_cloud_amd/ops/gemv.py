@@ -53,7 +53,10 @@ def skinny_linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | No
     # 12.4 vs 18.4 us); on the QKV / MLP weights hipBLASLt is faster from M = 2 (GPT-J decode B=2 4.69 ms
     # with the skinny kernel vs 4.54 ms at B=4 through hipBLASLt); MFMA GEMMs beyond
     small = N * K <= (16 << 20)
-    if (_lib.use_native(x, weight) and (M <= _SKINNY_MAX_M or (M <= 4 and small)) and K % 8 == 0
+    # M = 2 takes the register-resident K-split form only for K <= 8192 (GPT-J); BLOOM's K = 14336
+    # QKV / fc_in at M = 2 would fall to the row-per-wave kernel, which hipBLASLt beats on big weights
+    regs = M == 1 or K <= 8192 or small
+    if (_lib.use_native(x, weight) and ((M <= _SKINNY_MAX_M and regs) or (M <= 4 and small)) and K % 8 == 0
             and x.stride(1) == 1
             and x.stride(0) % 8 == 0
             and weight.is_contiguous() and x.data_ptr() % 16 == 0 and weight.data_ptr() % 16 == 0

@@ -164,13 +164,15 @@ def _group_norm_nhwc_add(x, add, weight, bias, groups, eps, silu):
     """Inference GroupNorm of ``x + add[:, :, None, None]`` without forming the sum."""
     n, c = x.shape[0], x.shape[1]
     p = x.numel() // (n * c)
-    add = add.to(torch.float32).contiguous()
+    add = add.to(torch.float32)
+    if add.stride(1) != 1 or add.stride(0) < c:  # a row-strided slice (the UNet's batched time GEMM) is read in place
+        add = add.contiguous()
     y = torch.empty_like(x)
     mean = torch.empty(n * groups, device=x.device, dtype=torch.float32)
     rstd = torch.empty_like(mean)
     ws = torch.empty(_lib.require().kca_groupnorm_nhwc_ws(n, p, c), device=x.device, dtype=torch.float32)
     _lib.call("kca_groupnorm_nhwc_fwd_add", x.data_ptr(), weight.data_ptr(), _lib.ptr(bias), add.data_ptr(),
-              y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), ws.data_ptr(), n, p, c, groups, float(eps),
+              add.stride(0), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), ws.data_ptr(), n, p, c, groups, float(eps),
               int(silu), _lib.stream())
     return y
 

@@ -1,0 +1,106 @@
+"""SD-1.5 upsamplers (nearest x2 + 3x3 conv) as one GEMM: csrc/kernels/sd_upsample.hip.
+
+The UNet's three and the VAE decoder's three upsamplers
+(online-inference/stable-diffusion/service/service.py:244-252 runs both per image) are
+``conv3x3(nearest_x2(x))``. Per output phase (a, b) that is a 2x2 conv of the low-resolution input
+(``phase_weights``): 16 instead of 36 multiply-adds per (input pixel, Cin, Cout), and no 4x
+upsampled activation. ``upsample_conv_phase`` runs it as im2col (one bandwidth pass) + one
+hipBLASLt GEMM whose output is the *phase layout* [N, h+1, w+1, 4C]: the UNet's concat GroupNorm
+reads it in place (ops.norms.group_norm_cat ``phase=True``); ``phase_to_dense`` materialises it
+(+ the conv bias) for the VAE decoder.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+
+# nearest-x2 then 3x3 conv (padding 1) == per output phase (a, b) a 2x2 conv of the low-resolution
+# input (padding 1, output window offset (a, b)) whose taps sum the 3x3 taps that land on the same
+# input pixel: rows/cols {0} {1,2} for phase 0 and {0,1} {2} for phase 1
+_PHASE_TAPS = (((0,), (1, 2)), ((0, 1), (2,)))
+
+
+def phase_weights(w: torch.Tensor) -> torch.Tensor:
+    """[Cout, Cin, 3, 3] -> [4 * Cout, Cin, 2, 2]: output channel block k = 2a + b holds phase (a, b)."""
+    wf = w.float()
+    out = wf.new_zeros(4, w.shape[0], w.shape[1], 2, 2)
+    for a in range(2):
+        for b in range(2):
+            for s_ in range(2):
+                for t in range(2):
+                    rows, cols = _PHASE_TAPS[a][s_], _PHASE_TAPS[b][t]
+                    out[2 * a + b, :, :, s_, t] = wf[:, :, list(rows)][:, :, :, list(cols)].sum(dim=(2, 3))
+    return out.reshape(4 * w.shape[0], w.shape[1], 2, 2).to(w.dtype)
+
+
+def phase_gemm_weights(w: torch.Tensor) -> torch.Tensor:
+    """[Cout, Cin, 3, 3] -> the GEMM operand [4 * Cout, 4 * Cin], K in im2col order (s, t, cin)."""
+    wp = phase_weights(w)
+    return wp.permute(0, 2, 3, 1).reshape(wp.shape[0], 4 * w.shape[1]).contiguous()
+
+
+def _nhwc(x: torch.Tensor) -> bool:
+    return x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)
+
+
+def native_ok(x: torch.Tensor) -> bool:
+    return (_lib.use_native(x) and _nhwc(x) and x.shape[1] % 8 == 0 and x.data_ptr() % 16 == 0
+            and _lib.has("kca_im2col2x2_nhwc"))
+
+
+def im2col2x2(x: torch.Tensor) -> torch.Tensor:
+    """x [N, C, h, w] channels-last -> [N*(h+1)*(w+1), 4C]: the 2x2 (padding 1) patches, (s, t, c)."""
+    N, C, h, w = x.shape
+    if native_ok(x):
+        a = torch.empty(N * (h + 1) * (w + 1), 4 * C, device=x.device, dtype=x.dtype)
+        _lib.call("kca_im2col2x2_nhwc", x.data_ptr(), a.data_ptr(), N, h, w, C, _lib.stream())
+        return a
+    xp = F.pad(x.permute(0, 2, 3, 1), (0, 0, 1, 1, 1, 1))  # [N, h+2, w+2, C]
+    taps = [xp[:, s:s + h + 1, t:t + w + 1, :] for s in range(2) for t in range(2)]
+    return torch.cat(taps, dim=-1).reshape(N * (h + 1) * (w + 1), 4 * C)
+
+
+def upsample_conv_phase(x: torch.Tensor, wg: torch.Tensor) -> torch.Tensor:
+    """conv3x3(nearest_x2(x)) without bias, in the phase layout: [N, 4C, h+1, w+1] channels-last
+    (memory [N, h+1, w+1, 4C]); ``wg`` from ``phase_gemm_weights``."""
+    N, C, h, w = x.shape
+    cout = wg.shape[0] // 4
+    t = F.linear(im2col2x2(x), wg)  # [N*(h+1)*(w+1), 4*cout]
+    return t.view(N, h + 1, w + 1, 4 * cout).permute(0, 3, 1, 2)
+
+
+def phase_to_dense(t: torch.Tensor, hw: tuple, bias: torch.Tensor | None = None) -> torch.Tensor:
+    """Phase layout [N, 4C, h+1, w+1] (+ bias [C]) -> dense [N, C, 2h, 2w] channels-last."""
+    N, C4, hp, wp = t.shape
+    C, (H, W) = C4 // 4, hw
+    assert H == 2 * (hp - 1) and W == 2 * (wp - 1), (t.shape, hw)
+    if (_lib.use_native(t, bias) and _nhwc(t) and C % 8 == 0 and t.data_ptr() % 16 == 0
+            and _lib.has("kca_phase_to_dense_nhwc")):
+        out = torch.empty(N, H, W, C, device=t.device, dtype=t.dtype)
+        _lib.call("kca_phase_to_dense_nhwc", t.data_ptr(), _lib.ptr(bias.contiguous() if bias is not None else None),
+                  out.data_ptr(), N, hp - 1, wp - 1, C, _lib.stream())
+        return out.permute(0, 3, 1, 2)
+    out = t.new_empty(N, C, H, W)
+    for a in range(2):
+        for b in range(2):
+            k = 2 * a + b
+            out[:, :, a::2, b::2] = t[:, k * C:(k + 1) * C, a:a + H // 2, b:b + W // 2]
+    if bias is not None:
+        out = out + bias.to(out.dtype)[None, :, None, None]
+    return out.contiguous(memory_format=torch.channels_last)
+
+
+def upsample_nearest2x(x: torch.Tensor) -> torch.Tensor:
+    """Nearest x2 of a channels-last [N, C, h, w] tensor (native NHWC kernel on the GPU)."""
+    N, C, h, w = x.shape
+    if native_ok(x) and _lib.has("kca_upsample2x_nhwc"):
+        out = torch.empty(N, 2 * h, 2 * w, C, device=x.device, dtype=x.dtype)
+        _lib.call("kca_upsample2x_nhwc", x.data_ptr(), out.data_ptr(), N, h, w, C, _lib.stream())
+        return out.permute(0, 3, 1, 2)
+    return F.interpolate(x, scale_factor=2.0, mode="nearest")
+
+
+__all__ = ["phase_weights", "phase_gemm_weights", "im2col2x2", "upsample_conv_phase", "phase_to_dense",
+           "upsample_nearest2x"]

@@ -253,3 +253,22 @@ def test_fused_noise_prep_reference_matches_scheduler_math(v_pred):
     from kubernetes_cloud_amd.ops import mse_loss
     assert torch.allclose(mse_split_reference(p, target, 0.5),
                           mse_loss(p[:2], target[:2]) + 0.5 * mse_loss(p[2:], target[2:]))
+
+
+def test_phase_gemm_upsampler_equals_nearest_conv3x3_cpu():
+    """ops/upsample.py reference path (what csrc/kernels/sd_upsample.hip implements on the GPU):
+    im2col 2x2 + GEMM with the phase kernels, densified with the bias, equals nearest-x2 + 3x3 conv."""
+    import torch
+    import torch.nn.functional as F
+
+    from kubernetes_cloud_amd.ops import upsample as up
+    torch.manual_seed(0)
+    for N, C, h, w in [(2, 8, 5, 4), (1, 16, 3, 3)]:
+        x = torch.randn(N, C, h, w).contiguous(memory_format=torch.channels_last)
+        wt = torch.randn(C, C, 3, 3) / (3 * C ** 0.5)
+        b = torch.randn(C)
+        t = up.upsample_conv_phase(x, up.phase_gemm_weights(wt))
+        assert t.shape == (N, 4 * C, h + 1, w + 1)
+        got = up.phase_to_dense(t, (2 * h, 2 * w), b)
+        ref = F.conv2d(F.interpolate(x, scale_factor=2.0, mode="nearest"), wt, b, padding=1)
+        assert torch.allclose(got, ref, atol=1e-4, rtol=1e-4)

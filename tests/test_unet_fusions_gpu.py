@@ -1,6 +1,8 @@
 """SD UNet inference fusions on MI355X: the concat GroupNorm (no concatenated copy for the
-norm, the upsampler's sub-pixel phase layout read in place) against cat + GroupNorm, and the
-phase-conv upsampler + fused up-block against the plain UNet path."""
+norm, the upsampler's sub-pixel phase layout read in place) against cat + GroupNorm, the
+im2col + GEMM phase upsampler (csrc/kernels/sd_upsample.hip) against nearest-x2 + conv3x3 in fp32,
+and the fused UNet (phase upsamplers, concat GroupNorm, batched time projections) against the plain
+path."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -48,7 +50,55 @@ def test_unet_phase_upsampler_and_fused_upblocks_match_plain(monkeypatch):
     ctx = torch.randn(2, 8, cfg.cross_attention_dim, device=DEV, dtype=torch.bfloat16)
     with torch.no_grad():
         fused = m(x, 10, ctx)
-        monkeypatch.setattr(unet, "_FUSE_UP", False)
+        for flag in ("_PHASE_UP", "_CAT_GN", "_TEMB_BATCH"):
+            monkeypatch.setattr(unet, flag, False)
         plain = m(x, 10, ctx)
+    err = (fused.float() - plain.float()).abs().max().item()
+    assert err < 0.03 * plain.float().abs().max().item() + 1e-3, err
+
+
+@pytest.mark.parametrize("N,C,S", [(2, 64, 8), (3, 320, 16), (2, 1280, 4)])
+def test_phase_gemm_upsampler_matches_fp32_reference(N, C, S):
+    from kubernetes_cloud_amd.ops import upsample as up
+    torch.manual_seed(N * C + S)
+    x = _cl(N, C, S, S)
+    w = (torch.randn(C, C, 3, 3, device=DEV) * (9 * C) ** -0.5).bfloat16()
+    bias = torch.randn(C, device=DEV, dtype=torch.bfloat16)
+    with torch.no_grad():
+        a = up.im2col2x2(x)
+        ref_a = up.im2col2x2(x.float())  # torch reference path (CPU/fp32 branch of the op)
+        assert a.shape == ref_a.shape and torch.equal(a.float(), ref_a)
+        t = up.upsample_conv_phase(x, up.phase_gemm_weights(w))
+        dense = up.phase_to_dense(t, (2 * S, 2 * S), bias)
+        ref = F.conv2d(F.interpolate(x.float(), scale_factor=2.0, mode="nearest"), w.float(), bias.float(), padding=1)
+    assert _lib.has("kca_im2col2x2_nhwc") and _lib.has("kca_phase_to_dense_nhwc")
+    assert dense.is_contiguous(memory_format=CL) and dense.shape == ref.shape
+    err = (dense.float() - ref).abs().max().item()
+    assert err < 0.03 * ref.abs().max().item(), err
+
+
+def test_native_upsample2x_matches_interpolate():
+    from kubernetes_cloud_amd.ops.upsample import upsample_nearest2x
+    x = _cl(2, 96, 7, 5)
+    with torch.no_grad():
+        y = upsample_nearest2x(x)
+    assert y.is_contiguous(memory_format=CL)
+    assert torch.equal(y, F.interpolate(x, scale_factor=2.0, mode="nearest"))
+
+
+def test_vae_decoder_phase_upsampler_matches_plain(monkeypatch):
+    from kubernetes_cloud_amd.models import unet
+    from kubernetes_cloud_amd.models.unet import to_channels_last
+    from kubernetes_cloud_amd.models.vae import AutoencoderKL, VAEConfig
+    torch.manual_seed(1)
+    cfg = VAEConfig(block_out_channels=(64, 64, 128, 128))
+    vae = to_channels_last(AutoencoderKL(cfg).to(DEV).bfloat16().eval())
+    z = torch.randn(1, cfg.latent_channels, 16, 16, device=DEV, dtype=torch.bfloat16)
+    with torch.no_grad():
+        fused = vae.decode(z)
+        monkeypatch.setattr(unet, "_PHASE_UP", False)
+        plain = vae.decode(z)
+    fused = fused.sample if hasattr(fused, "sample") else fused
+    plain = plain.sample if hasattr(plain, "sample") else plain
     err = (fused.float() - plain.float()).abs().max().item()
     assert err < 0.03 * plain.float().abs().max().item() + 1e-3, err

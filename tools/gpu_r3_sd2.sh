@@ -18,10 +18,6 @@ for rep in 1 2; do
 done
 timeout -k 10 300 python -u bench/upsample_conv_bench.py > gpurun_out/r3_upconv.jsonl 2> gpurun_out/r3_upconv.err || { tail -5 gpurun_out/r3_upconv.err; exit 5; }
 cat gpurun_out/r3_upconv.jsonl
-mkdir -p gpurun_out/miotune_up/db gpurun_out/miotune_up/cache && cp tuning/miopen/*.txt gpurun_out/miotune_up/db/
-MIOPEN_USER_DB_PATH=$PWD/gpurun_out/miotune_up/db MIOPEN_CUSTOM_CACHE_DIR=$PWD/gpurun_out/miotune_up/cache MIOPEN_FIND_ENFORCE=3 \
-  timeout -k 10 400 python -u bench/upsample_conv_bench.py > gpurun_out/r3_upconv_tuned.jsonl 2> gpurun_out/r3_upconv_tuned.err || { tail -5 gpurun_out/r3_upconv_tuned.err; exit 6; }
-cat gpurun_out/r3_upconv_tuned.jsonl
 export TMPDIR=/tmp
 cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/sd_prof_r3 -o sd -- python3 $GRAFT_REPO_ROOT/bench/sd_bench.py --mode infer --steps 1 --warmup 1 --infer-steps 10 > $GRAFT_REPO_ROOT/gpurun_out/sd_prof_r3.log 2>&1 || exit 4
 ls -R $GRAFT_REPO_ROOT/gpurun_out/sd_prof_r3 | head
