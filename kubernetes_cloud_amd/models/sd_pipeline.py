@@ -82,6 +82,13 @@ class UNetGraph:
         self.unet = unet
         self.graphs: dict = {}
         self.pad_gen = -1
+        # the text context of the last call and its cross-attention K/V: one prompt batch calls the
+        # UNet with the same ``ctx`` tensor every step, so K/V are projected once per batch
+        # (models/unet.py CtxKV); the strong reference keeps the address from being reused
+        self._ctx_ref = None
+        self._ctx_ver = -1
+        self._kv_fresh = False
+        self.ctx_kv = os.environ.get("KCA_SD_CTX_KV", "1") not in ("0", "false") and hasattr(unet, "ctx_kv")
 
     def __call__(self, x, t, ctx):
         from .unet import pad_generation
@@ -90,19 +97,26 @@ class UNetGraph:
         key = (tuple(x.shape), x.dtype, tuple(t.shape), tuple(ctx.shape), ctx.dtype)
         g = self.graphs.get(key)
         if g is None:
+            self._ctx_ref = None
             g = self.graphs[key] = self._capture(x, t, ctx)
         if g is False:
             return self.unet(x, t, ctx)
         graph, sx, st, sc, out = g
         sx.copy_(x)
         st.copy_(t)
-        sc.copy_(ctx)
+        if self.ctx_kv:
+            if not (ctx is self._ctx_ref and ctx._version == self._ctx_ver):
+                self.unet.ctx_kv(ctx, out=sc)  # eager, once per prompt batch, into the graph's table
+                self._ctx_ref, self._ctx_ver = ctx, ctx._version
+        else:
+            sc.copy_(ctx)
         graph.replay()
         return out
 
     @torch.no_grad()
     def _capture(self, x, t, ctx):
-        sx, st, sc = x.clone(), t.clone(), ctx.clone()
+        sx, st = x.clone(), t.clone()
+        sc = self.unet.ctx_kv(ctx.clone()) if self.ctx_kv else ctx.clone()
         try:
             side = torch.cuda.Stream()
             side.wait_stream(torch.cuda.current_stream())

@@ -264,6 +264,7 @@ class Attention(nn.Module):
         self.to_k = _Linear(cross_dim or dim, inner, bias=bias_qkv)
         self.to_v = _Linear(cross_dim or dim, inner, bias=bias_qkv)
         self.to_out = nn.ModuleList([_Linear(inner, dim), nn.Dropout(0.0)])
+        self.cross = cross_dim is not None
         self._padded = None
 
     def train(self, mode: bool = True):
@@ -329,14 +330,39 @@ class Attention(nn.Module):
                                     rowsum_col=ROWSUM_COL if (dpad in (48, 64) and hd == ROWSUM_COL and _ROWSUM)
                                     else -1)
             return F.linear(o.reshape(B, S, -1), wo, self.to_out[0].bias)
-        c = x if ctx is None else ctx
-        q = self.to_q(x)
-        k = self.to_k(c)
-        v = self.to_v(c)
+        kv = ctx.get(self) if isinstance(ctx, CtxKV) else None
+        if kv is not None:  # text K/V precomputed once per prompt batch (UNet2DConditionModel.ctx_kv)
+            q = self.to_q(x)
+            k, v = kv
+        else:
+            c = x if ctx is None else (ctx.ctx if isinstance(ctx, CtxKV) else ctx)
+            q = self.to_q(x)
+            k = self.to_k(c)
+            v = self.to_v(c)
         hd = q.shape[-1] // self.heads
-        o = ops.flash_attention(q.view(B, S, self.heads, hd), k.view(B, c.shape[1], self.heads, hd),
-                                v.view(B, c.shape[1], self.heads, hd), causal=False)
+        L = k.shape[1]
+        o = ops.flash_attention(q.view(B, S, self.heads, hd), k.view(B, L, self.heads, hd),
+                                v.view(B, L, self.heads, hd), causal=False)
         return self.to_out[0](o.reshape(B, S, -1))
+
+
+class CtxKV:
+    """Inference: the text context's K and V for every cross-attention layer, from ONE GEMM over
+    the concatenated to_k / to_v weights (UNet2DConditionModel.ctx_kv). The context is fixed for
+    all denoising steps of a prompt batch, so the 50-step loop
+    (online-inference/stable-diffusion/service/service.py:244-252) computes these projections once
+    instead of 2 x 16 GEMMs per step; each layer reads its K / V slices of ``table`` [B, L, width]
+    in place (row stride = width)."""
+
+    def __init__(self, ctx, table, offsets):
+        self.ctx, self.table, self.offsets = ctx, table, offsets
+
+    def get(self, attn):
+        o = self.offsets.get(id(attn))
+        if o is None:
+            return None
+        ko, vo, n = o
+        return self.table[:, :, ko:ko + n], self.table[:, :, vo:vo + n]
 
 
 class GEGLU(nn.Module):
@@ -624,6 +650,32 @@ class UNet2DConditionModel(nn.Module):
         _, w, b, offs = c
         return _TembAdds(temb, torch.add(b, F.linear(F.silu(temb), w)), offs)
 
+    def ctx_kv(self, ctx: torch.Tensor, out: CtxKV | None = None) -> CtxKV:
+        """Every cross-attention layer's K and V of the text context ``ctx`` [B, L, cross_dim] as one
+        GEMM (see CtxKV). ``out``: recompute into that object's table (static graph buffers)."""
+        attns = [m for m in self.modules() if isinstance(m, Attention) and m.cross]
+        ps = [p for a in attns for p in (a.to_k.weight, a.to_v.weight, a.to_k.bias, a.to_v.bias) if p is not None]
+        key = tuple((p.data_ptr(), p._version) for p in ps)
+        c = getattr(self, "_ctxkv_cache", None)
+        if c is None or c[0] != key:
+            ws, bs, offs, o = [], [], {}, 0
+            for a in attns:
+                n = a.to_k.weight.shape[0]
+                offs[id(a)] = (o, o + n, n)
+                o += 2 * n
+                for lin in (a.to_k, a.to_v):
+                    ws.append(lin.weight)
+                    bs.append(lin.bias if lin.bias is not None else lin.weight.new_zeros(n))
+            has_b = any(lin.bias is not None for a in attns for lin in (a.to_k, a.to_v))
+            c = self._ctxkv_cache = (key, torch.cat(ws), torch.cat(bs) if has_b else None, offs)
+        _, w, b, offs = c
+        ctx = ctx.to(w.dtype)
+        if out is not None and out.table.shape[:2] == ctx.shape[:2] and out.table.shape[2] == w.shape[0]:
+            out.table.copy_(F.linear(ctx, w, b))
+            out.ctx = ctx
+            return out
+        return CtxKV(ctx, F.linear(ctx, w, b), offs)
+
     def _run(self, fn, *args):
         if self.gradient_checkpointing and self.training and torch.is_grad_enabled():
             from torch.utils.checkpoint import checkpoint
@@ -640,7 +692,8 @@ class UNet2DConditionModel(nn.Module):
         if (_TEMB_BATCH and _FOLD_BIAS and not torch.is_grad_enabled() and self.channels_last and temb.is_cuda
                 and temb.dtype == torch.bfloat16):
             temb = self._temb_adds(temb)
-        ctx = encoder_hidden_states.to(sample.dtype)
+        ctx = encoder_hidden_states if isinstance(encoder_hidden_states, CtxKV) else \
+            encoder_hidden_states.to(sample.dtype)
         if self.channels_last:
             sample = sample.contiguous(memory_format=torch.channels_last)
         x = self.conv_in(sample)

@@ -272,3 +272,28 @@ def test_phase_gemm_upsampler_equals_nearest_conv3x3_cpu():
         got = up.phase_to_dense(t, (2 * h, 2 * w), b)
         ref = F.conv2d(F.interpolate(x, scale_factor=2.0, mode="nearest"), wt, b, padding=1)
         assert torch.allclose(got, ref, atol=1e-4, rtol=1e-4)
+
+
+def test_unet_ctx_kv_precompute_matches_per_step_projection_cpu():
+    """models/unet.py CtxKV: the cross-attention K/V of the text context from one concatenated
+    GEMM, read as strided slices by every layer, give the same UNet output as per-layer to_k/to_v."""
+    import torch
+
+    from kubernetes_cloud_amd.models.unet import CtxKV, UNet2DConditionModel, UNetConfig
+    torch.manual_seed(0)
+    cfg = UNetConfig(block_out_channels=(32, 64, 64, 64), cross_attention_dim=32, sample_size=16,
+                     norm_num_groups=8)
+    m = UNet2DConditionModel(cfg).eval()
+    x = torch.randn(2, cfg.in_channels, 16, 16)
+    ctx = torch.randn(2, 7, cfg.cross_attention_dim)
+    with torch.no_grad():
+        ref = m(x, 10, ctx)
+        kv = m.ctx_kv(ctx)
+        assert isinstance(kv, CtxKV) and len(kv.offsets) == sum(1 for a in m.modules() if getattr(a, "cross", False))
+        got = m(x, 10, kv)
+        kv2 = m.ctx_kv(ctx * 2, out=kv)  # recompute in place (the graph's static table)
+        assert kv2 is kv
+        got2 = m(x, 10, kv)
+        ref2 = m(x, 10, ctx * 2)
+    assert torch.allclose(got, ref, atol=1e-5, rtol=1e-4)
+    assert torch.allclose(got2, ref2, atol=1e-5, rtol=1e-4)

@@ -102,3 +102,27 @@ def test_vae_decoder_phase_upsampler_matches_plain(monkeypatch):
     plain = plain.sample if hasattr(plain, "sample") else plain
     err = (fused.float() - plain.float()).abs().max().item()
     assert err < 0.03 * plain.float().abs().max().item() + 1e-3, err
+
+
+def test_unet_graph_ctx_kv_cache_tracks_context():
+    """sd_pipeline.UNetGraph projects the text K/V once per context tensor (CtxKV): replays with the
+    same ctx reuse them, a new ctx recomputes them, and both match the eager UNet."""
+    from kubernetes_cloud_amd.models.sd_pipeline import UNetGraph
+    from kubernetes_cloud_amd.models.unet import UNet2DConditionModel, UNetConfig, to_channels_last
+    torch.manual_seed(0)
+    cfg = UNetConfig(block_out_channels=(64, 128, 128, 128), cross_attention_dim=64, sample_size=32)
+    m = to_channels_last(UNet2DConditionModel(cfg).to(DEV).bfloat16().eval())
+    g = UNetGraph(m)
+    assert g.ctx_kv
+    x = torch.randn(2, cfg.in_channels, 32, 32, device=DEV, dtype=torch.bfloat16)
+    t = torch.full((2,), 10.0, device=DEV)
+    c1 = torch.randn(2, 8, cfg.cross_attention_dim, device=DEV, dtype=torch.bfloat16)
+    c2 = torch.randn(2, 8, cfg.cross_attention_dim, device=DEV, dtype=torch.bfloat16)
+    with torch.no_grad():
+        outs = []
+        for c in (c1, c1, c2, c2, c1):
+            outs.append(g(x, t, c).clone())
+        e1, e2 = m(x, t, c1), m(x, t, c2)
+    for o, e in zip(outs, (e1, e1, e2, e2, e1)):
+        err = (o.float() - e.float()).abs().max().item()
+        assert err < 0.02 * e.float().abs().max().item() + 1e-3, err
