@@ -4,11 +4,11 @@ from . import _lib
 from .activations import add_bias_nhwc, gelu, geglu, quick_gelu
 from .attention import attention_reference, flash_attention, qkv_rope_attention
 from .loss import cross_entropy, mse_loss
-from .norms import group_norm, layer_norm
+from .norms import group_norm, group_norm_cat, layer_norm
 from .rope import apply_rotary_, rope_tables, rotary_reference
 
 __all__ = [
     "_lib", "add_bias_nhwc", "gelu", "geglu", "quick_gelu", "flash_attention", "qkv_rope_attention",
-    "attention_reference", "cross_entropy", "mse_loss", "layer_norm", "group_norm",
+    "attention_reference", "cross_entropy", "mse_loss", "layer_norm", "group_norm", "group_norm_cat",
     "apply_rotary_", "rope_tables", "rotary_reference",
 ]
