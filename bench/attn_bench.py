@@ -35,6 +35,10 @@ SHAPES = {
     "d160_1k": (16, 1024, 1024, 8, 160, False),
     "d160_4k": (4, 4096, 4096, 8, 160, True),  # SD-1.5 1280-channel heads (native D=160 full tiles)
     "sd_cross": (16, 4096, 77, 8, 40, False),
+    # the UNet inference call: 40 real dims stored 48 wide, V column 40 = 1 (row sums on the MFMA) ...
+    "sd_64_pad48_rs": (16, 4096, 4096, 8, 48, False, "rowsum"),
+    # ... and K pre-scaled with column 40 = 1 (softmax offset in the S MFMA, attention_tiled.hip MC)
+    "sd_64_pad48_mc": (16, 4096, 4096, 8, 48, False, "maxcol"),
 }
 
 
@@ -51,18 +55,36 @@ def timeit(fn, iters=10, warmup=3):
     return s.elapsed_time(e) / iters
 
 
-def run(name, B, Sq, Sk, H, D, causal, sdpa=True, bwd=True):
+def run(name, B, Sq, Sk, H, D, causal, mode="", sdpa=True, bwd=True):
+    import math
     dev = "cuda"
     q = torch.randn(B, Sq, H, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
     k = torch.randn(B, Sk, H, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
     v = torch.randn(B, Sk, H, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
     flops = 4.0 * B * H * Sq * Sk * D * (0.5 if causal else 1.0)
     out = {"shape": name, "B": B, "Sq": Sq, "Sk": Sk, "H": H, "D": D, "causal": causal}
+    kw = {}
+    if mode:  # fwd-only inference variants on 40 real dims
+        bwd = sdpa = False
+        with torch.no_grad():
+            for t in (q, k, v):
+                t[..., 40:] = 0
+            v[..., 40] = 1.0
+            kw = dict(rowsum_col=40, scale=40 ** -0.5)
+            if mode == "maxcol":
+                k[..., :40] *= 40 ** -0.5 * math.log2(math.e)
+                k[..., 40] = 1.0
+                kw.update(max_col=40, scale=math.log(2.0))
 
     def f_fwd():
         with torch.no_grad():
-            ops.flash_attention(q, k, v, causal=causal)
+            ops.flash_attention(q, k, v, causal=causal, **kw)
 
+    if not bwd:
+        t = timeit(f_fwd)
+        out["native_fwd_ms"] = round(t, 3)
+        out["native_fwd_tflops"] = round(flops / t / 1e9, 1)
+        return out
     o = ops.flash_attention(q, k, v, causal=causal)
     g = torch.randn_like(o)
 

@@ -1029,12 +1029,14 @@ KCA_API int kca_attn_fwd_tiled(const void* q, const void* k, const void* v, void
                                long long k_st, long long k_sh, long long v_sb, long long v_st,
                                long long v_sh, long long o_sb, long long o_st, long long o_sh,
                                int B, int Sq, int Sk, int H, int Hkv, int d, int causal,
-                               float scale, int rowsum_col, int* flags, hipStream_t stream);
+                               float scale, int rowsum_col, int max_col, int* flags, hipStream_t stream);
 
 // workspace: >= 4 * ceil(Sq/128) * B * H ints for the full-tile fast path of
 // attention_tiled.hip (its overflow flags), or null for the generic kernel.
 // rowsum_col: >= 0 when V's padded column rowsum_col is all ones (the fast path then takes the
-// row sums from O; the generic kernel ignores it), -1 otherwise.
+// row sums from O; the generic kernel ignores it), -1 otherwise. max_col: >= 0 when K is pre-scaled
+// by scale' * log2(e) with column max_col = 1 (attention_tiled.hip MC; the caller passes scale = ln 2
+// so the generic fixup kernel, which reads Q's zero column max_col, computes the same softmax).
 KCA_API int kca_attn_fwd(const void* q, const void* k, const void* v, void* o,
                          float* lse, long long q_sb, long long q_st,
                          long long q_sh, long long k_sb, long long k_st,
@@ -1043,7 +1045,7 @@ KCA_API int kca_attn_fwd(const void* q, const void* k, const void* v, void* o,
                          long long o_sh, int B, int Sq, int Sk, int H, int Hkv,
                          int d_real, int causal, float scale,
                          const float* alibi, const int* kv_len, int window, const unsigned* key_mask,
-                         int rowsum_col, int* workspace, hipStream_t stream) {
+                         int rowsum_col, int max_col, int* workspace, hipStream_t stream) {
   if (d_real % 8 || H % Hkv || window < 0) return 1;
   const int D = pick_d(d_real);
   AttnParams p{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, lse,
@@ -1052,8 +1054,8 @@ KCA_API int kca_attn_fwd(const void* q, const void* k, const void* v, void* o,
                window, key_mask, (Sk + 31) / 32};
   if (g_attn_tiled && workspace && !alibi && !kv_len && !window && !key_mask &&
       kca_attn_fwd_tiled(q, k, v, o, lse, q_sb, q_st, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh,
-                         o_sb, o_st, o_sh, B, Sq, Sk, H, Hkv, d_real, causal, scale, rowsum_col, workspace,
-                         stream) == 0)
+                         o_sb, o_st, o_sh, B, Sq, Sk, H, Hkv, d_real, causal, scale, rowsum_col, max_col,
+                         workspace, stream) == 0)
     p.fix_flags = workspace;  // fixup launch below: only flagged blocks do work
   dim3 grid(((Sq + 127) / 128) * B * H);
   ATTN_D_DISPATCH(D, {

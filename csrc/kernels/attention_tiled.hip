@@ -313,7 +313,11 @@ __device__ __forceinline__ void store_tile_lds(bf16_t* row0, long long st, const
 // sum_k bf16(P) on the matrix pipe: the per-element f32 adds of the row sum leave the VALU, which
 // bounds this loop at D = 64 (SD-1.5's 40-wide heads, padded).
 // DS < D: heads stored DS wide (StagerNarrow); the contraction over d runs DS / 16 MFMA steps.
-template <int D, bool CAUSAL, int OC = -1, int DS = D>
+// MC >= 0 ("max column", with OC; non-causal): K arrives pre-scaled by scale * log2(e) with its zero-padded
+// column MC set to 1.0 (the SD UNet folds both into its padded QKV weights), and the kernel writes
+// -m into Q's column MC in registers once m is known, so the S MFMAs return s * log2(e) - m and
+// P = exp2(S) needs no per-element FMA: the D <= 64 loop is bound by that VALU work, not the MFMAs.
+template <int D, bool CAUSAL, int OC = -1, int DS = D, int MC = -1>
 __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel(FastFwdParams p) {
   constexpr int BM = 128, BN = 32;
   constexpr int TILE = BN * D * 2;           // bytes per K or V tile (LDS image)
@@ -338,7 +342,8 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel
   int kv_hi = p.Sk;
   if (CAUSAL) kv_hi = min(kv_hi, qb * BM + BM + off);
   const int ntiles = kv_hi > 0 ? (kv_hi + BN - 1) / BN : 0;
-  const float sl2 = p.scale * kLog2e;
+  static_assert(MC < 0 || (!CAUSAL && OC >= 0 && MC < DS), "max column: non-causal, with the row-sum column");
+  const float sl2 = MC >= 0 ? 1.f : p.scale * kLog2e;
 
   const bf16_t* qp = p.q + b * p.q_sb + h * p.q_sh;
   const bf16_t* kp = p.k + b * p.k_sb + hk * p.k_sh;
@@ -444,6 +449,14 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel
     for (int r = 1; r < 16; ++r) mt = fmaxf(mt, sa[r]);
     m = fmaxf(mt, __shfl_xor(mt, 32, 64)) * sl2;
   }
+  if constexpr (MC >= 0) {
+    // Q[MC] = -m (bf16: m is rounded so the MFMA's offset and lse agree); tile 0's S, taken
+    // before m existed, gets the offset here; tiles >= 1 come out of qk() with it
+    m = (float)(__bf16)m;
+    if (hh == (MC % 16) / 8) qf[MC / 16][MC % 8] = (__bf16)(-m);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sa[r] -= m;
+  }
   const float nm = -m;
   ASTAMP(0);
 
@@ -472,8 +485,8 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel
     bf16x8 pf0, pf1;
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
-      const float e0 = __builtin_amdgcn_exp2f(fmaf(sa[r], sl2, nm));
-      const float e1 = __builtin_amdgcn_exp2f(fmaf(sa[r + 8], sl2, nm));
+      const float e0 = __builtin_amdgcn_exp2f(MC >= 0 ? sa[r] : fmaf(sa[r], sl2, nm));
+      const float e1 = __builtin_amdgcn_exp2f(MC >= 0 ? sa[r + 8] : fmaf(sa[r + 8], sl2, nm));
       if constexpr (OC < 0) ps += e0 + e1;
       pf0[r] = (__bf16)e0;
       pf1[r] = (__bf16)e1;
@@ -971,10 +984,11 @@ KCA_API int kca_attn_fwd_tiled(const void* q, const void* k, const void* v, void
                                long long k_st, long long k_sh, long long v_sb, long long v_st,
                                long long v_sh, long long o_sb, long long o_st, long long o_sh,
                                int B, int Sq, int Sk, int H, int Hkv, int d, int causal,
-                               float scale, int rowsum_col, int* flags, hipStream_t stream) {
+                               float scale, int rowsum_col, int max_col, int* flags, hipStream_t stream) {
   if ((d != 48 && d != 64 && d != 96 && d != 128 && d != 160 && d != 256) || Sq % 128 || Sk % 32 || Sq <= 0 ||
       H % Hkv || !flags)
     return 1;
+  if (max_col >= 0 && (max_col != 40 || rowsum_col != 40 || d != 48)) return 1;  // instantiated variant
   if (d == 48 && causal) return 1;  // narrow storage: SD-1.5's (non-causal) 40-wide heads
   if (rowsum_col >= 0 && (rowsum_col != 40 || (d != 64 && d != 48) || causal)) return 1;  // instantiated variants
   if (causal && Sk < Sq) return 1;
@@ -997,7 +1011,8 @@ KCA_API int kca_attn_fwd_tiled(const void* q, const void* k, const void* v, void
     if (causal) hipLaunchKernelGGL((attn_fwd_tiled_kernel<96, true>), grid, dim3(256), 0, stream, p);
     else hipLaunchKernelGGL((attn_fwd_tiled_kernel<96, false>), grid, dim3(256), 0, stream, p);
   } else if (d == 48) {  // SD-1.5 heads (40) zero-padded to 48 by the UNet inference path, D = 64 image
-    if (rowsum_col == 40) hipLaunchKernelGGL((attn_fwd_tiled_kernel<64, false, 40, 48>), grid, dim3(256), 0, stream, p);
+    if (max_col == 40) hipLaunchKernelGGL((attn_fwd_tiled_kernel<64, false, 40, 48, 40>), grid, dim3(256), 0, stream, p);
+    else if (rowsum_col == 40) hipLaunchKernelGGL((attn_fwd_tiled_kernel<64, false, 40, 48>), grid, dim3(256), 0, stream, p);
     else hipLaunchKernelGGL((attn_fwd_tiled_kernel<64, false, -1, 48>), grid, dim3(256), 0, stream, p);
   } else {  // 64: GPT-2 / CLIP heads
     if (causal) hipLaunchKernelGGL((attn_fwd_tiled_kernel<64, true>), grid, dim3(256), 0, stream, p);

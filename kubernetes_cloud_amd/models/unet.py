@@ -233,6 +233,9 @@ _PAD_HEADS = os.environ.get("KCA_SD_PAD_HEADS", "1") not in ("0", "false")
 ROWSUM_COL = 40  # SD-1.5's 40-wide heads: padded V column 40 carries ones (softmax row sums on the MFMA)
 _ROWSUM = os.environ.get("KCA_SD_ROWSUM_COL", "1") not in ("0", "false")
 _PAD_TRAIN = os.environ.get("KCA_SD_PAD_HEADS_TRAIN", "1") not in ("0", "false")
+# inference, 48-wide heads: K stored pre-scaled by scale * log2(e) with pad column 40 = 1, so the tiled
+# kernel's S MFMAs also subtract the softmax offset (attention_tiled.hip MC); KCA_SD_MAX_COL=0 disables
+_MAX_COL = os.environ.get("KCA_SD_MAX_COL", "1") not in ("0", "false")
 _PAD_GEN = 0
 # inference: residual adds carried by the preceding GEMM's epilogue (ops.linear_residual);
 # KCA_SD_FUSE_RES=0 keeps the separate adds (A/B knob)
@@ -271,11 +274,13 @@ class Attention(nn.Module):
         self._padded = None  # weights may change while training: rebuild on the next inference call
         return super().train(mode)
 
-    def _padded_weights(self, hd: int, dp: int):
+    def _padded_weights(self, hd: int, dp: int, max_col: bool = False):
         """One fused QKV weight with each head zero-padded to dp rows, and the
         out-projection with matching zero columns (built once per eval phase;
-        ``train()`` drops it)."""
+        ``train()`` drops it). ``max_col``: K rows pre-scaled by scale * log2(e), K column 40 = 1."""
         p = getattr(self, "_padded", None)
+        if p is not None and p[3] != max_col:
+            p = None
         if p is None:
             global _PAD_GEN
             H = self.heads
@@ -293,12 +298,20 @@ class Attention(nn.Module):
                 # rowsum_col); the out-projection's zero columns ignore it
                 b[2, :, ROWSUM_COL] = 1.0
                 has_b = True
+            if max_col:  # softmax scale and log2(e) folded into K (fp32 product, one bf16 rounding)
+                f = math.log2(math.e) / math.sqrt(hd)
+                for i_, lin in ((1, self.to_k),):
+                    w[i_, :, :hd] = (lin.weight.float().view(H, hd, C) * f).to(w.dtype)
+                    if lin.bias is not None:
+                        b[i_, :, :hd] = (lin.bias.float().view(H, hd) * f).to(b.dtype)
+                b[1, :, ROWSUM_COL] = 1.0
             wo = self.to_out[0].weight
             wo_p = wo.new_zeros(wo.shape[0], H, dp)
             wo_p[:, :, :hd] = wo.view(wo.shape[0], H, hd)
-            p = self._padded = (w.view(3 * H * dp, C), b.view(-1) if has_b else None, wo_p.view(wo.shape[0], H * dp))
+            p = self._padded = (w.view(3 * H * dp, C), b.view(-1) if has_b else None, wo_p.view(wo.shape[0], H * dp),
+                                max_col)
             _PAD_GEN += 1
-        return p
+        return p[:3]
 
     def forward(self, x, ctx=None):
         B, S, _ = x.shape
@@ -323,12 +336,13 @@ class Attention(nn.Module):
             # columns leave Q.K^T unchanged, zero v columns give zero outputs that meet zero
             # out-projection columns. SD-1.5 64x64-latent self-attention (B16 H8 S4096 d40)
             # 1.04 -> 0.71 ms on MI355X at 64 wide (profiles/attn_bench_r1_v7_d64.jsonl).
-            w, b, wo = self._padded_weights(hd, dpad)
+            rs = dpad in (48, 64) and hd == ROWSUM_COL and _ROWSUM
+            mc = rs and dpad == 48 and _MAX_COL
+            w, b, wo = self._padded_weights(hd, dpad, max_col=mc)
             qkv = F.linear(x, w, b).view(B, S, 3, self.heads, dpad)
             o = ops.flash_attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], causal=False,
-                                    scale=1.0 / math.sqrt(hd),
-                                    rowsum_col=ROWSUM_COL if (dpad in (48, 64) and hd == ROWSUM_COL and _ROWSUM)
-                                    else -1)
+                                    scale=math.log(2.0) if mc else 1.0 / math.sqrt(hd),
+                                    rowsum_col=ROWSUM_COL if rs else -1, max_col=ROWSUM_COL if mc else -1)
             return F.linear(o.reshape(B, S, -1), wo, self.to_out[0].bias)
         kv = ctx.get(self) if isinstance(ctx, CtxKV) else None
         if kv is not None:  # text K/V precomputed once per prompt batch (UNet2DConditionModel.ctx_kv)

@@ -58,7 +58,7 @@ _SIGS = {
     "kca_sumsq": [P, LL, P, P, P],
     "kca_adamw8bit": [P, P, P, P, P, P, P, LL, P, F, F, F, F, F, F, F, P, P, P],
     "kca_clip_coef": [P, F, F, P, P, P, P],
-    "kca_attn_fwd": [P] * 5 + [LL] * 12 + [I] * 7 + [F, P, P, I, P, I, P, P],
+    "kca_attn_fwd": [P] * 5 + [LL] * 12 + [I] * 7 + [F, P, P, I, P, I, I, P, P],
     "kca_attn_bwd_preprocess": [P, P, P, LL, LL, LL, LL, LL, LL, I, I, I, I, P],
     "kca_attn_bwd": [P] * 10 + [LL] * 21 + [I] * 7 + [F, P, P, I, P, P],
     "kca_attn_set_tiled": [I],

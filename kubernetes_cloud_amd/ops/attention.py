@@ -94,7 +94,8 @@ def _masks(kv_len):
     return (kv_len, None) if kv_len.dim() == 1 else (None, kv_len)
 
 
-def _fwd(q, k, v, causal, scale, kv_len, alibi, out=None, window: int = 0, rowsum_col: int = -1):
+def _fwd(q, k, v, causal, scale, kv_len, alibi, out=None, window: int = 0, rowsum_col: int = -1,
+         max_col: int = -1):
     B, Sq, H, D = q.shape
     Sk, Hkv = k.shape[1], k.shape[2]
     o = out if out is not None else torch.empty(B, Sq, H, D, device=q.device, dtype=q.dtype)
@@ -105,7 +106,7 @@ def _fwd(q, k, v, causal, scale, kv_len, alibi, out=None, window: int = 0, rowsu
     _lib.call("kca_attn_fwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr(),
               *_strides(q), *_strides(k), *_strides(v), *_strides(o),
               B, Sq, Sk, H, Hkv, D, int(causal), float(scale), _lib.ptr(alibi), _lib.ptr(lens),
-              int(window), _lib.ptr(km), int(rowsum_col), flags.data_ptr(), _lib.stream())
+              int(window), _lib.ptr(km), int(rowsum_col), int(max_col), flags.data_ptr(), _lib.stream())
     return o, lse
 
 
@@ -166,18 +167,25 @@ def native_mask(kv_len, device):
 
 def flash_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool = False,
                     scale: float | None = None, kv_len: torch.Tensor | None = None,
-                    alibi: torch.Tensor | None = None, window: int = 0, rowsum_col: int = -1) -> torch.Tensor:
+                    alibi: torch.Tensor | None = None, window: int = 0, rowsum_col: int = -1,
+                    max_col: int = -1) -> torch.Tensor:
     """softmax(scale * Q K^T + alibi + mask) V over [B, S, H, D] views.
     ``rowsum_col`` (inference): V's zero-padded column that the caller filled
     with ones -- the D=64 fast kernel then takes the softmax row sums from the
-    output instead of summing on the VALU (the SD UNet's padded heads)."""
+    output instead of summing on the VALU (the SD UNet's padded heads).
+    ``max_col`` (inference, with ``rowsum_col``, 48-wide heads): K holds
+    K * s * log2(e) with its zero-padded column ``max_col`` set to 1, where s is the
+    true softmax scale, and ``scale`` must be ln 2 (attention_tiled.hip MC: the
+    softmax offset rides in the S MFMA)."""
     scale = scale if scale is not None else 1.0 / math.sqrt(q.shape[-1])
     if alibi is not None:
         alibi = alibi.to(device=q.device, dtype=torch.float32).contiguous()
     if rowsum_col >= 0 and _lib.use_native(q, k, v) and not torch.is_grad_enabled():
         _check(q, k, v)
         return _fwd(q, k, v, causal, scale, native_mask(kv_len, q.device), alibi, window=window,
-                    rowsum_col=rowsum_col)[0]
+                    rowsum_col=rowsum_col, max_col=max_col)[0]
+    if max_col >= 0:
+        raise ValueError("max_col needs rowsum_col and the native inference path")
     if _lib.use_native(q, k, v):
         return _FlashAttnFn.apply(q, k, v, causal, scale, native_mask(kv_len, q.device), alibi, int(window))
     o, _ = attention_reference(q, k, v, causal, scale, kv_len, alibi, window)

@@ -187,3 +187,41 @@ def test_unet_inference_heads_are_48_wide():
     assert unet.padded_head_dim(40, infer=True) == 48
     assert unet.padded_head_dim(40) == 64  # training keeps the fwd+bwd D=64 kernels
     assert unet.padded_head_dim(80, infer=True) == 96
+
+
+def test_narrow_48_max_column_matches_reference():
+    """attention_tiled.hip MC: K pre-scaled by s*log2(e) with pad column 40 = 1, scale = ln 2, V column
+    40 = 1 (row sums): the S MFMAs carry the softmax offset; equals the fp32 reference at scale s."""
+    import math
+    torch.manual_seed(13)
+    B, S, H = 2, 2048, 8
+    s = 40 ** -0.5
+    qkv = torch.zeros(B, S, 3, H, 48, device=DEV, dtype=torch.bfloat16)
+    qkv[..., :40] = (torch.randn(B, S, 3, H, 40, device=DEV) * 1.5).bfloat16()
+    ref, lse_ref = attention_reference(qkv[:, :, 0, :, :40], qkv[:, :, 1, :, :40], qkv[:, :, 2, :, :40], False, s)
+    qkv[:, :, 1, :, :40] = (qkv[:, :, 1, :, :40].float() * s * math.log2(math.e)).bfloat16()
+    qkv[:, :, 1, :, 40] = 1.0
+    qkv[:, :, 2, :, 40] = 1.0
+    q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+    with torch.no_grad(), torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CUDA]) as prof:
+        o = ops.flash_attention(q, k, v, causal=False, scale=math.log(2.0), rowsum_col=40, max_col=40)
+        torch.cuda.synchronize()
+    assert _rel(o[..., :40], ref) < 1.5e-2
+    assert float((o[..., 40].float() - 1).abs().max()) < 2e-2
+    names = [e.name for e in prof.events()]
+    assert any("attn_fwd_tiled" in n and "40, 48, 40" in n for n in names), sorted(set(names))[:8]
+
+
+def test_unet_attention_max_column_matches_plain(monkeypatch):
+    from kubernetes_cloud_amd.models import unet
+    from kubernetes_cloud_amd.models.unet import Attention
+    torch.manual_seed(5)
+    att = Attention(320, 8, 40).to(DEV).bfloat16().eval()
+    for p_ in att.parameters():
+        torch.nn.init.normal_(p_, std=0.05)
+    x = torch.randn(2, 4096, 320, device=DEV, dtype=torch.bfloat16)
+    with torch.no_grad():
+        fast = att(x)
+        monkeypatch.setattr(unet, "_MAX_COL", False)
+        plain = att(x)
+    assert _rel(fast, plain) < 2e-2
