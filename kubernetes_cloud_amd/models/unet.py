@@ -128,8 +128,10 @@ class TimestepEmbedding(nn.Module):
 _Linear = SplitKLinear if os.environ.get("KCA_SD_SPLITK_WGRAD", "1") not in ("0", "false") else nn.Linear
 
 
-# KCA_SD_FOLD_BIAS=0 keeps the biased convolutions + separate residual add at inference (A/B knob)
+# KCA_SD_FOLD_BIAS=0 keeps the biased convolutions + separate residual add at inference (A/B knob);
+# KCA_SD_FOLD_BIAS_TRAIN=0 the same in training
 _FOLD_BIAS = os.environ.get("KCA_SD_FOLD_BIAS", "1") not in ("0", "false")
+_FOLD_BIAS_TRAIN = os.environ.get("KCA_SD_FOLD_BIAS_TRAIN", "1") not in ("0", "false")
 
 
 class ResnetBlock2D(nn.Module):
@@ -149,6 +151,10 @@ class ResnetBlock2D(nn.Module):
             return self._forward_folded(x, temb)
         if isinstance(temb, _TembAdds):
             temb = temb.temb
+        if (_FOLD_BIAS_TRAIN and torch.is_grad_enabled() and x.is_cuda and x.dtype == torch.bfloat16
+                and x.is_contiguous(memory_format=torch.channels_last) and self.conv1.bias is not None
+                and self.conv2.bias is not None):
+            return self._forward_folded_train(x, temb)
         h = self.conv1(self.norm1(x))
         t = None
         if self.time_emb_proj is not None and temb is not None:
@@ -184,6 +190,26 @@ class ResnetBlock2D(nn.Module):
         _, bias = self._folded_biases()
         sc = F.conv2d(x, self.conv_shortcut.weight, None) if self.conv_shortcut is not None else x
         return ops.add_bias_nhwc(sc, h, bias)
+
+    def _forward_folded_train(self, x, temb):
+        """Training with the convolution biases folded out of the convolutions (as at inference):
+        conv1's bias joins the [B, C] time embedding the GroupNorm adds, conv2's (+ the shortcut's)
+        joins the residual add (ops.add_bias_nhwc_train, bias gradient by a column sum). Exact:
+        the same sums in another order; removes each biased convolution's broadcast-add pass and
+        PyTorch's bias-gradient reduction over the full activation."""
+        h = F.conv2d(self.norm1(x), self.conv1.weight, None, padding=1)
+        add = self.conv1.bias[None].expand(x.shape[0], -1)
+        if self.time_emb_proj is not None and temb is not None:
+            add = add + self.time_emb_proj(F.silu(temb))
+        h = F.conv2d(self.dropout(self.norm2(h, add=add)), self.conv2.weight, None, padding=1)
+        bias = self.conv2.bias.float()
+        if self.conv_shortcut is not None:
+            sc = F.conv2d(x, self.conv_shortcut.weight, None)
+            if self.conv_shortcut.bias is not None:
+                bias = bias + self.conv_shortcut.bias.float()
+        else:
+            sc = x
+        return ops.add_bias_nhwc_train(sc, h, bias)
 
     def _folded_biases(self):
         """fp32 conv1 bias and conv2 (+ shortcut) bias, cached while the parameters are unchanged
@@ -233,6 +259,9 @@ _PAD_HEADS = os.environ.get("KCA_SD_PAD_HEADS", "1") not in ("0", "false")
 ROWSUM_COL = 40  # SD-1.5's 40-wide heads: padded V column 40 carries ones (softmax row sums on the MFMA)
 _ROWSUM = os.environ.get("KCA_SD_ROWSUM_COL", "1") not in ("0", "false")
 _PAD_TRAIN = os.environ.get("KCA_SD_PAD_HEADS_TRAIN", "1") not in ("0", "false")
+# training: padded heads from one fused QKV GEMM (Attention.forward); KCA_SD_FUSED_QKV_TRAIN=0 keeps the
+# three projections + activation pads
+_FUSED_QKV_TRAIN = os.environ.get("KCA_SD_FUSED_QKV_TRAIN", "1") not in ("0", "false")
 # inference, 48-wide heads: K stored pre-scaled by scale * log2(e) with pad column 40 = 1, so the tiled
 # kernel's S MFMAs also subtract the softmax offset (attention_tiled.hip MC); KCA_SD_MAX_COL=0 disables
 _MAX_COL = os.environ.get("KCA_SD_MAX_COL", "1") not in ("0", "false")
@@ -319,6 +348,28 @@ class Attention(nn.Module):
         train = torch.is_grad_enabled()
         dpad = padded_head_dim(hd, infer=not train)
         pad = ctx is None and x.is_cuda and dpad != hd and hd % 8 == 0 and S % 128 == 0 and _PAD_HEADS
+        if pad and train and _PAD_TRAIN and _FUSED_QKV_TRAIN:
+            # training: ONE GEMM with the zero-padded q/k/v weights (built per step from the three
+            # Linears, differentiably: the weight gradients slice back through F.pad / cat) writes the
+            # padded heads straight into a fused [B, S, 3*H*dpad] buffer; the attention backward writes
+            # dQ/dK/dV into one buffer (ops.qkv_rope_attention); the out-projection takes the padded
+            # heads through zero weight columns -- no activation pads, slices or per-projection grad adds
+            H, C = self.heads, x.shape[-1]
+
+            def _padw(lin):
+                return F.pad(lin.weight.view(H, hd, C), (0, 0, 0, dpad - hd)).reshape(H * dpad, C)
+
+            w = torch.cat([_padw(self.to_q), _padw(self.to_k), _padw(self.to_v)])
+            bs = [lin.bias for lin in (self.to_q, self.to_k, self.to_v)]
+            b = None
+            if any(t is not None for t in bs):
+                b = torch.cat([F.pad((t if t is not None else w.new_zeros(H * hd)).view(H, hd), (0, dpad - hd))
+                               .reshape(-1) for t in bs])
+            qkv = linear_splitk_wgrad(x, w, b)
+            o = ops.qkv_rope_attention(qkv, H, dpad, 0, False, causal=False, scale=1.0 / math.sqrt(hd))
+            wo = self.to_out[0].weight
+            wo_p = F.pad(wo.view(wo.shape[0], H, hd), (0, dpad - hd)).reshape(wo.shape[0], H * dpad)
+            return linear_splitk_wgrad(o, wo_p, self.to_out[0].bias)
         if pad and train and _PAD_TRAIN:
             # training: pad the q/k/v activations instead (F.pad's backward slices the
             # gradients back) so the backward also runs the full-tile D=64 kernels.

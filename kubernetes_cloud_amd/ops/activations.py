@@ -87,3 +87,30 @@ def add_bias_nhwc(a: torch.Tensor, b: torch.Tensor | None, bias: torch.Tensor) -
     _lib.call("kca_add_bias_nhwc", a.data_ptr(), _lib.ptr(b), bf.data_ptr(), out.data_ptr(), a.numel(),
               a.shape[1], _lib.stream())
     return out
+
+
+class _AddBiasNHWCFn(torch.autograd.Function):
+    """Training form of ``add_bias_nhwc``: forward in one native pass; backward hands ``dout`` to
+    both summands and the bias gradient is the column sum of ``dout`` viewed as [N*H*W, C]
+    (``ops.linear.column_sum``) -- instead of a separate biased convolution's broadcast add and
+    PyTorch's reduction over the full activation."""
+
+    @staticmethod
+    def forward(ctx, a, b, bias):
+        ctx.C = a.shape[1]
+        ctx.has_b = b is not None
+        return add_bias_nhwc(a, b, bias)
+
+    @staticmethod
+    def backward(ctx, dout):
+        from .linear import column_sum
+        d = dout.contiguous(memory_format=torch.channels_last)
+        db = column_sum(d.permute(0, 2, 3, 1).reshape(-1, ctx.C), out_dtype=torch.float32)
+        return d, (d if ctx.has_b else None), db
+
+
+def add_bias_nhwc_train(a: torch.Tensor, b: torch.Tensor | None, bias: torch.Tensor) -> torch.Tensor:
+    """``a + b + bias`` (channels-last) with autograd; the inference kernel when no grad is recorded."""
+    if torch.is_grad_enabled() and (a.requires_grad or (b is not None and b.requires_grad) or bias.requires_grad):
+        return _AddBiasNHWCFn.apply(a, b, bias)
+    return add_bias_nhwc(a, b, bias)

@@ -150,18 +150,19 @@ def _wgrad_splits(tokens: int, n: int, k: int) -> int:
 _COLSUM = __import__("os").environ.get("KCA_COLSUM", "1") not in ("0", "false")  # A/B knob
 
 
-def column_sum(x2: torch.Tensor) -> torch.Tensor:
-    """Sum over the rows of a [M, N] tensor (a bias gradient), in x2's dtype: ``kca_colsum_bf16``
-    (row-chunk partials, then a small fp32 sum) for contiguous bf16 on the GPU."""
+def column_sum(x2: torch.Tensor, out_dtype: torch.dtype | None = None) -> torch.Tensor:
+    """Sum over the rows of a [M, N] tensor (a bias gradient), in ``out_dtype`` (default x2's):
+    ``kca_colsum_bf16`` (row-chunk partials, then a small fp32 sum) for contiguous bf16 on the GPU."""
     M, N = x2.shape
+    out_dtype = out_dtype or x2.dtype
     if not (_COLSUM and _lib.use_native(x2) and x2.dtype == torch.bfloat16 and x2.is_contiguous() and N % 8 == 0
             and x2.data_ptr() % 16 == 0 and _lib.has("kca_colsum_bf16")):
-        return x2.sum(0)
+        return x2.sum(0) if out_dtype == x2.dtype else x2.sum(0, dtype=torch.float32).to(out_dtype)
     rb = max(64, -(-M // 256) // 8 * 8)  # ~256 row chunks
     nb = -(-M // rb)
     part = torch.empty(nb, N, device=x2.device, dtype=torch.float32)
     _lib.call("kca_colsum_bf16", x2.data_ptr(), part.data_ptr(), M, N, rb, _lib.stream())
-    return part.sum(0).to(x2.dtype)
+    return part.sum(0).to(out_dtype)
 
 
 class _LinearSplitKW(torch.autograd.Function):

@@ -126,3 +126,41 @@ def test_unet_graph_ctx_kv_cache_tracks_context():
     for o, e in zip(outs, (e1, e1, e2, e2, e1)):
         err = (o.float() - e.float()).abs().max().item()
         assert err < 0.02 * e.float().abs().max().item() + 1e-3, err
+
+
+def test_unet_training_fusions_match_plain_grads(monkeypatch):
+    """Training fusions (models/unet.py): conv biases folded into the time-embedding add and the
+    residual add (ops.add_bias_nhwc_train, bias grads by column sums) and the padded heads from one
+    fused QKV GEMM. Both bf16 paths are compared with an fp32 copy of the model (PyTorch reference
+    ops): per parameter, the fused path's gradient error is within the plain path's bf16 noise."""
+    import copy
+    from kubernetes_cloud_amd.models import unet
+    from kubernetes_cloud_amd.models.unet import UNet2DConditionModel, UNetConfig, to_channels_last
+    torch.manual_seed(0)
+    cfg = UNetConfig(block_out_channels=(320, 640, 640, 640), cross_attention_dim=64, sample_size=32)
+    base = UNet2DConditionModel(cfg).to(DEV).train()
+    m = to_channels_last(copy.deepcopy(base).bfloat16())
+    ref = to_channels_last(base.float())
+    x = torch.randn(2, cfg.in_channels, 32, 32, device=DEV).contiguous(memory_format=CL)
+    ctx = torch.randn(2, 8, cfg.cross_attention_dim, device=DEV)
+    tgt = torch.randn(2, cfg.out_channels, 32, 32, device=DEV, dtype=torch.float32)
+
+    def run(model, dt):
+        model.zero_grad(set_to_none=True)
+        loss = F.mse_loss(model(x.to(dt), 10, ctx.to(dt)).float(), tgt)
+        loss.backward()
+        return loss.item(), {n: p.grad.float().clone() for n, p in model.named_parameters() if p.grad is not None}
+
+    l1, g1 = run(m, torch.bfloat16)
+    monkeypatch.setattr(unet, "_FOLD_BIAS_TRAIN", False)
+    monkeypatch.setattr(unet, "_FUSED_QKV_TRAIN", False)
+    l0, g0 = run(m, torch.bfloat16)
+    lr, gr = run(ref, torch.float32)
+    assert abs(l1 - lr) < 1e-2 * abs(lr) + 1e-4, (l1, l0, lr)
+    assert set(g1) == set(g0) == set(gr)
+
+    def rel(a, b):
+        return ((a - b).norm() / (b.norm() + 1e-12)).item()
+    bad = [(n, rel(g1[n], gr[n]), rel(g0[n], gr[n])) for n in gr
+           if rel(g1[n], gr[n]) > max(2.0 * rel(g0[n], gr[n]), 0.03)]
+    assert not bad, bad[:5]
