@@ -14,6 +14,9 @@
 //                        that do not read the phase layout in place (the VAE decoder; the UNet's
 //                        concat GroupNorm reads it directly, groupnorm_nhwc.hip).
 //   kca_upsample2x_nhwc : plain nearest-x2 (the A/B baseline and the non-GEMM fallback).
+// Training (ops/upsample.py UpsampleConvPhase): the backward of the dense scatter is
+// kca_dense_to_phase_nhwc (the gather, zero where a phase's grid position is unused) and the
+// backward of the im2col is kca_col2im2x2_nhwc (each input pixel sums its 4 patch copies).
 #include "common.h"
 
 namespace {
@@ -81,6 +84,54 @@ __global__ void __launch_bounds__(256) upsample2x_kernel(const bf16_t* __restric
   *reinterpret_cast<u32x4*>(out + idx * 8) = *reinterpret_cast<const u32x4*>(x + src * 8);
 }
 
+// one thread per 16-B chunk of the phase layout [N, h+1, w+1, 4C]: the dense gradient [N, 2h, 2w, C]
+// gathered back (phase (a, b) of grid position (i, j) is dense pixel (2(i-a)+a, 2(j-b)+b) when
+// a <= i < h + a and b <= j < w + b, else unused: 0)
+__global__ void __launch_bounds__(256) dense_to_phase_kernel(const bf16_t* __restrict__ d, bf16_t* __restrict__ t,
+                                                             int h, int w, int C8, long long total) {
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total) return;
+  const int q = (int)(idx % (4 * C8));
+  const long long r = idx / (4 * C8);
+  const int k = q / C8, c8 = q % C8, a = k >> 1, b = k & 1;
+  const int j = (int)(r % (w + 1));
+  const long long ni = r / (w + 1);
+  const int i = (int)(ni % (h + 1));
+  const long long n = ni / (h + 1);
+  u32x4 v = {0u, 0u, 0u, 0u};
+  if (i >= a && i < h + a && j >= b && j < w + b) {
+    const int Y = 2 * (i - a) + a, X = 2 * (j - b) + b;
+    v = *reinterpret_cast<const u32x4*>(d + (((n * 2 * h + Y) * 2 * w + X) * (long long)C8 + c8) * 8);
+  }
+  *reinterpret_cast<u32x4*>(t + idx * 8) = v;
+}
+
+// one thread per 16-B chunk of dx [N, h, w, C]: dx[n, y, x] = sum over the 4 patches holding it,
+// dA[(n, y+1-s, x+1-t), (2s+t)C + c] (fp32 sum, one rounding)
+__global__ void __launch_bounds__(256) col2im2x2_kernel(const bf16_t* __restrict__ da, bf16_t* __restrict__ dx,
+                                                        int h, int w, int C8, long long total) {
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total) return;
+  const int c8 = (int)(idx % C8);
+  const long long pix = idx / C8;
+  const int x = (int)(pix % w);
+  const long long ny = pix / w;
+  const int y = (int)(ny % h);
+  const long long n = ny / h;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const long long row = (n * (h + 1) + (y + 1 - s)) * (w + 1) + (x + 1 - t);
+      float v[8];
+      load8(da + (row * 4 + (2 * s + t)) * (long long)C8 * 8 + c8 * 8, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += v[e];
+    }
+  store8(dx + idx * 8, acc);
+}
+
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 inline unsigned blocks_for(long long total) { return (unsigned)((total + 255) / 256); }
@@ -113,5 +164,23 @@ KCA_API int kca_upsample2x_nhwc(const void* x, void* out, int N, int h, int w, i
   const long long total = (long long)N * (2 * h) * (2 * w) * (C / 8);
   hipLaunchKernelGGL(upsample2x_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, (const bf16_t*)x,
                      (bf16_t*)out, h, w, C / 8, total);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// d [N, 2h, 2w, C] (dense gradient) -> t [N, h+1, w+1, 4C] phase layout
+KCA_API int kca_dense_to_phase_nhwc(const void* d, void* t, int N, int h, int w, int C, hipStream_t stream) {
+  if (C % 8 || N <= 0 || h <= 0 || w <= 0 || !aligned16(d) || !aligned16(t)) return 1;
+  const long long total = (long long)N * (h + 1) * (w + 1) * 4 * (C / 8);
+  hipLaunchKernelGGL(dense_to_phase_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, (const bf16_t*)d,
+                     (bf16_t*)t, h, w, C / 8, total);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// da [N*(h+1)*(w+1), 4C] (im2col gradient) -> dx [N, h, w, C]
+KCA_API int kca_col2im2x2_nhwc(const void* da, void* dx, int N, int h, int w, int C, hipStream_t stream) {
+  if (C % 8 || N <= 0 || h <= 0 || w <= 0 || !aligned16(da) || !aligned16(dx)) return 1;
+  const long long total = (long long)N * h * w * (C / 8);
+  hipLaunchKernelGGL(col2im2x2_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, (const bf16_t*)da,
+                     (bf16_t*)dx, h, w, C / 8, total);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

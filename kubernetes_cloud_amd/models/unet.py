@@ -26,7 +26,8 @@ import torch.nn.functional as F
 
 from .. import ops
 from ..ops.linear import SplitKLinear, linear_residual, linear_splitk_wgrad
-from ..ops.upsample import phase_gemm_weights, phase_to_dense, phase_weights, upsample_conv_phase, upsample_nearest2x
+from ..ops.upsample import (phase_gemm_weights, phase_to_dense, phase_weights, upsample_conv_phase,
+                           upsample_conv_train, upsample_nearest2x)
 
 
 @dataclasses.dataclass
@@ -274,6 +275,9 @@ _FUSE_RES = os.environ.get("KCA_SD_FUSE_RES", "1") not in ("0", "false")
 # up blocks read that phase layout in place in their concat GroupNorm, the VAE gets it densified.
 # KCA_SD_PHASE_UP=0: nearest-x2 (native NHWC kernel) + the 3x3 conv
 _PHASE_UP = os.environ.get("KCA_SD_PHASE_UP", "1") not in ("0", "false")
+# training: the same phase GEMM with its backward (ops/upsample.py upsample_conv_train); KCA_SD_PHASE_UP_TRAIN=0
+# keeps nearest-x2 + the 3x3 convolution
+_PHASE_UP_TRAIN = os.environ.get("KCA_SD_PHASE_UP_TRAIN", "1") not in ("0", "false")
 # inference: the up blocks' GroupNorm reads [x | skip] in place and writes the concat once for the
 # 1x1 shortcut (ops.group_norm_cat) instead of torch.cat + GroupNorm; KCA_SD_CAT_GN=0 disables
 _CAT_GN = os.environ.get("KCA_SD_CAT_GN", "1") not in ("0", "false")
@@ -576,6 +580,8 @@ class Upsample2D(nn.Module):
             return phase_to_dense(t, hw, self.conv.bias)
         if infer:
             return self.conv(upsample_nearest2x(x))
+        if _PHASE_UP_TRAIN and torch.is_grad_enabled() and x.is_cuda and x.dtype == torch.bfloat16 and _is_cl(x):
+            return upsample_conv_train(x, self.conv.weight, self.conv.bias)
         return self.conv(F.interpolate(x, scale_factor=2.0, mode="nearest"))
 
 

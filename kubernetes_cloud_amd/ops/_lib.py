@@ -50,6 +50,7 @@ _SIGS = {
     "kca_geglu_bwd": [P, P, P, LL, I, P],
     "kca_rope": [P, P, I, I, LL, I, LL, LL, LL, LL, I, I, P, P, P, F, P],
     "kca_accum_grad": [P, P, F, I, LL, P],
+    "kca_accum_grad_multi": [P, I, F, P],
     "kca_cast_f32_bf16": [P, P, LL, P],
     "kca_ema": [P, P, F, LL, P],
     "kca_cross_entropy_fwd": [P, LL, P, I, I, I, P, P, P],
@@ -92,6 +93,8 @@ _SIGS = {
     "kca_im2col2x2_nhwc": [P, P, I, I, I, I, P],
     "kca_phase_to_dense_nhwc": [P, P, P, I, I, I, I, P],
     "kca_upsample2x_nhwc": [P, P, I, I, I, I, P],
+    "kca_dense_to_phase_nhwc": [P, P, I, I, I, I, P],
+    "kca_col2im2x2_nhwc": [P, P, I, I, I, I, P],
     "kca_sample_logits": [P, LL, I, I, I, P, P, P, P, P, P, P, I, P, LL, P, P, P, P, P],
 }
 

@@ -102,5 +102,51 @@ def upsample_nearest2x(x: torch.Tensor) -> torch.Tensor:
     return F.interpolate(x, scale_factor=2.0, mode="nearest")
 
 
-__all__ = ["phase_weights", "phase_gemm_weights", "im2col2x2", "upsample_conv_phase", "phase_to_dense",
-           "upsample_nearest2x"]
+class _UpsampleConvPhaseFn(torch.autograd.Function):
+    """Training form of ``conv3x3(nearest_x2(x)) + bias`` as im2col + GEMM + dense scatter
+    (channels-last bf16 on the GPU): backward = phase gather of the output gradient
+    (``kca_dense_to_phase_nhwc``), the bias gradient as its column sum, dWg = dT^T A (A recomputed
+    from x rather than saved), dA = dT Wg and dx = col2im(dA) (``kca_col2im2x2_nhwc``). The phase
+    weights' gradient flows to the 3x3 kernel through ``phase_gemm_weights`` (torch ops)."""
+
+    @staticmethod
+    def forward(ctx, x, wg, bias):
+        N, C, h, w = x.shape
+        t = F.linear(im2col2x2(x), wg)
+        ctx.save_for_backward(x, wg)
+        ctx.has_bias = bias is not None
+        out = phase_to_dense(t.view(N, h + 1, w + 1, -1).permute(0, 3, 1, 2), (2 * h, 2 * w), bias)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        from .linear import column_sum
+        x, wg = ctx.saved_tensors
+        N, C, h, w = x.shape
+        cout = wg.shape[0] // 4
+        d = dout.contiguous(memory_format=torch.channels_last)
+        dt = torch.empty(N * (h + 1) * (w + 1), 4 * cout, device=x.device, dtype=x.dtype)
+        _lib.call("kca_dense_to_phase_nhwc", d.data_ptr(), dt.data_ptr(), N, h, w, cout, _lib.stream())
+        db = column_sum(d.permute(0, 2, 3, 1).reshape(-1, cout)) if ctx.has_bias else None
+        dwg = dx = None
+        if ctx.needs_input_grad[1]:
+            dwg = dt.t() @ im2col2x2(x)
+        if ctx.needs_input_grad[0]:
+            da = dt @ wg
+            dxn = torch.empty(N, h, w, C, device=x.device, dtype=x.dtype)
+            _lib.call("kca_col2im2x2_nhwc", da.data_ptr(), dxn.data_ptr(), N, h, w, C, _lib.stream())
+            dx = dxn.permute(0, 3, 1, 2)
+        return dx, dwg, db
+
+
+def upsample_conv_train(x: torch.Tensor, w3: torch.Tensor, bias: torch.Tensor | None) -> torch.Tensor:
+    """``conv3x3(nearest_x2(x), w3, bias, padding=1)`` with autograd through the phase GEMM on the
+    GPU (channels-last bf16, C % 8 == 0); the plain form otherwise."""
+    if (native_ok(x) and w3.shape[0] % 8 == 0 and _lib.has("kca_col2im2x2_nhwc")
+            and (bias is None or bias.dtype == x.dtype)):
+        return _UpsampleConvPhaseFn.apply(x, phase_gemm_weights(w3), bias)
+    return F.conv2d(F.interpolate(x, scale_factor=2.0, mode="nearest"), w3, bias, padding=1)
+
+
+__all__ = ["upsample_conv_train", "phase_weights", "phase_gemm_weights", "im2col2x2", "upsample_conv_phase",
+           "phase_to_dense", "upsample_nearest2x"]

@@ -64,6 +64,12 @@ log = logging.getLogger("kca.engine")
 
 ALIGN = 64
 _NONE, _INFLIGHT, _READY = 0, 1, 2
+# gradients of at most this many elements are accumulated in batches (kca_accum_grad_multi);
+# KCA_MULTI_ACCUM=0 launches kca_accum_grad per parameter
+_SMALL_GRAD = 1 << 18
+_MULTI_ACCUM = __import__("os").environ.get("KCA_MULTI_ACCUM", "1") not in ("0", "false")
+# tests: KCA_DEFER_CPU=1 runs the batching logic on CPU tensors of any float dtype (torch-op flush)
+_DEFER_CPU = __import__("os").environ.get("KCA_DEFER_CPU", "0") == "1"
 
 
 @dataclasses.dataclass
@@ -307,6 +313,7 @@ class TrainEngine:
         self._deferred = set()    # buckets launched in step() after the pre-reduce hooks
         self._touched = set()     # params with a grad this optimizer step
         self._seen = set()        # params with a grad this micro-batch
+        self._pend = []           # small-gradient accumulations awaiting one batched launch
         self._pre_reduce, self._pre_step = [], []
         self._norm_group, self._replicated, self._rep_ranges = None, {}, []
         self._hooks = [s.param.register_post_accumulate_grad_hook(self._hook) for s in slots]
@@ -430,7 +437,15 @@ class TrainEngine:
         if g.dim() == 4 and _is_cl(p):  # flat slot holds the NHWC order
             g = g.permute(0, 2, 3, 1)
             g = g.reshape(-1) if g.is_contiguous() else g.contiguous().reshape(-1)
-        if self.native and g.dtype == torch.bfloat16 and g.is_contiguous():
+        if ((self.native and g.dtype == torch.bfloat16 or _DEFER_CPU) and g.is_contiguous()
+                and s.numel <= _SMALL_GRAD and _MULTI_ACCUM
+                and not (g.is_cuda and torch.cuda.is_current_stream_capturing())):
+            # small gradients are batched into one kca_accum_grad_multi launch (flushed before any
+            # bucket collective and at the end of backward); the entry keeps g alive until then
+            self._pend.append((dst, g.reshape(-1), bool(first), scale))
+            if len(self._pend) >= 256:
+                self._flush_small()
+        elif self.native and g.dtype == torch.bfloat16 and g.is_contiguous():
             _lib.call("kca_accum_grad", dst.data_ptr(), g.data_ptr(), scale, int(first), s.numel,
                       _lib.stream())
         elif (self.native and g.dtype == torch.bfloat16 and g.dim() == 2 and g.stride(1) == 1
@@ -451,7 +466,31 @@ class TrainEngine:
                         and s.bucket not in self._deferred:
                     self._launch(s.bucket)
 
+    def _flush_small(self):
+        """One launch for the pending small-gradient accumulations (see _accum)."""
+        pend, self._pend = self._pend, []
+        if not pend:
+            return
+        if not self.native:  # CPU emulation of the batched path (tests of the engine logic)
+            for dst, g, first, scale in pend:
+                if first:
+                    dst.copy_(g.float() * scale)
+                else:
+                    dst.add_(g.float(), alpha=scale)
+            return
+        import numpy as np
+        by_scale: dict = {}
+        for e in pend:
+            by_scale.setdefault(e[3], []).append(e)
+        for scale, es in by_scale.items():
+            # the entries go to the kernel by value (kernel arguments), nothing on the device to manage
+            tbl = np.array([[d.data_ptr(), g.data_ptr(), d.numel(), int(f)] for d, g, f, _ in es], dtype=np.int64)
+            _lib.call("kca_accum_grad_multi", tbl.ctypes.data, len(es), float(scale), _lib.stream())
+        # the gradient tensors are freed after the launch: the caching allocator only hands their
+        # memory to work queued later on this stream
+
     def _launch(self, bi: int):
+        self._flush_small()
         if self._bucket_launched[bi]:
             return
         self._bucket_launched[bi] = True
@@ -535,6 +574,7 @@ class TrainEngine:
             loss.backward()
         finally:
             self._in_bwd = False
+            self._flush_small()
         self._end_micro()
         self._micro += 1
 
@@ -548,6 +588,7 @@ class TrainEngine:
             torch.autograd.backward(tensors, grads)
         finally:
             self._in_bwd = False
+            self._flush_small()
         self._end_micro()
         self._micro += 1
 

@@ -796,3 +796,31 @@ def test_column_sum_kernel(M, N):
     got = column_sum(x)
     assert got.dtype == torch.bfloat16 and got.shape == (N,)
     assert (got.float() - ref).abs().max() <= 0.01 * ref.abs().max() + 0.05
+
+
+def test_accum_grad_multi_matches_reference():
+    """kca_accum_grad_multi (train/engine.py batches small gradients): fp32 dst (+)= bf16 src * scale
+    per entry -- aligned and misaligned pointers, tails, first (overwrite) and accumulate entries,
+    more entries than one launch carries (96 by value in the kernel arguments)."""
+    import numpy as np
+    torch.manual_seed(1)
+    g_ = torch.Generator().manual_seed(2)
+    sizes = [1, 7, 8, 9, 300, 2047, 2048, 2049, 65536, 100003] + \
+        torch.randint(1, 5000, (190,), generator=g_).tolist()
+    flat = torch.randn(sum(sizes) + 5 * len(sizes) + 64, device=DEV, dtype=torch.float32)
+    ref = flat.clone()
+    rows, keep, off = [], [], 3  # offset 3: misaligned fp32 destinations
+    for i, n in enumerate(sizes):
+        g = torch.randn(n + 1, device=DEV, dtype=torch.bfloat16)[i % 2:i % 2 + n]  # odd entries misaligned
+        keep.append(g)
+        first = i % 3 == 0
+        rows.append([flat[off:off + n].data_ptr(), g.data_ptr(), n, int(first)])
+        seg = ref[off:off + n]
+        seg.copy_(g.float() * 0.5 if first else seg + g.float() * 0.5)
+        off += n + (i % 5)
+    tbl = np.array(rows, dtype=np.int64)
+    _lib.call("kca_accum_grad_multi", tbl[:3].ctypes.data, 3, 0.5, _lib.stream())
+    tail = np.ascontiguousarray(tbl[3:])
+    _lib.call("kca_accum_grad_multi", tail.ctypes.data, len(rows) - 3, 0.5, _lib.stream())
+    torch.cuda.synchronize()
+    assert torch.allclose(flat, ref, rtol=1e-6, atol=1e-6)

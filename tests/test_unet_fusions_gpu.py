@@ -164,3 +164,30 @@ def test_unet_training_fusions_match_plain_grads(monkeypatch):
     bad = [(n, rel(g1[n], gr[n]), rel(g0[n], gr[n])) for n in gr
            if rel(g1[n], gr[n]) > max(2.0 * rel(g0[n], gr[n]), 0.03)]
     assert not bad, bad[:5]
+
+
+@pytest.mark.parametrize("N,C,S,bias", [(2, 64, 8, True), (2, 320, 16, False), (1, 1280, 4, True)])
+def test_phase_upsampler_training_grads_match_fp32(N, C, S, bias):
+    """ops/upsample.py upsample_conv_train (im2col + GEMM + scatter, kca_dense_to_phase / col2im
+    backward) against nearest-x2 + conv3x3 in fp32: output, dx, dW, db."""
+    from kubernetes_cloud_amd.ops.upsample import upsample_conv_train
+    torch.manual_seed(N + C + S)
+    x = _cl(N, C, S, S).requires_grad_()
+    w = ((torch.randn(C, C, 3, 3, device=DEV) * (9 * C) ** -0.5).bfloat16()
+         .contiguous(memory_format=CL).requires_grad_())
+    b = torch.randn(C, device=DEV, dtype=torch.bfloat16).requires_grad_() if bias else None
+    g = torch.randn(N, C, 2 * S, 2 * S, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=CL)
+    y = upsample_conv_train(x, w, b)
+    y.backward(g)
+    xf, wf = x.detach().float().requires_grad_(), w.detach().float().requires_grad_()
+    bf = b.detach().float().requires_grad_() if bias else None
+    yf = F.conv2d(F.interpolate(xf, scale_factor=2.0, mode="nearest"), wf, bf, padding=1)
+    yf.backward(g.float())
+    assert _rel(y, yf) < 1e-2 and _rel(x.grad, xf.grad) < 2e-2 and _rel(w.grad, wf.grad) < 2e-2
+    if bias:
+        assert _rel(b.grad, bf.grad) < 1e-2
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
