@@ -22,16 +22,21 @@ from . import _lib
 _PHASE_TAPS = (((0,), (1, 2)), ((0, 1), (2,)))
 
 
-def phase_weights(w: torch.Tensor) -> torch.Tensor:
-    """[Cout, Cin, 3, 3] -> [4 * Cout, Cin, 2, 2]: output channel block k = 2a + b holds phase (a, b)."""
-    wf = w.float()
-    out = wf.new_zeros(4, w.shape[0], w.shape[1], 2, 2)
+def _tap_matrix(device) -> torch.Tensor:
+    """M[a, s, u] = 1 when 3x3 tap row u lands on input row s of output phase a (_PHASE_TAPS)."""
+    m = torch.zeros(2, 2, 3, device=device)
     for a in range(2):
-        for b in range(2):
-            for s_ in range(2):
-                for t in range(2):
-                    rows, cols = _PHASE_TAPS[a][s_], _PHASE_TAPS[b][t]
-                    out[2 * a + b, :, :, s_, t] = wf[:, :, list(rows)][:, :, :, list(cols)].sum(dim=(2, 3))
+        for s_ in range(2):
+            for u in _PHASE_TAPS[a][s_]:
+                m[a, s_, u] = 1.0
+    return m
+
+
+def phase_weights(w: torch.Tensor) -> torch.Tensor:
+    """[Cout, Cin, 3, 3] -> [4 * Cout, Cin, 2, 2]: output channel block k = 2a + b holds phase (a, b).
+    One einsum with the 0/1 tap matrix (fp32), so the training backward is one einsum too."""
+    m = _tap_matrix(w.device)
+    out = torch.einsum("asu,btv,oiuv->aboist", m, m, w.float())
     return out.reshape(4 * w.shape[0], w.shape[1], 2, 2).to(w.dtype)
 
 

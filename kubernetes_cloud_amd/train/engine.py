@@ -70,6 +70,7 @@ _SMALL_GRAD = 1 << 18
 _MULTI_ACCUM = __import__("os").environ.get("KCA_MULTI_ACCUM", "1") not in ("0", "false")
 # tests: KCA_DEFER_CPU=1 runs the batching logic on CPU tensors of any float dtype (torch-op flush)
 _DEFER_CPU = __import__("os").environ.get("KCA_DEFER_CPU", "0") == "1"
+_FLUSH_TORCH = __import__("os").environ.get("KCA_FLUSH_TORCH", "0") == "1"  # diagnostic: torch-op flush on GPU
 
 
 @dataclasses.dataclass
@@ -314,6 +315,7 @@ class TrainEngine:
         self._touched = set()     # params with a grad this optimizer step
         self._seen = set()        # params with a grad this micro-batch
         self._pend = []           # small-gradient accumulations awaiting one batched launch
+        self._pend_ids = set()    # their parameters (one entry per parameter per launch)
         self._pre_reduce, self._pre_step = [], []
         self._norm_group, self._replicated, self._rep_ranges = None, {}, []
         self._hooks = [s.param.register_post_accumulate_grad_hook(self._hook) for s in slots]
@@ -442,7 +444,12 @@ class TrainEngine:
                 and not (g.is_cuda and torch.cuda.is_current_stream_capturing())):
             # small gradients are batched into one kca_accum_grad_multi launch (flushed before any
             # bucket collective and at the end of backward); the entry keeps g alive until then
+            # a parameter fed twice in one backward (a block applied twice: two sink calls) must not
+            # have two entries in one launch -- their blocks would race on the same destination
+            if id(p) in self._pend_ids:
+                self._flush_small()
             self._pend.append((dst, g.reshape(-1), bool(first), scale))
+            self._pend_ids.add(id(p))
             if len(self._pend) >= 256:
                 self._flush_small()
         elif self.native and g.dtype == torch.bfloat16 and g.is_contiguous():
@@ -469,9 +476,10 @@ class TrainEngine:
     def _flush_small(self):
         """One launch for the pending small-gradient accumulations (see _accum)."""
         pend, self._pend = self._pend, []
+        self._pend_ids = set()
         if not pend:
             return
-        if not self.native:  # CPU emulation of the batched path (tests of the engine logic)
+        if not self.native or _FLUSH_TORCH:  # CPU emulation of the batched path (tests of the engine logic)
             for dst, g, first, scale in pend:
                 if first:
                     dst.copy_(g.float() * scale)

@@ -300,3 +300,36 @@ def test_chunked_prefill_window_model():
     assert eng.stats["prefill_chunks"] >= 4
     assert r1.output == greedy_recompute(m, short, 12)
     assert r2.output == greedy_recompute(m, long, 5)
+
+
+def test_batched_small_grad_accum_param_fed_twice(monkeypatch):
+    """train/engine.py batches small gradient accumulations (kca_accum_grad_multi on the GPU); a
+    parameter fed twice in one backward through the gradient sink (a fused block applied twice)
+    must not get two entries in one launch. CPU emulation of the batched path: the result equals
+    the per-parameter path."""
+    import torch
+    from kubernetes_cloud_amd.ops import grad_sink
+    from kubernetes_cloud_amd.train import engine as E
+
+    def run(defer):
+        monkeypatch.setattr(E, "_DEFER_CPU", defer)
+        torch.manual_seed(0)
+        lin = torch.nn.Linear(8, 8).to(torch.bfloat16)
+        eng = E.TrainEngine(lin, lr=0.0, zero_stage=0, grad_accum=1)
+        flushes = []
+        orig = eng._flush_small
+        eng._flush_small = lambda: (flushes.append(len(eng._pend)), orig())[1]
+        sink = grad_sink.lookup(lin.weight)
+        g1 = torch.randn(8, 8).to(torch.bfloat16)
+        g2 = torch.randn(8, 8).to(torch.bfloat16)
+        sink(lin.weight, g1)
+        sink(lin.weight, g2)
+        eng._flush_small()
+        out = eng.grad[eng._by_param[id(lin.weight)].offset:][:64].clone()
+        eng.remove_hooks()
+        return out, flushes, g1, g2
+
+    got, flushes, g1, g2 = run(True)
+    assert flushes[0] == 1  # the second entry for the same parameter flushed the first
+    ref = g1.float().reshape(-1) + g2.float().reshape(-1)
+    assert torch.allclose(got, ref)
