@@ -22,7 +22,9 @@
 // [page][kv_head][ps][D] (ps = 1 << ps_shift tokens) and token t of sequence
 // `seq` lives in page tbl[seq * tbl_stride + (t >> ps_shift)] -- requests hold
 // only the pages they use, and beams share their prefix pages.
-#include "common.h"
+#include <type_traits>
+
+#include "gemv_m1.h"  // gemv_m1_accum / _finish for the fused decode-layer kernels
 
 // element offset of token t of sequence `seq` (paged or contiguous)
 __device__ __forceinline__ long long kv_row(const int* __restrict__ tbl, int tbl_stride, int ps_shift, int seq,
@@ -268,15 +270,16 @@ __device__ void fanin_combine(const DecodeParams& p, int b, int hk, int nsplit) 
 
 // LPT lanes cooperate on one token row (8 dims per lane); TPW = 64/LPT tokens per
 // wave step; G query heads share each K/V row (GQA group).
+// (the workgroup's (split, kv-head, sequence) coordinates are arguments: decode_attn_kernel passes
+// its block index, the fused decode-layer kernel below a slice of its grid)
 template <int LPT, int G, bool PAGED, bool ONLINE>
-__global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
+__device__ __forceinline__ void decode_attn_body(const DecodeParams& p, const int split, const int hk, const int b,
+                                                 const int nsplit) {
   constexpr int TPW = 64 / LPT;
   constexpr int TPB = 4 * TPW;
   constexpr int U = 4;  // tokens per lane per iteration: 2U independent 16-B row loads in flight
   extern __shared__ float smem[];
   DSTAMP(0);
-  const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
-  const int nsplit = gridDim.x;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int D = p.D, ND = D >> 3;
   const int dslot = lane % LPT, tsub = lane / LPT;
@@ -688,6 +691,143 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
   if (nsplit > 1 && p.cnt) fanin_combine<G>(p, b, hk, nsplit);
 }
 
+template <int LPT, int G, bool PAGED, bool ONLINE>
+__global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
+  decode_attn_body<LPT, G, PAGED, ONLINE>(p, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x);
+}
+
+// ---------------------------------------------------------------- fused decode layer (batch 1)
+// A parallel-residual layer (GPT-J: h' = h + attn(LN h) + mlp(LN h)) at batch 1 is weight
+// streaming plus a latency-bound attention chain. Two streams (attention on one, the MLP GEMVs on
+// the other) overlap them but pay a cross-queue fork and join per layer (~10 us each in the graph
+// timeline, profiles/decode_gptj_b1_timeline_r3.txt). One queue, three launches instead:
+//   QKV GEMV  ->  decode_attn_gemv_kernel: workgroups [0, n_attn) run the RoPE + KV append +
+//                 split-K attention, the rest the fc_in GEMV (+ GELU) -- the attention hides in the
+//                 weight stream, dispatched first so it starts at once
+//             ->  gemv_dual_ln_kernel: y = o Wout^T + g Wfc_out^T + b in one K-concatenated GEMV
+//                 (two weight streams, one output), and the last workgroup to finish (arrival
+//                 counter) adds y to the residual stream and normalises it for the next layer --
+//                 no separate LayerNorm launch.
+struct GemvM1 {
+  const bf16_t* x;
+  const bf16_t* w;
+  const bf16_t* bias;
+  bf16_t* y;
+  int N, K, act;
+};
+
+template <int LPT, int G, bool PAGED, bool ONLINE>
+__global__ __launch_bounds__(256) void decode_attn_gemv_kernel(DecodeParams p, int nsplit, int n_attn, GemvM1 g) {
+  constexpr int R = 4;
+  __shared__ float part[4][R];
+  const int bid = blockIdx.x;
+  if (bid < n_attn) {
+    const int split = bid % nsplit, rest = bid / nsplit;
+    decode_attn_body<LPT, G, PAGED, ONLINE>(p, split, rest % p.Hkv, rest / p.Hkv, nsplit);
+    return;
+  }
+  const int n0 = (bid - n_attn) * R;
+  float acc[R] = {0.f, 0.f, 0.f, 0.f};
+  gemv_m1_accum<R>(g.x, g.w, g.N, g.K, n0, acc);
+  const float v = gemv_m1_finish<R>(acc, part, g.bias, n0, g.N, g.act);
+  if (threadIdx.x < R && n0 + threadIdx.x < g.N) g.y[n0 + threadIdx.x] = f2bf(v);
+}
+
+struct DualLn {
+  const bf16_t* x1;  // [K1] (attention output)
+  const bf16_t* w1;  // [N, K1]
+  const bf16_t* x2;  // [K2] (GELU(fc_in))
+  const bf16_t* w2;  // [N, K2]
+  const bf16_t* bias;  // [N] (nullable)
+  float* ypart;        // [N] fp32 workspace (write-through: the finishing workgroup reads it)
+  unsigned int* cnt;   // arrival counter, zero before the first launch, re-armed by the last workgroup
+  const bf16_t* h;     // [N] residual stream in
+  bf16_t* h_out;       // [N] h + y (bf16)
+  const bf16_t* gamma; // next LayerNorm
+  const bf16_t* beta;
+  float eps;
+  bf16_t* xn_out;      // [N] LN(h + y)
+  int N, K1, K2;
+};
+
+template <int R>
+__global__ __launch_bounds__(256) void gemv_dual_ln_kernel(DualLn a) {
+  __shared__ float part[4][R];
+  __shared__ float red[16];
+  __shared__ int s_last;
+  const int tid = threadIdx.x;
+  const int n0 = blockIdx.x * R;
+  float acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = 0.f;
+  gemv_m1_accum<R>(a.x1, a.w1, a.N, a.K1, n0, acc);
+  gemv_m1_accum<R>(a.x2, a.w2, a.N, a.K2, n0, acc);
+  const float v = gemv_m1_finish<R>(acc, part, a.bias, n0, a.N, 0);
+  if (tid < R && n0 + tid < a.N) st_pub(&a.ypart[n0 + tid], v);
+  // publish (cdna_hip_programming.md Guideline 16, R1): write-through stores drained, barrier, one
+  // agent-scope arrival; the last workgroup re-arms the counter and acquires
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(a.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == gridDim.x - 1;
+    if (last) {
+      __hip_atomic_store(a.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    s_last = last;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  // h' = bf16(h + y), LN(h') -- the ln_rows_kernel math (statistics over the bf16-rounded sum)
+  constexpr int PER = 4;  // N <= 8192: 256 threads x 8 x PER
+  float hv[PER][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int k = (i * 256 + tid) * 8;
+    if (k < a.N) {
+      float y8[8];
+      load8(a.h + k, hv[i]);
+      load8f(a.ypart + k, y8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        hv[i][j] = bf2f(f2bf(hv[i][j] + y8[j]));
+        s += hv[i][j];
+      }
+      store8(a.h_out + k, hv[i]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) hv[i][j] = 0.f;
+    }
+  }
+  const float mean = block_sum(s, red) / a.N;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    if ((i * 256 + tid) * 8 >= a.N) continue;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) q += (hv[i][j] - mean) * (hv[i][j] - mean);
+  }
+  const float rstd = rsqrtf(block_sum(q, red + 8) / a.N + a.eps);
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int k = (i * 256 + tid) * 8;
+    if (k >= a.N) continue;
+    float gm[8], bt[8];
+    load8(a.gamma + k, gm);
+    if (a.beta) load8(a.beta + k, bt);
+    else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bt[j] = 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) hv[i][j] = (hv[i][j] - mean) * rstd * gm[j] + bt[j];
+    store8(a.xn_out + k, hv[i]);
+  }
+}
+
 // One workgroup per (sequence, head): split maxima and weights in one
 // parallel pass into LDS, then every lane owns one output dim and sums the
 // splits with 8 independent loads in flight (the old per-split serial chain
@@ -863,6 +1003,91 @@ static int decode_attn_launch(DecodeParams p, float* ws, long long ws_floats, in
     hipLaunchKernelGGL(decode_combine_kernel, dim3(B * H), dim3(256), 0, stream, p.ws_o, p.ws_ml,
                        p.out, p.o_bs, H, D, nsplit);
   return 0;
+}
+
+// Fused decode layer, part 1 (batch 1, see decode_attn_gemv_kernel): kca_decode_prep_attn's
+// arguments plus the fc_in GEMV (gx [gK] -> gy [gN], bias, act). Returns 10 when the shape is
+// outside the instantiated fused variants (G == 1, head_dim 128 / 256, split-K fan-in or one
+// split): the caller then runs the two-stream path.
+KCA_API int kca_decode_prep_attn_gemv(const void* qkv, long long ld, const void* kc, const void* vc,
+                                      long long cs_slot, long long cs_head, long long cs_pos,
+                                      const int* slots, const int* kv_lens, void* out, long long o_bs,
+                                      float* ws, long long ws_floats, int B, int H, int Hkv, int D,
+                                      int max_kv, int chunk, float scale, const float* alibi, const int* tbl,
+                                      int tbl_stride, int ps_shift, int rot, int interleaved, const float* cos_t,
+                                      const float* sin_t, int window, const void* gx, const void* gw,
+                                      const void* gbias, void* gy, int gN, int gK, int gact, hipStream_t stream) {
+  if (rot > D || (rot & 1) || (rot > 0 && (!cos_t || !sin_t))) return 8;
+  if (window < 0) return 9;
+  if (B != 1 || H != Hkv || D % 8 || D > 256 || max_kv <= 0 || gK % 8 || gN <= 0) return 10;
+  const int nd = D / 8;
+  if (nd <= 8) return 10;
+  if (((uintptr_t)gx | (uintptr_t)gw) & 15) return 10;
+  DecodeParams p{(const bf16_t*)qkv, ld, (const bf16_t*)kc, (const bf16_t*)vc, cs_slot, cs_head,
+                 cs_pos, slots, kv_lens, (bf16_t*)out, o_bs, nullptr, nullptr, alibi, tbl, tbl_stride, ps_shift,
+                 H, Hkv, D, chunk, scale, 1, rot, interleaved, cos_t, sin_t, nullptr, nullptr, window};
+  if (tbl && (ps_shift < 4 || ps_shift > 20 || tbl_stride <= 0)) return 5;
+  if (chunk <= 0) chunk = kca_decode_chunk(B, Hkv, max_kv);
+  if (tbl && chunk > 1024) return 6;
+  const int nsplit = (max_kv + chunk - 1) / chunk;
+  if (nsplit > 1024) return 7;
+  p.chunk = chunk;
+  if (nsplit > 1) {
+    if (!fanin_enabled()) return 10;  // the fused launch has no room for the separate combine kernel
+    const long long cw = fanin_words(B, H);
+    const long long need = cw + (long long)B * H * nsplit * (D + 2);
+    if (!ws || ws_floats < need) return 4;
+    p.cnt = reinterpret_cast<unsigned int*>(ws);
+    p.ws_o = ws + cw;
+    p.ws_ml = p.ws_o + (long long)B * H * nsplit * D;
+  }
+  const GemvM1 g{(const bf16_t*)gx, (const bf16_t*)gw, (const bf16_t*)gbias, (bf16_t*)gy, gN, gK, gact};
+  const int n_attn = nsplit * Hkv * B;
+  const dim3 grid(n_attn + (gN + 3) / 4);
+  auto go = [&](auto lpt) {
+    constexpr int LPT = decltype(lpt)::value;
+    constexpr int TPB = 4 * (64 / LPT), U = 4;
+    if (p.chunk > TPB * U) {
+      const size_t lds = (size_t)4 * (2 + p.D) * sizeof(float);
+      if (p.tbl) hipLaunchKernelGGL((decode_attn_gemv_kernel<LPT, 1, true, true>), grid, dim3(256), lds, stream, p, nsplit, n_attn, g);
+      else hipLaunchKernelGGL((decode_attn_gemv_kernel<LPT, 1, false, true>), grid, dim3(256), lds, stream, p, nsplit, n_attn, g);
+    } else {
+      const size_t lds = (size_t)(p.chunk + 4 * p.D) * sizeof(float);
+      if (p.tbl) hipLaunchKernelGGL((decode_attn_gemv_kernel<LPT, 1, true, false>), grid, dim3(256), lds, stream, p, nsplit, n_attn, g);
+      else hipLaunchKernelGGL((decode_attn_gemv_kernel<LPT, 1, false, false>), grid, dim3(256), lds, stream, p, nsplit, n_attn, g);
+    }
+  };
+  if (nd <= 16) go(std::integral_constant<int, 16>{});
+  else go(std::integral_constant<int, 32>{});
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// Fused decode layer, part 2: y = x1 W1^T + x2 W2^T + bias ([N]), h_out = bf16(h + y),
+// xn_out = LN(h_out) (gamma, beta, eps). ypart: [N] fp32 workspace; cnt: one zero-initialised
+// unsigned counter (re-armed by every launch's last workgroup).
+KCA_API int kca_gemv_dual_ln(const void* x1, const void* w1, int K1, const void* x2, const void* w2, int K2,
+                             const void* bias, float* ypart, unsigned int* cnt, const void* h, void* h_out,
+                             const void* gamma, const void* beta, float eps, void* xn_out, int N,
+                             hipStream_t stream) {
+  if (N <= 0 || N % 8 || N > 8192 || K1 % 8 || K2 % 8 || K1 <= 0 || K2 <= 0 || !ypart || !cnt || !gamma || !xn_out ||
+      !h || !h_out)
+    return 1;
+  if (((uintptr_t)x1 | (uintptr_t)w1 | (uintptr_t)x2 | (uintptr_t)w2 | (uintptr_t)h | (uintptr_t)h_out |
+       (uintptr_t)gamma | (uintptr_t)beta | (uintptr_t)xn_out | (uintptr_t)ypart) & 15)
+    return 2;
+  const DualLn a{(const bf16_t*)x1, (const bf16_t*)w1, (const bf16_t*)x2, (const bf16_t*)w2, (const bf16_t*)bias,
+                 ypart, cnt, (const bf16_t*)h, (bf16_t*)h_out, (const bf16_t*)gamma, (const bf16_t*)beta, eps,
+                 (bf16_t*)xn_out, N, K1, K2};
+  // rows per workgroup: 4 (N / 4 workgroups, one residency wave at GPT-J's N = 4096) or 2 (twice the
+  // workgroups in flight; KCA_DUAL_ROWS=2, A/B)
+  static int rows = -1;
+  if (rows < 0) {
+    const char* e = getenv("KCA_DUAL_ROWS");
+    rows = (e && e[0] == '2') ? 2 : 4;
+  }
+  if (rows == 2) hipLaunchKernelGGL(gemv_dual_ln_kernel<2>, dim3((N + 1) / 2), dim3(256), 0, stream, a);
+  else hipLaunchKernelGGL(gemv_dual_ln_kernel<4>, dim3((N + 3) / 4), dim3(256), 0, stream, a);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
 // --------------------------------------------------------------- sampling

@@ -9,19 +9,7 @@
 // one wave-reduction per (row, m) at the end. Bias and GELU (tanh or erf) are
 // fused into the store, replacing the separate bias/GELU kernels of the
 // FT / DS-Inference decoders (SURVEY K1/K5 decode shapes).
-#include "common.h"
-
-struct LnArgs {
-  const bf16_t* r1;     // residual adds (nullable): h = x (+ r1) (+ r2)
-  const bf16_t* r2;
-  bf16_t* h_out;        // updated residual stream, written by workgroup 0 (nullable)
-  long long ldh;        // row stride of r1 / r2 / h_out
-  const bf16_t* gamma;  // [K]
-  const bf16_t* beta;   // [K] (nullable)
-  float eps;
-  bf16_t* xn_out;       // normalised rows [M][K], written by workgroup 0 (nullable): GPT-J's shared LN
-                        // feeds the fc_in GEMV too, which then skips its own prologue
-};
+#include "gemv_m1.h"  // LnArgs, ld_w16 (shared with decode.hip's fused decode-layer kernels)
 
 // LayerNorm prologue: every workgroup normalises the M activation rows itself
 // (K*M*2 B of L2-resident reads, ~1 us) straight into the LDS tile the GEMM
@@ -82,16 +70,6 @@ __device__ __forceinline__ void ln_prologue(const bf16_t* __restrict__ x, long l
       if (a.xn_out && blockIdx.x == 0) store8(a.xn_out + m * K + k, v);
     }
   }
-}
-
-// Weight stream loads: every weight byte of a decode GEMV is read once, by one workgroup, so
-// they are non-temporal (global_load_dwordx4 ... nt): they do not displace the L2 / MALL lines the
-// latency-bound attention chain and the activations re-read (MI355X_MICROARCH.md, nt-weights:
-// decode layers 5-10 % faster with nt weight streams).
-typedef unsigned int u32x4_nt __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ uint4 ld_w16(const bf16_t* p) {
-  const u32x4_nt v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_nt*>(p));
-  return make_uint4(v.x, v.y, v.z, v.w);
 }
 
 template <int M, int R, bool LN>

@@ -33,7 +33,7 @@ import torch
 
 from .. import ops
 from ..ops import decode as dops
-from ..ops.gemv import ln_skinny_linear, skinny_linear
+from ..ops.gemv import ln_rows, ln_skinny_linear, skinny_linear
 
 
 def _next_pow2(n: int, lo: int = 1) -> int:
@@ -350,6 +350,12 @@ class ModelRunner:
         self._par_mlp = (cfg.parallel_residual and on_gpu and not tp and not self.multi_device
                          and os.environ.get("KCA_DECODE_PAR_MLP", "1") not in ("0", "false"))
         self._side = torch.cuda.Stream(device=self.device) if self._par_mlp else None
+        # batch-1 decode of GPT-J-style layers (parallel residual, one shared LayerNorm) as three
+        # launches per layer on ONE queue (ops/decode.py decode_prep_attention_gemv + gemv_dual_ln):
+        # no cross-queue fork/join, no separate LayerNorm launch. KCA_DECODE_FUSED=0: the two-stream form
+        self._fused_ok = (self._par_mlp and all(blk.ln_2 is None for blk in model.h)
+                          and os.environ.get("KCA_DECODE_FUSED", "1") not in ("0", "false"))
+        self._fz: dict = {}
 
     # ------------------------------------------------------------- prefill
     @torch.no_grad()
@@ -451,8 +457,58 @@ class ModelRunner:
         return h.to(dev), tuple(p_.to(dev) for p_ in pending)
 
     # -------------------------------------------------------------- decode
+    def _fused_bufs(self):
+        """Static buffers of the fused batch-1 layer (allocated outside any graph capture)."""
+        fz = self._fz.get("b1")
+        if fz is None:
+            d, f = self.cfg.hidden, self.model.h[0].mlp.fc_in.weight.shape[0]
+            z = dict(device=self.device, dtype=self.dtype)
+            biases = []
+            for blk in self.model.h:
+                bo, bf = blk.attn.out.bias, blk.mlp.fc_out.bias
+                biases.append(bf if bo is None else (bo if bf is None else (bo.float() + bf.float()).to(self.dtype)))
+            fz = self._fz["b1"] = {
+                "g": torch.empty(1, f, **z), "h": torch.empty(1, d, **z), "xn": torch.empty(1, d, **z),
+                "ypart": torch.empty(d, device=self.device, dtype=torch.float32),
+                "cnt": torch.zeros(4, device=self.device, dtype=torch.int32), "bias": biases}
+        return fz
+
+    def _layers_decode_fused(self, tokens, pos, slots, kv_lens, max_kv, ws, obuf):
+        """Batch-1 GPT-J-style decode step, three launches per layer (see _fused_ok). Returns None
+        (nothing launched) when the fused kernels do not cover the shape."""
+        m, cfg = self.model, self.cfg
+        fz = self._fused_bufs()
+        h0 = m.embed(tokens, pos.long())
+        blk0 = m.h[0]
+        xn, h = ln_rows(h0, blk0.ln_1.weight, blk0.ln_1.bias, blk0.ln_1.eps)
+        hb, xb, g = fz["h"], fz["xn"], fz["g"]
+        kc, vc, tbl = self.cache.k[0], self.cache.v[0], self.cache.table_on(self.device)
+        for li, blk in enumerate(m.h):
+            at, mlp = blk.attn, blk.mlp
+            act = 1 if mlp.approx in ("tanh", True) else 2
+            qkv = skinny_linear(xn, at.qkv.weight, at.qkv.bias)
+            kc, vc = self.cache.k[li], self.cache.v[li]
+            if not dops.decode_prep_attention_gemv(qkv, self.H, self.Hkv, self.D, self.rot, cfg.rotary_interleaved,
+                                                   self.cos, self.sin, pos, slots, kc, vc, kv_lens, max_kv, at.scale,
+                                                   at.alibi, obuf, ws, tbl, at.window, xn, mlp.fc_in.weight,
+                                                   mlp.fc_in.bias, g, act):
+                if li == 0:
+                    return None
+                raise RuntimeError("fused decode layer: shape support changed between layers")
+            nxt = m.h[li + 1].ln_1 if li + 1 < len(m.h) else m.ln_f
+            dops.gemv_dual_ln(obuf, at.out.weight, g, mlp.fc_out.weight, fz["bias"][li], h, nxt.weight, nxt.bias,
+                              nxt.eps, fz["ypart"], fz["cnt"], hb, xb)
+            h, xn = hb, xb
+        if m.lm_head is None:
+            return skinny_linear(xn, m.wte.weight)
+        return self._lin(m.lm_head, xn)
+
     def _layers_decode(self, tokens, pos, slots, kv_lens, max_kv, ws, obuf):
         m, cfg = self.model, self.cfg
+        if self._fused_ok and tokens.shape[0] == 1 and obuf is not None:
+            y = self._layers_decode_fused(tokens, pos, slots, kv_lens, max_kv, ws, obuf)
+            if y is not None:
+                return y
         h = m.embed(tokens, pos.long())
         pending = ()
         per_dev = {self.device: (pos, slots, kv_lens, ws, obuf)}

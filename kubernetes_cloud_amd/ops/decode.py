@@ -191,6 +191,60 @@ def decode_prep_attention(qkv: torch.Tensor, n_heads: int, kv_heads: int, head_d
                             block_table=block_table, window=window)
 
 
+def decode_prep_attention_gemv(qkv, n_heads, kv_heads, head_dim, rot, interleaved, cos, sin, pos, slots,
+                               k_cache, v_cache, kv_lens, max_kv, scale, alibi, out, ws, block_table, window,
+                               gx: torch.Tensor, gw: torch.Tensor, gbias: torch.Tensor | None, gy: torch.Tensor,
+                               act: int) -> bool:
+    """Fused decode layer, part 1 (batch 1; csrc/kernels/decode.hip decode_attn_gemv_kernel): the
+    ``decode_prep_attention`` launch and the fc_in GEMV ``gy = act(gx W^T + b)`` as ONE launch
+    (attention workgroups first, the weight stream on the rest). Returns False (nothing launched)
+    for shapes outside the fused variants; the caller then runs the two separately."""
+    B = qkv.shape[0]
+    _, Hkv, L, D = k_cache.shape
+    if not (_lib.use_native(qkv, k_cache, gx, gw) and _lib.has("kca_decode_prep_attn_gemv") and B == 1
+            and gx.is_contiguous() and gw.is_contiguous() and gy.is_contiguous()
+            and (gbias is None or gbias.dtype == torch.bfloat16)):
+        return False
+    tbl, tstride, shift = _table_args(block_table, k_cache)
+    chunk = decode_chunk(B, Hkv, max_kv)
+    need = decode_ws_floats(B, n_heads, Hkv, D, max_kv, chunk)
+    if need and (ws is None or ws.numel() < need):
+        return False
+    rc = _lib.require().kca_decode_prep_attn_gemv(
+        qkv.data_ptr(), qkv.stride(0), k_cache.data_ptr(), v_cache.data_ptr(), k_cache.stride(0), k_cache.stride(1),
+        k_cache.stride(2), slots.data_ptr(), kv_lens.data_ptr(), out.data_ptr(), out.stride(0), _lib.ptr(ws),
+        ws.numel() if ws is not None else 0, B, n_heads, Hkv, D, max_kv, chunk, float(scale), _lib.ptr(alibi), tbl,
+        tstride, shift, rot, int(interleaved), _lib.ptr(cos), _lib.ptr(sin), int(window), gx.data_ptr(),
+        gw.data_ptr(), _lib.ptr(gbias), gy.data_ptr(), gw.shape[0], gw.shape[1], int(act), _lib.stream())
+    if rc == 10:
+        return False
+    if rc != 0:
+        raise RuntimeError(f"kca_decode_prep_attn_gemv returned status {rc}")
+    return True
+
+
+def gemv_dual_ln(x1: torch.Tensor, w1: torch.Tensor, x2: torch.Tensor, w2: torch.Tensor, bias, h: torch.Tensor,
+                 gamma: torch.Tensor, beta, eps: float, ypart: torch.Tensor, cnt: torch.Tensor,
+                 h_out: torch.Tensor, xn_out: torch.Tensor) -> None:
+    """Fused decode layer, part 2 (batch 1; ``kca_gemv_dual_ln``): y = x1 W1^T + x2 W2^T + b, then
+    h_out = h + y and xn_out = LayerNorm(h_out) -- the out-projection, fc_out, the parallel residual
+    and the next layer's LayerNorm in one launch. ``cnt``: a zero-initialised int32 [1] counter."""
+    _lib.call("kca_gemv_dual_ln", x1.data_ptr(), w1.data_ptr(), w1.shape[1], x2.data_ptr(), w2.data_ptr(),
+              w2.shape[1], _lib.ptr(bias), ypart.data_ptr(), cnt.data_ptr(), h.data_ptr(), h_out.data_ptr(),
+              gamma.data_ptr(), _lib.ptr(beta), float(eps), xn_out.data_ptr(), w1.shape[0], _lib.stream())
+
+
+def gemv_dual_ln_reference(x1, w1, x2, w2, bias, h, gamma, beta, eps):
+    """fp32 reference of ``gemv_dual_ln``: (h + y rounded to bf16, LayerNorm of it)."""
+    y = x1.float() @ w1.float().t() + x2.float() @ w2.float().t()
+    if bias is not None:
+        y = y + bias.float()
+    hn = (h.float() + y).to(h.dtype)
+    xn = torch.nn.functional.layer_norm(hn.float(), (hn.shape[-1],), gamma.float(),
+                                        beta.float() if beta is not None else None, eps)
+    return hn, xn
+
+
 def decode_attention_reference(q, k_cache, v_cache, slots, kv_lens, n_heads, scale, alibi=None, out=None,
                                block_table=None, window: int = 0):
     B = q.shape[0]
