@@ -733,13 +733,15 @@ __global__ __launch_bounds__(256) void decode_attn_gemv_kernel(DecodeParams p, i
   if (threadIdx.x < R && n0 + threadIdx.x < g.N) g.y[n0 + threadIdx.x] = f2bf(v);
 }
 
+constexpr int kDualSub = 64;  // sub-counters of gemv_dual_ln_kernel's arrival (cnt: 32 * (1 + 64) uints)
+
 struct DualLn {
   const bf16_t* x1;  // [K1] (attention output)
   const bf16_t* w1;  // [N, K1]
   const bf16_t* x2;  // [K2] (GELU(fc_in))
   const bf16_t* w2;  // [N, K2]
   const bf16_t* bias;  // [N] (nullable)
-  float* ypart;        // [N] fp32 workspace (write-through: the finishing workgroup reads it)
+  float* ypart;        // [NC, N] fp32 K-chunk partials (write-through: the finishing workgroup reads them)
   unsigned int* cnt;   // arrival counter, zero before the first launch, re-armed by the last workgroup
   const bf16_t* h;     // [N] residual stream in
   bf16_t* h_out;       // [N] h + y (bf16)
@@ -747,30 +749,57 @@ struct DualLn {
   const bf16_t* beta;
   float eps;
   bf16_t* xn_out;      // [N] LN(h + y)
-  int N, K1, K2;
+  int N, K1, K2, NC;   // NC = 1 + K2 / K1 K-chunks of K1 columns
 };
 
+// Workgroup (chunk c, row group g): R rows x K1 columns -- chunk 0 of W1 . x1, chunk c >= 1 the
+// (c-1)-th K1-wide slice of W2 . x2: every workgroup streams the same 4 x K1 weight tile as the
+// QKV GEMV's (the shape that reaches ~6 TB/s), NC x as many workgroups as one per row group
+// (one residency wave at N = 4096 streamed ~4.6 TB/s). Partials go to ypart[c]; the last workgroup
+// sums the NC chunks in a fixed order (deterministic), adds bias and residual and normalises.
 template <int R>
 __global__ __launch_bounds__(256) void gemv_dual_ln_kernel(DualLn a) {
   __shared__ float part[4][R];
   __shared__ float red[16];
   __shared__ int s_last;
   const int tid = threadIdx.x;
-  const int n0 = blockIdx.x * R;
+  const int ngrp = (a.N + R - 1) / R;
+  // chunk fastest: the workgroups in flight together cover whole weight rows (a chunk-major order
+  // had every resident workgroup reading one 8-KB piece of each 32-KB W2 row -- 1 / 4 of the HBM
+  // channels busy, 3.47 vs 2.41 ms/token)
+  const int c = blockIdx.x % a.NC, n0 = (blockIdx.x / a.NC) * R;
+  (void)ngrp;
   float acc[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) acc[r] = 0.f;
-  gemv_m1_accum<R>(a.x1, a.w1, a.N, a.K1, n0, acc);
-  gemv_m1_accum<R>(a.x2, a.w2, a.N, a.K2, n0, acc);
-  const float v = gemv_m1_finish<R>(acc, part, a.bias, n0, a.N, 0);
-  if (tid < R && n0 + tid < a.N) st_pub(&a.ypart[n0 + tid], v);
+  if (a.NC == 1) {  // unchunked (A/B): W1 then W2, whole rows
+    gemv_m1_accum<R>(a.x1, a.w1, a.N, a.K1, n0, acc);
+    gemv_m1_accum<R>(a.x2, a.w2, a.N, a.K2, n0, acc);
+  } else if (c == 0) {
+    gemv_m1_accum<R>(a.x1, a.w1, a.N, a.K1, n0, acc);
+  } else {
+    gemv_m1_accum<R>(a.x2 + (long long)(c - 1) * a.K1, a.w2 + (long long)(c - 1) * a.K1, a.N, a.K1, n0, acc, a.K2);
+  }
+  const float v = gemv_m1_finish<R>(acc, part, nullptr, n0, a.N, 0);
+  if (tid < R && n0 + tid < a.N) st_pub(&a.ypart[(long long)c * a.N + n0 + tid], v);
   // publish (cdna_hip_programming.md Guideline 16, R1): write-through stores drained, barrier, one
   // agent-scope arrival; the last workgroup re-arms the counter and acquires
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  // two-level arrival: thousands of workgroups adding to ONE address serialise at the memory side
+  // (~7 ns each: 5120 arrivals were +38 us per layer), so workgroup b counts into sub-counter b % 64
+  // (128 B apart) and each sub-counter's last arrival counts into the top one (cnt[0])
   if (tid == 0) {
-    const unsigned prev = __hip_atomic_fetch_add(a.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = prev == gridDim.x - 1;
+    constexpr int NSUB = kDualSub;
+    const int G = gridDim.x, sub = blockIdx.x % NSUB;
+    const int nsub = G < NSUB ? G : NSUB;
+    const unsigned members = (unsigned)((G - sub + NSUB - 1) / NSUB);
+    unsigned* sc = a.cnt + 32 * (1 + sub);
+    int last = 0;
+    if (__hip_atomic_fetch_add(sc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == members - 1) {
+      __hip_atomic_store(sc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+      last = __hip_atomic_fetch_add(a.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)nsub - 1;
+    }
     if (last) {
       __hip_atomic_store(a.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -788,9 +817,19 @@ __global__ __launch_bounds__(256) void gemv_dual_ln_kernel(DualLn a) {
   for (int i = 0; i < PER; ++i) {
     const int k = (i * 256 + tid) * 8;
     if (k < a.N) {
-      float y8[8];
-      load8(a.h + k, hv[i]);
+      float y8[8], t8[8], b8[8];
       load8f(a.ypart + k, y8);
+      for (int cc = 1; cc < a.NC; ++cc) {
+        load8f(a.ypart + (long long)cc * a.N + k, t8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y8[j] += t8[j];
+      }
+      if (a.bias) {
+        load8(a.bias + k, b8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y8[j] += b8[j];
+      }
+      load8(a.h + k, hv[i]);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         hv[i][j] = bf2f(f2bf(hv[i][j] + y8[j]));
@@ -1063,30 +1102,30 @@ KCA_API int kca_decode_prep_attn_gemv(const void* qkv, long long ld, const void*
 }
 
 // Fused decode layer, part 2: y = x1 W1^T + x2 W2^T + bias ([N]), h_out = bf16(h + y),
-// xn_out = LN(h_out) (gamma, beta, eps). ypart: [N] fp32 workspace; cnt: one zero-initialised
-// unsigned counter (re-armed by every launch's last workgroup).
+// xn_out = LN(h_out) (gamma, beta, eps). ypart: >= (1 + K2 / K1) * N fp32 workspace (K2 % K1 == 0);
+// cnt: 32 * (1 + kDualSub) zero-initialised unsigned counters (re-armed by every launch).
 KCA_API int kca_gemv_dual_ln(const void* x1, const void* w1, int K1, const void* x2, const void* w2, int K2,
                              const void* bias, float* ypart, unsigned int* cnt, const void* h, void* h_out,
                              const void* gamma, const void* beta, float eps, void* xn_out, int N,
                              hipStream_t stream) {
-  if (N <= 0 || N % 8 || N > 8192 || K1 % 8 || K2 % 8 || K1 <= 0 || K2 <= 0 || !ypart || !cnt || !gamma || !xn_out ||
-      !h || !h_out)
+  if (N <= 0 || N % 8 || N > 8192 || K1 % 8 || K2 % 8 || K1 <= 0 || K2 <= 0 || K2 % K1 || !ypart || !cnt || !gamma ||
+      !xn_out || !h || !h_out)
     return 1;
   if (((uintptr_t)x1 | (uintptr_t)w1 | (uintptr_t)x2 | (uintptr_t)w2 | (uintptr_t)h | (uintptr_t)h_out |
        (uintptr_t)gamma | (uintptr_t)beta | (uintptr_t)xn_out | (uintptr_t)ypart) & 15)
     return 2;
+  // default: one workgroup per 4 rows over K1 + K2 (2.31 ms/token); KCA_DUAL_CHUNK=1 splits K into
+  // QKV-shaped chunks (more, shorter workgroups: 2.39 ms/token, profiles/decode_fused_b1_ab_r3.txt)
+  static int chunked = -1;
+  if (chunked < 0) {
+    const char* e = getenv("KCA_DUAL_CHUNK");
+    chunked = e && e[0] == '1';
+  }
+  const int NC = chunked ? 1 + K2 / K1 : 1;
   const DualLn a{(const bf16_t*)x1, (const bf16_t*)w1, (const bf16_t*)x2, (const bf16_t*)w2, (const bf16_t*)bias,
                  ypart, cnt, (const bf16_t*)h, (bf16_t*)h_out, (const bf16_t*)gamma, (const bf16_t*)beta, eps,
-                 (bf16_t*)xn_out, N, K1, K2};
-  // rows per workgroup: 4 (N / 4 workgroups, one residency wave at GPT-J's N = 4096) or 2 (twice the
-  // workgroups in flight; KCA_DUAL_ROWS=2, A/B)
-  static int rows = -1;
-  if (rows < 0) {
-    const char* e = getenv("KCA_DUAL_ROWS");
-    rows = (e && e[0] == '2') ? 2 : 4;
-  }
-  if (rows == 2) hipLaunchKernelGGL(gemv_dual_ln_kernel<2>, dim3((N + 1) / 2), dim3(256), 0, stream, a);
-  else hipLaunchKernelGGL(gemv_dual_ln_kernel<4>, dim3((N + 3) / 4), dim3(256), 0, stream, a);
+                 (bf16_t*)xn_out, N, K1, K2, NC};
+  hipLaunchKernelGGL(gemv_dual_ln_kernel<4>, dim3(((N + 3) / 4) * NC), dim3(256), 0, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

@@ -31,7 +31,8 @@ __device__ __forceinline__ uint4 ld_w16(const bf16_t* p) {
 // run it on a subset of its workgroups. Not reduced across lanes: call gemv_m1_finish.
 template <int R>
 __device__ __forceinline__ void gemv_m1_accum(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, int N,
-                                              int K, int n0, float (&acc)[R]) {
+                                              int K, int n0, float (&acc)[R], long long ldw = -1) {
+  if (ldw < 0) ldw = K;  // row stride of w (a K-chunk of a wider matrix: the full row length)
   constexpr int U = 4;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int kl = wid * 512 + lane * 8;
@@ -40,7 +41,7 @@ __device__ __forceinline__ void gemv_m1_accum(const bf16_t* __restrict__ x, cons
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     rv[r] = n0 + r < N;
-    wr[r] = w + (long long)(rv[r] ? n0 + r : 0) * K;
+    wr[r] = w + (long long)(rv[r] ? n0 + r : 0) * ldw;
   }
   const int NI = (K + 2047) / 2048;
   for (int i0 = 0; i0 < NI; i0 += U) {

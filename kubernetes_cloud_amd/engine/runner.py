@@ -469,8 +469,9 @@ class ModelRunner:
                 biases.append(bf if bo is None else (bo if bf is None else (bo.float() + bf.float()).to(self.dtype)))
             fz = self._fz["b1"] = {
                 "g": torch.empty(1, f, **z), "h": torch.empty(1, d, **z), "xn": torch.empty(1, d, **z),
-                "ypart": torch.empty(d, device=self.device, dtype=torch.float32),
-                "cnt": torch.zeros(4, device=self.device, dtype=torch.int32), "bias": biases}
+                "ypart": torch.empty((1 + f // d) * d if f % d == 0 else d, device=self.device,
+                                     dtype=torch.float32),
+                "cnt": torch.zeros(32 * 65, device=self.device, dtype=torch.int32), "bias": biases}
         return fz
 
     def _layers_decode_fused(self, tokens, pos, slots, kv_lens, max_kv, ws, obuf):

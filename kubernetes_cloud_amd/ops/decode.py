@@ -228,7 +228,8 @@ def gemv_dual_ln(x1: torch.Tensor, w1: torch.Tensor, x2: torch.Tensor, w2: torch
                  h_out: torch.Tensor, xn_out: torch.Tensor) -> None:
     """Fused decode layer, part 2 (batch 1; ``kca_gemv_dual_ln``): y = x1 W1^T + x2 W2^T + b, then
     h_out = h + y and xn_out = LayerNorm(h_out) -- the out-projection, fc_out, the parallel residual
-    and the next layer's LayerNorm in one launch. ``cnt``: a zero-initialised int32 [1] counter."""
+    and the next layer's LayerNorm in one launch (K-chunked: W2's width a multiple of W1's; ``ypart``
+    holds 1 + K2 / K1 fp32 partial rows). ``cnt``: zero-initialised int32 [32 * 65] arrival counters."""
     _lib.call("kca_gemv_dual_ln", x1.data_ptr(), w1.data_ptr(), w1.shape[1], x2.data_ptr(), w2.data_ptr(),
               w2.shape[1], _lib.ptr(bias), ypart.data_ptr(), cnt.data_ptr(), h.data_ptr(), h_out.data_ptr(),
               gamma.data_ptr(), _lib.ptr(beta), float(eps), xn_out.data_ptr(), w1.shape[0], _lib.stream())

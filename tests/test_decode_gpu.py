@@ -496,8 +496,8 @@ def test_gemv_dual_ln_matches_reference():
     w1, w2 = torch.randn(N, K1, **bf) * K1 ** -0.5, torch.randn(N, K2, **bf) * K2 ** -0.5
     b, h = torch.randn(N, **bf), torch.randn(1, N, **bf)
     gamma, beta = torch.randn(N, **bf), torch.randn(N, **bf)
-    ypart = torch.empty(N, device=dev, dtype=torch.float32)
-    cnt = torch.zeros(4, device=dev, dtype=torch.int32)
+    ypart = torch.empty((1 + K2 // K1) * N, device=dev, dtype=torch.float32)
+    cnt = torch.zeros(32 * 65, device=dev, dtype=torch.int32)
     hn_ref, xn_ref = dops.gemv_dual_ln_reference(x1, w1, x2, w2, b, h, gamma, beta, 1e-5)
     for _ in range(3):
         h_out, xn = torch.empty(1, N, **bf), torch.empty(1, N, **bf)
@@ -505,7 +505,7 @@ def test_gemv_dual_ln_matches_reference():
         torch.cuda.synchronize()
         assert (h_out.float() - hn_ref.float()).abs().max() < 0.05
         assert (xn.float() - xn_ref).abs().max() < 0.08
-    assert int(cnt[0]) == 0  # re-armed
+    assert int(cnt.abs().sum()) == 0  # every counter re-armed
 
 
 @pytest.mark.parametrize("PS", [0, 64])
