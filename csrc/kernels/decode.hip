@@ -1151,6 +1151,7 @@ __device__ __forceinline__ uint32_t fkey(float f) {  // order-preserving float -
 }
 
 constexpr int SAMPLE_THREADS = 1024;
+constexpr int SAMPLE_CMAX = 2048;  // top-k survivors held in LDS (compact mode)
 
 // Wave 0 scans the 256-bin histogram from the top bin down and finds the bin in
 // which the running total first reaches `target` (excl < target <= incl).
@@ -1200,13 +1201,16 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(
     const float* __restrict__ top_p, const float* __restrict__ rep_pen, uint8_t* __restrict__ seen,
     const int* __restrict__ slots, const int* __restrict__ ban_ids, int n_ban,
     const unsigned long long* __restrict__ seeds, long long step, float* __restrict__ ws,
-    long long* __restrict__ out_ids, float* __restrict__ out_lp, int* __restrict__ out_kept) {
+    long long* __restrict__ out_ids, float* __restrict__ out_lp, int* __restrict__ out_kept, int compact) {
   __shared__ float hist[256];
   __shared__ float red[SAMPLE_THREADS / 64];
   __shared__ float sh_excl;
   __shared__ int sh_bin;
   __shared__ float scan[SAMPLE_THREADS / 64];
   __shared__ int sh_idx;
+  __shared__ float c_v[SAMPLE_CMAX];  // top-k survivors, index order (compact mode)
+  __shared__ int c_i[SAMPLE_CMAX];
+  __shared__ int iscan[SAMPLE_THREADS / 64];
   const int b = blockIdx.x, tid = threadIdx.x;
   const float T = temperature ? temperature[b] : 1.f;
   const float rp = rep_pen ? rep_pen[b] : 1.f;
@@ -1291,6 +1295,48 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(
     }
     thr = prefix;
   }
+  // compact mode: after a top-k select the survivors (k + ties) move to LDS in index order, so the
+  // top-p select and the multinomial below scan them instead of V (5 of the kernel's ~11 passes
+  // over the vocabulary); the index order keeps the multinomial's cumulative order unchanged
+  int nc = V;
+  bool cmp = false;
+  if (compact && k > 0 && k < V) {
+    const int sg = (V + SAMPLE_THREADS - 1) / SAMPLE_THREADS;
+    const int l0 = min(V, tid * sg), l1 = min(V, l0 + sg);
+    int cnt = 0;
+    for (int i = l0; i < l1; ++i) {
+      const float v = x[i];
+      cnt += (v != -INFINITY && fkey(v) >= thr) ? 1 : 0;
+    }
+    const int lane_ = tid & 63, wid_ = tid >> 6;
+    int inc = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(inc, o, 64);
+      if (lane_ >= o) inc += t;
+    }
+    if (lane_ == 63) iscan[wid_] = inc;
+    __syncthreads();
+    int off = inc - cnt, tot = 0;
+    for (int w = 0; w < SAMPLE_THREADS / 64; ++w) {
+      if (w < wid_) off += iscan[w];
+      tot += iscan[w];
+    }
+    if (tot <= SAMPLE_CMAX) {
+      for (int i = l0; i < l1 && cnt > 0; ++i) {
+        const float v = x[i];
+        if (v != -INFINITY && fkey(v) >= thr) {
+          c_v[off] = v;
+          c_i[off] = i;
+          ++off;
+          --cnt;
+        }
+      }
+      nc = tot;
+      cmp = true;
+    }
+    __syncthreads();
+  }
   // top-p: smallest key whose inclusive descending mass reaches p (HF keeps the
   // tokens whose ascending cumulative probability exceeds 1-p)
   const float pp = top_p ? top_p[b] : 1.f;
@@ -1300,8 +1346,8 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(
     for (int shift = 24; shift >= 0; shift -= 8) {
       for (int i = tid; i < 256; i += SAMPLE_THREADS) hist[i] = 0.f;
       __syncthreads();
-      for (int i = tid; i < V; i += SAMPLE_THREADS) {
-        const float v = x[i];
+      for (int i = tid; i < nc; i += SAMPLE_THREADS) {
+        const float v = cmp ? c_v[i] : x[i];
         const uint32_t key = fkey(v);
         if (key >= thr && (key & mask) == prefix && v != -INFINITY)
           atomicAdd(&hist[(key >> shift) & 255], __expf(v - M));
@@ -1328,12 +1374,12 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(
   }
 
   // multinomial over kept tokens in index order: segment sums + block scan
-  const int seg = (V + SAMPLE_THREADS - 1) / SAMPLE_THREADS;
-  const int lo = min(V, tid * seg), hi = min(V, lo + seg);
+  const int seg = (nc + SAMPLE_THREADS - 1) / SAMPLE_THREADS;
+  const int lo = min(nc, tid * seg), hi = min(nc, lo + seg);
   float ssum = 0.f;
   int kept = 0;
   for (int i = lo; i < hi; ++i) {
-    const float v = x[i];
+    const float v = cmp ? c_v[i] : x[i];
     if (v != -INFINITY && fkey(v) >= thr) {
       ssum += __expf(v - M);
       ++kept;
@@ -1376,9 +1422,9 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(
     float run = excl;
     int pick = -1;
     for (int i = lo; i < hi; ++i) {
-      const float v = x[i];
+      const float v = cmp ? c_v[i] : x[i];
       if (v != -INFINITY && fkey(v) >= thr) {
-        pick = i;
+        pick = cmp ? c_i[i] : i;
         run += __expf(v - M);
         if (run >= u) break;
       }
@@ -1389,11 +1435,13 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(
   if (tid == 0) {
     int id = sh_idx;
     if (id < 0) {  // float rounding at the very top of the range: last kept token
-      for (int i = V - 1; i >= 0; --i)
-        if (x[i] != -INFINITY && fkey(x[i]) >= thr) {
-          id = i;
+      for (int i = nc - 1; i >= 0; --i) {
+        const float v = cmp ? c_v[i] : x[i];
+        if (v != -INFINITY && fkey(v) >= thr) {
+          id = cmp ? c_i[i] : i;
           break;
         }
+      }
       if (id < 0) id = 0;
     }
     out_ids[b] = id;
@@ -1414,8 +1462,13 @@ KCA_API int kca_sample_logits(const void* logits, long long ld, int is_bf16, int
                               long long step, float* ws, long long* out_ids, float* out_lp,
                               int* out_kept, hipStream_t stream) {
   if (B <= 0 || V <= 0 || !ws || !out_ids) return 1;
+  static int compact = -1;  // KCA_SAMPLE_COMPACT=0: top-p / multinomial over the full vocabulary (A/B)
+  if (compact < 0) {
+    const char* e = getenv("KCA_SAMPLE_COMPACT");
+    compact = !(e && e[0] == '0');
+  }
   hipLaunchKernelGGL(sample_kernel, dim3(B), dim3(SAMPLE_THREADS), 0, stream, logits, ld, is_bf16,
                      V, temperature, top_k, top_p, rep_pen, (uint8_t*)seen, slots, ban_ids, n_ban,
-                     seeds, step, ws, out_ids, out_lp, out_kept);
+                     seeds, step, ws, out_ids, out_lp, out_kept, compact);
   return 0;
 }

@@ -67,11 +67,31 @@ def skinny_linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | No
         _lib.call("kca_skinny_gemm", x.data_ptr(), x.stride(0), weight.data_ptr(), _lib.ptr(bias), out.data_ptr(),
                   out.stride(0), M, N, K, int(act), _lib.stream())
         return out
-    y = _act_ref(F.linear(x, weight, bias), act)
+    y = _linear_act(x, weight, bias, act)
     if out is not None:
         out.copy_(y)
         return out
     return y
+
+
+# hipBLASLt decode linears with an activation (M > the skinny kernel's rows: fc_in at B >= 3): the
+# GELU as ONE native in-place pass (kca_gelu_fwd) instead of three eager kernels (to fp32, gelu,
+# to bf16: ~25 us per layer at B = 32, on the MLP branch's critical path); KCA_DECODE_GELU=epi
+# takes hipBLASLt's GELU epilogue (tanh form only), =torch the eager chain (A/B)
+_DECODE_GELU = os.environ.get("KCA_DECODE_GELU", "native")
+
+
+def _linear_act(x, weight, bias, act):
+    if not act:
+        return F.linear(x, weight, bias)
+    if _DECODE_GELU == "epi" and act == 1 and bias is not None and x.is_cuda:
+        return torch._addmm_activation(bias, x, weight.t(), use_gelu=True)
+    y = F.linear(x, weight, bias)
+    if _DECODE_GELU != "torch" and _lib.use_native(y) and y.is_contiguous() and y.numel() % 8 == 0 \
+            and y.data_ptr() % 16 == 0 and y.dtype == torch.bfloat16:
+        _lib.call("kca_gelu_fwd", y.data_ptr(), y.data_ptr(), y.numel(), int(act == 1), _lib.stream())
+        return y
+    return _act_ref(y, act)
 
 
 def _ln_ok(x, M, K, weight, residuals, gamma, beta, bias):

@@ -4,6 +4,7 @@ import math
 
 import pytest
 import torch
+import torch.nn.functional as F
 
 from kubernetes_cloud_amd.ops import _lib
 from kubernetes_cloud_amd.ops import decode as dops
@@ -97,6 +98,26 @@ def test_sample_greedy_and_masks(V):
             expect = int((x[b] >= x[b][keep].min()).sum())
             assert int(keep.sum()) <= int(kept[b]) <= expect + max(1, expect // 100), (t, k, p, b)
             assert bool(keep[ids[b]]), (t, k, p, b)
+
+
+def test_sample_topk_topp_distribution():
+    """Top-k + top-p sampling (the compact path: survivors of the top-k select in LDS) draws from
+    the renormalised kept set."""
+    torch.manual_seed(1)
+    V, B, k, p = 3000, 8192, 12, 0.9
+    base = torch.randn(V, device=dev) * 2
+    logits = base[None].expand(B, V).contiguous()
+    seeds = torch.randint(0, 2**62, (B,), device=dev)
+    kept = torch.empty(B, dtype=torch.int32, device=dev)
+    ids, lp = dops.sample_logits(logits, **_params(B, 1.0, k, p), seeds=seeds, out_kept=kept)
+    keep = dops.keep_mask_reference(base.float(), k, p)
+    assert bool(keep[ids].all())
+    assert int(kept[0]) == int(keep.sum())
+    probs = torch.where(keep, base.float(), torch.full_like(base, -float("inf"))).softmax(-1)
+    freq = torch.bincount(ids, minlength=V).float() / B
+    assert (freq - probs).abs().max() < 0.03
+    ref_lp = torch.log_softmax(base.float(), -1)[ids]
+    assert torch.allclose(lp, ref_lp, atol=1e-3)
 
 
 def test_sample_penalty_bans_distribution():
@@ -576,3 +597,18 @@ def test_engine_fused_b1_decode_matches_two_stream():
             top2 = row.topk(2).values
             if float(top2[0] - top2[1]) > 0.1:
                 assert int(row.argmax()) == t, i
+
+
+@pytest.mark.parametrize("act", [1, 2])
+def test_decode_linear_gelu_many_rows(act):
+    """Decode linears past the skinny kernel's rows (hipBLASLt + the native in-place GELU) match
+    an fp32 reference."""
+    from kubernetes_cloud_amd.ops.gemv import skinny_linear
+    torch.manual_seed(0)
+    M, K, N = 32, 512, 2048
+    x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=dev) / K ** 0.5).to(torch.bfloat16)
+    b = torch.randn(N, device=dev).to(torch.bfloat16)
+    y = skinny_linear(x, w, b, act)
+    ref = F.gelu(x.float() @ w.float().t() + b.float(), approximate="tanh" if act == 1 else "none")
+    assert (y.float() - ref).abs().max() < 3e-2
