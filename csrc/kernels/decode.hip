@@ -1152,6 +1152,42 @@ __device__ __forceinline__ uint32_t fkey(float f) {  // order-preserving float -
 
 constexpr int SAMPLE_THREADS = 1024;
 constexpr int SAMPLE_CMAX = 2048;  // top-k survivors held in LDS (compact mode)
+constexpr int SAMPLE_UN = 8;       // loads in flight per thread in the vocabulary passes
+
+// hist[bin] += w (weighted) or += 1 over the wave's lanes with bin >= 0, one LDS atomic per distinct
+// bin (ballot rounds, uniform loop; all 64 lanes must be active: wave_sum)
+__device__ __forceinline__ void hist_agg(float* hist, int bin, float w, bool weighted) {
+  unsigned long long act = __ballot(bin >= 0);
+  const int lane = threadIdx.x & 63;
+  while (act) {
+    const int leader = __ffsll((long long)act) - 1;
+    const int b0 = __shfl(bin, leader, 64);
+    const unsigned long long same = __ballot(bin == b0);
+    const float t = weighted ? wave_sum(bin == b0 ? w : 0.f) : (float)__popcll(same);
+    if (lane == leader) atomicAdd(&hist[b0], t);
+    act &= ~same;
+  }
+}
+
+// f(i, x[i]) for i = tid, tid + T, ... < n (increasing i per thread), SAMPLE_UN loads issued before
+// any is used: ONE workgroup walks the whole vocabulary, so a load-use-load loop is latency bound
+// (~50 dependent L2 round trips per pass at V = 50400)
+template <typename F>
+__device__ __forceinline__ void vocab_pass(const float* __restrict__ x, int n, F&& f) {
+  for (int base = threadIdx.x; base < n; base += SAMPLE_THREADS * SAMPLE_UN) {
+    float v[SAMPLE_UN];
+#pragma unroll
+    for (int u = 0; u < SAMPLE_UN; ++u) {
+      const int i = base + u * SAMPLE_THREADS;
+      v[u] = i < n ? x[i] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < SAMPLE_UN; ++u) {
+      const int i = base + u * SAMPLE_THREADS;
+      if (i < n) f(i, v[u]);
+    }
+  }
+}
 
 // Wave 0 scans the 256-bin histogram from the top bin down and finds the bin in
 // which the running total first reaches `target` (excl < target <= incl).
@@ -1221,10 +1257,27 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(
   const float inv_t = (greedy || T == 1.f) ? 1.f : 1.f / T;
 
   // pass 1: penalties + temperature -> ws
-  for (int i = tid; i < V; i += SAMPLE_THREADS) {
-    float v = is_bf16 ? bf2f(((const bf16_t*)logits)[b * ld + i]) : ((const float*)logits)[b * ld + i];
-    if (rp != 1.f && sn && sn[i]) v = v < 0.f ? v * rp : v / rp;
-    x[i] = v * inv_t;
+  const bool pen = rp != 1.f && sn;
+  for (int base = tid; base < V; base += SAMPLE_THREADS * SAMPLE_UN) {
+    float v[SAMPLE_UN];
+    uint8_t sv[SAMPLE_UN];
+#pragma unroll
+    for (int u = 0; u < SAMPLE_UN; ++u) {
+      const int i = base + u * SAMPLE_THREADS;
+      v[u] = 0.f;
+      sv[u] = 0;
+      if (i < V) {
+        v[u] = is_bf16 ? bf2f(((const bf16_t*)logits)[b * ld + i]) : ((const float*)logits)[b * ld + i];
+        if (pen) sv[u] = sn[i];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < SAMPLE_UN; ++u) {
+      const int i = base + u * SAMPLE_THREADS;
+      float w = v[u];
+      if (sv[u]) w = w < 0.f ? w * rp : w / rp;
+      if (i < V) x[i] = w * inv_t;
+    }
   }
   __syncthreads();
   if (ban_ids)
@@ -1237,8 +1290,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(
   // pass 2: max (+ argmax) and softmax normaliser
   float m = -INFINITY, s = 0.f;
   int am = 0x7fffffff;
-  for (int i = tid; i < V; i += SAMPLE_THREADS) {
-    const float v = x[i];
+  vocab_pass(x, V, [&](int i, float v) {
     if (v > m) {
       s = s * __expf(m - v) + 1.f;
       m = v;
@@ -1246,7 +1298,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(
     } else if (v != -INFINITY) {
       s += __expf(v - m);
     }
-  }
+  });
   const float M = block_max(m, red);
   s = (m == -INFINITY) ? 0.f : s * __expf(m - M);
   const float Z = block_sum(s, red);
@@ -1280,10 +1332,10 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(
     for (int shift = 24; shift >= 0; shift -= 8) {
       for (int i = tid; i < 256; i += SAMPLE_THREADS) hist[i] = 0.f;
       __syncthreads();
-      for (int i = tid; i < V; i += SAMPLE_THREADS) {
-        const uint32_t key = fkey(x[i]);
+      vocab_pass(x, V, [&](int, float v) {
+        const uint32_t key = fkey(v);
         if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1.f);
-      }
+      });
       __syncthreads();
       find_bin_desc(hist, remaining, &sh_excl, &sh_bin);
       const int bin = sh_bin;
@@ -1304,6 +1356,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(
     const int sg = (V + SAMPLE_THREADS - 1) / SAMPLE_THREADS;
     const int l0 = min(V, tid * sg), l1 = min(V, l0 + sg);
     int cnt = 0;
+#pragma unroll 8
     for (int i = l0; i < l1; ++i) {
       const float v = x[i];
       cnt += (v != -INFINITY && fkey(v) >= thr) ? 1 : 0;
@@ -1346,12 +1399,11 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(
     for (int shift = 24; shift >= 0; shift -= 8) {
       for (int i = tid; i < 256; i += SAMPLE_THREADS) hist[i] = 0.f;
       __syncthreads();
-      for (int i = tid; i < nc; i += SAMPLE_THREADS) {
-        const float v = cmp ? c_v[i] : x[i];
+      vocab_pass(cmp ? c_v : x, nc, [&](int, float v) {
         const uint32_t key = fkey(v);
         if (key >= thr && (key & mask) == prefix && v != -INFINITY)
           atomicAdd(&hist[(key >> shift) & 255], __expf(v - M));
-      }
+      });
       __syncthreads();
       if (shift == 24) {  // total kept mass after top-k
         float t = 0.f;
@@ -1378,6 +1430,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(
   const int lo = min(nc, tid * seg), hi = min(nc, lo + seg);
   float ssum = 0.f;
   int kept = 0;
+#pragma unroll 8
   for (int i = lo; i < hi; ++i) {
     const float v = cmp ? c_v[i] : x[i];
     if (v != -INFINITY && fkey(v) >= thr) {
@@ -1455,6 +1508,261 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(
   }
 }
 
+// Register-resident sampler (bf16 logits, V <= RPT * 1024, GPT-J's 50400 at 128 per thread x 512 threads): the row is read
+// ONCE into registers (element i = u * 1024 + tid, value u of the thread) and every later pass -- max / normaliser, the top-k
+// and top-p radix selects, the multinomial -- runs on registers and LDS histograms, not on a fp32
+// copy re-read from memory: one workgroup walking the vocabulary from L2 was ~15-20 us per pass.
+// Same selection semantics as sample_kernel (ties at the top-k / top-p thresholds kept, first index
+// for greedy); the multinomial's cumulative order is thread-major (tid, then u), fixed per seed.
+template <int RPT, int NT>
+__global__ __launch_bounds__(NT) void sample_reg_kernel(
+    const void* __restrict__ logits, long long ld, int V,
+    const float* __restrict__ temperature, const int* __restrict__ top_k,
+    const float* __restrict__ top_p, const float* __restrict__ rep_pen, uint8_t* __restrict__ seen,
+    const int* __restrict__ slots, const int* __restrict__ ban_ids, int n_ban,
+    const unsigned long long* __restrict__ seeds, long long step,
+    long long* __restrict__ out_ids, float* __restrict__ out_lp, int* __restrict__ out_kept) {
+  __shared__ float hist[256];
+  __shared__ float red[NT / 64];
+  __shared__ float sh_excl;
+  __shared__ int sh_bin;
+  __shared__ float scan[NT / 64];
+  __shared__ int sh_key;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const float T = temperature ? temperature[b] : 1.f;
+  const float rp = rep_pen ? rep_pen[b] : 1.f;
+  const int slot = slots ? slots[b] : b;
+  const uint8_t* sn = seen ? seen + (long long)slot * V : nullptr;
+  const bool greedy = !(T > 0.f);
+  const float inv_t = (greedy || T == 1.f) ? 1.f : 1.f / T;
+  const bool pen = rp != 1.f && sn;
+
+  // bf16 logits kept as raw bits, two per register (128 values in 64 VGPRs at 512 threads), the
+  // penalty as one bit per value; val(u) rebuilds the processed logit with the same fp32 ops every
+  // pass (bans and padding: bf16 -inf)
+  uint32_t raw[RPT / 2];
+  unsigned long long pbits[(RPT + 63) / 64] = {};
+  static_assert(RPT <= 128 && RPT % 2 == 0 && NT % 64 == 0, "register sampler: <= 128 values per thread");
+#pragma unroll
+  for (int u = 0; u < RPT; u += 2) {
+    uint32_t lo = 0xff80u, hi = 0xff80u;
+    const int i0 = u * NT + tid, i1 = i0 + NT;
+    const bf16_t* row = (const bf16_t*)logits + b * ld;
+    if (i0 < V) {
+      lo = row[i0];
+      if (pen && sn[i0]) pbits[u / 64] |= 1ull << (u % 64);
+    }
+    if (i1 < V) {
+      hi = row[i1];
+      if (pen && sn[i1]) pbits[(u + 1) / 64] |= 1ull << ((u + 1) % 64);
+    }
+    raw[u / 2] = lo | (hi << 16);
+  }
+  if (ban_ids)
+    for (int j = 0; j < n_ban; ++j) {
+      const int id = ban_ids[(long long)b * n_ban + j];
+      if (id >= 0 && id < V && (id & (NT - 1)) == tid) {
+        const int uu = id / NT;
+#pragma unroll
+        for (int u = 0; u < RPT; ++u)
+          if (u == uu) raw[u / 2] = (u & 1) ? ((raw[u / 2] & 0xffffu) | 0xff800000u) : ((raw[u / 2] & 0xffff0000u) | 0xff80u);
+      }
+    }
+  // each pass re-derives the values from the packed bits: the opaque touch stops the compiler from
+  // hoisting 64 unpacked floats out of the radix loops (they would not fit beside the packed copy)
+  auto touch = [&]() {
+#pragma unroll
+    for (int q = 0; q < RPT / 2; ++q) asm volatile("" : "+v"(raw[q]));
+  };
+  auto val = [&](int u) -> float {
+    float w = __uint_as_float((u & 1) ? (raw[u / 2] & 0xffff0000u) : (raw[u / 2] << 16));
+    if ((pbits[u / 64] >> (u % 64)) & 1ull) w = w < 0.f ? w * rp : w / rp;
+    return w * inv_t;
+  };
+  // max (+ first argmax) and softmax normaliser
+  float m = -INFINITY, s = 0.f;
+  int am = 0x7fffffff;
+  touch();
+#pragma unroll
+  for (int u = 0; u < RPT; ++u) {
+    const float w = val(u);
+    if (w > m) {
+      s = s * __expf(m - w) + 1.f;
+      m = w;
+      am = u * NT + tid;
+    } else if (w != -INFINITY) {
+      s += __expf(w - m);
+    }
+  }
+  const float M = block_max(m, red);
+  s = (m == -INFINITY) ? 0.f : s * __expf(m - M);
+  const float Z = block_sum(s, red);
+  const float lZ = M + __logf(Z);
+  if (greedy) {
+    int cand = (m == M) ? am : 0x7fffffff;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cand = min(cand, __shfl_xor(cand, o, 64));
+    __syncthreads();
+    if ((tid & 63) == 0) red[tid >> 6] = __int_as_float(cand);
+    __syncthreads();
+    int best = 0x7fffffff;
+    for (int w = 0; w < NT / 64; ++w) best = min(best, __float_as_int(red[w]));
+    if (best < V && (best & (NT - 1)) == tid) {  // the owner of the winning element
+      const int uu = best / NT;
+      float xb = 0.f;
+#pragma unroll
+      for (int u = 0; u < RPT; ++u)
+        if (u == uu) xb = val(u);
+      out_ids[b] = best;
+      if (out_lp) out_lp[b] = xb - lZ;
+      if (seen) seen[(long long)slot * V + best] = 1;
+      if (out_kept) out_kept[b] = 1;
+    }
+    return;
+  }
+
+  // top-k: radix select of the k-th largest key over the valid elements
+  uint32_t thr = 0;
+  const int k = top_k ? top_k[b] : 0;
+  if (k > 0 && k < V) {
+    uint32_t prefix = 0, mask = 0;
+    float remaining = (float)k;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+      for (int i = tid; i < 256; i += NT) hist[i] = 0.f;
+      __syncthreads();
+      touch();
+#pragma unroll
+      for (int u = 0; u < RPT; ++u) {
+        const uint32_t key = fkey(val(u));
+        hist_agg(hist, (u * NT + tid < V && (key & mask) == prefix) ? (int)((key >> shift) & 255) : -1, 1.f, false);
+      }
+      __syncthreads();
+      find_bin_desc(hist, remaining, &sh_excl, &sh_bin);
+      const int bin = sh_bin;
+      if (bin < 0) break;
+      prefix |= (uint32_t)bin << shift;
+      mask |= 255u << shift;
+      remaining -= sh_excl;
+      __syncthreads();
+    }
+    thr = prefix;
+  }
+  // top-p over the survivors
+  const float pp = top_p ? top_p[b] : 1.f;
+  if (pp < 1.f) {
+    uint32_t prefix = 0, mask = 0;
+    float above = 0.f, target = 0.f;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+      for (int i = tid; i < 256; i += NT) hist[i] = 0.f;
+      __syncthreads();
+      touch();
+#pragma unroll
+      for (int u = 0; u < RPT; ++u) {
+        const float w = val(u);
+        const uint32_t key = fkey(w);
+        const bool in = key >= thr && (key & mask) == prefix && w != -INFINITY;
+        hist_agg(hist, in ? (int)((key >> shift) & 255) : -1, in ? __expf(w - M) : 0.f, true);
+      }
+      __syncthreads();
+      if (shift == 24) {
+        float t = 0.f;
+        for (int i = tid; i < 256; i += NT) t += hist[i];
+        target = pp * block_sum(t, red);
+      }
+      find_bin_desc(hist, target - above, &sh_excl, &sh_bin);
+      const int bin = sh_bin;
+      if (bin < 0) {
+        prefix = 0;
+        mask = 0;
+        break;
+      }
+      prefix |= (uint32_t)bin << shift;
+      mask |= 255u << shift;
+      above += sh_excl;
+      __syncthreads();
+    }
+    if (mask == 0xffffffffu && prefix > thr) thr = prefix;
+  }
+
+  // multinomial over the kept elements, thread-major order: per-thread mass, block scan
+  float ssum = 0.f;
+  int kept = 0, last_u = -1;
+  touch();
+#pragma unroll
+  for (int u = 0; u < RPT; ++u) {
+    const float w = val(u);
+    if (w != -INFINITY && fkey(w) >= thr) {
+      ssum += __expf(w - M);
+      ++kept;
+      last_u = u;
+    }
+  }
+  const int lane = tid & 63, wid = tid >> 6;
+  float incl = ssum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  __syncthreads();
+  if (lane == 63) scan[wid] = incl;
+  int kept_tot = kept;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) kept_tot += __shfl_xor(kept_tot, o, 64);
+  if (lane == 0) red[wid] = __int_as_float(kept_tot);
+  if (tid == 0) sh_key = -1;
+  __syncthreads();
+  float woff = 0.f, total = 0.f;
+  for (int w = 0; w < NT / 64; ++w) {
+    if (w < wid) woff += scan[w];
+    total += scan[w];
+  }
+  incl += woff;
+  const float excl = incl - ssum;
+  uint32_t c[4] = {seeds ? 0u : (uint32_t)b, (uint32_t)step, (uint32_t)((unsigned long long)step >> 32), 0x5eedu};
+  const unsigned long long sd = seeds ? seeds[b] : 0ull;
+  philox4x32_10(c, (uint32_t)sd, (uint32_t)(sd >> 32));
+  const float r = ((c[0] >> 8) + 1) * (1.0f / 16777216.0f);  // (0, 1]
+  const float uu = r * total;
+  if (ssum > 0.f && excl < uu && uu <= incl) {
+    float run = excl;
+    int pick = -1;
+    touch();
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+      const float w = val(u);
+      if (pick < 0 && w != -INFINITY && fkey(w) >= thr) {
+        run += __expf(w - M);
+        if (run >= uu || u == last_u) pick = u;
+      }
+    }
+    if (pick >= 0) atomicMax(&sh_key, tid * RPT + pick);
+  }
+  __syncthreads();
+  if (sh_key < 0 && kept > 0) atomicMax(&sh_key, tid * RPT + last_u);  // rounding at the top of the range
+  __syncthreads();
+  const int key = sh_key;
+  if (key >= 0 && key / RPT == tid) {
+    const int pu = key % RPT, id = pu * NT + tid;
+    float xb = 0.f;
+#pragma unroll
+    for (int u = 0; u < RPT; ++u)
+      if (u == pu) xb = val(u);
+    out_ids[b] = id;
+    if (out_lp) out_lp[b] = xb - lZ;
+    if (seen) seen[(long long)slot * V + id] = 1;
+    if (out_kept) {
+      int kt = 0;
+      for (int w = 0; w < NT / 64; ++w) kt += __float_as_int(red[w]);
+      out_kept[b] = kt;
+    }
+  } else if (key < 0 && tid == 0) {  // nothing kept (all -inf): token 0, as sample_kernel
+    out_ids[b] = 0;
+    if (out_lp) out_lp[b] = -INFINITY;
+    if (out_kept) out_kept[b] = 0;
+  }
+}
+
 KCA_API int kca_sample_logits(const void* logits, long long ld, int is_bf16, int B, int V,
                               const float* temperature, const int* top_k, const float* top_p,
                               const float* rep_pen, void* seen, const int* slots,
@@ -1466,6 +1774,22 @@ KCA_API int kca_sample_logits(const void* logits, long long ld, int is_bf16, int
   if (compact < 0) {
     const char* e = getenv("KCA_SAMPLE_COMPACT");
     compact = !(e && e[0] == '0');
+  }
+  static int reg = -1;  // KCA_SAMPLE_REG=0: the memory-pass kernel for every vocabulary (A/B)
+  if (reg < 0) {
+    const char* e = getenv("KCA_SAMPLE_REG");
+    reg = !(e && e[0] == '0');
+  }
+  if (reg && is_bf16 && V <= 50 * 1024) {
+#define KCA_SAMPLE_REG_LAUNCH(R)                                                                          \
+  hipLaunchKernelGGL((sample_reg_kernel<R, 1024>), dim3(B), dim3(1024), 0, stream, logits, ld, V,            \
+                     temperature, top_k, top_p, rep_pen, (uint8_t*)seen, slots, ban_ids, n_ban, seeds, step,     \
+                     out_ids, out_lp, out_kept)
+    if (V <= 16 * 1024) KCA_SAMPLE_REG_LAUNCH(16);
+    else if (V <= 32 * 1024) KCA_SAMPLE_REG_LAUNCH(32);
+    else KCA_SAMPLE_REG_LAUNCH(50);  // GPT-2 / GPT-J / NeoX vocabularies (50257 / 50400 / 50432)
+#undef KCA_SAMPLE_REG_LAUNCH
+    return hipGetLastError() == hipSuccess ? 0 : 2;
   }
   hipLaunchKernelGGL(sample_kernel, dim3(B), dim3(SAMPLE_THREADS), 0, stream, logits, ld, is_bf16,
                      V, temperature, top_k, top_p, rep_pen, (uint8_t*)seen, slots, ban_ids, n_ban,

@@ -100,13 +100,14 @@ def test_sample_greedy_and_masks(V):
             assert bool(keep[ids[b]]), (t, k, p, b)
 
 
-def test_sample_topk_topp_distribution():
-    """Top-k + top-p sampling (the compact path: survivors of the top-k select in LDS) draws from
-    the renormalised kept set."""
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_sample_topk_topp_distribution(dtype):
+    """Top-k + top-p sampling draws from the renormalised kept set: fp32 logits take the memory-pass
+    kernel (top-k survivors compacted in LDS), bf16 the register-resident one."""
     torch.manual_seed(1)
     V, B, k, p = 3000, 8192, 12, 0.9
-    base = torch.randn(V, device=dev) * 2
-    logits = base[None].expand(B, V).contiguous()
+    base = (torch.randn(V, device=dev) * 2).to(dtype).float()
+    logits = base[None].expand(B, V).contiguous().to(dtype)
     seeds = torch.randint(0, 2**62, (B,), device=dev)
     kept = torch.empty(B, dtype=torch.int32, device=dev)
     ids, lp = dops.sample_logits(logits, **_params(B, 1.0, k, p), seeds=seeds, out_kept=kept)
@@ -118,6 +119,35 @@ def test_sample_topk_topp_distribution():
     assert (freq - probs).abs().max() < 0.03
     ref_lp = torch.log_softmax(base.float(), -1)[ids]
     assert torch.allclose(lp, ref_lp, atol=1e-3)
+
+
+@pytest.mark.parametrize("V", [1000, 50400])
+def test_sample_register_kernel_penalty_bans(V):
+    """bf16 logits (the register-resident sampler): repetition penalty through the seen mask and
+    banned ids match the reference for greedy picks, top-k kept counts match HF masks."""
+    torch.manual_seed(3)
+    B = 4
+    logits = (torch.randn(B, V, device=dev) * 3).to(torch.bfloat16)
+    top = logits.float().argmax(-1)
+    seen = torch.zeros(B, V, dtype=torch.uint8, device=dev)
+    seen[0, top[0]] = 1
+    seen[2, top[2]] = 1
+    slots = torch.arange(B, dtype=torch.int32, device=dev)
+    bans = torch.full((B, 2), -1, dtype=torch.int32, device=dev)
+    bans[1, 0] = top[1]
+    bans[3, 1] = top[3]
+    ref = dops.sample_logits_reference(logits.float().cpu(), *(v.cpu() for v in _params(B, 0.0, 0, 1.0, 30.0).values()),
+                                       seen=seen.cpu().clone(), slots=slots.cpu(), ban_ids=bans.cpu())[0]
+    ids, lp = dops.sample_logits(logits, **_params(B, 0.0, 0, 1.0, 30.0), seen=seen.clone(), slots=slots,
+                                 ban_ids=bans)
+    assert ids.tolist() == ref.tolist()
+    assert all(int(ids[b]) != int(top[b]) for b in range(B))
+    kept = torch.empty(B, dtype=torch.int32, device=dev)
+    ids, _ = dops.sample_logits(logits, **_params(B, 0.8, 40, 1.0), seeds=torch.arange(B, device=dev), out_kept=kept)
+    for b in range(B):
+        keep = dops.keep_mask_reference(logits[b].float() / 0.8, 40, 1.0)
+        expect = int((logits[b].float() / 0.8 >= (logits[b].float() / 0.8)[keep].min()).sum())
+        assert int(keep.sum()) <= int(kept[b]) <= expect and bool(keep[ids[b]])
 
 
 def test_sample_penalty_bans_distribution():

@@ -1,9 +1,17 @@
 #!/bin/bash
-# compact top-k sampler: decode tests, decode-only A/B at batch 1 and 32, then a batch-32 timeline
+# sampler kernel times per mode under rocprofv3 (kernel trace + stats)
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-GPU_AB_TESTS="tests/test_decode_gpu.py" bash tools/gpu_ab.sh samp1 2 "KCA_SAMPLE_COMPACT=0" "KCA_SAMPLE_COMPACT=1" 300 \
-  python -u bench/decode_bench.py --batches 1 --decode-only 48 &&
-bash tools/gpu_ab.sh samp32 1 "KCA_SAMPLE_COMPACT=0" "KCA_SAMPLE_COMPACT=1" 300 \
-  python -u bench/decode_bench.py --batches 32 --decode-only 24 &&
-B=32 bash tools/gpu_decode_timeline.sh && python3 tools/timeline.py gpurun_out/dec_tl/dec_kernel_trace.csv --show 40 > gpurun_out/dec_tl_b32.txt
+export TMPDIR=/tmp
+cd /tmp && timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/samp_prof -o samp -- python3 $GRAFT_REPO_ROOT/tools/sample_bench.py > $GRAFT_REPO_ROOT/gpurun_out/samp_prof.log 2>&1 &&
+python3 - <<'PY'
+import csv, glob, os, collections
+f = glob.glob(os.environ["GRAFT_REPO_ROOT"] + "/gpurun_out/samp_prof/**/*kernel_trace.csv", recursive=True)[0]
+rows = [r for r in csv.DictReader(open(f)) if "sample" in r["Kernel_Name"]]
+# 5 modes x (5 warm + 200 timed) calls in order
+n = 205
+for mi, name in enumerate(["greedy", "multinomial", "topk50", "topp0.95", "topk50_topp0.95"]):
+    seg = rows[mi * n + 5:(mi + 1) * n]
+    d = sorted(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in seg)
+    print(name, rows[mi * n]["Kernel_Name"][:40], "median us", d[len(d) // 2] / 1000)
+PY

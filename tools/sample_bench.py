@@ -1,0 +1,25 @@
+"""Sampler latency (kca_sample_logits, one workgroup per row) at GPT-J's vocabulary: greedy and
+top-k 50 / top-p 0.95, batch 1 and 32."""
+import sys, time, os
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+from kubernetes_cloud_amd.ops import decode as dops
+
+dev = torch.device("cuda", 0)
+V = 50400
+for B in (1,):
+    logits = (torch.randn(B, V, device=dev) * 4).to(torch.bfloat16)
+    for name, (t, k, p) in {"greedy": (0.0, 0, 1.0), "multinomial": (1.0, 0, 1.0), "topk50": (1.0, 50, 1.0),
+                          "topp0.95": (1.0, 0, 0.95), "topk50_topp0.95": (1.0, 50, 0.95)}.items():
+        f = lambda v, dt: torch.full((B,), v, dtype=dt, device=dev)  # noqa: E731
+        kw = dict(temperature=f(t, torch.float32), top_k=f(k, torch.int32), top_p=f(p, torch.float32),
+                  rep_penalty=f(1.0, torch.float32), seeds=torch.arange(B, device=dev))
+        for _ in range(5):
+            dops.sample_logits(logits, **kw)
+        torch.cuda.synchronize()
+        n = 200
+        t0 = time.perf_counter()
+        for _ in range(n):
+            dops.sample_logits(logits, **kw)
+        torch.cuda.synchronize()
+        print(f"B={B} {name}: {(time.perf_counter() - t0) / n * 1e6:.1f} us/call (host-launched, incl. launch)")
