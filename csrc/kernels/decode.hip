@@ -1154,21 +1154,6 @@ constexpr int SAMPLE_THREADS = 1024;
 constexpr int SAMPLE_CMAX = 2048;  // top-k survivors held in LDS (compact mode)
 constexpr int SAMPLE_UN = 8;       // loads in flight per thread in the vocabulary passes
 
-// hist[bin] += w (weighted) or += 1 over the wave's lanes with bin >= 0, one LDS atomic per distinct
-// bin (ballot rounds, uniform loop; all 64 lanes must be active: wave_sum)
-__device__ __forceinline__ void hist_agg(float* hist, int bin, float w, bool weighted) {
-  unsigned long long act = __ballot(bin >= 0);
-  const int lane = threadIdx.x & 63;
-  while (act) {
-    const int leader = __ffsll((long long)act) - 1;
-    const int b0 = __shfl(bin, leader, 64);
-    const unsigned long long same = __ballot(bin == b0);
-    const float t = weighted ? wave_sum(bin == b0 ? w : 0.f) : (float)__popcll(same);
-    if (lane == leader) atomicAdd(&hist[b0], t);
-    act &= ~same;
-  }
-}
-
 // f(i, x[i]) for i = tid, tid + T, ... < n (increasing i per thread), SAMPLE_UN loads issued before
 // any is used: ONE workgroup walks the whole vocabulary, so a load-use-load loop is latency bound
 // (~50 dependent L2 round trips per pass at V = 50400)
@@ -1522,12 +1507,14 @@ __global__ __launch_bounds__(NT) void sample_reg_kernel(
     const int* __restrict__ slots, const int* __restrict__ ban_ids, int n_ban,
     const unsigned long long* __restrict__ seeds, long long step,
     long long* __restrict__ out_ids, float* __restrict__ out_lp, int* __restrict__ out_kept) {
-  __shared__ float hist[256];
+  __shared__ float hist[16];
   __shared__ float red[NT / 64];
-  __shared__ float sh_excl;
-  __shared__ int sh_bin;
   __shared__ float scan[NT / 64];
   __shared__ int sh_key;
+  __shared__ uint32_t cnt16[NT / 64 * 8];
+  __shared__ int tot16[16];
+  __shared__ int sel[2];
+  __shared__ float selp[2];
   const int b = blockIdx.x, tid = threadIdx.x;
   const float T = temperature ? temperature[b] : 1.f;
   const float rp = rep_pen ? rep_pen[b] : 1.f;
@@ -1621,65 +1608,127 @@ __global__ __launch_bounds__(NT) void sample_reg_kernel(
     return;
   }
 
-  // top-k: radix select of the k-th largest key over the valid elements
+  // Radix selects on 4-bit digits (MSB first) with per-thread counters in registers: a 256-bin LDS
+  // histogram of the first digits takes most of the vocabulary into a few bins, and those LDS
+  // atomics serialise (~20 us per digit). Counts: 16 x 8-bit counters packed in 4 words (<= RPT
+  // per thread), reduced as 16-bit pairs (8 words) per wave then across waves in LDS.
+  // top-k: the k-th largest key among the valid elements (ties at it kept)
   uint32_t thr = 0;
   const int k = top_k ? top_k[b] : 0;
+  const int lane = tid & 63, wid = tid >> 6;
   if (k > 0 && k < V) {
     uint32_t prefix = 0, mask = 0;
-    float remaining = (float)k;
-    for (int shift = 24; shift >= 0; shift -= 8) {
-      for (int i = tid; i < 256; i += NT) hist[i] = 0.f;
-      __syncthreads();
+    int remaining = k;
+    for (int shift = 28; shift >= 0; shift -= 4) {
+      uint32_t w4[4] = {0u, 0u, 0u, 0u};
       touch();
 #pragma unroll
       for (int u = 0; u < RPT; ++u) {
         const uint32_t key = fkey(val(u));
-        hist_agg(hist, (u * NT + tid < V && (key & mask) == prefix) ? (int)((key >> shift) & 255) : -1, 1.f, false);
+        if (u * NT + tid < V && (key & mask) == prefix) {
+          const uint32_t d = (key >> shift) & 15u, inc = 1u << ((d & 3u) << 3);
+          w4[0] += d < 4 ? inc : 0u;
+          w4[1] += (d >> 2) == 1 ? inc : 0u;
+          w4[2] += (d >> 2) == 2 ? inc : 0u;
+          w4[3] += d >= 12 ? inc : 0u;
+        }
+      }
+      // 8-bit counters -> 16-bit pairs (digit 2j in the low half, 2j + 1 in the high half), wave sums
+      uint32_t w8[8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        w8[2 * q] = (w4[q] & 0xffu) | ((w4[q] & 0xff00u) << 8);
+        w8[2 * q + 1] = ((w4[q] >> 16) & 0xffu) | ((w4[q] >> 8) & 0xff0000u);
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) w8[q] += __shfl_xor(w8[q], o, 64);
+      __syncthreads();
+      if (lane < 8) {
+        uint32_t mine = w8[0];
+#pragma unroll
+        for (int q = 1; q < 8; ++q)
+          if (lane == q) mine = w8[q];
+        cnt16[wid * 8 + lane] = mine;
       }
       __syncthreads();
-      find_bin_desc(hist, remaining, &sh_excl, &sh_bin);
-      const int bin = sh_bin;
-      if (bin < 0) break;
-      prefix |= (uint32_t)bin << shift;
-      mask |= 255u << shift;
-      remaining -= sh_excl;
+      if (tid < 16) {  // digit totals, then one thread picks the digit
+        uint32_t t = 0;
+        for (int w = 0; w < NT / 64; ++w) t += cnt16[w * 8 + (tid >> 1)];
+        tot16[tid] = (int)((tid & 1) ? (t >> 16) : (t & 0xffffu));
+      }
       __syncthreads();
+      if (tid == 0) {
+        int run = 0, dsel = -1;
+        for (int j = 15; j >= 0; --j) {
+          if (run + tot16[j] >= remaining) {
+            dsel = j;
+            break;
+          }
+          run += tot16[j];
+        }
+        sel[0] = dsel;
+        sel[1] = run;
+      }
+      __syncthreads();
+      const int dsel = sel[0], run = sel[1];
+      if (dsel < 0) break;  // fewer valid elements than k (cannot happen: k < V)
+      prefix |= (uint32_t)dsel << shift;
+      mask |= 15u << shift;
+      remaining -= run;
     }
     thr = prefix;
   }
-  // top-p over the survivors
+  // top-p over the survivors: the smallest key whose descending inclusive mass reaches p * kept mass
+  // (LDS float atomics: after a top-k only a few dozen elements take part)
   const float pp = top_p ? top_p[b] : 1.f;
   if (pp < 1.f) {
     uint32_t prefix = 0, mask = 0;
-    float above = 0.f, target = 0.f;
-    for (int shift = 24; shift >= 0; shift -= 8) {
-      for (int i = tid; i < 256; i += NT) hist[i] = 0.f;
+    float above = 0.f, target = -1.f;
+    for (int shift = 28; shift >= 0; shift -= 4) {
+      if (tid < 16) hist[tid] = 0.f;
       __syncthreads();
       touch();
 #pragma unroll
       for (int u = 0; u < RPT; ++u) {
         const float w = val(u);
         const uint32_t key = fkey(w);
-        const bool in = key >= thr && (key & mask) == prefix && w != -INFINITY;
-        hist_agg(hist, in ? (int)((key >> shift) & 255) : -1, in ? __expf(w - M) : 0.f, true);
+        if (key >= thr && (key & mask) == prefix && w != -INFINITY)
+          atomicAdd(&hist[(key >> shift) & 15u], __expf(w - M));
       }
       __syncthreads();
-      if (shift == 24) {
-        float t = 0.f;
-        for (int i = tid; i < 256; i += NT) t += hist[i];
-        target = pp * block_sum(t, red);
+      if (tid == 0) {
+        if (target < 0.f) {  // first digit: total kept mass after top-k
+          float t = 0.f;
+          for (int j = 0; j < 16; ++j) t += hist[j];
+          target = pp * t;
+        }
+        float run = 0.f;
+        int dsel = -1;
+        for (int j = 15; j >= 0; --j) {
+          if (hist[j] > 0.f && run + hist[j] >= target - above) {
+            dsel = j;
+            break;
+          }
+          run += hist[j];
+        }
+        sel[0] = dsel;
+        selp[0] = run;
+        selp[1] = target;
       }
-      find_bin_desc(hist, target - above, &sh_excl, &sh_bin);
-      const int bin = sh_bin;
-      if (bin < 0) {
+      __syncthreads();
+      const int dsel = sel[0];
+      const float run = selp[0];
+      target = selp[1];
+      if (dsel < 0) {  // rounding: target not reached -> keep everything so far
         prefix = 0;
         mask = 0;
         break;
       }
-      prefix |= (uint32_t)bin << shift;
-      mask |= 255u << shift;
-      above += sh_excl;
-      __syncthreads();
+      prefix |= (uint32_t)dsel << shift;
+      mask |= 15u << shift;
+      above += run;
     }
     if (mask == 0xffffffffu && prefix > thr) thr = prefix;
   }
@@ -1697,7 +1746,6 @@ __global__ __launch_bounds__(NT) void sample_reg_kernel(
       last_u = u;
     }
   }
-  const int lane = tid & 63, wid = tid >> 6;
   float incl = ssum;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
