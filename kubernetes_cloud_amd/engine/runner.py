@@ -757,7 +757,10 @@ class ModelRunner:
         if self._pool is None:
             self._pool = torch.cuda.graph_pool_handle()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, pool=self._pool):
+        # thread-local capture: the RCCL process-group watchdog thread polls its work events while a
+        # capture runs; under the default global mode that query fails ("operation not permitted when
+        # stream is capturing") and the watchdog aborts the process
+        with torch.cuda.graph(g, pool=self._pool, capture_error_mode="thread_local"):
             self._step_body(st, Bb, Kb)
         self._graphs[(Bb, Kb)] = g
         return g

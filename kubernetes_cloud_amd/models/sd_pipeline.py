@@ -125,7 +125,7 @@ class UNetGraph:
                     self.unet(sx, st, sc)
             torch.cuda.current_stream().wait_stream(side)
             graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
+            with torch.cuda.graph(graph, capture_error_mode="thread_local"):  # see engine/runner.py _capture
                 out = self.unet(sx, st, sc)
             from .unet import pad_generation
             self.pad_gen = pad_generation()
