@@ -11,8 +11,12 @@
 // microseconds -- no collective, no syscall on the hot path.
 //
 // Layout (one mapping, created by the writer, opened by readers):
-//   Header   magic, geometry, head (next sequence to write), closed flag,
-//            cursor[r] (next sequence reader r will read), one cache line each
+//   Header   magic, geometry, writer pid (+ its pid namespace), head (next
+//            sequence to write), closed flag, cursor[r] (next sequence reader r
+//            will read), one cache line each
+// A reader that times out checks that the writer process still exists: a
+// writer killed without closing (OOM, SIGKILL) makes recv return -4, so the
+// follower ranks exit instead of spinning forever on their GPUs.
 //   Slot[n]  seq (published sequence + 1), length | LAST bit, payload
 // A message larger than a slot is split into fragments (LAST on the final
 // one). The writer reuses slot s for sequence q only after every reader's
@@ -21,6 +25,7 @@
 // slot.seq before copying (x86-TSO or not, the atomics carry the ordering).
 #include <errno.h>
 #include <fcntl.h>
+#include <signal.h>
 #include <sched.h>
 #include <stdint.h>
 #include <string.h>
@@ -57,6 +62,8 @@ struct Header {
   uint64_t nslots;
   uint64_t slot_bytes;
   uint64_t readers;
+  uint64_t writer_pid;
+  uint64_t writer_pidns;  // inode of the writer's /proc/self/ns/pid (0: unknown)
   Line head;
   Line closed;
   Line cursor[kMaxReaders];
@@ -104,6 +111,17 @@ struct Backoff {
   }
 };
 
+uint64_t pid_ns() {
+  struct stat st;
+  return stat("/proc/self/ns/pid", &st) == 0 ? (uint64_t)st.st_ino : 0;
+}
+
+// false only when the writer is provably gone: same pid namespace and no such process
+bool writer_alive(const Header* h) {
+  if (!h->writer_pid || !h->writer_pidns || h->writer_pidns != pid_ns()) return true;
+  return !(kill((pid_t)h->writer_pid, 0) != 0 && errno == ESRCH);
+}
+
 size_t map_size(uint64_t nslots, uint64_t slot_bytes) {
   return sizeof(Header) + nslots * (sizeof(SlotHdr) + slot_bytes);
 }
@@ -135,6 +153,8 @@ KCA_HOST_API void* kca_chan_create(const char* name, long long nslots, long long
   h->nslots = (uint64_t)nslots;
   h->slot_bytes = (uint64_t)slot_bytes;
   h->readers = (uint64_t)readers;
+  h->writer_pid = (uint64_t)getpid();
+  h->writer_pidns = pid_ns();
   h->head.v.store(0, std::memory_order_relaxed);
   h->closed.v.store(0, std::memory_order_relaxed);
   for (int r = 0; r < kMaxReaders; ++r) h->cursor[r].v.store(0, std::memory_order_relaxed);
@@ -229,7 +249,7 @@ KCA_HOST_API int kca_chan_send(void* hc, const void* data, long long len, int ti
 
 // Reader r: copy the next fragment into buf (cap >= the slot size) and set
 // *last when it ends a message. Returns its length; -1 bad args; -2 timeout;
-// -3 closed and drained. A fragment is consumed (its slot released to the
+// -3 closed and drained; -4 the writer process died without closing. A fragment is consumed (its slot released to the
 // writer) as soon as it is copied, so messages longer than the ring stream.
 KCA_HOST_API long long kca_chan_recv(void* hc, int reader, void* buf, long long cap, int timeout_ms, int* last) {
   Chan* c = static_cast<Chan*>(hc);
@@ -241,7 +261,7 @@ KCA_HOST_API long long kca_chan_recv(void* hc, int reader, void* buf, long long 
   Backoff bo;
   while (s->seq.load(std::memory_order_acquire) != seq + 1) {
     if (h->closed.v.load(std::memory_order_acquire) && h->head.v.load(std::memory_order_acquire) <= seq) return -3;
-    if (now_ms() - t0 > timeout_ms) return -2;
+    if (now_ms() - t0 > timeout_ms) return writer_alive(h) ? -2 : -4;
     bo.wait();
   }
   const uint64_t len = s->len;

@@ -87,9 +87,9 @@ class ShmChannel:
                                         1000 if self.block else self.timeout_ms, ctypes.byref(last))
             if n == -2 and self.block:
                 continue
-            if n < 0:
+            if n < 0:  # -4: the writer died without closing (a blocking reader must not spin forever)
                 raise ChannelError(f"shm channel recv failed ({n}: "
-                                   f"{ {-2: 'timeout', -3: 'closed'}.get(n, 'bad args') })")
+                                   f"{ {-2: 'timeout', -3: 'closed', -4: 'writer died'}.get(n, 'bad args') })")
             parts.append(self._buf.raw[:n])
             if last.value:
                 break

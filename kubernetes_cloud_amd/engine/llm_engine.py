@@ -326,6 +326,8 @@ class LLMEngine:
             self._decode_lookahead(finished)
         elif self.running or self._inflight:
             self._drain(finished)
+            # the drained step may have finished requests (slot released, pages freed)
+            self.running = [r for r in self.running if not r.done]
             rows = [self._row(r) for r in self.running]
             if rows:
                 toks, lps = self.runner.decode(rows)

@@ -139,6 +139,18 @@ def exists(uri: str, timeout_s: float = 5.0) -> bool:
         return False
 
 
+def is_kca_object(uri: str, timeout_s: float = 5.0) -> bool:
+    """True when the object at ``uri`` starts with this framework's ``.tensors`` magic (an
+    8-byte ranged GET); False for a foreign object (e.g. a CoreWeave tensorizer file, whose
+    wire format is not in the tree) or an unreachable one."""
+    from .tensors import MAGIC
+    try:
+        head, _ = get_range(resolve(uri, timeout_s), 0, len(MAGIC))
+    except (IOError, OSError, ValueError):
+        return False
+    return head[:len(MAGIC)] == MAGIC
+
+
 def read_header(uri: str, timeout_s: float = 30.0) -> tuple[dict, int, Remote]:
     from .tensors import ALIGN, MAGIC
     r = resolve(uri, timeout_s)
@@ -207,7 +219,12 @@ def public_tensorized_uri(model: str, fp16: bool = False, timeout_s: float = 5.0
     """The reference's public-bucket probe (finetuner.py:395-410): if
     ``{org}/{name}`` is published under the ``tensorized`` bucket, return its
     ``s3://`` URI (fp16 variant with ``fp16``), else None. ``KCA_TENSORIZED_BASE``
-    overrides the probe base URL; ``KCA_TENSORIZED_PROBE=0`` disables it."""
+    overrides the probe base URL; ``KCA_TENSORIZED_PROBE=0`` disables it.
+
+    The published objects may be in CoreWeave's tensorizer wire format, which this
+    framework does not read (parity unpinned: not in the tree): an object without the
+    ``.tensors`` magic logs a warning and returns None, so the caller falls back to
+    ``--model`` exactly as the reference's ``except OSError: pass`` does."""
     if os.environ.get("KCA_TENSORIZED_PROBE", "1") in ("0", "false", "no"):
         return None
     model_id = "/".join(model.rstrip("/").split("/")[-2:])
@@ -215,10 +232,17 @@ def public_tensorized_uri(model: str, fp16: bool = False, timeout_s: float = 5.0
     if not exists(f"{base}/{model_id}/model.tensors", timeout_s):
         return None
     sub = "fp16/" if fp16 else ""
+    probe = f"{base}/{model_id}/{sub}model.tensors"
+    if not is_kca_object(probe, timeout_s):
+        import logging
+        logging.getLogger(__name__).warning(
+            "%s exists but is not a kca .tensors object (foreign tensorizer format?): loading --model instead",
+            probe)
+        return None
     if base == PUBLIC_TENSORIZED:
         return f"s3://tensorized/{model_id}/{sub}model.tensors"
-    return f"{base}/{model_id}/{sub}model.tensors"
+    return probe
 
 
-__all__ = ["Remote", "is_remote", "resolve", "exists", "read_header", "stream", "get_range",
+__all__ = ["Remote", "is_remote", "resolve", "exists", "is_kca_object", "read_header", "stream", "get_range",
            "public_tensorized_uri"]

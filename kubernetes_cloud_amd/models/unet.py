@@ -217,7 +217,7 @@ class ResnetBlock2D(nn.Module):
         (one cast/add kernel pair less per block and step)."""
         ps = [p for p in (self.conv1.bias, self.conv2.bias,
                           self.conv_shortcut.bias if self.conv_shortcut is not None else None) if p is not None]
-        key = tuple((p.data_ptr(), p._version) for p in ps)
+        key = (_WEIGHT_GEN,) + tuple((p.data_ptr(), p._version) for p in ps)
         c = getattr(self, "_fb_cache", None)
         if c is None or c[0] != key:
             b2 = self.conv2.bias.float()
@@ -267,6 +267,11 @@ _FUSED_QKV_TRAIN = os.environ.get("KCA_SD_FUSED_QKV_TRAIN", "1") not in ("0", "f
 # kernel's S MFMAs also subtract the softmax offset (attention_tiled.hip MC); KCA_SD_MAX_COL=0 disables
 _MAX_COL = os.environ.get("KCA_SD_MAX_COL", "1") not in ("0", "false")
 _PAD_GEN = 0
+# Derived-weight caches (folded biases, phase GEMM weights, time-projection and context-K/V tables)
+# key on (data_ptr, _version); the native optimizer (kca_adamw) updates parameters in place through
+# raw pointers without bumping _version, so the training engine bumps this generation instead
+# (UNet2DConditionModel.invalidate_weight_caches, called from TrainEngine._refresh_derived).
+_WEIGHT_GEN = 0
 # inference: residual adds carried by the preceding GEMM's epilogue (ops.linear_residual);
 # KCA_SD_FUSE_RES=0 keeps the separate adds (A/B knob)
 _FUSE_RES = os.environ.get("KCA_SD_FUSE_RES", "1") not in ("0", "false")
@@ -563,7 +568,7 @@ class Upsample2D(nn.Module):
 
     def _gemm_weights(self):
         cw = self.conv.weight
-        key = (cw.data_ptr(), cw._version)
+        key = (_WEIGHT_GEN, cw.data_ptr(), cw._version)
         c = getattr(self, "_phase_cache", None)
         if c is None or c[0] != key:  # re-derived when the conv weight is replaced or updated
             c = self._phase_cache = (key, phase_gemm_weights(cw))
@@ -701,12 +706,20 @@ class UNet2DConditionModel(nn.Module):
     def enable_gradient_checkpointing(self, on: bool = True):
         self.gradient_checkpointing = on
 
+    def invalidate_weight_caches(self):
+        """Parameters changed in place: every derived-weight cache rebuilds on next use."""
+        global _WEIGHT_GEN
+        _WEIGHT_GEN += 1
+        for m in self.modules():
+            if isinstance(m, Attention):
+                m._padded = None
+
     def _temb_adds(self, temb: torch.Tensor) -> _TembAdds:
         """One GEMM for every ResNet block's time projection (+ its conv1 bias, fp32): see _TembAdds."""
         rs = [m for m in self.modules() if isinstance(m, ResnetBlock2D) and m.time_emb_proj is not None
               and m.conv1.bias is not None]
         ps = [p for r in rs for p in (r.time_emb_proj.weight, r.time_emb_proj.bias, r.conv1.bias) if p is not None]
-        key = tuple((p.data_ptr(), p._version) for p in ps)
+        key = (_WEIGHT_GEN,) + tuple((p.data_ptr(), p._version) for p in ps)
         c = getattr(self, "_temb_cache", None)
         if c is None or c[0] != key:
             w = torch.cat([r.time_emb_proj.weight for r in rs])
@@ -726,7 +739,7 @@ class UNet2DConditionModel(nn.Module):
         GEMM (see CtxKV). ``out``: recompute into that object's table (static graph buffers)."""
         attns = [m for m in self.modules() if isinstance(m, Attention) and m.cross]
         ps = [p for a in attns for p in (a.to_k.weight, a.to_v.weight, a.to_k.bias, a.to_v.bias) if p is not None]
-        key = tuple((p.data_ptr(), p._version) for p in ps)
+        key = (_WEIGHT_GEN,) + tuple((p.data_ptr(), p._version) for p in ps)
         c = getattr(self, "_ctxkv_cache", None)
         if c is None or c[0] != key:
             ws, bs, offs, o = [], [], {}, 0

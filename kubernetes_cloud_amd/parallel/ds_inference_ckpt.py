@@ -85,9 +85,9 @@ def export_ds_inference(model_or_dir, out_dir: str, tp_size: int, shards_per_ran
                 tp[r][k] = s.contiguous()
     torch.save(non_tp, os.path.join(out_dir, "non-tp.pt"))
     names = []
-    for r in range(tp_size):
-        keys = sorted(tp[r])
-        for s in range(shards_per_rank):
+    for s in range(shards_per_rank):  # partition-major, as DeepSpeed's TP save lists them
+        for r in range(tp_size):
+            keys = sorted(tp[r])
             part = {k: tp[r][k] for k in keys[s::shards_per_rank]}
             fn = f"tp_{r:02d}_{s:02d}.pt"
             torch.save(part, os.path.join(out_dir, fn))
@@ -103,14 +103,15 @@ def export_ds_inference(model_or_dir, out_dir: str, tp_size: int, shards_per_ran
 
 def _tp_files_by_rank(files: list, tp_size: int) -> dict:
     """Checkpoint rank -> its files. DeepSpeed assigns ``checkpoints.tp`` by
-    POSITION: with n = len(files) / tp_size, rank r reads files[r*n:(r+1)*n]
-    (file names carry no contract)."""
+    POSITION, partition-major: with n = len(files) / tp_size partitions, rank r
+    reads files[i*tp_size + r] for i < n (its loader's ``ckpt_index = i *
+    ckpt_mp_size + sd_offset``); file names carry no contract."""
     if not files:
         return {}
     if len(files) % tp_size:
         raise ValueError(f"{len(files)} tp checkpoint files do not split over tp_size {tp_size}")
     n = len(files) // tp_size
-    return {r: list(files[r * n:(r + 1) * n]) for r in range(tp_size)}
+    return {r: [files[i * tp_size + r] for i in range(n)] for r in range(tp_size)}
 
 
 def _unwrap(v):

@@ -752,7 +752,10 @@ class TrainEngine:
         self.publish(self.opt.master)
 
     def _refresh_derived(self):
-        """Weights changed: re-derive per-model caches (transposed weight copies)."""
+        """Weights changed: re-derive per-model caches (transposed weight copies, UNet tables)."""
+        inv = getattr(self.model, "invalidate_weight_caches", None)
+        if inv is not None:
+            inv()
         if self.part_params:
             return
         fn = getattr(self.model, "refresh_transposed_weights", None)

@@ -8,9 +8,12 @@ CLI = the union of resnet50_pytorch.py:28-70 and resnet50_horovod.py:18-62
 ``-j/--workers``, ``--wandb-project``/``--wandb-run``, ``--backend``; Horovod's
 ``--fp16-allreduce``, ``--use-mixed-precision``, ``--gradient-predivide-factor``,
 ``--use-adasum``: Horovod's Adasum combination (resnet50_horovod.py:115-139;
-``adasum_hook``, recursive doubling with per-tensor coefficients, LR not
-scaled by the world size -- the reference's "Adasum doesn't need scaling up
-learning rate").
+``adasum_hook``, recursive doubling with per-tensor coefficients). On GPUs it is
+Horovod's hierarchical form: gradients are AVERAGED inside the node and
+combined with Adasum across nodes (one cross-node group per local rank), with
+the LR scaled by the local size (resnet50_horovod.py:121-123); on CPU it is
+flat Adasum over all ranks at LR x 1 ("Adasum doesn't need scaling up learning
+rate", :115-116).
 
 MI355X choices: DDP over RCCL with 100 MB buckets (fewer, larger ring
 all-reduces over the point-to-point xGMI links), gradient all-reduce
@@ -193,19 +196,24 @@ def main(argv=None):
         miopen.configure()  # keep MIOpen's naive NHWC solvers out of the conv search
         model = model.to(memory_format=torch.channels_last)
     adasum = args.use_adasum and world > 1
-    if adasum and world & (world - 1):
-        print(f"[resnet] --use-adasum needs a power-of-two world size (got {world}); averaging instead", flush=True)
+    # GPU: average inside the node, Adasum across nodes (Horovod's NCCL build); CPU: flat Adasum
+    local = local_size(world) if use_cuda else 1
+    if adasum and (world // local) & (world // local - 1):
+        print(f"[resnet] --use-adasum needs a power-of-two Adasum group (got {world // local}); averaging instead",
+              flush=True)
         adasum = False
     if world > 1:
         model = nn.parallel.DistributedDataParallel(model, device_ids=[dev.index] if use_cuda else None,
                                                     bucket_cap_mb=args.bucket_mb, gradient_as_bucket_view=True)
         if adasum:
-            model.register_comm_hook(state=AdasumState(dist.group.WORLD, args.fp16_allreduce), hook=adasum_hook)
+            lg, cg = adasum_groups(world, rank, local)
+            model.register_comm_hook(state=AdasumState(cg, args.fp16_allreduce, lg), hook=adasum_hook)
         elif args.fp16_allreduce or args.gradient_predivide_factor != 1.0:
             model.register_comm_hook(state=(dist.group.WORLD, args.fp16_allreduce, args.gradient_predivide_factor),
                                      hook=_compressed_allreduce_hook)
-    # Horovod's LR scaler: x world for averaging, 1 for Adasum (resnet50_horovod.py:115-116)
-    opt = torch.optim.SGD(model.parameters(), lr=args.lr * (1 if adasum else world), momentum=args.momentum)
+    # Horovod's LR scaler: x world for averaging, 1 for Adasum, x local size for GPU Adasum
+    # (resnet50_horovod.py:115-123)
+    opt = torch.optim.SGD(model.parameters(), lr=args.lr * (local if adasum else world), momentum=args.momentum)
     sink = MetricsSink(str(args.log_dir), args.wandb_run or "resnet50",
                        project=args.wandb_project or "resnet50-imagenet", enabled=rank == 0)
     amp = args.use_mixed_precision and use_cuda
@@ -293,9 +301,36 @@ def _compressed_allreduce_hook(state, bucket):
 
 
 class AdasumState:
-    def __init__(self, group, compress: bool = False):
-        self.group, self.compress = group, compress
+    """``group``: the ranks combined with Adasum; ``local_group`` (hierarchical form): the ranks
+    averaged first (one node), None for flat Adasum."""
+
+    def __init__(self, group, compress: bool = False, local_group=None):
+        self.group, self.compress, self.local_group = group, compress, local_group
         self.segments: dict = {}  # bucket index -> (segment ids, n tensors)
+
+
+def local_size(world: int) -> int:
+    """GPUs per node: torchrun's LOCAL_WORLD_SIZE (Horovod's hvd.local_size()), else all ranks."""
+    n = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+    return n if n > 0 and world % n == 0 else world
+
+
+def adasum_groups(world: int, rank: int, local: int):
+    """(local group, cross group) of ``rank`` for hierarchical Adasum: nodes are runs of ``local``
+    consecutive ranks; the cross group holds the ranks of equal local rank. Every rank creates
+    every group (dist.new_group is collective); a size-1 group is returned as None."""
+    lg = cg = None
+    for n in range(world // local):
+        ranks = list(range(n * local, (n + 1) * local))
+        g = dist.new_group(ranks) if local > 1 else None
+        if rank in ranks:
+            lg = g
+    for lr in range(local):
+        ranks = list(range(lr, world, local))
+        g = dist.new_group(ranks) if len(ranks) > 1 else None
+        if rank in ranks:
+            cg = g
+    return lg, cg
 
 
 def adasum_pair(a: torch.Tensor, b: torch.Tensor, seg: torch.Tensor, n: int) -> torch.Tensor:
@@ -333,6 +368,18 @@ def adasum_allreduce(buf: torch.Tensor, seg: torch.Tensor, n: int, group=None, c
     return buf
 
 
+def hierarchical_adasum(buf: torch.Tensor, seg: torch.Tensor, n: int, local_group=None, cross_group=None,
+                        compress: bool = False):
+    """Average over ``local_group`` (skipped when None), then Adasum over ``cross_group``
+    (skipped when None): Horovod's GPU Adasum, node-local reduction + cross-node Adasum."""
+    if local_group is not None:
+        dist.all_reduce(buf, group=local_group)
+        buf.div_(dist.get_world_size(local_group))
+    if cross_group is not None:
+        adasum_allreduce(buf, seg, n, cross_group, compress)
+    return buf
+
+
 def adasum_hook(state: AdasumState, bucket):
     """DDP comm hook: the bucket's flat gradient is combined with Adasum, one
     coefficient pair per parameter tensor of the bucket."""
@@ -343,7 +390,7 @@ def adasum_hook(state: AdasumState, bucket):
         ids = [torch.full((g.numel(),), i, dtype=torch.long) for i, g in enumerate(bucket.gradients())]
         seg = (torch.cat(ids).to(buf.device), len(ids))
         state.segments[key] = seg
-    adasum_allreduce(buf, seg[0], seg[1], state.group, state.compress)
+    hierarchical_adasum(buf, seg[0], seg[1], state.local_group, state.group, state.compress)
     fut = torch.futures.Future()
     fut.set_result(buf)
     return fut

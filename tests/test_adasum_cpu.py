@@ -41,6 +41,41 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
+def _hier_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from kubernetes_cloud_amd.train.resnet import adasum_groups, hierarchical_adasum
+    lg, cg = adasum_groups(world, rank, 2)
+    buf = _grads(world)[rank].clone()
+    seg, n = _seg()
+    hierarchical_adasum(buf, seg, n, lg, cg)
+    q.put((rank, buf))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_hierarchical_adasum_averages_in_node_then_adasum_across():
+    """Horovod's GPU Adasum (resnet50_horovod.py:121-123): 2 nodes x 2 local ranks ->
+    Adasum(mean(g0, g1), mean(g2, g3)) on every rank (the LR is scaled by the local size)."""
+    world = 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_hier_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    seg, n = _seg()
+    g = _grads(world)
+    ref = adasum_pair((g[0] + g[1]) / 2, (g[2] + g[3]) / 2, seg, n)
+    for r in range(world):
+        assert torch.equal(res[r], res[0])
+    assert torch.allclose(res[0], ref, atol=1e-5)
+
+
 def _tree(gs, seg, n):
     while len(gs) > 1:
         gs = [adasum_pair(gs[i], gs[i + 1], seg, n) for i in range(0, len(gs), 2)]

@@ -78,3 +78,36 @@ def test_as_channel_wraps_process_groups():
         assert as_channel(ch) is ch
     finally:
         dist.destroy_process_group()
+
+
+def _doomed_writer(name, q):
+    from kubernetes_cloud_amd.engine.ctrl_channel import ShmChannel
+    w = ShmChannel(name, -1, readers=1, slots=4, slot_bytes=4096)
+    w.send("hello")
+    q.put("sent")
+    time.sleep(600)  # killed by the test without closing the channel
+
+
+def test_blocking_reader_raises_when_writer_dies():
+    """a blocking follower (timeout_s=None) must not spin forever when rank 0 is
+    SIGKILLed / OOM-killed without closing -- recv sees the writer pid gone and raises."""
+    from kubernetes_cloud_amd.engine.ctrl_channel import ChannelError, ShmChannel
+    name = f"/kca_test_{os.getpid()}_{uuid.uuid4().hex[:8]}"
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_doomed_writer, args=(name, q))
+    p.start()
+    assert q.get(timeout=120) == "sent"
+    r = ShmChannel(name, 0)  # blocking reader
+    assert r.recv() == "hello"
+    p.kill()
+    p.join(timeout=30)
+    t0 = time.monotonic()
+    with pytest.raises(ChannelError, match="writer died"):
+        r.recv()
+    assert time.monotonic() - t0 < 30
+    r.close()
+    try:
+        os.unlink("/dev/shm" + name)  # the killed writer never unlinked it
+    except OSError:
+        pass

@@ -54,8 +54,10 @@ def test_ds_inference_deepspeed_layout(bloom, tmp_path):
     cfgj = json.load(open(os.path.join(src, "ds_inference_config.json")))
     out = tmp_path / "ds"
     out.mkdir()
+    # DeepSpeed's TP save lists partition-major: [m0 r0, m0 r1, m1 r0, m1 r1]
+    assert cfgj["checkpoints"]["tp"] == ["tp_00_00.pt", "tp_01_00.pt", "tp_00_01.pt", "tp_01_01.pt"]
     names = []
-    for i, fn in enumerate(cfgj["checkpoints"]["tp"]):  # rank-major order, renamed
+    for i, fn in enumerate(cfgj["checkpoints"]["tp"]):  # same positions, names without ranks
         sd = torch.load(os.path.join(src, fn), weights_only=True)
         sd = {k: ([v, "torch.float32"] if "query_key_value" in k else v) for k, v in sd.items()}
         name = f"bloom-ds-shard-{chr(ord('a') + i)}.pt"

@@ -333,3 +333,28 @@ def test_batched_small_grad_accum_param_fed_twice(monkeypatch):
     assert flushes[0] == 1  # the second entry for the same parameter flushed the first
     ref = g1.float().reshape(-1) + g2.float().reshape(-1)
     assert torch.allclose(got, ref)
+
+
+def test_lookahead_to_fallback_drops_finished_requests():
+    """A request finishing in the drained in-flight step must not be decoded again when the
+    engine leaves lookahead (a multi-token bad word arrives): its slot is already released."""
+    m = tiny("gpt-j-6b")
+    sp = SamplingParams(max_new_tokens=6, do_sample=False)
+    short = SamplingParams(max_new_tokens=2, do_sample=False)
+    ban = SamplingParams(max_new_tokens=6, do_sample=False, bad_words_ids=[[96, 95]])
+    solo = [LLMEngine(m, max_slots=1, max_len=40).generate([p], s)[0].output
+            for p, s in (([3, 4], short), ([9, 8, 7], sp), ([5, 6], ban))]
+    eng = LLMEngine(m, max_slots=3, max_len=40, pipeline=True)
+    real = eng.runner.decode
+
+    def checked(rows, *a, **kw):  # a released slot is -1: out of bounds in the GPU cache kernels
+        assert all(r["slot"] >= 0 for r in rows), [r["slot"] for r in rows]
+        return real(rows, *a, **kw)
+    eng.runner.decode = checked
+    b = eng.add_request([9, 8, 7], sp)  # slot 2: the row a stale slot -1 would alias
+    a = eng.add_request([3, 4], short)
+    eng.step()  # prefill (token 1) + lookahead launch of token 2
+    c = eng.add_request([5, 6], ban)  # next step falls back; a's last token is in flight
+    eng.run_until_done()
+    assert [a.output, b.output, c.output] == solo
+    assert a.finish_reason == "length" and eng.stats["finished"] == 3 and sorted(eng.free) == [0, 1, 2]

@@ -191,3 +191,36 @@ def test_phase_upsampler_training_grads_match_fp32(N, C, S, bias):
 def _rel(a, b):
     a, b = a.float(), b.float()
     return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def test_unet_inference_caches_follow_native_optimizer_steps():
+    """kca_adamw updates the bf16 parameters in place (no _version bump): the folded-bias,
+    phase-GEMM, time-projection and context-K/V caches must still follow the new weights
+    (TrainEngine._refresh_derived -> invalidate_weight_caches), e.g. DreamBooth's image logging."""
+    import copy
+
+    from kubernetes_cloud_amd.models.unet import UNet2DConditionModel, UNetConfig, to_channels_last
+    from kubernetes_cloud_amd.train.engine import TrainEngine
+    torch.manual_seed(0)
+    cfg = UNetConfig(block_out_channels=(64, 128, 128, 128), cross_attention_dim=64, sample_size=32)
+    m = to_channels_last(UNet2DConditionModel(cfg).to(DEV).bfloat16())
+    x = torch.randn(2, cfg.in_channels, 32, 32, device=DEV, dtype=torch.bfloat16)
+    ctx = torch.randn(2, 8, cfg.cross_attention_dim, device=DEV, dtype=torch.bfloat16)
+    eng = TrainEngine(m, lr=1e-2, zero_stage=0)
+    m.eval()
+    with torch.no_grad():
+        m(x, 10, ctx)  # populate every cache
+        m.ctx_kv(ctx)
+    m.train()
+    eng.train_batch([x], lambda b: m(b, 10, ctx).float().pow(2).mean())
+    m.eval()
+    with torch.no_grad():
+        got = m(x, 10, ctx)
+        fresh = copy.deepcopy(m)  # same weights, no caches
+        for mod in fresh.modules():
+            for a in ("_fb_cache", "_phase_cache", "_temb_cache", "_ctxkv_cache"):
+                if hasattr(mod, a):
+                    delattr(mod, a)
+        ref = fresh(x, 10, ctx)
+    err = (got.float() - ref.float()).abs().max().item()
+    assert err <= 1e-3 * ref.float().abs().max().item(), err
