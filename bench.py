@@ -33,7 +33,11 @@ the headline always prints):
   ``secondary_bloom_slice`` BLOOM-176B, 8 of 70 layers + embeddings/head, TP
                             modules under a one-rank RCCL group, batch 1/8/32;
   ``secondary_weight_load`` GPT-J fp16 ``.tensors`` -> HBM GB/s (file written
-                            in the run, O_DIRECT read).
+                            in the run, O_DIRECT read);
+  ``secondary_serving``     the tensorized GPT-J KServe predictor and the BLOOM
+                            predictor over HTTP (bench/serving_bench.py):
+                            req/s, p50/p99, tokens/s at concurrency 1/8/32, and
+                            the same requests without the HTTP layer.
 
 ``KCA_BENCH_SHARED_GPU=1`` (rehearsal only, parallel/shared_gpu.py): N ranks
 share cuda:0 with gloo collectives staged through the host, so the N > 1 paths
@@ -363,11 +367,17 @@ def _extras(args, dev, rec):
         if time.perf_counter() > deadline:
             return
         t0 = time.perf_counter()
+        torch.cuda.reset_peak_memory_stats()  # per-phase peaks, not the GPT-J step's
         try:
             out = fn()
         except Exception as e:  # noqa: BLE001 - the headline line must still print
             print(f"[bench] {key} failed: {e!r}", file=sys.stderr, flush=True)
             out = {"error": repr(e)[:300]}
+        peak = round(torch.cuda.max_memory_allocated() / 2**30, 1)
+        if isinstance(out, dict):
+            out.setdefault("phase_peak_mem_gib", peak)
+        elif isinstance(out, list):
+            out = {"phase_peak_mem_gib": peak, "records": out}
         torch.cuda.empty_cache()
         print(f"[bench] {key}: {time.perf_counter() - t0:.1f}s", file=sys.stderr, flush=True)
         if rec is not None:
@@ -387,20 +397,32 @@ def _extras(args, dev, rec):
         store = dist.HashStore()
         dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=dev)
         try:
-            return _load_bench("bloom_tp_bench").run_tp_decode("bloom-176b", layers=8, batches=(1, 8, 32),
+            recs = _load_bench("bloom_tp_bench").run_tp_decode("bloom-176b", layers=8, batches=(1, 8, 32),
                                                                prompt_len=128, new_tokens=32)
         finally:
             dist.destroy_process_group()
+        return {"proxy": "TP=1 (one-rank RCCL group), 8 of 70 layers, bf16: a proxy for BASELINE config 4 "
+                         "(TP=8, all 70 layers, fp16 checkpoint, engine + HTTP); fp16 checkpoints load as bf16 "
+                         "(same bytes per weight; the decode kernels are bf16-native)",
+                "records": recs}
 
     def weight_load():
         d = os.environ.get("KCA_WEIGHT_LOAD_DIR", os.environ.get("TMPDIR", "/tmp"))
         return _load_bench("weight_load_bench").run_weight_load("gpt-j-6b", d, threads=8, sources=("cold",))
+
+    def serving():
+        # the tensorized GPT-J KServe predictor and the BLOOM predictor contract over HTTP
+        # (loadgen at concurrency 1 / 8 / 32) next to the same requests straight into predict
+        sb = _load_bench("serving_bench")
+        d = os.environ.get("KCA_WEIGHT_LOAD_DIR", os.environ.get("TMPDIR", "/tmp"))
+        return {"gptj": sb.run_gptj(d), "bloom_slice": sb.run_bloom_slice(8)}
 
     try:
         fenced("secondary_dreambooth", dreambooth)
         fenced("secondary_decode", decode)
         fenced("secondary_bloom_slice", bloom_slice)
         fenced("secondary_weight_load", weight_load)
+        fenced("secondary_serving", serving)
     finally:
         timer.cancel()
 

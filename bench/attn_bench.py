@@ -128,7 +128,11 @@ def main():
     ap.add_argument("--no-sdpa", action="store_true")
     ap.add_argument("--fwd-only", action="store_true")
     ap.add_argument("--generic", action="store_true", help="disable the full-tile fast kernels")
+    ap.add_argument("--variant", type=int, default=-1, help="kca_attn_set_variant bits (A/B); -1 = default")
     a = ap.parse_args()
+    if a.variant >= 0:
+        from kubernetes_cloud_amd.ops.attention import set_variant
+        set_variant(a.variant)
     if a.generic:
         from kubernetes_cloud_amd.ops.attention import set_tiled_path
         set_tiled_path(False)

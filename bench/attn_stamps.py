@@ -29,6 +29,8 @@ SEGMENTS = {
                 "O+=PV", "LDS store + barrier", "epilogue (O, lse stores)"]),
     "dq": (16, ["prologue", "issue K/V loads", "S, dP MFMAs", "softmax / dS", "dQ MFMAs",
                 "LDS store + barrier", "epilogue (dQ stores)"]),
+    "fwd_w8": (48, ["pre-wait (prologue, skipped tiles)", "vmcnt wait + barrier", "LDS-DMA issue",
+                    "S=QK^T MFMAs", "mask + softmax", "O+=PV", "epilogue"]),
     "dkdv": (32, ["prologue (K, V image)", "issue Q/dO loads", "S, dP MFMAs", "softmax / dS",
                   "dV, dK MFMAs", "LDS store + barrier", "epilogue (dK, dV stores)"]),
 }

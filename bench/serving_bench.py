@@ -1,0 +1,210 @@
+#!/usr/bin/env python3
+"""End-to-end serving benchmark over HTTP (bench.py ``secondary_serving``).
+
+The reference ships a load test for its InferenceServices
+(online-inference/tensorizer-isvc/benchmark/load_test.py:135-180) and asks for
+BLOOM "at the engine and end-to-end over HTTP" (BASELINE.md config 4). This
+measures what a user of those services sees on one MI355X:
+
+* ``gptj``: the tensorized GPT-J KServe predictor (serving/predictors.py
+  ``GPTJPredictor``, kserve_api.py:47-72 contract: ``{"instances": [prompt]}``,
+  ``max_new_tokens`` 50, ``do_sample`` True) loaded from a random-init
+  ``gptj.tensors`` written in the run, behind the V1 REST server
+  (serving/server.py) on 127.0.0.1, driven by serving/loadgen.py at
+  concurrency 1 / 8 / 32;
+* ``bloom_slice``: the BLOOM predictor contract (bloom.py env options,
+  ``MAX_LENGTH`` 40) on an 8-of-70-layer random-init BLOOM-176B slice (TP=1
+  proxy for config 4), same loads.
+
+For each level the same requests are also pushed through ``predict`` directly
+from a thread pool of the same width ("engine"): the difference is the HTTP
+layer (uvicorn + JSON + the loadgen client). Tokenizer: a small byte-level BPE
+trained in the run (no network for the GPT-2 vocabulary); prompt lengths are
+therefore ~1 token per byte, which moves only prefill.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import shutil
+import socket
+import statistics
+import sys
+import tempfile
+import threading
+import time
+from concurrent.futures import ThreadPoolExecutor
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch
+
+LEVELS = ((1, 8), (8, 32), (32, 96))  # (concurrency, requests)
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _tokenizer(path: str):
+    from tokenizers import Tokenizer, decoders, models, pre_tokenizers, trainers
+    from transformers import PreTrainedTokenizerFast
+    from kubernetes_cloud_amd.serving.loadgen import PROMPTS
+    tok = Tokenizer(models.BPE())
+    tok.pre_tokenizer = pre_tokenizers.ByteLevel(add_prefix_space=False)
+    tok.decoder = decoders.ByteLevel()
+    tr = trainers.BpeTrainer(vocab_size=400, special_tokens=["<|endoftext|>"],
+                             initial_alphabet=pre_tokenizers.ByteLevel.alphabet())
+    tok.train_from_iterator(list(PROMPTS) * 10, tr)
+    fast = PreTrainedTokenizerFast(tokenizer_object=tok, eos_token="<|endoftext|>", bos_token="<|endoftext|>",
+                                   unk_token="<|endoftext|>")
+    fast.save_pretrained(path)
+    return fast
+
+
+class _Server:
+    """The repo's V1/V2 REST app (serving/server.py) under uvicorn in a thread."""
+
+    def __init__(self, models):
+        import uvicorn
+
+        from kubernetes_cloud_amd.serving.server import ModelServer
+        self.port = _free_port()
+        app = ModelServer(http_port=self.port, argv=[]).create_app(models)
+        cfg = uvicorn.Config(app, host="127.0.0.1", port=self.port, log_level="warning", access_log=False)
+        self.srv = uvicorn.Server(cfg)
+        self.th = threading.Thread(target=self.srv.run, daemon=True)
+        self.th.start()
+        t0 = time.time()
+        while not self.srv.started:
+            if time.time() - t0 > 60:
+                raise RuntimeError("uvicorn did not start")
+            time.sleep(0.05)
+        self.url = f"http://127.0.0.1:{self.port}"
+
+    def close(self):
+        self.srv.should_exit = True
+        self.th.join(timeout=30)
+
+
+def _engine(pred, n: int, conc: int, seed: int = 0) -> dict:
+    """The same request stream straight into ``predict`` (no HTTP), ``conc`` in flight."""
+    import random
+
+    from kubernetes_cloud_amd.serving.loadgen import PROMPTS
+    rnd = random.Random(seed)
+    payloads = [{"instances": [rnd.choice(PROMPTS)]} for _ in range(n)]
+
+    def one(p):
+        t = time.perf_counter()
+        pred.predict(p)
+        return time.perf_counter() - t
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(conc) as ex:
+        lat = sorted(ex.map(one, payloads))
+    dt = time.perf_counter() - t0
+    return {"throughput_rps": n / dt, "mean_latency_s": statistics.mean(lat), "p50_s": lat[int(0.5 * (n - 1))],
+            "p99_s": lat[int(0.99 * (n - 1))]}
+
+
+def _levels(pred, model_name: str, new_tokens: int | None, levels=LEVELS) -> list:
+    from kubernetes_cloud_amd.serving.loadgen import benchmark
+    srv = _Server([pred])
+    out = []
+    try:
+        benchmark(srv.url, "kserve", 4, concurrency=4, model=model_name, seed=99)  # warm: graphs, allocator
+        _engine(pred, 4, 4, seed=98)
+        for conc, n in levels:
+            h = benchmark(srv.url, "kserve", n, concurrency=conc, model=model_name, seed=conc)
+            e = _engine(pred, n, conc, seed=conc)
+            rec = {"concurrency": conc, "requests": n, "successes": h["successes"],
+                   "http_rps": round(h["throughput_rps"], 3),
+                   **({"http_tokens_per_s": round(h["goodput_rps"] * new_tokens, 1)} if new_tokens else {}),
+                   "http_p50_s": round(h.get("p50_s", float("nan")), 4),
+                   "http_p99_s": round(h.get("p99_s", float("nan")), 4),
+                   "engine_rps": round(e["throughput_rps"], 3),
+                   "engine_p50_s": round(e["p50_s"], 4), "engine_p99_s": round(e["p99_s"], 4)}
+            rec["http_overhead_p50_ms"] = round((rec["http_p50_s"] - rec["engine_p50_s"]) * 1e3, 2)
+            out.append(rec)
+    finally:
+        srv.close()
+    return out
+
+
+def _device():
+    return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+
+
+def run_gptj(directory: str | None = None, levels=LEVELS, overrides: dict | None = None) -> dict:
+    """Random-init GPT-J-6B -> ``{dir}/gptj.tensors`` -> GPTJPredictor (tensorizer load) -> HTTP.
+    ``overrides``: config fields (CPU tests shrink the model)."""
+    from kubernetes_cloud_amd.io.hf import serialize_causal_lm
+    from kubernetes_cloud_amd.models.causal_lm import build_model
+    from kubernetes_cloud_amd.models.config import preset
+    from kubernetes_cloud_amd.serving.predictors import GPTJPredictor
+    dev = _device()
+    d = tempfile.mkdtemp(prefix="kca_serving_", dir=directory)
+    try:
+        cfg = preset("gpt-j-6b", **(overrides or {}))
+        m = build_model(cfg, device=dev, dtype=torch.bfloat16 if dev.type == "cuda" else torch.float32, seed=0)
+        with open(os.path.join(d, "config.json"), "w") as f:
+            json.dump(cfg.to_hf(), f)
+        serialize_causal_lm(m, os.path.join(d, "gptj.tensors"))
+        del m
+        torch.cuda.empty_cache()
+        _tokenizer(d)
+        pred = GPTJPredictor(model_path=d, load_type="tensorizer")
+        pred.load()
+        os.remove(os.path.join(d, "gptj.tensors"))
+        try:
+            lv = _levels(pred, "gptj", 50, levels)
+        finally:
+            pred.generator.close()
+        return {"metric": "gpt-j-6b KServe V1 over HTTP", "model": "gpt-j-6b", "load": "tensorizer (.tensors file)",
+                "load_s": round(pred.load_seconds, 2), "new_tokens": 50, "sampling": "do_sample, top_k 50",
+                "dtype": "bf16", "levels": lv, "data": "random-init weights, loadgen prompts"}
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
+def run_bloom_slice(layers: int = 8, levels=LEVELS, overrides: dict | None = None) -> dict:
+    """BLOOM predictor contract (bloom.py options, MAX_LENGTH 40) on a random-init BLOOM-176B slice."""
+    from kubernetes_cloud_amd.models.causal_lm import build_model
+    from kubernetes_cloud_amd.models.config import preset
+    from kubernetes_cloud_amd.serving.predictors import BloomPredictor
+    from kubernetes_cloud_amd.serving.text import TextGenerator
+    dev = _device()
+    cfg = preset("bloom-176b", **(overrides or {}))
+    cfg.n_layers = layers
+    d = tempfile.mkdtemp(prefix="kca_bloom_tok_")
+    try:
+        tok = _tokenizer(d)
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    m = build_model(cfg, device=dev, dtype=torch.bfloat16 if dev.type == "cuda" else torch.float32, seed=0).eval()
+    gen = TextGenerator(m, tok, max_slots=32, max_len=64)
+    pred = BloomPredictor(name="bigscience-bloom", generator=gen)
+    try:
+        lv = _levels(pred, pred.name, None, levels)
+    finally:
+        gen.close()
+    return {"metric": "bloom-176b predictor over HTTP", "proxy": f"TP=1, {layers} of 70 layers, bf16 (config 4 is "
+            "TP=8 fp16 over 70 layers)", "max_length": 40, "sampling": "temperature 1, top_k 50", "levels": lv,
+            "data": "random-init weights, loadgen prompts"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--which", default="gptj,bloom_slice")
+    a = ap.parse_args()
+    for w in a.which.split(","):
+        r = run_gptj() if w == "gptj" else run_bloom_slice()
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()

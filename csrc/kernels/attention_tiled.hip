@@ -568,6 +568,291 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel
 }
 
 
+// ================================================== forward, 8 waves (2 per SIMD), 256 query rows
+// The 4-wave kernel above runs one wave per SIMD: every LDS round trip, softmax and K/V tile wait of
+// that wave idles its SIMD's matrix pipe (~0.29 MFMA busy at D = 256), and each 32-key tile feeds
+// only 128 query rows, so the per-CU K/V stream bounds the loop (profiles/attn_stamps_r2.md). Here a
+// workgroup holds 8 waves x 32 query rows = 256 rows: the two waves of a SIMD cover each other's
+// stalls, and every staged K/V byte serves twice the MFMA work.
+//
+// The price is the register file: at two waves per SIMD a wave has 256 registers, and O^T (128),
+// the Q^T fragments (D/4 = 64) and one S tile (16) leave no room for register-staged K/V tiles. So
+// the tiles arrive by LDS-DMA (buffer_load ... lds: no VGPR destination), four buffers deep, issued
+// two tiles ahead, one barrier per tile after a COUNTED vmcnt. hipcc drains every LDS-DMA
+// (vmcnt(0)) before any LDS read it can see, so the loop's LDS reads (K rows: ds_read_b128; V^T:
+// ds_read_b64_tr_b16) are inline asm with hand-counted lgkmcnt waits, each wait tied to the
+// fragment it retires ("+v") so no MFMA can be scheduled above it.
+// An LDS-DMA wave-instruction writes 1 KiB at consecutive addresses (lane-linear); the image's
+// sub-tile swizzle (img_off) is applied on the per-lane SOURCE address instead.
+// Causal: a wave skips the tiles past its own diagonal (its SIMD partner gets the matrix pipe).
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+// (the asm bodies exist only in the device pass: the host pass parses this kernel for its launch
+// stub and rejects the VGPR constraints)
+template <int OFF>
+__device__ __forceinline__ u32x4 ads_b128(unsigned addr) {
+  u32x4 r;
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+#endif
+  return r;
+}
+template <int OFF>
+__device__ __forceinline__ u32x2 ads_tr(unsigned addr) {
+  u32x2 r;
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+#endif
+  return r;
+}
+// s_waitcnt lgkmcnt(N) that the named fragments depend on
+template <int N>
+__device__ __forceinline__ void lgkm_wait(u32x4& x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(x) : "n"(N));
+#endif
+}
+template <int N>
+__device__ __forceinline__ void lgkm_wait(u32x2& x, u32x2& y, u32x2& z, u32x2& w) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(x), "+v"(y), "+v"(z), "+v"(w) : "n"(N));
+#endif
+}
+__device__ __forceinline__ bf16x8 as_bf8(u32x4 x) { return *reinterpret_cast<bf16x8*>(&x); }
+__device__ __forceinline__ bf16x8 as_bf8(u32x2 lo, u32x2 hi) {
+  u32x4 x{lo[0], lo[1], hi[0], hi[1]};
+  return *reinterpret_cast<bf16x8*>(&x);
+}
+
+template <int D, bool CAUSAL>
+__global__ void __launch_bounds__(512, 1) attn_fwd_w8_kernel(FastFwdParams p) {
+  constexpr int BM = 256, BN = 32, NW = 8, NBUF = 4;
+  constexpr int TILE = BN * D * 2;            // one K or V image
+  constexpr int STAGE = 2 * TILE;
+  constexpr int KS = D / 16;
+  constexpr int PIECES = TILE / 1024;         // 1-KiB LDS-DMA pieces per image
+  constexpr int PPW = PIECES / NW;            // per wave per image
+#ifdef KCA_W8_NOSTAGGER  // A/B arm: both halves in lock step (S -> softmax -> PV), tiles issued 3 ahead
+  constexpr bool STAGGER = false;
+#else
+  constexpr bool STAGGER = true;
+#endif
+  constexpr int LEAD = STAGGER ? NBUF - 2 : NBUF - 1;    // tiles issued ahead of the one computed
+  constexpr int INFLIGHT = (LEAD - 1) * 2 * PPW;  // DMA instructions issued after tile t when t is waited
+  static_assert(D == 256 || D == 128, "8-wave forward: D = 128 / 256");
+  static_assert(PPW >= 1 && PIECES % NW == 0, "whole pieces per wave");
+  constexpr int SMEM = (NBUF * STAGE > NW * 32 * D * 2) ? NBUF * STAGE : NW * 32 * D * 2;
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];  // [buf][K|V]; epilogue: [wave][32][D]
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int nqb = p.Sq / BM;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int qi = lid % nqb;
+  const int qb = CAUSAL ? (nqb - 1 - qi) : qi;
+  const int bh = lid / nqb;
+  const int b = bh / p.H, h = bh % p.H;
+  const int hk = h / (p.H / p.Hkv);
+  const int off = p.Sk - p.Sq;
+  const int q0 = qb * BM + wave * 32;
+  const int qrow = q0 + l32;
+  int kv_hi = p.Sk;
+  if (CAUSAL) kv_hi = min(kv_hi, qb * BM + BM + off);
+  const int ntiles = kv_hi / BN;
+  const int mytiles = CAUSAL ? min(ntiles, (q0 + 32 + off) / BN) : ntiles;
+  const float sl2 = p.scale * kLog2e;
+
+  const bf16_t* qp = p.q + b * p.q_sb + h * p.q_sh;
+  bf16x8 qf[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+    qf[s] = *reinterpret_cast<const bf16x8*>(qp + (long long)qrow * p.q_st + 16 * s + 8 * hh);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // Q landed before any DMA is counted
+
+  // LDS-DMA sources: piece j of an image covers image bytes [1024 j, 1024 j + 1024); lane L writes
+  // byte 1024 j + 16 L, i.e. (row, chunk) = img_off^-1 of it
+  const __amdgpu_buffer_rsrc_t rk = head_rsrc(p.k + b * p.k_sb + hk * p.k_sh);
+  const __amdgpu_buffer_rsrc_t rv = head_rsrc(p.v + b * p.v_sb + hk * p.v_sh);
+  int kvo[PPW], vvo[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int byte = 1024 * (wave * PPW + i) + 16 * lane;
+    const int rg = byte / (16 * D), rem = byte % (16 * D);
+    const int chh = rem / 512, w5 = rem % 512;
+    const int row = rg * 8 + w5 / 64;
+    const int ch = chh * 4 + (((w5 % 64) / 16) ^ ((row >> 2) & 3));
+    kvo[i] = (int)(((long long)row * p.k_st + ch * 8) * 2);
+    vvo[i] = (int)(((long long)row * p.v_st + ch * 8) * 2);
+  }
+  typedef __attribute__((address_space(3))) char lds_char;
+  lds_char* lsm = (lds_char*)smem;
+  auto issue = [&](int tile, int buf) {
+    const int kt = min(tile, ntiles - 1);  // clamped: the last tiles re-load a tile nobody reads
+    const int sok = __builtin_amdgcn_readfirstlane(kt * BN * (int)p.k_st * 2);
+    const int sov = __builtin_amdgcn_readfirstlane(kt * BN * (int)p.v_st * 2);
+#if defined(__HIP_DEVICE_COMPILE__)  // (the host pass drops the launch stub over this builtin)
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (void __attribute__((address_space(3)))*)(
+          lsm + buf * STAGE + 1024 * (wave * PPW + i)), 16, kvo[i], sok, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (void __attribute__((address_space(3)))*)(
+          lsm + buf * STAGE + TILE + 1024 * (wave * PPW + i)), 16, vvo[i], sov, 0, 0);
+    }
+#endif
+  };
+
+  f32x16 oacc[D / 32];
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) oacc[i][r] = 0.f;
+  float m = 0.f, lsum = 0.f;
+
+  // per-lane LDS read bases (bytes, relative to a stage)
+  const unsigned sbase = (unsigned)(size_t)lsm;
+  const int xr = (l32 >> 2) & 3;
+  const unsigned kb_e = (l32 >> 3) * 16 * D + 64 * (l32 & 7) + 16 * (hh ^ xr);
+  const unsigned kb_o = (l32 >> 3) * 16 * D + 64 * (l32 & 7) + 16 * ((2 + hh) ^ xr);
+  const int gi = lane & 15;
+  const int c3 = 2 * ((lane >> 4) & 1) + ((gi & 3) >> 1);
+  const unsigned vb_1 = TILE + 64 * (4 * hh + (gi >> 2)) + 16 * (c3 ^ hh) + 8 * (gi & 1);
+  const unsigned vb_2 = TILE + 16 * D + 64 * (4 * hh + (gi >> 2)) + 16 * (c3 ^ hh ^ 2) + 8 * (gi & 1);
+
+  ASTAMP_DECL
+#pragma unroll
+  for (int t = 0; t < LEAD; ++t) issue(t, t);
+
+  bf16x8 pf0, pf1;  // P^T of the tile whose PV is pending
+  // S^T = K.Q^T of tile t (K row fragments two k-steps ahead of their MFMA), softmax into pf0/pf1
+  auto sm_part = [&](int buf, auto masked, auto first, int t) {
+    constexpr bool MASKED = decltype(masked)::value, FIRST = decltype(first)::value;
+    const unsigned st0 = sbase + buf * STAGE;
+    const unsigned ke = st0 + kb_e, ko = st0 + kb_o;
+    f32x16 sa;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sa[r] = 0.f;
+    u32x4 fk[3];
+    fk[0] = ads_b128<0>(ke);
+    fk[1] = ads_b128<0>(ko);
+    static_for<0, KS>([&](auto S_) {
+      constexpr int s = decltype(S_)::value;
+      if constexpr (s + 2 < KS) fk[(s + 2) % 3] = ads_b128<512 * ((s + 2) >> 1)>(((s + 2) & 1) ? ko : ke);
+      constexpr int after = (s + 2 < KS) ? 2 : (KS - 1 - s);
+      lgkm_wait<after>(fk[s % 3]);
+      sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(fk[s % 3]), qf[s], sa, 0, 0, 0);
+    });
+    ASTAMP(3);
+    if constexpr (MASKED) {
+      const int lim = qrow + off - t * BN - 4 * hh;
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if ((r & 3) + 8 * (r >> 2) > lim) sa[r] = -INFINITY;
+    }
+    if constexpr (FIRST) {  // reference max = the first tile's row max (see attn_fwd_tiled_kernel)
+      float mt = sa[0];
+#pragma unroll
+      for (int r = 1; r < 16; ++r) mt = fmaxf(mt, sa[r]);
+      m = fmaxf(mt, __shfl_xor(mt, 32, 64)) * sl2;
+    }
+    const float nm = -m;
+    float ps = 0.f;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const float e0 = __builtin_amdgcn_exp2f(fmaf(sa[r], sl2, nm));
+      const float e1 = __builtin_amdgcn_exp2f(fmaf(sa[r + 8], sl2, nm));
+      ps += e0 + e1;
+      pf0[r] = (__bf16)e0;
+      pf1[r] = (__bf16)e1;
+    }
+    lsum += ps;
+    ASTAMP(4);
+  };
+  // O^T += V^T.P^T of the tile in `buf`: the V^T reads of d-block db+1 in flight under block db's MFMAs
+  auto pv_part = [&](int buf) {
+    const unsigned st0 = sbase + buf * STAGE;
+    const unsigned v1 = st0 + vb_1, v2 = st0 + vb_2;
+    u32x2 va0 = ads_tr<0>(v1), va1 = ads_tr<0>(v2);
+    u32x2 vb0 = ads_tr<2 * 16 * D>(v1), vb1 = ads_tr<2 * 16 * D>(v2);
+    static_for<0, D / 32>([&](auto DB_) {
+      constexpr int db = decltype(DB_)::value;
+      u32x2 na0, na1, nb0, nb1;
+      if constexpr (db + 1 < D / 32) {
+        na0 = ads_tr<512 * (db + 1)>(v1);
+        na1 = ads_tr<512 * (db + 1)>(v2);
+        nb0 = ads_tr<2 * 16 * D + 512 * (db + 1)>(v1);
+        nb1 = ads_tr<2 * 16 * D + 512 * (db + 1)>(v2);
+        lgkm_wait<4>(va0, va1, vb0, vb1);
+      } else {
+        lgkm_wait<0>(va0, va1, vb0, vb1);
+      }
+      oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(va0, va1), pf0, oacc[db], 0, 0, 0);
+      oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(vb0, vb1), pf1, oacc[db], 0, 0, 0);
+      if constexpr (db + 1 < D / 32) {
+        va0 = na0; va1 = na1; vb0 = nb0; vb1 = nb1;
+      }
+    });
+    ASTAMP(5);
+  };
+
+  // Staggered halves (ping-pong): after each barrier waves 0-3 run S -> softmax -> PV of tile t
+  // while waves 4-7 (their SIMD partners) run PV of tile t-1, then S -> softmax of tile t. The two
+  // waves of a SIMD never sit in their softmax (VALU, no MFMA) at the same time: one barrier per
+  // tile kept them in lock step -- both in softmax, the matrix pipe idle.
+  // Tile t: wait for this wave's pieces of tile t, barrier (every piece landed; every wave done with
+  // tile t-2, whose buffer the lagging half read last), refill that buffer with tile t+NBUF-2.
+  const bool lag = STAGGER && wave >= NW / 2;
+  auto sync_issue = [&](int t) {
+    ASTAMP(0);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INFLIGHT) : "memory");
+    __builtin_amdgcn_s_barrier();
+    ASTAMP(1);
+    issue(t + LEAD, (t + LEAD) % NBUF);
+    ASTAMP(2);
+  };
+  // causal: the mask is applied on every tile (16 selects that change nothing before the diagonal):
+  // separate masked / mask-free bodies made hipcc spill ~170 registers
+  sync_issue(0);
+  sm_part(0, std::integral_constant<bool, CAUSAL>{}, std::true_type{}, 0);
+  if (!lag) pv_part(0);
+  for (int t = 1; t < ntiles; ++t) {
+    sync_issue(t);
+    if (lag && t - 1 < mytiles) pv_part((t - 1) % NBUF);
+    if (t < mytiles) {
+      sm_part(t % NBUF, std::integral_constant<bool, CAUSAL>{}, std::false_type{}, t);
+      if (!lag) pv_part(t % NBUF);
+    }
+  }
+  if (lag && ntiles - 1 < mytiles) pv_part((ntiles - 1) % NBUF);
+
+  const float ltot = lsum + __shfl_xor(lsum, 32, 64);
+  const bool bad = !(ltot < 1.2676506e30f);
+  const int any_bad = __any(bad);
+  // overflow flags in the 4-wave kernel's layout (4 per 128-row block, lid order of the generic fixup)
+  {
+    const int nqb128 = p.Sq / 128, qb128 = q0 / 128, w128 = (q0 % 128) / 32;
+    const int lid128 = bh * nqb128 + (CAUSAL ? nqb128 - 1 - qb128 : qb128);
+    if (lane == 0) p.flags[lid128 * 4 + w128] = any_bad;
+  }
+  const float inv = ltot > 0.f ? 1.f / ltot : 0.f;
+  if (hh == 0 && p.lse)
+    p.lse[((long long)b * p.H + h) * p.Sq + qrow] = ltot > 0.f ? (m + log2f(ltot)) * kLn2 : INFINITY;
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // the clamped tail DMAs
+  __syncthreads();  // the tile buffers become the epilogue images
+  store_tile_lds<D, D>(p.o + b * p.o_sb + h * p.o_sh + (long long)q0 * p.o_st, p.o_st, oacc, lane, inv,
+                       smem + wave * 32 * D * 2);
+  ASTAMP(6);
+  ASTAMP_FLUSH(48);
+}
+
 // ====================================================================== backward
 // Same image and fragment conventions as the forward. Two kernels, no float
 // atomics, deterministic:
@@ -977,6 +1262,13 @@ inline bool offsets_fit(long long rows, long long stride) { return (rows + 128) 
 
 }  // namespace
 
+// A/B knob for the full-tile kernels: bit 0 = 8-wave D = 256 forward (attn_fwd_w8_kernel).
+static int g_attn_variant = 1;
+KCA_API int kca_attn_set_variant(int v) {
+  g_attn_variant = v;
+  return 0;
+}
+
 // Returns 0 when launched, 1 when the shape is outside the fast path (the
 // caller then uses the generic kernel).
 KCA_API int kca_attn_fwd_tiled(const void* q, const void* k, const void* v, void* o, float* lse,
@@ -998,7 +1290,11 @@ KCA_API int kca_attn_fwd_tiled(const void* q, const void* k, const void* v, void
                   B, Sq, Sk, H, Hkv, scale};
   dim3 grid((Sq / 128) * B * H);
   (void)hipGetLastError();
-  if (d == 256) {
+  if (d == 256 && (g_attn_variant & 1) && Sq % 256 == 0) {
+    dim3 g8((Sq / 256) * B * H);
+    if (causal) hipLaunchKernelGGL((attn_fwd_w8_kernel<256, true>), g8, dim3(512), 0, stream, p);
+    else hipLaunchKernelGGL((attn_fwd_w8_kernel<256, false>), g8, dim3(512), 0, stream, p);
+  } else if (d == 256) {
     if (causal) hipLaunchKernelGGL((attn_fwd_tiled_kernel<256, true>), grid, dim3(256), 0, stream, p);
     else hipLaunchKernelGGL((attn_fwd_tiled_kernel<256, false>), grid, dim3(256), 0, stream, p);
   } else if (d == 160) {  // SD-1.5 1280-channel heads

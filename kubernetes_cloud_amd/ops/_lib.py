@@ -63,6 +63,7 @@ _SIGS = {
     "kca_attn_bwd_preprocess": [P, P, P, LL, LL, LL, LL, LL, LL, I, I, I, I, P],
     "kca_attn_bwd": [P] * 10 + [LL] * 21 + [I] * 7 + [F, P, P, I, P, P],
     "kca_attn_set_tiled": [I],
+    "kca_attn_set_variant": [I],
     "kca_transpose_bf16": [P, LL, P, LL, I, I, P],
     "kca_gelu_fwd_t": [P, LL, P, LL, P, LL, I, I, I, P],
     "kca_gelu_bwd_t": [P, LL, P, LL, P, LL, P, LL, P, I, I, I, P],

@@ -71,6 +71,17 @@ def set_tiled_path(enable: bool) -> None:
     _lib.call("kca_attn_set_tiled", int(bool(enable)))
 
 
+_VARIANT = [1]
+
+
+def set_variant(v: int) -> int:
+    """Full-tile kernel variants (A/B knob, attention_tiled.hip): bit 0 = the 8-wave D = 256
+    forward (default on). Returns the previous value."""
+    _lib.call("kca_attn_set_variant", int(v))
+    old, _VARIANT[0] = _VARIANT[0], int(v)
+    return old
+
+
 def _strides(t):
     return t.stride(0), t.stride(1), t.stride(2)
 

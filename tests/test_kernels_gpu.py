@@ -824,3 +824,26 @@ def test_accum_grad_multi_matches_reference():
     _lib.call("kca_accum_grad_multi", tail.ctypes.data, len(rows) - 3, 0.5, _lib.stream())
     torch.cuda.synchronize()
     assert torch.allclose(flat, ref, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("causal", [True, False])
+def test_attention_w8_forward_matches_4wave_and_fp32(causal):
+    """The 8-wave D = 256 forward (LDS-DMA staging, 256-row blocks, asm LDS reads; bit 0 of
+    kca_attn_set_variant) against the 4-wave kernel and an fp32 reference, on a GPT-J-like
+    shape with several 256-row blocks per head (causal skips, diagonal masks, the clamped
+    tail DMAs)."""
+    from kubernetes_cloud_amd.ops.attention import set_variant
+    torch.manual_seed(11)
+    B, S, H, D = 2, 1024, 3, 256
+    q, k, v = (torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16) for _ in range(3))
+    outs = {}
+    for var in (1, 0):
+        old = set_variant(var)
+        try:
+            with torch.no_grad():
+                outs[var] = ops.flash_attention(q, k, v, causal=causal).float()
+        finally:
+            set_variant(old)
+    orf, _ = ops.attention_reference(q.float(), k.float(), v.float(), causal)
+    assert _rel(outs[1], orf) < 1e-2, _rel(outs[1], orf)
+    assert _rel(outs[1], outs[0]) < 5e-3, _rel(outs[1], outs[0])

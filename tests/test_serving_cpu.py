@@ -301,3 +301,25 @@ def test_dalle_mini_predictor_png_params_and_kv_cache(tmp_path):
     assert torch.allclose(full, step, atol=1e-4)
     (tmp_path / ".ready.txt").write_text("ok")
     wait_ready(str(tmp_path), 1, interval=0.01)
+
+
+def test_serving_bench_http_and_engine_levels_cpu(tmp_path):
+    """bench/serving_bench.py (bench.py secondary_serving) end to end on CPU with shrunk models:
+    .tensors write -> GPTJPredictor tensorizer load -> uvicorn V1 server -> loadgen at two
+    concurrency levels, plus the same requests straight into predict (engine)."""
+    import importlib.util
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("kca_serving_bench", os.path.join(root, "bench", "serving_bench.py"))
+    sb = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(sb)
+    lv = ((1, 2), (4, 4))
+    g = sb.run_gptj(str(tmp_path), levels=lv, overrides=dict(n_embd=64, n_layer=2, n_head=4, rotary_dim=8,
+                                                            vocab_size=512, n_positions=128))
+    assert [r["concurrency"] for r in g["levels"]] == [1, 4]
+    for r in g["levels"]:
+        assert r["successes"] == r["requests"] and r["http_rps"] > 0 and r["engine_rps"] > 0
+        assert "http_tokens_per_s" in r and "http_overhead_p50_ms" in r
+    assert not os.listdir(tmp_path)  # model dir and .tensors removed
+    b = sb.run_bloom_slice(layers=2, levels=lv, overrides=dict(hidden_size=64, n_head=4, vocab_size=512))
+    assert all(r["successes"] == r["requests"] for r in b["levels"]) and "proxy" in b

@@ -33,6 +33,7 @@ from collections import defaultdict
 # kernel-name regex -> (case in bench/kernel_pmc.py, FLOP key or None, byte key or None)
 CASE_OF = [
     (r"attn_fwd_tiled_kernel<256", "attn_gptj", "fwd_flops", None),
+    (r"attn_fwd_w8_kernel<256", "attn_gptj", "fwd_flops", None),
     (r"attn_bwd_dq_tiled_kernel<256", "attn_gptj", "bwd_flops_dq", None),
     (r"attn_bwd_dkdv_tiled_kernel<256", "attn_gptj", "bwd_flops_dkdv", None),
     (r"attn_fwd_kernel<64, false>", "attn_sd64", "fwd_flops", None),
