@@ -578,7 +578,7 @@ __global__ void __launch_bounds__(256, (D <= 128 ? 2 : 1)) attn_fwd_tiled_kernel
 // The price is the register file: at two waves per SIMD a wave has 256 registers, and O^T (128),
 // the Q^T fragments (D/4 = 64) and one S tile (16) leave no room for register-staged K/V tiles. So
 // the tiles arrive by LDS-DMA (buffer_load ... lds: no VGPR destination), four buffers deep, issued
-// two tiles ahead, one barrier per tile after a COUNTED vmcnt. hipcc drains every LDS-DMA
+// three tiles ahead, one barrier per tile after a COUNTED vmcnt. hipcc drains every LDS-DMA
 // (vmcnt(0)) before any LDS read it can see, so the loop's LDS reads (K rows: ds_read_b128; V^T:
 // ds_read_b64_tr_b16) are inline asm with hand-counted lgkmcnt waits, each wait tied to the
 // fragment it retires ("+v") so no MFMA can be scheduled above it.
@@ -640,12 +640,7 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_w8_kernel(FastFwdParams p) {
   constexpr int KS = D / 16;
   constexpr int PIECES = TILE / 1024;         // 1-KiB LDS-DMA pieces per image
   constexpr int PPW = PIECES / NW;            // per wave per image
-#ifdef KCA_W8_NOSTAGGER  // A/B arm: both halves in lock step (S -> softmax -> PV), tiles issued 3 ahead
-  constexpr bool STAGGER = false;
-#else
-  constexpr bool STAGGER = true;
-#endif
-  constexpr int LEAD = STAGGER ? NBUF - 2 : NBUF - 1;    // tiles issued ahead of the one computed
+  constexpr int LEAD = NBUF - 1;                  // tiles issued ahead of the one computed
   constexpr int INFLIGHT = (LEAD - 1) * 2 * PPW;  // DMA instructions issued after tile t when t is waited
   static_assert(D == 256 || D == 128, "8-wave forward: D = 128 / 256");
   static_assert(PPW >= 1 && PIECES % NW == 0, "whole pieces per wave");
@@ -731,10 +726,10 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_w8_kernel(FastFwdParams p) {
 #pragma unroll
   for (int t = 0; t < LEAD; ++t) issue(t, t);
 
-  bf16x8 pf0, pf1;  // P^T of the tile whose PV is pending
+  bf16x8 pf0, pf1;  // P^T of the tile in flight (softmax -> PV)
   // S^T = K.Q^T of tile t (K row fragments two k-steps ahead of their MFMA), softmax into pf0/pf1
-  auto sm_part = [&](int buf, auto masked, auto first, int t) {
-    constexpr bool MASKED = decltype(masked)::value, FIRST = decltype(first)::value;
+  auto sm_part = [&](int buf, auto masked, int t) {
+    constexpr bool MASKED = decltype(masked)::value;
     const unsigned st0 = sbase + buf * STAGE;
     const unsigned ke = st0 + kb_e, ko = st0 + kb_o;
     f32x16 sa;
@@ -757,7 +752,7 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_w8_kernel(FastFwdParams p) {
       for (int r = 0; r < 16; ++r)
         if ((r & 3) + 8 * (r >> 2) > lim) sa[r] = -INFINITY;
     }
-    if constexpr (FIRST) {  // reference max = the first tile's row max (see attn_fwd_tiled_kernel)
+    if (t == 0) {  // reference max = the first tile's row max (see attn_fwd_tiled_kernel)
       float mt = sa[0];
 #pragma unroll
       for (int r = 1; r < 16; ++r) mt = fmaxf(mt, sa[r]);
@@ -803,13 +798,11 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_w8_kernel(FastFwdParams p) {
     ASTAMP(5);
   };
 
-  // Staggered halves (ping-pong): after each barrier waves 0-3 run S -> softmax -> PV of tile t
-  // while waves 4-7 (their SIMD partners) run PV of tile t-1, then S -> softmax of tile t. The two
-  // waves of a SIMD never sit in their softmax (VALU, no MFMA) at the same time: one barrier per
-  // tile kept them in lock step -- both in softmax, the matrix pipe idle.
-  // Tile t: wait for this wave's pieces of tile t, barrier (every piece landed; every wave done with
-  // tile t-2, whose buffer the lagging half read last), refill that buffer with tile t+NBUF-2.
-  const bool lag = STAGGER && wave >= NW / 2;
+  // Tile t: wait for this wave's pieces of tile t (INFLIGHT younger DMA instructions may remain),
+  // barrier (every piece landed; every wave done with tile t-1), refill tile t-1's buffer with tile
+  // t+LEAD, compute. Measured and not kept (same-box A/B, GPT-J fwd): a ping-pong schedule (waves 4-7
+  // one PV behind, so the two waves of a SIMD never sit in softmax together; two tiles ahead) 5 %
+  // slower; two tiles per barrier (vmcnt(0), one superstep ahead) 3-5 % slower.
   auto sync_issue = [&](int t) {
     ASTAMP(0);
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INFLIGHT) : "memory");
@@ -820,18 +813,14 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_w8_kernel(FastFwdParams p) {
   };
   // causal: the mask is applied on every tile (16 selects that change nothing before the diagonal):
   // separate masked / mask-free bodies made hipcc spill ~170 registers
-  sync_issue(0);
-  sm_part(0, std::integral_constant<bool, CAUSAL>{}, std::true_type{}, 0);
-  if (!lag) pv_part(0);
-  for (int t = 1; t < ntiles; ++t) {
+  constexpr auto CM = std::integral_constant<bool, CAUSAL>{};
+  for (int t = 0; t < ntiles; ++t) {
     sync_issue(t);
-    if (lag && t - 1 < mytiles) pv_part((t - 1) % NBUF);
     if (t < mytiles) {
-      sm_part(t % NBUF, std::integral_constant<bool, CAUSAL>{}, std::false_type{}, t);
-      if (!lag) pv_part(t % NBUF);
+      sm_part(t % NBUF, CM, t);
+      pv_part(t % NBUF);
     }
   }
-  if (lag && ntiles - 1 < mytiles) pv_part((ntiles - 1) % NBUF);
 
   const float ltot = lsum + __shfl_xor(lsum, 32, 64);
   const bool bad = !(ltot < 1.2676506e30f);
@@ -1263,6 +1252,8 @@ inline bool offsets_fit(long long rows, long long stride) { return (rows + 128) 
 }  // namespace
 
 // A/B knob for the full-tile kernels: bit 0 = 8-wave D = 256 forward (attn_fwd_w8_kernel).
+// (An LDS-DMA dQ kernel -- four buffers, three K/V tiles in flight, asm LDS reads -- measured
+// 1.5-2.5 % slower on GPT-J fwd+bwd than the register-staged one and was dropped.)
 static int g_attn_variant = 1;
 KCA_API int kca_attn_set_variant(int v) {
   g_attn_variant = v;

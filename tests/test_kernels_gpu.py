@@ -847,3 +847,4 @@ def test_attention_w8_forward_matches_4wave_and_fp32(causal):
     orf, _ = ops.attention_reference(q.float(), k.float(), v.float(), causal)
     assert _rel(outs[1], orf) < 1e-2, _rel(outs[1], orf)
     assert _rel(outs[1], outs[0]) < 5e-3, _rel(outs[1], outs[0])
+
