@@ -22,10 +22,18 @@ on this stack:
   ch 128, ch_mult (1, 1, 2, 2, 4), 2 res blocks, attention at 16x16) on the
   SD building blocks (fused GroupNorm+SiLU, channels-last convolutions).
 
-Weights: ``from_pretrained(dir)`` reads ``config.json`` (dalle-mini field names)
-and a PyTorch ``*.safetensors`` / ``*.bin`` state dict when present (the Flax
-msgpack checkpoints need a one-off conversion outside this image); otherwise
-the model is random-init for the given config (benchmarks, tests).
+Weights: ``load_dalle(dir)`` reads ``config.json`` (dalle-mini field names) and
+either the Flax checkpoint the reference's downloader fetches
+(``flax_model.msgpack``, decoded without JAX by ``io/flax_msgpack.py`` and
+mapped onto these modules by ``dalle_from_flax`` / ``vqgan_from_flax``: Dense
+kernels [in, out] -> Linear weights, Conv kernels [kh, kw, in, out] -> OIHW,
+LayerNorm/GroupNorm ``scale`` -> weight, scanned (stacked) or per-layer
+DalleBart layouts) or a PyTorch ``*.safetensors`` / ``*.bin`` state dict;
+otherwise the model is random-init for the given config (benchmarks, tests).
+The Flax names follow dalle-mini's modeling code (auto-named ``LayerNorm_k`` /
+``FlaxBartAttention_k`` / ``GLU_0`` sub-modules) and vqgan-jax's; no released
+checkpoint is in the tree, so parity with the published files is unpinned --
+unmatched names are reported, not guessed.
 """
 from __future__ import annotations
 
@@ -332,7 +340,242 @@ class VQGANDecoder(nn.Module):
         return ((x.float() + 1.0) / 2.0).clamp(0.0, 1.0)
 
 
+# ------------------------------------------------------------- Flax checkpoints
+def _dalle_flax_names(c: DalleBartConfig):
+    """(our key prefix, Flax path, kind) for every DalleBart tensor; kind: dense (kernel, transposed),
+    embed, ln (scale/bias). Layer paths use '{L}' for the per-layer part (layers/{i} or scanned)."""
+    out = [("embed_tokens", "model/encoder/embed_tokens", "embed"),
+           ("embed_positions", "model/encoder/embed_positions", "embed"),
+           ("layernorm_embedding", "model/encoder/layernorm_embedding", "ln"),
+           ("encoder_final_ln", "model/encoder/final_ln", "ln"),
+           ("dec_embed_tokens", "model/decoder/embed_tokens", "embed"),
+           ("dec_embed_positions", "model/decoder/embed_positions", "embed"),
+           ("dec_layernorm_embedding", "model/decoder/layernorm_embedding", "ln"),
+           ("decoder_final_ln", "model/decoder/final_ln", "ln"),
+           ("lm_head", "lm_head", "dense")]
+    glu = [("glu.ln0", "GLU_0/LayerNorm_0", "ln"), ("glu.fc0", "GLU_0/Dense_0", "dense"),
+           ("glu.fc1", "GLU_0/Dense_1", "dense"), ("glu.ln1", "GLU_0/LayerNorm_1", "ln"),
+           ("glu.fc2", "GLU_0/Dense_2", "dense")]
+
+    def attn(ours, flax):
+        return [(f"{ours}.{n}", f"{flax}/{n}", "dense") for n in ("q_proj", "k_proj", "v_proj", "out_proj")]
+    enc = [("pre_self_attn_layer_norm", "LayerNorm_0", "ln"), *attn("self_attn", "FlaxBartAttention_0"),
+           ("self_attn_layer_norm", "LayerNorm_1", "ln"), *glu]
+    dec = [("pre_self_attn_layer_norm", "LayerNorm_0", "ln"), *attn("self_attn", "FlaxBartAttention_0"),
+           ("self_attn_layer_norm", "LayerNorm_1", "ln"), ("pre_encoder_attn_layer_norm", "LayerNorm_2", "ln"),
+           *attn("encoder_attn", "FlaxBartAttention_1"), ("encoder_attn_layer_norm", "LayerNorm_3", "ln"), *glu]
+    layers = [("encoder_layers", "model/encoder/layers", "FlaxBartEncoderLayers", c.encoder_layers, enc),
+              ("decoder_layers", "model/decoder/layers", "FlaxBartDecoderLayers", c.decoder_layers, dec)]
+    return out, layers
+
+
+def _flax_get(flat: dict, path: str, kind: str, layer: int | None = None, stacked: bool = False):
+    """{'weight': t, 'bias': t?} of one module from a flat Flax dict (None when absent)."""
+    def g(name):
+        t = flat.get(f"{path}/{name}")
+        if t is not None and stacked:
+            t = t[layer]
+        return t
+    if kind == "embed":
+        t = g("embedding")
+        return None if t is None else {"weight": t}
+    if kind == "dense":
+        t = g("kernel")
+        if t is None:
+            return None
+        d = {"weight": t.t().contiguous()}
+        b = g("bias")
+        if b is not None:
+            d["bias"] = b
+        return d
+    if kind == "conv":
+        t = g("kernel")
+        if t is None:
+            return None
+        d = {"weight": t.permute(3, 2, 0, 1).contiguous()}
+        b = g("bias")
+        if b is not None:
+            d["bias"] = b
+        return d
+    sc, b = g("scale"), g("bias")  # ln / gn: a norm built with use_scale=False has no scale
+    if sc is None and b is None:
+        return None
+    d = {}
+    if sc is not None:
+        d["weight"] = sc
+    if b is not None:
+        d["bias"] = b
+    return d
+
+
+def _strip_root(flat: dict) -> dict:
+    if flat and all(k.startswith("params/") for k in flat):
+        return {k[len("params/"):]: v for k, v in flat.items()}
+    return flat
+
+
+def dalle_from_flax(flat: dict, c: DalleBartConfig) -> tuple[dict, list]:
+    """Flax DalleBart params (flattened 'a/b/c' keys) -> (our state dict, unmatched Flax keys).
+    Per-layer ('layers/{i}/...') and scanned ('layers/FlaxBart{Encoder,Decoder}Layers/...', leading
+    layer axis) layouts; a final LayerNorm stored as the last layer's extra norm (LayerNorm_2 in an
+    encoder layer, LayerNorm_4 in a decoder layer) is accepted for ``final_ln``."""
+    flat = _strip_root(flat)
+    used: set = set()
+    sd: dict = {}
+
+    def put(ours, mod):
+        for k, v in mod.items():
+            sd[f"{ours}.{k}"] = v
+
+    def take(path, kind, ours, layer=None, stacked=False):
+        mod = _flax_get(flat, path, kind, layer, stacked)
+        if mod is not None:
+            put(ours, mod)
+            used.update(k for k in flat if k.startswith(path + "/"))
+        return mod is not None
+
+    top, layers = _dalle_flax_names(c)
+    for ours, path, kind in top:
+        if not take(path, kind, ours) and ours.endswith("final_ln"):
+            side = "encoder" if ours.startswith("encoder") else "decoder"
+            n = c.encoder_layers if side == "encoder" else c.decoder_layers
+            extra = "LayerNorm_2" if side == "encoder" else "LayerNorm_4"
+            if not take(f"model/{side}/layers/{n - 1}/{extra}", "ln", ours):
+                scan = f"model/{side}/layers/FlaxBart{side.capitalize()}Layers/{extra}"
+                take(scan, "ln", ours, n - 1, True)
+    for ours_root, root, scan_name, n, subs in layers:
+        stacked = any(k.startswith(f"{root}/{scan_name}/") for k in flat)
+        for i in range(n):
+            for ours, sub, kind in subs:
+                path = f"{root}/{scan_name}/{sub}" if stacked else f"{root}/{i}/{sub}"
+                take(path, kind, f"{ours_root}.{i}.{ours}", i, stacked)
+    return sd, sorted(k for k in flat if k not in used)
+
+
+def dalle_to_flax(model: "DalleBart", stacked: bool = False) -> dict:
+    """Our DalleBart -> flat Flax params in the layout ``dalle_from_flax`` reads (tests, exports)."""
+    c = model.config
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+
+    def vals(ours, kind):
+        w, b = sd.get(f"{ours}.weight"), sd.get(f"{ours}.bias")
+        if kind == "embed":
+            return {"embedding": w}
+        if kind == "dense":
+            return {"kernel": w.t().contiguous(), **({"bias": b} if b is not None else {})}
+        return {"scale": w, "bias": b}
+    flat = {}
+    top, layers = _dalle_flax_names(c)
+    for ours, path, kind in top:
+        for k, v in vals(ours, kind).items():
+            flat[f"{path}/{k}"] = v
+    for ours_root, root, scan_name, n, subs in layers:
+        for ours, sub, kind in subs:
+            per = [vals(f"{ours_root}.{i}.{ours}", kind) for i in range(n)]
+            for k in per[0]:
+                if stacked:
+                    flat[f"{root}/{scan_name}/{sub}/{k}"] = torch.stack([d[k] for d in per])
+                else:
+                    for i in range(n):
+                        flat[f"{root}/{i}/{sub}/{k}"] = per[i][k]
+    return flat
+
+
+def _vqgan_flax_names(m: "VQGANDecoder"):
+    """(our module prefix, Flax path, kind) for the vqgan-jax VQModel decoder side."""
+    c = m.config
+    out = [("embedding", "quantize/embedding", "embed"), ("post_quant_conv", "post_quant_conv", "conv"),
+           ("conv_in", "decoder/conv_in", "conv"), ("norm_out", "decoder/norm_out", "ln"),
+           ("conv_out", "decoder/conv_out", "conv")]
+
+    def res(ours, flax, has_sc):
+        r = [(f"{ours}.norm1", f"{flax}/norm1", "ln"), (f"{ours}.conv1", f"{flax}/conv1", "conv"),
+             (f"{ours}.norm2", f"{flax}/norm2", "ln"), (f"{ours}.conv2", f"{flax}/conv2", "conv")]
+        if has_sc:
+            r.append((f"{ours}.conv_shortcut", f"{flax}/nin_shortcut", "conv"))
+        return r
+
+    def att(ours, flax):
+        return [(f"{ours}.{n}", f"{flax}/{n}", "ln" if n == "norm" else "conv")
+                for n in ("norm", "q", "k", "v", "proj_out")]
+    out += res("mid.0", "decoder/mid/block_1", m.mid[0].conv_shortcut is not None)
+    out += att("mid.1", "decoder/mid/attn_1")
+    out += res("mid.2", "decoder/mid/block_2", m.mid[2].conv_shortcut is not None)
+    L = len(c.ch_mult)
+    for ui, blocks in enumerate(m.up):
+        lvl = L - 1 - ui  # our up[0] is the lowest resolution; vqgan-jax's up_{lvl} is indexed by level
+        j_res = j_att = 0
+        for bi, blk in enumerate(blocks):
+            ours = f"up.{ui}.{bi}"
+            if isinstance(blk, ResnetBlock2D):
+                out += res(ours, f"decoder/up_{lvl}/block_{j_res}", blk.conv_shortcut is not None)
+                j_res += 1
+            elif isinstance(blk, _VQAttn):
+                out += att(ours, f"decoder/up_{lvl}/attn_{j_att}")
+                j_att += 1
+            else:  # Upsample2D
+                out.append((f"{ours}.conv", f"decoder/up_{lvl}/upsample/conv", "conv"))
+    return out
+
+
+def vqgan_from_flax(flat: dict, m: "VQGANDecoder") -> tuple[dict, list]:
+    """Flax VQModel params -> (our VQGANDecoder state dict, unmatched Flax keys; the VQGAN
+    encoder / quant_conv halves are not used by decode_code and are reported there)."""
+    flat = _strip_root(flat)
+    sd, used = {}, set()
+    for ours, path, kind in _vqgan_flax_names(m):
+        mod = _flax_get(flat, path, kind)
+        if mod is not None:
+            for k, v in mod.items():
+                sd[f"{ours}.{k}"] = v
+            used.update(k for k in flat if k.startswith(path + "/"))
+    return sd, sorted(k for k in flat if k not in used)
+
+
+def vqgan_to_flax(m: "VQGANDecoder") -> dict:
+    sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    flat = {}
+    for ours, path, kind in _vqgan_flax_names(m):
+        w, b = sd[f"{ours}.weight"], sd.get(f"{ours}.bias")
+        if kind == "embed":
+            flat[f"{path}/embedding"] = w
+        elif kind == "conv":
+            flat[f"{path}/kernel"] = w.permute(2, 3, 1, 0).contiguous()
+            flat[f"{path}/bias"] = b
+        else:
+            flat[f"{path}/scale"], flat[f"{path}/bias"] = w, b
+    return flat
+
+
+def _load_flax(module: nn.Module, path: str) -> bool:
+    f = os.path.join(path, "flax_model.msgpack")
+    if not os.path.exists(f):
+        return False
+    from ..io import flax_msgpack
+    flat = flax_msgpack.flatten(flax_msgpack.read(f))
+    if isinstance(module, DalleBart):
+        sd, extra = dalle_from_flax(flat, module.config)
+    else:
+        sd, extra = vqgan_from_flax(flat, module)
+    import logging
+    log = logging.getLogger("kca.dalle")
+    own = module.state_dict()
+    for k, v in sd.items():  # norms saved without a scale keep their ones
+        if k in own:
+            own[k] = v.to(own[k].dtype).reshape(own[k].shape)
+    missing = [k for k in own if k not in sd]
+    if missing:
+        log.warning("%s: %d parameters not in the Flax checkpoint (kept as initialised), e.g. %s", f,
+                    len(missing), missing[:4])
+    if extra:
+        log.info("%s: %d Flax tensors unused (e.g. %s)", f, len(extra), extra[:4])
+    module.load_state_dict(own)
+    return True
+
+
 def _load_state(module: nn.Module, path: str) -> bool:
+    if _load_flax(module, path):
+        return True
     for name in ("model.safetensors", "pytorch_model.safetensors", "pytorch_model.bin", "model.bin"):
         f = os.path.join(path, name)
         if os.path.exists(f):
@@ -372,4 +615,5 @@ def load_dalle(path: str | None, device="cpu", dtype=torch.float32, config: Dall
     return model, vq
 
 
-__all__ = ["DalleBartConfig", "DalleBart", "VQGANConfig", "VQGANDecoder", "load_dalle", "sample_next"]
+__all__ = ["DalleBartConfig", "DalleBart", "VQGANConfig", "VQGANDecoder", "load_dalle", "sample_next",
+           "dalle_from_flax", "dalle_to_flax", "vqgan_from_flax", "vqgan_to_flax"]
