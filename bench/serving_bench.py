@@ -18,7 +18,7 @@ measures what a user of those services sees on one MI355X:
 
 For each level the same requests are also pushed through ``predict`` directly
 from a thread pool of the same width ("engine"): the difference is the HTTP
-layer (uvicorn + JSON + the loadgen client). Tokenizer: a small byte-level BPE
+layer (uvicorn + JSON + the loadgen client, which runs in its own process). Tokenizer: a small byte-level BPE
 trained in the run (no network for the GPT-2 vocabulary); prompt lengths are
 therefore ~1 token per byte, which moves only prefill.
 """
@@ -111,15 +111,29 @@ def _engine(pred, n: int, conc: int, seed: int = 0) -> dict:
             "p99_s": lat[int(0.99 * (n - 1))]}
 
 
+def _client(url: str, n: int, conc: int, model_name: str, seed: int) -> dict:
+    """serving/loadgen.py in its own process (as a client on another host would be): it does not
+    share the server's interpreter lock."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "kubernetes_cloud_amd.serving.loadgen", "--url", url, "--kserve", "--requests",
+           str(n), "--concurrency", str(conc), "--model-name", model_name, "--seed", str(seed), "--json", "-q"]
+    env = dict(os.environ, PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""),
+               CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=root)
+    if r.returncode != 0:
+        raise RuntimeError(f"loadgen failed: {r.stderr[-500:]}")
+    return json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+
+
 def _levels(pred, model_name: str, new_tokens: int | None, levels=LEVELS) -> list:
-    from kubernetes_cloud_amd.serving.loadgen import benchmark
     srv = _Server([pred])
     out = []
     try:
-        benchmark(srv.url, "kserve", 4, concurrency=4, model=model_name, seed=99)  # warm: graphs, allocator
+        _client(srv.url, 4, 4, model_name, 99)  # warm: graphs, allocator
         _engine(pred, 4, 4, seed=98)
         for conc, n in levels:
-            h = benchmark(srv.url, "kserve", n, concurrency=conc, model=model_name, seed=conc)
+            h = _client(srv.url, n, conc, model_name, conc)
             e = _engine(pred, n, conc, seed=conc)
             rec = {"concurrency": conc, "requests": n, "successes": h["successes"],
                    "http_rps": round(h["throughput_rps"], 3),

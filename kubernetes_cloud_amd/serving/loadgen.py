@@ -140,6 +140,7 @@ def main(argv=None):
     p.add_argument("--model-name", default="gptj")
     p.add_argument("--prompts-file", default="")
     p.add_argument("--json", action="store_true")
+    p.add_argument("--seed", type=int, default=0, help="prompt choice seed")
     p.add_argument("--verbose", "-v", dest="log_level", action="store_const", const=logging.INFO)
     p.add_argument("--quiet", "-q", dest="log_level", action="store_const", const=logging.ERROR)
     a = p.parse_args(argv)
@@ -150,7 +151,8 @@ def main(argv=None):
     if a.prompts_file:
         with open(a.prompts_file) as f:
             prompts = [ln.strip() for ln in f if ln.strip()]
-    r = benchmark(a.url, a.kind, a.requests, a.asynchronous, a.concurrency or None, a.model_name, prompts)
+    r = benchmark(a.url, a.kind, a.requests, a.asynchronous, a.concurrency or None, a.model_name, prompts,
+                  seed=a.seed)
     print(json.dumps(r)) if a.json else report(r)
     return r
 

@@ -104,14 +104,20 @@ class BloomPredictor(Model):
                 rp[k.upper()] = v
         return rp
 
-    def predict(self, request: dict, headers=None) -> dict:
+    def _gen_kwargs(self, request: dict) -> dict:
         if "instances" not in request:
             raise InvalidInput("request must contain 'instances'")
         rp = self.request_params(request)
-        return {"predictions": self.generator(
-            request["instances"], min_length=rp["MIN_LENGTH"], max_length=rp["MAX_LENGTH"],
-            temperature=rp["TEMPERATURE"], top_k=rp["TOP_K"], top_p=rp["TOP_P"],
-            repetition_penalty=rp["REPETITION_PENALTY"])}
+        return dict(min_length=rp["MIN_LENGTH"], max_length=rp["MAX_LENGTH"], temperature=rp["TEMPERATURE"],
+                    top_k=rp["TOP_K"], top_p=rp["TOP_P"], repetition_penalty=rp["REPETITION_PENALTY"])
+
+    def predict(self, request: dict, headers=None) -> dict:
+        kw = self._gen_kwargs(request)
+        return {"predictions": self.generator(request["instances"], **kw)}
+
+    async def apredict(self, request: dict, headers=None) -> dict:
+        kw = self._gen_kwargs(request)
+        return {"predictions": await self.generator.acall(request["instances"], **kw)}
 
 
 # ----------------------------------------------------------------- GPT-J
@@ -147,7 +153,7 @@ class GPTJPredictor(Model):
             0, max_new_tokens=50, do_sample=True, seed=self.seed + idx)])[0]
         return g.tokenizer.decode(r.prompt + r.output, skip_special_tokens=True)
 
-    def predict(self, payload: dict, headers=None) -> dict:
+    def _requests(self, payload: dict):
         if not isinstance(payload, dict):
             raise InvalidInput("Expected payload to be a dict")
         inputs = payload.get("instances") or ["Please input some text"]
@@ -155,8 +161,17 @@ class GPTJPredictor(Model):
         prompts = [g.tokenizer.encode(t) for t in inputs]
         params = [g.sampling_params(0, max_new_tokens=50, do_sample=True, seed=self.seed + i)
                   for i in range(len(prompts))]
-        reqs = g.generate_ids(prompts, params)
-        return {"predictions": [g.tokenizer.decode(r.prompt + r.output, skip_special_tokens=True) for r in reqs]}
+        return prompts, params
+
+    def _texts(self, reqs) -> dict:
+        tok = self.generator.tokenizer
+        return {"predictions": [tok.decode(r.prompt + r.output, skip_special_tokens=True) for r in reqs]}
+
+    def predict(self, payload: dict, headers=None) -> dict:
+        return self._texts(self.generator.generate_ids(*self._requests(payload)))
+
+    async def apredict(self, payload: dict, headers=None) -> dict:
+        return self._texts(await self.generator.agenerate_ids(*self._requests(payload)))
 
 
 def create_gptj_text_app(predictor: GPTJPredictor):

@@ -79,13 +79,21 @@ class Model:
         return r.json()
 
     async def __call__(self, payload, headers: dict | None = None):
+        """preprocess -> predict -> postprocess. A sync stage runs on the event loop's executor; the
+        base class's identity pre/postprocess are skipped, and a predictor with an async
+        ``apredict`` (the continuous-batching text predictors: submit to the engine, await its
+        future) holds no executor thread while it generates -- with every request parked in a
+        blocking ``predict``, 32 in flight exhausted the executor and queued the next requests'
+        pre/postprocess behind them (+143 ms p50 at concurrency 32, bench/serving_bench.py)."""
         async def run(fn, *a):
             if inspect.iscoroutinefunction(fn):
                 return await fn(*a)
             return await asyncio.get_running_loop().run_in_executor(None, lambda: fn(*a))
-        x = await run(self.preprocess, payload, headers)
-        y = await run(self.predict, x, headers)
-        return await run(self.postprocess, y, headers)
+        cls = type(self)
+        x = payload if cls.preprocess is Model.preprocess else await run(self.preprocess, payload, headers)
+        apredict = getattr(self, "apredict", None)
+        y = await apredict(x, headers) if apredict is not None else await run(self.predict, x, headers)
+        return y if cls.postprocess is Model.postprocess else await run(self.postprocess, y, headers)
 
 
 def parse_server_args(argv=None):

@@ -125,7 +125,16 @@ class TextGenerator:
         self.engine.run_until_done(reqs)
         return reqs
 
-    def __call__(self, text_inputs, return_full_text: bool = True, num_return_sequences: int = 1, **kw):
+    async def agenerate_ids(self, prompts: list[list[int]], params: list[SamplingParams]):
+        """``generate_ids`` for an event loop: the requests go to the background engine and the
+        caller awaits their futures (no thread blocked while they generate)."""
+        import asyncio
+        if not self.background:
+            return await asyncio.get_running_loop().run_in_executor(None, self.generate_ids, prompts, params)
+        futs = [self.engine.submit(p, sp) for p, sp in zip(prompts, params)]
+        return list(await asyncio.gather(*(asyncio.wrap_future(f) for f in futs)))
+
+    def _prepare(self, text_inputs, num_return_sequences: int = 1, **kw):
         single = isinstance(text_inputs, str)
         texts = [text_inputs] if single else list(text_inputs)
         tok = self.tokenizer
@@ -137,7 +146,10 @@ class TextGenerator:
                 prompts.append(ids)
                 s = None if seed is None else int(seed) + i * 1000 + j
                 params.append(self.sampling_params(len(ids), seed=s, **kw))
-        reqs = self.generate_ids(prompts, params)
+        return single, texts, enc, prompts, params
+
+    def _finish(self, reqs, single, texts, enc, return_full_text: bool, num_return_sequences: int):
+        tok = self.tokenizer
         out, k = [], 0
         for t, ids in zip(texts, enc):
             group = []
@@ -150,6 +162,16 @@ class TextGenerator:
                 group.append({"generated_text": (t + new) if return_full_text else new})
             out.append(group)
         return out[0] if single else out
+
+    def __call__(self, text_inputs, return_full_text: bool = True, num_return_sequences: int = 1, **kw):
+        single, texts, enc, prompts, params = self._prepare(text_inputs, num_return_sequences, **kw)
+        return self._finish(self.generate_ids(prompts, params), single, texts, enc, return_full_text,
+                            num_return_sequences)
+
+    async def acall(self, text_inputs, return_full_text: bool = True, num_return_sequences: int = 1, **kw):
+        single, texts, enc, prompts, params = self._prepare(text_inputs, num_return_sequences, **kw)
+        return self._finish(await self.agenerate_ids(prompts, params), single, texts, enc, return_full_text,
+                            num_return_sequences)
 
 
 __all__ = ["load_lm", "TextGenerator"]
