@@ -92,6 +92,7 @@ def run_tp_decode(model_name="bloom-176b", layers=0, batches=(1, 8, 32), prompt_
                         "tokens_per_s": round((sum(len(r.output) for r in reqs) - 2 * B) / dt, 1),
                         "layers": cfg.n_layers, "tp": world, "load_s": round(load_s, 1), "dtype": "bf16",
                         "custom_allreduce": ar is not None, "ctrl": chan.kind if chan is not None else None,
+                        "pipelined": bool(eng.pipeline),
                         "data": "random-init weights"})
         if world > 1:
             run.shutdown()

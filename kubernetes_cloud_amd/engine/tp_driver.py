@@ -27,7 +27,11 @@ def as_channel(ctrl):
 
 
 class CollectiveRunner:
-    pipelined = False  # every call is mirrored to the followers: no decode_async lookahead
+    # decode_async is mirrored too: rank 0 publishes step t+1 (rows chaining their input token from
+    # step t on the device) before it reads step t, and the followers replay the same chain, so TP
+    # decode gets the engine's one-step lookahead (the host's pickling / channel hop / scheduling
+    # overlaps the GPU's step instead of sitting between steps)
+    pipelined = True
 
     def __init__(self, runner, ctrl=None):
         self.runner = runner
@@ -52,6 +56,10 @@ class CollectiveRunner:
     def decode(self, rows):
         self._send(("decode", rows))
         return self.runner.decode(rows)
+
+    def decode_async(self, rows, prev=None):
+        self._send(("decode_async", rows, prev is not None))
+        return self.runner.decode_async(rows, prev=prev)
 
     # beam search (engine.beam): scoring pass, cache re-order, and page release in lock step
     def decode_topk(self, tokens, positions, slots, k):
@@ -81,6 +89,7 @@ def follower_loop(runner, ctrl=None):
     """Ranks > 0: mirror rank 0's runner calls until it sends ``stop``."""
     chan = as_channel(ctrl)
     last_logits = None
+    prev = older = None  # the last two decode_async handles (their chained tokens stay on the device)
     while True:
         obj = [chan.recv()]
         op = obj[0][0]
@@ -93,6 +102,13 @@ def follower_loop(runner, ctrl=None):
             runner.sample_first(last_logits, obj[0][1])
         elif op == "decode":
             runner.decode(obj[0][1])
+        elif op == "decode_async":
+            # at most one step ahead of the GPU, as rank 0's engine (it reads step t before launching
+            # t+2): step t+2 reuses step t's pinned upload / download buffers
+            if older is not None and older.event is not None:
+                older.event.synchronize()
+            h = runner.decode_async(obj[0][1], prev=prev if obj[0][2] else None)
+            older, prev = prev, h
         elif op == "decode_topk":
             runner.decode_topk(*obj[0][1:])
         elif op == "copy_slots":

@@ -52,6 +52,11 @@ def init_distributed(backend: str | None = None, timeout_s: int = 1800) -> DistI
     global _INFO
     rank, local, world = env_world()
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    from . import shared_gpu
+    shared = shared_gpu.enabled() and torch.cuda.is_available()
+    if shared:  # rehearsal: every rank on cuda:0, gloo, device collectives staged through the host
+        torch.cuda.set_device(0)
+        backend = "gloo"
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     if torch.cuda.is_available() and backend == "nccl":
@@ -63,6 +68,8 @@ def init_distributed(backend: str | None = None, timeout_s: int = 1800) -> DistI
         if backend == "nccl":
             kw["device_id"] = torch.device("cuda", torch.cuda.current_device())
         dist.init_process_group(backend=backend, timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    if shared and world > 1:
+        shared_gpu.install()
     _INFO = DistInfo(rank=rank, local_rank=local, world_size=world,
                      backend=backend if world > 1 else "none")
     return _INFO

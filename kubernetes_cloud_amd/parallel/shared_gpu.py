@@ -11,6 +11,12 @@ tensors through host copies (gloo's device paths do not cover every
 collective the engine uses; the host path covers all of them). The custom xGMI kernels need no change: two processes
 on one device map each other's IPC buffers the same way as two devices do.
 
+Point-to-point traffic (``batch_isend_irecv`` of the pipeline stages and of
+Adasum's recursive doubling, ``send`` / ``recv``) is staged the same way; the
+``isend`` / ``irecv`` functions themselves stay the originals, because
+``dist.P2POp`` accepts only those. ``parallel.dist.init_distributed`` enters
+this mode for every entry point (trainers, servers) when the env var is set.
+
 Never used by production runs: everything here is a no-op unless
 ``install()`` is called, which only ``bench.py`` (under the env var) and the
 GPU rehearsal tests do. Only the call sites that go through the ``dist``
@@ -32,13 +38,48 @@ def enabled() -> bool:
 
 
 class _Done:
-    """Completed ``Work`` stand-in for ``async_op=True`` callers."""
+    """Completed ``Work`` stand-in for ``async_op=True`` callers (``get_future`` as DDP comm hooks
+    use it: resolves to ``[result]``)."""
+
+    def __init__(self, result=None):
+        self._result = result
 
     def wait(self, *a, **k):
         return True
 
     def is_completed(self):
         return True
+
+    def get_future(self):
+        f = torch.futures.Future()
+        f.set_result([self._result])
+        return f
+
+
+class _Recv:
+    """A host-staged receive: ``wait`` completes the gloo receive, then copies into the device tensor."""
+
+    def __init__(self, work, host, dst):
+        self.work, self.host, self.dst = work, host, dst
+
+    def wait(self, *a, **k):
+        self.work.wait()
+        self.dst.copy_(self.host)
+        return True
+
+    def is_completed(self):
+        return self.work.is_completed()
+
+
+class _Send:
+    def __init__(self, work, host):
+        self.work, self.host = work, host  # the host copy lives until the send completes
+
+    def wait(self, *a, **k):
+        return self.work.wait()
+
+    def is_completed(self):
+        return self.work.is_completed()
 
 
 def _staged(t: torch.Tensor, force: bool) -> bool:
@@ -50,12 +91,14 @@ def install(force: bool = False):
     ``force``: stage CPU tensors too (CPU tests of the staging logic)."""
     if _ORIG:
         return
-    names = ("all_reduce", "reduce_scatter_tensor", "all_gather_into_tensor", "broadcast", "all_gather")
+    names = ("all_reduce", "reduce_scatter_tensor", "all_gather_into_tensor", "broadcast", "all_gather",
+             "batch_isend_irecv", "send", "recv")
     for n in names:
         _ORIG[n] = getattr(dist, n)
+    _ORIG["isend"], _ORIG["irecv"] = dist.isend, dist.irecv
 
-    def _ret(async_op):
-        return _Done() if async_op else None
+    def _ret(async_op, result=None):
+        return _Done(result) if async_op else None
 
     def all_reduce(tensor, op=dist.ReduceOp.SUM, group=None, async_op=False):
         if not _staged(tensor, force):
@@ -63,7 +106,37 @@ def install(force: bool = False):
         h = tensor.detach().to("cpu", copy=True)
         _ORIG["all_reduce"](h, op=op, group=group)
         tensor.copy_(h)
-        return _ret(async_op)
+        return _ret(async_op, tensor)
+
+    def batch_isend_irecv(p2p_op_list):
+        """Pipeline stage exchanges and Adasum pairs (parallel/pipeline.py, train/resnet.py): each
+        op runs as its own gloo isend / irecv on a host copy; a receive lands in the device tensor
+        when its work is waited on."""
+        if not any(_staged(o.tensor, force) for o in p2p_op_list):
+            return _ORIG["batch_isend_irecv"](p2p_op_list)
+        works = []
+        for o in p2p_op_list:
+            tag = getattr(o, "tag", 0) or 0
+            if o.op is _ORIG["isend"]:
+                h = o.tensor.detach().to("cpu", copy=True).contiguous()
+                works.append(_Send(_ORIG["isend"](h, o.peer, group=o.group, tag=tag), h))
+            else:
+                h = torch.empty(o.tensor.shape, dtype=o.tensor.dtype)
+                works.append(_Recv(_ORIG["irecv"](h, o.peer, group=o.group, tag=tag), h, o.tensor))
+        return works
+
+    def send(tensor, dst=None, group=None, tag=0, **kw):
+        if not _staged(tensor, force):
+            return _ORIG["send"](tensor, dst, group=group, tag=tag, **kw)
+        return _ORIG["send"](tensor.detach().to("cpu", copy=True).contiguous(), dst, group=group, tag=tag, **kw)
+
+    def recv(tensor, src=None, group=None, tag=0, **kw):
+        if not _staged(tensor, force):
+            return _ORIG["recv"](tensor, src, group=group, tag=tag, **kw)
+        h = torch.empty(tensor.shape, dtype=tensor.dtype)
+        r = _ORIG["recv"](h, src, group=group, tag=tag, **kw)
+        tensor.copy_(h)
+        return r
 
     def reduce_scatter_tensor(output, input, op=dist.ReduceOp.SUM, group=None, async_op=False):
         if not _staged(input, force):
@@ -104,13 +177,15 @@ def install(force: bool = False):
 
     for n, f in (("all_reduce", all_reduce), ("reduce_scatter_tensor", reduce_scatter_tensor),
                  ("all_gather_into_tensor", all_gather_into_tensor), ("broadcast", broadcast),
-                 ("all_gather", all_gather)):
+                 ("all_gather", all_gather), ("batch_isend_irecv", batch_isend_irecv), ("send", send),
+                 ("recv", recv)):
         setattr(dist, n, f)
 
 
 def uninstall():
     for n, f in _ORIG.items():
-        setattr(dist, n, f)
+        if n not in ("isend", "irecv"):  # never patched (P2POp only accepts the originals)
+            setattr(dist, n, f)
     _ORIG.clear()
 
 

@@ -170,12 +170,16 @@ def main(argv=None):
     use_cuda = torch.cuda.is_available() and not args.no_cuda
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", max(args.local_rank, 0)))
+    from ..parallel import shared_gpu
+    shared = use_cuda and shared_gpu.enabled()  # rehearsal: all ranks on cuda:0, gloo (parallel/shared_gpu.py)
     if use_cuda:
-        torch.cuda.set_device(local % torch.cuda.device_count())
+        torch.cuda.set_device(0 if shared else local % torch.cuda.device_count())
     dev = torch.device("cuda", torch.cuda.current_device()) if use_cuda else torch.device("cpu")
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group(backend=args.backend or ("nccl" if use_cuda else "gloo"))
+        dist.init_process_group(backend="gloo" if shared else (args.backend or ("nccl" if use_cuda else "gloo")))
+        if shared:
+            shared_gpu.install()
     rank = dist.get_rank() if dist.is_initialized() else 0
     torch.manual_seed(args.seed)
     if args.synthetic:
@@ -208,7 +212,8 @@ def main(argv=None):
         if adasum:
             lg, cg = adasum_groups(world, rank, local)
             model.register_comm_hook(state=AdasumState(cg, args.fp16_allreduce, lg), hook=adasum_hook)
-        elif args.fp16_allreduce or args.gradient_predivide_factor != 1.0:
+        elif args.fp16_allreduce or args.gradient_predivide_factor != 1.0 or shared:
+            # (shared-GPU rehearsal: the hook's dist.all_reduce is the host-staged one)
             model.register_comm_hook(state=(dist.group.WORLD, args.fp16_allreduce, args.gradient_predivide_factor),
                                      hook=_compressed_allreduce_hook)
     # Horovod's LR scaler: x world for averaging, 1 for Adasum, x local size for GPU Adasum

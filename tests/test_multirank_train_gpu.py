@@ -1,0 +1,112 @@
+"""Multi-rank TRAINING paths rehearsed on the one GPU of the box.
+
+Two (or four) ranks share ``cuda:0`` (``KCA_BENCH_SHARED_GPU=1``:
+``parallel.dist.init_distributed`` puts every rank on device 0 with a gloo
+default group and installs ``parallel/shared_gpu.py``, which stages device
+collectives AND the point-to-point ``batch_isend_irecv`` of the pipeline
+stages / Adasum through the host). The 8-GPU driver run is otherwise the first
+execution of:
+
+* the NeoX-style 3D trainer (``train/parallel_trainer.py``; the reference's
+  gpt-neox/04-finetune-workflow.yaml:199-244): TP=2 (column/row backward
+  all-reduces), PP=2 (1F1B P2P activations / gradients), DP=2 x TP=2 with
+  ZeRO-1 over the DP group -- each against the same trainer at world 1 on the
+  GPU (bf16 both sides);
+* the ResNet-50 trainer (``train/resnet.py``, resnet50_pytorch.py:93-125 /
+  resnet50_horovod.py:129-140): world 1 on the GPU (channels-last, MIOpen,
+  bf16 autocast) and DDP + Adasum at world 2;
+* the SD / DreamBooth trainer (``train/sd_finetuner.py``) at world 2.
+"""
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from .helpers import make_images, make_model_dir, make_sd_dir
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+STEPS, MB, GAS, SEQ = 3, 2, 4, 64
+
+
+def _launch(n: int, module: str, argv: list, timeout: int = 400, extra_env: dict | None = None):
+    cmd = [sys.executable, "-u", "-m", "kubernetes_cloud_amd.launch", "--num_gpus", str(n), "-m", module] + argv
+    env = dict(os.environ, PYTHONPATH=ROOT, KCA_BENCH_SHARED_GPU="1" if n > 1 else "0",
+               HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2", **(extra_env or {}))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    return r
+
+
+def _neox_args(model_dir, out, tp, pp, zero=0):
+    return ["--model", model_dir, "--tp", str(tp), "--pp", str(pp), "--zero-stage", str(zero),
+            "--micro-batch", str(MB), "--gradients", str(GAS), "--seq-len", str(SEQ), "--max-steps", str(STEPS),
+            "--lr", "1e-3", "--lr-schedule", "constant", "--warmup-ratio", "0", "--output-path", out,
+            "--weight-decay", "0.01"]
+
+
+@pytest.fixture(scope="module")
+def neox_ref(tmp_path_factory):
+    from kubernetes_cloud_amd.io.hf import load_pretrained
+    from kubernetes_cloud_amd.train.parallel_trainer import consolidate
+    tmp = tmp_path_factory.mktemp("neox")
+    d = make_model_dir(str(tmp / "m"), "gpt-j-6b", vocab_size=256, tokenizer=False, n_embd=256, n_layer=4,
+                       n_head=4, rotary_dim=16)
+    _launch(1, "kubernetes_cloud_amd.train.parallel_trainer", _neox_args(d, str(tmp / "w1"), 1, 1))
+    merged = consolidate(os.path.join(str(tmp / "w1"), f"checkpoint-{STEPS}"), str(tmp / "w1m"))
+    init = load_pretrained(d, dtype=torch.float32).state_dict()
+    return d, tmp, load_pretrained(merged, dtype=torch.float32).state_dict(), init
+
+
+@pytest.mark.parametrize("tp,pp,dp,zero", [(2, 1, 1, 0), (1, 2, 1, 0), (2, 1, 2, 1)])
+def test_neox_3d_trainer_on_gpu_matches_world1(neox_ref, tp, pp, dp, zero):
+    from kubernetes_cloud_amd.io.hf import load_pretrained
+    from kubernetes_cloud_amd.train.parallel_trainer import consolidate
+    d, tmp, ref, init = neox_ref
+    tag = f"tp{tp}pp{pp}dp{dp}"
+    out = str(tmp / tag)
+    _launch(tp * pp * dp, "kubernetes_cloud_amd.train.parallel_trainer", _neox_args(d, out, tp, pp, zero))
+    ck = os.path.join(out, f"checkpoint-{STEPS}")
+    assert len([f for f in os.listdir(ck) if f.startswith("mp_rank_")]) == tp * pp
+    got = load_pretrained(consolidate(ck, str(tmp / (tag + "m"))), dtype=torch.float32).state_dict()
+    if dp > 1:  # a DP replica sees a different data stream (seed + dp index): compare the size of the update
+        for k in ref:
+            if k.endswith("alibi"):
+                continue
+            dg, dr = (got[k] - init[k]).norm(), (ref[k] - init[k]).norm()
+            assert torch.isfinite(got[k]).all() and 0.3 < float(dg / dr.clamp_min(1e-12)) < 3.0, (k, dg, dr)
+        return
+    worst = 0.0
+    for k in ref:
+        if k.endswith("alibi"):
+            continue
+        delta = (ref[k] - init[k]).abs().max().item()
+        err = (got[k] - ref[k]).abs().max().item()
+        worst = max(worst, err / max(delta, 1e-6))
+    assert worst < 0.25, worst  # bf16 on both sides, different reduction orders
+
+
+def test_resnet_trainer_gpu_world1_and_ddp_adasum_world2(tmp_path):
+    common = ["--synthetic", "16", "--batch-size", "4", "--epochs", "1", "--max-steps", "3",
+              "--train-crop-size", "64", "--val-crop-size", "64", "--workers", "0", "--num-classes", "10",
+              "--use-mixed-precision"]
+    r1 = _launch(1, "kubernetes_cloud_amd.train.resnet", common + ["--log-dir", str(tmp_path / "l1")])
+    assert "Test Epoch: 1" in r1.stdout
+    r2 = _launch(2, "kubernetes_cloud_amd.train.resnet", common + ["--use-adasum", "--log-dir",
+                                                                  str(tmp_path / "l2")])
+    assert "Test Epoch: 1" in r2.stdout
+
+
+def test_sd_trainer_world2_on_gpu(tmp_path):
+    d = make_sd_dir(str(tmp_path / "sd"))
+    data = make_images(str(tmp_path / "data"), 4)
+    argv = ["--model", d, "--run_name", "w2", "--dataset", data, "--resolution", "32", "--batch_size", "1",
+            "--epochs", "1", "--output_path", str(tmp_path / "o"), "--image_log_steps", "0", "--save_steps", "0"]
+    r = _launch(2, "kubernetes_cloud_amd.train.sd_finetuner", argv)
+    outs = [os.path.join(dp, f) for dp, _, fs in os.walk(str(tmp_path / "o")) for f in fs]
+    assert any("unet" in p for p in outs), (outs[:20], r.stderr[-2000:])
