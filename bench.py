@@ -389,7 +389,8 @@ def _extras(args, dev, rec):
         return sdb.bench_train(a, dev)
 
     def decode():
-        return _load_bench("decode_bench").run_decode("gpt-j-6b", batches=(1, 32), prompt_len=512, new_tokens=64)
+        return _load_bench("decode_bench").run_decode("gpt-j-6b", batches=(1, 32), prompt_len=512, new_tokens=64,
+                                                     sampling=("greedy", "ft_topk10"))
 
     def bloom_slice():
         import torch.distributed as dist

@@ -19,9 +19,17 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 
 
-def run_decode(model="gpt-j-6b", batches=(1, 32), prompt_len=512, new_tokens=64):
-    """bench.py's ``secondary_decode``: per batch size, prefill ms and pure
-    decode ms/token (greedy, HIP graphs, all requests running) -- the FT GPT-J
+SAMPLING = {
+    "greedy": dict(do_sample=False),
+    # the FasterTransformer GPT-J request (online-inference/fastertransformer: runtime_top_k 10,
+    # temperature 1.0): sampled on the device inside the decode graph
+    "ft_topk10": dict(do_sample=True, temperature=1.0, top_k=10, top_p=1.0, seed=1),
+}
+
+
+def run_decode(model="gpt-j-6b", batches=(1, 32), prompt_len=512, new_tokens=64, sampling=("greedy",)):
+    """bench.py's ``secondary_decode``: per batch size and sampling mode, prefill ms and pure
+    decode ms/token (HIP graphs, all requests running) -- the FT GPT-J
     serving row (request_output_len 64)."""
     from kubernetes_cloud_amd.engine.llm_engine import LLMEngine, SamplingParams
     from kubernetes_cloud_amd.models.causal_lm import build_model
@@ -33,9 +41,9 @@ def run_decode(model="gpt-j-6b", batches=(1, 32), prompt_len=512, new_tokens=64)
     eng = LLMEngine(m, max_slots=max(batches), max_len=prompt_len + new_tokens + 16)
     g = torch.Generator().manual_seed(0)
     out = []
-    for B in batches:
+    for B, mode in ((b, s) for b in batches for s in sampling):
         prompts = [torch.randint(0, cfg.vocab_size, (prompt_len,), generator=g).tolist() for _ in range(B)]
-        sp = SamplingParams(max_new_tokens=new_tokens, do_sample=False)
+        sp = SamplingParams(max_new_tokens=new_tokens, **SAMPLING[mode])
         eng.generate(prompts, sp)  # warm-up + graph capture for this bucket
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -51,7 +59,8 @@ def run_decode(model="gpt-j-6b", batches=(1, 32), prompt_len=512, new_tokens=64)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         n = eng.stats["decode_steps"] - s0
-        out.append({"metric": f"{model} decode", "batch": B, "prompt_len": prompt_len, "new_tokens": new_tokens,
+        out.append({"metric": f"{model} decode", "batch": B, "sampling": mode, "prompt_len": prompt_len,
+                    "new_tokens": new_tokens,
                     "prefill_ms_one_seq": round(prefill_ms, 2), "decode_ms_per_token": round(dt / max(n, 1) * 1e3, 3),
                     "decode_tokens_per_s": round(B * n / dt, 1), "dtype": "bf16", "graphs": eng.runner.use_graphs,
                     "data": "random-init weights, random prompts"})

@@ -906,11 +906,16 @@ __device__ __forceinline__ void store_acc_t(bf16_t* rowp, const f32x16 (&acc)[D 
   }
 }
 
-template <int D, bool CAUSAL>
+// DS < D ("narrow storage", as the forward): heads stored DS wide (SD-1.5's 40-wide heads in 48 columns,
+// D = 64 images, the pad chunks of every image zeroed once); the S / dP contractions run DS / 16 MFMA
+// steps, the dQ (dK, dV) tiles are stored DS wide.
+template <int D, bool CAUSAL, int DS = D>
 __global__ void __launch_bounds__(256, 1) attn_bwd_dq_tiled_kernel(FastBwdParams p) {
   constexpr int BM = 128, BN = 32;
   constexpr int TILE = BN * D * 2;
-  constexpr int CPT = Stager<D>::CPT;
+  using Stg = StagerFor<D, DS>;
+  constexpr int CPT = Stg::CPT;
+  constexpr int KSD = DS / 16;  // contraction steps over the stored columns
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE];
   ASTAMP_DECL
 
@@ -933,9 +938,9 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq_tiled_kernel(FastBwdParams
 
   const bf16_t* qp = p.q + b * p.q_sb + h * p.q_sh + (long long)qrow * p.q_st;
   const bf16_t* gp = p.dout + b * p.do_sb + h * p.do_sh + (long long)qrow * p.do_st;
-  bf16x8 qf[D / 16], gf[D / 16];
+  bf16x8 qf[KSD], gf[KSD];
 #pragma unroll
-  for (int s = 0; s < D / 16; ++s) {
+  for (int s = 0; s < KSD; ++s) {
     qf[s] = *reinterpret_cast<const bf16x8*>(qp + 16 * s + 8 * hh);
     gf[s] = *reinterpret_cast<const bf16x8*>(gp + 16 * s + 8 * hh);
   }
@@ -950,12 +955,19 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq_tiled_kernel(FastBwdParams
 
   const bf16_t* kst = p.k + b * p.k_sb + hk * p.k_sh;
   const bf16_t* vst = p.v + b * p.v_sb + hk * p.v_sh;
-  Stager<D> stg(tid, p.k_st, p.v_st);
+  Stg stg(tid, p.k_st, p.v_st);
   stg.bind(kst, vst, p.k_st, p.v_st);
   u32x4 sk[CPT], sv[CPT];
   int be, bo, b1, b2;
   row_bases<D>(l32, hh, be, bo);
   tr_bases<D>(lane, b1, b2);
+  if constexpr (DS < D) {  // K / V image chunks DS/8.. are never loaded: zero them in both buffers once
+    constexpr int PC = D / 8 - DS / 8, NZ = 2 * 2 * 32 * PC;
+    for (int i = tid; i < NZ; i += 256) {
+      const int img = i / (32 * PC), row = (i / PC) % 32, ch = DS / 8 + i % PC;
+      *reinterpret_cast<u32x4*>(smem + img * TILE + img_off<D>(row, ch)) = u32x4{0, 0, 0, 0};
+    }
+  }
 
   stg.load(sk, sv, kst, vst, 0, p.k_st, p.v_st);
   stg.store(sk, sv, smem);
@@ -987,8 +999,8 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq_tiled_kernel(FastBwdParams
       fv[1] = row_frag<D>(Vs, be, bo, 1);
       __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
 #pragma unroll
-      for (int s = 0; s < D / 16; ++s) {
-        if (s + 2 < D / 16) {
+      for (int s = 0; s < KSD; ++s) {
+        if (s + 2 < KSD) {
           fk[(s + 2) % 3] = row_frag<D>(Ks, be, bo, s + 2);
           fv[(s + 2) % 3] = row_frag<D>(Vs, be, bo, s + 2);
           __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
@@ -1039,17 +1051,19 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq_tiled_kernel(FastBwdParams
   const int nfree = CAUSAL ? ntiles - 4 : ntiles;
   for (int t = 0; t < nfree; ++t) tile_step(t, std::false_type{});
   for (int t = max(nfree, 0); t < ntiles; ++t) tile_step(t, std::true_type{});
-  store_tile_lds<D>(p.dq + b * p.dq_sb + h * p.dq_sh + (long long)q0 * p.dq_st, p.dq_st, dq, lane, p.scale,
-                    smem + wave * 32 * D * 2);
+  store_tile_lds<D, DS>(p.dq + b * p.dq_sb + h * p.dq_sh + (long long)q0 * p.dq_st, p.dq_st, dq, lane, p.scale,
+                        smem + wave * 32 * D * 2);
   ASTAMP(6);
   ASTAMP_FLUSH(16);
 }
 
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, int DS = D>
 __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_tiled_kernel(FastBwdParams p) {
   constexpr int BK = 128, BQ = 32;
   constexpr int TILE = BQ * D * 2;                  // one 32-row image
-  constexpr int NCH = D / 8, CPT = Stager<D>::CPT;
+  using Stg = StagerFor<D, DS>;
+  constexpr int NCH = D / 8, NCS = DS / 8, CPT = Stg::CPT;
+  constexpr int KSD = DS / 16;                      // contraction steps over the stored columns
   constexpr int VOFF = 4 * TILE;                    // V images of the 4 waves
   constexpr int LOFF = VOFF + 4 * TILE;             // lse/delta: [buf][64] floats
   __shared__ __attribute__((aligned(16))) char smem[LOFF + 2 * 64 * 4];
@@ -1069,17 +1083,24 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_tiled_kernel(FastBwdPara
 
   const bf16_t* kp = p.k + b * p.k_sb + hk * p.k_sh;
   const bf16_t* vp = p.v + b * p.v_sb + hk * p.v_sh;
-  bf16x8 kf[D / 16];
+  bf16x8 kf[KSD];
 #pragma unroll
-  for (int s = 0; s < D / 16; ++s)
+  for (int s = 0; s < KSD; ++s)
     kf[s] = *reinterpret_cast<const bf16x8*>(kp + (long long)key * p.k_st + 16 * s + 8 * hh);
-  // this wave's 32 V rows -> its own image (read back by rows for dP)
+  // this wave's 32 V rows -> its own image (read back by rows for dP; pad chunks zero)
   char* vimg = smem + VOFF + wave * TILE;
 #pragma unroll
   for (int i = 0; i < 32 * NCH / 64; ++i) {
     const int idx = lane + 64 * i, row = idx / NCH, ch = idx % NCH;
     *reinterpret_cast<u32x4*>(vimg + img_off<D>(row, ch)) =
-        *reinterpret_cast<const u32x4*>(vp + (long long)(kw + row) * p.v_st + ch * 8);
+        ch < NCS ? *reinterpret_cast<const u32x4*>(vp + (long long)(kw + row) * p.v_st + ch * 8) : u32x4{0, 0, 0, 0};
+  }
+  if constexpr (DS < D) {  // Q / dO image chunks DS/8.. are never loaded: zero them in both buffers once
+    constexpr int PC = NCH - NCS, NZ = 2 * 2 * 32 * PC;
+    for (int i = tid; i < NZ; i += 256) {
+      const int img = i / (32 * PC), row = (i / PC) % 32, ch = NCS + i % PC;
+      *reinterpret_cast<u32x4*>(smem + img * TILE + img_off<D>(row, ch)) = u32x4{0, 0, 0, 0};
+    }
   }
   f32x16 dk[D / 32], dv[D / 32];
 #pragma unroll
@@ -1092,7 +1113,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_tiled_kernel(FastBwdPara
   const int nqt = (p.Sq - q_lo) / BQ;
   const int total = nqt * grp;
 
-  Stager<D> stg(tid, p.q_st, p.do_st);
+  Stg stg(tid, p.q_st, p.do_st);
   stg.bind(p.q + b * p.q_sb + hk * grp * p.q_sh, p.dout + b * p.do_sb + hk * grp * p.do_sh, p.q_st, p.do_st);
   u32x4 sq[CPT], sg[CPT];
   float lreg = 0.f;
@@ -1149,14 +1170,14 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_tiled_kernel(FastBwdPara
       bf16x8 fq1, fg1, fv1;
       __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
 #pragma unroll
-      for (int s = 0; s < D / 16; ++s) {
+      for (int s = 0; s < KSD; ++s) {
         bf16x8& cq = (s & 1) ? fq1 : fq0;
         bf16x8& cg = (s & 1) ? fg1 : fg0;
         bf16x8& cv = (s & 1) ? fv1 : fv0;
         bf16x8& nq = (s & 1) ? fq0 : fq1;
         bf16x8& ng = (s & 1) ? fg0 : fg1;
         bf16x8& nv = (s & 1) ? fv0 : fv1;
-        if (s + 1 < D / 16) {
+        if (s + 1 < KSD) {
           nq = row_frag<D>(Qs, be, bo, s + 1);
           ng = row_frag<D>(Gs, be, bo, s + 1);
           nv = row_frag<D>(vimg, be, bo, s + 1);
@@ -1236,9 +1257,9 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_tiled_kernel(FastBwdPara
     store_acc_t<D>(p.dk + b * p.dk_sb + hk * p.dk_sh + (long long)key * p.dk_st, dk, hh, p.scale);
     store_acc_t<D>(p.dv + b * p.dv_sb + hk * p.dv_sh + (long long)key * p.dv_st, dv, hh, 1.f);
   } else {
-    store_tile_lds<D>(p.dk + b * p.dk_sb + hk * p.dk_sh + (long long)kw * p.dk_st, p.dk_st, dk, lane, p.scale,
+    store_tile_lds<D, DS>(p.dk + b * p.dk_sb + hk * p.dk_sh + (long long)kw * p.dk_st, p.dk_st, dk, lane, p.scale,
                       smem + wave * 32 * D * 2);
-    store_tile_lds<D>(p.dv + b * p.dv_sb + hk * p.dv_sh + (long long)kw * p.dv_st, p.dv_st, dv, lane, 1.f,
+    store_tile_lds<D, DS>(p.dv + b * p.dv_sb + hk * p.dv_sh + (long long)kw * p.dv_st, p.dv_st, dv, lane, 1.f,
                       smem + wave * 32 * D * 2);
   }
   ASTAMP(6);
@@ -1320,8 +1341,10 @@ KCA_API int kca_attn_bwd_tiled(const void* q, const void* k, const void* v, cons
                                long long dk_st, long long dk_sh, long long dv_sb, long long dv_st,
                                long long dv_sh, int B, int Sq, int Sk, int H, int Hkv, int d,
                                int causal, float scale, hipStream_t stream) {
-  if ((d != 64 && d != 96 && d != 128 && d != 160 && d != 256) || Sq % 128 || Sk % 128 || Sq <= 0 || H % Hkv)
+  if ((d != 48 && d != 64 && d != 96 && d != 128 && d != 160 && d != 256) || Sq % 128 || Sk % 128 || Sq <= 0 ||
+      H % Hkv)
     return 1;
+  if (d == 48 && causal) return 1;  // narrow storage: SD-1.5's (non-causal) 40-wide heads
   if (causal && Sk < Sq) return 1;
   if (!offsets_fit(Sk, k_st) || !offsets_fit(Sk, v_st) || !offsets_fit(Sq, q_st) || !offsets_fit(Sq, do_st)) return 1;
   FastBwdParams p{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout,
@@ -1330,7 +1353,10 @@ KCA_API int kca_attn_bwd_tiled(const void* q, const void* k, const void* v, cons
                   dq_sb, dq_st, dq_sh, dk_sb, dk_st, dk_sh, dv_sb, dv_st, dv_sh,
                   B, Sq, Sk, H, Hkv, scale};
   dim3 g1((Sk / 128) * B * Hkv), g2((Sq / 128) * B * H);
-  if (d == 256) {
+  if (d == 48) {  // heads stored 48 wide in D = 64 images (the UNet's 40-wide heads, training)
+    hipLaunchKernelGGL((attn_bwd_dkdv_tiled_kernel<64, false, 48>), g1, dim3(256), 0, stream, p);
+    hipLaunchKernelGGL((attn_bwd_dq_tiled_kernel<64, false, 48>), g2, dim3(256), 0, stream, p);
+  } else if (d == 256) {
     if (causal) {
       hipLaunchKernelGGL((attn_bwd_dkdv_tiled_kernel<256, true>), g1, dim3(256), 0, stream, p);
       hipLaunchKernelGGL((attn_bwd_dq_tiled_kernel<256, true>), g2, dim3(256), 0, stream, p);

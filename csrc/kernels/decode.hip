@@ -1493,6 +1493,9 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(
   }
 }
 
+constexpr int MWG_KMAX_ = 64;  // (= MWG_KMAX below)
+__device__ __forceinline__ bool mwg_row(float T, int k) { return !(T > 0.f) || (k >= 1 && k <= MWG_KMAX_); }
+
 // Register-resident sampler (bf16 logits, V <= RPT * 1024, GPT-J's 50400 at 128 per thread x 512 threads): the row is read
 // ONCE into registers (element i = u * 1024 + tid, value u of the thread) and every later pass -- max / normaliser, the top-k
 // and top-p radix selects, the multinomial -- runs on registers and LDS histograms, not on a fp32
@@ -1506,7 +1509,7 @@ __global__ __launch_bounds__(NT) void sample_reg_kernel(
     const float* __restrict__ top_p, const float* __restrict__ rep_pen, uint8_t* __restrict__ seen,
     const int* __restrict__ slots, const int* __restrict__ ban_ids, int n_ban,
     const unsigned long long* __restrict__ seeds, long long step,
-    long long* __restrict__ out_ids, float* __restrict__ out_lp, int* __restrict__ out_kept) {
+    long long* __restrict__ out_ids, float* __restrict__ out_lp, int* __restrict__ out_kept, int skip_mwg) {
   __shared__ float hist[16];
   __shared__ float red[NT / 64];
   __shared__ float scan[NT / 64];
@@ -1517,6 +1520,7 @@ __global__ __launch_bounds__(NT) void sample_reg_kernel(
   __shared__ float selp[2];
   const int b = blockIdx.x, tid = threadIdx.x;
   const float T = temperature ? temperature[b] : 1.f;
+  if (skip_mwg && mwg_row(T, top_k ? top_k[b] : 0)) return;  // sample_mwg_kernel's row
   const float rp = rep_pen ? rep_pen[b] : 1.f;
   const int slot = slots ? slots[b] : b;
   const uint8_t* sn = seen ? seen + (long long)slot * V : nullptr;
@@ -1811,13 +1815,458 @@ __global__ __launch_bounds__(NT) void sample_reg_kernel(
   }
 }
 
+// ------------------------------------------------------ multi-workgroup sampler (top-k <= 64 or greedy)
+// The register sampler above runs one workgroup per row: at batch 1 the whole 50400-entry row and
+// every radix pass sit on ONE of 256 CUs (top-k 50: 93 us, + top-p: 133 us, profiles/sampler_r3.txt).
+// Here a row is split over MWG_G workgroups of 256 threads (a contiguous chunk each, ~13 values per
+// thread): each computes its chunk's max / softmax sum / first argmax and -- for a sampled row -- its
+// local k-th largest key t_g by a 4-bit radix select, and writes the chunk's elements >= t_g (in index
+// order, at most MWG_CMAX) to the workspace. The global k-th largest key is >= every t_g (chunk g
+// alone holds k elements >= t_g), so the union of the chunk lists, cut at T0 = max_g t_g, holds the
+// global top-k with its ties. The last workgroup to arrive (agent-scope release / acquire around one
+// counter per row) merges: global max and normaliser, the top-k select over the ~k..2k candidates,
+// top-p over the survivors (4-bit radix on the mass, as the register sampler), and the Philox
+// multinomial in index order. Rows with top_k == 0 or > 64 (top-p over the whole vocabulary) are
+// left to sample_reg_kernel, launched after this one with `skip_mwg` (each kernel takes exactly the
+// rows the other leaves: the choice is made on the device, so captured decode graphs keep working
+// whatever the requests' parameters are).
+constexpr int MWG_G = 16, MWG_NT = 256, MWG_CMAX = 128, MWG_KMAX = MWG_KMAX_;
+constexpr int MWG_PART = 8;  // floats per workgroup partial: max, sum, t_g (key bits), count, argmax
+
+// 4-bit radix select of the k-th largest key over (key, valid) pairs spread across the block:
+// per-thread packed 8-bit counters (<= 255 elements per thread), wave sums of 16-bit pairs, digit
+// pick by thread 0. Returns the key prefix (ties at it kept); 0 when fewer than k are valid.
+template <int EPT, typename KeyFn>
+__device__ uint32_t block_kth_key(int k, KeyFn key_of, uint32_t* cnt16, int* sel) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = blockDim.x >> 6;
+  uint32_t prefix = 0, mask = 0;
+  int remaining = k;
+  for (int shift = 28; shift >= 0; shift -= 4) {
+    uint32_t w4[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) {
+      uint32_t key;
+      if (key_of(e, key) && (key & mask) == prefix) {
+        const uint32_t d = (key >> shift) & 15u, inc = 1u << ((d & 3u) << 3);
+        w4[0] += d < 4 ? inc : 0u;
+        w4[1] += (d >> 2) == 1 ? inc : 0u;
+        w4[2] += (d >> 2) == 2 ? inc : 0u;
+        w4[3] += d >= 12 ? inc : 0u;
+      }
+    }
+    uint32_t w8[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      w8[2 * q] = (w4[q] & 0xffu) | ((w4[q] & 0xff00u) << 8);
+      w8[2 * q + 1] = ((w4[q] >> 16) & 0xffu) | ((w4[q] >> 8) & 0xff0000u);
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) w8[q] += __shfl_xor(w8[q], o, 64);
+    __syncthreads();
+    if (lane < 8) {
+      uint32_t mine = w8[0];
+#pragma unroll
+      for (int q = 1; q < 8; ++q)
+        if (lane == q) mine = w8[q];
+      cnt16[wid * 8 + lane] = mine;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int run = 0, dsel = -1;
+      for (int j = 15; j >= 0; --j) {
+        uint32_t t = 0;
+        for (int w = 0; w < nw; ++w) t += cnt16[w * 8 + (j >> 1)];
+        const int c = (int)((j & 1) ? (t >> 16) : (t & 0xffffu));
+        if (run + c >= remaining) {
+          dsel = j;
+          break;
+        }
+        run += c;
+      }
+      sel[0] = dsel;
+      sel[1] = run;
+    }
+    __syncthreads();
+    const int dsel = sel[0], run = sel[1];
+    if (dsel < 0) return 0u;  // fewer than k valid: keep every valid element
+    prefix |= (uint32_t)dsel << shift;
+    mask |= 15u << shift;
+    remaining -= run;
+  }
+  return prefix;
+}
+
+template <int VPT>
+__global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
+    const bf16_t* __restrict__ logits, long long ld, int V, int CS,
+    const float* __restrict__ temperature, const int* __restrict__ top_k,
+    const float* __restrict__ top_p, const float* __restrict__ rep_pen, uint8_t* __restrict__ seen,
+    const int* __restrict__ slots, const int* __restrict__ ban_ids, int n_ban,
+    const unsigned long long* __restrict__ seeds, long long step, float* __restrict__ ws,
+    unsigned int* __restrict__ cnt, long long* __restrict__ out_ids, float* __restrict__ out_lp,
+    int* __restrict__ out_kept) {
+  __shared__ float red[MWG_NT / 64];
+  __shared__ uint32_t cnt16[MWG_NT / 64 * 8];
+  __shared__ int sel[2];
+  __shared__ int iscan[MWG_NT / 64];
+  __shared__ int sh_last;
+  __shared__ float Lv[MWG_G * MWG_CMAX];
+  __shared__ int Li[MWG_G * MWG_CMAX];
+  __shared__ float hist[16];
+  __shared__ float selp[2];
+  __shared__ int goff[MWG_G + 1];
+  const int g = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const float T = temperature ? temperature[b] : 1.f;
+  const int k = top_k ? top_k[b] : 0;
+  if (!mwg_row(T, k)) return;  // sample_reg_kernel's row
+  const bool greedy = !(T > 0.f);
+  const float rp = rep_pen ? rep_pen[b] : 1.f;
+  const int slot = slots ? slots[b] : b;
+  const uint8_t* sn = seen ? seen + (long long)slot * V : nullptr;
+  const float inv_t = (greedy || T == 1.f) ? 1.f : 1.f / T;
+  const bool pen = rp != 1.f && sn;
+  float* part = ws + (long long)b * MWG_G * (MWG_PART + 2 * MWG_CMAX);  // [G][PART + 2*CMAX]
+  float* mine = part + g * (MWG_PART + 2 * MWG_CMAX);
+
+  // ---- this workgroup's chunk [c0, c1): thread t owns the contiguous run [c0 + t*VPT, +VPT)
+  const int c0 = g * CS, c1 = min(V, c0 + CS);
+  const int e0 = c0 + tid * VPT;
+  float x[VPT];
+  const bf16_t* row = logits + b * ld;
+#pragma unroll
+  for (int e = 0; e < VPT; ++e) {
+    const int i = e0 + e;
+    float w = -INFINITY;
+    if (i < c1) {
+      w = bf2f(row[i]);
+      if (pen && sn[i]) w = w < 0.f ? w * rp : w / rp;
+      w *= inv_t;
+    }
+    x[e] = w;
+  }
+  if (ban_ids)
+    for (int j = 0; j < n_ban; ++j) {
+      const int id = ban_ids[(long long)b * n_ban + j];
+      if (id >= e0 && id < e0 + VPT && id < c1) {
+#pragma unroll
+        for (int e = 0; e < VPT; ++e)
+          if (e0 + e == id) x[e] = -INFINITY;
+      }
+    }
+  float m = -INFINITY, s = 0.f;
+  int am = 0x7fffffff;
+#pragma unroll
+  for (int e = 0; e < VPT; ++e) {
+    const float w = x[e];
+    if (w > m) {
+      s = s * __expf(m - w) + 1.f;
+      m = w;
+      am = e0 + e;
+    } else if (w != -INFINITY) {
+      s += __expf(w - m);
+    }
+  }
+  const float Mg = block_max(m, red);
+  s = (m == -INFINITY) ? 0.f : s * __expf(m - Mg);
+  const float Sg = block_sum(s, red);
+  int cand = (m == Mg && Mg != -INFINITY) ? am : 0x7fffffff;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) cand = min(cand, __shfl_xor(cand, o, 64));
+  __syncthreads();
+  if (lane == 0) iscan[wid] = cand;
+  __syncthreads();
+  int amg = 0x7fffffff;
+  for (int w = 0; w < MWG_NT / 64; ++w) amg = min(amg, iscan[w]);
+
+  // ---- local top-k threshold and the chunk's candidates (index order, at most CMAX)
+  int count = 0;
+  uint32_t tg = 0;
+  if (!greedy) {
+    tg = block_kth_key<VPT>(k, [&](int e, uint32_t& key) {
+      key = fkey(x[e]);
+      return x[e] != -INFINITY;
+    }, cnt16, sel);
+    int c = 0;
+#pragma unroll
+    for (int e = 0; e < VPT; ++e) c += (x[e] != -INFINITY && fkey(x[e]) >= tg) ? 1 : 0;
+    int inc = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += t;
+    }
+    __syncthreads();
+    if (lane == 63) iscan[wid] = inc;
+    __syncthreads();
+    int off = inc - c, tot = 0;
+    for (int w = 0; w < MWG_NT / 64; ++w) {
+      if (w < wid) off += iscan[w];
+      tot += iscan[w];
+    }
+    count = min(tot, MWG_CMAX);  // (> CMAX only with massive ties at t_g: the first CMAX by index stay)
+#pragma unroll
+    for (int e = 0; e < VPT; ++e) {
+      if (x[e] != -INFINITY && fkey(x[e]) >= tg) {
+        if (off < MWG_CMAX) {
+          mine[MWG_PART + off] = x[e];
+          reinterpret_cast<int*>(mine)[MWG_PART + MWG_CMAX + off] = e0 + e;
+        }
+        ++off;
+      }
+    }
+  }
+  if (tid == 0) {  // (integer fields stored as integers: key / index bit patterns as floats could be NaNs)
+    mine[0] = Mg;
+    mine[1] = Sg;
+    unsigned* mu = reinterpret_cast<unsigned*>(mine);
+    mu[2] = tg;
+    mu[3] = (unsigned)count;
+    mu[4] = (unsigned)amg;
+  }
+  // ---- arrival: every wave's stores drained, one agent-scope release, one counter per row
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = __hip_atomic_fetch_add(&cnt[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sh_last = prev == MWG_G - 1;
+    if (sh_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!sh_last) return;
+
+  // ================= merge (the last workgroup of the row)
+  if (tid == 0) cnt[b] = 0;  // re-armed for the next launch
+  float M = -INFINITY;
+  for (int q = 0; q < MWG_G; ++q) M = fmaxf(M, part[q * (MWG_PART + 2 * MWG_CMAX)]);
+  float Z = 0.f;
+  int best = 0x7fffffff;
+  uint32_t T0 = 0;
+  for (int q = 0; q < MWG_G; ++q) {
+    const float* pq = part + q * (MWG_PART + 2 * MWG_CMAX);
+    if (pq[0] != -INFINITY) Z += pq[1] * __expf(pq[0] - M);
+    const unsigned* pu = reinterpret_cast<const unsigned*>(pq);
+    if (pq[0] == M && best == 0x7fffffff) best = (int)pu[4];  // first chunk holding the max
+    T0 = max(T0, pu[2]);
+  }
+  const float lZ = M + __logf(Z);
+  if (greedy || M == -INFINITY) {
+    if (tid == 0) {
+      const int id = (M == -INFINITY || best >= V) ? 0 : best;
+      out_ids[b] = id;
+      if (out_lp) out_lp[b] = M == -INFINITY ? -INFINITY : M - lZ;
+      if (seen && M != -INFINITY) seen[(long long)slot * V + id] = 1;
+      if (out_kept) out_kept[b] = M == -INFINITY ? 0 : 1;
+    }
+    return;
+  }
+  // gather the candidates >= T0 into LDS in (chunk, position) = index order
+  if (tid == 0) {
+    int o = 0;
+    for (int q = 0; q < MWG_G; ++q) {
+      goff[q] = o;
+      o += reinterpret_cast<const int*>(part)[q * (MWG_PART + 2 * MWG_CMAX) + 3];
+    }
+    goff[MWG_G] = o;
+  }
+  __syncthreads();
+  const int ntot = goff[MWG_G];
+  constexpr int EPT = (MWG_G * MWG_CMAX + MWG_NT - 1) / MWG_NT;
+  int keepc = 0;
+  float cv[EPT];
+  int ci[EPT];
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+    const int j = tid * EPT + e;
+    cv[e] = -INFINITY;
+    ci[e] = 0;
+    if (j < ntot) {
+      int q = 0;
+      while (goff[q + 1] <= j) ++q;
+      const float* pq = part + q * (MWG_PART + 2 * MWG_CMAX);
+      const float v = pq[MWG_PART + (j - goff[q])];
+      if (fkey(v) >= T0) {
+        cv[e] = v;
+        ci[e] = reinterpret_cast<const int*>(pq)[MWG_PART + MWG_CMAX + (j - goff[q])];
+        ++keepc;
+      }
+    }
+  }
+  int inc = keepc;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += t;
+  }
+  __syncthreads();
+  if (lane == 63) iscan[wid] = inc;
+  __syncthreads();
+  int off = inc - keepc, n = 0;
+  for (int w = 0; w < MWG_NT / 64; ++w) {
+    if (w < wid) off += iscan[w];
+    n += iscan[w];
+  }
+#pragma unroll
+  for (int e = 0; e < EPT; ++e)
+    if (cv[e] != -INFINITY) {
+      Lv[off] = cv[e];
+      Li[off] = ci[e];
+      ++off;
+    }
+  __syncthreads();
+  // global top-k over L (n elements, thread t holds [t*E2, t*E2 + E2))
+  const int E2 = (n + MWG_NT - 1) / MWG_NT;
+  uint32_t thr = block_kth_key<EPT>(k, [&](int e, uint32_t& key) {
+    const int j = tid * E2 + e;
+    if (e >= E2 || j >= n) return false;
+    key = fkey(Lv[j]);
+    return true;
+  }, cnt16, sel);
+  // top-p over the survivors: the smallest key whose descending inclusive mass reaches p * kept mass
+  const float pp = top_p ? top_p[b] : 1.f;
+  if (pp < 1.f) {
+    uint32_t prefix = 0, mask = 0;
+    float above = 0.f, target = -1.f;
+    for (int shift = 28; shift >= 0; shift -= 4) {
+      if (tid < 16) hist[tid] = 0.f;
+      __syncthreads();
+      for (int j = tid; j < n; j += MWG_NT) {
+        const uint32_t key = fkey(Lv[j]);
+        if (key >= thr && (key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 15u], __expf(Lv[j] - M));
+      }
+      __syncthreads();
+      if (tid == 0) {
+        if (target < 0.f) {
+          float t = 0.f;
+          for (int j = 0; j < 16; ++j) t += hist[j];
+          target = pp * t;
+        }
+        float run = 0.f;
+        int dsel = -1;
+        for (int j = 15; j >= 0; --j) {
+          if (hist[j] > 0.f && run + hist[j] >= target - above) {
+            dsel = j;
+            break;
+          }
+          run += hist[j];
+        }
+        sel[0] = dsel;
+        selp[0] = run;
+        selp[1] = target;
+      }
+      __syncthreads();
+      const int dsel = sel[0];
+      const float run = selp[0];
+      target = selp[1];
+      if (dsel < 0) {
+        prefix = 0;
+        mask = 0;
+        break;
+      }
+      prefix |= (uint32_t)dsel << shift;
+      mask |= 15u << shift;
+      above += run;
+    }
+    if (mask == 0xffffffffu && prefix > thr) thr = prefix;
+  }
+  // multinomial over the kept entries of L, index order: per-thread mass, block scan, Philox draw
+  float ssum = 0.f;
+  int kept = 0, last_j = -1;
+  for (int e = 0; e < E2; ++e) {
+    const int j = tid * E2 + e;
+    if (j < n && fkey(Lv[j]) >= thr) {
+      ssum += __expf(Lv[j] - M);
+      ++kept;
+      last_j = j;
+    }
+  }
+  float incl = ssum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  int kept_tot = kept;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) kept_tot += __shfl_xor(kept_tot, o, 64);
+  __syncthreads();
+  if (lane == 63) red[wid] = incl;
+  if (lane == 0) iscan[wid] = kept_tot;
+  if (tid == 0) sel[0] = -1;
+  __syncthreads();
+  float woff = 0.f, total = 0.f;
+  int ktot = 0;
+  for (int w = 0; w < MWG_NT / 64; ++w) {
+    if (w < wid) woff += red[w];
+    total += red[w];
+    ktot += iscan[w];
+  }
+  incl += woff;
+  const float excl = incl - ssum;
+  uint32_t c[4] = {seeds ? 0u : (uint32_t)b, (uint32_t)step, (uint32_t)((unsigned long long)step >> 32), 0x5eedu};
+  const unsigned long long sd = seeds ? seeds[b] : 0ull;
+  philox4x32_10(c, (uint32_t)sd, (uint32_t)(sd >> 32));
+  const float r = ((c[0] >> 8) + 1) * (1.0f / 16777216.0f);  // (0, 1]
+  const float u = r * total;
+  if (ssum > 0.f && excl < u && u <= incl) {
+    float run = excl;
+    int pick = -1;
+    for (int e = 0; e < E2 && pick < 0; ++e) {
+      const int j = tid * E2 + e;
+      if (j < n && fkey(Lv[j]) >= thr) {
+        run += __expf(Lv[j] - M);
+        if (run >= u || j == last_j) pick = j;
+      }
+    }
+    if (pick >= 0) atomicMax(&sel[0], pick);
+  }
+  __syncthreads();
+  if (sel[0] < 0 && kept > 0) atomicMax(&sel[0], last_j);  // rounding at the top of the range
+  __syncthreads();
+  if (tid == 0) {
+    const int j = sel[0];
+    const int id = j >= 0 ? Li[j] : 0;
+    out_ids[b] = id;
+    if (out_lp) out_lp[b] = j >= 0 ? Lv[j] - lZ : -INFINITY;
+    if (seen && j >= 0) seen[(long long)slot * V + id] = 1;
+    if (out_kept) out_kept[b] = ktot;
+  }
+}
+
+// cnt: >= B zero-initialised counters (the multi-workgroup path re-arms them), or null to keep every
+// row on the one-workgroup kernels.
 KCA_API int kca_sample_logits(const void* logits, long long ld, int is_bf16, int B, int V,
                               const float* temperature, const int* top_k, const float* top_p,
                               const float* rep_pen, void* seen, const int* slots,
                               const int* ban_ids, int n_ban, const unsigned long long* seeds,
                               long long step, float* ws, long long* out_ids, float* out_lp,
-                              int* out_kept, hipStream_t stream) {
+                              int* out_kept, unsigned int* cnt, hipStream_t stream) {
   if (B <= 0 || V <= 0 || !ws || !out_ids) return 1;
+  static int mwg = -1;  // KCA_SAMPLE_MWG=0: every row on the one-workgroup kernels (A/B)
+  if (mwg < 0) {
+    const char* e = getenv("KCA_SAMPLE_MWG");
+    mwg = !(e && e[0] == '0');
+  }
+  const int CS = (V + MWG_G - 1) / MWG_G, vpt = (CS + MWG_NT - 1) / MWG_NT;
+  const bool use_mwg = mwg && cnt && is_bf16 && V <= 50 * 1024 && vpt <= 16 &&
+                       (long long)MWG_G * (MWG_PART + 2 * MWG_CMAX) <= V;  // (the rest: sample_reg_kernel)
+  if (use_mwg) {
+#define KCA_SAMPLE_MWG_LAUNCH(P)                                                                           \
+  hipLaunchKernelGGL((sample_mwg_kernel<P>), dim3(MWG_G, B), dim3(MWG_NT), 0, stream, (const bf16_t*)logits, ld, \
+                     V, CS, temperature, top_k, top_p, rep_pen, (uint8_t*)seen, slots, ban_ids, n_ban, seeds,  \
+                     step, ws, cnt, out_ids, out_lp, out_kept)
+    if (vpt <= 4) KCA_SAMPLE_MWG_LAUNCH(4);
+    else if (vpt <= 8) KCA_SAMPLE_MWG_LAUNCH(8);
+    else if (vpt <= 13) KCA_SAMPLE_MWG_LAUNCH(13);  // GPT-2 / GPT-J / NeoX vocabularies
+    else KCA_SAMPLE_MWG_LAUNCH(16);
+#undef KCA_SAMPLE_MWG_LAUNCH
+  }
   static int compact = -1;  // KCA_SAMPLE_COMPACT=0: top-p / multinomial over the full vocabulary (A/B)
   if (compact < 0) {
     const char* e = getenv("KCA_SAMPLE_COMPACT");
@@ -1832,7 +2281,7 @@ KCA_API int kca_sample_logits(const void* logits, long long ld, int is_bf16, int
 #define KCA_SAMPLE_REG_LAUNCH(R)                                                                          \
   hipLaunchKernelGGL((sample_reg_kernel<R, 1024>), dim3(B), dim3(1024), 0, stream, logits, ld, V,            \
                      temperature, top_k, top_p, rep_pen, (uint8_t*)seen, slots, ban_ids, n_ban, seeds, step,     \
-                     out_ids, out_lp, out_kept)
+                     out_ids, out_lp, out_kept, (int)use_mwg)
     if (V <= 16 * 1024) KCA_SAMPLE_REG_LAUNCH(16);
     else if (V <= 32 * 1024) KCA_SAMPLE_REG_LAUNCH(32);
     else KCA_SAMPLE_REG_LAUNCH(50);  // GPT-2 / GPT-J / NeoX vocabularies (50257 / 50400 / 50432)

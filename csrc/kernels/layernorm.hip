@@ -117,8 +117,16 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(
   for (int row = blockIdx.x; row < rows; row += gridDim.x) {
     const size_t base = (size_t)row * d;
     const float mean = mean_in[row], rstd = rstd_in[row];
-    float xh[NV][8], gy[NV][8];
+    float xh[NV][8], gy[NV][8], rr[NV][8];
     float s1 = 0.f, s2 = 0.f;
+    // the residual gradient is loaded with h and dy, ahead of the two row reductions: loaded after
+    // them (as before) its HBM round trip sat serially in every row (0.29 ms per GPT-J-shaped call,
+    // ~2x its byte roofline)
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int vi = threadIdx.x + i * blockDim.x;
+      if (dres && vi < nvec) load8(dres + base + vi * 8, rr[i]);
+    }
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int vi = threadIdx.x + i * blockDim.x;
@@ -150,10 +158,8 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = rstd * (gy[i][j] - m1 - xh[i][j] * m2);
         if (dres) {
-          float r[8];
-          load8(dres + base + vi * 8, r);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] += r[j];
+          for (int j = 0; j < 8; ++j) o[j] += rr[i][j];
         }
         store8(dx + base + vi * 8, o);
       }
@@ -357,7 +363,9 @@ KCA_API int kca_layernorm_fwd(const void* x, const void* r1, const void* r2,
 
 // workspace: 2 * nparts * d floats, nparts = kca_layernorm_bwd_parts(rows).
 KCA_API int kca_layernorm_bwd_parts(int rows) {
-  return rows < 512 ? (rows > 0 ? rows : 1) : 512;
+  // 1024 workgroups (4 per CU) keep more rows' loads in flight than 512 did; the partials grow to
+  // 2 x 1024 x d floats (32 MB at d = 4096), reduced by col_reduce
+  return rows < 1024 ? (rows > 0 ? rows : 1) : 1024;
 }
 
 KCA_API int kca_layernorm_bwd(const void* dy, const void* h, const float* mean,

@@ -191,7 +191,9 @@ class CausalLM(nn.Module):
         if cfg.tie_embeddings:
             self.lm_head = None
         else:
-            self.lm_head = nn.Linear(d, cfg.vocab_size, bias=cfg.lm_head_bias)
+            # TLinear: dX of the LM head as a TN GEMM off a transposed weight copy (the NN dgrad ran at
+            # ~1.1 PF/s, 12 ms of the GPT-J step: profiles/gptj_step_kernel_stats_r4.md)
+            self.lm_head = TLinear(d, cfg.vocab_size, bias=cfg.lm_head_bias)
         self.gradient_checkpointing = False
 
     # ------------------------------------------------------------------ init
@@ -267,7 +269,7 @@ class CausalLM(nn.Module):
         self.wte = new
         if self.lm_head is not None:
             oh = self.lm_head
-            nh = nn.Linear(oh.in_features, n, bias=oh.bias is not None).to(old.device, old.dtype)
+            nh = TLinear(oh.in_features, n, bias=oh.bias is not None).to(old.device, old.dtype)
             with torch.no_grad():
                 nh.weight.normal_(0.0, 0.02)
                 nh.weight[:k] = oh.weight[:k]

@@ -245,14 +245,17 @@ class _TembAdds:
 # disables it, KCA_SD_PAD_HEADS_TRAIN=0 only in training. _PAD_GEN counts padded-weight rebuilds so a HIP
 # graph captured over the old buffers knows to re-capture (sd_pipeline.UNetGraph).
 _TILED_DIMS = (64, 96, 128, 160, 256)  # attention_tiled.hip instantiations (fwd + bwd)
-# forward-only narrow storage: heads stored 48 wide, staged into the D=64 LDS image
-# (attention_tiled.hip StagerNarrow); KCA_SD_NARROW_HEADS=0 pads inference heads to 64 as training does
+# narrow storage: heads stored 48 wide, staged into the D=64 LDS images of the forward and of both
+# backward kernels (attention_tiled.hip StagerNarrow, DS = 48); KCA_SD_NARROW_HEADS=0 pads inference
+# heads to 64, KCA_SD_NARROW_TRAIN=0 training heads
 _NARROW = os.environ.get("KCA_SD_NARROW_HEADS", "1") not in ("0", "false")
+_NARROW_TRAIN = os.environ.get("KCA_SD_NARROW_TRAIN", "1") not in ("0", "false")
 
 
 def padded_head_dim(hd: int, infer: bool = False) -> int:
-    """Smallest full-tile head dim >= hd: 40 -> 64 (inference: 48), 80 -> 96 (160 runs natively)."""
-    dims = ((48,) if infer and _NARROW else ()) + _TILED_DIMS
+    """Smallest full-tile head dim >= hd: 40 -> 48 (64 with the narrow path off), 80 -> 96 (160 runs
+    natively)."""
+    dims = ((48,) if (_NARROW if infer else _NARROW_TRAIN) else ()) + _TILED_DIMS
     return next((d for d in dims if d >= hd), hd)
 
 

@@ -269,6 +269,21 @@ def decode_attention_reference(q, k_cache, v_cache, slots, kv_lens, n_heads, sca
 
 
 # --------------------------------------------------------------- sampling
+_CNT: dict = {}
+
+
+def _sample_counters(dev: torch.device, B: int):
+    """Zeroed per-row arrival counters of the multi-workgroup sampler (decode.hip sample_mwg_kernel
+    re-arms them). Allocated outside graph capture (the runner warms up eagerly first); None inside
+    a capture that would need a new buffer, which keeps those rows on the one-workgroup kernels."""
+    c = _CNT.get(dev)
+    if c is None or c.numel() < B:
+        if torch.cuda.is_current_stream_capturing():
+            return None
+        c = _CNT[dev] = torch.zeros(max(4096, B), dtype=torch.int32, device=dev)
+    return c
+
+
 def sample_logits(logits: torch.Tensor, *, temperature: torch.Tensor, top_k: torch.Tensor,
                   top_p: torch.Tensor, rep_penalty: torch.Tensor | None = None,
                   seen: torch.Tensor | None = None, slots: torch.Tensor | None = None,
@@ -291,11 +306,12 @@ def sample_logits(logits: torch.Tensor, *, temperature: torch.Tensor, top_k: tor
             ws = torch.empty(B * V, device=dev, dtype=torch.float32)
         assert logits.stride(-1) == 1
         n_ban = ban_ids.shape[1] if ban_ids is not None else 0
+        cnt = _sample_counters(dev, B)
         _lib.call("kca_sample_logits", logits.data_ptr(), logits.stride(0),
                   int(logits.dtype == torch.bfloat16), B, V, temperature.data_ptr(), top_k.data_ptr(),
                   top_p.data_ptr(), _lib.ptr(rep_penalty), _lib.ptr(seen), _lib.ptr(slots),
                   _lib.ptr(ban_ids), n_ban, _lib.ptr(seeds), int(step), ws.data_ptr(),
-                  out_ids.data_ptr(), out_logprobs.data_ptr(), _lib.ptr(out_kept), _lib.stream())
+                  out_ids.data_ptr(), out_logprobs.data_ptr(), _lib.ptr(out_kept), _lib.ptr(cnt), _lib.stream())
         return out_ids, out_logprobs
     return sample_logits_reference(logits, temperature, top_k, top_p, rep_penalty, seen, slots, ban_ids,
                                    seeds, step, out_ids, out_logprobs, out_kept)

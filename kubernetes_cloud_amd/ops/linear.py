@@ -109,8 +109,10 @@ class TLinear(nn.Linear):
         self._tn = False
 
     def enable_tn(self, on: bool = True):
+        # any 8-aligned shape: dX always runs TN off weight_t; dW only when dY / X tile by 64
+        # (the LM head's 50400 rows take the NT dW and the torch transpose for weight_t)
         self._tn = bool(on) and self.weight.is_cuda and self.weight.dtype == torch.bfloat16 \
-            and self.weight.shape[0] % 64 == 0 and self.weight.shape[1] % 64 == 0
+            and self.weight.shape[0] % 8 == 0 and self.weight.shape[1] % 8 == 0
         self.weight_t = torch.empty(self.weight.shape[1], self.weight.shape[0], device=self.weight.device,
                                     dtype=self.weight.dtype) if self._tn else None
         self.refresh_transposed()
@@ -119,6 +121,9 @@ class TLinear(nn.Linear):
     def refresh_transposed(self):
         if self.weight_t is not None:
             w = self.weight.detach()
+            if not _tn_ok(w):
+                self.weight_t.copy_(w.t())
+                return
             _lib.call("kca_transpose_bf16", w.data_ptr(), w.stride(0), self.weight_t.data_ptr(), w.shape[0],
                       w.shape[0], w.shape[1], _lib.stream())
 

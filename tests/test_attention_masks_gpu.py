@@ -185,8 +185,36 @@ def test_narrow_48_storage_matches_reference(rowsum):
 def test_unet_inference_heads_are_48_wide():
     from kubernetes_cloud_amd.models import unet
     assert unet.padded_head_dim(40, infer=True) == 48
-    assert unet.padded_head_dim(40) == 64  # training keeps the fwd+bwd D=64 kernels
+    assert unet.padded_head_dim(40) == (48 if unet._NARROW_TRAIN else 64)  # fwd + bwd narrow kernels
     assert unet.padded_head_dim(80, infer=True) == 96
+
+
+def test_narrow_48_backward_matches_fp32_reference():
+    """Training heads stored 48 wide (40 real + 8 zero) in ONE fused QKV buffer
+    (models/unet.py, ops.qkv_rope_attention): the DS = 48 dQ and dK/dV kernels
+    (attention_tiled.hip, D = 64 images, pad chunks zeroed in LDS) give the fp32
+    reference gradients on the 40 real dims, zeros on the pad, and are the ones that ran."""
+    torch.manual_seed(17)
+    B, S, H = 2, 1024, 8
+    base = torch.zeros(B, S, 3, H, 48, device=DEV)
+    base[..., :40] = torch.randn(B, S, 3, H, 40, device=DEV)
+    qkv = base.bfloat16().view(B, S, 3 * H * 48).requires_grad_(True)
+    g = torch.randn(B, S, H, 48, device=DEV).bfloat16()
+    g[..., 40:] = 0
+    with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CUDA]) as prof:
+        o = ops.qkv_rope_attention(qkv, H, 48, 0, False, causal=False, scale=40 ** -0.5)
+        o.backward(g.view(B, S, H * 48))
+        torch.cuda.synchronize()
+    ref_in = qkv.detach().float().view(B, S, 3, H, 48)[..., :40].clone().requires_grad_(True)
+    ro, _ = attention_reference(ref_in[:, :, 0], ref_in[:, :, 1], ref_in[:, :, 2], False, 40 ** -0.5)
+    ro.backward(g[..., :40].float())
+    gq = qkv.grad.view(B, S, 3, H, 48)
+    assert float(gq[..., 40:].float().abs().max()) == 0.0
+    for i in range(3):
+        assert _rel(gq[:, :, i, :, :40], ref_in.grad[:, :, i]) < 2e-2, i
+    names = [e.name for e in prof.events()]
+    for kern in ("attn_bwd_dq_tiled", "attn_bwd_dkdv_tiled"):
+        assert any(kern in n and "48" in n for n in names), (kern, sorted(set(names))[:12])
 
 
 def test_narrow_48_max_column_matches_reference():

@@ -642,3 +642,47 @@ def test_decode_linear_gelu_many_rows(act):
     y = skinny_linear(x, w, b, act)
     ref = F.gelu(x.float() @ w.float().t() + b.float(), approximate="tanh" if act == 1 else "none")
     assert (y.float() - ref).abs().max() < 3e-2
+
+
+def test_sample_multiworkgroup_distribution_and_mixed_rows():
+    """GPT-J vocabulary, bf16: rows with 1 <= top_k <= 64 (or greedy) take the multi-workgroup sampler
+    (16 chunk workgroups + a last-arriver merge), the others the register kernel, in one call."""
+    torch.manual_seed(7)
+    V, B, k, p = 50400, 4096, 12, 0.9
+    # distinct (bf16-exact) peaks so the top-k / top-p cuts fall between values, not inside a tie group
+    # (the kernels keep a whole tie group at a cut; HF's sort keeps an arbitrary part of it)
+    base = torch.randn(V, device=dev) * 0.5
+    peaks = torch.randperm(V, device=dev)[:20]
+    base[peaks] = 4.0 + 0.25 * torch.arange(20, device=dev, dtype=torch.float32)
+    base = base.to(torch.bfloat16).float()
+    logits = base[None].expand(B, V).contiguous().to(torch.bfloat16)
+    seeds = torch.randint(0, 2**62, (B,), device=dev)
+    kept = torch.empty(B, dtype=torch.int32, device=dev)
+    ids, lp = dops.sample_logits(logits, **_params(B, 1.0, k, p), seeds=seeds, out_kept=kept)
+    keep = dops.keep_mask_reference(base, k, p)
+    assert bool(keep[ids].all())
+    assert int(kept.min()) == int(kept.max()) == int(keep.sum())
+    probs = torch.where(keep, base, torch.full_like(base, -float("inf"))).softmax(-1)
+    freq = torch.bincount(ids, minlength=V).float() / B
+    assert (freq - probs).abs().max() < 0.03
+    assert torch.allclose(lp, torch.log_softmax(base, -1)[ids], atol=1e-3)
+    # mixed batch: greedy / top-k (multi-workgroup) and top-p only / top-k 100 (register kernel)
+    rows = [(0.0, 0, 1.0), (1.0, 50, 0.95), (1.0, 0, 0.9), (0.8, 100, 1.0), (1.0, 10, 1.0), (1.2, 64, 0.5)]
+    Bm = len(rows)
+    lg = (torch.randn(Bm, V, device=dev) * 3).to(torch.bfloat16)
+    t = torch.tensor([r[0] for r in rows], device=dev)
+    kk = torch.tensor([r[1] for r in rows], device=dev, dtype=torch.int32)
+    pp = torch.tensor([r[2] for r in rows], device=dev)
+    out_kept = torch.empty(Bm, dtype=torch.int32, device=dev)
+    ids = torch.full((Bm,), -7, dtype=torch.int64, device=dev)
+    dops.sample_logits(lg, temperature=t, top_k=kk, top_p=pp, rep_penalty=torch.ones(Bm, device=dev),
+                       seeds=torch.arange(Bm, device=dev), out_ids=ids, out_kept=out_kept)
+    assert int(ids[0]) == int(lg[0].float().argmax())
+    for b, (tb, kb, pb) in enumerate(rows):
+        if tb <= 0:
+            continue
+        x = lg[b].float() / tb
+        keep = dops.keep_mask_reference(x, kb, pb)
+        tie_incl = x >= x[keep].min()  # the kernels keep whole tie groups at a cut
+        assert bool(tie_incl[ids[b]]), (b, rows[b])
+        assert int(keep.sum()) <= int(out_kept[b]) <= int(tie_incl.sum()) + 1, (b, rows[b])
