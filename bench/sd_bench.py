@@ -43,6 +43,34 @@ def build(dev, dtype):
     return unet, vae, te
 
 
+def _attrib(step):
+    """--attrib: one step under torch.profiler; the eager PyTorch (at::native) kernels and the device
+    copies grouped by the aten op that launched them and its nearest repo stack frame (stderr)."""
+    import collections
+
+    from torch.profiler import ProfilerActivity, profile
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True,
+                 with_stack=True) as prof:
+        step()
+        torch.cuda.synchronize()
+    agg, total, eager = collections.defaultdict(lambda: [0, 0.0]), 0.0, 0.0
+    for ev in prof.events():
+        for k in getattr(ev, "kernels", []) or []:
+            us = k.duration
+            total += us
+            if "at::native" not in k.name and "rocclr" not in k.name:
+                continue
+            eager += us
+            frame = next((f for f in (ev.stack or []) if "kubernetes_cloud_amd" in f or "bench/" in f), "?")
+            key = (ev.name, str(ev.input_shapes)[:90], frame.split("kubernetes_cloud_amd/")[-1][:70])
+            agg[key][0] += 1
+            agg[key][1] += us
+    print(f"[sd_bench attrib] kernel time {total / 1e3:.1f} ms, eager/copy {eager / 1e3:.2f} ms "
+          f"({100 * eager / max(total, 1):.2f} %)", file=sys.stderr)
+    for (name, shp, fr), (n, us) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:40]:
+        print(f"  {us:9.1f} us {n:4d}x {name:28s} {fr:70s} {shp}", file=sys.stderr)
+
+
 def bench_train(args, dev):
     from kubernetes_cloud_amd.models.schedulers import DDPMScheduler, sd_scheduler_config
     from kubernetes_cloud_amd.ops import mse_loss
@@ -92,6 +120,8 @@ def bench_train(args, dev):
         torch.cuda.synchronize()
         print(f"[sd_bench] train warmup {i}: {time.perf_counter() - tw:.1f}s", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
+    if getattr(args, "attrib", False):
+        _attrib(step)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
@@ -162,6 +192,7 @@ def main():
     ap.add_argument("--tunableop", choices=["auto", "use", "tune", "off"], default="auto",
                     help="hipBLASLt solution choices from tuning/tunableop_sd.csv (utils/tunable.py)")
     ap.add_argument("--tunableop-file", default=None)
+    ap.add_argument("--attrib", action="store_true", help="train: attribute eager kernels of one step (stderr)")
     args = ap.parse_args()
     if args.deterministic:
         torch.backends.cudnn.deterministic = True

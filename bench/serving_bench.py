@@ -40,7 +40,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch
 
-LEVELS = ((1, 8), (8, 32), (32, 96))  # (concurrency, requests)
+LEVELS = ((1, 8), (8, 64), (32, 256))  # (concurrency, requests): ~8 requests per connection at 32
 
 
 def _free_port() -> int:

@@ -632,9 +632,13 @@ __device__ __forceinline__ bf16x8 as_bf8(u32x2 lo, u32x2 hi) {
   return *reinterpret_cast<bf16x8*>(&x);
 }
 
-template <int D, bool CAUSAL>
-__global__ void __launch_bounds__(512, 1) attn_fwd_w8_kernel(FastFwdParams p) {
-  constexpr int BM = 256, BN = 32, NW = 8, NBUF = 4;
+// NW = 4, NBUF = 2, D = 512 (non-causal): the VAE mid-block's single 512-wide head (one wave per
+// SIMD, O^T = 256 registers, Q^T fragments 128; two 64-KiB stages, the next tile's DMA in flight
+// under the current tile). Inference only: the overflow flags go back to the caller, which has no
+// generic D = 512 kernel to fix rows up with and reruns flagged calls on the GEMM path.
+template <int D, bool CAUSAL, int NW = 8, int NBUF = 4>
+__global__ void __launch_bounds__(NW * 64, 1) attn_fwd_w8_kernel(FastFwdParams p) {
+  constexpr int BM = NW * 32, BN = 32;
   constexpr int TILE = BN * D * 2;            // one K or V image
   constexpr int STAGE = 2 * TILE;
   constexpr int KS = D / 16;
@@ -642,7 +646,8 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_w8_kernel(FastFwdParams p) {
   constexpr int PPW = PIECES / NW;            // per wave per image
   constexpr int LEAD = NBUF - 1;                  // tiles issued ahead of the one computed
   constexpr int INFLIGHT = (LEAD - 1) * 2 * PPW;  // DMA instructions issued after tile t when t is waited
-  static_assert(D == 256 || D == 128, "8-wave forward: D = 128 / 256");
+  static_assert(((D == 256 || D == 128) && NW == 8) || (D == 512 && NW == 4 && NBUF == 2 && !CAUSAL),
+                "multi-wave LDS-DMA forward: 8 waves at D = 128 / 256, 4 waves at D = 512");
   static_assert(PPW >= 1 && PIECES % NW == 0, "whole pieces per wave");
   constexpr int SMEM = (NBUF * STAGE > NW * 32 * D * 2) ? NBUF * STAGE : NW * 32 * D * 2;
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];  // [buf][K|V]; epilogue: [wave][32][D]
@@ -677,16 +682,18 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_w8_kernel(FastFwdParams p) {
   // byte 1024 j + 16 L, i.e. (row, chunk) = img_off^-1 of it
   const __amdgpu_buffer_rsrc_t rk = head_rsrc(p.k + b * p.k_sb + hk * p.k_sh);
   const __amdgpu_buffer_rsrc_t rv = head_rsrc(p.v + b * p.v_sb + hk * p.v_sh);
-  int kvo[PPW], vvo[PPW];
-#pragma unroll
-  for (int i = 0; i < PPW; ++i) {
-    const int byte = 1024 * (wave * PPW + i) + 16 * lane;
+  // A wave's PPW pieces lie in one 8-row group (D / 64 pieces per group), piece i of them 2 sub-tiles
+  // = 8 chunks = 128 source bytes after piece 0: one per-lane offset, the rest a scalar add
+  static_assert((D / 64) % PPW == 0, "a wave's pieces within one row group");
+  int kvo, vvo;
+  {
+    const int byte = 1024 * (wave * PPW) + 16 * lane;
     const int rg = byte / (16 * D), rem = byte % (16 * D);
     const int chh = rem / 512, w5 = rem % 512;
     const int row = rg * 8 + w5 / 64;
     const int ch = chh * 4 + (((w5 % 64) / 16) ^ ((row >> 2) & 3));
-    kvo[i] = (int)(((long long)row * p.k_st + ch * 8) * 2);
-    vvo[i] = (int)(((long long)row * p.v_st + ch * 8) * 2);
+    kvo = (int)(((long long)row * p.k_st + ch * 8) * 2);
+    vvo = (int)(((long long)row * p.v_st + ch * 8) * 2);
   }
   typedef __attribute__((address_space(3))) char lds_char;
   lds_char* lsm = (lds_char*)smem;
@@ -698,9 +705,9 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_w8_kernel(FastFwdParams p) {
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (void __attribute__((address_space(3)))*)(
-          lsm + buf * STAGE + 1024 * (wave * PPW + i)), 16, kvo[i], sok, 0, 0);
+          lsm + buf * STAGE + 1024 * (wave * PPW + i)), 16, kvo, sok + 128 * i, 0, 0);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (void __attribute__((address_space(3)))*)(
-          lsm + buf * STAGE + TILE + 1024 * (wave * PPW + i)), 16, vvo[i], sov, 0, 0);
+          lsm + buf * STAGE + TILE + 1024 * (wave * PPW + i)), 16, vvo, sov + 128 * i, 0, 0);
     }
 #endif
   };
@@ -1329,6 +1336,24 @@ KCA_API int kca_attn_fwd_tiled(const void* q, const void* k, const void* v, void
   }
   // a failed launch leaves the flags unwritten: report it so the caller runs
   // the generic kernel on every block instead of trusting stale flags
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+// The VAE's single 512-wide head (non-causal, no masks): 0 = launched (flags[4 * (Sq/128) * B * H]
+// hold per-32-row overflow marks the caller must check), 1 = shape outside this path.
+KCA_API int kca_attn_fwd_wide(const void* q, const void* k, const void* v, void* o, float* lse, long long q_sb,
+                              long long q_st, long long q_sh, long long k_sb, long long k_st, long long k_sh,
+                              long long v_sb, long long v_st, long long v_sh, long long o_sb, long long o_st,
+                              long long o_sh, int B, int Sq, int Sk, int H, int Hkv, int d, float scale, int* flags,
+                              hipStream_t stream) {
+  if (d != 512 || Sq % 128 || Sk % 32 || Sq <= 0 || Sk <= 0 || H % Hkv || !flags) return 1;
+  if (!offsets_fit(Sk, k_st) || !offsets_fit(Sk, v_st)) return 1;
+  if ((q_st | k_st | v_st | o_st) % 8) return 1;  // 16-B row chunks
+  FastFwdParams p{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, lse, flags,
+                  q_sb, q_st, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh, o_sb, o_st, o_sh,
+                  B, Sq, Sk, H, Hkv, scale};
+  (void)hipGetLastError();
+  hipLaunchKernelGGL((attn_fwd_w8_kernel<512, false, 4, 2>), dim3((Sq / 128) * B * H), dim3(256), 0, stream, p);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

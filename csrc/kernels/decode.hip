@@ -1833,15 +1833,34 @@ __global__ __launch_bounds__(NT) void sample_reg_kernel(
 constexpr int MWG_G = 16, MWG_NT = 256, MWG_CMAX = 128, MWG_KMAX = MWG_KMAX_;
 constexpr int MWG_PART = 8;  // floats per workgroup partial: max, sum, t_g (key bits), count, argmax
 
+// Wave sum of a uint32 (every lane gets it): DPP quad swaps and row mirrors within 16 lanes, then
+// two cross-row steps.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_mov_u(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+  v += dpp_mov_u<0xB1>(v);
+  v += dpp_mov_u<0x4E>(v);
+  v += dpp_mov_u<0x141>(v);
+  v += dpp_mov_u<0x140>(v);
+  v += (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401F);  // xor 16 within 32 lanes
+  v += (uint32_t)__shfl_xor((int)v, 32, 64);
+  return v;
+}
+
 // 4-bit radix select of the k-th largest key over (key, valid) pairs spread across the block:
-// per-thread packed 8-bit counters (<= 255 elements per thread), wave sums of 16-bit pairs, digit
-// pick by thread 0. Returns the key prefix (ties at it kept); 0 when fewer than k are valid.
+// per-thread packed 8-bit counters (<= 255 elements per thread), DPP wave sums of 16-bit pairs into
+// a double-buffered LDS table (one barrier per pass), and the digit picked redundantly by every lane
+// from that table (no broadcast round). Returns the key prefix (ties at it kept); 0 when fewer than
+// k are valid. cnt16: 2 x (blockDim/64) x 8 words.
 template <int EPT, typename KeyFn>
-__device__ uint32_t block_kth_key(int k, KeyFn key_of, uint32_t* cnt16, int* sel) {
+__device__ uint32_t block_kth_key(int k, KeyFn key_of, uint32_t* cnt16) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = blockDim.x >> 6;
   uint32_t prefix = 0, mask = 0;
   int remaining = k;
-  for (int shift = 28; shift >= 0; shift -= 4) {
+  int pass = 0;
+  for (int shift = 28; shift >= 0; shift -= 4, ++pass) {
     uint32_t w4[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
     for (int e = 0; e < EPT; ++e) {
@@ -1854,42 +1873,33 @@ __device__ uint32_t block_kth_key(int k, KeyFn key_of, uint32_t* cnt16, int* sel
         w4[3] += d >= 12 ? inc : 0u;
       }
     }
-    uint32_t w8[8];
+    uint32_t* tab = cnt16 + (pass & 1) * nw * 8;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      w8[2 * q] = (w4[q] & 0xffu) | ((w4[q] & 0xff00u) << 8);
-      w8[2 * q + 1] = ((w4[q] >> 16) & 0xffu) | ((w4[q] >> 8) & 0xff0000u);
-    }
-#pragma unroll
-    for (int q = 0; q < 8; ++q)
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) w8[q] += __shfl_xor(w8[q], o, 64);
-    __syncthreads();
-    if (lane < 8) {
-      uint32_t mine = w8[0];
-#pragma unroll
-      for (int q = 1; q < 8; ++q)
-        if (lane == q) mine = w8[q];
-      cnt16[wid * 8 + lane] = mine;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      int run = 0, dsel = -1;
-      for (int j = 15; j >= 0; --j) {
-        uint32_t t = 0;
-        for (int w = 0; w < nw; ++w) t += cnt16[w * 8 + (j >> 1)];
-        const int c = (int)((j & 1) ? (t >> 16) : (t & 0xffffu));
-        if (run + c >= remaining) {
-          dsel = j;
-          break;
-        }
-        run += c;
+      const uint32_t lo = wave_sum_u32((w4[q] & 0xffu) | ((w4[q] & 0xff00u) << 8));
+      const uint32_t hi = wave_sum_u32(((w4[q] >> 16) & 0xffu) | ((w4[q] >> 8) & 0xff0000u));
+      if (lane == 0) {
+        tab[wid * 8 + 2 * q] = lo;
+        tab[wid * 8 + 2 * q + 1] = hi;
       }
-      sel[0] = dsel;
-      sel[1] = run;
     }
     __syncthreads();
-    const int dsel = sel[0], run = sel[1];
+    // digit j's count: 16-bit half (j & 1) of word j >> 1, summed over the waves
+    uint32_t words[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) words[q] = 0u;
+    for (int w = 0; w < nw; ++w)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) words[q] += tab[w * 8 + q];
+    int run = 0, dsel = -1;
+#pragma unroll
+    for (int j = 15; j >= 0; --j) {
+      const int c = (int)((j & 1) ? (words[j >> 1] >> 16) : (words[j >> 1] & 0xffffu));
+      if (dsel < 0) {
+        if (run + c >= remaining) dsel = j;
+        else run += c;
+      }
+    }
     if (dsel < 0) return 0u;  // fewer than k valid: keep every valid element
     prefix |= (uint32_t)dsel << shift;
     mask |= 15u << shift;
@@ -1908,14 +1918,13 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
     unsigned int* __restrict__ cnt, long long* __restrict__ out_ids, float* __restrict__ out_lp,
     int* __restrict__ out_kept) {
   __shared__ float red[MWG_NT / 64];
-  __shared__ uint32_t cnt16[MWG_NT / 64 * 8];
+  __shared__ uint32_t cnt16[2 * MWG_NT / 64 * 8];
   __shared__ int sel[2];
   __shared__ int iscan[MWG_NT / 64];
   __shared__ int sh_last;
   __shared__ float Lv[MWG_G * MWG_CMAX];
   __shared__ int Li[MWG_G * MWG_CMAX];
-  __shared__ float hist[16];
-  __shared__ float selp[2];
+  __shared__ float hist[48];
   __shared__ int goff[MWG_G + 1];
   const int g = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const float T = temperature ? temperature[b] : 1.f;
@@ -1987,7 +1996,7 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
     tg = block_kth_key<VPT>(k, [&](int e, uint32_t& key) {
       key = fkey(x[e]);
       return x[e] != -INFINITY;
-    }, cnt16, sel);
+    }, cnt16);
     int c = 0;
 #pragma unroll
     for (int e = 0; e < VPT; ++e) c += (x[e] != -INFINITY && fkey(x[e]) >= tg) ? 1 : 0;
@@ -2127,43 +2136,44 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
     if (e >= E2 || j >= n) return false;
     key = fkey(Lv[j]);
     return true;
-  }, cnt16, sel);
+  }, cnt16);
   // top-p over the survivors: the smallest key whose descending inclusive mass reaches p * kept mass
   const float pp = top_p ? top_p[b] : 1.f;
   if (pp < 1.f) {
     uint32_t prefix = 0, mask = 0;
     float above = 0.f, target = -1.f;
-    for (int shift = 28; shift >= 0; shift -= 4) {
-      if (tid < 16) hist[tid] = 0.f;
-      __syncthreads();
+    // triple-buffered histogram: pass p accumulates into buffer p % 3 and, after its barrier,
+    // clears buffer (p + 2) % 3 (read in pass p - 1, filled in pass p + 2); every lane picks the
+    // digit from its own read of the table (no broadcast round)
+    if (tid < 48) hist[tid] = 0.f;
+    __syncthreads();
+    int pass = 0;
+    for (int shift = 28; shift >= 0; shift -= 4, ++pass) {
+      float* hb = hist + 16 * (pass % 3);
       for (int j = tid; j < n; j += MWG_NT) {
         const uint32_t key = fkey(Lv[j]);
-        if (key >= thr && (key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 15u], __expf(Lv[j] - M));
+        if (key >= thr && (key & mask) == prefix) atomicAdd(&hb[(key >> shift) & 15u], __expf(Lv[j] - M));
       }
       __syncthreads();
-      if (tid == 0) {
-        if (target < 0.f) {
-          float t = 0.f;
-          for (int j = 0; j < 16; ++j) t += hist[j];
-          target = pp * t;
-        }
-        float run = 0.f;
-        int dsel = -1;
-        for (int j = 15; j >= 0; --j) {
-          if (hist[j] > 0.f && run + hist[j] >= target - above) {
-            dsel = j;
-            break;
-          }
-          run += hist[j];
-        }
-        sel[0] = dsel;
-        selp[0] = run;
-        selp[1] = target;
+      float hv[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) hv[j] = hb[j];
+      if (tid < 16) hist[16 * ((pass + 2) % 3) + tid] = 0.f;
+      if (target < 0.f) {
+        float t = 0.f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) t += hv[j];
+        target = pp * t;
       }
-      __syncthreads();
-      const int dsel = sel[0];
-      const float run = selp[0];
-      target = selp[1];
+      float run = 0.f;
+      int dsel = -1;
+#pragma unroll
+      for (int j = 15; j >= 0; --j) {
+        if (dsel < 0) {
+          if (hv[j] > 0.f && run + hv[j] >= target - above) dsel = j;
+          else run += hv[j];
+        }
+      }
       if (dsel < 0) {
         prefix = 0;
         mask = 0;

@@ -56,11 +56,15 @@ class VAEConfig:
 
 def _wide_head_attention(q, k, v, scale):
     """Single-head attention over [B, S, C] with C > 256 (the VAE mid-block,
-    C = 512, S = 4096 at 512 px). bf16 operands on the MFMA GEMM path with the
-    logits produced in fp32 (``out_dtype``) and an fp32 softmax; the previous
-    all-fp32 einsum ran the two GEMMs at ~150 TFLOP/s (1.8 ms each at B16 in
-    the DreamBooth step's VAE encode)."""
+    C = 512, S = 4096 at 512 px). Inference: the 512-wide LDS-DMA flash kernel
+    (ops.attention.wide_head_attention; no [B, S, S] scores). Otherwise (autograd,
+    odd shapes, a flagged softmax overflow) bf16 operands on the MFMA GEMM path
+    with the logits produced in fp32 (``out_dtype``) and an fp32 softmax."""
     global _BMM_OUT_DTYPE
+    if _FLASH_WIDE:
+        o = ops.attention.wide_head_attention(q, k, v, scale)
+        if o is not None:
+            return o
     if q.is_cuda and q.dtype == torch.bfloat16 and _BMM_OUT_DTYPE is not False:
         try:  # aten::bmm.dtype (bf16 in, fp32 out) is a GPU-only kernel
             s = torch.bmm(q, k.transpose(1, 2), out_dtype=torch.float32)
@@ -75,6 +79,7 @@ def _wide_head_attention(q, k, v, scale):
 
 
 _BMM_OUT_DTYPE = None  # probed on the first GPU call
+_FLASH_WIDE = os.environ.get("KCA_VAE_FLASH", "1") not in ("0", "false")  # A/B knob
 
 
 class VAEAttention(nn.Module):
@@ -96,7 +101,7 @@ class VAEAttention(nn.Module):
         q, k, v = self.to_q(h), self.to_k(h), self.to_v(h)
         if C <= 256:
             o = ops.flash_attention(q[:, :, None], k[:, :, None], v[:, :, None], causal=False)[:, :, 0]
-        else:  # head_dim 512 > the flash kernels' 256: two library GEMMs around an fp32 softmax
+        else:  # head_dim 512: the wide flash kernel (inference) or two GEMMs around an fp32 softmax
             o = _wide_head_attention(q, k, v, C ** -0.5)
         o = self.to_out[0](o)
         return x + o.transpose(1, 2).reshape(B, C, H, W)

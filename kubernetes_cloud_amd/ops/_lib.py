@@ -62,6 +62,7 @@ _SIGS = {
     "kca_attn_fwd": [P] * 5 + [LL] * 12 + [I] * 7 + [F, P, P, I, P, I, I, P, P],
     "kca_attn_bwd_preprocess": [P, P, P, LL, LL, LL, LL, LL, LL, I, I, I, I, P],
     "kca_attn_bwd": [P] * 10 + [LL] * 21 + [I] * 7 + [F, P, P, I, P, P],
+    "kca_attn_fwd_wide": [P] * 5 + [LL] * 12 + [I] * 6 + [F, P, P],
     "kca_attn_set_tiled": [I],
     "kca_attn_set_variant": [I],
     "kca_transpose_bf16": [P, LL, P, LL, I, I, P],
@@ -167,6 +168,15 @@ def call(name: str, *args):
             torch.cuda.synchronize()
         except RuntimeError as e:  # pragma: no cover - needs a faulting kernel
             raise RuntimeError(f"GPU fault after native launch {name}: {e}") from e
+    return rc
+
+
+def call_rc(name: str, *args) -> int:
+    """``call`` for entry points whose nonzero status means "shape outside this kernel" (the caller
+    takes another path) rather than an error."""
+    rc = getattr(require(), name)(*args)
+    if rc == 0 and SYNC_LAUNCH and torch.cuda.is_available():
+        torch.cuda.synchronize()
     return rc
 
 

@@ -203,6 +203,30 @@ def flash_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: b
     return o
 
 
+def wide_head_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float):
+    """Single-head attention over [B, S, 512] bf16 rows (the VAE mid-block, inference) on the
+    LDS-DMA flash kernel (attention_tiled.hip ``kca_attn_fwd_wide``). Returns None when the shape is
+    outside that kernel, or when a row's softmax overflowed its first-tile reference max (one flag
+    read back: the caller reruns those rare inputs on its GEMM path)."""
+    if not (_lib.use_native(q, k, v) and q.dim() == 3 and q.shape[-1] == 512 and not torch.is_grad_enabled()):
+        return None
+    if any(t.stride(-1) != 1 or t.dtype != torch.bfloat16 for t in (q, k, v)):
+        return None
+    B, Sq, D = q.shape
+    Sk = k.shape[1]
+    if Sq % 128 or Sk % 32:
+        return None
+    o = torch.empty(B, Sq, D, device=q.device, dtype=q.dtype)
+    flags = torch.empty(4 * (Sq // 128) * B, device=q.device, dtype=torch.int32)
+    st = lambda t: (t.stride(0), t.stride(1), 0)  # noqa: E731  (one head: head stride unused)
+    rc = _lib.call_rc("kca_attn_fwd_wide", q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), None,
+                      *st(q), *st(k), *st(v), *st(o), B, Sq, Sk, 1, 1, D, float(scale), flags.data_ptr(),
+                      _lib.stream())
+    if rc != 0 or bool(flags.any()):
+        return None
+    return o
+
+
 class _QKVRopeAttnFn(torch.autograd.Function):
     """qkv: [B, S, 3*H*D] fused projection output (consumed and rotated in place)."""
 

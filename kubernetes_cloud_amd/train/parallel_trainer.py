@@ -65,6 +65,8 @@ def build_parser():
     p.add_argument("--save-steps", type=int, default=0)
     p.add_argument("--seed", type=int, default=42)
     p.add_argument("--log-dir", default="")
+    p.add_argument("--local_rank", "--local-rank", type=int, default=-1,
+                   help="appended by the DeepSpeed-style launcher (kubernetes_cloud_amd.launch); LOCAL_RANK wins")
     return p
 
 

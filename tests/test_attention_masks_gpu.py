@@ -253,3 +253,38 @@ def test_unet_attention_max_column_matches_plain(monkeypatch):
         monkeypatch.setattr(unet, "_MAX_COL", False)
         plain = att(x)
     assert _rel(fast, plain) < 2e-2
+
+
+def test_wide_head_512_flash_matches_reference():
+    """The VAE mid-block's single 512-wide head on the 4-wave LDS-DMA flash kernel
+    (attention_tiled.hip attn_fwd_w8_kernel<512, false, 4, 2>) against the fp32 reference,
+    with no [B, S, S] score tensor or softmax kernel on the way."""
+    from kubernetes_cloud_amd.ops.attention import wide_head_attention
+    torch.manual_seed(19)
+    B, S, C = 2, 1024, 512
+    q, k, v = (torch.randn(B, S, C, device=DEV) * 0.5).bfloat16(), torch.randn(B, S, C, device=DEV).bfloat16(), \
+        torch.randn(B, S, C, device=DEV).bfloat16()
+    with torch.no_grad(), torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CUDA]) as prof:
+        o = wide_head_attention(q, k, v, C ** -0.5)
+        torch.cuda.synchronize()
+    assert o is not None
+    ref, _ = attention_reference(q[:, :, None], k[:, :, None], v[:, :, None], False, C ** -0.5)
+    assert _rel(o, ref[:, :, 0]) < 1e-2
+    names = [e.name for e in prof.events()]
+    assert any("attn_fwd_w8_kernel" in n and "512" in n for n in names), sorted(set(names))[:8]
+    assert not any("softmax" in n.lower() for n in names)
+
+
+def test_vae_mid_attention_uses_wide_flash():
+    from kubernetes_cloud_amd.models import vae as vae_mod
+    torch.manual_seed(23)
+    att = vae_mod.VAEAttention(512, 32).to(DEV).bfloat16().eval()
+    x = torch.randn(2, 512, 32, 32, device=DEV).bfloat16()
+    with torch.no_grad():
+        fast = att(x)
+        vae_mod._FLASH_WIDE = False
+        try:
+            slow = att(x)
+        finally:
+            vae_mod._FLASH_WIDE = True
+    assert _rel(fast, slow) < 1e-2

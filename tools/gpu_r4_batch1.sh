@@ -3,7 +3,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_attention_masks_gpu.py -x -q --timeout 200 --timeout-method thread -k "narrow or unet" > gpurun_out/narrow_tests_r4.log 2>&1 || { tail -30 gpurun_out/narrow_tests_r4.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_attention_masks_gpu.py -x -q --timeout 200 --timeout-method thread -k "narrow or unet or wide or vae" > gpurun_out/narrow_tests_r4.log 2>&1 || { tail -30 gpurun_out/narrow_tests_r4.log; exit 1; }
 tail -2 gpurun_out/narrow_tests_r4.log
 timeout -k 10 300 python -u -m pytest tests/test_decode_gpu.py -x -q --timeout 200 --timeout-method thread -k sample > gpurun_out/sampler_tests_r4.log 2>&1 || { tail -30 gpurun_out/sampler_tests_r4.log; exit 1; }
 tail -2 gpurun_out/sampler_tests_r4.log
