@@ -61,7 +61,10 @@ def _attrib(step):
             if "at::native" not in k.name and "rocclr" not in k.name:
                 continue
             eager += us
-            frame = next((f for f in (ev.stack or []) if "kubernetes_cloud_amd" in f or "bench/" in f), "?")
+            e, frame = ev, "?"
+            while e is not None and frame == "?":  # nearest ancestor op called from Python carries the stack
+                frame = next((f for f in (e.stack or []) if "kubernetes_cloud_amd" in f), "?")
+                e = getattr(e, "cpu_parent", None)
             key = (ev.name, str(ev.input_shapes)[:90], frame.split("kubernetes_cloud_amd/")[-1][:70])
             agg[key][0] += 1
             agg[key][1] += us

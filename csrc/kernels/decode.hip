@@ -1839,14 +1839,43 @@ template <int CTRL>
 __device__ __forceinline__ uint32_t dpp_mov_u(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
 }
+// (wave-uniform result: the four 16-lane row sums are read out with v_readlane -- no LDS crossbar
+// round trips, which at one dependent ds_swizzle / ds_bpermute pair per word made every radix pass
+// ~2 us, profiles/sampler_r4.txt)
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
   v += dpp_mov_u<0xB1>(v);
   v += dpp_mov_u<0x4E>(v);
   v += dpp_mov_u<0x141>(v);
   v += dpp_mov_u<0x140>(v);
-  v += (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401F);  // xor 16 within 32 lanes
-  v += (uint32_t)__shfl_xor((int)v, 32, 64);
-  return v;
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) + (uint32_t)__builtin_amdgcn_readlane((int)v, 16) +
+         (uint32_t)__builtin_amdgcn_readlane((int)v, 32) + (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov_f(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float rl(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
+__device__ __forceinline__ float wave_max_dpp(float v) {
+  v = fmaxf(v, dpp_mov_f<0xB1>(v));
+  v = fmaxf(v, dpp_mov_f<0x4E>(v));
+  v = fmaxf(v, dpp_mov_f<0x141>(v));
+  v = fmaxf(v, dpp_mov_f<0x140>(v));
+  return fmaxf(fmaxf(rl(v, 0), rl(v, 16)), fmaxf(rl(v, 32), rl(v, 48)));
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += dpp_mov_f<0xB1>(v);
+  v += dpp_mov_f<0x4E>(v);
+  v += dpp_mov_f<0x141>(v);
+  v += dpp_mov_f<0x140>(v);
+  return (rl(v, 0) + rl(v, 16)) + (rl(v, 32) + rl(v, 48));
+}
+__device__ __forceinline__ int wave_min_i(int v) {
+  v = min(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false));
+  v = min(v, __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false));
+  v = min(v, __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, false));
+  v = min(v, __builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, false));
+  return min(min(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+             min(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
 }
 
 // 4-bit radix select of the k-th largest key over (key, valid) pairs spread across the block:
@@ -1854,59 +1883,109 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 // a double-buffered LDS table (one barrier per pass), and the digit picked redundantly by every lane
 // from that table (no broadcast round). Returns the key prefix (ties at it kept); 0 when fewer than
 // k are valid. cnt16: 2 x (blockDim/64) x 8 words.
-template <int EPT, typename KeyFn>
-__device__ uint32_t block_kth_key(int k, KeyFn key_of, uint32_t* cnt16) {
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = blockDim.x >> 6;
+template <int EPT, int NW>
+__device__ uint32_t block_kth_key(int k, const uint32_t (&key)[EPT], const bool (&ok)[EPT], uint32_t* cnt16) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   uint32_t prefix = 0, mask = 0;
   int remaining = k;
   int pass = 0;
+#pragma unroll 1
   for (int shift = 28; shift >= 0; shift -= 4, ++pass) {
     uint32_t w4[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
     for (int e = 0; e < EPT; ++e) {
-      uint32_t key;
-      if (key_of(e, key) && (key & mask) == prefix) {
-        const uint32_t d = (key >> shift) & 15u, inc = 1u << ((d & 3u) << 3);
+      if (ok[e] && (key[e] & mask) == prefix) {
+        const uint32_t d = (key[e] >> shift) & 15u, inc = 1u << ((d & 3u) << 3);
         w4[0] += d < 4 ? inc : 0u;
         w4[1] += (d >> 2) == 1 ? inc : 0u;
         w4[2] += (d >> 2) == 2 ? inc : 0u;
         w4[3] += d >= 12 ? inc : 0u;
       }
     }
-    uint32_t* tab = cnt16 + (pass & 1) * nw * 8;
+    uint4* tab = reinterpret_cast<uint4*>(cnt16) + (pass & 1) * NW * 2;
+    uint32_t sw[8];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const uint32_t lo = wave_sum_u32((w4[q] & 0xffu) | ((w4[q] & 0xff00u) << 8));
-      const uint32_t hi = wave_sum_u32(((w4[q] >> 16) & 0xffu) | ((w4[q] >> 8) & 0xff0000u));
-      if (lane == 0) {
-        tab[wid * 8 + 2 * q] = lo;
-        tab[wid * 8 + 2 * q + 1] = hi;
-      }
+      sw[2 * q] = wave_sum_u32((w4[q] & 0xffu) | ((w4[q] & 0xff00u) << 8));
+      sw[2 * q + 1] = wave_sum_u32(((w4[q] >> 16) & 0xffu) | ((w4[q] >> 8) & 0xff0000u));
+    }
+    if (lane == 0) {
+      tab[wid * 2] = make_uint4(sw[0], sw[1], sw[2], sw[3]);
+      tab[wid * 2 + 1] = make_uint4(sw[4], sw[5], sw[6], sw[7]);
     }
     __syncthreads();
-    // digit j's count: 16-bit half (j & 1) of word j >> 1, summed over the waves
-    uint32_t words[8];
+    // digit j's count: 16-bit half (j & 1) of word j >> 1, summed over the waves (all 2 NW rows
+    // requested before the first use)
+    uint4 rows[2 * NW];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) words[q] = 0u;
-    for (int w = 0; w < nw; ++w)
+    for (int i = 0; i < 2 * NW; ++i) rows[i] = tab[i];
+    uint32_t words[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
 #pragma unroll
-      for (int q = 0; q < 8; ++q) words[q] += tab[w * 8 + q];
-    int run = 0, dsel = -1;
+    for (int w = 0; w < NW; ++w) {
+      words[0] += rows[2 * w].x; words[1] += rows[2 * w].y; words[2] += rows[2 * w].z; words[3] += rows[2 * w].w;
+      words[4] += rows[2 * w + 1].x; words[5] += rows[2 * w + 1].y; words[6] += rows[2 * w + 1].z;
+      words[7] += rows[2 * w + 1].w;
+    }
+    int run = 0, dsel = -1, csel = 0;
 #pragma unroll
     for (int j = 15; j >= 0; --j) {
       const int c = (int)((j & 1) ? (words[j >> 1] >> 16) : (words[j >> 1] & 0xffffu));
       if (dsel < 0) {
-        if (run + c >= remaining) dsel = j;
-        else run += c;
+        if (run + c >= remaining) {
+          dsel = j;
+          csel = c;
+        } else {
+          run += c;
+        }
       }
     }
     if (dsel < 0) return 0u;  // fewer than k valid: keep every valid element
     prefix |= (uint32_t)dsel << shift;
     mask |= 15u << shift;
     remaining -= run;
+    // the selected bucket holds exactly the elements still needed: every key >= prefix (lower
+    // bits zero) is in the top k -- done, the remaining passes would only walk that bucket down
+    if (csel == remaining) return prefix;
   }
   return prefix;
 }
+
+// Diagnostic build only (tools/build_ext.py --stamps, tools/sample_stamps.py): s_memtime segment
+// sums of the multi-workgroup sampler -- chunk phase of workgroup 0 of row 0 (slots 0..5) and the
+// merging workgroup of row 0 (slots 8..13); slot 15 counts launches. Empty in the normal build.
+#ifdef KCA_ATTN_STAMPS
+__device__ unsigned long long g_sample_stamps[16];
+__device__ __forceinline__ unsigned long long sst_now() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define SSTAMP_DECL unsigned long long sst_prev_ = sst_now();
+#define SSTAMP_COUNT(on) \
+  if ((on) && threadIdx.x == 0) atomicAdd(&g_sample_stamps[15], 1ull)
+#define SSTAMP(k, on)                                                   \
+  do {                                                                  \
+    const unsigned long long n_ = sst_now();                            \
+    if ((on) && threadIdx.x == 0) atomicAdd(&g_sample_stamps[k], n_ - sst_prev_); \
+    sst_prev_ = n_;                                                     \
+  } while (0)
+KCA_API int kca_sample_stamps(unsigned long long* out, int reset) {
+  if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sample_stamps), sizeof(g_sample_stamps)) != hipSuccess) return 2;
+  if (reset) {
+    unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_sample_stamps), z, sizeof(z)) != hipSuccess) return 2;
+  }
+  return 0;
+}
+#else
+#define SSTAMP_DECL
+#define SSTAMP_COUNT(on)
+#define SSTAMP(k, on) \
+  do {                \
+  } while (0)
+#endif
 
 template <int VPT>
 __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
@@ -1917,19 +1996,20 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
     const unsigned long long* __restrict__ seeds, long long step, float* __restrict__ ws,
     unsigned int* __restrict__ cnt, long long* __restrict__ out_ids, float* __restrict__ out_lp,
     int* __restrict__ out_kept) {
-  __shared__ float red[MWG_NT / 64];
-  __shared__ uint32_t cnt16[2 * MWG_NT / 64 * 8];
+  __shared__ float red[2 * MWG_NT / 64];
+  __shared__ __attribute__((aligned(16))) uint32_t cnt16[2 * MWG_NT / 64 * 8];
   __shared__ int sel[2];
   __shared__ int iscan[MWG_NT / 64];
   __shared__ int sh_last;
   __shared__ float Lv[MWG_G * MWG_CMAX];
   __shared__ int Li[MWG_G * MWG_CMAX];
-  __shared__ float hist[48];
-  __shared__ int goff[MWG_G + 1];
+  __shared__ __attribute__((aligned(16))) float hist[48];
   const int g = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const float T = temperature ? temperature[b] : 1.f;
   const int k = top_k ? top_k[b] : 0;
   if (!mwg_row(T, k)) return;  // sample_reg_kernel's row
+  SSTAMP_DECL
+  const bool st0 = g == 0 && b == 0;
   const bool greedy = !(T > 0.f);
   const float rp = rep_pen ? rep_pen[b] : 1.f;
   const int slot = slots ? slots[b] : b;
@@ -1966,6 +2046,7 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
     }
   float m = -INFINITY, s = 0.f;
   int am = 0x7fffffff;
+  SSTAMP(0, st0);
 #pragma unroll
   for (int e = 0; e < VPT; ++e) {
     const float w = x[e];
@@ -1977,26 +2058,45 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
       s += __expf(w - m);
     }
   }
-  const float Mg = block_max(m, red);
-  s = (m == -INFINITY) ? 0.f : s * __expf(m - Mg);
-  const float Sg = block_sum(s, red);
-  int cand = (m == Mg && Mg != -INFINITY) ? am : 0x7fffffff;
+  // chunk max / normaliser / first argmax: per wave by DPP + readlane, combined after ONE barrier
+  float Mg, Sg;
+  int amg;
+  {
+    const float wm = wave_max_dpp(m);
+    const float ws_ = wave_sum_dpp(m == -INFINITY ? 0.f : s * __expf(m - wm));
+    const int wi = wave_min_i((m == wm && wm != -INFINITY) ? am : 0x7fffffff);
+    if (lane == 0) {
+      red[wid] = wm;
+      red[4 + wid] = ws_;
+      iscan[wid] = wi;
+    }
+    __syncthreads();
+    Mg = -INFINITY;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) cand = min(cand, __shfl_xor(cand, o, 64));
-  __syncthreads();
-  if (lane == 0) iscan[wid] = cand;
-  __syncthreads();
-  int amg = 0x7fffffff;
-  for (int w = 0; w < MWG_NT / 64; ++w) amg = min(amg, iscan[w]);
+    for (int w = 0; w < MWG_NT / 64; ++w) Mg = fmaxf(Mg, red[w]);
+    Sg = 0.f;
+    amg = 0x7fffffff;
+#pragma unroll
+    for (int w = 0; w < MWG_NT / 64; ++w) {
+      if (red[w] != -INFINITY) Sg += red[4 + w] * __expf(red[w] - Mg);
+      if (red[w] == Mg && Mg != -INFINITY) amg = min(amg, iscan[w]);
+    }
+  }
+  SSTAMP(1, st0);
 
   // ---- local top-k threshold and the chunk's candidates (index order, at most CMAX)
   int count = 0;
   uint32_t tg = 0;
   if (!greedy) {
-    tg = block_kth_key<VPT>(k, [&](int e, uint32_t& key) {
-      key = fkey(x[e]);
-      return x[e] != -INFINITY;
-    }, cnt16);
+    uint32_t xk[VPT];
+    bool xo[VPT];
+#pragma unroll
+    for (int e = 0; e < VPT; ++e) {
+      xk[e] = fkey(x[e]);
+      xo[e] = x[e] != -INFINITY;
+    }
+    tg = block_kth_key<VPT, MWG_NT / 64>(k, xk, xo, cnt16);
+    SSTAMP(2, st0);
     int c = 0;
 #pragma unroll
     for (int e = 0; e < VPT; ++e) c += (x[e] != -INFINITY && fkey(x[e]) >= tg) ? 1 : 0;
@@ -2026,6 +2126,7 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
       }
     }
   }
+  SSTAMP(3, st0);
   if (tid == 0) {  // (integer fields stored as integers: key / index bit patterns as floats could be NaNs)
     mine[0] = Mg;
     mine[1] = Sg;
@@ -2048,7 +2149,10 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
     }
   }
   __syncthreads();
+  SSTAMP(4, st0);
   if (!sh_last) return;
+  const bool sm0 = b == 0;
+  SSTAMP_COUNT(sm0);
 
   // ================= merge (the last workgroup of the row)
   if (tid == 0) cnt[b] = 0;  // re-armed for the next launch
@@ -2075,70 +2179,48 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
     }
     return;
   }
-  // gather the candidates >= T0 into LDS in (chunk, position) = index order
-  if (tid == 0) {
-    int o = 0;
-    for (int q = 0; q < MWG_G; ++q) {
-      goff[q] = o;
-      o += reinterpret_cast<const int*>(part)[q * (MWG_PART + 2 * MWG_CMAX) + 3];
-    }
-    goff[MWG_G] = o;
-  }
-  __syncthreads();
-  const int ntot = goff[MWG_G];
-  constexpr int EPT = (MWG_G * MWG_CMAX + MWG_NT - 1) / MWG_NT;
-  int keepc = 0;
-  float cv[EPT];
-  int ci[EPT];
+  // candidates >= T0 into fixed LDS slots j = chunk * CMAX + position (= index order; empty and
+  // cut slots -inf): thread t owns slots [8t, 8t + 8) of one chunk -- no search, independent loads
+  constexpr int EPT = MWG_G * MWG_CMAX / MWG_NT;
+  static_assert(MWG_CMAX % EPT == 0, "a thread's slots within one chunk");
+  const int n = MWG_G * MWG_CMAX;
+  // (the thread keeps its slots' values and keys in registers; LDS holds them for the final pick)
+  float lv[EPT];
+  uint32_t lk[EPT];
+  bool lo[EPT];
+  {
+    const int j0 = tid * EPT, q = j0 / MWG_CMAX, p0 = j0 % MWG_CMAX;
+    const float* pq = part + q * (MWG_PART + 2 * MWG_CMAX);
+    const int cq = reinterpret_cast<const int*>(pq)[3];
 #pragma unroll
-  for (int e = 0; e < EPT; ++e) {
-    const int j = tid * EPT + e;
-    cv[e] = -INFINITY;
-    ci[e] = 0;
-    if (j < ntot) {
-      int q = 0;
-      while (goff[q + 1] <= j) ++q;
-      const float* pq = part + q * (MWG_PART + 2 * MWG_CMAX);
-      const float v = pq[MWG_PART + (j - goff[q])];
-      if (fkey(v) >= T0) {
-        cv[e] = v;
-        ci[e] = reinterpret_cast<const int*>(pq)[MWG_PART + MWG_CMAX + (j - goff[q])];
-        ++keepc;
+    for (int e = 0; e < EPT; ++e) {
+      float v = -INFINITY;
+      int id = 0;
+      if (p0 + e < cq) {
+        v = pq[MWG_PART + p0 + e];
+        id = reinterpret_cast<const int*>(pq)[MWG_PART + MWG_CMAX + p0 + e];
+        if (fkey(v) < T0) v = -INFINITY;
       }
+      Lv[j0 + e] = v;
+      Li[j0 + e] = id;
+      lv[e] = v;
+      lk[e] = fkey(v);
+      lo[e] = v != -INFINITY;
     }
   }
-  int inc = keepc;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int t = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += t;
-  }
-  __syncthreads();
-  if (lane == 63) iscan[wid] = inc;
-  __syncthreads();
-  int off = inc - keepc, n = 0;
-  for (int w = 0; w < MWG_NT / 64; ++w) {
-    if (w < wid) off += iscan[w];
-    n += iscan[w];
-  }
-#pragma unroll
-  for (int e = 0; e < EPT; ++e)
-    if (cv[e] != -INFINITY) {
-      Lv[off] = cv[e];
-      Li[off] = ci[e];
-      ++off;
-    }
-  __syncthreads();
-  // global top-k over L (n elements, thread t holds [t*E2, t*E2 + E2))
-  const int E2 = (n + MWG_NT - 1) / MWG_NT;
-  uint32_t thr = block_kth_key<EPT>(k, [&](int e, uint32_t& key) {
-    const int j = tid * E2 + e;
-    if (e >= E2 || j >= n) return false;
-    key = fkey(Lv[j]);
-    return true;
-  }, cnt16);
+  SSTAMP(8, sm0);
+  SSTAMP(9, sm0);
+  // global top-k over L (thread t holds slots [t*EPT, t*EPT + EPT)); the barriers inside also
+  // publish the LDS slots
+  constexpr int E2 = EPT;
+  uint32_t thr = block_kth_key<EPT, MWG_NT / 64>(k, lk, lo, cnt16);
+  __syncthreads();  // (block_kth_key may return before its first barrier: fewer than k valid)
+  SSTAMP(10, sm0);
   // top-p over the survivors: the smallest key whose descending inclusive mass reaches p * kept mass
   const float pp = top_p ? top_p[b] : 1.f;
+  float lm[EPT];  // the slots' unnormalised probability mass
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) lm[e] = lo[e] ? __expf(lv[e] - M) : 0.f;
   if (pp < 1.f) {
     uint32_t prefix = 0, mask = 0;
     float above = 0.f, target = -1.f;
@@ -2150,14 +2232,16 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
     int pass = 0;
     for (int shift = 28; shift >= 0; shift -= 4, ++pass) {
       float* hb = hist + 16 * (pass % 3);
-      for (int j = tid; j < n; j += MWG_NT) {
-        const uint32_t key = fkey(Lv[j]);
-        if (key >= thr && (key & mask) == prefix) atomicAdd(&hb[(key >> shift) & 15u], __expf(Lv[j] - M));
-      }
+#pragma unroll
+      for (int e = 0; e < E2; ++e)
+        if (lo[e] && lk[e] >= thr && (lk[e] & mask) == prefix) atomicAdd(&hb[(lk[e] >> shift) & 15u], lm[e]);
       __syncthreads();
       float hv[16];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) hv[j] = hb[j];
+      for (int j = 0; j < 4; ++j) {
+        const float4 t4 = reinterpret_cast<const float4*>(hb)[j];
+        hv[4 * j] = t4.x; hv[4 * j + 1] = t4.y; hv[4 * j + 2] = t4.z; hv[4 * j + 3] = t4.w;
+      }
       if (tid < 16) hist[16 * ((pass + 2) % 3) + tid] = 0.f;
       if (target < 0.f) {
         float t = 0.f;
@@ -2185,15 +2269,16 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
     }
     if (mask == 0xffffffffu && prefix > thr) thr = prefix;
   }
+  SSTAMP(11, sm0);
   // multinomial over the kept entries of L, index order: per-thread mass, block scan, Philox draw
   float ssum = 0.f;
   int kept = 0, last_j = -1;
+#pragma unroll
   for (int e = 0; e < E2; ++e) {
-    const int j = tid * E2 + e;
-    if (j < n && fkey(Lv[j]) >= thr) {
-      ssum += __expf(Lv[j] - M);
+    if (lo[e] && lk[e] >= thr) {
+      ssum += lm[e];
       ++kept;
-      last_j = j;
+      last_j = tid * E2 + e;
     }
   }
   float incl = ssum;
@@ -2227,10 +2312,11 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
   if (ssum > 0.f && excl < u && u <= incl) {
     float run = excl;
     int pick = -1;
-    for (int e = 0; e < E2 && pick < 0; ++e) {
+#pragma unroll
+    for (int e = 0; e < E2; ++e) {
       const int j = tid * E2 + e;
-      if (j < n && fkey(Lv[j]) >= thr) {
-        run += __expf(Lv[j] - M);
+      if (pick < 0 && lo[e] && lk[e] >= thr) {
+        run += lm[e];
         if (run >= u || j == last_j) pick = j;
       }
     }
@@ -2247,6 +2333,7 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
     if (seen && j >= 0) seen[(long long)slot * V + id] = 1;
     if (out_kept) out_kept[b] = ktot;
   }
+  SSTAMP(12, sm0);
 }
 
 // cnt: >= B zero-initialised counters (the multi-workgroup path re-arms them), or null to keep every

@@ -342,11 +342,27 @@ __global__ __launch_bounds__(256) void gemv1_kernel(const bf16_t* __restrict__ x
 // five operand streams are requested in one round, then two block
 // reductions -- the M = 1 decode step normalises once here and streams the
 // weights with the plain gemv1 kernel (ops/gemv.py:_LN_SPLIT_M1).
-template <int PER>
+// EmbedSrc (kca_embed_ln_rows): row m of x is embedding row id = chain[m] >= 0 ? prev[chain[m]] :
+// tokens[m] (clamped to [0, V)): the decode step's first kernel gathers the token embedding, takes a
+// chained token straight from the previous step's sampled ids on the device, and normalises it.
+struct EmbedSrc {
+  const long long* tokens;
+  const int* chain;       // nullable
+  const long long* prev;  // the previous step's sampled ids (with chain)
+  int V;
+};
+
+template <int PER, bool GATHER = false>
 __global__ __launch_bounds__(256) void ln_rows_kernel(const bf16_t* __restrict__ x, long long ldx, LnArgs a,
-                                                      int K) {
+                                                      int K, EmbedSrc es = EmbedSrc{}) {
   __shared__ float red[16];
   const int tid = threadIdx.x, m = blockIdx.x;
+  if constexpr (GATHER) {
+    const int c = es.chain ? es.chain[m] : -1;
+    long long id = c >= 0 ? es.prev[c] : es.tokens[m];
+    id = id < 0 ? 0 : (id >= es.V ? es.V - 1 : id);
+    x += (id - m) * ldx;  // the row reads below index x + m * ldx
+  }
   // gamma / beta requested with the row: they are independent of the statistics, so the
   // kernel pays one memory round trip instead of two
   U16x8 gr[PER], br[PER];
@@ -419,6 +435,25 @@ KCA_API int kca_ln_rows(const void* x, long long ldx, const void* r1, const void
   if (per <= 2) hipLaunchKernelGGL((ln_rows_kernel<2>), dim3(M), dim3(256), 0, stream, (const bf16_t*)x, ldx, a, K);
   else if (per <= 4) hipLaunchKernelGGL((ln_rows_kernel<4>), dim3(M), dim3(256), 0, stream, (const bf16_t*)x, ldx, a, K);
   else hipLaunchKernelGGL((ln_rows_kernel<8>), dim3(M), dim3(256), 0, stream, (const bf16_t*)x, ldx, a, K);
+  return 0;
+}
+
+// h_out[m] = wte[id_m] (bf16), xn_out[m] = LN(h_out[m]); id_m from tokens / chain / prev (EmbedSrc).
+KCA_API int kca_embed_ln_rows(const void* wte, long long ldw, const long long* tokens, const int* chain,
+                              const long long* prev, int V, void* h_out, long long ldh, const void* gamma,
+                              const void* beta, float eps, void* xn_out, int M, int K, hipStream_t stream) {
+  if (M < 1 || K % 8 || K > 16384 || ldw % 8 || ldh % 8 || !xn_out || !h_out || !tokens || V < 1) return 1;
+  if (chain && !prev) return 1;
+  if (((uintptr_t)wte | (uintptr_t)h_out | (uintptr_t)gamma | (uintptr_t)beta | (uintptr_t)xn_out) & 15) return 2;
+  LnArgs a{nullptr, nullptr, (bf16_t*)h_out, ldh, (const bf16_t*)gamma, (const bf16_t*)beta, eps, (bf16_t*)xn_out};
+  EmbedSrc es{tokens, chain, prev, V};
+  const int per = (K + 2047) / 2048;
+  if (per <= 2)
+    hipLaunchKernelGGL((ln_rows_kernel<2, true>), dim3(M), dim3(256), 0, stream, (const bf16_t*)wte, ldw, a, K, es);
+  else if (per <= 4)
+    hipLaunchKernelGGL((ln_rows_kernel<4, true>), dim3(M), dim3(256), 0, stream, (const bf16_t*)wte, ldw, a, K, es);
+  else
+    hipLaunchKernelGGL((ln_rows_kernel<8, true>), dim3(M), dim3(256), 0, stream, (const bf16_t*)wte, ldw, a, K, es);
   return 0;
 }
 

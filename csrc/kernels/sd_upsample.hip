@@ -84,6 +84,23 @@ __global__ void __launch_bounds__(256) upsample2x_kernel(const bf16_t* __restric
   *reinterpret_cast<u32x4*>(out + idx * 8) = *reinterpret_cast<const u32x4*>(x + src * 8);
 }
 
+// one thread per 16-B chunk of the output [N, h+1, w+1, C]: x with one zero row below and one zero
+// column to the right (the VAE encoder's Downsample2D pad (0, 1, 0, 1), channels-last in and out)
+__global__ void __launch_bounds__(256) pad_br_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ out, int h,
+                                                     int w, int C8, long long total) {
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total) return;
+  const int c8 = (int)(idx % C8);
+  const long long pix = idx / C8;
+  const int X = (int)(pix % (w + 1));
+  const long long nY = pix / (w + 1);
+  const int Y = (int)(nY % (h + 1));
+  const long long n = nY / (h + 1);
+  u32x4 v{0u, 0u, 0u, 0u};
+  if (Y < h && X < w) v = *reinterpret_cast<const u32x4*>(x + (((n * h + Y) * w + X) * (long long)C8 + c8) * 8);
+  *reinterpret_cast<u32x4*>(out + idx * 8) = v;
+}
+
 // one thread per 16-B chunk of the phase layout [N, h+1, w+1, 4C]: the dense gradient [N, 2h, 2w, C]
 // gathered back (phase (a, b) of grid position (i, j) is dense pixel (2(i-a)+a, 2(j-b)+b) when
 // a <= i < h + a and b <= j < w + b, else unused: 0)
@@ -182,5 +199,14 @@ KCA_API int kca_col2im2x2_nhwc(const void* da, void* dx, int N, int h, int w, in
   const long long total = (long long)N * h * w * (C / 8);
   hipLaunchKernelGGL(col2im2x2_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, (const bf16_t*)da,
                      (bf16_t*)dx, h, w, C / 8, total);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// x [N, h, w, C] -> out [N, h+1, w+1, C], zero bottom row and right column
+KCA_API int kca_pad_br_nhwc(const void* x, void* out, int N, int h, int w, int C, hipStream_t stream) {
+  if (C % 8 || N <= 0 || h <= 0 || w <= 0 || !aligned16(x) || !aligned16(out)) return 1;
+  const long long total = (long long)N * (h + 1) * (w + 1) * (C / 8);
+  hipLaunchKernelGGL(pad_br_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, (const bf16_t*)x, (bf16_t*)out, h,
+                     w, C / 8, total);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

@@ -33,7 +33,7 @@ import torch
 
 from .. import ops
 from ..ops import decode as dops
-from ..ops.gemv import ln_rows, ln_skinny_linear, skinny_linear
+from ..ops.gemv import embed_ln_rows, ln_rows, ln_skinny_linear, skinny_linear
 
 
 def _next_pow2(n: int, lo: int = 1) -> int:
@@ -356,6 +356,14 @@ class ModelRunner:
         self._fused_ok = (self._par_mlp and all(blk.ln_2 is None for blk in model.h)
                           and os.environ.get("KCA_DECODE_FUSED", "1") not in ("0", "false"))
         self._fz: dict = {}
+        self._outbufs: dict = {}
+        self._chain_src = None
+        # the fused step head gathers the token embedding itself (no learned positions / scale / LN on
+        # the embedding) and resolves chained tokens on the device: KCA_DECODE_EMBED_HEAD=0 keeps the
+        # torch embedding + cast + LN launches
+        self._embed_head = (self._fused_ok and getattr(model, "wpe", None) is None
+                            and getattr(model, "emb_ln", None) is None and cfg.embed_scale == 1.0
+                            and os.environ.get("KCA_DECODE_EMBED_HEAD", "1") not in ("0", "false"))
 
     # ------------------------------------------------------------- prefill
     @torch.no_grad()
@@ -479,9 +487,14 @@ class ModelRunner:
         (nothing launched) when the fused kernels do not cover the shape."""
         m, cfg = self.model, self.cfg
         fz = self._fused_bufs()
-        h0 = m.embed(tokens, pos.long())
         blk0 = m.h[0]
-        xn, h = ln_rows(h0, blk0.ln_1.weight, blk0.ln_1.bias, blk0.ln_1.eps)
+        if self._embed_head:  # token gather (+ chained token) + LayerNorm: one kernel
+            chain, prev = self._chain_src if self._chain_src is not None else (None, None)
+            xn, h = embed_ln_rows(m.wte.weight, tokens, blk0.ln_1.weight, blk0.ln_1.bias, blk0.ln_1.eps,
+                                  chain=chain, prev=prev)
+        else:
+            h0 = m.embed(tokens, pos.long())
+            xn, h = ln_rows(h0, blk0.ln_1.weight, blk0.ln_1.bias, blk0.ln_1.eps)
         hb, xb, g = fz["h"], fz["xn"], fz["g"]
         kc, vc, tbl = self.cache.k[0], self.cache.v[0], self.cache.table_on(self.device)
         for li, blk in enumerate(m.h):
@@ -510,6 +523,10 @@ class ModelRunner:
             y = self._layers_decode_fused(tokens, pos, slots, kv_lens, max_kv, ws, obuf)
             if y is not None:
                 return y
+        if self._chain_src is not None and obuf is not None:  # chained rows not resolved by a fused head
+            chain, prev = self._chain_src
+            tokens = torch.where(chain[:tokens.shape[0]] >= 0, prev[chain[:tokens.shape[0]].clamp(min=0).long()],
+                                 tokens)
         h = m.embed(tokens, pos.long())
         pending = ()
         per_dev = {self.device: (pos, slots, kv_lens, ws, obuf)}
@@ -603,25 +620,40 @@ class ModelRunner:
         pk = _Packed({"tokens": (torch.int64, Bb), "seeds": (torch.int64, Bb), "pos": (torch.int32, Bb),
                       "slots": (torch.int32, Bb), "kv_lens": (torch.int32, Bb), "top_k": (torch.int32, Bb),
                       "temperature": (torch.float32, Bb), "top_p": (torch.float32, Bb),
-                      "rep": (torch.float32, Bb), "bans": (torch.int32, Bb * NB)}, self.device)
+                      "rep": (torch.float32, Bb), "bans": (torch.int32, Bb * NB),
+                      "chain": (torch.int32, Bb)}, self.device)
         ws_n = dops.decode_ws_floats(Bb, self.H, self.Hkv, self.D, Kb)
+        ob = self._outbuf(Bb)
         st = {
             "pk": pk,
             "ws": torch.zeros(max(ws_n, 1), device=self.device, dtype=torch.float32),  # zeroed: fan-in counters
             "obuf": torch.empty(Bb, self.H * self.D, device=self.device, dtype=self.dtype),
             "sws": torch.empty(Bb * self.V, device=self.device, dtype=torch.float32),
-            "ids": torch.empty(Bb, device=self.device, dtype=torch.int64),
-            "lps": torch.empty(Bb, device=self.device, dtype=torch.float32),
-            # pinned landing buffers of the ids / log-probs D2H copies, one per host pk buffer
-            "ids_h": [torch.empty(Bb, dtype=torch.int64, pin_memory=self.device.type == "cuda") for _ in range(2)],
-            "lps_h": [torch.empty(Bb, dtype=torch.float32, pin_memory=self.device.type == "cuda")
-                      for _ in range(2)],
+            **ob,
         }
         self._static[key] = st
         return st
 
+    def _outbuf(self, Bb: int):
+        """Sampled ids (int64) and log-probs (fp32) of a batch bucket in ONE device buffer shared by its
+        kv-length buckets -- one D2H copy per step, and a chained token (decode_async) is read by the
+        next step's embedding kernel from a fixed address whatever kv bucket that step lands in --
+        with two pinned landing buffers (one per host pk buffer)."""
+        ob = self._outbufs.get(Bb)
+        if ob is None:
+            pin = self.device.type == "cuda"
+            dev = torch.empty(3 * Bb, device=self.device, dtype=torch.int32)
+            hs = [torch.empty(3 * Bb, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
+            ob = {"out": dev, "ids": dev[:2 * Bb].view(torch.int64), "lps": dev[2 * Bb:].view(torch.float32),
+                  "out_h": hs, "ids_h": [h[:2 * Bb].view(torch.int64) for h in hs],
+                  "lps_h": [h[2 * Bb:].view(torch.float32) for h in hs]}
+            self._outbufs[Bb] = ob
+        return ob
+
     def _step_body(self, st, Bb, Kb):
         pk = st["pk"]
+        # chained tokens resolved on the device by the fused B = 1 step head (_layers_decode_fused)
+        self._chain_src = (pk.d("chain"), st["ids"]) if (Bb == 1 and self._embed_head) else None
         logits = self._layers_decode(pk.d("tokens"), pk.d("pos"), pk.d("slots"), pk.d("kv_lens"), Kb,
                                      st["ws"], st["obuf"])
         dops.sample_logits(logits, temperature=pk.d("temperature"), top_k=pk.d("top_k"), top_p=pk.d("top_p"),
@@ -695,6 +727,8 @@ class ModelRunner:
         tok, sd, pos, sl, kl = a["tokens"], a["seeds"], a["pos"], a["slots"], a["kv_lens"]
         tk, te, tp, rp, bans = a["top_k"], a["temperature"], a["top_p"], a["rep"], a["bans"]
         bans.fill(-1)
+        ch = a["chain"]
+        ch.fill(-1)
         chain_dst, chain_src = [], []
         for i in range(Bb):
             if i < n:
@@ -715,10 +749,17 @@ class ModelRunner:
             else:  # padding row -> scratch slot
                 tok[i], pos[i], sl[i], kl[i] = 0, 0, self.cache.scratch, 1
                 te[i], tk[i], tp[i], rp[i], sd[i] = 0.0, 0, 1.0, 1.0, 0
+        if chain_dst and prev is None:
+            raise ValueError("rows chain their token from a previous launch, but prev is None")
+        # chained tokens read on the device by the step's first kernel: the previous step wrote them into
+        # this bucket's shared output buffer (same batch bucket); otherwise copied into `tokens` below
+        fold = (bool(chain_dst) and Bb == 1 and self._embed_head
+                and prev.ids_dev.data_ptr() == st["ids"].data_ptr())
+        if fold:
+            for d_, s_ in zip(chain_dst, chain_src):
+                ch[d_] = s_
         pk.upload()
-        if chain_dst:
-            if prev is None:
-                raise ValueError("rows chain their token from a previous launch, but prev is None")
+        if chain_dst and not fold:
             dst = pk.d("tokens")
             m = len(chain_dst)
             if chain_dst == chain_src == list(range(m)):  # the common case: same rows, same order
@@ -737,13 +778,11 @@ class ModelRunner:
         k = pk.cur
         ids_h, lps_h = st["ids_h"][k], st["lps_h"][k]
         if self.device.type == "cuda":
-            ids_h[:n].copy_(st["ids"][:n], non_blocking=True)
-            lps_h[:n].copy_(st["lps"][:n], non_blocking=True)
+            st["out_h"][k].copy_(st["out"], non_blocking=True)  # ids + log-probs, one copy
             ev = torch.cuda.Event()
             ev.record()
         else:
-            ids_h[:n].copy_(st["ids"][:n])
-            lps_h[:n].copy_(st["lps"][:n])
+            st["out_h"][k].copy_(st["out"])
             ev = None
         return DecodeHandle(ids_h, lps_h, n, ev, st["ids"])
 

@@ -25,6 +25,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
+from ..ops import _lib
 from ..ops.linear import SplitKLinear, linear_residual, linear_splitk_wgrad
 from ..ops.upsample import (phase_gemm_weights, phase_to_dense, phase_weights, upsample_conv_phase,
                            upsample_conv_train, upsample_nearest2x)
@@ -557,9 +558,19 @@ class Downsample2D(nn.Module):
     def forward(self, x):
         if self.asym:
             cl = _is_cl(x)
-            x = F.pad(x, (0, 1, 0, 1))
-            if cl:
-                x = x.contiguous(memory_format=torch.channels_last)
+            if cl and _lib.use_native(x) and not (torch.is_grad_enabled() and x.requires_grad) \
+                    and x.shape[1] % 8 == 0 and x.data_ptr() % 16 == 0:
+                # channels-last pad in one pass (F.pad leaves channels-last: fill + transposing copy +
+                # the copy back, ~1.3 ms at 16 x 128 x 512^2 in the DreamBooth step's VAE encode)
+                N, C, H, W = x.shape
+                out = torch.empty(N, C, H + 1, W + 1, device=x.device, dtype=x.dtype,
+                                  memory_format=torch.channels_last)
+                _lib.call("kca_pad_br_nhwc", x.data_ptr(), out.data_ptr(), N, H, W, C, _lib.stream())
+                x = out
+            else:
+                x = F.pad(x, (0, 1, 0, 1))
+                if cl:
+                    x = x.contiguous(memory_format=torch.channels_last)
         return self.conv(x)
 
 

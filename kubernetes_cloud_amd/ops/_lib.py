@@ -82,6 +82,7 @@ _SIGS = {
     "kca_skinny_set_splitk": [I],
     "kca_ln_skinny_gemm": [P, LL, P, P, P, LL, P, P, F, P, P, P, LL, I, I, I, I, P, P],
     "kca_ln_rows": [P, LL, P, P, P, LL, P, P, F, P, I, I, P],
+    "kca_embed_ln_rows": [P, LL, P, P, P, I, P, LL, P, P, F, P, I, I, P],
     "kca_decode_prep": [P, LL, I, I, I, I, I, I, P, P, P, P, P, P, LL, LL, LL, P, I, I, P],
     "kca_decode_chunk": [I, I, I],
     "kca_decode_set_stamps": [P],
@@ -97,6 +98,7 @@ _SIGS = {
     "kca_upsample2x_nhwc": [P, P, I, I, I, I, P],
     "kca_dense_to_phase_nhwc": [P, P, I, I, I, I, P],
     "kca_col2im2x2_nhwc": [P, P, I, I, I, I, P],
+    "kca_pad_br_nhwc": [P, P, I, I, I, I, P],
     "kca_gemv_dual_ln": [P, P, I, P, P, I, P, P, P, P, P, P, P, F, P, I, P],
     "kca_sample_logits": [P, LL, I, I, I, P, P, P, P, P, P, P, I, P, LL, P, P, P, P, P, P],
 }

@@ -132,6 +132,26 @@ def ln_rows(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor | None, eps
     return layer_norm(x, gamma, beta, eps), x
 
 
+def embed_ln_rows(wte: torch.Tensor, tokens: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor | None,
+                  eps: float, chain: torch.Tensor | None = None, prev: torch.Tensor | None = None):
+    """Decode step head: ``(xn, h)`` with h[m] = wte[id_m] and xn = LN(h), id_m = prev[chain[m]] where
+    chain[m] >= 0 (a token sampled by the previous step, still on the device) else tokens[m] --
+    one launch (``kca_embed_ln_rows``) instead of the embedding gather, the position cast and the LN."""
+    M, K = tokens.shape[0], wte.shape[1]
+    if not (_lib.use_native(wte) and K % 8 == 0 and K <= 16384 and wte.stride(1) == 1 and wte.stride(0) % 8 == 0
+            and gamma.is_contiguous() and (beta is None or beta.is_contiguous()) and tokens.dtype == torch.int64):
+        ids = tokens
+        if chain is not None:
+            ids = torch.where(chain >= 0, prev[chain.clamp(min=0).long()], tokens)
+        return ln_rows(wte[ids], gamma, beta, eps)
+    h = torch.empty(M, K, device=wte.device, dtype=wte.dtype)
+    xn = torch.empty(M, K, device=wte.device, dtype=wte.dtype)
+    _lib.call("kca_embed_ln_rows", wte.data_ptr(), wte.stride(0), tokens.data_ptr(), _lib.ptr(chain), _lib.ptr(prev),
+              wte.shape[0], h.data_ptr(), K, gamma.data_ptr(), _lib.ptr(beta), float(eps), xn.data_ptr(), M, K,
+              _lib.stream())
+    return xn, h
+
+
 def ln_skinny_linear(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor | None, eps: float,
                      weight: torch.Tensor, bias: torch.Tensor | None = None, residuals=(), act: int = 0,
                      want_h: bool = False, want_xn: bool = False):

@@ -167,7 +167,36 @@ def column_sum(x2: torch.Tensor, out_dtype: torch.dtype | None = None) -> torch.
     nb = -(-M // rb)
     part = torch.empty(nb, N, device=x2.device, dtype=torch.float32)
     _lib.call("kca_colsum_bf16", x2.data_ptr(), part.data_ptr(), M, N, rb, _lib.stream())
+    return sum_parts(part, out_dtype)
+
+
+def sum_parts(part: torch.Tensor, out_dtype: torch.dtype) -> torch.Tensor:
+    """[S, *shape] fp32 partials -> their sum over S in ``out_dtype`` (bf16 / fp32): one native pass
+    (``kca_col_reduce_f32``) instead of torch's sum + cast."""
+    S = part.shape[0]
+    C = part[0].numel()
+    if (part.is_cuda and part.dtype == torch.float32 and part.is_contiguous() and C % 64 == 0
+            and out_dtype in (torch.bfloat16, torch.float32) and _lib.has("kca_col_reduce_f32")):
+        out = torch.empty(part.shape[1:], device=part.device, dtype=out_dtype)
+        bf = out_dtype == torch.bfloat16
+        _lib.call("kca_col_reduce_f32", part.data_ptr(), S, C, out.data_ptr() if bf else None,
+                  None if bf else out.data_ptr(), _lib.stream())
+        return out
     return part.sum(0).to(out_dtype)
+
+
+_BMM_F32 = [None]  # aten::bmm.dtype (bf16 in, fp32 out): probed on first use
+
+
+def _bmm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    if _BMM_F32[0] is not False and a.is_cuda and a.dtype == torch.bfloat16:
+        try:
+            r = torch.bmm(a, b, out_dtype=torch.float32)
+            _BMM_F32[0] = True
+            return r
+        except (TypeError, RuntimeError, NotImplementedError):
+            _BMM_F32[0] = False
+    return torch.bmm(a, b).float()
 
 
 class _LinearSplitKW(torch.autograd.Function):
@@ -192,8 +221,8 @@ class _LinearSplitKW(torch.autograd.Function):
             if s > 1:
                 gy2c = gy2 if gy2.is_contiguous() else gy2.contiguous()
                 x2c = x2 if x2.is_contiguous() else x2.contiguous()
-                gw = torch.bmm(gy2c.view(s, t // s, n).transpose(1, 2), x2c.view(s, t // s, k)).float().sum(0)
-                gw = gw.to(w.dtype)
+                # per-chunk products in fp32 straight from the GEMM, one native reduction to w's dtype
+                gw = sum_parts(_bmm_f32(gy2c.view(s, t // s, n).transpose(1, 2), x2c.view(s, t // s, k)), w.dtype)
             else:
                 gw = gy2.t() @ x2
         if ctx.has_bias and ctx.needs_input_grad[2]:

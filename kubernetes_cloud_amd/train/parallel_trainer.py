@@ -279,11 +279,11 @@ def main(argv=None):
               (args.micro_batch, args.seq_len, cfg.hidden), dtype, dev)
     total = args.max_steps or 10 ** 9
     warm = int(total * args.warmup_ratio) if args.max_steps else 0
+    log_rank = (topo.pp - 1) * topo.tp  # dp 0, last stage, tp 0: the rank that holds the loss
     sink = MetricsSink(args.log_dir or os.path.join(args.output_path or ".", "logs"), "parallel-trainer",
-                       enabled=topo.rank == 0 and bool(args.log_dir or args.output_path))
+                       enabled=topo.rank == log_rank and bool(args.log_dir or args.output_path))
     step, losses = 0, []
     t0 = time.perf_counter()
-    log_rank = (topo.pp - 1) * topo.tp  # dp 0, last stage, tp 0
     for mbs in data_stream(args, cfg, topo, dev):
         lr = lr_at(step, args.lr, total, warm, args.lr_schedule, args.min_lr)
         loss_sum = one_f_one_b(stage, eng, p2p, mbs, topo.pp_idx, topo.pp)

@@ -63,6 +63,12 @@ def neox_ref(tmp_path_factory):
     return d, tmp, load_pretrained(merged, dtype=torch.float32).state_dict(), init
 
 
+def _losses(out):
+    import json
+    with open(os.path.join(out, "logs", "parallel-trainer.metrics.jsonl")) as f:
+        return [json.loads(ln)["train/loss"] for ln in f if ln.strip()]
+
+
 @pytest.mark.parametrize("tp,pp,dp,zero", [(2, 1, 1, 0), (1, 2, 1, 0), (2, 1, 2, 1)])
 def test_neox_3d_trainer_on_gpu_matches_world1(neox_ref, tp, pp, dp, zero):
     from kubernetes_cloud_amd.io.hf import load_pretrained
@@ -81,14 +87,24 @@ def test_neox_3d_trainer_on_gpu_matches_world1(neox_ref, tp, pp, dp, zero):
             dg, dr = (got[k] - init[k]).norm(), (ref[k] - init[k]).norm()
             assert torch.isfinite(got[k]).all() and 0.3 < float(dg / dr.clamp_min(1e-12)) < 3.0, (k, dg, dr)
         return
-    worst = 0.0
+    # same data and init: the loss curves agree to bf16 noise (step 1 is the forward of identical
+    # weights through the sharded layers: TP column/row all-reduces, PP activation P2P)
+    lr_, lg = _losses(str(tmp / "w1")), _losses(out)
+    assert len(lr_) == len(lg) == STEPS, (lr_, lg)
+    for a, b in zip(lr_, lg):
+        assert abs(a - b) <= 0.02 * abs(a), (lr_, lg)
+    # parameters after 3 Adam steps: per tensor ||got - ref|| / ||ref - init||. Adam moves every
+    # element by ~lr whatever its gradient's size, so elements whose bf16 gradient sits at the noise
+    # level take either sign -- an element-wise max would measure that noise, not the parallel layout
+    rel = {}
     for k in ref:
         if k.endswith("alibi"):
             continue
-        delta = (ref[k] - init[k]).abs().max().item()
-        err = (got[k] - ref[k]).abs().max().item()
-        worst = max(worst, err / max(delta, 1e-6))
-    assert worst < 0.25, worst  # bf16 on both sides, different reduction orders
+        d = (ref[k] - init[k]).norm()
+        if d > 0:
+            rel[k] = float((got[k] - ref[k]).norm() / d)
+    vals = sorted(rel.values())
+    assert vals[len(vals) // 2] < 0.35 and vals[-1] < 1.0, sorted(rel.items(), key=lambda kv: -kv[1])[:6]
 
 
 def test_resnet_trainer_gpu_world1_and_ddp_adasum_world2(tmp_path):
