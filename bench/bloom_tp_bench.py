@@ -27,8 +27,10 @@ import torch.distributed as dist
 
 
 def run_tp_decode(model_name="bloom-176b", layers=0, batches=(1, 8, 32), prompt_len=128, new_tokens=64,
-                  custom_ar=True):
-    """All ranks call this inside an initialised process group (or world 1).
+                  custom_ar=True, dtype="bf16"):
+    """All ranks call this inside an initialised process group (or world 1). ``dtype`` "fp16" runs
+    the model in float16 as BASELINE config 4 states (the native decode kernels are bf16: fp16 takes
+    the eager PyTorch paths, for comparison only).
     Returns the per-batch records on rank 0, None on followers."""
     from kubernetes_cloud_amd.engine.llm_engine import LLMEngine, SamplingParams
     from kubernetes_cloud_amd.engine.runner import ModelRunner
@@ -43,13 +45,14 @@ def run_tp_decode(model_name="bloom-176b", layers=0, batches=(1, 8, 32), prompt_
     if layers:
         cfg.n_layers = layers
     dev = torch.device("cuda", torch.cuda.current_device())
+    tdt = {"bf16": torch.bfloat16, "fp16": torch.float16}[dtype]
     t0 = time.perf_counter()
     if dist.is_initialized():  # TP modules even at world 1: exercises the RCCL collectives in the decode graph
         from kubernetes_cloud_amd.parallel.tensor_parallel import load_tp_model
-        model = load_tp_model(cfg, rank, world, None, device=dev, dtype=torch.bfloat16, random_init=True)
+        model = load_tp_model(cfg, rank, world, None, device=dev, dtype=tdt, random_init=True)
     else:
         from kubernetes_cloud_amd.models.causal_lm import build_model
-        model = build_model(cfg, device=dev, dtype=torch.bfloat16, seed=0)
+        model = build_model(cfg, device=dev, dtype=tdt, seed=0)
     torch.cuda.synchronize()
     load_s = time.perf_counter() - t0
     ar = None
@@ -90,7 +93,7 @@ def run_tp_decode(model_name="bloom-176b", layers=0, batches=(1, 8, 32), prompt_
             out.append({"metric": f"{model_name} TP={world} decode", "batch": B, "prompt_len": prompt_len,
                         "prefill_ms": round(prefill_ms, 2), "decode_ms_per_token": round(dt / max(n, 1) * 1e3, 3),
                         "tokens_per_s": round((sum(len(r.output) for r in reqs) - 2 * B) / dt, 1),
-                        "layers": cfg.n_layers, "tp": world, "load_s": round(load_s, 1), "dtype": "bf16",
+                        "layers": cfg.n_layers, "tp": world, "load_s": round(load_s, 1), "dtype": dtype,
                         "custom_allreduce": ar is not None, "ctrl": chan.kind if chan is not None else None,
                         "pipelined": bool(eng.pipeline),
                         "data": "random-init weights"})
@@ -115,6 +118,8 @@ def main():
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--new-tokens", type=int, default=64)
     ap.add_argument("--no-custom-ar", action="store_true", help="TP all-reduces through RCCL only")
+    ap.add_argument("--dtype", choices=["bf16", "fp16"], default="bf16",
+                    help="fp16: BASELINE config 4's dtype (eager PyTorch paths; the native kernels are bf16)")
     ap.add_argument("--force-pg", action="store_true",
                     help="one-rank RCCL process group: TP modules + collectives captured in the decode graph")
     args = ap.parse_args()
@@ -125,7 +130,7 @@ def main():
         os.environ.setdefault("MASTER_PORT", "29511")
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     recs = run_tp_decode(args.model, args.layers, [int(b) for b in args.batches.split(",")], args.prompt_len,
-                         args.new_tokens, custom_ar=not args.no_custom_ar)
+                         args.new_tokens, custom_ar=not args.no_custom_ar, dtype=args.dtype)
     for r in recs or ():
         print(json.dumps(r), flush=True)
 

@@ -44,13 +44,34 @@ def build(dev, dtype):
 
 
 def _attrib(step):
-    """--attrib: one step under torch.profiler; the eager PyTorch (at::native) kernels and the device
-    copies grouped by the aten op that launched them and its nearest repo stack frame (stderr)."""
+    """--attrib: where the eager PyTorch (at::native) kernels and device copies of one step come from.
+    One step under a TorchDispatchMode records the first repo stack frame of every aten call by (op,
+    shapes) (the profiler's own Python stacks are empty on this build); one step under torch.profiler
+    times the kernels each (op, shapes) launched. stderr."""
     import collections
+    import traceback
 
     from torch.profiler import ProfilerActivity, profile
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True,
-                 with_stack=True) as prof:
+    from torch.utils._python_dispatch import TorchDispatchMode
+
+    frames = collections.defaultdict(collections.Counter)
+
+    def _shape(a):
+        return list(a.shape) if isinstance(a, torch.Tensor) else []
+
+    class _Where(TorchDispatchMode):
+        def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+            st = traceback.extract_stack()
+            fr = next((f"{f.filename.split('kubernetes_cloud_amd/')[-1]}:{f.lineno}" for f in reversed(st)
+                       if "kubernetes_cloud_amd" in f.filename and "_python_dispatch" not in f.filename), "?")
+            name = "aten::" + func.__name__.split(".")[0]
+            frames[(name, str([_shape(x) for x in args[:2]]))][fr] += 1
+            return func(*args, **(kwargs or {}))
+
+    with _Where():
+        step()
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
         step()
         torch.cuda.synchronize()
     agg, total, eager = collections.defaultdict(lambda: [0, 0.0]), 0.0, 0.0
@@ -61,17 +82,18 @@ def _attrib(step):
             if "at::native" not in k.name and "rocclr" not in k.name:
                 continue
             eager += us
-            e, frame = ev, "?"
-            while e is not None and frame == "?":  # nearest ancestor op called from Python carries the stack
-                frame = next((f for f in (e.stack or []) if "kubernetes_cloud_amd" in f), "?")
-                e = getattr(e, "cpu_parent", None)
-            key = (ev.name, str(ev.input_shapes)[:90], frame.split("kubernetes_cloud_amd/")[-1][:70])
+            e = ev
+            while getattr(e, "cpu_parent", None) is not None and not e.name.startswith("aten::"):
+                e = e.cpu_parent
+            key = (e.name, str([list(x) if isinstance(x, (list, tuple)) else [] for x in e.input_shapes[:2]]))
             agg[key][0] += 1
             agg[key][1] += us
     print(f"[sd_bench attrib] kernel time {total / 1e3:.1f} ms, eager/copy {eager / 1e3:.2f} ms "
           f"({100 * eager / max(total, 1):.2f} %)", file=sys.stderr)
-    for (name, shp, fr), (n, us) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:40]:
-        print(f"  {us:9.1f} us {n:4d}x {name:28s} {fr:70s} {shp}", file=sys.stderr)
+    for (name, shp), (n, us) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:40]:
+        fr = frames.get((name, shp))
+        where = ", ".join(f"{f} x{c}" for f, c in fr.most_common(2)) if fr else "?"
+        print(f"  {us:9.1f} us {n:4d}x {name:22s} {shp:60s} {where}", file=sys.stderr)
 
 
 def bench_train(args, dev):

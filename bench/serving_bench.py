@@ -133,6 +133,8 @@ def _levels(pred, model_name: str, new_tokens: int | None, levels=LEVELS) -> lis
         _client(srv.url, 4, 4, model_name, 99)  # warm: graphs, allocator
         _engine(pred, 4, 4, seed=98)
         for conc, n in levels:
+            # warm this level's batch buckets first (decode-graph captures), so neither timed pass pays them
+            _engine(pred, 2 * conc, conc, seed=1000 + conc)
             h = _client(srv.url, n, conc, model_name, conc)
             e = _engine(pred, n, conc, seed=conc)
             rec = {"concurrency": conc, "requests": n, "successes": h["successes"],

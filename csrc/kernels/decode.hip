@@ -1893,14 +1893,14 @@ __device__ uint32_t block_kth_key(int k, const uint32_t (&key)[EPT], const bool 
   for (int shift = 28; shift >= 0; shift -= 4, ++pass) {
     uint32_t w4[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-    for (int e = 0; e < EPT; ++e) {
-      if (ok[e] && (key[e] & mask) == prefix) {
-        const uint32_t d = (key[e] >> shift) & 15u, inc = 1u << ((d & 3u) << 3);
-        w4[0] += d < 4 ? inc : 0u;
-        w4[1] += (d >> 2) == 1 ? inc : 0u;
-        w4[2] += (d >> 2) == 2 ? inc : 0u;
-        w4[3] += d >= 12 ? inc : 0u;
-      }
+    for (int e = 0; e < EPT; ++e) {  // branch-free: selects, no exec-mask regions per element
+      const uint32_t d = (key[e] >> shift) & 15u;
+      const uint32_t inc = (ok[e] && (key[e] & mask) == prefix) ? 1u << ((d & 3u) << 3) : 0u;
+      const uint32_t g4 = d >> 2;
+      w4[0] += g4 == 0 ? inc : 0u;
+      w4[1] += g4 == 1 ? inc : 0u;
+      w4[2] += g4 == 2 ? inc : 0u;
+      w4[3] += g4 == 3 ? inc : 0u;
     }
     uint4* tab = reinterpret_cast<uint4*>(cnt16) + (pass & 1) * NW * 2;
     uint32_t sw[8];
@@ -1950,6 +1950,64 @@ __device__ uint32_t block_kth_key(int k, const uint32_t (&key)[EPT], const bool 
   return prefix;
 }
 
+// block_kth_key for keys held by ONE wave: the counts are wave sums (uniform scalars), so no LDS
+// table and no barrier per pass -- the small selections (256 thread maxima, <= 256 candidates) run
+// here while the other waves wait at one barrier.
+template <int EPT>
+__device__ uint32_t wave_kth_key(int k, const uint32_t (&key)[EPT], const bool (&ok)[EPT]) {
+  uint32_t prefix = 0, mask = 0;
+  int remaining = k;
+#pragma unroll 1
+  for (int shift = 28; shift >= 0; shift -= 4) {
+    uint32_t w4[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) {
+      const uint32_t d = (key[e] >> shift) & 15u;
+      const uint32_t inc = (ok[e] && (key[e] & mask) == prefix) ? 1u << ((d & 3u) << 3) : 0u;
+      const uint32_t g4 = d >> 2;
+      w4[0] += g4 == 0 ? inc : 0u;
+      w4[1] += g4 == 1 ? inc : 0u;
+      w4[2] += g4 == 2 ? inc : 0u;
+      w4[3] += g4 == 3 ? inc : 0u;
+    }
+    uint32_t words[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      words[2 * q] = wave_sum_u32((w4[q] & 0xffu) | ((w4[q] & 0xff00u) << 8));
+      words[2 * q + 1] = wave_sum_u32(((w4[q] >> 16) & 0xffu) | ((w4[q] >> 8) & 0xff0000u));
+    }
+    int run = 0, dsel = -1, csel = 0;
+#pragma unroll
+    for (int j = 15; j >= 0; --j) {
+      const int c = (int)((j & 1) ? (words[j >> 1] >> 16) : (words[j >> 1] & 0xffffu));
+      if (dsel < 0) {
+        if (run + c >= remaining) {
+          dsel = j;
+          csel = c;
+        } else {
+          run += c;
+        }
+      }
+    }
+    if (dsel < 0) return 0u;
+    prefix |= (uint32_t)dsel << shift;
+    mask |= 15u << shift;
+    remaining -= run;
+    if (csel == remaining) return prefix;
+  }
+  return prefix;
+}
+
+// Wave-wide inclusive prefix sum (Hillis-Steele over ds_bpermute shuffles)
+__device__ __forceinline__ float wave_incl_scan(float v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
 // Diagnostic build only (tools/build_ext.py --stamps, tools/sample_stamps.py): s_memtime segment
 // sums of the multi-workgroup sampler -- chunk phase of workgroup 0 of row 0 (slots 0..5) and the
 // merging workgroup of row 0 (slots 8..13); slot 15 counts launches. Empty in the normal build.
@@ -1996,14 +2054,18 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
     const unsigned long long* __restrict__ seeds, long long step, float* __restrict__ ws,
     unsigned int* __restrict__ cnt, long long* __restrict__ out_ids, float* __restrict__ out_lp,
     int* __restrict__ out_kept) {
-  __shared__ float red[2 * MWG_NT / 64];
+  __shared__ float red[8 + MWG_NT];  // [0, 8): per-wave partials; [8, 8 + NT): thread maxima
   __shared__ __attribute__((aligned(16))) uint32_t cnt16[2 * MWG_NT / 64 * 8];
   __shared__ int sel[2];
   __shared__ int iscan[MWG_NT / 64];
   __shared__ int sh_last;
   __shared__ float Lv[MWG_G * MWG_CMAX];
   __shared__ int Li[MWG_G * MWG_CMAX];
+  __shared__ float L2v[MWG_G * MWG_CMAX];  // the candidates after the per-wave narrowing
+  __shared__ int L2i[MWG_G * MWG_CMAX];
   __shared__ __attribute__((aligned(16))) float hist[48];
+  __shared__ float Kv[64];
+  __shared__ int Kj[64];
   const int g = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const float T = temperature ? temperature[b] : 1.f;
   const int k = top_k ? top_k[b] : 0;
@@ -2085,39 +2147,72 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
   SSTAMP(1, st0);
 
   // ---- local top-k threshold and the chunk's candidates (index order, at most CMAX)
+  // t_g only has to leave k <= count(x >= t_g) <= CMAX. First try the k-th largest of the 256
+  // per-thread maxima (k threads each hold an element >= it; one key per thread makes the radix
+  // passes ~13x cheaper); when that keeps more than CMAX (top values bunched in few threads, e.g.
+  // sorted logits), the exact k-th largest element.
   int count = 0;
   uint32_t tg = 0;
   if (!greedy) {
     uint32_t xk[VPT];
     bool xo[VPT];
+    float tmx = -INFINITY;
 #pragma unroll
     for (int e = 0; e < VPT; ++e) {
       xk[e] = fkey(x[e]);
       xo[e] = x[e] != -INFINITY;
+      tmx = fmaxf(tmx, x[e]);
     }
-    tg = block_kth_key<VPT, MWG_NT / 64>(k, xk, xo, cnt16);
+    {  // the 256 thread maxima to wave 0 (4 per lane), selected there; one barrier each way
+      red[8 + tid] = tmx;
+      __syncthreads();
+      if (wid == 0) {
+        uint32_t mk[4];
+        bool mo[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float v = red[8 + 4 * lane + e];
+          mk[e] = fkey(v);
+          mo[e] = v != -INFINITY;
+        }
+        const uint32_t t = wave_kth_key<4>(k, mk, mo);
+        if (lane == 0) sel[0] = (int)t;
+      }
+      __syncthreads();
+      tg = (uint32_t)sel[0];
+    }
     SSTAMP(2, st0);
-    int c = 0;
+    int c, off, tot;
+    auto scan = [&]() {
+      c = 0;
 #pragma unroll
-    for (int e = 0; e < VPT; ++e) c += (x[e] != -INFINITY && fkey(x[e]) >= tg) ? 1 : 0;
-    int inc = c;
+      for (int e = 0; e < VPT; ++e) c += (xo[e] && xk[e] >= tg) ? 1 : 0;
+      int inc = c;
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int t = __shfl_up(inc, o, 64);
-      if (lane >= o) inc += t;
-    }
-    __syncthreads();
-    if (lane == 63) iscan[wid] = inc;
-    __syncthreads();
-    int off = inc - c, tot = 0;
-    for (int w = 0; w < MWG_NT / 64; ++w) {
-      if (w < wid) off += iscan[w];
-      tot += iscan[w];
+      for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += t;
+      }
+      __syncthreads();
+      if (lane == 63) iscan[wid] = inc;
+      __syncthreads();
+      off = inc - c;
+      tot = 0;
+#pragma unroll
+      for (int w = 0; w < MWG_NT / 64; ++w) {
+        if (w < wid) off += iscan[w];
+        tot += iscan[w];
+      }
+    };
+    scan();
+    if (tot > MWG_CMAX) {  // uniform: every thread read the same iscan
+      tg = block_kth_key<VPT, MWG_NT / 64>(k, xk, xo, cnt16);
+      scan();
     }
     count = min(tot, MWG_CMAX);  // (> CMAX only with massive ties at t_g: the first CMAX by index stay)
 #pragma unroll
     for (int e = 0; e < VPT; ++e) {
-      if (x[e] != -INFINITY && fkey(x[e]) >= tg) {
+      if (xo[e] && xk[e] >= tg) {
         if (off < MWG_CMAX) {
           mine[MWG_PART + off] = x[e];
           reinterpret_cast<int*>(mine)[MWG_PART + MWG_CMAX + off] = e0 + e;
@@ -2179,159 +2274,319 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
     }
     return;
   }
-  // candidates >= T0 into fixed LDS slots j = chunk * CMAX + position (= index order; empty and
-  // cut slots -inf): thread t owns slots [8t, 8t + 8) of one chunk -- no search, independent loads
-  constexpr int EPT = MWG_G * MWG_CMAX / MWG_NT;
-  static_assert(MWG_CMAX % EPT == 0, "a thread's slots within one chunk");
-  const int n = MWG_G * MWG_CMAX;
-  // (the thread keeps its slots' values and keys in registers; LDS holds them for the final pick)
-  float lv[EPT];
-  uint32_t lk[EPT];
-  bool lo[EPT];
+  // candidates >= T0, compacted into LDS in (chunk, position) = index order: thread t reads slots
+  // [8t, 8t + 8) of one chunk's list (no search, independent loads), a block scan places them
+  constexpr int SPT = MWG_G * MWG_CMAX / MWG_NT;
+  static_assert(MWG_CMAX % SPT == 0, "a thread's slots within one chunk");
+  int nv;
   {
-    const int j0 = tid * EPT, q = j0 / MWG_CMAX, p0 = j0 % MWG_CMAX;
+    float sv[SPT];
+    int si[SPT];
+    int c = 0;
+    const int j0 = tid * SPT, q = j0 / MWG_CMAX, p0 = j0 % MWG_CMAX;
     const float* pq = part + q * (MWG_PART + 2 * MWG_CMAX);
     const int cq = reinterpret_cast<const int*>(pq)[3];
 #pragma unroll
-    for (int e = 0; e < EPT; ++e) {
-      float v = -INFINITY;
-      int id = 0;
+    for (int e = 0; e < SPT; ++e) {
+      sv[e] = -INFINITY;
+      si[e] = 0;
       if (p0 + e < cq) {
-        v = pq[MWG_PART + p0 + e];
-        id = reinterpret_cast<const int*>(pq)[MWG_PART + MWG_CMAX + p0 + e];
-        if (fkey(v) < T0) v = -INFINITY;
-      }
-      Lv[j0 + e] = v;
-      Li[j0 + e] = id;
-      lv[e] = v;
-      lk[e] = fkey(v);
-      lo[e] = v != -INFINITY;
-    }
-  }
-  SSTAMP(8, sm0);
-  SSTAMP(9, sm0);
-  // global top-k over L (thread t holds slots [t*EPT, t*EPT + EPT)); the barriers inside also
-  // publish the LDS slots
-  constexpr int E2 = EPT;
-  uint32_t thr = block_kth_key<EPT, MWG_NT / 64>(k, lk, lo, cnt16);
-  __syncthreads();  // (block_kth_key may return before its first barrier: fewer than k valid)
-  SSTAMP(10, sm0);
-  // top-p over the survivors: the smallest key whose descending inclusive mass reaches p * kept mass
-  const float pp = top_p ? top_p[b] : 1.f;
-  float lm[EPT];  // the slots' unnormalised probability mass
-#pragma unroll
-  for (int e = 0; e < EPT; ++e) lm[e] = lo[e] ? __expf(lv[e] - M) : 0.f;
-  if (pp < 1.f) {
-    uint32_t prefix = 0, mask = 0;
-    float above = 0.f, target = -1.f;
-    // triple-buffered histogram: pass p accumulates into buffer p % 3 and, after its barrier,
-    // clears buffer (p + 2) % 3 (read in pass p - 1, filled in pass p + 2); every lane picks the
-    // digit from its own read of the table (no broadcast round)
-    if (tid < 48) hist[tid] = 0.f;
-    __syncthreads();
-    int pass = 0;
-    for (int shift = 28; shift >= 0; shift -= 4, ++pass) {
-      float* hb = hist + 16 * (pass % 3);
-#pragma unroll
-      for (int e = 0; e < E2; ++e)
-        if (lo[e] && lk[e] >= thr && (lk[e] & mask) == prefix) atomicAdd(&hb[(lk[e] >> shift) & 15u], lm[e]);
-      __syncthreads();
-      float hv[16];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float4 t4 = reinterpret_cast<const float4*>(hb)[j];
-        hv[4 * j] = t4.x; hv[4 * j + 1] = t4.y; hv[4 * j + 2] = t4.z; hv[4 * j + 3] = t4.w;
-      }
-      if (tid < 16) hist[16 * ((pass + 2) % 3) + tid] = 0.f;
-      if (target < 0.f) {
-        float t = 0.f;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) t += hv[j];
-        target = pp * t;
-      }
-      float run = 0.f;
-      int dsel = -1;
-#pragma unroll
-      for (int j = 15; j >= 0; --j) {
-        if (dsel < 0) {
-          if (hv[j] > 0.f && run + hv[j] >= target - above) dsel = j;
-          else run += hv[j];
+        const float v = pq[MWG_PART + p0 + e];
+        if (fkey(v) >= T0) {
+          sv[e] = v;
+          si[e] = reinterpret_cast<const int*>(pq)[MWG_PART + MWG_CMAX + p0 + e];
+          ++c;
         }
       }
-      if (dsel < 0) {
-        prefix = 0;
-        mask = 0;
-        break;
+    }
+    int inc = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += t;
+    }
+    __syncthreads();
+    if (lane == 63) iscan[wid] = inc;
+    __syncthreads();
+    int off = inc - c;
+    nv = 0;
+#pragma unroll
+    for (int w = 0; w < MWG_NT / 64; ++w) {
+      if (w < wid) off += iscan[w];
+      nv += iscan[w];
+    }
+#pragma unroll
+    for (int e = 0; e < SPT; ++e)
+      if (sv[e] != -INFINITY) {
+        Lv[off] = sv[e];
+        Li[off] = si[e];
+        ++off;
       }
-      prefix |= (uint32_t)dsel << shift;
-      mask |= 15u << shift;
-      above += run;
-    }
-    if (mask == 0xffffffffu && prefix > thr) thr = prefix;
+    __syncthreads();
   }
-  SSTAMP(11, sm0);
-  // multinomial over the kept entries of L, index order: per-thread mass, block scan, Philox draw
-  float ssum = 0.f;
-  int kept = 0, last_j = -1;
-#pragma unroll
-  for (int e = 0; e < E2; ++e) {
-    if (lo[e] && lk[e] >= thr) {
-      ssum += lm[e];
-      ++kept;
-      last_j = tid * E2 + e;
-    }
-  }
-  float incl = ssum;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const float t = __shfl_up(incl, o, 64);
-    if (lane >= o) incl += t;
-  }
-  int kept_tot = kept;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) kept_tot += __shfl_xor(kept_tot, o, 64);
-  __syncthreads();
-  if (lane == 63) red[wid] = incl;
-  if (lane == 0) iscan[wid] = kept_tot;
-  if (tid == 0) sel[0] = -1;
-  __syncthreads();
-  float woff = 0.f, total = 0.f;
-  int ktot = 0;
-  for (int w = 0; w < MWG_NT / 64; ++w) {
-    if (w < wid) woff += red[w];
-    total += red[w];
-    ktot += iscan[w];
-  }
-  incl += woff;
-  const float excl = incl - ssum;
-  uint32_t c[4] = {seeds ? 0u : (uint32_t)b, (uint32_t)step, (uint32_t)((unsigned long long)step >> 32), 0x5eedu};
+  SSTAMP(8, sm0);
+  const float pp = top_p ? top_p[b] : 1.f;
+  uint32_t c4[4] = {seeds ? 0u : (uint32_t)b, (uint32_t)step, (uint32_t)((unsigned long long)step >> 32), 0x5eedu};
   const unsigned long long sd = seeds ? seeds[b] : 0ull;
-  philox4x32_10(c, (uint32_t)sd, (uint32_t)(sd >> 32));
-  const float r = ((c[0] >> 8) + 1) * (1.0f / 16777216.0f);  // (0, 1]
-  const float u = r * total;
-  if (ssum > 0.f && excl < u && u <= incl) {
-    float run = excl;
-    int pick = -1;
+  philox4x32_10(c4, (uint32_t)sd, (uint32_t)(sd >> 32));
+  const float r = ((c4[0] >> 8) + 1) * (1.0f / 16777216.0f);  // (0, 1]
+  SSTAMP(9, sm0);
+  // top-k, top-p and the multinomial over the nv compacted candidates, E per thread (contiguous,
+  // index order): E = 1 in the common case (nv <= 256), so each radix pass costs one key per thread
+  auto tail = [&](auto EC) {
+    constexpr int E = decltype(EC)::value;
+    float lv[E], lm[E];
+    uint32_t lk[E];
+    bool lo[E];
 #pragma unroll
-    for (int e = 0; e < E2; ++e) {
-      const int j = tid * E2 + e;
-      if (pick < 0 && lo[e] && lk[e] >= thr) {
-        run += lm[e];
-        if (run >= u || j == last_j) pick = j;
+    for (int e = 0; e < E; ++e) {
+      const int j = tid * E + e;
+      lo[e] = j < nv;
+      lv[e] = lo[e] ? Lv[j] : -INFINITY;
+      lk[e] = fkey(lv[e]);
+      lm[e] = lo[e] ? __expf(lv[e] - M) : 0.f;
+    }
+    uint32_t thr = block_kth_key<E, MWG_NT / 64>(k, lk, lo, cnt16);
+    SSTAMP(10, sm0);
+    // top-p over the survivors: the smallest key whose descending inclusive mass reaches p * kept mass
+    if (pp < 1.f) {
+      uint32_t prefix = 0, mask = 0;
+      float above = 0.f, target = -1.f;
+      // triple-buffered histogram: pass p accumulates into buffer p % 3 and, after its barrier,
+      // clears buffer (p + 2) % 3 (read in pass p - 1, filled in pass p + 2); every lane picks the
+      // digit from its own read of the table (no broadcast round)
+      if (tid < 48) hist[tid] = 0.f;
+      __syncthreads();
+      int pass = 0;
+#pragma unroll 1
+      for (int shift = 28; shift >= 0; shift -= 4, ++pass) {
+        float* hb = hist + 16 * (pass % 3);
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+          if (lo[e] && lk[e] >= thr && (lk[e] & mask) == prefix) atomicAdd(&hb[(lk[e] >> shift) & 15u], lm[e]);
+        __syncthreads();
+        float hv[16];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float4 t4 = reinterpret_cast<const float4*>(hb)[j];
+          hv[4 * j] = t4.x; hv[4 * j + 1] = t4.y; hv[4 * j + 2] = t4.z; hv[4 * j + 3] = t4.w;
+        }
+        if (tid < 16) hist[16 * ((pass + 2) % 3) + tid] = 0.f;
+        if (target < 0.f) {
+          float t = 0.f;
+#pragma unroll
+          for (int j = 0; j < 16; ++j) t += hv[j];
+          target = pp * t;
+        }
+        float run = 0.f;
+        int dsel = -1;
+#pragma unroll
+        for (int j = 15; j >= 0; --j) {
+          if (dsel < 0) {
+            if (hv[j] > 0.f && run + hv[j] >= target - above) dsel = j;
+            else run += hv[j];
+          }
+        }
+        if (dsel < 0) {
+          prefix = 0;
+          mask = 0;
+          break;
+        }
+        prefix |= (uint32_t)dsel << shift;
+        mask |= 15u << shift;
+        above += run;
+      }
+      if (mask == 0xffffffffu && prefix > thr) thr = prefix;
+    }
+    SSTAMP(11, sm0);
+    // multinomial over the kept candidates, index order: per-thread mass, block scan, Philox draw
+    float ssum = 0.f;
+    int kept = 0, last_j = -1;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      if (lo[e] && lk[e] >= thr) {
+        ssum += lm[e];
+        ++kept;
+        last_j = tid * E + e;
       }
     }
-    if (pick >= 0) atomicMax(&sel[0], pick);
+    float incl = ssum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const float t = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += t;
+    }
+    int kept_tot = kept;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) kept_tot += __shfl_xor(kept_tot, o, 64);
+    __syncthreads();
+    if (lane == 63) red[wid] = incl;
+    if (lane == 0) iscan[wid] = kept_tot;
+    if (tid == 0) sel[0] = -1;
+    __syncthreads();
+    float woff = 0.f, total = 0.f;
+    int ktot = 0;
+    for (int w = 0; w < MWG_NT / 64; ++w) {
+      if (w < wid) woff += red[w];
+      total += red[w];
+      ktot += iscan[w];
+    }
+    incl += woff;
+    const float excl = incl - ssum;
+    const float u = r * total;
+    if (ssum > 0.f && excl < u && u <= incl) {
+      float run = excl;
+      int pick = -1;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int j = tid * E + e;
+        if (pick < 0 && lo[e] && lk[e] >= thr) {
+          run += lm[e];
+          if (run >= u || j == last_j) pick = j;
+        }
+      }
+      if (pick >= 0) atomicMax(&sel[0], pick);
+    }
+    __syncthreads();
+    if (sel[0] < 0 && kept > 0) atomicMax(&sel[0], last_j);  // rounding at the top of the range
+    __syncthreads();
+    if (tid == 0) {
+      const int j = sel[0];
+      const int id = j >= 0 ? Li[j] : 0;
+      out_ids[b] = id;
+      if (out_lp) out_lp[b] = j >= 0 ? Lv[j] - lZ : -INFINITY;
+      if (seen && j >= 0) seen[(long long)slot * V + id] = 1;
+      if (out_kept) out_kept[b] = ktot;
+    }
+  };
+  // Narrowing: each wave's exact top-k key over its 512 compacted slots (wave sums only, the four
+  // waves in parallel); T1 = the largest of them is <= the global k-th key (that wave alone holds k
+  // elements >= T1), so the candidates >= T1 -- about 4k -- still hold the top k with its ties.
+  int n2;
+  {
+    uint32_t k8[SPT];
+    bool o8[SPT];
+    int c = 0;
+#pragma unroll
+    for (int e = 0; e < SPT; ++e) {
+      const int j = tid * SPT + e;
+      o8[e] = j < nv;
+      k8[e] = o8[e] ? fkey(Lv[j]) : 0u;
+    }
+    const uint32_t tw = wave_kth_key<SPT>(k, k8, o8);
+    if (lane == 0) Kj[wid] = (int)tw;
+    __syncthreads();
+    uint32_t T1 = 0;
+#pragma unroll
+    for (int w = 0; w < MWG_NT / 64; ++w) T1 = max(T1, (uint32_t)Kj[w]);
+#pragma unroll
+    for (int e = 0; e < SPT; ++e) c += (o8[e] && k8[e] >= T1) ? 1 : 0;
+    int inc = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += t;
+    }
+    if (lane == 63) iscan[wid] = inc;
+    __syncthreads();
+    int off = inc - c;
+    n2 = 0;
+#pragma unroll
+    for (int w = 0; w < MWG_NT / 64; ++w) {
+      if (w < wid) off += iscan[w];
+      n2 += iscan[w];
+    }
+#pragma unroll
+    for (int e = 0; e < SPT; ++e)
+      if (o8[e] && k8[e] >= T1) {
+        L2v[off] = Lv[tid * SPT + e];
+        L2i[off] = Li[tid * SPT + e];
+        ++off;
+      }
+    __syncthreads();
+  }
+  SSTAMP(10, sm0);
+  // Fast path, one wave, no barriers: <= 256 candidates (4 per lane) -> top-k key; the kept ones
+  // (<= 64: one per lane, index order) -> top-p by each element's mass of strictly larger keys
+  // (kept iff that mass is below p x the kept mass: the tied cut key stays whole), multinomial in
+  // index order -- the same selection and draw as the block path below, which takes the rest.
+  if (wid == 0) {
+    int done = 0;
+    if (n2 <= 256) {
+      float v4[4];
+      uint32_t k4[4];
+      bool o4[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int j = lane * 4 + e;
+        o4[e] = j < n2;
+        v4[e] = o4[e] ? L2v[j] : -INFINITY;
+        k4[e] = fkey(v4[e]);
+      }
+      const uint32_t thr = wave_kth_key<4>(k, k4, o4);
+      int kc = 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) kc += (o4[e] && k4[e] >= thr) ? 1 : 0;
+      int kin = kc;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(kin, o, 64);
+        if (lane >= o) kin += t;
+      }
+      const int nk = __builtin_amdgcn_readlane(kin, 63);
+      if (nk <= 64) {
+        int w = kin - kc;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (o4[e] && k4[e] >= thr) {
+            Kv[w] = v4[e];
+            Kj[w] = lane * 4 + e;
+            ++w;
+          }
+        // (one wave: its LDS accesses execute in order, the reads below see these writes)
+        const bool kv_ok = lane < nk;
+        const float kv = kv_ok ? Kv[lane] : -INFINITY;
+        const int kj = kv_ok ? Kj[lane] : 0;
+        const uint32_t kk = fkey(kv);
+        const float mass = kv_ok ? __expf(kv - M) : 0.f;
+        bool keep = kv_ok;
+        if (pp < 1.f) {
+          const float tot = wave_sum_dpp(mass);
+          float above = 0.f;
+          for (int t = 0; t < nk; ++t) {
+            const uint32_t kt = (uint32_t)__builtin_amdgcn_readlane((int)kk, t);
+            const float mt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mass), t));
+            above += kt > kk ? mt : 0.f;
+          }
+          keep = kv_ok && above < pp * tot;
+        }
+        const float km = keep ? mass : 0.f;
+        const float incl = wave_incl_scan(km, lane);
+        const float total = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(incl), 63));
+        const float u = r * total;
+        const unsigned long long hit = __ballot(keep && incl >= u && total > 0.f);
+        const unsigned long long kb = __ballot(keep);
+        int pl = -1;
+        if (hit) pl = __builtin_ctzll(hit);
+        else if (kb) pl = 63 - __builtin_clzll(kb);  // rounding at the top of the range
+        if (lane == 0) {
+          const int j = pl >= 0 ? __builtin_amdgcn_readlane(kj, pl) : -1;
+          const float vj = pl >= 0 ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(kv), pl)) : -INFINITY;
+          const int id = j >= 0 ? L2i[j] : 0;
+          out_ids[b] = id;
+          if (out_lp) out_lp[b] = j >= 0 ? vj - lZ : -INFINITY;
+          if (seen && j >= 0) seen[(long long)slot * V + id] = 1;
+          if (out_kept) out_kept[b] = (int)__popcll(kb);
+        }
+        done = 1;
+      }
+    }
+    if (lane == 0) sel[1] = done;
   }
   __syncthreads();
-  if (sel[0] < 0 && kept > 0) atomicMax(&sel[0], last_j);  // rounding at the top of the range
-  __syncthreads();
-  if (tid == 0) {
-    const int j = sel[0];
-    const int id = j >= 0 ? Li[j] : 0;
-    out_ids[b] = id;
-    if (out_lp) out_lp[b] = j >= 0 ? Lv[j] - lZ : -INFINITY;
-    if (seen && j >= 0) seen[(long long)slot * V + id] = 1;
-    if (out_kept) out_kept[b] = ktot;
+  if (!sel[1]) {
+    if (nv <= MWG_NT) tail(std::integral_constant<int, 1>{});
+    else tail(std::integral_constant<int, SPT>{});
   }
   SSTAMP(12, sm0);
 }

@@ -72,6 +72,48 @@ KCA_API int kca_gelu_bwd(const void* dy, const void* u, void* du, long long n,
   return 0;
 }
 
+// CLIP's quick GELU, x * sigmoid(1.702 x) (one pass instead of torch's mul + sigmoid + mul)
+__global__ void quick_gelu_fwd_kernel(const bf16_t* __restrict__ u, bf16_t* __restrict__ y, long long n8) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8;
+       i += (long long)gridDim.x * blockDim.x) {
+    float v[8];
+    load8(u + i * 8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = v[j] / (1.f + __expf(-1.702f * v[j]));
+    store8(y + i * 8, v);
+  }
+}
+
+__global__ void quick_gelu_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ u,
+                                      bf16_t* __restrict__ du, long long n8) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8;
+       i += (long long)gridDim.x * blockDim.x) {
+    float g[8], v[8];
+    load8(dy + i * 8, g);
+    load8(u + i * 8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float sg = 1.f / (1.f + __expf(-1.702f * v[j]));
+      v[j] = g[j] * (sg + 1.702f * v[j] * sg * (1.f - sg));
+    }
+    store8(du + i * 8, v);
+  }
+}
+
+KCA_API int kca_quick_gelu_fwd(const void* u, void* y, long long n, hipStream_t stream) {
+  if (n % 8) return 1;
+  hipLaunchKernelGGL(quick_gelu_fwd_kernel, dim3(kca_grid(n / 8, 256)), dim3(256), 0, stream, (const bf16_t*)u,
+                     (bf16_t*)y, n / 8);
+  return 0;
+}
+
+KCA_API int kca_quick_gelu_bwd(const void* dy, const void* u, void* du, long long n, hipStream_t stream) {
+  if (n % 8) return 1;
+  hipLaunchKernelGGL(quick_gelu_bwd_kernel, dim3(kca_grid(n / 8, 256)), dim3(256), 0, stream, (const bf16_t*)dy,
+                     (const bf16_t*)u, (bf16_t*)du, n / 8);
+  return 0;
+}
+
 // ---------------------------------------------------------------- RoPE
 // In-place rotary embedding on the first `rot` dims of every head of a
 // [tokens, heads, head_dim] view with arbitrary token/head strides (so it runs

@@ -147,10 +147,16 @@ class ResnetBlock2D(nn.Module):
         self.conv2 = nn.Conv2d(cout, cout, 3, padding=1)
         self.conv_shortcut = nn.Conv2d(cin, cout, 1) if cin != cout else None
 
-    def forward(self, x, temb=None):
+    def forward(self, x, temb=None, in_bias=None):
+        """``in_bias`` (inference, folded path): a per-channel bias still owed by x's producer (the
+        VAE encoder's conv_in): normalised through norm1's add and carried by the residual add."""
         if _FOLD_BIAS and not torch.is_grad_enabled() and x.is_cuda and x.dtype == torch.bfloat16 \
                 and x.is_contiguous(memory_format=torch.channels_last) and self.conv1.bias is not None:
-            return self._forward_folded(x, temb)
+            return self._forward_folded(x, temb, in_bias=in_bias)
+        if in_bias is not None:
+            x = x + in_bias.view(1, -1, 1, 1).to(x.dtype)
+        if isinstance(temb, _TembAct):
+            return self._forward_act(x, temb.act)
         if isinstance(temb, _TembAdds):
             temb = temb.temb
         if (_FOLD_BIAS_TRAIN and torch.is_grad_enabled() and x.is_cuda and x.dtype == torch.bfloat16
@@ -174,12 +180,30 @@ class ResnetBlock2D(nn.Module):
                                      x1_add=x1.bias if ph else None)
         return self._forward_folded(raw, temb, xn=xn)
 
-    def _forward_folded(self, x, temb, xn=None):
+    def _forward_act(self, x, act):
+        """Training with the shared silu(temb) (_TembAct)."""
+        if (_FOLD_BIAS_TRAIN and x.is_cuda and x.dtype == torch.bfloat16
+                and x.is_contiguous(memory_format=torch.channels_last) and self.conv1.bias is not None
+                and self.conv2.bias is not None):
+            return self._forward_folded_train(x, None, act=act)
+        h = self.conv1(self.norm1(x))
+        t = self.time_emb_proj(act) if self.time_emb_proj is not None else None
+        h = self.conv2(self.dropout(self.norm2(h, add=t)))
+        sc = self.conv_shortcut(x) if self.conv_shortcut is not None else x
+        return sc + h
+
+    def _forward_folded(self, x, temb, xn=None, in_bias=None):
         """Inference: the convolutions run without bias (MIOpen adds a conv bias in a separate
         broadcast pass over the whole output): conv1's bias joins the time embedding that norm2
         adds inside its statistics, and conv2's (+ the 1x1 shortcut's) bias joins the residual add
         -- one full read+write pass fewer per convolution (profiles/sd_unet_add_attribution_r2.txt)."""
-        h = F.conv2d(self.norm1(x) if xn is None else xn, self.conv1.weight, None, padding=1)
+        if in_bias is not None and (xn is not None or self.conv_shortcut is not None):
+            x = x + in_bias.view(1, -1, 1, 1).to(x.dtype)  # (the fold below needs the identity shortcut)
+            in_bias = None
+        if xn is None:
+            xn = self.norm1(x) if in_bias is None else \
+                self.norm1(x, add=in_bias.float()[None].expand(x.shape[0], -1))
+        h = F.conv2d(xn, self.conv1.weight, None, padding=1)
         add = temb.get(self) if isinstance(temb, _TembAdds) else None  # conv1 bias + time projection, fp32
         if add is None:
             if isinstance(temb, _TembAdds):
@@ -190,10 +214,12 @@ class ResnetBlock2D(nn.Module):
                 add = add + self.time_emb_proj(F.silu(temb)).float()
         h = F.conv2d(self.norm2(h, add=add), self.conv2.weight, None, padding=1)
         _, bias = self._folded_biases()
+        if in_bias is not None:
+            bias = bias + in_bias.float()
         sc = F.conv2d(x, self.conv_shortcut.weight, None) if self.conv_shortcut is not None else x
         return ops.add_bias_nhwc(sc, h, bias)
 
-    def _forward_folded_train(self, x, temb):
+    def _forward_folded_train(self, x, temb, act=None):
         """Training with the convolution biases folded out of the convolutions (as at inference):
         conv1's bias joins the [B, C] time embedding the GroupNorm adds, conv2's (+ the shortcut's)
         joins the residual add (ops.add_bias_nhwc_train, bias gradient by a column sum). Exact:
@@ -201,8 +227,8 @@ class ResnetBlock2D(nn.Module):
         PyTorch's bias-gradient reduction over the full activation."""
         h = F.conv2d(self.norm1(x), self.conv1.weight, None, padding=1)
         add = self.conv1.bias[None].expand(x.shape[0], -1)
-        if self.time_emb_proj is not None and temb is not None:
-            add = add + self.time_emb_proj(F.silu(temb))
+        if self.time_emb_proj is not None and (temb is not None or act is not None):
+            add = add + self.time_emb_proj(act if act is not None else F.silu(temb))
         h = F.conv2d(self.dropout(self.norm2(h, add=add)), self.conv2.weight, None, padding=1)
         bias = self.conv2.bias.float()
         if self.conv_shortcut is not None:
@@ -226,6 +252,14 @@ class ResnetBlock2D(nn.Module):
                 b2 = b2 + self.conv_shortcut.bias.float()
             c = self._fb_cache = (key, self.conv1.bias.float(), b2)
         return c[1], c[2]
+
+
+class _TembAct:
+    """Training: ``silu(temb)`` computed once per UNet forward and shared by every ResNet block's time
+    projection -- one SiLU + one SiLU backward per step instead of one pair per block."""
+
+    def __init__(self, act):
+        self.act = act
 
 
 class _TembAdds:
@@ -790,6 +824,8 @@ class UNet2DConditionModel(nn.Module):
         if (_TEMB_BATCH and _FOLD_BIAS and not torch.is_grad_enabled() and self.channels_last and temb.is_cuda
                 and temb.dtype == torch.bfloat16):
             temb = self._temb_adds(temb)
+        elif torch.is_grad_enabled() and temb.is_cuda and not self.gradient_checkpointing:
+            temb = _TembAct(F.silu(temb))
         ctx = encoder_hidden_states if isinstance(encoder_hidden_states, CtxKV) else \
             encoder_hidden_states.to(sample.dtype)
         if self.channels_last:

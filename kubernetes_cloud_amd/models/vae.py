@@ -125,9 +125,9 @@ class _DownEnc(nn.Module):
         self.resnets = nn.ModuleList([ResnetBlock2D(cin if i == 0 else cout, cout, 0, groups, 1e-6) for i in range(n)])
         self.downsamplers = nn.ModuleList([Downsample2D(cout, pad=0)]) if add_down else None
 
-    def forward(self, x):
-        for r in self.resnets:
-            x = r(x)
+    def forward(self, x, in_bias=None):
+        for i, r in enumerate(self.resnets):
+            x = r(x, None, in_bias) if i == 0 and in_bias is not None else r(x)
         if self.downsamplers is not None:
             x = self.downsamplers[0](x)
         return x
@@ -163,8 +163,18 @@ class Encoder(nn.Module):
         self.conv_out = nn.Conv2d(ch[-1], 2 * c.latent_channels, 3, padding=1)
 
     def forward(self, x):
-        x = self.conv_in(x)
-        for b in self.down_blocks:
+        if (not torch.is_grad_enabled() and x.is_cuda and x.dtype == torch.bfloat16 and self.conv_in.bias is not None
+                and x.is_contiguous(memory_format=torch.channels_last)):
+            # conv_in's bias rides in the first ResNet block (its GroupNorm's add and the residual add)
+            # instead of a broadcast pass over the full-resolution output (16 x 128 x 512^2 at DreamBooth
+            # batch: 0.43 ms)
+            x = F.conv2d(x, self.conv_in.weight, None, padding=1)
+            x = self.down_blocks[0](x, in_bias=self.conv_in.bias)
+            rest = self.down_blocks[1:]
+        else:
+            x = self.conv_in(x)
+            rest = self.down_blocks
+        for b in rest:
             x = b(x)
         x = self.mid_block(x)
         return self.conv_out(self.conv_norm_out(x))

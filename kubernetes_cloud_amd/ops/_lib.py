@@ -44,6 +44,8 @@ _SIGS = {
     "kca_layernorm_bwd": [P, P, P, P, P, P, P, P, P, I, P, I, I, P],
     "kca_gelu_fwd": [P, P, LL, I, P],
     "kca_gelu_bwd": [P, P, P, LL, I, P],
+    "kca_quick_gelu_fwd": [P, P, LL, P],
+    "kca_quick_gelu_bwd": [P, P, P, LL, P],
     "kca_geglu_fwd": [P, P, LL, I, P],
     "kca_add_bias_nhwc": [P, P, P, P, LL, I, P],
     "kca_colsum_bf16": [P, P, I, I, I, P],

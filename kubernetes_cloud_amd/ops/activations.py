@@ -36,8 +36,28 @@ def gelu(u: torch.Tensor, approximate: str = "tanh") -> torch.Tensor:
     return F.gelu(u.float(), approximate="tanh" if approx else "none").to(u.dtype)
 
 
+class _QuickGeluFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, u):
+        u = u.contiguous()
+        y = torch.empty_like(u)
+        _lib.call("kca_quick_gelu_fwd", u.data_ptr(), y.data_ptr(), u.numel(), _lib.stream())
+        ctx.save_for_backward(u)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (u,) = ctx.saved_tensors
+        dy = dy.contiguous()
+        du = torch.empty_like(u)
+        _lib.call("kca_quick_gelu_bwd", dy.data_ptr(), u.data_ptr(), du.data_ptr(), u.numel(), _lib.stream())
+        return du
+
+
 def quick_gelu(x: torch.Tensor) -> torch.Tensor:
-    """CLIP's x * sigmoid(1.702 x)."""
+    """CLIP's x * sigmoid(1.702 x): one native pass on bf16 GPU tensors (torch: mul + sigmoid + mul)."""
+    if _lib.use_native(x) and x.numel() % 8 == 0:
+        return _QuickGeluFn.apply(x)
     return x * torch.sigmoid(1.702 * x)
 
 

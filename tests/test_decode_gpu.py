@@ -686,3 +686,22 @@ def test_sample_multiworkgroup_distribution_and_mixed_rows():
         tie_incl = x >= x[keep].min()  # the kernels keep whole tie groups at a cut
         assert bool(tie_incl[ids[b]]), (b, rows[b])
         assert int(keep.sum()) <= int(out_kept[b]) <= int(tie_incl.sum()) + 1, (b, rows[b])
+
+
+def test_sample_multiworkgroup_wide_ties_take_the_block_path():
+    """Tie groups that leave more than 64 candidates after the top-k cut (or more than 256 after the
+    chunk cuts) miss the single-wave merge and take the block merge: same selection rules -- the
+    whole tie group at the cut is kept, the draw is uniform over it."""
+    torch.manual_seed(9)
+    V, B = 50400, 2048
+    base = torch.randn(V, device=dev) * 0.5
+    top = torch.randperm(V, device=dev)[:300]
+    base[top] = 5.0  # 300 tied maxima: top-k 20 keeps all 300
+    logits = base.to(torch.bfloat16)[None].expand(B, V).contiguous()
+    kept = torch.empty(B, dtype=torch.int32, device=dev)
+    ids, _ = dops.sample_logits(logits, **_params(B, 1.0, 20, 1.0), seeds=torch.randint(0, 2**62, (B,), device=dev),
+                                out_kept=kept)
+    assert int(kept.min()) == int(kept.max()) == 300
+    assert bool((base[ids] == 5.0).all())
+    freq = torch.bincount(ids, minlength=V)[top].float()
+    assert (freq / B - 1 / 300).abs().max() < 0.01

@@ -222,5 +222,25 @@ def test_unet_inference_caches_follow_native_optimizer_steps():
                 if hasattr(mod, a):
                     delattr(mod, a)
         ref = fresh(x, 10, ctx)
+    # a stale cache after an lr 1e-2 Adam step is off by O(1); a rebuilt one by bf16 rounding (the
+    # caches fold weights in fp32 and round once: 1 ulp at the output's max, 2^-6 at 3.5)
     err = (got.float() - ref.float()).abs().max().item()
-    assert err <= 1e-3 * ref.float().abs().max().item(), err
+    assert _rel(got, ref) < 5e-3 and err <= 1e-2 * ref.float().abs().max().item(), (err, _rel(got, ref))
+
+
+def test_vae_encoder_conv_in_bias_fold_matches_plain():
+    """Inference VAE encode: conv_in's bias carried by the first ResNet block (GroupNorm add +
+    residual add) equals the plain biased convolution; the channels-last Downsample2D pad kernel too."""
+    from kubernetes_cloud_amd.models.unet import to_channels_last
+    from kubernetes_cloud_amd.models.vae import AutoencoderKL, VAEConfig
+    torch.manual_seed(2)
+    vae = to_channels_last(AutoencoderKL(VAEConfig(block_out_channels=(64, 128, 128, 128))).to(DEV).bfloat16().eval())
+    for p_ in vae.parameters():
+        if p_.dim() == 1:
+            torch.nn.init.normal_(p_, std=0.1)
+    x = torch.randn(2, 3, 64, 64, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
+    with torch.no_grad():
+        got = vae.encode_moments(x)
+    with torch.enable_grad():  # the unfolded path (and F.pad in the downsamplers)
+        ref = vae.encode_moments(x).detach()
+    assert _rel(got, ref) < 1e-2

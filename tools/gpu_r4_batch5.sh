@@ -3,7 +3,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_suite_r4.log 2>&1 || { tail -40 gpurun_out/gpu_suite_r4.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > gpurun_out/gpu_suite_r4.log 2>&1 || { tail -40 gpurun_out/gpu_suite_r4.log; exit 1; }
 tail -3 gpurun_out/gpu_suite_r4.log
 KCA_KERNEL_LIB=$PWD/ab/libkca_kernels_stamps.so timeout -k 10 120 python -u tools/sample_stamps.py --modes topk10,topk50,topk50_topp0.95 > gpurun_out/sampler_stamps_r4d.txt 2>&1 || { tail -20 gpurun_out/sampler_stamps_r4d.txt; exit 1; }
 cat gpurun_out/sampler_stamps_r4d.txt
