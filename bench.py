@@ -416,7 +416,10 @@ def _extras(args, dev, rec):
         # (loadgen at concurrency 1 / 8 / 32) next to the same requests straight into predict
         sb = _load_bench("serving_bench")
         d = os.environ.get("KCA_WEIGHT_LOAD_DIR", os.environ.get("TMPDIR", "/tmp"))
-        return {"gptj": sb.run_gptj(d), "bloom_slice": sb.run_bloom_slice(8)}
+        out = {"gptj": sb.run_gptj(d), "bloom_slice": sb.run_bloom_slice(8)}
+        torch.cuda.empty_cache()
+        out["sd_txt2img"] = sb.run_sd()  # the txt2img InferenceService contract (PNG per request)
+        return out
 
     try:
         fenced("secondary_dreambooth", dreambooth)

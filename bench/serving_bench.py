@@ -90,13 +90,14 @@ class _Server:
         self.th.join(timeout=30)
 
 
-def _engine(pred, n: int, conc: int, seed: int = 0) -> dict:
+def _engine(pred, n: int, conc: int, seed: int = 0, kind: str = "kserve") -> dict:
     """The same request stream straight into ``predict`` (no HTTP), ``conc`` in flight."""
     import random
 
     from kubernetes_cloud_amd.serving.loadgen import PROMPTS
     rnd = random.Random(seed)
-    payloads = [{"instances": [rnd.choice(PROMPTS)]} for _ in range(n)]
+    payloads = [{"instances": [rnd.choice(PROMPTS)]} if kind == "kserve" else
+                {"prompt": rnd.choice(PROMPTS), "parameters": {"seed": i}} for i in range(n)]
 
     def one(p):
         t = time.perf_counter()
@@ -111,12 +112,12 @@ def _engine(pred, n: int, conc: int, seed: int = 0) -> dict:
             "p99_s": lat[int(0.99 * (n - 1))]}
 
 
-def _client(url: str, n: int, conc: int, model_name: str, seed: int) -> dict:
+def _client(url: str, n: int, conc: int, model_name: str, seed: int, kind: str = "kserve") -> dict:
     """serving/loadgen.py in its own process (as a client on another host would be): it does not
     share the server's interpreter lock."""
     import subprocess
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    cmd = [sys.executable, "-m", "kubernetes_cloud_amd.serving.loadgen", "--url", url, "--kserve", "--requests",
+    cmd = [sys.executable, "-m", "kubernetes_cloud_amd.serving.loadgen", "--url", url, f"--{kind}", "--requests",
            str(n), "--concurrency", str(conc), "--model-name", model_name, "--seed", str(seed), "--json", "-q"]
     env = dict(os.environ, PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""),
                CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
@@ -126,17 +127,17 @@ def _client(url: str, n: int, conc: int, model_name: str, seed: int) -> dict:
     return json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
 
 
-def _levels(pred, model_name: str, new_tokens: int | None, levels=LEVELS) -> list:
+def _levels(pred, model_name: str, new_tokens: int | None, levels=LEVELS, kind: str = "kserve") -> list:
     srv = _Server([pred])
     out = []
     try:
-        _client(srv.url, 4, 4, model_name, 99)  # warm: graphs, allocator
-        _engine(pred, 4, 4, seed=98)
+        _client(srv.url, 4, 4, model_name, 99, kind)  # warm: graphs, allocator
+        _engine(pred, 4, 4, seed=98, kind=kind)
         for conc, n in levels:
             # warm this level's batch buckets first (decode-graph captures), so neither timed pass pays them
-            _engine(pred, 2 * conc, conc, seed=1000 + conc)
-            h = _client(srv.url, n, conc, model_name, conc)
-            e = _engine(pred, n, conc, seed=conc)
+            _engine(pred, 2 * conc, conc, seed=1000 + conc, kind=kind)
+            h = _client(srv.url, n, conc, model_name, conc, kind)
+            e = _engine(pred, n, conc, seed=conc, kind=kind)
             rec = {"concurrency": conc, "requests": n, "successes": h["successes"],
                    "http_rps": round(h["throughput_rps"], 3),
                    **({"http_tokens_per_s": round(h["goodput_rps"] * new_tokens, 1)} if new_tokens else {}),
@@ -213,12 +214,44 @@ def run_bloom_slice(layers: int = 8, levels=LEVELS, overrides: dict | None = Non
             "data": "random-init weights, loadgen prompts"}
 
 
+SD_LEVELS = ((1, 4), (4, 8), (8, 16))
+
+
+def run_sd(levels=SD_LEVELS, resolution: int = 512, steps: int = 50) -> dict:
+    """The txt2img predictor (serving/sd_service.py: ``{"prompt", "parameters"}`` -> PNG, dynamic
+    micro-batcher up to 8) on random-init SD-1.5 weights, LMS 50 steps, CFG 7, 512 px."""
+    import importlib.util
+
+    from kubernetes_cloud_amd.models.schedulers import load_scheduler, sd_scheduler_config
+    from kubernetes_cloud_amd.models.sd_pipeline import StableDiffusionPipeline
+    from kubernetes_cloud_amd.serving.sd_service import SDPredictor
+    root = os.path.dirname(os.path.abspath(__file__))
+    spec = importlib.util.spec_from_file_location("_sdb", os.path.join(root, "sd_bench.py"))
+    sdb = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(sdb)
+    dev = _device()
+    unet, vae, te = sdb.build(dev, torch.bfloat16 if dev.type == "cuda" else torch.float32)
+    d = tempfile.mkdtemp(prefix="kca_sd_tok_")
+    try:
+        tok = _tokenizer(d)
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    tok.pad_token = tok.eos_token
+    pipe = StableDiffusionPipeline(unet, vae, te, tok, load_scheduler(sd_scheduler_config(), "LMSDiscreteScheduler"))
+    pred = SDPredictor("sd", "random-init", pipeline=pipe, num_inference_steps=steps, width=resolution,
+                       height=resolution, max_batch=8)
+    lv = _levels(pred, "sd", None, levels, kind="sd")
+    return {"metric": "SD-1.5 txt2img predictor over HTTP (PNG responses)", "resolution": resolution,
+            "steps": steps, "guidance": 7.0, "scheduler": "LMSDiscreteScheduler", "micro_batch_max": 8,
+            "levels": lv, "data": "random-init weights, loadgen prompts; images/s = req/s"}
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--which", default="gptj,bloom_slice")
+    ap.add_argument("--which", default="gptj,bloom_slice,sd")
     a = ap.parse_args()
     for w in a.which.split(","):
-        r = run_gptj() if w == "gptj" else run_bloom_slice()
+        r = run_gptj() if w == "gptj" else (run_sd() if w == "sd" else run_bloom_slice())
         print(json.dumps(r), flush=True)
 
 
