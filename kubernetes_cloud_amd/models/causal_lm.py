@@ -222,6 +222,11 @@ class CausalLM(nn.Module):
                 p.zero_()
         return self
 
+    # train/engine.py: ZeRO-1/2 parameter all-gathers may finish under the next forward -- every
+    # parameter is read inside a ModuleList block's forward or by a module called for it (wte, ln_f,
+    # lm_head; the tied head reads wte after the embedding's pre-hook)
+    supports_deferred_param_gather = True
+
     def enable_tn_grads(self, on: bool = True):
         """TN-layout backward GEMMs for the block linears (ops/linear.py): keeps a
         transposed bf16 copy of each block weight (+1x the block weights in HBM).

@@ -138,6 +138,18 @@ def find_units(model: nn.Module) -> list:
     return [model] + blocks
 
 
+def param_consumers(model: nn.Module) -> list:
+    """Forward-order modules that read the trainable params (stages 1-2 deferred all-gather): every
+    element of every ``nn.ModuleList`` that owns params (a transformer block, read as a whole -- fused
+    block paths take their sub-layers' weights directly), then each remaining module with direct
+    params (embeddings, final norm, head -- each is called as a module where it is used)."""
+    blocks = find_units(model)[1:]
+    claimed = {id(p) for b in blocks for p in b.parameters()}
+    leaves = [m for m in model.modules()
+              if any(p.requires_grad and id(p) not in claimed for p in m.parameters(recurse=False))]
+    return leaves + blocks
+
+
 def _param_linear_forward(mod: nn.Linear, x):
     from ..ops.linear import param_linear
     return param_linear(x, mod.weight, mod.bias)
@@ -302,6 +314,28 @@ class TrainEngine:
                     m.register_forward_hook(functools.partial(self._post_fwd, u)),
                     m.register_full_backward_pre_hook(functools.partial(self._pre_bwd, u)),
                 ]
+
+        # ---- stages 1-2: deferred parameter all-gather. AdamW updates the rank's shard; instead of
+        # gathering every bucket right after it (an exposed collective of all the bf16 params: ~12 GB
+        # for GPT-J, tens of ms over xGMI at 8 ranks), step() launches the gathers asynchronously in
+        # forward order and each consumer module's forward pre-hook makes the compute stream wait
+        # for just its buckets (then re-derives its transposed weight copies): the next step's
+        # forward runs under the remaining gathers. Models opt in (supports_deferred_param_gather);
+        # state_dict() / publish() / sync_params() wait for everything. KCA_DEFER_ALLGATHER=0: off.
+        import os as _os
+        self._defer_ag = (self.sharded and not self.part_params and self.world > 1
+                          and getattr(model, "supports_deferred_param_gather", False)
+                          and _os.environ.get("KCA_DEFER_ALLGATHER", "1") not in ("0", "false"))
+        self._ag_works: dict = {}
+        self._consumers = []
+        if self._defer_ag:
+            for m in param_consumers(model):
+                bs = sorted({self._by_param[id(p)].bucket for p in m.parameters() if id(p) in self._by_param})
+                if bs:
+                    self._consumers.append([m, bs, False])  # module, buckets, needs refresh
+            for c in self._consumers:
+                self._mod_hooks.append(c[0].register_forward_pre_hook(functools.partial(self._pre_consume, c)))
+            self._mod_hooks.append(model.register_state_dict_pre_hook(lambda *a, **k: self.sync_params()))
 
         # ---- gradient hooks
         self._micro = 0
@@ -686,16 +720,73 @@ class TrainEngine:
             dist.all_reduce(sumsq, group=self._norm_group)
         self.opt.set_clip(sumsq, self.max_grad_norm, inv)
         self.opt.step(lr, use_clip=True)
+        deferred = False
         if self.sharded and not self.part_params:
-            self._all_gather_params()
+            if self._defer_ag:
+                self._launch_param_gathers()
+                deferred = True
+            else:
+                self._all_gather_params()
         if self.loss_scaler is not None and self.loss_scaler.enabled:
             self.loss_scaler.update(bool(self.opt.skipped.item()))
-        self._refresh_derived()
+        self._refresh_derived(deferred=deferred)
         self._micro = 0
         self._works = []
         self._bucket_done = [0] * len(self.buckets)
         self._bucket_launched = [False] * len(self.buckets)
         self._touched = set()
+
+    def _launch_param_gathers(self):
+        """Every bucket's bf16 all-gather, async, in the consumers' forward order."""
+        self.sync_params()  # (a previous step's gathers not consumed yet: finish them first)
+        order, seen = [], set()
+        for c in self._consumers:
+            for b in c[1]:
+                if b not in seen:
+                    seen.add(b)
+                    order.append(b)
+        order += [b for b in range(len(self.buckets)) if b not in seen]
+        for b in order:
+            bk = self.buckets[b]
+            piece = bk.size // self.world
+            self._ag_works[b] = dist.all_gather_into_tensor(
+                self.flat[bk.start:bk.start + bk.size], self.shard_bf16[bk.shard_off:bk.shard_off + piece],
+                group=self.group, async_op=True)
+        for c in self._consumers:
+            c[2] = True
+
+    def _pre_consume(self, c, module, args):
+        if not c[2]:
+            return None
+        for b in c[1]:
+            w = self._ag_works.pop(b, None)
+            if w is not None:
+                w.wait()  # the compute stream waits for this bucket's gather (no host block on RCCL)
+        c[2] = False
+        self._refresh_module(module)
+        return None
+
+    @staticmethod
+    def _refresh_module(module):
+        from ..ops.linear import TLinear
+        for m in module.modules():
+            if isinstance(m, TLinear):
+                m.refresh_transposed()
+        fused = getattr(module, "fused", None)
+        if fused is not None and hasattr(fused, "refresh"):
+            fused.refresh()
+
+    def sync_params(self):
+        """Finish every deferred parameter gather and re-derive what depends on the params."""
+        if not self._ag_works and not any(c[2] for c in self._consumers):
+            return
+        for w in list(self._ag_works.values()):
+            w.wait()
+        self._ag_works.clear()
+        for c in self._consumers:
+            if c[2]:
+                c[2] = False
+                self._refresh_module(c[0])
 
     def _all_gather_params(self):
         ws = []
@@ -751,12 +842,14 @@ class TrainEngine:
         self.opt.load_state_dict(sd)
         self.publish(self.opt.master)
 
-    def _refresh_derived(self):
-        """Weights changed: re-derive per-model caches (transposed weight copies, UNet tables)."""
+    def _refresh_derived(self, deferred: bool = False):
+        """Weights changed: re-derive per-model caches (transposed weight copies, UNet tables).
+        ``deferred``: the params are still being gathered; each consumer re-derives its own copies
+        in its forward pre-hook."""
         inv = getattr(self.model, "invalidate_weight_caches", None)
         if inv is not None:
             inv()
-        if self.part_params:
+        if self.part_params or deferred:
             return
         fn = getattr(self.model, "refresh_transposed_weights", None)
         if fn is not None:
@@ -765,6 +858,7 @@ class TrainEngine:
     def publish(self, master_like: torch.Tensor):
         """Write bf16 model params from an fp32 tensor laid out like the
         optimizer master (the shard when ZeRO>=1), e.g. EMA weights for export."""
+        self.sync_params()
         if self.sharded:
             self.shard_bf16.copy_(master_like)
             if not self.part_params:

@@ -45,9 +45,13 @@ def _worker(rank, world, port, stage, bucket, ckpt, out_path):
     m.train()
     eng = TrainEngine(m, lr=1e-2, weight_decay=0.01, zero_stage=stage, grad_accum=2, bucket_elems=bucket)
     mem = eng.memory_report()
+    # ZeRO-1/2: the parameter all-gathers finish under the next forward (per-consumer waits)
+    assert eng._defer_ag == (stage in (1, 2) and os.environ.get("KCA_DEFER_ALLGATHER", "1") != "0")
     for step in _batches(world, 2):
         mbs = [b[rank * 2:(rank + 1) * 2] for b in step]
         eng.train_batch(mbs, lambda ids: m(ids, labels=ids))
+        if eng._defer_ag:
+            assert eng._ag_works, "step() should leave the param gathers in flight"
     if stage == 3:  # released between steps: only this rank's shard is resident
         assert all(p.numel() == 0 for p in m.parameters()), "ZeRO-3 params not released"
     with eng.gathered():
