@@ -26,7 +26,7 @@ import torch.nn.functional as F
 
 from .. import ops
 from ..ops import _lib
-from ..ops.linear import SplitKLinear, linear_residual, linear_splitk_wgrad
+from ..ops.linear import SplitKLinear, linear_residual, linear_residual_train, linear_splitk_wgrad
 from ..ops.upsample import (phase_gemm_weights, phase_to_dense, phase_weights, upsample_conv_phase,
                            upsample_conv_train, upsample_nearest2x)
 
@@ -510,9 +510,9 @@ class BasicTransformerBlock(nn.Module):
         # the residual adds after attn1 / attn2 ride in the next LayerNorm kernel
         n2, x = self.norm2(self.attn1(self.norm1(x)), residual=(x,))
         n3, x = self.norm3(self.attn2(n2, ctx), residual=(x,))
-        if _FUSE_RES and not torch.is_grad_enabled():  # FF out-projection + bias + residual: one GEMM
+        if _FUSE_RES:  # FF out-projection + bias + residual: one GEMM (training: with its own backward)
             out = self.ff.net[2]
-            return linear_residual(self.ff.net[0](n3), out.weight, out.bias, x)
+            return linear_residual_train(self.ff.net[0](n3), out.weight, out.bias, x)
         return x + self.ff(n3)
 
 
@@ -536,10 +536,10 @@ class Transformer2DModel(nn.Module):
             t = _proj(self.proj_in, t)
             for blk in self.transformer_blocks:
                 t = blk(t, ctx)
-            if _FUSE_RES and not torch.is_grad_enabled():  # proj_out + bias + residual: one GEMM
+            if _FUSE_RES:  # proj_out + bias + residual: one GEMM (training: with its own backward)
                 w = self.proj_out.weight
-                o = linear_residual(t, w.reshape(w.shape[0], w.shape[1]), self.proj_out.bias,
-                                    res.permute(0, 2, 3, 1))
+                o = linear_residual_train(t, w.reshape(w.shape[0], w.shape[1]), self.proj_out.bias,
+                                          res.permute(0, 2, 3, 1))
                 return o.permute(0, 3, 1, 2)
             t = _proj(self.proj_out, t)
             return t.view(B, H, W, C).permute(0, 3, 1, 2) + res

@@ -257,6 +257,46 @@ def _workspace(dev: torch.device) -> torch.Tensor | None:
     return ws
 
 
+class _LinearResidualFn(torch.autograd.Function):
+    """Training ``res + F.linear(x, W, b)``: the forward is the one-GEMM epilogue form; the backward
+    passes dY through to ``res`` (no copy), dX = dY W, dW by the split-K weight gradient, db by the
+    column-sum kernel -- the residual add's separate read-read-write pass is gone."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, res):
+        with torch.no_grad():
+            y = linear_residual(x, weight, bias, res)
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gb = None
+        gx, gw, gb0 = _LinearSplitKW.backward(_Saved(x, w, ctx.has_bias, ctx.needs_input_grad[:3]), gy)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            gb = gb0
+        return gx, gw, gb, (gy if ctx.needs_input_grad[3] else None)
+
+
+class _Saved:
+    """ctx stand-in for reusing _LinearSplitKW.backward."""
+
+    def __init__(self, x, w, has_bias, needs):
+        self.saved_tensors = (x, w)
+        self.has_bias = has_bias
+        self.needs_input_grad = tuple(needs)
+
+
+def linear_residual_train(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None,
+                          res: torch.Tensor) -> torch.Tensor:
+    """``res + F.linear(x, weight, bias)`` with autograd, fused on the GPU (see _LinearResidualFn)."""
+    if torch.is_grad_enabled() and _lib.use_native(x, weight, res) and res.stride(-1) == 1 and x.stride(-1) == 1:
+        return _LinearResidualFn.apply(x, weight, bias, res)
+    return linear_residual(x, weight, bias, res)
+
+
 def linear_residual(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None,
                     res: torch.Tensor) -> torch.Tensor:
     """``res + F.linear(x, weight, bias)`` in ONE hipBLASLt GEMM (bias and residual in its epilogue,

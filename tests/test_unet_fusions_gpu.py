@@ -244,3 +244,25 @@ def test_vae_encoder_conv_in_bias_fold_matches_plain():
     with torch.enable_grad():  # the unfolded path (and F.pad in the downsamplers)
         ref = vae.encode_moments(x).detach()
     assert _rel(got, ref) < 1e-2
+
+
+@pytest.mark.parametrize("tokens", [4096, 65536])
+def test_linear_residual_train_grads_match_reference(tokens):
+    """Training res + x W^T + b in one GEMM epilogue (ops.linear_residual_train): the output and the
+    x / W / b / res gradients match the two-pass autograd form in fp32."""
+    from kubernetes_cloud_amd.ops.linear import linear_residual_train
+    torch.manual_seed(4)
+    K, N = 640, 320
+    x = (torch.randn(tokens, K, device=DEV) * 0.5).bfloat16().requires_grad_(True)
+    w = (torch.randn(N, K, device=DEV) / K ** 0.5).bfloat16().requires_grad_(True)
+    b = torch.randn(N, device=DEV).bfloat16().requires_grad_(True)
+    r = torch.randn(tokens, N, device=DEV).bfloat16().requires_grad_(True)
+    y = linear_residual_train(x, w, b, r)
+    g = torch.randn_like(y)
+    y.backward(g)
+    xf, wf, bf, rf = (t.detach().float().requires_grad_(True) for t in (x, w, b, r))
+    yf = rf + xf @ wf.t() + bf
+    yf.backward(g.float())
+    assert _rel(y, yf) < 1e-2
+    for got, ref in ((x.grad, xf.grad), (w.grad, wf.grad), (b.grad, bf.grad), (r.grad, rf.grad)):
+        assert _rel(got, ref) < 2e-2
