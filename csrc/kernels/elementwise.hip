@@ -472,6 +472,44 @@ KCA_API int kca_add_bias_nhwc(const void* a, const void* b, const float* bias, v
   return 0;
 }
 
+// Training form: the two convolution biases (conv2's, the 1x1 shortcut's or null) are read as the
+// bf16 parameters themselves -- no per-step fp32 casts and adds of them on the host side.
+__global__ void add_bias2_nhwc_kernel(const bf16_t* __restrict__ a, const bf16_t* __restrict__ b,
+                                      const bf16_t* __restrict__ b1, const bf16_t* __restrict__ b2,
+                                      bf16_t* __restrict__ out, int c8, long long n8) {
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < n8;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(t % c8) * 8;
+    float x[8], y[8];
+    load8(a + t * 8, x);
+    if (b) {
+      load8(b + t * 8, y);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] += y[j];
+    }
+    load8(b1 + c, y);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] += y[j];
+    if (b2) {
+      load8(b2 + c, y);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] += y[j];
+    }
+    store8(out + t * 8, x);
+  }
+}
+
+KCA_API int kca_add_bias2_nhwc(const void* a, const void* b, const void* bias1, const void* bias2, void* out,
+                               long long n, int C, hipStream_t stream) {
+  if (C % 8 || n % C || !a || !bias1 || !out) return 1;
+  if (((uintptr_t)a | (uintptr_t)b | (uintptr_t)out | (uintptr_t)bias1 | (uintptr_t)bias2) & 15) return 2;
+  const long long n8 = n / 8;
+  if (n8 == 0) return 0;
+  hipLaunchKernelGGL(add_bias2_nhwc_kernel, dim3(kca_grid(n8, 256, 8192)), dim3(256), 0, stream, (const bf16_t*)a,
+                     (const bf16_t*)b, (const bf16_t*)bias1, (const bf16_t*)bias2, (bf16_t*)out, C / 8, n8);
+  return 0;
+}
+
 // ---------------------------------------------------------------- column sums (bias gradients)
 // part[by][c] = sum over rows [by*RB, by*RB + RB) of x[r][c], x [M][N] bf16 row-major (N % 8 == 0):
 // 32 column groups of 8 (16-B loads, coalesced along the row) x 8 row lanes per workgroup, the row

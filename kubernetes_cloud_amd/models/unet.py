@@ -230,14 +230,13 @@ class ResnetBlock2D(nn.Module):
         if self.time_emb_proj is not None and (temb is not None or act is not None):
             add = add + self.time_emb_proj(act if act is not None else F.silu(temb))
         h = F.conv2d(self.dropout(self.norm2(h, add=add)), self.conv2.weight, None, padding=1)
-        bias = self.conv2.bias.float()
+        b2 = None
         if self.conv_shortcut is not None:
             sc = F.conv2d(x, self.conv_shortcut.weight, None)
-            if self.conv_shortcut.bias is not None:
-                bias = bias + self.conv_shortcut.bias.float()
+            b2 = self.conv_shortcut.bias
         else:
             sc = x
-        return ops.add_bias_nhwc_train(sc, h, bias)
+        return ops.add_bias2_nhwc_train(sc, h, self.conv2.bias, b2)  # bf16 biases read in the kernel
 
     def _folded_biases(self):
         """fp32 conv1 bias and conv2 (+ shortcut) bias, cached while the parameters are unchanged

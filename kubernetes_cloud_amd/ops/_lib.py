@@ -48,6 +48,7 @@ _SIGS = {
     "kca_quick_gelu_bwd": [P, P, P, LL, P],
     "kca_geglu_fwd": [P, P, LL, I, P],
     "kca_add_bias_nhwc": [P, P, P, P, LL, I, P],
+    "kca_add_bias2_nhwc": [P, P, P, P, P, LL, I, P],
     "kca_colsum_bf16": [P, P, I, I, I, P],
     "kca_geglu_bwd": [P, P, P, LL, I, P],
     "kca_rope": [P, P, I, I, LL, I, LL, LL, LL, LL, I, I, P, P, P, F, P],

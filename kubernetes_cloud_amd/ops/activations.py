@@ -129,6 +129,42 @@ class _AddBiasNHWCFn(torch.autograd.Function):
         return d, (d if ctx.has_b else None), db
 
 
+class _AddBias2NHWCFn(torch.autograd.Function):
+    """``a + b + bias1 + bias2`` (channels-last) with the bf16 bias parameters read in the kernel; the
+    backward's column sum lands in bf16 once and is the gradient of both biases."""
+
+    @staticmethod
+    def forward(ctx, a, b, bias1, bias2):
+        ctx.C = a.shape[1]
+        ctx.has_b, ctx.has_b2 = b is not None, bias2 is not None
+        out = torch.empty_like(a)
+        _lib.call("kca_add_bias2_nhwc", a.data_ptr(), _lib.ptr(b), bias1.data_ptr(), _lib.ptr(bias2),
+                  out.data_ptr(), a.numel(), a.shape[1], _lib.stream())
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        from .linear import column_sum
+        d = dout.contiguous(memory_format=torch.channels_last)
+        db = column_sum(d.permute(0, 2, 3, 1).reshape(-1, ctx.C), out_dtype=torch.bfloat16)
+        return d, (d if ctx.has_b else None), db, (db if ctx.has_b2 else None)
+
+
+def add_bias2_nhwc_train(a: torch.Tensor, b: torch.Tensor | None, bias1: torch.Tensor,
+                         bias2: torch.Tensor | None) -> torch.Tensor:
+    """``a + b + bias1 + bias2`` for the SD ResNet block's residual add (training): bf16 biases as
+    parameters, one native pass; falls back to add_bias_nhwc_train off the fast path."""
+    ok = (_lib.use_native(a, bias1) and a.dim() == 4 and a.shape[1] % 8 == 0 and bias1.is_contiguous()
+          and a.is_contiguous(memory_format=torch.channels_last) and _lib.has("kca_add_bias2_nhwc")
+          and (bias2 is None or (bias2.dtype == torch.bfloat16 and bias2.is_contiguous()))
+          and (b is None or (b.shape == a.shape and b.dtype == a.dtype
+                             and b.is_contiguous(memory_format=torch.channels_last))))
+    if not ok:
+        bias = bias1.float() + (bias2.float() if bias2 is not None else 0.0)
+        return add_bias_nhwc_train(a, b, bias)
+    return _AddBias2NHWCFn.apply(a, b, bias1, bias2)
+
+
 def add_bias_nhwc_train(a: torch.Tensor, b: torch.Tensor | None, bias: torch.Tensor) -> torch.Tensor:
     """``a + b + bias`` (channels-last) with autograd; the inference kernel when no grad is recorded."""
     if torch.is_grad_enabled() and (a.requires_grad or (b is not None and b.requires_grad) or bias.requires_grad):

@@ -4,7 +4,7 @@ computed directly from every rank's gradient, is bitwise identical on all
 ranks, reduces to the mean-free sum for orthogonal gradients and to the
 gradient itself for identical ones, and the ResNet trainer runs with it."""
 import os
-import socket
+import tempfile
 
 import pytest
 import torch
@@ -15,9 +15,11 @@ from kubernetes_cloud_amd.train.resnet import adasum_pair
 
 
 def _port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    # a file store: no TCP port to race for when the suite runs under pytest-xdist
+    fd, path = tempfile.mkstemp(prefix="kca_adasum_")
+    os.close(fd)
+    os.unlink(path)
+    return path
 
 
 def _grads(world, n=300, seed=0):
@@ -30,8 +32,7 @@ def _seg(n=300):
 
 
 def _worker(rank, world, port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=f"file://{port}", rank=rank, world_size=world)
     from kubernetes_cloud_amd.train.resnet import adasum_allreduce
     buf = _grads(world)[rank].clone()
     seg, n = _seg()
@@ -42,8 +43,7 @@ def _worker(rank, world, port, q):
 
 
 def _hier_worker(rank, world, port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=f"file://{port}", rank=rank, world_size=world)
     from kubernetes_cloud_amd.train.resnet import adasum_groups, hierarchical_adasum
     lg, cg = adasum_groups(world, rank, 2)
     buf = _grads(world)[rank].clone()
