@@ -39,6 +39,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tokens", type=int, default=32768)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--layer-gemms", action="store_true",
+                    help="also time the block's forward / data-grad GEMMs (TN, as ops/fused_block.py issues them)")
     ap.add_argument("--tunableop", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                          "tuning", "tunableop_results.csv"))
     args = ap.parse_args()
@@ -81,6 +83,19 @@ def main():
                           "fused_pf": round(fl / t_f / 1e12, 3), "err_split": e_s, "err_fused": e_f}), flush=True)
         del dyt, xt, acc0, acc_s, acc_f, ref
         torch.cuda.empty_cache()
+    if args.layer_gemms:
+        for name, (n, k) in SHAPES.items():
+            x = torch.randn(T, k, device=dev, dtype=torch.bfloat16)
+            w = torch.randn(n, k, device=dev, dtype=torch.bfloat16)
+            dy = torch.randn(T, n, device=dev, dtype=torch.bfloat16)
+            wt = w.t().contiguous()
+            fl = 2.0 * n * k * T
+            t_f = timed(lambda: F.linear(x, w), args.iters)
+            t_d = timed(lambda: F.linear(dy, wt), args.iters)
+            print(json.dumps({"gemm": name, "fwd_ms": round(t_f, 3), "fwd_pf": round(fl / t_f / 1e12, 3),
+                              "dgrad_ms": round(t_d, 3), "dgrad_pf": round(fl / t_d / 1e12, 3)}), flush=True)
+            del x, w, dy, wt
+            torch.cuda.empty_cache()
 
 
 if __name__ == "__main__":

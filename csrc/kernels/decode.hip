@@ -22,6 +22,7 @@
 // [page][kv_head][ps][D] (ps = 1 << ps_shift tokens) and token t of sequence
 // `seq` lives in page tbl[seq * tbl_stride + (t >> ps_shift)] -- requests hold
 // only the pages they use, and beams share their prefix pages.
+#include <cstdio>
 #include <type_traits>
 
 #include "gemv_m1.h"  // gemv_m1_accum / _finish for the fused decode-layer kernels
@@ -144,7 +145,29 @@ struct DecodeParams {
   // arrive combines the partials in place of the separate decode_combine_kernel (nullptr: that kernel)
   unsigned int* cnt;
   int window;  // > 0: attend only the last `window` positions (GPT-Neo local layers)
+  // merged QKV + attention + fc_in launch (decode_qkv_attn_gemv_kernel): per-kv-head QKV readiness
+  // counters (128 B apart), the count that means "all of this head's Q/K/V rows are stored", re-armed
+  // by the head's last split (nullptr elsewhere)
+  unsigned int* ready;
+  int ready_target;
 };
+
+// Merged launch: wait until the QKV GEMV workgroups of kv-head hk have stored their rows. Producer
+// side (recipe R1 of cdna_hip_programming.md Guideline 16): write-through stores drained, barrier,
+// one relaxed agent-scope add; here one lane polls (bounded: a lost count costs a wrong token, never
+// a hung queue), then an agent-scope acquire and a barrier before any load of the QKV row.
+__device__ __forceinline__ void wait_qkv_ready(const DecodeParams& p, int hk) {
+  if (threadIdx.x == 0) {
+    const unsigned* c = p.ready + 32 * hk;
+    for (int it = 0; it < (1 << 18); ++it) {
+      if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)p.ready_target) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
 
 // Partials that another workgroup of the same launch combines: write-through (sc1) stores, so a
 // drain (vmcnt(0)) + barrier + counter add publishes them across XCDs without a release fence
@@ -231,6 +254,8 @@ __device__ void fanin_combine(const DecodeParams& p, int b, int hk, int nsplit) 
     const int last = prev == (unsigned)(nsplit - 1);
     if (last) {
       __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm for the next call
+      // merged launch: every split of this head is past its QKV wait -> re-arm the readiness counter
+      if (p.ready) __hip_atomic_store(p.ready + 32 * hk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -272,7 +297,7 @@ __device__ void fanin_combine(const DecodeParams& p, int b, int hk, int nsplit) 
 // wave step; G query heads share each K/V row (GQA group).
 // (the workgroup's (split, kv-head, sequence) coordinates are arguments: decode_attn_kernel passes
 // its block index, the fused decode-layer kernel below a slice of its grid)
-template <int LPT, int G, bool PAGED, bool ONLINE>
+template <int LPT, int G, bool PAGED, bool ONLINE, bool WAIT = false>
 __device__ __forceinline__ void decode_attn_body(const DecodeParams& p, const int split, const int hk, const int b,
                                                  const int nsplit) {
   constexpr int TPW = 64 / LPT;
@@ -292,16 +317,19 @@ __device__ __forceinline__ void decode_attn_body(const DecodeParams& p, const in
   const int L = p.kv_lens[b];
   const int seq = p.slots[b];
   U16x8 qraw[G];  // inactive lanes read dims [0, 8) (unused) instead of branching around the load
-#pragma unroll
-  for (int g = 0; g < G; ++g)
-    qraw[g] = *reinterpret_cast<const U16x8*>(p.q + b * p.q_bs + (long long)(hk * G + g) * D + (dact ? dslot : 0) * 8);
   const bf16_t* krow = p.q + b * p.q_bs + (long long)(p.H + hk) * D;
   const bf16_t* vrow = p.q + b * p.q_bs + (long long)(p.H + p.Hkv + hk) * D;
   U16x8 knraw, vnraw;  // the new token's K / V slice of lane tid (< ND), from the fused QKV row
-  if (p.fused && tid < ND) {
-    knraw = *reinterpret_cast<const U16x8*>(krow + tid * 8);
-    vnraw = *reinterpret_cast<const U16x8*>(vrow + tid * 8);
-  }
+  auto load_qkv_rows = [&]() {
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+      qraw[g] = *reinterpret_cast<const U16x8*>(p.q + b * p.q_bs + (long long)(hk * G + g) * D + (dact ? dslot : 0) * 8);
+    if (p.fused && tid < ND) {
+      knraw = *reinterpret_cast<const U16x8*>(krow + tid * 8);
+      vnraw = *reinterpret_cast<const U16x8*>(vrow + tid * 8);
+    }
+  };
+  if constexpr (!WAIT) load_qkv_rows();
   // paged: this split's page ids staged in LDS (chunk <= 1024 tokens, pages >= 16 tokens), so a
   // token's address costs an LDS read instead of a dependent global load in front of every K/V
   // load; the whole chunk's range is staged (clipped to the table row), independent of the length
@@ -311,6 +339,10 @@ __device__ __forceinline__ void decode_attn_body(const DecodeParams& p, const in
     const int npg = min(((c0 + p.chunk - 1) >> p.ps_shift) - pg0 + 1, p.tbl_stride - pg0);
     KCA_DASSERT(npg <= 1024 / 16 + 2);
     for (int i = tid; i < npg; i += 256) pg[i] = p.tbl[(long long)seq * p.tbl_stride + pg0 + i];
+  }
+  if constexpr (WAIT) {  // merged launch: the length, slot and page ids arrived while the QKV rows were produced
+    wait_qkv_ready(p, hk);
+    load_qkv_rows();
   }
   const int c1 = min(c0 + p.chunk, L);
   // sliding window: positions below L - window are never read (splits left of it are empty)
@@ -723,14 +755,72 @@ __global__ __launch_bounds__(256) void decode_attn_gemv_kernel(DecodeParams p, i
   const int bid = blockIdx.x;
   if (bid < n_attn) {
     const int split = bid % nsplit, rest = bid / nsplit;
+#ifdef KCA_AB_NO_DEC_ATTN  // timing A/B only (zero attention output): the fc_in GEMV without the attention chain
+    if (split == 0) {
+      const int hk = rest % p.Hkv, b = rest / p.Hkv;
+      for (int i = threadIdx.x; i < G * p.D; i += 256) p.out[b * p.o_bs + (long long)hk * G * p.D + i] = f2bf(0.f);
+    }
+    return;
+#endif
     decode_attn_body<LPT, G, PAGED, ONLINE>(p, split, rest % p.Hkv, rest / p.Hkv, nsplit);
+    DSTAMP(7);
     return;
   }
+  DSTAMP(0);
   const int n0 = (bid - n_attn) * R;
   float acc[R] = {0.f, 0.f, 0.f, 0.f};
   gemv_m1_accum<R>(g.x, g.w, g.N, g.K, n0, acc);
   const float v = gemv_m1_finish<R>(acc, part, g.bias, n0, g.N, g.act);
   if (threadIdx.x < R && n0 + threadIdx.x < g.N) g.y[n0 + threadIdx.x] = f2bf(v);
+  DSTAMP(7);
+}
+
+// Merged decode layer, part 1 (batch 1, H == Hkv): the QKV GEMV, the attention and the fc_in GEMV in
+// ONE launch. Workgroups [0, n_qkv) stream Wqkv head-major (head h's Q, K and V row groups, then head
+// h+1's) and count each head's finished rows; [n_qkv, n_qkv + n_attn) are the attention splits: they
+// resolve the length, the slot and the page ids while the QKV rows are produced, wait for their head's
+// count, then run the RoPE + KV append + split-K attention under the fc_in weight stream of the
+// remaining workgroups. One kernel boundary per layer less than QKV GEMV -> decode_attn_gemv_kernel,
+// and the attention chain starts as soon as its head's rows exist. Every wait is on workgroups with
+// lower indices that never wait themselves, and the attention workgroups (a few hundred) cannot fill
+// the chip's resident slots, so the producers always make progress.
+template <int LPT, bool PAGED, bool ONLINE>
+__global__ __launch_bounds__(256) void decode_qkv_attn_gemv_kernel(DecodeParams p, int nsplit, int n_qkv, int n_attn,
+                                                                   GemvM1 qg, GemvM1 g) {
+  constexpr int R = 4;
+  __shared__ float part[4][R];
+  const int bid = blockIdx.x;
+  if (bid < n_qkv) {
+    DSTAMP(0);
+    const int per = p.D / R;  // row groups per head and per Q / K / V part
+    const int hh = bid / (3 * per), rem = bid % (3 * per);
+    const int n0 = (rem / per) * p.H * p.D + hh * p.D + (rem % per) * R;
+    float acc[R] = {0.f, 0.f, 0.f, 0.f};
+    gemv_m1_accum<R>(qg.x, qg.w, qg.N, qg.K, n0, acc);
+    const float v = gemv_m1_finish<R>(acc, part, qg.bias, n0, qg.N, 0);
+    if (threadIdx.x < R)  // write-through (agent scope): read by attention workgroups on any XCD
+      __hip_atomic_store(reinterpret_cast<unsigned short*>(qg.y + n0 + threadIdx.x), f2bf(v), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(p.ready + 32 * hh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    DSTAMP(7);
+    return;
+  }
+  if (bid < n_qkv + n_attn) {
+    const int a = bid - n_qkv;
+    const int split = a % nsplit, rest = a / nsplit;
+    decode_attn_body<LPT, 1, PAGED, ONLINE, true>(p, split, rest % p.Hkv, rest / p.Hkv, nsplit);
+    DSTAMP(7);
+    return;
+  }
+  DSTAMP(0);
+  const int n0 = (bid - n_qkv - n_attn) * R;
+  float acc[R] = {0.f, 0.f, 0.f, 0.f};
+  gemv_m1_accum<R>(g.x, g.w, g.N, g.K, n0, acc);
+  const float v = gemv_m1_finish<R>(acc, part, g.bias, n0, g.N, g.act);
+  if (threadIdx.x < R && n0 + threadIdx.x < g.N) g.y[n0 + threadIdx.x] = f2bf(v);
+  DSTAMP(7);
 }
 
 constexpr int kDualSub = 64;  // sub-counters of gemv_dual_ln_kernel's arrival (cnt: 32 * (1 + 64) uints)
@@ -750,6 +840,8 @@ struct DualLn {
   float eps;
   bf16_t* xn_out;      // [N] LN(h + y)
   int N, K1, K2, NC;   // NC = 1 + K2 / K1 K-chunks of K1 columns
+  int tail;            // 1: arrival + LayerNorm by the last workgroup; 0 (NC == 1): each workgroup writes
+                       // its rows of h_out = h + y and the next GEMV normalises in its prologue
 };
 
 // Workgroup (chunk c, row group g): R rows x K1 columns -- chunk 0 of W1 . x1, chunk c >= 1 the
@@ -781,7 +873,20 @@ __global__ __launch_bounds__(256) void gemv_dual_ln_kernel(DualLn a) {
     gemv_m1_accum<R>(a.x2 + (long long)(c - 1) * a.K1, a.w2 + (long long)(c - 1) * a.K1, a.N, a.K1, n0, acc, a.K2);
   }
   const float v = gemv_m1_finish<R>(acc, part, nullptr, n0, a.N, 0);
+  if (!a.tail) {  // whole rows (NC == 1): h_out = bf16(h + y + b), nothing crosses workgroups
+    if (tid < R && n0 + tid < a.N) {
+      const float b = a.bias ? bf2f(a.bias[n0 + tid]) : 0.f;
+      a.h_out[n0 + tid] = f2bf(bf2f(a.h[n0 + tid]) + (v + b));
+    }
+    return;
+  }
   if (tid < R && n0 + tid < a.N) st_pub(&a.ypart[(long long)c * a.N + n0 + tid], v);
+#ifdef KCA_AB_NO_DUAL_TAIL  // timing A/B only (wrong output): the K-chunked GEMV without arrival + LayerNorm
+  if (blockIdx.x == 0) {  // keep the residual stream finite: h_out = xn_out = h
+    for (int k = tid; k < a.N; k += 256) { a.h_out[k] = a.h[k]; a.xn_out[k] = a.h[k]; }
+  }
+  return;
+#endif
   // publish (cdna_hip_programming.md Guideline 16, R1): write-through stores drained, barrier, one
   // agent-scope arrival; the last workgroup re-arms the counter and acquires
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1044,6 +1149,18 @@ static int decode_attn_launch(DecodeParams p, float* ws, long long ws_floats, in
   return 0;
 }
 
+// A/B knob: extra dynamic LDS per workgroup (bytes) for the decode layer kernels, which caps the
+// workgroups resident per CU (160 KB / (LDS per workgroup)) -- fewer weight loads in flight, shorter
+// memory latency under load for the attention chain. KCA_DEC_LDS_PAD=<k2>,<k3> (0: off).
+static size_t dec_lds_pad(int which) {
+  static long long pad[2] = {-1, -1};
+  if (pad[0] < 0) {
+    pad[0] = pad[1] = 0;
+    if (const char* e = getenv("KCA_DEC_LDS_PAD")) sscanf(e, "%lld,%lld", &pad[0], &pad[1]);
+  }
+  return (size_t)pad[which];
+}
+
 // Fused decode layer, part 1 (batch 1, see decode_attn_gemv_kernel): kca_decode_prep_attn's
 // arguments plus the fc_in GEMV (gx [gK] -> gy [gN], bias, act). Returns 10 when the shape is
 // outside the instantiated fused variants (G == 1, head_dim 128 / 256, split-K fan-in or one
@@ -1064,7 +1181,7 @@ KCA_API int kca_decode_prep_attn_gemv(const void* qkv, long long ld, const void*
   if (((uintptr_t)gx | (uintptr_t)gw) & 15) return 10;
   DecodeParams p{(const bf16_t*)qkv, ld, (const bf16_t*)kc, (const bf16_t*)vc, cs_slot, cs_head,
                  cs_pos, slots, kv_lens, (bf16_t*)out, o_bs, nullptr, nullptr, alibi, tbl, tbl_stride, ps_shift,
-                 H, Hkv, D, chunk, scale, 1, rot, interleaved, cos_t, sin_t, nullptr, nullptr, window};
+                 H, Hkv, D, chunk, scale, 1, rot, interleaved, cos_t, sin_t, g_decode_stamps, nullptr, window};
   if (tbl && (ps_shift < 4 || ps_shift > 20 || tbl_stride <= 0)) return 5;
   if (chunk <= 0) chunk = kca_decode_chunk(B, Hkv, max_kv);
   if (tbl && chunk > 1024) return 6;
@@ -1087,16 +1204,74 @@ KCA_API int kca_decode_prep_attn_gemv(const void* qkv, long long ld, const void*
     constexpr int LPT = decltype(lpt)::value;
     constexpr int TPB = 4 * (64 / LPT), U = 4;
     if (p.chunk > TPB * U) {
-      const size_t lds = (size_t)4 * (2 + p.D) * sizeof(float);
+      const size_t lds = (size_t)4 * (2 + p.D) * sizeof(float) + dec_lds_pad(0);
       if (p.tbl) hipLaunchKernelGGL((decode_attn_gemv_kernel<LPT, 1, true, true>), grid, dim3(256), lds, stream, p, nsplit, n_attn, g);
       else hipLaunchKernelGGL((decode_attn_gemv_kernel<LPT, 1, false, true>), grid, dim3(256), lds, stream, p, nsplit, n_attn, g);
     } else {
-      const size_t lds = (size_t)(p.chunk + 4 * p.D) * sizeof(float);
+      const size_t lds = (size_t)(p.chunk + 4 * p.D) * sizeof(float) + dec_lds_pad(0);
       if (p.tbl) hipLaunchKernelGGL((decode_attn_gemv_kernel<LPT, 1, true, false>), grid, dim3(256), lds, stream, p, nsplit, n_attn, g);
       else hipLaunchKernelGGL((decode_attn_gemv_kernel<LPT, 1, false, false>), grid, dim3(256), lds, stream, p, nsplit, n_attn, g);
     }
   };
   if (nd <= 16) go(std::integral_constant<int, 16>{});
+  else go(std::integral_constant<int, 32>{});
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// Merged decode layer, part 1 (see decode_qkv_attn_gemv_kernel): kca_decode_prep_attn_gemv's
+// arguments plus the QKV GEMV (gx . qw^T + qbias -> qkv, which is also the attention's input) and
+// `ready`: >= 32 * H zero-initialised unsigned counters (re-armed by every launch). With a single
+// split (short contexts) the attention stays in kca_decode_prep_attn_gemv (returns 10).
+KCA_API int kca_decode_qkv_attn_gemv(const void* qkv, long long ld, const void* kc, const void* vc,
+                                     long long cs_slot, long long cs_head, long long cs_pos,
+                                     const int* slots, const int* kv_lens, void* out, long long o_bs,
+                                     float* ws, long long ws_floats, int B, int H, int Hkv, int D,
+                                     int max_kv, int chunk, float scale, const float* alibi, const int* tbl,
+                                     int tbl_stride, int ps_shift, int rot, int interleaved, const float* cos_t,
+                                     const float* sin_t, int window, const void* gx, const void* gw,
+                                     const void* gbias, void* gy, int gN, int gK, int gact, const void* qw,
+                                     const void* qbias, unsigned int* ready, hipStream_t stream) {
+  if (rot > D || (rot & 1) || (rot > 0 && (!cos_t || !sin_t))) return 8;
+  if (window < 0) return 9;
+  if (B != 1 || H != Hkv || D % 8 || D > 256 || max_kv <= 0 || gK % 8 || gN <= 0 || !ready || !qw) return 10;
+  if (D / 8 <= 8 || ld != 3LL * H * D) return 10;
+  if (((uintptr_t)gx | (uintptr_t)gw | (uintptr_t)qw | (uintptr_t)qkv) & 15) return 10;
+  DecodeParams p{(const bf16_t*)qkv, ld, (const bf16_t*)kc, (const bf16_t*)vc, cs_slot, cs_head,
+                 cs_pos, slots, kv_lens, (bf16_t*)out, o_bs, nullptr, nullptr, alibi, tbl, tbl_stride, ps_shift,
+                 H, Hkv, D, chunk, scale, 1, rot, interleaved, cos_t, sin_t, g_decode_stamps, nullptr, window,
+                 ready, 3 * (D / 4)};
+  if (tbl && (ps_shift < 4 || ps_shift > 20 || tbl_stride <= 0)) return 5;
+  if (chunk <= 0) chunk = kca_decode_chunk(B, Hkv, max_kv);
+  if (tbl && chunk > 1024) return 6;
+  const int nsplit = (max_kv + chunk - 1) / chunk;
+  if (nsplit > 1024) return 7;
+  if (nsplit < 2 || !fanin_enabled()) return 10;  // the split fan-in re-arms the readiness counters
+  p.chunk = chunk;
+  const long long cw = fanin_words(B, H);
+  const long long need = cw + (long long)B * H * nsplit * (D + 2);
+  if (!ws || ws_floats < need) return 4;
+  p.cnt = reinterpret_cast<unsigned int*>(ws);
+  p.ws_o = ws + cw;
+  p.ws_ml = p.ws_o + (long long)B * H * nsplit * D;
+  const GemvM1 q{(const bf16_t*)gx, (const bf16_t*)qw, (const bf16_t*)qbias, (bf16_t*)qkv, 3 * H * D, gK, 0};
+  const GemvM1 g{(const bf16_t*)gx, (const bf16_t*)gw, (const bf16_t*)gbias, (bf16_t*)gy, gN, gK, gact};
+  const int n_qkv = 3 * H * (D / 4);
+  const int n_attn = nsplit * Hkv * B;
+  const dim3 grid(n_qkv + n_attn + (gN + 3) / 4);
+  auto go = [&](auto lpt) {
+    constexpr int LPT = decltype(lpt)::value;
+    constexpr int TPB = 4 * (64 / LPT), U = 4;
+    if (p.chunk > TPB * U) {
+      const size_t lds = (size_t)4 * (2 + p.D) * sizeof(float) + dec_lds_pad(0);
+      if (p.tbl) hipLaunchKernelGGL((decode_qkv_attn_gemv_kernel<LPT, true, true>), grid, dim3(256), lds, stream, p, nsplit, n_qkv, n_attn, q, g);
+      else hipLaunchKernelGGL((decode_qkv_attn_gemv_kernel<LPT, false, true>), grid, dim3(256), lds, stream, p, nsplit, n_qkv, n_attn, q, g);
+    } else {
+      const size_t lds = (size_t)(p.chunk + 4 * p.D) * sizeof(float) + dec_lds_pad(0);
+      if (p.tbl) hipLaunchKernelGGL((decode_qkv_attn_gemv_kernel<LPT, true, false>), grid, dim3(256), lds, stream, p, nsplit, n_qkv, n_attn, q, g);
+      else hipLaunchKernelGGL((decode_qkv_attn_gemv_kernel<LPT, false, false>), grid, dim3(256), lds, stream, p, nsplit, n_qkv, n_attn, q, g);
+    }
+  };
+  if (D / 8 <= 16) go(std::integral_constant<int, 16>{});
   else go(std::integral_constant<int, 32>{});
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
@@ -1124,8 +1299,21 @@ KCA_API int kca_gemv_dual_ln(const void* x1, const void* w1, int K1, const void*
   const int NC = chunked ? 1 + K2 / K1 : 1;
   const DualLn a{(const bf16_t*)x1, (const bf16_t*)w1, (const bf16_t*)x2, (const bf16_t*)w2, (const bf16_t*)bias,
                  ypart, cnt, (const bf16_t*)h, (bf16_t*)h_out, (const bf16_t*)gamma, (const bf16_t*)beta, eps,
-                 (bf16_t*)xn_out, N, K1, K2, NC};
-  hipLaunchKernelGGL(gemv_dual_ln_kernel<4>, dim3(((N + 3) / 4) * NC), dim3(256), 0, stream, a);
+                 (bf16_t*)xn_out, N, K1, K2, NC, 1};
+  hipLaunchKernelGGL(gemv_dual_ln_kernel<4>, dim3(((N + 3) / 4) * NC), dim3(256), dec_lds_pad(1), stream, a);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// Fused decode layer, part 2 without the LayerNorm tail: h_out = h + x1 W1^T + x2 W2^T + bias, each
+// workgroup storing its own rows (h_out may alias h). The next layer's QKV GEMV normalises h_out in
+// its prologue (kca_ln_skinny_gemm), so no workgroup waits for the others.
+KCA_API int kca_gemv_dual_res(const void* x1, const void* w1, int K1, const void* x2, const void* w2, int K2,
+                              const void* bias, const void* h, void* h_out, int N, hipStream_t stream) {
+  if (N <= 0 || K1 % 8 || K2 % 8 || K1 <= 0 || K2 <= 0 || !h || !h_out) return 1;
+  if (((uintptr_t)x1 | (uintptr_t)w1 | (uintptr_t)x2 | (uintptr_t)w2) & 15) return 2;
+  const DualLn a{(const bf16_t*)x1, (const bf16_t*)w1, (const bf16_t*)x2, (const bf16_t*)w2, (const bf16_t*)bias,
+                 nullptr, nullptr, (const bf16_t*)h, (bf16_t*)h_out, nullptr, nullptr, 0.f, nullptr, N, K1, K2, 1, 0};
+  hipLaunchKernelGGL(gemv_dual_ln_kernel<4>, dim3((N + 3) / 4), dim3(256), dec_lds_pad(1), stream, a);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

@@ -33,7 +33,17 @@ import torch
 
 from .. import ops
 from ..ops import decode as dops
-from ..ops.gemv import embed_ln_rows, ln_rows, ln_skinny_linear, skinny_linear
+from ..ops.gemv import embed_ln_rows, ln_gemv_m1, ln_rows, ln_skinny_linear, skinny_linear
+
+# batch-1 fused decode, two measured-slower alternatives kept as A/B switches (docs/PERF.md, round 4):
+# KCA_DECODE_MERGED=1 runs the QKV GEMV, attention and fc_in as one launch (ops/decode.py
+# decode_qkv_attention_gemv: 2.39 vs 2.28 ms/token -- the attention chain, dispatched behind the QKV
+# workgroups, becomes the launch's tail)
+_MERGED_QKV = os.environ.get("KCA_DECODE_MERGED", "0") in ("1", "true")
+# KCA_DECODE_LN_PROLOGUE=1: the out-projection/fc_out kernel stores h + y row by row and the next
+# layer's QKV GEMV normalises in its prologue (ops/gemv.py ln_gemv_m1), no last-workgroup LayerNorm
+# tail -- bit-identical, but 2.33 vs 2.27 ms/token (every QKV workgroup re-reads h, gamma and beta)
+_LN_PROLOGUE = os.environ.get("KCA_DECODE_LN_PROLOGUE", "0") in ("1", "true")
 
 
 def _next_pow2(n: int, lo: int = 1) -> int:
@@ -479,7 +489,9 @@ class ModelRunner:
                 "g": torch.empty(1, f, **z), "h": torch.empty(1, d, **z), "xn": torch.empty(1, d, **z),
                 "ypart": torch.empty((1 + f // d) * d if f % d == 0 else d, device=self.device,
                                      dtype=torch.float32),
-                "cnt": torch.zeros(32 * 65, device=self.device, dtype=torch.int32), "bias": biases}
+                "cnt": torch.zeros(32 * 65, device=self.device, dtype=torch.int32), "bias": biases,
+                "ready": torch.zeros(32 * self.H, device=self.device, dtype=torch.int32),
+                "qkv": torch.empty(1, 3 * self.H * self.D, **z)}
         return fz
 
     def _layers_decode_fused(self, tokens, pos, slots, kv_lens, max_kv, ws, obuf):
@@ -500,15 +512,32 @@ class ModelRunner:
         for li, blk in enumerate(m.h):
             at, mlp = blk.attn, blk.mlp
             act = 1 if mlp.approx in ("tanh", True) else 2
-            qkv = skinny_linear(xn, at.qkv.weight, at.qkv.bias)
             kc, vc = self.cache.k[li], self.cache.v[li]
-            if not dops.decode_prep_attention_gemv(qkv, self.H, self.Hkv, self.D, self.rot, cfg.rotary_interleaved,
-                                                   self.cos, self.sin, pos, slots, kc, vc, kv_lens, max_kv, at.scale,
-                                                   at.alibi, obuf, ws, tbl, at.window, xn, mlp.fc_in.weight,
-                                                   mlp.fc_in.bias, g, act):
+            qkv = None
+            if xn is None:  # the previous layer left h + y un-normalised: LN in the QKV GEMV's prologue
+                qkv = fz["qkv"]
+                if not ln_gemv_m1(h, blk.ln_1.weight, blk.ln_1.bias, blk.ln_1.eps, at.qkv.weight, at.qkv.bias,
+                                  qkv, xb):
+                    raise RuntimeError("fused decode layer: LN-prologue QKV GEMV does not cover the shape")
+                xn = xb
+            # one launch for QKV GEMV + attention + fc_in where the merged kernel covers the shape
+            # (several attention splits); else the QKV GEMV, then attention + fc_in
+            if not (qkv is None and _MERGED_QKV and dops.decode_qkv_attention_gemv(
+                    xn, at.qkv.weight, at.qkv.bias, fz["qkv"], self.H, self.Hkv, self.D, self.rot,
+                    cfg.rotary_interleaved, self.cos, self.sin, pos, slots, kc, vc, kv_lens, max_kv, at.scale,
+                    at.alibi, obuf, ws, tbl, at.window, mlp.fc_in.weight, mlp.fc_in.bias, g, act, fz["ready"])) \
+                    and not dops.decode_prep_attention_gemv(
+                        qkv if qkv is not None else skinny_linear(xn, at.qkv.weight, at.qkv.bias), self.H, self.Hkv,
+                        self.D, self.rot, cfg.rotary_interleaved, self.cos, self.sin, pos, slots, kc, vc, kv_lens,
+                        max_kv, at.scale, at.alibi, obuf, ws, tbl, at.window, xn, mlp.fc_in.weight, mlp.fc_in.bias,
+                        g, act):
                 if li == 0:
                     return None
                 raise RuntimeError("fused decode layer: shape support changed between layers")
+            if _LN_PROLOGUE and li + 1 < len(m.h) and self.D * 3 * self.H == m.h[li + 1].attn.qkv.weight.shape[0]:
+                dops.gemv_dual_res(obuf, at.out.weight, g, mlp.fc_out.weight, fz["bias"][li], h, hb)
+                h, xn = hb, None
+                continue
             nxt = m.h[li + 1].ln_1 if li + 1 < len(m.h) else m.ln_f
             dops.gemv_dual_ln(obuf, at.out.weight, g, mlp.fc_out.weight, fz["bias"][li], h, nxt.weight, nxt.bias,
                               nxt.eps, fz["ypart"], fz["cnt"], hb, xb)

@@ -190,4 +190,22 @@ def ln_skinny_linear(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor | 
     return (y, h, xn) if want_xn else (y, h)
 
 
-__all__ = ["skinny_linear", "ln_skinny_linear", "ln_rows", "ACT"]
+def ln_gemv_m1(h: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor | None, eps: float, weight: torch.Tensor,
+               bias: torch.Tensor | None, y: torch.Tensor, xn_out: torch.Tensor) -> bool:
+    """Decode (one row): y = LayerNorm(h) W^T + b with the normalisation in every GEMV workgroup's
+    register prologue (``kca_ln_skinny_gemm``, gemv1_kernel<4, true>) and workgroup 0 storing LN(h) to
+    ``xn_out`` for a second consumer (GPT-J's fc_in). Returns False when the shape is outside it."""
+    K = h.shape[-1]
+    if not (_lib.use_native(h, weight) and h.shape[0] == 1 and K % 8 == 0 and K <= 8192 and h.is_contiguous()
+            and weight.is_contiguous() and gamma.is_contiguous() and (beta is None or beta.is_contiguous())
+            and (bias is None or bias.dtype == torch.bfloat16)
+            and all(t.data_ptr() % 16 == 0 for t in (h, weight, gamma, xn_out))):
+        return False
+    _set_mode()
+    _lib.call("kca_ln_skinny_gemm", h.data_ptr(), K, None, None, None, K, gamma.data_ptr(), _lib.ptr(beta),
+              float(eps), weight.data_ptr(), _lib.ptr(bias), y.data_ptr(), y.stride(0), 1, weight.shape[0], K, 0,
+              xn_out.data_ptr(), _lib.stream())
+    return True
+
+
+__all__ = ["skinny_linear", "ln_skinny_linear", "ln_rows", "ln_gemv_m1", "ACT"]

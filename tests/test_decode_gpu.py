@@ -600,6 +600,80 @@ def test_decode_attention_gemv_fused_matches_separate(PS, L0):
     assert (y0.float() - y1.float()).abs().max() < 0.02
 
 
+@pytest.mark.parametrize("PS", [0, 64])
+@pytest.mark.parametrize("L0", [40, 600])
+def test_decode_qkv_attention_gemv_merged_matches_separate(PS, L0):
+    """decode_qkv_attn_gemv_kernel (QKV GEMV + attention + fc_in in one launch, the attention waiting
+    on per-head device counters) against the QKV GEMV followed by decode_attn_gemv_kernel: the same
+    QKV row, attention output and cache append bit for bit, the fc_in values within bf16 rounding,
+    and every readiness counter re-armed after each launch."""
+    from kubernetes_cloud_amd.ops.gemv import skinny_linear
+    torch.manual_seed(11 + L0)
+    H, D, rot, L = 16, 256, 64, 1024
+    bf = dict(device=dev, dtype=torch.bfloat16)
+    kc0 = torch.randn(2, H, L, D, device=dev).to(torch.bfloat16)
+    vc0 = torch.randn_like(kc0)
+    tbl = None
+    if PS:
+        kc0, tbl = _paginate(kc0, PS, 3)
+        vc0, _ = _paginate(vc0, PS, 3)
+    cos, sin = rope_tables(rot, L, 10000.0, dev)
+    slots = torch.tensor([1], device=dev, dtype=torch.int32)
+    pos = torch.tensor([L0 - 1], device=dev, dtype=torch.int32)
+    kv_lens = pos + 1
+    xn = torch.randn(1, 4096, **bf)
+    qw, qb = torch.randn(3 * H * D, 4096, **bf) * 0.02, torch.randn(3 * H * D, **bf)
+    gw, gb = torch.randn(16384, 4096, **bf) * 0.02, torch.randn(16384, **bf)
+    ws = torch.zeros(max(dops.decode_ws_floats(1, H, H, D, L), 1), device=dev, dtype=torch.float32)
+    ready = torch.zeros(32 * H, device=dev, dtype=torch.int32)
+    res = []
+    for merged in (False, True, True):
+        kc, vc, out = kc0.clone(), vc0.clone(), torch.empty(1, H * D, **bf)
+        gy = torch.empty(1, 16384, **bf)
+        if merged:
+            qkv = torch.full((1, 3 * H * D), float("nan"), **bf)
+            assert dops.decode_qkv_attention_gemv(xn, qw, qb, qkv, H, H, D, rot, True, cos, sin, pos, slots, kc, vc,
+                                                  kv_lens, L, D ** -0.5, None, out, ws, tbl, 0, gw, gb, gy, 1, ready)
+        else:
+            qkv = skinny_linear(xn, qw, qb)
+            assert dops.decode_prep_attention_gemv(qkv, H, H, D, rot, True, cos, sin, pos, slots, kc, vc,
+                                                   kv_lens, L, D ** -0.5, None, out, ws, tbl, 0, xn, gw, gb, gy, 1)
+        torch.cuda.synchronize()
+        assert int(ready.abs().sum()) == 0
+        res.append((qkv, out, gy, kc, vc))
+    (q0, o0, y0, k0, v0) = res[0]
+    for q1, o1, y1, k1, v1 in res[1:]:
+        assert torch.equal(q0, q1)
+        assert torch.equal(k0, k1) and torch.equal(v0, v1)
+        assert torch.equal(o0, o1)
+        assert torch.equal(y0, y1)
+
+
+def test_engine_fused_b1_ln_prologue_bit_identical(monkeypatch):
+    """The fused batch-1 layer with the LayerNorm in the next QKV GEMV's prologue (gemv_dual_res +
+    ln_gemv_m1) computes the same bf16 values as the last-workgroup LayerNorm tail (gemv_dual_ln):
+    same statistics partition, same rounding -- identical greedy tokens and logits."""
+    from kubernetes_cloud_amd.engine import runner as runner_mod
+    from kubernetes_cloud_amd.engine.llm_engine import LLMEngine, SamplingParams
+    from kubernetes_cloud_amd.models.causal_lm import build_model
+    from kubernetes_cloud_amd.models.config import PRESETS_HF, LMConfig
+    cfg = dict(PRESETS_HF["gpt-j-6b"])
+    cfg.update(n_embd=1024, n_layer=3, n_head=4, rotary_dim=64, n_positions=512)
+    m = build_model(LMConfig.from_hf(cfg), device=dev, dtype=torch.bfloat16, seed=0)
+    p = [int(x) for x in torch.randint(0, 1000, (40,))]
+    sp = SamplingParams(max_new_tokens=12, do_sample=False, logprobs=True)
+    outs = []
+    for pro in (True, False):
+        monkeypatch.setattr(runner_mod, "_LN_PROLOGUE", pro)
+        eng = LLMEngine(m, max_slots=2, max_len=256, use_graphs=True)
+        assert eng.runner._fused_ok
+        r = eng.generate([p], sp)[0]
+        outs.append((r.output, getattr(r, "logprobs", None)))
+    assert outs[0][0] == outs[1][0]
+    if outs[0][1] is not None:
+        assert outs[0][1] == outs[1][1]
+
+
 def test_engine_fused_b1_decode_matches_two_stream():
     """ModelRunner's fused batch-1 GPT-J layer (three launches per layer on one queue) against the
     two-stream form: same greedy tokens where the top-2 logits are not near-tied."""
