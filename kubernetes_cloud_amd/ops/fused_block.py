@@ -88,6 +88,17 @@ def _emit(param: torch.Tensor, grad: torch.Tensor):
     return grad
 
 
+def _emit_wgrad(param: torch.Tensor, a: torch.Tensor, w: torch.Tensor):
+    """Weight gradient ``a w^T`` (TN operands): accumulated by the engine's GEMM sink straight into its
+    fp32 buffer when it has one for ``param``, else computed here and handed on like ``_emit``."""
+    if param is None or not param.requires_grad:
+        return None
+    sink = grad_sink.lookup_gemm(param)
+    if sink is not None and sink(param, a, w):
+        return None
+    return _emit(param, F.linear(a, w))
+
+
 class _FusedBlockFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w_qkv, w_out, w_fc_in, b_fc_in, w_fc_out, b_fc_out, fb, kv_len):
@@ -137,12 +148,12 @@ class _FusedBlockFn(torch.autograd.Function):
         _lib.call("kca_transpose_colsum", dm2.data_ptr(), d, dmt.data_ptr(), T, _lib.ptr(part), T, d, st)
         g_b_out = _emit(mlp.fc_out.bias, _col_sums(part, dt)) if part is not None else None
         dg = F.linear(dm2, mlp.fc_out.weight_t)  # [T, f]
-        g_fc_out = _emit(mlp.fc_out.weight, F.linear(dmt, gt))
+        g_fc_out = _emit_wgrad(mlp.fc_out.weight, dmt, gt)
         if da2.data_ptr() != dm2.data_ptr():
             dat = transpose(da2)
         else:
             dat = dmt
-        g_out = _emit(a.out.weight, F.linear(dat, transpose(o)))
+        g_out = _emit_wgrad(a.out.weight, dat, transpose(o))
         do = F.linear(da2, a.out.weight_t).view(B, S, H, D)
         del dat, dmt
 
@@ -171,9 +182,9 @@ class _FusedBlockFn(torch.autograd.Function):
             dx = F.linear(dqkv, a.qkv.weight_t)
             dx.addmm_(du, mlp.fc_in.weight_t.t())
         xt = transpose(x.reshape(T, d))
-        g_fc_in = _emit(mlp.fc_in.weight, F.linear(dut, xt))
+        g_fc_in = _emit_wgrad(mlp.fc_in.weight, dut, xt)
         del dut, du
-        g_qkv = _emit(a.qkv.weight, F.linear(transpose(dqkv), xt))
+        g_qkv = _emit_wgrad(a.qkv.weight, transpose(dqkv), xt)
         return (dx.view(B, S, d) if dx is not None else None, g_qkv, g_out, g_fc_in, g_b_in, g_fc_out, g_b_out,
                 None, None)
 

@@ -52,6 +52,7 @@ import contextlib
 import dataclasses
 import functools
 import logging
+import os
 
 import torch
 import torch.distributed as dist
@@ -64,6 +65,10 @@ log = logging.getLogger("kca.engine")
 
 ALIGN = 64
 _NONE, _INFLIGHT, _READY = 0, 1, 2
+# weight gradients that fused ops hand over as GEMM operands (ops/fused_block.py) are accumulated
+# by the GEMM itself into the fp32 buffer (ops/linear.py gemm_acc_f32); KCA_WGRAD_GEMM_ACC=0: a bf16
+# dW GEMM, then the accumulation kernel
+_GEMM_ACC = os.environ.get("KCA_WGRAD_GEMM_ACC", "1") not in ("0", "false")
 # gradients of at most this many elements are accumulated in batches (kca_accum_grad_multi);
 # KCA_MULTI_ACCUM=0 launches kca_accum_grad per parameter
 _SMALL_GRAD = 1 << 18
@@ -355,6 +360,8 @@ class TrainEngine:
         self._hooks = [s.param.register_post_accumulate_grad_hook(self._hook) for s in slots]
         for s in slots:
             grad_sink.register(s.param, self._accum)
+            if _GEMM_ACC:
+                grad_sink.register_gemm(s.param, self._accum_gemm)
         self.native = dev.type == "cuda"
         # TN-layout backward GEMMs (ops/linear.py) for models that support them (they keep
         # full transposed weight copies, so not with partitioned params)
@@ -451,12 +458,8 @@ class TrainEngine:
         p.grad = None
         self._accum(p, g)
 
-    def _accum(self, p: torch.Tensor, g: torch.Tensor):
-        """Add one micro-batch gradient of ``p`` into fp32 storage (the full grad
-        buffer, or the bucket's staging buffer under ZeRO-2/3) and launch the
-        bucket's collective once the bucket is complete. Also the gradient sink
-        (ops/grad_sink.py) that fused ops (ops/fused_block.py) call directly
-        with row-strided column slices of a concatenated-weight dW."""
+    def _dst(self, p: torch.Tensor):
+        """(slot, fp32 destination of p's gradient this micro-batch, write-not-add, first micro-batch)."""
         s = self._by_param[id(p)]
         first_micro = id(p) not in self._seen
         # stages 0-1 accumulate across micro-batches in the full buffer; 2-3 start a fresh staging buffer
@@ -469,6 +472,28 @@ class TrainEngine:
             dst = st[s.offset - bk.start:s.offset - bk.start + s.numel]
         else:
             dst = self.grad[s.offset:s.offset + s.numel]
+        return s, dst, first, first_micro
+
+    def _accum_gemm(self, p: torch.Tensor, a: torch.Tensor, w: torch.Tensor) -> bool:
+        """Gradient sink for weight gradients given as GEMM operands (ops/fused_block.py): dW = a w^T
+        accumulated by ONE hipBLASLt GEMM into the fp32 storage (beta 0 on the first write, 1 after;
+        alpha the micro-batch scale) -- no bf16 dW, no accumulation pass. False: not applicable."""
+        from ..ops.linear import gemm_acc_f32
+        if not self.native or p.dim() != 2 or id(p) in self._pend_ids:
+            return False
+        s, dst, first, first_micro = self._dst(p)
+        if not gemm_acc_f32(a, w, dst.view(p.shape), 1.0 / self.grad_accum, 0.0 if first else 1.0):
+            return False
+        self._accounted(p, s, first_micro)
+        return True
+
+    def _accum(self, p: torch.Tensor, g: torch.Tensor):
+        """Add one micro-batch gradient of ``p`` into fp32 storage (the full grad
+        buffer, or the bucket's staging buffer under ZeRO-2/3) and launch the
+        bucket's collective once the bucket is complete. Also the gradient sink
+        (ops/grad_sink.py) that fused ops (ops/fused_block.py) call directly
+        with row-strided column slices of a concatenated-weight dW."""
+        s, dst, first, first_micro = self._dst(p)
         scale = 1.0 / self.grad_accum
         if g.dim() == 4 and _is_cl(p):  # flat slot holds the NHWC order
             g = g.permute(0, 2, 3, 1)
@@ -498,6 +523,11 @@ class TrainEngine:
                 dst.copy_(g.reshape(-1).float() * scale)
             else:
                 dst.add_(g.reshape(-1).float(), alpha=scale)
+        self._accounted(p, s, first_micro)
+
+    def _accounted(self, p, s, first_micro: bool):
+        """Bookkeeping after p's micro-batch gradient landed: launch its bucket's collective once every
+        slot of the bucket has one."""
         self._touched.add(id(p))
         if first_micro:
             self._seen.add(id(p))
