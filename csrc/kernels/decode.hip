@@ -150,6 +150,10 @@ struct DecodeParams {
   // by the head's last split (nullptr elsewhere)
   unsigned int* ready;
   int ready_target;
+  // per-step descriptors uploaded with the step's inputs (fused batch-1 decode): bit 0 -- cos_t /
+  // sin_t hold row b's RoPE angles at index b (not the position table); bit 1 -- tbl holds row b's
+  // page ids at row b (not the slot's). Neither then waits for the length or the slot to arrive.
+  int by_row;
 };
 
 // Merged launch: wait until the QKV GEMV workgroups of kv-head hk have stored their rows. Producer
@@ -213,6 +217,44 @@ __device__ __forceinline__ void rope8(const bf16_t* __restrict__ row, int d0, fl
     }
     const float c = cos_t[(long long)pos * half + fi], sn = sin_t[(long long)pos * half + fi];
     x[j] = bf2f(f2bf(x[j] * c + sgn * bf2f(row[partner]) * sn));
+  }
+}
+
+// The cos / sin of dims [d0, d0+8) at table row `pos` (rope8's entries), loaded ahead of use.
+__device__ __forceinline__ void rope_tab8(const float* __restrict__ cos_t, const float* __restrict__ sin_t, int pos,
+                                          int d0, int rot, int interleaved, float (&c)[8], float (&sn)[8]) {
+  const int half = rot >> 1;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int d = d0 + j;
+    c[j] = 1.f;
+    sn[j] = 0.f;
+    if (d >= rot) continue;
+    const int fi = interleaved ? d >> 1 : (d < half ? d : d - half);
+    c[j] = cos_t[(long long)pos * half + fi];
+    sn[j] = sin_t[(long long)pos * half + fi];
+  }
+}
+
+// rope8 with the angles in registers (rope_tab8); interleaved pairs take the partner from the
+// lane's own raw values, rotate-half partners are read from the unrotated row as rope8 does.
+__device__ __forceinline__ void rope8_reg(const bf16_t* __restrict__ row, int d0, float (&x)[8],
+                                          const float (&raw)[8], const float (&c)[8], const float (&sn)[8],
+                                          int rot, int interleaved) {
+  const int half = rot >> 1;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int d = d0 + j;
+    if (d >= rot) continue;
+    float pv, sgn;
+    if (interleaved) {
+      pv = raw[j ^ 1];
+      sgn = (d & 1) ? 1.f : -1.f;
+    } else {
+      pv = bf2f(row[d < half ? d + half : d - half]);
+      sgn = d < half ? -1.f : 1.f;
+    }
+    x[j] = bf2f(f2bf(x[j] * c[j] + sgn * pv * sn[j]));
   }
 }
 
@@ -330,6 +372,10 @@ __device__ __forceinline__ void decode_attn_body(const DecodeParams& p, const in
     }
   };
   if constexpr (!WAIT) load_qkv_rows();
+  // per-step RoPE row (by_row bit 0): the angles do not wait for the length
+  const bool pre_rope = (p.by_row & 1) && p.fused && p.rot > 0;
+  float rc[8], rs[8];
+  if (pre_rope && dact) rope_tab8(p.cos_t, p.sin_t, b, dslot * 8, p.rot, p.interleaved, rc, rs);
   // paged: this split's page ids staged in LDS (chunk <= 1024 tokens, pages >= 16 tokens), so a
   // token's address costs an LDS read instead of a dependent global load in front of every K/V
   // load; the whole chunk's range is staged (clipped to the table row), independent of the length
@@ -338,7 +384,8 @@ __device__ __forceinline__ void decode_attn_body(const DecodeParams& p, const in
   if constexpr (PAGED) {
     const int npg = min(((c0 + p.chunk - 1) >> p.ps_shift) - pg0 + 1, p.tbl_stride - pg0);
     KCA_DASSERT(npg <= 1024 / 16 + 2);
-    for (int i = tid; i < npg; i += 256) pg[i] = p.tbl[(long long)seq * p.tbl_stride + pg0 + i];
+    const int trow = (p.by_row & 2) ? b : seq;  // per-step page rows: no wait for the slot
+    for (int i = tid; i < npg; i += 256) pg[i] = p.tbl[(long long)trow * p.tbl_stride + pg0 + i];
   }
   if constexpr (WAIT) {  // merged launch: the length, slot and page ids arrived while the QKV rows were produced
     wait_qkv_ready(p, hk);
@@ -367,9 +414,15 @@ __device__ __forceinline__ void decode_attn_body(const DecodeParams& p, const in
     if (dact) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) q[g][j] = bf2f(qraw[g].v[j]);
-      if (p.fused && p.rot > 0)
+      if (pre_rope) {
+        float raw[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) raw[j] = q[g][j];
+        rope8_reg(p.q + b * p.q_bs + (long long)(hk * G + g) * D, dslot * 8, q[g], raw, rc, rs, p.rot, p.interleaved);
+      } else if (p.fused && p.rot > 0) {
         rope8(p.q + b * p.q_bs + (long long)(hk * G + g) * D, dslot * 8, q[g], pnew, p.rot, p.interleaved, p.cos_t,
               p.sin_t);
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) q[g][j] *= p.scale;
     } else {
@@ -411,7 +464,14 @@ __device__ __forceinline__ void decode_attn_body(const DecodeParams& p, const in
       kx[j] = bf2f(knraw.v[j]);
       vx[j] = bf2f(vnraw.v[j]);
     }
-    if (p.rot > 0) rope8(krow, tid * 8, kx, pnew, p.rot, p.interleaved, p.cos_t, p.sin_t);
+    if (pre_rope) {  // tid < ND <= LPT: this lane's dslot is tid, its angles are rc / rs
+      float raw[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) raw[j] = kx[j];
+      rope8_reg(krow, tid * 8, kx, raw, rc, rs, p.rot, p.interleaved);
+    } else if (p.rot > 0) {
+      rope8(krow, tid * 8, kx, pnew, p.rot, p.interleaved, p.cos_t, p.sin_t);
+    }
     const long long o = toff(pnew) + hk * p.cs_head + tid * 8;  // toff: offset inside the sequence
     store8(const_cast<bf16_t*>(p.kc) + (PAGED ? 0 : (long long)seq * p.cs_slot) + o, kx);
     store8(const_cast<bf16_t*>(p.vc) + (PAGED ? 0 : (long long)seq * p.cs_slot) + o, vx);
@@ -1172,7 +1232,8 @@ KCA_API int kca_decode_prep_attn_gemv(const void* qkv, long long ld, const void*
                                       int max_kv, int chunk, float scale, const float* alibi, const int* tbl,
                                       int tbl_stride, int ps_shift, int rot, int interleaved, const float* cos_t,
                                       const float* sin_t, int window, const void* gx, const void* gw,
-                                      const void* gbias, void* gy, int gN, int gK, int gact, hipStream_t stream) {
+                                      const void* gbias, void* gy, int gN, int gK, int gact, int by_row,
+                                      hipStream_t stream) {
   if (rot > D || (rot & 1) || (rot > 0 && (!cos_t || !sin_t))) return 8;
   if (window < 0) return 9;
   if (B != 1 || H != Hkv || D % 8 || D > 256 || max_kv <= 0 || gK % 8 || gN <= 0) return 10;
@@ -1182,6 +1243,7 @@ KCA_API int kca_decode_prep_attn_gemv(const void* qkv, long long ld, const void*
   DecodeParams p{(const bf16_t*)qkv, ld, (const bf16_t*)kc, (const bf16_t*)vc, cs_slot, cs_head,
                  cs_pos, slots, kv_lens, (bf16_t*)out, o_bs, nullptr, nullptr, alibi, tbl, tbl_stride, ps_shift,
                  H, Hkv, D, chunk, scale, 1, rot, interleaved, cos_t, sin_t, g_decode_stamps, nullptr, window};
+  p.by_row = by_row;
   if (tbl && (ps_shift < 4 || ps_shift > 20 || tbl_stride <= 0)) return 5;
   if (chunk <= 0) chunk = kca_decode_chunk(B, Hkv, max_kv);
   if (tbl && chunk > 1024) return 6;
@@ -1230,7 +1292,7 @@ KCA_API int kca_decode_qkv_attn_gemv(const void* qkv, long long ld, const void* 
                                      int tbl_stride, int ps_shift, int rot, int interleaved, const float* cos_t,
                                      const float* sin_t, int window, const void* gx, const void* gw,
                                      const void* gbias, void* gy, int gN, int gK, int gact, const void* qw,
-                                     const void* qbias, unsigned int* ready, hipStream_t stream) {
+                                     const void* qbias, unsigned int* ready, int by_row, hipStream_t stream) {
   if (rot > D || (rot & 1) || (rot > 0 && (!cos_t || !sin_t))) return 8;
   if (window < 0) return 9;
   if (B != 1 || H != Hkv || D % 8 || D > 256 || max_kv <= 0 || gK % 8 || gN <= 0 || !ready || !qw) return 10;
@@ -1239,7 +1301,7 @@ KCA_API int kca_decode_qkv_attn_gemv(const void* qkv, long long ld, const void* 
   DecodeParams p{(const bf16_t*)qkv, ld, (const bf16_t*)kc, (const bf16_t*)vc, cs_slot, cs_head,
                  cs_pos, slots, kv_lens, (bf16_t*)out, o_bs, nullptr, nullptr, alibi, tbl, tbl_stride, ps_shift,
                  H, Hkv, D, chunk, scale, 1, rot, interleaved, cos_t, sin_t, g_decode_stamps, nullptr, window,
-                 ready, 3 * (D / 4)};
+                 ready, 3 * (D / 4), by_row};
   if (tbl && (ps_shift < 4 || ps_shift > 20 || tbl_stride <= 0)) return 5;
   if (chunk <= 0) chunk = kca_decode_chunk(B, Hkv, max_kv);
   if (tbl && chunk > 1024) return 6;

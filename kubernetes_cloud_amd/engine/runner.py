@@ -44,6 +44,10 @@ _MERGED_QKV = os.environ.get("KCA_DECODE_MERGED", "0") in ("1", "true")
 # layer's QKV GEMV normalises in its prologue (ops/gemv.py ln_gemv_m1), no last-workgroup LayerNorm
 # tail -- bit-identical, but 2.33 vs 2.27 ms/token (every QKV workgroup re-reads h, gamma and beta)
 _LN_PROLOGUE = os.environ.get("KCA_DECODE_LN_PROLOGUE", "0") in ("1", "true")
+# batch-1 fused decode: the step's RoPE row and page-table row travel with the step's packed inputs
+# (fixed device addresses), so each layer's attention chain loads them in its first memory round
+# trip instead of after the length / slot arrive; KCA_DECODE_STEP_DESC=0: look them up on the device
+_STEP_DESC = os.environ.get("KCA_DECODE_STEP_DESC", "1") not in ("0", "false")
 
 
 def _next_pow2(n: int, lo: int = 1) -> int:
@@ -338,6 +342,8 @@ class ModelRunner:
         for d in self.cache.devices:
             self._rope[d] = ops.rope_tables(self.rot, self.max_len, cfg.rotary_base, d) if self.rot > 0 else (None, None)
         self.cos, self.sin = self._rope[self.device]
+        self._rope_h = (self.cos.cpu().numpy(), self.sin.cpu().numpy()) if self.rot > 0 else None
+        self._step_desc = None
         self.seen = torch.zeros(max_slots + 1, self.V, dtype=torch.uint8, device=self.device)
         self.max_bans = max_bans
         on_gpu = self.device.type == "cuda"
@@ -509,6 +515,12 @@ class ModelRunner:
             xn, h = ln_rows(h0, blk0.ln_1.weight, blk0.ln_1.bias, blk0.ln_1.eps)
         hb, xb, g = fz["h"], fz["xn"], fz["g"]
         kc, vc, tbl = self.cache.k[0], self.cache.v[0], self.cache.table_on(self.device)
+        cos, sin, by_row = self.cos, self.sin, 0
+        if self._step_desc is not None:  # the step's RoPE row (+ page row) at fixed addresses
+            cos, sin, pages = self._step_desc
+            by_row = 1
+            if pages is not None and tbl is not None:
+                tbl, by_row = pages, 3
         for li, blk in enumerate(m.h):
             at, mlp = blk.attn, blk.mlp
             act = 1 if mlp.approx in ("tanh", True) else 2
@@ -524,13 +536,14 @@ class ModelRunner:
             # (several attention splits); else the QKV GEMV, then attention + fc_in
             if not (qkv is None and _MERGED_QKV and dops.decode_qkv_attention_gemv(
                     xn, at.qkv.weight, at.qkv.bias, fz["qkv"], self.H, self.Hkv, self.D, self.rot,
-                    cfg.rotary_interleaved, self.cos, self.sin, pos, slots, kc, vc, kv_lens, max_kv, at.scale,
-                    at.alibi, obuf, ws, tbl, at.window, mlp.fc_in.weight, mlp.fc_in.bias, g, act, fz["ready"])) \
+                    cfg.rotary_interleaved, cos, sin, pos, slots, kc, vc, kv_lens, max_kv, at.scale,
+                    at.alibi, obuf, ws, tbl, at.window, mlp.fc_in.weight, mlp.fc_in.bias, g, act, fz["ready"],
+                    by_row)) \
                     and not dops.decode_prep_attention_gemv(
                         qkv if qkv is not None else skinny_linear(xn, at.qkv.weight, at.qkv.bias), self.H, self.Hkv,
-                        self.D, self.rot, cfg.rotary_interleaved, self.cos, self.sin, pos, slots, kc, vc, kv_lens,
+                        self.D, self.rot, cfg.rotary_interleaved, cos, sin, pos, slots, kc, vc, kv_lens,
                         max_kv, at.scale, at.alibi, obuf, ws, tbl, at.window, xn, mlp.fc_in.weight, mlp.fc_in.bias,
-                        g, act):
+                        g, act, by_row):
                 if li == 0:
                     return None
                 raise RuntimeError("fused decode layer: shape support changed between layers")
@@ -650,7 +663,7 @@ class ModelRunner:
                       "slots": (torch.int32, Bb), "kv_lens": (torch.int32, Bb), "top_k": (torch.int32, Bb),
                       "temperature": (torch.float32, Bb), "top_p": (torch.float32, Bb),
                       "rep": (torch.float32, Bb), "bans": (torch.int32, Bb * NB),
-                      "chain": (torch.int32, Bb)}, self.device)
+                      "chain": (torch.int32, Bb), **self._desc_fields(Bb)}, self.device)
         ws_n = dops.decode_ws_floats(Bb, self.H, self.Hkv, self.D, Kb)
         ob = self._outbuf(Bb)
         st = {
@@ -662,6 +675,30 @@ class ModelRunner:
         }
         self._static[key] = st
         return st
+
+    def _desc_on(self, Bb: int) -> bool:
+        return _STEP_DESC and Bb == 1 and self._fused_ok and self.rot > 0 and self.device.type == "cuda"
+
+    def _desc_fields(self, Bb: int) -> dict:
+        """Per-step descriptor arrays of the fused batch-1 step (see _STEP_DESC)."""
+        if not self._desc_on(Bb):
+            return {}
+        f = {"rcos": (torch.float32, Bb * (self.rot // 2)), "rsin": (torch.float32, Bb * (self.rot // 2))}
+        if self.cache.paged:
+            f["pages"] = (torch.int32, Bb * self.cache.blocks)
+        return f
+
+    def _fill_desc(self, a, rows_pos_slot):
+        """Host side of the step descriptors: row i's RoPE angles at its position and its page row."""
+        half = self.rot // 2
+        ch, sh = self._rope_h
+        tbl = self.cache.table_h.numpy() if self.cache.paged else None
+        for i, (p_, s_) in enumerate(rows_pos_slot):
+            a["rcos"][i * half:(i + 1) * half] = ch[p_]
+            a["rsin"][i * half:(i + 1) * half] = sh[p_]
+            if tbl is not None:
+                nb = self.cache.blocks
+                a["pages"][i * nb:(i + 1) * nb] = tbl[s_]
 
     def _outbuf(self, Bb: int):
         """Sampled ids (int64) and log-probs (fp32) of a batch bucket in ONE device buffer shared by its
@@ -683,8 +720,14 @@ class ModelRunner:
         pk = st["pk"]
         # chained tokens resolved on the device by the fused B = 1 step head (_layers_decode_fused)
         self._chain_src = (pk.d("chain"), st["ids"]) if (Bb == 1 and self._embed_head) else None
-        logits = self._layers_decode(pk.d("tokens"), pk.d("pos"), pk.d("slots"), pk.d("kv_lens"), Kb,
-                                     st["ws"], st["obuf"])
+        if "rcos" in pk.fields:
+            pages = pk.d("pages").view(Bb, self.cache.blocks) if "pages" in pk.fields else None
+            self._step_desc = (pk.d("rcos"), pk.d("rsin"), pages)
+        try:
+            logits = self._layers_decode(pk.d("tokens"), pk.d("pos"), pk.d("slots"), pk.d("kv_lens"), Kb,
+                                         st["ws"], st["obuf"])
+        finally:
+            self._step_desc = None
         dops.sample_logits(logits, temperature=pk.d("temperature"), top_k=pk.d("top_k"), top_p=pk.d("top_p"),
                            rep_penalty=pk.d("rep"), seen=self.seen, slots=pk.d("slots"),
                            ban_ids=pk.d("bans").view(Bb, self.max_bans), seeds=pk.d("seeds"), step=0,
@@ -778,6 +821,8 @@ class ModelRunner:
             else:  # padding row -> scratch slot
                 tok[i], pos[i], sl[i], kl[i] = 0, 0, self.cache.scratch, 1
                 te[i], tk[i], tp[i], rp[i], sd[i] = 0.0, 0, 1.0, 1.0, 0
+        if "rcos" in pk.fields:
+            self._fill_desc(a, [(int(pos[i]), int(sl[i])) for i in range(Bb)])
         if chain_dst and prev is None:
             raise ValueError("rows chain their token from a previous launch, but prev is None")
         # chained tokens read on the device by the step's first kernel: the previous step wrote them into

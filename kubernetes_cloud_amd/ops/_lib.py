@@ -111,8 +111,8 @@ _SIGS = {
 
 # fused decode layer (batch 1): kca_decode_prep_attn's arguments (minus the stream), then the fc_in
 # GEMV's x, W, bias, y, N, K, act, then the stream
-_SIGS["kca_decode_prep_attn_gemv"] = _SIGS["kca_decode_prep_attn"][:-1] + [P, P, P, P, I, I, I, P]
-_SIGS["kca_decode_qkv_attn_gemv"] = _SIGS["kca_decode_prep_attn_gemv"][:-1] + [P, P, P, P]
+_SIGS["kca_decode_prep_attn_gemv"] = _SIGS["kca_decode_prep_attn"][:-1] + [P, P, P, P, I, I, I, I, P]
+_SIGS["kca_decode_qkv_attn_gemv"] = _SIGS["kca_decode_prep_attn_gemv"][:-2] + [P, P, P, I, P]
 
 
 def _load():

@@ -194,11 +194,14 @@ def decode_prep_attention(qkv: torch.Tensor, n_heads: int, kv_heads: int, head_d
 def decode_prep_attention_gemv(qkv, n_heads, kv_heads, head_dim, rot, interleaved, cos, sin, pos, slots,
                                k_cache, v_cache, kv_lens, max_kv, scale, alibi, out, ws, block_table, window,
                                gx: torch.Tensor, gw: torch.Tensor, gbias: torch.Tensor | None, gy: torch.Tensor,
-                               act: int) -> bool:
+                               act: int, by_row: int = 0) -> bool:
     """Fused decode layer, part 1 (batch 1; csrc/kernels/decode.hip decode_attn_gemv_kernel): the
     ``decode_prep_attention`` launch and the fc_in GEMV ``gy = act(gx W^T + b)`` as ONE launch
     (attention workgroups first, the weight stream on the rest). Returns False (nothing launched)
-    for shapes outside the fused variants; the caller then runs the two separately."""
+    for shapes outside the fused variants; the caller then runs the two separately.
+    ``by_row``: bit 0 -- ``cos`` / ``sin`` are the step's rows (row b = sequence b's angles at its
+    position), bit 1 -- ``block_table`` row b is sequence b's page row (per-step descriptors uploaded
+    with the step's inputs: the attention chain does not wait for the length or the slot first)."""
     B = qkv.shape[0]
     _, Hkv, L, D = k_cache.shape
     if not (_lib.use_native(qkv, k_cache, gx, gw) and _lib.has("kca_decode_prep_attn_gemv") and B == 1
@@ -215,7 +218,7 @@ def decode_prep_attention_gemv(qkv, n_heads, kv_heads, head_dim, rot, interleave
         k_cache.stride(2), slots.data_ptr(), kv_lens.data_ptr(), out.data_ptr(), out.stride(0), _lib.ptr(ws),
         ws.numel() if ws is not None else 0, B, n_heads, Hkv, D, max_kv, chunk, float(scale), _lib.ptr(alibi), tbl,
         tstride, shift, rot, int(interleaved), _lib.ptr(cos), _lib.ptr(sin), int(window), gx.data_ptr(),
-        gw.data_ptr(), _lib.ptr(gbias), gy.data_ptr(), gw.shape[0], gw.shape[1], int(act), _lib.stream())
+        gw.data_ptr(), _lib.ptr(gbias), gy.data_ptr(), gw.shape[0], gw.shape[1], int(act), int(by_row), _lib.stream())
     if rc == 10:
         return False
     if rc != 0:
@@ -226,7 +229,8 @@ def decode_prep_attention_gemv(qkv, n_heads, kv_heads, head_dim, rot, interleave
 def decode_qkv_attention_gemv(xn: torch.Tensor, qw: torch.Tensor, qbias: torch.Tensor | None, qkv: torch.Tensor,
                               n_heads, kv_heads, head_dim, rot, interleaved, cos, sin, pos, slots, k_cache, v_cache,
                               kv_lens, max_kv, scale, alibi, out, ws, block_table, window, gw: torch.Tensor,
-                              gbias: torch.Tensor | None, gy: torch.Tensor, act: int, ready: torch.Tensor) -> bool:
+                              gbias: torch.Tensor | None, gy: torch.Tensor, act: int, ready: torch.Tensor,
+                              by_row: int = 0) -> bool:
     """Merged decode layer, part 1 (batch 1; csrc/kernels/decode.hip decode_qkv_attn_gemv_kernel): the
     QKV GEMV ``qkv = xn Wqkv^T + b``, ``decode_prep_attention`` on it and the fc_in GEMV
     ``gy = act(xn Wfc_in^T + b)`` as ONE launch -- the attention workgroups wait for their head's QKV
@@ -252,7 +256,7 @@ def decode_qkv_attention_gemv(xn: torch.Tensor, qw: torch.Tensor, qbias: torch.T
         ws.numel() if ws is not None else 0, B, n_heads, Hkv, D, max_kv, chunk, float(scale), _lib.ptr(alibi), tbl,
         tstride, shift, rot, int(interleaved), _lib.ptr(cos), _lib.ptr(sin), int(window), xn.data_ptr(),
         gw.data_ptr(), _lib.ptr(gbias), gy.data_ptr(), gw.shape[0], gw.shape[1], int(act), qw.data_ptr(),
-        _lib.ptr(qbias), ready.data_ptr(), _lib.stream())
+        _lib.ptr(qbias), ready.data_ptr(), int(by_row), _lib.stream())
     if rc == 10:
         return False
     if rc != 0:

@@ -602,6 +602,46 @@ def test_decode_attention_gemv_fused_matches_separate(PS, L0):
 
 @pytest.mark.parametrize("PS", [0, 64])
 @pytest.mark.parametrize("L0", [40, 600])
+def test_decode_attention_gemv_step_descriptors(PS, L0):
+    """by_row descriptors (the step's RoPE row and page row at fixed addresses, uploaded with the step
+    inputs) give exactly the table-lookup path's attention output and cache append."""
+    torch.manual_seed(3 + L0)
+    H, D, rot, L = 16, 256, 64, 1024
+    bf = dict(device=dev, dtype=torch.bfloat16)
+    kc0 = torch.randn(2, H, L, D, device=dev).to(torch.bfloat16)
+    vc0 = torch.randn_like(kc0)
+    tbl = None
+    if PS:
+        kc0, tbl = _paginate(kc0, PS, 3)
+        vc0, _ = _paginate(vc0, PS, 3)
+    qkv = torch.randn(1, 3 * H * D, **bf)
+    cos, sin = rope_tables(rot, L, 10000.0, dev)
+    slots = torch.tensor([1], device=dev, dtype=torch.int32)
+    pos = torch.tensor([L0 - 1], device=dev, dtype=torch.int32)
+    kv_lens = pos + 1
+    gx, gw, gb = torch.randn(1, 4096, **bf), torch.randn(16384, 4096, **bf) * 0.02, torch.randn(16384, **bf)
+    ws = torch.zeros(max(dops.decode_ws_floats(1, H, H, D, L), 1), device=dev, dtype=torch.float32)
+    res = []
+    for desc in (False, True):
+        kc, vc, out, gy = kc0.clone(), vc0.clone(), torch.empty(1, H * D, **bf), torch.empty(1, 16384, **bf)
+        c, s_, t, by = cos, sin, tbl, 0
+        if desc:
+            c, s_ = cos[L0 - 1:L0].contiguous(), sin[L0 - 1:L0].contiguous()
+            by = 1
+            if tbl is not None:
+                t, by = tbl[1:2].contiguous(), 3
+        assert dops.decode_prep_attention_gemv(qkv.clone(), H, H, D, rot, True, c, s_, pos, slots, kc, vc, kv_lens,
+                                               L, D ** -0.5, None, out, ws, t, 0, gx, gw, gb, gy, 1, by)
+        torch.cuda.synchronize()
+        res.append((out, gy, kc, vc))
+    (o0, y0, k0, v0), (o1, y1, k1, v1) = res
+    assert torch.equal(k0, k1) and torch.equal(v0, v1)
+    assert torch.equal(o0, o1)
+    assert torch.equal(y0, y1)
+
+
+@pytest.mark.parametrize("PS", [0, 64])
+@pytest.mark.parametrize("L0", [40, 600])
 def test_decode_qkv_attention_gemv_merged_matches_separate(PS, L0):
     """decode_qkv_attn_gemv_kernel (QKV GEMV + attention + fc_in in one launch, the attention waiting
     on per-head device counters) against the QKV GEMV followed by decode_attn_gemv_kernel: the same
@@ -652,7 +692,8 @@ def test_decode_qkv_attention_gemv_merged_matches_separate(PS, L0):
 def test_engine_fused_b1_ln_prologue_bit_identical(monkeypatch):
     """The fused batch-1 layer with the LayerNorm in the next QKV GEMV's prologue (gemv_dual_res +
     ln_gemv_m1) computes the same bf16 values as the last-workgroup LayerNorm tail (gemv_dual_ln):
-    same statistics partition, same rounding -- identical greedy tokens and logits."""
+    same statistics partition, same rounding -- identical greedy tokens and logits; so do the
+    per-step RoPE / page-row descriptors against the device-side lookups."""
     from kubernetes_cloud_amd.engine import runner as runner_mod
     from kubernetes_cloud_amd.engine.llm_engine import LLMEngine, SamplingParams
     from kubernetes_cloud_amd.models.causal_lm import build_model
@@ -663,15 +704,17 @@ def test_engine_fused_b1_ln_prologue_bit_identical(monkeypatch):
     p = [int(x) for x in torch.randint(0, 1000, (40,))]
     sp = SamplingParams(max_new_tokens=12, do_sample=False, logprobs=True)
     outs = []
-    for pro in (True, False):
+    for pro, desc in ((True, True), (False, False), (False, True)):
         monkeypatch.setattr(runner_mod, "_LN_PROLOGUE", pro)
+        monkeypatch.setattr(runner_mod, "_STEP_DESC", desc)
         eng = LLMEngine(m, max_slots=2, max_len=256, use_graphs=True)
         assert eng.runner._fused_ok
         r = eng.generate([p], sp)[0]
         outs.append((r.output, getattr(r, "logprobs", None)))
-    assert outs[0][0] == outs[1][0]
-    if outs[0][1] is not None:
-        assert outs[0][1] == outs[1][1]
+    for o in outs[1:]:
+        assert outs[0][0] == o[0]
+        if outs[0][1] is not None:
+            assert outs[0][1] == o[1]
 
 
 def test_engine_fused_b1_decode_matches_two_stream():
