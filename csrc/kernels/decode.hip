@@ -1170,12 +1170,13 @@ KCA_API int kca_decode_prep_attn(const void* qkv, long long ld, const void* kc, 
                                  float* ws, long long ws_floats, int B, int H, int Hkv, int D,
                                  int max_kv, int chunk, float scale, const float* alibi, const int* tbl,
                                  int tbl_stride, int ps_shift, int rot, int interleaved, const float* cos_t,
-                                 const float* sin_t, int window, hipStream_t stream) {
+                                 const float* sin_t, int window, int by_row, hipStream_t stream) {
   if (rot > D || (rot & 1) || (rot > 0 && (!cos_t || !sin_t))) return 8;
   if (window < 0) return 9;
   DecodeParams p{(const bf16_t*)qkv, ld, (const bf16_t*)kc, (const bf16_t*)vc, cs_slot, cs_head,
                  cs_pos, slots, kv_lens, (bf16_t*)out, o_bs, nullptr, nullptr, alibi, tbl, tbl_stride, ps_shift,
                  H, Hkv, D, chunk, scale, 1, rot, interleaved, cos_t, sin_t, g_decode_stamps, nullptr, window};
+  p.by_row = by_row;  // per-step RoPE / page rows (see DecodeParams::by_row)
   return decode_attn_launch(p, ws, ws_floats, B, max_kv, chunk, stream);
 }
 

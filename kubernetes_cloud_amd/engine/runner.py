@@ -44,10 +44,12 @@ _MERGED_QKV = os.environ.get("KCA_DECODE_MERGED", "0") in ("1", "true")
 # layer's QKV GEMV normalises in its prologue (ops/gemv.py ln_gemv_m1), no last-workgroup LayerNorm
 # tail -- bit-identical, but 2.33 vs 2.27 ms/token (every QKV workgroup re-reads h, gamma and beta)
 _LN_PROLOGUE = os.environ.get("KCA_DECODE_LN_PROLOGUE", "0") in ("1", "true")
-# batch-1 fused decode: the step's RoPE row and page-table row travel with the step's packed inputs
-# (fixed device addresses), so each layer's attention chain loads them in its first memory round
-# trip instead of after the length / slot arrive; KCA_DECODE_STEP_DESC=0: look them up on the device
+# decode steps: each row's RoPE angles and page-table row travel with the step's packed inputs (fixed
+# device addresses), so every layer's attention chain loads them in its first memory round trip
+# instead of after the length / slot arrive; KCA_DECODE_STEP_DESC=0: look them up on the device
 _STEP_DESC = os.environ.get("KCA_DECODE_STEP_DESC", "1") not in ("0", "false")
+# ... also for batch > 1 (the unfused per-layer path); KCA_DECODE_STEP_DESC_BATCHED=0: batch 1 only
+_STEP_DESC_BATCHED = os.environ.get("KCA_DECODE_STEP_DESC_BATCHED", "1") not in ("0", "false")
 
 
 def _next_pow2(n: int, lo: int = 1) -> int:
@@ -500,6 +502,18 @@ class ModelRunner:
                 "qkv": torch.empty(1, 3 * self.H * self.D, **z)}
         return fz
 
+    def _desc_args(self, cos, sin, tbl):
+        """(cos, sin, block table, by_row) for the decode attention: the step descriptors' rows where
+        this step has them (see _STEP_DESC), else the position tables and the device block table."""
+        by_row = 0
+        if self._step_desc is not None:
+            rc, rs, pages = self._step_desc
+            if rc is not None and cos is not None:
+                cos, sin, by_row = rc, rs, 1
+            if pages is not None and tbl is not None:
+                tbl, by_row = pages, by_row | 2
+        return cos, sin, tbl, by_row
+
     def _layers_decode_fused(self, tokens, pos, slots, kv_lens, max_kv, ws, obuf):
         """Batch-1 GPT-J-style decode step, three launches per layer (see _fused_ok). Returns None
         (nothing launched) when the fused kernels do not cover the shape."""
@@ -515,12 +529,7 @@ class ModelRunner:
             xn, h = ln_rows(h0, blk0.ln_1.weight, blk0.ln_1.bias, blk0.ln_1.eps)
         hb, xb, g = fz["h"], fz["xn"], fz["g"]
         kc, vc, tbl = self.cache.k[0], self.cache.v[0], self.cache.table_on(self.device)
-        cos, sin, by_row = self.cos, self.sin, 0
-        if self._step_desc is not None:  # the step's RoPE row (+ page row) at fixed addresses
-            cos, sin, pages = self._step_desc
-            by_row = 1
-            if pages is not None and tbl is not None:
-                tbl, by_row = pages, 3
+        cos, sin, tbl, by_row = self._desc_args(self.cos, self.sin, tbl)
         for li, blk in enumerate(m.h):
             at, mlp = blk.attn, blk.mlp
             act = 1 if mlp.approx in ("tanh", True) else 2
@@ -606,11 +615,14 @@ class ModelRunner:
                     h.record_stream(self._side)
             kc, vc, tbl = self.cache.k[li], self.cache.v[li], self.cache.table_on(dev)
             cos, sin = self._rope[dev]
+            by_row = 0
+            if obuf is not None and not self.multi_device:  # a graph-bucket step: its descriptors
+                cos, sin, tbl, by_row = self._desc_args(cos, sin, tbl)
             # RoPE + cache append + split-K attention (one launch on the GPU; GPT-Neo local layers read
             # only the last `window` positions)
             o = dops.decode_prep_attention(qkv, self.H, self.Hkv, self.D, self.rot, cfg.rotary_interleaved,
                                            cos, sin, pos, slots, kc, vc, kv_lens, max_kv, at.scale, at.alibi,
-                                           out=obuf, ws=ws, block_table=tbl, window=at.window)
+                                           out=obuf, ws=ws, block_table=tbl, window=at.window, by_row=by_row)
             a = self._lin(at.out, o)
             if side_out is not None:  # join
                 cur.wait_stream(self._side)
@@ -677,28 +689,36 @@ class ModelRunner:
         return st
 
     def _desc_on(self, Bb: int) -> bool:
-        return _STEP_DESC and Bb == 1 and self._fused_ok and self.rot > 0 and self.device.type == "cuda"
+        return (_STEP_DESC and (Bb == 1 or _STEP_DESC_BATCHED) and self.device.type == "cuda"
+                and not self.multi_device and (self.rot > 0 or self.cache.paged))
 
     def _desc_fields(self, Bb: int) -> dict:
-        """Per-step descriptor arrays of the fused batch-1 step (see _STEP_DESC)."""
+        """Per-step descriptor arrays (see _STEP_DESC): row i's RoPE angles and page-table row."""
         if not self._desc_on(Bb):
             return {}
-        f = {"rcos": (torch.float32, Bb * (self.rot // 2)), "rsin": (torch.float32, Bb * (self.rot // 2))}
+        f = {}
+        if self.rot > 0:
+            f["rcos"] = (torch.float32, Bb * (self.rot // 2))
+            f["rsin"] = (torch.float32, Bb * (self.rot // 2))
         if self.cache.paged:
             f["pages"] = (torch.int32, Bb * self.cache.blocks)
         return f
 
-    def _fill_desc(self, a, rows_pos_slot):
+    def _fill_desc(self, a, Bb: int, pos, slots):
         """Host side of the step descriptors: row i's RoPE angles at its position and its page row."""
-        half = self.rot // 2
-        ch, sh = self._rope_h
-        tbl = self.cache.table_h.numpy() if self.cache.paged else None
-        for i, (p_, s_) in enumerate(rows_pos_slot):
-            a["rcos"][i * half:(i + 1) * half] = ch[p_]
-            a["rsin"][i * half:(i + 1) * half] = sh[p_]
-            if tbl is not None:
-                nb = self.cache.blocks
-                a["pages"][i * nb:(i + 1) * nb] = tbl[s_]
+        if "rcos" in a:
+            half = self.rot // 2
+            ch, sh = self._rope_h
+            a["rcos"].reshape(Bb, half)[:] = ch[pos[:Bb]]
+            a["rsin"].reshape(Bb, half)[:] = sh[pos[:Bb]]
+        if "pages" in a:
+            a["pages"].reshape(Bb, self.cache.blocks)[:] = self.cache.table_h.numpy()[slots[:Bb]]
+
+    def _desc_views(self, pk, Bb: int):
+        """(cos rows, sin rows, page rows) device views of the step descriptors (None where absent)."""
+        f = pk.fields
+        return (pk.d("rcos") if "rcos" in f else None, pk.d("rsin") if "rsin" in f else None,
+                pk.d("pages").view(Bb, self.cache.blocks) if "pages" in f else None)
 
     def _outbuf(self, Bb: int):
         """Sampled ids (int64) and log-probs (fp32) of a batch bucket in ONE device buffer shared by its
@@ -720,9 +740,8 @@ class ModelRunner:
         pk = st["pk"]
         # chained tokens resolved on the device by the fused B = 1 step head (_layers_decode_fused)
         self._chain_src = (pk.d("chain"), st["ids"]) if (Bb == 1 and self._embed_head) else None
-        if "rcos" in pk.fields:
-            pages = pk.d("pages").view(Bb, self.cache.blocks) if "pages" in pk.fields else None
-            self._step_desc = (pk.d("rcos"), pk.d("rsin"), pages)
+        if "rcos" in pk.fields or "pages" in pk.fields:
+            self._step_desc = self._desc_views(pk, Bb)
         try:
             logits = self._layers_decode(pk.d("tokens"), pk.d("pos"), pk.d("slots"), pk.d("kv_lens"), Kb,
                                          st["ws"], st["obuf"])
@@ -821,8 +840,8 @@ class ModelRunner:
             else:  # padding row -> scratch slot
                 tok[i], pos[i], sl[i], kl[i] = 0, 0, self.cache.scratch, 1
                 te[i], tk[i], tp[i], rp[i], sd[i] = 0.0, 0, 1.0, 1.0, 0
-        if "rcos" in pk.fields:
-            self._fill_desc(a, [(int(pos[i]), int(sl[i])) for i in range(Bb)])
+        if "rcos" in pk.fields or "pages" in pk.fields:
+            self._fill_desc(a, Bb, pos, sl)
         if chain_dst and prev is None:
             raise ValueError("rows chain their token from a previous launch, but prev is None")
         # chained tokens read on the device by the step's first kernel: the previous step wrote them into

@@ -96,7 +96,7 @@ _SIGS = {
     "kca_mse_split_bwd": [P, P, P, LL, LL, F, P, P],
     "kca_sd_lms_step": [P, P, P, P, LL, P, I, I, I, I, I, F, F, F, P],
     "kca_decode_prep_attn": [P, LL, P, P, LL, LL, LL, P, P, P, LL, P, LL, I, I, I, I, I, I, F, P, P, I, I, I, I, P,
-                             P, I, P],
+                             P, I, I, P],
     "kca_im2col2x2_nhwc": [P, P, I, I, I, I, P],
     "kca_phase_to_dense_nhwc": [P, P, P, I, I, I, I, P],
     "kca_upsample2x_nhwc": [P, P, I, I, I, I, P],
@@ -111,7 +111,7 @@ _SIGS = {
 
 # fused decode layer (batch 1): kca_decode_prep_attn's arguments (minus the stream), then the fc_in
 # GEMV's x, W, bias, y, N, K, act, then the stream
-_SIGS["kca_decode_prep_attn_gemv"] = _SIGS["kca_decode_prep_attn"][:-1] + [P, P, P, P, I, I, I, I, P]
+_SIGS["kca_decode_prep_attn_gemv"] = _SIGS["kca_decode_prep_attn"][:-2] + [P, P, P, P, I, I, I, I, P]
 _SIGS["kca_decode_qkv_attn_gemv"] = _SIGS["kca_decode_prep_attn_gemv"][:-2] + [P, P, P, I, P]
 
 

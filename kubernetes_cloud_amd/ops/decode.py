@@ -161,8 +161,9 @@ def decode_prep_attention(qkv: torch.Tensor, n_heads: int, kv_heads: int, head_d
                           kv_lens: torch.Tensor, max_kv: int, scale: float | None = None,
                           alibi: torch.Tensor | None = None, out: torch.Tensor | None = None,
                           ws: torch.Tensor | None = None, block_table: torch.Tensor | None = None,
-                          window: int = 0) -> torch.Tensor:
+                          window: int = 0, by_row: int = 0) -> torch.Tensor:
     """``decode_prep`` + ``decode_attention`` for the decode step (kv_lens = pos + 1).
+    ``by_row``: per-step descriptors as in ``decode_prep_attention_gemv`` (native path only).
     Native: ONE launch (``kca_decode_prep_attn``) that rotates Q itself and lets
     the split holding the new token rotate and append K/V (the prep kernel's ~5 us
     per layer at B=1 disappears); bit-identical to the two-kernel path."""
@@ -184,8 +185,9 @@ def decode_prep_attention(qkv: torch.Tensor, n_heads: int, kv_heads: int, head_d
                   k_cache.stride(0), k_cache.stride(1), k_cache.stride(2), slots.data_ptr(), kv_lens.data_ptr(),
                   out.data_ptr(), out.stride(0), _lib.ptr(ws), ws.numel() if ws is not None else 0, B, H, Hkv, D,
                   max_kv, chunk, float(scale), _lib.ptr(alibi), tbl, tstride, shift, rot, int(interleaved),
-                  _lib.ptr(cos), _lib.ptr(sin), int(window), _lib.stream())
+                  _lib.ptr(cos), _lib.ptr(sin), int(window), int(by_row), _lib.stream())
         return out
+    assert not by_row, "per-step descriptors are a native-kernel feature"
     decode_prep(qkv, H, Hkv, D, rot, interleaved, cos, sin, pos, slots, k_cache, v_cache, block_table)
     return decode_attention(qkv, k_cache, v_cache, slots, kv_lens, H, max_kv, scale, alibi, out, ws,
                             block_table=block_table, window=window)

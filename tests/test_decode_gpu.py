@@ -717,6 +717,26 @@ def test_engine_fused_b1_ln_prologue_bit_identical(monkeypatch):
             assert outs[0][1] == o[1]
 
 
+def test_engine_step_descriptors_batched_bit_identical(monkeypatch):
+    """Batched decode (the unfused per-layer path, paged KV) with the per-step RoPE / page-row
+    descriptors gives exactly the tokens and log-probs of the device-side table lookups."""
+    from kubernetes_cloud_amd.engine import runner as runner_mod
+    from kubernetes_cloud_amd.engine.llm_engine import LLMEngine, SamplingParams
+    from kubernetes_cloud_amd.models.causal_lm import build_model
+    from kubernetes_cloud_amd.models.config import PRESETS_HF, LMConfig
+    cfg = dict(PRESETS_HF["gpt-j-6b"])
+    cfg.update(n_embd=1024, n_layer=2, n_head=4, rotary_dim=64, n_positions=512)
+    m = build_model(LMConfig.from_hf(cfg), device=dev, dtype=torch.bfloat16, seed=0)
+    ps = [[int(x) for x in torch.randint(0, 1000, (n,))] for n in (40, 70, 23)]
+    sp = SamplingParams(max_new_tokens=10, do_sample=False, logprobs=True)
+    outs = []
+    for desc in (True, False):
+        monkeypatch.setattr(runner_mod, "_STEP_DESC", desc)
+        eng = LLMEngine(m, max_slots=4, max_len=256, use_graphs=True)
+        outs.append([(r.output, r.logprobs) for r in eng.generate(ps, sp)])
+    assert outs[0] == outs[1]
+
+
 def test_engine_fused_b1_decode_matches_two_stream():
     """ModelRunner's fused batch-1 GPT-J layer (three launches per layer on one queue) against the
     two-stream form: same greedy tokens where the top-2 logits are not near-tied."""
