@@ -902,7 +902,6 @@ struct DualLn {
   int N, K1, K2, NC;   // NC = 1 + K2 / K1 K-chunks of K1 columns
   int tail;            // 1: arrival + LayerNorm by the last workgroup; 0 (NC == 1): each workgroup writes
                        // its rows of h_out = h + y and the next GEMV normalises in its prologue
-  int flat;            // A/B: one arrival counter for every workgroup (no sub-counters)
 };
 
 // Workgroup (chunk c, row group g): R rows x K1 columns -- chunk 0 of W1 . x1, chunk c >= 1 the
@@ -962,9 +961,7 @@ __global__ __launch_bounds__(256) void gemv_dual_ln_kernel(DualLn a) {
     const unsigned members = (unsigned)((G - sub + NSUB - 1) / NSUB);
     unsigned* sc = a.cnt + 32 * (1 + sub);
     int last = 0;
-    if (a.flat) {
-      last = __hip_atomic_fetch_add(a.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)G - 1;
-    } else if (__hip_atomic_fetch_add(sc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == members - 1) {
+    if (__hip_atomic_fetch_add(sc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == members - 1) {
       __hip_atomic_store(sc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
       last = __hip_atomic_fetch_add(a.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)nsub - 1;
     }
@@ -1363,15 +1360,9 @@ KCA_API int kca_gemv_dual_ln(const void* x1, const void* w1, int K1, const void*
     chunked = e && e[0] == '1';
   }
   const int NC = chunked ? 1 + K2 / K1 : 1;
-  DualLn a{(const bf16_t*)x1, (const bf16_t*)w1, (const bf16_t*)x2, (const bf16_t*)w2, (const bf16_t*)bias,
-           ypart, cnt, (const bf16_t*)h, (bf16_t*)h_out, (const bf16_t*)gamma, (const bf16_t*)beta, eps,
-           (bf16_t*)xn_out, N, K1, K2, NC, 1, 0};
-  static int flat = -1;
-  if (flat < 0) {
-    const char* e = getenv("KCA_DUAL_FLAT");
-    flat = e && e[0] == '1';
-  }
-  a.flat = flat;
+  const DualLn a{(const bf16_t*)x1, (const bf16_t*)w1, (const bf16_t*)x2, (const bf16_t*)w2, (const bf16_t*)bias,
+                 ypart, cnt, (const bf16_t*)h, (bf16_t*)h_out, (const bf16_t*)gamma, (const bf16_t*)beta, eps,
+                 (bf16_t*)xn_out, N, K1, K2, NC, 1};
   hipLaunchKernelGGL(gemv_dual_ln_kernel<4>, dim3(((N + 3) / 4) * NC), dim3(256), dec_lds_pad(1), stream, a);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
@@ -1384,7 +1375,7 @@ KCA_API int kca_gemv_dual_res(const void* x1, const void* w1, int K1, const void
   if (N <= 0 || K1 % 8 || K2 % 8 || K1 <= 0 || K2 <= 0 || !h || !h_out) return 1;
   if (((uintptr_t)x1 | (uintptr_t)w1 | (uintptr_t)x2 | (uintptr_t)w2) & 15) return 2;
   const DualLn a{(const bf16_t*)x1, (const bf16_t*)w1, (const bf16_t*)x2, (const bf16_t*)w2, (const bf16_t*)bias,
-                 nullptr, nullptr, (const bf16_t*)h, (bf16_t*)h_out, nullptr, nullptr, 0.f, nullptr, N, K1, K2, 1, 0, 0};
+                 nullptr, nullptr, (const bf16_t*)h, (bf16_t*)h_out, nullptr, nullptr, 0.f, nullptr, N, K1, K2, 1, 0};
   hipLaunchKernelGGL(gemv_dual_ln_kernel<4>, dim3((N + 3) / 4), dim3(256), dec_lds_pad(1), stream, a);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
