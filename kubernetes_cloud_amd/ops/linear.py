@@ -263,7 +263,7 @@ def gemm_acc_f32(a: torch.Tensor, w: torch.Tensor, acc: torch.Tensor, alpha: flo
     accumulator (``kca_gemm_lt_acc``). Returns False (nothing launched) when it does not apply."""
     M, K = a.shape
     N = w.shape[0]
-    if not (_lib.use_native(a, w, acc) and _lib.has("kca_gemm_lt_acc") and a.dtype == w.dtype == torch.bfloat16
+    if not (_lib.use_native(a, w) and acc.is_cuda and _lib.has("kca_gemm_lt_acc") and a.dtype == w.dtype == torch.bfloat16
             and acc.dtype == torch.float32 and acc.is_contiguous() and acc.numel() == M * N
             and w.shape[1] == K and a.stride(1) == 1 and w.stride(1) == 1):
         return False

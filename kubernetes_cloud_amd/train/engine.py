@@ -65,10 +65,11 @@ log = logging.getLogger("kca.engine")
 
 ALIGN = 64
 _NONE, _INFLIGHT, _READY = 0, 1, 2
-# weight gradients that fused ops hand over as GEMM operands (ops/fused_block.py) are accumulated
-# by the GEMM itself into the fp32 buffer (ops/linear.py gemm_acc_f32); KCA_WGRAD_GEMM_ACC=0: a bf16
-# dW GEMM, then the accumulation kernel
-_GEMM_ACC = os.environ.get("KCA_WGRAD_GEMM_ACC", "1") not in ("0", "false")
+# KCA_WGRAD_GEMM_ACC=1: weight gradients that fused ops hand over as GEMM operands (ops/fused_block.py)
+# are accumulated by the GEMM itself into the fp32 buffer (ops/linear.py gemm_acc_f32) instead of a
+# bf16 dW GEMM + the accumulation kernel. Off by default: hipBLASLt's fp32-output kernels for these
+# shapes are slower than the bf16 ones plus the pass (GPT-J step 1878 -> 1916 ms, docs/PERF.md)
+_GEMM_ACC = os.environ.get("KCA_WGRAD_GEMM_ACC", "0") in ("1", "true")
 # gradients of at most this many elements are accumulated in batches (kca_accum_grad_multi);
 # KCA_MULTI_ACCUM=0 launches kca_accum_grad per parameter
 _SMALL_GRAD = 1 << 18

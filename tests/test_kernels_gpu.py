@@ -576,7 +576,7 @@ def test_engine_wgrad_gemm_accumulate_matches_split(monkeypatch):
     ids = [torch.randint(0, 1024, (2, 128), device=DEV) for _ in range(2)]
     calls = []
     real = lin.gemm_acc_f32
-    monkeypatch.setattr(lin, "gemm_acc_f32", lambda *a: bool(calls.append(1)) or real(*a))
+    monkeypatch.setattr(lin, "gemm_acc_f32", lambda *a: real(*a) and not calls.append(1))  # counts launches
     grads = []
     for acc in (True, False):
         monkeypatch.setattr(engine_mod, "_GEMM_ACC", acc)
