@@ -339,7 +339,7 @@ __device__ void fanin_combine(const DecodeParams& p, int b, int hk, int nsplit) 
 // wave step; G query heads share each K/V row (GQA group).
 // (the workgroup's (split, kv-head, sequence) coordinates are arguments: decode_attn_kernel passes
 // its block index, the fused decode-layer kernel below a slice of its grid)
-template <int LPT, int G, bool PAGED, bool ONLINE, bool WAIT = false>
+template <int LPT, int G, bool PAGED, bool ONLINE, bool WAIT = false, bool PF = false>
 __device__ __forceinline__ void decode_attn_body(const DecodeParams& p, const int split, const int hk, const int b,
                                                  const int nsplit) {
   constexpr int TPW = 64 / LPT;
@@ -514,15 +514,26 @@ __device__ __forceinline__ void decode_attn_body(const DecodeParams& p, const in
   // inactive lanes (dslot >= ND) and tokens past the split read an in-range row instead of branching
   // around their loads: no branch in the loop, so all 2U loads of an iteration are in flight together
   const long long dfix = dact ? 0 : -(long long)dslot * 8;
-  for (int t0 = ca + wid * TPW + tsub; t0 < ce; t0 += TPB * U) {
+  auto load_kv = [&](int tb, U16x8 (&kk)[U], U16x8 (&vv)[U]) {
     long long o[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) o[u] = toff(min(t0 + u * TPB, ce - 1)) + dfix;
-    U16x8 kr[U], vr[U];
+    for (int u = 0; u < U; ++u) o[u] = toff(min(tb + u * TPB, ce - 1)) + dfix;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      kr[u] = *reinterpret_cast<const U16x8*>(kb + o[u]);
-      vr[u] = *reinterpret_cast<const U16x8*>(vb + o[u]);
+      kk[u] = *reinterpret_cast<const U16x8*>(kb + o[u]);
+      vv[u] = *reinterpret_cast<const U16x8*>(vb + o[u]);
+    }
+  };
+  // PF (long splits, the standalone launch): the next iteration's K / V rows are requested before this
+  // iteration's scores, so a split of many iterations streams instead of paying one round trip each
+  U16x8 kr[U], vr[U];
+  if (PF && ca + wid * TPW + tsub < ce) load_kv(ca + wid * TPW + tsub, kr, vr);
+  for (int t0 = ca + wid * TPW + tsub; t0 < ce; t0 += TPB * U) {
+    U16x8 kn[U], vn[U];
+    if constexpr (PF) {
+      if (t0 + TPB * U < ce) load_kv(t0 + TPB * U, kn, vn);
+    } else {
+      load_kv(t0, kr, vr);
     }
     // the U scores of this iteration are independent (their lane-group sums overlap), then ONE
     // online-softmax update folds them in: the dependent chain per iteration is one reduction and
@@ -562,6 +573,13 @@ __device__ __forceinline__ void decode_attn_body(const DecodeParams& p, const in
         acc[g][j] = a;
       }
       m[g] = mn;
+    }
+    if constexpr (PF) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        kr[u] = kn[u];
+        vr[u] = vn[u];
+      }
     }
   }
   DSTAMP(4);
@@ -785,7 +803,12 @@ __device__ __forceinline__ void decode_attn_body(const DecodeParams& p, const in
 
 template <int LPT, int G, bool PAGED, bool ONLINE>
 __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
+#ifdef KCA_AB_NO_PF  // A/B build: no K/V prefetch across iterations
   decode_attn_body<LPT, G, PAGED, ONLINE>(p, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x);
+#else
+  // G == 1 only: the prefetched rows cost GQA groups a residency step (G = 2: 119 -> 135 VGPRs)
+  decode_attn_body<LPT, G, PAGED, ONLINE, false, ONLINE && G == 1>(p, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x);
+#endif
 }
 
 // ---------------------------------------------------------------- fused decode layer (batch 1)
