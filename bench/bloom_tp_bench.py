@@ -27,10 +27,12 @@ import torch.distributed as dist
 
 
 def run_tp_decode(model_name="bloom-176b", layers=0, batches=(1, 8, 32), prompt_len=128, new_tokens=64,
-                  custom_ar=True, dtype="bf16"):
+                  custom_ar=True, dtype="bf16", emulate_tp=0):
     """All ranks call this inside an initialised process group (or world 1). ``dtype`` "fp16" runs
     the model in float16 as BASELINE config 4 states (the native decode kernels are bf16: fp16 takes
-    the eager PyTorch paths, for comparison only).
+    the eager PyTorch paths, for comparison only). ``emulate_tp`` N > 1 (one process, no process
+    group): rank 0's shard of a TP=N layout with stand-in collectives (parallel/tp_emulation.py) --
+    the per-rank weight stream and kernel schedule of the real run, all-reduces priced separately.
     Returns the per-batch records on rank 0, None on followers."""
     from kubernetes_cloud_amd.engine.llm_engine import LLMEngine, SamplingParams
     from kubernetes_cloud_amd.engine.runner import ModelRunner
@@ -47,7 +49,14 @@ def run_tp_decode(model_name="bloom-176b", layers=0, batches=(1, 8, 32), prompt_
     dev = torch.device("cuda", torch.cuda.current_device())
     tdt = {"bf16": torch.bfloat16, "fp16": torch.float16}[dtype]
     t0 = time.perf_counter()
-    if dist.is_initialized():  # TP modules even at world 1: exercises the RCCL collectives in the decode graph
+    emu = None
+    if emulate_tp > 1:
+        if world > 1:
+            raise ValueError("emulate_tp runs one process")
+        from kubernetes_cloud_amd.parallel.tp_emulation import emulated_rank_model
+        model = emulated_rank_model(cfg, emulate_tp, 0, device=dev, dtype=tdt)
+        emu = model.h[0].attn.out.group
+    elif dist.is_initialized():  # TP modules even at world 1: exercises the RCCL collectives in the decode graph
         from kubernetes_cloud_amd.parallel.tensor_parallel import load_tp_model
         model = load_tp_model(cfg, rank, world, None, device=dev, dtype=tdt, random_init=True)
     else:
@@ -90,13 +99,17 @@ def run_tp_decode(model_name="bloom-176b", layers=0, batches=(1, 8, 32), prompt_
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
             n = eng.stats["decode_steps"] - s0
-            out.append({"metric": f"{model_name} TP={world} decode", "batch": B, "prompt_len": prompt_len,
+            tp = emulate_tp if emu is not None else world
+            out.append({"metric": f"{model_name} TP={tp} decode" + (" (rank-0 emulation, 1 GPU)" if emu else ""),
+                        "batch": B, "prompt_len": prompt_len,
                         "prefill_ms": round(prefill_ms, 2), "decode_ms_per_token": round(dt / max(n, 1) * 1e3, 3),
                         "tokens_per_s": round((sum(len(r.output) for r in reqs) - 2 * B) / dt, 1),
-                        "layers": cfg.n_layers, "tp": world, "load_s": round(load_s, 1), "dtype": dtype,
+                        "layers": cfg.n_layers, "tp": tp, "load_s": round(load_s, 1), "dtype": dtype,
                         "custom_allreduce": ar is not None, "ctrl": chan.kind if chan is not None else None,
                         "pipelined": bool(eng.pipeline),
                         "data": "random-init weights"})
+            if emu is not None:
+                out[-1].update(_emulation_notes(model, cfg, B, emulate_tp))
         if world > 1:
             run.shutdown()
     if ar is not None:
@@ -110,6 +123,20 @@ def run_tp_decode(model_name="bloom-176b", layers=0, batches=(1, 8, 32), prompt_
     return out
 
 
+def _emulation_notes(model, cfg, B, tp):
+    """What the rank-local run streams and what it leaves out (the collectives)."""
+    nbytes = sum(p.numel() * p.element_size() for n, p in model.named_parameters() if n != "wte.weight")
+    head = model.lm_head.local_weight()
+    stream = nbytes + head.numel() * head.element_size()  # layers + LN params + the head's vocab shard
+    return {"emulated_rank": 0, "rank_weight_gb": round(stream / 1e9, 2),
+            "weight_floor_ms_6p3tbs": round(stream / 6.3e12 * 1e3, 2),
+            "collectives_excluded": {"all_reduce_per_token": 2 * cfg.n_layers,
+                                     "all_reduce_bytes": B * cfg.hidden * 2,
+                                     "all_gather_logits_bytes": B * (cfg.vocab_size // tp) * 2,
+                                     "note": "stand-in collectives (identity / local tile): a TP=8 node adds "
+                                             "2 xGMI all-reduces per layer, priced by allreduce_bench"}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="bloom-176b")
@@ -120,17 +147,21 @@ def main():
     ap.add_argument("--no-custom-ar", action="store_true", help="TP all-reduces through RCCL only")
     ap.add_argument("--dtype", choices=["bf16", "fp16"], default="bf16",
                     help="fp16: BASELINE config 4's dtype (eager PyTorch paths; the native kernels are bf16)")
+    ap.add_argument("--emulate-tp", type=int, default=0,
+                    help="N > 1: rank 0 of a TP=N layout on this one GPU, stand-in collectives")
     ap.add_argument("--force-pg", action="store_true",
                     help="one-rank RCCL process group: TP modules + collectives captured in the decode graph")
     args = ap.parse_args()
     from kubernetes_cloud_amd.parallel.dist import init_distributed
-    init_distributed()
+    if not args.emulate_tp:
+        init_distributed()
     if args.force_pg and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     recs = run_tp_decode(args.model, args.layers, [int(b) for b in args.batches.split(",")], args.prompt_len,
-                         args.new_tokens, custom_ar=not args.no_custom_ar, dtype=args.dtype)
+                         args.new_tokens, custom_ar=not args.no_custom_ar, dtype=args.dtype,
+                         emulate_tp=args.emulate_tp)
     for r in recs or ():
         print(json.dumps(r), flush=True)
 

@@ -124,23 +124,19 @@ struct Stager;
 // Loads go through buffer resources (T8): the per-thread byte offsets are loop constants in
 // VGPRs and the tile's row offset k0 * stride is ONE scalar -- no 64-bit address arithmetic on the
 // VALU per load, which at D = 64 (SD-1.5's padded heads) is VALU-issue-bound.
-// (-DKCA_ATTN_FLAT_LOADS: the flat-pointer form, A/B)
 template <int D>
 struct Stager<D, true> {
   static constexpr int NCH = D / 8, CPT = 32 * NCH / 256, RPI = 256 / NCH;
   long long ok_, ov_;  // element offset of this thread's first chunk in a K / V tile
   int row0_, ch_;
-#ifndef KCA_ATTN_FLAT_LOADS
   __amdgpu_buffer_rsrc_t rk_, rv_;
   int vok_[CPT], vov_[CPT];  // byte offsets of this thread's chunks (tile row 0)
-#endif
   __device__ __forceinline__ Stager(int tid, long long k_st, long long v_st) {
     row0_ = tid / NCH;
     ch_ = tid % NCH;
     ok_ = (long long)row0_ * k_st + ch_ * 8;
     ov_ = (long long)row0_ * v_st + ch_ * 8;
   }
-#ifndef KCA_ATTN_FLAT_LOADS
   // kb / vb: the (batch, kv head) base pointers -- workgroup-uniform (readfirstlane'd so the
   // descriptor is provably scalar: no waterfall loop, T20). Offsets stay < 2^31 bytes per head slice.
   __device__ __forceinline__ void bind(const bf16_t* kb, const bf16_t* vb, long long k_st, long long v_st) {
@@ -156,13 +152,8 @@ struct Stager<D, true> {
     rk_ = head_rsrc(kb);
     rv_ = head_rsrc(vb);
   }
-#else
-  __device__ __forceinline__ void bind(const bf16_t*, const bf16_t*, long long, long long) {}
-  __device__ __forceinline__ void set_base(const bf16_t*, const bf16_t*) {}
-#endif
   __device__ __forceinline__ void load(u32x4 (&sk)[CPT], u32x4 (&sv)[CPT], const bf16_t* kb, const bf16_t* vb,
                                        int k0, long long k_st, long long v_st) const {
-#ifndef KCA_ATTN_FLAT_LOADS
     const int sok = __builtin_amdgcn_readfirstlane((int)(k0 * k_st * 2));
     const int sov = __builtin_amdgcn_readfirstlane((int)(k0 * v_st * 2));
 #pragma unroll
@@ -172,13 +163,6 @@ struct Stager<D, true> {
       sk[i] = *reinterpret_cast<const u32x4*>(&a);
       sv[i] = *reinterpret_cast<const u32x4*>(&b);
     }
-#else
-#pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      sk[i] = *reinterpret_cast<const u32x4*>(kb + ok_ + (long long)(k0 + i * RPI) * k_st);
-      sv[i] = *reinterpret_cast<const u32x4*>(vb + ov_ + (long long)(k0 + i * RPI) * v_st);
-    }
-#endif
   }
   __device__ __forceinline__ void store(const u32x4 (&sk)[CPT], const u32x4 (&sv)[CPT], char* buf) const {
 #pragma unroll

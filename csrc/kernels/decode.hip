@@ -145,33 +145,11 @@ struct DecodeParams {
   // arrive combines the partials in place of the separate decode_combine_kernel (nullptr: that kernel)
   unsigned int* cnt;
   int window;  // > 0: attend only the last `window` positions (GPT-Neo local layers)
-  // merged QKV + attention + fc_in launch (decode_qkv_attn_gemv_kernel): per-kv-head QKV readiness
-  // counters (128 B apart), the count that means "all of this head's Q/K/V rows are stored", re-armed
-  // by the head's last split (nullptr elsewhere)
-  unsigned int* ready;
-  int ready_target;
   // per-step descriptors uploaded with the step's inputs (fused batch-1 decode): bit 0 -- cos_t /
   // sin_t hold row b's RoPE angles at index b (not the position table); bit 1 -- tbl holds row b's
   // page ids at row b (not the slot's). Neither then waits for the length or the slot to arrive.
   int by_row;
 };
-
-// Merged launch: wait until the QKV GEMV workgroups of kv-head hk have stored their rows. Producer
-// side (recipe R1 of cdna_hip_programming.md Guideline 16): write-through stores drained, barrier,
-// one relaxed agent-scope add; here one lane polls (bounded: a lost count costs a wrong token, never
-// a hung queue), then an agent-scope acquire and a barrier before any load of the QKV row.
-__device__ __forceinline__ void wait_qkv_ready(const DecodeParams& p, int hk) {
-  if (threadIdx.x == 0) {
-    const unsigned* c = p.ready + 32 * hk;
-    for (int it = 0; it < (1 << 18); ++it) {
-      if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)p.ready_target) break;
-      __builtin_amdgcn_s_sleep(1);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-}
 
 // Partials that another workgroup of the same launch combines: write-through (sc1) stores, so a
 // drain (vmcnt(0)) + barrier + counter add publishes them across XCDs without a release fence
@@ -296,8 +274,6 @@ __device__ void fanin_combine(const DecodeParams& p, int b, int hk, int nsplit) 
     const int last = prev == (unsigned)(nsplit - 1);
     if (last) {
       __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm for the next call
-      // merged launch: every split of this head is past its QKV wait -> re-arm the readiness counter
-      if (p.ready) __hip_atomic_store(p.ready + 32 * hk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -339,7 +315,7 @@ __device__ void fanin_combine(const DecodeParams& p, int b, int hk, int nsplit) 
 // wave step; G query heads share each K/V row (GQA group).
 // (the workgroup's (split, kv-head, sequence) coordinates are arguments: decode_attn_kernel passes
 // its block index, the fused decode-layer kernel below a slice of its grid)
-template <int LPT, int G, bool PAGED, bool ONLINE, bool WAIT = false, bool PF = false>
+template <int LPT, int G, bool PAGED, bool ONLINE, bool PF = false>
 __device__ __forceinline__ void decode_attn_body(const DecodeParams& p, const int split, const int hk, const int b,
                                                  const int nsplit) {
   constexpr int TPW = 64 / LPT;
@@ -371,7 +347,7 @@ __device__ __forceinline__ void decode_attn_body(const DecodeParams& p, const in
       vnraw = *reinterpret_cast<const U16x8*>(vrow + tid * 8);
     }
   };
-  if constexpr (!WAIT) load_qkv_rows();
+  load_qkv_rows();
   // per-step RoPE row (by_row bit 0): the angles do not wait for the length
   const bool pre_rope = (p.by_row & 1) && p.fused && p.rot > 0;
   float rc[8], rs[8];
@@ -386,10 +362,6 @@ __device__ __forceinline__ void decode_attn_body(const DecodeParams& p, const in
     KCA_DASSERT(npg <= 1024 / 16 + 2);
     const int trow = (p.by_row & 2) ? b : seq;  // per-step page rows: no wait for the slot
     for (int i = tid; i < npg; i += 256) pg[i] = p.tbl[(long long)trow * p.tbl_stride + pg0 + i];
-  }
-  if constexpr (WAIT) {  // merged launch: the length, slot and page ids arrived while the QKV rows were produced
-    wait_qkv_ready(p, hk);
-    load_qkv_rows();
   }
   const int c1 = min(c0 + p.chunk, L);
   // sliding window: positions below L - window are never read (splits left of it are empty)
@@ -803,12 +775,8 @@ __device__ __forceinline__ void decode_attn_body(const DecodeParams& p, const in
 
 template <int LPT, int G, bool PAGED, bool ONLINE>
 __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
-#ifdef KCA_AB_NO_PF  // A/B build: no K/V prefetch across iterations
-  decode_attn_body<LPT, G, PAGED, ONLINE>(p, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x);
-#else
   // G == 1 only: the prefetched rows cost GQA groups a residency step (G = 2: 119 -> 135 VGPRs)
-  decode_attn_body<LPT, G, PAGED, ONLINE, false, ONLINE && G == 1>(p, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x);
-#endif
+  decode_attn_body<LPT, G, PAGED, ONLINE, ONLINE && G == 1>(p, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x);
 }
 
 // ---------------------------------------------------------------- fused decode layer (batch 1)
@@ -838,13 +806,6 @@ __global__ __launch_bounds__(256) void decode_attn_gemv_kernel(DecodeParams p, i
   const int bid = blockIdx.x;
   if (bid < n_attn) {
     const int split = bid % nsplit, rest = bid / nsplit;
-#ifdef KCA_AB_NO_DEC_ATTN  // timing A/B only (zero attention output): the fc_in GEMV without the attention chain
-    if (split == 0) {
-      const int hk = rest % p.Hkv, b = rest / p.Hkv;
-      for (int i = threadIdx.x; i < G * p.D; i += 256) p.out[b * p.o_bs + (long long)hk * G * p.D + i] = f2bf(0.f);
-    }
-    return;
-#endif
     decode_attn_body<LPT, G, PAGED, ONLINE>(p, split, rest % p.Hkv, rest / p.Hkv, nsplit);
     DSTAMP(7);
     return;
@@ -858,118 +819,47 @@ __global__ __launch_bounds__(256) void decode_attn_gemv_kernel(DecodeParams p, i
   DSTAMP(7);
 }
 
-// Merged decode layer, part 1 (batch 1, H == Hkv): the QKV GEMV, the attention and the fc_in GEMV in
-// ONE launch. Workgroups [0, n_qkv) stream Wqkv head-major (head h's Q, K and V row groups, then head
-// h+1's) and count each head's finished rows; [n_qkv, n_qkv + n_attn) are the attention splits: they
-// resolve the length, the slot and the page ids while the QKV rows are produced, wait for their head's
-// count, then run the RoPE + KV append + split-K attention under the fc_in weight stream of the
-// remaining workgroups. One kernel boundary per layer less than QKV GEMV -> decode_attn_gemv_kernel,
-// and the attention chain starts as soon as its head's rows exist. Every wait is on workgroups with
-// lower indices that never wait themselves, and the attention workgroups (a few hundred) cannot fill
-// the chip's resident slots, so the producers always make progress.
-template <int LPT, bool PAGED, bool ONLINE>
-__global__ __launch_bounds__(256) void decode_qkv_attn_gemv_kernel(DecodeParams p, int nsplit, int n_qkv, int n_attn,
-                                                                   GemvM1 qg, GemvM1 g) {
-  constexpr int R = 4;
-  __shared__ float part[4][R];
-  const int bid = blockIdx.x;
-  if (bid < n_qkv) {
-    DSTAMP(0);
-    const int per = p.D / R;  // row groups per head and per Q / K / V part
-    const int hh = bid / (3 * per), rem = bid % (3 * per);
-    const int n0 = (rem / per) * p.H * p.D + hh * p.D + (rem % per) * R;
-    float acc[R] = {0.f, 0.f, 0.f, 0.f};
-    gemv_m1_accum<R>(qg.x, qg.w, qg.N, qg.K, n0, acc);
-    const float v = gemv_m1_finish<R>(acc, part, qg.bias, n0, qg.N, 0);
-    if (threadIdx.x < R)  // write-through (agent scope): read by attention workgroups on any XCD
-      __hip_atomic_store(reinterpret_cast<unsigned short*>(qg.y + n0 + threadIdx.x), f2bf(v), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(p.ready + 32 * hh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    DSTAMP(7);
-    return;
-  }
-  if (bid < n_qkv + n_attn) {
-    const int a = bid - n_qkv;
-    const int split = a % nsplit, rest = a / nsplit;
-    decode_attn_body<LPT, 1, PAGED, ONLINE, true>(p, split, rest % p.Hkv, rest / p.Hkv, nsplit);
-    DSTAMP(7);
-    return;
-  }
-  DSTAMP(0);
-  const int n0 = (bid - n_qkv - n_attn) * R;
-  float acc[R] = {0.f, 0.f, 0.f, 0.f};
-  gemv_m1_accum<R>(g.x, g.w, g.N, g.K, n0, acc);
-  const float v = gemv_m1_finish<R>(acc, part, g.bias, n0, g.N, g.act);
-  if (threadIdx.x < R && n0 + threadIdx.x < g.N) g.y[n0 + threadIdx.x] = f2bf(v);
-  DSTAMP(7);
-}
-
 constexpr int kDualSub = 64;  // sub-counters of gemv_dual_ln_kernel's arrival (cnt: 32 * (1 + 64) uints)
 
 struct DualLn {
-  const bf16_t* x1;  // [K1] (attention output)
-  const bf16_t* w1;  // [N, K1]
-  const bf16_t* x2;  // [K2] (GELU(fc_in))
-  const bf16_t* w2;  // [N, K2]
+  const bf16_t* x1;    // [K1] (attention output)
+  const bf16_t* w1;    // [N, K1]
+  const bf16_t* x2;    // [K2] (GELU(fc_in)); nullable: one GEMV (sequential-residual layers)
+  const bf16_t* w2;    // [N, K2]
   const bf16_t* bias;  // [N] (nullable)
-  float* ypart;        // [NC, N] fp32 K-chunk partials (write-through: the finishing workgroup reads them)
-  unsigned int* cnt;   // arrival counter, zero before the first launch, re-armed by the last workgroup
+  float* ypart;        // [N] fp32 row results (write-through: the finishing workgroup reads them)
+  unsigned int* cnt;   // arrival counters, zero before the first launch, re-armed by the last workgroup
   const bf16_t* h;     // [N] residual stream in
   bf16_t* h_out;       // [N] h + y (bf16)
   const bf16_t* gamma; // next LayerNorm
   const bf16_t* beta;
   float eps;
   bf16_t* xn_out;      // [N] LN(h + y)
-  int N, K1, K2, NC;   // NC = 1 + K2 / K1 K-chunks of K1 columns
-  int tail;            // 1: arrival + LayerNorm by the last workgroup; 0 (NC == 1): each workgroup writes
-                       // its rows of h_out = h + y and the next GEMV normalises in its prologue
+  const bf16_t* gamma2;  // nullable: a second LayerNorm of the same h + y (GPT-NeoX's ln_2: parallel
+  const bf16_t* beta2;   // residual with two norms), sharing the statistics
+  bf16_t* xn2_out;
+  int N, K1, K2;
 };
 
-// Workgroup (chunk c, row group g): R rows x K1 columns -- chunk 0 of W1 . x1, chunk c >= 1 the
-// (c-1)-th K1-wide slice of W2 . x2: every workgroup streams the same 4 x K1 weight tile as the
-// QKV GEMV's (the shape that reaches ~6 TB/s), NC x as many workgroups as one per row group
-// (one residency wave at N = 4096 streamed ~4.6 TB/s). Partials go to ypart[c]; the last workgroup
-// sums the NC chunks in a fixed order (deterministic), adds bias and residual and normalises.
-template <int R>
+// Workgroup g: R rows over W1 . x1 (+ W2 . x2) -- one weight stream per row group, the shape the QKV
+// GEMV reaches ~6 TB/s with; its R results go to ypart. The last workgroup to arrive (two-level
+// counter) adds bias + residual, rounds h' to bf16 and normalises it for the next projection(s):
+// the out-projection / fc_out, the residual add and the next LayerNorm in one launch, no LayerNorm
+// launch of its own. PER: h' register slices of 2048 columns (N <= 256 * 8 * PER).
+template <int R, int PER>
 __global__ __launch_bounds__(256) void gemv_dual_ln_kernel(DualLn a) {
   __shared__ float part[4][R];
   __shared__ float red[16];
   __shared__ int s_last;
   const int tid = threadIdx.x;
-  const int ngrp = (a.N + R - 1) / R;
-  // chunk fastest: the workgroups in flight together cover whole weight rows (a chunk-major order
-  // had every resident workgroup reading one 8-KB piece of each 32-KB W2 row -- 1 / 4 of the HBM
-  // channels busy, 3.47 vs 2.41 ms/token)
-  const int c = blockIdx.x % a.NC, n0 = (blockIdx.x / a.NC) * R;
-  (void)ngrp;
+  const int n0 = blockIdx.x * R;
   float acc[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) acc[r] = 0.f;
-  if (a.NC == 1) {  // unchunked (A/B): W1 then W2, whole rows
-    gemv_m1_accum<R>(a.x1, a.w1, a.N, a.K1, n0, acc);
-    gemv_m1_accum<R>(a.x2, a.w2, a.N, a.K2, n0, acc);
-  } else if (c == 0) {
-    gemv_m1_accum<R>(a.x1, a.w1, a.N, a.K1, n0, acc);
-  } else {
-    gemv_m1_accum<R>(a.x2 + (long long)(c - 1) * a.K1, a.w2 + (long long)(c - 1) * a.K1, a.N, a.K1, n0, acc, a.K2);
-  }
+  gemv_m1_accum<R>(a.x1, a.w1, a.N, a.K1, n0, acc);
+  if (a.x2) gemv_m1_accum<R>(a.x2, a.w2, a.N, a.K2, n0, acc);
   const float v = gemv_m1_finish<R>(acc, part, nullptr, n0, a.N, 0);
-  if (!a.tail) {  // whole rows (NC == 1): h_out = bf16(h + y + b), nothing crosses workgroups
-    if (tid < R && n0 + tid < a.N) {
-      const float b = a.bias ? bf2f(a.bias[n0 + tid]) : 0.f;
-      a.h_out[n0 + tid] = f2bf(bf2f(a.h[n0 + tid]) + (v + b));
-    }
-    return;
-  }
-  if (tid < R && n0 + tid < a.N) st_pub(&a.ypart[(long long)c * a.N + n0 + tid], v);
-#ifdef KCA_AB_NO_DUAL_TAIL  // timing A/B only (wrong output): the K-chunked GEMV without arrival + LayerNorm
-  if (blockIdx.x == 0) {  // keep the residual stream finite: h_out = xn_out = h
-    for (int k = tid; k < a.N; k += 256) { a.h_out[k] = a.h[k]; a.xn_out[k] = a.h[k]; }
-  }
-  return;
-#endif
+  if (tid < R && n0 + tid < a.N) st_pub(&a.ypart[n0 + tid], v);
   // publish (cdna_hip_programming.md Guideline 16, R1): write-through stores drained, barrier, one
   // agent-scope arrival; the last workgroup re-arms the counter and acquires
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -997,21 +887,15 @@ __global__ __launch_bounds__(256) void gemv_dual_ln_kernel(DualLn a) {
   }
   __syncthreads();
   if (!s_last) return;
-  // h' = bf16(h + y), LN(h') -- the ln_rows_kernel math (statistics over the bf16-rounded sum)
-  constexpr int PER = 4;  // N <= 8192: 256 threads x 8 x PER
+  // h' = bf16(h + y + b), LN(h') -- the ln_rows_kernel math (statistics over the bf16-rounded sum)
   float hv[PER][8];
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     const int k = (i * 256 + tid) * 8;
     if (k < a.N) {
-      float y8[8], t8[8], b8[8];
+      float y8[8], b8[8];
       load8f(a.ypart + k, y8);
-      for (int cc = 1; cc < a.NC; ++cc) {
-        load8f(a.ypart + (long long)cc * a.N + k, t8);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) y8[j] += t8[j];
-      }
       if (a.bias) {
         load8(a.bias + k, b8);
 #pragma unroll
@@ -1042,7 +926,9 @@ __global__ __launch_bounds__(256) void gemv_dual_ln_kernel(DualLn a) {
   for (int i = 0; i < PER; ++i) {
     const int k = (i * 256 + tid) * 8;
     if (k >= a.N) continue;
-    float gm[8], bt[8];
+    float gm[8], bt[8], o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) hv[i][j] = (hv[i][j] - mean) * rstd;
     load8(a.gamma + k, gm);
     if (a.beta) load8(a.beta + k, bt);
     else {
@@ -1050,8 +936,15 @@ __global__ __launch_bounds__(256) void gemv_dual_ln_kernel(DualLn a) {
       for (int j = 0; j < 8; ++j) bt[j] = 0.f;
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) hv[i][j] = (hv[i][j] - mean) * rstd * gm[j] + bt[j];
-    store8(a.xn_out + k, hv[i]);
+    for (int j = 0; j < 8; ++j) o[j] = hv[i][j] * gm[j] + bt[j];
+    store8(a.xn_out + k, o);
+    if (a.xn2_out) {
+      load8(a.gamma2 + k, gm);
+      if (a.beta2) load8(a.beta2 + k, bt);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = hv[i][j] * gm[j] + bt[j];
+      store8(a.xn2_out + k, o);
+    }
   }
 }
 
@@ -1233,18 +1126,6 @@ static int decode_attn_launch(DecodeParams p, float* ws, long long ws_floats, in
   return 0;
 }
 
-// A/B knob: extra dynamic LDS per workgroup (bytes) for the decode layer kernels, which caps the
-// workgroups resident per CU (160 KB / (LDS per workgroup)) -- fewer weight loads in flight, shorter
-// memory latency under load for the attention chain. KCA_DEC_LDS_PAD=<k2>,<k3> (0: off).
-static size_t dec_lds_pad(int which) {
-  static long long pad[2] = {-1, -1};
-  if (pad[0] < 0) {
-    pad[0] = pad[1] = 0;
-    if (const char* e = getenv("KCA_DEC_LDS_PAD")) sscanf(e, "%lld,%lld", &pad[0], &pad[1]);
-  }
-  return (size_t)pad[which];
-}
-
 // Fused decode layer, part 1 (batch 1, see decode_attn_gemv_kernel): kca_decode_prep_attn's
 // arguments plus the fc_in GEMV (gx [gK] -> gy [gN], bias, act). Returns 10 when the shape is
 // outside the instantiated fused variants (G == 1, head_dim 128 / 256, split-K fan-in or one
@@ -1290,11 +1171,11 @@ KCA_API int kca_decode_prep_attn_gemv(const void* qkv, long long ld, const void*
     constexpr int LPT = decltype(lpt)::value;
     constexpr int TPB = 4 * (64 / LPT), U = 4;
     if (p.chunk > TPB * U) {
-      const size_t lds = (size_t)4 * (2 + p.D) * sizeof(float) + dec_lds_pad(0);
+      const size_t lds = (size_t)4 * (2 + p.D) * sizeof(float);
       if (p.tbl) hipLaunchKernelGGL((decode_attn_gemv_kernel<LPT, 1, true, true>), grid, dim3(256), lds, stream, p, nsplit, n_attn, g);
       else hipLaunchKernelGGL((decode_attn_gemv_kernel<LPT, 1, false, true>), grid, dim3(256), lds, stream, p, nsplit, n_attn, g);
     } else {
-      const size_t lds = (size_t)(p.chunk + 4 * p.D) * sizeof(float) + dec_lds_pad(0);
+      const size_t lds = (size_t)(p.chunk + 4 * p.D) * sizeof(float);
       if (p.tbl) hipLaunchKernelGGL((decode_attn_gemv_kernel<LPT, 1, true, false>), grid, dim3(256), lds, stream, p, nsplit, n_attn, g);
       else hipLaunchKernelGGL((decode_attn_gemv_kernel<LPT, 1, false, false>), grid, dim3(256), lds, stream, p, nsplit, n_attn, g);
     }
@@ -1304,102 +1185,30 @@ KCA_API int kca_decode_prep_attn_gemv(const void* qkv, long long ld, const void*
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
-// Merged decode layer, part 1 (see decode_qkv_attn_gemv_kernel): kca_decode_prep_attn_gemv's
-// arguments plus the QKV GEMV (gx . qw^T + qbias -> qkv, which is also the attention's input) and
-// `ready`: >= 32 * H zero-initialised unsigned counters (re-armed by every launch). With a single
-// split (short contexts) the attention stays in kca_decode_prep_attn_gemv (returns 10).
-KCA_API int kca_decode_qkv_attn_gemv(const void* qkv, long long ld, const void* kc, const void* vc,
-                                     long long cs_slot, long long cs_head, long long cs_pos,
-                                     const int* slots, const int* kv_lens, void* out, long long o_bs,
-                                     float* ws, long long ws_floats, int B, int H, int Hkv, int D,
-                                     int max_kv, int chunk, float scale, const float* alibi, const int* tbl,
-                                     int tbl_stride, int ps_shift, int rot, int interleaved, const float* cos_t,
-                                     const float* sin_t, int window, const void* gx, const void* gw,
-                                     const void* gbias, void* gy, int gN, int gK, int gact, const void* qw,
-                                     const void* qbias, unsigned int* ready, int by_row, hipStream_t stream) {
-  if (rot > D || (rot & 1) || (rot > 0 && (!cos_t || !sin_t))) return 8;
-  if (window < 0) return 9;
-  if (B != 1 || H != Hkv || D % 8 || D > 256 || max_kv <= 0 || gK % 8 || gN <= 0 || !ready || !qw) return 10;
-  if (D / 8 <= 8 || ld != 3LL * H * D) return 10;
-  if (((uintptr_t)gx | (uintptr_t)gw | (uintptr_t)qw | (uintptr_t)qkv) & 15) return 10;
-  DecodeParams p{(const bf16_t*)qkv, ld, (const bf16_t*)kc, (const bf16_t*)vc, cs_slot, cs_head,
-                 cs_pos, slots, kv_lens, (bf16_t*)out, o_bs, nullptr, nullptr, alibi, tbl, tbl_stride, ps_shift,
-                 H, Hkv, D, chunk, scale, 1, rot, interleaved, cos_t, sin_t, g_decode_stamps, nullptr, window,
-                 ready, 3 * (D / 4), by_row};
-  if (tbl && (ps_shift < 4 || ps_shift > 20 || tbl_stride <= 0)) return 5;
-  if (chunk <= 0) chunk = kca_decode_chunk(B, Hkv, max_kv);
-  if (tbl && chunk > 1024) return 6;
-  const int nsplit = (max_kv + chunk - 1) / chunk;
-  if (nsplit > 1024) return 7;
-  if (nsplit < 2 || !fanin_enabled()) return 10;  // the split fan-in re-arms the readiness counters
-  p.chunk = chunk;
-  const long long cw = fanin_words(B, H);
-  const long long need = cw + (long long)B * H * nsplit * (D + 2);
-  if (!ws || ws_floats < need) return 4;
-  p.cnt = reinterpret_cast<unsigned int*>(ws);
-  p.ws_o = ws + cw;
-  p.ws_ml = p.ws_o + (long long)B * H * nsplit * D;
-  const GemvM1 q{(const bf16_t*)gx, (const bf16_t*)qw, (const bf16_t*)qbias, (bf16_t*)qkv, 3 * H * D, gK, 0};
-  const GemvM1 g{(const bf16_t*)gx, (const bf16_t*)gw, (const bf16_t*)gbias, (bf16_t*)gy, gN, gK, gact};
-  const int n_qkv = 3 * H * (D / 4);
-  const int n_attn = nsplit * Hkv * B;
-  const dim3 grid(n_qkv + n_attn + (gN + 3) / 4);
-  auto go = [&](auto lpt) {
-    constexpr int LPT = decltype(lpt)::value;
-    constexpr int TPB = 4 * (64 / LPT), U = 4;
-    if (p.chunk > TPB * U) {
-      const size_t lds = (size_t)4 * (2 + p.D) * sizeof(float) + dec_lds_pad(0);
-      if (p.tbl) hipLaunchKernelGGL((decode_qkv_attn_gemv_kernel<LPT, true, true>), grid, dim3(256), lds, stream, p, nsplit, n_qkv, n_attn, q, g);
-      else hipLaunchKernelGGL((decode_qkv_attn_gemv_kernel<LPT, false, true>), grid, dim3(256), lds, stream, p, nsplit, n_qkv, n_attn, q, g);
-    } else {
-      const size_t lds = (size_t)(p.chunk + 4 * p.D) * sizeof(float) + dec_lds_pad(0);
-      if (p.tbl) hipLaunchKernelGGL((decode_qkv_attn_gemv_kernel<LPT, true, false>), grid, dim3(256), lds, stream, p, nsplit, n_qkv, n_attn, q, g);
-      else hipLaunchKernelGGL((decode_qkv_attn_gemv_kernel<LPT, false, false>), grid, dim3(256), lds, stream, p, nsplit, n_qkv, n_attn, q, g);
-    }
-  };
-  if (D / 8 <= 16) go(std::integral_constant<int, 16>{});
-  else go(std::integral_constant<int, 32>{});
-  return hipGetLastError() == hipSuccess ? 0 : 2;
-}
-
-// Fused decode layer, part 2: y = x1 W1^T + x2 W2^T + bias ([N]), h_out = bf16(h + y),
-// xn_out = LN(h_out) (gamma, beta, eps). ypart: >= (1 + K2 / K1) * N fp32 workspace (K2 % K1 == 0);
-// cnt: 32 * (1 + kDualSub) zero-initialised unsigned counters (re-armed by every launch).
+// Fused decode layer, tail: y = x1 W1^T (+ x2 W2^T) + bias ([N]), h_out = bf16(h + y), xn_out =
+// LN(h_out) (gamma, beta, eps) and, with gamma2, xn2_out = the second LayerNorm of h_out (same
+// statistics). x2 / w2 nullable (K2 = 0: one GEMV -- a sequential-residual layer's out-projection or
+// fc_out). ypart: >= N fp32 words; cnt: 32 * (1 + kDualSub) zero-initialised unsigned counters
+// (re-armed by every launch).
 KCA_API int kca_gemv_dual_ln(const void* x1, const void* w1, int K1, const void* x2, const void* w2, int K2,
                              const void* bias, float* ypart, unsigned int* cnt, const void* h, void* h_out,
-                             const void* gamma, const void* beta, float eps, void* xn_out, int N,
-                             hipStream_t stream) {
-  if (N <= 0 || N % 8 || N > 8192 || K1 % 8 || K2 % 8 || K1 <= 0 || K2 <= 0 || K2 % K1 || !ypart || !cnt || !gamma ||
-      !xn_out || !h || !h_out)
+                             const void* gamma, const void* beta, float eps, void* xn_out, const void* gamma2,
+                             const void* beta2, void* xn2_out, int N, hipStream_t stream) {
+  if (N <= 0 || N % 8 || N > 16384 || K1 % 8 || K1 <= 0 || !ypart || !cnt || !gamma || !xn_out || !h || !h_out)
     return 1;
+  if (x2 && (K2 <= 0 || K2 % 8 || !w2)) return 1;
+  if (xn2_out && !gamma2) return 1;
   if (((uintptr_t)x1 | (uintptr_t)w1 | (uintptr_t)x2 | (uintptr_t)w2 | (uintptr_t)h | (uintptr_t)h_out |
-       (uintptr_t)gamma | (uintptr_t)beta | (uintptr_t)xn_out | (uintptr_t)ypart) & 15)
+       (uintptr_t)gamma | (uintptr_t)beta | (uintptr_t)xn_out | (uintptr_t)ypart | (uintptr_t)gamma2 |
+       (uintptr_t)beta2 | (uintptr_t)xn2_out) & 15)
     return 2;
-  // default: one workgroup per 4 rows over K1 + K2 (2.31 ms/token); KCA_DUAL_CHUNK=1 splits K into
-  // QKV-shaped chunks (more, shorter workgroups: 2.39 ms/token, profiles/decode_fused_b1_ab_r3.txt)
-  static int chunked = -1;
-  if (chunked < 0) {
-    const char* e = getenv("KCA_DUAL_CHUNK");
-    chunked = e && e[0] == '1';
-  }
-  const int NC = chunked ? 1 + K2 / K1 : 1;
   const DualLn a{(const bf16_t*)x1, (const bf16_t*)w1, (const bf16_t*)x2, (const bf16_t*)w2, (const bf16_t*)bias,
                  ypart, cnt, (const bf16_t*)h, (bf16_t*)h_out, (const bf16_t*)gamma, (const bf16_t*)beta, eps,
-                 (bf16_t*)xn_out, N, K1, K2, NC, 1};
-  hipLaunchKernelGGL(gemv_dual_ln_kernel<4>, dim3(((N + 3) / 4) * NC), dim3(256), dec_lds_pad(1), stream, a);
-  return hipGetLastError() == hipSuccess ? 0 : 2;
-}
-
-// Fused decode layer, part 2 without the LayerNorm tail: h_out = h + x1 W1^T + x2 W2^T + bias, each
-// workgroup storing its own rows (h_out may alias h). The next layer's QKV GEMV normalises h_out in
-// its prologue (kca_ln_skinny_gemm), so no workgroup waits for the others.
-KCA_API int kca_gemv_dual_res(const void* x1, const void* w1, int K1, const void* x2, const void* w2, int K2,
-                              const void* bias, const void* h, void* h_out, int N, hipStream_t stream) {
-  if (N <= 0 || K1 % 8 || K2 % 8 || K1 <= 0 || K2 <= 0 || !h || !h_out) return 1;
-  if (((uintptr_t)x1 | (uintptr_t)w1 | (uintptr_t)x2 | (uintptr_t)w2) & 15) return 2;
-  const DualLn a{(const bf16_t*)x1, (const bf16_t*)w1, (const bf16_t*)x2, (const bf16_t*)w2, (const bf16_t*)bias,
-                 nullptr, nullptr, (const bf16_t*)h, (bf16_t*)h_out, nullptr, nullptr, 0.f, nullptr, N, K1, K2, 1, 0};
-  hipLaunchKernelGGL(gemv_dual_ln_kernel<4>, dim3((N + 3) / 4), dim3(256), dec_lds_pad(1), stream, a);
+                 (bf16_t*)xn_out, (const bf16_t*)gamma2, (const bf16_t*)beta2, (bf16_t*)xn2_out,
+                 N, K1, x2 ? K2 : 0};
+  const dim3 grid((N + 3) / 4);
+  if (N <= 8192) hipLaunchKernelGGL((gemv_dual_ln_kernel<4, 4>), grid, dim3(256), 0, stream, a);
+  else hipLaunchKernelGGL((gemv_dual_ln_kernel<4, 8>), grid, dim3(256), 0, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

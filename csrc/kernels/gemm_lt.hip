@@ -149,80 +149,3 @@ KCA_API int kca_gemm_lt(const void* A, long long lda, const void* W, long long l
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
-// Weight-gradient accumulation in the GEMM: D (fp32, row-major [M, N], ld ldd) = alpha * A . W^T +
-// beta * D, in place -- a micro-batch's dW = dY^T X lands in the training engine's fp32 gradient
-// buffer directly (beta 0 on the first micro-batch, 1 after), with no bf16 dW and no separate
-// accumulation pass over it (train/engine.py gradient sinks). Tuning: the first eager call per shape
-// times up to kTune candidates on a zeroed scratch D (the real accumulator is never touched twice).
-KCA_API int kca_gemm_lt_acc(const void* A, long long lda, const void* W, long long ldw, float* D, long long ldd,
-                            int M, int N, int K, float alpha, float beta, void* ws, long long ws_bytes,
-                            hipStream_t stream) {
-  if (!A || !W || !D || M <= 0 || N <= 0 || K <= 0 || lda < K || ldw < K || ldd < N || ws_bytes < 0) return 1;
-  int dev = 0;
-  hipGetDevice(&dev);
-  const bool has_c = beta != 0.f;
-  const Key key{dev, M, N, K, lda, ldw, has_c ? ldd : 0, ldd, 0, has_c, 1};
-  std::lock_guard<std::mutex> lock(g_mu);
-  hipblasLtHandle_t h = handle_for(dev);
-  if (!h) return 2;
-  auto it = g_plans.find(key);
-  if (it == g_plans.end()) {
-    Plan p;
-    if (!build(p, M, N, K, lda, ldw, ldd, ldd, false, has_c, true)) return 2;
-    it = g_plans.emplace(key, p).first;
-  }
-  Plan& p = it->second;
-  const float b = has_c ? beta : 0.f;
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  hipStreamIsCapturing(stream, &cap);
-  const bool capturing = cap != hipStreamCaptureStatusNone;
-  if (!p.tuned) {
-    hipblasLtMatmulPreference_t pref = nullptr;
-    hipblasLtMatmulPreferenceCreate(&pref);
-    const uint64_t wsb = (uint64_t)ws_bytes;
-    hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb, sizeof(wsb));
-    constexpr int kAcc = 16;
-    hipblasLtMatmulHeuristicResult_t res[kAcc];
-    int n = 0;
-    hipblasLtMatmulAlgoGetHeuristic(h, p.desc, p.la, p.lb, p.lc, p.ld, pref, kAcc, res, &n);
-    hipblasLtMatmulPreferenceDestroy(pref);
-    if (n <= 0) return 2;
-    int best = 0;
-    while (best < n && (res[best].state != HIPBLAS_STATUS_SUCCESS || res[best].workspaceSize > (size_t)ws_bytes)) ++best;
-    if (best == n) return 2;
-    float* scratch = nullptr;
-    if (!capturing && n > 1 && hipMalloc(&scratch, (size_t)M * ldd * sizeof(float)) == hipSuccess) {
-      hipMemsetAsync(scratch, 0, (size_t)M * ldd * sizeof(float), stream);
-      hipEvent_t e0, e1;
-      hipEventCreate(&e0);
-      hipEventCreate(&e1);
-      float best_ms = 1e30f;
-      for (int i = 0; i < n; ++i) {
-        if (res[i].state != HIPBLAS_STATUS_SUCCESS || res[i].workspaceSize > (size_t)ws_bytes) continue;
-        if (!ok(hipblasLtMatmul(h, p.desc, &alpha, W, p.la, A, p.lb, &b, scratch, p.lc, scratch, p.ld, &res[i].algo,
-                                ws, res[i].workspaceSize, stream)))
-          continue;
-        hipEventRecord(e0, stream);
-        for (int r = 0; r < 3; ++r)
-          hipblasLtMatmul(h, p.desc, &alpha, W, p.la, A, p.lb, &b, scratch, p.lc, scratch, p.ld, &res[i].algo, ws,
-                          res[i].workspaceSize, stream);
-        hipEventRecord(e1, stream);
-        hipEventSynchronize(e1);
-        float ms = 0.f;
-        hipEventElapsedTime(&ms, e0, e1);
-        if (ms < best_ms) best_ms = ms, best = i;
-      }
-      hipEventDestroy(e0);
-      hipEventDestroy(e1);
-      hipStreamSynchronize(stream);
-      hipFree(scratch);
-    }
-    p.algo = res[best].algo;
-    p.ws = res[best].workspaceSize;
-    p.tuned = !capturing;
-  }
-  (void)hipGetLastError();
-  if (!ok(hipblasLtMatmul(h, p.desc, &alpha, W, p.la, A, p.lb, &b, D, p.lc, D, p.ld, &p.algo, ws, p.ws, stream)))
-    return 3;
-  return hipGetLastError() == hipSuccess ? 0 : 3;
-}

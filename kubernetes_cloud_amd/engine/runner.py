@@ -33,17 +33,8 @@ import torch
 
 from .. import ops
 from ..ops import decode as dops
-from ..ops.gemv import embed_ln_rows, ln_gemv_m1, ln_rows, ln_skinny_linear, skinny_linear
+from ..ops.gemv import embed_ln_rows, ln_rows, ln_skinny_linear, skinny_linear
 
-# batch-1 fused decode, two measured-slower alternatives kept as A/B switches (docs/PERF.md, round 4):
-# KCA_DECODE_MERGED=1 runs the QKV GEMV, attention and fc_in as one launch (ops/decode.py
-# decode_qkv_attention_gemv: 2.39 vs 2.28 ms/token -- the attention chain, dispatched behind the QKV
-# workgroups, becomes the launch's tail)
-_MERGED_QKV = os.environ.get("KCA_DECODE_MERGED", "0") in ("1", "true")
-# KCA_DECODE_LN_PROLOGUE=1: the out-projection/fc_out kernel stores h + y row by row and the next
-# layer's QKV GEMV normalises in its prologue (ops/gemv.py ln_gemv_m1), no last-workgroup LayerNorm
-# tail -- bit-identical, but 2.33 vs 2.27 ms/token (every QKV workgroup re-reads h, gamma and beta)
-_LN_PROLOGUE = os.environ.get("KCA_DECODE_LN_PROLOGUE", "0") in ("1", "true")
 # decode steps: each row's RoPE angles and page-table row travel with the step's packed inputs (fixed
 # device addresses), so every layer's attention chain loads them in its first memory round trip
 # instead of after the length / slot arrive; KCA_DECODE_STEP_DESC=0: look them up on the device
@@ -364,23 +355,39 @@ class ModelRunner:
         # step's graph as a fork/join. Not under TP: two concurrent collectives could interleave
         # differently across ranks.
         from ..parallel.tensor_parallel import RowParallelLinear
-        tp = any(isinstance(mm, RowParallelLinear) for mm in model.modules())
+        from ..parallel.tp_emulation import is_emulated
+        rows = [mm for mm in model.modules() if isinstance(mm, RowParallelLinear)]
+        tp = bool(rows)
+        # one rank of a TP layout on one GPU (parallel/tp_emulation.py): its collectives are local
+        # stand-ins, so the fused single-device layer applies to its shard shapes
+        tp_local = all(is_emulated(mm.group) for mm in rows)
         self._par_mlp = (cfg.parallel_residual and on_gpu and not tp and not self.multi_device
                          and os.environ.get("KCA_DECODE_PAR_MLP", "1") not in ("0", "false"))
         self._side = torch.cuda.Stream(device=self.device) if self._par_mlp else None
-        # batch-1 decode of GPT-J-style layers (parallel residual, one shared LayerNorm) as three
-        # launches per layer on ONE queue (ops/decode.py decode_prep_attention_gemv + gemv_dual_ln):
-        # no cross-queue fork/join, no separate LayerNorm launch. KCA_DECODE_FUSED=0: the two-stream form
-        self._fused_ok = (self._par_mlp and all(blk.ln_2 is None for blk in model.h)
-                          and os.environ.get("KCA_DECODE_FUSED", "1") not in ("0", "false"))
+        # batch-1 decode layer on ONE queue, the residual add and the next LayerNorm in the tail of the
+        # projection that produces it (ops/decode.py gemv_dual_ln), no LayerNorm launch of its own:
+        #   "gptj" parallel residual, one shared LN: QKV GEMV -> attention + fc_in -> out + fc_out + LN
+        #   "neox" parallel residual, ln_1 / ln_2 of the same h: as gptj, the tail writes both norms
+        #   "seq"  sequential residual (BLOOM, GPT-2, GPT-Neo): QKV GEMV -> attention -> out-proj +
+        #          residual + ln_2 -> fc_in GEMV -> fc_out + residual + next ln_1
+        # KCA_DECODE_FUSED=0: the per-projection path (two-stream for parallel-residual models)
+        ln2 = [blk.ln_2 for blk in model.h]
+        self._layer_kind = ("gptj" if all(x is None for x in ln2) else "neox") if cfg.parallel_residual else "seq"
+        self._fused_ok = (on_gpu and not self.multi_device and (not tp or tp_local)
+                          and os.environ.get("KCA_DECODE_FUSED", "1") not in ("0", "false")
+                          and cfg.hidden <= 16384
+                          and (self._layer_kind != "neox"
+                               or all(x.eps == blk.ln_1.eps for x, blk in zip(ln2, model.h)))
+                          and (self._layer_kind == "seq"
+                               or (self.H == self.Hkv and self.D % 8 == 0 and 64 < self.D <= 256)))
         self._fz: dict = {}
         self._outbufs: dict = {}
         self._chain_src = None
         # the fused step head gathers the token embedding itself (no learned positions / scale / LN on
         # the embedding) and resolves chained tokens on the device: KCA_DECODE_EMBED_HEAD=0 keeps the
         # torch embedding + cast + LN launches
-        self._embed_head = (self._fused_ok and getattr(model, "wpe", None) is None
-                            and getattr(model, "emb_ln", None) is None and cfg.embed_scale == 1.0
+        # (BLOOM's embedding LayerNorm: the gather kernel normalises with it, one ln_rows launch follows)
+        self._embed_head = (self._fused_ok and getattr(model, "wpe", None) is None and cfg.embed_scale == 1.0
                             and os.environ.get("KCA_DECODE_EMBED_HEAD", "1") not in ("0", "false"))
 
     # ------------------------------------------------------------- prefill
@@ -495,11 +502,8 @@ class ModelRunner:
                 biases.append(bf if bo is None else (bo if bf is None else (bo.float() + bf.float()).to(self.dtype)))
             fz = self._fz["b1"] = {
                 "g": torch.empty(1, f, **z), "h": torch.empty(1, d, **z), "xn": torch.empty(1, d, **z),
-                "ypart": torch.empty((1 + f // d) * d if f % d == 0 else d, device=self.device,
-                                     dtype=torch.float32),
-                "cnt": torch.zeros(32 * 65, device=self.device, dtype=torch.int32), "bias": biases,
-                "ready": torch.zeros(32 * self.H, device=self.device, dtype=torch.int32),
-                "qkv": torch.empty(1, 3 * self.H * self.D, **z)}
+                "xn2": torch.empty(1, d, **z), "ypart": torch.empty(d, device=self.device, dtype=torch.float32),
+                "cnt": torch.zeros(32 * 65, device=self.device, dtype=torch.int32), "bias": biases}
         return fz
 
     def _desc_args(self, cos, sin, tbl):
@@ -515,55 +519,61 @@ class ModelRunner:
         return cos, sin, tbl, by_row
 
     def _layers_decode_fused(self, tokens, pos, slots, kv_lens, max_kv, ws, obuf):
-        """Batch-1 GPT-J-style decode step, three launches per layer (see _fused_ok). Returns None
-        (nothing launched) when the fused kernels do not cover the shape."""
+        """Batch-1 decode step, one queue, the residual + next LayerNorm in each layer's last projection
+        (see _fused_ok for the three layer kinds). Returns None (nothing launched) when the fused kernels
+        do not cover the shape."""
         m, cfg = self.model, self.cfg
         fz = self._fused_bufs()
+        kind = self._layer_kind
         blk0 = m.h[0]
         if self._embed_head:  # token gather (+ chained token) + LayerNorm: one kernel
             chain, prev = self._chain_src if self._chain_src is not None else (None, None)
-            xn, h = embed_ln_rows(m.wte.weight, tokens, blk0.ln_1.weight, blk0.ln_1.bias, blk0.ln_1.eps,
-                                  chain=chain, prev=prev)
+            if m.emb_ln is not None:  # BLOOM: the residual stream starts at LN_emb(wte[id])
+                h, _ = embed_ln_rows(m.wte.weight, tokens, m.emb_ln.weight, m.emb_ln.bias, m.emb_ln.eps,
+                                     chain=chain, prev=prev)
+                xn, _ = ln_rows(h, blk0.ln_1.weight, blk0.ln_1.bias, blk0.ln_1.eps)
+            else:
+                xn, h = embed_ln_rows(m.wte.weight, tokens, blk0.ln_1.weight, blk0.ln_1.bias, blk0.ln_1.eps,
+                                      chain=chain, prev=prev)
         else:
             h0 = m.embed(tokens, pos.long())
             xn, h = ln_rows(h0, blk0.ln_1.weight, blk0.ln_1.bias, blk0.ln_1.eps)
-        hb, xb, g = fz["h"], fz["xn"], fz["g"]
-        kc, vc, tbl = self.cache.k[0], self.cache.v[0], self.cache.table_on(self.device)
+        xn2 = ln_rows(h, blk0.ln_2.weight, blk0.ln_2.bias, blk0.ln_2.eps)[0] if kind == "neox" else None
+        hb, xb, x2b, g = fz["h"], fz["xn"], fz["xn2"], fz["g"]
+        tbl = self.cache.table_on(self.device)
         cos, sin, tbl, by_row = self._desc_args(self.cos, self.sin, tbl)
         for li, blk in enumerate(m.h):
             at, mlp = blk.attn, blk.mlp
             act = 1 if mlp.approx in ("tanh", True) else 2
             kc, vc = self.cache.k[li], self.cache.v[li]
-            qkv = None
-            if xn is None:  # the previous layer left h + y un-normalised: LN in the QKV GEMV's prologue
-                qkv = fz["qkv"]
-                if not ln_gemv_m1(h, blk.ln_1.weight, blk.ln_1.bias, blk.ln_1.eps, at.qkv.weight, at.qkv.bias,
-                                  qkv, xb):
-                    raise RuntimeError("fused decode layer: LN-prologue QKV GEMV does not cover the shape")
-                xn = xb
-            # one launch for QKV GEMV + attention + fc_in where the merged kernel covers the shape
-            # (several attention splits); else the QKV GEMV, then attention + fc_in
-            if not (qkv is None and _MERGED_QKV and dops.decode_qkv_attention_gemv(
-                    xn, at.qkv.weight, at.qkv.bias, fz["qkv"], self.H, self.Hkv, self.D, self.rot,
-                    cfg.rotary_interleaved, cos, sin, pos, slots, kc, vc, kv_lens, max_kv, at.scale,
-                    at.alibi, obuf, ws, tbl, at.window, mlp.fc_in.weight, mlp.fc_in.bias, g, act, fz["ready"],
-                    by_row)) \
-                    and not dops.decode_prep_attention_gemv(
-                        qkv if qkv is not None else skinny_linear(xn, at.qkv.weight, at.qkv.bias), self.H, self.Hkv,
-                        self.D, self.rot, cfg.rotary_interleaved, cos, sin, pos, slots, kc, vc, kv_lens,
-                        max_kv, at.scale, at.alibi, obuf, ws, tbl, at.window, xn, mlp.fc_in.weight, mlp.fc_in.bias,
-                        g, act, by_row):
+            nxt = m.h[li + 1] if li + 1 < len(m.h) else None
+            nln = nxt.ln_1 if nxt is not None else m.ln_f
+            qkv = skinny_linear(xn, at.qkv.weight, at.qkv.bias)
+            if kind == "seq":
+                o = dops.decode_prep_attention(qkv, self.H, self.Hkv, self.D, self.rot, cfg.rotary_interleaved,
+                                               cos, sin, pos, slots, kc, vc, kv_lens, max_kv, at.scale, at.alibi,
+                                               out=obuf, ws=ws, block_table=tbl, window=at.window, by_row=by_row)
+                # out-projection + residual + ln_2, then fc_in (+ GELU), then fc_out + residual + next ln_1
+                dops.gemv_dual_ln(o, at.out.weight, None, None, at.out.bias, h, blk.ln_2.weight, blk.ln_2.bias,
+                                  blk.ln_2.eps, fz["ypart"], fz["cnt"], hb, x2b)
+                f = skinny_linear(x2b, mlp.fc_in.weight, mlp.fc_in.bias, act, out=g)
+                dops.gemv_dual_ln(f, mlp.fc_out.weight, None, None, mlp.fc_out.bias, hb, nln.weight, nln.bias,
+                                  nln.eps, fz["ypart"], fz["cnt"], hb, xb)
+                h, xn = hb, xb
+                continue
+            # parallel residual: attention + fc_in (of ln_2's output for NeoX) in one launch
+            if not dops.decode_prep_attention_gemv(
+                    qkv, self.H, self.Hkv, self.D, self.rot, cfg.rotary_interleaved, cos, sin, pos, slots, kc, vc,
+                    kv_lens, max_kv, at.scale, at.alibi, obuf, ws, tbl, at.window,
+                    xn2 if kind == "neox" else xn, mlp.fc_in.weight, mlp.fc_in.bias, g, act, by_row):
                 if li == 0:
                     return None
                 raise RuntimeError("fused decode layer: shape support changed between layers")
-            if _LN_PROLOGUE and li + 1 < len(m.h) and self.D * 3 * self.H == m.h[li + 1].attn.qkv.weight.shape[0]:
-                dops.gemv_dual_res(obuf, at.out.weight, g, mlp.fc_out.weight, fz["bias"][li], h, hb)
-                h, xn = hb, None
-                continue
-            nxt = m.h[li + 1].ln_1 if li + 1 < len(m.h) else m.ln_f
-            dops.gemv_dual_ln(obuf, at.out.weight, g, mlp.fc_out.weight, fz["bias"][li], h, nxt.weight, nxt.bias,
-                              nxt.eps, fz["ypart"], fz["cnt"], hb, xb)
-            h, xn = hb, xb
+            two = kind == "neox" and nxt is not None
+            dops.gemv_dual_ln(obuf, at.out.weight, g, mlp.fc_out.weight, fz["bias"][li], h, nln.weight, nln.bias,
+                              nln.eps, fz["ypart"], fz["cnt"], hb, xb,
+                              *((nxt.ln_2.weight, nxt.ln_2.bias, x2b) if two else ()))
+            h, xn, xn2 = hb, xb, (x2b if two else None)
         if m.lm_head is None:
             return skinny_linear(xn, m.wte.weight)
         return self._lin(m.lm_head, xn)
@@ -730,8 +740,12 @@ class ModelRunner:
             pin = self.device.type == "cuda"
             dev = torch.empty(3 * Bb, device=self.device, dtype=torch.int32)
             hs = [torch.empty(3 * Bb, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
+            # "flip": the landing buffer of the latest launch, counted per BATCH bucket (every kv bucket of
+            # this Bb copies into these two buffers, so consecutive launches must alternate here even when
+            # they land in different kv buckets -- a per-(Bb, Kb) counter could hand two in-flight steps
+            # the same buffer)
             ob = {"out": dev, "ids": dev[:2 * Bb].view(torch.int64), "lps": dev[2 * Bb:].view(torch.float32),
-                  "out_h": hs, "ids_h": [h[:2 * Bb].view(torch.int64) for h in hs],
+                  "flip": [0], "out_h": hs, "ids_h": [h[:2 * Bb].view(torch.int64) for h in hs],
                   "lps_h": [h[2 * Bb:].view(torch.float32) for h in hs]}
             self._outbufs[Bb] = ob
         return ob
@@ -846,8 +860,11 @@ class ModelRunner:
             raise ValueError("rows chain their token from a previous launch, but prev is None")
         # chained tokens read on the device by the step's first kernel: the previous step wrote them into
         # this bucket's shared output buffer (same batch bucket); otherwise copied into `tokens` below
+        # (not on a step that captures its graph: the capture's eager warm-up runs would read the chained
+        # token from the output buffer their own first run already overwrote)
         fold = (bool(chain_dst) and Bb == 1 and self._embed_head
-                and prev.ids_dev.data_ptr() == st["ids"].data_ptr())
+                and prev.ids_dev.data_ptr() == st["ids"].data_ptr()
+                and (not self.use_graphs or (Bb, Kb) in self._graphs))
         if fold:
             for d_, s_ in zip(chain_dst, chain_src):
                 ch[d_] = s_
@@ -868,7 +885,9 @@ class ModelRunner:
             g.replay()
         else:
             self._step_body(st, Bb, Kb)
-        k = pk.cur
+        fl = st["flip"]
+        fl[0] ^= 1
+        k = fl[0]
         ids_h, lps_h = st["ids_h"][k], st["lps_h"][k]
         if self.device.type == "cuda":
             st["out_h"][k].copy_(st["out"], non_blocking=True)  # ids + log-probs, one copy

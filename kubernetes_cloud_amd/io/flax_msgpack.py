@@ -32,6 +32,13 @@ _TORCH = {"float32": torch.float32, "float16": torch.float16, "bfloat16": torch.
           "uint8": torch.uint8, "int16": torch.int16, "bool": torch.bool}
 
 
+def _shape_of(shape) -> tuple:
+    """A chunked array's shape: flax writes a tuple as {"0": d0, "1": d1, ...}; a list is accepted too."""
+    if isinstance(shape, dict):
+        return tuple(int(shape[str(i)]) for i in range(len(shape)))
+    return tuple(int(d) for d in shape)
+
+
 def _array_from_bytes(data: bytes) -> torch.Tensor:
     shape, name, buf = msgpack.unpackb(data, raw=True)
     name = name.decode() if isinstance(name, bytes) else name
@@ -58,7 +65,7 @@ def _unchunk(tree):
     if isinstance(tree, dict):
         if tree.get(_CHUNKED):
             chunks = [tree["chunks"][str(i)] for i in range(len(tree["chunks"]))]
-            return torch.cat([c.reshape(-1) for c in chunks]).reshape(tuple(tree["shape"]))
+            return torch.cat([c.reshape(-1) for c in chunks]).reshape(_shape_of(tree["shape"]))
         return {k: _unchunk(v) for k, v in tree.items()}
     return tree
 
@@ -99,7 +106,8 @@ def _chunk(tree, max_chunk: int):
         flat = tree.reshape(-1)
         per = max(1, max_chunk // tree.element_size())
         parts = {str(i): flat[o:o + per].clone() for i, o in enumerate(range(0, flat.numel(), per))}
-        return {_CHUNKED: True, "shape": list(tree.shape), "chunks": parts}
+        # flax stores the shape tuple through its tuple -> {"0": d0, "1": d1, ...} state-dict mapping
+        return {_CHUNKED: True, "shape": {str(i): int(d) for i, d in enumerate(tree.shape)}, "chunks": parts}
     return tree
 
 

@@ -281,15 +281,14 @@ class _TembAdds:
 _TILED_DIMS = (64, 96, 128, 160, 256)  # attention_tiled.hip instantiations (fwd + bwd)
 # narrow storage: heads stored 48 wide, staged into the D=64 LDS images of the forward and of both
 # backward kernels (attention_tiled.hip StagerNarrow, DS = 48); KCA_SD_NARROW_HEADS=0 pads inference
-# heads to 64, KCA_SD_NARROW_TRAIN=0 training heads
+# heads to 64 (training always runs narrow)
 _NARROW = os.environ.get("KCA_SD_NARROW_HEADS", "1") not in ("0", "false")
-_NARROW_TRAIN = os.environ.get("KCA_SD_NARROW_TRAIN", "1") not in ("0", "false")
 
 
 def padded_head_dim(hd: int, infer: bool = False) -> int:
     """Smallest full-tile head dim >= hd: 40 -> 48 (64 with the narrow path off), 80 -> 96 (160 runs
     natively)."""
-    dims = ((48,) if (_NARROW if infer else _NARROW_TRAIN) else ()) + _TILED_DIMS
+    dims = ((48,) if (_NARROW or not infer) else ()) + _TILED_DIMS
     return next((d for d in dims if d >= hd), hd)
 
 

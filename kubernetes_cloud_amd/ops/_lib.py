@@ -40,7 +40,6 @@ F = ctypes.c_float
 _SIGS = {
     "kca_layernorm_fwd": [P, P, P, P, P, P, P, P, P, I, I, F, P],
     "kca_gemm_lt": [P, LL, P, LL, P, P, LL, P, LL, I, I, I, F, P, LL, P],
-    "kca_gemm_lt_acc": [P, LL, P, LL, P, LL, I, I, I, F, F, P, LL, P],
     "kca_layernorm_bwd_parts": [I],
     "kca_layernorm_bwd": [P, P, P, P, P, P, P, P, P, I, P, I, I, P],
     "kca_gelu_fwd": [P, P, LL, I, P],
@@ -103,8 +102,7 @@ _SIGS = {
     "kca_dense_to_phase_nhwc": [P, P, I, I, I, I, P],
     "kca_col2im2x2_nhwc": [P, P, I, I, I, I, P],
     "kca_pad_br_nhwc": [P, P, I, I, I, I, P],
-    "kca_gemv_dual_ln": [P, P, I, P, P, I, P, P, P, P, P, P, P, F, P, I, P],
-    "kca_gemv_dual_res": [P, P, I, P, P, I, P, P, P, I, P],
+    "kca_gemv_dual_ln": [P, P, I, P, P, I, P, P, P, P, P, P, P, F, P, P, P, P, I, P],
     "kca_sample_logits": [P, LL, I, I, I, P, P, P, P, P, P, P, I, P, LL, P, P, P, P, P, P],
 }
 
@@ -112,7 +110,6 @@ _SIGS = {
 # fused decode layer (batch 1): kca_decode_prep_attn's arguments (minus the stream), then the fc_in
 # GEMV's x, W, bias, y, N, K, act, then the stream
 _SIGS["kca_decode_prep_attn_gemv"] = _SIGS["kca_decode_prep_attn"][:-2] + [P, P, P, P, I, I, I, I, P]
-_SIGS["kca_decode_qkv_attn_gemv"] = _SIGS["kca_decode_prep_attn_gemv"][:-2] + [P, P, P, I, P]
 
 
 def _load():

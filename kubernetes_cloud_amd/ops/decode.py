@@ -97,8 +97,7 @@ def decode_ws_floats(B: int, H: int, Hkv: int, D: int, max_kv: int, chunk: int =
     return -(-(B * H) // 4) * 4 + B * H * ns * (D + 2) if ns > 1 else 0
 
 
-_DECODE_WGS = int(os.environ.get("KCA_DECODE_WGS", "256"))  # split-K workgroup target (A/B knob)
-_OLD_POLICY = os.environ.get("KCA_DECODE_SPLIT_POLICY", "") == "wgs1024"
+_DECODE_WGS = 256  # split-K workgroup target
 
 
 def decode_chunk(B: int, Hkv: int, max_kv: int) -> int:
@@ -109,9 +108,6 @@ def decode_chunk(B: int, Hkv: int, max_kv: int) -> int:
     workgroups of >= 64 tokens beat many short splits (B=1, 600 cached tokens: 64-token
     splits 11.5 us vs 32-token 20.1 us), a cache of <= 256 tokens is one split, and
     long caches stop at 256-token splits (more workgroups beat longer chains there)."""
-    if _OLD_POLICY:  # A/B: the earlier ~1024-workgroup, 32..1024-token policy
-        want = -(-1024 // (B * Hkv))
-        return max(32, min(1024, -(-(-(-max_kv // want)) // 32) * 32))
     if max_kv <= 256:
         return max(64, -(-max_kv // 32) * 32)
     work = B * Hkv
@@ -228,67 +224,27 @@ def decode_prep_attention_gemv(qkv, n_heads, kv_heads, head_dim, rot, interleave
     return True
 
 
-def decode_qkv_attention_gemv(xn: torch.Tensor, qw: torch.Tensor, qbias: torch.Tensor | None, qkv: torch.Tensor,
-                              n_heads, kv_heads, head_dim, rot, interleaved, cos, sin, pos, slots, k_cache, v_cache,
-                              kv_lens, max_kv, scale, alibi, out, ws, block_table, window, gw: torch.Tensor,
-                              gbias: torch.Tensor | None, gy: torch.Tensor, act: int, ready: torch.Tensor,
-                              by_row: int = 0) -> bool:
-    """Merged decode layer, part 1 (batch 1; csrc/kernels/decode.hip decode_qkv_attn_gemv_kernel): the
-    QKV GEMV ``qkv = xn Wqkv^T + b``, ``decode_prep_attention`` on it and the fc_in GEMV
-    ``gy = act(xn Wfc_in^T + b)`` as ONE launch -- the attention workgroups wait for their head's QKV
-    rows on device counters (``ready``: zero-initialised int32 [32 * n_heads], re-armed by every launch)
-    instead of a kernel boundary. Returns False (nothing launched) outside the merged variants (the
-    caller runs the QKV GEMV and ``decode_prep_attention_gemv``)."""
-    B = qkv.shape[0]
-    _, Hkv, L, D = k_cache.shape
-    if not (_lib.use_native(qkv, k_cache, xn, gw, qw) and _lib.has("kca_decode_qkv_attn_gemv") and B == 1
-            and xn.is_contiguous() and gw.is_contiguous() and gy.is_contiguous() and qw.is_contiguous()
-            and qkv.is_contiguous() and ready.numel() >= 32 * n_heads and ready.dtype == torch.int32
-            and all(b is None or b.dtype == torch.bfloat16 for b in (gbias, qbias))
-            and qw.shape[1] == gw.shape[1] == xn.shape[-1]):
-        return False
-    tbl, tstride, shift = _table_args(block_table, k_cache)
-    chunk = decode_chunk(B, Hkv, max_kv)
-    need = decode_ws_floats(B, n_heads, Hkv, D, max_kv, chunk)
-    if need and (ws is None or ws.numel() < need):
-        return False
-    rc = _lib.require().kca_decode_qkv_attn_gemv(
-        qkv.data_ptr(), qkv.stride(0), k_cache.data_ptr(), v_cache.data_ptr(), k_cache.stride(0), k_cache.stride(1),
-        k_cache.stride(2), slots.data_ptr(), kv_lens.data_ptr(), out.data_ptr(), out.stride(0), _lib.ptr(ws),
-        ws.numel() if ws is not None else 0, B, n_heads, Hkv, D, max_kv, chunk, float(scale), _lib.ptr(alibi), tbl,
-        tstride, shift, rot, int(interleaved), _lib.ptr(cos), _lib.ptr(sin), int(window), xn.data_ptr(),
-        gw.data_ptr(), _lib.ptr(gbias), gy.data_ptr(), gw.shape[0], gw.shape[1], int(act), qw.data_ptr(),
-        _lib.ptr(qbias), ready.data_ptr(), int(by_row), _lib.stream())
-    if rc == 10:
-        return False
-    if rc != 0:
-        raise RuntimeError(f"kca_decode_qkv_attn_gemv returned status {rc}")
-    return True
-
-
-def gemv_dual_ln(x1: torch.Tensor, w1: torch.Tensor, x2: torch.Tensor, w2: torch.Tensor, bias, h: torch.Tensor,
-                 gamma: torch.Tensor, beta, eps: float, ypart: torch.Tensor, cnt: torch.Tensor,
-                 h_out: torch.Tensor, xn_out: torch.Tensor) -> None:
-    """Fused decode layer, part 2 (batch 1; ``kca_gemv_dual_ln``): y = x1 W1^T + x2 W2^T + b, then
-    h_out = h + y and xn_out = LayerNorm(h_out) -- the out-projection, fc_out, the parallel residual
-    and the next layer's LayerNorm in one launch (K-chunked: W2's width a multiple of W1's; ``ypart``
-    holds 1 + K2 / K1 fp32 partial rows). ``cnt``: zero-initialised int32 [32 * 65] arrival counters."""
-    _lib.call("kca_gemv_dual_ln", x1.data_ptr(), w1.data_ptr(), w1.shape[1], x2.data_ptr(), w2.data_ptr(),
-              w2.shape[1], _lib.ptr(bias), ypart.data_ptr(), cnt.data_ptr(), h.data_ptr(), h_out.data_ptr(),
-              gamma.data_ptr(), _lib.ptr(beta), float(eps), xn_out.data_ptr(), w1.shape[0], _lib.stream())
-
-
-def gemv_dual_res(x1: torch.Tensor, w1: torch.Tensor, x2: torch.Tensor, w2: torch.Tensor, bias, h: torch.Tensor,
-                  h_out: torch.Tensor) -> None:
-    """``gemv_dual_ln`` without the LayerNorm tail (``kca_gemv_dual_res``): h_out = h + x1 W1^T +
-    x2 W2^T + b, every workgroup writing its own rows (h_out may be h); the consumer normalises."""
-    _lib.call("kca_gemv_dual_res", x1.data_ptr(), w1.data_ptr(), w1.shape[1], x2.data_ptr(), w2.data_ptr(),
-              w2.shape[1], _lib.ptr(bias), h.data_ptr(), h_out.data_ptr(), w1.shape[0], _lib.stream())
+def gemv_dual_ln(x1: torch.Tensor, w1: torch.Tensor, x2: torch.Tensor | None, w2: torch.Tensor | None, bias,
+                 h: torch.Tensor, gamma: torch.Tensor, beta, eps: float, ypart: torch.Tensor, cnt: torch.Tensor,
+                 h_out: torch.Tensor, xn_out: torch.Tensor, gamma2: torch.Tensor | None = None, beta2=None,
+                 xn2_out: torch.Tensor | None = None) -> None:
+    """Fused decode layer, tail (batch 1; ``kca_gemv_dual_ln``): y = x1 W1^T (+ x2 W2^T) + b, then
+    h_out = h + y and xn_out = LayerNorm(h_out) in one launch -- GPT-J's out-projection + fc_out +
+    parallel residual (two weight streams), a sequential-residual layer's out-projection or fc_out
+    (``x2`` None), and with ``gamma2`` the second LayerNorm of the same h_out into ``xn2_out`` (GPT-NeoX:
+    ln_1 and ln_2 of one residual stream share the statistics). ``ypart``: >= N fp32 words;
+    ``cnt``: zero-initialised int32 [32 * 65] arrival counters. N <= 16384."""
+    _lib.call("kca_gemv_dual_ln", x1.data_ptr(), w1.data_ptr(), w1.shape[1], _lib.ptr(x2), _lib.ptr(w2),
+              w2.shape[1] if w2 is not None else 0, _lib.ptr(bias), ypart.data_ptr(), cnt.data_ptr(), h.data_ptr(),
+              h_out.data_ptr(), gamma.data_ptr(), _lib.ptr(beta), float(eps), xn_out.data_ptr(), _lib.ptr(gamma2),
+              _lib.ptr(beta2), _lib.ptr(xn2_out), w1.shape[0], _lib.stream())
 
 
 def gemv_dual_ln_reference(x1, w1, x2, w2, bias, h, gamma, beta, eps):
     """fp32 reference of ``gemv_dual_ln``: (h + y rounded to bf16, LayerNorm of it)."""
-    y = x1.float() @ w1.float().t() + x2.float() @ w2.float().t()
+    y = x1.float() @ w1.float().t()
+    if x2 is not None:
+        y = y + x2.float() @ w2.float().t()
     if bias is not None:
         y = y + bias.float()
     hn = (h.float() + y).to(h.dtype)

@@ -89,12 +89,8 @@ def _emit(param: torch.Tensor, grad: torch.Tensor):
 
 
 def _emit_wgrad(param: torch.Tensor, a: torch.Tensor, w: torch.Tensor):
-    """Weight gradient ``a w^T`` (TN operands): accumulated by the engine's GEMM sink straight into its
-    fp32 buffer when it has one for ``param``, else computed here and handed on like ``_emit``."""
+    """Weight gradient ``a w^T`` (TN operands), handed on like ``_emit``."""
     if param is None or not param.requires_grad:
-        return None
-    sink = grad_sink.lookup_gemm(param)
-    if sink is not None and sink(param, a, w):
         return None
     return _emit(param, F.linear(a, w))
 

@@ -76,18 +76,12 @@ def skinny_linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | No
 
 # hipBLASLt decode linears with an activation (M > the skinny kernel's rows: fc_in at B >= 3): the
 # GELU as ONE native in-place pass (kca_gelu_fwd) instead of three eager kernels (to fp32, gelu,
-# to bf16: ~25 us per layer at B = 32, on the MLP branch's critical path); KCA_DECODE_GELU=epi
-# takes hipBLASLt's GELU epilogue (tanh form only), =torch the eager chain (A/B)
-_DECODE_GELU = os.environ.get("KCA_DECODE_GELU", "native")
-
-
+# to bf16: ~25 us per layer at B = 32, on the MLP branch's critical path)
 def _linear_act(x, weight, bias, act):
     if not act:
         return F.linear(x, weight, bias)
-    if _DECODE_GELU == "epi" and act == 1 and bias is not None and x.is_cuda:
-        return torch._addmm_activation(bias, x, weight.t(), use_gelu=True)
     y = F.linear(x, weight, bias)
-    if _DECODE_GELU != "torch" and _lib.use_native(y) and y.is_contiguous() and y.numel() % 8 == 0 \
+    if _lib.use_native(y) and y.is_contiguous() and y.numel() % 8 == 0 \
             and y.data_ptr() % 16 == 0 and y.dtype == torch.bfloat16:
         _lib.call("kca_gelu_fwd", y.data_ptr(), y.data_ptr(), y.numel(), int(act == 1), _lib.stream())
         return y
@@ -190,22 +184,4 @@ def ln_skinny_linear(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor | 
     return (y, h, xn) if want_xn else (y, h)
 
 
-def ln_gemv_m1(h: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor | None, eps: float, weight: torch.Tensor,
-               bias: torch.Tensor | None, y: torch.Tensor, xn_out: torch.Tensor) -> bool:
-    """Decode (one row): y = LayerNorm(h) W^T + b with the normalisation in every GEMV workgroup's
-    register prologue (``kca_ln_skinny_gemm``, gemv1_kernel<4, true>) and workgroup 0 storing LN(h) to
-    ``xn_out`` for a second consumer (GPT-J's fc_in). Returns False when the shape is outside it."""
-    K = h.shape[-1]
-    if not (_lib.use_native(h, weight) and h.shape[0] == 1 and K % 8 == 0 and K <= 8192 and h.is_contiguous()
-            and weight.is_contiguous() and gamma.is_contiguous() and (beta is None or beta.is_contiguous())
-            and (bias is None or bias.dtype == torch.bfloat16)
-            and all(t.data_ptr() % 16 == 0 for t in (h, weight, gamma, xn_out))):
-        return False
-    _set_mode()
-    _lib.call("kca_ln_skinny_gemm", h.data_ptr(), K, None, None, None, K, gamma.data_ptr(), _lib.ptr(beta),
-              float(eps), weight.data_ptr(), _lib.ptr(bias), y.data_ptr(), y.stride(0), 1, weight.shape[0], K, 0,
-              xn_out.data_ptr(), _lib.stream())
-    return True
-
-
-__all__ = ["skinny_linear", "ln_skinny_linear", "ln_rows", "ln_gemv_m1", "ACT"]
+__all__ = ["skinny_linear", "ln_skinny_linear", "ln_rows", "ACT"]

@@ -9,7 +9,6 @@ from __future__ import annotations
 import weakref
 
 _SINKS: dict = {}
-_GEMM_SINKS: dict = {}
 
 
 def register(param, fn) -> None:
@@ -17,23 +16,9 @@ def register(param, fn) -> None:
 
 
 def unregister(param) -> None:
-    for tbl in (_SINKS, _GEMM_SINKS):
-        ent = tbl.get(id(param))
-        if ent is not None and ent[0]() is param:
-            del tbl[id(param)]
-
-
-def register_gemm(param, fn) -> None:
-    """``fn(param, a, w)`` accumulates the weight gradient ``a w^T`` itself (a GEMM whose epilogue
-    adds into the owner's fp32 storage); returns False when it cannot, and the caller falls back."""
-    _GEMM_SINKS[id(param)] = (weakref.ref(param), fn)
-
-
-def lookup_gemm(param):
-    ent = _GEMM_SINKS.get(id(param))
-    if ent is None or ent[0]() is not param:
-        return None
-    return ent[1]
+    ent = _SINKS.get(id(param))
+    if ent is not None and ent[0]() is param:
+        del _SINKS[id(param)]
 
 
 def lookup(param):

@@ -257,22 +257,6 @@ def _workspace(dev: torch.device) -> torch.Tensor | None:
     return ws
 
 
-def gemm_acc_f32(a: torch.Tensor, w: torch.Tensor, acc: torch.Tensor, alpha: float, beta: float) -> bool:
-    """acc = alpha * a w^T + beta * acc in place, bf16 operands (K-contiguous rows), fp32 ``acc``
-    [a.shape[0], w.shape[0]] contiguous -- one hipBLASLt GEMM whose epilogue reads and writes the fp32
-    accumulator (``kca_gemm_lt_acc``). Returns False (nothing launched) when it does not apply."""
-    M, K = a.shape
-    N = w.shape[0]
-    if not (_lib.use_native(a, w) and acc.is_cuda and _lib.has("kca_gemm_lt_acc") and a.dtype == w.dtype == torch.bfloat16
-            and acc.dtype == torch.float32 and acc.is_contiguous() and acc.numel() == M * N
-            and w.shape[1] == K and a.stride(1) == 1 and w.stride(1) == 1):
-        return False
-    ws = _workspace(a.device)
-    _lib.call("kca_gemm_lt_acc", a.data_ptr(), a.stride(0), w.data_ptr(), w.stride(0), acc.data_ptr(), N, M, N, K,
-              float(alpha), float(beta), _lib.ptr(ws), _WS_BYTES if ws is not None else 0, _lib.stream())
-    return True
-
-
 class _LinearResidualFn(torch.autograd.Function):
     """Training ``res + F.linear(x, W, b)``: the forward is the one-GEMM epilogue form; the backward
     passes dY through to ``res`` (no copy), dX = dY W, dW by the split-K weight gradient, db by the

@@ -86,6 +86,9 @@ def copy_to_tp(x, group):
 
 
 def reduce_from_tp(x, group):
+    from .tp_emulation import is_emulated
+    if is_emulated(group):  # one rank of a TP layout on one GPU (parallel/tp_emulation.py)
+        return group.all_reduce_(x)
     if torch.is_grad_enabled() and x.requires_grad:
         return _ReduceFromTP.apply(x, group)
     x = x.contiguous()
@@ -98,6 +101,9 @@ def reduce_from_tp(x, group):
 
 
 def gather_last_dim(x, group):
+    from .tp_emulation import is_emulated
+    if is_emulated(group):
+        return group.all_gather_last(x)
     if torch.is_grad_enabled() and x.requires_grad:
         return _GatherLastDim.apply(x, group)
     return _gather_nograd(x, group)

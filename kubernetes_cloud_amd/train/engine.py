@@ -65,11 +65,6 @@ log = logging.getLogger("kca.engine")
 
 ALIGN = 64
 _NONE, _INFLIGHT, _READY = 0, 1, 2
-# KCA_WGRAD_GEMM_ACC=1: weight gradients that fused ops hand over as GEMM operands (ops/fused_block.py)
-# are accumulated by the GEMM itself into the fp32 buffer (ops/linear.py gemm_acc_f32) instead of a
-# bf16 dW GEMM + the accumulation kernel. Off by default: hipBLASLt's fp32-output kernels for these
-# shapes are slower than the bf16 ones plus the pass (GPT-J step 1878 -> 1916 ms, docs/PERF.md)
-_GEMM_ACC = os.environ.get("KCA_WGRAD_GEMM_ACC", "0") in ("1", "true")
 # gradients of at most this many elements are accumulated in batches (kca_accum_grad_multi);
 # KCA_MULTI_ACCUM=0 launches kca_accum_grad per parameter
 _SMALL_GRAD = 1 << 18
@@ -151,9 +146,17 @@ def param_consumers(model: nn.Module) -> list:
     params (embeddings, final norm, head -- each is called as a module where it is used)."""
     blocks = find_units(model)[1:]
     claimed = {id(p) for b in blocks for p in b.parameters()}
-    leaves = [m for m in model.modules()
-              if any(p.requires_grad and id(p) not in claimed for p in m.parameters(recurse=False))]
-    return leaves + blocks
+    # registration order stands in for forward order: modules registered before the first block
+    # (embeddings) are read before it, the rest (final norm, LM head -- the largest bucket) after the
+    # last block, so block 0's gathers are not queued behind the head's
+    first = id(blocks[0]) if blocks else None
+    before, after, seen_block = [], [], False
+    for m in model.modules():
+        if id(m) == first:
+            seen_block = True
+        if any(p.requires_grad and id(p) not in claimed for p in m.parameters(recurse=False)):
+            (after if seen_block else before).append(m)
+    return before + blocks + after
 
 
 def _param_linear_forward(mod: nn.Linear, x):
@@ -361,8 +364,6 @@ class TrainEngine:
         self._hooks = [s.param.register_post_accumulate_grad_hook(self._hook) for s in slots]
         for s in slots:
             grad_sink.register(s.param, self._accum)
-            if _GEMM_ACC:
-                grad_sink.register_gemm(s.param, self._accum_gemm)
         self.native = dev.type == "cuda"
         # TN-layout backward GEMMs (ops/linear.py) for models that support them (they keep
         # full transposed weight copies, so not with partitioned params)
@@ -434,8 +435,13 @@ class TrainEngine:
     def gathered(self):
         """Full parameters materialised on every rank for the duration (no-op
         below stage 3): checkpoint/final save (``stage3_gather_16bit_weights_
-        on_model_save``), sampling, evaluation. All ranks must enter it."""
+        on_model_save``), sampling, evaluation. All ranks must enter it.
+
+        Stages 1-2 with deferred gathers: the last step's all-gathers finish first -- readers such as
+        the decode engine take weights straight from sub-modules, so no block pre-hook would wait."""
         if not self.part_params:
+            if self._defer_ag:
+                self.sync_params()
             yield
             return
         for u in self.units:
@@ -474,19 +480,6 @@ class TrainEngine:
         else:
             dst = self.grad[s.offset:s.offset + s.numel]
         return s, dst, first, first_micro
-
-    def _accum_gemm(self, p: torch.Tensor, a: torch.Tensor, w: torch.Tensor) -> bool:
-        """Gradient sink for weight gradients given as GEMM operands (ops/fused_block.py): dW = a w^T
-        accumulated by ONE hipBLASLt GEMM into the fp32 storage (beta 0 on the first write, 1 after;
-        alpha the micro-batch scale) -- no bf16 dW, no accumulation pass. False: not applicable."""
-        from ..ops.linear import gemm_acc_f32
-        if not self.native or p.dim() != 2 or id(p) in self._pend_ids:
-            return False
-        s, dst, first, first_micro = self._dst(p)
-        if not gemm_acc_f32(a, w, dst.view(p.shape), 1.0 / self.grad_accum, 0.0 if first else 1.0):
-            return False
-        self._accounted(p, s, first_micro)
-        return True
 
     def _accum(self, p: torch.Tensor, g: torch.Tensor):
         """Add one micro-batch gradient of ``p`` into fp32 storage (the full grad

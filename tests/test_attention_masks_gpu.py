@@ -185,7 +185,7 @@ def test_narrow_48_storage_matches_reference(rowsum):
 def test_unet_inference_heads_are_48_wide():
     from kubernetes_cloud_amd.models import unet
     assert unet.padded_head_dim(40, infer=True) == 48
-    assert unet.padded_head_dim(40) == (48 if unet._NARROW_TRAIN else 64)  # fwd + bwd narrow kernels
+    assert unet.padded_head_dim(40) == 48  # fwd + bwd narrow kernels
     assert unet.padded_head_dim(80, infer=True) == 96
 
 

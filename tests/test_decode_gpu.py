@@ -537,25 +537,35 @@ def test_engine_gpu_chunked_prefill(preset):
         assert float(top2[0] - top2[1]) < 0.1, (preset, i)
 
 
-def test_gemv_dual_ln_matches_reference():
-    """decode.hip gemv_dual_ln_kernel: y = x1 W1^T + x2 W2^T + b, h' = h + y, LN(h') in one launch
-    (arrival counter, last workgroup normalises); repeated launches reuse the re-armed counter."""
+@pytest.mark.parametrize("N,K1,K2,two_ln", [(4096, 4096, 16384, False), (6144, 6144, 24576, True),
+                                             (14336, 1792, 0, False), (14336, 7168, 0, True)])
+def test_gemv_dual_ln_matches_reference(N, K1, K2, two_ln):
+    """decode.hip gemv_dual_ln_kernel: y = x1 W1^T (+ x2 W2^T) + b, h' = h + y, LN(h') in one launch
+    (arrival counter, last workgroup normalises) -- GPT-J (two weight streams), GPT-NeoX-20B (two
+    LayerNorms of h'), BLOOM TP=8 rank shapes (one stream, N = 14336); repeated launches reuse the
+    re-armed counter."""
     torch.manual_seed(3)
-    N, K1, K2 = 4096, 4096, 16384
     bf = dict(device=dev, dtype=torch.bfloat16)
-    x1, x2 = torch.randn(1, K1, **bf), torch.randn(1, K2, **bf)
-    w1, w2 = torch.randn(N, K1, **bf) * K1 ** -0.5, torch.randn(N, K2, **bf) * K2 ** -0.5
+    x1 = torch.randn(1, K1, **bf)
+    w1 = torch.randn(N, K1, **bf) * K1 ** -0.5
+    x2 = torch.randn(1, K2, **bf) if K2 else None
+    w2 = torch.randn(N, K2, **bf) * K2 ** -0.5 if K2 else None
     b, h = torch.randn(N, **bf), torch.randn(1, N, **bf)
     gamma, beta = torch.randn(N, **bf), torch.randn(N, **bf)
-    ypart = torch.empty((1 + K2 // K1) * N, device=dev, dtype=torch.float32)
+    g2, b2 = torch.randn(N, **bf), torch.randn(N, **bf)
+    ypart = torch.empty(N, device=dev, dtype=torch.float32)
     cnt = torch.zeros(32 * 65, device=dev, dtype=torch.int32)
     hn_ref, xn_ref = dops.gemv_dual_ln_reference(x1, w1, x2, w2, b, h, gamma, beta, 1e-5)
+    xn2_ref = F.layer_norm(hn_ref.float(), (N,), g2.float(), b2.float(), 1e-5)
     for _ in range(3):
-        h_out, xn = torch.empty(1, N, **bf), torch.empty(1, N, **bf)
-        dops.gemv_dual_ln(x1, w1, x2, w2, b, h, gamma, beta, 1e-5, ypart, cnt, h_out, xn)
+        h_out, xn, xn2 = torch.empty(1, N, **bf), torch.empty(1, N, **bf), torch.empty(1, N, **bf)
+        dops.gemv_dual_ln(x1, w1, x2, w2, b, h, gamma, beta, 1e-5, ypart, cnt, h_out, xn,
+                          *((g2, b2, xn2) if two_ln else ()))
         torch.cuda.synchronize()
         assert (h_out.float() - hn_ref.float()).abs().max() < 0.05
         assert (xn.float() - xn_ref).abs().max() < 0.08
+        if two_ln:
+            assert (xn2.float() - xn2_ref).abs().max() < 0.08
     assert int(cnt.abs().sum()) == 0  # every counter re-armed
 
 
@@ -640,60 +650,9 @@ def test_decode_attention_gemv_step_descriptors(PS, L0):
     assert torch.equal(y0, y1)
 
 
-@pytest.mark.parametrize("PS", [0, 64])
-@pytest.mark.parametrize("L0", [40, 600])
-def test_decode_qkv_attention_gemv_merged_matches_separate(PS, L0):
-    """decode_qkv_attn_gemv_kernel (QKV GEMV + attention + fc_in in one launch, the attention waiting
-    on per-head device counters) against the QKV GEMV followed by decode_attn_gemv_kernel: the same
-    QKV row, attention output and cache append bit for bit, the fc_in values within bf16 rounding,
-    and every readiness counter re-armed after each launch."""
-    from kubernetes_cloud_amd.ops.gemv import skinny_linear
-    torch.manual_seed(11 + L0)
-    H, D, rot, L = 16, 256, 64, 1024
-    bf = dict(device=dev, dtype=torch.bfloat16)
-    kc0 = torch.randn(2, H, L, D, device=dev).to(torch.bfloat16)
-    vc0 = torch.randn_like(kc0)
-    tbl = None
-    if PS:
-        kc0, tbl = _paginate(kc0, PS, 3)
-        vc0, _ = _paginate(vc0, PS, 3)
-    cos, sin = rope_tables(rot, L, 10000.0, dev)
-    slots = torch.tensor([1], device=dev, dtype=torch.int32)
-    pos = torch.tensor([L0 - 1], device=dev, dtype=torch.int32)
-    kv_lens = pos + 1
-    xn = torch.randn(1, 4096, **bf)
-    qw, qb = torch.randn(3 * H * D, 4096, **bf) * 0.02, torch.randn(3 * H * D, **bf)
-    gw, gb = torch.randn(16384, 4096, **bf) * 0.02, torch.randn(16384, **bf)
-    ws = torch.zeros(max(dops.decode_ws_floats(1, H, H, D, L), 1), device=dev, dtype=torch.float32)
-    ready = torch.zeros(32 * H, device=dev, dtype=torch.int32)
-    res = []
-    for merged in (False, True, True):
-        kc, vc, out = kc0.clone(), vc0.clone(), torch.empty(1, H * D, **bf)
-        gy = torch.empty(1, 16384, **bf)
-        if merged:
-            qkv = torch.full((1, 3 * H * D), float("nan"), **bf)
-            assert dops.decode_qkv_attention_gemv(xn, qw, qb, qkv, H, H, D, rot, True, cos, sin, pos, slots, kc, vc,
-                                                  kv_lens, L, D ** -0.5, None, out, ws, tbl, 0, gw, gb, gy, 1, ready)
-        else:
-            qkv = skinny_linear(xn, qw, qb)
-            assert dops.decode_prep_attention_gemv(qkv, H, H, D, rot, True, cos, sin, pos, slots, kc, vc,
-                                                   kv_lens, L, D ** -0.5, None, out, ws, tbl, 0, xn, gw, gb, gy, 1)
-        torch.cuda.synchronize()
-        assert int(ready.abs().sum()) == 0
-        res.append((qkv, out, gy, kc, vc))
-    (q0, o0, y0, k0, v0) = res[0]
-    for q1, o1, y1, k1, v1 in res[1:]:
-        assert torch.equal(q0, q1)
-        assert torch.equal(k0, k1) and torch.equal(v0, v1)
-        assert torch.equal(o0, o1)
-        assert torch.equal(y0, y1)
-
-
-def test_engine_fused_b1_ln_prologue_bit_identical(monkeypatch):
-    """The fused batch-1 layer with the LayerNorm in the next QKV GEMV's prologue (gemv_dual_res +
-    ln_gemv_m1) computes the same bf16 values as the last-workgroup LayerNorm tail (gemv_dual_ln):
-    same statistics partition, same rounding -- identical greedy tokens and logits; so do the
-    per-step RoPE / page-row descriptors against the device-side lookups."""
+def test_engine_fused_b1_step_descriptors_bit_identical(monkeypatch):
+    """The fused batch-1 layer with the per-step RoPE / page-row descriptors computes exactly the
+    tokens and log-probs of the device-side table lookups."""
     from kubernetes_cloud_amd.engine import runner as runner_mod
     from kubernetes_cloud_amd.engine.llm_engine import LLMEngine, SamplingParams
     from kubernetes_cloud_amd.models.causal_lm import build_model
@@ -704,17 +663,13 @@ def test_engine_fused_b1_ln_prologue_bit_identical(monkeypatch):
     p = [int(x) for x in torch.randint(0, 1000, (40,))]
     sp = SamplingParams(max_new_tokens=12, do_sample=False, logprobs=True)
     outs = []
-    for pro, desc in ((True, True), (False, False), (False, True)):
-        monkeypatch.setattr(runner_mod, "_LN_PROLOGUE", pro)
+    for desc in (True, False):
         monkeypatch.setattr(runner_mod, "_STEP_DESC", desc)
         eng = LLMEngine(m, max_slots=2, max_len=256, use_graphs=True)
         assert eng.runner._fused_ok
         r = eng.generate([p], sp)[0]
-        outs.append((r.output, getattr(r, "logprobs", None)))
-    for o in outs[1:]:
-        assert outs[0][0] == o[0]
-        if outs[0][1] is not None:
-            assert outs[0][1] == o[1]
+        outs.append((r.output, r.logprobs))
+    assert outs[0] == outs[1]
 
 
 def test_engine_step_descriptors_batched_bit_identical(monkeypatch):
@@ -842,3 +797,97 @@ def test_sample_multiworkgroup_wide_ties_take_the_block_path():
     assert bool((base[ids] == 5.0).all())
     freq = torch.bincount(ids, minlength=V)[top].float()
     assert (freq / B - 1 / 300).abs().max() < 0.01
+
+
+@pytest.mark.parametrize("B", [1, 3])
+def test_engine_lookahead_across_kv_buckets_matches_unpipelined(B):
+    """The one-step lookahead launches step t+1 before the host reads step t. When t+1 lands in a
+    different kv-length bucket (max_kv crosses 256 -> 257, its own graph and packed inputs), the two
+    in-flight steps must still land their sampled ids in different pinned buffers: the pipelined run
+    equals the unpipelined one token for token (the landing buffer flips per batch bucket)."""
+    from kubernetes_cloud_amd.engine.llm_engine import LLMEngine, SamplingParams
+    m = _gpu_model("gpt-j-6b")
+    g = torch.Generator().manual_seed(3)
+    # prompts end just below the 256 bucket edge, so the decode crosses it a few tokens in
+    prompts = [[int(x) for x in torch.randint(0, 1000, (n,), generator=g)] for n in (250, 245, 200)[:B]]
+    sp = SamplingParams(max_new_tokens=24, do_sample=False, logprobs=True)
+    outs = []
+    for pipe in (False, True):
+        eng = LLMEngine(m, max_slots=4, max_len=512, use_graphs=True, pipeline=pipe)
+        assert eng.pipeline == pipe
+        outs.append([(r.output, r.logprobs) for r in eng.generate(prompts, sp)])
+    assert outs[0] == outs[1]
+
+
+def _small_lm(preset, **over):
+    from kubernetes_cloud_amd.models.causal_lm import build_model
+    from kubernetes_cloud_amd.models.config import PRESETS_HF, LMConfig
+    small = {"gpt-neox-20b": dict(hidden_size=768, num_hidden_layers=3, num_attention_heads=8,
+                                  intermediate_size=3072, max_position_embeddings=512),
+             "pythia-2.8b": dict(hidden_size=640, num_hidden_layers=3, num_attention_heads=8,
+                                 intermediate_size=2560, max_position_embeddings=512),
+             "bloom-560m": dict(hidden_size=512, n_layer=3, n_head=4),
+             "gpt2": dict(n_embd=512, n_layer=3, n_head=8, n_positions=512)}[preset]
+    cfg = dict(PRESETS_HF[preset])
+    cfg.update(small, **over)
+    return build_model(LMConfig.from_hf(cfg), device=dev, dtype=torch.bfloat16, seed=0)
+
+
+def _check_against_forward(m, prompt, out, margin=0.1):
+    """Every generated token with a clear top-2 margin is the argmax of a full forward (random-init
+    logits are flat: near-ties flip between two bf16 roundings of the same math)."""
+    with torch.no_grad():
+        lg = m(torch.tensor([prompt + out], device=dev))[0].float()
+    for i, t in enumerate(out):
+        row = lg[len(prompt) - 1 + i]
+        top2 = row.topk(2).values
+        if float(top2[0] - top2[1]) > margin:
+            assert int(row.argmax()) == t, i
+
+
+@pytest.mark.parametrize("preset,kind", [("gpt-neox-20b", "neox"), ("pythia-2.8b", "neox"),
+                                         ("bloom-560m", "seq"), ("gpt2", "seq")])
+def test_engine_fused_b1_layer_kinds(preset, kind):
+    """The batch-1 fused decode layer for GPT-NeoX (parallel residual, ln_1 and ln_2 of one stream from
+    one tail: head_dim 96 / 80, rotate-half RoPE on 25 % of it) and for sequential-residual models
+    (BLOOM: ALiBi + embedding LayerNorm; GPT-2: learned positions): greedy tokens of the fused and
+    the per-projection paths each match a full forward of their own continuation, with HIP graphs."""
+    from kubernetes_cloud_amd.engine.llm_engine import LLMEngine, SamplingParams
+    m = _small_lm(preset)
+    g = torch.Generator().manual_seed(5)
+    p = [int(x) for x in torch.randint(0, 1000, (70,), generator=g)]
+    sp = SamplingParams(max_new_tokens=16, do_sample=False)
+    outs = []
+    for fused in (True, False):
+        eng = LLMEngine(m, max_slots=2, max_len=256, use_graphs=True)
+        assert eng.runner._fused_ok and eng.runner._layer_kind == kind
+        eng.runner._fused_ok = fused
+        outs.append(eng.generate([p], sp)[0].output)
+    for out in outs:
+        _check_against_forward(m, p, out)
+    # sampled decode through the fused graph is reproducible
+    eng = LLMEngine(m, max_slots=2, max_len=256, use_graphs=True)
+    sp2 = SamplingParams(max_new_tokens=12, temperature=0.8, top_k=10, seed=3)
+    assert eng.generate([p], sp2)[0].output == eng.generate([p], sp2)[0].output
+
+
+def test_engine_bloom_tp_emulated_rank_fused():
+    """Rank 0 of a TP=4 BLOOM layout on one GPU (parallel/tp_emulation.py): the fused sequential layer
+    runs on the shard shapes (row-parallel out-projection / fc_out with their replicated biases in the
+    LayerNorm tail, vocab-parallel head tiled to the full vocabulary); its tokens match the model's own
+    full forward through the same stand-in collectives."""
+    from kubernetes_cloud_amd.engine.llm_engine import LLMEngine, SamplingParams
+    from kubernetes_cloud_amd.models.config import PRESETS_HF, LMConfig
+    from kubernetes_cloud_amd.parallel.tp_emulation import emulated_rank_model
+    cfg = dict(PRESETS_HF["bloom-560m"])
+    cfg.update(hidden_size=1024, n_layer=3, n_head=16, vocab_size=4096)
+    m = emulated_rank_model(LMConfig.from_hf(cfg), 4, 0, device=dev)
+    assert m.h[0].attn.qkv.weight.shape == (3 * 4 * 64, 1024) and m.lm_head.local_weight().shape[0] == 1024
+    g = torch.Generator().manual_seed(9)
+    p = [int(x) for x in torch.randint(0, 4096, (50,), generator=g)]
+    sp = SamplingParams(max_new_tokens=12, do_sample=False)
+    eng = LLMEngine(m, max_slots=2, max_len=256, use_graphs=True)
+    assert eng.runner._fused_ok and eng.runner._layer_kind == "seq"
+    out = eng.generate([p], sp)[0].output
+    _check_against_forward(m, p, out)
+    assert m.h[0].attn.out.group.allreduce_calls > 0

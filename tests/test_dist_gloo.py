@@ -54,7 +54,8 @@ def _worker(rank, world, port, stage, bucket, ckpt, out_path):
             assert eng._ag_works, "step() should leave the param gathers in flight"
     if stage == 3:  # released between steps: only this rank's shard is resident
         assert all(p.numel() == 0 for p in m.parameters()), "ZeRO-3 params not released"
-    with eng.gathered():
+    with eng.gathered():  # stages 1-2: the deferred gathers are finished inside (sampling reads weights directly)
+        assert not eng._ag_works and not any(c[2] for c in eng._consumers)
         sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
     if rank == 0:
         torch.save({"sd": sd, "mem": mem}, out_path)
@@ -155,3 +156,16 @@ def test_launcher_runs_finetuner_two_ranks(stage, tmp_path):
     assert "RESUMED" in r.stderr
     fin4 = read_hf_state_dict(str(rd / "final"))
     assert any(not torch.equal(fin4[k], fin[k]) for k in fin)
+
+
+def test_param_consumers_forward_order():
+    """Deferred ZeRO-1/2 gathers launch in forward order: embedding, blocks, then final norm / head."""
+    from kubernetes_cloud_amd.train.engine import param_consumers
+    m = _model()
+    cons = param_consumers(m)
+    names = {id(mod): n for n, mod in m.named_modules()}
+    order = [names[id(c)] for c in cons]
+    assert order[0] == "wte", order
+    blocks = [i for i, n in enumerate(order) if n.startswith("h.")]
+    assert blocks == list(range(1, 1 + len(m.h))), order
+    assert set(order[1 + len(m.h):]) >= {"ln_f"}, order

@@ -564,34 +564,6 @@ def test_engine_fused_block_matches_unfused(monkeypatch):
     assert _rel(out[0], out[1]) < 5e-3
 
 
-def test_engine_wgrad_gemm_accumulate_matches_split(monkeypatch):
-    """The fused block's weight gradients accumulated by hipBLASLt straight into the engine's fp32
-    buffer (kca_gemm_lt_acc: beta 0 on the first micro-batch, 1 after) against a bf16 dW GEMM plus
-    the accumulation kernel: the same GAS-2 gradients up to the split path's bf16 rounding of dW."""
-    from kubernetes_cloud_amd.models.causal_lm import build_model
-    from kubernetes_cloud_amd.ops import linear as lin
-    from kubernetes_cloud_amd.train import engine as engine_mod
-    from kubernetes_cloud_amd.train.engine import TrainEngine
-    monkeypatch.setenv("KCA_FUSED_BLOCK", "1")
-    ids = [torch.randint(0, 1024, (2, 128), device=DEV) for _ in range(2)]
-    calls = []
-    real = lin.gemm_acc_f32
-    monkeypatch.setattr(lin, "gemm_acc_f32", lambda *a: real(*a) and not calls.append(1))  # counts launches
-    grads = []
-    for acc in (True, False):
-        monkeypatch.setattr(engine_mod, "_GEMM_ACC", acc)
-        m = build_model(_tiny_gptj(256, 4, 32), device=DEV, dtype=torch.bfloat16, seed=0)
-        eng = TrainEngine(m, lr=1e-3, weight_decay=0.01, grad_accum=2)
-        n0 = len(calls)
-        for b in ids:
-            eng.backward(m(b, labels=b))
-        torch.cuda.synchronize()
-        assert (len(calls) - n0 == 2 * 4 * len(m.h)) == acc  # 4 block weights x layers x micro-batches
-        grads.append(eng.grad.clone())
-        eng.remove_hooks()
-    assert _rel(grads[0], grads[1]) < 1e-2
-
-
 def test_unet_padded_head_self_attention():
     """Inference self-attention with 40-wide heads zero-padded to 64 (fused
     padded QKV GEMM + D=64 full-tile kernel, models/unet.py Attention.forward)

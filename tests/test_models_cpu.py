@@ -181,3 +181,19 @@ def test_dalle_flax_msgpack_roundtrip(tmp_path, stacked):
         assert torch.allclose(got, ref, atol=1e-5), (got - ref).abs().max()
         codes = torch.randint(0, 64, (1, 4))
         assert torch.allclose(vq2.decode_code(codes), vq.decode_code(codes), atol=1e-5)
+
+
+def test_flax_msgpack_chunked_shape_forms():
+    """A chunked array (flax splits arrays over ~1 GiB) carries its shape as flax's tuple mapping
+    {"0": d0, "1": d1}; the reader accepts that form and a plain list."""
+    import msgpack
+
+    from kubernetes_cloud_amd.io import flax_msgpack
+    t = torch.arange(96, dtype=torch.float32).reshape(4, 24)
+    blob = flax_msgpack.dumps({"w": t}, max_chunk=64)
+    got = flax_msgpack.loads(blob)["w"]
+    assert torch.equal(got, t)
+    raw = msgpack.unpackb(blob, raw=False, strict_map_key=False)
+    assert raw["w"]["shape"] == {"0": 4, "1": 24}
+    raw["w"]["shape"] = [4, 24]
+    assert torch.equal(flax_msgpack.loads(msgpack.packb(raw, use_bin_type=True))["w"], t)
