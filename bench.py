@@ -28,12 +28,15 @@ the headline always prints):
 * N = 1 only (``--extra``):
   ``secondary_dreambooth``  SD-1.5 DreamBooth samples/s (BASELINE config 3,
                             the reference formula: instance batch / step time);
-  ``secondary_decode``      GPT-J-6B decode ms/token at batch 1 and 32, prompt
-                            512 (the FasterTransformer GPT-J serving row);
-  ``secondary_bloom_slice`` BLOOM-176B, 8 of 70 layers + embeddings/head, TP
-                            modules under a one-rank RCCL group, batch 1/8/32;
-  ``secondary_weight_load`` GPT-J fp16 ``.tensors`` -> HBM GB/s (file written
-                            in the run, O_DIRECT read);
+  ``secondary_decode``      GPT-J-6B and GPT-NeoX-20B decode ms/token at batch 1
+                            and 32, prompt 512, greedy and FT top_k 10 (the two
+                            FasterTransformer serving rows);
+  ``secondary_bloom_tp8_rank`` BLOOM-176B TP=8, rank 0's shard of all 70 layers +
+                            its vocab shard of the head on this one GPU, stand-in
+                            collectives (parallel/tp_emulation.py), batch 1/8/32;
+  ``secondary_weight_load`` GPT-J fp16 and BLOOM TP=8 rank-0 shard ``.tensors``
+                            -> HBM GB/s (files written in the run, O_DIRECT read)
+                            next to the raw O_DIRECT storage read rate;
   ``secondary_serving``     the tensorized GPT-J KServe predictor and the BLOOM
                             predictor over HTTP (bench/serving_bench.py):
                             req/s, p50/p99, tokens/s at concurrency 1/8/32, and
@@ -88,7 +91,7 @@ def main():
     ap.add_argument("--extra", choices=["auto", "on", "off"], default="auto",
                     help="N=1 secondaries (DreamBooth, GPT-J decode, BLOOM 8-layer slice, weight load); "
                          "'auto' = when N == 1")
-    ap.add_argument("--extra-timeout", type=float, default=330.0,
+    ap.add_argument("--extra-timeout", type=float, default=600.0,
                     help="seconds for all N=1 secondaries together; on overrun the line prints with what finished")
     # rehearsal shrink flags (tests/test_bench_shared_gpu.py): NOT the BASELINE config
     ap.add_argument("--layers", type=int, default=0)
@@ -389,27 +392,31 @@ def _extras(args, dev, rec):
         return sdb.bench_train(a, dev)
 
     def decode():
-        return _load_bench("decode_bench").run_decode("gpt-j-6b", batches=(1, 32), prompt_len=512, new_tokens=64,
-                                                     sampling=("greedy", "ft_topk10"))
+        db = _load_bench("decode_bench")
+        out = db.run_decode("gpt-j-6b", batches=(1, 32), prompt_len=512, new_tokens=64,
+                            sampling=("greedy", "ft_topk10"))
+        torch.cuda.empty_cache()
+        return out + db.run_decode("gpt-neox-20b", batches=(1, 32), prompt_len=512, new_tokens=64,
+                                   sampling=("greedy", "ft_topk10"))
 
-    def bloom_slice():
-        import torch.distributed as dist
-        # one-rank RCCL group: TP modules + vocab-parallel head, collectives captured in the decode graph
-        store = dist.HashStore()
-        dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=dev)
-        try:
-            recs = _load_bench("bloom_tp_bench").run_tp_decode("bloom-176b", layers=8, batches=(1, 8, 32),
-                                                               prompt_len=128, new_tokens=32)
-        finally:
-            dist.destroy_process_group()
-        return {"proxy": "TP=1 (one-rank RCCL group), 8 of 70 layers, bf16: a proxy for BASELINE config 4 "
-                         "(TP=8, all 70 layers, fp16 checkpoint, engine + HTTP); fp16 checkpoints load as bf16 "
-                         "(same bytes per weight; the decode kernels are bf16-native)",
+    def bloom_tp8_rank():
+        recs = _load_bench("bloom_tp_bench").run_tp_decode("bloom-176b", layers=0, batches=(1, 8, 32),
+                                                           prompt_len=128, new_tokens=32, emulate_tp=8)
+        return {"layout": "rank 0 of TP=8 on one GPU: all 70 layers at the per-rank shard shapes (QKV "
+                          "14336->5376, out 1792->14336, fc_in 14336->7168, fc_out 7168->14336) + the "
+                          "31,360-row head shard; all-reduces / the logits all-gather are stand-ins "
+                          "(identity / local tile), their count and bytes reported per record; bf16 (fp16 "
+                          "checkpoints load as bf16: same bytes per weight)",
                 "records": recs}
 
     def weight_load():
         d = os.environ.get("KCA_WEIGHT_LOAD_DIR", os.environ.get("TMPDIR", "/tmp"))
-        return _load_bench("weight_load_bench").run_weight_load("gpt-j-6b", d, threads=8, sources=("cold",))
+        wl = _load_bench("weight_load_bench")
+        out = wl.run_weight_load("gpt-j-6b", d, threads=8, sources=("cold",))
+        torch.cuda.empty_cache()
+        # BASELINE.md:55's "one BLOOM TP shard": rank 0 of TP=8, 10 of 70 layers + the embedding,
+        # extrapolated to the whole shard at the measured rate
+        return out + wl.run_weight_load("bloom-176b", d, threads=8, sources=("cold",), tp=8, layers=10)
 
     def serving():
         # the tensorized GPT-J KServe predictor and the BLOOM predictor contract over HTTP
@@ -424,7 +431,7 @@ def _extras(args, dev, rec):
     try:
         fenced("secondary_dreambooth", dreambooth)
         fenced("secondary_decode", decode)
-        fenced("secondary_bloom_slice", bloom_slice)
+        fenced("secondary_bloom_tp8_rank", bloom_tp8_rank)
         fenced("secondary_weight_load", weight_load)
         fenced("secondary_serving", serving)
     finally:

@@ -40,7 +40,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch
 
-LEVELS = ((1, 8), (8, 64), (32, 256))  # (concurrency, requests): ~8 requests per connection at 32
+# (concurrency, requests): >= 32 requests per level, so a level's p99 and stdev rest on >= 32 samples
+LEVELS = ((1, 32), (8, 64), (32, 256))
 
 
 def _free_port() -> int:
@@ -108,8 +109,14 @@ def _engine(pred, n: int, conc: int, seed: int = 0, kind: str = "kserve") -> dic
     with ThreadPoolExecutor(conc) as ex:
         lat = sorted(ex.map(one, payloads))
     dt = time.perf_counter() - t0
-    return {"throughput_rps": n / dt, "mean_latency_s": statistics.mean(lat), "p50_s": lat[int(0.5 * (n - 1))],
-            "p99_s": lat[int(0.99 * (n - 1))]}
+    return {"throughput_rps": n / dt, "latencies": lat, **_lat_stats(lat)}
+
+
+def _lat_stats(lat: list) -> dict:
+    lat = sorted(lat)
+    n = len(lat)
+    return {"mean_latency_s": statistics.mean(lat), "stdev_latency_s": statistics.stdev(lat) if n > 1 else 0.0,
+            "p50_s": lat[int(0.5 * (n - 1))], "p99_s": lat[int(0.99 * (n - 1))]}
 
 
 def _client(url: str, n: int, conc: int, model_name: str, seed: int, kind: str = "kserve") -> dict:
@@ -134,18 +141,30 @@ def _levels(pred, model_name: str, new_tokens: int | None, levels=LEVELS, kind: 
         _client(srv.url, 4, 4, model_name, 99, kind)  # warm: graphs, allocator
         _engine(pred, 4, 4, seed=98, kind=kind)
         for conc, n in levels:
-            # warm this level's batch buckets first (decode-graph captures), so neither timed pass pays them
+            # warm this level's batch buckets first (decode-graph captures), so no timed pass pays them
             _engine(pred, 2 * conc, conc, seed=1000 + conc, kind=kind)
+            # interleaved engine / HTTP / engine passes over the same request stream: the HTTP pass is
+            # compared with the engine passes on either side of it (drift and box noise show up as the
+            # spread between the two engine passes), latency as mean +- sample stdev as load_test.py
+            # reports it (tensorizer-isvc/benchmark/load_test.py:155-180)
+            e1 = _engine(pred, n, conc, seed=conc, kind=kind)
             h = _client(srv.url, n, conc, model_name, conc, kind)
-            e = _engine(pred, n, conc, seed=conc, kind=kind)
+            e2 = _engine(pred, n, conc, seed=conc, kind=kind)
+            e = _lat_stats(e1["latencies"] + e2["latencies"])
+            e_rps = (e1["throughput_rps"] + e2["throughput_rps"]) / 2
             rec = {"concurrency": conc, "requests": n, "successes": h["successes"],
                    "http_rps": round(h["throughput_rps"], 3),
                    **({"http_tokens_per_s": round(h["goodput_rps"] * new_tokens, 1)} if new_tokens else {}),
+                   "http_mean_s": round(h.get("mean_latency_s", float("nan")), 4),
+                   "http_stdev_s": round(h.get("stdev_latency_s", float("nan")), 4),
                    "http_p50_s": round(h.get("p50_s", float("nan")), 4),
                    "http_p99_s": round(h.get("p99_s", float("nan")), 4),
-                   "engine_rps": round(e["throughput_rps"], 3),
+                   "engine_rps": round(e_rps, 3),
+                   "engine_rps_passes": [round(e1["throughput_rps"], 3), round(e2["throughput_rps"], 3)],
+                   "engine_mean_s": round(e["mean_latency_s"], 4), "engine_stdev_s": round(e["stdev_latency_s"], 4),
                    "engine_p50_s": round(e["p50_s"], 4), "engine_p99_s": round(e["p99_s"], 4)}
-            rec["http_overhead_p50_ms"] = round((rec["http_p50_s"] - rec["engine_p50_s"]) * 1e3, 2)
+            rec["http_overhead_mean_ms"] = round((rec["http_mean_s"] - rec["engine_mean_s"]) * 1e3, 2)
+            rec["http_rps_loss"] = round(1.0 - rec["http_rps"] / max(e_rps, 1e-9), 4)
             out.append(rec)
     finally:
         srv.close()

@@ -63,34 +63,72 @@ class _SendfileRange(http.server.BaseHTTPRequestHandler):
                 off += sent
 
 
-def run_weight_load(model="gpt-j-6b", directory="/tmp", threads=8, sources=("cold", "repeat")):
-    """bench.py's ``secondary_weight_load``: write a random-init fp16 model as
-    ``.tensors``, then time no-init construction + native O_DIRECT stream into
-    HBM. Returns one record per source; the file is removed."""
-    from kubernetes_cloud_amd.io.hf import load_tensorized, serialize_causal_lm
+def _build(cfg, dev, tp):
+    if tp:  # rank 0's shard, random-init on the device (a 176B shard never touches host memory)
+        from kubernetes_cloud_amd.parallel.tensor_parallel import load_tp_model
+        return load_tp_model(cfg, 0, tp, None, device=dev, dtype=torch.float16, random_init=True)
     from kubernetes_cloud_amd.models.causal_lm import build_model
+    return build_model(cfg, device=dev, dtype=torch.float16, seed=0)
+
+
+def _load(cfg, uri, dev, tp, threads):
+    """-> (model, stream stats): no-init construction + native stream into preallocated HBM."""
+    from kubernetes_cloud_amd.io.hf import load_tensorized
+    if not tp:
+        return load_tensorized(uri, None, device=dev, dtype=torch.float16, threads=threads)
+    from kubernetes_cloud_amd.io.tensors import load_into_module
+    from kubernetes_cloud_amd.models.causal_lm import CausalLM
+    from kubernetes_cloud_amd.parallel.tensor_parallel import tp_convert_
+    with torch.device("meta"):
+        model = CausalLM(cfg)
+    tp_convert_(model, 0, tp, None)
+    model = model.to(torch.float16).to_empty(device=dev)
+    return model, load_into_module(model, uri, device=dev, threads=threads)
+
+
+def run_weight_load(model="gpt-j-6b", directory="/tmp", threads=8, sources=("cold", "repeat"), tp=0, layers=0):
+    """bench.py's ``secondary_weight_load``: write a random-init fp16 model (or rank 0's TP=``tp``
+    shard; ``layers`` > 0: the first layers only, the record extrapolates the full shard) as
+    ``.tensors``, read the file raw with O_DIRECT (the storage ceiling, no device copy), then time
+    no-init construction + native O_DIRECT stream into HBM. Returns one record per source; the file
+    is removed."""
+    from kubernetes_cloud_amd.io.hf import serialize_causal_lm
+    from kubernetes_cloud_amd.io.native import storage_read_rate
     from kubernetes_cloud_amd.models.config import preset
     dev = torch.device("cuda", torch.cuda.current_device())
     cfg = preset(model)
-    path = os.path.join(directory, f"kca_bench_{model}_{os.getpid()}.tensors")
-    m = build_model(cfg, device=dev, dtype=torch.float16, seed=0)
+    full_layers = cfg.n_layers
+    if layers:
+        cfg.n_layers = layers
+    path = os.path.join(directory, f"kca_bench_{model}{f'_tp{tp}r0' if tp else ''}_{os.getpid()}.tensors")
+    m = _build(cfg, dev, tp)
     ref = {k: v.float().abs().sum().item() for k, v in list(m.state_dict().items())[:3]}
+    layer_bytes = sum(p.numel() * p.element_size() for p in m.h[0].parameters())
+    total = sum(p.numel() * p.element_size() for p in m.parameters())
     serialize_causal_lm(m, path)
     del m
     torch.cuda.empty_cache()
     out = []
     try:
+        raw = storage_read_rate(path, threads=threads)  # O_DIRECT: nothing of it stays in the page cache
         for src in sources:
             torch.cuda.synchronize()
             t = time.perf_counter()
-            model_, st = load_tensorized(path, None, device=dev, dtype=torch.float16, threads=threads)
+            model_, st = _load(cfg, path, dev, tp, threads)
             torch.cuda.synchronize()
             ready = time.perf_counter() - t
             got = {k: v.float().abs().sum().item() for k, v in list(model_.state_dict().items())[:3]}
             assert all(abs(got[k] - ref[k]) <= 1e-3 * max(1.0, ref[k]) for k in ref), (got, ref)
-            out.append({"metric": "weight load", "source": f"file O_DIRECT ({src})", "model": model, "dtype": "fp16",
-                        "bytes": int(st["bytes"]), "gbps": round(st["gbps"], 2),
-                        "seconds_to_ready": round(ready, 3), "threads": threads, "data": "random-init weights"})
+            rec = {"metric": "weight load", "source": f"file O_DIRECT ({src})",
+                   "model": model + (f" TP={tp} rank-0 shard" if tp else ""), "dtype": "fp16",
+                   "bytes": int(st["bytes"]), "gbps": round(st["gbps"], 2), "seconds_to_ready": round(ready, 3),
+                   "storage_gbps": round(raw["gbps"], 2), "of_storage": round(st["gbps"] / max(raw["gbps"], 1e-9), 3),
+                   "threads": threads, "data": "random-init weights"}
+            if layers and layers < full_layers:  # the whole shard at the measured rate
+                full = total + (full_layers - layers) * layer_bytes
+                rec.update(layers=f"{layers} of {full_layers}", full_bytes=int(full),
+                           full_seconds_at_rate=round(full / (st["gbps"] * 1e9), 2))
+            out.append(rec)
             del model_
             torch.cuda.empty_cache()
     finally:

@@ -192,3 +192,56 @@ KCA_HOST_API int kca_stream_to_device(const char* path, int n, const int64_t* of
   }
   return err.load();
 }
+
+// Raw storage read rate of `path` (BASELINE.md weight load: "saturate the storage read rate"): the
+// whole file read with O_DIRECT (page cache bypassed) by n_threads into per-thread aligned host
+// buffers, nothing copied to the device -- the ceiling kca_stream_to_device's pipeline can reach.
+// stats[0] = bytes, stats[1] = seconds.
+KCA_HOST_API int kca_read_bandwidth(const char* path, int n_threads, int64_t chunk, int use_odirect,
+                                    double* stats) {
+  if (chunk <= 0) chunk = 64 << 20;
+  chunk = (chunk + kAlign - 1) / kAlign * kAlign;
+  int fd = ::open(path, O_RDONLY | (use_odirect ? O_DIRECT : 0));
+  if (fd < 0) return 1;
+  const off_t size = ::lseek(fd, 0, SEEK_END);
+  if (size <= 0) {
+    ::close(fd);
+    return 1;
+  }
+  n_threads = std::max(1, std::min(n_threads, 64));
+  const int64_t n_chunks = (size + chunk - 1) / chunk;
+  std::atomic<int64_t> next{0};
+  std::atomic<int> err{0};
+  double t0 = now_s();
+  auto work = [&]() {
+    void* buf = nullptr;
+    if (posix_memalign(&buf, kAlign, (size_t)chunk) != 0) {
+      err = 4;
+      return;
+    }
+    for (;;) {
+      const int64_t i = next.fetch_add(1);
+      if (i >= n_chunks || err.load()) break;
+      const int64_t off = i * chunk, len = std::min<int64_t>(chunk, size - off);
+      const int64_t alen = (len + kAlign - 1) / kAlign * kAlign;  // O_DIRECT: whole blocks (EOF short)
+      int64_t done = 0;
+      while (done < len) {
+        const ssize_t r = ::pread(fd, (char*)buf + done, (size_t)(alen - done), (off_t)(off + done));
+        if (r < 0 && errno == EINTR) continue;
+        if (r <= 0) break;
+        done += r;
+      }
+      if (done < len) err = 2;
+    }
+    free(buf);
+  };
+  std::vector<std::thread> th;
+  for (int t = 0; t < n_threads; ++t) th.emplace_back(work);
+  for (auto& t : th) t.join();
+  ::close(fd);
+  if (stats) {
+    stats[0] = (double)size;
+    stats[1] = now_s() - t0;
+  }
+  return err.load();
+}

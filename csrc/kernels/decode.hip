@@ -1299,13 +1299,18 @@ __device__ void find_bin_desc(const float* hist, float target, float* sh_excl, i
 }
 
 // One workgroup per row. ws: fp32 scratch [B, V] (processed logits).
+// rows of the multi-workgroup sampler (sample_mwg_kernel): greedy, or top-k in [1, 64]
+constexpr int MWG_KMAX_ = 64;  // (= MWG_KMAX below)
+__device__ __forceinline__ bool mwg_row(float T, int k) { return !(T > 0.f) || (k >= 1 && k <= MWG_KMAX_); }
+
 __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(
     const void* __restrict__ logits, long long ld, int is_bf16, int V,
     const float* __restrict__ temperature, const int* __restrict__ top_k,
     const float* __restrict__ top_p, const float* __restrict__ rep_pen, uint8_t* __restrict__ seen,
     const int* __restrict__ slots, const int* __restrict__ ban_ids, int n_ban,
     const unsigned long long* __restrict__ seeds, long long step, float* __restrict__ ws,
-    long long* __restrict__ out_ids, float* __restrict__ out_lp, int* __restrict__ out_kept, int compact) {
+    long long* __restrict__ out_ids, float* __restrict__ out_lp, int* __restrict__ out_kept, int compact,
+    int skip_mwg) {
   __shared__ float hist[256];
   __shared__ float red[SAMPLE_THREADS / 64];
   __shared__ float sh_excl;
@@ -1316,6 +1321,8 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(
   __shared__ int c_i[SAMPLE_CMAX];
   __shared__ int iscan[SAMPLE_THREADS / 64];
   const int b = blockIdx.x, tid = threadIdx.x;
+  // rows the multi-workgroup sampler took (launched first): decided on the device, as sample_reg_kernel
+  if (skip_mwg && mwg_row(temperature ? temperature[b] : 1.f, top_k ? top_k[b] : 0)) return;
   const float T = temperature ? temperature[b] : 1.f;
   const float rp = rep_pen ? rep_pen[b] : 1.f;
   const int slot = slots ? slots[b] : b;
@@ -1576,8 +1583,6 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(
   }
 }
 
-constexpr int MWG_KMAX_ = 64;  // (= MWG_KMAX below)
-__device__ __forceinline__ bool mwg_row(float T, int k) { return !(T > 0.f) || (k >= 1 && k <= MWG_KMAX_); }
 
 // Register-resident sampler (bf16 logits, V <= RPT * 1024, GPT-J's 50400 at 128 per thread x 512 threads): the row is read
 // ONCE into registers (element i = u * 1024 + tid, value u of the thread) and every later pass -- max / normaliser, the top-k
@@ -2128,7 +2133,7 @@ KCA_API int kca_sample_stamps(unsigned long long* out, int reset) {
   } while (0)
 #endif
 
-template <int VPT>
+template <int VPT, int G = MWG_G, int CMAX = MWG_CMAX>
 __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
     const bf16_t* __restrict__ logits, long long ld, int V, int CS,
     const float* __restrict__ temperature, const int* __restrict__ top_k,
@@ -2142,10 +2147,10 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
   __shared__ int sel[2];
   __shared__ int iscan[MWG_NT / 64];
   __shared__ int sh_last;
-  __shared__ float Lv[MWG_G * MWG_CMAX];
-  __shared__ int Li[MWG_G * MWG_CMAX];
-  __shared__ float L2v[MWG_G * MWG_CMAX];  // the candidates after the per-wave narrowing
-  __shared__ int L2i[MWG_G * MWG_CMAX];
+  __shared__ float Lv[G * CMAX];
+  __shared__ int Li[G * CMAX];
+  __shared__ float L2v[G * CMAX];  // the candidates after the per-wave narrowing
+  __shared__ int L2i[G * CMAX];
   __shared__ __attribute__((aligned(16))) float hist[48];
   __shared__ float Kv[64];
   __shared__ int Kj[64];
@@ -2161,8 +2166,8 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
   const uint8_t* sn = seen ? seen + (long long)slot * V : nullptr;
   const float inv_t = (greedy || T == 1.f) ? 1.f : 1.f / T;
   const bool pen = rp != 1.f && sn;
-  float* part = ws + (long long)b * MWG_G * (MWG_PART + 2 * MWG_CMAX);  // [G][PART + 2*CMAX]
-  float* mine = part + g * (MWG_PART + 2 * MWG_CMAX);
+  float* part = ws + (long long)b * G * (MWG_PART + 2 * CMAX);  // [G][PART + 2*CMAX]
+  float* mine = part + g * (MWG_PART + 2 * CMAX);
 
   // ---- this workgroup's chunk [c0, c1): thread t owns the contiguous run [c0 + t*VPT, +VPT)
   const int c0 = g * CS, c1 = min(V, c0 + CS);
@@ -2288,17 +2293,17 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
       }
     };
     scan();
-    if (tot > MWG_CMAX) {  // uniform: every thread read the same iscan
+    if (tot > CMAX) {  // uniform: every thread read the same iscan
       tg = block_kth_key<VPT, MWG_NT / 64>(k, xk, xo, cnt16);
       scan();
     }
-    count = min(tot, MWG_CMAX);  // (> CMAX only with massive ties at t_g: the first CMAX by index stay)
+    count = min(tot, CMAX);  // (> CMAX only with massive ties at t_g: the first CMAX by index stay)
 #pragma unroll
     for (int e = 0; e < VPT; ++e) {
       if (xo[e] && xk[e] >= tg) {
-        if (off < MWG_CMAX) {
+        if (off < CMAX) {
           mine[MWG_PART + off] = x[e];
-          reinterpret_cast<int*>(mine)[MWG_PART + MWG_CMAX + off] = e0 + e;
+          reinterpret_cast<int*>(mine)[MWG_PART + CMAX + off] = e0 + e;
         }
         ++off;
       }
@@ -2320,7 +2325,7 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned prev = __hip_atomic_fetch_add(&cnt[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    sh_last = prev == MWG_G - 1;
+    sh_last = prev == G - 1;
     if (sh_last) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2335,12 +2340,12 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
   // ================= merge (the last workgroup of the row)
   if (tid == 0) cnt[b] = 0;  // re-armed for the next launch
   float M = -INFINITY;
-  for (int q = 0; q < MWG_G; ++q) M = fmaxf(M, part[q * (MWG_PART + 2 * MWG_CMAX)]);
+  for (int q = 0; q < G; ++q) M = fmaxf(M, part[q * (MWG_PART + 2 * CMAX)]);
   float Z = 0.f;
   int best = 0x7fffffff;
   uint32_t T0 = 0;
-  for (int q = 0; q < MWG_G; ++q) {
-    const float* pq = part + q * (MWG_PART + 2 * MWG_CMAX);
+  for (int q = 0; q < G; ++q) {
+    const float* pq = part + q * (MWG_PART + 2 * CMAX);
     if (pq[0] != -INFINITY) Z += pq[1] * __expf(pq[0] - M);
     const unsigned* pu = reinterpret_cast<const unsigned*>(pq);
     if (pq[0] == M && best == 0x7fffffff) best = (int)pu[4];  // first chunk holding the max
@@ -2359,15 +2364,15 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
   }
   // candidates >= T0, compacted into LDS in (chunk, position) = index order: thread t reads slots
   // [8t, 8t + 8) of one chunk's list (no search, independent loads), a block scan places them
-  constexpr int SPT = MWG_G * MWG_CMAX / MWG_NT;
-  static_assert(MWG_CMAX % SPT == 0, "a thread's slots within one chunk");
+  constexpr int SPT = G * CMAX / MWG_NT;
+  static_assert(CMAX % SPT == 0, "a thread's slots within one chunk");
   int nv;
   {
     float sv[SPT];
     int si[SPT];
     int c = 0;
-    const int j0 = tid * SPT, q = j0 / MWG_CMAX, p0 = j0 % MWG_CMAX;
-    const float* pq = part + q * (MWG_PART + 2 * MWG_CMAX);
+    const int j0 = tid * SPT, q = j0 / CMAX, p0 = j0 % CMAX;
+    const float* pq = part + q * (MWG_PART + 2 * CMAX);
     const int cq = reinterpret_cast<const int*>(pq)[3];
 #pragma unroll
     for (int e = 0; e < SPT; ++e) {
@@ -2377,7 +2382,7 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
         const float v = pq[MWG_PART + p0 + e];
         if (fkey(v) >= T0) {
           sv[e] = v;
-          si[e] = reinterpret_cast<const int*>(pq)[MWG_PART + MWG_CMAX + p0 + e];
+          si[e] = reinterpret_cast<const int*>(pq)[MWG_PART + CMAX + p0 + e];
           ++c;
         }
       }
@@ -2688,10 +2693,18 @@ KCA_API int kca_sample_logits(const void* logits, long long ld, int is_bf16, int
     const char* e = getenv("KCA_SAMPLE_MWG");
     mwg = !(e && e[0] == '0');
   }
-  const int CS = (V + MWG_G - 1) / MWG_G, vpt = (CS + MWG_NT - 1) / MWG_NT;
-  const bool use_mwg = mwg && cnt && is_bf16 && V <= 50 * 1024 && vpt <= 16 &&
-                       (long long)MWG_G * (MWG_PART + 2 * MWG_CMAX) <= V;  // (the rest: sample_reg_kernel)
-  if (use_mwg) {
+  // the large-vocabulary form (BLOOM's 250,880: 32 chunks of 7,840, 64 candidates each) runs its
+  // greedy and top-k rows here too; its top-p-only rows take the one-workgroup memory-pass kernel
+  const bool big = V > 50 * 1024;
+  const int G = big ? 32 : MWG_G;
+  const int CS = (V + G - 1) / G, vpt = (CS + MWG_NT - 1) / MWG_NT;
+  const bool use_mwg = mwg && cnt && is_bf16 && (big ? vpt <= 32 : vpt <= 16) &&
+                       (long long)G * (MWG_PART + 2 * (big ? 64 : MWG_CMAX)) <= V;  // (the rest: sample_reg_kernel)
+  if (use_mwg && big) {
+    hipLaunchKernelGGL((sample_mwg_kernel<32, 32, 64>), dim3(32, B), dim3(MWG_NT), 0, stream, (const bf16_t*)logits,
+                       ld, V, CS, temperature, top_k, top_p, rep_pen, (uint8_t*)seen, slots, ban_ids, n_ban, seeds,
+                       step, ws, cnt, out_ids, out_lp, out_kept);
+  } else if (use_mwg) {
 #define KCA_SAMPLE_MWG_LAUNCH(P)                                                                           \
   hipLaunchKernelGGL((sample_mwg_kernel<P>), dim3(MWG_G, B), dim3(MWG_NT), 0, stream, (const bf16_t*)logits, ld, \
                      V, CS, temperature, top_k, top_p, rep_pen, (uint8_t*)seen, slots, ban_ids, n_ban, seeds,  \
@@ -2725,6 +2738,6 @@ KCA_API int kca_sample_logits(const void* logits, long long ld, int is_bf16, int
   }
   hipLaunchKernelGGL(sample_kernel, dim3(B), dim3(SAMPLE_THREADS), 0, stream, logits, ld, is_bf16,
                      V, temperature, top_k, top_p, rep_pen, (uint8_t*)seen, slots, ban_ids, n_ban,
-                     seeds, step, ws, out_ids, out_lp, out_kept, compact);
-  return 0;
+                     seeds, step, ws, out_ids, out_lp, out_kept, compact, (int)use_mwg);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
 }

@@ -18,6 +18,7 @@ P, I, LL, F, D = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_floa
 _SIGS = {
     "kca_read_ranges": (I, [ctypes.c_char_p, I, P, P, P, I, LL, P]),
     "kca_stream_to_device": (I, [ctypes.c_char_p, I, P, P, P, I, I, LL, I, P]),
+    "kca_read_bandwidth": (I, [ctypes.c_char_p, I, LL, I, P]),
     "kca_http_get_range": (I, [ctypes.c_char_p, I, I, I, ctypes.c_char_p, ctypes.c_char_p, LL, LL, P, P, D]),
     "kca_http_stream": (I, [ctypes.c_char_p, I, I, I, ctypes.c_char_p, ctypes.c_char_p, I, P, P, P, I, I, LL, D,
                             P]),
@@ -68,3 +69,14 @@ def available() -> bool:
         return True
     except Exception:
         return False
+
+
+def storage_read_rate(path: str, threads: int = 8, chunk: int = 64 << 20, odirect: bool = True) -> dict:
+    """Raw read rate of ``path`` into host memory (O_DIRECT: the page cache bypassed), no device copy:
+    the storage ceiling of the weight streamer. -> {"bytes", "seconds", "gbps"}."""
+    lib = load()
+    st = (ctypes.c_double * 2)()
+    rc = lib.kca_read_bandwidth(path.encode(), int(threads), int(chunk), int(odirect), st)
+    if rc != 0:
+        raise OSError(f"kca_read_bandwidth({path}) failed: {rc}")
+    return {"bytes": int(st[0]), "seconds": st[1], "gbps": st[0] / max(st[1], 1e-9) / 1e9}

@@ -714,6 +714,14 @@ class TrainEngine:
             adj -= w * g[lo:hi].float().pow(2).sum()
         return adj
 
+    def grad_norm(self) -> float:
+        """Global L2 norm of the last step's (averaged, unscaled, pre-clip) gradient -- the value the
+        clip used; equal across data-parallel layouts of the same global batch (one host sync)."""
+        if getattr(self, "_gn", None) is None:
+            return float("nan")
+        sumsq, inv = self._gn
+        return float(sumsq.float().sqrt() * inv)
+
     def step(self, lr: float | None = None) -> None:
         if not self.part_grads:
             # grads of params that got no gradient this step are zero
@@ -742,6 +750,7 @@ class TrainEngine:
             dist.all_reduce(sumsq, group=self.group)
         if self._norm_group is not None:
             dist.all_reduce(sumsq, group=self._norm_group)
+        self._gn = (sumsq.detach().clone(), inv)
         self.opt.set_clip(sumsq, self.max_grad_norm, inv)
         self.opt.step(lr, use_clip=True)
         deferred = False

