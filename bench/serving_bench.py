@@ -233,7 +233,7 @@ def run_bloom_slice(layers: int = 8, levels=LEVELS, overrides: dict | None = Non
             "data": "random-init weights, loadgen prompts"}
 
 
-SD_LEVELS = ((1, 4), (4, 8), (8, 16))
+SD_LEVELS = ((1, 32), (4, 32), (8, 32))  # >= 32 requests per level
 
 
 def run_sd(levels=SD_LEVELS, resolution: int = 512, steps: int = 50) -> dict:
@@ -268,7 +268,12 @@ def run_sd(levels=SD_LEVELS, resolution: int = 512, steps: int = 50) -> dict:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--which", default="gptj,bloom_slice,sd")
+    ap.add_argument("--switch-interval", type=float, default=0.0,
+                    help="sys.setswitchinterval for this run (A/B of the GIL hand-off; 0 keeps the server's)")
     a = ap.parse_args()
+    if a.switch_interval > 0:
+        from kubernetes_cloud_amd.serving import server as _srv
+        _srv.GIL_SWITCH_S = a.switch_interval
     for w in a.which.split(","):
         r = run_gptj() if w == "gptj" else (run_sd() if w == "sd" else run_bloom_slice())
         print(json.dumps(r), flush=True)

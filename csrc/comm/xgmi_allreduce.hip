@@ -35,6 +35,7 @@
 #include <cstring>
 
 #include "../kernels/common.h"
+#include "../kernels/decode_tail.h"
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -241,6 +242,43 @@ __global__ __launch_bounds__(512) void ag_kernel(ARPeers peers, ARCtl* ctl, int 
   ar_end(ctl, call);
 }
 
+// ------------------------------------------------- one-shot + residual + LayerNorm (TP decode)
+// Closes a row-parallel projection of the batch-1 decode layer (BLOOM TP=8: the out-projection and
+// fc_out, N = 14336): every rank stages its partial y, one sync round, each workgroup sums its slice
+// over the W stagings in fp32 and publishes it (st_pub) -- then the decode tail's last arriver adds
+// bias + residual, rounds h' and writes LN(h') for the next projection (dual_ln_arrive_tail). The
+// separate bias add and LayerNorm launches of a plain all-reduce disappear from every layer. 256
+// threads (the tail's shape); the call sequence / parity protocol is the one-shot kernel's.
+template <int W, int PER>
+__global__ __launch_bounds__(256) void ar_res_ln_kernel(ARPeers peers, ARCtl* ctl, int rank,
+                                                        const bf16_t* __restrict__ in, long long n8,
+                                                        long long spin_limit, DualLn a) {
+  const int b = blockIdx.x, nb = gridDim.x, tid = threadIdx.x;
+  const uint32_t call = ar_begin(ctl);
+  const int par = call & 1;
+  const long long per = (n8 + nb - 1) / nb;
+  const long long lo = b * per, hi = min(n8, lo + per);
+  uint4* mine = reinterpret_cast<uint4*>(peers.stage[par][rank]);
+  for (long long i = lo + tid; i < hi; i += blockDim.x) mine[i] = reinterpret_cast<const uint4*>(in)[i];
+  const bool ok = ar_sync<W>(peers, ctl, rank, 0, call, spin_limit);
+  for (long long i = lo + tid; i < hi; i += blockDim.x) {
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int r = 0; r < W; ++r) {
+      const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(peers.stage[par][r]) + i);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[2 * j] += __uint_as_float(v[j] << 16);
+        acc[2 * j + 1] += __uint_as_float(v[j] & 0xffff0000u);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) st_pub(a.ypart + i * 8 + j, ok ? acc[j] : __int_as_float(0x7fc00000));
+  }
+  ar_end(ctl, call);
+  dual_ln_arrive_tail<PER>(a);
+}
+
 KCA_API int kca_ar_signal_bytes() { return (int)sizeof(ARSignal); }
 KCA_API int kca_ar_max_blocks() { return AR_MAX_BLOCKS; }
 
@@ -318,4 +356,49 @@ KCA_API int kca_ar_error(const void* ctl, int* err) {
   if (hipMemcpy(&e, (const char*)ctl + offsetof(ARCtl, error), 4, hipMemcpyDeviceToHost) != hipSuccess) return 1;
   *err = (int)e;
   return 0;
+}
+
+// Row-parallel projection close for batch-1 decode: all-reduce `in` (bf16 [N], this rank's partial),
+// then h_out = bf16(h + sum + bias), xn_out = LN(h_out) (gamma / beta / eps; gamma2 -> xn2_out: a
+// second LayerNorm of the same h_out). ypart: >= N fp32 local words; cnt: 32 * 65 zero-initialised
+// arrival counters (re-armed by every call). N % 8 == 0, N <= 16384, 2N bytes <= the staging size.
+KCA_API int kca_ar_res_ln(void* const* stage0, void* const* stage1, void* const* sig, void* ctl, int rank, int world,
+                          const void* in, int N, int blocks, long long spin_limit, const void* bias, const void* h,
+                          void* h_out, const void* gamma, const void* beta, float eps, void* xn_out,
+                          const void* gamma2, const void* beta2, void* xn2_out, float* ypart, unsigned int* cnt,
+                          hipStream_t stream) {
+  if (world < 1 || world > AR_MAX_RANKS || rank < 0 || rank >= world || N % 8 || N <= 0 || N > 16384 || blocks < 1 ||
+      blocks > AR_MAX_BLOCKS || !ypart || !cnt || !h || !h_out || !gamma || !xn_out || (xn2_out && !gamma2))
+    return 1;
+  if (((uintptr_t)in | (uintptr_t)h | (uintptr_t)h_out | (uintptr_t)gamma | (uintptr_t)beta | (uintptr_t)xn_out |
+       (uintptr_t)ypart | (uintptr_t)gamma2 | (uintptr_t)beta2 | (uintptr_t)xn2_out) & 15)
+    return 2;
+  ARPeers p{};
+  for (int r = 0; r < world; ++r) {
+    p.stage[0][r] = (bf16_t*)stage0[r];
+    p.stage[1][r] = (bf16_t*)stage1[r];
+    p.sig[r] = (ARSignal*)sig[r];
+  }
+  const DualLn a{nullptr, nullptr, nullptr, nullptr, (const bf16_t*)bias, ypart, cnt, (const bf16_t*)h,
+                 (bf16_t*)h_out, (const bf16_t*)gamma, (const bf16_t*)beta, eps, (bf16_t*)xn_out,
+                 (const bf16_t*)gamma2, (const bf16_t*)beta2, (bf16_t*)xn2_out, N, 0, 0};
+  ARCtl* c = (ARCtl*)ctl;
+  const long long n8 = N / 8;
+  switch (world) {
+#define KCA_AR_LN_CASE(WW)                                                                                      \
+  case WW:                                                                                                      \
+    if (N <= 8192)                                                                                              \
+      hipLaunchKernelGGL((ar_res_ln_kernel<WW, 4>), dim3(blocks), dim3(256), 0, stream, p, c, rank,             \
+                         (const bf16_t*)in, n8, spin_limit, a);                                                 \
+    else                                                                                                        \
+      hipLaunchKernelGGL((ar_res_ln_kernel<WW, 8>), dim3(blocks), dim3(256), 0, stream, p, c, rank,             \
+                         (const bf16_t*)in, n8, spin_limit, a);                                                 \
+    break;
+    KCA_AR_LN_CASE(1) KCA_AR_LN_CASE(2) KCA_AR_LN_CASE(3) KCA_AR_LN_CASE(4) KCA_AR_LN_CASE(5) KCA_AR_LN_CASE(6)
+    KCA_AR_LN_CASE(7) KCA_AR_LN_CASE(8)
+#undef KCA_AR_LN_CASE
+    default:
+      return 3;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : 4;
 }

@@ -22,9 +22,11 @@
 // [page][kv_head][ps][D] (ps = 1 << ps_shift tokens) and token t of sequence
 // `seq` lives in page tbl[seq * tbl_stride + (t >> ps_shift)] -- requests hold
 // only the pages they use, and beams share their prefix pages.
+#include <algorithm>
 #include <cstdio>
 #include <type_traits>
 
+#include "decode_tail.h"  // DualLn + the last-arriver residual / LayerNorm tail
 #include "gemv_m1.h"  // gemv_m1_accum / _finish for the fused decode-layer kernels
 
 // element offset of token t of sequence `seq` (paged or contiguous)
@@ -149,14 +151,19 @@ struct DecodeParams {
   // sin_t hold row b's RoPE angles at index b (not the position table); bit 1 -- tbl holds row b's
   // page ids at row b (not the slot's). Neither then waits for the length or the slot to arrive.
   int by_row;
+  // 1: the attention output is consumed inside the same launch (decode_attn_out_ln_kernel): stored
+  // write-through (agent scope), so a drain + counter add publishes it without a release fence
+  int pub_out;
 };
 
-// Partials that another workgroup of the same launch combines: write-through (sc1) stores, so a
-// drain (vmcnt(0)) + barrier + counter add publishes them across XCDs without a release fence
-// (cdna_hip_programming.md Guideline 16, recipe R1).
-__device__ __forceinline__ void st_pub(float* a, float v) {
-  __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ void store_out(const DecodeParams& p, long long i, float v) {
+  if (p.pub_out)
+    __hip_atomic_store(reinterpret_cast<unsigned short*>(p.out + i), f2bf(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  else
+    p.out[i] = f2bf(v);
 }
+
 
 // diagnostic stamps (bench/decode_attn_bench.py --stamps): 8 per workgroup, 100 MHz clock
 static unsigned long long* g_decode_stamps = nullptr;
@@ -305,7 +312,7 @@ __device__ void fanin_combine(const DecodeParams& p, int b, int hk, int nsplit) 
         const float ov = o[(long long)s * D + tid];
         acc = wsp[s] > 0.f ? fmaf(wsp[s], ov, acc) : acc;
       }
-      p.out[b * p.o_bs + (hk * G + g) * (long long)D + tid] = f2bf(acc * inv);
+      store_out(p, b * p.o_bs + (hk * G + g) * (long long)D + tid, acc * inv);
     }
     __syncthreads();  // wsp / red reused by the next head
   }
@@ -623,7 +630,7 @@ __device__ __forceinline__ void decode_attn_body(const DecodeParams& p, const in
       O = fmaf(w, gacc[(r * G + g) * D + d], O);
     }
     if (nsplit == 1) {
-      p.out[b * p.o_bs + (long long)(hk * G + g) * D + d] = f2bf(Ls > 0.f ? O / Ls : 0.f);
+      store_out(p, b * p.o_bs + (long long)(hk * G + g) * D + d, Ls > 0.f ? O / Ls : 0.f);
     } else {
       st_pub(&p.ws_o[((bh0 + g) * nsplit + split) * D + d], O);
       if (d == 0) {
@@ -759,7 +766,7 @@ __device__ __forceinline__ void decode_attn_body(const DecodeParams& p, const in
       const float s = red[(0 * G + g) * D + d] + red[(1 * G + g) * D + d] +
                       red[(2 * G + g) * D + d] + red[(3 * G + g) * D + d];
       if (nsplit == 1) {
-        p.out[b * p.o_bs + (long long)(hk * G + g) * D + d] = f2bf(lg[g] > 0.f ? s / lg[g] : 0.f);
+        store_out(p, b * p.o_bs + (long long)(hk * G + g) * D + d, lg[g] > 0.f ? s / lg[g] : 0.f);
       } else {
         st_pub(&p.ws_o[((bh0 + g) * nsplit + split) * D + d], s);
       }
@@ -819,133 +826,35 @@ __global__ __launch_bounds__(256) void decode_attn_gemv_kernel(DecodeParams p, i
   DSTAMP(7);
 }
 
-constexpr int kDualSub = 64;  // sub-counters of gemv_dual_ln_kernel's arrival (cnt: 32 * (1 + 64) uints)
-
-struct DualLn {
-  const bf16_t* x1;    // [K1] (attention output)
-  const bf16_t* w1;    // [N, K1]
-  const bf16_t* x2;    // [K2] (GELU(fc_in)); nullable: one GEMV (sequential-residual layers)
-  const bf16_t* w2;    // [N, K2]
-  const bf16_t* bias;  // [N] (nullable)
-  float* ypart;        // [N] fp32 row results (write-through: the finishing workgroup reads them)
-  unsigned int* cnt;   // arrival counters, zero before the first launch, re-armed by the last workgroup
-  const bf16_t* h;     // [N] residual stream in
-  bf16_t* h_out;       // [N] h + y (bf16)
-  const bf16_t* gamma; // next LayerNorm
-  const bf16_t* beta;
-  float eps;
-  bf16_t* xn_out;      // [N] LN(h + y)
-  const bf16_t* gamma2;  // nullable: a second LayerNorm of the same h + y (GPT-NeoX's ln_2: parallel
-  const bf16_t* beta2;   // residual with two norms), sharing the statistics
-  bf16_t* xn2_out;
-  int N, K1, K2;
-};
-
 // Workgroup g: R rows over W1 . x1 (+ W2 . x2) -- one weight stream per row group, the shape the QKV
 // GEMV reaches ~6 TB/s with; its R results go to ypart. The last workgroup to arrive (two-level
 // counter) adds bias + residual, rounds h' to bf16 and normalises it for the next projection(s):
 // the out-projection / fc_out, the residual add and the next LayerNorm in one launch, no LayerNorm
-// launch of its own. PER: h' register slices of 2048 columns (N <= 256 * 8 * PER).
+// launch of its own.
 template <int R, int PER>
 __global__ __launch_bounds__(256) void gemv_dual_ln_kernel(DualLn a) {
   __shared__ float part[4][R];
-  __shared__ float red[16];
-  __shared__ int s_last;
   const int tid = threadIdx.x;
-  const int n0 = blockIdx.x * R;
-  float acc[R];
+  // row groups g = blockIdx.x, + gridDim.x, ...: the grid is at most one residency round, so a
+  // workgroup's drain + arrival (~3 us of latency it holds its slot for) is paid once per workgroup,
+  // not once per 4-row group (no workgroup waits on another: dispatch order does not matter)
+  const int ngrp = (a.N + R - 1) / R;
+  for (int grp = blockIdx.x; grp < ngrp; grp += gridDim.x) {
+    const int n0 = grp * R;
+    float acc[R];
 #pragma unroll
-  for (int r = 0; r < R; ++r) acc[r] = 0.f;
-  gemv_m1_accum<R>(a.x1, a.w1, a.N, a.K1, n0, acc);
-  if (a.x2) gemv_m1_accum<R>(a.x2, a.w2, a.N, a.K2, n0, acc);
-  const float v = gemv_m1_finish<R>(acc, part, nullptr, n0, a.N, 0);
-  if (tid < R && n0 + tid < a.N) st_pub(&a.ypart[n0 + tid], v);
-  // publish (cdna_hip_programming.md Guideline 16, R1): write-through stores drained, barrier, one
-  // agent-scope arrival; the last workgroup re-arms the counter and acquires
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  // two-level arrival: thousands of workgroups adding to ONE address serialise at the memory side
-  // (~7 ns each: 5120 arrivals were +38 us per layer), so workgroup b counts into sub-counter b % 64
-  // (128 B apart) and each sub-counter's last arrival counts into the top one (cnt[0])
-  if (tid == 0) {
-    constexpr int NSUB = kDualSub;
-    const int G = gridDim.x, sub = blockIdx.x % NSUB;
-    const int nsub = G < NSUB ? G : NSUB;
-    const unsigned members = (unsigned)((G - sub + NSUB - 1) / NSUB);
-    unsigned* sc = a.cnt + 32 * (1 + sub);
-    int last = 0;
-    if (__hip_atomic_fetch_add(sc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == members - 1) {
-      __hip_atomic_store(sc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
-      last = __hip_atomic_fetch_add(a.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)nsub - 1;
-    }
-    if (last) {
-      __hip_atomic_store(a.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    s_last = last;
-  }
-  __syncthreads();
-  if (!s_last) return;
-  // h' = bf16(h + y + b), LN(h') -- the ln_rows_kernel math (statistics over the bf16-rounded sum)
-  float hv[PER][8];
-  float s = 0.f;
-#pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int k = (i * 256 + tid) * 8;
-    if (k < a.N) {
-      float y8[8], b8[8];
-      load8f(a.ypart + k, y8);
-      if (a.bias) {
-        load8(a.bias + k, b8);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) y8[j] += b8[j];
-      }
-      load8(a.h + k, hv[i]);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        hv[i][j] = bf2f(f2bf(hv[i][j] + y8[j]));
-        s += hv[i][j];
-      }
-      store8(a.h_out + k, hv[i]);
+    for (int r = 0; r < R; ++r) acc[r] = 0.f;
+    if (a.x2 && a.K1 % 2048 == 0) {
+      gemv_m1_accum2<R>(a.x1, a.w1, a.K1, a.x2, a.w2, a.K2, a.N, n0, acc);
     } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) hv[i][j] = 0.f;
+      gemv_m1_accum<R>(a.x1, a.w1, a.N, a.K1, n0, acc);
+      if (a.x2) gemv_m1_accum<R>(a.x2, a.w2, a.N, a.K2, n0, acc);
     }
+    const float v = gemv_m1_finish<R>(acc, part, nullptr, n0, a.N, 0);
+    if (tid < R && n0 + tid < a.N) st_pub(&a.ypart[n0 + tid], v);
+    __syncthreads();  // part[] is rewritten by the next group
   }
-  const float mean = block_sum(s, red) / a.N;
-  float q = 0.f;
-#pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    if ((i * 256 + tid) * 8 >= a.N) continue;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) q += (hv[i][j] - mean) * (hv[i][j] - mean);
-  }
-  const float rstd = rsqrtf(block_sum(q, red + 8) / a.N + a.eps);
-#pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int k = (i * 256 + tid) * 8;
-    if (k >= a.N) continue;
-    float gm[8], bt[8], o[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) hv[i][j] = (hv[i][j] - mean) * rstd;
-    load8(a.gamma + k, gm);
-    if (a.beta) load8(a.beta + k, bt);
-    else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) bt[j] = 0.f;
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = hv[i][j] * gm[j] + bt[j];
-    store8(a.xn_out + k, o);
-    if (a.xn2_out) {
-      load8(a.gamma2 + k, gm);
-      if (a.beta2) load8(a.beta2 + k, bt);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = hv[i][j] * gm[j] + bt[j];
-      store8(a.xn2_out + k, o);
-    }
-  }
+  dual_ln_arrive_tail<PER>(a);
 }
 
 // One workgroup per (sequence, head): split maxima and weights in one
@@ -1190,10 +1099,11 @@ KCA_API int kca_decode_prep_attn_gemv(const void* qkv, long long ld, const void*
 // statistics). x2 / w2 nullable (K2 = 0: one GEMV -- a sequential-residual layer's out-projection or
 // fc_out). ypart: >= N fp32 words; cnt: 32 * (1 + kDualSub) zero-initialised unsigned counters
 // (re-armed by every launch).
+// rows: weight rows per workgroup (4 / 8 / 16; 0 = 4).
 KCA_API int kca_gemv_dual_ln(const void* x1, const void* w1, int K1, const void* x2, const void* w2, int K2,
                              const void* bias, float* ypart, unsigned int* cnt, const void* h, void* h_out,
                              const void* gamma, const void* beta, float eps, void* xn_out, const void* gamma2,
-                             const void* beta2, void* xn2_out, int N, hipStream_t stream) {
+                             const void* beta2, void* xn2_out, int N, int rows, hipStream_t stream) {
   if (N <= 0 || N % 8 || N > 16384 || K1 % 8 || K1 <= 0 || !ypart || !cnt || !gamma || !xn_out || !h || !h_out)
     return 1;
   if (x2 && (K2 <= 0 || K2 % 8 || !w2)) return 1;
@@ -1206,10 +1116,151 @@ KCA_API int kca_gemv_dual_ln(const void* x1, const void* w1, int K1, const void*
                  ypart, cnt, (const bf16_t*)h, (bf16_t*)h_out, (const bf16_t*)gamma, (const bf16_t*)beta, eps,
                  (bf16_t*)xn_out, (const bf16_t*)gamma2, (const bf16_t*)beta2, (bf16_t*)xn2_out,
                  N, K1, x2 ? K2 : 0};
-  const dim3 grid((N + 3) / 4);
-  if (N <= 8192) hipLaunchKernelGGL((gemv_dual_ln_kernel<4, 4>), grid, dim3(256), 0, stream, a);
-  else hipLaunchKernelGGL((gemv_dual_ln_kernel<4, 8>), grid, dim3(256), 0, stream, a);
+  if (rows <= 0) rows = 4;  // (8 / 16 rows measured slower at every shape: bench/gemv_dual_ln_bench.py)
+  if (rows != 4 && rows != 8 && rows != 16) return 1;
+  // at most one residency round (8 workgroups of 256 threads per CU); larger N loops row groups
+  static int cu_count[64] = {};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  int& cus = cu_count[dev & 63];
+  if (!cus && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+  const dim3 grid((unsigned)std::min((N + rows - 1) / rows, 8 * cus));
+  auto go = [&](auto rc) {
+    constexpr int R = decltype(rc)::value;
+    if (N <= 8192) hipLaunchKernelGGL((gemv_dual_ln_kernel<R, 4>), grid, dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL((gemv_dual_ln_kernel<R, 8>), grid, dim3(256), 0, stream, a);
+  };
+  if (rows == 4) go(std::integral_constant<int, 4>{});
+  else if (rows == 8) go(std::integral_constant<int, 8>{});
+  else go(std::integral_constant<int, 16>{});
   return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// Sequential-residual decode layer (batch 1: BLOOM, GPT-2, GPT-Neo), attention -> out-projection ->
+// residual + ln_2 as ONE launch. Workgroups [0, n_attn) run the RoPE + KV append + split-K
+// attention (their output stored write-through, pub_out) and count themselves on `done`; then EVERY
+// workgroup streams out-projection row groups, the first group's weights requested before it waits
+// for done == n_attn -- the attention chain runs under the first weight loads instead of in front
+// of a kernel boundary. The grid never exceeds one residency round (kca_decode_attn_out_ln sizes it
+// from the occupancy API with a margin), so the waiting workgroups cannot keep the attention ones
+// off the chip, whatever the dispatch order. The last arrival re-arms `done` (dual_ln_arrive_tail).
+template <int LPT, bool PAGED, bool ONLINE, int PER>
+__global__ __launch_bounds__(256) void decode_attn_out_ln_kernel(DecodeParams p, int nsplit, int n_attn, DualLn a,
+                                                                 unsigned int* done) {
+  constexpr int R = 4;
+  __shared__ float part[4][R];
+  const int bid = blockIdx.x, tid = threadIdx.x;
+  if (bid < n_attn) {
+    const int split = bid % nsplit, rest = bid / nsplit;
+    decode_attn_body<LPT, 1, PAGED, ONLINE>(p, split, rest % p.Hkv, rest / p.Hkv, nsplit);
+    // R1 publish: every storing wave drains its write-through stores, barrier, one counter add
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  const int ngrp = (a.N + R - 1) / R;
+  bool waited = false;
+  for (int grp = bid; grp < ngrp; grp += gridDim.x) {
+    const int n0 = grp * R;
+    float acc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = 0.f;
+    gemv_m1_accum<R>(a.x1, a.w1, a.N, a.K1, n0, acc, -1, waited ? nullptr : done, (unsigned)n_attn);
+    waited = true;
+    const float v = gemv_m1_finish<R>(acc, part, nullptr, n0, a.N, 0);
+    if (tid < R && n0 + tid < a.N) st_pub(&a.ypart[n0 + tid], v);
+    __syncthreads();
+  }
+  dual_ln_arrive_tail<PER>(a, done);
+}
+
+// kca_decode_prep_attn's arguments (B = 1, H == Hkv) plus the out-projection tail of kca_gemv_dual_ln
+// (ow [N, H*D], bias, residual h, ln_2) and `done`: a zero-initialised counter (re-armed by every
+// launch). Returns 10 when the shape is outside it (the caller runs the two launches).
+KCA_API int kca_decode_attn_out_ln(const void* qkv, long long ld, const void* kc, const void* vc,
+                                   long long cs_slot, long long cs_head, long long cs_pos,
+                                   const int* slots, const int* kv_lens, void* out, long long o_bs,
+                                   float* ws, long long ws_floats, int B, int H, int Hkv, int D,
+                                   int max_kv, int chunk, float scale, const float* alibi, const int* tbl,
+                                   int tbl_stride, int ps_shift, int rot, int interleaved, const float* cos_t,
+                                   const float* sin_t, int window, int by_row, const void* ow, const void* obias,
+                                   float* ypart, unsigned int* cnt, const void* h, void* h_out, const void* gamma,
+                                   const void* beta, float eps, void* xn_out, int N, unsigned int* done,
+                                   hipStream_t stream) {
+  if (rot > D || (rot & 1) || (rot > 0 && (!cos_t || !sin_t))) return 8;
+  if (window < 0) return 9;
+  if (B != 1 || H != Hkv || D % 8 || D > 256 || max_kv <= 0 || !done || !ypart || !cnt || !h || !h_out ||
+      !gamma || !xn_out || N <= 0 || N % 8 || N > 16384 || o_bs != (long long)H * D)
+    return 10;
+  if (((uintptr_t)ow | (uintptr_t)out | (uintptr_t)h | (uintptr_t)h_out | (uintptr_t)gamma | (uintptr_t)beta |
+       (uintptr_t)xn_out | (uintptr_t)ypart) & 15)
+    return 10;
+  DecodeParams p{(const bf16_t*)qkv, ld, (const bf16_t*)kc, (const bf16_t*)vc, cs_slot, cs_head,
+                 cs_pos, slots, kv_lens, (bf16_t*)out, o_bs, nullptr, nullptr, alibi, tbl, tbl_stride, ps_shift,
+                 H, Hkv, D, chunk, scale, 1, rot, interleaved, cos_t, sin_t, g_decode_stamps, nullptr, window};
+  p.by_row = by_row;
+  p.pub_out = 1;
+  if (tbl && (ps_shift < 4 || ps_shift > 20 || tbl_stride <= 0)) return 5;
+  if (chunk <= 0) chunk = kca_decode_chunk(B, Hkv, max_kv);
+  if (tbl && chunk > 1024) return 6;
+  const int nsplit = (max_kv + chunk - 1) / chunk;
+  if (nsplit > 1024) return 7;
+  p.chunk = chunk;
+  if (nsplit > 1) {
+    if (!fanin_enabled()) return 10;
+    const long long cw = fanin_words(B, H);
+    const long long need = cw + (long long)B * H * nsplit * (D + 2);
+    if (!ws || ws_floats < need) return 4;
+    p.cnt = reinterpret_cast<unsigned int*>(ws);
+    p.ws_o = ws + cw;
+    p.ws_ml = p.ws_o + (long long)B * H * nsplit * D;
+  }
+  const DualLn a{(const bf16_t*)out, (const bf16_t*)ow, nullptr, nullptr, (const bf16_t*)obias, ypart, cnt,
+                 (const bf16_t*)h, (bf16_t*)h_out, (const bf16_t*)gamma, (const bf16_t*)beta, eps, (bf16_t*)xn_out,
+                 nullptr, nullptr, nullptr, N, H * D, 0};
+  const int n_attn = nsplit * Hkv * B;
+  const int ngrp = (N + 3) / 4;
+  static int cu_count[64] = {};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  int& cus = cu_count[dev & 63];
+  if (!cus && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+  int rc = 10;
+  auto go = [&](auto lpt, auto paged, auto online, auto per) {
+    constexpr int LPT = decltype(lpt)::value;
+    constexpr bool PG = decltype(paged)::value, ON = decltype(online)::value;
+    constexpr int PR = decltype(per)::value;
+    auto kern = decode_attn_out_ln_kernel<LPT, PG, ON, PR>;
+    const size_t lds = ON ? (size_t)4 * (2 + p.D) * sizeof(float) : (size_t)(p.chunk + 4 * p.D) * sizeof(float);
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 256, lds) != hipSuccess || occ < 2) return;
+    // one residency round with a margin of one workgroup per CU (the occupancy API can read one
+    // high: MI355X_MICROARCH.md, correctness boundaries)
+    const int grid = std::min(ngrp, cus * (occ - 1));
+    if (grid <= n_attn) return;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, stream, p, nsplit, n_attn, a, done);
+    rc = hipGetLastError() == hipSuccess ? 0 : 2;
+  };
+  const int nd = D / 8;
+  constexpr int TPB16 = 4 * (64 / 16), TPB32 = 4 * (64 / 32), TPB8 = 4 * (64 / 8), U = 4;
+  auto by_lpt = [&](auto lpt, int tpb) {
+    const bool online = p.chunk > tpb * U;
+    auto per = [&](auto pg, auto on) {
+      if (N <= 8192) go(lpt, pg, on, std::integral_constant<int, 4>{});
+      else go(lpt, pg, on, std::integral_constant<int, 8>{});
+    };
+    if (p.tbl) {
+      if (online) per(std::true_type{}, std::true_type{});
+      else per(std::true_type{}, std::false_type{});
+    } else {
+      if (online) per(std::false_type{}, std::true_type{});
+      else per(std::false_type{}, std::false_type{});
+    }
+  };
+  if (nd <= 8) by_lpt(std::integral_constant<int, 8>{}, TPB8);
+  else if (nd <= 16) by_lpt(std::integral_constant<int, 16>{}, TPB16);
+  else by_lpt(std::integral_constant<int, 32>{}, TPB32);
+  return rc;
 }
 
 // --------------------------------------------------------------- sampling

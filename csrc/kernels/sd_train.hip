@@ -49,6 +49,11 @@ struct NoiseArgs {
   float scale;
   int v_pred;
   unsigned long long seed;
+  // Philox counters run over GLOBAL sample indices: local sample b draws as sample_base + b *
+  // sample_stride of the step's whole batch (rank r of W under an interleaving sampler: base r,
+  // stride W), so a sample's noise does not depend on how the batch is split across ranks
+  long long sample_base;
+  int sample_stride;
 };
 
 __global__ __launch_bounds__(256) void sd_noise_prep_kernel(NoiseArgs a) {
@@ -62,7 +67,9 @@ __global__ __launch_bounds__(256) void sd_noise_prep_kernel(NoiseArgs a) {
     const int b = (int)(r / a.C);
     const long long io = b * a.in.b + c * a.in.c + h * a.in.h + w * a.in.w;
     const long long oo = b * a.out.b + c * a.out.c + h * a.out.h + w * a.out.w;
-    uint32_t ctr[4] = {(uint32_t)i, (uint32_t)(i >> 32), 0x5344u, 0u};
+    const long long chw = (long long)a.C * a.H * a.W;
+    const long long gi = (a.sample_base + (long long)b * a.sample_stride) * chw + (i - (long long)b * chw);
+    uint32_t ctr[4] = {(uint32_t)gi, (uint32_t)(gi >> 32), 0x5344u, 0u};
     philox10(ctr, k0, k1);
     // Box-Muller: two independent standard normals from four 32-bit draws
     const float u1 = ((ctr[0] >> 8) + 1) * (1.0f / 16777216.0f), u2 = (ctr[1] >> 8) * (1.0f / 16777216.0f);
@@ -84,13 +91,15 @@ __global__ __launch_bounds__(256) void sd_noise_prep_kernel(NoiseArgs a) {
 KCA_API int kca_sd_noise_prep(const void* mean, const void* logvar, const long long* in_strides, void* noisy,
                               void* target, const long long* out_strides, const float* acp, const void* e_in,
                               const void* n_in, int B, int C, int H, int W, float scale, int v_pred,
-                              unsigned long long seed, hipStream_t stream) {
-  if (B <= 0 || C <= 0 || H <= 0 || W <= 0) return 1;
+                              unsigned long long seed, long long sample_base, int sample_stride,
+                              hipStream_t stream) {
+  if (B <= 0 || C <= 0 || H <= 0 || W <= 0 || sample_stride <= 0 || sample_base < 0) return 1;
   NoiseArgs a{(const bf16_t*)mean, (const bf16_t*)logvar,
               {in_strides[0], in_strides[1], in_strides[2], in_strides[3]},
               (bf16_t*)noisy, (bf16_t*)target,
               {out_strides[0], out_strides[1], out_strides[2], out_strides[3]},
-              acp, (const bf16_t*)e_in, (const bf16_t*)n_in, B, C, H, W, scale, v_pred, seed};
+              acp, (const bf16_t*)e_in, (const bf16_t*)n_in, B, C, H, W, scale, v_pred, seed, sample_base,
+              sample_stride};
   const long long n = (long long)B * C * H * W;
   hipLaunchKernelGGL(sd_noise_prep_kernel, dim3(kca_grid(n, 256)), dim3(256), 0, stream, a);
   return 0;

@@ -28,14 +28,17 @@ __global__ void __launch_bounds__(256) transpose_bf16_kernel(const bf16_t* __res
                                                              bf16_t* __restrict__ out, long long ld_out,
                                                              int R, int C) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int tiles_c = C >> 6;
+  const int tiles_c = (C + 63) >> 6;
   const long long tile = (long long)blockIdx.x * 4 + wave;
-  const long long ntiles = (long long)(R >> 6) * tiles_c;
+  const long long ntiles = (long long)((R + 63) >> 6) * tiles_c;
   if (tile >= ntiles) return;
   const int tr = (int)(tile / tiles_c), tc = (int)(tile % tiles_c);
   const int rb = lane & 7, cb = lane >> 3;
   const long long r0 = (long long)tr * 64 + rb * 8;
   const long long c0 = (long long)tc * 64 + cb * 8;
+  // edge tiles (R or C not a multiple of 64, both multiples of 8): a lane's 8 x 8 block is wholly
+  // inside or wholly outside
+  if (r0 >= R || c0 >= C) return;
   u32x4 a[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -56,12 +59,13 @@ __global__ void __launch_bounds__(256) transpose_bf16_kernel(const bf16_t* __res
 }  // namespace
 
 // out[C, R] (row stride ld_out) = in[R, C]^T (row stride ld_in); R, C multiples
-// of 64, strides multiples of 8 elements, 16-B aligned pointers.
+// of 8 (GPT-J's 50400-row LM head: its weight-gradient GEMM runs TN too), strides
+// multiples of 8 elements, 16-B aligned pointers.
 KCA_API int kca_transpose_bf16(const void* in, long long ld_in, void* out, long long ld_out, int R, int C,
                                hipStream_t stream) {
-  if (R % 64 || C % 64 || ld_in % 8 || ld_out % 8 || ld_in < C || ld_out < R) return 1;
+  if (R % 8 || C % 8 || ld_in % 8 || ld_out % 8 || ld_in < C || ld_out < R) return 1;
   if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15) return 1;
-  const long long tiles = (long long)(R / 64) * (C / 64);
+  const long long tiles = (long long)((R + 63) / 64) * ((C + 63) / 64);
   if (tiles == 0) return 0;
   hipLaunchKernelGGL(transpose_bf16_kernel, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, stream,
                      (const bf16_t*)in, ld_in, (bf16_t*)out, ld_out, R, C);

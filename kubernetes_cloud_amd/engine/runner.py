@@ -373,7 +373,15 @@ class ModelRunner:
         # KCA_DECODE_FUSED=0: the per-projection path (two-stream for parallel-residual models)
         ln2 = [blk.ln_2 for blk in model.h]
         self._layer_kind = ("gptj" if all(x is None for x in ln2) else "neox") if cfg.parallel_residual else "seq"
-        self._fused_ok = (on_gpu and not self.multi_device and (not tp or tp_local)
+        # a real TP group (BLOOM TP=8 serving): sequential layers close each row-parallel projection with
+        # the custom all-reduce's fused residual + LayerNorm tail (parallel/custom_ar.py res_ln)
+        self._tp_ar = None
+        if tp and not tp_local and self._layer_kind == "seq":
+            from ..parallel.custom_ar import lookup
+            ars = {id(mm.group): lookup(mm.group) for mm in rows}
+            if len(ars) == 1 and None not in ars.values():
+                self._tp_ar = next(iter(ars.values()))
+        self._fused_ok = (on_gpu and not self.multi_device and (not tp or tp_local or self._tp_ar is not None)
                           and os.environ.get("KCA_DECODE_FUSED", "1") not in ("0", "false")
                           and cfg.hidden <= 16384
                           and (self._layer_kind != "neox"
@@ -503,7 +511,8 @@ class ModelRunner:
             fz = self._fz["b1"] = {
                 "g": torch.empty(1, f, **z), "h": torch.empty(1, d, **z), "xn": torch.empty(1, d, **z),
                 "xn2": torch.empty(1, d, **z), "ypart": torch.empty(d, device=self.device, dtype=torch.float32),
-                "cnt": torch.zeros(32 * 65, device=self.device, dtype=torch.int32), "bias": biases}
+                "cnt": torch.zeros(32 * 65, device=self.device, dtype=torch.int32), "bias": biases,
+                "done": torch.zeros(32, device=self.device, dtype=torch.int32)}
         return fz
 
     def _desc_args(self, cos, sin, tbl):
@@ -549,13 +558,33 @@ class ModelRunner:
             nxt = m.h[li + 1] if li + 1 < len(m.h) else None
             nln = nxt.ln_1 if nxt is not None else m.ln_f
             qkv = skinny_linear(xn, at.qkv.weight, at.qkv.bias)
-            if kind == "seq":
+            if kind == "seq" and self._tp_ar is not None:
+                # TP rank: partial projections, each closed by all-reduce + bias + residual + LayerNorm
+                ar = self._tp_ar
                 o = dops.decode_prep_attention(qkv, self.H, self.Hkv, self.D, self.rot, cfg.rotary_interleaved,
                                                cos, sin, pos, slots, kc, vc, kv_lens, max_kv, at.scale, at.alibi,
                                                out=obuf, ws=ws, block_table=tbl, window=at.window, by_row=by_row)
-                # out-projection + residual + ln_2, then fc_in (+ GELU), then fc_out + residual + next ln_1
-                dops.gemv_dual_ln(o, at.out.weight, None, None, at.out.bias, h, blk.ln_2.weight, blk.ln_2.bias,
-                                  blk.ln_2.eps, fz["ypart"], fz["cnt"], hb, x2b)
+                ar.res_ln(skinny_linear(o, at.out.weight), at.out.bias, h, hb, blk.ln_2.weight, blk.ln_2.bias,
+                          blk.ln_2.eps, x2b)
+                f = skinny_linear(x2b, mlp.fc_in.weight, mlp.fc_in.bias, act, out=g)
+                ar.res_ln(skinny_linear(f, mlp.fc_out.weight), mlp.fc_out.bias, hb, hb, nln.weight, nln.bias,
+                          nln.eps, xb)
+                h, xn = hb, xb
+                continue
+            if kind == "seq":
+                # attention + out-projection + residual + ln_2 (one launch where the fused kernel covers
+                # the shape), then fc_in (+ GELU), then fc_out + residual + next ln_1
+                if not dops.decode_attn_out_ln(
+                        qkv, self.H, self.Hkv, self.D, self.rot, cfg.rotary_interleaved, cos, sin, pos, slots, kc,
+                        vc, kv_lens, max_kv, at.scale, at.alibi, obuf, ws, tbl, at.window, by_row, at.out.weight,
+                        at.out.bias, h, blk.ln_2.weight, blk.ln_2.bias, blk.ln_2.eps, fz["ypart"], fz["cnt"], hb,
+                        x2b, fz["done"]):
+                    o = dops.decode_prep_attention(qkv, self.H, self.Hkv, self.D, self.rot,
+                                                   cfg.rotary_interleaved, cos, sin, pos, slots, kc, vc, kv_lens,
+                                                   max_kv, at.scale, at.alibi, out=obuf, ws=ws, block_table=tbl,
+                                                   window=at.window, by_row=by_row)
+                    dops.gemv_dual_ln(o, at.out.weight, None, None, at.out.bias, h, blk.ln_2.weight,
+                                      blk.ln_2.bias, blk.ln_2.eps, fz["ypart"], fz["cnt"], hb, x2b)
                 f = skinny_linear(x2b, mlp.fc_in.weight, mlp.fc_in.bias, act, out=g)
                 dops.gemv_dual_ln(f, mlp.fc_out.weight, None, None, mlp.fc_out.bias, hb, nln.weight, nln.bias,
                                   nln.eps, fz["ypart"], fz["cnt"], hb, xb)

@@ -26,11 +26,13 @@ def _strides(t: torch.Tensor):
 
 def noise_prep(mean: torch.Tensor, logvar: torch.Tensor, acp: torch.Tensor, scale: float, v_pred: bool,
                seed: int = 0, e: torch.Tensor | None = None, n: torch.Tensor | None = None,
-               channels_last: bool | None = None):
+               channels_last: bool | None = None, sample_base: int = 0, sample_stride: int = 1):
     """mean / logvar: [B, C, H, W] views of the VAE moments; acp: [B] fp32
     alphas_cumprod of each sample's timestep. Returns (noisy, target) bf16 in
     the moments' memory format (or ``channels_last`` when given). ``e`` / ``n``
-    (logical [B, C, H, W]) replace the internal draws (tests)."""
+    (logical [B, C, H, W]) replace the internal draws (tests). Local sample b draws as global sample
+    ``sample_base + b * sample_stride`` of the step (data-parallel ranks: the same noise per sample
+    whatever the split)."""
     B, C, H, W = mean.shape
     if channels_last is None:
         channels_last = mean.is_contiguous(memory_format=torch.channels_last) or (
@@ -47,7 +49,7 @@ def noise_prep(mean: torch.Tensor, logvar: torch.Tensor, acp: torch.Tensor, scal
         _lib.call("kca_sd_noise_prep", mean.data_ptr(), logvar.data_ptr(), ctypes.addressof(s_in),
                   noisy.data_ptr(), target.data_ptr(), ctypes.addressof(s_out), acp.data_ptr(),
                   _lib.ptr(ec), _lib.ptr(nc), B, C, H, W, float(scale), int(v_pred), seed & ((1 << 64) - 1),
-                  _lib.stream())
+                  int(sample_base), int(sample_stride), _lib.stream())
         return noisy, target
     return noise_prep_reference(mean, logvar, acp, scale, v_pred, e, n, fmt)
 

@@ -88,6 +88,10 @@ class XGMIAllReduce:
                                        ctypes.c_int, ctypes.c_int, P, P, ctypes.c_longlong, ctypes.c_int,
                                        ctypes.c_longlong, ctypes.c_int, P])
         self._err = _fn("kca_ar_error", [P, ctypes.POINTER(ctypes.c_int)])
+        self._res_ln = _fn("kca_ar_res_ln", [ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(P), P, ctypes.c_int,
+                                             ctypes.c_int, P, ctypes.c_int, ctypes.c_int, ctypes.c_longlong, P, P, P,
+                                             P, P, ctypes.c_float, P, P, P, P, P, P, P])
+        self._tails: dict = {}
         lib = _lib.require()
         self.max_blocks = int(lib.kca_ar_max_blocks())
         sig_bytes = lib.kca_ar_signal_bytes()
@@ -167,6 +171,34 @@ class XGMIAllReduce:
             raise RuntimeError(f"kca_ar_run (all-gather) status {rc}")
         self.calls += 1
         return out
+
+    def res_ln(self, t: torch.Tensor, bias, h: torch.Tensor, h_out: torch.Tensor, gamma: torch.Tensor, beta,
+               eps: float, xn_out: torch.Tensor, gamma2=None, beta2=None, xn2_out=None) -> None:
+        """Close a row-parallel projection of the batch-1 decode layer in ONE launch: all-reduce this
+        rank's partial ``t`` ([1, N] bf16), then h_out = bf16(h + sum + bias) and xn_out = LayerNorm(h_out)
+        (and xn2_out with gamma2 / beta2) -- no bias add, no LayerNorm launch after the collective
+        (``kca_ar_res_ln``; graph-capturable like ``all_reduce_``)."""
+        n = t.numel()
+        if not self.eligible(t) or n > 16384:
+            raise ValueError("tensor not eligible for the fused all-reduce + LayerNorm (bf16 [N], N <= 16384)")
+        ws = self._tail_ws(t.device)
+        blocks = max(1, min(64, -(-(n // 8) // 128)))
+        rc = self._res_ln(self._stage0, self._stage1, self._sig, P(self._ctl), self.rank, self.world, t.data_ptr(),
+                          n, blocks, self.spin_limit, _lib.ptr(bias), h.data_ptr(), h_out.data_ptr(),
+                          gamma.data_ptr(), _lib.ptr(beta), float(eps), xn_out.data_ptr(), _lib.ptr(gamma2),
+                          _lib.ptr(beta2), _lib.ptr(xn2_out), ws[0].data_ptr(), ws[1].data_ptr(), _lib.stream())
+        if rc != 0:
+            raise RuntimeError(f"kca_ar_res_ln status {rc}")
+        self.calls += 1
+
+    def _tail_ws(self, dev):
+        """fp32 [16384] sums + the tail's zero-initialised arrival counters (local, not IPC-shared)."""
+        ws = self._tails.get(str(dev))
+        if ws is None:
+            ws = (torch.empty(16384, device=dev, dtype=torch.float32),
+                  torch.zeros(32 * 65, device=dev, dtype=torch.int32))
+            self._tails[str(dev)] = ws
+        return ws
 
     def error(self) -> int:
         e = ctypes.c_int(0)

@@ -26,12 +26,19 @@ import asyncio
 import inspect
 import logging
 import os
+import sys
 import time
 
 from fastapi import Request
 from fastapi.responses import JSONResponse, Response
 
 from . import v2
+
+# GIL hand-off interval of the serving process. The engine's step loop runs in its own thread and gives
+# the interpreter lock up at every device wait; under the default 5 ms interval, a request thread busy
+# in JSON / tokenizer work can hold the engine off for up to 5 ms per hand-off (bench/serving_bench.py
+# --switch-interval A/B)
+GIL_SWITCH_S = 5e-4
 
 log = logging.getLogger("kca.serving")
 
@@ -126,6 +133,8 @@ class ModelServer:
 
         for m in models or []:
             self.register(m)
+        if GIL_SWITCH_S > 0:
+            sys.setswitchinterval(GIL_SWITCH_S)
         app = FastAPI(title="kubernetes-cloud-amd model server")
         app.add_middleware(CORSMiddleware, allow_origins=["*"], allow_methods=["*"], allow_headers=["*"])
         reg = CollectorRegistry()

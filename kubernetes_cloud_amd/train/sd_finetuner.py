@@ -185,9 +185,10 @@ def main(argv=None):
                                args.class_dataset, args.num_class_images, gen_class_images, sync=barrier, **tf)
     else:
         ds = LocalBase(tok, args.dataset, ucg=args.ucg, shuffle=args.shuffle, **tf)
-    sampler = torch.utils.data.DistributedSampler(ds, world, rank, shuffle=args.shuffle, seed=args.seed) \
-        if world > 1 else None
-    dl = torch.utils.data.DataLoader(ds, batch_size=args.batch_size, shuffle=(args.shuffle and sampler is None),
+    # one sampler for every world size: the same seeded permutation, rank r taking every world-th sample,
+    # so a world-W step consumes exactly the samples of a world-1 step with batch W x batch_size
+    sampler = torch.utils.data.DistributedSampler(ds, world, rank, shuffle=args.shuffle, seed=args.seed)
+    dl = torch.utils.data.DataLoader(ds, batch_size=args.batch_size, shuffle=False,
                                      sampler=sampler, collate_fn=ds.get_collate_fn(), num_workers=2,
                                      drop_last=world > 1)
     if args.use_8bit_adam and info.is_main:
@@ -237,9 +238,15 @@ def main(argv=None):
                 with torch.no_grad():
                     mean, logvar = vae.encode_moments(px).chunk(2, dim=1)
                     ctx = te(ids)
-                ts = torch.randint(0, noise_sched.N, (mean.shape[0],), device=dev)
+                # timesteps and noise per GLOBAL sample (rank r's sample j is sample r + W j of the step
+                # under the interleaving sampler): a data-parallel step draws what one process would
+                nb = mean.shape[0]
+                tg = torch.Generator().manual_seed(args.seed * 7919 + step)
+                ts = torch.randint(0, noise_sched.N, (nb * info.world_size,), generator=tg)
+                ts = ts[info.rank::info.world_size][:nb].to(dev, non_blocking=True)
                 noisy, target = noise_prep(mean, logvar, acp_dev[ts], scale, pred_type == "v_prediction",
-                                           seed=(args.seed * 1000003 + step * info.world_size + info.rank))
+                                           seed=args.seed * 1000003 + step, sample_base=info.rank,
+                                           sample_stride=info.world_size)
                 pred = unet(noisy, ts, ctx)
                 loss = mse_split(pred, target, args.prior_loss_weight if args.is_dreambooth else None)
             else:
@@ -267,7 +274,12 @@ def main(argv=None):
                 torch.cuda.synchronize()
             dt_s = time.perf_counter() - t0
             rsps = args.batch_size / dt_s
-            logs = {"train/loss": loss.item(), "train/lr": lr, "train/epoch": epoch, "train/step": step,
+            lv = loss.detach().float().reshape(1)
+            if world > 1:  # the step's loss over the whole (global) batch, as one process would log it
+                torch.distributed.all_reduce(lv)
+                lv = lv / world
+            logs = {"train/loss": float(lv), "train/grad_norm": eng.grad_norm(), "train/lr": lr,
+                    "train/epoch": epoch, "train/step": step,
                     "train/samples_seen": step * args.batch_size * world,
                     "perf/rank_samples_per_second": rsps, "perf/world_samples_per_second": rsps * world}
             sink.log(logs, step=step)

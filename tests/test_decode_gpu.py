@@ -537,9 +537,10 @@ def test_engine_gpu_chunked_prefill(preset):
         assert float(top2[0] - top2[1]) < 0.1, (preset, i)
 
 
+@pytest.mark.parametrize("rows", [0, 4, 8, 16])
 @pytest.mark.parametrize("N,K1,K2,two_ln", [(4096, 4096, 16384, False), (6144, 6144, 24576, True),
                                              (14336, 1792, 0, False), (14336, 7168, 0, True)])
-def test_gemv_dual_ln_matches_reference(N, K1, K2, two_ln):
+def test_gemv_dual_ln_matches_reference(N, K1, K2, two_ln, rows):
     """decode.hip gemv_dual_ln_kernel: y = x1 W1^T (+ x2 W2^T) + b, h' = h + y, LN(h') in one launch
     (arrival counter, last workgroup normalises) -- GPT-J (two weight streams), GPT-NeoX-20B (two
     LayerNorms of h'), BLOOM TP=8 rank shapes (one stream, N = 14336); repeated launches reuse the
@@ -560,7 +561,7 @@ def test_gemv_dual_ln_matches_reference(N, K1, K2, two_ln):
     for _ in range(3):
         h_out, xn, xn2 = torch.empty(1, N, **bf), torch.empty(1, N, **bf), torch.empty(1, N, **bf)
         dops.gemv_dual_ln(x1, w1, x2, w2, b, h, gamma, beta, 1e-5, ypart, cnt, h_out, xn,
-                          *((g2, b2, xn2) if two_ln else ()))
+                          *((g2, b2, xn2) if two_ln else (None, None, None)), rows=rows)
         torch.cuda.synchronize()
         assert (h_out.float() - hn_ref.float()).abs().max() < 0.05
         assert (xn.float() - xn_ref).abs().max() < 0.08
@@ -891,3 +892,51 @@ def test_engine_bloom_tp_emulated_rank_fused():
     out = eng.generate([p], sp)[0].output
     _check_against_forward(m, p, out)
     assert m.h[0].attn.out.group.allreduce_calls > 0
+
+
+@pytest.mark.parametrize("PS", [0, 64])
+@pytest.mark.parametrize("L0", [40, 600])
+@pytest.mark.parametrize("alibi", [False, True])
+def test_decode_attn_out_ln_fused_matches_two_launches(PS, L0, alibi):
+    """decode_attn_out_ln_kernel (sequential-residual layer: attention, out-projection, residual + ln_2
+    in one launch, the projection's workgroups waiting on the attention's write-through output) gives
+    exactly the two-launch result: decode_prep_attention, then gemv_dual_ln with one weight stream.
+    Three launches in a row on the same counters: every counter re-armed."""
+    torch.manual_seed(11 + L0)
+    H, D, L, N = 14, 128, 1024, 14336  # a BLOOM TP=8 rank: 14 heads of 128, hidden 14336
+    bf = dict(device=dev, dtype=torch.bfloat16)
+    kc0 = torch.randn(2, H, L, D, device=dev).to(torch.bfloat16)
+    vc0 = torch.randn_like(kc0)
+    tbl = None
+    if PS:
+        kc0, tbl = _paginate(kc0, PS, 3)
+        vc0, _ = _paginate(vc0, PS, 3)
+    qkv = torch.randn(1, 3 * H * D, **bf)
+    slots = torch.tensor([1], device=dev, dtype=torch.int32)
+    pos = torch.tensor([L0 - 1], device=dev, dtype=torch.int32)
+    kv_lens = pos + 1
+    al = torch.rand(H, device=dev) * 0.5 if alibi else None
+    ow, ob = torch.randn(N, H * D, **bf) * 0.02, torch.randn(N, **bf)
+    h, g, be = torch.randn(1, N, **bf), torch.randn(N, **bf), torch.randn(N, **bf)
+    ws = torch.zeros(max(dops.decode_ws_floats(1, H, H, D, L), 1), device=dev, dtype=torch.float32)
+    ypart = torch.empty(N, device=dev, dtype=torch.float32)
+    cnt = torch.zeros(32 * 65, device=dev, dtype=torch.int32)
+    done = torch.zeros(32, device=dev, dtype=torch.int32)
+    res = []
+    for fused in (False, True, True, True):
+        kc, vc, out = kc0.clone(), vc0.clone(), torch.empty(1, H * D, **bf)
+        ho, xn = torch.empty(1, N, **bf), torch.empty(1, N, **bf)
+        if fused:
+            assert dops.decode_attn_out_ln(qkv.clone(), H, H, D, 0, False, None, None, pos, slots, kc, vc, kv_lens, L,
+                                           D ** -0.5, al, out, ws, tbl, 0, 0, ow, ob, h, g, be, 1e-5, ypart, cnt,
+                                           ho, xn, done)
+        else:
+            dops.decode_prep_attention(qkv.clone(), H, H, D, 0, False, None, None, pos, slots, kc, vc, kv_lens, L,
+                                       D ** -0.5, al, out=out, ws=ws, block_table=tbl)
+            dops.gemv_dual_ln(out, ow, None, None, ob, h, g, be, 1e-5, ypart, cnt, ho, xn)
+        torch.cuda.synchronize()
+        res.append((out, ho, xn, kc, vc))
+    for r in res[1:]:
+        for a, b in zip(res[0], r):
+            assert torch.equal(a, b)
+    assert int(cnt.abs().sum()) == 0 and int(done.abs().sum()) == 0

@@ -400,7 +400,8 @@ def test_engine_host_offload_matches_hbm_optimizer():
     assert _rel(out[0], out[1]) < 2e-3
 
 
-@pytest.mark.parametrize("R,C,ld", [(64, 64, 64), (128, 4096, 4096), (4096, 192, 256), (16384, 640, 640)])
+@pytest.mark.parametrize("R,C,ld", [(64, 64, 64), (128, 4096, 4096), (4096, 192, 256), (16384, 640, 640),
+                                    (2048, 50400, 50400), (72, 40, 48)])  # edge tiles: GPT-J vocab, tiny
 def test_transpose_bf16(R, C, ld):
     from kubernetes_cloud_amd.ops.linear import transpose
     base = torch.randn(R, ld, device=DEV).bfloat16()
