@@ -832,7 +832,7 @@ __global__ __launch_bounds__(256) void decode_attn_gemv_kernel(DecodeParams p, i
 // the out-projection / fc_out, the residual add and the next LayerNorm in one launch, no LayerNorm
 // launch of its own.
 template <int R, int PER>
-__global__ __launch_bounds__(256) void gemv_dual_ln_kernel(DualLn a) {
+__global__ __launch_bounds__(256) void gemv_dual_ln_kernel(DualLn a, int split_loops, int no_tail) {
   __shared__ float part[4][R];
   const int tid = threadIdx.x;
   // row groups g = blockIdx.x, + gridDim.x, ...: the grid is at most one residency round, so a
@@ -844,7 +844,7 @@ __global__ __launch_bounds__(256) void gemv_dual_ln_kernel(DualLn a) {
     float acc[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r] = 0.f;
-    if (a.x2 && a.K1 % 2048 == 0) {
+    if (a.x2 && a.K1 % 2048 == 0 && !split_loops) {
       gemv_m1_accum2<R>(a.x1, a.w1, a.K1, a.x2, a.w2, a.K2, a.N, n0, acc);
     } else {
       gemv_m1_accum<R>(a.x1, a.w1, a.N, a.K1, n0, acc);
@@ -854,6 +854,7 @@ __global__ __launch_bounds__(256) void gemv_dual_ln_kernel(DualLn a) {
     if (tid < R && n0 + tid < a.N) st_pub(&a.ypart[n0 + tid], v);
     __syncthreads();  // part[] is rewritten by the next group
   }
+  if (no_tail) return;  // timing A/B only (variant bit 2): the GEMV without arrival + LayerNorm
   dual_ln_arrive_tail<PER>(a);
 }
 
@@ -1103,7 +1104,7 @@ KCA_API int kca_decode_prep_attn_gemv(const void* qkv, long long ld, const void*
 KCA_API int kca_gemv_dual_ln(const void* x1, const void* w1, int K1, const void* x2, const void* w2, int K2,
                              const void* bias, float* ypart, unsigned int* cnt, const void* h, void* h_out,
                              const void* gamma, const void* beta, float eps, void* xn_out, const void* gamma2,
-                             const void* beta2, void* xn2_out, int N, int rows, hipStream_t stream) {
+                             const void* beta2, void* xn2_out, int N, int rows, int variant, hipStream_t stream) {
   if (N <= 0 || N % 8 || N > 16384 || K1 % 8 || K1 <= 0 || !ypart || !cnt || !gamma || !xn_out || !h || !h_out)
     return 1;
   if (x2 && (K2 <= 0 || K2 % 8 || !w2)) return 1;
@@ -1118,17 +1119,21 @@ KCA_API int kca_gemv_dual_ln(const void* x1, const void* w1, int K1, const void*
                  N, K1, x2 ? K2 : 0};
   if (rows <= 0) rows = 4;  // (8 / 16 rows measured slower at every shape: bench/gemv_dual_ln_bench.py)
   if (rows != 4 && rows != 8 && rows != 16) return 1;
-  // at most one residency round (8 workgroups of 256 threads per CU); larger N loops row groups
+  // variant (A/B sweep, bench/gemv_dual_ln_bench.py): bit 0 -- grid capped at one residency round (8
+  // workgroups of 256 threads per CU, row groups looped); bit 1 -- the two weight streams as two loops;
+  // bit 2 -- no arrival / LayerNorm tail (timing only: h_out / xn_out are not written)
   static int cu_count[64] = {};
   int dev = 0;
   (void)hipGetDevice(&dev);
   int& cus = cu_count[dev & 63];
   if (!cus && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
-  const dim3 grid((unsigned)std::min((N + rows - 1) / rows, 8 * cus));
+  const int ngrp = (N + rows - 1) / rows;
+  const dim3 grid((unsigned)((variant & 1) ? std::min(ngrp, 8 * cus) : ngrp));
+  const int split_loops = (variant >> 1) & 1, no_tail = (variant >> 2) & 1;
   auto go = [&](auto rc) {
     constexpr int R = decltype(rc)::value;
-    if (N <= 8192) hipLaunchKernelGGL((gemv_dual_ln_kernel<R, 4>), grid, dim3(256), 0, stream, a);
-    else hipLaunchKernelGGL((gemv_dual_ln_kernel<R, 8>), grid, dim3(256), 0, stream, a);
+    if (N <= 8192) hipLaunchKernelGGL((gemv_dual_ln_kernel<R, 4>), grid, dim3(256), 0, stream, a, split_loops, no_tail);
+    else hipLaunchKernelGGL((gemv_dual_ln_kernel<R, 8>), grid, dim3(256), 0, stream, a, split_loops, no_tail);
   };
   if (rows == 4) go(std::integral_constant<int, 4>{});
   else if (rows == 8) go(std::integral_constant<int, 8>{});
@@ -1263,6 +1268,94 @@ KCA_API int kca_decode_attn_out_ln(const void* qkv, long long ld, const void* kc
   return rc;
 }
 
+// Fused decode tail + the NEXT projection in one launch (batch 1): phase A is gemv_dual_ln_kernel
+// (y = x1 W1^T (+ x2 W2^T), last arriver: residual + LayerNorm -> xn_out, published with `ready`);
+// phase B streams the next GEMV on xn_out (the next layer's QKV, or fc_in after an out-projection),
+// each workgroup requesting its first row group's weights BEFORE it waits for `ready` -- the tail and
+// the kernel boundary run under the next weight stream instead of in front of it. Phase-B waiters
+// never block phase-A work: the grid is at most one residency round (occupancy API, with a margin).
+// `ready` and `cnt2` (phase-B arrivals) are re-armed by the last workgroup through phase B.
+template <int PER>
+__global__ __launch_bounds__(256) void gemv_ln_gemv_kernel(DualLn a, GemvM1 nx, unsigned int* ready,
+                                                           unsigned int* cnt2) {
+  constexpr int R = 4;
+  __shared__ float part[4][R];
+  const int tid = threadIdx.x;
+  const int ngrp = (a.N + R - 1) / R;
+  for (int grp = blockIdx.x; grp < ngrp; grp += gridDim.x) {
+    const int n0 = grp * R;
+    float acc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = 0.f;
+    gemv_m1_accum<R>(a.x1, a.w1, a.N, a.K1, n0, acc);
+    if (a.x2) gemv_m1_accum<R>(a.x2, a.w2, a.N, a.K2, n0, acc);
+    const float v = gemv_m1_finish<R>(acc, part, nullptr, n0, a.N, 0);
+    if (tid < R && n0 + tid < a.N) st_pub(&a.ypart[n0 + tid], v);
+    __syncthreads();
+  }
+  dual_ln_arrive_tail<PER>(a, nullptr, ready);
+  const int ngrp2 = (nx.N + R - 1) / R;
+  bool waited = false;
+  for (int grp = blockIdx.x; grp < ngrp2; grp += gridDim.x) {
+    const int n0 = grp * R;
+    float acc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = 0.f;
+    gemv_m1_accum<R>(nx.x, nx.w, nx.N, nx.K, n0, acc, -1, waited ? nullptr : ready, 1u);
+    waited = true;
+    const float v = gemv_m1_finish<R>(acc, part, nx.bias, n0, nx.N, nx.act);
+    if (tid < R && n0 + tid < nx.N) nx.y[n0 + tid] = f2bf(v);
+    __syncthreads();
+  }
+  // phase-B arrival: the last workgroup (every one has passed its wait) re-arms `ready` and cnt2
+  if (tid == 0) {
+    if (__hip_atomic_fetch_add(cnt2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+      __hip_atomic_store(cnt2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ready, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// kca_gemv_dual_ln's arguments (rows 4) plus the next projection ny = act(xn_out nw^T + nbias)
+// ([nN, N] weights, K = N) and `flags`: >= 64 zero-initialised words (re-armed by every launch).
+// Returns 10 when the grid cannot hold the phases in one residency round (the caller launches them
+// separately).
+KCA_API int kca_gemv_ln_gemv(const void* x1, const void* w1, int K1, const void* x2, const void* w2, int K2,
+                             const void* bias, float* ypart, unsigned int* cnt, const void* h, void* h_out,
+                             const void* gamma, const void* beta, float eps, void* xn_out, const void* gamma2,
+                             const void* beta2, void* xn2_out, int N, const void* nw, const void* nbias, void* ny,
+                             int nN, int act, unsigned int* flags, hipStream_t stream) {
+  if (N <= 0 || N % 8 || N > 16384 || K1 % 8 || K1 <= 0 || !ypart || !cnt || !gamma || !xn_out || !h || !h_out ||
+      !nw || !ny || nN <= 0 || !flags)
+    return 1;
+  if (x2 && (K2 <= 0 || K2 % 8 || !w2)) return 1;
+  if (xn2_out && !gamma2) return 1;
+  if (((uintptr_t)x1 | (uintptr_t)w1 | (uintptr_t)x2 | (uintptr_t)w2 | (uintptr_t)h | (uintptr_t)h_out |
+       (uintptr_t)gamma | (uintptr_t)beta | (uintptr_t)xn_out | (uintptr_t)ypart | (uintptr_t)gamma2 |
+       (uintptr_t)beta2 | (uintptr_t)xn2_out | (uintptr_t)nw) & 15)
+    return 2;
+  const DualLn a{(const bf16_t*)x1, (const bf16_t*)w1, (const bf16_t*)x2, (const bf16_t*)w2, (const bf16_t*)bias,
+                 ypart, cnt, (const bf16_t*)h, (bf16_t*)h_out, (const bf16_t*)gamma, (const bf16_t*)beta, eps,
+                 (bf16_t*)xn_out, (const bf16_t*)gamma2, (const bf16_t*)beta2, (bf16_t*)xn2_out,
+                 N, K1, x2 ? K2 : 0};
+  const GemvM1 nx{(const bf16_t*)xn_out, (const bf16_t*)nw, (const bf16_t*)nbias, (bf16_t*)ny, nN, N, act};
+  static int cu_count[64] = {};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  int& cus = cu_count[dev & 63];
+  if (!cus && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+  auto go = [&](auto per) -> int {
+    constexpr int PR = decltype(per)::value;
+    auto kern = gemv_ln_gemv_kernel<PR>;
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 256, 0) != hipSuccess || occ < 2) return 10;
+    const int grid = std::min((N + 3) / 4, cus * (occ - 1));
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, stream, a, nx, flags, flags + 32);
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+  };
+  return N <= 8192 ? go(std::integral_constant<int, 4>{}) : go(std::integral_constant<int, 8>{});
+}
+
 // --------------------------------------------------------------- sampling
 __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
 #pragma unroll
@@ -1350,9 +1443,17 @@ __device__ void find_bin_desc(const float* hist, float target, float* sh_excl, i
 }
 
 // One workgroup per row. ws: fp32 scratch [B, V] (processed logits).
-// rows of the multi-workgroup sampler (sample_mwg_kernel): greedy, or top-k in [1, 64]
+// rows of the multi-workgroup sampler (sample_mwg_kernel): greedy, top-k in [1, 64], or top-p only
+// (top-k off, top_p < 1). A top-p-only row's merge falls back -- out_ids[b] = -1 -- when its candidates
+// do not hold the nucleus; the one-workgroup kernel launched after it then takes the row (mwg_took).
 constexpr int MWG_KMAX_ = 64;  // (= MWG_KMAX below)
-__device__ __forceinline__ bool mwg_row(float T, int k) { return !(T > 0.f) || (k >= 1 && k <= MWG_KMAX_); }
+__device__ __forceinline__ bool mwg_row(float T, int k, float p) {
+  return !(T > 0.f) || (k >= 1 && k <= MWG_KMAX_) || (k <= 0 && p < 1.f);
+}
+__device__ __forceinline__ bool mwg_took(float T, int k, float p, const long long* out_ids, int b) {
+  if (!mwg_row(T, k, p)) return false;
+  return !(T > 0.f && k <= 0) || out_ids[b] >= 0;
+}
 
 __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(
     const void* __restrict__ logits, long long ld, int is_bf16, int V,
@@ -1373,7 +1474,9 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(
   __shared__ int iscan[SAMPLE_THREADS / 64];
   const int b = blockIdx.x, tid = threadIdx.x;
   // rows the multi-workgroup sampler took (launched first): decided on the device, as sample_reg_kernel
-  if (skip_mwg && mwg_row(temperature ? temperature[b] : 1.f, top_k ? top_k[b] : 0)) return;
+  if (skip_mwg && mwg_took(temperature ? temperature[b] : 1.f, top_k ? top_k[b] : 0, top_p ? top_p[b] : 1.f,
+                           out_ids, b))
+    return;
   const float T = temperature ? temperature[b] : 1.f;
   const float rp = rep_pen ? rep_pen[b] : 1.f;
   const int slot = slots ? slots[b] : b;
@@ -1659,7 +1762,7 @@ __global__ __launch_bounds__(NT) void sample_reg_kernel(
   __shared__ float selp[2];
   const int b = blockIdx.x, tid = threadIdx.x;
   const float T = temperature ? temperature[b] : 1.f;
-  if (skip_mwg && mwg_row(T, top_k ? top_k[b] : 0)) return;  // sample_mwg_kernel's row
+  if (skip_mwg && mwg_took(T, top_k ? top_k[b] : 0, top_p ? top_p[b] : 1.f, out_ids, b)) return;  // mwg's row
   const float rp = rep_pen ? rep_pen[b] : 1.f;
   const int slot = slots ? slots[b] : b;
   const uint8_t* sn = seen ? seen + (long long)slot * V : nullptr;
@@ -1965,10 +2068,12 @@ __global__ __launch_bounds__(NT) void sample_reg_kernel(
 // global top-k with its ties. The last workgroup to arrive (agent-scope release / acquire around one
 // counter per row) merges: global max and normaliser, the top-k select over the ~k..2k candidates,
 // top-p over the survivors (4-bit radix on the mass, as the register sampler), and the Philox
-// multinomial in index order. Rows with top_k == 0 or > 64 (top-p over the whole vocabulary) are
-// left to sample_reg_kernel, launched after this one with `skip_mwg` (each kernel takes exactly the
-// rows the other leaves: the choice is made on the device, so captured decode graphs keep working
-// whatever the requests' parameters are).
+// multinomial in index order. Top-p-only rows (top_k off) list each chunk's top CMAX / 2; the merge
+// samples them when the union -- every element >= T0 -- holds p of the row's mass (the nucleus is
+// then inside it), else it marks the row (out_ids = -1). Rows with top_k > 64, pure multinomial rows
+// and marked rows are left to sample_reg_kernel, launched after this one with `skip_mwg` (each kernel
+// takes exactly the rows the other leaves: the choice is made on the device, so captured decode
+// graphs keep working whatever the requests' parameters are).
 constexpr int MWG_G = 16, MWG_NT = 256, MWG_CMAX = 128, MWG_KMAX = MWG_KMAX_;
 constexpr int MWG_PART = 8;  // floats per workgroup partial: max, sum, t_g (key bits), count, argmax
 
@@ -2208,10 +2313,15 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
   const int g = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const float T = temperature ? temperature[b] : 1.f;
   const int k = top_k ? top_k[b] : 0;
-  if (!mwg_row(T, k)) return;  // sample_reg_kernel's row
+  const float pp = top_p ? top_p[b] : 1.f;
+  if (!mwg_row(T, k, pp)) return;  // sample_reg_kernel's row
   SSTAMP_DECL
   const bool st0 = g == 0 && b == 0;
   const bool greedy = !(T > 0.f);
+  // top-p only: each chunk lists its top KC (half the list, room for bf16 ties at the cut); the merge
+  // checks that the union -- every element >= T0 -- holds the nucleus's mass before it samples
+  const bool tponly = !greedy && k <= 0;
+  const int kc = tponly ? CMAX / 2 : k;
   const float rp = rep_pen ? rep_pen[b] : 1.f;
   const int slot = slots ? slots[b] : b;
   const uint8_t* sn = seen ? seen + (long long)slot * V : nullptr;
@@ -2290,7 +2400,7 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
   // per-thread maxima (k threads each hold an element >= it; one key per thread makes the radix
   // passes ~13x cheaper); when that keeps more than CMAX (top values bunched in few threads, e.g.
   // sorted logits), the exact k-th largest element.
-  int count = 0;
+  int count = 0, over = 0;
   uint32_t tg = 0;
   if (!greedy) {
     uint32_t xk[VPT];
@@ -2314,7 +2424,7 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
           mk[e] = fkey(v);
           mo[e] = v != -INFINITY;
         }
-        const uint32_t t = wave_kth_key<4>(k, mk, mo);
+        const uint32_t t = wave_kth_key<4>(kc, mk, mo);
         if (lane == 0) sel[0] = (int)t;
       }
       __syncthreads();
@@ -2345,9 +2455,10 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
     };
     scan();
     if (tot > CMAX) {  // uniform: every thread read the same iscan
-      tg = block_kth_key<VPT, MWG_NT / 64>(k, xk, xo, cnt16);
+      tg = block_kth_key<VPT, MWG_NT / 64>(kc, xk, xo, cnt16);
       scan();
     }
+    over = tot > CMAX;
     count = min(tot, CMAX);  // (> CMAX only with massive ties at t_g: the first CMAX by index stay)
 #pragma unroll
     for (int e = 0; e < VPT; ++e) {
@@ -2368,6 +2479,7 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
     mu[2] = tg;
     mu[3] = (unsigned)count;
     mu[4] = (unsigned)amg;
+    mu[5] = (unsigned)over;  // the list dropped elements tied at t_g (a top-p-only row falls back)
   }
   // ---- arrival: every wave's stores drained, one agent-scope release, one counter per row
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2394,13 +2506,14 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
   for (int q = 0; q < G; ++q) M = fmaxf(M, part[q * (MWG_PART + 2 * CMAX)]);
   float Z = 0.f;
   int best = 0x7fffffff;
-  uint32_t T0 = 0;
+  uint32_t T0 = 0, anyover = 0;
   for (int q = 0; q < G; ++q) {
     const float* pq = part + q * (MWG_PART + 2 * CMAX);
     if (pq[0] != -INFINITY) Z += pq[1] * __expf(pq[0] - M);
     const unsigned* pu = reinterpret_cast<const unsigned*>(pq);
     if (pq[0] == M && best == 0x7fffffff) best = (int)pu[4];  // first chunk holding the max
     T0 = max(T0, pu[2]);
+    anyover |= pu[5];
   }
   const float lZ = M + __logf(Z);
   if (greedy || M == -INFINITY) {
@@ -2464,7 +2577,6 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
     __syncthreads();
   }
   SSTAMP(8, sm0);
-  const float pp = top_p ? top_p[b] : 1.f;
   uint32_t c4[4] = {seeds ? 0u : (uint32_t)b, (uint32_t)step, (uint32_t)((unsigned long long)step >> 32), 0x5eedu};
   const unsigned long long sd = seeds ? seeds[b] : 0ull;
   philox4x32_10(c4, (uint32_t)sd, (uint32_t)(sd >> 32));
@@ -2485,7 +2597,7 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
       lk[e] = fkey(lv[e]);
       lm[e] = lo[e] ? __expf(lv[e] - M) : 0.f;
     }
-    uint32_t thr = block_kth_key<E, MWG_NT / 64>(k, lk, lo, cnt16);
+    uint32_t thr = tponly ? 0u : block_kth_key<E, MWG_NT / 64>(k, lk, lo, cnt16);
     SSTAMP(10, sm0);
     // top-p over the survivors: the smallest key whose descending inclusive mass reaches p * kept mass
     if (pp < 1.f) {
@@ -2511,11 +2623,11 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
           hv[4 * j] = t4.x; hv[4 * j + 1] = t4.y; hv[4 * j + 2] = t4.z; hv[4 * j + 3] = t4.w;
         }
         if (tid < 16) hist[16 * ((pass + 2) % 3) + tid] = 0.f;
-        if (target < 0.f) {
-          float t = 0.f;
+        if (target < 0.f) {  // p x the kept mass; top-p only: p x the whole row's (the merge checked
+          float t = 0.f;      // that the candidates hold it)
 #pragma unroll
           for (int j = 0; j < 16; ++j) t += hv[j];
-          target = pp * t;
+          target = pp * (tponly ? Z : t);
         }
         float run = 0.f;
         int dsel = -1;
@@ -2598,6 +2710,27 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
       if (out_kept) out_kept[b] = ktot;
     }
   };
+  if (tponly) {
+    // the candidates are every element >= T0 (no chunk list dropped a tie): the nucleus lies among
+    // them iff their mass reaches p x Z -- else the one-workgroup kernel launched next takes the row
+    float mc = 0.f;
+    for (int j = tid; j < nv; j += MWG_NT) mc += __expf(Lv[j] - M);
+    mc = wave_sum_dpp(mc);
+    __syncthreads();
+    if (lane == 0) red[wid] = mc;
+    __syncthreads();
+    float mt = 0.f;
+#pragma unroll
+    for (int w = 0; w < MWG_NT / 64; ++w) mt += red[w];
+    __syncthreads();  // (red is reused by the tail's scan)
+    if (anyover || !(mt > pp * Z)) {
+      if (tid == 0) out_ids[b] = -1;
+      return;
+    }
+    if (nv <= MWG_NT) tail(std::integral_constant<int, 1>{});
+    else tail(std::integral_constant<int, SPT>{});
+    return;
+  }
   // Narrowing: each wave's exact top-k key over its 512 compacted slots (wave sums only, the four
   // waves in parallel); T1 = the largest of them is <= the global k-th key (that wave alone holds k
   // elements >= T1), so the candidates >= T1 -- about 4k -- still hold the top k with its ties.
@@ -2745,7 +2878,7 @@ KCA_API int kca_sample_logits(const void* logits, long long ld, int is_bf16, int
     mwg = !(e && e[0] == '0');
   }
   // the large-vocabulary form (BLOOM's 250,880: 32 chunks of 7,840, 64 candidates each) runs its
-  // greedy and top-k rows here too; its top-p-only rows take the one-workgroup memory-pass kernel
+  // greedy, top-k and top-p-only rows here too; the rest take the one-workgroup memory-pass kernel
   const bool big = V > 50 * 1024;
   const int G = big ? 32 : MWG_G;
   const int CS = (V + G - 1) / G, vpt = (CS + MWG_NT - 1) / MWG_NT;

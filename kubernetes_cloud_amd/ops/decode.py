@@ -262,7 +262,7 @@ def decode_attn_out_ln(qkv, n_heads, kv_heads, head_dim, rot, interleaved, cos, 
 def gemv_dual_ln(x1: torch.Tensor, w1: torch.Tensor, x2: torch.Tensor | None, w2: torch.Tensor | None, bias,
                  h: torch.Tensor, gamma: torch.Tensor, beta, eps: float, ypart: torch.Tensor, cnt: torch.Tensor,
                  h_out: torch.Tensor, xn_out: torch.Tensor, gamma2: torch.Tensor | None = None, beta2=None,
-                 xn2_out: torch.Tensor | None = None, rows: int = 0) -> None:
+                 xn2_out: torch.Tensor | None = None, rows: int = 0, variant: int = 0) -> None:
     """Fused decode layer, tail (batch 1; ``kca_gemv_dual_ln``): y = x1 W1^T (+ x2 W2^T) + b, then
     h_out = h + y and xn_out = LayerNorm(h_out) in one launch -- GPT-J's out-projection + fc_out +
     parallel residual (two weight streams), a sequential-residual layer's out-projection or fc_out
@@ -273,7 +273,31 @@ def gemv_dual_ln(x1: torch.Tensor, w1: torch.Tensor, x2: torch.Tensor | None, w2
     _lib.call("kca_gemv_dual_ln", x1.data_ptr(), w1.data_ptr(), w1.shape[1], _lib.ptr(x2), _lib.ptr(w2),
               w2.shape[1] if w2 is not None else 0, _lib.ptr(bias), ypart.data_ptr(), cnt.data_ptr(), h.data_ptr(),
               h_out.data_ptr(), gamma.data_ptr(), _lib.ptr(beta), float(eps), xn_out.data_ptr(), _lib.ptr(gamma2),
-              _lib.ptr(beta2), _lib.ptr(xn2_out), w1.shape[0], int(rows), _lib.stream())
+              _lib.ptr(beta2), _lib.ptr(xn2_out), w1.shape[0], int(rows), int(variant), _lib.stream())
+
+
+def gemv_ln_gemv(x1: torch.Tensor, w1: torch.Tensor, x2: torch.Tensor | None, w2: torch.Tensor | None, bias,
+                 h: torch.Tensor, gamma: torch.Tensor, beta, eps: float, ypart: torch.Tensor, cnt: torch.Tensor,
+                 h_out: torch.Tensor, xn_out: torch.Tensor, nw: torch.Tensor, nbias, ny: torch.Tensor, act: int,
+                 flags: torch.Tensor, gamma2: torch.Tensor | None = None, beta2=None,
+                 xn2_out: torch.Tensor | None = None) -> bool:
+    """``gemv_dual_ln`` and the next projection ny = act(xn_out nw^T + nbias) in ONE launch
+    (``kca_gemv_ln_gemv``): the next weights stream while the LayerNorm tail finishes. ``flags``:
+    zero-initialised int32 [64] (re-armed by every launch). False: not launched (caller runs both)."""
+    if not (_lib.use_native(x1, w1, nw) and _lib.has("kca_gemv_ln_gemv") and nw.is_contiguous()
+            and ny.is_contiguous() and nw.shape[1] == w1.shape[0] and (nbias is None or nbias.dtype == torch.bfloat16)):
+        return False
+    rc = _lib.require().kca_gemv_ln_gemv(
+        x1.data_ptr(), w1.data_ptr(), w1.shape[1], _lib.ptr(x2), _lib.ptr(w2), w2.shape[1] if w2 is not None else 0,
+        _lib.ptr(bias), ypart.data_ptr(), cnt.data_ptr(), h.data_ptr(), h_out.data_ptr(), gamma.data_ptr(),
+        _lib.ptr(beta), float(eps), xn_out.data_ptr(), _lib.ptr(gamma2), _lib.ptr(beta2), _lib.ptr(xn2_out),
+        w1.shape[0], nw.data_ptr(), _lib.ptr(nbias), ny.data_ptr(), nw.shape[0], int(act), flags.data_ptr(),
+        _lib.stream())
+    if rc == 10:
+        return False
+    if rc != 0:
+        raise RuntimeError(f"kca_gemv_ln_gemv returned status {rc}")
+    return True
 
 
 def gemv_dual_ln_reference(x1, w1, x2, w2, bias, h, gamma, beta, eps):

@@ -570,6 +570,49 @@ def test_gemv_dual_ln_matches_reference(N, K1, K2, two_ln, rows):
     assert int(cnt.abs().sum()) == 0  # every counter re-armed
 
 
+@pytest.mark.parametrize("N,K1,K2,two_ln,nN,act", [(4096, 4096, 16384, False, 12288, 0),
+                                                  (6144, 6144, 24576, True, 18432, 0),
+                                                  (4096, 4096, 16384, False, 50400, 0),
+                                                  (14336, 1792, 0, False, 7168, 1),
+                                                  (14336, 7168, 0, False, 5376, 0)])
+def test_gemv_ln_gemv_matches_separate_launches(N, K1, K2, two_ln, nN, act):
+    """decode.hip gemv_ln_gemv_kernel: the dual-GEMV + residual + LayerNorm tail and the NEXT projection
+    (QKV, LM head, BLOOM TP=8 fc_in with GELU) in one launch give the two separate launches' values
+    (gemv_dual_ln, then skinny_linear on its LayerNorm output); repeated launches reuse the re-armed
+    flags."""
+    from kubernetes_cloud_amd.ops.gemv import skinny_linear
+    torch.manual_seed(4)
+    bf = dict(device=dev, dtype=torch.bfloat16)
+    x1 = torch.randn(1, K1, **bf)
+    w1 = torch.randn(N, K1, **bf) * K1 ** -0.5
+    x2 = torch.randn(1, K2, **bf) if K2 else None
+    w2 = torch.randn(N, K2, **bf) * K2 ** -0.5 if K2 else None
+    b, h = torch.randn(N, **bf), torch.randn(1, N, **bf)
+    gamma, beta = torch.randn(N, **bf), torch.randn(N, **bf)
+    g2, b2 = (torch.randn(N, **bf), torch.randn(N, **bf)) if two_ln else (None, None)
+    nw, nb = torch.randn(nN, N, **bf) * N ** -0.5, torch.randn(nN, **bf)
+    ypart = torch.empty(N, device=dev, dtype=torch.float32)
+    cnt = torch.zeros(32 * 65, device=dev, dtype=torch.int32)
+    flags = torch.zeros(64, device=dev, dtype=torch.int32)
+    h_r, xn_r = torch.empty(1, N, **bf), torch.empty(1, N, **bf)
+    xn2_r = torch.empty(1, N, **bf) if two_ln else None
+    dops.gemv_dual_ln(x1, w1, x2, w2, b, h, gamma, beta, 1e-5, ypart, cnt, h_r, xn_r, g2, b2, xn2_r)
+    y_r = skinny_linear(xn_r, nw, nb, act)
+    torch.cuda.synchronize()
+    for _ in range(3):
+        h_o, xn_o, y = torch.empty(1, N, **bf), torch.empty(1, N, **bf), torch.empty(1, nN, **bf)
+        xn2_o = torch.empty(1, N, **bf) if two_ln else None
+        assert dops.gemv_ln_gemv(x1, w1, x2, w2, b, h, gamma, beta, 1e-5, ypart, cnt, h_o, xn_o, nw, nb, y, act,
+                                 flags, g2, b2, xn2_o)
+        torch.cuda.synchronize()
+        assert torch.equal(h_o, h_r) and torch.equal(xn_o, xn_r)
+        if two_ln:
+            assert torch.equal(xn2_o, xn2_r)
+        assert (y.float() - y_r.float()).abs().max() <= 1e-2 * y_r.float().abs().max(), \
+            float((y.float() - y_r.float()).abs().max())
+    assert int(cnt.abs().sum()) == 0 and int(flags.abs().sum()) == 0  # every counter re-armed
+
+
 @pytest.mark.parametrize("PS", [0, 64])
 @pytest.mark.parametrize("L0", [40, 600])
 def test_decode_attention_gemv_fused_matches_separate(PS, L0):
@@ -779,6 +822,35 @@ def test_sample_multiworkgroup_distribution_and_mixed_rows():
         tie_incl = x >= x[keep].min()  # the kernels keep whole tie groups at a cut
         assert bool(tie_incl[ids[b]]), (b, rows[b])
         assert int(keep.sum()) <= int(out_kept[b]) <= int(tie_incl.sum()) + 1, (b, rows[b])
+
+
+@pytest.mark.parametrize("V", [50400, 250880])
+@pytest.mark.parametrize("peaked", [True, False])
+def test_sample_multiworkgroup_top_p_only(V, peaked):
+    """Top-p-only rows (top_k off) on the multi-workgroup sampler: a peaked row's nucleus lies inside the
+    chunk candidate lists and the merge samples it (kept set = the HF top-p mask, draw frequencies =
+    the renormalised nucleus); a flat row's nucleus does not (its candidates hold < p of the mass), the
+    merge marks the row and the one-workgroup kernel launched after it samples it -- same kept set."""
+    torch.manual_seed(11)
+    B, p = 2048, 0.9
+    base = torch.randn(V, device=dev) * (0.5 if peaked else 0.05)
+    if peaked:
+        peaks = torch.randperm(V, device=dev)[:24]
+        base[peaks] = 10.0 + 0.25 * torch.arange(24, device=dev, dtype=torch.float32)
+    base = base.to(torch.bfloat16).float()
+    logits = base[None].expand(B, V).contiguous().to(torch.bfloat16)
+    kept = torch.empty(B, dtype=torch.int32, device=dev)
+    ids, lp = dops.sample_logits(logits, **_params(B, 1.0, 0, p), seeds=torch.randint(0, 2**62, (B,), device=dev),
+                                 out_kept=kept)
+    keep = dops.keep_mask_reference(base, 0, p)
+    tie_incl = base >= base[keep].min()
+    assert bool(tie_incl[ids].all())
+    assert int(keep.sum()) <= int(kept.min()) and int(kept.max()) <= int(tie_incl.sum())
+    assert torch.allclose(lp, torch.log_softmax(base, -1)[ids], atol=1e-3)
+    if peaked:  # a few hundred kept tokens at most: the frequencies are testable
+        probs = torch.where(keep, base, torch.full_like(base, -float("inf"))).softmax(-1)
+        freq = torch.bincount(ids, minlength=V).float() / B
+        assert (freq - probs).abs().max() < 0.04
 
 
 def test_sample_multiworkgroup_wide_ties_take_the_block_path():
