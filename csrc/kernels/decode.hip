@@ -151,18 +151,9 @@ struct DecodeParams {
   // sin_t hold row b's RoPE angles at index b (not the position table); bit 1 -- tbl holds row b's
   // page ids at row b (not the slot's). Neither then waits for the length or the slot to arrive.
   int by_row;
-  // 1: the attention output is consumed inside the same launch (decode_attn_out_ln_kernel): stored
-  // write-through (agent scope), so a drain + counter add publishes it without a release fence
-  int pub_out;
 };
 
-__device__ __forceinline__ void store_out(const DecodeParams& p, long long i, float v) {
-  if (p.pub_out)
-    __hip_atomic_store(reinterpret_cast<unsigned short*>(p.out + i), f2bf(v), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  else
-    p.out[i] = f2bf(v);
-}
+__device__ __forceinline__ void store_out(const DecodeParams& p, long long i, float v) { p.out[i] = f2bf(v); }
 
 
 // diagnostic stamps (bench/decode_attn_bench.py --stamps): 8 per workgroup, 100 MHz clock
@@ -832,7 +823,7 @@ __global__ __launch_bounds__(256) void decode_attn_gemv_kernel(DecodeParams p, i
 // the out-projection / fc_out, the residual add and the next LayerNorm in one launch, no LayerNorm
 // launch of its own.
 template <int R, int PER>
-__global__ __launch_bounds__(256) void gemv_dual_ln_kernel(DualLn a, int split_loops, int no_tail) {
+__global__ __launch_bounds__(256) void gemv_dual_ln_kernel(DualLn a) {
   __shared__ float part[4][R];
   const int tid = threadIdx.x;
   // row groups g = blockIdx.x, + gridDim.x, ...: the grid is at most one residency round, so a
@@ -844,17 +835,14 @@ __global__ __launch_bounds__(256) void gemv_dual_ln_kernel(DualLn a, int split_l
     float acc[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r] = 0.f;
-    if (a.x2 && a.K1 % 2048 == 0 && !split_loops) {
-      gemv_m1_accum2<R>(a.x1, a.w1, a.K1, a.x2, a.w2, a.K2, a.N, n0, acc);
-    } else {
-      gemv_m1_accum<R>(a.x1, a.w1, a.N, a.K1, n0, acc);
-      if (a.x2) gemv_m1_accum<R>(a.x2, a.w2, a.N, a.K2, n0, acc);
-    }
+    // (the two streams as two loops: one loop across the seam measured 1.5 us slower at GPT-J / NeoX
+    // shapes, profiles/decode_launch_structure_ab_r5.txt)
+    gemv_m1_accum<R>(a.x1, a.w1, a.N, a.K1, n0, acc);
+    if (a.x2) gemv_m1_accum<R>(a.x2, a.w2, a.N, a.K2, n0, acc);
     const float v = gemv_m1_finish<R>(acc, part, nullptr, n0, a.N, 0);
     if (tid < R && n0 + tid < a.N) st_pub(&a.ypart[n0 + tid], v);
     __syncthreads();  // part[] is rewritten by the next group
   }
-  if (no_tail) return;  // timing A/B only (variant bit 2): the GEMV without arrival + LayerNorm
   dual_ln_arrive_tail<PER>(a);
 }
 
@@ -1100,11 +1088,14 @@ KCA_API int kca_decode_prep_attn_gemv(const void* qkv, long long ld, const void*
 // statistics). x2 / w2 nullable (K2 = 0: one GEMV -- a sequential-residual layer's out-projection or
 // fc_out). ypart: >= N fp32 words; cnt: 32 * (1 + kDualSub) zero-initialised unsigned counters
 // (re-armed by every launch).
-// rows: weight rows per workgroup (4 / 8 / 16; 0 = 4).
+// Geometry (bench/gemv_dual_ln_bench.py, profiles/decode_launch_structure_ab_r5.txt): 4 rows per
+// workgroup, except one short weight stream (K <= 2048: BLOOM TP=8's out-projection) at 16 rows --
+// a quarter of the arrivals for the same bytes (31.8 -> 23.8 us); the grid capped at one residency
+// round (8 workgroups per CU), the row groups looped.
 KCA_API int kca_gemv_dual_ln(const void* x1, const void* w1, int K1, const void* x2, const void* w2, int K2,
                              const void* bias, float* ypart, unsigned int* cnt, const void* h, void* h_out,
                              const void* gamma, const void* beta, float eps, void* xn_out, const void* gamma2,
-                             const void* beta2, void* xn2_out, int N, int rows, int variant, hipStream_t stream) {
+                             const void* beta2, void* xn2_out, int N, hipStream_t stream) {
   if (N <= 0 || N % 8 || N > 16384 || K1 % 8 || K1 <= 0 || !ypart || !cnt || !gamma || !xn_out || !h || !h_out)
     return 1;
   if (x2 && (K2 <= 0 || K2 % 8 || !w2)) return 1;
@@ -1117,243 +1108,21 @@ KCA_API int kca_gemv_dual_ln(const void* x1, const void* w1, int K1, const void*
                  ypart, cnt, (const bf16_t*)h, (bf16_t*)h_out, (const bf16_t*)gamma, (const bf16_t*)beta, eps,
                  (bf16_t*)xn_out, (const bf16_t*)gamma2, (const bf16_t*)beta2, (bf16_t*)xn2_out,
                  N, K1, x2 ? K2 : 0};
-  if (rows <= 0) rows = 4;  // (8 / 16 rows measured slower at every shape: bench/gemv_dual_ln_bench.py)
-  if (rows != 4 && rows != 8 && rows != 16) return 1;
-  // variant (A/B sweep, bench/gemv_dual_ln_bench.py): bit 0 -- grid capped at one residency round (8
-  // workgroups of 256 threads per CU, row groups looped); bit 1 -- the two weight streams as two loops;
-  // bit 2 -- no arrival / LayerNorm tail (timing only: h_out / xn_out are not written)
   static int cu_count[64] = {};
   int dev = 0;
   (void)hipGetDevice(&dev);
   int& cus = cu_count[dev & 63];
   if (!cus && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
-  const int ngrp = (N + rows - 1) / rows;
-  const dim3 grid((unsigned)((variant & 1) ? std::min(ngrp, 8 * cus) : ngrp));
-  const int split_loops = (variant >> 1) & 1, no_tail = (variant >> 2) & 1;
+  const int rows = (!x2 && K1 <= 2048) ? 16 : 4;
+  const dim3 grid((unsigned)std::min((N + rows - 1) / rows, 8 * cus));
   auto go = [&](auto rc) {
     constexpr int R = decltype(rc)::value;
-    if (N <= 8192) hipLaunchKernelGGL((gemv_dual_ln_kernel<R, 4>), grid, dim3(256), 0, stream, a, split_loops, no_tail);
-    else hipLaunchKernelGGL((gemv_dual_ln_kernel<R, 8>), grid, dim3(256), 0, stream, a, split_loops, no_tail);
+    if (N <= 8192) hipLaunchKernelGGL((gemv_dual_ln_kernel<R, 4>), grid, dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL((gemv_dual_ln_kernel<R, 8>), grid, dim3(256), 0, stream, a);
   };
   if (rows == 4) go(std::integral_constant<int, 4>{});
-  else if (rows == 8) go(std::integral_constant<int, 8>{});
   else go(std::integral_constant<int, 16>{});
   return hipGetLastError() == hipSuccess ? 0 : 2;
-}
-
-// Sequential-residual decode layer (batch 1: BLOOM, GPT-2, GPT-Neo), attention -> out-projection ->
-// residual + ln_2 as ONE launch. Workgroups [0, n_attn) run the RoPE + KV append + split-K
-// attention (their output stored write-through, pub_out) and count themselves on `done`; then EVERY
-// workgroup streams out-projection row groups, the first group's weights requested before it waits
-// for done == n_attn -- the attention chain runs under the first weight loads instead of in front
-// of a kernel boundary. The grid never exceeds one residency round (kca_decode_attn_out_ln sizes it
-// from the occupancy API with a margin), so the waiting workgroups cannot keep the attention ones
-// off the chip, whatever the dispatch order. The last arrival re-arms `done` (dual_ln_arrive_tail).
-template <int LPT, bool PAGED, bool ONLINE, int PER>
-__global__ __launch_bounds__(256) void decode_attn_out_ln_kernel(DecodeParams p, int nsplit, int n_attn, DualLn a,
-                                                                 unsigned int* done) {
-  constexpr int R = 4;
-  __shared__ float part[4][R];
-  const int bid = blockIdx.x, tid = threadIdx.x;
-  if (bid < n_attn) {
-    const int split = bid % nsplit, rest = bid / nsplit;
-    decode_attn_body<LPT, 1, PAGED, ONLINE>(p, split, rest % p.Hkv, rest / p.Hkv, nsplit);
-    // R1 publish: every storing wave drains its write-through stores, barrier, one counter add
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  const int ngrp = (a.N + R - 1) / R;
-  bool waited = false;
-  for (int grp = bid; grp < ngrp; grp += gridDim.x) {
-    const int n0 = grp * R;
-    float acc[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) acc[r] = 0.f;
-    gemv_m1_accum<R>(a.x1, a.w1, a.N, a.K1, n0, acc, -1, waited ? nullptr : done, (unsigned)n_attn);
-    waited = true;
-    const float v = gemv_m1_finish<R>(acc, part, nullptr, n0, a.N, 0);
-    if (tid < R && n0 + tid < a.N) st_pub(&a.ypart[n0 + tid], v);
-    __syncthreads();
-  }
-  dual_ln_arrive_tail<PER>(a, done);
-}
-
-// kca_decode_prep_attn's arguments (B = 1, H == Hkv) plus the out-projection tail of kca_gemv_dual_ln
-// (ow [N, H*D], bias, residual h, ln_2) and `done`: a zero-initialised counter (re-armed by every
-// launch). Returns 10 when the shape is outside it (the caller runs the two launches).
-KCA_API int kca_decode_attn_out_ln(const void* qkv, long long ld, const void* kc, const void* vc,
-                                   long long cs_slot, long long cs_head, long long cs_pos,
-                                   const int* slots, const int* kv_lens, void* out, long long o_bs,
-                                   float* ws, long long ws_floats, int B, int H, int Hkv, int D,
-                                   int max_kv, int chunk, float scale, const float* alibi, const int* tbl,
-                                   int tbl_stride, int ps_shift, int rot, int interleaved, const float* cos_t,
-                                   const float* sin_t, int window, int by_row, const void* ow, const void* obias,
-                                   float* ypart, unsigned int* cnt, const void* h, void* h_out, const void* gamma,
-                                   const void* beta, float eps, void* xn_out, int N, unsigned int* done,
-                                   hipStream_t stream) {
-  if (rot > D || (rot & 1) || (rot > 0 && (!cos_t || !sin_t))) return 8;
-  if (window < 0) return 9;
-  if (B != 1 || H != Hkv || D % 8 || D > 256 || max_kv <= 0 || !done || !ypart || !cnt || !h || !h_out ||
-      !gamma || !xn_out || N <= 0 || N % 8 || N > 16384 || o_bs != (long long)H * D)
-    return 10;
-  if (((uintptr_t)ow | (uintptr_t)out | (uintptr_t)h | (uintptr_t)h_out | (uintptr_t)gamma | (uintptr_t)beta |
-       (uintptr_t)xn_out | (uintptr_t)ypart) & 15)
-    return 10;
-  DecodeParams p{(const bf16_t*)qkv, ld, (const bf16_t*)kc, (const bf16_t*)vc, cs_slot, cs_head,
-                 cs_pos, slots, kv_lens, (bf16_t*)out, o_bs, nullptr, nullptr, alibi, tbl, tbl_stride, ps_shift,
-                 H, Hkv, D, chunk, scale, 1, rot, interleaved, cos_t, sin_t, g_decode_stamps, nullptr, window};
-  p.by_row = by_row;
-  p.pub_out = 1;
-  if (tbl && (ps_shift < 4 || ps_shift > 20 || tbl_stride <= 0)) return 5;
-  if (chunk <= 0) chunk = kca_decode_chunk(B, Hkv, max_kv);
-  if (tbl && chunk > 1024) return 6;
-  const int nsplit = (max_kv + chunk - 1) / chunk;
-  if (nsplit > 1024) return 7;
-  p.chunk = chunk;
-  if (nsplit > 1) {
-    if (!fanin_enabled()) return 10;
-    const long long cw = fanin_words(B, H);
-    const long long need = cw + (long long)B * H * nsplit * (D + 2);
-    if (!ws || ws_floats < need) return 4;
-    p.cnt = reinterpret_cast<unsigned int*>(ws);
-    p.ws_o = ws + cw;
-    p.ws_ml = p.ws_o + (long long)B * H * nsplit * D;
-  }
-  const DualLn a{(const bf16_t*)out, (const bf16_t*)ow, nullptr, nullptr, (const bf16_t*)obias, ypart, cnt,
-                 (const bf16_t*)h, (bf16_t*)h_out, (const bf16_t*)gamma, (const bf16_t*)beta, eps, (bf16_t*)xn_out,
-                 nullptr, nullptr, nullptr, N, H * D, 0};
-  const int n_attn = nsplit * Hkv * B;
-  const int ngrp = (N + 3) / 4;
-  static int cu_count[64] = {};
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  int& cus = cu_count[dev & 63];
-  if (!cus && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
-  int rc = 10;
-  auto go = [&](auto lpt, auto paged, auto online, auto per) {
-    constexpr int LPT = decltype(lpt)::value;
-    constexpr bool PG = decltype(paged)::value, ON = decltype(online)::value;
-    constexpr int PR = decltype(per)::value;
-    auto kern = decode_attn_out_ln_kernel<LPT, PG, ON, PR>;
-    const size_t lds = ON ? (size_t)4 * (2 + p.D) * sizeof(float) : (size_t)(p.chunk + 4 * p.D) * sizeof(float);
-    int occ = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 256, lds) != hipSuccess || occ < 2) return;
-    // one residency round with a margin of one workgroup per CU (the occupancy API can read one
-    // high: MI355X_MICROARCH.md, correctness boundaries)
-    const int grid = std::min(ngrp, cus * (occ - 1));
-    if (grid <= n_attn) return;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, stream, p, nsplit, n_attn, a, done);
-    rc = hipGetLastError() == hipSuccess ? 0 : 2;
-  };
-  const int nd = D / 8;
-  constexpr int TPB16 = 4 * (64 / 16), TPB32 = 4 * (64 / 32), TPB8 = 4 * (64 / 8), U = 4;
-  auto by_lpt = [&](auto lpt, int tpb) {
-    const bool online = p.chunk > tpb * U;
-    auto per = [&](auto pg, auto on) {
-      if (N <= 8192) go(lpt, pg, on, std::integral_constant<int, 4>{});
-      else go(lpt, pg, on, std::integral_constant<int, 8>{});
-    };
-    if (p.tbl) {
-      if (online) per(std::true_type{}, std::true_type{});
-      else per(std::true_type{}, std::false_type{});
-    } else {
-      if (online) per(std::false_type{}, std::true_type{});
-      else per(std::false_type{}, std::false_type{});
-    }
-  };
-  if (nd <= 8) by_lpt(std::integral_constant<int, 8>{}, TPB8);
-  else if (nd <= 16) by_lpt(std::integral_constant<int, 16>{}, TPB16);
-  else by_lpt(std::integral_constant<int, 32>{}, TPB32);
-  return rc;
-}
-
-// Fused decode tail + the NEXT projection in one launch (batch 1): phase A is gemv_dual_ln_kernel
-// (y = x1 W1^T (+ x2 W2^T), last arriver: residual + LayerNorm -> xn_out, published with `ready`);
-// phase B streams the next GEMV on xn_out (the next layer's QKV, or fc_in after an out-projection),
-// each workgroup requesting its first row group's weights BEFORE it waits for `ready` -- the tail and
-// the kernel boundary run under the next weight stream instead of in front of it. Phase-B waiters
-// never block phase-A work: the grid is at most one residency round (occupancy API, with a margin).
-// `ready` and `cnt2` (phase-B arrivals) are re-armed by the last workgroup through phase B.
-template <int PER>
-__global__ __launch_bounds__(256) void gemv_ln_gemv_kernel(DualLn a, GemvM1 nx, unsigned int* ready,
-                                                           unsigned int* cnt2) {
-  constexpr int R = 4;
-  __shared__ float part[4][R];
-  const int tid = threadIdx.x;
-  const int ngrp = (a.N + R - 1) / R;
-  for (int grp = blockIdx.x; grp < ngrp; grp += gridDim.x) {
-    const int n0 = grp * R;
-    float acc[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) acc[r] = 0.f;
-    gemv_m1_accum<R>(a.x1, a.w1, a.N, a.K1, n0, acc);
-    if (a.x2) gemv_m1_accum<R>(a.x2, a.w2, a.N, a.K2, n0, acc);
-    const float v = gemv_m1_finish<R>(acc, part, nullptr, n0, a.N, 0);
-    if (tid < R && n0 + tid < a.N) st_pub(&a.ypart[n0 + tid], v);
-    __syncthreads();
-  }
-  dual_ln_arrive_tail<PER>(a, nullptr, ready);
-  const int ngrp2 = (nx.N + R - 1) / R;
-  bool waited = false;
-  for (int grp = blockIdx.x; grp < ngrp2; grp += gridDim.x) {
-    const int n0 = grp * R;
-    float acc[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) acc[r] = 0.f;
-    gemv_m1_accum<R>(nx.x, nx.w, nx.N, nx.K, n0, acc, -1, waited ? nullptr : ready, 1u);
-    waited = true;
-    const float v = gemv_m1_finish<R>(acc, part, nx.bias, n0, nx.N, nx.act);
-    if (tid < R && n0 + tid < nx.N) nx.y[n0 + tid] = f2bf(v);
-    __syncthreads();
-  }
-  // phase-B arrival: the last workgroup (every one has passed its wait) re-arms `ready` and cnt2
-  if (tid == 0) {
-    if (__hip_atomic_fetch_add(cnt2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
-      __hip_atomic_store(cnt2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(ready, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-// kca_gemv_dual_ln's arguments (rows 4) plus the next projection ny = act(xn_out nw^T + nbias)
-// ([nN, N] weights, K = N) and `flags`: >= 64 zero-initialised words (re-armed by every launch).
-// Returns 10 when the grid cannot hold the phases in one residency round (the caller launches them
-// separately).
-KCA_API int kca_gemv_ln_gemv(const void* x1, const void* w1, int K1, const void* x2, const void* w2, int K2,
-                             const void* bias, float* ypart, unsigned int* cnt, const void* h, void* h_out,
-                             const void* gamma, const void* beta, float eps, void* xn_out, const void* gamma2,
-                             const void* beta2, void* xn2_out, int N, const void* nw, const void* nbias, void* ny,
-                             int nN, int act, unsigned int* flags, hipStream_t stream) {
-  if (N <= 0 || N % 8 || N > 16384 || K1 % 8 || K1 <= 0 || !ypart || !cnt || !gamma || !xn_out || !h || !h_out ||
-      !nw || !ny || nN <= 0 || !flags)
-    return 1;
-  if (x2 && (K2 <= 0 || K2 % 8 || !w2)) return 1;
-  if (xn2_out && !gamma2) return 1;
-  if (((uintptr_t)x1 | (uintptr_t)w1 | (uintptr_t)x2 | (uintptr_t)w2 | (uintptr_t)h | (uintptr_t)h_out |
-       (uintptr_t)gamma | (uintptr_t)beta | (uintptr_t)xn_out | (uintptr_t)ypart | (uintptr_t)gamma2 |
-       (uintptr_t)beta2 | (uintptr_t)xn2_out | (uintptr_t)nw) & 15)
-    return 2;
-  const DualLn a{(const bf16_t*)x1, (const bf16_t*)w1, (const bf16_t*)x2, (const bf16_t*)w2, (const bf16_t*)bias,
-                 ypart, cnt, (const bf16_t*)h, (bf16_t*)h_out, (const bf16_t*)gamma, (const bf16_t*)beta, eps,
-                 (bf16_t*)xn_out, (const bf16_t*)gamma2, (const bf16_t*)beta2, (bf16_t*)xn2_out,
-                 N, K1, x2 ? K2 : 0};
-  const GemvM1 nx{(const bf16_t*)xn_out, (const bf16_t*)nw, (const bf16_t*)nbias, (bf16_t*)ny, nN, N, act};
-  static int cu_count[64] = {};
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  int& cus = cu_count[dev & 63];
-  if (!cus && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
-  auto go = [&](auto per) -> int {
-    constexpr int PR = decltype(per)::value;
-    auto kern = gemv_ln_gemv_kernel<PR>;
-    int occ = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 256, 0) != hipSuccess || occ < 2) return 10;
-    const int grid = std::min((N + 3) / 4, cus * (occ - 1));
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, stream, a, nx, flags, flags + 32);
-    return hipGetLastError() == hipSuccess ? 0 : 2;
-  };
-  return N <= 8192 ? go(std::integral_constant<int, 4>{}) : go(std::integral_constant<int, 8>{});
 }
 
 // --------------------------------------------------------------- sampling

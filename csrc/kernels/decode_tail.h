@@ -35,12 +35,10 @@ struct DualLn {
 };
 
 // Arrival of every workgroup of a fused decode tail launch, then -- in the last one -- h' = bf16(h + y
-// + bias) and its LayerNorm(s) (DualLn). ypart holds y; `rearm`: one more counter the last workgroup
-// zeroes (every workgroup has passed its wait on it by then); `ready`: set to 1 once h_out / xn_out
-// are published (agent-scope release) for consumers inside the same launch. 256-thread workgroups; PER: h' register
-// slices of 2048 columns (N <= 256 * 8 * PER).
+// + bias) and its LayerNorm(s) (DualLn). ypart holds y. 256-thread workgroups; PER: h' register slices
+// of 2048 columns (N <= 256 * 8 * PER).
 template <int PER>
-__device__ void dual_ln_arrive_tail(const DualLn& a, unsigned int* rearm = nullptr, unsigned int* ready = nullptr) {
+__device__ void dual_ln_arrive_tail(const DualLn& a) {
   __shared__ float red[16];
   __shared__ int s_last;
   const int tid = threadIdx.x;
@@ -64,7 +62,6 @@ __device__ void dual_ln_arrive_tail(const DualLn& a, unsigned int* rearm = nullp
     }
     if (last) {
       __hip_atomic_store(a.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (rearm) __hip_atomic_store(rearm, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -138,15 +135,6 @@ __device__ void dual_ln_arrive_tail(const DualLn& a, unsigned int* rearm = nullp
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = hv[i][j] * gm[j] + bt[j];
       store8(a.xn2_out + k, o);
-    }
-  }
-  if (ready) {  // in-launch consumers of xn_out (gemv_ln_gemv_kernel): drain, release, flag
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(ready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }

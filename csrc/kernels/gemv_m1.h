@@ -29,27 +29,9 @@ __device__ __forceinline__ uint4 ld_w16(const bf16_t* p) {
 // w, lane l) owns positions i*2048 + w*512 + l*8), R weight rows, 16 / R slabs of loads in flight --
 // the gemv1_kernel<R, false, 1> loop (gemv.hip) as a device function, so that a fused kernel can
 // run it on a subset of its workgroups. Not reduced across lanes: call gemv_m1_finish.
-// In-launch hand-off (cdna_hip_programming.md Guideline 16): wait until *cnt >= target -- one lane
-// polls relaxed (bounded: a lost count costs a wrong token, never a hung queue), then ONE agent-scope
-// acquire and a barrier before the workgroup's loads of the published bytes.
-__device__ __forceinline__ void wait_count(const unsigned int* cnt, unsigned target) {
-  if (threadIdx.x == 0) {
-    for (int it = 0; it < (1 << 22); ++it) {
-      if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
-      __builtin_amdgcn_s_sleep(2);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-}
-
 template <int R>
 __device__ __forceinline__ void gemv_m1_accum(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, int N,
-                                              int K, int n0, float (&acc)[R], long long ldw = -1,
-                                              const unsigned int* wait_cnt = nullptr, unsigned wait_target = 0) {
-  // wait_cnt: x is produced inside this launch -- the first slabs' WEIGHT loads are issued, then the
-  // workgroup waits for x's publication (wait_count), then loads x: the wait overlaps the weight stream
+                                              int K, int n0, float (&acc)[R], long long ldw = -1) {
   if (ldw < 0) ldw = K;  // row stride of w (a K-chunk of a wider matrix: the full row length)
   constexpr int U = R >= 16 ? 1 : (R >= 8 ? 2 : 4);  // 16 weight loads in flight per lane, any R
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -74,7 +56,6 @@ __device__ __forceinline__ void gemv_m1_accum(const bf16_t* __restrict__ x, cons
         if (k < K && rv[r]) wv[u][r] = ld_w16(wr[r] + k);
       }
     }
-    if (wait_cnt && i0 == 0) wait_count(wait_cnt, wait_target);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int k = (i0 + u) * 2048 + kl;
@@ -84,63 +65,6 @@ __device__ __forceinline__ void gemv_m1_accum(const bf16_t* __restrict__ x, cons
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if ((i0 + u) * 2048 + kl >= K) continue;
-      const uint32_t xq[4] = {xr[u].x, xr[u].y, xr[u].z, xr[u].w};
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const uint32_t q[4] = {wv[u][r].x, wv[u][r].y, wv[u][r].z, wv[u][r].w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          acc[r] = fmaf(__uint_as_float(q[j] << 16), __uint_as_float(xq[j] << 16), acc[r]);
-          acc[r] = fmaf(__uint_as_float(q[j] & 0xffff0000u), __uint_as_float(xq[j] & 0xffff0000u), acc[r]);
-        }
-      }
-    }
-  }
-}
-
-// gemv_m1_accum over two weight streams as ONE K range: acc[r] += W1[n0 + r, :K1] . x1 + W2[n0 + r, :K2] . x2
-// (the fused decode tail's out-projection + fc_out). Slabs of 2048 columns run across the seam, so the
-// second stream's first loads are in flight while the first one's last are landing -- two separate
-// loops drain at the seam (a K1 = 4096 first stream fills only half of the U slabs). K1 % 2048 == 0.
-template <int R>
-__device__ __forceinline__ void gemv_m1_accum2(const bf16_t* __restrict__ x1, const bf16_t* __restrict__ w1, int K1,
-                                               const bf16_t* __restrict__ x2, const bf16_t* __restrict__ w2, int K2,
-                                               int N, int n0, float (&acc)[R]) {
-  constexpr int U = R >= 16 ? 1 : (R >= 8 ? 2 : 4);  // 16 weight loads in flight per lane, any R
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int kl = wid * 512 + lane * 8;
-  const bf16_t* wr1[R];
-  const bf16_t* wr2[R];
-  bool rv[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    rv[r] = n0 + r < N;
-    const long long row = rv[r] ? n0 + r : 0;
-    wr1[r] = w1 + row * K1;
-    wr2[r] = w2 + row * K2;
-  }
-  const int S1 = K1 / 2048, NI = S1 + (K2 + 2047) / 2048;
-  for (int i0 = 0; i0 < NI; i0 += U) {
-    uint4 wv[U][R];
-    uint4 xr[U];
-    bool ok[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int i = i0 + u;
-      const bool first = i < S1;
-      const int k = (first ? i : i - S1) * 2048 + kl;
-      ok[u] = i < NI && (first || k < K2);
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        wv[u][r] = make_uint4(0u, 0u, 0u, 0u);
-        if (ok[u] && rv[r]) wv[u][r] = ld_w16((first ? wr1[r] : wr2[r]) + k);
-      }
-      xr[u] = make_uint4(0u, 0u, 0u, 0u);
-      if (ok[u]) xr[u] = *reinterpret_cast<const uint4*>((first ? x1 : x2) + k);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (!ok[u]) continue;
       const uint32_t xq[4] = {xr[u].x, xr[u].y, xr[u].z, xr[u].w};
 #pragma unroll
       for (int r = 0; r < R; ++r) {

@@ -388,11 +388,6 @@ class ModelRunner:
                                or all(x.eps == blk.ln_1.eps for x, blk in zip(ln2, model.h)))
                           and (self._layer_kind == "seq"
                                or (self.H == self.Hkv and self.D % 8 == 0 and 64 < self.D <= 256)))
-        # _chain: each tail launch also runs the projection that consumes its LayerNorm (next QKV / LM head /
-        # BLOOM's fc_in: ops/decode.py gemv_ln_gemv); _attn_out_fused: BLOOM's attention + out-projection +
-        # ln_2 in one launch (decode_attn_out_ln) instead of attention, then out-projection chained to fc_in
-        self._chain = True
-        self._attn_out_fused = True
         self._fz: dict = {}
         self._outbufs: dict = {}
         self._chain_src = None
@@ -516,10 +511,7 @@ class ModelRunner:
             fz = self._fz["b1"] = {
                 "g": torch.empty(1, f, **z), "h": torch.empty(1, d, **z), "xn": torch.empty(1, d, **z),
                 "xn2": torch.empty(1, d, **z), "ypart": torch.empty(d, device=self.device, dtype=torch.float32),
-                "cnt": torch.zeros(32 * 65, device=self.device, dtype=torch.int32), "bias": biases,
-                "done": torch.zeros(32, device=self.device, dtype=torch.int32),
-                "flags": torch.zeros(64, device=self.device, dtype=torch.int32),
-                "qkv": torch.empty(1, self.model.h[0].attn.qkv.weight.shape[0], **z)}
+                "cnt": torch.zeros(32 * 65, device=self.device, dtype=torch.int32), "bias": biases}
         return fz
 
     def _desc_args(self, cos, sin, tbl):
@@ -558,21 +550,13 @@ class ModelRunner:
         hb, xb, x2b, g = fz["h"], fz["xn"], fz["xn2"], fz["g"]
         tbl = self.cache.table_on(self.device)
         cos, sin, tbl, by_row = self._desc_args(self.cos, self.sin, tbl)
-        head = self._head_for_chain()
-        qkv = None  # this layer's QKV when the previous layer's tail launch already produced it
         for li, blk in enumerate(m.h):
             at, mlp = blk.attn, blk.mlp
             act = 1 if mlp.approx in ("tanh", True) else 2
             kc, vc = self.cache.k[li], self.cache.v[li]
             nxt = m.h[li + 1] if li + 1 < len(m.h) else None
             nln = nxt.ln_1 if nxt is not None else m.ln_f
-            if qkv is None:
-                qkv = skinny_linear(xn, at.qkv.weight, at.qkv.bias)
-            # the projection that consumes this layer's closing LayerNorm: the next QKV, or the LM head
-            if nxt is not None:
-                nproj = (nxt.attn.qkv.weight, nxt.attn.qkv.bias, fz["qkv"])
-            else:
-                nproj = head
+            qkv = skinny_linear(xn, at.qkv.weight, at.qkv.bias)
             if kind == "seq" and self._tp_ar is not None:
                 # TP rank: partial projections, each closed by all-reduce + bias + residual + LayerNorm
                 ar = self._tp_ar
@@ -584,32 +568,20 @@ class ModelRunner:
                 f = skinny_linear(x2b, mlp.fc_in.weight, mlp.fc_in.bias, act, out=g)
                 ar.res_ln(skinny_linear(f, mlp.fc_out.weight), mlp.fc_out.bias, hb, hb, nln.weight, nln.bias,
                           nln.eps, xb)
-                h, xn, qkv = hb, xb, None
+                h, xn = hb, xb
                 continue
             if kind == "seq":
-                # attention + out-projection + residual + ln_2 (one launch where the fused kernel covers
-                # the shape), then fc_in (+ GELU), then fc_out + residual + next ln_1
-                f = None
-                if not (self._attn_out_fused and dops.decode_attn_out_ln(
-                        qkv, self.H, self.Hkv, self.D, self.rot, cfg.rotary_interleaved, cos, sin, pos, slots, kc,
-                        vc, kv_lens, max_kv, at.scale, at.alibi, obuf, ws, tbl, at.window, by_row, at.out.weight,
-                        at.out.bias, h, blk.ln_2.weight, blk.ln_2.bias, blk.ln_2.eps, fz["ypart"], fz["cnt"], hb,
-                        x2b, fz["done"])):
-                    o = dops.decode_prep_attention(qkv, self.H, self.Hkv, self.D, self.rot,
-                                                   cfg.rotary_interleaved, cos, sin, pos, slots, kc, vc, kv_lens,
-                                                   max_kv, at.scale, at.alibi, out=obuf, ws=ws, block_table=tbl,
-                                                   window=at.window, by_row=by_row)
-                    if self._chain and dops.gemv_ln_gemv(
-                            o, at.out.weight, None, None, at.out.bias, h, blk.ln_2.weight, blk.ln_2.bias,
-                            blk.ln_2.eps, fz["ypart"], fz["cnt"], hb, x2b, mlp.fc_in.weight, mlp.fc_in.bias, g, act,
-                            fz["flags"]):
-                        f = g
-                    else:
-                        dops.gemv_dual_ln(o, at.out.weight, None, None, at.out.bias, h, blk.ln_2.weight,
-                                          blk.ln_2.bias, blk.ln_2.eps, fz["ypart"], fz["cnt"], hb, x2b)
-                if f is None:
-                    f = skinny_linear(x2b, mlp.fc_in.weight, mlp.fc_in.bias, act, out=g)
-                qkv = self._tail(f, mlp.fc_out.weight, None, None, mlp.fc_out.bias, hb, nln, fz, hb, xb, nproj)
+                # attention, out-projection + residual + ln_2, fc_in (+ GELU), fc_out + residual + next ln_1
+                # (a fused attention + out-projection launch and a tail launch chained to the next
+                # projection both measured slower: profiles/decode_launch_structure_ab_r5.txt)
+                o = dops.decode_prep_attention(qkv, self.H, self.Hkv, self.D, self.rot, cfg.rotary_interleaved,
+                                               cos, sin, pos, slots, kc, vc, kv_lens, max_kv, at.scale, at.alibi,
+                                               out=obuf, ws=ws, block_table=tbl, window=at.window, by_row=by_row)
+                dops.gemv_dual_ln(o, at.out.weight, None, None, at.out.bias, h, blk.ln_2.weight, blk.ln_2.bias,
+                                  blk.ln_2.eps, fz["ypart"], fz["cnt"], hb, x2b)
+                f = skinny_linear(x2b, mlp.fc_in.weight, mlp.fc_in.bias, act, out=g)
+                dops.gemv_dual_ln(f, mlp.fc_out.weight, None, None, mlp.fc_out.bias, hb, nln.weight, nln.bias,
+                                  nln.eps, fz["ypart"], fz["cnt"], hb, xb)
                 h, xn = hb, xb
                 continue
             # parallel residual: attention + fc_in (of ln_2's output for NeoX) in one launch
@@ -621,48 +593,13 @@ class ModelRunner:
                     return None
                 raise RuntimeError("fused decode layer: shape support changed between layers")
             two = kind == "neox" and nxt is not None
-            qkv = self._tail(obuf, at.out.weight, g, mlp.fc_out.weight, fz["bias"][li], h, nln, fz, hb, xb, nproj,
-                             *((nxt.ln_2.weight, nxt.ln_2.bias, x2b) if two else ()))
+            dops.gemv_dual_ln(obuf, at.out.weight, g, mlp.fc_out.weight, fz["bias"][li], h, nln.weight, nln.bias,
+                              nln.eps, fz["ypart"], fz["cnt"], hb, xb,
+                              *((nxt.ln_2.weight, nxt.ln_2.bias, x2b) if two else ()))
             h, xn, xn2 = hb, xb, (x2b if two else None)
-        if qkv is not None:  # the last tail launch computed the logits
-            return head[3](qkv)
         if m.lm_head is None:
             return skinny_linear(xn, m.wte.weight)
         return self._lin(m.lm_head, xn)
-
-    def _head_for_chain(self):
-        """(weight, bias, logits buffer, finish) of the LM head for the last layer's chained tail launch, or
-        None (TP heads: the gather runs after the local projection, so the local logits chain too)."""
-        if not self._chain:
-            return None
-        m = self.model
-        from ..parallel.tensor_parallel import ParallelLMHead, gather_last_dim
-        lm = m.lm_head
-        if lm is None:
-            w, b, fin = m.wte.weight, None, (lambda y: y)
-        elif isinstance(lm, ParallelLMHead):
-            w, b, fin = lm.local_weight(), lm.bias, (lambda y, g=lm.group: gather_last_dim(y, g))
-        elif type(lm) is torch.nn.Linear or hasattr(lm, "weight") and not hasattr(lm, "group"):
-            w, b, fin = lm.weight, lm.bias, (lambda y: y)
-        else:
-            return None
-        st = self._fz.setdefault("logits", {})
-        buf = st.get(w.shape[0])
-        if buf is None:
-            buf = st[w.shape[0]] = torch.empty(1, w.shape[0], device=self.device, dtype=self.dtype)
-        return (w, b, buf, fin)
-
-    def _tail(self, x1, w1, x2, w2, bias, h, nln, fz, hb, xb, nproj, gamma2=None, beta2=None, xn2=None):
-        """A layer's closing projection(s) + residual + next LayerNorm, chained with the projection that
-        consumes the LayerNorm (nproj: next layer's QKV or the LM head) when the two-phase kernel covers it.
-        Returns nproj's output, or None when only the tail ran."""
-        if self._chain and nproj is not None and dops.gemv_ln_gemv(
-                x1, w1, x2, w2, bias, h, nln.weight, nln.bias, nln.eps, fz["ypart"], fz["cnt"], hb, xb,
-                nproj[0], nproj[1], nproj[2], 0, fz["flags"], gamma2, beta2, xn2):
-            return nproj[2]
-        dops.gemv_dual_ln(x1, w1, x2, w2, bias, h, nln.weight, nln.bias, nln.eps, fz["ypart"], fz["cnt"], hb, xb,
-                          gamma2, beta2, xn2)
-        return None
 
     def _layers_decode(self, tokens, pos, slots, kv_lens, max_kv, ws, obuf):
         m, cfg = self.model, self.cfg

@@ -102,8 +102,7 @@ _SIGS = {
     "kca_dense_to_phase_nhwc": [P, P, I, I, I, I, P],
     "kca_col2im2x2_nhwc": [P, P, I, I, I, I, P],
     "kca_pad_br_nhwc": [P, P, I, I, I, I, P],
-    "kca_gemv_dual_ln": [P, P, I, P, P, I, P, P, P, P, P, P, P, F, P, P, P, P, I, I, I, P],
-    "kca_gemv_ln_gemv": [P, P, I, P, P, I, P, P, P, P, P, P, P, F, P, P, P, P, I, P, P, P, I, I, P, P],
+    "kca_gemv_dual_ln": [P, P, I, P, P, I, P, P, P, P, P, P, P, F, P, P, P, P, I, P],
     "kca_sample_logits": [P, LL, I, I, I, P, P, P, P, P, P, P, I, P, LL, P, P, P, P, P, P],
 }
 
@@ -111,9 +110,6 @@ _SIGS = {
 # fused decode layer (batch 1): kca_decode_prep_attn's arguments (minus the stream), then the fc_in
 # GEMV's x, W, bias, y, N, K, act, then the stream
 _SIGS["kca_decode_prep_attn_gemv"] = _SIGS["kca_decode_prep_attn"][:-2] + [P, P, P, P, I, I, I, I, P]
-# kca_decode_prep_attn's arguments up to by_row, then ow, obias, ypart, cnt, h, h_out, gamma, beta, eps,
-# xn_out, N, done, stream
-_SIGS["kca_decode_attn_out_ln"] = _SIGS["kca_decode_prep_attn"][:-1] + [P, P, P, P, P, P, P, P, F, P, I, P, P]
 
 
 def _load():

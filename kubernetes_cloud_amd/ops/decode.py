@@ -224,80 +224,20 @@ def decode_prep_attention_gemv(qkv, n_heads, kv_heads, head_dim, rot, interleave
     return True
 
 
-def decode_attn_out_ln(qkv, n_heads, kv_heads, head_dim, rot, interleaved, cos, sin, pos, slots, k_cache, v_cache,
-                       kv_lens, max_kv, scale, alibi, out, ws, block_table, window, by_row: int,
-                       ow: torch.Tensor, obias, h: torch.Tensor, gamma: torch.Tensor, beta, eps: float,
-                       ypart: torch.Tensor, cnt: torch.Tensor, h_out: torch.Tensor, xn_out: torch.Tensor,
-                       done: torch.Tensor) -> bool:
-    """Sequential-residual decode layer, attention -> out-projection -> residual + ln_2 as ONE launch
-    (batch 1; csrc/kernels/decode.hip decode_attn_out_ln_kernel): ``decode_prep_attention`` into
-    ``out``, then h_out = h + out ow^T + obias and xn_out = LayerNorm(h_out), the out-projection's first
-    weight loads in flight while the attention runs. ``done``: zero-initialised int32 (re-armed by
-    every launch). Returns False (nothing launched) outside the fused shapes."""
-    B = qkv.shape[0]
-    _, Hkv, L, D = k_cache.shape
-    if not (_lib.use_native(qkv, k_cache, ow, h) and _lib.has("kca_decode_attn_out_ln") and B == 1
-            and ow.is_contiguous() and out.is_contiguous() and (obias is None or obias.dtype == torch.bfloat16)):
-        return False
-    tbl, tstride, shift = _table_args(block_table, k_cache)
-    chunk = decode_chunk(B, Hkv, max_kv)
-    need = decode_ws_floats(B, n_heads, Hkv, D, max_kv, chunk)
-    if need and (ws is None or ws.numel() < need):
-        return False
-    rc = _lib.require().kca_decode_attn_out_ln(
-        qkv.data_ptr(), qkv.stride(0), k_cache.data_ptr(), v_cache.data_ptr(), k_cache.stride(0), k_cache.stride(1),
-        k_cache.stride(2), slots.data_ptr(), kv_lens.data_ptr(), out.data_ptr(), out.stride(0), _lib.ptr(ws),
-        ws.numel() if ws is not None else 0, B, n_heads, Hkv, D, max_kv, chunk, float(scale), _lib.ptr(alibi), tbl,
-        tstride, shift, rot, int(interleaved), _lib.ptr(cos), _lib.ptr(sin), int(window), int(by_row),
-        ow.data_ptr(), _lib.ptr(obias), ypart.data_ptr(), cnt.data_ptr(), h.data_ptr(), h_out.data_ptr(),
-        gamma.data_ptr(), _lib.ptr(beta), float(eps), xn_out.data_ptr(), ow.shape[0], done.data_ptr(),
-        _lib.stream())
-    if rc == 10:
-        return False
-    if rc != 0:
-        raise RuntimeError(f"kca_decode_attn_out_ln returned status {rc}")
-    return True
-
-
 def gemv_dual_ln(x1: torch.Tensor, w1: torch.Tensor, x2: torch.Tensor | None, w2: torch.Tensor | None, bias,
                  h: torch.Tensor, gamma: torch.Tensor, beta, eps: float, ypart: torch.Tensor, cnt: torch.Tensor,
                  h_out: torch.Tensor, xn_out: torch.Tensor, gamma2: torch.Tensor | None = None, beta2=None,
-                 xn2_out: torch.Tensor | None = None, rows: int = 0, variant: int = 0) -> None:
+                 xn2_out: torch.Tensor | None = None) -> None:
     """Fused decode layer, tail (batch 1; ``kca_gemv_dual_ln``): y = x1 W1^T (+ x2 W2^T) + b, then
     h_out = h + y and xn_out = LayerNorm(h_out) in one launch -- GPT-J's out-projection + fc_out +
     parallel residual (two weight streams), a sequential-residual layer's out-projection or fc_out
     (``x2`` None), and with ``gamma2`` the second LayerNorm of the same h_out into ``xn2_out`` (GPT-NeoX:
     ln_1 and ln_2 of one residual stream share the statistics). ``ypart``: >= N fp32 words;
-    ``cnt``: zero-initialised int32 [32 * 65] arrival counters. N <= 16384. ``rows``: weight rows per
-    workgroup (4 / 8 / 16; 0 = chosen by shape)."""
+    ``cnt``: zero-initialised int32 [32 * 65] arrival counters. N <= 16384."""
     _lib.call("kca_gemv_dual_ln", x1.data_ptr(), w1.data_ptr(), w1.shape[1], _lib.ptr(x2), _lib.ptr(w2),
               w2.shape[1] if w2 is not None else 0, _lib.ptr(bias), ypart.data_ptr(), cnt.data_ptr(), h.data_ptr(),
               h_out.data_ptr(), gamma.data_ptr(), _lib.ptr(beta), float(eps), xn_out.data_ptr(), _lib.ptr(gamma2),
-              _lib.ptr(beta2), _lib.ptr(xn2_out), w1.shape[0], int(rows), int(variant), _lib.stream())
-
-
-def gemv_ln_gemv(x1: torch.Tensor, w1: torch.Tensor, x2: torch.Tensor | None, w2: torch.Tensor | None, bias,
-                 h: torch.Tensor, gamma: torch.Tensor, beta, eps: float, ypart: torch.Tensor, cnt: torch.Tensor,
-                 h_out: torch.Tensor, xn_out: torch.Tensor, nw: torch.Tensor, nbias, ny: torch.Tensor, act: int,
-                 flags: torch.Tensor, gamma2: torch.Tensor | None = None, beta2=None,
-                 xn2_out: torch.Tensor | None = None) -> bool:
-    """``gemv_dual_ln`` and the next projection ny = act(xn_out nw^T + nbias) in ONE launch
-    (``kca_gemv_ln_gemv``): the next weights stream while the LayerNorm tail finishes. ``flags``:
-    zero-initialised int32 [64] (re-armed by every launch). False: not launched (caller runs both)."""
-    if not (_lib.use_native(x1, w1, nw) and _lib.has("kca_gemv_ln_gemv") and nw.is_contiguous()
-            and ny.is_contiguous() and nw.shape[1] == w1.shape[0] and (nbias is None or nbias.dtype == torch.bfloat16)):
-        return False
-    rc = _lib.require().kca_gemv_ln_gemv(
-        x1.data_ptr(), w1.data_ptr(), w1.shape[1], _lib.ptr(x2), _lib.ptr(w2), w2.shape[1] if w2 is not None else 0,
-        _lib.ptr(bias), ypart.data_ptr(), cnt.data_ptr(), h.data_ptr(), h_out.data_ptr(), gamma.data_ptr(),
-        _lib.ptr(beta), float(eps), xn_out.data_ptr(), _lib.ptr(gamma2), _lib.ptr(beta2), _lib.ptr(xn2_out),
-        w1.shape[0], nw.data_ptr(), _lib.ptr(nbias), ny.data_ptr(), nw.shape[0], int(act), flags.data_ptr(),
-        _lib.stream())
-    if rc == 10:
-        return False
-    if rc != 0:
-        raise RuntimeError(f"kca_gemv_ln_gemv returned status {rc}")
-    return True
+              _lib.ptr(beta2), _lib.ptr(xn2_out), w1.shape[0], _lib.stream())
 
 
 def gemv_dual_ln_reference(x1, w1, x2, w2, bias, h, gamma, beta, eps):
