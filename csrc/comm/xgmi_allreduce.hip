@@ -272,8 +272,13 @@ __global__ __launch_bounds__(256) void ar_res_ln_kernel(ARPeers peers, ARCtl* ct
         acc[2 * j + 1] += __uint_as_float(v[j] & 0xffff0000u);
       }
     }
+    // h' = bf16(h + y + bias) for these 8 columns, handed to the LayerNorm tail (NaN on a timed-out sync)
+    float h8[8], b8[8];
+    load8(a.h + i * 8, h8);
+    if (a.bias) load8(a.bias + i * 8, b8);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) st_pub(a.ypart + i * 8 + j, ok ? acc[j] : __int_as_float(0x7fc00000));
+    for (int j = 0; j < 8; ++j) h8[j] = ok ? h8[j] + (acc[j] + (a.bias ? b8[j] : 0.f)) : __int_as_float(0x7fc00000);
+    st_pub_bf16x8(a.h_out + i * 8, h8);
   }
   ar_end(ctl, call);
   dual_ln_arrive_tail<PER>(a);

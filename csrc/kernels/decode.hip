@@ -826,9 +826,8 @@ template <int R, int PER>
 __global__ __launch_bounds__(256) void gemv_dual_ln_kernel(DualLn a) {
   __shared__ float part[4][R];
   const int tid = threadIdx.x;
-  // row groups g = blockIdx.x, + gridDim.x, ...: the grid is at most one residency round, so a
-  // workgroup's drain + arrival (~3 us of latency it holds its slot for) is paid once per workgroup,
-  // not once per 4-row group (no workgroup waits on another: dispatch order does not matter)
+  // row groups g = blockIdx.x, + gridDim.x, ... (no workgroup waits on another: dispatch order does
+  // not matter)
   const int ngrp = (a.N + R - 1) / R;
   for (int grp = blockIdx.x; grp < ngrp; grp += gridDim.x) {
     const int n0 = grp * R;
@@ -840,7 +839,10 @@ __global__ __launch_bounds__(256) void gemv_dual_ln_kernel(DualLn a) {
     gemv_m1_accum<R>(a.x1, a.w1, a.N, a.K1, n0, acc);
     if (a.x2) gemv_m1_accum<R>(a.x2, a.w2, a.N, a.K2, n0, acc);
     const float v = gemv_m1_finish<R>(acc, part, nullptr, n0, a.N, 0);
-    if (tid < R && n0 + tid < a.N) st_pub(&a.ypart[n0 + tid], v);
+    if (tid < R && n0 + tid < a.N) {  // this row's h' = bf16(h + y + bias), handed to the tail
+      const int n = n0 + tid;
+      st_pub_bf16(a.h_out + n, bf2f(a.h[n]) + (v + (a.bias ? bf2f(a.bias[n]) : 0.f)));
+    }
     __syncthreads();  // part[] is rewritten by the next group
   }
   dual_ln_arrive_tail<PER>(a);
@@ -1088,10 +1090,9 @@ KCA_API int kca_decode_prep_attn_gemv(const void* qkv, long long ld, const void*
 // statistics). x2 / w2 nullable (K2 = 0: one GEMV -- a sequential-residual layer's out-projection or
 // fc_out). ypart: >= N fp32 words; cnt: 32 * (1 + kDualSub) zero-initialised unsigned counters
 // (re-armed by every launch).
-// Geometry (bench/gemv_dual_ln_bench.py, profiles/decode_launch_structure_ab_r5.txt): 4 rows per
-// workgroup, except one short weight stream (K <= 2048: BLOOM TP=8's out-projection) at 16 rows --
-// a quarter of the arrivals for the same bytes (31.8 -> 23.8 us); the grid capped at one residency
-// round (8 workgroups per CU), the row groups looped.
+// Geometry: 4 weight rows per workgroup, one workgroup per row group. (16 rows for a short stream and
+// a grid capped at one residency round won in isolated replays but lost inside the BLOOM TP=8 decode
+// step, 26.4 vs 23.9 and 47.5 vs 44.6 us: profiles/decode_launch_structure_ab_r5.txt.)
 KCA_API int kca_gemv_dual_ln(const void* x1, const void* w1, int K1, const void* x2, const void* w2, int K2,
                              const void* bias, float* ypart, unsigned int* cnt, const void* h, void* h_out,
                              const void* gamma, const void* beta, float eps, void* xn_out, const void* gamma2,
@@ -1108,20 +1109,9 @@ KCA_API int kca_gemv_dual_ln(const void* x1, const void* w1, int K1, const void*
                  ypart, cnt, (const bf16_t*)h, (bf16_t*)h_out, (const bf16_t*)gamma, (const bf16_t*)beta, eps,
                  (bf16_t*)xn_out, (const bf16_t*)gamma2, (const bf16_t*)beta2, (bf16_t*)xn2_out,
                  N, K1, x2 ? K2 : 0};
-  static int cu_count[64] = {};
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  int& cus = cu_count[dev & 63];
-  if (!cus && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
-  const int rows = (!x2 && K1 <= 2048) ? 16 : 4;
-  const dim3 grid((unsigned)std::min((N + rows - 1) / rows, 8 * cus));
-  auto go = [&](auto rc) {
-    constexpr int R = decltype(rc)::value;
-    if (N <= 8192) hipLaunchKernelGGL((gemv_dual_ln_kernel<R, 4>), grid, dim3(256), 0, stream, a);
-    else hipLaunchKernelGGL((gemv_dual_ln_kernel<R, 8>), grid, dim3(256), 0, stream, a);
-  };
-  if (rows == 4) go(std::integral_constant<int, 4>{});
-  else go(std::integral_constant<int, 16>{});
+  const dim3 grid((unsigned)((N + 3) / 4));
+  if (N <= 8192) hipLaunchKernelGGL((gemv_dual_ln_kernel<4, 4>), grid, dim3(256), 0, stream, a);
+  else hipLaunchKernelGGL((gemv_dual_ln_kernel<4, 8>), grid, dim3(256), 0, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
@@ -1837,7 +1827,7 @@ __global__ __launch_bounds__(NT) void sample_reg_kernel(
 // global top-k with its ties. The last workgroup to arrive (agent-scope release / acquire around one
 // counter per row) merges: global max and normaliser, the top-k select over the ~k..2k candidates,
 // top-p over the survivors (4-bit radix on the mass, as the register sampler), and the Philox
-// multinomial in index order. Top-p-only rows (top_k off) list each chunk's top CMAX / 2; the merge
+// multinomial in index order. Top-p-only rows (top_k off) list each chunk's top 3/4 CMAX; the merge
 // samples them when the union -- every element >= T0 -- holds p of the row's mass (the nucleus is
 // then inside it), else it marks the row (out_ids = -1). Rows with top_k > 64, pure multinomial rows
 // and marked rows are left to sample_reg_kernel, launched after this one with `skip_mwg` (each kernel
@@ -2087,10 +2077,10 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
   SSTAMP_DECL
   const bool st0 = g == 0 && b == 0;
   const bool greedy = !(T > 0.f);
-  // top-p only: each chunk lists its top KC (half the list, room for bf16 ties at the cut); the merge
+  // top-p only: each chunk lists its top KC (3/4 of the list, room for bf16 ties at the cut); the merge
   // checks that the union -- every element >= T0 -- holds the nucleus's mass before it samples
   const bool tponly = !greedy && k <= 0;
-  const int kc = tponly ? CMAX / 2 : k;
+  const int kc = tponly ? CMAX * 3 / 4 : k;
   const float rp = rep_pen ? rep_pen[b] : 1.f;
   const int slot = slots ? slots[b] : b;
   const uint8_t* sn = seen ? seen + (long long)slot * V : nullptr;

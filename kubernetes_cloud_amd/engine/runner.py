@@ -572,8 +572,8 @@ class ModelRunner:
                 continue
             if kind == "seq":
                 # attention, out-projection + residual + ln_2, fc_in (+ GELU), fc_out + residual + next ln_1
-                # (a fused attention + out-projection launch and a tail launch chained to the next
-                # projection both measured slower: profiles/decode_launch_structure_ab_r5.txt)
+                # (a fused attention + out-projection launch and tail launches chained with the next
+                # projection measured slower: profiles/decode_launch_structure_ab_r5.txt)
                 o = dops.decode_prep_attention(qkv, self.H, self.Hkv, self.D, self.rot, cfg.rotary_interleaved,
                                                cos, sin, pos, slots, kc, vc, kv_lens, max_kv, at.scale, at.alibi,
                                                out=obuf, ws=ws, block_table=tbl, window=at.window, by_row=by_row)
