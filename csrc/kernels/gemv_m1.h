@@ -29,11 +29,12 @@ __device__ __forceinline__ uint4 ld_w16(const bf16_t* p) {
 // w, lane l) owns positions i*2048 + w*512 + l*8), R weight rows, 16 / R slabs of loads in flight --
 // the gemv1_kernel<R, false, 1> loop (gemv.hip) as a device function, so that a fused kernel can
 // run it on a subset of its workgroups. Not reduced across lanes: call gemv_m1_finish.
-template <int R>
+template <int R, int UO = 0>
 __device__ __forceinline__ void gemv_m1_accum(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, int N,
                                               int K, int n0, float (&acc)[R], long long ldw = -1) {
   if (ldw < 0) ldw = K;  // row stride of w (a K-chunk of a wider matrix: the full row length)
-  constexpr int U = R >= 16 ? 1 : (R >= 8 ? 2 : 4);  // 16 weight loads in flight per lane, any R
+  // 16 weight loads in flight per lane, any R (UO: another slab count)
+  constexpr int U = UO > 0 ? UO : (R >= 16 ? 1 : (R >= 8 ? 2 : 4));
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int kl = wid * 512 + lane * 8;
   const bf16_t* wr[R];
