@@ -64,9 +64,9 @@ def test_hierarchical_adasum_averages_in_node_then_adasum_across():
     ps = [ctx.Process(target=_hier_worker, args=(r, world, port, q)) for r in range(world)]
     for p in ps:
         p.start()
-    res = dict(q.get(timeout=120) for _ in ps)
+    res = dict(q.get(timeout=400) for _ in ps)
     for p in ps:
-        p.join(timeout=60)
+        p.join(timeout=300)
         assert p.exitcode == 0
     seg, n = _seg()
     g = _grads(world)
@@ -90,9 +90,9 @@ def test_adasum_recursive_doubling_matches_tree(world):
     ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in ps:
         p.start()
-    res = dict(q.get(timeout=120) for _ in ps)
+    res = dict(q.get(timeout=400) for _ in ps)
     for p in ps:
-        p.join(timeout=60)
+        p.join(timeout=300)
         assert p.exitcode == 0
     seg, n = _seg()
     ref = _tree(_grads(world), seg, n)
