@@ -7,10 +7,18 @@ with FasterTransformer's runtime_top_k / runtime_top_p / temperature /
 repetition_penalty / bad_words_list / stop_words_list / is_return_log_probs
 (download-weights-job-gptj.yml:101-175). One function covers both.
 
-On GPU (bf16/fp32 logits) the whole chain runs in ``kca_sample_logits`` (one
-workgroup per row: penalty + bans + temperature + top-k radix/bisection
-threshold + top-p nucleus + Philox multinomial + log-prob of the chosen token)
-when the kernel is present; the torch path below is the reference semantics.
+On GPU (bf16/fp32 logits) the whole chain -- penalty + bans + temperature +
+top-k threshold + top-p nucleus + Philox multinomial + log-prob of the chosen
+token -- runs in ``kca_sample_logits`` (csrc/kernels/decode.hip). Greedy rows,
+top-k rows (k <= 64) and top-p-only rows of bf16 logits take the multi-workgroup
+sampler: each row split over 16 chunk workgroups (32 for vocabularies past 50k,
+BLOOM's 250,880) that publish their chunk maxima / normalisers / candidate lists,
+the last one to arrive merging them; a top-p-only row whose candidates do not
+hold the nucleus is marked and re-sampled by the one-workgroup register kernel
+launched after it, which also takes every other row (top_k > 64, pure
+multinomial, fp32 logits). The choice is made per row on the device, so captured
+decode graphs serve any mix of request parameters. The torch path below is the
+reference semantics.
 """
 from __future__ import annotations
 
