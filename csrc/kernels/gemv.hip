@@ -475,8 +475,13 @@ static void launch_skinny(const bf16_t* x, long long ldx, const bf16_t* w, const
   // the LN prologue is redone by every workgroup: at BLOOM's K = 14336 the 4x workgroup count of the
   // split-K form costs more than it saves (B=1 8.75 -> 9.47 ms/token), so wide LN rows stay row-per-wave
   if constexpr (M == 1) if (g_skinny_sk && !(LN && K > 8192)) {
-    const dim3 grid((N + R - 1) / R);
-    hipLaunchKernelGGL((gemv1_kernel<R, LN>), grid, dim3(256), 0, s, x, w, bias, y, N, K, act, ln, 0LL, 0LL, 1);
+#ifdef KCA_AB_GEMV_R2
+    constexpr int R1 = 2;
+#else
+    constexpr int R1 = R;
+#endif
+    const dim3 grid((N + R1 - 1) / R1);
+    hipLaunchKernelGGL((gemv1_kernel<R1, LN>), grid, dim3(256), 0, s, x, w, bias, y, N, K, act, ln, 0LL, 0LL, 1);
     return;
   }
   // 2 rows without an LN prologue (decode batch 2): the K-split register-resident form, K <= 8192

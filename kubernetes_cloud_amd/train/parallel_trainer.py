@@ -64,6 +64,8 @@ def build_parser():
     p.add_argument("--max-steps", type=int, default=0)
     p.add_argument("--save-steps", type=int, default=0)
     p.add_argument("--seed", type=int, default=42)
+    p.add_argument("--fp32", action="store_true",
+                   help="fp32 parameters and math on the GPU (parity references; the native kernels are bf16)")
     p.add_argument("--log-dir", default="")
     p.add_argument("--local_rank", "--local-rank", type=int, default=-1,
                    help="appended by the DeepSpeed-style launcher (kubernetes_cloud_amd.launch); LOCAL_RANK wins")
@@ -267,7 +269,7 @@ def main(argv=None):
     info = init_distributed()
     topo = Topology(args.tp, args.pp)
     dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
-    dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
+    dtype = torch.bfloat16 if dev.type == "cuda" and not args.fp32 else torch.float32
     torch.manual_seed(args.seed)
     cfg, stage = build_model_shard(args, topo, dev, dtype)
     stage.train()
@@ -294,6 +296,10 @@ def main(argv=None):
         loss_sum = one_f_one_b(stage, eng, p2p, mbs, topo.pp_idx, topo.pp)
         eng.step(lr)
         step += 1
+        if topo.dp > 1:  # the global batch's loss: mean over the data-parallel replicas (every rank joins
+            ls = torch.as_tensor(loss_sum, dtype=torch.float32, device=dev).reshape(1)  # its own DP group)
+            dist.all_reduce(ls, group=topo.dp_group)
+            loss_sum = ls / topo.dp
         losses.append(float(loss_sum / args.gradients))  # meaningful on the last stage only
         if topo.rank == log_rank:
             tok_s = args.micro_batch * args.gradients * args.seq_len * topo.dp * step / (time.perf_counter() - t0)
