@@ -1048,8 +1048,13 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq_tiled_kernel(FastBwdParams
   ASTAMP_FLUSH(16);
 }
 
+#ifdef KCA_AB_DKDV64_OCC3
+#define KCA_DKDV_MINB(D) ((D) <= 64 ? 3 : 1)
+#else
+#define KCA_DKDV_MINB(D) 1
+#endif
 template <int D, bool CAUSAL, int DS = D>
-__global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_tiled_kernel(FastBwdParams p) {
+__global__ void __launch_bounds__(256, KCA_DKDV_MINB(D)) attn_bwd_dkdv_tiled_kernel(FastBwdParams p) {
   constexpr int BK = 128, BQ = 32;
   constexpr int TILE = BQ * D * 2;                  // one 32-row image
   using Stg = StagerFor<D, DS>;

@@ -836,13 +836,11 @@ __global__ __launch_bounds__(256) void gemv_dual_ln_kernel(DualLn a) {
     for (int r = 0; r < R; ++r) acc[r] = 0.f;
     // (the two streams as two loops: one loop across the seam measured 1.5 us slower at GPT-J / NeoX
     // shapes, profiles/decode_launch_structure_ab_r5.txt)
-#ifdef KCA_AB_DUAL_U2
-    constexpr int UD = R == 4 ? 2 : 0;
-#else
-    constexpr int UD = 0;
-#endif
-    gemv_m1_accum<R, UD>(a.x1, a.w1, a.N, a.K1, n0, acc);
-    if (a.x2) gemv_m1_accum<R, UD>(a.x2, a.w2, a.N, a.K2, n0, acc);
+    // 2 weight slabs in flight per lane (8 loads at 4 rows), not 16: 84 instead of 124 VGPRs, 5 instead
+    // of 4 waves per SIMD -- BLOOM TP=8 B=1 9.36 -> 9.06 ms/token, GPT-J neutral
+    // (profiles/decode_launch_structure_ab_r5.txt)
+    gemv_m1_accum<R, 2>(a.x1, a.w1, a.N, a.K1, n0, acc);
+    if (a.x2) gemv_m1_accum<R, 2>(a.x2, a.w2, a.N, a.K2, n0, acc);
     const float v = gemv_m1_finish<R>(acc, part, nullptr, n0, a.N, 0);
     if (tid < R && n0 + tid < a.N) {  // this row's h' = bf16(h + y + bias), handed to the tail
       const int n = n0 + tid;
@@ -1095,9 +1093,9 @@ KCA_API int kca_decode_prep_attn_gemv(const void* qkv, long long ld, const void*
 // statistics). x2 / w2 nullable (K2 = 0: one GEMV -- a sequential-residual layer's out-projection or
 // fc_out). ypart: >= N fp32 words; cnt: 32 * (1 + kDualSub) zero-initialised unsigned counters
 // (re-armed by every launch).
-// Geometry: 4 weight rows per workgroup, one workgroup per row group. (16 rows for a short stream and
-// a grid capped at one residency round won in isolated replays but lost inside the BLOOM TP=8 decode
-// step, 26.4 vs 23.9 and 47.5 vs 44.6 us: profiles/decode_launch_structure_ab_r5.txt.)
+// Geometry: 4 weight rows per workgroup, one workgroup per row group (8 or 16 rows measured equal or
+// slower inside the decode steps; a grid capped at one residency round slower:
+// profiles/decode_launch_structure_ab_r5.txt).
 KCA_API int kca_gemv_dual_ln(const void* x1, const void* w1, int K1, const void* x2, const void* w2, int K2,
                              const void* bias, float* ypart, unsigned int* cnt, const void* h, void* h_out,
                              const void* gamma, const void* beta, float eps, void* xn_out, const void* gamma2,
@@ -1114,19 +1112,6 @@ KCA_API int kca_gemv_dual_ln(const void* x1, const void* w1, int K1, const void*
                  ypart, cnt, (const bf16_t*)h, (bf16_t*)h_out, (const bf16_t*)gamma, (const bf16_t*)beta, eps,
                  (bf16_t*)xn_out, (const bf16_t*)gamma2, (const bf16_t*)beta2, (bf16_t*)xn2_out,
                  N, K1, x2 ? K2 : 0};
-#if defined(KCA_AB_DUAL_R16)
-  constexpr int RS = 16;
-#elif defined(KCA_AB_DUAL_R8)
-  constexpr int RS = 8;
-#else
-  constexpr int RS = 4;
-#endif
-  if (!x2 && RS != 4) {
-    const dim3 grid((unsigned)((N + RS - 1) / RS));
-    if (N <= 8192) hipLaunchKernelGGL((gemv_dual_ln_kernel<RS, 4>), grid, dim3(256), 0, stream, a);
-    else hipLaunchKernelGGL((gemv_dual_ln_kernel<RS, 8>), grid, dim3(256), 0, stream, a);
-    return hipGetLastError() == hipSuccess ? 0 : 2;
-  }
   const dim3 grid((unsigned)((N + 3) / 4));
   if (N <= 8192) hipLaunchKernelGGL((gemv_dual_ln_kernel<4, 4>), grid, dim3(256), 0, stream, a);
   else hipLaunchKernelGGL((gemv_dual_ln_kernel<4, 8>), grid, dim3(256), 0, stream, a);
