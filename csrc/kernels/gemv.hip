@@ -182,7 +182,11 @@ __global__ __launch_bounds__(256) void gemv1_kernel(const bf16_t* __restrict__ x
                                                     int N, int K, int act, LnArgs ln, long long ldx = 0,
                                                     long long ldy = 0, int mv = 1) {
   static_assert(MR == 1 || !LN, "the LN prologue is single-row");
+#ifdef KCA_AB_GEMV_U2
+  constexpr int U = LN ? 4 : 2;
+#else
   constexpr int U = 4;
+#endif
   __shared__ float red[16];
   __shared__ float part[4][R * MR];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -475,11 +479,10 @@ static void launch_skinny(const bf16_t* x, long long ldx, const bf16_t* w, const
   // the LN prologue is redone by every workgroup: at BLOOM's K = 14336 the 4x workgroup count of the
   // split-K form costs more than it saves (B=1 8.75 -> 9.47 ms/token), so wide LN rows stay row-per-wave
   if constexpr (M == 1) if (g_skinny_sk && !(LN && K > 8192)) {
-#ifdef KCA_AB_GEMV_R2
+    // 2 weight rows per workgroup: twice the workgroups of the 4-row form, a shorter ragged end to
+    // each launch (same box: BLOOM TP=8 B=1 9.03 -> 8.97 ms, GPT-J B=1 2.21 -> 2.20 ms;
+    // profiles/decode_launch_structure_ab_r5.txt)
     constexpr int R1 = 2;
-#else
-    constexpr int R1 = R;
-#endif
     const dim3 grid((N + R1 - 1) / R1);
     hipLaunchKernelGGL((gemv1_kernel<R1, LN>), grid, dim3(256), 0, s, x, w, bias, y, N, K, act, ln, 0LL, 0LL, 1);
     return;
