@@ -900,13 +900,10 @@ __device__ __forceinline__ void store_acc_t(bf16_t* rowp, const f32x16 (&acc)[D 
 // DS < D ("narrow storage", as the forward): heads stored DS wide (SD-1.5's 40-wide heads in 48 columns,
 // D = 64 images, the pad chunks of every image zeroed once); the S / dP contractions run DS / 16 MFMA
 // steps, the dQ (dK, dV) tiles are stored DS wide.
-#ifdef KCA_AB_DQ64_OCC4
-#define KCA_DQ_MINB(D, C) (((D) <= 64 && !(C)) ? 4 : 1)
-#else
-#define KCA_DQ_MINB(D, C) 1
-#endif
+// 64-wide heads without a causal mask (SD): registers capped for 4 waves per SIMD instead of 3 (a 16-byte
+// spill in the 48-wide form; DreamBooth +1.5-2.8 % same box, profiles/decode_launch_structure_ab_r5.txt)
 template <int D, bool CAUSAL, int DS = D>
-__global__ void __launch_bounds__(256, KCA_DQ_MINB(D, CAUSAL)) attn_bwd_dq_tiled_kernel(FastBwdParams p) {
+__global__ void __launch_bounds__(256, (D <= 64 && !CAUSAL) ? 4 : 1) attn_bwd_dq_tiled_kernel(FastBwdParams p) {
   constexpr int BM = 128, BN = 32;
   constexpr int TILE = BN * D * 2;
   using Stg = StagerFor<D, DS>;

@@ -811,11 +811,7 @@ __global__ __launch_bounds__(256) void decode_attn_gemv_kernel(DecodeParams p, i
   DSTAMP(0);
   const int n0 = (bid - n_attn) * R;
   float acc[R] = {0.f, 0.f, 0.f, 0.f};
-#ifdef KCA_AB_GEMV_U2
-  gemv_m1_accum<R, 2>(g.x, g.w, g.N, g.K, n0, acc);
-#else
   gemv_m1_accum<R>(g.x, g.w, g.N, g.K, n0, acc);
-#endif
   const float v = gemv_m1_finish<R>(acc, part, g.bias, n0, g.N, g.act);
   if (threadIdx.x < R && n0 + threadIdx.x < g.N) g.y[n0 + threadIdx.x] = f2bf(v);
   DSTAMP(7);

@@ -182,11 +182,7 @@ __global__ __launch_bounds__(256) void gemv1_kernel(const bf16_t* __restrict__ x
                                                     int N, int K, int act, LnArgs ln, long long ldx = 0,
                                                     long long ldy = 0, int mv = 1) {
   static_assert(MR == 1 || !LN, "the LN prologue is single-row");
-#ifdef KCA_AB_GEMV_U2
-  constexpr int U = LN ? 4 : 2;
-#else
   constexpr int U = 4;
-#endif
   __shared__ float red[16];
   __shared__ float part[4][R * MR];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
