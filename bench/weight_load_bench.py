@@ -106,6 +106,14 @@ def run_weight_load(model="gpt-j-6b", directory="/tmp", threads=8, sources=("col
     layer_bytes = sum(p.numel() * p.element_size() for p in m.h[0].parameters())
     total = sum(p.numel() * p.element_size() for p in m.parameters())
     serialize_causal_lm(m, path)
+    # flush the freshly written file before any timed read: an O_DIRECT read of a file with dirty pages
+    # first writes them back, so whichever read came first paid the writeback (round 4's 6.75 -> 6.11
+    # GB/s "drop", and a raw rate below the load rate)
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        os.fsync(fd)
+    finally:
+        os.close(fd)
     del m
     torch.cuda.empty_cache()
     out = []

@@ -58,6 +58,8 @@ def build_request(kind: str, base: str, prompt: str, model: str, i: int):
 
 
 async def run_async(reqs, concurrency: int, timeout: float):
+    """-> (latencies, seconds from the first request sent to the last response): the client's import,
+    construction and teardown are outside the measured window, as they are outside the server's."""
     import httpx
     sem = asyncio.Semaphore(concurrency)
     times = []
@@ -71,14 +73,17 @@ async def run_async(reqs, concurrency: int, timeout: float):
                     times.append(time.perf_counter() - t0)
                 except Exception as e:  # noqa: BLE001
                     log.info("request failed: %s", e)
+        t0 = time.perf_counter()
         await asyncio.gather(*(one(r) for r in reqs))
-    return times
+        total = time.perf_counter() - t0
+    return times, total
 
 
 def run_sync(reqs, timeout: float):
     import httpx
     times = []
     with httpx.Client(timeout=timeout) as cl:
+        t0 = time.perf_counter()
         for r in reqs:
             t0 = time.perf_counter()
             try:
@@ -87,7 +92,8 @@ def run_sync(reqs, timeout: float):
                 times.append(time.perf_counter() - t0)
             except Exception as e:  # noqa: BLE001
                 log.info("request failed: %s", e)
-    return times
+        total = time.perf_counter() - t0
+    return times, total
 
 
 def benchmark(url: str, kind: str, n: int, asynchronous: bool = True, concurrency: int | None = None,
@@ -96,12 +102,10 @@ def benchmark(url: str, kind: str, n: int, asynchronous: bool = True, concurrenc
     prompts = prompts or PROMPTS
     reqs = [build_request(kind, url.rstrip("/"), rnd.choice(prompts), model, i) for i in range(n)]
     print("Started benchmark", flush=True)
-    t0 = time.time()
     if asynchronous:
-        times = asyncio.run(run_async(reqs, concurrency or n, timeout))
+        times, total = asyncio.run(run_async(reqs, concurrency or n, timeout))
     else:
-        times = run_sync(reqs, timeout)
-    total = time.time() - t0
+        times, total = run_sync(reqs, timeout)
     ok = len(times)
     res = {"url": url, "kind": kind, "requests": n, "seconds": total, "successes": ok, "failures": n - ok,
            "throughput_rps": n / total, "goodput_rps": ok / total}
