@@ -34,7 +34,6 @@ import sys
 import tempfile
 import threading
 import time
-from concurrent.futures import ThreadPoolExecutor
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
@@ -92,7 +91,10 @@ class _Server:
 
 
 def _engine(pred, n: int, conc: int, seed: int = 0, kind: str = "kserve") -> dict:
-    """The same request stream straight into ``predict`` (no HTTP), ``conc`` in flight."""
+    """The same request stream through the model's serving entry point -- ``await model(payload)``,
+    exactly what the HTTP route awaits (preprocess, async predict, postprocess) -- on an event loop of
+    its own, ``conc`` in flight: the HTTP pass differs from this one only by HTTP."""
+    import asyncio
     import random
 
     from kubernetes_cloud_amd.serving.loadgen import PROMPTS
@@ -100,15 +102,20 @@ def _engine(pred, n: int, conc: int, seed: int = 0, kind: str = "kserve") -> dic
     payloads = [{"instances": [rnd.choice(PROMPTS)]} if kind == "kserve" else
                 {"prompt": rnd.choice(PROMPTS), "parameters": {"seed": i}} for i in range(n)]
 
-    def one(p):
-        t = time.perf_counter()
-        pred.predict(p)
-        return time.perf_counter() - t
+    async def run_all():
+        sem = asyncio.Semaphore(conc)
 
-    t0 = time.perf_counter()
-    with ThreadPoolExecutor(conc) as ex:
-        lat = sorted(ex.map(one, payloads))
-    dt = time.perf_counter() - t0
+        async def one(p):
+            async with sem:
+                t = time.perf_counter()
+                await pred(p, {})
+                return time.perf_counter() - t
+        t0 = time.perf_counter()
+        lat = await asyncio.gather(*(one(p) for p in payloads))
+        return lat, time.perf_counter() - t0
+
+    lat, dt = asyncio.run(run_all())
+    lat = sorted(lat)
     return {"throughput_rps": n / dt, "latencies": lat, **_lat_stats(lat)}
 
 
