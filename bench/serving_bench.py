@@ -66,13 +66,22 @@ def _tokenizer(path: str):
 
 
 class _Server:
-    """The repo's V1/V2 REST app (serving/server.py) under uvicorn in a thread."""
+    """The repo's V1/V2 REST app (serving/server.py) as ``ModelServer.start`` runs it: in a front-end
+    child process whose models forward to this one (serving/frontend.py), or -- ``inline`` -- under
+    uvicorn in a thread of this process."""
 
-    def __init__(self, models):
+    def __init__(self, models, inline: bool | None = None):
         import uvicorn
 
+        from kubernetes_cloud_amd.serving import server as _srv
         from kubernetes_cloud_amd.serving.server import ModelServer
         self.port = _free_port()
+        self.fe = None
+        if not (inline if inline is not None else _srv.HTTP_FRONTEND != "process"):
+            from kubernetes_cloud_amd.serving.frontend import FrontendServer
+            self.fe = FrontendServer(models, self.port)
+            self.url = f"http://127.0.0.1:{self.port}"
+            return
         app = ModelServer(http_port=self.port, argv=[]).create_app(models)
         cfg = uvicorn.Config(app, host="127.0.0.1", port=self.port, log_level="warning", access_log=False)
         self.srv = uvicorn.Server(cfg)
@@ -86,6 +95,9 @@ class _Server:
         self.url = f"http://127.0.0.1:{self.port}"
 
     def close(self):
+        if self.fe is not None:
+            self.fe.close()
+            return
         self.srv.should_exit = True
         self.th.join(timeout=30)
 

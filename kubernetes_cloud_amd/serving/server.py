@@ -39,6 +39,9 @@ from . import v2
 # in JSON / tokenizer work can hold the engine off for up to 5 ms per hand-off (bench/serving_bench.py
 # --switch-interval A/B)
 GIL_SWITCH_S = 5e-4
+# KCA_HTTP_FRONTEND=inline: the REST app in the engine's process (the default runs it in a child process
+# whose models forward to this one: serving/frontend.py)
+HTTP_FRONTEND = os.environ.get("KCA_HTTP_FRONTEND", "process")
 
 log = logging.getLogger("kca.serving")
 
@@ -265,7 +268,17 @@ class ModelServer:
             self.grpc_server = serve(self.models, self.grpc_port, self.host)
         log.info("serving %s on %s:%d", list(self.models), self.host, self.http_port)
         try:
-            uvicorn.run(app, host=self.host, port=self.http_port, workers=1, log_level="info")
+            if HTTP_FRONTEND == "process" and extra_routes is None:
+                # the REST stack in a child process, the engine's interpreter lock left to the engine
+                # (serving/frontend.py)
+                from .frontend import FrontendServer
+                fe = FrontendServer(list(self.models.values()), self.http_port, self.host)
+                try:
+                    fe.proc.wait()
+                finally:
+                    fe.close()
+            else:
+                uvicorn.run(app, host=self.host, port=self.http_port, workers=1, log_level="info")
         finally:
             if self.grpc_server is not None:
                 self.grpc_server.stop(grace=2)

@@ -1,0 +1,62 @@
+"""The REST front-end in its own process (serving/frontend.py): V1 predict, V2 infer and metadata through
+the proxy models, the model's errors mapped to the same status codes as in process, and concurrent
+requests answered in any order."""
+import socket
+from concurrent.futures import ThreadPoolExecutor
+
+import httpx
+import numpy as np
+
+from kubernetes_cloud_amd.serving.frontend import FrontendServer
+from kubernetes_cloud_amd.serving.server import InvalidInput, Model
+
+
+class Echo(Model):
+    def __init__(self):
+        super().__init__("echo")
+        self.ready = True
+
+    async def apredict(self, payload, headers=None):
+        if "instances" not in payload:
+            raise InvalidInput("request must contain 'instances'")
+        if payload["instances"] == ["boom"]:
+            raise RuntimeError("model failed")
+        return {"predictions": [s[::-1] for s in payload["instances"]]}
+
+    def infer(self, inputs, request, headers=None):
+        return {"y": np.asarray(inputs["x"]) * 2}
+
+    def metadata(self):
+        return {"name": "echo", "versions": ["1"], "platform": "test", "inputs": [], "outputs": []}
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_frontend_process_routes_errors_and_concurrency():
+    port = _port()
+    fe = FrontendServer([Echo()], port)
+    try:
+        base = f"http://127.0.0.1:{port}"
+        r = httpx.post(f"{base}/v1/models/echo:predict", json={"instances": ["abc", "xyz"]})
+        assert r.status_code == 200 and r.json() == {"predictions": ["cba", "zyx"]}
+        assert httpx.post(f"{base}/v1/models/echo:predict", json={"nope": 1}).status_code == 400
+        assert httpx.post(f"{base}/v1/models/echo:predict", json={"instances": ["boom"]}).status_code == 500
+        assert httpx.post(f"{base}/v1/models/other:predict", json={"instances": []}).status_code == 404
+        assert httpx.get(f"{base}/v2/models/echo").json()["platform"] == "test"
+        body = {"inputs": [{"name": "x", "shape": [3], "datatype": "FP32", "data": [1.0, 2.0, 3.0]}]}
+        out = httpx.post(f"{base}/v2/models/echo/infer", json=body).json()
+        assert out["outputs"][0]["data"] == [2.0, 4.0, 6.0]
+        words = [f"w{i:03d}" for i in range(48)]
+        with ThreadPoolExecutor(16) as ex:
+            got = list(ex.map(lambda w: httpx.post(f"{base}/v1/models/echo:predict",
+                                                   json={"instances": [w]}).json()["predictions"][0], words))
+        assert got == [w[::-1] for w in words]
+    finally:
+        fe.close()
+    assert fe.proc.poll() is not None
