@@ -165,6 +165,10 @@ class FrontendServer:
 
     def __init__(self, models: list, port: int, host: str = "127.0.0.1", start_timeout: float = 120.0):
         from multiprocessing.connection import Listener
+
+        from . import server as _srv
+        if _srv.GIL_SWITCH_S > 0:  # this process's threads (engine loop, model loop, reader) hand off often
+            sys.setswitchinterval(_srv.GIL_SWITCH_S)
         self.port, self.host = port, host
         self.models = {m.name: m for m in models}
         d = tempfile.mkdtemp(prefix="kca_frontend_")
