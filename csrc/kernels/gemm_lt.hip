@@ -52,16 +52,23 @@ hipblasLtHandle_t handle_for(int dev) {
 bool ok(hipblasStatus_t s) { return s == HIPBLAS_STATUS_SUCCESS; }
 
 bool build(Plan& p, int M, int N, int K, long long lda, long long ldw, long long ldc, long long ldd, bool bias,
-           bool has_c, bool f32out = false) {
+           bool has_c, bool f32out = false, uint32_t epi_over = 0, long long ldaux = 0, int opts = 0) {
   if (!ok(hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F))) return false;
   const int32_t opT = HIPBLAS_OP_T, opN = HIPBLAS_OP_N;
   hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &opT, sizeof(opT));
   hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &opN, sizeof(opN));
-  const uint32_t epi = bias ? HIPBLASLT_EPILOGUE_BIAS : HIPBLASLT_EPILOGUE_DEFAULT;
+  const uint32_t epi = epi_over ? epi_over : bias ? HIPBLASLT_EPILOGUE_BIAS : HIPBLASLT_EPILOGUE_DEFAULT;
   hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &epi, sizeof(epi));
   if (bias) {
-    const int32_t bt = HIP_R_16BF;
+    // DGELU_BGRAD writes the bias gradient: fp32 sums; the other epilogues read a bf16 bias
+    const int32_t bt = (epi == HIPBLASLT_EPILOGUE_DGELU_BGRAD || (opts & 4)) ? HIP_R_32F : HIP_R_16BF;
     hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt));
+  }
+  if (ldaux) {  // the GELU epilogues' pre-activation matrix, laid out like D
+    const int64_t ld = ldaux;
+    const int32_t at = HIP_R_16BF;
+    hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_LD, &ld, sizeof(ld));
+    if (!(opts & 8)) hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_DATA_TYPE, &at, sizeof(at));
   }
   // A operand of the column-major problem = W (K x N, ld ldw, transposed); B = A (K x M, ld lda)
   if (!ok(hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16BF, K, N, ldw))) return false;
@@ -74,29 +81,27 @@ bool build(Plan& p, int M, int N, int K, long long lda, long long ldw, long long
 
 }  // namespace
 
-// Returns 0 on success; 1 bad arguments; 2 no hipBLASLt algorithm; 3 launch failure.
-// C may be null (beta ignored); C must not alias D when the shape still has to be tuned.
-KCA_API int kca_gemm_lt(const void* A, long long lda, const void* W, long long ldw, const void* bias,
-                        const void* C, long long ldc, void* D, long long ldd, int M, int N, int K, float beta,
-                        void* ws, long long ws_bytes, hipStream_t stream) {
-  if (!A || !W || !D || M <= 0 || N <= 0 || K <= 0 || lda < K || ldw < K || ldd < N || (C && ldc < N) ||
-      ws_bytes < 0)
-    return 1;
+namespace {
+
+int run(const void* A, long long lda, const void* W, long long ldw, const void* bias, const void* C, long long ldc,
+        void* D, long long ldd, int M, int N, int K, float beta, uint32_t epi, void* aux, long long ldaux, void* ws,
+        long long ws_bytes, hipStream_t stream, int opts = 0) {
   int dev = 0;
   hipGetDevice(&dev);
   const bool has_c = C != nullptr && beta != 0.f;
-  const Key key{dev, M, N, K, lda, ldw, has_c ? ldc : 0, ldd, bias != nullptr, has_c, 0};
+  const Key key{dev, M, N, K, lda, ldw, has_c ? ldc : 0, ldd, bias != nullptr, has_c, (int)epi | (opts << 20)};
   std::lock_guard<std::mutex> lock(g_mu);
   hipblasLtHandle_t h = handle_for(dev);
   if (!h) return 2;
   auto it = g_plans.find(key);
   if (it == g_plans.end()) {
     Plan p;
-    if (!build(p, M, N, K, lda, ldw, ldc, ldd, bias != nullptr, has_c)) return 2;
+    if (!build(p, M, N, K, lda, ldw, ldc, ldd, bias != nullptr, has_c, false, epi, aux ? ldaux : 0, opts)) return 2;
     it = g_plans.emplace(key, p).first;
   }
   Plan& p = it->second;
   if (bias) hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias));
+  if (aux) hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_POINTER, &aux, sizeof(aux));
   const float alpha = 1.f, b = has_c ? beta : 0.f;
   const void* cptr = has_c ? C : D;
 
@@ -112,7 +117,7 @@ KCA_API int kca_gemm_lt(const void* A, long long lda, const void* W, long long l
     int n = 0;
     hipblasLtMatmulAlgoGetHeuristic(h, p.desc, p.la, p.lb, p.lc, p.ld, pref, kTune, res, &n);
     hipblasLtMatmulPreferenceDestroy(pref);
-    if (n <= 0) return 2;
+    if (n <= 0) return 4;
     int best = 0;
     while (best < n && (res[best].state != HIPBLAS_STATUS_SUCCESS || res[best].workspaceSize > (size_t)ws_bytes)) ++best;
     if (best == n) return 2;
@@ -147,5 +152,38 @@ KCA_API int kca_gemm_lt(const void* A, long long lda, const void* W, long long l
   if (!ok(hipblasLtMatmul(h, p.desc, &alpha, W, p.la, A, p.lb, &b, cptr, p.lc, D, p.ld, &p.algo, ws, p.ws, stream)))
     return 3;
   return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+}  // namespace
+
+// Returns 0 on success; 1 bad arguments; 2 no hipBLASLt algorithm; 3 launch failure.
+// C may be null (beta ignored); C must not alias D when the shape still has to be tuned.
+KCA_API int kca_gemm_lt(const void* A, long long lda, const void* W, long long ldw, const void* bias,
+                        const void* C, long long ldc, void* D, long long ldd, int M, int N, int K, float beta,
+                        void* ws, long long ws_bytes, hipStream_t stream) {
+  if (!A || !W || !D || M <= 0 || N <= 0 || K <= 0 || lda < K || ldw < K || ldd < N || (C && ldc < N) ||
+      ws_bytes < 0)
+    return 1;
+  return run(A, lda, W, ldw, bias, C, ldc, D, ldd, M, N, K, beta, 0, nullptr, 0, ws, ws_bytes, stream);
+}
+
+// D = act(A . W^T + bias) with hipBLASLt's GELU epilogues (tanh form), row-major bf16:
+//   kind 1  GELU_AUX_BIAS  D = gelu(A W^T + bias), aux = A W^T + bias (the pre-activation, ld ldaux)
+//   kind 2  DGELU_BGRAD    D = (A W^T) * gelu'(aux); bias <- fp32 column sums of D (the bias gradient)
+// (kind | 4: the GELU_AUX_BIAS bias in fp32; kind | 8: aux type left at hipBLASLt's default)
+// Measured against the separate GELU passes in bench/gelu_epilogue_bench.py.
+KCA_API int kca_gemm_lt_gelu(const void* A, long long lda, const void* W, long long ldw, int kind, void* bias,
+                             void* aux, long long ldaux, void* D, long long ldd, int M, int N, int K, void* ws,
+                             long long ws_bytes, hipStream_t stream) {
+  if (!A || !W || !D || !aux || M <= 0 || N <= 0 || K <= 0 || lda < K || ldw < K || ldd < N || ldaux < N ||
+      ws_bytes < 0 || (kind & 3) == 0)
+    return 1;
+  const int opts = kind & ~3;
+  kind &= 3;
+  const uint32_t epi = kind == 1   ? (bias ? HIPBLASLT_EPILOGUE_GELU_AUX_BIAS : HIPBLASLT_EPILOGUE_GELU_AUX)
+                       : kind == 2 ? (bias ? HIPBLASLT_EPILOGUE_DGELU_BGRAD : HIPBLASLT_EPILOGUE_DGELU)
+                                   : (bias ? HIPBLASLT_EPILOGUE_GELU_BIAS : HIPBLASLT_EPILOGUE_GELU);
+  return run(A, lda, W, ldw, bias, nullptr, 0, D, ldd, M, N, K, 0.f, epi, kind == 3 ? nullptr : aux, ldaux, ws,
+             ws_bytes, stream, opts);
 }
 

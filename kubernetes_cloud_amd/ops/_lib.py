@@ -40,6 +40,7 @@ F = ctypes.c_float
 _SIGS = {
     "kca_layernorm_fwd": [P, P, P, P, P, P, P, P, P, I, I, F, P],
     "kca_gemm_lt": [P, LL, P, LL, P, P, LL, P, LL, I, I, I, F, P, LL, P],
+    "kca_gemm_lt_gelu": [P, LL, P, LL, I, P, P, LL, P, LL, I, I, I, P, LL, P],
     "kca_layernorm_bwd_parts": [I],
     "kca_layernorm_bwd": [P, P, P, P, P, P, P, P, P, I, P, I, I, P],
     "kca_gelu_fwd": [P, P, LL, I, P],
