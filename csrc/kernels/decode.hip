@@ -1875,6 +1875,23 @@ __device__ __forceinline__ float wave_sum_dpp(float v) {
   v += dpp_mov_f<0x140>(v);
   return (rl(v, 0) + rl(v, 16)) + (rl(v, 32) + rl(v, 48));
 }
+// wave OR / AND of a uint32 (uniform result), the same butterfly as wave_sum_u32
+__device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
+  v |= dpp_mov_u<0xB1>(v);
+  v |= dpp_mov_u<0x4E>(v);
+  v |= dpp_mov_u<0x141>(v);
+  v |= dpp_mov_u<0x140>(v);
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) | (uint32_t)__builtin_amdgcn_readlane((int)v, 16) |
+         (uint32_t)__builtin_amdgcn_readlane((int)v, 32) | (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+}
+__device__ __forceinline__ uint32_t wave_and_u32(uint32_t v) {
+  v &= dpp_mov_u<0xB1>(v);
+  v &= dpp_mov_u<0x4E>(v);
+  v &= dpp_mov_u<0x141>(v);
+  v &= dpp_mov_u<0x140>(v);
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) & (uint32_t)__builtin_amdgcn_readlane((int)v, 16) &
+         (uint32_t)__builtin_amdgcn_readlane((int)v, 32) & (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+}
 __device__ __forceinline__ int wave_min_i(int v) {
   v = min(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false));
   v = min(v, __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false));
@@ -1889,14 +1906,51 @@ __device__ __forceinline__ int wave_min_i(int v) {
 // a double-buffered LDS table (one barrier per pass), and the digit picked redundantly by every lane
 // from that table (no broadcast round). Returns the key prefix (ties at it kept); 0 when fewer than
 // k are valid. cnt16: 2 x (blockDim/64) x 8 words.
+//
+// Digits every valid key shares (the bits where the block's OR equals its AND) select themselves:
+// such a pass would find all candidates in one bucket, so it is skipped -- bf16 logits leave the
+// low 16 key bits constant, and bunched top values share the sign / exponent nibbles, so most
+// selections run 2-4 of the 8 passes (same threshold, same kept set).
 template <int EPT, int NW>
 __device__ uint32_t block_kth_key(int k, const uint32_t (&key)[EPT], const bool (&ok)[EPT], uint32_t* cnt16) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   uint32_t prefix = 0, mask = 0;
   int remaining = k;
-  int pass = 0;
+  int pass = 0;  // executed passes (the count tables alternate between them)
+  uint32_t common, vary;
+  {
+    uint32_t vo = 0u, va = ~0u;
+#pragma unroll
+    for (int e = 0; e < EPT; ++e)
+      if (ok[e]) {
+        vo |= key[e];
+        va &= key[e];
+      }
+    vo = wave_or_u32(vo);
+    va = wave_and_u32(va);
+    // (table 1 is next written by the second executed pass, after every thread passed the first's barrier)
+    if (lane == 0) {
+      cnt16[NW * 8 + 2 * wid] = vo;
+      cnt16[NW * 8 + 2 * wid + 1] = va;
+    }
+    __syncthreads();
+    vo = 0u;
+    va = ~0u;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      vo |= cnt16[NW * 8 + 2 * w];
+      va &= cnt16[NW * 8 + 2 * w + 1];
+    }
+    common = va;
+    vary = vo ^ va;
+  }
 #pragma unroll 1
-  for (int shift = 28; shift >= 0; shift -= 4, ++pass) {
+  for (int shift = 28; shift >= 0; shift -= 4) {
+    if (((vary >> shift) & 15u) == 0u) {  // forced digit
+      prefix |= common & (15u << shift);
+      mask |= 15u << shift;
+      continue;
+    }
     uint32_t w4[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
     for (int e = 0; e < EPT; ++e) {  // branch-free: selects, no exec-mask regions per element
@@ -1949,6 +2003,7 @@ __device__ uint32_t block_kth_key(int k, const uint32_t (&key)[EPT], const bool 
     prefix |= (uint32_t)dsel << shift;
     mask |= 15u << shift;
     remaining -= run;
+    ++pass;
     // the selected bucket holds exactly the elements still needed: every key >= prefix (lower
     // bits zero) is in the top k -- done, the remaining passes would only walk that bucket down
     if (csel == remaining) return prefix;
@@ -1963,8 +2018,21 @@ template <int EPT>
 __device__ uint32_t wave_kth_key(int k, const uint32_t (&key)[EPT], const bool (&ok)[EPT]) {
   uint32_t prefix = 0, mask = 0;
   int remaining = k;
+  uint32_t vo = 0u, va = ~0u;  // forced digits skipped as in block_kth_key
+#pragma unroll
+  for (int e = 0; e < EPT; ++e)
+    if (ok[e]) {
+      vo |= key[e];
+      va &= key[e];
+    }
+  const uint32_t common = wave_and_u32(va), vary = wave_or_u32(vo) ^ common;
 #pragma unroll 1
   for (int shift = 28; shift >= 0; shift -= 4) {
+    if (((vary >> shift) & 15u) == 0u) {
+      prefix |= common & (15u << shift);
+      mask |= 15u << shift;
+      continue;
+    }
     uint32_t w4[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
     for (int e = 0; e < EPT; ++e) {
@@ -2002,6 +2070,86 @@ __device__ uint32_t wave_kth_key(int k, const uint32_t (&key)[EPT], const bool (
     if (csel == remaining) return prefix;
   }
   return prefix;
+}
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+  v = min(v, dpp_mov_u<0xB1>(v));
+  v = min(v, dpp_mov_u<0x4E>(v));
+  v = min(v, dpp_mov_u<0x141>(v));
+  v = min(v, dpp_mov_u<0x140>(v));
+  return min(min((uint32_t)__builtin_amdgcn_readlane((int)v, 0), (uint32_t)__builtin_amdgcn_readlane((int)v, 16)),
+             min((uint32_t)__builtin_amdgcn_readlane((int)v, 32), (uint32_t)__builtin_amdgcn_readlane((int)v, 48)));
+}
+
+// The exact k-th largest valid key of the keys ONE wave holds (0 when fewer than k are valid), by
+// 8-bit digits: per pass the candidates' digits go into a wave-private 256-bin LDS histogram (ds_add),
+// each lane reads 4 bins from the top, one wave scan finds the bin where the count from the top reaches
+// the rank. Digits all valid keys share are forced (no pass), so bf16 logits (low 16 key bits
+// constant) take at most 2 passes; once the chosen bin holds exactly the remaining rank, the k-th key
+// is the bin's smallest (a wave min). hist: 256 words of LDS this wave alone uses (16-byte aligned).
+template <int EPT>
+__device__ __forceinline__ uint32_t wave_kth_key8(int k, const uint32_t (&key)[EPT], const bool (&ok)[EPT],
+                                                  uint32_t* hist) {
+  const int lane = threadIdx.x & 63;
+  uint32_t vo = 0u, va = ~0u;
+#pragma unroll
+  for (int e = 0; e < EPT; ++e)
+    if (ok[e]) {
+      vo |= key[e];
+      va &= key[e];
+    }
+  const uint32_t common = wave_and_u32(va), vary = wave_or_u32(vo) ^ common;
+  uint32_t prefix = 0, mask = 0;
+  int remaining = k;
+#pragma unroll 1
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    if (((vary >> shift) & 255u) == 0u) {
+      prefix |= common & (255u << shift);
+      mask |= 255u << shift;
+      continue;
+    }
+    reinterpret_cast<uint4*>(hist)[lane] = make_uint4(0u, 0u, 0u, 0u);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int e = 0; e < EPT; ++e)
+      if (ok[e] && (key[e] & mask) == prefix) __hip_atomic_fetch_add(&hist[(key[e] >> shift) & 255u], 1u,
+                                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __builtin_amdgcn_wave_barrier();
+    // lane l: bins 255-4l (c.w) .. 252-4l (c.x), highest first
+    const uint4 c = reinterpret_cast<const uint4*>(hist)[63 - lane];
+    const int ls = (int)(c.x + c.y + c.z + c.w);
+    int incl = ls;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += t;
+    }
+    const unsigned long long reach = __ballot(incl >= remaining);
+    if (!reach) return 0u;  // fewer than k valid
+    const int L = __builtin_ctzll(reach);
+    int run = incl - ls, dsel = 0, csel = 0;
+    {
+      const int cw = (int)c.w, cz = (int)c.z, cy = (int)c.y, cx = (int)c.x;
+      const int base = 255 - 4 * lane;
+      if (run + cw >= remaining) { dsel = base; csel = cw; }
+      else if (run + cw + cz >= remaining) { dsel = base - 1; csel = cz; run += cw; }
+      else if (run + cw + cz + cy >= remaining) { dsel = base - 2; csel = cy; run += cw + cz; }
+      else { dsel = base - 3; csel = cx; run += cw + cz + cy; }
+    }
+    dsel = __builtin_amdgcn_readlane(dsel, L);
+    csel = __builtin_amdgcn_readlane(csel, L);
+    run = __builtin_amdgcn_readlane(run, L);
+    prefix |= (uint32_t)dsel << shift;
+    mask |= 255u << shift;
+    remaining -= run;
+    if (csel == remaining) break;
+  }
+  // the top k are the keys above the chosen bins plus the whole last bin: the k-th is its smallest
+  uint32_t mn = ~0u;
+#pragma unroll
+  for (int e = 0; e < EPT; ++e)
+    if (ok[e] && (key[e] & mask) == prefix) mn = min(mn, key[e]);
+  return wave_min_u32(mn);
 }
 
 // Wave-wide inclusive prefix sum (Hillis-Steele over ds_bpermute shuffles)
@@ -2060,14 +2208,14 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
     const unsigned long long* __restrict__ seeds, long long step, float* __restrict__ ws,
     unsigned int* __restrict__ cnt, long long* __restrict__ out_ids, float* __restrict__ out_lp,
     int* __restrict__ out_kept) {
-  __shared__ float red[8 + MWG_NT];  // [0, 8): per-wave partials; [8, 8 + NT): thread maxima
+  __shared__ __attribute__((aligned(16))) float red[8 + MWG_NT];  // [0, 8): per-wave partials; [8, 8 + NT): thread maxima
   __shared__ __attribute__((aligned(16))) uint32_t cnt16[2 * MWG_NT / 64 * 8];
   __shared__ int sel[2];
   __shared__ int iscan[MWG_NT / 64];
   __shared__ int sh_last;
-  __shared__ float Lv[G * CMAX];
+  __shared__ __attribute__((aligned(16))) float Lv[G * CMAX];
   __shared__ int Li[G * CMAX];
-  __shared__ float L2v[G * CMAX];  // the candidates after the per-wave narrowing
+  __shared__ __attribute__((aligned(16))) float L2v[G * CMAX];  // the candidates after the per-wave narrowing
   __shared__ int L2i[G * CMAX];
   __shared__ __attribute__((aligned(16))) float hist[48];
   __shared__ float Kv[64];
@@ -2186,7 +2334,7 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
           mk[e] = fkey(v);
           mo[e] = v != -INFINITY;
         }
-        const uint32_t t = wave_kth_key<4>(kc, mk, mo);
+        const uint32_t t = wave_kth_key8<4>(kc, mk, mo, reinterpret_cast<uint32_t*>(Lv));  // (Lv: merge only)
         if (lane == 0) sel[0] = (int)t;
       }
       __syncthreads();
@@ -2264,6 +2412,22 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
 
   // ================= merge (the last workgroup of the row)
   if (tid == 0) cnt[b] = 0;  // re-armed for the next launch
+  // candidate slots: thread t takes slots [SPT t, SPT t + SPT) of one chunk's list, requested together
+  // with the chunk headers (one round trip; the slots past the chunk's count are ignored below)
+  constexpr int SPT = G * CMAX / MWG_NT;
+  static_assert(CMAX % SPT == 0, "a thread's slots within one chunk");
+  const int j0 = tid * SPT, qs = j0 / CMAX, p0 = j0 % CMAX;
+  const float* pqs = part + qs * (MWG_PART + 2 * CMAX);
+  float rv[SPT];
+  int ri[SPT], cq = 0;
+  if (!greedy) {
+#pragma unroll
+    for (int e = 0; e < SPT; ++e) {
+      rv[e] = pqs[MWG_PART + p0 + e];
+      ri[e] = reinterpret_cast<const int*>(pqs)[MWG_PART + CMAX + p0 + e];
+    }
+    cq = reinterpret_cast<const int*>(pqs)[3];
+  }
   float M = -INFINITY;
   for (int q = 0; q < G; ++q) M = fmaxf(M, part[q * (MWG_PART + 2 * CMAX)]);
   float Z = 0.f;
@@ -2288,29 +2452,21 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
     }
     return;
   }
-  // candidates >= T0, compacted into LDS in (chunk, position) = index order: thread t reads slots
-  // [8t, 8t + 8) of one chunk's list (no search, independent loads), a block scan places them
-  constexpr int SPT = G * CMAX / MWG_NT;
-  static_assert(CMAX % SPT == 0, "a thread's slots within one chunk");
+  // candidates >= T0, compacted into LDS in (chunk, position) = index order: a block scan places
+  // the slots loaded above
   int nv;
   {
     float sv[SPT];
     int si[SPT];
     int c = 0;
-    const int j0 = tid * SPT, q = j0 / CMAX, p0 = j0 % CMAX;
-    const float* pq = part + q * (MWG_PART + 2 * CMAX);
-    const int cq = reinterpret_cast<const int*>(pq)[3];
 #pragma unroll
     for (int e = 0; e < SPT; ++e) {
       sv[e] = -INFINITY;
       si[e] = 0;
-      if (p0 + e < cq) {
-        const float v = pq[MWG_PART + p0 + e];
-        if (fkey(v) >= T0) {
-          sv[e] = v;
-          si[e] = reinterpret_cast<const int*>(pq)[MWG_PART + CMAX + p0 + e];
-          ++c;
-        }
+      if (p0 + e < cq && fkey(rv[e]) >= T0) {
+        sv[e] = rv[e];
+        si[e] = ri[e];
+        ++c;
       }
     }
     int inc = c;
@@ -2367,12 +2523,39 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
       float above = 0.f, target = -1.f;
       // triple-buffered histogram: pass p accumulates into buffer p % 3 and, after its barrier,
       // clears buffer (p + 2) % 3 (read in pass p - 1, filled in pass p + 2); every lane picks the
-      // digit from its own read of the table (no broadcast round)
+      // digit from its own read of the table (no broadcast round). Digits all survivors share are
+      // forced (no pass, as in block_kth_key; p counts executed passes); Kj is free scratch here.
+      uint32_t vo = 0u, va = ~0u;
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+        if (lo[e] && lk[e] >= thr) {
+          vo |= lk[e];
+          va &= lk[e];
+        }
+      vo = wave_or_u32(vo);
+      va = wave_and_u32(va);
+      if (lane == 0) {
+        Kj[2 * wid] = (int)vo;
+        Kj[2 * wid + 1] = (int)va;
+      }
       if (tid < 48) hist[tid] = 0.f;
       __syncthreads();
+      vo = 0u;
+      va = ~0u;
+#pragma unroll
+      for (int w = 0; w < MWG_NT / 64; ++w) {
+        vo |= (uint32_t)Kj[2 * w];
+        va &= (uint32_t)Kj[2 * w + 1];
+      }
+      const uint32_t common = va, vary = vo ^ va;
       int pass = 0;
 #pragma unroll 1
-      for (int shift = 28; shift >= 0; shift -= 4, ++pass) {
+      for (int shift = 28; shift >= 0; shift -= 4) {
+        if (((vary >> shift) & 15u) == 0u) {
+          prefix |= common & (15u << shift);
+          mask |= 15u << shift;
+          continue;
+        }
         float* hb = hist + 16 * (pass % 3);
 #pragma unroll
         for (int e = 0; e < E; ++e)
@@ -2408,6 +2591,7 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
         prefix |= (uint32_t)dsel << shift;
         mask |= 15u << shift;
         above += run;
+        ++pass;
       }
       if (mask == 0xffffffffu && prefix > thr) thr = prefix;
     }
@@ -2507,7 +2691,8 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
       o8[e] = j < nv;
       k8[e] = o8[e] ? fkey(Lv[j]) : 0u;
     }
-    const uint32_t tw = wave_kth_key<SPT>(k, k8, o8);
+    // (L2v is written only after the barrier below: each wave's histogram lives there until then)
+    const uint32_t tw = wave_kth_key8<SPT>(k, k8, o8, reinterpret_cast<uint32_t*>(L2v) + 256 * wid);
     if (lane == 0) Kj[wid] = (int)tw;
     __syncthreads();
     uint32_t T1 = 0;
@@ -2557,7 +2742,8 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
         v4[e] = o4[e] ? L2v[j] : -INFINITY;
         k4[e] = fkey(v4[e]);
       }
-      const uint32_t thr = wave_kth_key<4>(k, k4, o4);
+      // (red[8..]: the thread maxima of the chunk phase, free in the merge until the block tail's scan)
+      const uint32_t thr = wave_kth_key8<4>(k, k4, o4, reinterpret_cast<uint32_t*>(red + 8));
       int kc = 0;
 #pragma unroll
       for (int e = 0; e < 4; ++e) kc += (o4[e] && k4[e] >= thr) ? 1 : 0;
@@ -2632,7 +2818,7 @@ KCA_API int kca_sample_logits(const void* logits, long long ld, int is_bf16, int
                               const float* rep_pen, void* seen, const int* slots,
                               const int* ban_ids, int n_ban, const unsigned long long* seeds,
                               long long step, float* ws, long long* out_ids, float* out_lp,
-                              int* out_kept, unsigned int* cnt, hipStream_t stream) {
+                              int* out_kept, unsigned int* cnt, int mwg_complete, hipStream_t stream) {
   if (B <= 0 || V <= 0 || !ws || !out_ids) return 1;
   static int mwg = -1;  // KCA_SAMPLE_MWG=0: every row on the one-workgroup kernels (A/B)
   if (mwg < 0) {
@@ -2661,6 +2847,10 @@ KCA_API int kca_sample_logits(const void* logits, long long ld, int is_bf16, int
     else KCA_SAMPLE_MWG_LAUNCH(16);
 #undef KCA_SAMPLE_MWG_LAUNCH
   }
+  // mwg_complete: the caller knows every row is greedy or has 1 <= top_k <= 64 -- rows the multi-workgroup
+  // merge always finishes -- so the closing one-workgroup kernel (4-5 us even when every row skips it,
+  // profiles/sampler_r5.txt) is not launched
+  if (use_mwg && mwg_complete) return hipGetLastError() == hipSuccess ? 0 : 2;
   static int compact = -1;  // KCA_SAMPLE_COMPACT=0: top-p / multinomial over the full vocabulary (A/B)
   if (compact < 0) {
     const char* e = getenv("KCA_SAMPLE_COMPACT");

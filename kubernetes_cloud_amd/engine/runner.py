@@ -773,7 +773,7 @@ class ModelRunner:
             self._outbufs[Bb] = ob
         return ob
 
-    def _step_body(self, st, Bb, Kb):
+    def _step_body(self, st, Bb, Kb, mc=False):
         pk = st["pk"]
         # chained tokens resolved on the device by the fused B = 1 step head (_layers_decode_fused)
         self._chain_src = (pk.d("chain"), st["ids"]) if (Bb == 1 and self._embed_head) else None
@@ -787,7 +787,7 @@ class ModelRunner:
         dops.sample_logits(logits, temperature=pk.d("temperature"), top_k=pk.d("top_k"), top_p=pk.d("top_p"),
                            rep_penalty=pk.d("rep"), seen=self.seen, slots=pk.d("slots"),
                            ban_ids=pk.d("bans").view(Bb, self.max_bans), seeds=pk.d("seeds"), step=0,
-                           ws=st["sws"], out_ids=st["ids"], out_logprobs=st["lps"])
+                           ws=st["sws"], out_ids=st["ids"], out_logprobs=st["lps"], mwg_complete=mc)
 
     # ----------------------------------------------------------- beam search
     @torch.no_grad()
@@ -879,6 +879,10 @@ class ModelRunner:
                 te[i], tk[i], tp[i], rp[i], sd[i] = 0.0, 0, 1.0, 1.0, 0
         if "rcos" in pk.fields or "pages" in pk.fields:
             self._fill_desc(a, Bb, pos, sl)
+        # every row (padding rows are greedy) on the multi-workgroup sampler: no closing kernel; the
+        # step graphs are keyed by it too
+        mc = bool(((~(te[:Bb] > 0)) | ((tk[:Bb] >= 1) & (tk[:Bb] <= dops.MWG_KMAX))).all())
+        gk = (Bb, Kb, mc)
         if chain_dst and prev is None:
             raise ValueError("rows chain their token from a previous launch, but prev is None")
         # chained tokens read on the device by the step's first kernel: the previous step wrote them into
@@ -887,7 +891,7 @@ class ModelRunner:
         # token from the output buffer their own first run already overwrote)
         fold = (bool(chain_dst) and Bb == 1 and self._embed_head
                 and prev.ids_dev.data_ptr() == st["ids"].data_ptr()
-                and (not self.use_graphs or (Bb, Kb) in self._graphs))
+                and (not self.use_graphs or gk in self._graphs))
         if fold:
             for d_, s_ in zip(chain_dst, chain_src):
                 ch[d_] = s_
@@ -902,12 +906,12 @@ class ModelRunner:
                 si = torch.tensor(chain_src, dtype=torch.long).to(self.device, non_blocking=True)
                 dst.index_copy_(0, di, prev.ids_dev.index_select(0, si))
         if self.use_graphs:
-            g = self._graphs.get((Bb, Kb))
+            g = self._graphs.get(gk)
             if g is None:
-                g = self._capture(st, Bb, Kb)
+                g = self._capture(st, Bb, Kb, mc)
             g.replay()
         else:
-            self._step_body(st, Bb, Kb)
+            self._step_body(st, Bb, Kb, mc)
         fl = st["flip"]
         fl[0] ^= 1
         k = fl[0]
@@ -921,12 +925,12 @@ class ModelRunner:
             ev = None
         return DecodeHandle(ids_h, lps_h, n, ev, st["ids"])
 
-    def _capture(self, st, Bb, Kb):
+    def _capture(self, st, Bb, Kb, mc=False):
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(2):  # warm up (allocator, hipBLASLt heuristics)
-                self._step_body(st, Bb, Kb)
+                self._step_body(st, Bb, Kb, mc)
         torch.cuda.current_stream().wait_stream(s)
         if self._pool is None:
             self._pool = torch.cuda.graph_pool_handle()
@@ -935,8 +939,8 @@ class ModelRunner:
         # capture runs; under the default global mode that query fails ("operation not permitted when
         # stream is capturing") and the watchdog aborts the process
         with torch.cuda.graph(g, pool=self._pool, capture_error_mode="thread_local"):
-            self._step_body(st, Bb, Kb)
-        self._graphs[(Bb, Kb)] = g
+            self._step_body(st, Bb, Kb, mc)
+        self._graphs[(Bb, Kb, mc)] = g
         return g
 
     @torch.no_grad()
@@ -953,7 +957,8 @@ class ModelRunner:
         ids, lps = dops.sample_logits(
             logits.contiguous(), temperature=f("temperature", torch.float32), top_k=f("top_k", torch.int32),
             top_p=f("top_p", torch.float32), rep_penalty=f("rep", torch.float32), seen=self.seen,
-            slots=f("slot", torch.int32), ban_ids=bans.to(dev), seeds=f("seed", torch.int64), step=0)
+            slots=f("slot", torch.int32), ban_ids=bans.to(dev), seeds=f("seed", torch.int64), step=0,
+            mwg_complete=dops.mwg_complete_rows([r["temperature"] for r in rows], [r["top_k"] for r in rows]))
         return ids.tolist(), lps.tolist()
 
 

@@ -104,7 +104,7 @@ _SIGS = {
     "kca_col2im2x2_nhwc": [P, P, I, I, I, I, P],
     "kca_pad_br_nhwc": [P, P, I, I, I, I, P],
     "kca_gemv_dual_ln": [P, P, I, P, P, I, P, P, P, P, P, P, P, F, P, P, P, P, I, P],
-    "kca_sample_logits": [P, LL, I, I, I, P, P, P, P, P, P, P, I, P, LL, P, P, P, P, P, P],
+    "kca_sample_logits": [P, LL, I, I, I, P, P, P, P, P, P, P, I, P, LL, P, P, P, P, P, I, P],
 }
 
 

@@ -296,12 +296,16 @@ def sample_logits(logits: torch.Tensor, *, temperature: torch.Tensor, top_k: tor
                   seen: torch.Tensor | None = None, slots: torch.Tensor | None = None,
                   ban_ids: torch.Tensor | None = None, seeds: torch.Tensor | None = None, step: int = 0,
                   ws: torch.Tensor | None = None, out_ids: torch.Tensor | None = None,
-                  out_logprobs: torch.Tensor | None = None, out_kept: torch.Tensor | None = None):
+                  out_logprobs: torch.Tensor | None = None, out_kept: torch.Tensor | None = None,
+                  mwg_complete: bool = False):
     """Per-row parameters (all [B]): temperature (<= 0 -> greedy), top_k (0 = off),
     top_p (1 = off), rep_penalty. ``seen`` is a [slots, V] uint8 mask of tokens
     already in each sequence (repetition penalty; the chosen id is marked).
     ``ban_ids`` [B, n] (-1 padded) get -inf. Returns (ids int64 [B], logprob [B])
-    where logprob is under the penalised, temperature-scaled distribution."""
+    where logprob is under the penalised, temperature-scaled distribution.
+    ``mwg_complete``: the caller guarantees every row is greedy or has 1 <= top_k <= MWG_KMAX
+    (``mwg_complete_rows``), so the multi-workgroup kernel finishes every row and the closing
+    one-workgroup kernel is not launched."""
     B, V = logits.shape
     dev = logits.device
     if out_ids is None:
@@ -318,10 +322,19 @@ def sample_logits(logits: torch.Tensor, *, temperature: torch.Tensor, top_k: tor
                   int(logits.dtype == torch.bfloat16), B, V, temperature.data_ptr(), top_k.data_ptr(),
                   top_p.data_ptr(), _lib.ptr(rep_penalty), _lib.ptr(seen), _lib.ptr(slots),
                   _lib.ptr(ban_ids), n_ban, _lib.ptr(seeds), int(step), ws.data_ptr(),
-                  out_ids.data_ptr(), out_logprobs.data_ptr(), _lib.ptr(out_kept), _lib.ptr(cnt), _lib.stream())
+                  out_ids.data_ptr(), out_logprobs.data_ptr(), _lib.ptr(out_kept), _lib.ptr(cnt),
+                  int(bool(mwg_complete)), _lib.stream())
         return out_ids, out_logprobs
     return sample_logits_reference(logits, temperature, top_k, top_p, rep_penalty, seen, slots, ban_ids,
                                    seeds, step, out_ids, out_logprobs, out_kept)
+
+
+MWG_KMAX = 64  # decode.hip: top-k rows the multi-workgroup sampler takes
+
+
+def mwg_complete_rows(temperatures, top_ks) -> bool:
+    """Host-side check for ``sample_logits(mwg_complete=True)``: every row greedy or 1 <= top_k <= 64."""
+    return all((not t > 0) or 1 <= int(k) <= MWG_KMAX for t, k in zip(temperatures, top_ks))
 
 
 def processed_logits_reference(logits, temperature, rep_penalty, seen, slots, ban_ids):

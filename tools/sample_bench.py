@@ -15,7 +15,8 @@ for B in (1, 32):
                           "topk50_topp0.95": (1.0, 50, 0.95), "topp0.95": (1.0, 0, 0.95)}.items():
         f = lambda v, dt: torch.full((B,), v, dtype=dt, device=dev)  # noqa: E731
         kw = dict(temperature=f(t, torch.float32), top_k=f(k, torch.int32), top_p=f(p, torch.float32),
-                  rep_penalty=f(1.0, torch.float32), seeds=torch.arange(B, device=dev))
+                  rep_penalty=f(1.0, torch.float32), seeds=torch.arange(B, device=dev),
+                  mwg_complete=dops.mwg_complete_rows([t] * B, [k] * B))  # as the decode engine passes it
         for _ in range(5):
             dops.sample_logits(logits, **kw)
         torch.cuda.synchronize()

@@ -4,9 +4,10 @@
     rocprofv3 --kernel-trace --output-format csv -d gpurun_out/samp -o s -- python3 tools/sample_bench.py
     python tools/sampler_profile.py gpurun_out/samp/s_kernel_trace.csv
 
-Every ``kca_sample_logits`` call ends with the one-workgroup kernel (sample_reg_kernel / sample_kernel,
-which skips the multi-workgroup rows), optionally preceded by sample_mwg_kernel; a call's time is
-the sum of its kernels. sample_bench.py runs, per batch size, each mode 5 + 200 times in a fixed
+Every ``kca_sample_logits`` call of the bench starts with sample_mwg_kernel (all its modes are
+multi-workgroup rows), followed by the closing one-workgroup kernel (sample_reg_kernel / sample_kernel)
+unless the caller passed mwg_complete (greedy / top-k rows, as the decode engine does); a call's time
+is the sum of its kernels. sample_bench.py runs, per batch size, each mode 5 + 200 times in a fixed
 order; the table gives the median over the 200 timed calls of each (batch, mode)."""
 import csv
 import statistics
@@ -18,15 +19,16 @@ BATCHES = [1, 32]
 
 def main(path):
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-    calls, cur = [], 0.0
+    calls = []
     for r in rows:
         name = r["Kernel_Name"]
         if not name.startswith(("sample_", "void sample_")):
             continue
-        cur += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-        if "sample_mwg_kernel" not in name:  # the closing one-workgroup kernel
-            calls.append(cur)
-            cur = 0.0
+        t = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        if "sample_mwg_kernel" in name or not calls:
+            calls.append(t)
+        else:  # the closing one-workgroup kernel of the call before
+            calls[-1] += t
     per = 205
     need = per * len(MODES) * len(BATCHES)
     if len(calls) < need:
