@@ -131,6 +131,11 @@ def _engine(pred, n: int, conc: int, seed: int = 0, kind: str = "kserve") -> dic
     return {"throughput_rps": n / dt, "latencies": lat, **_lat_stats(lat)}
 
 
+def _engine_stats(pred) -> dict | None:
+    eng = getattr(getattr(pred, "generator", None), "engine", None)
+    return dict(eng.stats) if eng is not None and hasattr(eng, "stats") else None
+
+
 def _lat_stats(lat: list) -> dict:
     lat = sorted(lat)
     n = len(lat)
@@ -166,9 +171,13 @@ def _levels(pred, model_name: str, new_tokens: int | None, levels=LEVELS, kind: 
             # compared with the engine passes on either side of it (drift and box noise show up as the
             # spread between the two engine passes), latency as mean +- sample stdev as load_test.py
             # reports it (tensorizer-isvc/benchmark/load_test.py:155-180)
+            st = _engine_stats(pred)
             e1 = _engine(pred, n, conc, seed=conc, kind=kind)
+            st1 = _engine_stats(pred)
             h = _client(srv.url, n, conc, model_name, conc, kind)
+            st2 = _engine_stats(pred)
             e2 = _engine(pred, n, conc, seed=conc, kind=kind)
+            st3 = _engine_stats(pred)
             e = _lat_stats(e1["latencies"] + e2["latencies"])
             e_rps = (e1["throughput_rps"] + e2["throughput_rps"]) / 2
             rec = {"concurrency": conc, "requests": n, "successes": h["successes"],
@@ -182,6 +191,10 @@ def _levels(pred, model_name: str, new_tokens: int | None, levels=LEVELS, kind: 
                    "engine_rps_passes": [round(e1["throughput_rps"], 3), round(e2["throughput_rps"], 3)],
                    "engine_mean_s": round(e["mean_latency_s"], 4), "engine_stdev_s": round(e["stdev_latency_s"], 4),
                    "engine_p50_s": round(e["p50_s"], 4), "engine_p99_s": round(e["p99_s"], 4)}
+            if st is not None:  # engine steps / prefill launches per pass (engine, HTTP, engine)
+                rec["steps_passes"] = [b["steps"] - a["steps"] for a, b in ((st, st1), (st1, st2), (st2, st3))]
+                rec["prefill_batches_passes"] = [b["prefill_batches"] - a["prefill_batches"]
+                                                 for a, b in ((st, st1), (st1, st2), (st2, st3))]
             rec["http_overhead_mean_ms"] = round((rec["http_mean_s"] - rec["engine_mean_s"]) * 1e3, 2)
             rec["http_rps_loss"] = round(1.0 - rec["http_rps"] / max(e_rps, 1e-9), 4)
             out.append(rec)

@@ -10,9 +10,15 @@ arguments) over a Unix-socket connection, and the engine process runs the real m
 an event loop thread of its own and sends the result back -- its per-request Python is the pickle of
 a small dict each way.
 
-    srv = FrontendServer(models, port)   # engine process: starts the child, serves the calls
+    srv = FrontendServer(models, port)   # engine process: starts the children, serves the calls
     ...
     srv.close()
+
+``workers`` front-end processes (KCA_HTTP_WORKERS, default 1) listen on the same port (SO_REUSEPORT:
+the kernel spreads connections over them), each with its own connection to the engine process. GPT-J
+at concurrency 32 served 121 req/s with 4 of them against 137 with one (bench/serving_bench.py,
+round 5): the per-request work left at that load is in the engine process (result pickling, the
+model coroutines' tokenisation, thread hand-offs), and more connections only add hand-offs there.
 
 Errors raised by the model (``InvalidInput``, ``ValueError`` ...) are re-raised in the front-end with
 their type, so the REST layer maps them to the same status codes.
@@ -44,31 +50,33 @@ def _rebuild_error(kind: str, msg: str) -> Exception:
 
 
 class _Engine:
-    """Engine-process side: one connection from the front-end; a reader thread, and the models'
-    coroutines on an event loop thread."""
+    """Engine-process side: one connection per front-end process, a reader thread each, and the
+    models' coroutines on ONE event loop thread."""
 
-    def __init__(self, models: dict, conn):
-        self.models, self.conn = models, conn
-        self.send_lock = threading.Lock()
+    def __init__(self, models: dict, conns: list):
+        self.models, self.conns = models, list(conns)
+        self.send_locks = [threading.Lock() for _ in self.conns]
         self.loop = asyncio.new_event_loop()
         self.loop_th = threading.Thread(target=self.loop.run_forever, name="kca-engine-loop", daemon=True)
         self.loop_th.start()
-        self.reader = threading.Thread(target=self._read, name="kca-frontend-reader", daemon=True)
-        self.reader.start()
+        self.readers = [threading.Thread(target=self._read, args=(i,), name=f"kca-frontend-reader-{i}", daemon=True)
+                        for i in range(len(self.conns))]
+        for th in self.readers:
+            th.start()
 
-    def _send(self, msg):
-        with self.send_lock:
-            self.conn.send(msg)
+    def _send(self, i, msg):
+        with self.send_locks[i]:
+            self.conns[i].send(msg)
 
-    def _read(self):
+    def _read(self, i):
         while True:
             try:
-                msg = self.conn.recv()
+                msg = self.conns[i].recv()
             except (EOFError, OSError):
                 return
-            asyncio.run_coroutine_threadsafe(self._handle(*msg), self.loop)
+            asyncio.run_coroutine_threadsafe(self._handle(i, *msg), self.loop)
 
-    async def _handle(self, rid, name, op, args):
+    async def _handle(self, i, rid, name, op, args):
         try:
             m = self.models[name]
             if op == "call":
@@ -77,16 +85,20 @@ class _Engine:
                 res = await asyncio.get_running_loop().run_in_executor(None, lambda: m.infer(*args))
             else:
                 raise ValueError(f"unknown operation {op}")
-            self._send((rid, True, res))
+            self._send(i, (rid, True, res))
         except Exception as e:  # noqa: BLE001 - every failure goes back to the waiting request
             kind = type(e).__name__
-            self._send((rid, False, (kind if kind in _ERRORS else "RuntimeError", str(e))))
+            try:
+                self._send(i, (rid, False, (kind if kind in _ERRORS else "RuntimeError", str(e))))
+            except OSError:  # that front-end process is gone
+                pass
 
     def close(self):
-        try:
-            self.conn.close()
-        except OSError:
-            pass
+        for c in self.conns:
+            try:
+                c.close()
+            except OSError:
+                pass
         self.loop.call_soon_threadsafe(self.loop.stop)
 
 
@@ -144,7 +156,8 @@ def _proxy_models(client: _Client, meta: dict):
 
 
 def _frontend_main():
-    """Child process: connect back, build the proxies, serve the REST app."""
+    """Child process: connect back, build the proxies, listen on the shared port, serve the REST app."""
+    import socket
     from multiprocessing.connection import Client
 
     import uvicorn
@@ -154,54 +167,86 @@ def _frontend_main():
     key = bytes.fromhex(os.environ.pop("KCA_FRONTEND_KEY"))
     conn = Client(addr, family="AF_UNIX", authkey=key)
     meta = conn.recv()  # {name: metadata}
-    client = _Client(conn)
-    app = ModelServer(http_port=port, argv=[]).create_app(_proxy_models(client, meta))
-    uvicorn.run(app, host=host, port=port, workers=1, log_level="warning", access_log=False)
+    app = ModelServer(http_port=port, argv=[]).create_app(_proxy_models(_Client(conn), meta))
+    fam = socket.AF_INET6 if ":" in host else socket.AF_INET
+    # (proto given explicitly: asyncio sets TCP_NODELAY only on sockets whose proto is IPPROTO_TCP --
+    # with proto 0 the accepted connections keep Nagle, +40 ms per response at concurrency 1)
+    sock = socket.socket(fam, socket.SOCK_STREAM, socket.IPPROTO_TCP)
+    sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+    sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEPORT, 1)
+    sock.bind((host, port))
+    sock.listen(2048)  # (connections queue here until the loop below runs)
+    conn.send("listening")  # (before any request: the client's reader only receives)
+    server = uvicorn.Server(uvicorn.Config(app, host=host, port=port, log_level="warning", access_log=False))
+    server.run(sockets=[sock])
 
 
 class FrontendServer:
-    """Engine process: start the front-end child on ``port`` and serve its model calls until
-    ``close()`` (the constructor returns once the child answers its health route)."""
+    """Engine process: start ``workers`` front-end processes on ``port`` and serve their model calls
+    until ``close()`` (the constructor returns once they listen and one answers the health route)."""
 
-    def __init__(self, models: list, port: int, host: str = "127.0.0.1", start_timeout: float = 120.0):
+    def __init__(self, models: list, port: int, host: str = "127.0.0.1", start_timeout: float = 120.0,
+                 workers: int | None = None):
         from multiprocessing.connection import Listener
 
         from . import server as _srv
-        if _srv.GIL_SWITCH_S > 0:  # this process's threads (engine loop, model loop, reader) hand off often
+        if _srv.GIL_SWITCH_S > 0:  # this process's threads (engine loop, model loop, readers) hand off often
             sys.setswitchinterval(_srv.GIL_SWITCH_S)
         self.port, self.host = port, host
+        self.workers = max(1, int(os.environ.get("KCA_HTTP_WORKERS", "1")) if workers is None else int(workers))
         self.models = {m.name: m for m in models}
         d = tempfile.mkdtemp(prefix="kca_frontend_")
         self.addr = os.path.join(d, "sock")
         key = secrets.token_bytes(16)
-        listener = Listener(self.addr, family="AF_UNIX", authkey=key)
+        listener = Listener(self.addr, family="AF_UNIX", authkey=key, backlog=max(self.workers, 1))
         env = dict(os.environ, KCA_FRONTEND_KEY=key.hex(), CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
         root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         env["PYTHONPATH"] = root + os.pathsep + env.get("PYTHONPATH", "")
-        self.proc = subprocess.Popen([sys.executable, "-m", "kubernetes_cloud_amd.serving.frontend", self.addr,
-                                      str(port), host], env=env)
-        got: list = []
-        th = threading.Thread(target=lambda: got.append(listener.accept()), daemon=True)
+        self.procs = [subprocess.Popen([sys.executable, "-m", "kubernetes_cloud_amd.serving.frontend", self.addr,
+                                        str(port), host], env=env) for _ in range(self.workers)]
+        self.proc = self.procs[0]
+        conns: list = []
+
+        def accept_all():
+            try:
+                while len(conns) < self.workers:
+                    conns.append(listener.accept())
+            except OSError:  # listener closed by the watchdog below
+                pass
+        th = threading.Thread(target=accept_all, daemon=True)
         th.start()
         t0 = time.time()
-        while th.is_alive():  # (accept has no timeout: watch the child instead)
-            th.join(timeout=0.2)
-            if self.proc.poll() is not None or time.time() - t0 > start_timeout:
-                listener.close()
-                self.proc.kill()
-                raise RuntimeError("HTTP front-end did not connect")
+        try:
+            while th.is_alive():  # (accept has no timeout: watch the children instead)
+                th.join(timeout=0.2)
+                if any(p.poll() is not None for p in self.procs) or time.time() - t0 > start_timeout:
+                    raise RuntimeError("HTTP front-end did not connect")
+            meta = {n: m.metadata() for n, m in self.models.items()}
+            for c in conns:
+                c.send(meta)
+            for c in conns:  # each child has bound and listens on the port
+                if not c.poll(start_timeout) or c.recv() != "listening":
+                    raise RuntimeError("HTTP front-end did not listen")
+        except BaseException:
+            listener.close()
+            self._kill()
+            raise
         listener.close()
-        conn = got[0]
-        conn.send({n: m.metadata() for n, m in self.models.items()})
-        self.engine = _Engine(self.models, conn)
+        self.engine = _Engine(self.models, conns)
         self._wait_ready(start_timeout)
+
+    def _kill(self):
+        for p in self.procs:
+            if p.poll() is None:
+                p.kill()
 
     def _wait_ready(self, timeout: float):
         import httpx
         t0 = time.time()
         while time.time() - t0 < timeout:
-            if self.proc.poll() is not None:
-                raise RuntimeError(f"HTTP front-end exited with {self.proc.returncode}")
+            dead = [p.returncode for p in self.procs if p.poll() is not None]
+            if dead:
+                raise RuntimeError(f"HTTP front-end exited with {dead[0]}")
             try:
                 if httpx.get(f"http://{self.host}:{self.port}/", timeout=2.0).status_code == 200:
                     return
@@ -211,12 +256,14 @@ class FrontendServer:
         raise RuntimeError("HTTP front-end did not start")
 
     def close(self):
-        self.proc.terminate()
-        try:
-            self.proc.wait(timeout=30)
-        except subprocess.TimeoutExpired:
-            self.proc.kill()
-            self.proc.wait(timeout=30)
+        for p in self.procs:
+            p.terminate()
+        for p in self.procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait(timeout=30)
         self.engine.close()
         try:
             os.unlink(self.addr)

@@ -1,6 +1,6 @@
-"""The REST front-end in its own process (serving/frontend.py): V1 predict, V2 infer and metadata through
-the proxy models, the model's errors mapped to the same status codes as in process, and concurrent
-requests answered in any order."""
+"""The REST front-end in processes of its own (serving/frontend.py, three sharing the port): V1 predict,
+V2 infer and metadata through the proxy models, the model's errors mapped to the same status codes as
+in process, and concurrent requests answered in any order."""
 import socket
 from concurrent.futures import ThreadPoolExecutor
 
@@ -40,7 +40,7 @@ def _port():
 
 def test_frontend_process_routes_errors_and_concurrency():
     port = _port()
-    fe = FrontendServer([Echo()], port)
+    fe = FrontendServer([Echo()], port, workers=3)
     try:
         base = f"http://127.0.0.1:{port}"
         r = httpx.post(f"{base}/v1/models/echo:predict", json={"instances": ["abc", "xyz"]})
@@ -53,10 +53,10 @@ def test_frontend_process_routes_errors_and_concurrency():
         out = httpx.post(f"{base}/v2/models/echo/infer", json=body).json()
         assert out["outputs"][0]["data"] == [2.0, 4.0, 6.0]
         words = [f"w{i:03d}" for i in range(48)]
-        with ThreadPoolExecutor(16) as ex:
+        with ThreadPoolExecutor(16) as ex:  # new connections: spread over the three front-end processes
             got = list(ex.map(lambda w: httpx.post(f"{base}/v1/models/echo:predict",
                                                    json={"instances": [w]}).json()["predictions"][0], words))
         assert got == [w[::-1] for w in words]
     finally:
         fe.close()
-    assert fe.proc.poll() is not None
+    assert len(fe.procs) == 3 and all(p.poll() is not None for p in fe.procs)
