@@ -143,13 +143,15 @@ def _lat_stats(lat: list) -> dict:
             "p50_s": lat[int(0.5 * (n - 1))], "p99_s": lat[int(0.99 * (n - 1))]}
 
 
-def _client(url: str, n: int, conc: int, model_name: str, seed: int, kind: str = "kserve") -> dict:
-    """serving/loadgen.py in its own process (as a client on another host would be): it does not
+def _client(url: str, n: int, conc: int, model_name: str, seed: int, kind: str = "kserve",
+            processes: int = 1) -> dict:
+    """serving/loadgen.py in its own process(es) (as a client on another host would be): it does not
     share the server's interpreter lock."""
     import subprocess
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     cmd = [sys.executable, "-m", "kubernetes_cloud_amd.serving.loadgen", "--url", url, f"--{kind}", "--requests",
-           str(n), "--concurrency", str(conc), "--model-name", model_name, "--seed", str(seed), "--json", "-q"]
+           str(n), "--concurrency", str(conc), "--model-name", model_name, "--seed", str(seed), "--json", "-q",
+           "--processes", str(processes)]
     env = dict(os.environ, PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""),
                CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=root)
@@ -166,7 +168,8 @@ def _levels(pred, model_name: str, new_tokens: int | None, levels=LEVELS, kind: 
         _engine(pred, 4, 4, seed=98, kind=kind)
         for conc, n in levels:
             # warm this level's batch buckets first (decode-graph captures), so no timed pass pays them
-            _engine(pred, 2 * conc, conc, seed=1000 + conc, kind=kind)
+            # (the full level: a shorter warm-up left the first timed engine pass 10-15 % slow at 32)
+            _engine(pred, n, conc, seed=1000 + conc, kind=kind)
             # interleaved engine / HTTP / engine passes over the same request stream: the HTTP pass is
             # compared with the engine passes on either side of it (drift and box noise show up as the
             # spread between the two engine passes), latency as mean +- sample stdev as load_test.py
@@ -174,7 +177,9 @@ def _levels(pred, model_name: str, new_tokens: int | None, levels=LEVELS, kind: 
             st = _engine_stats(pred)
             e1 = _engine(pred, n, conc, seed=conc, kind=kind)
             st1 = _engine_stats(pred)
-            h = _client(srv.url, n, conc, model_name, conc, kind)
+            # one client process per 8 in flight: one asyncio + httpx process is itself the bottleneck
+            # at concurrency 32 (~1-2 ms of client Python per request, profiles/serving_r5_frontend_ab.jsonl)
+            h = _client(srv.url, n, conc, model_name, conc, kind, processes=max(1, conc // 8))
             st2 = _engine_stats(pred)
             e2 = _engine(pred, n, conc, seed=conc, kind=kind)
             st3 = _engine_stats(pred)

@@ -96,13 +96,40 @@ def run_sync(reqs, timeout: float):
     return times, total
 
 
+def _proc_worker(args):
+    """One client process of ``benchmark(processes=P)``: wait for the common start time, then run its
+    share -> (latencies, wall-clock first send, wall-clock last response)."""
+    reqs, concurrency, timeout, start_at = args
+    time.sleep(max(0.0, start_at - time.time()))
+    t0 = time.time()
+    times, total = asyncio.run(run_async(reqs, concurrency, timeout))
+    return times, t0, t0 + total
+
+
+def run_processes(reqs, concurrency: int, timeout: float, processes: int):
+    """The async client split over ``processes`` processes (request i to process i % P, concurrency
+    divided among them) starting at one wall-clock instant: a single asyncio + httpx process spends
+    ~1-2 ms of Python per request, which at concurrency 32 is itself the bottleneck."""
+    import multiprocessing as mp
+    P = max(1, min(processes, concurrency))
+    shares = [reqs[i::P] for i in range(P)]
+    concs = [concurrency // P + (1 if i < concurrency % P else 0) for i in range(P)]
+    start_at = time.time() + 3.0  # (room for the children's interpreter start and imports)
+    with mp.get_context("spawn").Pool(P) as pool:
+        outs = pool.map(_proc_worker, [(sh, c, timeout, start_at) for sh, c in zip(shares, concs)])
+    times = [t for o in outs for t in o[0]]
+    return times, max(o[2] for o in outs) - min(o[1] for o in outs)
+
+
 def benchmark(url: str, kind: str, n: int, asynchronous: bool = True, concurrency: int | None = None,
-              model: str = "gptj", prompts=None, timeout: float = 600.0, seed: int = 0) -> dict:
+              model: str = "gptj", prompts=None, timeout: float = 600.0, seed: int = 0, processes: int = 1) -> dict:
     rnd = random.Random(seed)
     prompts = prompts or PROMPTS
     reqs = [build_request(kind, url.rstrip("/"), rnd.choice(prompts), model, i) for i in range(n)]
     print("Started benchmark", flush=True)
-    if asynchronous:
+    if asynchronous and processes > 1:
+        times, total = run_processes(reqs, concurrency or n, timeout, processes)
+    elif asynchronous:
         times, total = asyncio.run(run_async(reqs, concurrency or n, timeout))
     else:
         times, total = run_sync(reqs, timeout)
@@ -145,6 +172,7 @@ def main(argv=None):
     p.add_argument("--prompts-file", default="")
     p.add_argument("--json", action="store_true")
     p.add_argument("--seed", type=int, default=0, help="prompt choice seed")
+    p.add_argument("--processes", type=int, default=1, help="client processes sharing the load (async mode)")
     p.add_argument("--verbose", "-v", dest="log_level", action="store_const", const=logging.INFO)
     p.add_argument("--quiet", "-q", dest="log_level", action="store_const", const=logging.ERROR)
     a = p.parse_args(argv)
@@ -156,7 +184,7 @@ def main(argv=None):
         with open(a.prompts_file) as f:
             prompts = [ln.strip() for ln in f if ln.strip()]
     r = benchmark(a.url, a.kind, a.requests, a.asynchronous, a.concurrency or None, a.model_name, prompts,
-                  seed=a.seed)
+                  seed=a.seed, processes=a.processes)
     print(json.dumps(r)) if a.json else report(r)
     return r
 
