@@ -71,6 +71,7 @@ class SDPredictor(Model):
         self.parameters = {"GUIDANCE_SCALE": guidance_scale, "NUM_INFERENCE_STEPS": num_inference_steps,
                            "SEED": seed, "WIDTH": width, "HEIGHT": height}
         self.max_batch, self.window = max_batch, batch_window_ms / 1000.0
+        self.expect_wait = float(os.getenv("BATCH_EXPECT_WAIT_MS", 50.0)) / 1000.0
         self.deterministic = deterministic
         self.pipeline = pipeline
         self.device = device
@@ -138,7 +139,11 @@ class SDPredictor(Model):
         fut: Future = Future()
         self._q.put((request["prompt"], rp, fut))
         self._ensure_worker()
-        return fut.result()
+        # the batcher hands back the image; its PNG is encoded here, in the request's own thread: encoded
+        # on the batcher thread, the batch's 8 responses left ~10-20 ms apart, the next wave of requests
+        # arrived as far apart, and the 5 ms collection window split it (concurrency 8 over HTTP: 5.1 ->
+        # 3.6 images/s with a 3.5 s p99 in one run)
+        return png_bytes(fut.result())
 
     # ------------------------------------------------------ micro-batcher
     def _ensure_worker(self):
@@ -147,23 +152,30 @@ class SDPredictor(Model):
             self._worker.start()
 
     def _loop(self):
+        # collection: ``window`` after the first request -- but while fewer requests wait than the last
+        # batch held (its clients are likely sending their next ones: over HTTP the responses, and so the
+        # next requests, arrive spread over more than the window) up to ``expect_wait`` (50 ms, ~7 % of
+        # a 512 px batch); one short batch resets the expectation
         pending = []
+        expect = 1
         while True:
             if not pending:
                 pending.append(self._q.get())
-            deadline = time.perf_counter() + self.window
+            t0 = time.perf_counter()
             while len(pending) < 4 * self.max_batch:
+                wait = self.window if len(pending) >= expect else max(self.window, self.expect_wait)
                 try:
-                    pending.append(self._q.get(timeout=max(0.0, deadline - time.perf_counter())))
+                    pending.append(self._q.get(timeout=max(0.0, t0 + wait - time.perf_counter())))
                 except queue.Empty:
                     break
             key = self._key(pending[0][1])
             batch = [x for x in pending if self._key(x[1]) == key][: self.max_batch]
             pending = [x for x in pending if x not in batch]
+            expect = len(batch)
             try:
                 imgs = self.generate([b[0] for b in batch], batch[0][1], [b[1]["SEED"] for b in batch])
                 for (_, _, fut), im in zip(batch, imgs):
-                    fut.set_result(png_bytes(im))
+                    fut.set_result(im)
             except Exception as e:  # noqa: BLE001
                 for _, _, fut in batch:
                     fut.set_exception(e)
