@@ -1,6 +1,10 @@
 #!/bin/bash
 # Sampler change check on one GPU: draw identity against the previous library, the sampler tests,
 # segment stamps and per-mode kernel times (tools/sampler_profile.py).
+# Needs (built on the CPU first): ab/libkca_kernels_old.so -- the baseline commit's kernels, e.g.
+#   git worktree add ab/oldtree <commit> && (cd ab/oldtree && python tools/build_ext.py) &&
+#   cp ab/oldtree/kubernetes_cloud_amd/_lib/libkca_kernels.so ab/libkca_kernels_old.so
+# -- and ab/libkca_kernels_stamps.so (python tools/build_ext.py --stamps).
 set -o pipefail
 cd /root/repo && mkdir -p gpurun_out/samp && export TMPDIR=/tmp
 KCA_KERNEL_LIB=$PWD/ab/libkca_kernels_old.so timeout -k 10 120 python tools/sampler_identity.py --out gpurun_out/samp/old.pt &&
