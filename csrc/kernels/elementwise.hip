@@ -274,6 +274,47 @@ KCA_API int kca_accum_grad(float* acc, const void* g, float scale,
   return 0;
 }
 
+// The first two micro-batches' gradients of one parameter in one pass: acc = g1 * scale + g2 * scale
+// (the same rounding as kca_accum_grad overwrite-then-accumulate, the fp32 accumulator written once
+// instead of written, re-read and re-written: 8 instead of 14 bytes per element over the pair)
+__global__ void accum_grad_pair_kernel(float* __restrict__ acc, const bf16_t* __restrict__ g1,
+                                       const bf16_t* __restrict__ g2, float scale, long long n8) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8;
+       i += (long long)gridDim.x * blockDim.x) {
+    float v1[8], v2[8], a[8];
+    load8(g1 + i * 8, v1);
+    load8(g2 + i * 8, v2);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      a[j] = v1[j] * scale;
+      a[j] += v2[j] * scale;
+    }
+    store8f(acc + i * 8, a);
+  }
+}
+
+__global__ void accum_grad_pair_tail_kernel(float* acc, const bf16_t* g1, const bf16_t* g2, float scale,
+                                            long long start, long long n) {
+  long long i = start + blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (i < n) {
+    float a = bf2f(g1[i]) * scale;
+    a += bf2f(g2[i]) * scale;
+    acc[i] = a;
+  }
+}
+
+KCA_API int kca_accum_grad_pair(float* acc, const void* g1, const void* g2, float scale, long long n,
+                                hipStream_t stream) {
+  const long long n8 = n / 8;
+  if (n8)
+    hipLaunchKernelGGL(accum_grad_pair_kernel, dim3(kca_grid(n8, 256)), dim3(256), 0, stream, acc,
+                       (const bf16_t*)g1, (const bf16_t*)g2, scale, n8);
+  if (n % 8)
+    hipLaunchKernelGGL(accum_grad_pair_tail_kernel, dim3(1), dim3(64), 0, stream, acc, (const bf16_t*)g1,
+                       (const bf16_t*)g2, scale, n8 * 8, n);
+  return 0;
+}
+
 // Many small gradients in one launch: the SD UNet has ~690 parameters, most of them norms,
 // biases and small projections, and one kca_accum_grad launch each cost ~5 us of GPU time per
 // micro-batch (profiled DreamBooth step) for a few KB of work. The entries {dst fp32*, src bf16*,

@@ -54,6 +54,7 @@ _SIGS = {
     "kca_geglu_bwd": [P, P, P, LL, I, P],
     "kca_rope": [P, P, I, I, LL, I, LL, LL, LL, LL, I, I, P, P, P, F, P],
     "kca_accum_grad": [P, P, F, I, LL, P],
+    "kca_accum_grad_pair": [P, P, P, F, LL, P],
     "kca_accum_grad_multi": [P, I, F, P],
     "kca_cast_f32_bf16": [P, P, LL, P],
     "kca_ema": [P, P, F, LL, P],

@@ -827,6 +827,24 @@ def test_accum_grad_multi_matches_reference():
     assert torch.allclose(flat, ref, rtol=1e-6, atol=1e-6)
 
 
+@pytest.mark.parametrize("n", [8, 4096 + 5, 1 << 20])
+def test_accum_grad_pair_bitwise_equals_two_passes(n):
+    """kca_accum_grad_pair (train/engine.py lands micro-batches 0 and 1 together) writes exactly what
+    kca_accum_grad overwrite-then-accumulate writes (same products, same fma), and both match fp32."""
+    torch.manual_seed(3)
+    g1 = torch.randn(n, device=DEV, dtype=torch.bfloat16)
+    g2 = torch.randn(n, device=DEV, dtype=torch.bfloat16)
+    two = torch.full((n,), float("nan"), device=DEV)
+    one = torch.full((n,), float("nan"), device=DEV)
+    st = _lib.stream()
+    _lib.call("kca_accum_grad", two.data_ptr(), g1.data_ptr(), 0.5, 1, n, st)
+    _lib.call("kca_accum_grad", two.data_ptr(), g2.data_ptr(), 0.5, 0, n, st)
+    _lib.call("kca_accum_grad_pair", one.data_ptr(), g1.data_ptr(), g2.data_ptr(), 0.5, n, st)
+    torch.cuda.synchronize()
+    assert torch.equal(one, two)
+    assert torch.allclose(one, (g1.float() + g2.float()) * 0.5, rtol=1e-6, atol=1e-7)
+
+
 @pytest.mark.parametrize("causal", [True, False])
 def test_attention_w8_forward_matches_4wave_and_fp32(causal):
     """The 8-wave D = 256 forward (LDS-DMA staging, 256-row blocks, asm LDS reads; bit 0 of
