@@ -1,0 +1,501 @@
+// Batched-decode GEMM on the matrix cores: y[M, N] = epilogue(x[M, K] . W[N, K]^T), M = 1..64.
+//
+// FasterTransformer's / DS-Inference's decoder at batch > 1 (max_batch_size 1024 in the FT GPT-J /
+// NeoX services, the BLOOM predictors' batched instances): every decode linear streams its weight
+// once per step and does 2*M FLOP per weight element -- 64 FLOP/B at M = 64, 4x what the VALU can
+// issue next to an 8 TB/s stream once the bf16 -> fp32 unpacking is counted. So the dot products run
+// on v_mfma_f32_16x16x32_{bf16,f16}, and the kernel is built around the weight stream
+// (measurements: profiles/stream_probe_r6.jsonl, profiles/mm_bench_r6_*.jsonl):
+//
+//   * weight: each wave owns NRW 16-row tiles of the workgroup's N block and streams them as row
+//     runs (RPI rows x KC*2 contiguous bytes per load instruction, non-temporal). The mfma A-operand
+//     map itself (16 rows x 64 B per instruction) tops out near 5 TB/s; 256-B-1-KB row runs reach
+//     6-6.8. The run is transposed through the wave's own LDS slot, 16-B pieces XOR-swizzled by row
+//     (conflict-free writes and ds_read_b128 fragment reads), one chunk prefetched in registers.
+//   * activation: the workgroup's 4 waves split N, not K, so they share each K chunk of x: staged
+//     once per workgroup in LDS (double-buffered, same swizzle), read as B fragments. Per-wave K
+//     splits re-read x from L2 once per wave -- as many bytes as the weight itself at M = 16, which
+//     capped the first version at 3-4 TB/s and 1.2-1.8 TB/s at M = 64.
+//   * LN-on-load: when the activation is the residual stream h, its per-row (mean, rstd) -- published
+//     by the previous projection's tail (mm_tail.h) -- and gamma / beta normalise the chunk as it is
+//     staged (once per workgroup), ln_rows' math rounded to the element type. No LayerNorm launch,
+//     no normalised-row buffer.
+//   * K split over workgroups (grid.y) so a launch fills the chip whatever N is: fp32 partial tiles
+//     published write-through, the last arriving workgroup of an N block sums them (fan-in counter
+//     per block, re-armed) and runs the epilogue.
+//   * epilogues: bias + GELU (fc_in); bias + residual add -> new residual stream, plus the row-stats
+//     tail (out-projection / fc_out), whose last arriver writes the next LayerNorm's (mean, rstd).
+//   * two jobs per launch: N-concatenated (QKV and fc_in of a parallel-residual layer share their
+//     input) or one job with two K-concatenated parts (GPT-J's out-projection + fc_out into one
+//     residual: y = o.Wo^T + g.Wf^T).
+//
+// SURVEY N6 / K1 / K5 (decode shapes); the batch-1 GEMV path is gemv.hip / decode.hip.
+#include "common.h"
+#include "gemv_m1.h"
+#include "mm_tail.h"
+
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+// DT 0 = bf16, 1 = fp16 (FasterTransformer / DS-Inference serve fp16)
+template <int DT>
+__device__ __forceinline__ float e2f(uint32_t u16) {
+  if constexpr (DT == 0) return __uint_as_float(u16 << 16);
+  else return (float)__builtin_bit_cast(_Float16, (uint16_t)u16);
+}
+template <int DT>
+__device__ __forceinline__ uint32_t f2e(float f) {
+  if constexpr (DT == 0) return (uint32_t)f2bf(f);
+  else return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)f);
+}
+
+template <int DT>
+__device__ __forceinline__ f32x4 mfma16(const u32x4v& a, const u32x4v& b, const f32x4& c) {
+  if constexpr (DT == 0)
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                   0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0,
+                                                  0, 0);
+}
+
+__device__ __forceinline__ u32x4v ld_nt16(const uint16_t* p) {
+  return __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(p));
+}
+__device__ __forceinline__ u32x4v ld16(const uint16_t* p) { return *reinterpret_cast<const u32x4v*>(p); }
+
+struct MmPart {
+  const uint16_t* x;      // [M, K] activation rows (row stride ldx)
+  long long ldx;
+  const uint16_t* w;      // [N, K] weight (row stride ldw)
+  long long ldw;
+  int K;
+  const float* stats;     // [M][2] (mean, rstd): x is the residual stream, normalised on load (or null)
+  const uint16_t* gamma;  // [K] (with stats)
+  const uint16_t* beta;   // [K] (nullable)
+};
+
+struct MmJob {
+  MmPart p[2];
+  int nparts;             // 1, or 2: K-concatenated parts summed into one output
+  int N;
+  int tiles;              // workgroups of this job (set by the host entry point)
+  const uint16_t* bias;   // [N] (nullable)
+  int act;                // 0 none, 1 GELU tanh, 2 GELU erf (not with res)
+  uint16_t* y;            // [M, N] (row stride ldy)
+  long long ldy;
+  const uint16_t* res;    // [M, N] residual added after the bias (nullable; may alias y)
+  long long ldr;
+  float* part;            // row-stats tail (nullable): RowStats.part
+  float* stats_out;       // RowStats.stats
+  unsigned* cnt;          // RowStats.cnt
+  float eps;
+};
+
+struct MmArgs {
+  MmJob j[2];
+  int njobs;
+  int M;
+  int ks;         // K split over workgroups (0: host picks; the kernel sees the chosen value)
+  int nr;         // 16-row weight tiles per wave (0: host picks)
+  float* ws;      // split-K partial tiles (ks > 1): kca_mm_skinny_plan floats
+  unsigned* bcnt; // per-N-block arrival counters (ks > 1), zero-initialised, re-armed every launch
+  long long ws_floats;
+  int bcnt_n;
+  int pad_;
+};
+
+// One finished 16x16 tile: rows n_base + 4*(lane>>4) + i (i < 4) of the output's N axis, column m =
+// mt*16 + (lane & 15) of its M axis (the mfma_f32_16x16x32 C layout).
+template <int DT>
+__device__ __forceinline__ void mm_store(const MmJob& J, int M, int n_base, int mt, int lane, const f32x4& v,
+                                         int tile) {
+  const int r16 = lane & 15, g = lane >> 4;
+  const int m = mt * 16 + r16;
+  const int n = n_base + g * 4;
+  const bool nok = n < J.N, ok = nok && m < M;
+  float o[4] = {v[0], v[1], v[2], v[3]};
+  if (J.bias && nok) {
+    const uint2 b = *reinterpret_cast<const uint2*>(J.bias + n);
+    o[0] += e2f<DT>(b.x & 0xffffu);
+    o[1] += e2f<DT>(b.x >> 16);
+    o[2] += e2f<DT>(b.y & 0xffffu);
+    o[3] += e2f<DT>(b.y >> 16);
+  }
+  if (J.act == 1) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = gelu_tanh(o[i]);
+  } else if (J.act == 2) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = 0.5f * o[i] * (1.f + erff(o[i] * 0.70710678118654752f));
+  }
+  if (J.res && ok) {
+    const uint2 r = *reinterpret_cast<const uint2*>(J.res + (long long)m * J.ldr + n);
+    o[0] += e2f<DT>(r.x & 0xffffu);
+    o[1] += e2f<DT>(r.x >> 16);
+    o[2] += e2f<DT>(r.y & 0xffffu);
+    o[3] += e2f<DT>(r.y >> 16);
+  }
+  uint32_t q[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) q[i] = f2e<DT>(o[i]);
+  if (ok) *reinterpret_cast<uint2*>(J.y + (long long)m * J.ldy + n) = make_uint2(q[0] | (q[1] << 16), q[2] | (q[3] << 16));
+  if (J.part) {
+    // statistics over the rounded new residual stream (ln_rows' convention); every lane shuffles
+    float f[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) f[i] = e2f<DT>(q[i]);
+    float mean_t, m2_t;
+    rs_tile16(f, mean_t, m2_t);
+    if (g == 0 && m < M) {
+      const RowStats s{J.part, J.stats_out, J.cnt, M, J.N, J.eps};
+      rs_publish(s, m, tile, mean_t, m2_t);
+    }
+  }
+}
+
+constexpr int MM_WAVES = 4;  // waves per workgroup (they split the workgroup's N block)
+
+// Wave-local ordering of the LDS transpose: the lanes that read a fragment are not the lanes that
+// wrote it, so the compiler must not move a read above the writes; the LDS runs one wave's
+// operations in issue order.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Chunk c of the job's concatenated K (part 0's chunks, then part 1's): part index and offset.
+__device__ __forceinline__ int chunk_part(const MmJob& J, int c, int nc0, int kc, int& k0) {
+  const int pi = (J.nparts > 1 && c >= nc0) ? 1 : 0;
+  k0 = (c - (pi ? nc0 : 0)) * kc;
+  return pi;
+}
+
+template <int MT, int NRW, int KC>
+struct MmTile {
+  static constexpr int PPR = KC / 8;    // 16-B pieces per row per chunk
+  static constexpr int RPI = 64 / PPR;  // weight rows per load instruction
+  static constexpr int NI = 16 / RPI;   // load instructions per 16-row tile
+  static constexpr int S = KC / 32;     // MFMA steps per chunk
+  static constexpr int XP = (MT * 16 * PPR + 255) / 256;  // x pieces per thread per chunk
+  static constexpr int XS = MT * 16 * KC;                 // one x stage (elements)
+  static constexpr int SLOT = NRW * 16 * KC;              // one wave's transpose slot (elements)
+  static constexpr int LDS = (2 * XS + MM_WAVES * SLOT) * 2;
+  static_assert(PPR >= 16 && PPR <= 64, "swizzle needs 16..64 pieces per row");
+};
+
+template <int DT, int MT, int NRW, int KC, bool LN>
+__global__ __launch_bounds__(256) void mm_skinny_kernel(MmArgs a) {
+  using T = MmTile<MT, NRW, KC>;
+  extern __shared__ __attribute__((aligned(16))) uint16_t mm_lds[];  // xs[2][MT*16][KC], slots[4][NRW*16][KC]
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int r16 = lane & 15, g = lane >> 4;
+  int b = blockIdx.x;
+  const int bglob = b;
+  const bool second = b >= a.j[0].tiles;
+  const MmJob& J = second ? a.j[1] : a.j[0];
+  if (second) b -= a.j[0].tiles;
+  const int M = a.M, N = J.N;
+  const int kz = blockIdx.y, KS = gridDim.y;
+  const int nw0 = b * (MM_WAVES * NRW * 16) + wv * (NRW * 16);  // this wave's first row
+  uint16_t* xs = mm_lds;
+  uint16_t* slot = mm_lds + 2 * T::XS + wv * T::SLOT;
+
+  // K chunks of the concatenated parts, this workgroup's share [c_lo, c_hi)
+  const int nc0 = (J.p[0].K + KC - 1) / KC;
+  const int nct = nc0 + (J.nparts > 1 ? (J.p[1].K + KC - 1) / KC : 0);
+  const int per = (nct + KS - 1) / KS;
+  const int c_lo = kz * per, c_hi = min(nct, c_lo + per);
+
+  // weight load map: lane takes row lr of each instruction, piece lp
+  const int lr = lane / T::PPR, lp = lane % T::PPR;
+  auto load_w = [&](int c, u32x4v (&wr)[NRW][T::NI]) {
+    int k0;
+    const MmPart& P = J.p[chunk_part(J, c, nc0, KC, k0)];
+    const bool kv = k0 + lp * 8 < P.K;
+#pragma unroll
+    for (int nr = 0; nr < NRW; ++nr)
+#pragma unroll
+      for (int i = 0; i < T::NI; ++i) {
+        int n = nw0 + nr * 16 + i * T::RPI + lr;
+        n = n < N ? n : N - 1;  // rows past N: any valid row (their outputs are never stored)
+        wr[nr][i] = kv ? ld_nt16(P.w + (long long)n * P.ldw + k0 + lp * 8) : u32x4v{0u, 0u, 0u, 0u};
+      }
+  };
+  // activation chunk: piece q = tid + 256 j of the [MT*16][PPR] stage
+  auto load_x = [&](int c, u32x4v (&xr)[T::XP]) {
+    int k0;
+    const MmPart& P = J.p[chunk_part(J, c, nc0, KC, k0)];
+#pragma unroll
+    for (int j = 0; j < T::XP; ++j) {
+      const int q = tid + 256 * j, m = q / T::PPR, k = k0 + (q % T::PPR) * 8;
+      xr[j] = u32x4v{0u, 0u, 0u, 0u};
+      if (m < M && k < P.K) {
+        xr[j] = ld16(P.x + (long long)m * P.ldx + k);
+        if constexpr (LN) {
+          const float mu = P.stats[2 * m], rs = P.stats[2 * m + 1];
+          const u32x4v gv = ld16(P.gamma + k);
+          const u32x4v bv = P.beta ? ld16(P.beta + k) : u32x4v{0u, 0u, 0u, 0u};
+          u32x4v o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const uint32_t hx = xr[j][e], gg = gv[e], bb = bv[e];
+            const float lo = (e2f<DT>(hx & 0xffffu) - mu) * rs * e2f<DT>(gg & 0xffffu) + e2f<DT>(bb & 0xffffu);
+            const float hi = (e2f<DT>(hx >> 16) - mu) * rs * e2f<DT>(gg >> 16) + e2f<DT>(bb >> 16);
+            o[e] = f2e<DT>(lo) | (f2e<DT>(hi) << 16);
+          }
+          xr[j] = o;
+        }
+      }
+    }
+  };
+  auto store_x = [&](const u32x4v (&xr)[T::XP], int buf) {
+#pragma unroll
+    for (int j = 0; j < T::XP; ++j) {
+      const int q = tid + 256 * j, m = q / T::PPR, p = q % T::PPR;
+      if (m < MT * 16)
+        *reinterpret_cast<u32x4v*>(xs + buf * T::XS + m * KC + ((p ^ (m & 15)) << 3)) = xr[j];
+    }
+  };
+
+  f32x4 acc[NRW][MT];
+#pragma unroll
+  for (int nr = 0; nr < NRW; ++nr)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[nr][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  u32x4v wn[NRW][T::NI];
+  u32x4v xr[T::XP];
+  if (c_lo < c_hi) {
+    load_w(c_lo, wn);
+    load_x(c_lo, xr);
+    store_x(xr, 0);
+  }
+  __syncthreads();
+  for (int c = c_lo; c < c_hi; ++c) {
+    const int buf = (c - c_lo) & 1;
+    u32x4v wc[NRW][T::NI];
+#pragma unroll
+    for (int nr = 0; nr < NRW; ++nr)
+#pragma unroll
+      for (int i = 0; i < T::NI; ++i) wc[nr][i] = wn[nr][i];
+    const bool nx = c + 1 < c_hi;
+    if (nx) {  // next chunk in flight under this one
+      load_w(c + 1, wn);
+      load_x(c + 1, xr);
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int nr = 0; nr < NRW; ++nr)
+#pragma unroll
+      for (int i = 0; i < T::NI; ++i) {
+        const int row = i * T::RPI + lr;
+        *reinterpret_cast<u32x4v*>(slot + (nr * 16 + row) * KC + ((lp ^ (row & 15)) << 3)) = wc[nr][i];
+      }
+    wave_lds_sync();
+    const uint16_t* xb = xs + buf * T::XS;
+#pragma unroll
+    for (int st = 0; st < T::S; ++st) {
+      u32x4v bf[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+        bf[mt] = *reinterpret_cast<const u32x4v*>(xb + (mt * 16 + r16) * KC + (((4 * st + g) ^ r16) << 3));
+#pragma unroll
+      for (int nr = 0; nr < NRW; ++nr) {
+        const u32x4v af = *reinterpret_cast<const u32x4v*>(slot + (nr * 16 + r16) * KC + (((4 * st + g) ^ r16) << 3));
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc[nr][mt] = mfma16<DT>(af, bf[mt], acc[nr][mt]);
+      }
+    }
+    if (nx) store_x(xr, buf ^ 1);
+    __syncthreads();
+  }
+
+  // split-K: publish this slice's tiles, the last arriving slice of the N block sums and stores
+  bool fin = true;
+  if (KS > 1) {
+    constexpr int TPW = NRW * MT;  // tiles per wave
+    const long long blk = (long long)bglob * (MM_WAVES * TPW) + wv * TPW;
+    const long long nblk = (long long)gridDim.x * (MM_WAVES * TPW);
+#pragma unroll
+    for (int nr = 0; nr < NRW; ++nr)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        float* d = a.ws + ((kz * nblk + blk + nr * MT + mt) * 64 + lane) * 4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) st_pub(d + e, acc[nr][mt][e]);
+      }
+    __shared__ int s_fin;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      unsigned* bc = a.bcnt + bglob;
+      const int last = __hip_atomic_fetch_add(bc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)KS - 1;
+      if (last) {
+        __hip_atomic_store(bc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      s_fin = last;
+    }
+    __syncthreads();
+    fin = s_fin != 0;
+    if (fin) {
+      for (int z = 0; z < KS; ++z) {
+        if (z == kz) continue;
+#pragma unroll
+        for (int nr = 0; nr < NRW; ++nr)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) {
+            const float* d = a.ws + ((z * nblk + blk + nr * MT + mt) * 64 + lane) * 4;
+            acc[nr][mt] += *reinterpret_cast<const f32x4*>(d);
+          }
+      }
+    }
+  }
+  if (!fin) return;  // (workgroup-uniform)
+#pragma unroll
+  for (int nr = 0; nr < NRW; ++nr)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+      mm_store<DT>(J, M, nw0 + nr * 16, mt, lane, acc[nr][mt], (nw0 >> 4) + nr);
+  if (J.part) {
+    const RowStats s{J.part, J.stats_out, J.cnt, M, J.N, J.eps};
+    rs_arrive_of(s, b, J.tiles);
+  }
+}
+
+// launch-shape knob (same-box A/B): workgroups a launch aims for when it splits K
+static int g_mm_target_wg = 1024;
+KCA_API int kca_mm_skinny_set(int target_wg) {
+  if (target_wg > 0) g_mm_target_wg = target_wg;
+  return 0;
+}
+
+// KC: K per chunk -- 256 (2 weight rows x 512 B per load instruction) for one output tile per
+// wave, 128 (4 rows x 256 B) where the wave holds more tiles, so every variant fits 128 VGPRs.
+constexpr int mm_kc(int MT, int NRW) { return MT * NRW >= 2 ? 128 : 256; }
+
+struct MmPlan {
+  int mt, nrw, kc, ks, nblk;
+  long long ws_floats;
+};
+
+static MmPlan mm_plan(MmArgs& a) {
+  MmPlan p;
+  p.mt = a.M <= 16 ? 1 : (a.M <= 32 ? 2 : 4);
+  p.nrw = (a.nr == 2 && p.mt < 4) ? 2 : 1;
+  p.kc = mm_kc(p.mt, p.nrw);
+  const int rows = MM_WAVES * p.nrw * 16;
+  p.nblk = 0;
+  int nct = 1;
+  for (int i = 0; i < a.njobs; ++i) {
+    a.j[i].tiles = (a.j[i].N + rows - 1) / rows;
+    p.nblk += a.j[i].tiles;
+    int c = 0;
+    for (int q = 0; q < a.j[i].nparts; ++q) c += (a.j[i].p[q].K + p.kc - 1) / p.kc;
+    nct = c > nct ? c : nct;
+  }
+  if (a.njobs < 2) a.j[1].tiles = 0;
+  int ks = a.ks > 0 ? a.ks : (g_mm_target_wg + p.nblk - 1) / p.nblk;
+  if (ks > nct) ks = nct;
+  if (ks > 32) ks = 32;
+  if (ks < 1) ks = 1;
+  const int per = (nct + ks - 1) / ks;  // no empty slices
+  ks = (nct + per - 1) / per;
+  p.ks = ks;
+  p.ws_floats = ks > 1 ? (long long)ks * p.nblk * MM_WAVES * p.nrw * p.mt * 256 : 0;
+  return p;
+}
+
+template <int DT, int MT, int NRW, bool LN>
+static void mm_launch(const MmArgs& a, const MmPlan& p, hipStream_t s) {
+  constexpr int KC = mm_kc(MT, NRW);
+  using T = MmTile<MT, NRW, KC>;
+  hipLaunchKernelGGL((mm_skinny_kernel<DT, MT, NRW, KC, LN>), dim3(p.nblk, p.ks), dim3(256), T::LDS, s, a);
+}
+
+template <int DT, int MT, bool LN>
+static void mm_dispatch_nr(const MmArgs& a, const MmPlan& p, hipStream_t s) {
+  if constexpr (MT < 4) {
+    if (p.nrw == 2) {
+      mm_launch<DT, MT, 2, LN>(a, p, s);
+      return;
+    }
+  }
+  mm_launch<DT, MT, 1, LN>(a, p, s);
+}
+
+template <int DT, bool LN>
+static void mm_dispatch_mt(const MmArgs& a, const MmPlan& p, hipStream_t s) {
+  if (p.mt == 1) mm_dispatch_nr<DT, 1, LN>(a, p, s);
+  else if (p.mt == 2) mm_dispatch_nr<DT, 2, LN>(a, p, s);
+  else mm_dispatch_nr<DT, 4, LN>(a, p, s);
+}
+
+static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+static bool al8(const void* p) { return ((uintptr_t)p & 7) == 0; }
+
+static int mm_check(const MmArgs& a, int dtype, int& ln) {
+  if (a.njobs < 1 || a.njobs > 2 || a.M < 1 || a.M > 64 || dtype < 0 || dtype > 1) return 1;
+  ln = -1;
+  for (int i = 0; i < a.njobs; ++i) {
+    const MmJob& J = a.j[i];
+    if (J.N < 1 || J.N % 4 || J.nparts < 1 || J.nparts > 2 || !J.y || J.ldy % 4 || !al8(J.y) || !al8(J.bias)) return 1;
+    if (J.res && (J.ldr % 4 || !al8(J.res) || J.act)) return 1;
+    if (J.part && (J.N % 16 || !J.stats_out || !J.cnt)) return 1;
+    for (int q = 0; q < J.nparts; ++q) {
+      const MmPart& P = J.p[q];
+      if (P.K < 8 || P.K % 8 || P.ldx % 8 || P.ldw % 8 || !P.x || !P.w || !al16(P.x) || !al16(P.w)) return 2;
+      const int l = P.stats ? 1 : 0;
+      if (ln >= 0 && l != ln) return 3;  // one LN mode per launch
+      ln = l;
+      if (l && (!P.gamma || !al16(P.gamma) || !al16(P.beta))) return 2;
+    }
+  }
+  return 0;
+}
+
+// Workspace a launch of these arguments needs: ws floats and per-block counters (0 if no K split).
+KCA_API int kca_mm_skinny_plan(const MmArgs* in, int dtype, long long* ws_floats, int* bcnt_n, int* ks) {
+  if (!in) return 1;
+  MmArgs a = *in;
+  int ln;
+  const int rc = mm_check(a, dtype, ln);
+  if (rc) return rc;
+  const MmPlan p = mm_plan(a);
+  *ws_floats = p.ws_floats;
+  *bcnt_n = p.ks > 1 ? p.nblk : 0;
+  *ks = p.ks;
+  return 0;
+}
+
+// dtype: 0 bf16, 1 fp16. Returns nonzero (nothing launched) for shapes outside the kernel or a
+// workspace smaller than kca_mm_skinny_plan's.
+KCA_API int kca_mm_skinny(const MmArgs* in, int dtype, hipStream_t stream) {
+  if (!in) return 1;
+  MmArgs a = *in;
+  int ln;
+  const int rc = mm_check(a, dtype, ln);
+  if (rc) return rc;
+  const MmPlan p = mm_plan(a);
+  if (p.ks > 1 && (!a.ws || !a.bcnt || a.ws_floats < p.ws_floats || a.bcnt_n < p.nblk || !al16(a.ws))) return 5;
+  a.ks = p.ks;
+  if (dtype == 0) {
+    if (ln) mm_dispatch_mt<0, true>(a, p, stream);
+    else mm_dispatch_mt<0, false>(a, p, stream);
+  } else {
+    if (ln) mm_dispatch_mt<1, true>(a, p, stream);
+    else mm_dispatch_mt<1, false>(a, p, stream);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : 4;
+}
+
+// Sizes the Python mirror of the descriptor checks (ctypes.Structure layout == this ABI)
+KCA_API int kca_mm_skinny_abi(int* sizes) {
+  sizes[0] = (int)sizeof(MmPart);
+  sizes[1] = (int)sizeof(MmJob);
+  sizes[2] = (int)sizeof(MmArgs);
+  return 0;
+}

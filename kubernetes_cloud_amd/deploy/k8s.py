@@ -12,14 +12,16 @@ from __future__ import annotations
 GPU_RESOURCE = "amd.com/gpu"
 GPU_CLASS_LABEL = "gpu.amd.com/class"
 REGION_LABEL = "topology.kubernetes.io/region"
+# built by deploy/images/Dockerfile (targets: kubernetes_cloud_amd/deploy/images.py)
 IMAGE = "ghcr.io/kubernetes-cloud-amd/kca"
+DEV_IMAGE = "ghcr.io/kubernetes-cloud-amd/kca-dev"  # + sshd, tini, JupyterLab (dev-ssh, Jupyter)
 TAG = "rocm7.2-gfx950"
 
 
-def image(tag_param: str | None = None, image_param: str | None = None) -> str:
+def image(tag_param: str | None = None, image_param: str | None = None, dev: bool = False) -> str:
     if tag_param:
         return f"{{{{workflow.parameters.{image_param}}}}}:{{{{workflow.parameters.{tag_param}}}}}"
-    return f"{IMAGE}:{TAG}"
+    return f"{DEV_IMAGE if dev else IMAGE}:{TAG}"
 
 
 def affinity(gpu_class: str | None, region: str | None) -> dict:

@@ -37,14 +37,14 @@ def _service(name: str, port: int, target: int, svc_type: str = "LoadBalancer", 
 
 
 def dev_ssh(gpus: int = 6) -> dict:
-    init = {"name": "init", "image": image(), "command": ["/bin/bash", "-c"],
+    init = {"name": "init", "image": image(dev=True), "command": ["/bin/bash", "-c"],
             "args": ["if [ ! -f /target/initialized ]; then dpkg-reconfigure openssh-server && cp -ax / /target && "
                      "echo 'Initialization complete' && touch /target/initialized; fi"],
             "resources": {"requests": {"cpu": 1, "memory": "1Gi"}},
             "volumeMounts": [{"name": "root-storage", "mountPath": "/target"}]}
     mounts = [{"name": "data-storage", "mountPath": "/mnt/data"}, {"name": "dshm", "mountPath": "/dev/shm"}]
     mounts += [{"name": "root-storage", "mountPath": f"/{d}", "subPath": d} for d in ROOT_DIRS]
-    main = {"name": "sshd", "image": image(), "command": ["/usr/bin/tini", "--"],
+    main = {"name": "sshd", "image": image(dev=True), "command": ["/usr/bin/tini", "--"],
             "args": ["service", "ssh", "start", "-D"], "tty": True,
             "ports": [{"name": "sshd", "containerPort": 22, "protocol": "TCP"}],
             "env": [{"name": "HSA_ENABLE_IPC_MODE_LEGACY", "value": "0"}],
@@ -62,7 +62,7 @@ def dev_ssh(gpus: int = 6) -> dict:
 
 
 def jupyter(gpus: int = 2) -> dict:
-    c = {"name": "jupyter", "image": image(), "command": ["jupyter", "lab"],
+    c = {"name": "jupyter", "image": image(dev=True), "command": ["jupyter", "lab"],
          "args": ["--ip=0.0.0.0", "--port=8888", "--no-browser", "--allow-root",
                   "--ServerApp.token=$(JUPYTER_TOKEN)", "--notebook-dir=/mnt/pvc"],
          "env": [{"name": "JUPYTER_TOKEN", "valueFrom": {"secretKeyRef": {"name": "jupyter-token", "key": "token"}}}],
@@ -95,7 +95,7 @@ def spark() -> dict:
                                    "values": ["amd-epyc-genoa", "amd-epyc-turin"]},
                                   {"key": "topology.kubernetes.io/region", "operator": "In",
                                    "values": ["ORD1"]}]}]}}}}}
-    drv = {"name": "jupyter", "image": image(), "command": ["jupyter", "lab"],
+    drv = {"name": "jupyter", "image": image(dev=True), "command": ["jupyter", "lab"],
            "args": ["--ip=0.0.0.0", "--port=8888", "--no-browser", "--allow-root", "--notebook-dir=/mnt/pvc"],
            "ports": [{"containerPort": 8888}, {"containerPort": 7078, "name": "driver-rpc"},
                      {"containerPort": 7079, "name": "blockmanager"}],

@@ -1,0 +1,224 @@
+"""Batched-decode GEMMs on the matrix cores (``csrc/kernels/skinny_mfma.hip``).
+
+``y[M, N] = epilogue(x[M, K] . W[N, K]^T)`` for M = 2..64 decode rows (FasterTransformer's decoder at
+batch > 1): the weight streams once from HBM straight into MFMA fragments, the activation rows are
+re-read from L2, and the epilogues / prologues of a decode layer are folded in:
+
+* ``act``: bias + GELU (fc_in);
+* ``res``: bias + residual -> the new residual stream, with a **row-stats tail** (``stats=RowStatsBuf``)
+  whose last-arriving workgroup writes the next LayerNorm's per-row (mean, rstd);
+* ``ln=(stats, gamma, beta)`` on an input part: the activation is the residual stream, normalised on
+  load with those statistics (no LayerNorm launch, no normalised-row buffer);
+* two jobs per launch (N-concatenated, e.g. QKV and fc_in of a parallel-residual layer) or two
+  K-concatenated parts of one job (GPT-J's ``o.Wo^T + g.Wf^T`` into one residual).
+
+bf16 and fp16 (the precision FT / DS-Inference serve, BASELINE config 4). The descriptor is a
+``ctypes.Structure`` mirroring ``MmArgs``; the entry point copies it into the kernel arguments, so a
+launch is graph-capturable like any other.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+
+_P = ctypes.c_void_p
+_LL = ctypes.c_longlong
+_I = ctypes.c_int
+_F = ctypes.c_float
+
+
+class _Part(ctypes.Structure):
+    _fields_ = [("x", _P), ("ldx", _LL), ("w", _P), ("ldw", _LL), ("K", _I), ("stats", _P), ("gamma", _P),
+                ("beta", _P)]
+
+
+class _Job(ctypes.Structure):
+    _fields_ = [("p", _Part * 2), ("nparts", _I), ("N", _I), ("tiles", _I), ("bias", _P), ("act", _I), ("y", _P),
+                ("ldy", _LL), ("res", _P), ("ldr", _LL), ("part", _P), ("stats_out", _P), ("cnt", _P),
+                ("eps", _F)]
+
+
+class _Args(ctypes.Structure):
+    _fields_ = [("j", _Job * 2), ("njobs", _I), ("M", _I), ("ks", _I), ("nr", _I), ("ws", _P), ("bcnt", _P),
+                ("ws_floats", _LL), ("bcnt_n", _I), ("pad_", _I)]
+
+
+_DT = {torch.bfloat16: 0, torch.float16: 1}
+MAX_M = 64
+# launch-shape knobs for same-box A/B runs (0 = the entry point's choice): K split over workgroups,
+# 16-row weight tiles per wave
+_KS = int(os.environ.get("KCA_MM_KS", "0"))
+_NR = int(os.environ.get("KCA_MM_NR", "1"))
+# split-K workspaces (fp32 partial tiles + zeroed per-block arrival counters), one per (device, stream):
+# launches on one stream are ordered, launches on two streams must not share the counters
+_WS: dict = {}
+_ABI_OK = None
+
+
+def _abi_ok() -> bool:
+    global _ABI_OK
+    if _ABI_OK is None:
+        sizes = (ctypes.c_int * 3)()
+        fn = getattr(_lib.require(), "kca_mm_skinny_abi")
+        fn.argtypes = [ctypes.c_void_p]
+        fn(ctypes.cast(sizes, ctypes.c_void_p))
+        _ABI_OK = (sizes[0], sizes[1], sizes[2]) == (ctypes.sizeof(_Part), ctypes.sizeof(_Job), ctypes.sizeof(_Args))
+        if not _ABI_OK:
+            raise RuntimeError(f"kca_mm_skinny descriptor ABI mismatch: C {tuple(sizes)} vs ctypes "
+                               f"{(ctypes.sizeof(_Part), ctypes.sizeof(_Job), ctypes.sizeof(_Args))}")
+    return _ABI_OK
+
+
+class RowStatsBuf:
+    """Workspace of one row-stats tail: per-tile partials, the (mean, rstd) output, arrival counters
+    (zero-initialised, re-armed by every launch). One instance serves consecutive tails on a stream."""
+
+    def __init__(self, M: int, N: int, device):
+        self.M, self.N = M, N
+        self.part = torch.empty(M * (N // 16) * 2, device=device, dtype=torch.float32)
+        self.stats = torch.zeros(M, 2, device=device, dtype=torch.float32)
+        self.cnt = torch.zeros(32 * 65, device=device, dtype=torch.int32)
+
+
+def supported(x: torch.Tensor, w: torch.Tensor) -> bool:
+    """Shapes / dtypes the MFMA kernel takes (the caller falls back otherwise)."""
+    M, K = x.shape
+    return (x.is_cuda and x.dtype in _DT and w.dtype == x.dtype and 1 <= M <= MAX_M and K % 8 == 0
+            and x.stride(1) == 1 and x.stride(0) % 8 == 0 and w.stride(1) == 1 and w.stride(0) % 8 == 0
+            and x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0 and w.shape[1] == K)
+
+
+def part(x, w, ln=None):
+    """One K-part: x [M, K], w [N, K]; ``ln=(stats [M, 2] fp32, gamma, beta)`` normalises x on load."""
+    p = _Part()
+    p.x, p.ldx, p.w, p.ldw, p.K = x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), x.shape[1]
+    if ln is not None:
+        st, g, b = ln
+        p.stats, p.gamma, p.beta = st.data_ptr(), g.data_ptr(), _lib.ptr(b)
+    return p
+
+
+def job(parts, N: int, y: torch.Tensor, bias=None, act: int = 0, res=None, stats: RowStatsBuf | None = None,
+        eps: float = 1e-5):
+    j = _Job()
+    for i, p in enumerate(parts):
+        j.p[i] = p
+    j.nparts, j.N, j.bias, j.act = len(parts), N, _lib.ptr(bias), int(act)
+    j.y, j.ldy = y.data_ptr(), y.stride(0)
+    if res is not None:
+        j.res, j.ldr = res.data_ptr(), res.stride(0)
+    if stats is not None:
+        j.part, j.stats_out, j.cnt, j.eps = stats.part.data_ptr(), stats.stats.data_ptr(), stats.cnt.data_ptr(), eps
+    return j
+
+
+def _workspace(device, floats: int, nblk: int):
+    key = (str(device), torch.cuda.current_stream(device).cuda_stream)
+    ws = _WS.get(key)
+    if ws is None or ws[0].numel() < floats or ws[1].numel() < nblk:
+        f = max(floats, ws[0].numel() if ws else 0, 1 << 20)
+        n = max(nblk, ws[1].numel() if ws else 0, 4096)
+        ws = (torch.empty(f, device=device, dtype=torch.float32), torch.zeros(n, device=device, dtype=torch.int32))
+        _WS[key] = ws
+    return ws
+
+
+def plan(jobs, M: int, dtype: torch.dtype, ks: int | None = None, nr: int | None = None):
+    """(K split, workspace floats, block counters) the entry point picks for these jobs."""
+    a = _args(jobs, M, ks, nr)
+    wsf, nb, k = ctypes.c_longlong(0), ctypes.c_int(0), ctypes.c_int(0)
+    fn = _lib.require().kca_mm_skinny_plan
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    fn.restype = ctypes.c_int
+    rc = fn(ctypes.addressof(a), _DT[dtype], ctypes.addressof(wsf), ctypes.addressof(nb), ctypes.addressof(k))
+    if rc != 0:
+        raise RuntimeError(f"kca_mm_skinny_plan returned status {rc} (unsupported shape/arguments)")
+    return k.value, wsf.value, nb.value
+
+
+def _args(jobs, M, ks, nr):
+    _abi_ok()
+    a = _Args()
+    for i, j in enumerate(jobs):
+        a.j[i] = j
+    a.njobs, a.M = len(jobs), M
+    a.ks = _KS if ks is None else ks
+    a.nr = _NR if nr is None else nr
+    return a
+
+
+def launch(jobs, M: int, dtype: torch.dtype, ks: int | None = None, nr: int | None = None) -> None:
+    """One kernel launch over 1-2 jobs on the current stream."""
+    k, wsf, nb = plan(jobs, M, dtype, ks, nr)
+    a = _args(jobs, M, ks, nr)
+    if k > 1:
+        dev = torch.device("cuda", torch.cuda.current_device())
+        ws, bc = _workspace(dev, wsf, nb)
+        a.ws, a.bcnt, a.ws_floats, a.bcnt_n = ws.data_ptr(), bc.data_ptr(), ws.numel(), bc.numel()
+    fn = _lib.require().kca_mm_skinny
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    fn.restype = ctypes.c_int
+    rc = fn(ctypes.addressof(a), _DT[dtype], _lib.stream())
+    if rc != 0:
+        raise RuntimeError(f"kca_mm_skinny returned status {rc} (unsupported shape/arguments)")
+    if _lib.SYNC_LAUNCH:
+        torch.cuda.synchronize()
+
+
+def mm(x: torch.Tensor, w: torch.Tensor, bias=None, act: int = 0, out=None, res=None, stats=None, eps=1e-5,
+       ln=None) -> torch.Tensor:
+    """Single-job convenience: ``act(LN?(x) W^T + b) (+ res)``."""
+    M = x.shape[0]
+    N = w.shape[0]
+    if out is None:
+        out = torch.empty(M, N, device=x.device, dtype=x.dtype)
+    launch([job([part(x, w, ln)], N, out, bias, act, res, stats, eps)], M, x.dtype)
+    return out
+
+
+# ----------------------------------------------------------------------------- reference math (fp32)
+def _act_ref(y, act):
+    if act == 1:
+        return F.gelu(y, approximate="tanh")
+    if act == 2:
+        return F.gelu(y)
+    return y
+
+
+def ln_on_load_reference(h, stats, gamma, beta):
+    """The prologue: (h - mean) * rstd * gamma + beta, rounded to h's dtype."""
+    hf = h.float()
+    y = (hf - stats[:, :1]) * stats[:, 1:] * gamma.float() + (0 if beta is None else beta.float())
+    return y.to(h.dtype)
+
+
+def row_stats_reference(h, eps):
+    """(mean, rstd) per row of the rounded residual stream (fp32, two-pass)."""
+    hf = h.float()
+    mean = hf.mean(-1, keepdim=True)
+    var = ((hf - mean) ** 2).mean(-1, keepdim=True)
+    return torch.cat([mean, torch.rsqrt(var + eps)], dim=1)
+
+
+def mm_reference(parts, bias=None, act=0, res=None, dtype=torch.bfloat16):
+    """parts: [(x, w, ln)] -> the job's output (rounded to dtype) in fp32 math."""
+    y = None
+    for x, w, ln in parts:
+        xx = x if ln is None else ln_on_load_reference(x, *ln)
+        t = xx.float() @ w.float().t()
+        y = t if y is None else y + t
+    if bias is not None:
+        y = y + bias.float()
+    y = _act_ref(y, act)
+    if res is not None:
+        y = y + res.float()
+    return y.to(dtype)
+
+
+__all__ = ["RowStatsBuf", "supported", "part", "job", "launch", "mm", "mm_reference", "row_stats_reference",
+           "ln_on_load_reference", "MAX_M"]

@@ -83,13 +83,13 @@ def run_sync(reqs, timeout: float):
     import httpx
     times = []
     with httpx.Client(timeout=timeout) as cl:
-        t0 = time.perf_counter()
+        t0 = time.perf_counter()  # the whole run's window (throughput)
         for r in reqs:
-            t0 = time.perf_counter()
+            ts = time.perf_counter()  # this request's start (latency)
             try:
                 resp = cl.request(r[0], r[1], content=r[2], headers=r[3])
                 resp.raise_for_status()
-                times.append(time.perf_counter() - t0)
+                times.append(time.perf_counter() - ts)
             except Exception as e:  # noqa: BLE001
                 log.info("request failed: %s", e)
         total = time.perf_counter() - t0

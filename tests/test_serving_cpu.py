@@ -324,3 +324,37 @@ def test_serving_bench_http_and_engine_levels_cpu(tmp_path):
     assert not os.listdir(tmp_path)  # model dir and .tensors removed
     b = sb.run_bloom_slice(layers=2, levels=lv, overrides=dict(hidden_size=64, n_head=4, vocab_size=512))
     assert all(r["successes"] == r["requests"] for r in b["levels"]) and "proxy" in b
+
+
+def test_loadgen_sync_window_covers_every_request():
+    """--sync mode: the throughput window spans all requests, each latency only its own (ADVICE r5:
+    the per-request start used to overwrite the run's start, inflating req/s by ~n)."""
+    import http.server
+    import threading
+    import time as _t
+
+    from kubernetes_cloud_amd.serving.loadgen import run_sync
+
+    class _H(http.server.BaseHTTPRequestHandler):
+        def do_POST(self):  # noqa: N802
+            self.rfile.read(int(self.headers.get("content-length", 0)))
+            _t.sleep(0.03)
+            self.send_response(200)
+            self.send_header("content-length", "2")
+            self.end_headers()
+            self.wfile.write(b"{}")
+
+        def log_message(self, *a):
+            pass
+
+    srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), _H)
+    th = threading.Thread(target=srv.serve_forever, daemon=True)
+    th.start()
+    try:
+        url = f"http://127.0.0.1:{srv.server_address[1]}/"
+        reqs = [("POST", url, b"{}", {"content-type": "application/json"})] * 5
+        times, total = run_sync(reqs, timeout=10.0)
+    finally:
+        srv.shutdown()
+    assert len(times) == 5 and all(t >= 0.03 for t in times)
+    assert total >= sum(times) * 0.99 and total >= 0.15
