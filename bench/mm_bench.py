@@ -23,6 +23,7 @@ SHAPES = {
     "gptj.qkv": (12288, 4096), "gptj.out": (4096, 4096), "gptj.fc_in": (16384, 4096), "gptj.fc_out": (4096, 16384),
     "bloom8.qkv": (5376, 14336), "bloom8.out": (14336, 1792), "bloom8.fc_in": (7168, 14336),
     "bloom8.fc_out": (14336, 7168),
+    "gptj.qkv_fcin": (28672, 4096), "gptj.out_fcout": (4096, 20480),
     "neox.qkv": (18432, 6144), "neox.out": (6144, 6144), "neox.fc_in": (24576, 6144), "neox.fc_out": (6144, 24576),
 }
 

@@ -4,28 +4,44 @@
 //
 // The batch-1 tail (decode_tail.h) normalises the whole new residual row in the last-arriving
 // workgroup. At M rows that is M x N elements through one workgroup (BLOOM B=32: 917 KB), so here
-// the producer only publishes statistics: every 16-column tile of every row contributes its own
-// (mean, M2) -- exact two-pass over 16 values -- and the last arriver merges them (Chan's parallel
-// variance: all tiles hold 16 values, so mean = avg(mean_t), M2 = sum(M2_t) + 16 sum (mean_t - mean)^2)
-// into (mean, rstd) per row. The consumer GEMM (next QKV / fc_in / LM head) normalises its activation
-// fragments on load (skinny_mfma.hip, LN-on-load), so no LayerNorm launch and no normalised-row
-// round trip exists in the layer loop.
+// the producer only publishes statistics: every `tw`-column slice of every row contributes its own
+// (mean, M2) -- exact two-pass over 16 values, merged up to the slice inside the producing workgroup --
+// and the last arriver merges them (Chan's parallel variance: all slices hold tw values, so
+// mean = avg(mean_t), M2 = sum(M2_t) + tw sum (mean_t - mean)^2) into (mean, rstd) per row. The
+// consumer GEMM (next QKV / fc_in / LM head) normalises its activation fragments on load
+// (skinny_mfma.hip, LN-on-load), so no LayerNorm launch and no normalised-row round trip exists in
+// the layer loop.
 #pragma once
 #include "decode_tail.h"
 
 struct RowStats {
-  float* part;     // [M][N/16][2] per-tile (mean, M2), published with st_pub
+  float* part;     // [M][N/tw][2] per-slice (mean, M2), published with st_pub
   float* stats;    // [M][2] (mean, rstd) -- written by the last arriver
   unsigned* cnt;   // 32 * (1 + 64) arrival counters, zero before the first launch, re-armed every launch
-  int M, N;        // N % 16 == 0
+  int M, N;        // N % tw == 0
   float eps;
+  int tw;          // columns per published partial
 };
 
-// Publish one tile's partial (called by one lane per (row, tile)).
-__device__ __forceinline__ void rs_publish(const RowStats& s, int m, int tile, float mean_t, float m2_t) {
-  float* p = s.part + ((long long)m * (s.N >> 4) + tile) * 2;
+// Publish one slice's partial (called by one thread per (row, slice)).
+__device__ __forceinline__ void rs_publish(const RowStats& s, int m, int slice, float mean_t, float m2_t) {
+  float* p = s.part + ((long long)m * (s.N / s.tw) + slice) * 2;
   st_pub(p, mean_t);
   st_pub(p + 1, m2_t);
+}
+
+// Chan merge of n equal-count groups' (mean, M2) (count c each)
+template <int n>
+__device__ __forceinline__ void chan_merge(const float (&mean)[n], const float (&m2)[n], float c, float& mo,
+                                           float& m2o) {
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < n; ++i) s += mean[i];
+  mo = s * (1.f / n);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < n; ++i) q += m2[i] + c * (mean[i] - mo) * (mean[i] - mo);
+  m2o = q;
 }
 
 // (mean, M2) of 16 values spread as 4 per lane over the 4 lanes {l, l^16, l^32, l^48} (the
@@ -43,24 +59,43 @@ __device__ __forceinline__ void rs_tile16(const float (&v)[4], float& mean_t, fl
   m2_t = q;
 }
 
-// The last arriver: merge the tiles of every row (one wave per row, lanes over tiles).
+// The last arriver: merge the slices of every row. One wave per group of RG rows, lanes over slices,
+// every load of the group issued before any is used (a row-at-a-time loop was a chain of dependent L2
+// round trips: +100-200 us per step at B = 32, profiles/decode_suite_r6_v1_batched.jsonl).
 __device__ __forceinline__ void rs_merge(const RowStats& s) {
+  constexpr int RG = 4, PL = 4;  // rows per group, slices per lane (NT <= 256)
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const int NT = s.N >> 4;
-  for (int m = wv; m < s.M; m += nw) {
-    const float* p = s.part + (long long)m * NT * 2;
-    float sm = 0.f;
-    for (int t = lane; t < NT; t += 64) sm += p[2 * t];
-    const float mean = wave_sum(sm) / NT;
-    float q = 0.f;
-    for (int t = lane; t < NT; t += 64) {
-      const float d = p[2 * t] - mean;
-      q += p[2 * t + 1] + 16.f * d * d;
-    }
-    const float var = wave_sum(q) / s.N;
-    if (lane == 0) {
-      s.stats[2 * m] = mean;
-      s.stats[2 * m + 1] = rsqrtf(var + s.eps);
+  const int NT = s.N / s.tw;
+  for (int m0 = wv * RG; m0 < s.M; m0 += nw * RG) {
+    float mt[RG][PL], qt[RG][PL];
+#pragma unroll
+    for (int r = 0; r < RG; ++r)
+#pragma unroll
+      for (int i = 0; i < PL; ++i) {
+        const int t = lane + 64 * i, m = m0 + r;
+        mt[r][i] = 0.f;
+        qt[r][i] = 0.f;
+        if (m < s.M && t < NT) {
+          const float2 v = *reinterpret_cast<const float2*>(s.part + ((long long)m * NT + t) * 2);
+          mt[r][i] = v.x;
+          qt[r][i] = v.y;
+        }
+      }
+#pragma unroll
+    for (int r = 0; r < RG; ++r) {
+      float sm = 0.f;
+#pragma unroll
+      for (int i = 0; i < PL; ++i) sm += mt[r][i];
+      const float mean = wave_sum(sm) / NT;
+      float q = 0.f;
+#pragma unroll
+      for (int i = 0; i < PL; ++i)
+        if (lane + 64 * i < NT) q += qt[r][i] + s.tw * (mt[r][i] - mean) * (mt[r][i] - mean);
+      const float var = wave_sum(q) / s.N;
+      if (lane == 0 && m0 + r < s.M) {
+        s.stats[2 * (m0 + r)] = mean;
+        s.stats[2 * (m0 + r) + 1] = rsqrtf(var + s.eps);
+      }
     }
   }
 }

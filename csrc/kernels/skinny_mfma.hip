@@ -98,6 +98,8 @@ struct MmArgs {
   int M;
   int ks;         // K split over workgroups (0: host picks; the kernel sees the chosen value)
   int nr;         // 16-row weight tiles per wave (0: host picks)
+  int kc;         // K per chunk, 128 / 256 (0: host picks)
+  int wv;         // waves per workgroup, 4 / 8 (0: host picks)
   float* ws;      // split-K partial tiles (ks > 1): kca_mm_skinny_plan floats
   unsigned* bcnt; // per-N-block arrival counters (ks > 1), zero-initialised, re-armed every launch
   long long ws_floats;
@@ -109,7 +111,7 @@ struct MmArgs {
 // mt*16 + (lane & 15) of its M axis (the mfma_f32_16x16x32 C layout).
 template <int DT>
 __device__ __forceinline__ void mm_store(const MmJob& J, int M, int n_base, int mt, int lane, const f32x4& v,
-                                         int tile) {
+                                         float& mean_t, float& m2_t) {
   const int r16 = lane & 15, g = lane >> 4;
   const int m = mt * 16 + r16;
   const int n = n_base + g * 4;
@@ -145,16 +147,9 @@ __device__ __forceinline__ void mm_store(const MmJob& J, int M, int n_base, int 
     float f[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) f[i] = e2f<DT>(q[i]);
-    float mean_t, m2_t;
     rs_tile16(f, mean_t, m2_t);
-    if (g == 0 && m < M) {
-      const RowStats s{J.part, J.stats_out, J.cnt, M, J.N, J.eps};
-      rs_publish(s, m, tile, mean_t, m2_t);
-    }
   }
 }
-
-constexpr int MM_WAVES = 4;  // waves per workgroup (they split the workgroup's N block)
 
 // Wave-local ordering of the LDS transpose: the lanes that read a fragment are not the lanes that
 // wrote it, so the compiler must not move a read above the writes; the LDS runs one wave's
@@ -172,23 +167,23 @@ __device__ __forceinline__ int chunk_part(const MmJob& J, int c, int nc0, int kc
   return pi;
 }
 
-template <int MT, int NRW, int KC>
+template <int MT, int NRW, int KC, int WV>
 struct MmTile {
   static constexpr int PPR = KC / 8;    // 16-B pieces per row per chunk
   static constexpr int RPI = 64 / PPR;  // weight rows per load instruction
   static constexpr int NI = 16 / RPI;   // load instructions per 16-row tile
   static constexpr int S = KC / 32;     // MFMA steps per chunk
-  static constexpr int XP = (MT * 16 * PPR + 255) / 256;  // x pieces per thread per chunk
+  static constexpr int XP = (MT * 16 * PPR + WV * 64 - 1) / (WV * 64);  // x pieces per thread per chunk
   static constexpr int XS = MT * 16 * KC;                 // one x stage (elements)
   static constexpr int SLOT = NRW * 16 * KC;              // one wave's transpose slot (elements)
-  static constexpr int LDS = (2 * XS + MM_WAVES * SLOT) * 2;
+  static constexpr int LDS = (2 * XS + WV * SLOT) * 2;
   static_assert(PPR >= 16 && PPR <= 64, "swizzle needs 16..64 pieces per row");
 };
 
-template <int DT, int MT, int NRW, int KC, bool LN>
-__global__ __launch_bounds__(256) void mm_skinny_kernel(MmArgs a) {
-  using T = MmTile<MT, NRW, KC>;
-  extern __shared__ __attribute__((aligned(16))) uint16_t mm_lds[];  // xs[2][MT*16][KC], slots[4][NRW*16][KC]
+template <int DT, int MT, int NRW, int KC, int WV, bool LN>
+__global__ __launch_bounds__(WV * 64) void mm_skinny_kernel(MmArgs a) {
+  using T = MmTile<MT, NRW, KC, WV>;
+  extern __shared__ __attribute__((aligned(16))) uint16_t mm_lds[];  // xs[2][MT*16][KC], slots[WV][NRW*16][KC]
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int r16 = lane & 15, g = lane >> 4;
   int b = blockIdx.x;
@@ -198,7 +193,7 @@ __global__ __launch_bounds__(256) void mm_skinny_kernel(MmArgs a) {
   if (second) b -= a.j[0].tiles;
   const int M = a.M, N = J.N;
   const int kz = blockIdx.y, KS = gridDim.y;
-  const int nw0 = b * (MM_WAVES * NRW * 16) + wv * (NRW * 16);  // this wave's first row
+  const int nw0 = b * (WV * NRW * 16) + wv * (NRW * 16);  // this wave's first row
   uint16_t* xs = mm_lds;
   uint16_t* slot = mm_lds + 2 * T::XS + wv * T::SLOT;
 
@@ -223,13 +218,13 @@ __global__ __launch_bounds__(256) void mm_skinny_kernel(MmArgs a) {
         wr[nr][i] = kv ? ld_nt16(P.w + (long long)n * P.ldw + k0 + lp * 8) : u32x4v{0u, 0u, 0u, 0u};
       }
   };
-  // activation chunk: piece q = tid + 256 j of the [MT*16][PPR] stage
+  // activation chunk: piece q = tid + WV*64 j of the [MT*16][PPR] stage
   auto load_x = [&](int c, u32x4v (&xr)[T::XP]) {
     int k0;
     const MmPart& P = J.p[chunk_part(J, c, nc0, KC, k0)];
 #pragma unroll
     for (int j = 0; j < T::XP; ++j) {
-      const int q = tid + 256 * j, m = q / T::PPR, k = k0 + (q % T::PPR) * 8;
+      const int q = tid + WV * 64 * j, m = q / T::PPR, k = k0 + (q % T::PPR) * 8;
       xr[j] = u32x4v{0u, 0u, 0u, 0u};
       if (m < M && k < P.K) {
         xr[j] = ld16(P.x + (long long)m * P.ldx + k);
@@ -253,7 +248,7 @@ __global__ __launch_bounds__(256) void mm_skinny_kernel(MmArgs a) {
   auto store_x = [&](const u32x4v (&xr)[T::XP], int buf) {
 #pragma unroll
     for (int j = 0; j < T::XP; ++j) {
-      const int q = tid + 256 * j, m = q / T::PPR, p = q % T::PPR;
+      const int q = tid + WV * 64 * j, m = q / T::PPR, p = q % T::PPR;
       if (m < MT * 16)
         *reinterpret_cast<u32x4v*>(xs + buf * T::XS + m * KC + ((p ^ (m & 15)) << 3)) = xr[j];
     }
@@ -265,34 +260,23 @@ __global__ __launch_bounds__(256) void mm_skinny_kernel(MmArgs a) {
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[nr][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  u32x4v wn[NRW][T::NI];
+  // one chunk: its weight registers -> the wave's LDS slot, then the next chunk is requested into the
+  // freed registers, the next activation chunk is staged, the MFMAs run (one chunk in flight per wave:
+  // two measured no faster, the registers cost occupancy -- profiles/mm_sweep_r6/)
   u32x4v xr[T::XP];
-  if (c_lo < c_hi) {
-    load_w(c_lo, wn);
-    load_x(c_lo, xr);
-    store_x(xr, 0);
-  }
-  __syncthreads();
-  for (int c = c_lo; c < c_hi; ++c) {
+  auto chunk = [&](int c, u32x4v (&w)[NRW][T::NI]) {
     const int buf = (c - c_lo) & 1;
-    u32x4v wc[NRW][T::NI];
-#pragma unroll
-    for (int nr = 0; nr < NRW; ++nr)
-#pragma unroll
-      for (int i = 0; i < T::NI; ++i) wc[nr][i] = wn[nr][i];
-    const bool nx = c + 1 < c_hi;
-    if (nx) {  // next chunk in flight under this one
-      load_w(c + 1, wn);
-      load_x(c + 1, xr);
-    }
     wave_lds_sync();
 #pragma unroll
     for (int nr = 0; nr < NRW; ++nr)
 #pragma unroll
       for (int i = 0; i < T::NI; ++i) {
         const int row = i * T::RPI + lr;
-        *reinterpret_cast<u32x4v*>(slot + (nr * 16 + row) * KC + ((lp ^ (row & 15)) << 3)) = wc[nr][i];
+        *reinterpret_cast<u32x4v*>(slot + (nr * 16 + row) * KC + ((lp ^ (row & 15)) << 3)) = w[nr][i];
       }
+    if (c + 1 < c_hi) load_w(c + 1, w);
+    const bool nx = c + 1 < c_hi;
+    if (nx) load_x(c + 1, xr);
     wave_lds_sync();
     const uint16_t* xb = xs + buf * T::XS;
 #pragma unroll
@@ -310,14 +294,22 @@ __global__ __launch_bounds__(256) void mm_skinny_kernel(MmArgs a) {
     }
     if (nx) store_x(xr, buf ^ 1);
     __syncthreads();
+  };
+  u32x4v wa[NRW][T::NI];
+  if (c_lo < c_hi) {
+    load_w(c_lo, wa);
+    load_x(c_lo, xr);
+    store_x(xr, 0);
   }
+  __syncthreads();
+  for (int c = c_lo; c < c_hi; ++c) chunk(c, wa);
 
   // split-K: publish this slice's tiles, the last arriving slice of the N block sums and stores
   bool fin = true;
   if (KS > 1) {
     constexpr int TPW = NRW * MT;  // tiles per wave
-    const long long blk = (long long)bglob * (MM_WAVES * TPW) + wv * TPW;
-    const long long nblk = (long long)gridDim.x * (MM_WAVES * TPW);
+    const long long blk = (long long)bglob * (WV * TPW) + wv * TPW;
+    const long long nblk = (long long)gridDim.x * (WV * TPW);
 #pragma unroll
     for (int nr = 0; nr < NRW; ++nr)
 #pragma unroll
@@ -342,96 +334,182 @@ __global__ __launch_bounds__(256) void mm_skinny_kernel(MmArgs a) {
     __syncthreads();
     fin = s_fin != 0;
     if (fin) {
-      for (int z = 0; z < KS; ++z) {
-        if (z == kz) continue;
+      // the other slices' tiles, UZ slices' loads in flight at a time (a serial chain of KS - 1 L2
+      // round trips sat on every block's critical path: profiles/mm_bench_r6_v4_nsplit_splitk.jsonl)
+      constexpr int UZ = TPW >= 4 ? 2 : (TPW >= 2 ? 4 : 8);
+      for (int z0 = 0; z0 < KS; z0 += UZ) {
+        f32x4 part[UZ][NRW][MT];
 #pragma unroll
-        for (int nr = 0; nr < NRW; ++nr)
+        for (int u = 0; u < UZ; ++u) {
+          const int z = z0 + u;
 #pragma unroll
-          for (int mt = 0; mt < MT; ++mt) {
-            const float* d = a.ws + ((z * nblk + blk + nr * MT + mt) * 64 + lane) * 4;
-            acc[nr][mt] += *reinterpret_cast<const f32x4*>(d);
-          }
+          for (int nr = 0; nr < NRW; ++nr)
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) {
+              part[u][nr][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+              if (z < KS && z != kz)
+                part[u][nr][mt] =
+                    *reinterpret_cast<const f32x4*>(a.ws + ((z * nblk + blk + nr * MT + mt) * 64 + lane) * 4);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < UZ; ++u)
+#pragma unroll
+          for (int nr = 0; nr < NRW; ++nr)
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) acc[nr][mt] += part[u][nr][mt];
       }
     }
   }
   if (!fin) return;  // (workgroup-uniform)
+  float tm[NRW][MT], tq[NRW][MT];
 #pragma unroll
   for (int nr = 0; nr < NRW; ++nr)
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-      mm_store<DT>(J, M, nw0 + nr * 16, mt, lane, acc[nr][mt], (nw0 >> 4) + nr);
+    for (int mt = 0; mt < MT; ++mt) mm_store<DT>(J, M, nw0 + nr * 16, mt, lane, acc[nr][mt], tm[nr][mt], tq[nr][mt]);
   if (J.part) {
-    const RowStats s{J.part, J.stats_out, J.cnt, M, J.N, J.eps};
+    // the block's row statistics: the wave's NRW tiles merged in registers, the WV waves through LDS,
+    // one (mean, M2) per row per block published (N % (WV * NRW * 16) == 0 for a stats job)
+    float* red = reinterpret_cast<float*>(mm_lds);  // [WV][MT*16][2]
+    __syncthreads();  // (the LDS held the last chunk's stages)
+    if (g == 0) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        float mean[NRW], m2[NRW], mo, qo;
+#pragma unroll
+        for (int nr = 0; nr < NRW; ++nr) {
+          mean[nr] = tm[nr][mt];
+          m2[nr] = tq[nr][mt];
+        }
+        chan_merge<NRW>(mean, m2, 16.f, mo, qo);
+        red[(wv * MT * 16 + mt * 16 + r16) * 2] = mo;
+        red[(wv * MT * 16 + mt * 16 + r16) * 2 + 1] = qo;
+      }
+    }
+    __syncthreads();
+    const RowStats s{J.part, J.stats_out, J.cnt, M, J.N, J.eps, WV * NRW * 16};
+    for (int m = tid; m < M; m += WV * 64) {
+      float mean[WV], m2[WV], mo, qo;
+#pragma unroll
+      for (int w = 0; w < WV; ++w) {
+        mean[w] = red[(w * MT * 16 + m) * 2];
+        m2[w] = red[(w * MT * 16 + m) * 2 + 1];
+      }
+      chan_merge<WV>(mean, m2, 16.f * NRW, mo, qo);
+      rs_publish(s, m, b, mo, qo);
+    }
     rs_arrive_of(s, b, J.tiles);
   }
 }
 
 // launch-shape knob (same-box A/B): workgroups a launch aims for when it splits K
-static int g_mm_target_wg = 1024;
+// launch-shape knob (same-box A/B): workgroups a K-split launch aims for (0: built-in, mm_plan_ks)
+static int g_mm_target_wg = 0;
 KCA_API int kca_mm_skinny_set(int target_wg) {
-  if (target_wg > 0) g_mm_target_wg = target_wg;
+  g_mm_target_wg = target_wg > 0 ? target_wg : 0;
   return 0;
 }
 
-// KC: K per chunk -- 256 (2 weight rows x 512 B per load instruction) for one output tile per
-// wave, 128 (4 rows x 256 B) where the wave holds more tiles, so every variant fits 128 VGPRs.
-constexpr int mm_kc(int MT, int NRW) { return MT * NRW >= 2 ? 128 : 256; }
+// Variants: KC (K per chunk: 256 = 2 weight rows x 512 B per load instruction, 128 = 4 rows x
+// 256 B) and WV (waves per workgroup, 4 or 8: an 8-wave block shares each activation chunk over
+// twice the weight rows). Defaults per (MT, NRW) from the mm_bench sweeps (profiles/mm_sweep_r6/);
+// a.kc / a.wv override (A/B).
+constexpr int mm_kc_default(int MT, int NRW) { return MT * NRW >= 4 ? 128 : 256; }
 
 struct MmPlan {
-  int mt, nrw, kc, ks, nblk;
+  int mt, nrw, kc, wv, ks, nblk;
   long long ws_floats;
 };
+
+// K split: about T workgroups per launch, T = 512 (one 16-row activation tile) / 384 (more), i.e.
+// ks = round(T / blocks). From a forced-split sweep over the fused-layer shapes
+// (profiles/mm_ks_sweep_r6/): the best split landed every launch at 448-768 workgroups at M = 8 and
+// 224-512 at M = 32 (2 resident per CU there); filling the resident slots exactly (ks = cap / blocks)
+// under-filled the 448-block GPT-J [QKV | fc_in] launch's neighbours and a time model that charged
+// a workgroup one chunk of overhead over-split every shape (profiles/mm_bench_r6_v6_ks_model_rejected.jsonl).
+static void mm_plan_ks(MmArgs& a, MmPlan& p, int target) {
+  int nct = 1;
+  for (int i = 0; i < a.njobs; ++i) {
+    int c = 0;
+    for (int q = 0; q < a.j[i].nparts; ++q) c += (a.j[i].p[q].K + p.kc - 1) / p.kc;
+    nct = c > nct ? c : nct;
+  }
+  int ks = a.ks > 0 ? a.ks : (2 * target + p.nblk) / (2 * p.nblk);
+  if (ks > nct) ks = nct;
+  if (ks > 32) ks = 32;
+  if (ks < 1) ks = 1;
+  const int per = (nct + ks - 1) / ks;
+  ks = (nct + per - 1) / per;
+  p.ks = ks;
+  p.ws_floats = ks > 1 ? (long long)ks * p.nblk * p.wv * p.nrw * p.mt * 256 : 0;
+}
+
+template <int DT, int MT, int NRW, int KC, int WV, bool LN>
+static void mm_go(MmArgs& a, MmPlan& p, hipStream_t s, bool launch) {
+  using T = MmTile<MT, NRW, KC, WV>;
+  mm_plan_ks(a, p, g_mm_target_wg > 0 ? g_mm_target_wg : (MT == 1 ? 512 : 384));
+  if (!launch) return;
+  a.ks = p.ks;
+  hipLaunchKernelGGL((mm_skinny_kernel<DT, MT, NRW, KC, WV, LN>), dim3(p.nblk, p.ks), dim3(WV * 64), T::LDS, s, a);
+}
+
+template <int DT, int MT, int NRW, bool LN>
+static void mm_dispatch_kc(MmArgs& a, MmPlan& p, hipStream_t s, bool launch) {
+  if (p.kc == 256) {
+    if (p.wv == 8) mm_go<DT, MT, NRW, 256, 8, LN>(a, p, s, launch);
+    else mm_go<DT, MT, NRW, 256, 4, LN>(a, p, s, launch);
+  } else {
+    if (p.wv == 8) mm_go<DT, MT, NRW, 128, 8, LN>(a, p, s, launch);
+    else mm_go<DT, MT, NRW, 128, 4, LN>(a, p, s, launch);
+  }
+}
+
+template <int DT, int MT, bool LN>
+static void mm_dispatch_nr(MmArgs& a, MmPlan& p, hipStream_t s, bool launch) {
+  if constexpr (MT < 4) {
+    if (p.nrw == 2) {
+      mm_dispatch_kc<DT, MT, 2, LN>(a, p, s, launch);
+      return;
+    }
+  }
+  mm_dispatch_kc<DT, MT, 1, LN>(a, p, s, launch);
+}
+
+template <int DT, bool LN>
+static void mm_dispatch_mt(MmArgs& a, MmPlan& p, hipStream_t s, bool launch) {
+  if (p.mt == 1) mm_dispatch_nr<DT, 1, LN>(a, p, s, launch);
+  else if (p.mt == 2) mm_dispatch_nr<DT, 2, LN>(a, p, s, launch);
+  else mm_dispatch_nr<DT, 4, LN>(a, p, s, launch);
+}
 
 static MmPlan mm_plan(MmArgs& a) {
   MmPlan p;
   p.mt = a.M <= 16 ? 1 : (a.M <= 32 ? 2 : 4);
   p.nrw = (a.nr == 2 && p.mt < 4) ? 2 : 1;
-  p.kc = mm_kc(p.mt, p.nrw);
-  const int rows = MM_WAVES * p.nrw * 16;
+  p.kc = a.kc == 128 || a.kc == 256 ? a.kc : mm_kc_default(p.mt, p.nrw);
+  if (p.kc == 256 && p.mt * p.nrw >= 4) p.kc = 128;  // (register budget)
+  p.wv = a.wv == 4 || a.wv == 8 ? a.wv : 4;
+  const int rows = p.wv * p.nrw * 16;
   p.nblk = 0;
-  int nct = 1;
   for (int i = 0; i < a.njobs; ++i) {
     a.j[i].tiles = (a.j[i].N + rows - 1) / rows;
     p.nblk += a.j[i].tiles;
-    int c = 0;
-    for (int q = 0; q < a.j[i].nparts; ++q) c += (a.j[i].p[q].K + p.kc - 1) / p.kc;
-    nct = c > nct ? c : nct;
+    if (a.j[i].part && (a.j[i].N % rows || a.j[i].N / rows > 256)) p.nblk = -1;  // whole blocks, <= 256 slices
   }
   if (a.njobs < 2) a.j[1].tiles = 0;
-  int ks = a.ks > 0 ? a.ks : (g_mm_target_wg + p.nblk - 1) / p.nblk;
-  if (ks > nct) ks = nct;
-  if (ks > 32) ks = 32;
-  if (ks < 1) ks = 1;
-  const int per = (nct + ks - 1) / ks;  // no empty slices
-  ks = (nct + per - 1) / per;
-  p.ks = ks;
-  p.ws_floats = ks > 1 ? (long long)ks * p.nblk * MM_WAVES * p.nrw * p.mt * 256 : 0;
+  p.ks = 1;
+  p.ws_floats = 0;
   return p;
 }
 
-template <int DT, int MT, int NRW, bool LN>
-static void mm_launch(const MmArgs& a, const MmPlan& p, hipStream_t s) {
-  constexpr int KC = mm_kc(MT, NRW);
-  using T = MmTile<MT, NRW, KC>;
-  hipLaunchKernelGGL((mm_skinny_kernel<DT, MT, NRW, KC, LN>), dim3(p.nblk, p.ks), dim3(256), T::LDS, s, a);
-}
-
-template <int DT, int MT, bool LN>
-static void mm_dispatch_nr(const MmArgs& a, const MmPlan& p, hipStream_t s) {
-  if constexpr (MT < 4) {
-    if (p.nrw == 2) {
-      mm_launch<DT, MT, 2, LN>(a, p, s);
-      return;
-    }
+static void mm_dispatch(MmArgs& a, MmPlan& p, int dtype, int ln, hipStream_t s, bool launch) {
+  if (dtype == 0) {
+    if (ln) mm_dispatch_mt<0, true>(a, p, s, launch);
+    else mm_dispatch_mt<0, false>(a, p, s, launch);
+  } else {
+    if (ln) mm_dispatch_mt<1, true>(a, p, s, launch);
+    else mm_dispatch_mt<1, false>(a, p, s, launch);
   }
-  mm_launch<DT, MT, 1, LN>(a, p, s);
-}
-
-template <int DT, bool LN>
-static void mm_dispatch_mt(const MmArgs& a, const MmPlan& p, hipStream_t s) {
-  if (p.mt == 1) mm_dispatch_nr<DT, 1, LN>(a, p, s);
-  else if (p.mt == 2) mm_dispatch_nr<DT, 2, LN>(a, p, s);
-  else mm_dispatch_nr<DT, 4, LN>(a, p, s);
 }
 
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
@@ -464,7 +542,9 @@ KCA_API int kca_mm_skinny_plan(const MmArgs* in, int dtype, long long* ws_floats
   int ln;
   const int rc = mm_check(a, dtype, ln);
   if (rc) return rc;
-  const MmPlan p = mm_plan(a);
+  MmPlan p = mm_plan(a);
+  if (p.nblk < 0) return 6;
+  mm_dispatch(a, p, dtype, ln, nullptr, false);
   *ws_floats = p.ws_floats;
   *bcnt_n = p.ks > 1 ? p.nblk : 0;
   *ks = p.ks;
@@ -479,16 +559,11 @@ KCA_API int kca_mm_skinny(const MmArgs* in, int dtype, hipStream_t stream) {
   int ln;
   const int rc = mm_check(a, dtype, ln);
   if (rc) return rc;
-  const MmPlan p = mm_plan(a);
+  MmPlan p = mm_plan(a);
+  if (p.nblk < 0) return 6;
+  mm_dispatch(a, p, dtype, ln, stream, false);
   if (p.ks > 1 && (!a.ws || !a.bcnt || a.ws_floats < p.ws_floats || a.bcnt_n < p.nblk || !al16(a.ws))) return 5;
-  a.ks = p.ks;
-  if (dtype == 0) {
-    if (ln) mm_dispatch_mt<0, true>(a, p, stream);
-    else mm_dispatch_mt<0, false>(a, p, stream);
-  } else {
-    if (ln) mm_dispatch_mt<1, true>(a, p, stream);
-    else mm_dispatch_mt<1, false>(a, p, stream);
-  }
+  mm_dispatch(a, p, dtype, ln, stream, true);
   return hipGetLastError() == hipSuccess ? 0 : 4;
 }
 

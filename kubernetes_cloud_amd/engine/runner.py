@@ -33,6 +33,7 @@ import torch
 
 from .. import ops
 from ..ops import decode as dops
+from ..ops import skinny_mm as smm
 from ..ops.gemv import embed_ln_rows, ln_rows, ln_skinny_linear, skinny_linear
 
 # decode steps: each row's RoPE angles and page-table row travel with the step's packed inputs (fixed
@@ -397,6 +398,16 @@ class ModelRunner:
         # (BLOOM's embedding LayerNorm: the gather kernel normalises with it, one ln_rows launch follows)
         self._embed_head = (self._fused_ok and getattr(model, "wpe", None) is None and cfg.embed_scale == 1.0
                             and os.environ.get("KCA_DECODE_EMBED_HEAD", "1") not in ("0", "false"))
+        # batch 2..64: the matrix-core decode layer (ops/skinny_mm.py): every projection one weight-streaming
+        # MFMA launch with its epilogue fused -- LayerNorm applied to the activation on load from the row
+        # statistics the previous residual projection published, bias + GELU, bias + residual -- so the
+        # layer loop has no LayerNorm, bias or hipBLASLt launch (parallel residual: [QKV | fc_in] one launch,
+        # out-proj + fc_out one K-concatenated launch). KCA_DECODE_FUSED_BATCHED=0: per-projection path.
+        d_model = cfg.hidden
+        self.batched_steps = 0
+        self._batched_ok = (self._fused_ok and self._tp_ar is None and self.dtype == torch.bfloat16
+                            and d_model % 64 == 0 and d_model <= 16384
+                            and os.environ.get("KCA_DECODE_FUSED_BATCHED", "1") not in ("0", "false"))
 
     # ------------------------------------------------------------- prefill
     @torch.no_grad()
@@ -601,12 +612,116 @@ class ModelRunner:
             return skinny_linear(xn, m.wte.weight)
         return self._lin(m.lm_head, xn)
 
+    def _batched_bufs(self, B: int):
+        """Static buffers of the batched matrix-core layer for a batch bucket (outside graph capture)."""
+        key = ("mm", B)
+        fz = self._fz.get(key)
+        if fz is None:
+            m = self.model
+            d = self.cfg.hidden
+            at0, mlp0 = m.h[0].attn, m.h[0].mlp
+            z = dict(device=self.device, dtype=self.dtype)
+            biases = []
+            for blk in m.h:
+                bo, bf = blk.attn.out.bias, blk.mlp.fc_out.bias
+                biases.append(bf if bo is None else (bo if bf is None else (bo.float() + bf.float()).to(self.dtype)))
+            fz = self._fz[key] = {
+                "h": torch.empty(B, d, **z), "xn": torch.empty(B, d, **z), "xn2": torch.empty(B, d, **z),
+                "qkv": torch.empty(B, at0.qkv.weight.shape[0], **z), "g": torch.empty(B, mlp0.fc_in.weight.shape[0], **z),
+                "st": smm.RowStatsBuf(B, d, self.device), "bias": biases}
+        return fz
+
+    def _head_weight(self):
+        from ..parallel.tensor_parallel import ParallelLMHead
+        m = self.model
+        if m.lm_head is None:
+            return m.wte.weight, None, None
+        if isinstance(m.lm_head, ParallelLMHead):
+            return m.lm_head.local_weight(), m.lm_head.bias, m.lm_head.group
+        return m.lm_head.weight, m.lm_head.bias, None
+
+    def _layers_decode_batched(self, tokens, pos, slots, kv_lens, max_kv, ws, obuf):
+        """Decode step at batch 2..64 on the matrix cores (see _batched_ok). Per layer kind:
+          seq  : QKV(LN1 on load) -> attention -> out + b + h (stats) -> fc_in(LN2 on load, GELU) -> fc_out + b + h
+          gptj : [QKV | fc_in+GELU](LN1 on load) -> attention -> o.Wo + g.Wf + b + h (stats)
+          neox : as gptj, fc_in normalising with ln_2's gamma / beta (same statistics)
+        Layer 0 reads the step head's normalised rows; the LM head normalises with ln_f on load."""
+        m, cfg = self.model, self.cfg
+        B = tokens.shape[0]
+        fz = self._batched_bufs(B)
+        self.batched_steps += 1  # (counted when a step is built: eager runs and graph captures)
+        kind = self._layer_kind
+        blk0 = m.h[0]
+        hb, st, qkv, g = fz["h"], fz["st"], fz["qkv"], fz["g"]
+        dt = self.dtype
+        # step head: token rows (+ BLOOM's embedding LayerNorm) and ln_1 (+ ln_2 for NeoX) of layer 0
+        if self._embed_head:
+            if m.emb_ln is not None:
+                h, _ = embed_ln_rows(m.wte.weight, tokens, m.emb_ln.weight, m.emb_ln.bias, m.emb_ln.eps)
+                xn, h = ln_rows(h, blk0.ln_1.weight, blk0.ln_1.bias, blk0.ln_1.eps)
+            else:
+                xn, h = embed_ln_rows(m.wte.weight, tokens, blk0.ln_1.weight, blk0.ln_1.bias, blk0.ln_1.eps)
+        else:
+            xn, h = ln_rows(m.embed(tokens, pos.long()), blk0.ln_1.weight, blk0.ln_1.bias, blk0.ln_1.eps)
+        xn2 = ln_rows(h, blk0.ln_2.weight, blk0.ln_2.bias, blk0.ln_2.eps)[0] if kind == "neox" else None
+        hb.copy_(h)
+        tbl = self.cache.table_on(self.device)
+        cos, sin, tbl, by_row = self._desc_args(self.cos, self.sin, tbl)
+        for li, blk in enumerate(m.h):
+            at, mlp = blk.attn, blk.mlp
+            act = 1 if mlp.approx in ("tanh", True) else 2
+            nxt = m.h[li + 1] if li + 1 < len(m.h) else None
+            nln = nxt.ln_1 if nxt is not None else m.ln_f
+            first = li == 0
+            ln1 = None if first else (st.stats, blk.ln_1.weight, blk.ln_1.bias)
+            x1 = xn if first else hb
+            kc, vc = self.cache.k[li], self.cache.v[li]
+            if kind == "seq":
+                smm.launch([smm.job([smm.part(x1, at.qkv.weight, ln1)], qkv.shape[1], qkv, at.qkv.bias)], B, dt)
+                o = dops.decode_prep_attention(qkv, self.H, self.Hkv, self.D, self.rot, cfg.rotary_interleaved,
+                                               cos, sin, pos, slots, kc, vc, kv_lens, max_kv, at.scale, at.alibi,
+                                               out=obuf, ws=ws, block_table=tbl, window=at.window, by_row=by_row)
+                smm.launch([smm.job([smm.part(o, at.out.weight)], hb.shape[1], hb, at.out.bias, res=hb, stats=st,
+                                    eps=blk.ln_2.eps)], B, dt)
+                smm.launch([smm.job([smm.part(hb, mlp.fc_in.weight, (st.stats, blk.ln_2.weight, blk.ln_2.bias))],
+                                    g.shape[1], g, mlp.fc_in.bias, act)], B, dt)
+                smm.launch([smm.job([smm.part(g, mlp.fc_out.weight)], hb.shape[1], hb, mlp.fc_out.bias, res=hb,
+                                    stats=st, eps=nln.eps)], B, dt)
+                continue
+            # parallel residual: [QKV | fc_in] of the same residual rows, one launch
+            if kind == "neox":
+                ln2 = (st.stats, blk.ln_2.weight, blk.ln_2.bias) if not first else None
+                x2 = xn2 if first else hb
+            else:
+                ln2, x2 = ln1, x1
+            smm.launch([smm.job([smm.part(x1, at.qkv.weight, ln1)], qkv.shape[1], qkv, at.qkv.bias),
+                        smm.job([smm.part(x2, mlp.fc_in.weight, ln2)], g.shape[1], g, mlp.fc_in.bias, act)], B, dt)
+            o = dops.decode_prep_attention(qkv, self.H, self.Hkv, self.D, self.rot, cfg.rotary_interleaved,
+                                           cos, sin, pos, slots, kc, vc, kv_lens, max_kv, at.scale, at.alibi,
+                                           out=obuf, ws=ws, block_table=tbl, window=at.window, by_row=by_row)
+            smm.launch([smm.job([smm.part(o, at.out.weight), smm.part(g, mlp.fc_out.weight)], hb.shape[1], hb,
+                                fz["bias"][li], res=hb, stats=st, eps=nln.eps)], B, dt)
+        w, b, grp = self._head_weight()
+        V = w.shape[0]
+        if V % 4 == 0:
+            logits = smm.mm(hb, w, b, ln=(st.stats, m.ln_f.weight, m.ln_f.bias))
+        else:  # (GPT-2's 50257 rows: the head takes the normalised rows through the plain path)
+            y = smm.ln_on_load_reference(hb, st.stats, m.ln_f.weight, m.ln_f.bias)
+            logits = skinny_linear(y, w, b)
+        if grp is not None:
+            from ..parallel.tensor_parallel import gather_last_dim
+            logits = gather_last_dim(logits, grp)
+        return logits
+
     def _layers_decode(self, tokens, pos, slots, kv_lens, max_kv, ws, obuf):
         m, cfg = self.model, self.cfg
         if self._fused_ok and tokens.shape[0] == 1 and obuf is not None:
             y = self._layers_decode_fused(tokens, pos, slots, kv_lens, max_kv, ws, obuf)
             if y is not None:
                 return y
+        if (self._batched_ok and 2 <= tokens.shape[0] <= smm.MAX_M and obuf is not None
+                and self._chain_src is None):
+            return self._layers_decode_batched(tokens, pos, slots, kv_lens, max_kv, ws, obuf)
         if self._chain_src is not None and obuf is not None:  # chained rows not resolved by a fused head
             chain, prev = self._chain_src
             tokens = torch.where(chain[:tokens.shape[0]] >= 0, prev[chain[:tokens.shape[0]].clamp(min=0).long()],

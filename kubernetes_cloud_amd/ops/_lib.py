@@ -85,6 +85,7 @@ _SIGS = {
     "kca_groupnorm_nhwc_bwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P],
     "kca_skinny_gemm": [P, LL, P, P, P, LL, I, I, I, I, P],
     "kca_skinny_set_splitk": [I],
+    "kca_mm_skinny_set": [I],
     "kca_ln_skinny_gemm": [P, LL, P, P, P, LL, P, P, F, P, P, P, LL, I, I, I, I, P, P],
     "kca_ln_rows": [P, LL, P, P, P, LL, P, P, F, P, I, I, P],
     "kca_embed_ln_rows": [P, LL, P, P, P, I, P, LL, P, P, F, P, I, I, P],

@@ -44,8 +44,8 @@ class _Job(ctypes.Structure):
 
 
 class _Args(ctypes.Structure):
-    _fields_ = [("j", _Job * 2), ("njobs", _I), ("M", _I), ("ks", _I), ("nr", _I), ("ws", _P), ("bcnt", _P),
-                ("ws_floats", _LL), ("bcnt_n", _I), ("pad_", _I)]
+    _fields_ = [("j", _Job * 2), ("njobs", _I), ("M", _I), ("ks", _I), ("nr", _I), ("kc", _I), ("wv", _I),
+                ("ws", _P), ("bcnt", _P), ("ws_floats", _LL), ("bcnt_n", _I), ("pad_", _I)]
 
 
 _DT = {torch.bfloat16: 0, torch.float16: 1}
@@ -54,6 +54,8 @@ MAX_M = 64
 # 16-row weight tiles per wave
 _KS = int(os.environ.get("KCA_MM_KS", "0"))
 _NR = int(os.environ.get("KCA_MM_NR", "1"))
+_KC = int(os.environ.get("KCA_MM_KC", "0"))  # K per chunk 128 / 256
+_WV = int(os.environ.get("KCA_MM_WV", "0"))  # waves per workgroup 4 / 8
 # split-K workspaces (fp32 partial tiles + zeroed per-block arrival counters), one per (device, stream):
 # launches on one stream are ordered, launches on two streams must not share the counters
 _WS: dict = {}
@@ -63,6 +65,9 @@ _ABI_OK = None
 def _abi_ok() -> bool:
     global _ABI_OK
     if _ABI_OK is None:
+        tgt = int(os.environ.get("KCA_MM_TARGET_WG", "0"))  # workgroups a K-split launch aims for (A/B)
+        if tgt > 0:
+            _lib.call("kca_mm_skinny_set", tgt)
         sizes = (ctypes.c_int * 3)()
         fn = getattr(_lib.require(), "kca_mm_skinny_abi")
         fn.argtypes = [ctypes.c_void_p]
@@ -149,6 +154,7 @@ def _args(jobs, M, ks, nr):
     a.njobs, a.M = len(jobs), M
     a.ks = _KS if ks is None else ks
     a.nr = _NR if nr is None else nr
+    a.kc, a.wv = _KC, _WV
     return a
 
 

@@ -922,3 +922,53 @@ def test_engine_bloom_tp_emulated_rank_fused():
     assert m.h[0].attn.out.group.allreduce_calls > 0
 
 
+
+
+@pytest.mark.parametrize("preset", ["gpt-j-6b", "gpt-neox-20b", "bloom-560m", "gpt2"])
+@pytest.mark.parametrize("B", [3, 20])
+def test_engine_batched_mfma_layer(preset, B):
+    """The batch 2..64 matrix-core decode layer (runner._layers_decode_batched: LayerNorm on load from the
+    previous tail's row statistics, [QKV | fc_in] / K-concatenated out-proj + fc_out launches for the
+    parallel-residual kinds, ALiBi + embedding LayerNorm for BLOOM, learned positions and an odd
+    vocabulary for GPT-2), HIP graphs on: every row's greedy tokens match a full forward of its own
+    continuation, and so do the per-projection path's."""
+    from kubernetes_cloud_amd.engine.llm_engine import LLMEngine, SamplingParams
+    over = {"gpt-j-6b": dict(n_embd=1024, n_layer=3, n_head=4, rotary_dim=64, n_positions=512)}.get(preset)
+    if over:
+        from kubernetes_cloud_amd.models.causal_lm import build_model
+        from kubernetes_cloud_amd.models.config import PRESETS_HF, LMConfig
+        cfg = dict(PRESETS_HF[preset])
+        cfg.update(over)
+        m = build_model(LMConfig.from_hf(cfg), device=dev, dtype=torch.bfloat16, seed=0)
+    else:
+        m = _small_lm(preset)
+    g = torch.Generator().manual_seed(B)
+    prompts = [[int(x) for x in torch.randint(0, 1000, (int(n),), generator=g)]
+               for n in torch.randint(8, 90, (B,), generator=g)]
+    sp = SamplingParams(max_new_tokens=10, do_sample=False)
+    for batched in (True, False):
+        eng = LLMEngine(m, max_slots=B, max_len=256, use_graphs=True)
+        assert eng.runner._batched_ok
+        eng.runner._batched_ok = batched
+        outs = [r.output for r in eng.generate(prompts, sp)]
+        assert (eng.runner.batched_steps > 0) == batched
+        for p, o in zip(prompts, outs):
+            _check_against_forward(m, p, o)
+
+
+def test_engine_batched_mfma_bloom_tp_emulated_rank():
+    """Rank 0 of a TP=4 BLOOM layout (parallel/tp_emulation.py) at batch 6 through the matrix-core layer:
+    shard shapes, vocab-parallel head gathered by the stand-in group."""
+    from kubernetes_cloud_amd.engine.llm_engine import LLMEngine, SamplingParams
+    from kubernetes_cloud_amd.models.config import PRESETS_HF, LMConfig
+    from kubernetes_cloud_amd.parallel.tp_emulation import emulated_rank_model
+    cfg = dict(PRESETS_HF["bloom-560m"])
+    cfg.update(hidden_size=1024, n_layer=3, n_head=16, vocab_size=4096)
+    m = emulated_rank_model(LMConfig.from_hf(cfg), 4, 0, device=dev)
+    g = torch.Generator().manual_seed(11)
+    prompts = [[int(x) for x in torch.randint(0, 4096, (40 + 3 * i,), generator=g)] for i in range(6)]
+    eng = LLMEngine(m, max_slots=8, max_len=256, use_graphs=True)
+    outs = [r.output for r in eng.generate(prompts, SamplingParams(max_new_tokens=10, do_sample=False))]
+    assert eng.runner.batched_steps > 0
+    for p, o in zip(prompts, outs):
+        _check_against_forward(m, p, o)
