@@ -36,6 +36,7 @@
 
 #include "../kernels/common.h"
 #include "../kernels/decode_tail.h"
+#include "../kernels/mm_tail.h"
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -284,6 +285,70 @@ __global__ __launch_bounds__(256) void ar_res_ln_kernel(ARPeers peers, ARCtl* ct
   dual_ln_arrive_tail<PER>(a);
 }
 
+// ----------------------------------------- one-shot + residual + row statistics (TP decode, M rows)
+// The batch 2..64 form of ar_res_ln_kernel for the matrix-core decode layer (skinny_mfma.hip): `in` is
+// this rank's partial [M, N] (row-parallel out-projection / fc_out), every rank stages it, one sync
+// round, each workgroup sums its slice over the W stagings in fp32 and writes h_out = bf16(h + sum +
+// bias) -- then the row-statistics tail (mm_tail.h): each 8-thread group (64 columns of one row)
+// publishes (mean, M2) of its rounded values, the last arriving workgroup merges them into the next
+// LayerNorm's per-row (mean, rstd), which the next projection applies to h_out on load. Block slices
+// are whole 64-column groups (N % 64 == 0).
+template <int W>
+__global__ __launch_bounds__(256) void ar_res_stats_kernel(ARPeers peers, ARCtl* ctl, int rank,
+                                                           const bf16_t* __restrict__ in, long long n8,
+                                                           long long spin_limit, const bf16_t* __restrict__ bias,
+                                                           const bf16_t* h, bf16_t* h_out, RowStats rs) {
+  const int b = blockIdx.x, nb = gridDim.x, tid = threadIdx.x;
+  const uint32_t call = ar_begin(ctl);
+  const int par = call & 1;
+  const long long groups = n8 / 8;  // 8 x 16 B = 64 columns
+  const long long gper = (groups + nb - 1) / nb;
+  const long long lo = b * gper * 8, hi = min(n8, lo + gper * 8);
+  uint4* mine = reinterpret_cast<uint4*>(peers.stage[par][rank]);
+  for (long long i = lo + tid; i < hi; i += blockDim.x) mine[i] = reinterpret_cast<const uint4*>(in)[i];
+  const bool ok = ar_sync<W>(peers, ctl, rank, 0, call, spin_limit);
+  const long long n8row = rs.N / 8;
+  for (long long i = lo + tid; i < hi; i += blockDim.x) {  // (8-thread groups stay whole: lo, hi, 256 % 8)
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int r = 0; r < W; ++r) {
+      const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(peers.stage[par][r]) + i);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[2 * j] += __uint_as_float(v[j] << 16);
+        acc[2 * j + 1] += __uint_as_float(v[j] & 0xffff0000u);
+      }
+    }
+    const long long row = i / n8row, col = (i % n8row) * 8;
+    float h8[8], b8[8];
+    load8(h + i * 8, h8);
+    if (bias) load8(bias + col, b8);
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      v[j] = ok ? h8[j] + (acc[j] + (bias ? b8[j] : 0.f)) : __int_as_float(0x7fc00000);
+      v[j] = bf2f(f2bf(v[j]));  // statistics over the rounded stream (ln_rows' convention)
+    }
+    store8(h_out + i * 8, v);
+    float sm = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sm += v[j];
+    sm += __shfl_xor(sm, 1, 64);
+    sm += __shfl_xor(sm, 2, 64);
+    sm += __shfl_xor(sm, 4, 64);
+    const float mean = sm * (1.f / 64.f);
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) q += (v[j] - mean) * (v[j] - mean);
+    q += __shfl_xor(q, 1, 64);
+    q += __shfl_xor(q, 2, 64);
+    q += __shfl_xor(q, 4, 64);
+    if ((tid & 7) == 0) rs_publish(rs, (int)row, (int)(col / 64), mean, q);
+  }
+  ar_end(ctl, call);
+  rs_arrive_of(rs, b, nb);
+}
+
 KCA_API int kca_ar_signal_bytes() { return (int)sizeof(ARSignal); }
 KCA_API int kca_ar_max_blocks() { return AR_MAX_BLOCKS; }
 
@@ -402,6 +467,44 @@ KCA_API int kca_ar_res_ln(void* const* stage0, void* const* stage1, void* const*
     KCA_AR_LN_CASE(1) KCA_AR_LN_CASE(2) KCA_AR_LN_CASE(3) KCA_AR_LN_CASE(4) KCA_AR_LN_CASE(5) KCA_AR_LN_CASE(6)
     KCA_AR_LN_CASE(7) KCA_AR_LN_CASE(8)
 #undef KCA_AR_LN_CASE
+    default:
+      return 3;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : 4;
+}
+
+// Row-parallel projection close for batch 2..64 decode: all-reduce `in` (bf16 [M, N], this rank's
+// partial), h_out = bf16(h + sum + bias) (h_out may alias h), and the row statistics of h_out for the
+// next LayerNorm (stats [M][2] = (mean, rstd) with eps) through part ([M][N/64][2] fp32) and cnt
+// (32 * 65 zero-initialised counters, re-armed by every call). N % 64 == 0, N <= 16384, M <= 64.
+KCA_API int kca_ar_res_stats(void* const* stage0, void* const* stage1, void* const* sig, void* ctl, int rank,
+                             int world, const void* in, int M, int N, int blocks, long long spin_limit,
+                             const void* bias, const void* h, void* h_out, float eps, float* part, float* stats,
+                             unsigned int* cnt, hipStream_t stream) {
+  if (world < 1 || world > AR_MAX_RANKS || rank < 0 || rank >= world || N % 64 || N <= 0 || N > 16384 || M < 1 ||
+      M > 64 || blocks < 1 || blocks > AR_MAX_BLOCKS || !part || !stats || !cnt || !h || !h_out)
+    return 1;
+  if (((uintptr_t)in | (uintptr_t)h | (uintptr_t)h_out | (uintptr_t)bias | (uintptr_t)part | (uintptr_t)stats) & 15)
+    return 2;
+  ARPeers p{};
+  for (int r = 0; r < world; ++r) {
+    p.stage[0][r] = (bf16_t*)stage0[r];
+    p.stage[1][r] = (bf16_t*)stage1[r];
+    p.sig[r] = (ARSignal*)sig[r];
+  }
+  const RowStats rs{part, stats, cnt, M, N, eps, 64};
+  ARCtl* c = (ARCtl*)ctl;
+  const long long n8 = (long long)M * N / 8;
+  switch (world) {
+#define KCA_AR_ST_CASE(WW)                                                                                      \
+  case WW:                                                                                                      \
+    hipLaunchKernelGGL((ar_res_stats_kernel<WW>), dim3(blocks), dim3(256), 0, stream, p, c, rank,               \
+                       (const bf16_t*)in, n8, spin_limit, (const bf16_t*)bias, (const bf16_t*)h, (bf16_t*)h_out, \
+                       rs);                                                                                     \
+    break;
+    KCA_AR_ST_CASE(1) KCA_AR_ST_CASE(2) KCA_AR_ST_CASE(3) KCA_AR_ST_CASE(4) KCA_AR_ST_CASE(5) KCA_AR_ST_CASE(6)
+    KCA_AR_ST_CASE(7) KCA_AR_ST_CASE(8)
+#undef KCA_AR_ST_CASE
     default:
       return 3;
   }

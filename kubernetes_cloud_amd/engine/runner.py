@@ -377,7 +377,8 @@ class ModelRunner:
         # a real TP group (BLOOM TP=8 serving): sequential layers close each row-parallel projection with
         # the custom all-reduce's fused residual + LayerNorm tail (parallel/custom_ar.py res_ln)
         self._tp_ar = None
-        if tp and not tp_local and self._layer_kind == "seq":
+        if (tp and not tp_local and self._layer_kind == "seq"
+                and os.environ.get("KCA_TP_FUSED_TAIL", "1") not in ("0", "false")):
             from ..parallel.custom_ar import lookup
             ars = {id(mm.group): lookup(mm.group) for mm in rows}
             if len(ars) == 1 and None not in ars.values():
@@ -405,7 +406,9 @@ class ModelRunner:
         # out-proj + fc_out one K-concatenated launch). KCA_DECODE_FUSED_BATCHED=0: per-projection path.
         d_model = cfg.hidden
         self.batched_steps = 0
-        self._batched_ok = (self._fused_ok and self._tp_ar is None and self.dtype == torch.bfloat16
+        # (real TP: sequential layers only -- each row-parallel projection closed by the custom all-reduce's
+        # residual + row-statistics tail, parallel/custom_ar.py res_stats)
+        self._batched_ok = (self._fused_ok and self.dtype == torch.bfloat16
                             and d_model % 64 == 0 and d_model <= 16384
                             and os.environ.get("KCA_DECODE_FUSED_BATCHED", "1") not in ("0", "false"))
 
@@ -628,6 +631,7 @@ class ModelRunner:
             fz = self._fz[key] = {
                 "h": torch.empty(B, d, **z), "xn": torch.empty(B, d, **z), "xn2": torch.empty(B, d, **z),
                 "qkv": torch.empty(B, at0.qkv.weight.shape[0], **z), "g": torch.empty(B, mlp0.fc_in.weight.shape[0], **z),
+                "y": torch.empty(B, d, **z),  # a TP rank's partial projection before the all-reduce
                 "st": smm.RowStatsBuf(B, d, self.device), "bias": biases}
         return fz
 
@@ -676,6 +680,20 @@ class ModelRunner:
             ln1 = None if first else (st.stats, blk.ln_1.weight, blk.ln_1.bias)
             x1 = xn if first else hb
             kc, vc = self.cache.k[li], self.cache.v[li]
+            if kind == "seq" and self._tp_ar is not None:
+                # TP rank: partial projections, each closed by all-reduce + bias + residual + row statistics
+                ar, y = self._tp_ar, fz["y"]
+                smm.launch([smm.job([smm.part(x1, at.qkv.weight, ln1)], qkv.shape[1], qkv, at.qkv.bias)], B, dt)
+                o = dops.decode_prep_attention(qkv, self.H, self.Hkv, self.D, self.rot, cfg.rotary_interleaved,
+                                               cos, sin, pos, slots, kc, vc, kv_lens, max_kv, at.scale, at.alibi,
+                                               out=obuf, ws=ws, block_table=tbl, window=at.window, by_row=by_row)
+                smm.mm(o, at.out.weight, out=y)
+                ar.res_stats(y, at.out.bias, hb, hb, st, blk.ln_2.eps)
+                smm.launch([smm.job([smm.part(hb, mlp.fc_in.weight, (st.stats, blk.ln_2.weight, blk.ln_2.bias))],
+                                    g.shape[1], g, mlp.fc_in.bias, act)], B, dt)
+                smm.mm(g, mlp.fc_out.weight, out=y)
+                ar.res_stats(y, mlp.fc_out.bias, hb, hb, st, nln.eps)
+                continue
             if kind == "seq":
                 smm.launch([smm.job([smm.part(x1, at.qkv.weight, ln1)], qkv.shape[1], qkv, at.qkv.bias)], B, dt)
                 o = dops.decode_prep_attention(qkv, self.H, self.Hkv, self.D, self.rot, cfg.rotary_interleaved,

@@ -91,7 +91,13 @@ class XGMIAllReduce:
         self._res_ln = _fn("kca_ar_res_ln", [ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(P), P, ctypes.c_int,
                                              ctypes.c_int, P, ctypes.c_int, ctypes.c_int, ctypes.c_longlong, P, P, P,
                                              P, P, ctypes.c_float, P, P, P, P, P, P, P])
+        self._res_stats = _fn("kca_ar_res_stats", [ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(P), P,
+                                                   ctypes.c_int, ctypes.c_int, P, ctypes.c_int, ctypes.c_int,
+                                                   ctypes.c_int, ctypes.c_longlong, P, P, P, ctypes.c_float, P, P,
+                                                   P, P])
         self._tails: dict = {}
+        self.res_ln_calls = 0  # fused tail launches (tests assert the TP decode layer took them)
+        self.res_stats_calls = 0
         lib = _lib.require()
         self.max_blocks = int(lib.kca_ar_max_blocks())
         sig_bytes = lib.kca_ar_signal_bytes()
@@ -190,6 +196,27 @@ class XGMIAllReduce:
         if rc != 0:
             raise RuntimeError(f"kca_ar_res_ln status {rc}")
         self.calls += 1
+        self.res_ln_calls += 1
+
+    def res_stats(self, t: torch.Tensor, bias, h: torch.Tensor, h_out: torch.Tensor, stats, eps: float) -> None:
+        """Close a row-parallel projection of the batch 2..64 matrix-core decode layer in ONE launch:
+        all-reduce this rank's partial ``t`` ([M, N] bf16), h_out = bf16(h + sum + bias), and the next
+        LayerNorm's per-row (mean, rstd) into ``stats`` (an ``ops.skinny_mm.RowStatsBuf``), which the
+        next projection applies on load (``kca_ar_res_stats``; graph-capturable)."""
+        M, N = t.shape
+        if not self.eligible(t) or N % 64 or N > 16384 or M > 64 or not h.is_contiguous() or h.shape != t.shape:
+            raise ValueError("tensor not eligible for the fused all-reduce + row statistics (bf16 [M<=64, N], "
+                             "N % 64 == 0, N <= 16384)")
+        groups = t.numel() // 64
+        blocks = max(1, min(self.max_blocks, -(-groups // 32)))
+        rc = self._res_stats(self._stage0, self._stage1, self._sig, P(self._ctl), self.rank, self.world,
+                             t.data_ptr(), M, N, blocks, self.spin_limit, _lib.ptr(bias), h.data_ptr(),
+                             h_out.data_ptr(), float(eps), stats.part.data_ptr(), stats.stats.data_ptr(),
+                             stats.cnt.data_ptr(), _lib.stream())
+        if rc != 0:
+            raise RuntimeError(f"kca_ar_res_stats status {rc}")
+        self.calls += 1
+        self.res_stats_calls += 1
 
     def _tail_ws(self, dev):
         """fp32 [16384] sums + the tail's zero-initialised arrival counters (local, not IPC-shared)."""

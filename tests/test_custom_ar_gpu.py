@@ -34,12 +34,63 @@ def _inputs(world, n, it):
     return [torch.randint(-8, 8, (n,), generator=g).to(torch.bfloat16) for _ in range(world)]
 
 
+def _tails(rank, world, ar):
+    """kca_ar_res_ln (batch 1) and kca_ar_res_stats (M rows) against fp32: the all-reduced partials +
+    bias + residual, rounded once (bit-exact: same summation order), then LayerNorm / row statistics
+    of the kernel's own rounded stream."""
+    import torch.nn.functional as F
+
+    from kubernetes_cloud_amd.ops.skinny_mm import RowStatsBuf, row_stats_reference
+    errs = []
+    for N in (1024, 14336):
+        for two in (False, True):
+            g = torch.Generator().manual_seed(N + two)
+            ts = [(0.5 * torch.randn(N, generator=g)).bfloat16() for _ in range(world)]
+            h = (2 * torch.randn(N, generator=g)).bfloat16()
+            bias = (0.1 * torch.randn(N, generator=g)).bfloat16()
+            gam = [(1 + 0.1 * torch.randn(N, generator=g)).bfloat16() for _ in range(2)]
+            bet = [(0.1 * torch.randn(N, generator=g)).bfloat16() for _ in range(2)]
+            d = "cuda"
+            h_out, xn, xn2 = (torch.empty(N, device=d, dtype=torch.bfloat16) for _ in range(3))
+            ar.res_ln(ts[rank].to(d), bias.to(d), h.to(d), h_out, gam[0].to(d), bet[0].to(d), 1e-5, xn,
+                      *((gam[1].to(d), bet[1].to(d), xn2) if two else ()))
+            torch.cuda.synchronize()
+            ref_h = (h.float() + (sum(t.float() for t in ts) + bias.float())).bfloat16()
+            errs.append(float((h_out.cpu().float() - ref_h.float()).abs().max()))
+            ho = h_out.cpu().float()
+            for gm, bt, out in ((gam[0], bet[0], xn),) + (((gam[1], bet[1], xn2),) if two else ()):
+                ref = F.layer_norm(ho, (N,), gm.float(), bt.float(), 1e-5)
+                errs.append(max(0.0, float((out.cpu().float() - ref).abs().max()) - 0.05))
+        for M in (3, 32):
+            g = torch.Generator().manual_seed(7 * M + N)
+            ts = [(0.5 * torch.randn(M, N, generator=g)).bfloat16() for _ in range(world)]
+            h = (2 * torch.randn(M, N, generator=g) + 1).bfloat16()
+            bias = (0.1 * torch.randn(N, generator=g)).bfloat16()
+            st = RowStatsBuf(M, N, "cuda")
+            hb = h.cuda()
+            ar.res_stats(ts[rank].cuda(), bias.cuda(), hb, hb, st, 1e-5)  # in place, as the decode layer runs it
+            torch.cuda.synchronize()
+            ref_h = (h.float() + (sum(t.float() for t in ts) + bias.float())).bfloat16()
+            errs.append(float((hb.cpu().float() - ref_h.float()).abs().max()))
+            ref_st = row_stats_reference(hb.cpu(), 1e-5)
+            rel = ((st.stats.cpu() - ref_st).abs() / (ref_st.abs() + 1e-3)).max()
+            errs.append(max(0.0, float(rel) - 1e-4))
+    return errs
+
+
 def _worker(rank, world, port, q, mode):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
     from kubernetes_cloud_amd.parallel.custom_ar import ONE_SHOT, TWO_SHOT, AllReduceError, XGMIAllReduce
     try:
+        if mode == "tails":
+            ar = XGMIAllReduce(None, max_bytes=4 << 20, spin_limit=1 << 24)
+            errs = _tails(rank, world, ar)
+            q.put((rank, ar.error() == 0 and ar.res_ln_calls == 4 and ar.res_stats_calls == 4, errs))
+            dist.barrier()
+            ar.close()
+            return
         if mode == "timeout":
             ar = XGMIAllReduce(None, max_bytes=1 << 20, spin_limit=4000)
             ok = True
@@ -105,3 +156,11 @@ def test_xgmi_allreduce_interleaved_sizes_with_rank_skew_is_exact():
 def test_xgmi_allreduce_timeout_poisons_and_raises():
     for rank, ok, _ in _run("timeout"):
         assert ok, rank
+
+
+def test_xgmi_fused_tails_match_fp32():
+    """The TP decode layer's all-reduce tails: residual + bias + LayerNorm (batch 1, with and without the
+    second LayerNorm) and residual + bias + row statistics (M rows), N = 1024 and BLOOM's 14336."""
+    for rank, ok, errs in _run("tails"):
+        assert ok, rank
+        assert max(errs) == 0.0, (rank, errs)
