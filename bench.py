@@ -251,9 +251,48 @@ def main():
     if args.extra == "on" or (args.extra == "auto" and world == 1):
         _extras(args, dev, rec)
     if rec is not None:
+        summ = _summary(rec)
+        rec["summary"] = summ  # last key: the tail of the (long) line carries every headline value
         print(json.dumps(rec), flush=True)
+        print("[bench] summary " + json.dumps(summ, separators=(",", ":")), file=sys.stderr, flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
+
+
+def _summary(rec) -> dict:
+    """Every secondary's headline value in a few hundred bytes (the driver keeps
+    only the tail of the ~10 KB line): txt2img, DreamBooth, decode ms/token per (model, batch,
+    sampling), BLOOM TP=8 rank ms/token per batch, weight-load GB/s (and of its storage ceiling)."""
+    out = {"gptj_train_tok_s": rec.get("value")}
+
+    def val(key):
+        v = rec.get(key)
+        return v.get("value") if isinstance(v, dict) else None
+
+    out["txt2img_img_s"] = val("secondary")
+    out["dreambooth_samples_s"] = val("secondary_dreambooth")
+    dec = rec.get("secondary_decode")
+    for r in (dec or {}).get("records", []) if isinstance(dec, dict) else []:
+        m = "gptj" if "gpt-j" in str(r.get("metric")) else "neox"
+        s_ = "" if r.get("sampling") in (None, "greedy") else "_" + str(r["sampling"])
+        out[f"decode_{m}_b{r.get('batch')}{s_}_ms"] = r.get("decode_ms_per_token")
+    bl = rec.get("secondary_bloom_tp8_rank")
+    for r in (bl or {}).get("records", []) if isinstance(bl, dict) else []:
+        if isinstance(r, dict) and "batch" in r:
+            out[f"bloom_tp8_rank_b{r['batch']}_ms"] = r.get("decode_ms_per_token")
+    wl = rec.get("secondary_weight_load")
+    for r in (wl or {}).get("records", []) if isinstance(wl, dict) else []:
+        if isinstance(r, dict) and "gbps" in r:
+            k = "bloom_shard" if "bloom" in str(r.get("model")) else "gptj"
+            out[f"load_{k}_gbps"] = r.get("gbps")
+            out[f"load_{k}_of_storage"] = r.get("of_storage")
+            out[f"load_{k}_path"] = r.get("read_path")
+    bt = rec.get("bloom_tp")
+    if isinstance(bt, dict):
+        for r in bt.get("records", []) or []:
+            if isinstance(r, dict) and "batch" in r:
+                out[f"bloom_tp{rec.get('n_gpus')}_b{r['batch']}_ms"] = r.get("decode_ms_per_token")
+    return {k: v for k, v in out.items() if v is not None}
 
 
 def _bloom_tp(args, info, rec):

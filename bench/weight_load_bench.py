@@ -86,14 +86,29 @@ def _load(cfg, uri, dev, tp, threads):
     return model, load_into_module(model, uri, device=dev, threads=threads)
 
 
+def _ceiling_file(src: str, dst: str) -> None:
+    """A second file of the same bytes, written and flushed after the timed loads: the raw read that
+    prices the storage never touches the file the loads read (a raw read of the
+    SAME file just before the "cold" load warmed whatever cache sits below the page cache, and the
+    load then beat its own ceiling, of_storage 1.229)."""
+    import shutil
+    shutil.copyfile(src, dst)
+    fd = os.open(dst, os.O_RDONLY)
+    try:
+        os.fsync(fd)
+    finally:
+        os.close(fd)
+
+
 def run_weight_load(model="gpt-j-6b", directory="/tmp", threads=8, sources=("cold", "repeat"), tp=0, layers=0):
     """bench.py's ``secondary_weight_load``: write a random-init fp16 model (or rank 0's TP=``tp``
     shard; ``layers`` > 0: the first layers only, the record extrapolates the full shard) as
-    ``.tensors``, read the file raw with O_DIRECT (the storage ceiling, no device copy), then time
-    no-init construction + native O_DIRECT stream into HBM. Returns one record per source; the file
-    is removed."""
+    ``.tensors`` and flush it; time no-init construction + native O_DIRECT stream into HBM FIRST (the
+    file has not been read since it was written: "cold"), then price the storage with a raw O_DIRECT
+    read of a separate copy. Each record carries the bytes the streamer read with O_DIRECT and the
+    bytes that fell back to buffered reads. Returns one record per source; the files are removed."""
     from kubernetes_cloud_amd.io.hf import serialize_causal_lm
-    from kubernetes_cloud_amd.io.native import storage_read_rate
+    from kubernetes_cloud_amd.io.native import storage_ceiling
     from kubernetes_cloud_amd.models.config import preset
     dev = torch.device("cuda", torch.cuda.current_device())
     cfg = preset(model)
@@ -101,14 +116,14 @@ def run_weight_load(model="gpt-j-6b", directory="/tmp", threads=8, sources=("col
     if layers:
         cfg.n_layers = layers
     path = os.path.join(directory, f"kca_bench_{model}{f'_tp{tp}r0' if tp else ''}_{os.getpid()}.tensors")
+    ceil_path = path + ".ceiling"
     m = _build(cfg, dev, tp)
     ref = {k: v.float().abs().sum().item() for k, v in list(m.state_dict().items())[:3]}
     layer_bytes = sum(p.numel() * p.element_size() for p in m.h[0].parameters())
     total = sum(p.numel() * p.element_size() for p in m.parameters())
     serialize_causal_lm(m, path)
     # flush the freshly written file before any timed read: an O_DIRECT read of a file with dirty pages
-    # first writes them back, so whichever read came first paid the writeback (round 4's 6.75 -> 6.11
-    # GB/s "drop", and a raw rate below the load rate)
+    # first writes them back (round 4's 6.75 -> 6.11 GB/s "drop")
     fd = os.open(path, os.O_RDONLY)
     try:
         os.fsync(fd)
@@ -118,7 +133,6 @@ def run_weight_load(model="gpt-j-6b", directory="/tmp", threads=8, sources=("col
     torch.cuda.empty_cache()
     out = []
     try:
-        raw = storage_read_rate(path, threads=threads)  # O_DIRECT: nothing of it stays in the page cache
         for src in sources:
             torch.cuda.synchronize()
             t = time.perf_counter()
@@ -130,7 +144,9 @@ def run_weight_load(model="gpt-j-6b", directory="/tmp", threads=8, sources=("col
             rec = {"metric": "weight load", "source": f"file O_DIRECT ({src})",
                    "model": model + (f" TP={tp} rank-0 shard" if tp else ""), "dtype": "fp16",
                    "bytes": int(st["bytes"]), "gbps": round(st["gbps"], 2), "seconds_to_ready": round(ready, 3),
-                   "storage_gbps": round(raw["gbps"], 2), "of_storage": round(st["gbps"] / max(raw["gbps"], 1e-9), 3),
+                   "odirect_bytes": st.get("odirect_bytes"), "buffered_bytes": st.get("buffered_bytes"),
+                   "read_path": ("O_DIRECT" if not st.get("buffered_bytes") else
+                                 ("buffered" if not st.get("odirect_bytes") else "mixed")),
                    "threads": threads, "data": "random-init weights"}
             if layers and layers < full_layers:  # the whole shard at the measured rate
                 full = total + (full_layers - layers) * layer_bytes
@@ -139,8 +155,16 @@ def run_weight_load(model="gpt-j-6b", directory="/tmp", threads=8, sources=("col
             out.append(rec)
             del model_
             torch.cuda.empty_cache()
+        _ceiling_file(path, ceil_path)
+        raw = storage_ceiling(ceil_path)  # O_DIRECT, best of several queue depths
+        for rec in out:
+            rec.update(storage_gbps=round(raw["gbps"], 2), storage_file="separate copy, read after the loads",
+                       storage_queue=f"{raw['threads']} threads x {raw['chunk'] >> 20} MiB",
+                       of_storage=round(rec["gbps"] / max(raw["gbps"], 1e-9), 3))
     finally:
-        os.remove(path)
+        for p_ in (path, ceil_path):
+            if os.path.exists(p_):
+                os.remove(p_)
     return out
 
 

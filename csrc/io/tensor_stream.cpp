@@ -111,7 +111,9 @@ KCA_HOST_API int kca_read_ranges(const char* path, int n, const int64_t* offs, c
 }
 
 // Stream byte ranges of `path` into device memory on `device`.
-// stats[0] = bytes, stats[1] = seconds (wall, including the final sync).
+// stats[0] = bytes, stats[1] = seconds (wall, including the final sync), stats[2] = payload bytes
+// read with O_DIRECT, stats[3] = payload bytes that took the buffered path (O_DIRECT not requested,
+// refused at open, or a short read) -- the record says which path a "cold" number measured.
 KCA_HOST_API int kca_stream_to_device(const char* path, int n, const int64_t* offs,
                                       const int64_t* lens, void** dev_dsts, int device,
                                       int n_threads, int64_t chunk, int use_odirect,
@@ -125,6 +127,7 @@ KCA_HOST_API int kca_stream_to_device(const char* path, int n, const int64_t* of
   n_threads = std::max(1, std::min(n_threads, 32));
   std::atomic<size_t> next{0};
   std::atomic<int> err{0};
+  std::atomic<int64_t> direct_bytes{0}, buffered_bytes{0};
   double t0 = now_s();
   auto work = [&]() {
     if (hipSetDevice(device) != hipSuccess) { err = 3; return; }
@@ -157,12 +160,16 @@ KCA_HOST_API int kca_stream_to_device(const char* path, int n, const int64_t* of
         int64_t alen = (lead + c.len + kAlign - 1) / kAlign * kAlign;
         ssize_t r = ::pread(fd_dir, hb, (size_t)alen, (off_t)a0);
         ok = r >= lead + c.len;
-        if (!ok) {  // short read at EOF or O_DIRECT refusal: buffered fallback
+        if (ok) {
+          direct_bytes += c.len;
+        } else {  // short read at EOF or O_DIRECT refusal: buffered fallback
           lead = 0;
           ok = pread_full(fd_buf, hb, c.len, c.off);
+          buffered_bytes += c.len;
         }
       } else {
         ok = pread_full(fd_buf, hb, c.len, c.off);
+        buffered_bytes += c.len;
       }
       if (!ok) { err = 2; break; }
       if (hipMemcpyAsync(c.dst, hb + lead, (size_t)c.len, hipMemcpyHostToDevice, st) != hipSuccess) {
@@ -189,6 +196,8 @@ KCA_HOST_API int kca_stream_to_device(const char* path, int n, const int64_t* of
     for (int i = 0; i < n; ++i) tot += lens[i];
     stats[0] = (double)tot;
     stats[1] = now_s() - t0;
+    stats[2] = (double)direct_bytes.load();
+    stats[3] = (double)buffered_bytes.load();
   }
   return err.load();
 }

@@ -219,38 +219,62 @@ __global__ __launch_bounds__(WV * 64) void mm_skinny_kernel(MmArgs a) {
       }
   };
   // activation chunk: piece q = tid + WV*64 j of the [MT*16][PPR] stage
-  auto load_x = [&](int c, u32x4v (&xr)[T::XP]) {
-    int k0;
-    const MmPart& P = J.p[chunk_part(J, c, nc0, KC, k0)];
+  // activation chunk: piece q = tid + WV*64 j of the [MT*16][PPR] stage -- row m_j = q / PPR (fixed per
+  // thread and j), column piece tid % PPR (the same for every j). LN-on-load: the rows' (mean, rstd)
+  // are read once per part, gamma / beta once per chunk, the normalisation runs at staging time (the
+  // first version re-read all four per piece: 5 loads per 16 B of activation)
+  static_assert((WV * 64) % T::PPR == 0, "a thread's pieces share one column");
+  const int xp = tid % T::PPR;
+  float mu[2][T::XP], rsd[2][T::XP];
+  if constexpr (LN) {
 #pragma unroll
-    for (int j = 0; j < T::XP; ++j) {
-      const int q = tid + WV * 64 * j, m = q / T::PPR, k = k0 + (q % T::PPR) * 8;
-      xr[j] = u32x4v{0u, 0u, 0u, 0u};
-      if (m < M && k < P.K) {
-        xr[j] = ld16(P.x + (long long)m * P.ldx + k);
-        if constexpr (LN) {
-          const float mu = P.stats[2 * m], rs = P.stats[2 * m + 1];
-          const u32x4v gv = ld16(P.gamma + k);
-          const u32x4v bv = P.beta ? ld16(P.beta + k) : u32x4v{0u, 0u, 0u, 0u};
-          u32x4v o;
+    for (int pi = 0; pi < 2; ++pi)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const uint32_t hx = xr[j][e], gg = gv[e], bb = bv[e];
-            const float lo = (e2f<DT>(hx & 0xffffu) - mu) * rs * e2f<DT>(gg & 0xffffu) + e2f<DT>(bb & 0xffffu);
-            const float hi = (e2f<DT>(hx >> 16) - mu) * rs * e2f<DT>(gg >> 16) + e2f<DT>(bb >> 16);
-            o[e] = f2e<DT>(lo) | (f2e<DT>(hi) << 16);
-          }
-          xr[j] = o;
+      for (int j = 0; j < T::XP; ++j) {
+        const int m = (tid + WV * 64 * j) / T::PPR;
+        mu[pi][j] = 0.f;
+        rsd[pi][j] = 0.f;
+        if (pi < J.nparts && m < M) {
+          const float2 v = *reinterpret_cast<const float2*>(J.p[pi].stats + 2 * m);
+          mu[pi][j] = v.x;
+          rsd[pi][j] = v.y;
         }
       }
-    }
-  };
-  auto store_x = [&](const u32x4v (&xr)[T::XP], int buf) {
+  }
+  auto load_x = [&](int c, u32x4v (&xr)[T::XP], u32x4v& gv, u32x4v& bv) {
+    int k0;
+    const MmPart& P = J.p[chunk_part(J, c, nc0, KC, k0)];
+    const int k = k0 + xp * 8;
 #pragma unroll
     for (int j = 0; j < T::XP; ++j) {
-      const int q = tid + WV * 64 * j, m = q / T::PPR, p = q % T::PPR;
-      if (m < MT * 16)
-        *reinterpret_cast<u32x4v*>(xs + buf * T::XS + m * KC + ((p ^ (m & 15)) << 3)) = xr[j];
+      const int m = (tid + WV * 64 * j) / T::PPR;
+      xr[j] = (m < M && k < P.K) ? ld16(P.x + (long long)m * P.ldx + k) : u32x4v{0u, 0u, 0u, 0u};
+    }
+    if constexpr (LN) {
+      gv = k < P.K ? ld16(P.gamma + k) : u32x4v{0u, 0u, 0u, 0u};
+      bv = (P.beta && k < P.K) ? ld16(P.beta + k) : u32x4v{0u, 0u, 0u, 0u};
+    }
+  };
+  auto store_x = [&](u32x4v (&xr)[T::XP], const u32x4v& gv, const u32x4v& bv, int c, int buf) {
+#pragma unroll
+    for (int j = 0; j < T::XP; ++j) {
+      const int m = (tid + WV * 64 * j) / T::PPR;
+      if (m >= MT * 16) continue;
+      if constexpr (LN) {
+        int k0;
+        const int pi = chunk_part(J, c, nc0, KC, k0);
+        const float mj = pi ? mu[1][j] : mu[0][j], rj = pi ? rsd[1][j] : rsd[0][j];
+        u32x4v o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t hx = xr[j][e], gg = gv[e], bb = bv[e];
+          const float lo = (e2f<DT>(hx & 0xffffu) - mj) * rj * e2f<DT>(gg & 0xffffu) + e2f<DT>(bb & 0xffffu);
+          const float hi = (e2f<DT>(hx >> 16) - mj) * rj * e2f<DT>(gg >> 16) + e2f<DT>(bb >> 16);
+          o[e] = f2e<DT>(lo) | (f2e<DT>(hi) << 16);
+        }
+        xr[j] = m < M ? o : u32x4v{0u, 0u, 0u, 0u};
+      }
+      *reinterpret_cast<u32x4v*>(xs + buf * T::XS + m * KC + ((xp ^ (m & 15)) << 3)) = xr[j];
     }
   };
 
@@ -263,7 +287,7 @@ __global__ __launch_bounds__(WV * 64) void mm_skinny_kernel(MmArgs a) {
   // one chunk: its weight registers -> the wave's LDS slot, then the next chunk is requested into the
   // freed registers, the next activation chunk is staged, the MFMAs run (one chunk in flight per wave:
   // two measured no faster, the registers cost occupancy -- profiles/mm_sweep_r6/)
-  u32x4v xr[T::XP];
+  u32x4v xr[T::XP], gv = {0u, 0u, 0u, 0u}, bv = {0u, 0u, 0u, 0u};
   auto chunk = [&](int c, u32x4v (&w)[NRW][T::NI]) {
     const int buf = (c - c_lo) & 1;
     wave_lds_sync();
@@ -276,7 +300,7 @@ __global__ __launch_bounds__(WV * 64) void mm_skinny_kernel(MmArgs a) {
       }
     if (c + 1 < c_hi) load_w(c + 1, w);
     const bool nx = c + 1 < c_hi;
-    if (nx) load_x(c + 1, xr);
+    if (nx) load_x(c + 1, xr, gv, bv);
     wave_lds_sync();
     const uint16_t* xb = xs + buf * T::XS;
 #pragma unroll
@@ -292,14 +316,14 @@ __global__ __launch_bounds__(WV * 64) void mm_skinny_kernel(MmArgs a) {
         for (int mt = 0; mt < MT; ++mt) acc[nr][mt] = mfma16<DT>(af, bf[mt], acc[nr][mt]);
       }
     }
-    if (nx) store_x(xr, buf ^ 1);
+    if (nx) store_x(xr, gv, bv, c + 1, buf ^ 1);
     __syncthreads();
   };
   u32x4v wa[NRW][T::NI];
   if (c_lo < c_hi) {
     load_w(c_lo, wa);
-    load_x(c_lo, xr);
-    store_x(xr, 0);
+    load_x(c_lo, xr, gv, bv);
+    store_x(xr, gv, bv, c_lo, 0);
   }
   __syncthreads();
   for (int c = c_lo; c < c_hi; ++c) chunk(c, wa);

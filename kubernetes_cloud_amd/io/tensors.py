@@ -98,13 +98,13 @@ def read_header(path: str) -> tuple[dict, int]:
 
 
 def _stream(path: str, offs, lens, ptrs, device: torch.device, threads: int, chunk: int,
-            odirect: bool) -> tuple[float, float]:
+            odirect: bool, info: dict | None = None) -> tuple[float, float]:
     from . import native
     n = len(offs)
     a_off = (ctypes.c_longlong * n)(*offs)
     a_len = (ctypes.c_longlong * n)(*lens)
     a_ptr = (ctypes.c_void_p * n)(*ptrs)
-    stats = (ctypes.c_double * 2)()
+    stats = (ctypes.c_double * 4)()
     lib = native.load()
     if device.type == "cuda":
         rc = lib.kca_stream_to_device(path.encode(), n, a_off, a_len, a_ptr,
@@ -114,6 +114,8 @@ def _stream(path: str, offs, lens, ptrs, device: torch.device, threads: int, chu
         rc = lib.kca_read_ranges(path.encode(), n, a_off, a_len, a_ptr, threads, chunk, stats)
     if rc != 0:
         raise IOError(f"native streamer failed on {path} (code {rc})")
+    if info is not None and device.type == "cuda":  # which read path carried the payload
+        info["odirect_bytes"], info["buffered_bytes"] = int(stats[2]), int(stats[3])
     return stats[0], stats[1]
 
 
@@ -175,12 +177,13 @@ def load_into_module(module: torch.nn.Module, path: str, device=None, strict: bo
         if missing:
             raise KeyError(f"missing in {path}: {missing[:8]}")
     from . import native
+    paths: dict = {}
     if rem is not None:
         from . import remote
         nbytes, secs = remote.stream(rem, offs, lens, ptrs, dev, threads=max(threads, 16),
                                      chunk=min(chunk, 16 << 20))
     elif native.available():
-        nbytes, secs = _stream(path, offs, lens, ptrs, dev, threads, chunk, odirect)
+        nbytes, secs = _stream(path, offs, lens, ptrs, dev, threads, chunk, odirect, paths)
     else:
         if dev.type == "cuda":
             native.load()  # raises: never silently fall back on a GPU load
@@ -191,7 +194,7 @@ def load_into_module(module: torch.nn.Module, path: str, device=None, strict: bo
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     return {"bytes": nbytes, "seconds": secs, "gbps": nbytes / max(secs, 1e-9) / 1e9,
-            "seconds_total": time.perf_counter() - t_begin, "source": "http" if rem is not None else "file"}
+            "seconds_total": time.perf_counter() - t_begin, "source": "http" if rem is not None else "file", **paths}
 
 
 def load_state_dict(path: str, device="cpu", threads: int = 8) -> dict:
@@ -207,6 +210,7 @@ def load_state_dict(path: str, device="cpu", threads: int = 8) -> dict:
             ptrs.append(t.data_ptr())
             ts.append(t)
     from . import native
+    paths: dict = {}
     if rem is not None:
         from . import remote
         remote.stream(rem, offs, lens, ptrs, dev, threads=max(threads, 16))
