@@ -68,6 +68,13 @@ def run_tp_decode(model_name="bloom-176b", layers=0, batches=(1, 8, 32), prompt_
     if world > 1 and custom_ar:
         from kubernetes_cloud_amd.parallel.custom_ar import register
         ar = register(None)
+    elif emu is not None and custom_ar:
+        # a rank-local custom all-reduce for the emulated group: the emulated rank closes each row-parallel
+        # projection with the same fused all-reduce tail kernels a TP=8 rank runs (kca_ar_res_ln at batch 1,
+        # kca_ar_res_stats at batch > 1), itself the only peer -- the measured step has the deployment's
+        # launch structure, minus the xGMI transfers
+        from kubernetes_cloud_amd.parallel.custom_ar import register
+        ar = register(emu)
     runner = ModelRunner(model, max_slots=max(batches), max_len=prompt_len + new_tokens + 8)
     chan = None
     if world > 1:
@@ -107,6 +114,10 @@ def run_tp_decode(model_name="bloom-176b", layers=0, batches=(1, 8, 32), prompt_
                         "layers": cfg.n_layers, "tp": tp, "load_s": round(load_s, 1), "dtype": dtype,
                         "custom_allreduce": ar is not None, "ctrl": chan.kind if chan is not None else None,
                         "pipelined": bool(eng.pipeline),
+                        "step_launches": runner.step_launches.get(next((b for b in sorted(runner.step_launches)
+                                                                       if b >= B), B)),
+                        "launch_structure": ("real-TP fused tails" if runner._tp_ar is not None else
+                                             "single-device fused layer"),
                         "data": "random-init weights"})
             if emu is not None:
                 out[-1].update(_emulation_notes(model, cfg, B, emulate_tp))
@@ -133,8 +144,10 @@ def _emulation_notes(model, cfg, B, tp):
             "collectives_excluded": {"all_reduce_per_token": 2 * cfg.n_layers,
                                      "all_reduce_bytes": B * cfg.hidden * 2,
                                      "all_gather_logits_bytes": B * (cfg.vocab_size // tp) * 2,
-                                     "note": "stand-in collectives (identity / local tile): a TP=8 node adds "
-                                             "2 xGMI all-reduces per layer, priced by allreduce_bench"}}
+                                     "note": "with the rank-local custom all-reduce the fused all-reduce tails run "
+                                             "(staging, sync round, tail) with the rank as its only peer; a TP=8 "
+                                             "node adds the xGMI reads of the 7 peers' partials, priced by "
+                                             "allreduce_bench"}}
 
 
 def main():

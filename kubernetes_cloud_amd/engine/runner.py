@@ -33,6 +33,7 @@ import torch
 
 from .. import ops
 from ..ops import decode as dops
+from ..ops import _lib
 from ..ops import skinny_mm as smm
 from ..ops.gemv import embed_ln_rows, ln_rows, ln_skinny_linear, skinny_linear
 
@@ -376,8 +377,10 @@ class ModelRunner:
         self._layer_kind = ("gptj" if all(x is None for x in ln2) else "neox") if cfg.parallel_residual else "seq"
         # a real TP group (BLOOM TP=8 serving): sequential layers close each row-parallel projection with
         # the custom all-reduce's fused residual + LayerNorm tail (parallel/custom_ar.py res_ln)
+        # (an emulated rank -- parallel/tp_emulation.py -- whose group has a rank-local custom all-reduce
+        # registered runs the same kernels: bench/bloom_tp_bench.py measures the deployment's launches)
         self._tp_ar = None
-        if (tp and not tp_local and self._layer_kind == "seq"
+        if (tp and self._layer_kind == "seq"
                 and os.environ.get("KCA_TP_FUSED_TAIL", "1") not in ("0", "false")):
             from ..parallel.custom_ar import lookup
             ars = {id(mm.group): lookup(mm.group) for mm in rows}
@@ -391,6 +394,7 @@ class ModelRunner:
                           and (self._layer_kind == "seq"
                                or (self.H == self.Hkv and self.D % 8 == 0 and 64 < self.D <= 256)))
         self._fz: dict = {}
+        self.step_launches: dict = {}
         self._outbufs: dict = {}
         self._chain_src = None
         # the fused step head gathers the token embedding itself (no learned positions / scale / LN on
@@ -907,6 +911,14 @@ class ModelRunner:
         return ob
 
     def _step_body(self, st, Bb, Kb, mc=False):
+        n0 = _lib.LAUNCHES[0]
+        try:
+            self._step_body_inner(st, Bb, Kb, mc)
+        finally:
+            # native launches one decode step issues (counted when the step is built: eager, or graph capture)
+            self.step_launches[Bb] = _lib.LAUNCHES[0] - n0
+
+    def _step_body_inner(self, st, Bb, Kb, mc=False):
         pk = st["pk"]
         # chained tokens resolved on the device by the fused B = 1 step head (_layers_decode_fused)
         self._chain_src = (pk.d("chain"), st["ids"]) if (Bb == 1 and self._embed_head) else None

@@ -165,9 +165,15 @@ def has(name: str) -> bool:
 SYNC_LAUNCH = os.environ.get("KCA_SYNC_LAUNCH", "0") in ("1", "true")
 
 
+# native launches issued through this module, ops/skinny_mm.py and parallel/custom_ar.py (the serving
+# runner reports launches per decode step from it)
+LAUNCHES = [0]
+
+
 def call(name: str, *args):
     lib = require()
     fn = getattr(lib, name)
+    LAUNCHES[0] += 1
     rc = fn(*args)
     if rc != 0:
         raise RuntimeError(f"{name} returned status {rc} (unsupported shape/arguments)")
@@ -183,6 +189,7 @@ def call_rc(name: str, *args) -> int:
     """``call`` for entry points whose nonzero status means "shape outside this kernel" (the caller
     takes another path) rather than an error."""
     rc = getattr(require(), name)(*args)
+    LAUNCHES[0] += rc == 0
     if rc == 0 and SYNC_LAUNCH and torch.cuda.is_available():
         torch.cuda.synchronize()
     return rc

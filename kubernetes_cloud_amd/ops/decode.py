@@ -221,6 +221,7 @@ def decode_prep_attention_gemv(qkv, n_heads, kv_heads, head_dim, rot, interleave
         return False
     if rc != 0:
         raise RuntimeError(f"kca_decode_prep_attn_gemv returned status {rc}")
+    _lib.LAUNCHES[0] += 1
     return True
 
 

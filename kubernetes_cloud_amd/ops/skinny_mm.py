@@ -172,6 +172,7 @@ def launch(jobs, M: int, dtype: torch.dtype, ks: int | None = None, nr: int | No
     rc = fn(ctypes.addressof(a), _DT[dtype], _lib.stream())
     if rc != 0:
         raise RuntimeError(f"kca_mm_skinny returned status {rc} (unsupported shape/arguments)")
+    _lib.LAUNCHES[0] += 1
     if _lib.SYNC_LAUNCH:
         torch.cuda.synchronize()
 

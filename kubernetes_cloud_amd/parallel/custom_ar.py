@@ -68,10 +68,13 @@ class AllReduceError(RuntimeError):
 
 class XGMIAllReduce:
     def __init__(self, group=None, max_bytes: int = 64 << 20, one_shot_max: int = 256 << 10,
-                 spin_limit: int = 1 << 26):
+                 spin_limit: int = 1 << 26, local: bool = False):
+        """``local=True``: a world-1 instance with no process group (parallel/tp_emulation.py: one rank of
+        a TP layout on one GPU runs the deployment's all-reduce kernels -- staging, sync round, fused
+        tails -- with itself as the only peer)."""
         self.group = group
-        self.rank = dist.get_rank(group)
-        self.world = dist.get_world_size(group)
+        self.rank = 0 if local else dist.get_rank(group)
+        self.world = 1 if local else dist.get_world_size(group)
         if self.world > 8:
             raise ValueError("xGMI all-reduce supports up to 8 ranks (one node)")
         self.max_bytes = max_bytes
@@ -119,7 +122,10 @@ class XGMIAllReduce:
                 raise RuntimeError("hipIpcGetMemHandle failed (is HSA_ENABLE_IPC_MODE_LEGACY=0 exported?)")
             hs.append(buf.raw)
         allh = [None] * self.world
-        dist.all_gather_object(allh, hs, group=group)
+        if local:
+            allh[0] = hs
+        else:
+            dist.all_gather_object(allh, hs, group=group)
         self._opened = []
         ptrs = [[0] * self.world for _ in range(3)]
         for r in range(self.world):
@@ -137,7 +143,8 @@ class XGMIAllReduce:
         self._stage0 = arr(*ptrs[0])
         self._stage1 = arr(*ptrs[1])
         self._sig = arr(*ptrs[2])
-        dist.barrier(group=group)
+        if not local:
+            dist.barrier(group=group)
 
     def eligible(self, t: torch.Tensor) -> bool:
         return (t.is_cuda and t.dtype == torch.bfloat16 and t.is_contiguous() and t.numel() % 8 == 0
@@ -157,6 +164,7 @@ class XGMIAllReduce:
         if rc != 0:
             raise RuntimeError(f"kca_ar_run status {rc}")
         self.calls += 1
+        _lib.LAUNCHES[0] += 1
         return t
 
     def all_gather(self, t: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
@@ -176,6 +184,7 @@ class XGMIAllReduce:
         if rc != 0:
             raise RuntimeError(f"kca_ar_run (all-gather) status {rc}")
         self.calls += 1
+        _lib.LAUNCHES[0] += 1
         return out
 
     def res_ln(self, t: torch.Tensor, bias, h: torch.Tensor, h_out: torch.Tensor, gamma: torch.Tensor, beta,
@@ -197,6 +206,7 @@ class XGMIAllReduce:
             raise RuntimeError(f"kca_ar_res_ln status {rc}")
         self.calls += 1
         self.res_ln_calls += 1
+        _lib.LAUNCHES[0] += 1
 
     def res_stats(self, t: torch.Tensor, bias, h: torch.Tensor, h_out: torch.Tensor, stats, eps: float) -> None:
         """Close a row-parallel projection of the batch 2..64 matrix-core decode layer in ONE launch:
@@ -217,6 +227,7 @@ class XGMIAllReduce:
             raise RuntimeError(f"kca_ar_res_stats status {rc}")
         self.calls += 1
         self.res_stats_calls += 1
+        _lib.LAUNCHES[0] += 1
 
     def _tail_ws(self, dev):
         """fp32 [16384] sums + the tail's zero-initialised arrival counters (local, not IPC-shared)."""
@@ -252,9 +263,15 @@ class XGMIAllReduce:
 
 def register(group=None, max_bytes: int = 64 << 20) -> XGMIAllReduce | None:
     """Enable the custom all-reduce for ``group`` (no-op off GPU or if disabled
-    with KCA_CUSTOM_AR=0)."""
+    with KCA_CUSTOM_AR=0). An emulated TP group (parallel/tp_emulation.py) gets a rank-local
+    instance, so the emulated rank runs the same tail kernels as a real rank."""
     if not torch.cuda.is_available() or os.environ.get("KCA_CUSTOM_AR", "1") == "0":
         return None
+    from .tp_emulation import is_emulated
+    if is_emulated(group):
+        ar = XGMIAllReduce(None, max_bytes, local=True)
+        _REGISTRY[id(group)] = ar
+        return ar
     if dist.get_world_size(group) < 2:  # nothing to exchange
         return None
     ar = XGMIAllReduce(group, max_bytes)

@@ -972,3 +972,29 @@ def test_engine_batched_mfma_bloom_tp_emulated_rank():
     assert eng.runner.batched_steps > 0
     for p, o in zip(prompts, outs):
         _check_against_forward(m, p, o)
+
+
+def test_engine_emulated_rank_runs_real_tp_tails():
+    """with a rank-local custom all-reduce registered for the emulated group, rank 0 of a
+    TP=4 BLOOM layout closes every row-parallel projection with the deployment's fused all-reduce tails
+    (kca_ar_res_ln at batch 1, kca_ar_res_stats at batch > 1) -- the kernels bench/bloom_tp_bench.py then
+    measures -- and still matches the model's own forward through the same stand-in collectives."""
+    from kubernetes_cloud_amd.engine.llm_engine import LLMEngine, SamplingParams
+    from kubernetes_cloud_amd.models.config import PRESETS_HF, LMConfig
+    from kubernetes_cloud_amd.parallel.custom_ar import register
+    from kubernetes_cloud_amd.parallel.tp_emulation import emulated_rank_model
+    cfg = dict(PRESETS_HF["bloom-560m"])
+    cfg.update(hidden_size=1024, n_layer=3, n_head=16, vocab_size=4096)
+    m = emulated_rank_model(LMConfig.from_hf(cfg), 4, 0, device=dev)
+    ar = register(m.h[0].attn.out.group)
+    assert ar is not None and ar.world == 1
+    g = torch.Generator().manual_seed(13)
+    prompts = [[int(x) for x in torch.randint(0, 4096, (30 + 7 * i,), generator=g)] for i in range(6)]
+    eng = LLMEngine(m, max_slots=8, max_len=256, use_graphs=True)
+    assert eng.runner._tp_ar is ar and eng.runner._batched_ok
+    sp = SamplingParams(max_new_tokens=10, do_sample=False)
+    outs = [eng.generate([prompts[0]], sp)[0].output] + [r.output for r in eng.generate(prompts, sp)]
+    assert ar.res_ln_calls > 0 and ar.res_stats_calls > 0 and ar.error() == 0
+    assert eng.runner.step_launches  # launches per step recorded for the bench
+    for p, o in zip([prompts[0]] + prompts, outs):
+        _check_against_forward(m, p, o)
