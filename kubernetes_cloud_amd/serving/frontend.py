@@ -81,6 +81,8 @@ class _Engine:
             m = self.models[name]
             if op == "call":
                 res = await m(*args)
+            elif op == "ready":  # the front-end's health / readiness routes ask the real model
+                res = bool(getattr(m, "ready", True))
             elif op == "infer":
                 res = await asyncio.get_running_loop().run_in_executor(None, lambda: m.infer(*args))
             else:
@@ -139,9 +141,30 @@ def _proxy_models(client: _Client, meta: dict):
     from .server import Model
 
     class ProxyModel(Model):
+        """The engine-side model seen from the front-end: calls go over the connection; ``ready`` is the
+        real model's, asked again at most every READY_TTL_S seconds (a constant True kept
+        /v2/health/ready and the model-ready routes green whatever the engine's model said)."""
+        READY_TTL_S = 1.0
+
         def __init__(self, name, md):
             super().__init__(name)
-            self.ready, self._md = True, md
+            self._md = md
+            self._ready_at, self._ready_val = 0.0, False
+
+        @property
+        def ready(self):
+            now = time.monotonic()
+            if now - self._ready_at > self.READY_TTL_S:
+                try:
+                    self._ready_val = bool(client.submit(self.name, "ready").result(timeout=5.0))
+                except Exception:  # noqa: BLE001 - engine unreachable: not ready
+                    self._ready_val = False
+                self._ready_at = now
+            return self._ready_val
+
+        @ready.setter
+        def ready(self, v):  # (Model.__init__ assigns it)
+            self._ready_val = bool(v)
 
         async def __call__(self, payload, headers=None):
             return await asyncio.wrap_future(client.submit(self.name, "call", payload, headers))
@@ -234,6 +257,18 @@ class FrontendServer:
         listener.close()
         self.engine = _Engine(self.models, conns)
         self._wait_ready(start_timeout)
+
+    def wait(self) -> int:
+        """Block until ANY front-end process exits (watching only the first left a dead
+        second worker unnoticed while its share of connections failed); the others are stopped.
+        Returns that process's exit code."""
+        while True:
+            for p in self.procs:
+                rc = p.poll()
+                if rc is not None:
+                    log.error("front-end process %d exited with %s; stopping the server", p.pid, rc)
+                    return rc
+            time.sleep(0.5)
 
     def _kill(self):
         for p in self.procs:

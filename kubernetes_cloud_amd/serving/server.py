@@ -274,7 +274,7 @@ class ModelServer:
                 from .frontend import FrontendServer
                 fe = FrontendServer(list(self.models.values()), self.http_port, self.host)
                 try:
-                    fe.proc.wait()
+                    fe.wait()  # any front-end process dying ends the server (the pod restarts it)
                 finally:
                     fe.close()
             else:

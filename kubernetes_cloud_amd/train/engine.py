@@ -75,6 +75,10 @@ _FLUSH_TORCH = __import__("os").environ.get("KCA_FLUSH_TORCH", "0") == "1"  # di
 # large bf16 gradients of the first micro-batch are kept until the second one's arrive and both go
 # into the fp32 buffer in one pass (kca_accum_grad_pair); KCA_PAIR_ACCUM=0 accumulates each at once
 _PAIR_ACCUM = __import__("os").environ.get("KCA_PAIR_ACCUM", "1") not in ("0", "false")
+# the stash holds micro-batch 0's bf16 gradients until micro-batch 1 (2 bytes per stashed parameter): capped
+# so a large model keeps the rest on the one-pass path (GPT-J: 12 GB fits; a NeoX-20B ZeRO-1 run would
+# otherwise stash ~40 GB) -- KCA_PAIR_ACCUM_MAX_GB
+_PAIR_ACCUM_MAX_BYTES = int(float(__import__("os").environ.get("KCA_PAIR_ACCUM_MAX_GB", "16")) * (1 << 30))
 
 
 @dataclasses.dataclass
@@ -363,6 +367,7 @@ class TrainEngine:
         self._pend = []           # small-gradient accumulations awaiting one batched launch
         self._pend_ids = set()    # their parameters (one entry per parameter per launch)
         self._stash = {}          # id(param) -> (dst, micro-batch-0 bf16 grad, scale): see _accum
+        self._stash_bytes = 0     # bf16 bytes the stash holds (capped: _PAIR_ACCUM_MAX_BYTES)
         self._pre_reduce, self._pre_step = [], []
         self._norm_group, self._replicated, self._rep_ranges = None, {}, []
         self._hooks = [s.param.register_post_accumulate_grad_hook(self._hook) for s in slots]
@@ -496,9 +501,19 @@ class TrainEngine:
         if g.dim() == 4 and _is_cl(p):  # flat slot holds the NHWC order
             g = g.permute(0, 2, 3, 1)
             g = g.reshape(-1) if g.is_contiguous() else g.contiguous().reshape(-1)
-        if ((self.native and g.dtype == torch.bfloat16 or _DEFER_CPU) and g.is_contiguous()
-                and s.numel <= _SMALL_GRAD and _MULTI_ACCUM
-                and not (g.is_cuda and torch.cuda.is_current_stream_capturing())):
+        small = ((self.native and g.dtype == torch.bfloat16 or _DEFER_CPU) and g.is_contiguous()
+                 and s.numel <= _SMALL_GRAD and _MULTI_ACCUM
+                 and not (g.is_cuda and torch.cuda.is_current_stream_capturing()))
+        stashed = self._stash.get(id(p))
+        if stashed is not None and (small or not (self.native and g.dtype == torch.bfloat16 and g.is_contiguous())
+                                    or stashed[1].numel() != s.numel):
+            # micro-batch 0's stashed gradient meets a micro-batch-1 gradient the pair kernel cannot take
+            # (another branch below): land it first, so this one accumulates onto it (it used to
+            # be overwritten by a later _land_stash)
+            self._land(self._stash.pop(id(p)))
+            self._stash_bytes -= stashed[1].numel() * 2
+            first = False
+        if small:
             # small gradients are batched into one kca_accum_grad_multi launch (flushed before any
             # bucket collective and at the end of backward); the entry keeps g alive until then
             # a parameter fed twice in one backward (a block applied twice: two sink calls) must not
@@ -511,6 +526,8 @@ class TrainEngine:
                 self._flush_small()
         elif self.native and g.dtype == torch.bfloat16 and g.is_contiguous():
             st = self._stash.pop(id(p), None)
+            if st is not None:
+                self._stash_bytes -= st[1].numel() * 2
             if st is not None and st[1].numel() == s.numel:
                 # micro-batch 1: both micro-batches' gradients into the buffer in one pass (8 instead of
                 # 14 bytes per element; micro-batch 0 wrote nothing) -- bit-identical to the two passes
@@ -521,8 +538,10 @@ class TrainEngine:
                     self._land(st)
                     first = False
                 if (_PAIR_ACCUM and first and first_micro and self._micro == 0 and self.grad_accum >= 2
-                        and not self.part_grads and not torch.cuda.is_current_stream_capturing()):
+                        and not self.part_grads and not torch.cuda.is_current_stream_capturing()
+                        and self._stash_bytes + 2 * s.numel <= _PAIR_ACCUM_MAX_BYTES):
                     self._stash[id(p)] = (dst, g.reshape(-1), scale, s.bucket)  # lands with micro-batch 1's
+                    self._stash_bytes += 2 * s.numel
                 else:
                     _lib.call("kca_accum_grad", dst.data_ptr(), g.data_ptr(), scale, int(first), s.numel,
                               _lib.stream())
@@ -582,7 +601,9 @@ class TrainEngine:
         before the optimizer; a bucket's before its collective reads the buffer): written as a first
         accumulation would have."""
         for k in [k for k, e in self._stash.items() if bucket is None or e[3] == bucket]:
-            self._land(self._stash.pop(k))
+            e = self._stash.pop(k)
+            self._stash_bytes -= e[1].numel() * 2
+            self._land(e)
 
     def _launch(self, bi: int):
         self._flush_small()

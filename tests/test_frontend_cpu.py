@@ -60,3 +60,27 @@ def test_frontend_process_routes_errors_and_concurrency():
     finally:
         fe.close()
     assert len(fe.procs) == 3 and all(p.poll() is not None for p in fe.procs)
+
+
+def test_frontend_readiness_follows_engine_model_and_dead_worker_ends_wait():
+    """the proxies report the engine-side model's readiness (not a constant True), and
+    FrontendServer.wait() returns when ANY front-end process dies."""
+    import time
+
+    port = _port()
+    m = Echo()
+    m.ready = False
+    fe = FrontendServer([m], port, workers=2)
+    try:
+        base = f"http://127.0.0.1:{port}"
+        assert httpx.get(f"{base}/v2/models/echo/ready").status_code != 200
+        m.ready = True
+        time.sleep(1.2)  # the proxy re-asks after its TTL
+        ok = [httpx.get(f"{base}/v2/models/echo/ready").status_code for _ in range(4)]
+        assert all(c == 200 for c in ok), ok
+        fe.procs[1].kill()
+        t0 = time.time()
+        rc = fe.wait()
+        assert rc is not None and time.time() - t0 < 10
+    finally:
+        fe.close()

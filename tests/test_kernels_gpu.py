@@ -867,3 +867,27 @@ def test_attention_w8_forward_matches_4wave_and_fp32(causal):
     assert _rel(outs[1], orf) < 1e-2, _rel(outs[1], orf)
     assert _rel(outs[1], outs[0]) < 5e-3, _rel(outs[1], outs[0])
 
+
+
+def test_pair_accum_stash_lands_before_another_branch():
+    """micro-batch 0's stashed gradient (paired accumulation, train/engine.py) must not be
+    lost when micro-batch 1's gradient for the same parameter arrives in a form the pair kernel does not
+    take (here non-contiguous: the torch fallback) -- the buffer holds (g0 + g1) / 2."""
+    from kubernetes_cloud_amd.train.engine import TrainEngine
+    lin = torch.nn.Linear(1024, 1024, bias=False).to(DEV, torch.bfloat16)  # 1 Mi elements: not the small path
+    eng = TrainEngine(lin, grad_accum=2)
+    p = lin.weight
+    g0 = torch.randn(1024, 1024, device=DEV).bfloat16()
+    g1 = torch.randn(1024, 1024, device=DEV).bfloat16().t()  # non-contiguous
+    eng._micro = 0
+    eng._accum(p, g0)
+    assert id(p) in eng._stash
+    eng._micro = 1
+    eng._accum(p, g1)
+    eng._land_stash()
+    torch.cuda.synchronize()
+    s = eng._by_param[id(p)]
+    got = eng.grad[s.offset:s.offset + s.numel].view(1024, 1024)
+    ref = (g0.float() + g1.float()) / 2
+    assert _rel(got, ref) < 1e-6 and eng._stash_bytes == 0 and not eng._stash
+    eng.remove_hooks()
