@@ -358,9 +358,19 @@ __global__ __launch_bounds__(WV * 64) void mm_skinny_kernel(MmArgs a) {
     __syncthreads();
     fin = s_fin != 0;
     if (fin) {
-      // the other slices' tiles, UZ slices' loads in flight at a time (a serial chain of KS - 1 L2
-      // round trips sat on every block's critical path: profiles/mm_bench_r6_v4_nsplit_splitk.jsonl)
+      // every slice's tile summed in slice order 0..KS-1 (this slice's own from registers), whichever
+      // slice arrives last -- the result is deterministic (seeded sampling reproduces under replay);
+      // UZ slices' loads in flight at a time (a serial chain of KS - 1 L2 round trips sat on every
+      // block's critical path: profiles/mm_bench_r6_v4_nsplit_splitk.jsonl)
       constexpr int UZ = TPW >= 4 ? 2 : (TPW >= 2 ? 4 : 8);
+      f32x4 own[NRW][MT];
+#pragma unroll
+      for (int nr = 0; nr < NRW; ++nr)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          own[nr][mt] = acc[nr][mt];
+          acc[nr][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
       for (int z0 = 0; z0 < KS; z0 += UZ) {
         f32x4 part[UZ][NRW][MT];
 #pragma unroll
@@ -381,7 +391,7 @@ __global__ __launch_bounds__(WV * 64) void mm_skinny_kernel(MmArgs a) {
 #pragma unroll
           for (int nr = 0; nr < NRW; ++nr)
 #pragma unroll
-            for (int mt = 0; mt < MT; ++mt) acc[nr][mt] += part[u][nr][mt];
+            for (int mt = 0; mt < MT; ++mt) acc[nr][mt] += (z0 + u == kz) ? own[nr][mt] : part[u][nr][mt];
       }
     }
   }
