@@ -275,11 +275,13 @@ def _summary(rec) -> dict:
     for r in (dec or {}).get("records", []) if isinstance(dec, dict) else []:
         m = "gptj" if "gpt-j" in str(r.get("metric")) else "neox"
         s_ = "" if r.get("sampling") in (None, "greedy") else "_" + str(r["sampling"])
+        s_ += "_fp16" if r.get("dtype") == "fp16" else ""
         out[f"decode_{m}_b{r.get('batch')}{s_}_ms"] = r.get("decode_ms_per_token")
     bl = rec.get("secondary_bloom_tp8_rank")
     for r in (bl or {}).get("records", []) if isinstance(bl, dict) else []:
         if isinstance(r, dict) and "batch" in r:
-            out[f"bloom_tp8_rank_b{r['batch']}_ms"] = r.get("decode_ms_per_token")
+            f16 = "_fp16" if r.get("dtype") == "fp16" else ""
+            out[f"bloom_tp8_rank_b{r['batch']}{f16}_ms"] = r.get("decode_ms_per_token")
     wl = rec.get("secondary_weight_load")
     for r in (wl or {}).get("records", []) if isinstance(wl, dict) else []:
         if isinstance(r, dict) and "gbps" in r:
@@ -435,17 +437,29 @@ def _extras(args, dev, rec):
         out = db.run_decode("gpt-j-6b", batches=(1, 32), prompt_len=512, new_tokens=64,
                             sampling=("greedy", "ft_topk10"))
         torch.cuda.empty_cache()
-        return out + db.run_decode("gpt-neox-20b", batches=(1, 32), prompt_len=512, new_tokens=64,
-                                   sampling=("greedy", "ft_topk10"))
+        out += db.run_decode("gpt-neox-20b", batches=(1, 32), prompt_len=512, new_tokens=64,
+                             sampling=("greedy", "ft_topk10"))
+        torch.cuda.empty_cache()
+        # FT's data_type: fp16 (download-weights-job-gptj.yml:225-227): the native fp16 decode step
+        for model in ("gpt-j-6b", "gpt-neox-20b"):
+            out += db.run_decode(model, batches=(1, 32), prompt_len=512, new_tokens=64, sampling=("greedy",),
+                                 dtype="fp16")
+            torch.cuda.empty_cache()
+        return out
 
     def bloom_tp8_rank():
-        recs = _load_bench("bloom_tp_bench").run_tp_decode("bloom-176b", layers=0, batches=(1, 8, 32),
-                                                           prompt_len=128, new_tokens=32, emulate_tp=8)
+        tb = _load_bench("bloom_tp_bench")
+        recs = tb.run_tp_decode("bloom-176b", layers=0, batches=(1, 8, 32), prompt_len=128, new_tokens=32,
+                                emulate_tp=8)
+        torch.cuda.empty_cache()
+        # DS-Inference's fp16 (bloom-176b-deepspeed isvc-patch): the native fp16 step
+        recs += tb.run_tp_decode("bloom-176b", layers=0, batches=(1, 8, 32), prompt_len=128, new_tokens=32,
+                                 emulate_tp=8, dtype="fp16")
         return {"layout": "rank 0 of TP=8 on one GPU: all 70 layers at the per-rank shard shapes (QKV "
                           "14336->5376, out 1792->14336, fc_in 14336->7168, fc_out 7168->14336) + the "
-                          "31,360-row head shard; all-reduces / the logits all-gather are stand-ins "
-                          "(identity / local tile), their count and bytes reported per record; bf16 (fp16 "
-                          "checkpoints load as bf16: same bytes per weight)",
+                          "31,360-row head shard; the all-reduces run the deployment's fused tail kernels "
+                          "over a rank-local custom all-reduce (no peer traffic), the logits all-gather is a "
+                          "stand-in; bf16 and fp16 records",
                 "records": recs}
 
     def weight_load():

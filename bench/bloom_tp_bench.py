@@ -29,8 +29,8 @@ import torch.distributed as dist
 def run_tp_decode(model_name="bloom-176b", layers=0, batches=(1, 8, 32), prompt_len=128, new_tokens=64,
                   custom_ar=True, dtype="bf16", emulate_tp=0):
     """All ranks call this inside an initialised process group (or world 1). ``dtype`` "fp16" runs
-    the model in float16 as BASELINE config 4 states (the native decode kernels are bf16: fp16 takes
-    the eager PyTorch paths, for comparison only). ``emulate_tp`` N > 1 (one process, no process
+    the model in float16 as BASELINE config 4 / DS-Inference state (the native fp16 decode step: the
+    matrix-core layer at every batch, the all-reduce tails' fp16 instantiations). ``emulate_tp`` N > 1 (one process, no process
     group): rank 0's shard of a TP=N layout with stand-in collectives (parallel/tp_emulation.py) --
     the per-rank weight stream and kernel schedule of the real run, all-reduces priced separately.
     Returns the per-batch records on rank 0, None on followers."""
@@ -159,7 +159,7 @@ def main():
     ap.add_argument("--new-tokens", type=int, default=64)
     ap.add_argument("--no-custom-ar", action="store_true", help="TP all-reduces through RCCL only")
     ap.add_argument("--dtype", choices=["bf16", "fp16"], default="bf16",
-                    help="fp16: BASELINE config 4's dtype (eager PyTorch paths; the native kernels are bf16)")
+                    help="fp16: BASELINE config 4's dtype (native fp16 decode step)")
     ap.add_argument("--emulate-tp", type=int, default=0,
                     help="N > 1: rank 0 of a TP=N layout on this one GPU, stand-in collectives")
     ap.add_argument("--force-pg", action="store_true",

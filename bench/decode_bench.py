@@ -27,16 +27,18 @@ SAMPLING = {
 }
 
 
-def run_decode(model="gpt-j-6b", batches=(1, 32), prompt_len=512, new_tokens=64, sampling=("greedy",)):
+def run_decode(model="gpt-j-6b", batches=(1, 32), prompt_len=512, new_tokens=64, sampling=("greedy",),
+               dtype="bf16"):
     """bench.py's ``secondary_decode``: per batch size and sampling mode, prefill ms and pure
     decode ms/token (HIP graphs, all requests running) -- the FT GPT-J
-    serving row (request_output_len 64)."""
+    serving row (request_output_len 64). ``dtype`` "fp16": FT's ``data_type: fp16`` (the native
+    fp16 decode step: matrix-core layer at every batch)."""
     from kubernetes_cloud_amd.engine.llm_engine import LLMEngine, SamplingParams
     from kubernetes_cloud_amd.models.causal_lm import build_model
     from kubernetes_cloud_amd.models.config import preset
     dev = torch.device("cuda", torch.cuda.current_device())
     cfg = preset(model)
-    m = build_model(cfg, device=dev, dtype=torch.bfloat16, seed=0)
+    m = build_model(cfg, device=dev, dtype={"bf16": torch.bfloat16, "fp16": torch.float16}[dtype], seed=0)
     m.eval()
     eng = LLMEngine(m, max_slots=max(batches), max_len=prompt_len + new_tokens + 16)
     g = torch.Generator().manual_seed(0)
@@ -62,7 +64,7 @@ def run_decode(model="gpt-j-6b", batches=(1, 32), prompt_len=512, new_tokens=64,
         out.append({"metric": f"{model} decode", "batch": B, "sampling": mode, "prompt_len": prompt_len,
                     "new_tokens": new_tokens,
                     "prefill_ms_one_seq": round(prefill_ms, 2), "decode_ms_per_token": round(dt / max(n, 1) * 1e3, 3),
-                    "decode_tokens_per_s": round(B * n / dt, 1), "dtype": "bf16", "graphs": eng.runner.use_graphs,
+                    "decode_tokens_per_s": round(B * n / dt, 1), "dtype": dtype, "graphs": eng.runner.use_graphs,
                     "data": "random-init weights, random prompts"})
     del eng, m
     return out

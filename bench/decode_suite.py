@@ -32,19 +32,20 @@ def main():
     ap.add_argument("--batches", default="1,8,32")
     ap.add_argument("--sampling", default="greedy")
     ap.add_argument("--new-tokens", type=int, default=64)
+    ap.add_argument("--dtypes", default="bf16", help="comma list of bf16 / fp16")
     args = ap.parse_args()
     import torch
     batches = tuple(int(b) for b in args.batches.split(","))
     tag = {"batched_fused": os.environ.get("KCA_DECODE_FUSED_BATCHED", "1")}
-    for name in args.models.split(","):
+    for name, dt in ((n, d) for n in args.models.split(",") for d in args.dtypes.split(",")):
         if name in ("gptj", "neox"):
             model = {"gptj": "gpt-j-6b", "neox": "gpt-neox-20b"}[name]
             recs = _load("decode_bench").run_decode(model, batches=batches, prompt_len=512,
                                                     new_tokens=args.new_tokens,
-                                                    sampling=tuple(args.sampling.split(",")))
+                                                    sampling=tuple(args.sampling.split(",")), dtype=dt)
         elif name == "bloom8":
             recs = _load("bloom_tp_bench").run_tp_decode("bloom-176b", layers=0, batches=batches, prompt_len=128,
-                                                         new_tokens=32, emulate_tp=8)
+                                                         new_tokens=32, emulate_tp=8, dtype=dt)
         else:
             raise ValueError(name)
         for r in recs:

@@ -118,33 +118,43 @@ __device__ __forceinline__ void debug_delay(int delay) {
   for (int i = 0; i < delay; ++i) __builtin_amdgcn_s_sleep(127);
 }
 
-template <int W>
-__device__ __forceinline__ uint4 sum_peers(const ARPeers& peers, int par, long long i) {
-  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+// fp32 sums of 8 elements (one 16-byte chunk `i`) over the W stagings. DT: 0 bf16, 1 fp16 (common.h)
+template <int W, int DT>
+__device__ __forceinline__ void sum_peers8(const ARPeers& peers, int par, long long i, float (&acc)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
 #pragma unroll
   for (int r = 0; r < W; ++r) {
     const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(peers.stage[par][r]) + i);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      acc[2 * j] += __uint_as_float(v[j] << 16);
-      acc[2 * j + 1] += __uint_as_float(v[j] & 0xffff0000u);
+      acc[2 * j] += e2f<DT>(v[j] & 0xffffu);
+      acc[2 * j + 1] += e2f<DT>(v[j] >> 16);
     }
   }
+}
+
+template <int W, int DT>
+__device__ __forceinline__ uint4 sum_peers(const ARPeers& peers, int par, long long i) {
+  float acc[8];
+  sum_peers8<W, DT>(peers, par, i, acc);
   uint4 o;
-  o.x = pack_bf16x2(acc[0], acc[1]);
-  o.y = pack_bf16x2(acc[2], acc[3]);
-  o.z = pack_bf16x2(acc[4], acc[5]);
-  o.w = pack_bf16x2(acc[6], acc[7]);
+  o.x = f2e<DT>(acc[0]) | (f2e<DT>(acc[1]) << 16);
+  o.y = f2e<DT>(acc[2]) | (f2e<DT>(acc[3]) << 16);
+  o.z = f2e<DT>(acc[4]) | (f2e<DT>(acc[5]) << 16);
+  o.w = f2e<DT>(acc[6]) | (f2e<DT>(acc[7]) << 16);
   return o;
 }
 
-__device__ __forceinline__ uint4 nan_bf16x8() {
-  const uint32_t q = 0x7fc07fc0u;
+// 8 quiet NaNs of the element type: the poison a timed-out sync leaves in the output
+template <int DT>
+__device__ __forceinline__ uint4 nan8() {
+  const uint32_t q = DT == 0 ? 0x7fc07fc0u : 0x7e007e00u;
   return make_uint4(q, q, q, q);
 }
 
 // ---------------------------------------------------------------- one-shot
-template <int W>
+template <int W, int DT>
 __global__ __launch_bounds__(512) void ar_one_shot_kernel(ARPeers peers, ARCtl* ctl, int rank,
                                                           const bf16_t* __restrict__ in, bf16_t* __restrict__ out,
                                                           long long n8, long long spin_limit, int delay) {
@@ -158,7 +168,7 @@ __global__ __launch_bounds__(512) void ar_one_shot_kernel(ARPeers peers, ARCtl* 
   const bool ok = ar_sync<W>(peers, ctl, rank, 0, call, spin_limit);
   debug_delay(delay);
   for (long long i = lo + tid; i < hi; i += blockDim.x)
-    reinterpret_cast<uint4*>(out)[i] = ok ? sum_peers<W>(peers, par, i) : nan_bf16x8();
+    reinterpret_cast<uint4*>(out)[i] = ok ? sum_peers<W, DT>(peers, par, i) : nan8<DT>();
   ar_end(ctl, call);
 }
 
@@ -170,7 +180,7 @@ __global__ __launch_bounds__(512) void ar_one_shot_kernel(ARPeers peers, ARCtl* 
 //            writes the bf16 result in place into its OWN staging (no peer
 //            reads partition r of rank r's staging before phase B); sync
 //   gather : read sub-slice b of partition p from rank p's staging, all p.
-template <int W>
+template <int W, int DT>
 __global__ __launch_bounds__(512) void ar_two_shot_kernel(ARPeers peers, ARCtl* ctl, int rank,
                                                           const bf16_t* __restrict__ in, bf16_t* __restrict__ out,
                                                           long long n8, long long spin_limit, int delay) {
@@ -193,8 +203,8 @@ __global__ __launch_bounds__(512) void ar_two_shot_kernel(ARPeers peers, ARCtl* 
     const long long pend = min(n8, (long long)(rank + 1) * part);
     const long long lo = rank * part + b * sub, hi = min(pend, lo + sub);
     for (long long i = lo + tid; i < hi; i += blockDim.x) {
-      const uint4 v = sum_peers<W>(peers, par, i);
-      mine[i] = ok ? v : nan_bf16x8();
+      const uint4 v = sum_peers<W, DT>(peers, par, i);
+      mine[i] = ok ? v : nan8<DT>();
     }
   }
   ok = ar_sync<W>(peers, ctl, rank, 1, call, spin_limit) && ok;
@@ -206,7 +216,7 @@ __global__ __launch_bounds__(512) void ar_two_shot_kernel(ARPeers peers, ARCtl* 
     const u32x4* s = reinterpret_cast<const u32x4*>(peers.stage[par][p]);
     for (long long i = lo + tid; i < hi; i += blockDim.x) {
       const u32x4 v = __builtin_nontemporal_load(s + i);
-      dst[i] = ok ? make_uint4(v[0], v[1], v[2], v[3]) : nan_bf16x8();
+      dst[i] = ok ? make_uint4(v[0], v[1], v[2], v[3]) : nan8<DT>();
     }
   }
   ar_end(ctl, call);
@@ -217,7 +227,7 @@ __global__ __launch_bounds__(512) void ar_two_shot_kernel(ARPeers peers, ARCtl* 
 // LM head's logits): stage own input, one sync round, read every
 // peer's staging. Shares the call sequence (and its race argument) with the
 // all-reduce kernels above, so the two can be interleaved freely.
-template <int W>
+template <int W, int DT>
 __global__ __launch_bounds__(512) void ag_kernel(ARPeers peers, ARCtl* ctl, int rank,
                                                  const bf16_t* __restrict__ in, bf16_t* __restrict__ out,
                                                  long long n8, long long spin_limit, int delay) {
@@ -237,7 +247,7 @@ __global__ __launch_bounds__(512) void ag_kernel(ARPeers peers, ARCtl* ctl, int 
     const u32x4* s = reinterpret_cast<const u32x4*>(peers.stage[par][p]);
     for (long long i = lo + tid; i < hi; i += blockDim.x) {
       const u32x4 v = __builtin_nontemporal_load(s + i);
-      dst[p * n8 + i] = ok ? make_uint4(v[0], v[1], v[2], v[3]) : nan_bf16x8();
+      dst[p * n8 + i] = ok ? make_uint4(v[0], v[1], v[2], v[3]) : nan8<DT>();
     }
   }
   ar_end(ctl, call);
@@ -250,7 +260,7 @@ __global__ __launch_bounds__(512) void ag_kernel(ARPeers peers, ARCtl* ctl, int 
 // bias + residual, rounds h' and writes LN(h') for the next projection (dual_ln_arrive_tail). The
 // separate bias add and LayerNorm launches of a plain all-reduce disappear from every layer. 256
 // threads (the tail's shape); the call sequence / parity protocol is the one-shot kernel's.
-template <int W, int PER>
+template <int W, int PER, int DT = 0>
 __global__ __launch_bounds__(256) void ar_res_ln_kernel(ARPeers peers, ARCtl* ctl, int rank,
                                                         const bf16_t* __restrict__ in, long long n8,
                                                         long long spin_limit, DualLn a) {
@@ -263,26 +273,18 @@ __global__ __launch_bounds__(256) void ar_res_ln_kernel(ARPeers peers, ARCtl* ct
   for (long long i = lo + tid; i < hi; i += blockDim.x) mine[i] = reinterpret_cast<const uint4*>(in)[i];
   const bool ok = ar_sync<W>(peers, ctl, rank, 0, call, spin_limit);
   for (long long i = lo + tid; i < hi; i += blockDim.x) {
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-    for (int r = 0; r < W; ++r) {
-      const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(peers.stage[par][r]) + i);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        acc[2 * j] += __uint_as_float(v[j] << 16);
-        acc[2 * j + 1] += __uint_as_float(v[j] & 0xffff0000u);
-      }
-    }
+    float acc[8];
+    sum_peers8<W, DT>(peers, par, i, acc);
     // h' = bf16(h + y + bias) for these 8 columns, handed to the LayerNorm tail (NaN on a timed-out sync)
     float h8[8], b8[8];
-    load8(a.h + i * 8, h8);
-    if (a.bias) load8(a.bias + i * 8, b8);
+    load8_t<DT>(a.h + i * 8, h8);
+    if (a.bias) load8_t<DT>(a.bias + i * 8, b8);
 #pragma unroll
     for (int j = 0; j < 8; ++j) h8[j] = ok ? h8[j] + (acc[j] + (a.bias ? b8[j] : 0.f)) : __int_as_float(0x7fc00000);
-    st_pub_bf16x8(a.h_out + i * 8, h8);
+    st_pub_x8<DT>(a.h_out + i * 8, h8);
   }
   ar_end(ctl, call);
-  dual_ln_arrive_tail<PER>(a);
+  dual_ln_arrive_tail<PER, DT>(a);
 }
 
 // ----------------------------------------- one-shot + residual + row statistics (TP decode, M rows)
@@ -293,7 +295,7 @@ __global__ __launch_bounds__(256) void ar_res_ln_kernel(ARPeers peers, ARCtl* ct
 // publishes (mean, M2) of its rounded values, the last arriving workgroup merges them into the next
 // LayerNorm's per-row (mean, rstd), which the next projection applies to h_out on load. Block slices
 // are whole 64-column groups (N % 64 == 0).
-template <int W>
+template <int W, int DT>
 __global__ __launch_bounds__(256) void ar_res_stats_kernel(ARPeers peers, ARCtl* ctl, int rank,
                                                            const bf16_t* __restrict__ in, long long n8,
                                                            long long spin_limit, const bf16_t* __restrict__ bias,
@@ -309,27 +311,19 @@ __global__ __launch_bounds__(256) void ar_res_stats_kernel(ARPeers peers, ARCtl*
   const bool ok = ar_sync<W>(peers, ctl, rank, 0, call, spin_limit);
   const long long n8row = rs.N / 8;
   for (long long i = lo + tid; i < hi; i += blockDim.x) {  // (8-thread groups stay whole: lo, hi, 256 % 8)
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-    for (int r = 0; r < W; ++r) {
-      const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(peers.stage[par][r]) + i);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        acc[2 * j] += __uint_as_float(v[j] << 16);
-        acc[2 * j + 1] += __uint_as_float(v[j] & 0xffff0000u);
-      }
-    }
+    float acc[8];
+    sum_peers8<W, DT>(peers, par, i, acc);
     const long long row = i / n8row, col = (i % n8row) * 8;
     float h8[8], b8[8];
-    load8(h + i * 8, h8);
-    if (bias) load8(bias + col, b8);
+    load8_t<DT>(h + i * 8, h8);
+    if (bias) load8_t<DT>(bias + col, b8);
     float v[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       v[j] = ok ? h8[j] + (acc[j] + (bias ? b8[j] : 0.f)) : __int_as_float(0x7fc00000);
-      v[j] = bf2f(f2bf(v[j]));  // statistics over the rounded stream (ln_rows' convention)
+      v[j] = e2f<DT>(f2e<DT>(v[j]));  // statistics over the rounded stream (ln_rows' convention)
     }
-    store8(h_out + i * 8, v);
+    store8_t<DT>(h_out + i * 8, v);
     float sm = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) sm += v[j];
@@ -384,9 +378,10 @@ KCA_API int kca_ipc_close(void* ptr) { return hipIpcCloseMemHandle(ptr) == hipSu
 // algo 0 = one-shot, 1 = two-shot all-reduce (in/out: n elements); algo 2 =
 // all-gather (in: n elements, out: world*n). `n` bf16 elements, multiple of 8,
 // and n*2 must fit the staging buffers (checked by the Python wrapper).
-KCA_API int kca_ar_run(void* const* stage0, void* const* stage1, void* const* sig, void* ctl, int rank, int world,
-                       int algo, const void* in, void* out, long long n, int blocks, long long spin_limit, int delay,
-                       hipStream_t stream) {
+template <int DT>
+static int ar_run(void* const* stage0, void* const* stage1, void* const* sig, void* ctl, int rank, int world,
+                  int algo, const void* in, void* out, long long n, int blocks, long long spin_limit, int delay,
+                  hipStream_t stream) {
   if (world < 1 || world > AR_MAX_RANKS || rank < 0 || rank >= world || n % 8 || n <= 0 || blocks < 1 ||
       blocks > AR_MAX_BLOCKS || algo < 0 || algo > 2)
     return 1;
@@ -403,13 +398,13 @@ KCA_API int kca_ar_run(void* const* stage0, void* const* stage1, void* const* si
 #define KCA_AR_CASE(WW)                                                                                        \
   case WW:                                                                                                     \
     if (algo == 0)                                                                                             \
-      hipLaunchKernelGGL(ar_one_shot_kernel<WW>, dim3(blocks), dim3(512), 0, stream, p, c, rank,               \
+      hipLaunchKernelGGL((ar_one_shot_kernel<WW, DT>), dim3(blocks), dim3(512), 0, stream, p, c, rank,               \
                          (const bf16_t*)in, (bf16_t*)out, n8, spin_limit, delay);                              \
     else if (algo == 2)                                                                                        \
-      hipLaunchKernelGGL(ag_kernel<WW>, dim3(blocks), dim3(512), 0, stream, p, c, rank, (const bf16_t*)in,     \
+      hipLaunchKernelGGL((ag_kernel<WW, DT>), dim3(blocks), dim3(512), 0, stream, p, c, rank, (const bf16_t*)in,     \
                          (bf16_t*)out, n8, spin_limit, delay);                                                 \
     else                                                                                                       \
-      hipLaunchKernelGGL(ar_two_shot_kernel<WW>, dim3(blocks), dim3(512), 0, stream, p, c, rank,               \
+      hipLaunchKernelGGL((ar_two_shot_kernel<WW, DT>), dim3(blocks), dim3(512), 0, stream, p, c, rank,               \
                          (const bf16_t*)in, (bf16_t*)out, n8, spin_limit, delay);                              \
     break;
     KCA_AR_CASE(1) KCA_AR_CASE(2) KCA_AR_CASE(3) KCA_AR_CASE(4) KCA_AR_CASE(5) KCA_AR_CASE(6)
@@ -419,6 +414,19 @@ KCA_API int kca_ar_run(void* const* stage0, void* const* stage1, void* const* si
       return 3;
   }
   return hipGetLastError() == hipSuccess ? 0 : 4;
+}
+
+KCA_API int kca_ar_run(void* const* stage0, void* const* stage1, void* const* sig, void* ctl, int rank, int world,
+                       int algo, const void* in, void* out, long long n, int blocks, long long spin_limit, int delay,
+                       hipStream_t stream) {
+  return ar_run<0>(stage0, stage1, sig, ctl, rank, world, algo, in, out, n, blocks, spin_limit, delay, stream);
+}
+
+// fp16 elements (the sums; the all-gather copies bytes either way)
+KCA_API int kca_ar_run_f16(void* const* stage0, void* const* stage1, void* const* sig, void* ctl, int rank,
+                           int world, int algo, const void* in, void* out, long long n, int blocks,
+                           long long spin_limit, int delay, hipStream_t stream) {
+  return ar_run<1>(stage0, stage1, sig, ctl, rank, world, algo, in, out, n, blocks, spin_limit, delay, stream);
 }
 
 KCA_API int kca_ar_error(const void* ctl, int* err) {
@@ -432,11 +440,11 @@ KCA_API int kca_ar_error(const void* ctl, int* err) {
 // then h_out = bf16(h + sum + bias), xn_out = LN(h_out) (gamma / beta / eps; gamma2 -> xn2_out: a
 // second LayerNorm of the same h_out). ypart: >= N fp32 local words; cnt: 32 * 65 zero-initialised
 // arrival counters (re-armed by every call). N % 8 == 0, N <= 16384, 2N bytes <= the staging size.
-KCA_API int kca_ar_res_ln(void* const* stage0, void* const* stage1, void* const* sig, void* ctl, int rank, int world,
-                          const void* in, int N, int blocks, long long spin_limit, const void* bias, const void* h,
-                          void* h_out, const void* gamma, const void* beta, float eps, void* xn_out,
-                          const void* gamma2, const void* beta2, void* xn2_out, float* ypart, unsigned int* cnt,
-                          hipStream_t stream) {
+template <int DT>
+static int ar_res_ln(void* const* stage0, void* const* stage1, void* const* sig, void* ctl, int rank, int world,
+                     const void* in, int N, int blocks, long long spin_limit, const void* bias, const void* h,
+                     void* h_out, const void* gamma, const void* beta, float eps, void* xn_out, const void* gamma2,
+                     const void* beta2, void* xn2_out, float* ypart, unsigned int* cnt, hipStream_t stream) {
   if (world < 1 || world > AR_MAX_RANKS || rank < 0 || rank >= world || N % 8 || N <= 0 || N > 16384 || blocks < 1 ||
       blocks > AR_MAX_BLOCKS || !ypart || !cnt || !h || !h_out || !gamma || !xn_out || (xn2_out && !gamma2))
     return 1;
@@ -458,10 +466,10 @@ KCA_API int kca_ar_res_ln(void* const* stage0, void* const* stage1, void* const*
 #define KCA_AR_LN_CASE(WW)                                                                                      \
   case WW:                                                                                                      \
     if (N <= 8192)                                                                                              \
-      hipLaunchKernelGGL((ar_res_ln_kernel<WW, 4>), dim3(blocks), dim3(256), 0, stream, p, c, rank,             \
+      hipLaunchKernelGGL((ar_res_ln_kernel<WW, 4, DT>), dim3(blocks), dim3(256), 0, stream, p, c, rank,             \
                          (const bf16_t*)in, n8, spin_limit, a);                                                 \
     else                                                                                                        \
-      hipLaunchKernelGGL((ar_res_ln_kernel<WW, 8>), dim3(blocks), dim3(256), 0, stream, p, c, rank,             \
+      hipLaunchKernelGGL((ar_res_ln_kernel<WW, 8, DT>), dim3(blocks), dim3(256), 0, stream, p, c, rank,             \
                          (const bf16_t*)in, n8, spin_limit, a);                                                 \
     break;
     KCA_AR_LN_CASE(1) KCA_AR_LN_CASE(2) KCA_AR_LN_CASE(3) KCA_AR_LN_CASE(4) KCA_AR_LN_CASE(5) KCA_AR_LN_CASE(6)
@@ -473,14 +481,34 @@ KCA_API int kca_ar_res_ln(void* const* stage0, void* const* stage1, void* const*
   return hipGetLastError() == hipSuccess ? 0 : 4;
 }
 
+KCA_API int kca_ar_res_ln(void* const* stage0, void* const* stage1, void* const* sig, void* ctl, int rank, int world,
+                          const void* in, int N, int blocks, long long spin_limit, const void* bias, const void* h,
+                          void* h_out, const void* gamma, const void* beta, float eps, void* xn_out,
+                          const void* gamma2, const void* beta2, void* xn2_out, float* ypart, unsigned int* cnt,
+                          hipStream_t stream) {
+  return ar_res_ln<0>(stage0, stage1, sig, ctl, rank, world, in, N, blocks, spin_limit, bias, h, h_out, gamma, beta,
+                      eps, xn_out, gamma2, beta2, xn2_out, ypart, cnt, stream);
+}
+
+// fp16 twin (same arguments)
+KCA_API int kca_ar_res_ln_f16(void* const* stage0, void* const* stage1, void* const* sig, void* ctl, int rank,
+                              int world, const void* in, int N, int blocks, long long spin_limit, const void* bias,
+                              const void* h, void* h_out, const void* gamma, const void* beta, float eps,
+                              void* xn_out, const void* gamma2, const void* beta2, void* xn2_out, float* ypart,
+                              unsigned int* cnt, hipStream_t stream) {
+  return ar_res_ln<1>(stage0, stage1, sig, ctl, rank, world, in, N, blocks, spin_limit, bias, h, h_out, gamma, beta,
+                      eps, xn_out, gamma2, beta2, xn2_out, ypart, cnt, stream);
+}
+
 // Row-parallel projection close for batch 2..64 decode: all-reduce `in` (bf16 [M, N], this rank's
 // partial), h_out = bf16(h + sum + bias) (h_out may alias h), and the row statistics of h_out for the
 // next LayerNorm (stats [M][2] = (mean, rstd) with eps) through part ([M][N/64][2] fp32) and cnt
 // (32 * 65 zero-initialised counters, re-armed by every call). N % 64 == 0, N <= 16384, M <= 64.
-KCA_API int kca_ar_res_stats(void* const* stage0, void* const* stage1, void* const* sig, void* ctl, int rank,
-                             int world, const void* in, int M, int N, int blocks, long long spin_limit,
-                             const void* bias, const void* h, void* h_out, float eps, float* part, float* stats,
-                             unsigned int* cnt, hipStream_t stream) {
+template <int DT>
+static int ar_res_stats(void* const* stage0, void* const* stage1, void* const* sig, void* ctl, int rank,
+                        int world, const void* in, int M, int N, int blocks, long long spin_limit,
+                        const void* bias, const void* h, void* h_out, float eps, float* part, float* stats,
+                        unsigned int* cnt, hipStream_t stream) {
   if (world < 1 || world > AR_MAX_RANKS || rank < 0 || rank >= world || N % 64 || N <= 0 || N > 16384 || M < 1 ||
       M > 64 || blocks < 1 || blocks > AR_MAX_BLOCKS || !part || !stats || !cnt || !h || !h_out)
     return 1;
@@ -498,7 +526,7 @@ KCA_API int kca_ar_res_stats(void* const* stage0, void* const* stage1, void* con
   switch (world) {
 #define KCA_AR_ST_CASE(WW)                                                                                      \
   case WW:                                                                                                      \
-    hipLaunchKernelGGL((ar_res_stats_kernel<WW>), dim3(blocks), dim3(256), 0, stream, p, c, rank,               \
+    hipLaunchKernelGGL((ar_res_stats_kernel<WW, DT>), dim3(blocks), dim3(256), 0, stream, p, c, rank,               \
                        (const bf16_t*)in, n8, spin_limit, (const bf16_t*)bias, (const bf16_t*)h, (bf16_t*)h_out, \
                        rs);                                                                                     \
     break;
@@ -509,4 +537,21 @@ KCA_API int kca_ar_res_stats(void* const* stage0, void* const* stage1, void* con
       return 3;
   }
   return hipGetLastError() == hipSuccess ? 0 : 4;
+}
+
+KCA_API int kca_ar_res_stats(void* const* stage0, void* const* stage1, void* const* sig, void* ctl, int rank,
+                             int world, const void* in, int M, int N, int blocks, long long spin_limit,
+                             const void* bias, const void* h, void* h_out, float eps, float* part, float* stats,
+                             unsigned int* cnt, hipStream_t stream) {
+  return ar_res_stats<0>(stage0, stage1, sig, ctl, rank, world, in, M, N, blocks, spin_limit, bias, h, h_out, eps,
+                         part, stats, cnt, stream);
+}
+
+// fp16 twin: the fp16 serving layer's row-parallel close (same arguments, fp16 tensors)
+KCA_API int kca_ar_res_stats_f16(void* const* stage0, void* const* stage1, void* const* sig, void* ctl, int rank,
+                                 int world, const void* in, int M, int N, int blocks, long long spin_limit,
+                                 const void* bias, const void* h, void* h_out, float eps, float* part,
+                                 float* stats, unsigned int* cnt, hipStream_t stream) {
+  return ar_res_stats<1>(stage0, stage1, sig, ctl, rank, world, in, M, N, blocks, spin_limit, bias, h, h_out, eps,
+                         part, stats, cnt, stream);
 }

@@ -84,6 +84,56 @@ __device__ __forceinline__ void store8f(float* p, const float (&x)[8]) {
   *reinterpret_cast<float4*>(p + 4) = make_float4(x[4], x[5], x[6], x[7]);
 }
 
+// Element type of the 16-bit serving kernels: DT 0 = bf16, 1 = fp16 (FasterTransformer / DS-Inference
+// serve fp16). DT 0 is exactly bf2f / f2bf.
+template <int DT>
+__device__ __forceinline__ float e2f(uint32_t u16) {
+  if constexpr (DT == 0) return __uint_as_float(u16 << 16);
+  else return (float)__builtin_bit_cast(_Float16, (uint16_t)u16);
+}
+template <int DT>
+__device__ __forceinline__ uint32_t f2e(float f) {
+  if constexpr (DT == 0) return (uint32_t)f2bf(f);
+  else return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)f);
+}
+template <int DT>
+__device__ __forceinline__ void load8_t(const uint16_t* p, float (&x)[8]) {
+  U16x8 u = *reinterpret_cast<const U16x8*>(p);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) x[i] = e2f<DT>(u.v[i]);
+}
+template <int DT>
+__device__ __forceinline__ void store8_t(uint16_t* p, const float (&x)[8]) {
+  U16x8 u;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) u.v[i] = (uint16_t)f2e<DT>(x[i]);
+  *reinterpret_cast<U16x8*>(p) = u;
+}
+
+// The two elements of a packed 32-bit pair (low / high half), and acc + w.lo * x.lo + w.hi * x.hi of
+// two pairs -- the GEMV inner step. bf16: a shift / mask per element and two FMAs (the original
+// expressions); fp16: one v_dot2_f32_f16 (fp32 accumulation).
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+template <int DT>
+__device__ __forceinline__ float lo2f(uint32_t q) {
+  if constexpr (DT == 0) return __uint_as_float(q << 16);
+  else return (float)__builtin_bit_cast(_Float16, (uint16_t)(q & 0xffffu));
+}
+template <int DT>
+__device__ __forceinline__ float hi2f(uint32_t q) {
+  if constexpr (DT == 0) return __uint_as_float(q & 0xffff0000u);
+  else return (float)__builtin_bit_cast(_Float16, (uint16_t)(q >> 16));
+}
+template <int DT>
+__device__ __forceinline__ float dot2_acc(uint32_t w, uint32_t x, float acc) {
+  if constexpr (DT == 0) {
+    acc = fmaf(lo2f<0>(w), lo2f<0>(x), acc);
+    return fmaf(hi2f<0>(w), hi2f<0>(x), acc);
+  } else {
+    return __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2, w), __builtin_bit_cast(f16x2, x), acc, false);
+  }
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -153,7 +153,8 @@ struct DecodeParams {
   int by_row;
 };
 
-__device__ __forceinline__ void store_out(const DecodeParams& p, long long i, float v) { p.out[i] = f2bf(v); }
+template <int DT = 0>
+__device__ __forceinline__ void store_out(const DecodeParams& p, long long i, float v) { p.out[i] = (bf16_t)f2e<DT>(v); }
 
 
 // diagnostic stamps (bench/decode_attn_bench.py --stamps): 8 per workgroup, 100 MHz clock
@@ -172,6 +173,7 @@ KCA_API int kca_decode_set_stamps(void* buf) {
 // RoPE of the 8 dims [d0, d0+8) of a head row at position `pos`, matching
 // decode_prep_kernel (partner values read from the unrotated row; the result is
 // rounded to bf16 as the stored rotation would be).
+template <int DT = 0>
 __device__ __forceinline__ void rope8(const bf16_t* __restrict__ row, int d0, float (&x)[8], int pos, int rot,
                                       int interleaved, const float* __restrict__ cos_t,
                                       const float* __restrict__ sin_t) {
@@ -192,7 +194,7 @@ __device__ __forceinline__ void rope8(const bf16_t* __restrict__ row, int d0, fl
       sgn = d < half ? -1.f : 1.f;
     }
     const float c = cos_t[(long long)pos * half + fi], sn = sin_t[(long long)pos * half + fi];
-    x[j] = bf2f(f2bf(x[j] * c + sgn * bf2f(row[partner]) * sn));
+    x[j] = e2f<DT>(f2e<DT>(x[j] * c + sgn * e2f<DT>(row[partner]) * sn));
   }
 }
 
@@ -214,6 +216,7 @@ __device__ __forceinline__ void rope_tab8(const float* __restrict__ cos_t, const
 
 // rope8 with the angles in registers (rope_tab8); interleaved pairs take the partner from the
 // lane's own raw values, rotate-half partners are read from the unrotated row as rope8 does.
+template <int DT = 0>
 __device__ __forceinline__ void rope8_reg(const bf16_t* __restrict__ row, int d0, float (&x)[8],
                                           const float (&raw)[8], const float (&c)[8], const float (&sn)[8],
                                           int rot, int interleaved) {
@@ -227,10 +230,10 @@ __device__ __forceinline__ void rope8_reg(const bf16_t* __restrict__ row, int d0
       pv = raw[j ^ 1];
       sgn = (d & 1) ? 1.f : -1.f;
     } else {
-      pv = bf2f(row[d < half ? d + half : d - half]);
+      pv = e2f<DT>(row[d < half ? d + half : d - half]);
       sgn = d < half ? -1.f : 1.f;
     }
-    x[j] = bf2f(f2bf(x[j] * c[j] + sgn * pv * sn[j]));
+    x[j] = e2f<DT>(f2e<DT>(x[j] * c[j] + sgn * pv * sn[j]));
   }
 }
 
@@ -258,7 +261,7 @@ __device__ __forceinline__ float group_sum(float v) {
 // workgroup that brings it to nsplit re-arms it, acquires (agent scope: drops this CU's stale
 // lines) and combines the G heads' splits -- what decode_combine_kernel does, minus a launch and
 // its dependency gap on the decode critical path (one per layer).
-template <int G>
+template <int G, int DT = 0>
 __device__ void fanin_combine(const DecodeParams& p, int b, int hk, int nsplit) {
   __shared__ float wsp[1024];
   __shared__ float red[8];
@@ -303,7 +306,7 @@ __device__ void fanin_combine(const DecodeParams& p, int b, int hk, int nsplit) 
         const float ov = o[(long long)s * D + tid];
         acc = wsp[s] > 0.f ? fmaf(wsp[s], ov, acc) : acc;
       }
-      store_out(p, b * p.o_bs + (hk * G + g) * (long long)D + tid, acc * inv);
+      store_out<DT>(p, b * p.o_bs + (hk * G + g) * (long long)D + tid, acc * inv);
     }
     __syncthreads();  // wsp / red reused by the next head
   }
@@ -313,7 +316,7 @@ __device__ void fanin_combine(const DecodeParams& p, int b, int hk, int nsplit) 
 // wave step; G query heads share each K/V row (GQA group).
 // (the workgroup's (split, kv-head, sequence) coordinates are arguments: decode_attn_kernel passes
 // its block index, the fused decode-layer kernel below a slice of its grid)
-template <int LPT, int G, bool PAGED, bool ONLINE, bool PF = false>
+template <int LPT, int G, bool PAGED, bool ONLINE, bool PF = false, int DT = 0>
 __device__ __forceinline__ void decode_attn_body(const DecodeParams& p, const int split, const int hk, const int b,
                                                  const int nsplit) {
   constexpr int TPW = 64 / LPT;
@@ -369,7 +372,7 @@ __device__ __forceinline__ void decode_attn_body(const DecodeParams& p, const in
       st_pub(&p.ws_ml[((bh0 + tid) * nsplit + split) * 2], -INFINITY);
       st_pub(&p.ws_ml[((bh0 + tid) * nsplit + split) * 2 + 1], 0.f);
     }
-    if (nsplit > 1 && p.cnt) fanin_combine<G>(p, b, hk, nsplit);
+    if (nsplit > 1 && p.cnt) fanin_combine<G, DT>(p, b, hk, nsplit);
     return;
   }
   DSTAMP(1);
@@ -383,14 +386,14 @@ __device__ __forceinline__ void decode_attn_body(const DecodeParams& p, const in
   for (int g = 0; g < G; ++g) {
     if (dact) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) q[g][j] = bf2f(qraw[g].v[j]);
+      for (int j = 0; j < 8; ++j) q[g][j] = e2f<DT>(qraw[g].v[j]);
       if (pre_rope) {
         float raw[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) raw[j] = q[g][j];
-        rope8_reg(p.q + b * p.q_bs + (long long)(hk * G + g) * D, dslot * 8, q[g], raw, rc, rs, p.rot, p.interleaved);
+        rope8_reg<DT>(p.q + b * p.q_bs + (long long)(hk * G + g) * D, dslot * 8, q[g], raw, rc, rs, p.rot, p.interleaved);
       } else if (p.fused && p.rot > 0) {
-        rope8(p.q + b * p.q_bs + (long long)(hk * G + g) * D, dslot * 8, q[g], pnew, p.rot, p.interleaved, p.cos_t,
+        rope8<DT>(p.q + b * p.q_bs + (long long)(hk * G + g) * D, dslot * 8, q[g], pnew, p.rot, p.interleaved, p.cos_t,
               p.sin_t);
       }
 #pragma unroll
@@ -431,22 +434,22 @@ __device__ __forceinline__ void decode_attn_body(const DecodeParams& p, const in
   if (own_new && tid < ND) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      kx[j] = bf2f(knraw.v[j]);
-      vx[j] = bf2f(vnraw.v[j]);
+      kx[j] = e2f<DT>(knraw.v[j]);
+      vx[j] = e2f<DT>(vnraw.v[j]);
     }
     if (pre_rope) {  // tid < ND <= LPT: this lane's dslot is tid, its angles are rc / rs
       float raw[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) raw[j] = kx[j];
-      rope8_reg(krow, tid * 8, kx, raw, rc, rs, p.rot, p.interleaved);
+      rope8_reg<DT>(krow, tid * 8, kx, raw, rc, rs, p.rot, p.interleaved);
     } else if (p.rot > 0) {
-      rope8(krow, tid * 8, kx, pnew, p.rot, p.interleaved, p.cos_t, p.sin_t);
+      rope8<DT>(krow, tid * 8, kx, pnew, p.rot, p.interleaved, p.cos_t, p.sin_t);
     }
     const long long o = toff(pnew) + hk * p.cs_head + tid * 8;  // toff: offset inside the sequence
-    store8(const_cast<bf16_t*>(p.kc) + (PAGED ? 0 : (long long)seq * p.cs_slot) + o, kx);
-    store8(const_cast<bf16_t*>(p.vc) + (PAGED ? 0 : (long long)seq * p.cs_slot) + o, vx);
+    store8_t<DT>(const_cast<bf16_t*>(p.kc) + (PAGED ? 0 : (long long)seq * p.cs_slot) + o, kx);
+    store8_t<DT>(const_cast<bf16_t*>(p.vc) + (PAGED ? 0 : (long long)seq * p.cs_slot) + o, vx);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) knraw.v[j] = f2bf(kx[j]);  // exact: the rotation is bf16-rounded
+    for (int j = 0; j < 8; ++j) knraw.v[j] = (uint16_t)f2e<DT>(kx[j]);  // exact: the rotation is bf16-rounded
   } else if (own_last && tid < ND) {
     const long long o = (PAGED ? 0 : (long long)seq * p.cs_slot) + toff(pnew) + hk * p.cs_head + tid * 8;
     knraw = *reinterpret_cast<const U16x8*>(p.kc + o);
@@ -516,7 +519,7 @@ __device__ __forceinline__ void decode_attn_body(const DecodeParams& p, const in
       for (int g = 0; g < G; ++g) {
         float d = 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) d = fmaf(q[g][j], bf2f(kr[u].v[j]), d);  // q == 0 on inactive lanes
+        for (int j = 0; j < 8; ++j) d = fmaf(q[g][j], e2f<DT>(kr[u].v[j]), d);  // q == 0 on inactive lanes
         d = group_sum<LPT>(d);
         sv[g][u] = t < ce ? d + slope[g] * (float)(t - (L - 1)) : -INFINITY;
       }
@@ -539,7 +542,7 @@ __device__ __forceinline__ void decode_attn_body(const DecodeParams& p, const in
       for (int j = 0; j < 8; ++j) {
         float a = acc[g][j] * cs;
 #pragma unroll
-        for (int u = 0; u < U; ++u) a = fmaf(pu[u], bf2f(vr[u].v[j]), a);
+        for (int u = 0; u < U; ++u) a = fmaf(pu[u], e2f<DT>(vr[u].v[j]), a);
         acc[g][j] = a;
       }
       m[g] = mn;
@@ -561,7 +564,7 @@ __device__ __forceinline__ void decode_attn_body(const DecodeParams& p, const in
       float sv = 0.f;
       if (dact) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) sv = fmaf(q[g][j], bf2f(knraw.v[j]), sv);
+        for (int j = 0; j < 8; ++j) sv = fmaf(q[g][j], e2f<DT>(knraw.v[j]), sv);
       }
       sv = group_sum<LPT>(sv);
       const float mn = fmaxf(m[g], sv);
@@ -569,7 +572,7 @@ __device__ __forceinline__ void decode_attn_body(const DecodeParams& p, const in
       l[g] = l[g] * cs + pv;
       if (dact) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[g][j] = fmaf(acc[g][j], cs, pv * bf2f(vnraw.v[j]));
+        for (int j = 0; j < 8; ++j) acc[g][j] = fmaf(acc[g][j], cs, pv * e2f<DT>(vnraw.v[j]));
       }
       m[g] = mn;
     }
@@ -621,7 +624,7 @@ __device__ __forceinline__ void decode_attn_body(const DecodeParams& p, const in
       O = fmaf(w, gacc[(r * G + g) * D + d], O);
     }
     if (nsplit == 1) {
-      store_out(p, b * p.o_bs + (long long)(hk * G + g) * D + d, Ls > 0.f ? O / Ls : 0.f);
+      store_out<DT>(p, b * p.o_bs + (long long)(hk * G + g) * D + d, Ls > 0.f ? O / Ls : 0.f);
     } else {
       st_pub(&p.ws_o[((bh0 + g) * nsplit + split) * D + d], O);
       if (d == 0) {
@@ -660,7 +663,7 @@ __device__ __forceinline__ void decode_attn_body(const DecodeParams& p, const in
 #pragma unroll
           for (int j = 0; j < 8; ++j) kr[u][j] = knew[dslot * 8 + j];
         } else {
-          load8(kb + toff(t), kr[u]);
+          load8_t<DT>(kb + toff(t), kr[u]);
         }
       } else {
 #pragma unroll
@@ -720,9 +723,9 @@ __device__ __forceinline__ void decode_attn_body(const DecodeParams& p, const in
           for (int j = 0; j < 8; ++j) vr[u][j] = vnew[dslot * 8 + j];
         } else if (t0 == tv0) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) vr[u][j] = bf2f(vpre[u].v[j]);
+          for (int j = 0; j < 8; ++j) vr[u][j] = e2f<DT>(vpre[u].v[j]);
         } else {
-          load8(vb + toff(t), vr[u]);
+          load8_t<DT>(vb + toff(t), vr[u]);
         }
       } else {
 #pragma unroll
@@ -757,7 +760,7 @@ __device__ __forceinline__ void decode_attn_body(const DecodeParams& p, const in
       const float s = red[(0 * G + g) * D + d] + red[(1 * G + g) * D + d] +
                       red[(2 * G + g) * D + d] + red[(3 * G + g) * D + d];
       if (nsplit == 1) {
-        store_out(p, b * p.o_bs + (long long)(hk * G + g) * D + d, lg[g] > 0.f ? s / lg[g] : 0.f);
+        store_out<DT>(p, b * p.o_bs + (long long)(hk * G + g) * D + d, lg[g] > 0.f ? s / lg[g] : 0.f);
       } else {
         st_pub(&p.ws_o[((bh0 + g) * nsplit + split) * D + d], s);
       }
@@ -768,13 +771,13 @@ __device__ __forceinline__ void decode_attn_body(const DecodeParams& p, const in
     }
   }
   }
-  if (nsplit > 1 && p.cnt) fanin_combine<G>(p, b, hk, nsplit);
+  if (nsplit > 1 && p.cnt) fanin_combine<G, DT>(p, b, hk, nsplit);
 }
 
-template <int LPT, int G, bool PAGED, bool ONLINE>
+template <int LPT, int G, bool PAGED, bool ONLINE, int DT = 0>
 __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeParams p) {
   // G == 1 only: the prefetched rows cost GQA groups a residency step (G = 2: 119 -> 135 VGPRs)
-  decode_attn_body<LPT, G, PAGED, ONLINE, ONLINE && G == 1>(p, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x);
+  decode_attn_body<LPT, G, PAGED, ONLINE, ONLINE && G == 1, DT>(p, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x);
 }
 
 // ---------------------------------------------------------------- fused decode layer (batch 1)
@@ -797,23 +800,23 @@ struct GemvM1 {
   int N, K, act;
 };
 
-template <int LPT, int G, bool PAGED, bool ONLINE>
+template <int LPT, int G, bool PAGED, bool ONLINE, int DT = 0>
 __global__ __launch_bounds__(256) void decode_attn_gemv_kernel(DecodeParams p, int nsplit, int n_attn, GemvM1 g) {
   constexpr int R = 4;
   __shared__ float part[4][R];
   const int bid = blockIdx.x;
   if (bid < n_attn) {
     const int split = bid % nsplit, rest = bid / nsplit;
-    decode_attn_body<LPT, G, PAGED, ONLINE>(p, split, rest % p.Hkv, rest / p.Hkv, nsplit);
+    decode_attn_body<LPT, G, PAGED, ONLINE, false, DT>(p, split, rest % p.Hkv, rest / p.Hkv, nsplit);
     DSTAMP(7);
     return;
   }
   DSTAMP(0);
   const int n0 = (bid - n_attn) * R;
   float acc[R] = {0.f, 0.f, 0.f, 0.f};
-  gemv_m1_accum<R>(g.x, g.w, g.N, g.K, n0, acc);
-  const float v = gemv_m1_finish<R>(acc, part, g.bias, n0, g.N, g.act);
-  if (threadIdx.x < R && n0 + threadIdx.x < g.N) g.y[n0 + threadIdx.x] = f2bf(v);
+  gemv_m1_accum<R, 0, DT>(g.x, g.w, g.N, g.K, n0, acc);
+  const float v = gemv_m1_finish<R, DT>(acc, part, g.bias, n0, g.N, g.act);
+  if (threadIdx.x < R && n0 + threadIdx.x < g.N) g.y[n0 + threadIdx.x] = (bf16_t)f2e<DT>(v);
   DSTAMP(7);
 }
 
@@ -822,7 +825,7 @@ __global__ __launch_bounds__(256) void decode_attn_gemv_kernel(DecodeParams p, i
 // counter) adds bias + residual, rounds h' to bf16 and normalises it for the next projection(s):
 // the out-projection / fc_out, the residual add and the next LayerNorm in one launch, no LayerNorm
 // launch of its own.
-template <int R, int PER>
+template <int R, int PER, int DT = 0>
 __global__ __launch_bounds__(256) void gemv_dual_ln_kernel(DualLn a) {
   __shared__ float part[4][R];
   const int tid = threadIdx.x;
@@ -839,22 +842,23 @@ __global__ __launch_bounds__(256) void gemv_dual_ln_kernel(DualLn a) {
     // 2 weight slabs in flight per lane (8 loads at 4 rows), not 16: 84 instead of 124 VGPRs, 5 instead
     // of 4 waves per SIMD -- BLOOM TP=8 B=1 9.36 -> 9.06 ms/token, GPT-J neutral
     // (profiles/decode_launch_structure_ab_r5.txt)
-    gemv_m1_accum<R, 2>(a.x1, a.w1, a.N, a.K1, n0, acc);
-    if (a.x2) gemv_m1_accum<R, 2>(a.x2, a.w2, a.N, a.K2, n0, acc);
-    const float v = gemv_m1_finish<R>(acc, part, nullptr, n0, a.N, 0);
+    gemv_m1_accum<R, 2, DT>(a.x1, a.w1, a.N, a.K1, n0, acc);
+    if (a.x2) gemv_m1_accum<R, 2, DT>(a.x2, a.w2, a.N, a.K2, n0, acc);
+    const float v = gemv_m1_finish<R, DT>(acc, part, nullptr, n0, a.N, 0);
     if (tid < R && n0 + tid < a.N) {  // this row's h' = bf16(h + y + bias), handed to the tail
       const int n = n0 + tid;
-      st_pub_bf16(a.h_out + n, bf2f(a.h[n]) + (v + (a.bias ? bf2f(a.bias[n]) : 0.f)));
+      st_pub_e<DT>(a.h_out + n, e2f<DT>(a.h[n]) + (v + (a.bias ? e2f<DT>(a.bias[n]) : 0.f)));
     }
     __syncthreads();  // part[] is rewritten by the next group
   }
-  dual_ln_arrive_tail<PER>(a);
+  dual_ln_arrive_tail<PER, DT>(a);
 }
 
 // One workgroup per (sequence, head): split maxima and weights in one
 // parallel pass into LDS, then every lane owns one output dim and sums the
 // splits with 8 independent loads in flight (the old per-split serial chain
 // of dependent L2 loads cost ~9 us per layer at B=1).
+template <int DT = 0>
 __global__ __launch_bounds__(256) void decode_combine_kernel(const float* __restrict__ ws_o,
                                                              const float* __restrict__ ws_ml,
                                                              bf16_t* __restrict__ out, long long o_bs,
@@ -896,7 +900,7 @@ __global__ __launch_bounds__(256) void decode_combine_kernel(const float* __rest
       const float ov = o[(long long)s * D + tid];
       acc = wsp[s] > 0.f ? fmaf(wsp[s], ov, acc) : acc;
     }
-    out[b * o_bs + (long long)h * D + tid] = f2bf(acc * inv);
+    out[b * o_bs + (long long)h * D + tid] = (bf16_t)f2e<DT>(acc * inv);
   }
 }
 
@@ -934,34 +938,34 @@ KCA_API long long kca_decode_ws_floats(int B, int H, int D, int max_kv, int chun
   return ns > 1 ? fanin_words(B, H) + (long long)B * H * ns * (D + 2) : 0;
 }
 
-template <int LPT, int G>
+template <int LPT, int G, int DT = 0>
 static void launch_decode(const DecodeParams& p, int B, int nsplit, hipStream_t stream) {
   constexpr int TPB = 4 * (64 / LPT), U = 4;
   const dim3 grid(nsplit, p.Hkv, B);
   if (p.chunk > TPB * U) {  // long splits: one pass with online softmax
     const size_t lds = (size_t)4 * G * (2 + p.D) * sizeof(float);
-    if (p.tbl) hipLaunchKernelGGL((decode_attn_kernel<LPT, G, true, true>), grid, dim3(256), lds, stream, p);
-    else hipLaunchKernelGGL((decode_attn_kernel<LPT, G, false, true>), grid, dim3(256), lds, stream, p);
+    if (p.tbl) hipLaunchKernelGGL((decode_attn_kernel<LPT, G, true, true, DT>), grid, dim3(256), lds, stream, p);
+    else hipLaunchKernelGGL((decode_attn_kernel<LPT, G, false, true, DT>), grid, dim3(256), lds, stream, p);
   } else {
     const size_t lds = (size_t)(G * p.chunk + 4 * G * p.D) * sizeof(float);
-    if (p.tbl) hipLaunchKernelGGL((decode_attn_kernel<LPT, G, true, false>), grid, dim3(256), lds, stream, p);
-    else hipLaunchKernelGGL((decode_attn_kernel<LPT, G, false, false>), grid, dim3(256), lds, stream, p);
+    if (p.tbl) hipLaunchKernelGGL((decode_attn_kernel<LPT, G, true, false, DT>), grid, dim3(256), lds, stream, p);
+    else hipLaunchKernelGGL((decode_attn_kernel<LPT, G, false, false, DT>), grid, dim3(256), lds, stream, p);
   }
 }
 
-template <int LPT>
+template <int LPT, int DT = 0>
 static int launch_decode_g(const DecodeParams& p, int G, int B, int nsplit, hipStream_t s) {
   switch (G) {
-    case 1: launch_decode<LPT, 1>(p, B, nsplit, s); return 0;
-    case 2: launch_decode<LPT, 2>(p, B, nsplit, s); return 0;
-    case 4: launch_decode<LPT, 4>(p, B, nsplit, s); return 0;
-    case 8: launch_decode<LPT, 8>(p, B, nsplit, s); return 0;
+    case 1: launch_decode<LPT, 1, DT>(p, B, nsplit, s); return 0;
+    case 2: launch_decode<LPT, 2, DT>(p, B, nsplit, s); return 0;
+    case 4: launch_decode<LPT, 4, DT>(p, B, nsplit, s); return 0;
+    case 8: launch_decode<LPT, 8, DT>(p, B, nsplit, s); return 0;
   }
   return 3;
 }
 
 static int decode_attn_launch(DecodeParams p, float* ws, long long ws_floats, int B, int max_kv, int chunk,
-                              hipStream_t stream);
+                              hipStream_t stream, int dt = 0);
 
 KCA_API int kca_decode_attn(const void* q, long long q_bs, const void* kc, const void* vc,
                             long long cs_slot, long long cs_head, long long cs_pos,
@@ -996,8 +1000,26 @@ KCA_API int kca_decode_prep_attn(const void* qkv, long long ld, const void* kc, 
   return decode_attn_launch(p, ws, ws_floats, B, max_kv, chunk, stream);
 }
 
+// kca_decode_prep_attn on fp16 rows / caches (the precision FT and DS-Inference serve, BASELINE
+// config 4): the same kernels instantiated with fp16 loads, RoPE rounding and stores.
+KCA_API int kca_decode_prep_attn_f16(const void* qkv, long long ld, const void* kc, const void* vc,
+                                     long long cs_slot, long long cs_head, long long cs_pos,
+                                     const int* slots, const int* kv_lens, void* out, long long o_bs,
+                                     float* ws, long long ws_floats, int B, int H, int Hkv, int D,
+                                     int max_kv, int chunk, float scale, const float* alibi, const int* tbl,
+                                     int tbl_stride, int ps_shift, int rot, int interleaved, const float* cos_t,
+                                     const float* sin_t, int window, int by_row, hipStream_t stream) {
+  if (rot > D || (rot & 1) || (rot > 0 && (!cos_t || !sin_t))) return 8;
+  if (window < 0) return 9;
+  DecodeParams p{(const bf16_t*)qkv, ld, (const bf16_t*)kc, (const bf16_t*)vc, cs_slot, cs_head,
+                 cs_pos, slots, kv_lens, (bf16_t*)out, o_bs, nullptr, nullptr, alibi, tbl, tbl_stride, ps_shift,
+                 H, Hkv, D, chunk, scale, 1, rot, interleaved, cos_t, sin_t, g_decode_stamps, nullptr, window};
+  p.by_row = by_row;
+  return decode_attn_launch(p, ws, ws_floats, B, max_kv, chunk, stream, 1);
+}
+
 static int decode_attn_launch(DecodeParams p, float* ws, long long ws_floats, int B, int max_kv, int chunk,
-                              hipStream_t stream) {
+                              hipStream_t stream, int dt) {
   const int H = p.H, Hkv = p.Hkv, D = p.D;
   const int* tbl = p.tbl;
   const int ps_shift = p.ps_shift, tbl_stride = p.tbl_stride;
@@ -1019,13 +1041,24 @@ static int decode_attn_launch(DecodeParams p, float* ws, long long ws_floats, in
   }
   const int nd = D / 8;
   int rc;
-  if (nd <= 8) rc = launch_decode_g<8>(p, G, B, nsplit, stream);
-  else if (nd <= 16) rc = launch_decode_g<16>(p, G, B, nsplit, stream);
-  else rc = launch_decode_g<32>(p, G, B, nsplit, stream);
+  if (dt == 1) {
+    if (nd <= 8) rc = launch_decode_g<8, 1>(p, G, B, nsplit, stream);
+    else if (nd <= 16) rc = launch_decode_g<16, 1>(p, G, B, nsplit, stream);
+    else rc = launch_decode_g<32, 1>(p, G, B, nsplit, stream);
+  } else {
+    if (nd <= 8) rc = launch_decode_g<8>(p, G, B, nsplit, stream);
+    else if (nd <= 16) rc = launch_decode_g<16>(p, G, B, nsplit, stream);
+    else rc = launch_decode_g<32>(p, G, B, nsplit, stream);
+  }
   if (rc) return rc;
-  if (nsplit > 1 && !p.cnt)
-    hipLaunchKernelGGL(decode_combine_kernel, dim3(B * H), dim3(256), 0, stream, p.ws_o, p.ws_ml,
-                       p.out, p.o_bs, H, D, nsplit);
+  if (nsplit > 1 && !p.cnt) {
+    if (dt == 1)
+      hipLaunchKernelGGL((decode_combine_kernel<1>), dim3(B * H), dim3(256), 0, stream, p.ws_o, p.ws_ml, p.out,
+                         p.o_bs, H, D, nsplit);
+    else
+      hipLaunchKernelGGL((decode_combine_kernel<0>), dim3(B * H), dim3(256), 0, stream, p.ws_o, p.ws_ml, p.out,
+                         p.o_bs, H, D, nsplit);
+  }
   return 0;
 }
 
@@ -1033,15 +1066,14 @@ static int decode_attn_launch(DecodeParams p, float* ws, long long ws_floats, in
 // arguments plus the fc_in GEMV (gx [gK] -> gy [gN], bias, act). Returns 10 when the shape is
 // outside the instantiated fused variants (G == 1, head_dim 128 / 256, split-K fan-in or one
 // split): the caller then runs the two-stream path.
-KCA_API int kca_decode_prep_attn_gemv(const void* qkv, long long ld, const void* kc, const void* vc,
-                                      long long cs_slot, long long cs_head, long long cs_pos,
-                                      const int* slots, const int* kv_lens, void* out, long long o_bs,
-                                      float* ws, long long ws_floats, int B, int H, int Hkv, int D,
-                                      int max_kv, int chunk, float scale, const float* alibi, const int* tbl,
-                                      int tbl_stride, int ps_shift, int rot, int interleaved, const float* cos_t,
-                                      const float* sin_t, int window, const void* gx, const void* gw,
-                                      const void* gbias, void* gy, int gN, int gK, int gact, int by_row,
-                                      hipStream_t stream) {
+template <int DT>
+static int prep_attn_gemv(const void* qkv, long long ld, const void* kc, const void* vc, long long cs_slot,
+                          long long cs_head, long long cs_pos, const int* slots, const int* kv_lens, void* out,
+                          long long o_bs, float* ws, long long ws_floats, int B, int H, int Hkv, int D, int max_kv,
+                          int chunk, float scale, const float* alibi, const int* tbl, int tbl_stride, int ps_shift,
+                          int rot, int interleaved, const float* cos_t, const float* sin_t, int window,
+                          const void* gx, const void* gw, const void* gbias, void* gy, int gN, int gK, int gact,
+                          int by_row, hipStream_t stream) {
   if (rot > D || (rot & 1) || (rot > 0 && (!cos_t || !sin_t))) return 8;
   if (window < 0) return 9;
   if (B != 1 || H != Hkv || D % 8 || D > 256 || max_kv <= 0 || gK % 8 || gN <= 0) return 10;
@@ -1075,17 +1107,46 @@ KCA_API int kca_decode_prep_attn_gemv(const void* qkv, long long ld, const void*
     constexpr int TPB = 4 * (64 / LPT), U = 4;
     if (p.chunk > TPB * U) {
       const size_t lds = (size_t)4 * (2 + p.D) * sizeof(float);
-      if (p.tbl) hipLaunchKernelGGL((decode_attn_gemv_kernel<LPT, 1, true, true>), grid, dim3(256), lds, stream, p, nsplit, n_attn, g);
-      else hipLaunchKernelGGL((decode_attn_gemv_kernel<LPT, 1, false, true>), grid, dim3(256), lds, stream, p, nsplit, n_attn, g);
+      if (p.tbl) hipLaunchKernelGGL((decode_attn_gemv_kernel<LPT, 1, true, true, DT>), grid, dim3(256), lds, stream, p, nsplit, n_attn, g);
+      else hipLaunchKernelGGL((decode_attn_gemv_kernel<LPT, 1, false, true, DT>), grid, dim3(256), lds, stream, p, nsplit, n_attn, g);
     } else {
       const size_t lds = (size_t)(p.chunk + 4 * p.D) * sizeof(float);
-      if (p.tbl) hipLaunchKernelGGL((decode_attn_gemv_kernel<LPT, 1, true, false>), grid, dim3(256), lds, stream, p, nsplit, n_attn, g);
-      else hipLaunchKernelGGL((decode_attn_gemv_kernel<LPT, 1, false, false>), grid, dim3(256), lds, stream, p, nsplit, n_attn, g);
+      if (p.tbl) hipLaunchKernelGGL((decode_attn_gemv_kernel<LPT, 1, true, false, DT>), grid, dim3(256), lds, stream, p, nsplit, n_attn, g);
+      else hipLaunchKernelGGL((decode_attn_gemv_kernel<LPT, 1, false, false, DT>), grid, dim3(256), lds, stream, p, nsplit, n_attn, g);
     }
   };
   if (nd <= 16) go(std::integral_constant<int, 16>{});
   else go(std::integral_constant<int, 32>{});
   return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+KCA_API int kca_decode_prep_attn_gemv(const void* qkv, long long ld, const void* kc, const void* vc,
+                                      long long cs_slot, long long cs_head, long long cs_pos,
+                                      const int* slots, const int* kv_lens, void* out, long long o_bs,
+                                      float* ws, long long ws_floats, int B, int H, int Hkv, int D,
+                                      int max_kv, int chunk, float scale, const float* alibi, const int* tbl,
+                                      int tbl_stride, int ps_shift, int rot, int interleaved, const float* cos_t,
+                                      const float* sin_t, int window, const void* gx, const void* gw,
+                                      const void* gbias, void* gy, int gN, int gK, int gact, int by_row,
+                                      hipStream_t stream) {
+  return prep_attn_gemv<0>(qkv, ld, kc, vc, cs_slot, cs_head, cs_pos, slots, kv_lens, out, o_bs, ws, ws_floats, B,
+                           H, Hkv, D, max_kv, chunk, scale, alibi, tbl, tbl_stride, ps_shift, rot, interleaved,
+                           cos_t, sin_t, window, gx, gw, gbias, gy, gN, gK, gact, by_row, stream);
+}
+
+// fp16 twin (same arguments; qkv / caches / out / gx / gw / gbias / gy fp16)
+KCA_API int kca_decode_prep_attn_gemv_f16(const void* qkv, long long ld, const void* kc, const void* vc,
+                                          long long cs_slot, long long cs_head, long long cs_pos,
+                                          const int* slots, const int* kv_lens, void* out, long long o_bs,
+                                          float* ws, long long ws_floats, int B, int H, int Hkv, int D,
+                                          int max_kv, int chunk, float scale, const float* alibi, const int* tbl,
+                                          int tbl_stride, int ps_shift, int rot, int interleaved,
+                                          const float* cos_t, const float* sin_t, int window, const void* gx,
+                                          const void* gw, const void* gbias, void* gy, int gN, int gK, int gact,
+                                          int by_row, hipStream_t stream) {
+  return prep_attn_gemv<1>(qkv, ld, kc, vc, cs_slot, cs_head, cs_pos, slots, kv_lens, out, o_bs, ws, ws_floats, B,
+                           H, Hkv, D, max_kv, chunk, scale, alibi, tbl, tbl_stride, ps_shift, rot, interleaved,
+                           cos_t, sin_t, window, gx, gw, gbias, gy, gN, gK, gact, by_row, stream);
 }
 
 // Fused decode layer, tail: y = x1 W1^T (+ x2 W2^T) + bias ([N]), h_out = bf16(h + y), xn_out =
@@ -1096,10 +1157,11 @@ KCA_API int kca_decode_prep_attn_gemv(const void* qkv, long long ld, const void*
 // Geometry: 4 weight rows per workgroup, one workgroup per row group (8 or 16 rows measured equal or
 // slower inside the decode steps; a grid capped at one residency round slower:
 // profiles/decode_launch_structure_ab_r5.txt).
-KCA_API int kca_gemv_dual_ln(const void* x1, const void* w1, int K1, const void* x2, const void* w2, int K2,
-                             const void* bias, float* ypart, unsigned int* cnt, const void* h, void* h_out,
-                             const void* gamma, const void* beta, float eps, void* xn_out, const void* gamma2,
-                             const void* beta2, void* xn2_out, int N, hipStream_t stream) {
+template <int DT>
+static int gemv_dual_ln(const void* x1, const void* w1, int K1, const void* x2, const void* w2, int K2,
+                        const void* bias, float* ypart, unsigned int* cnt, const void* h, void* h_out,
+                        const void* gamma, const void* beta, float eps, void* xn_out, const void* gamma2,
+                        const void* beta2, void* xn2_out, int N, hipStream_t stream) {
   if (N <= 0 || N % 8 || N > 16384 || K1 % 8 || K1 <= 0 || !ypart || !cnt || !gamma || !xn_out || !h || !h_out)
     return 1;
   if (x2 && (K2 <= 0 || K2 % 8 || !w2)) return 1;
@@ -1113,9 +1175,26 @@ KCA_API int kca_gemv_dual_ln(const void* x1, const void* w1, int K1, const void*
                  (bf16_t*)xn_out, (const bf16_t*)gamma2, (const bf16_t*)beta2, (bf16_t*)xn2_out,
                  N, K1, x2 ? K2 : 0};
   const dim3 grid((unsigned)((N + 3) / 4));
-  if (N <= 8192) hipLaunchKernelGGL((gemv_dual_ln_kernel<4, 4>), grid, dim3(256), 0, stream, a);
-  else hipLaunchKernelGGL((gemv_dual_ln_kernel<4, 8>), grid, dim3(256), 0, stream, a);
+  if (N <= 8192) hipLaunchKernelGGL((gemv_dual_ln_kernel<4, 4, DT>), grid, dim3(256), 0, stream, a);
+  else hipLaunchKernelGGL((gemv_dual_ln_kernel<4, 8, DT>), grid, dim3(256), 0, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+KCA_API int kca_gemv_dual_ln(const void* x1, const void* w1, int K1, const void* x2, const void* w2, int K2,
+                             const void* bias, float* ypart, unsigned int* cnt, const void* h, void* h_out,
+                             const void* gamma, const void* beta, float eps, void* xn_out, const void* gamma2,
+                             const void* beta2, void* xn2_out, int N, hipStream_t stream) {
+  return gemv_dual_ln<0>(x1, w1, K1, x2, w2, K2, bias, ypart, cnt, h, h_out, gamma, beta, eps, xn_out, gamma2,
+                         beta2, xn2_out, N, stream);
+}
+
+// fp16 twin (same arguments)
+KCA_API int kca_gemv_dual_ln_f16(const void* x1, const void* w1, int K1, const void* x2, const void* w2, int K2,
+                                 const void* bias, float* ypart, unsigned int* cnt, const void* h, void* h_out,
+                                 const void* gamma, const void* beta, float eps, void* xn_out, const void* gamma2,
+                                 const void* beta2, void* xn2_out, int N, hipStream_t stream) {
+  return gemv_dual_ln<1>(x1, w1, K1, x2, w2, K2, bias, ypart, cnt, h, h_out, gamma, beta, eps, xn_out, gamma2,
+                         beta2, xn2_out, N, stream);
 }
 
 // --------------------------------------------------------------- sampling
@@ -1258,7 +1337,9 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(
       v[u] = 0.f;
       sv[u] = 0;
       if (i < V) {
-        v[u] = is_bf16 ? bf2f(((const bf16_t*)logits)[b * ld + i]) : ((const float*)logits)[b * ld + i];
+        // is_bf16: the logits' dtype -- 0 fp32, 1 bf16, 2 fp16
+        v[u] = is_bf16 == 1 ? bf2f(((const bf16_t*)logits)[b * ld + i])
+               : (is_bf16 == 2 ? e2f<1>(((const bf16_t*)logits)[b * ld + i]) : ((const float*)logits)[b * ld + i]);
         if (pen) sv[u] = sn[i];
       }
     }
@@ -2199,7 +2280,7 @@ KCA_API int kca_sample_stamps(unsigned long long* out, int reset) {
   } while (0)
 #endif
 
-template <int VPT, int G = MWG_G, int CMAX = MWG_CMAX>
+template <int VPT, int G = MWG_G, int CMAX = MWG_CMAX, int DT = 0>
 __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
     const bf16_t* __restrict__ logits, long long ld, int V, int CS,
     const float* __restrict__ temperature, const int* __restrict__ top_k,
@@ -2250,7 +2331,7 @@ __global__ __launch_bounds__(MWG_NT) void sample_mwg_kernel(
     const int i = e0 + e;
     float w = -INFINITY;
     if (i < c1) {
-      w = bf2f(row[i]);
+      w = e2f<DT>(row[i]);
       if (pen && sn[i]) w = w < 0.f ? w * rp : w / rp;
       w *= inv_t;
     }
@@ -2830,21 +2911,37 @@ KCA_API int kca_sample_logits(const void* logits, long long ld, int is_bf16, int
   const bool big = V > 50 * 1024;
   const int G = big ? 32 : MWG_G;
   const int CS = (V + G - 1) / G, vpt = (CS + MWG_NT - 1) / MWG_NT;
+  // (is_bf16: the logits' dtype -- 0 fp32, 1 bf16, 2 fp16; the multi-workgroup kernel reads 16-bit logits)
   const bool use_mwg = mwg && cnt && is_bf16 && (big ? vpt <= 32 : vpt <= 16) &&
                        (long long)G * (MWG_PART + 2 * (big ? 64 : MWG_CMAX)) <= V;  // (the rest: sample_reg_kernel)
   if (use_mwg && big) {
-    hipLaunchKernelGGL((sample_mwg_kernel<32, 32, 64>), dim3(32, B), dim3(MWG_NT), 0, stream, (const bf16_t*)logits,
-                       ld, V, CS, temperature, top_k, top_p, rep_pen, (uint8_t*)seen, slots, ban_ids, n_ban, seeds,
-                       step, ws, cnt, out_ids, out_lp, out_kept);
+    if (is_bf16 == 2)
+      hipLaunchKernelGGL((sample_mwg_kernel<32, 32, 64, 1>), dim3(32, B), dim3(MWG_NT), 0, stream,
+                         (const bf16_t*)logits, ld, V, CS, temperature, top_k, top_p, rep_pen, (uint8_t*)seen, slots,
+                         ban_ids, n_ban, seeds, step, ws, cnt, out_ids, out_lp, out_kept);
+    else
+      hipLaunchKernelGGL((sample_mwg_kernel<32, 32, 64>), dim3(32, B), dim3(MWG_NT), 0, stream,
+                         (const bf16_t*)logits, ld, V, CS, temperature, top_k, top_p, rep_pen, (uint8_t*)seen, slots,
+                         ban_ids, n_ban, seeds, step, ws, cnt, out_ids, out_lp, out_kept);
   } else if (use_mwg) {
-#define KCA_SAMPLE_MWG_LAUNCH(P)                                                                           \
-  hipLaunchKernelGGL((sample_mwg_kernel<P>), dim3(MWG_G, B), dim3(MWG_NT), 0, stream, (const bf16_t*)logits, ld, \
-                     V, CS, temperature, top_k, top_p, rep_pen, (uint8_t*)seen, slots, ban_ids, n_ban, seeds,  \
-                     step, ws, cnt, out_ids, out_lp, out_kept)
-    if (vpt <= 4) KCA_SAMPLE_MWG_LAUNCH(4);
-    else if (vpt <= 8) KCA_SAMPLE_MWG_LAUNCH(8);
-    else if (vpt <= 13) KCA_SAMPLE_MWG_LAUNCH(13);  // GPT-2 / GPT-J / NeoX vocabularies
-    else KCA_SAMPLE_MWG_LAUNCH(16);
+#define KCA_SAMPLE_MWG_LAUNCH(P)                                                                               \
+  if (is_bf16 == 2)                                                                                            \
+    hipLaunchKernelGGL((sample_mwg_kernel<P, MWG_G, MWG_CMAX, 1>), dim3(MWG_G, B), dim3(MWG_NT), 0, stream,    \
+                       (const bf16_t*)logits, ld, V, CS, temperature, top_k, top_p, rep_pen, (uint8_t*)seen, slots, \
+                       ban_ids, n_ban, seeds, step, ws, cnt, out_ids, out_lp, out_kept);                      \
+  else                                                                                                         \
+    hipLaunchKernelGGL((sample_mwg_kernel<P>), dim3(MWG_G, B), dim3(MWG_NT), 0, stream, (const bf16_t*)logits,  \
+                       ld, V, CS, temperature, top_k, top_p, rep_pen, (uint8_t*)seen, slots, ban_ids, n_ban, seeds, \
+                       step, ws, cnt, out_ids, out_lp, out_kept)
+    if (vpt <= 4) {
+      KCA_SAMPLE_MWG_LAUNCH(4);
+    } else if (vpt <= 8) {
+      KCA_SAMPLE_MWG_LAUNCH(8);
+    } else if (vpt <= 13) {
+      KCA_SAMPLE_MWG_LAUNCH(13);  // GPT-2 / GPT-J / NeoX vocabularies
+    } else {
+      KCA_SAMPLE_MWG_LAUNCH(16);
+    }
 #undef KCA_SAMPLE_MWG_LAUNCH
   }
   // mwg_complete: the caller knows every row is greedy or has 1 <= top_k <= 64 -- rows the multi-workgroup
@@ -2861,7 +2958,7 @@ KCA_API int kca_sample_logits(const void* logits, long long ld, int is_bf16, int
     const char* e = getenv("KCA_SAMPLE_REG");
     reg = !(e && e[0] == '0');
   }
-  if (reg && is_bf16 && V <= 50 * 1024) {
+  if (reg && is_bf16 == 1 && V <= 50 * 1024) {  // (bit-level bf16 candidate packing: bf16 logits only)
 #define KCA_SAMPLE_REG_LAUNCH(R)                                                                          \
   hipLaunchKernelGGL((sample_reg_kernel<R, 1024>), dim3(B), dim3(1024), 0, stream, logits, ld, V,            \
                      temperature, top_k, top_p, rep_pen, (uint8_t*)seen, slots, ban_ids, n_ban, seeds, step,     \

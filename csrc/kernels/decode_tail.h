@@ -26,6 +26,24 @@ __device__ __forceinline__ void st_pub_bf16x8(bf16_t* p, const float (&v)[8]) {
   __hip_atomic_store(q + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// either element type (DT, common.h)
+template <int DT>
+__device__ __forceinline__ void st_pub_e(bf16_t* p, float v) {
+  __hip_atomic_store(reinterpret_cast<unsigned short*>(p), (unsigned short)f2e<DT>(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+template <int DT>
+__device__ __forceinline__ void st_pub_x8(bf16_t* p, const float (&v)[8]) {
+  unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
+  uint32_t w[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) w[j] = f2e<DT>(v[2 * j]) | (f2e<DT>(v[2 * j + 1]) << 16);
+  __hip_atomic_store(q, (unsigned long long)w[0] | ((unsigned long long)w[1] << 32), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(q + 1, (unsigned long long)w[2] | ((unsigned long long)w[3] << 32), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
 constexpr int kDualSub = 64;  // sub-counters of gemv_dual_ln_kernel's arrival (cnt: 32 * (1 + 64) uints)
 
 struct DualLn {
@@ -49,7 +67,7 @@ struct DualLn {
   int N, K1, K2;
 };
 
-template <int PER>
+template <int PER, int DT = 0>
 __device__ void dual_ln_finish(const DualLn& a);
 
 // Arrival of the work of a fused decode tail launch, then -- in the last arrival -- the LayerNorm(s) of
@@ -59,7 +77,7 @@ __device__ void dual_ln_finish(const DualLn& a);
 // kDualSub, 128 B apart; `members` items in all arrive there) and the arrival that completes a
 // sub-counter counts into the top one (cnt[0]; `nsub` sub-counters receive items). Default: one item per
 // workgroup, sub = blockIdx % 64. 256-thread workgroups; PER: 2048-column slices (N <= 256 * 8 * PER).
-template <int PER>
+template <int PER, int DT = 0>
 __device__ void dual_ln_arrive(const DualLn& a, int sub, unsigned members, int nsub, unsigned n) {
   __shared__ int s_last;
   const int tid = threadIdx.x;
@@ -84,19 +102,19 @@ __device__ void dual_ln_arrive(const DualLn& a, int sub, unsigned members, int n
   __syncthreads();
   const int last = s_last;
   __syncthreads();  // (s_last is rewritten by this workgroup's next arrival)
-  if (last) dual_ln_finish<PER>(a);
+  if (last) dual_ln_finish<PER, DT>(a);
 }
 
-template <int PER>
+template <int PER, int DT = 0>
 __device__ void dual_ln_arrive_tail(const DualLn& a) {
   constexpr int NSUB = kDualSub;
   const int G = gridDim.x, sub = blockIdx.x % NSUB;
-  dual_ln_arrive<PER>(a, sub, (unsigned)((G - sub + NSUB - 1) / NSUB), G < NSUB ? G : NSUB, 1u);
+  dual_ln_arrive<PER, DT>(a, sub, (unsigned)((G - sub + NSUB - 1) / NSUB), G < NSUB ? G : NSUB, 1u);
 }
 
 // The LayerNorm(s) of h' (h_out, complete and visible to this workgroup), written to xn_out (and
 // xn2_out).
-template <int PER>
+template <int PER, int DT>
 __device__ void dual_ln_finish(const DualLn& a) {
   __shared__ float red[16];
   const int tid = threadIdx.x;
@@ -117,7 +135,7 @@ __device__ void dual_ln_finish(const DualLn& a) {
   for (int i = 0; i < PER; ++i) {
     const uint32_t q4[4] = {hp[i].x, hp[i].y, hp[i].z, hp[i].w};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) s += __uint_as_float(q4[j] << 16) + __uint_as_float(q4[j] & 0xffff0000u);
+    for (int j = 0; j < 4; ++j) s += lo2f<DT>(q4[j]) + hi2f<DT>(q4[j]);
   }
   const float mean = block_sum(s, red) / a.N;
   float q = 0.f;
@@ -127,7 +145,7 @@ __device__ void dual_ln_finish(const DualLn& a) {
     const uint32_t q4[4] = {hp[i].x, hp[i].y, hp[i].z, hp[i].w};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float lo = __uint_as_float(q4[j] << 16) - mean, hi = __uint_as_float(q4[j] & 0xffff0000u) - mean;
+      const float lo = lo2f<DT>(q4[j]) - mean, hi = hi2f<DT>(q4[j]) - mean;
       q += lo * lo + hi * hi;
     }
   }
@@ -139,9 +157,9 @@ __device__ void dual_ln_finish(const DualLn& a) {
     const int k = (i * 256 + tid) * 8;
     if (k >= a.N) continue;
     float xh[8], gm[8], bt[8], o[8];
-    load8(a.h_out + k, xh);
-    load8(a.gamma + k, gm);
-    if (a.beta) load8(a.beta + k, bt);
+    load8_t<DT>(a.h_out + k, xh);
+    load8_t<DT>(a.gamma + k, gm);
+    if (a.beta) load8_t<DT>(a.beta + k, bt);
     else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) bt[j] = 0.f;
@@ -151,17 +169,17 @@ __device__ void dual_ln_finish(const DualLn& a) {
       xh[j] = (xh[j] - mean) * rstd;
       o[j] = xh[j] * gm[j] + bt[j];
     }
-    store8(a.xn_out + k, o);
+    store8_t<DT>(a.xn_out + k, o);
     if (a.xn2_out) {
-      load8(a.gamma2 + k, gm);
-      if (a.beta2) load8(a.beta2 + k, bt);
+      load8_t<DT>(a.gamma2 + k, gm);
+      if (a.beta2) load8_t<DT>(a.beta2 + k, bt);
       else {
 #pragma unroll
         for (int j = 0; j < 8; ++j) bt[j] = 0.f;
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = xh[j] * gm[j] + bt[j];
-      store8(a.xn2_out + k, o);
+      store8_t<DT>(a.xn2_out + k, o);
     }
   }
 }

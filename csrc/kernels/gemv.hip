@@ -176,7 +176,7 @@ __global__ __launch_bounds__(256) void skinny_gemm_kernel(
 // against 5.2 TB/s for the plain one at GPT-J shapes.)
 // MR > 1 (decode batch 2..4, no LN prologue): the same K-split structure over MR activation rows
 // held in registers -- W still streamed once, MR FMAs per weight element
-template <int R, bool LN, int MR = 1>
+template <int R, bool LN, int MR = 1, int DT = 0>
 __global__ __launch_bounds__(256) void gemv1_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
                                                     const bf16_t* __restrict__ bias, bf16_t* __restrict__ y,
                                                     int N, int K, int act, LnArgs ln, long long ldx = 0,
@@ -221,8 +221,8 @@ __global__ __launch_bounds__(256) void gemv1_kernel(const bf16_t* __restrict__ x
         const uint32_t q[4] = {wv[u][r].x, wv[u][r].y, wv[u][r].z, wv[u][r].w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          acc[0][r] = fmaf(__uint_as_float(q[j] << 16), xv[u][2 * j], acc[0][r]);
-          acc[0][r] = fmaf(__uint_as_float(q[j] & 0xffff0000u), xv[u][2 * j + 1], acc[0][r]);
+          acc[0][r] = fmaf(lo2f<DT>(q[j]), xv[u][2 * j], acc[0][r]);
+          acc[0][r] = fmaf(hi2f<DT>(q[j]), xv[u][2 * j + 1], acc[0][r]);
         }
       }
     }
@@ -236,23 +236,23 @@ __global__ __launch_bounds__(256) void gemv1_kernel(const bf16_t* __restrict__ x
       const int k = u * 2048 + kl;
       if (k < K) {
         float t[8];
-        load8(x + k, xv[u]);
+        load8_t<DT>(x + k, xv[u]);
         if (ln.r1) {
-          load8(ln.r1 + k, t);
+          load8_t<DT>(ln.r1 + k, t);
 #pragma unroll
           for (int j = 0; j < 8; ++j) xv[u][j] += t[j];
         }
         if (ln.r2) {
-          load8(ln.r2 + k, t);
+          load8_t<DT>(ln.r2 + k, t);
 #pragma unroll
           for (int j = 0; j < 8; ++j) xv[u][j] += t[j];
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          xv[u][j] = bf2f(f2bf(xv[u][j]));  // statistics over the bf16-rounded residual sum
+          xv[u][j] = e2f<DT>(f2e<DT>(xv[u][j]));  // statistics over the rounded residual sum
           s += xv[u][j];
         }
-        if (ln.h_out && blockIdx.x == 0) store8(ln.h_out + k, xv[u]);
+        if (ln.h_out && blockIdx.x == 0) store8_t<DT>(ln.h_out + k, xv[u]);
       } else {
 #pragma unroll
         for (int j = 0; j < 8; ++j) xv[u][j] = 0.f;
@@ -272,15 +272,15 @@ __global__ __launch_bounds__(256) void gemv1_kernel(const bf16_t* __restrict__ x
       const int k = u * 2048 + kl;
       if (k >= K) continue;
       float g[8], bb[8];
-      load8(ln.gamma + k, g);
-      if (ln.beta) load8(ln.beta + k, bb);
+      load8_t<DT>(ln.gamma + k, g);
+      if (ln.beta) load8_t<DT>(ln.beta + k, bb);
       else {
 #pragma unroll
         for (int j = 0; j < 8; ++j) bb[j] = 0.f;
       }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) xv[u][j] = bf2f(f2bf((xv[u][j] - mean) * rstd * g[j] + bb[j]));
-      if (ln.xn_out && blockIdx.x == 0) store8(ln.xn_out + k, xv[u]);
+      for (int j = 0; j < 8; ++j) xv[u][j] = e2f<DT>(f2e<DT>((xv[u][j] - mean) * rstd * g[j] + bb[j]));
+      if (ln.xn_out && blockIdx.x == 0) store8_t<DT>(ln.xn_out + k, xv[u]);
     }
     fma_w(0, xv);
   } else {
@@ -306,10 +306,7 @@ __global__ __launch_bounds__(256) void gemv1_kernel(const bf16_t* __restrict__ x
           for (int m = 0; m < MR; ++m) {
             const uint32_t xq[4] = {xr[m][u].x, xr[m][u].y, xr[m][u].z, xr[m][u].w};
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              acc[m][r] = fmaf(__uint_as_float(q[j] << 16), __uint_as_float(xq[j] << 16), acc[m][r]);
-              acc[m][r] = fmaf(__uint_as_float(q[j] & 0xffff0000u), __uint_as_float(xq[j] & 0xffff0000u), acc[m][r]);
-            }
+            for (int j = 0; j < 4; ++j) acc[m][r] = dot2_acc<DT>(q[j], xq[j], acc[m][r]);
           }
         }
       }
@@ -330,10 +327,10 @@ __global__ __launch_bounds__(256) void gemv1_kernel(const bf16_t* __restrict__ x
   if (tid < R * MR && m < mv && n0 + r < N) {
     const int i = m * R + r;
     float v = part[0][i] + part[1][i] + part[2][i] + part[3][i];
-    v += bias ? bf2f(bias[n0 + r]) : 0.f;
+    v += bias ? e2f<DT>(bias[n0 + r]) : 0.f;
     if (act == 1) v = gelu_tanh(v);
     else if (act == 2) v = 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
-    y[m * ldy + n0 + r] = f2bf(v);
+    y[m * ldy + n0 + r] = (bf16_t)f2e<DT>(v);
   }
 }
 
@@ -352,7 +349,7 @@ struct EmbedSrc {
   int V;
 };
 
-template <int PER, bool GATHER = false>
+template <int PER, bool GATHER = false, int DT = 0>
 __global__ __launch_bounds__(256) void ln_rows_kernel(const bf16_t* __restrict__ x, long long ldx, LnArgs a,
                                                       int K, EmbedSrc es = EmbedSrc{}) {
   __shared__ float red[16];
@@ -381,23 +378,23 @@ __global__ __launch_bounds__(256) void ln_rows_kernel(const bf16_t* __restrict__
     const int k = (i * 256 + tid) * 8;
     if (k < K) {
       float t[8];
-      load8(x + m * ldx + k, v[i]);
+      load8_t<DT>(x + m * ldx + k, v[i]);
       if (a.r1) {
-        load8(a.r1 + m * a.ldh + k, t);
+        load8_t<DT>(a.r1 + m * a.ldh + k, t);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[i][j] += t[j];
       }
       if (a.r2) {
-        load8(a.r2 + m * a.ldh + k, t);
+        load8_t<DT>(a.r2 + m * a.ldh + k, t);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[i][j] += t[j];
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        v[i][j] = bf2f(f2bf(v[i][j]));
+        v[i][j] = e2f<DT>(f2e<DT>(v[i][j]));
         s += v[i][j];
       }
-      if (a.h_out) store8(a.h_out + m * a.ldh + k, v[i]);
+      if (a.h_out) store8_t<DT>(a.h_out + m * a.ldh + k, v[i]);
     } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
@@ -418,8 +415,8 @@ __global__ __launch_bounds__(256) void ln_rows_kernel(const bf16_t* __restrict__
     if (k >= K) continue;
 #pragma unroll
     for (int j = 0; j < 8; ++j)
-      v[i][j] = (v[i][j] - mean) * rstd * bf2f(gr[i].v[j]) + (a.beta ? bf2f(br[i].v[j]) : 0.f);
-    store8(a.xn_out + (long long)m * K + k, v[i]);
+      v[i][j] = (v[i][j] - mean) * rstd * e2f<DT>(gr[i].v[j]) + (a.beta ? e2f<DT>(br[i].v[j]) : 0.f);
+    store8_t<DT>(a.xn_out + (long long)m * K + k, v[i]);
   }
 }
 
@@ -454,6 +451,46 @@ KCA_API int kca_embed_ln_rows(const void* wte, long long ldw, const long long* t
     hipLaunchKernelGGL((ln_rows_kernel<4, true>), dim3(M), dim3(256), 0, stream, (const bf16_t*)wte, ldw, a, K, es);
   else
     hipLaunchKernelGGL((ln_rows_kernel<8, true>), dim3(M), dim3(256), 0, stream, (const bf16_t*)wte, ldw, a, K, es);
+  return 0;
+}
+
+// fp16 rows (FT / DS-Inference serve fp16): kca_ln_rows / kca_embed_ln_rows with fp16 loads and stores
+KCA_API int kca_ln_rows_f16(const void* x, long long ldx, const void* r1, const void* r2, void* h_out, long long ldh,
+                            const void* gamma, const void* beta, float eps, void* xn_out, int M, int K,
+                            hipStream_t stream) {
+  if (M < 1 || K % 8 || K > 16384 || ldx % 8 || ldh % 8 || !xn_out) return 1;
+  if (((uintptr_t)x | (uintptr_t)r1 | (uintptr_t)r2 | (uintptr_t)h_out | (uintptr_t)gamma | (uintptr_t)beta |
+       (uintptr_t)xn_out) & 15) return 2;
+  LnArgs a{(const bf16_t*)r1, (const bf16_t*)r2, (bf16_t*)h_out, ldh, (const bf16_t*)gamma, (const bf16_t*)beta,
+           eps, (bf16_t*)xn_out};
+  const int per = (K + 2047) / 2048;
+  if (per <= 2)
+    hipLaunchKernelGGL((ln_rows_kernel<2, false, 1>), dim3(M), dim3(256), 0, stream, (const bf16_t*)x, ldx, a, K,
+                       EmbedSrc{});
+  else if (per <= 4)
+    hipLaunchKernelGGL((ln_rows_kernel<4, false, 1>), dim3(M), dim3(256), 0, stream, (const bf16_t*)x, ldx, a, K,
+                       EmbedSrc{});
+  else
+    hipLaunchKernelGGL((ln_rows_kernel<8, false, 1>), dim3(M), dim3(256), 0, stream, (const bf16_t*)x, ldx, a, K,
+                       EmbedSrc{});
+  return 0;
+}
+
+KCA_API int kca_embed_ln_rows_f16(const void* wte, long long ldw, const long long* tokens, const int* chain,
+                                  const long long* prev, int V, void* h_out, long long ldh, const void* gamma,
+                                  const void* beta, float eps, void* xn_out, int M, int K, hipStream_t stream) {
+  if (M < 1 || K % 8 || K > 16384 || ldw % 8 || ldh % 8 || !xn_out || !h_out || !tokens || V < 1) return 1;
+  if (chain && !prev) return 1;
+  if (((uintptr_t)wte | (uintptr_t)h_out | (uintptr_t)gamma | (uintptr_t)beta | (uintptr_t)xn_out) & 15) return 2;
+  LnArgs a{nullptr, nullptr, (bf16_t*)h_out, ldh, (const bf16_t*)gamma, (const bf16_t*)beta, eps, (bf16_t*)xn_out};
+  EmbedSrc es{tokens, chain, prev, V};
+  const int per = (K + 2047) / 2048;
+  if (per <= 2)
+    hipLaunchKernelGGL((ln_rows_kernel<2, true, 1>), dim3(M), dim3(256), 0, stream, (const bf16_t*)wte, ldw, a, K, es);
+  else if (per <= 4)
+    hipLaunchKernelGGL((ln_rows_kernel<4, true, 1>), dim3(M), dim3(256), 0, stream, (const bf16_t*)wte, ldw, a, K, es);
+  else
+    hipLaunchKernelGGL((ln_rows_kernel<8, true, 1>), dim3(M), dim3(256), 0, stream, (const bf16_t*)wte, ldw, a, K, es);
   return 0;
 }
 
@@ -514,6 +551,21 @@ KCA_API int kca_skinny_gemm(const void* x, long long ldx, const void* w, const v
   else if (M <= 8) launch_skinny<8>(xp, ldx, wp, bp, yp, ldy, M, N, K, act, stream);
   else launch_skinny<16>(xp, ldx, wp, bp, yp, ldy, M, N, K, act, stream);
   return 0;
+}
+
+// fp16 twin of kca_skinny_gemm for the decode step's single-row projections (the batch-1 fused layer's
+// QKV / fc_in / LM head GEMVs): M == 1 only (batch > 1 fp16 decode runs the matrix-core layer,
+// skinny_mfma.hip); returns 3 for other M so the caller falls back
+KCA_API int kca_skinny_gemm_f16(const void* x, long long ldx, const void* w, const void* bias, void* y,
+                                long long ldy, int M, int N, int K, int act, hipStream_t stream) {
+  if (M != 1) return 3;
+  if (K % 8 || N < 1) return 1;
+  if (((uintptr_t)x | (uintptr_t)w) & 15) return 2;
+  constexpr int R1 = 2;
+  hipLaunchKernelGGL((gemv1_kernel<R1, false, 1, 1>), dim3((N + R1 - 1) / R1), dim3(256), 0, stream,
+                     (const bf16_t*)x, (const bf16_t*)w, (const bf16_t*)bias, (bf16_t*)y, N, K, act, LnArgs{}, 0LL,
+                     0LL, 1);
+  return hipGetLastError() == hipSuccess ? 0 : 4;
 }
 
 // y = act(LayerNorm(x (+ r1) (+ r2)) . W^T + b); h_out (nullable) receives the

@@ -1,5 +1,5 @@
 // Single-row (decode batch 1) weight-streaming pieces shared by gemv.hip (the skinny GEMM / GEMV
-// kernels) and decode.hip (the fused decode-layer kernels).
+// kernels) and decode.hip (the fused decode-layer kernels). DT: element type (common.h e2f).
 #pragma once
 #include "common.h"
 
@@ -29,7 +29,7 @@ __device__ __forceinline__ uint4 ld_w16(const bf16_t* p) {
 // w, lane l) owns positions i*2048 + w*512 + l*8), R weight rows, 16 / R slabs of loads in flight --
 // the gemv1_kernel<R, false, 1> loop (gemv.hip) as a device function, so that a fused kernel can
 // run it on a subset of its workgroups. Not reduced across lanes: call gemv_m1_finish.
-template <int R, int UO = 0>
+template <int R, int UO = 0, int DT = 0>
 __device__ __forceinline__ void gemv_m1_accum(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, int N,
                                               int K, int n0, float (&acc)[R], long long ldw = -1) {
   if (ldw < 0) ldw = K;  // row stride of w (a K-chunk of a wider matrix: the full row length)
@@ -71,10 +71,7 @@ __device__ __forceinline__ void gemv_m1_accum(const bf16_t* __restrict__ x, cons
       for (int r = 0; r < R; ++r) {
         const uint32_t q[4] = {wv[u][r].x, wv[u][r].y, wv[u][r].z, wv[u][r].w};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          acc[r] = fmaf(__uint_as_float(q[j] << 16), __uint_as_float(xq[j] << 16), acc[r]);
-          acc[r] = fmaf(__uint_as_float(q[j] & 0xffff0000u), __uint_as_float(xq[j] & 0xffff0000u), acc[r]);
-        }
+        for (int j = 0; j < 4; ++j) acc[r] = dot2_acc<DT>(q[j], xq[j], acc[r]);
       }
     }
   }
@@ -83,7 +80,7 @@ __device__ __forceinline__ void gemv_m1_accum(const bf16_t* __restrict__ x, cons
 // Reduce the R per-lane partial dots over the workgroup (waves in LDS `part` [4][R]) and apply
 // bias + activation (0 none, 1 GELU tanh, 2 GELU erf). Returns the value for row n0 + tid in
 // threads tid < R (valid iff n0 + tid < N); callers store it.
-template <int R>
+template <int R, int DT = 0>
 __device__ __forceinline__ float gemv_m1_finish(float (&acc)[R], float (*part)[R], const bf16_t* __restrict__ bias,
                                                 int n0, int N, int act) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -97,7 +94,7 @@ __device__ __forceinline__ float gemv_m1_finish(float (&acc)[R], float (*part)[R
   float v = 0.f;
   if (tid < R && n0 + tid < N) {
     v = part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid];
-    v += bias ? bf2f(bias[n0 + tid]) : 0.f;
+    v += bias ? e2f<DT>(bias[n0 + tid]) : 0.f;
     if (act == 1) v = gelu_tanh(v);
     else if (act == 2) v = 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
   }

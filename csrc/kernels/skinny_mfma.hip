@@ -37,18 +37,7 @@
 typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
-// DT 0 = bf16, 1 = fp16 (FasterTransformer / DS-Inference serve fp16)
-template <int DT>
-__device__ __forceinline__ float e2f(uint32_t u16) {
-  if constexpr (DT == 0) return __uint_as_float(u16 << 16);
-  else return (float)__builtin_bit_cast(_Float16, (uint16_t)u16);
-}
-template <int DT>
-__device__ __forceinline__ uint32_t f2e(float f) {
-  if constexpr (DT == 0) return (uint32_t)f2bf(f);
-  else return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)f);
-}
-
+// DT 0 = bf16, 1 = fp16 (e2f / f2e: common.h)
 template <int DT>
 __device__ __forceinline__ f32x4 mfma16(const u32x4v& a, const u32x4v& b, const f32x4& c) {
   if constexpr (DT == 0)

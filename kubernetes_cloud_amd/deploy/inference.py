@@ -162,7 +162,7 @@ def fastertransformer() -> dict:
             [f"python3 -m kubernetes_cloud_amd.data.downloader -model {model} -dest /mnt/pvc/{name}-hf && "
              f"python3 -c 'from kubernetes_cloud_amd.serving.triton_ft import convert_main; convert_main()' "
              f"--model-dir /mnt/pvc/{name}-hf --output-dir /mnt/pvc/{store}/triton-model-store "
-             f"--n-inference-gpus 1 --data-type bf16"],
+             f"--n-inference-gpus 1 --data-type fp16"],
             "ft-model-storage", mount="/mnt/pvc", env=HF_TOKEN_ENV, cpu=16, memory="128Gi")
         c = _container(["python3", "-m", "kubernetes_cloud_amd.serving.triton_ft"],
                        ["--model-store", f"/mnt/pvc/{store}/triton-model-store", "--http-port", "80"],

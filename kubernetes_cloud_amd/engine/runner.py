@@ -410,9 +410,13 @@ class ModelRunner:
         # out-proj + fc_out one K-concatenated launch). KCA_DECODE_FUSED_BATCHED=0: per-projection path.
         d_model = cfg.hidden
         self.batched_steps = 0
+        self.fused_steps = 0  # batch-1 fused-layer steps built (eager runs and graph captures)
         # (real TP: sequential layers only -- each row-parallel projection closed by the custom all-reduce's
         # residual + row-statistics tail, parallel/custom_ar.py res_stats)
-        self._batched_ok = (self._fused_ok and self.dtype == torch.bfloat16
+        # fp16 (the precision FasterTransformer / DS-Inference serve, BASELINE config 4) runs the same two
+        # layers: every decode kernel (GEMVs, fused tails, attention, LayerNorm rows, MFMA layer, all-reduce
+        # tails, sampler) has an fp16 instantiation (the *_f16 entry points)
+        self._batched_ok = (self._fused_ok and self.dtype in (torch.bfloat16, torch.float16)
                             and d_model % 64 == 0 and d_model <= 16384
                             and os.environ.get("KCA_DECODE_FUSED_BATCHED", "1") not in ("0", "false"))
 
@@ -663,12 +667,15 @@ class ModelRunner:
         hb, st, qkv, g = fz["h"], fz["st"], fz["qkv"], fz["g"]
         dt = self.dtype
         # step head: token rows (+ BLOOM's embedding LayerNorm) and ln_1 (+ ln_2 for NeoX) of layer 0
-        if self._embed_head:
+        if self._embed_head:  # (resolves a chained token of the previous step on the device, as at B = 1)
+            chain, prev = self._chain_src if self._chain_src is not None else (None, None)
             if m.emb_ln is not None:
-                h, _ = embed_ln_rows(m.wte.weight, tokens, m.emb_ln.weight, m.emb_ln.bias, m.emb_ln.eps)
+                h, _ = embed_ln_rows(m.wte.weight, tokens, m.emb_ln.weight, m.emb_ln.bias, m.emb_ln.eps,
+                                     chain=chain, prev=prev)
                 xn, h = ln_rows(h, blk0.ln_1.weight, blk0.ln_1.bias, blk0.ln_1.eps)
             else:
-                xn, h = embed_ln_rows(m.wte.weight, tokens, blk0.ln_1.weight, blk0.ln_1.bias, blk0.ln_1.eps)
+                xn, h = embed_ln_rows(m.wte.weight, tokens, blk0.ln_1.weight, blk0.ln_1.bias, blk0.ln_1.eps,
+                                      chain=chain, prev=prev)
         else:
             xn, h = ln_rows(m.embed(tokens, pos.long()), blk0.ln_1.weight, blk0.ln_1.bias, blk0.ln_1.eps)
         xn2 = ln_rows(h, blk0.ln_2.weight, blk0.ln_2.bias, blk0.ln_2.eps)[0] if kind == "neox" else None
@@ -740,9 +747,10 @@ class ModelRunner:
         if self._fused_ok and tokens.shape[0] == 1 and obuf is not None:
             y = self._layers_decode_fused(tokens, pos, slots, kv_lens, max_kv, ws, obuf)
             if y is not None:
+                self.fused_steps += 1
                 return y
         if (self._batched_ok and 2 <= tokens.shape[0] <= smm.MAX_M and obuf is not None
-                and self._chain_src is None):
+                and (self._chain_src is None or self._embed_head)):
             return self._layers_decode_batched(tokens, pos, slots, kv_lens, max_kv, ws, obuf)
         if self._chain_src is not None and obuf is not None:  # chained rows not resolved by a fused head
             chain, prev = self._chain_src

@@ -110,6 +110,11 @@ _SIGS = {
 }
 
 
+# fp16 twins of the serving kernels (same arguments)
+for _n in ("kca_decode_prep_attn", "kca_ln_rows", "kca_embed_ln_rows", "kca_decode_prep_attn_gemv",
+           "kca_gemv_dual_ln", "kca_skinny_gemm"):
+    _SIGS[_n + "_f16"] = _SIGS[_n]
+
 # fused decode layer (batch 1): kca_decode_prep_attn's arguments (minus the stream), then the fc_in
 # GEMV's x, W, bias, y, N, K, act, then the stream
 _SIGS["kca_decode_prep_attn_gemv"] = _SIGS["kca_decode_prep_attn"][:-2] + [P, P, P, P, I, I, I, I, P]
@@ -201,6 +206,19 @@ def stream() -> int:
 
 def ptr(t: torch.Tensor | None) -> int | None:
     return None if t is None else t.data_ptr()
+
+
+def native_f16(*tensors: torch.Tensor | None) -> bool:
+    """True for fp16 GPU tensors (all of them): the serving kernels with fp16 twins
+    (``*_f16`` entry points) take them natively -- the precision FasterTransformer and
+    DS-Inference serve (BASELINE config 4)."""
+    on_gpu = False
+    for t in tensors:
+        if t is not None and t.is_cuda:
+            on_gpu = True
+            if t.dtype != torch.float16:
+                return False
+    return on_gpu
 
 
 def use_native(*tensors: torch.Tensor | None) -> bool:

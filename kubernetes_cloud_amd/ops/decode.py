@@ -4,7 +4,7 @@
 * ``decode_attention``  split-K flash-decoding over the head-major slot cache
 * ``sample_logits``     fused penalty/bans/temperature/top-k/top-p/multinomial
 
-bf16 GPU tensors run ``csrc/kernels/decode.hip``; CPU tensors run the fp32
+bf16 and fp16 GPU tensors run ``csrc/kernels/decode.hip`` (fp16: the ``*_f16`` entries); CPU tensors run the fp32
 references below (same semantics; used by the CPU test-suite and to pin the
 kernels in ``tests/test_decode_gpu.py``).
 
@@ -167,7 +167,8 @@ def decode_prep_attention(qkv: torch.Tensor, n_heads: int, kv_heads: int, head_d
     _, Hkv, L, D = k_cache.shape
     H = n_heads
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
-    if _lib.use_native(qkv, k_cache) and _lib.has("kca_decode_prep_attn"):
+    f16 = qkv.is_cuda and qkv.dtype == torch.float16 and k_cache.dtype == torch.float16
+    if (_lib.use_native(qkv, k_cache) and _lib.has("kca_decode_prep_attn")) or (f16 and _lib.has("kca_decode_prep_attn_f16")):
         assert qkv.stride(-1) == 1 and k_cache.stride() == v_cache.stride()
         assert kv_lens.dtype == torch.int32 and slots.dtype == torch.int32
         if out is None:
@@ -177,7 +178,8 @@ def decode_prep_attention(qkv: torch.Tensor, n_heads: int, kv_heads: int, head_d
         need = decode_ws_floats(B, H, Hkv, D, max_kv, chunk)
         if need and (ws is None or ws.numel() < need):
             ws = torch.zeros(need, device=qkv.device, dtype=torch.float32)
-        _lib.call("kca_decode_prep_attn", qkv.data_ptr(), qkv.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+        _lib.call("kca_decode_prep_attn_f16" if f16 else "kca_decode_prep_attn", qkv.data_ptr(), qkv.stride(0),
+                  k_cache.data_ptr(), v_cache.data_ptr(),
                   k_cache.stride(0), k_cache.stride(1), k_cache.stride(2), slots.data_ptr(), kv_lens.data_ptr(),
                   out.data_ptr(), out.stride(0), _lib.ptr(ws), ws.numel() if ws is not None else 0, B, H, Hkv, D,
                   max_kv, chunk, float(scale), _lib.ptr(alibi), tbl, tstride, shift, rot, int(interleaved),
@@ -202,16 +204,18 @@ def decode_prep_attention_gemv(qkv, n_heads, kv_heads, head_dim, rot, interleave
     with the step's inputs: the attention chain does not wait for the length or the slot first)."""
     B = qkv.shape[0]
     _, Hkv, L, D = k_cache.shape
-    if not (_lib.use_native(qkv, k_cache, gx, gw) and _lib.has("kca_decode_prep_attn_gemv") and B == 1
+    f16 = _lib.native_f16(qkv, k_cache, gx, gw)
+    if not ((_lib.use_native(qkv, k_cache, gx, gw) or f16) and _lib.has("kca_decode_prep_attn_gemv") and B == 1
             and gx.is_contiguous() and gw.is_contiguous() and gy.is_contiguous()
-            and (gbias is None or gbias.dtype == torch.bfloat16)):
+            and (gbias is None or gbias.dtype == gx.dtype)):
         return False
     tbl, tstride, shift = _table_args(block_table, k_cache)
     chunk = decode_chunk(B, Hkv, max_kv)
     need = decode_ws_floats(B, n_heads, Hkv, D, max_kv, chunk)
     if need and (ws is None or ws.numel() < need):
         return False
-    rc = _lib.require().kca_decode_prep_attn_gemv(
+    fn = getattr(_lib.require(), "kca_decode_prep_attn_gemv_f16" if f16 else "kca_decode_prep_attn_gemv")
+    rc = fn(
         qkv.data_ptr(), qkv.stride(0), k_cache.data_ptr(), v_cache.data_ptr(), k_cache.stride(0), k_cache.stride(1),
         k_cache.stride(2), slots.data_ptr(), kv_lens.data_ptr(), out.data_ptr(), out.stride(0), _lib.ptr(ws),
         ws.numel() if ws is not None else 0, B, n_heads, Hkv, D, max_kv, chunk, float(scale), _lib.ptr(alibi), tbl,
@@ -235,7 +239,7 @@ def gemv_dual_ln(x1: torch.Tensor, w1: torch.Tensor, x2: torch.Tensor | None, w2
     (``x2`` None), and with ``gamma2`` the second LayerNorm of the same h_out into ``xn2_out`` (GPT-NeoX:
     ln_1 and ln_2 of one residual stream share the statistics). ``ypart``: >= N fp32 words;
     ``cnt``: zero-initialised int32 [32 * 65] arrival counters. N <= 16384."""
-    _lib.call("kca_gemv_dual_ln", x1.data_ptr(), w1.data_ptr(), w1.shape[1], _lib.ptr(x2), _lib.ptr(w2),
+    _lib.call("kca_gemv_dual_ln_f16" if x1.dtype == torch.float16 else "kca_gemv_dual_ln", x1.data_ptr(), w1.data_ptr(), w1.shape[1], _lib.ptr(x2), _lib.ptr(w2),
               w2.shape[1] if w2 is not None else 0, _lib.ptr(bias), ypart.data_ptr(), cnt.data_ptr(), h.data_ptr(),
               h_out.data_ptr(), gamma.data_ptr(), _lib.ptr(beta), float(eps), xn_out.data_ptr(), _lib.ptr(gamma2),
               _lib.ptr(beta2), _lib.ptr(xn2_out), w1.shape[0], _lib.stream())
@@ -313,14 +317,15 @@ def sample_logits(logits: torch.Tensor, *, temperature: torch.Tensor, top_k: tor
         out_ids = torch.empty(B, dtype=torch.int64, device=dev)
     if out_logprobs is None:
         out_logprobs = torch.empty(B, dtype=torch.float32, device=dev)
-    if logits.is_cuda and logits.dtype in (torch.bfloat16, torch.float32):
+    if logits.is_cuda and logits.dtype in (torch.bfloat16, torch.float32, torch.float16):
         if ws is None or ws.numel() < B * V:
             ws = torch.empty(B * V, device=dev, dtype=torch.float32)
         assert logits.stride(-1) == 1
         n_ban = ban_ids.shape[1] if ban_ids is not None else 0
         cnt = _sample_counters(dev, B)
         _lib.call("kca_sample_logits", logits.data_ptr(), logits.stride(0),
-                  int(logits.dtype == torch.bfloat16), B, V, temperature.data_ptr(), top_k.data_ptr(),
+                  {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}[logits.dtype], B, V,
+                  temperature.data_ptr(), top_k.data_ptr(),
                   top_p.data_ptr(), _lib.ptr(rep_penalty), _lib.ptr(seen), _lib.ptr(slots),
                   _lib.ptr(ban_ids), n_ban, _lib.ptr(seeds), int(step), ws.data_ptr(),
                   out_ids.data_ptr(), out_logprobs.data_ptr(), _lib.ptr(out_kept), _lib.ptr(cnt),

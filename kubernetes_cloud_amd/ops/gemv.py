@@ -56,6 +56,14 @@ def skinny_linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | No
     # M = 2 takes the register-resident K-split form only for K <= 8192 (GPT-J); BLOOM's K = 14336
     # QKV / fc_in at M = 2 would fall to the row-per-wave kernel, which hipBLASLt beats on big weights
     regs = M == 1 or K <= 8192 or small
+    if M == 1 and _lib.native_f16(x, weight) and K % 8 == 0 and weight.is_contiguous() \
+            and x.data_ptr() % 16 == 0 and weight.data_ptr() % 16 == 0 and (bias is None or bias.dtype == x.dtype):
+        # fp16 (FT / DS-Inference serving precision): the single-row GEMV's fp16 instantiation
+        if out is None:
+            out = torch.empty(M, N, device=x.device, dtype=x.dtype)
+        _lib.call("kca_skinny_gemm_f16", x.data_ptr(), x.stride(0), weight.data_ptr(), _lib.ptr(bias),
+                  out.data_ptr(), out.stride(0), M, N, K, int(act), _lib.stream())
+        return out
     if (_lib.use_native(x, weight) and ((M <= _SKINNY_MAX_M and regs) or (M <= 4 and small)) and K % 8 == 0
             and x.stride(1) == 1
             and x.stride(0) % 8 == 0
@@ -109,14 +117,15 @@ def ln_rows(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor | None, eps
     and xn = LN(h) -- ``kca_ln_rows`` (one register-resident workgroup per row)."""
     M, K = x.shape
     residuals = tuple(r for r in residuals if r is not None)
-    if _lib.use_native(x) and K % 8 == 0 and K <= 16384 and x.stride(1) == 1 and x.stride(0) % 8 == 0 \
+    f16 = _lib.native_f16(x, gamma)
+    if (_lib.use_native(x) or f16) and K % 8 == 0 and K <= 16384 and x.stride(1) == 1 and x.stride(0) % 8 == 0 \
             and all(r.is_contiguous() and r.shape == x.shape for r in residuals) and len(residuals) <= 2 \
             and gamma.is_contiguous() and (beta is None or beta.is_contiguous()):
         h = torch.empty(M, K, device=x.device, dtype=x.dtype) if residuals else x
         xn = torch.empty(M, K, device=x.device, dtype=x.dtype)
         r1 = residuals[0] if residuals else None
         r2 = residuals[1] if len(residuals) > 1 else None
-        _lib.call("kca_ln_rows", x.data_ptr(), x.stride(0), _lib.ptr(r1), _lib.ptr(r2),
+        _lib.call("kca_ln_rows_f16" if f16 else "kca_ln_rows", x.data_ptr(), x.stride(0), _lib.ptr(r1), _lib.ptr(r2),
                   h.data_ptr() if residuals else None, h.stride(0) if residuals else K, gamma.data_ptr(),
                   _lib.ptr(beta), float(eps), xn.data_ptr(), M, K, _lib.stream())
         return xn, h
@@ -132,7 +141,8 @@ def embed_ln_rows(wte: torch.Tensor, tokens: torch.Tensor, gamma: torch.Tensor, 
     chain[m] >= 0 (a token sampled by the previous step, still on the device) else tokens[m] --
     one launch (``kca_embed_ln_rows``) instead of the embedding gather, the position cast and the LN."""
     M, K = tokens.shape[0], wte.shape[1]
-    if not (_lib.use_native(wte) and K % 8 == 0 and K <= 16384 and wte.stride(1) == 1 and wte.stride(0) % 8 == 0
+    f16 = _lib.native_f16(wte, gamma)
+    if not ((_lib.use_native(wte) or f16) and K % 8 == 0 and K <= 16384 and wte.stride(1) == 1 and wte.stride(0) % 8 == 0
             and gamma.is_contiguous() and (beta is None or beta.is_contiguous()) and tokens.dtype == torch.int64):
         ids = tokens
         if chain is not None:
@@ -140,7 +150,7 @@ def embed_ln_rows(wte: torch.Tensor, tokens: torch.Tensor, gamma: torch.Tensor, 
         return ln_rows(wte[ids], gamma, beta, eps)
     h = torch.empty(M, K, device=wte.device, dtype=wte.dtype)
     xn = torch.empty(M, K, device=wte.device, dtype=wte.dtype)
-    _lib.call("kca_embed_ln_rows", wte.data_ptr(), wte.stride(0), tokens.data_ptr(), _lib.ptr(chain), _lib.ptr(prev),
+    _lib.call("kca_embed_ln_rows_f16" if f16 else "kca_embed_ln_rows", wte.data_ptr(), wte.stride(0), tokens.data_ptr(), _lib.ptr(chain), _lib.ptr(prev),
               wte.shape[0], h.data_ptr(), K, gamma.data_ptr(), _lib.ptr(beta), float(eps), xn.data_ptr(), M, K,
               _lib.stream())
     return xn, h

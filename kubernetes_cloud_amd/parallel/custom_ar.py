@@ -87,17 +87,19 @@ class XGMIAllReduce:
         self._open = _fn("kca_ipc_open", [P, ctypes.POINTER(P)])
         self._close = _fn("kca_ipc_close", [P])
         self._free = _fn("kca_ar_free", [P])
-        self._run = _fn("kca_ar_run", [ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(P), P, ctypes.c_int,
-                                       ctypes.c_int, ctypes.c_int, P, P, ctypes.c_longlong, ctypes.c_int,
-                                       ctypes.c_longlong, ctypes.c_int, P])
+        run_args = [ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(P), P, ctypes.c_int, ctypes.c_int,
+                    ctypes.c_int, P, P, ctypes.c_longlong, ctypes.c_int, ctypes.c_longlong, ctypes.c_int, P]
+        # element type -> entry (fp16: the serving precision of FT / DS-Inference; the kernels sum in fp32)
+        self._runs = {torch.bfloat16: _fn("kca_ar_run", run_args), torch.float16: _fn("kca_ar_run_f16", run_args)}
         self._err = _fn("kca_ar_error", [P, ctypes.POINTER(ctypes.c_int)])
-        self._res_ln = _fn("kca_ar_res_ln", [ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(P), P, ctypes.c_int,
-                                             ctypes.c_int, P, ctypes.c_int, ctypes.c_int, ctypes.c_longlong, P, P, P,
-                                             P, P, ctypes.c_float, P, P, P, P, P, P, P])
-        self._res_stats = _fn("kca_ar_res_stats", [ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(P), P,
-                                                   ctypes.c_int, ctypes.c_int, P, ctypes.c_int, ctypes.c_int,
-                                                   ctypes.c_int, ctypes.c_longlong, P, P, P, ctypes.c_float, P, P,
-                                                   P, P])
+        ln_args = [ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(P), P, ctypes.c_int, ctypes.c_int, P,
+                   ctypes.c_int, ctypes.c_int, ctypes.c_longlong, P, P, P, P, P, ctypes.c_float, P, P, P, P, P, P, P]
+        self._res_lns = {torch.bfloat16: _fn("kca_ar_res_ln", ln_args),
+                         torch.float16: _fn("kca_ar_res_ln_f16", ln_args)}
+        st_args = [ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(P), P, ctypes.c_int, ctypes.c_int, P,
+                   ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_longlong, P, P, P, ctypes.c_float, P, P, P, P]
+        self._res_statss = {torch.bfloat16: _fn("kca_ar_res_stats", st_args),
+                            torch.float16: _fn("kca_ar_res_stats_f16", st_args)}
         self._tails: dict = {}
         self.res_ln_calls = 0  # fused tail launches (tests assert the TP decode layer took them)
         self.res_stats_calls = 0
@@ -147,18 +149,18 @@ class XGMIAllReduce:
             dist.barrier(group=group)
 
     def eligible(self, t: torch.Tensor) -> bool:
-        return (t.is_cuda and t.dtype == torch.bfloat16 and t.is_contiguous() and t.numel() % 8 == 0
+        return (t.is_cuda and t.dtype in (torch.bfloat16, torch.float16) and t.is_contiguous() and t.numel() % 8 == 0
                 and 0 < t.numel() * 2 <= self.max_bytes and t.data_ptr() % 16 == 0)
 
     def all_reduce_(self, t: torch.Tensor, algo: int | None = None) -> torch.Tensor:
         n = t.numel()
         if not self.eligible(t):
-            raise ValueError("tensor not eligible for the xGMI all-reduce (bf16, contiguous, 16B-aligned, "
+            raise ValueError("tensor not eligible for the xGMI all-reduce (bf16/fp16, contiguous, 16B-aligned, "
                              f"numel % 8 == 0, <= {self.max_bytes} bytes)")
         if algo is None:
             algo = pick(2 * n, self.world, self.one_shot_max)
         blocks = blocks_for(n, self.world, algo, self.max_blocks)
-        rc = self._run(self._stage0, self._stage1, self._sig, P(self._ctl), self.rank, self.world, algo,
+        rc = self._runs[t.dtype](self._stage0, self._stage1, self._sig, P(self._ctl), self.rank, self.world, algo,
                        t.data_ptr(), t.data_ptr(), n, blocks, self.spin_limit, int(self.debug_delay),
                        _lib.stream())
         if rc != 0:
@@ -171,14 +173,14 @@ class XGMIAllReduce:
         """[world * t.numel()] bf16: rank r's ``t`` at ``out[r*n:(r+1)*n]``."""
         n = t.numel()
         if not self.eligible(t):
-            raise ValueError("tensor not eligible for the xGMI all-gather (bf16, contiguous, 16B-aligned, "
+            raise ValueError("tensor not eligible for the xGMI all-gather (bf16/fp16, contiguous, 16B-aligned, "
                              f"numel % 8 == 0, <= {self.max_bytes} bytes)")
         if out is None:
             out = torch.empty(self.world * n, device=t.device, dtype=t.dtype)
         if out.numel() != self.world * n or not out.is_contiguous() or out.data_ptr() % 16:
             raise ValueError("all-gather output must be a contiguous 16B-aligned [world * n] tensor")
         blocks = blocks_for(n, self.world, ONE_SHOT, self.max_blocks)
-        rc = self._run(self._stage0, self._stage1, self._sig, P(self._ctl), self.rank, self.world, ALL_GATHER,
+        rc = self._runs[t.dtype](self._stage0, self._stage1, self._sig, P(self._ctl), self.rank, self.world, ALL_GATHER,
                        t.data_ptr(), out.data_ptr(), n, blocks, self.spin_limit, int(self.debug_delay),
                        _lib.stream())
         if rc != 0:
@@ -190,15 +192,15 @@ class XGMIAllReduce:
     def res_ln(self, t: torch.Tensor, bias, h: torch.Tensor, h_out: torch.Tensor, gamma: torch.Tensor, beta,
                eps: float, xn_out: torch.Tensor, gamma2=None, beta2=None, xn2_out=None) -> None:
         """Close a row-parallel projection of the batch-1 decode layer in ONE launch: all-reduce this
-        rank's partial ``t`` ([1, N] bf16), then h_out = bf16(h + sum + bias) and xn_out = LayerNorm(h_out)
+        rank's partial ``t`` ([1, N] bf16 or fp16), then h_out = bf16(h + sum + bias) and xn_out = LayerNorm(h_out)
         (and xn2_out with gamma2 / beta2) -- no bias add, no LayerNorm launch after the collective
         (``kca_ar_res_ln``; graph-capturable like ``all_reduce_``)."""
         n = t.numel()
         if not self.eligible(t) or n > 16384:
-            raise ValueError("tensor not eligible for the fused all-reduce + LayerNorm (bf16 [N], N <= 16384)")
+            raise ValueError("tensor not eligible for the fused all-reduce + LayerNorm (bf16/fp16 [N], N <= 16384)")
         ws = self._tail_ws(t.device)
         blocks = max(1, min(64, -(-(n // 8) // 128)))
-        rc = self._res_ln(self._stage0, self._stage1, self._sig, P(self._ctl), self.rank, self.world, t.data_ptr(),
+        rc = self._res_lns[t.dtype](self._stage0, self._stage1, self._sig, P(self._ctl), self.rank, self.world, t.data_ptr(),
                           n, blocks, self.spin_limit, _lib.ptr(bias), h.data_ptr(), h_out.data_ptr(),
                           gamma.data_ptr(), _lib.ptr(beta), float(eps), xn_out.data_ptr(), _lib.ptr(gamma2),
                           _lib.ptr(beta2), _lib.ptr(xn2_out), ws[0].data_ptr(), ws[1].data_ptr(), _lib.stream())
@@ -210,7 +212,7 @@ class XGMIAllReduce:
 
     def res_stats(self, t: torch.Tensor, bias, h: torch.Tensor, h_out: torch.Tensor, stats, eps: float) -> None:
         """Close a row-parallel projection of the batch 2..64 matrix-core decode layer in ONE launch:
-        all-reduce this rank's partial ``t`` ([M, N] bf16), h_out = bf16(h + sum + bias), and the next
+        all-reduce this rank's partial ``t`` ([M, N] bf16 or fp16), h_out = bf16(h + sum + bias), and the next
         LayerNorm's per-row (mean, rstd) into ``stats`` (an ``ops.skinny_mm.RowStatsBuf``), which the
         next projection applies on load (``kca_ar_res_stats``; graph-capturable)."""
         M, N = t.shape
@@ -219,7 +221,7 @@ class XGMIAllReduce:
                              "N % 64 == 0, N <= 16384)")
         groups = t.numel() // 64
         blocks = max(1, min(self.max_blocks, -(-groups // 32)))
-        rc = self._res_stats(self._stage0, self._stage1, self._sig, P(self._ctl), self.rank, self.world,
+        rc = self._res_statss[t.dtype](self._stage0, self._stage1, self._sig, P(self._ctl), self.rank, self.world,
                              t.data_ptr(), M, N, blocks, self.spin_limit, _lib.ptr(bias), h.data_ptr(),
                              h_out.data_ptr(), float(eps), stats.part.data_ptr(), stats.stats.data_ptr(),
                              stats.cnt.data_ptr(), _lib.stream())

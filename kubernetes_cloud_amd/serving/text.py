@@ -36,7 +36,7 @@ def load_lm(path: str, device=None, dtype=torch.bfloat16, tensors_file: str | No
     from ..models.config import PRESETS_HF, preset
     dev = torch.device(device) if device is not None else (
         torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu"))
-    if dev.type == "cpu" and dtype == torch.bfloat16:
+    if dev.type == "cpu" and dtype in (torch.bfloat16, torch.float16):
         dtype = torch.float32
     t0 = time.perf_counter()
     tok = None

@@ -31,7 +31,9 @@ def build_tp_engine_model(args, rank, world, group):
     from ..parallel.tensor_parallel import load_tp_model
     dev = torch.device("cuda", int(os.getenv("LOCAL_RANK", rank))) if torch.cuda.is_available() else \
         torch.device("cpu")
-    dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
+    # DS-Inference serves BLOOM in fp16 (bloom-176b-deepspeed isvc-patch): the default here too
+    dtype = {"fp16": torch.float16, "bf16": torch.bfloat16}[getattr(args, "dtype", "fp16")] \
+        if dev.type == "cuda" else torch.float32
     if args.random_init:
         cfg = preset(args.random_init)
         if args.layers:
@@ -59,6 +61,7 @@ def main(argv=None):
     ap.add_argument("--max-len", type=int, default=2048)
     ap.add_argument("--random-init", default=None, help="preset name: random weights (benchmarks)")
     ap.add_argument("--layers", type=int, default=0)
+    ap.add_argument("--dtype", choices=["fp16", "bf16"], default=os.getenv("KCA_SERVE_DTYPE", "fp16"))
     ap.add_argument("--model-name", default=os.getenv("MODEL_NAME", ""),
                     help="org/repo resolved in the read-only HF hub cache (bloom-176b-deepspeed layout)")
     args = ap.parse_args(argv)

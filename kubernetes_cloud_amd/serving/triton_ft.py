@@ -93,7 +93,7 @@ def parse_config_pbtxt(text: str) -> dict:
     return out
 
 
-def write_model_store(model_dir: str, store_dir: str, tensor_para_size: int = 1, data_type: str = "bf16",
+def write_model_store(model_dir: str, store_dir: str, tensor_para_size: int = 1, data_type: str = "fp16",
                       name: str = "fastertransformer") -> str:
     """HF checkpoint dir -> ``{store}/{name}/config.pbtxt`` + ``1/model.tensors``."""
     import torch
@@ -176,7 +176,12 @@ class FasterTransformerModel(Model):
         tp = int(self.config["parameters"].get("tensor_para_size", "1"))
         if tp != 1:
             log.warning("tensor_para_size=%d: serve with the TP launcher (serving.tp_server); loading TP=1", tp)
-        model, tok = load_lm(ck, tensors_file=os.path.join(ck, "model.tensors"))
+        # the store's data_type is the serving precision (FT's default fp16): the decode step runs it natively
+        # (fp16 instantiations of every decode kernel), no conversion to bf16 at load
+        import torch
+        dt = {"fp16": torch.float16, "bf16": torch.bfloat16, "fp32": torch.float32}[
+            self.config["parameters"].get("data_type", "fp16")]
+        model, tok = load_lm(ck, dtype=dt, tensors_file=os.path.join(ck, "model.tensors"))
         self.generator = TextGenerator(model, tok, max_slots=int(os.getenv("MAX_BATCH", 64)))
         if self.end_id is None:
             self.end_id = tok.eos_token_id if tok is not None else model.cfg.vocab_size - 1
@@ -350,7 +355,7 @@ def convert_main(argv=None):
     ap.add_argument("--model-dir", required=True)
     ap.add_argument("--output-dir", required=True)
     ap.add_argument("--n-inference-gpus", "--tensor-parallelism", dest="tp", type=int, default=1)
-    ap.add_argument("--data-type", default="bf16", choices=["bf16", "fp16", "fp32"])
+    ap.add_argument("--data-type", default="fp16", choices=["bf16", "fp16", "fp32"])
     a = ap.parse_args(argv)
     print(write_model_store(a.model_dir, a.output_dir, a.tp, a.data_type))
 

@@ -956,6 +956,44 @@ def test_engine_batched_mfma_layer(preset, B):
             _check_against_forward(m, p, o)
 
 
+@pytest.mark.parametrize("preset", ["gpt-j-6b", "gpt-neox-20b", "bloom-560m"])
+def test_engine_fp16_native_decode(preset, monkeypatch):
+    """fp16 serving (the precision of BASELINE config 4's FasterTransformer /
+    DS-Inference rows) runs the native decode step -- the fused GEMV layer at batch 1, the matrix-core
+    layer at batch > 1, the fp16 attention / LayerNorm-row / embedding-head instantiations and the sampler
+    reading fp16 logits -- with HIP graphs: the PyTorch fallbacks of the decode attention and the sampler
+    are made to fail, greedy tokens match a full fp16 forward, and seeded sampling is reproducible."""
+    from kubernetes_cloud_amd.engine.llm_engine import LLMEngine, SamplingParams
+    from kubernetes_cloud_amd.models.causal_lm import build_model
+    from kubernetes_cloud_amd.models.config import PRESETS_HF, LMConfig
+    from kubernetes_cloud_amd.ops import decode as dmod
+    small = {"gpt-j-6b": dict(n_embd=1024, n_layer=3, n_head=4, rotary_dim=64, n_positions=512),
+             "gpt-neox-20b": dict(hidden_size=768, num_hidden_layers=3, num_attention_heads=8,
+                                  intermediate_size=3072, max_position_embeddings=512),
+             "bloom-560m": dict(hidden_size=512, n_layer=3, n_head=4)}[preset]
+    cfg = dict(PRESETS_HF[preset])
+    cfg.update(small)
+    m = build_model(LMConfig.from_hf(cfg), device=dev, dtype=torch.float16, seed=0)
+
+    def boom(*a, **k):
+        raise AssertionError("fp16 decode fell back to PyTorch")
+    monkeypatch.setattr(dmod, "decode_attention_reference", boom)
+    monkeypatch.setattr(dmod, "sample_logits_reference", boom)
+    g = torch.Generator().manual_seed(3)
+    for B in (1, 5):
+        prompts = [[int(x) for x in torch.randint(0, 1000, (30 + 7 * i,), generator=g)] for i in range(B)]
+        eng = LLMEngine(m, max_slots=B, max_len=256, use_graphs=True)
+        assert eng.runner._batched_ok
+        outs = [r.output for r in eng.generate(prompts, SamplingParams(max_new_tokens=12, do_sample=False))]
+        assert (eng.runner.fused_steps if B == 1 else eng.runner.batched_steps) > 0
+        for p, o in zip(prompts, outs):
+            _check_against_forward(m, p, o)
+        sp = SamplingParams(max_new_tokens=8, do_sample=True, temperature=0.9, top_k=40, top_p=0.9, seed=17)
+        a = [r.output for r in eng.generate(prompts, sp)]
+        b = [r.output for r in eng.generate(prompts, sp)]
+        assert a == b and all(len(x) == 8 for x in a)
+
+
 def test_engine_batched_mfma_bloom_tp_emulated_rank():
     """Rank 0 of a TP=4 BLOOM layout (parallel/tp_emulation.py) at batch 6 through the matrix-core layer:
     shard shapes, vocab-parallel head gathered by the stand-in group."""
@@ -974,18 +1012,20 @@ def test_engine_batched_mfma_bloom_tp_emulated_rank():
         _check_against_forward(m, p, o)
 
 
-def test_engine_emulated_rank_runs_real_tp_tails():
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_engine_emulated_rank_runs_real_tp_tails(dtype):
     """with a rank-local custom all-reduce registered for the emulated group, rank 0 of a
     TP=4 BLOOM layout closes every row-parallel projection with the deployment's fused all-reduce tails
-    (kca_ar_res_ln at batch 1, kca_ar_res_stats at batch > 1) -- the kernels bench/bloom_tp_bench.py then
-    measures -- and still matches the model's own forward through the same stand-in collectives."""
+    (kca_ar_res_ln at batch 1, kca_ar_res_stats at batch > 1; fp16 -- DS-Inference's precision -- their
+    _f16 twins) -- the kernels bench/bloom_tp_bench.py then measures -- and still
+    matches the model's own forward through the same stand-in collectives."""
     from kubernetes_cloud_amd.engine.llm_engine import LLMEngine, SamplingParams
     from kubernetes_cloud_amd.models.config import PRESETS_HF, LMConfig
     from kubernetes_cloud_amd.parallel.custom_ar import register
     from kubernetes_cloud_amd.parallel.tp_emulation import emulated_rank_model
     cfg = dict(PRESETS_HF["bloom-560m"])
     cfg.update(hidden_size=1024, n_layer=3, n_head=16, vocab_size=4096)
-    m = emulated_rank_model(LMConfig.from_hf(cfg), 4, 0, device=dev)
+    m = emulated_rank_model(LMConfig.from_hf(cfg), 4, 0, device=dev, dtype=dtype)
     ar = register(m.h[0].attn.out.group)
     assert ar is not None and ar.world == 1
     g = torch.Generator().manual_seed(13)

@@ -24,14 +24,14 @@ def _port():
         return s.getsockname()[1]
 
 
-def _model(preset):
+def _model(preset, dtype=torch.bfloat16):
     from kubernetes_cloud_amd.models.causal_lm import build_model
     from kubernetes_cloud_amd.models.config import PRESETS_HF, LMConfig
     cfg = dict(PRESETS_HF[preset])
     cfg.update({"bloom-560m": dict(hidden_size=512, n_layer=2, n_head=8, vocab_size=1024),
                 "gpt-j-6b": dict(n_embd=512, n_layer=2, n_head=8, rotary_dim=32, vocab_size=1024,
                                  n_positions=512)}[preset])
-    return build_model(LMConfig.from_hf(cfg), device="cuda", dtype=torch.bfloat16, seed=0)
+    return build_model(LMConfig.from_hf(cfg), device="cuda", dtype=dtype, seed=0)
 
 
 PROMPTS = [[5, 9, 2, 7], list(range(10, 40)), [3, 3, 3], list(range(100, 117))]
@@ -108,7 +108,7 @@ def test_tp2_engine_on_gpu_matches_unsharded(preset):
         assert _near_tie_ok(full, PROMPTS[1], res["beam"][0], res["beam_ref"][0])
 
 
-def _worker_fused(rank, world, port, q):
+def _worker_fused(rank, world, port, q, dt="bf16"):
     """TP=2 BLOOM-shaped model with HIP graphs (the logits all-gather on the custom all-reduce is
     capturable): batch 1 (fused layer, kca_ar_res_ln tails) and batch 3 (matrix-core layer,
     kca_ar_res_stats tails), then the same requests with KCA_DECODE_FUSED=0 (per-projection path)."""
@@ -121,7 +121,7 @@ def _worker_fused(rank, world, port, q):
     from kubernetes_cloud_amd.parallel import custom_ar
     from kubernetes_cloud_amd.parallel.tensor_parallel import shard_model_from_full
     try:
-        full = _model("bloom-560m")
+        full = _model("bloom-560m", getattr(torch, dt))
         group = dist.new_group(backend="gloo")
         ar = custom_ar.register(group, max_bytes=4 << 20)
         tp = shard_model_from_full(full, rank, world, group)
@@ -158,22 +158,25 @@ def _worker_fused(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_tp2_fused_tails_b1_and_batched_with_graphs():
+@pytest.mark.parametrize("dt", ["bf16", "float16"])
+def test_tp2_fused_tails_b1_and_batched_with_graphs(dt):
     """VERDICT r5 item 2 / ADVICE r5: the real-TP decode layer that BLOOM TP=8 serving runs -- the
     row-parallel projections closed by the custom all-reduce's fused residual + LayerNorm tail at batch 1
     (kca_ar_res_ln) and residual + row-statistics tail at batch > 1 (kca_ar_res_stats), HIP graphs on --
-    matches the unsharded model and the per-projection path, and the fused tails really ran."""
+    matches the unsharded model and the per-projection path, and the fused tails really ran -- in bf16 and
+    in fp16 (DS-Inference's precision: the *_f16 instantiations of both tails)."""
+    dt = {"bf16": "bfloat16"}.get(dt, dt)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_worker_fused, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_worker_fused, args=(r, 2, port, q, dt)) for r in range(2)]
     for p in ps:
         p.start()
     got = dict(q.get(timeout=300) for _ in range(2))
     for p in ps:
         p.join(timeout=120)
         assert p.exitcode == 0
-    full = _model("bloom-560m")
+    full = _model("bloom-560m", getattr(torch, dt))
     r0 = got[0]
     assert r0["fused_ok"] == (True, True, True)
     for rank in (0, 1):
