@@ -111,9 +111,10 @@ __device__ __forceinline__ void store8_t(uint16_t* p, const float (&x)[8]) {
 }
 
 // The two elements of a packed 32-bit pair (low / high half), and acc + w.lo * x.lo + w.hi * x.hi of
-// two pairs -- the GEMV inner step. bf16: a shift / mask per element and two FMAs (the original
-// expressions); fp16: one v_dot2_f32_f16 (fp32 accumulation).
+// two pairs -- the GEMV inner step: one v_dot2c_f32_bf16 / v_dot2_f32_f16 (fp32 accumulation) instead of
+// two unpacks and two FMAs per pair (KCA_BF16_FMA_GEMV: the FMA form, for A/B).
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 template <int DT>
 __device__ __forceinline__ float lo2f(uint32_t q) {
   if constexpr (DT == 0) return __uint_as_float(q << 16);
@@ -127,8 +128,13 @@ __device__ __forceinline__ float hi2f(uint32_t q) {
 template <int DT>
 __device__ __forceinline__ float dot2_acc(uint32_t w, uint32_t x, float acc) {
   if constexpr (DT == 0) {
+#ifdef KCA_BF16_FMA_GEMV
     acc = fmaf(lo2f<0>(w), lo2f<0>(x), acc);
     return fmaf(hi2f<0>(w), hi2f<0>(x), acc);
+#else
+    return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, w), __builtin_bit_cast(bf16x2_t, x), acc,
+                                           false);
+#endif
   } else {
     return __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2, w), __builtin_bit_cast(f16x2, x), acc, false);
   }

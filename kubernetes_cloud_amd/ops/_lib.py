@@ -110,14 +110,14 @@ _SIGS = {
 }
 
 
+# fused decode layer (batch 1): kca_decode_prep_attn's arguments (minus the stream), then the fc_in
+# GEMV's x, W, bias, y, N, K, act, then the stream
+_SIGS["kca_decode_prep_attn_gemv"] = _SIGS["kca_decode_prep_attn"][:-2] + [P, P, P, P, I, I, I, I, P]
+
 # fp16 twins of the serving kernels (same arguments)
 for _n in ("kca_decode_prep_attn", "kca_ln_rows", "kca_embed_ln_rows", "kca_decode_prep_attn_gemv",
            "kca_gemv_dual_ln", "kca_skinny_gemm"):
     _SIGS[_n + "_f16"] = _SIGS[_n]
-
-# fused decode layer (batch 1): kca_decode_prep_attn's arguments (minus the stream), then the fc_in
-# GEMV's x, W, bias, y, N, K, act, then the stream
-_SIGS["kca_decode_prep_attn_gemv"] = _SIGS["kca_decode_prep_attn"][:-2] + [P, P, P, P, I, I, I, I, P]
 
 
 def _load():
