@@ -501,6 +501,14 @@ KCA_API int kca_skinny_set_splitk(int on) {
   return 0;
 }
 
+// rows per workgroup of the M = 1 GEMV when K <= 2048 (a BLOOM TP=8 out-projection row is 3.5 KB: two
+// rows give a workgroup 7 KB of weight and the launch 7168 workgroups) -- A/B knob, 2 / 4 / 8
+static int g_gemv_smallk_rows = 2;
+KCA_API int kca_skinny_set_smallk(int rows) {
+  g_gemv_smallk_rows = (rows == 4 || rows == 8) ? rows : 2;
+  return 0;
+}
+
 template <int M, bool LN = false>
 static void launch_skinny(const bf16_t* x, long long ldx, const bf16_t* w, const bf16_t* bias,
                           bf16_t* y, long long ldy, int mv, int N, int K, int act, hipStream_t s,
@@ -515,6 +523,16 @@ static void launch_skinny(const bf16_t* x, long long ldx, const bf16_t* w, const
     // 2 weight rows per workgroup: twice the workgroups of the 4-row form, a shorter ragged end to
     // each launch (same box: BLOOM TP=8 B=1 9.03 -> 8.97 ms, GPT-J B=1 2.21 -> 2.20 ms;
     // profiles/decode_launch_structure_ab_r5.txt)
+    if (!LN && K <= 2048 && g_gemv_smallk_rows == 8) {
+      hipLaunchKernelGGL((gemv1_kernel<8, LN>), dim3((N + 7) / 8), dim3(256), 0, s, x, w, bias, y, N, K, act, ln, 0LL,
+                         0LL, 1);
+      return;
+    }
+    if (!LN && K <= 2048 && g_gemv_smallk_rows == 4) {
+      hipLaunchKernelGGL((gemv1_kernel<4, LN>), dim3((N + 3) / 4), dim3(256), 0, s, x, w, bias, y, N, K, act, ln, 0LL,
+                         0LL, 1);
+      return;
+    }
     constexpr int R1 = 2;
     const dim3 grid((N + R1 - 1) / R1);
     hipLaunchKernelGGL((gemv1_kernel<R1, LN>), grid, dim3(256), 0, s, x, w, bias, y, N, K, act, ln, 0LL, 0LL, 1);

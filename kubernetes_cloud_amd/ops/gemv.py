@@ -35,6 +35,9 @@ def _set_mode():
         _MODE_SET = True
         if os.environ.get("KCA_SKINNY_SPLITK", "1") in ("0", "false") and _lib.has("kca_skinny_set_splitk"):
             _lib.call("kca_skinny_set_splitk", 0)
+        r = int(os.environ.get("KCA_GEMV_SMALLK_R", "0"))
+        if r and _lib.has("kca_skinny_set_smallk"):
+            _lib.call("kca_skinny_set_smallk", r)
 
 
 # rows up to which every weight streams through the skinny kernel (A/B knob): M = 1 and M = 2 run the
