@@ -93,6 +93,23 @@ __device__ __forceinline__ bool ar_sync(const ARPeers& peers, ARCtl* ctl, int ra
                                         long long spin_limit) {
   __shared__ int s_ok;
   const int b = blockIdx.x, tid = threadIdx.x;
+#ifndef KCA_AR_FULL_FENCE
+  // the staging and the flags are device-uncached (MTYPE UC, hipDeviceMallocUncached): a drained store
+  // is at the memory side, so the data -> flag order needs no L2 writeback / invalidate (the system-
+  // scope release / acquire, KCA_AR_FULL_FENCE): drain, barrier, relaxed flag store; relaxed polls.
+  // Per call at world 1: res_stats 13.3 -> 10.3 us (B=8), 24.3 -> 16.8 (B=32); BLOOM TP=8 rank
+  // B=8 12.04 -> 11.65 ms/token (profiles/ar_tail_r6.jsonl)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) s_ok = 1;
+  if (tid < W) __hip_atomic_store(&peers.sig[tid]->flag[phase][b][rank], call, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_SYSTEM);
+  __syncthreads();
+  if (tid < W) {
+    const uint32_t* f = &peers.sig[rank]->flag[phase][b][tid];
+    long long spins = 0;
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < call) {
+#else
   __threadfence_system();
   __syncthreads();
   if (tid == 0) s_ok = 1;
@@ -102,6 +119,7 @@ __device__ __forceinline__ bool ar_sync(const ARPeers& peers, ARCtl* ctl, int ra
     const uint32_t* f = &peers.sig[rank]->flag[phase][b][tid];
     long long spins = 0;
     while (ld_sys(f) < call) {
+#endif
       if (++spins > spin_limit) {
         __hip_atomic_fetch_or(&ctl->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_ok = 0;
@@ -287,6 +305,134 @@ __global__ __launch_bounds__(256) void ar_res_ln_kernel(ARPeers peers, ARCtl* ct
   dual_ln_arrive_tail<PER, DT>(a);
 }
 
+// The same close with the LayerNorm distributed over the launch (the default; kca_ar_set_variant(1)
+// selects the last-arriver form above): one 16-byte chunk per thread (blocks = ceil(N / 2048)), the
+// thread's residual / bias / gamma / beta requested before the sync round, h' kept in registers; each
+// block publishes its slice's (mean, M2), a launch-wide barrier (all blocks co-resident: <= 8 at N <=
+// 16384), every block merges the partials (Chan) and normalises its own slice. No block re-reads h'
+// and no single block walks the whole row (the last-arriver tail: ~10.4 us of a 10.8-us call at
+// N = 14336, world 1).
+template <int W, int DT>
+__global__ __launch_bounds__(256) void ar_res_ln_dist_kernel(ARPeers peers, ARCtl* ctl, int rank,
+                                                             const bf16_t* __restrict__ in, long long n8,
+                                                             long long spin_limit, DualLn a) {
+  __shared__ float red[16];
+  __shared__ float s_stat[2];
+  __shared__ int s_gen_ok;
+  const int b = blockIdx.x, nb = gridDim.x, tid = threadIdx.x, lane = tid & 63;
+  const long long i = (long long)b * 256 + tid;
+  const bool live = i < n8;
+  // local operands first: independent of the peers
+  u32x4 xin = {0u, 0u, 0u, 0u};
+  float h8[8], b8[8], g8[8], e8[8];
+  if (live) {
+    xin = *reinterpret_cast<const u32x4*>(reinterpret_cast<const uint4*>(in) + i);
+    load8_t<DT>(a.h + i * 8, h8);
+    load8_t<DT>(a.gamma + i * 8, g8);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) b8[j] = e8[j] = 0.f;
+  if (live && a.bias) load8_t<DT>(a.bias + i * 8, b8);
+  if (live && a.beta) load8_t<DT>(a.beta + i * 8, e8);
+  const uint32_t call = ar_begin(ctl);
+  const int par = call & 1;
+  if (live) reinterpret_cast<uint4*>(peers.stage[par][rank])[i] = make_uint4(xin[0], xin[1], xin[2], xin[3]);
+  const bool ok = ar_sync<W>(peers, ctl, rank, 0, call, spin_limit);
+  float v[8];
+  float sm = 0.f;
+  if (live) {
+    float acc[8];
+    sum_peers8<W, DT>(peers, par, i, acc);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      v[j] = ok ? h8[j] + (acc[j] + b8[j]) : __int_as_float(0x7fc00000);
+      v[j] = e2f<DT>(f2e<DT>(v[j]));  // h' rounded (the statistics are over the rounded stream)
+      sm += v[j];
+    }
+    store8_t<DT>(a.h_out + i * 8, v);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = 0.f;
+  }
+  // this block's slice: (mean, M2) over its cnt = 8 * live-chunks values
+  const long long hi = min(n8, (long long)(b + 1) * 256);
+  const float cnt = 8.f * (float)(hi - (long long)b * 256);
+  const float mb = block_sum(sm, red) / cnt;
+  float q = 0.f;
+  if (live) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) q += (v[j] - mb) * (v[j] - mb);
+  }
+  const float m2b = block_sum(q, red + 8);
+  // launch-wide barrier: publish, count, the last arrival re-arms the count and advances the generation
+  unsigned* bar = a.cnt + 8;  // [0] count, [8] generation (the last-arriver form's counters untouched)
+  if (tid == 0) {
+    st_pub(a.ypart + 2 * b, mb);
+    st_pub(a.ypart + 2 * b + 1, m2b);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned gen = __hip_atomic_load(bar + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int good = 1;
+    if (__hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)nb - 1) {
+      __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(bar + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      long long spins = 0;
+      while (__hip_atomic_load(bar + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
+        if (++spins > spin_limit) {
+          __hip_atomic_fetch_or(&ctl->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          good = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    s_gen_ok = good;
+  }
+  __syncthreads();
+  if (tid < 64) {  // wave 0 merges the nb (<= 64) partials
+    float nt = 0.f, mt = 0.f, qt = 0.f;
+    if (lane < nb) {
+      const long long lo_t = (long long)lane * 256, hi_t = min(n8, lo_t + 256);
+      nt = 8.f * (float)(hi_t - lo_t);
+      mt = a.ypart[2 * lane];
+      qt = a.ypart[2 * lane + 1];
+    }
+    const float ntot = wave_sum(nt);
+    const float mean = wave_sum(nt * mt) / ntot;
+    const float m2 = wave_sum(qt + nt * (mt - mean) * (mt - mean));
+    if (lane == 0) {
+      s_stat[0] = mean;
+      s_stat[1] = s_gen_ok ? rsqrtf(m2 / ntot + a.eps) : __int_as_float(0x7fc00000);
+    }
+  }
+  __syncthreads();
+  const float mean = s_stat[0], rstd = s_stat[1];
+  if (live) {
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      v[j] = (v[j] - mean) * rstd;
+      o[j] = v[j] * g8[j] + e8[j];
+    }
+    store8_t<DT>(a.xn_out + i * 8, o);
+    if (a.xn2_out) {
+      load8_t<DT>(a.gamma2 + i * 8, g8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) e8[j] = 0.f;
+      if (a.beta2) load8_t<DT>(a.beta2 + i * 8, e8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = v[j] * g8[j] + e8[j];
+      store8_t<DT>(a.xn2_out + i * 8, o);
+    }
+  }
+  ar_end(ctl, call);
+}
+
 // ----------------------------------------- one-shot + residual + row statistics (TP decode, M rows)
 // The batch 2..64 form of ar_res_ln_kernel for the matrix-core decode layer (skinny_mfma.hip): `in` is
 // this rank's partial [M, N] (row-parallel out-projection / fc_out), every rank stages it, one sync
@@ -308,15 +454,39 @@ __global__ __launch_bounds__(256) void ar_res_stats_kernel(ARPeers peers, ARCtl*
   const long long lo = b * gper * 8, hi = min(n8, lo + gper * 8);
   uint4* mine = reinterpret_cast<uint4*>(peers.stage[par][rank]);
   for (long long i = lo + tid; i < hi; i += blockDim.x) mine[i] = reinterpret_cast<const uint4*>(in)[i];
-  const bool ok = ar_sync<W>(peers, ctl, rank, 0, call, spin_limit);
   const long long n8row = rs.N / 8;
-  for (long long i = lo + tid; i < hi; i += blockDim.x) {  // (8-thread groups stay whole: lo, hi, 256 % 8)
+  // the first PRE chunks' residual / bias are requested before the sync round (local, peer-independent)
+  constexpr int PRE = 2;
+  u32x4 hpre[PRE], bpre[PRE];
+#pragma unroll
+  for (int u = 0; u < PRE; ++u) {
+    const long long i = lo + tid + (long long)u * blockDim.x;
+    hpre[u] = bpre[u] = u32x4{0u, 0u, 0u, 0u};
+    if (i < hi) {
+      hpre[u] = *reinterpret_cast<const u32x4*>(h + i * 8);
+      if (bias) bpre[u] = *reinterpret_cast<const u32x4*>(bias + (i % n8row) * 8);
+    }
+  }
+  const bool ok = ar_sync<W>(peers, ctl, rank, 0, call, spin_limit);
+  int it = 0;
+  for (long long i = lo + tid; i < hi; i += blockDim.x, ++it) {  // (8-thread groups stay whole: lo, hi, 256 % 8)
     float acc[8];
     sum_peers8<W, DT>(peers, par, i, acc);
     const long long row = i / n8row, col = (i % n8row) * 8;
     float h8[8], b8[8];
-    load8_t<DT>(h + i * 8, h8);
-    if (bias) load8_t<DT>(bias + col, b8);
+    if (it < PRE) {
+      const u32x4 hq = it == 0 ? hpre[0] : hpre[1], bq = it == 0 ? bpre[0] : bpre[1];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        h8[2 * j] = e2f<DT>(hq[j] & 0xffffu);
+        h8[2 * j + 1] = e2f<DT>(hq[j] >> 16);
+        b8[2 * j] = e2f<DT>(bq[j] & 0xffffu);
+        b8[2 * j + 1] = e2f<DT>(bq[j] >> 16);
+      }
+    } else {
+      load8_t<DT>(h + i * 8, h8);
+      if (bias) load8_t<DT>(bias + col, b8);
+    }
     float v[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -440,6 +610,12 @@ KCA_API int kca_ar_error(const void* ctl, int* err) {
 // then h_out = bf16(h + sum + bias), xn_out = LN(h_out) (gamma / beta / eps; gamma2 -> xn2_out: a
 // second LayerNorm of the same h_out). ypart: >= N fp32 local words; cnt: 32 * 65 zero-initialised
 // arrival counters (re-armed by every call). N % 8 == 0, N <= 16384, 2N bytes <= the staging size.
+static int g_ar_ln_variant = 0;  // 0: distributed LayerNorm (ar_res_ln_dist_kernel), 1: last-arriver tail
+KCA_API int kca_ar_set_variant(int v) {
+  g_ar_ln_variant = v ? 1 : 0;
+  return 0;
+}
+
 template <int DT>
 static int ar_res_ln(void* const* stage0, void* const* stage1, void* const* sig, void* ctl, int rank, int world,
                      const void* in, int N, int blocks, long long spin_limit, const void* bias, const void* h,
@@ -462,6 +638,22 @@ static int ar_res_ln(void* const* stage0, void* const* stage1, void* const* sig,
                  (const bf16_t*)gamma2, (const bf16_t*)beta2, (bf16_t*)xn2_out, N, 0, 0};
   ARCtl* c = (ARCtl*)ctl;
   const long long n8 = N / 8;
+  if (g_ar_ln_variant == 0) {
+    const int nb = (int)((n8 + 255) / 256);
+    switch (world) {
+#define KCA_AR_LND_CASE(WW)                                                                                     \
+  case WW:                                                                                                      \
+    hipLaunchKernelGGL((ar_res_ln_dist_kernel<WW, DT>), dim3(nb), dim3(256), 0, stream, p, c, rank,             \
+                       (const bf16_t*)in, n8, spin_limit, a);                                                   \
+    break;
+      KCA_AR_LND_CASE(1) KCA_AR_LND_CASE(2) KCA_AR_LND_CASE(3) KCA_AR_LND_CASE(4) KCA_AR_LND_CASE(5)
+      KCA_AR_LND_CASE(6) KCA_AR_LND_CASE(7) KCA_AR_LND_CASE(8)
+#undef KCA_AR_LND_CASE
+      default:
+        return 3;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : 4;
+  }
   switch (world) {
 #define KCA_AR_LN_CASE(WW)                                                                                      \
   case WW:                                                                                                      \

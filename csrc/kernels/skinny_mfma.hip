@@ -93,7 +93,7 @@ struct MmArgs {
   unsigned* bcnt; // per-N-block arrival counters (ks > 1), zero-initialised, re-armed every launch
   long long ws_floats;
   int bcnt_n;
-  int pad_;
+  int pf;         // weight chunks in flight per wave, 1..3 (0: host picks)
 };
 
 // One finished 16x16 tile: rows n_base + 4*(lane>>4) + i (i < 4) of the output's N axis, column m =
@@ -169,7 +169,7 @@ struct MmTile {
   static_assert(PPR >= 16 && PPR <= 64, "swizzle needs 16..64 pieces per row");
 };
 
-template <int DT, int MT, int NRW, int KC, int WV, bool LN>
+template <int DT, int MT, int NRW, int KC, int WV, bool LN, int PF>
 __global__ __launch_bounds__(WV * 64) void mm_skinny_kernel(MmArgs a) {
   using T = MmTile<MT, NRW, KC, WV>;
   extern __shared__ __attribute__((aligned(16))) uint16_t mm_lds[];  // xs[2][MT*16][KC], slots[WV][NRW*16][KC]
@@ -273,9 +273,10 @@ __global__ __launch_bounds__(WV * 64) void mm_skinny_kernel(MmArgs a) {
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[nr][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // one chunk: its weight registers -> the wave's LDS slot, then the next chunk is requested into the
-  // freed registers, the next activation chunk is staged, the MFMAs run (one chunk in flight per wave:
-  // two measured no faster, the registers cost occupancy -- profiles/mm_sweep_r6/)
+  // one chunk: its weight registers -> the wave's LDS slot, then chunk c + PF is requested into the
+  // freed registers (PF register sets in a ring: PF chunks of weight in flight per wave), the next
+  // activation chunk is staged, the MFMAs run. PF > 1 pays where the LDS, not the registers, caps the
+  // resident workgroups (M = 32: 64 KB per workgroup, 2 per CU)
   u32x4v xr[T::XP], gv = {0u, 0u, 0u, 0u}, bv = {0u, 0u, 0u, 0u};
   auto chunk = [&](int c, u32x4v (&w)[NRW][T::NI]) {
     const int buf = (c - c_lo) & 1;
@@ -287,7 +288,7 @@ __global__ __launch_bounds__(WV * 64) void mm_skinny_kernel(MmArgs a) {
         const int row = i * T::RPI + lr;
         *reinterpret_cast<u32x4v*>(slot + (nr * 16 + row) * KC + ((lp ^ (row & 15)) << 3)) = w[nr][i];
       }
-    if (c + 1 < c_hi) load_w(c + 1, w);
+    if (c + PF < c_hi) load_w(c + PF, w);
     const bool nx = c + 1 < c_hi;
     if (nx) load_x(c + 1, xr, gv, bv);
     wave_lds_sync();
@@ -308,14 +309,20 @@ __global__ __launch_bounds__(WV * 64) void mm_skinny_kernel(MmArgs a) {
     if (nx) store_x(xr, gv, bv, c + 1, buf ^ 1);
     __syncthreads();
   };
-  u32x4v wa[NRW][T::NI];
+  u32x4v wa[PF][NRW][T::NI];
+#pragma unroll
+  for (int q = 0; q < PF; ++q)
+    if (c_lo + q < c_hi) load_w(c_lo + q, wa[q]);
   if (c_lo < c_hi) {
-    load_w(c_lo, wa);
     load_x(c_lo, xr, gv, bv);
     store_x(xr, gv, bv, c_lo, 0);
   }
   __syncthreads();
-  for (int c = c_lo; c < c_hi; ++c) chunk(c, wa);
+  for (int c0 = c_lo; c0 < c_hi; c0 += PF) {
+#pragma unroll
+    for (int q = 0; q < PF; ++q)
+      if (c0 + q < c_hi) chunk(c0 + q, wa[q]);
+  }
 
   // split-K: publish this slice's tiles, the last arriving slice of the N block sums and stores
   bool fin = true;
@@ -440,7 +447,7 @@ KCA_API int kca_mm_skinny_set(int target_wg) {
 constexpr int mm_kc_default(int MT, int NRW) { return MT * NRW >= 4 ? 128 : 256; }
 
 struct MmPlan {
-  int mt, nrw, kc, wv, ks, nblk;
+  int mt, nrw, kc, wv, pf, ks, nblk;
   long long ws_floats;
 };
 
@@ -473,7 +480,10 @@ static void mm_go(MmArgs& a, MmPlan& p, hipStream_t s, bool launch) {
   mm_plan_ks(a, p, g_mm_target_wg > 0 ? g_mm_target_wg : (MT == 1 ? 512 : 384));
   if (!launch) return;
   a.ks = p.ks;
-  hipLaunchKernelGGL((mm_skinny_kernel<DT, MT, NRW, KC, WV, LN>), dim3(p.nblk, p.ks), dim3(WV * 64), T::LDS, s, a);
+  const dim3 grid(p.nblk, p.ks), blk(WV * 64);
+  if (p.pf == 3) hipLaunchKernelGGL((mm_skinny_kernel<DT, MT, NRW, KC, WV, LN, 3>), grid, blk, T::LDS, s, a);
+  else if (p.pf == 2) hipLaunchKernelGGL((mm_skinny_kernel<DT, MT, NRW, KC, WV, LN, 2>), grid, blk, T::LDS, s, a);
+  else hipLaunchKernelGGL((mm_skinny_kernel<DT, MT, NRW, KC, WV, LN, 1>), grid, blk, T::LDS, s, a);
 }
 
 template <int DT, int MT, int NRW, bool LN>
@@ -509,9 +519,20 @@ static MmPlan mm_plan(MmArgs& a) {
   MmPlan p;
   p.mt = a.M <= 16 ? 1 : (a.M <= 32 ? 2 : 4);
   p.nrw = (a.nr == 2 && p.mt < 4) ? 2 : 1;
-  p.kc = a.kc == 128 || a.kc == 256 ? a.kc : mm_kc_default(p.mt, p.nrw);
+  // 32-64 rows with a long K: 8-wave workgroups over 128-wide K chunks -- twice the weight rows share
+  // each staged activation chunk, whose L2 re-reads grow with M (M = 32: 465 -> 448 us, M = 64:
+  // 621 -> 541 us summed over the fused-layer shapes; short-K shapes lose: profiles/mm_shape_sweep_r6/)
+  int kmax = 0;
+  for (int i = 0; i < a.njobs; ++i) {
+    int k = 0;
+    for (int q = 0; q < a.j[i].nparts; ++q) k += a.j[i].p[q].K;
+    kmax = k > kmax ? k : kmax;
+  }
+  const bool wide = p.mt >= 2 && kmax >= 6144;
+  p.kc = a.kc == 128 || a.kc == 256 ? a.kc : (wide ? 128 : mm_kc_default(p.mt, p.nrw));
   if (p.kc == 256 && p.mt * p.nrw >= 4) p.kc = 128;  // (register budget)
-  p.wv = a.wv == 4 || a.wv == 8 ? a.wv : 4;
+  p.wv = a.wv == 4 || a.wv == 8 ? a.wv : (wide ? 8 : 4);
+  p.pf = a.pf >= 1 && a.pf <= 3 ? a.pf : 1;
   const int rows = p.wv * p.nrw * 16;
   p.nblk = 0;
   for (int i = 0; i < a.njobs; ++i) {

@@ -45,7 +45,7 @@ class _Job(ctypes.Structure):
 
 class _Args(ctypes.Structure):
     _fields_ = [("j", _Job * 2), ("njobs", _I), ("M", _I), ("ks", _I), ("nr", _I), ("kc", _I), ("wv", _I),
-                ("ws", _P), ("bcnt", _P), ("ws_floats", _LL), ("bcnt_n", _I), ("pad_", _I)]
+                ("ws", _P), ("bcnt", _P), ("ws_floats", _LL), ("bcnt_n", _I), ("pf", _I)]
 
 
 _DT = {torch.bfloat16: 0, torch.float16: 1}
@@ -56,6 +56,7 @@ _KS = int(os.environ.get("KCA_MM_KS", "0"))
 _NR = int(os.environ.get("KCA_MM_NR", "1"))
 _KC = int(os.environ.get("KCA_MM_KC", "0"))  # K per chunk 128 / 256
 _WV = int(os.environ.get("KCA_MM_WV", "0"))  # waves per workgroup 4 / 8
+_PF = int(os.environ.get("KCA_MM_PF", "0"))  # weight chunks in flight per wave 1..3
 # split-K workspaces (fp32 partial tiles + zeroed per-block arrival counters), one per (device, stream):
 # launches on one stream are ordered, launches on two streams must not share the counters
 _WS: dict = {}
@@ -154,7 +155,7 @@ def _args(jobs, M, ks, nr):
     a.njobs, a.M = len(jobs), M
     a.ks = _KS if ks is None else ks
     a.nr = _NR if nr is None else nr
-    a.kc, a.wv = _KC, _WV
+    a.kc, a.wv, a.pf = _KC, _WV, _PF
     return a
 
 

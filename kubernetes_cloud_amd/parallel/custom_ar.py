@@ -101,6 +101,8 @@ class XGMIAllReduce:
         self._res_statss = {torch.bfloat16: _fn("kca_ar_res_stats", st_args),
                             torch.float16: _fn("kca_ar_res_stats_f16", st_args)}
         self._tails: dict = {}
+        # batch-1 close: 0 = LayerNorm distributed over the launch (default), 1 = last-arriver tail (A/B)
+        _fn("kca_ar_set_variant", [ctypes.c_int])(int(os.environ.get("KCA_AR_LN_VARIANT", "0")))
         self.res_ln_calls = 0  # fused tail launches (tests assert the TP decode layer took them)
         self.res_stats_calls = 0
         lib = _lib.require()
