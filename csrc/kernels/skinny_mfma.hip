@@ -93,7 +93,7 @@ struct MmArgs {
   unsigned* bcnt; // per-N-block arrival counters (ks > 1), zero-initialised, re-armed every launch
   long long ws_floats;
   int bcnt_n;
-  int pf;         // weight chunks in flight per wave, 1..3 (0: host picks)
+  int pf;         // weight chunks in flight per wave (1; the kernel's PF ring, see mm_go)
 };
 
 // One finished 16x16 tile: rows n_base + 4*(lane>>4) + i (i < 4) of the output's N axis, column m =
@@ -480,10 +480,9 @@ static void mm_go(MmArgs& a, MmPlan& p, hipStream_t s, bool launch) {
   mm_plan_ks(a, p, g_mm_target_wg > 0 ? g_mm_target_wg : (MT == 1 ? 512 : 384));
   if (!launch) return;
   a.ks = p.ks;
-  const dim3 grid(p.nblk, p.ks), blk(WV * 64);
-  if (p.pf == 3) hipLaunchKernelGGL((mm_skinny_kernel<DT, MT, NRW, KC, WV, LN, 3>), grid, blk, T::LDS, s, a);
-  else if (p.pf == 2) hipLaunchKernelGGL((mm_skinny_kernel<DT, MT, NRW, KC, WV, LN, 2>), grid, blk, T::LDS, s, a);
-  else hipLaunchKernelGGL((mm_skinny_kernel<DT, MT, NRW, KC, WV, LN, 1>), grid, blk, T::LDS, s, a);
+  // (PF = 2 / 3 chunks in flight measured slower at every M, KC and shape: profiles/mm_pf_sweep_r6/ --
+  // the ring stays in the kernel, one instantiation is built)
+  hipLaunchKernelGGL((mm_skinny_kernel<DT, MT, NRW, KC, WV, LN, 1>), dim3(p.nblk, p.ks), dim3(WV * 64), T::LDS, s, a);
 }
 
 template <int DT, int MT, int NRW, bool LN>
@@ -532,7 +531,7 @@ static MmPlan mm_plan(MmArgs& a) {
   p.kc = a.kc == 128 || a.kc == 256 ? a.kc : (wide ? 128 : mm_kc_default(p.mt, p.nrw));
   if (p.kc == 256 && p.mt * p.nrw >= 4) p.kc = 128;  // (register budget)
   p.wv = a.wv == 4 || a.wv == 8 ? a.wv : (wide ? 8 : 4);
-  p.pf = a.pf >= 1 && a.pf <= 3 ? a.pf : 1;
+  p.pf = 1;
   const int rows = p.wv * p.nrw * 16;
   p.nblk = 0;
   for (int i = 0; i < a.njobs; ++i) {

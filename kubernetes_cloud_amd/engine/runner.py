@@ -419,6 +419,14 @@ class ModelRunner:
         self._batched_ok = (self._fused_ok and self.dtype in (torch.bfloat16, torch.float16)
                             and d_model % 64 == 0 and d_model <= 16384
                             and os.environ.get("KCA_DECODE_FUSED_BATCHED", "1") not in ("0", "false"))
+        # largest batch bucket the matrix-core layer takes, per layer kind, from same-box A/Bs against the
+        # per-projection path (hipBLASLt + the fused LN / GELU / all-reduce launches,
+        # profiles/decode_suite_r6_batched_vs_unfused.jsonl): GPT-J 3.49 vs 3.88 ms at B=16 but 4.63 vs
+        # 4.27 at 32 (the per-projection step overlaps the MLP GEMMs with the attention on a side stream);
+        # BLOOM TP=8 rank 11.46 vs 12.58 at 16, 14.25 vs 13.50 at 32 (hipBLASLt streams the 14336-wide
+        # shapes faster from M = 32); NeoX wins at every batch (12.84 vs 15.86 at 32, 25.9 vs 28.3 at 64)
+        self._batched_max_b = int(os.environ.get("KCA_DECODE_BATCHED_MAX_B", "0")) or \
+            {"gptj": 16, "seq": 16}.get(self._layer_kind, 64)
 
     # ------------------------------------------------------------- prefill
     @torch.no_grad()
@@ -749,7 +757,7 @@ class ModelRunner:
             if y is not None:
                 self.fused_steps += 1
                 return y
-        if (self._batched_ok and 2 <= tokens.shape[0] <= smm.MAX_M and obuf is not None
+        if (self._batched_ok and 2 <= tokens.shape[0] <= min(smm.MAX_M, self._batched_max_b) and obuf is not None
                 and (self._chain_src is None or self._embed_head)):
             return self._layers_decode_batched(tokens, pos, slots, kv_lens, max_kv, ws, obuf)
         if self._chain_src is not None and obuf is not None:  # chained rows not resolved by a fused head

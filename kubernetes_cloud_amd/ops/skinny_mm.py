@@ -56,7 +56,6 @@ _KS = int(os.environ.get("KCA_MM_KS", "0"))
 _NR = int(os.environ.get("KCA_MM_NR", "1"))
 _KC = int(os.environ.get("KCA_MM_KC", "0"))  # K per chunk 128 / 256
 _WV = int(os.environ.get("KCA_MM_WV", "0"))  # waves per workgroup 4 / 8
-_PF = int(os.environ.get("KCA_MM_PF", "0"))  # weight chunks in flight per wave 1..3
 # split-K workspaces (fp32 partial tiles + zeroed per-block arrival counters), one per (device, stream):
 # launches on one stream are ordered, launches on two streams must not share the counters
 _WS: dict = {}
@@ -155,7 +154,7 @@ def _args(jobs, M, ks, nr):
     a.njobs, a.M = len(jobs), M
     a.ks = _KS if ks is None else ks
     a.nr = _NR if nr is None else nr
-    a.kc, a.wv, a.pf = _KC, _WV, _PF
+    a.kc, a.wv = _KC, _WV
     return a
 
 

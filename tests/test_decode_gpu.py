@@ -950,6 +950,7 @@ def test_engine_batched_mfma_layer(preset, B):
         eng = LLMEngine(m, max_slots=B, max_len=256, use_graphs=True)
         assert eng.runner._batched_ok
         eng.runner._batched_ok = batched
+        eng.runner._batched_max_b = 64  # (the layer at every bucket, whatever the per-kind dispatch cap)
         outs = [r.output for r in eng.generate(prompts, sp)]
         assert (eng.runner.batched_steps > 0) == batched
         for p, o in zip(prompts, outs):
