@@ -97,7 +97,7 @@ def decode_ws_floats(B: int, H: int, Hkv: int, D: int, max_kv: int, chunk: int =
     return -(-(B * H) // 4) * 4 + B * H * ns * (D + 2) if ns > 1 else 0
 
 
-_DECODE_WGS = 256  # split-K workgroup target
+_DECODE_WGS = int(os.environ.get("KCA_DECODE_SPLIT_TARGET", "256"))  # split-K workgroup target (A/B knob)
 
 
 def decode_chunk(B: int, Hkv: int, max_kv: int) -> int:
