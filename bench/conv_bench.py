@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """SD-1.5 UNet 3x3 convolutions (channels-last bf16, txt2img batch 8 + CFG = 16) on MI355X:
-MIOpen (tuned db, utils/miopen.py) vs an explicit NHWC im2col + hipBLASLt GEMM.
+MIOpen (tuned db, utils/miopen.py) vs the matrix-core implicit GEMM (ops/conv.py) (and, with
+KCA_CONV_BENCH_IM2COL=1, an explicit NHWC im2col + hipBLASLt GEMM).
 
     python bench/conv_bench.py
 """
@@ -57,14 +58,20 @@ def main():
         w2 = w.permute(0, 2, 3, 1).reshape(Co, 9 * Ci).contiguous()
         flops = 2.0 * N * H * W * Co * 9 * Ci
         t_conv = timeit(lambda: F.conv2d(x, w, padding=1))
-        t_col = timeit(lambda: im2col_conv(x, w2))
-        ref = F.conv2d(x, w, padding=1).float()
-        got = im2col_conv(x, w2).float()
-        err = float((ref - got).abs().max() / (ref.abs().max() + 1e-6))
-        print(json.dumps({"shape": [N, H, W, Ci, Co], "miopen_ms": round(t_conv, 4), "im2col_gemm_ms": round(t_col, 4),
-                          "miopen_tflops": round(flops / t_conv / 1e9, 1),
-                          "im2col_tflops": round(flops / t_col / 1e9, 1), "rel_err": round(err, 5)}), flush=True)
-
+        from kubernetes_cloud_amd.ops import conv as kconv
+        from kubernetes_cloud_amd.ops.conv import supported
+        kconv._MODE = "all"  # the kernel on every supported shape (the model dispatch uses kconv._FAST)
+        conv3x3 = kconv.conv3x3
+        rec = {"shape": [N, H, W, Ci, Co], "miopen_ms": round(t_conv, 4), "miopen_tflops": round(flops / t_conv / 1e9, 1)}
+        if supported(x, w):
+            t_ig = timeit(lambda: conv3x3(x, w))
+            ref = F.conv2d(x.float(), w.float(), padding=1)
+            err = float((ref - conv3x3(x, w).float()).abs().max() / (ref.abs().max() + 1e-6))
+            rec.update(igemm_ms=round(t_ig, 4), igemm_tflops=round(flops / t_ig / 1e9, 1), igemm_rel_err=round(err, 5))
+        if os.environ.get("KCA_CONV_BENCH_IM2COL"):
+            t_col = timeit(lambda: im2col_conv(x, w2))
+            rec.update(im2col_gemm_ms=round(t_col, 4), im2col_tflops=round(flops / t_col / 1e9, 1))
+        print(json.dumps(rec), flush=True)
 
 if __name__ == "__main__":
     main()

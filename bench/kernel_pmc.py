@@ -147,6 +147,18 @@ def _decode_attn(B, H, D, L):
     return run, {"bytes": 2 * B * H * L * D * 2}
 
 
+def _conv(N, H, W, C, Co):
+    from kubernetes_cloud_amd.ops.conv import conv3x3
+
+    x = torch.randn(N, C, H, W, device=DEV, dtype=BF).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(Co, C, 3, 3, device=DEV, dtype=BF) * 0.02).contiguous(memory_format=torch.channels_last)
+
+    def run():
+        conv3x3(x, w)
+
+    return run, {"flops": 2.0 * N * H * W * Co * 9 * C}
+
+
 CASES = {
     "attn_gptj": lambda: _attn(8, 2048, 16, 256, True),
     "attn_sd64": lambda: _attn(16, 4096, 8, 40, False),
@@ -157,6 +169,8 @@ CASES = {
     "adamw_512m": lambda: _adamw(512 * 1024 * 1024),
     "gemv_fcin_m1": lambda: _gemv(16384, 4096),
     "decode_attn_b32": lambda: _decode_attn(32, 16, 256, 2048),
+    "conv_sd64": lambda: _conv(16, 64, 64, 320, 320),
+    "conv_sd32": lambda: _conv(16, 32, 32, 640, 640),
 }
 
 

@@ -26,6 +26,7 @@ import torch.nn.functional as F
 
 from .. import ops
 from ..ops import _lib
+from ..ops.conv import conv3x3
 from ..ops.linear import SplitKLinear, linear_residual, linear_residual_train, linear_splitk_wgrad
 from ..ops.upsample import (phase_gemm_weights, phase_to_dense, phase_weights, upsample_conv_phase,
                            upsample_conv_train, upsample_nearest2x)
@@ -203,7 +204,7 @@ class ResnetBlock2D(nn.Module):
         if xn is None:
             xn = self.norm1(x) if in_bias is None else \
                 self.norm1(x, add=in_bias.float()[None].expand(x.shape[0], -1))
-        h = F.conv2d(xn, self.conv1.weight, None, padding=1)
+        h = conv3x3(xn, self.conv1.weight)
         add = temb.get(self) if isinstance(temb, _TembAdds) else None  # conv1 bias + time projection, fp32
         if add is None:
             if isinstance(temb, _TembAdds):
@@ -212,7 +213,7 @@ class ResnetBlock2D(nn.Module):
             add = b1[None].expand(x.shape[0], -1)
             if self.time_emb_proj is not None and temb is not None:
                 add = add + self.time_emb_proj(F.silu(temb)).float()
-        h = F.conv2d(self.norm2(h, add=add), self.conv2.weight, None, padding=1)
+        h = conv3x3(self.norm2(h, add=add), self.conv2.weight)
         _, bias = self._folded_biases()
         if in_bias is not None:
             bias = bias + in_bias.float()
@@ -225,11 +226,11 @@ class ResnetBlock2D(nn.Module):
         joins the residual add (ops.add_bias_nhwc_train, bias gradient by a column sum). Exact:
         the same sums in another order; removes each biased convolution's broadcast-add pass and
         PyTorch's bias-gradient reduction over the full activation."""
-        h = F.conv2d(self.norm1(x), self.conv1.weight, None, padding=1)
+        h = conv3x3(self.norm1(x), self.conv1.weight)
         add = self.conv1.bias[None].expand(x.shape[0], -1)
         if self.time_emb_proj is not None and (temb is not None or act is not None):
             add = add + self.time_emb_proj(act if act is not None else F.silu(temb))
-        h = F.conv2d(self.dropout(self.norm2(h, add=add)), self.conv2.weight, None, padding=1)
+        h = conv3x3(self.dropout(self.norm2(h, add=add)), self.conv2.weight)
         b2 = None
         if self.conv_shortcut is not None:
             sc = F.conv2d(x, self.conv_shortcut.weight, None)

@@ -84,6 +84,8 @@ _SIGS = {
     "kca_groupnorm_nhwc_cat_fwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, I, P],
     "kca_groupnorm_nhwc_bwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P],
     "kca_skinny_set_smallk": [I],
+    "kca_conv3x3_fwd": [P, P, P, P, I, I, I, I, I, P],
+    "kca_conv3x3_set_variant": [I],
     "kca_skinny_gemm": [P, LL, P, P, P, LL, I, I, I, I, P],
     "kca_skinny_set_splitk": [I],
     "kca_mm_skinny_set": [I],

@@ -1,0 +1,92 @@
+"""3x3 convolution on the matrix cores (``csrc/kernels/conv_igemm.hip``: implicit GEMM over NHWC, no im2col
+buffer) for the SD-1.5 UNet / VAE convolutions.
+
+``conv3x3(x, w, bias)`` takes channels-last bf16 tensors (the layout the SD models run in,
+``models/unet.py`` ``to_channels_last``): x [N, C, H, W], w [Cout, C, 3, 3] (physically NHWC / KRSC),
+stride 1, padding 1. Shapes the kernel does not take (C or Cout not a multiple of 64, N*H*W not a
+multiple of 128, other dtypes / layouts, CPU tensors) run ``F.conv2d``. Forward only: under autograd
+the backward is PyTorch's ``convolution_backward`` (MIOpen).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+
+# "1": the measured shapes below, "all": every supported shape, "0" (default): off. In the SD models the
+# kernel on _FAST measured within run-to-run noise of MIOpen end to end (txt2img 6.20 / 6.33 vs 6.27 /
+# 6.23 images/s, DreamBooth 55.7 / 60.8 vs 58.3 / 61.7 samples/s, profiles/conv_sd_ab_r6.jsonl), so
+# the vendor path stays the default until the kernel is clearly ahead (see conv_igemm.hip for where
+# its time goes: the LDS store path of the register-staged tiles)
+_MODE = os.environ.get("KCA_CONV_IGEMM", "0")
+_ON = _MODE not in ("0", "false")
+# (H, W, C, Cout) where the kernel beat the tuned MIOpen solvers at the SD batch (N = 16) in same-box
+# runs (profiles/conv_bench_r6.jsonl): 64x64 concat convs 682 vs 637 and 715 vs 709 TFLOP/s, the 16x16
+# convs 560-596 vs 525-531. MIOpen stays on 64x64 320 -> 320 (599 vs 649), the 32x32 convs (597-620 vs
+# 740-800: 640 workgroups are 1.25 rounds of the chip) and 8x8 (a 16-block grid).
+_FAST = {(64, 64, 640, 320), (64, 64, 960, 320), (16, 16, 640, 1280), (16, 16, 1280, 1280), (16, 16, 2560, 1280)}
+_VARIANT_SET = False
+
+
+def supported(x: torch.Tensor, w: torch.Tensor) -> bool:
+    if not (_ON and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.dim() == 4
+            and w.dim() == 4 and tuple(w.shape[2:]) == (3, 3)):
+        return False
+    N, C, H, W = x.shape
+    Co = w.shape[0]
+    return (w.shape[1] == C and C % 64 == 0 and Co % 64 == 0 and (N * H * W) % 128 == 0
+            and x.is_contiguous(memory_format=torch.channels_last)
+            and w.is_contiguous(memory_format=torch.channels_last)
+            and x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0 and _lib.has("kca_conv3x3_fwd"))
+
+
+def _fwd(x, w, bias):
+    global _VARIANT_SET
+    if not _VARIANT_SET:  # A/B: 1 = 128 x 128 tiles, 2 = 256 x 128 tiles (0: by shape)
+        _VARIANT_SET = True
+        v = int(os.environ.get("KCA_CONV_VARIANT", "0"))
+        if v:
+            _lib.call("kca_conv3x3_set_variant", v)
+    N, C, H, W = x.shape
+    Co = w.shape[0]
+    y = torch.empty((N, Co, H, W), device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
+    b = bias if bias is not None and bias.dtype == x.dtype and bias.is_contiguous() else None
+    _lib.call("kca_conv3x3_fwd", x.data_ptr(), w.data_ptr(), _lib.ptr(b), y.data_ptr(), N, H, W, C, Co,
+              _lib.stream())
+    if bias is not None and b is None:
+        y = y + bias.view(1, -1, 1, 1)
+    return y
+
+
+class _Conv3x3(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, bias):
+        ctx.save_for_backward(x, w)
+        ctx.has_bias = bias is not None
+        return _fwd(x, w, bias)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gx, gw, gb = torch.ops.aten.convolution_backward(
+            gy.contiguous(memory_format=torch.channels_last), x, w, [w.shape[0]] if ctx.has_bias else None,
+            [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
+            [ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.has_bias and ctx.needs_input_grad[2]])
+        return gx, gw, gb
+
+
+def conv3x3(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
+    """stride 1, padding 1 3x3 convolution (see module docstring)."""
+    if not supported(x, w) or (_MODE != "all" and (x.shape[2], x.shape[3], x.shape[1], w.shape[0]) not in _FAST):
+        return F.conv2d(x, w, bias, padding=1)
+    if torch.is_grad_enabled() and (x.requires_grad or w.requires_grad or (bias is not None and bias.requires_grad)):
+        return _Conv3x3.apply(x, w, bias)
+    return _fwd(x, w, bias)
+
+
+def conv3x3_reference(x, w, bias=None):
+    """fp32 reference of ``conv3x3``."""
+    return F.conv2d(x.float(), w.float(), bias.float() if bias is not None else None, padding=1)
