@@ -21,7 +21,10 @@ from kubernetes_cloud_amd.utils import miopen
 # (N, H, W, Cin, Cout)
 SHAPES = [(16, 64, 64, 320, 320), (16, 64, 64, 640, 320), (16, 32, 32, 320, 640), (16, 32, 32, 640, 640),
           (16, 16, 16, 640, 1280), (16, 16, 16, 1280, 1280), (16, 8, 8, 1280, 1280), (16, 8, 8, 2560, 1280),
-          (16, 16, 16, 2560, 1280), (16, 32, 32, 1280, 640), (16, 64, 64, 960, 320)]
+          (16, 16, 16, 2560, 1280), (16, 32, 32, 1280, 640), (16, 64, 64, 960, 320),
+          # the VAE decoder at the txt2img batch (8)
+          (8, 64, 64, 512, 512), (8, 128, 128, 512, 512), (8, 256, 256, 512, 256), (8, 256, 256, 256, 256),
+          (8, 512, 512, 256, 128), (8, 512, 512, 128, 128)]
 
 
 def timeit(fn, iters=20, warmup=5):

@@ -10,15 +10,15 @@
 // the B tile (BN output channels x 64) is BN rows of 128 B of the KRSC weight (PyTorch channels-last
 // [Cout, C, 3, 3]). No im2col buffer.
 //
-//   * workgroup: 256 threads, a BM = 128 x BN = 128 output tile, waves 2 x 2 over it (64 x 64 each,
-//     2 x 2 v_mfma_f32_32x32x16_bf16 accumulators = 64 fp32 per lane);
-//   * LDS: A and B tiles double-buffered (64 KB, 2 workgroups per CU), 16-B pieces XOR-swizzled by
-//     row so the 32-row fragment reads are bank-conflict free (swz);
-//   * global loads: PF chunks in flight per thread in registers (a ring), issued two LDS stages ahead
-//     of their MFMAs;
-//   * block order: the BN tiles of one pixel block are consecutive ids, remapped so they share an
-//     XCD (its L2 serves the A tile to all of them; cdna_hip_programming.md XCD remap);
-//   * epilogue: fp32 accumulators (+ bias) -> bf16 through LDS, stored as whole 16-B pieces.
+// Two forms (kca_conv3x3_fwd picks; profiles/conv_bench_r6.jsonl):
+//   * conv3x3_dma_kernel (default where 256-pixel blocks tile the batch): 8 waves over a 256 x 128
+//     tile, the stages filled by LDS-DMA three deep -- 606-799 TFLOP/s on the SD UNet shapes, ahead
+//     of MIOpen on the 64x64 and 16x16 ones;
+//   * conv3x3_fwd_kernel: register-staged tiles (128 x 128 or 256 x 128) through ds_write_b128, whose
+//     transfer cost (~79 B/clk/CU) bounded it at 510-715 TFLOP/s.
+// Common to both: waves of 64 x 64 outputs (2 x 2 v_mfma_f32_32x32x16_bf16 accumulators), LDS pieces
+// swizzled conflict-free (swz), the BN tiles of one pixel block on one XCD (its L2 serves the A tile to
+// all of them), fp32 accumulators (+ bias) -> bf16 through LDS, stored as 16-B pieces.
 //
 // Shapes taken: C % 64 == 0, Cout % 64 == 0, N*H*W % 128 == 0 (every UNet / VAE conv but conv_in);
 // kca_conv3x3_fwd returns 1 for others (the caller keeps the vendor path).
@@ -199,6 +199,200 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void conv3x3_fwd_kernel(ConvArgs a
 
 int g_conv_pf = 2;
 
+// ---- LDS-DMA form: the A / B stages arrive by buffer_load ... lds (no VGPR staging, none of the
+// ds_write_b128 transfer cost that bounds the register-staged kernel), NBUF stages deep, one counted
+// vmcnt + one barrier per chunk; 8 waves over a 256 x 128 tile, one workgroup per CU. An LDS-DMA
+// wave-instruction writes 1 KiB lane-linearly (8 tile rows of 128 B), so the swizzle (swz) is applied
+// to each lane's SOURCE channel; rows in the padding (and output channels past Cout) read past the
+// buffer's end and land as zeros. hipcc drains every LDS-DMA before an LDS read it can see, so the
+// fragment reads are inline asm with counted lgkmcnt waits (attention_tiled.hip's pattern).
+__device__ __forceinline__ u32x4v cds_b128(unsigned addr) {
+  u32x4v r;
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(addr));
+#endif
+  return r;
+}
+template <int N>
+__device__ __forceinline__ void clgkm_wait(u32x4v& a, u32x4v& b, u32x4v& c, u32x4v& d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "n"(N));
+#endif
+}
+template <int N>
+__device__ __forceinline__ void cvm_wait() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+#endif
+}
+__device__ __forceinline__ bf16x8 cbf8(u32x4v x) { return *reinterpret_cast<bf16x8*>(&x); }
+
+constexpr unsigned kOOB = 0x7ffffff0u;  // a source offset past every buffer this kernel is given
+
+template <int NBUF>
+__global__ __launch_bounds__(512, 1) void conv3x3_dma_kernel(ConvArgs a) {
+  constexpr int BM = 256, BN = 128, WN = 2;
+  constexpr int ABYTES = BM * BK * 2, STAGE = (BM + BN) * BK * 2;
+  constexpr int AI = ABYTES / 1024 / 8, BI = BN * BK * 2 / 1024 / 8;  // DMA instructions per wave per stage
+  constexpr int PER = AI + BI;
+  extern __shared__ __attribute__((aligned(1024))) char csm[];
+  typedef __attribute__((address_space(3))) char lds_char;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int nbn = (a.Co + BN - 1) / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bm = bid / nbn, bn = bid % nbn;
+  const int p0 = bm * BM, n0 = bn * BN;
+  const int HW = a.H * a.W;
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.x, (short)0, (int)min((long long)a.N * HW * a.C * 2, (long long)kOOB - 1), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.w, (short)0, (int)min((long long)a.Co * 9 * a.C * 2, (long long)kOOB - 1), 0x00020000);
+
+  // this lane's DMA rows: A rows 8 (wave AI + i) + lane / 8, B rows 8 (wave BI + i) + lane / 8; the
+  // 16-B piece it writes is lane % 8, so it reads logical piece (lane % 8) ^ ((row >> 1) & 7)
+  int apix[AI], ah[AI], aw[AI], alp[AI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int row = 8 * (wave * AI + i) + (lane >> 3);
+    const int p = p0 + row;
+    const int n = p / HW, rem = p - n * HW;
+    ah[i] = rem / a.W;
+    aw[i] = rem - ah[i] * a.W;
+    apix[i] = p;
+    alp[i] = ((lane & 7) ^ ((row >> 1) & 7)) * 16;
+  }
+  unsigned vb[BI];
+#pragma unroll
+  for (int i = 0; i < BI; ++i) {
+    const int row = 8 * (wave * BI + i) + (lane >> 3);
+    const int co = n0 + row;
+    vb[i] = co < a.Co ? (unsigned)(co * 9 * a.C * 2 + ((lane & 7) ^ ((row >> 1) & 7)) * 16) : kOOB;
+  }
+  const int KC = a.C / BK;
+  const int nch = 9 * KC;
+  lds_char* lsm = (lds_char*)csm;
+  auto issue = [&](int cu, int buf) {
+    const int c = min(cu, nch - 1);  // past the end: re-load the last chunk (keeps the vmcnt count fixed)
+    const int tap = c / KC, cc = (c - tap * KC) * BK;
+    const int dr = tap / 3 - 1, ds = tap % 3 - 1;
+    const int sb = __builtin_amdgcn_readfirstlane((tap * a.C + cc) * 2);
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int hh = ah[i] + dr, ww = aw[i] + ds;
+      const bool ok = (unsigned)hh < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
+      const unsigned vo = ok ? (unsigned)(((apix[i] + dr * a.W + ds) * a.C + cc) * 2 + alp[i]) : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (void __attribute__((address_space(3)))*)(
+          lsm + buf * STAGE + 1024 * (wave * AI + i)), 16, vo, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (void __attribute__((address_space(3)))*)(
+          lsm + buf * STAGE + ABYTES + 1024 * (wave * BI + i)), 16, vb[i], sb, 0, 0);  // (kOOB + sb stays past the end)
+#endif
+  };
+
+  // fragment addresses (bytes from the stage base): k-step ks, A rows i, B rows j
+  const unsigned lbase = (unsigned)(size_t)lsm;
+  unsigned fa[4][2], fb[4][2];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const int piece = 2 * ks + (lane >> 5);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = wm * 64 + i * 32 + (lane & 31);
+      fa[ks][i] = lbase + row * 128 + ((piece ^ ((row >> 1) & 7)) << 4);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = wn * 64 + j * 32 + (lane & 31);
+      fb[ks][j] = lbase + ABYTES + row * 128 + ((piece ^ ((row >> 1) & 7)) << 4);
+    }
+  }
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+#pragma unroll
+  for (int s = 0; s < NBUF - 1; ++s) issue(s, s);
+  for (int c = 0; c < nch; ++c) {
+    const int buf = c % NBUF;
+    cvm_wait<(NBUF - 2) * PER>();  // this wave's DMAs of chunk c have landed
+    __syncthreads();                // ... and every wave's; chunk c - 1's stage is free
+    issue(c + NBUF - 1, (c + NBUF - 1) % NBUF);
+    const unsigned so = buf * STAGE;
+    u32x4v fr[4][4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      fr[ks][0] = cds_b128(fa[ks][0] + so);
+      fr[ks][1] = cds_b128(fa[ks][1] + so);
+      fr[ks][2] = cds_b128(fb[ks][0] + so);
+      fr[ks][3] = cds_b128(fb[ks][1] + so);
+    }
+    clgkm_wait<12>(fr[0][0], fr[0][1], fr[0][2], fr[0][3]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cbf8(fr[0][i]), cbf8(fr[0][2 + j]), acc[i][j], 0, 0, 0);
+    clgkm_wait<8>(fr[1][0], fr[1][1], fr[1][2], fr[1][3]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cbf8(fr[1][i]), cbf8(fr[1][2 + j]), acc[i][j], 0, 0, 0);
+    clgkm_wait<4>(fr[2][0], fr[2][1], fr[2][2], fr[2][3]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cbf8(fr[2][i]), cbf8(fr[2][2 + j]), acc[i][j], 0, 0, 0);
+    clgkm_wait<0>(fr[3][0], fr[3][1], fr[3][2], fr[3][3]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cbf8(fr[3][i]), cbf8(fr[3][2 + j]), acc[i][j], 0, 0, 0);
+  }
+  cvm_wait<0>();  // the clamped re-loads past the end land before the stages are reused
+  __syncthreads();
+
+  uint16_t* st = reinterpret_cast<uint16_t*>(csm) + wave * 64 * 64;
+  const int col = lane & 31, hi = lane >> 5;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int co = n0 + wn * 64 + j * 32 + col;
+    const float b = (a.bias && co < a.Co) ? bf2f(a.bias[co]) : 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int prow = i * 32 + 8 * (r >> 2) + 4 * hi + (r & 3);
+        st[prow * 64 + j * 32 + col] = f2bf(acc[i][j][r] + b);
+      }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int cbase = n0 + wn * 64;
+  if (cbase < a.Co) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int row = (lane >> 3) + 8 * t, pc = lane & 7;
+      const long long p = p0 + wm * 64 + row;
+      *reinterpret_cast<u32x4v*>(a.y + p * a.Co + cbase + pc * 8) =
+          *reinterpret_cast<const u32x4v*>(st + row * 64 + pc * 8);
+    }
+  }
+}
+
 template <int WM, int WN>
 int conv_launch(const ConvArgs& a, hipStream_t stream) {
   using T = ConvTile<WM, WN>;
@@ -215,7 +409,8 @@ int conv_launch(const ConvArgs& a, hipStream_t stream) {
   return hipGetLastError() == hipSuccess ? 0 : 4;
 }
 
-int g_conv_variant = 0;  // 0: by shape, 1: 128 x 128 tiles, 2: 256 x 128 tiles (A/B)
+int g_conv_variant = 0;  // 0: LDS-DMA where it tiles, else 128 x 128; 1 / 2: register-staged 128 x 128 /
+                         // 256 x 128 tiles; 3: LDS-DMA (A/B)
 
 }  // namespace
 
@@ -235,6 +430,14 @@ KCA_API int kca_conv3x3_fwd(const void* x, const void* w, const void* bias, void
   // 256 x 128 tiles (8 waves, one workgroup per CU) when they fill the chip at least twice over
   const bool big = g_conv_variant == 2 || (g_conv_variant == 0 && npix % 256 == 0 &&
                                            npix / 256 * ((Co + 127) / 128) >= 512);
+  // default: the LDS-DMA kernel whenever its 256-pixel blocks tile the batch
+  if ((g_conv_variant == 3 || g_conv_variant == 0) && npix % 256 == 0 && (long long)N * H * W * C * 2 < 0x70000000ll &&
+      (long long)Co * 9 * C * 2 < 0x70000000ll) {
+    constexpr int NB = 3;
+    const long long nblk = npix / 256 * ((Co + 127) / 128);
+    hipLaunchKernelGGL((conv3x3_dma_kernel<NB>), dim3((unsigned)nblk), dim3(512), NB * (256 + 128) * BK * 2, stream, a);
+    return hipGetLastError() == hipSuccess ? 0 : 4;
+  }
   if (big && npix % 256 == 0) return conv_launch<4, 2>(a, stream);
   return conv_launch<2, 2>(a, stream);
 }

@@ -16,23 +16,22 @@ import torch.nn.functional as F
 
 from . import _lib
 
-# "1": the measured shapes below, "all": every supported shape, "0" (default): off. In the SD models the
-# kernel on _FAST measured within run-to-run noise of MIOpen end to end (txt2img 6.20 / 6.33 vs 6.27 /
-# 6.23 images/s, DreamBooth 55.7 / 60.8 vs 58.3 / 61.7 samples/s, profiles/conv_sd_ab_r6.jsonl), so
-# the vendor path stays the default until the kernel is clearly ahead (see conv_igemm.hip for where
-# its time goes: the LDS store path of the register-staged tiles)
-_MODE = os.environ.get("KCA_CONV_IGEMM", "0")
-_ON = _MODE not in ("0", "false")
-# (H, W, C, Cout) where the kernel beat the tuned MIOpen solvers at the SD batch (N = 16) in same-box
-# runs (profiles/conv_bench_r6.jsonl): 64x64 concat convs 682 vs 637 and 715 vs 709 TFLOP/s, the 16x16
-# convs 560-596 vs 525-531. MIOpen stays on 64x64 320 -> 320 (599 vs 649), the 32x32 convs (597-620 vs
-# 740-800: 640 workgroups are 1.25 rounds of the chip) and 8x8 (a 16-block grid).
-_FAST = {(64, 64, 640, 320), (64, 64, 960, 320), (16, 16, 640, 1280), (16, 16, 1280, 1280), (16, 16, 2560, 1280)}
+# "1" (default): the measured shapes below, "all": every supported shape, "0": off (MIOpen everywhere).
+# End to end on the same box, KCA_CONV_IGEMM=0 -> 1: txt2img 6.378 / 6.416 -> 6.498 / 6.537 images/s,
+# DreamBooth 61.99 / 61.93 -> 62.16 / 62.31 samples/s (profiles/conv_sd_ab_r6.jsonl)
+_MODE = os.environ.get("KCA_CONV_IGEMM", "1")
+# (H, W, C, Cout) where the kernel (LDS-DMA form) beat the tuned MIOpen solvers in same-box runs
+# (profiles/conv_bench_r6.jsonl; UNet at N = 16, VAE decoder at N = 8): UNet 64x64 640 / 960 -> 320 773 /
+# 799 vs 625 / 704 TFLOP/s, 320 -> 320 684 vs 642, the 16x16 convs 606-686 vs 524-530; the VAE's 512x512
+# convs 871 / 792 vs 766 / 718. MIOpen keeps the UNet's 32x32 convs (606-663 vs 729-784: 320 workgroups
+# are 1.25 rounds of the chip), its 8x8 ones (16 blocks) and the VAE's 64-256 px convs (~1 PF there).
+_FAST = {(64, 64, 320, 320), (64, 64, 640, 320), (64, 64, 960, 320), (16, 16, 640, 1280), (16, 16, 1280, 1280),
+         (16, 16, 2560, 1280), (16, 16, 1920, 1280), (512, 512, 256, 128), (512, 512, 128, 128)}
 _VARIANT_SET = False
 
 
 def supported(x: torch.Tensor, w: torch.Tensor) -> bool:
-    if not (_ON and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.dim() == 4
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.dim() == 4
             and w.dim() == 4 and tuple(w.shape[2:]) == (3, 3)):
         return False
     N, C, H, W = x.shape
@@ -80,7 +79,8 @@ class _Conv3x3(torch.autograd.Function):
 
 def conv3x3(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
     """stride 1, padding 1 3x3 convolution (see module docstring)."""
-    if not supported(x, w) or (_MODE != "all" and (x.shape[2], x.shape[3], x.shape[1], w.shape[0]) not in _FAST):
+    if _MODE in ("0", "false") or not supported(x, w) or \
+            (_MODE != "all" and (x.shape[2], x.shape[3], x.shape[1], w.shape[0]) not in _FAST):
         return F.conv2d(x, w, bias, padding=1)
     if torch.is_grad_enabled() and (x.requires_grad or w.requires_grad or (bias is not None and bias.requires_grad)):
         return _Conv3x3.apply(x, w, bias)
