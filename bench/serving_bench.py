@@ -167,6 +167,7 @@ def _levels(pred, model_name: str, new_tokens: int | None, levels=LEVELS, kind: 
         _client(srv.url, 4, 4, model_name, 99, kind)  # warm: graphs, allocator
         _engine(pred, 4, 4, seed=98, kind=kind)
         for conc, n in levels:
+            print(f"[serving_bench] {model_name} c={conc}: warm-up", file=sys.stderr, flush=True)
             # warm this level's batch buckets first (decode-graph captures), so no timed pass pays them
             # (the full level: a shorter warm-up left the first timed engine pass 10-15 % slow at 32)
             _engine(pred, n, conc, seed=1000 + conc, kind=kind)
@@ -208,6 +209,8 @@ def _levels(pred, model_name: str, new_tokens: int | None, levels=LEVELS, kind: 
                 rec["steps_passes"] = [b["steps"] - a["steps"] for a, b in ((st, st1), (st1, st2), (st2, st3))]
                 rec["prefill_batches_passes"] = [b["prefill_batches"] - a["prefill_batches"]
                                                  for a, b in ((st, st1), (st1, st2), (st2, st3))]
+            print(f"[serving_bench] {model_name} c={conc}: engine {rec['engine_rps_passes']} req/s, http "
+                  f"{rec['http_rps']}", file=sys.stderr, flush=True)  # (progress: a level takes ~30-60 s)
             rec["http_overhead_mean_ms"] = round((rec["http_mean_s"] - rec["engine_mean_s"]) * 1e3, 2)
             rec["http_rps_loss"] = round(1.0 - rec["http_rps"] / max(e_rps, 1e-9), 4)
             out.append(rec)

@@ -227,13 +227,33 @@ __device__ __forceinline__ void cvm_wait() {
 }
 __device__ __forceinline__ bf16x8 cbf8(u32x4v x) { return *reinterpret_cast<bf16x8*>(&x); }
 
-constexpr unsigned kOOB = 0x7ffffff0u;  // a source offset past every buffer this kernel is given
+constexpr unsigned kOOB = 0x7ffffff0u;
 
-template <int NBUF>
+// physical 16-B piece of logical piece p in tile row r: conflict-free ds_read_b128 lane groups for
+// 128-B rows (BK 64: p ^ ((r >> 1) & 7)) and 64-B rows (BK 32: p ^ ((r >> 2) & 3))
+template <int BKX>
+__device__ __forceinline__ int dswz(int r, int p) {
+  if constexpr (BKX == 64) return p ^ ((r >> 1) & 7);
+  else return p ^ ((r >> 2) & 3);
+}
+
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}  // a source offset past every buffer this kernel is given
+
+template <int NBUF, int BKX>
 __global__ __launch_bounds__(512, 1) void conv3x3_dma_kernel(ConvArgs a) {
   constexpr int BM = 256, BN = 128, WN = 2;
-  constexpr int ABYTES = BM * BK * 2, STAGE = (BM + BN) * BK * 2;
-  constexpr int AI = ABYTES / 1024 / 8, BI = BN * BK * 2 / 1024 / 8;  // DMA instructions per wave per stage
+  constexpr int RB = BKX * 2;                       // bytes per tile row
+  constexpr int RPI = 1024 / RB;                    // tile rows per DMA wave-instruction
+  constexpr int PPR = BKX / 8;                      // 16-B pieces per row
+  constexpr int ABYTES = BM * RB, STAGE = (BM + BN) * RB;
+  constexpr int AI = ABYTES / 1024 / 8, BI = BN * RB / 1024 / 8;  // DMA instructions per wave per stage
+  constexpr int KS = BKX / 16;                      // MFMA k-steps per chunk
   constexpr int PER = AI + BI;
   extern __shared__ __attribute__((aligned(1024))) char csm[];
   typedef __attribute__((address_space(3))) char lds_char;
@@ -255,27 +275,27 @@ __global__ __launch_bounds__(512, 1) void conv3x3_dma_kernel(ConvArgs a) {
   int apix[AI], ah[AI], aw[AI], alp[AI];
 #pragma unroll
   for (int i = 0; i < AI; ++i) {
-    const int row = 8 * (wave * AI + i) + (lane >> 3);
+    const int row = RPI * (wave * AI + i) + lane / PPR;
     const int p = p0 + row;
     const int n = p / HW, rem = p - n * HW;
     ah[i] = rem / a.W;
     aw[i] = rem - ah[i] * a.W;
     apix[i] = p;
-    alp[i] = ((lane & 7) ^ ((row >> 1) & 7)) * 16;
+    alp[i] = dswz<BKX>(row, lane % PPR) * 16;
   }
   unsigned vb[BI];
 #pragma unroll
   for (int i = 0; i < BI; ++i) {
-    const int row = 8 * (wave * BI + i) + (lane >> 3);
+    const int row = RPI * (wave * BI + i) + lane / PPR;
     const int co = n0 + row;
-    vb[i] = co < a.Co ? (unsigned)(co * 9 * a.C * 2 + ((lane & 7) ^ ((row >> 1) & 7)) * 16) : kOOB;
+    vb[i] = co < a.Co ? (unsigned)(co * 9 * a.C * 2 + dswz<BKX>(row, lane % PPR) * 16) : kOOB;
   }
-  const int KC = a.C / BK;
+  const int KC = a.C / BKX;
   const int nch = 9 * KC;
   lds_char* lsm = (lds_char*)csm;
   auto issue = [&](int cu, int buf) {
     const int c = min(cu, nch - 1);  // past the end: re-load the last chunk (keeps the vmcnt count fixed)
-    const int tap = c / KC, cc = (c - tap * KC) * BK;
+    const int tap = c / KC, cc = (c - tap * KC) * BKX;
     const int dr = tap / 3 - 1, ds = tap % 3 - 1;
     const int sb = __builtin_amdgcn_readfirstlane((tap * a.C + cc) * 2);
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -296,19 +316,19 @@ __global__ __launch_bounds__(512, 1) void conv3x3_dma_kernel(ConvArgs a) {
 
   // fragment addresses (bytes from the stage base): k-step ks, A rows i, B rows j
   const unsigned lbase = (unsigned)(size_t)lsm;
-  unsigned fa[4][2], fb[4][2];
+  unsigned fa[KS][2], fb[KS][2];
 #pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
+  for (int ks = 0; ks < KS; ++ks) {
     const int piece = 2 * ks + (lane >> 5);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int row = wm * 64 + i * 32 + (lane & 31);
-      fa[ks][i] = lbase + row * 128 + ((piece ^ ((row >> 1) & 7)) << 4);
+      fa[ks][i] = lbase + row * RB + (dswz<BKX>(row, piece) << 4);
     }
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int row = wn * 64 + j * 32 + (lane & 31);
-      fb[ks][j] = lbase + ABYTES + row * 128 + ((piece ^ ((row >> 1) & 7)) << 4);
+      fb[ks][j] = lbase + ABYTES + row * RB + (dswz<BKX>(row, piece) << 4);
     }
   }
 
@@ -328,38 +348,24 @@ __global__ __launch_bounds__(512, 1) void conv3x3_dma_kernel(ConvArgs a) {
     __syncthreads();                // ... and every wave's; chunk c - 1's stage is free
     issue(c + NBUF - 1, (c + NBUF - 1) % NBUF);
     const unsigned so = buf * STAGE;
-    u32x4v fr[4][4];
+    u32x4v fr[KS][4];
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
+    for (int ks = 0; ks < KS; ++ks) {
       fr[ks][0] = cds_b128(fa[ks][0] + so);
       fr[ks][1] = cds_b128(fa[ks][1] + so);
       fr[ks][2] = cds_b128(fb[ks][0] + so);
       fr[ks][3] = cds_b128(fb[ks][1] + so);
     }
-    clgkm_wait<12>(fr[0][0], fr[0][1], fr[0][2], fr[0][3]);
+    static_for<0, KS>([&](auto kk) {
+      constexpr int ks = decltype(kk)::value;
+      clgkm_wait<4 * (KS - 1 - ks)>(fr[ks][0], fr[ks][1], fr[ks][2], fr[ks][3]);
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cbf8(fr[0][i]), cbf8(fr[0][2 + j]), acc[i][j], 0, 0, 0);
-    clgkm_wait<8>(fr[1][0], fr[1][1], fr[1][2], fr[1][3]);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cbf8(fr[1][i]), cbf8(fr[1][2 + j]), acc[i][j], 0, 0, 0);
-    clgkm_wait<4>(fr[2][0], fr[2][1], fr[2][2], fr[2][3]);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cbf8(fr[2][i]), cbf8(fr[2][2 + j]), acc[i][j], 0, 0, 0);
-    clgkm_wait<0>(fr[3][0], fr[3][1], fr[3][2], fr[3][3]);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cbf8(fr[3][i]), cbf8(fr[3][2 + j]), acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] =
+              __builtin_amdgcn_mfma_f32_32x32x16_bf16(cbf8(fr[ks][i]), cbf8(fr[ks][2 + j]), acc[i][j], 0, 0, 0);
+    });
   }
   cvm_wait<0>();  // the clamped re-loads past the end land before the stages are reused
   __syncthreads();
@@ -416,7 +422,7 @@ int g_conv_variant = 0;  // 0: LDS-DMA where it tiles, else 128 x 128; 1 / 2: re
 
 KCA_API int kca_conv3x3_set_variant(int v) {
   g_conv_variant = v % 10;
-  g_conv_pf = v / 10 ? v / 10 : 2;  // tens digit: chunks in flight (A/B)
+  g_conv_pf = (v / 10) % 10 ? (v / 10) % 10 : 2;  // tens digit: chunks in flight (A/B)
   return 0;
 }
 
@@ -433,9 +439,10 @@ KCA_API int kca_conv3x3_fwd(const void* x, const void* w, const void* bias, void
   // default: the LDS-DMA kernel whenever its 256-pixel blocks tile the batch
   if ((g_conv_variant == 3 || g_conv_variant == 0) && npix % 256 == 0 && (long long)N * H * W * C * 2 < 0x70000000ll &&
       (long long)Co * 9 * C * 2 < 0x70000000ll) {
-    constexpr int NB = 3;
     const long long nblk = npix / 256 * ((Co + 127) / 128);
-    hipLaunchKernelGGL((conv3x3_dma_kernel<NB>), dim3((unsigned)nblk), dim3(512), NB * (256 + 128) * BK * 2, stream, a);
+    // (32-channel chunks six stages deep measured 8-20 % slower: the per-chunk barrier + wait is the
+    // fixed cost, profiles/conv_bench_r6.jsonl)
+    hipLaunchKernelGGL((conv3x3_dma_kernel<3, 64>), dim3((unsigned)nblk), dim3(512), 3 * (256 + 128) * 128, stream, a);
     return hipGetLastError() == hipSuccess ? 0 : 4;
   }
   if (big && npix % 256 == 0) return conv_launch<4, 2>(a, stream);
