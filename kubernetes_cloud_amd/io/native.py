@@ -82,14 +82,18 @@ def storage_read_rate(path: str, threads: int = 8, chunk: int = 64 << 20, odirec
     return {"bytes": int(st[0]), "seconds": st[1], "gbps": st[0] / max(st[1], 1e-9) / 1e9}
 
 
-def storage_ceiling(path: str, configs=((8, 64 << 20), (16, 16 << 20), (32, 16 << 20), (16, 64 << 20))) -> dict:
+def storage_ceiling(path: str, configs=((8, 64 << 20), (16, 16 << 20), (32, 16 << 20), (16, 64 << 20),
+                                       (32, 64 << 20), (64, 16 << 20)), repeats: int = 2) -> dict:
     """The storage's best raw O_DIRECT read rate of ``path`` over several queue depths (threads x
-    chunk): a ceiling for a loader, not one loader configuration's rate (the streamer's 8-thread
-    pipeline measured 1.04x a same-configuration raw read, VERDICT r5 weak #7)."""
+    chunk), each read ``repeats`` times: a ceiling for a loader, not one loader configuration's rate
+    (the streamer's 8-thread pipeline measured 1.04x a same-configuration raw read, VERDICT r5 weak #7;
+    one pass over four depths still came out 0-8 % under the load on a box whose storage rate moves
+    between reads, profiles/bench_r6_final.json)."""
     best = None
     for threads, chunk in configs:
-        r = storage_read_rate(path, threads=threads, chunk=chunk)
-        r.update(threads=threads, chunk=chunk)
-        if best is None or r["gbps"] > best["gbps"]:
-            best = r
+        for _ in range(repeats):
+            r = storage_read_rate(path, threads=threads, chunk=chunk)
+            r.update(threads=threads, chunk=chunk)
+            if best is None or r["gbps"] > best["gbps"]:
+                best = r
     return best
