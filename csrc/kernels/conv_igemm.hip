@@ -295,7 +295,13 @@ __global__ __launch_bounds__(512, 1) void conv3x3_dma_kernel(ConvArgs a) {
   lds_char* lsm = (lds_char*)csm;
   auto issue = [&](int cu, int buf) {
     const int c = min(cu, nch - 1);  // past the end: re-load the last chunk (keeps the vmcnt count fixed)
+#ifdef KCA_CONV_TAP_MAJOR
     const int tap = c / KC, cc = (c - tap * KC) * BKX;
+#else
+    // channel-major: the 9 taps of one 64-channel slice back to back, so the shifted re-reads of the
+    // block's pixels (+ halo: ~50 KB per workgroup) hit the XCD's L2 instead of the Infinity Cache
+    const int tap = c % 9, cc = (c / 9) * BKX;
+#endif
     const int dr = tap / 3 - 1, ds = tap % 3 - 1;
     const int sb = __builtin_amdgcn_readfirstlane((tap * a.C + cc) * 2);
 #if defined(__HIP_DEVICE_COMPILE__)
