@@ -23,8 +23,9 @@ def _w(N, K, dt, g):
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("M", [2, 3, 4, 8, 16, 17, 32, 33, 64])
-@pytest.mark.parametrize("NK", [(1024, 4096), (4096, 1792), (1360, 1000)])
+@pytest.mark.parametrize("NK", [(1024, 4096), (4096, 1792), (1360, 1000), (640, 6208)])
 def test_mm_plain_bias_gelu(dt, M, NK):
+    """(K >= 6144 at M >= 17: the 8-wave, 128-wide-chunk workgroups of the long-K plan)"""
     N, K = NK
     g = torch.Generator(device=DEV).manual_seed(M * 7 + N)
     x = torch.randn(M, K, generator=g, device=DEV).to(dt)
