@@ -146,8 +146,9 @@ def _emulation_notes(model, cfg, B, tp):
                                      "all_gather_logits_bytes": B * (cfg.vocab_size // tp) * 2,
                                      "note": "with the rank-local custom all-reduce the fused all-reduce tails run "
                                              "(staging, sync round, tail) with the rank as its only peer; a TP=8 "
-                                             "node adds the xGMI reads of the 7 peers' partials, priced by "
-                                             "allreduce_bench"}}
+                                             "node adds the xGMI reads of the 7 peers' partials and the "
+                                             "system-scope release / acquire of each sync round (elided at "
+                                             "world 1), priced by allreduce_bench"}}
 
 
 def main():

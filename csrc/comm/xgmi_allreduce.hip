@@ -93,33 +93,30 @@ __device__ __forceinline__ bool ar_sync(const ARPeers& peers, ARCtl* ctl, int ra
                                         long long spin_limit) {
   __shared__ int s_ok;
   const int b = blockIdx.x, tid = threadIdx.x;
-#ifndef KCA_AR_FULL_FENCE
-  // the staging and the flags are device-uncached (MTYPE UC, hipDeviceMallocUncached): a drained store
-  // is at the memory side, so the data -> flag order needs no L2 writeback / invalidate (the system-
-  // scope release / acquire, KCA_AR_FULL_FENCE): drain, barrier, relaxed flag store; relaxed polls.
-  // Per call at world 1: res_stats 13.3 -> 10.3 us (B=8), 24.3 -> 16.8 (B=32); BLOOM TP=8 rank
-  // B=8 12.04 -> 11.65 ms/token (profiles/ar_tail_r6.jsonl)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // W = 1 (a TP rank emulated on one GPU, parallel/tp_emulation.py): no peer to order the staging
+  // against, so the round is a drain + barrier + relaxed flag store / poll without the system-scope
+  // L2 writeback / invalidate (res_stats 13.3 -> 10.3 us per call at B = 8, profiles/ar_tail_r6.jsonl).
+  // W > 1 keeps the system-scope release / acquire: whether a drained store to a peer's uncached
+  // memory over xGMI is visible before the flag is not something this tree can test on one GPU.
+  constexpr bool light = W == 1;
+  if constexpr (light) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    __threadfence_system();
+  }
   __syncthreads();
   if (tid == 0) s_ok = 1;
-  if (tid < W) __hip_atomic_store(&peers.sig[tid]->flag[phase][b][rank], call, __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_SYSTEM);
+  if (tid < W) {
+    if constexpr (light)
+      __hip_atomic_store(&peers.sig[tid]->flag[phase][b][rank], call, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else
+      st_sys(&peers.sig[tid]->flag[phase][b][rank], call);
+  }
   __syncthreads();
   if (tid < W) {
     const uint32_t* f = &peers.sig[rank]->flag[phase][b][tid];
     long long spins = 0;
-    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < call) {
-#else
-  __threadfence_system();
-  __syncthreads();
-  if (tid == 0) s_ok = 1;
-  if (tid < W) st_sys(&peers.sig[tid]->flag[phase][b][rank], call);
-  __syncthreads();
-  if (tid < W) {
-    const uint32_t* f = &peers.sig[rank]->flag[phase][b][tid];
-    long long spins = 0;
-    while (ld_sys(f) < call) {
-#endif
+    while ((light ? __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : ld_sys(f)) < call) {
       if (++spins > spin_limit) {
         __hip_atomic_fetch_or(&ctl->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_ok = 0;
