@@ -159,6 +159,21 @@ def _conv(N, H, W, C, Co):
     return run, {"flops": 2.0 * N * H * W * Co * 9 * C}
 
 
+def _mm(M, N, K):
+    from kubernetes_cloud_amd.ops import skinny_mm as smm
+
+    x = torch.randn(M, K, device=DEV, dtype=BF)
+    ws = [torch.randn(N, K, device=DEV, dtype=BF) * 0.02 for _ in range(4)]  # rotate: cold weights
+    b = torch.randn(N, device=DEV, dtype=BF)
+    it = [0]
+
+    def run():
+        smm.mm(x, ws[it[0] % 4], b)
+        it[0] += 1
+
+    return run, {"bytes": N * K * 2}
+
+
 CASES = {
     "attn_gptj": lambda: _attn(8, 2048, 16, 256, True),
     "attn_sd64": lambda: _attn(16, 4096, 8, 40, False),
@@ -170,6 +185,8 @@ CASES = {
     "gemv_fcin_m1": lambda: _gemv(16384, 4096),
     "decode_attn_b32": lambda: _decode_attn(32, 16, 256, 2048),
     "conv_sd64": lambda: _conv(16, 64, 64, 320, 320),
+    "mm_bloom_fcin_m8": lambda: _mm(8, 7168, 14336),
+    "mm_bloom_fcout_m8": lambda: _mm(8, 14336, 7168),
     "conv_sd32": lambda: _conv(16, 32, 32, 640, 640),
 }
 
