@@ -20,7 +20,9 @@
 // Ordering/race argument (this replaces round 1's per-block counters, whose
 // parities drifted apart when the block count or slice map changed between
 // calls): the call number is ONE per-rank sequence word, read by every block
-// at kernel start and advanced by the last block to finish. Flags compare
+// at kernel start and advanced once every block has read it (by the last block
+// to finish, or -- in the fused LayerNorm / row-statistics closes -- by the
+// block that sees the launch's own all-blocks exchange complete). Flags compare
 // `>= call`, so blocks that sat out intermediate calls are still correct.
 // Call k+2 reuses call k's parity; before ANY block of call k+1 on rank X
 // finished, it observed every peer Y arriving at call k+1, and Y's call-(k+1)
@@ -315,7 +317,6 @@ __global__ __launch_bounds__(256) void ar_res_ln_dist_kernel(ARPeers peers, ARCt
                                                              long long spin_limit, DualLn a) {
   __shared__ float red[16];
   __shared__ float s_stat[2];
-  __shared__ int s_gen_ok;
   const int b = blockIdx.x, nb = gridDim.x, tid = threadIdx.x, lane = tid & 63;
   const long long i = (long long)b * 256 + tid;
   const bool live = i < n8;
@@ -361,50 +362,47 @@ __global__ __launch_bounds__(256) void ar_res_ln_dist_kernel(ARPeers peers, ARCt
     for (int j = 0; j < 8; ++j) q += (v[j] - mb) * (v[j] - mb);
   }
   const float m2b = block_sum(q, red + 8);
-  // launch-wide barrier: publish, count, the last arrival re-arms the count and advances the generation
-  unsigned* bar = a.cnt + 8;  // [0] count, [8] generation (the last-arriver form's counters untouched)
+  // launch-wide exchange without a counter: each block publishes (mean, M2) as two 64-bit words
+  // {call, value} (single-copy atomic: a word is this call's or a stale one), and wave 0 of every block
+  // polls the nb slots until all carry this call -- one store + one poll round instead of publish,
+  // drain, count, re-arm and a generation spin (ypart: >= 2 nb 64-bit words, zeroed once)
+  unsigned long long* slot = reinterpret_cast<unsigned long long*>(a.ypart);
   if (tid == 0) {
-    st_pub(a.ypart + 2 * b, mb);
-    st_pub(a.ypart + 2 * b + 1, m2b);
+    const unsigned long long tag = (unsigned long long)call << 32;
+    __hip_atomic_store(slot + 2 * b, tag | __float_as_uint(mb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(slot + 2 * b + 1, tag | __float_as_uint(m2b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    const unsigned gen = __hip_atomic_load(bar + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int good = 1;
-    if (__hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)nb - 1) {
-      __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_fetch_add(bar + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
+  if (tid < 64) {  // wave 0 gathers and merges the nb (<= 64) partials
+    float nt = 0.f, mt = 0.f, qt = 0.f, bad = 0.f;
+    if (lane < nb) {
+      unsigned long long w0 = 0ull, w1 = 0ull;
       long long spins = 0;
-      while (__hip_atomic_load(bar + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
+      while (true) {
+        w0 = __hip_atomic_load(slot + 2 * lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        w1 = __hip_atomic_load(slot + 2 * lane + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((uint32_t)(w0 >> 32) == call && (uint32_t)(w1 >> 32) == call) break;
         if (++spins > spin_limit) {
           __hip_atomic_fetch_or(&ctl->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          good = 0;
+          bad = 1.f;
           break;
         }
         __builtin_amdgcn_s_sleep(1);
       }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    s_gen_ok = good;
-  }
-  __syncthreads();
-  if (tid < 64) {  // wave 0 merges the nb (<= 64) partials
-    float nt = 0.f, mt = 0.f, qt = 0.f;
-    if (lane < nb) {
       const long long lo_t = (long long)lane * 256, hi_t = min(n8, lo_t + 256);
       nt = 8.f * (float)(hi_t - lo_t);
-      mt = a.ypart[2 * lane];
-      qt = a.ypart[2 * lane + 1];
+      mt = __uint_as_float((uint32_t)w0);
+      qt = __uint_as_float((uint32_t)w1);
     }
     const float ntot = wave_sum(nt);
     const float mean = wave_sum(nt * mt) / ntot;
     const float m2 = wave_sum(qt + nt * (mt - mean) * (mt - mean));
+    const bool good = wave_sum(bad) == 0.f;
     if (lane == 0) {
       s_stat[0] = mean;
-      s_stat[1] = s_gen_ok ? rsqrtf(m2 / ntot + a.eps) : __int_as_float(0x7fc00000);
+      s_stat[1] = good ? rsqrtf(m2 / ntot + a.eps) : __int_as_float(0x7fc00000);
+      // every block has published, so every block has read the sequence word: block 0 advances it
+      // here instead of a finished-block count at exit (ar_end)
+      if (b == 0) __hip_atomic_store(&ctl->seq, call, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   __syncthreads();
@@ -427,7 +425,6 @@ __global__ __launch_bounds__(256) void ar_res_ln_dist_kernel(ARPeers peers, ARCt
       store8_t<DT>(a.xn2_out + i * 8, o);
     }
   }
-  ar_end(ctl, call);
 }
 
 // ----------------------------------------- one-shot + residual + row statistics (TP decode, M rows)
@@ -506,8 +503,7 @@ __global__ __launch_bounds__(256) void ar_res_stats_kernel(ARPeers peers, ARCtl*
     q += __shfl_xor(q, 4, 64);
     if ((tid & 7) == 0) rs_publish(rs, (int)row, (int)(col / 64), mean, q);
   }
-  ar_end(ctl, call);
-  rs_arrive_of(rs, b, nb);
+  rs_arrive_of(rs, b, nb, &ctl->seq, call);  // (its last arrival advances the sequence word)
 }
 
 KCA_API int kca_ar_signal_bytes() { return (int)sizeof(ARSignal); }

@@ -103,8 +103,11 @@ __device__ __forceinline__ void rs_merge(const RowStats& s) {
 // Arrival of one workgroup (every thread calls it): the decode_tail.h protocol -- write-through
 // partials drained, barrier, a two-level agent-scope count (sub-counter `sub` of 64, `members`
 // arrivals there; `nsub` sub-counters in use), the last arrival re-arms the counters, acquires, and
-// merges.
-__device__ __forceinline__ void rs_arrive(const RowStats& s, int sub, unsigned members, int nsub) {
+// merges. `seq` (the all-reduce close, xgmi_allreduce.hip): the last arrival also advances the
+// all-reduce's sequence word to `call` -- every workgroup has read it by then -- so that kernel needs
+// no finished-block count of its own.
+__device__ __forceinline__ void rs_arrive(const RowStats& s, int sub, unsigned members, int nsub,
+                                          uint32_t* seq = nullptr, uint32_t call = 0) {
   __shared__ int s_last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -117,6 +120,7 @@ __device__ __forceinline__ void rs_arrive(const RowStats& s, int sub, unsigned m
     }
     if (last) {
       __hip_atomic_store(s.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (seq) __hip_atomic_store(seq, call, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -129,8 +133,9 @@ __device__ __forceinline__ void rs_arrive(const RowStats& s, int sub, unsigned m
 }
 
 // Arrival of workgroup `b` of `G` taking part in one tail.
-__device__ __forceinline__ void rs_arrive_of(const RowStats& s, int b, int G) {
+__device__ __forceinline__ void rs_arrive_of(const RowStats& s, int b, int G, uint32_t* seq = nullptr,
+                                             uint32_t call = 0) {
   constexpr int NSUB = kDualSub;
   const int sub = b % NSUB;
-  rs_arrive(s, sub, (unsigned)((G - sub + NSUB - 1) / NSUB), G < NSUB ? G : NSUB);
+  rs_arrive(s, sub, (unsigned)((G - sub + NSUB - 1) / NSUB), G < NSUB ? G : NSUB, seq, call);
 }

@@ -237,7 +237,7 @@ class XGMIAllReduce:
         """fp32 [16384] sums + the tail's zero-initialised arrival counters (local, not IPC-shared)."""
         ws = self._tails.get(str(dev))
         if ws is None:
-            ws = (torch.empty(16384, device=dev, dtype=torch.float32),
+            ws = (torch.zeros(16384, device=dev, dtype=torch.float32),  # (zeroed: tagged slots, see kernel)
                   torch.zeros(32 * 65, device=dev, dtype=torch.int32))
             self._tails[str(dev)] = ws
         return ws
