@@ -17,16 +17,16 @@ __device__ __forceinline__ float gelu_erf_grad(float x) {
   return cdf + x * pdf;
 }
 
-template <bool TANH>
+template <bool TANH, int DT = 0>  // DT: 0 bf16, 1 fp16 (common.h)
 __global__ void gelu_fwd_kernel(const bf16_t* __restrict__ u,
                                 bf16_t* __restrict__ y, long long n8) {
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8;
        i += (long long)gridDim.x * blockDim.x) {
     float v[8];
-    load8(u + i * 8, v);
+    load8_t<DT>(u + i * 8, v);
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = TANH ? gelu_tanh(v[j]) : gelu_erf(v[j]);
-    store8(y + i * 8, v);
+    store8_t<DT>(y + i * 8, v);
   }
 }
 
@@ -56,6 +56,19 @@ KCA_API int kca_gelu_fwd(const void* u, void* y, long long n, int approx_tanh,
   else
     hipLaunchKernelGGL(gelu_fwd_kernel<false>, dim3(kca_grid(n8, 256)), dim3(256), 0,
                        stream, (const bf16_t*)u, (bf16_t*)y, n8);
+  return 0;
+}
+
+// fp16 (the FT / DS-Inference serving precision: decode fc_in after hipBLASLt at batch > the fused layer's)
+KCA_API int kca_gelu_fwd_f16(const void* u, void* y, long long n, int approx_tanh, hipStream_t stream) {
+  if (n % 8) return 1;
+  const long long n8 = n / 8;
+  if (approx_tanh)
+    hipLaunchKernelGGL((gelu_fwd_kernel<true, 1>), dim3(kca_grid(n8, 256)), dim3(256), 0, stream, (const bf16_t*)u,
+                       (bf16_t*)y, n8);
+  else
+    hipLaunchKernelGGL((gelu_fwd_kernel<false, 1>), dim3(kca_grid(n8, 256)), dim3(256), 0, stream, (const bf16_t*)u,
+                       (bf16_t*)y, n8);
   return 0;
 }
 

@@ -425,10 +425,11 @@ class ModelRunner:
         # 4.27 at 32 (the per-projection step overlaps the MLP GEMMs with the attention on a side stream);
         # BLOOM TP=8 rank 11.46 vs 12.58 at 16, 14.25 vs 13.50 at 32 (hipBLASLt streams the 14336-wide
         # shapes faster from M = 32); NeoX wins at every batch (12.84 vs 15.86 at 32, 25.9 vs 28.3 at 64)
-        # (fp16: the matrix-core layer at every batch -- the per-projection path's LayerNorm / GELU / bias
-        # steps are bf16-only kernels and run eager in fp16: GPT-J B=32 5.07 vs 4.76 ms)
+        # fp16 takes the same caps since the per-projection path's LayerNorm / GELU run their fp16
+        # instantiations (ln_rows, kca_gelu_fwd_f16) instead of eager kernels: B=32 GPT-J 4.40 vs 4.65 ms,
+        # BLOOM rank 13.38 vs 14.84 per-projection vs matrix-core layer (profiles/decode_fp16_cap_ab_r6.jsonl)
         self._batched_max_b = int(os.environ.get("KCA_DECODE_BATCHED_MAX_B", "0")) or \
-            (64 if self.dtype == torch.float16 else {"gptj": 16, "seq": 16}.get(self._layer_kind, 64))
+            {"gptj": 16, "seq": 16}.get(self._layer_kind, 64)
 
     # ------------------------------------------------------------- prefill
     @torch.no_grad()

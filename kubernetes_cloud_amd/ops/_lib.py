@@ -44,6 +44,7 @@ _SIGS = {
     "kca_layernorm_bwd_parts": [I],
     "kca_layernorm_bwd": [P, P, P, P, P, P, P, P, P, I, P, I, I, P],
     "kca_gelu_fwd": [P, P, LL, I, P],
+    "kca_gelu_fwd_f16": [P, P, LL, I, P],
     "kca_gelu_bwd": [P, P, P, LL, I, P],
     "kca_quick_gelu_fwd": [P, P, LL, P],
     "kca_quick_gelu_bwd": [P, P, P, LL, P],

@@ -92,9 +92,11 @@ def _linear_act(x, weight, bias, act):
     if not act:
         return F.linear(x, weight, bias)
     y = F.linear(x, weight, bias)
-    if _lib.use_native(y) and y.is_contiguous() and y.numel() % 8 == 0 \
-            and y.data_ptr() % 16 == 0 and y.dtype == torch.bfloat16:
-        _lib.call("kca_gelu_fwd", y.data_ptr(), y.data_ptr(), y.numel(), int(act == 1), _lib.stream())
+    f16 = _lib.native_f16(y) and _lib.has("kca_gelu_fwd_f16")
+    if (_lib.use_native(y) or f16) and y.is_contiguous() and y.numel() % 8 == 0 and y.data_ptr() % 16 == 0 \
+            and y.dtype in (torch.bfloat16, torch.float16):
+        _lib.call("kca_gelu_fwd_f16" if f16 else "kca_gelu_fwd", y.data_ptr(), y.data_ptr(), y.numel(),
+                  int(act == 1), _lib.stream())
         return y
     return _act_ref(y, act)
 
@@ -188,11 +190,14 @@ def ln_skinny_linear(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor | 
         xn, h = ln_rows(x, gamma, beta, eps, residuals)
         y = skinny_linear(xn, weight, bias, act)
         return (y, h, xn) if want_xn else (y, h)
-    from .norms import layer_norm
-    if residuals:
-        xn, h = layer_norm(x, gamma, beta, eps, residual=residuals)
+    if _lib.native_f16(x, gamma):  # fp16 rows: the register-resident LN kernel's fp16 instantiation
+        xn, h = ln_rows(x, gamma, beta, eps, residuals)
     else:
-        xn, h = layer_norm(x, gamma, beta, eps), x
+        from .norms import layer_norm
+        if residuals:
+            xn, h = layer_norm(x, gamma, beta, eps, residual=residuals)
+        else:
+            xn, h = layer_norm(x, gamma, beta, eps), x
     y = skinny_linear(xn, weight, bias, act)
     return (y, h, xn) if want_xn else (y, h)
 

@@ -980,13 +980,20 @@ def test_engine_fp16_native_decode(preset, monkeypatch):
         raise AssertionError("fp16 decode fell back to PyTorch")
     monkeypatch.setattr(dmod, "decode_attention_reference", boom)
     monkeypatch.setattr(dmod, "sample_logits_reference", boom)
+    from kubernetes_cloud_amd.ops import gemv as gmod
+    monkeypatch.setattr(gmod, "_act_ref", boom)  # the per-projection path's GELU: fp16 kernel, not eager
     g = torch.Generator().manual_seed(3)
-    for B in (1, 5):
-        prompts = [[int(x) for x in torch.randint(0, 1000, (30 + 7 * i,), generator=g)] for i in range(B)]
+    for B in (1, 5, 20):  # 20: above the GPT-J / BLOOM matrix-core cap -> the per-projection path in fp16
+        prompts = [[int(x) for x in torch.randint(0, 1000, (30 + 7 * (i % 5),), generator=g)] for i in range(B)]
         eng = LLMEngine(m, max_slots=B, max_len=256, use_graphs=True)
         assert eng.runner._batched_ok
         outs = [r.output for r in eng.generate(prompts, SamplingParams(max_new_tokens=12, do_sample=False))]
-        assert (eng.runner.fused_steps if B == 1 else eng.runner.batched_steps) > 0
+        if B == 1:
+            assert eng.runner.fused_steps > 0
+        elif B <= eng.runner._batched_max_b:
+            assert eng.runner.batched_steps > 0
+        else:
+            assert eng.runner.batched_steps == 0
         for p, o in zip(prompts, outs):
             _check_against_forward(m, p, o)
         sp = SamplingParams(max_new_tokens=8, do_sample=True, temperature=0.9, top_k=40, top_p=0.9, seed=17)
