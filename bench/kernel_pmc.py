@@ -50,6 +50,25 @@ def _attn(B, S, H, D, causal):
     return run, {"fwd_flops": f, "bwd_flops": 2.5 * f}
 
 
+def _attn_sd_tiled(B, S, H, hd, dp):
+    """The DreamBooth UNet self-attention as it runs in training (models/unet.py Attention.forward): one
+    fused [B, S, 3*H*dp] QKV buffer whose 40-wide heads are stored 48 wide (zero columns 40..47), the
+    narrow-storage tiled kernels (attention_tiled.hip StagerNarrow, DS = 48 in the D = 64 LDS images)."""
+    q5 = torch.randn(B, S, 3, H, dp, device=DEV, dtype=BF)
+    q5[..., hd:] = 0
+    qkv = q5.view(B, S, 3 * H * dp).requires_grad_(True)
+    do = torch.randn(B, S, H * dp, device=DEV, dtype=BF)
+    do.view(B, S, H, dp)[..., hd:] = 0
+
+    def run():
+        o = ops.qkv_rope_attention(qkv, H, dp, 0, False, causal=False, scale=hd ** -0.5)
+        o.backward(do)
+        qkv.grad = None
+
+    f = 4.0 * B * H * S * S * hd
+    return run, {"fwd_flops": f, "bwd_flops": 2.5 * f}
+
+
 def _layernorm(rows, d):
     x = torch.randn(rows, d, device=DEV, dtype=BF, requires_grad=True)
     w = torch.randn(d, device=DEV, dtype=BF, requires_grad=True)
@@ -177,6 +196,7 @@ def _mm(M, N, K):
 CASES = {
     "attn_gptj": lambda: _attn(8, 2048, 16, 256, True),
     "attn_sd64": lambda: _attn(16, 4096, 8, 40, False),
+    "attn_sd_tiled48": lambda: _attn_sd_tiled(16, 4096, 8, 40, 48),
     "layernorm_gptj": lambda: _layernorm(16384, 4096),
     "groupnorm_nhwc_sd": lambda: _groupnorm(8, 320, 64, 64),
     "geglu_sd": lambda: _geglu(32768, 1280),
