@@ -36,6 +36,9 @@ CASE_OF = [
     (r"attn_fwd_w8_kernel<256", "attn_gptj", "fwd_flops", None),
     (r"attn_bwd_dq_tiled_kernel<256", "attn_gptj", "bwd_flops_dq", None),
     (r"attn_bwd_dkdv_tiled_kernel<256", "attn_gptj", "bwd_flops_dkdv", None),
+    (r"attn_fwd_tiled_kernel<64, false, -1, 48", "attn_sd_tiled48", "fwd_flops", None),
+    (r"attn_bwd_dq_tiled_kernel<64, false, 48", "attn_sd_tiled48", "bwd_flops_dq", None),
+    (r"attn_bwd_dkdv_tiled_kernel<64, false, 48", "attn_sd_tiled48", "bwd_flops_dkdv", None),
     (r"attn_fwd_kernel<64, false>", "attn_sd64", "fwd_flops", None),
     (r"attn_bwd_dq_kernel<64, false>", "attn_sd64", "bwd_flops_dq", None),
     (r"attn_bwd_dkdv_kernel<64, false>", "attn_sd64", "bwd_flops_dkdv", None),
@@ -106,7 +109,7 @@ def main():
     rows = []
     for kern, ctr in merged.items():
         match = next((m for m in CASE_OF if re.search(m[0], kern)), None)
-        if match is None or kern not in trace:
+        if match is None or kern not in trace or match[1] not in cases:
             continue
         _, case, fkey, bkey = match
         ns = trace[kern]
