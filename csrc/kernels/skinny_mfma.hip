@@ -56,9 +56,13 @@ __device__ __forceinline__ u32x4v ld16(const uint16_t* p) { return *reinterpret_
 struct MmPart {
   const uint16_t* x;      // [M, K] activation rows (row stride ldx)
   long long ldx;
-  const uint16_t* w;      // [N, K] weight (row stride ldw)
+  const uint16_t* w;      // [N, K] weight (row stride ldw), or packed (below)
   long long ldw;
   int K;
+  // 1: w is the packed stream layout [ceil(N/16)][ceil(K/128)][16][128] (zero-padded; ldw = elements
+  // per 16-row block): a wave's 16 x 128 sub-tile is 4 KB contiguous and a KC = 128 load instruction
+  // reads 1 KB contiguous (the row-run pattern that streams at 6-6.8 TB/s, profiles/stream_probe_r6)
+  int packed;
   const float* stats;     // [M][2] (mean, rstd): x is the residual stream, normalised on load (or null)
   const uint16_t* gamma;  // [K] (with stats)
   const uint16_t* beta;   // [K] (nullable)
@@ -204,7 +208,11 @@ __global__ __launch_bounds__(WV * 64) void mm_skinny_kernel(MmArgs a) {
       for (int i = 0; i < T::NI; ++i) {
         int n = nw0 + nr * 16 + i * T::RPI + lr;
         n = n < N ? n : N - 1;  // rows past N: any valid row (their outputs are never stored)
-        wr[nr][i] = kv ? ld_nt16(P.w + (long long)n * P.ldw + k0 + lp * 8) : u32x4v{0u, 0u, 0u, 0u};
+        const int kk = k0 + lp * 8;
+        const long long off = P.packed ? (long long)(n >> 4) * P.ldw + ((long long)(kk >> 7) * 16 + (n & 15)) * 128 +
+                                             (kk & 127)
+                                       : (long long)n * P.ldw + kk;
+        wr[nr][i] = kv ? ld_nt16(P.w + off) : u32x4v{0u, 0u, 0u, 0u};
       }
   };
   // activation chunk: piece q = tid + WV*64 j of the [MT*16][PPR] stage

@@ -410,6 +410,7 @@ class ModelRunner:
         # out-proj + fc_out one K-concatenated launch). KCA_DECODE_FUSED_BATCHED=0: per-projection path.
         d_model = cfg.hidden
         self.batched_steps = 0
+        self._packs = {}  # packed weight twins of the matrix-core layer (_packed_w)
         self.fused_steps = 0  # batch-1 fused-layer steps built (eager runs and graph captures)
         # (real TP: sequential layers only -- each row-parallel projection closed by the custom all-reduce's
         # residual + row-statistics tail, parallel/custom_ar.py res_stats)
@@ -693,6 +694,11 @@ class ModelRunner:
         hb.copy_(h)
         tbl = self.cache.table_on(self.device)
         cos, sin, tbl, by_row = self._desc_args(self.cos, self.sin, tbl)
+        pk = self._packed_w
+
+        def part(x, w, ln=None):  # one K-part, streaming the weight's packed twin
+            return smm.part(x, w, ln, packed=pk(w))
+
         for li, blk in enumerate(m.h):
             at, mlp = blk.attn, blk.mlp
             act = 1 if mlp.approx in ("tanh", True) else 2
@@ -705,27 +711,27 @@ class ModelRunner:
             if kind == "seq" and self._tp_ar is not None:
                 # TP rank: partial projections, each closed by all-reduce + bias + residual + row statistics
                 ar, y = self._tp_ar, fz["y"]
-                smm.launch([smm.job([smm.part(x1, at.qkv.weight, ln1)], qkv.shape[1], qkv, at.qkv.bias)], B, dt)
+                smm.launch([smm.job([part(x1, at.qkv.weight, ln1)], qkv.shape[1], qkv, at.qkv.bias)], B, dt)
                 o = dops.decode_prep_attention(qkv, self.H, self.Hkv, self.D, self.rot, cfg.rotary_interleaved,
                                                cos, sin, pos, slots, kc, vc, kv_lens, max_kv, at.scale, at.alibi,
                                                out=obuf, ws=ws, block_table=tbl, window=at.window, by_row=by_row)
-                smm.mm(o, at.out.weight, out=y)
+                smm.mm(o, at.out.weight, out=y, packed=pk(at.out.weight))
                 ar.res_stats(y, at.out.bias, hb, hb, st, blk.ln_2.eps)
-                smm.launch([smm.job([smm.part(hb, mlp.fc_in.weight, (st.stats, blk.ln_2.weight, blk.ln_2.bias))],
+                smm.launch([smm.job([part(hb, mlp.fc_in.weight, (st.stats, blk.ln_2.weight, blk.ln_2.bias))],
                                     g.shape[1], g, mlp.fc_in.bias, act)], B, dt)
-                smm.mm(g, mlp.fc_out.weight, out=y)
+                smm.mm(g, mlp.fc_out.weight, out=y, packed=pk(mlp.fc_out.weight))
                 ar.res_stats(y, mlp.fc_out.bias, hb, hb, st, nln.eps)
                 continue
             if kind == "seq":
-                smm.launch([smm.job([smm.part(x1, at.qkv.weight, ln1)], qkv.shape[1], qkv, at.qkv.bias)], B, dt)
+                smm.launch([smm.job([part(x1, at.qkv.weight, ln1)], qkv.shape[1], qkv, at.qkv.bias)], B, dt)
                 o = dops.decode_prep_attention(qkv, self.H, self.Hkv, self.D, self.rot, cfg.rotary_interleaved,
                                                cos, sin, pos, slots, kc, vc, kv_lens, max_kv, at.scale, at.alibi,
                                                out=obuf, ws=ws, block_table=tbl, window=at.window, by_row=by_row)
-                smm.launch([smm.job([smm.part(o, at.out.weight)], hb.shape[1], hb, at.out.bias, res=hb, stats=st,
+                smm.launch([smm.job([part(o, at.out.weight)], hb.shape[1], hb, at.out.bias, res=hb, stats=st,
                                     eps=blk.ln_2.eps)], B, dt)
-                smm.launch([smm.job([smm.part(hb, mlp.fc_in.weight, (st.stats, blk.ln_2.weight, blk.ln_2.bias))],
+                smm.launch([smm.job([part(hb, mlp.fc_in.weight, (st.stats, blk.ln_2.weight, blk.ln_2.bias))],
                                     g.shape[1], g, mlp.fc_in.bias, act)], B, dt)
-                smm.launch([smm.job([smm.part(g, mlp.fc_out.weight)], hb.shape[1], hb, mlp.fc_out.bias, res=hb,
+                smm.launch([smm.job([part(g, mlp.fc_out.weight)], hb.shape[1], hb, mlp.fc_out.bias, res=hb,
                                     stats=st, eps=nln.eps)], B, dt)
                 continue
             # parallel residual: [QKV | fc_in] of the same residual rows, one launch
@@ -734,17 +740,17 @@ class ModelRunner:
                 x2 = xn2 if first else hb
             else:
                 ln2, x2 = ln1, x1
-            smm.launch([smm.job([smm.part(x1, at.qkv.weight, ln1)], qkv.shape[1], qkv, at.qkv.bias),
-                        smm.job([smm.part(x2, mlp.fc_in.weight, ln2)], g.shape[1], g, mlp.fc_in.bias, act)], B, dt)
+            smm.launch([smm.job([part(x1, at.qkv.weight, ln1)], qkv.shape[1], qkv, at.qkv.bias),
+                        smm.job([part(x2, mlp.fc_in.weight, ln2)], g.shape[1], g, mlp.fc_in.bias, act)], B, dt)
             o = dops.decode_prep_attention(qkv, self.H, self.Hkv, self.D, self.rot, cfg.rotary_interleaved,
                                            cos, sin, pos, slots, kc, vc, kv_lens, max_kv, at.scale, at.alibi,
                                            out=obuf, ws=ws, block_table=tbl, window=at.window, by_row=by_row)
-            smm.launch([smm.job([smm.part(o, at.out.weight), smm.part(g, mlp.fc_out.weight)], hb.shape[1], hb,
+            smm.launch([smm.job([part(o, at.out.weight), part(g, mlp.fc_out.weight)], hb.shape[1], hb,
                                 fz["bias"][li], res=hb, stats=st, eps=nln.eps)], B, dt)
         w, b, grp = self._head_weight()
         V = w.shape[0]
         if V % 4 == 0:
-            logits = smm.mm(hb, w, b, ln=(st.stats, m.ln_f.weight, m.ln_f.bias))
+            logits = smm.mm(hb, w, b, ln=(st.stats, m.ln_f.weight, m.ln_f.bias), packed=pk(w))
         else:  # (GPT-2's 50257 rows: the head takes the normalised rows through the plain path)
             y = smm.ln_on_load_reference(hb, st.stats, m.ln_f.weight, m.ln_f.bias)
             logits = skinny_linear(y, w, b)
@@ -752,6 +758,19 @@ class ModelRunner:
             from ..parallel.tensor_parallel import gather_last_dim
             logits = gather_last_dim(logits, grp)
         return logits
+
+    def _packed_w(self, w):
+        """The packed stream twin of a weight the matrix-core layer reads (``skinny_mm.pack_weight``):
+        built once, on the first (eager) step that uses it -- the graph-capture warm-up -- and kept for the
+        runner's life (KCA_MM_PACK=0: none, the row-major weight streams). Keyed by storage address,
+        shape and version (an in-place weight update re-packs)."""
+        if not smm.PACK:
+            return None
+        key = (w.data_ptr(), tuple(w.shape), w._version)
+        p = self._packs.get(key)
+        if p is None and not torch.cuda.is_current_stream_capturing():
+            p = self._packs[key] = smm.pack_weight(w.detach())
+        return p
 
     def _layers_decode(self, tokens, pos, slots, kv_lens, max_kv, ws, obuf):
         m, cfg = self.model, self.cfg

@@ -33,8 +33,8 @@ _F = ctypes.c_float
 
 
 class _Part(ctypes.Structure):
-    _fields_ = [("x", _P), ("ldx", _LL), ("w", _P), ("ldw", _LL), ("K", _I), ("stats", _P), ("gamma", _P),
-                ("beta", _P)]
+    _fields_ = [("x", _P), ("ldx", _LL), ("w", _P), ("ldw", _LL), ("K", _I), ("packed", _I), ("stats", _P),
+                ("gamma", _P), ("beta", _P)]
 
 
 class _Job(ctypes.Structure):
@@ -98,10 +98,30 @@ def supported(x: torch.Tensor, w: torch.Tensor) -> bool:
             and x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0 and w.shape[1] == K)
 
 
-def part(x, w, ln=None):
-    """One K-part: x [M, K], w [N, K]; ``ln=(stats [M, 2] fp32, gamma, beta)`` normalises x on load."""
+# packed weight stream (pack_weight): the decode runner keeps a packed twin of every weight the batched
+# layer streams (KCA_MM_PACK=0: the row-major weights themselves)
+PACK = os.environ.get("KCA_MM_PACK", "1") not in ("0", "false")
+
+
+def pack_weight(w: torch.Tensor) -> torch.Tensor:
+    """[N, K] -> the kernel's packed stream layout [ceil(N/16), ceil(K/128), 16, 128], zero-padded: each
+    wave's 16-row x 128-column sub-tile is one contiguous 4 KB block (``MmPart.packed``)."""
+    N, K = w.shape
+    Np, Kp = -(-N // 16) * 16, -(-K // 128) * 128
+    if (Np, Kp) != (N, K):
+        wz = w.new_zeros(Np, Kp)
+        wz[:N, :K] = w
+        w = wz
+    return w.reshape(Np // 16, 16, Kp // 128, 128).permute(0, 2, 1, 3).contiguous()
+
+
+def part(x, w, ln=None, packed=None):
+    """One K-part: x [M, K], w [N, K]; ``ln=(stats [M, 2] fp32, gamma, beta)`` normalises x on load;
+    ``packed``: ``pack_weight(w)``, streamed instead of w."""
     p = _Part()
     p.x, p.ldx, p.w, p.ldw, p.K = x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), x.shape[1]
+    if packed is not None:
+        p.w, p.ldw, p.packed = packed.data_ptr(), packed.shape[1] * 16 * 128, 1
     if ln is not None:
         st, g, b = ln
         p.stats, p.gamma, p.beta = st.data_ptr(), g.data_ptr(), _lib.ptr(b)
@@ -178,13 +198,13 @@ def launch(jobs, M: int, dtype: torch.dtype, ks: int | None = None, nr: int | No
 
 
 def mm(x: torch.Tensor, w: torch.Tensor, bias=None, act: int = 0, out=None, res=None, stats=None, eps=1e-5,
-       ln=None) -> torch.Tensor:
+       ln=None, packed=None) -> torch.Tensor:
     """Single-job convenience: ``act(LN?(x) W^T + b) (+ res)``."""
     M = x.shape[0]
     N = w.shape[0]
     if out is None:
         out = torch.empty(M, N, device=x.device, dtype=x.dtype)
-    launch([job([part(x, w, ln)], N, out, bias, act, res, stats, eps)], M, x.dtype)
+    launch([job([part(x, w, ln, packed)], N, out, bias, act, res, stats, eps)], M, x.dtype)
     return out
 
 

@@ -135,3 +135,49 @@ def test_split_k_is_deterministic(M):
         outs.append(y)
     torch.cuda.synchronize()
     assert all(torch.equal(outs[0], o) for o in outs[1:])
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M", [2, 8, 16, 32, 64])
+@pytest.mark.parametrize("NK", [(1024, 4096), (1360, 1000), (640, 6208), (2052, 1800)])
+def test_packed_weight_stream_is_bit_identical(dt, M, NK):
+    """The packed stream layout (pack_weight: 16 x 128 sub-tiles, zero-padded rows / columns) feeds the
+    same fragments as the row-major weight, so every variant's output is bit-identical -- two K parts,
+    the residual + row-stats tail and LN-on-load included -- and matches the fp32 reference."""
+    N, K = NK
+    g = torch.Generator(device=DEV).manual_seed(M * 13 + N)
+    x = torch.randn(M, K, generator=g, device=DEV).to(dt)
+    w = _w(N, K, dt, g)
+    wp = sm.pack_weight(w)
+    assert wp.shape == (-(-N // 16), -(-K // 128), 16, 128)
+    b = (0.1 * torch.randn(N, generator=g, device=DEV)).to(dt)
+    for act in (0, 1):
+        y0 = sm.mm(x, w, b, act)
+        y1 = sm.mm(x, w, b, act, packed=wp)
+        assert torch.equal(y0, y1)
+        _close(y1, sm.mm_reference([(x, w, None)], b, act, dtype=dt), 1.5e-2)
+    for kc in (128, 256):  # both chunk widths read the 128-wide sub-tiles
+        old = sm._KC
+        sm._KC = kc
+        try:
+            assert torch.equal(sm.mm(x, w, b), sm.mm(x, w, b, packed=wp))
+        finally:
+            sm._KC = old
+    # two K parts into one residual with the row-stats tail, then LN-on-load from those statistics
+    if N % 64 == 0:
+        K2 = 512
+        x2 = torch.randn(M, K2, generator=g, device=DEV).to(dt)
+        w2 = _w(N, K2, dt, g)
+        h = torch.randn(M, N, generator=g, device=DEV).to(dt)
+        outs = []
+        for pk in (False, True):
+            hb = h.clone()
+            st = sm.RowStatsBuf(M, N, DEV)
+            parts = [sm.part(x, w, packed=wp if pk else None),
+                     sm.part(x2, w2, packed=sm.pack_weight(w2) if pk else None)]
+            sm.launch([sm.job(parts, N, hb, b, res=hb, stats=st)], M, dt)
+            wn = _w(256, N, dt, g) if not outs else outs[0][2]
+            gam = torch.ones(N, device=DEV, dtype=dt)
+            y = sm.mm(hb, wn, ln=(st.stats, gam, None), packed=sm.pack_weight(wn) if pk else None)
+            outs.append((hb, y, wn))
+        assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
