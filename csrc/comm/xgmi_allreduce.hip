@@ -503,7 +503,10 @@ __global__ __launch_bounds__(256) void ar_res_stats_kernel(ARPeers peers, ARCtl*
     q += __shfl_xor(q, 4, 64);
     if ((tid & 7) == 0) rs_publish(rs, (int)row, (int)(col / 64), mean, q);
   }
-  rs_arrive_of(rs, b, nb, &ctl->seq, call);  // (its last arrival advances the sequence word)
+  if (rs.stats)
+    rs_arrive_of(rs, b, nb, &ctl->seq, call);  // (its last arrival advances the sequence word)
+  else
+    ar_end(ctl, call);  // publish-only: the consuming projection merges the partials (MmPart.st_nt)
 }
 
 KCA_API int kca_ar_signal_bytes() { return (int)sizeof(ARSignal); }
@@ -695,7 +698,7 @@ static int ar_res_stats(void* const* stage0, void* const* stage1, void* const* s
                         const void* bias, const void* h, void* h_out, float eps, float* part, float* stats,
                         unsigned int* cnt, hipStream_t stream) {
   if (world < 1 || world > AR_MAX_RANKS || rank < 0 || rank >= world || N % 64 || N <= 0 || N > 16384 || M < 1 ||
-      M > 64 || blocks < 1 || blocks > AR_MAX_BLOCKS || !part || !stats || !cnt || !h || !h_out)
+      M > 64 || blocks < 1 || blocks > AR_MAX_BLOCKS || !part || (stats && !cnt) || !h || !h_out)
     return 1;
   if (((uintptr_t)in | (uintptr_t)h | (uintptr_t)h_out | (uintptr_t)bias | (uintptr_t)part | (uintptr_t)stats) & 15)
     return 2;

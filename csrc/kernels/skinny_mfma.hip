@@ -66,6 +66,11 @@ struct MmPart {
   const float* stats;     // [M][2] (mean, rstd): x is the residual stream, normalised on load (or null)
   const uint16_t* gamma;  // [K] (with stats)
   const uint16_t* beta;   // [K] (nullable)
+  // st_nt > 0: `stats` holds the producer's unmerged per-slice partials [M][st_nt][2] (mean, M2 of K /
+  // st_nt columns each, mm_tail.h rs_publish) and every workgroup merges them in its prologue (st_eps:
+  // the LayerNorm's eps) -- the producing tail then needs no arrival count and no last-arriver merge
+  int st_nt;
+  float st_eps;
 };
 
 struct MmJob {
@@ -223,21 +228,63 @@ __global__ __launch_bounds__(WV * 64) void mm_skinny_kernel(MmArgs a) {
   static_assert((WV * 64) % T::PPR == 0, "a thread's pieces share one column");
   const int xp = tid % T::PPR;
   float mu[2][T::XP], rsd[2][T::XP];
-  if constexpr (LN) {
+  // the rows' (mean, rstd) per part: read (merged stats) or merged here from the producer's partials
+  // (st_nt > 0: one wave per row, lanes over slices, Chan's equal-count merge as mm_tail.h rs_merge)
+  __shared__ float s_ms[2][64][2];  // merged (mean, rstd) per part and row (st_nt > 0)
+  auto ln_stats = [&]() {
+    if constexpr (LN) {
+      bool merged = false;
 #pragma unroll
-    for (int pi = 0; pi < 2; ++pi)
+      for (int pi = 0; pi < 2; ++pi) {
+        if (pi >= J.nparts || J.p[pi].st_nt <= 0) continue;
+        merged = true;
+        const MmPart& P = J.p[pi];
+        const int NT = P.st_nt;
+        const float c = (float)P.K / (float)NT;
+        for (int m = wv; m < M; m += WV) {
+          const float* pp = P.stats + (long long)m * NT * 2;
+          float2 v[16];  // NT <= 1024 slices per row
 #pragma unroll
-      for (int j = 0; j < T::XP; ++j) {
-        const int m = (tid + WV * 64 * j) / T::PPR;
-        mu[pi][j] = 0.f;
-        rsd[pi][j] = 0.f;
-        if (pi < J.nparts && m < M) {
-          const float2 v = *reinterpret_cast<const float2*>(J.p[pi].stats + 2 * m);
-          mu[pi][j] = v.x;
-          rsd[pi][j] = v.y;
+          for (int i = 0; i < 16; ++i) {
+            const int t = lane + 64 * i;
+            v[i] = t < NT ? *reinterpret_cast<const float2*>(pp + 2 * t) : make_float2(0.f, 0.f);
+          }
+          float sm = 0.f;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) sm += v[i].x;
+          const float mean = wave_sum(sm) / (float)NT;
+          float q = 0.f;
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if (lane + 64 * i < NT) q += v[i].y + c * (v[i].x - mean) * (v[i].x - mean);
+          const float var = wave_sum(q) / (float)P.K;
+          if (lane == 0) {
+            s_ms[pi][m][0] = mean;
+            s_ms[pi][m][1] = rsqrtf(var + P.st_eps);
+          }
         }
       }
-  }
+      if (merged) __syncthreads();
+#pragma unroll
+      for (int pi = 0; pi < 2; ++pi)
+#pragma unroll
+        for (int j = 0; j < T::XP; ++j) {
+          const int m = (tid + WV * 64 * j) / T::PPR;
+          mu[pi][j] = 0.f;
+          rsd[pi][j] = 0.f;
+          if (pi < J.nparts && m < M) {
+            if (J.p[pi].st_nt > 0) {
+              mu[pi][j] = s_ms[pi][m][0];
+              rsd[pi][j] = s_ms[pi][m][1];
+            } else {
+              const float2 v = *reinterpret_cast<const float2*>(J.p[pi].stats + 2 * m);
+              mu[pi][j] = v.x;
+              rsd[pi][j] = v.y;
+            }
+          }
+        }
+    }
+  };
   auto load_x = [&](int c, u32x4v (&xr)[T::XP], u32x4v& gv, u32x4v& bv) {
     int k0;
     const MmPart& P = J.p[chunk_part(J, c, nc0, KC, k0)];
@@ -321,6 +368,7 @@ __global__ __launch_bounds__(WV * 64) void mm_skinny_kernel(MmArgs a) {
 #pragma unroll
   for (int q = 0; q < PF; ++q)
     if (c_lo + q < c_hi) load_w(c_lo + q, wa[q]);
+  ln_stats();  // (under the first weight chunk's loads)
   if (c_lo < c_hi) {
     load_x(c_lo, xr, gv, bv);
     store_x(xr, gv, bv, c_lo, 0);
@@ -405,7 +453,18 @@ __global__ __launch_bounds__(WV * 64) void mm_skinny_kernel(MmArgs a) {
   for (int nr = 0; nr < NRW; ++nr)
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) mm_store<DT>(J, M, nw0 + nr * 16, mt, lane, acc[nr][mt], tm[nr][mt], tq[nr][mt]);
-  if (J.part) {
+  if (J.part && !J.stats_out) {
+    // publish-only (the consumer merges, MmPart.st_nt): every 16-row tile's (mean, M2) per row, slice
+    // index = tile row / 16 -- no LDS reduction, no arrival
+    const RowStats s{J.part, nullptr, nullptr, M, J.N, J.eps, 16};
+#pragma unroll
+    for (int nr = 0; nr < NRW; ++nr)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int m = mt * 16 + r16;
+        if (g == 0 && m < M && nw0 + nr * 16 < J.N) rs_publish(s, m, (nw0 + nr * 16) >> 4, tm[nr][mt], tq[nr][mt]);
+      }
+  } else if (J.part) {
     // the block's row statistics: the wave's NRW tiles merged in registers, the WV waves through LDS,
     // one (mean, M2) per row per block published (N % (WV * NRW * 16) == 0 for a stats job)
     float* red = reinterpret_cast<float*>(mm_lds);  // [WV][MT*16][2]
@@ -573,7 +632,7 @@ static int mm_check(const MmArgs& a, int dtype, int& ln) {
     const MmJob& J = a.j[i];
     if (J.N < 1 || J.N % 4 || J.nparts < 1 || J.nparts > 2 || !J.y || J.ldy % 4 || !al8(J.y) || !al8(J.bias)) return 1;
     if (J.res && (J.ldr % 4 || !al8(J.res) || J.act)) return 1;
-    if (J.part && (J.N % 16 || !J.stats_out || !J.cnt)) return 1;
+    if (J.part && (J.N % 16 || (J.stats_out && !J.cnt))) return 1;
     for (int q = 0; q < J.nparts; ++q) {
       const MmPart& P = J.p[q];
       if (P.K < 8 || P.K % 8 || P.ldx % 8 || P.ldw % 8 || !P.x || !P.w || !al16(P.x) || !al16(P.w)) return 2;
@@ -581,6 +640,7 @@ static int mm_check(const MmArgs& a, int dtype, int& ln) {
       if (ln >= 0 && l != ln) return 3;  // one LN mode per launch
       ln = l;
       if (l && (!P.gamma || !al16(P.gamma) || !al16(P.beta))) return 2;
+      if (l && P.st_nt > 0 && (P.st_nt > 1024 || P.K % P.st_nt || !al8(P.stats))) return 2;
     }
   }
   return 0;

@@ -705,7 +705,7 @@ class ModelRunner:
             nxt = m.h[li + 1] if li + 1 < len(m.h) else None
             nln = nxt.ln_1 if nxt is not None else m.ln_f
             first = li == 0
-            ln1 = None if first else (st.stats, blk.ln_1.weight, blk.ln_1.bias)
+            ln1 = None if first else (st, blk.ln_1.weight, blk.ln_1.bias)
             x1 = xn if first else hb
             kc, vc = self.cache.k[li], self.cache.v[li]
             if kind == "seq" and self._tp_ar is not None:
@@ -717,7 +717,7 @@ class ModelRunner:
                                                out=obuf, ws=ws, block_table=tbl, window=at.window, by_row=by_row)
                 smm.mm(o, at.out.weight, out=y, packed=pk(at.out.weight))
                 ar.res_stats(y, at.out.bias, hb, hb, st, blk.ln_2.eps)
-                smm.launch([smm.job([part(hb, mlp.fc_in.weight, (st.stats, blk.ln_2.weight, blk.ln_2.bias))],
+                smm.launch([smm.job([part(hb, mlp.fc_in.weight, (st, blk.ln_2.weight, blk.ln_2.bias))],
                                     g.shape[1], g, mlp.fc_in.bias, act)], B, dt)
                 smm.mm(g, mlp.fc_out.weight, out=y, packed=pk(mlp.fc_out.weight))
                 ar.res_stats(y, mlp.fc_out.bias, hb, hb, st, nln.eps)
@@ -729,14 +729,14 @@ class ModelRunner:
                                                out=obuf, ws=ws, block_table=tbl, window=at.window, by_row=by_row)
                 smm.launch([smm.job([part(o, at.out.weight)], hb.shape[1], hb, at.out.bias, res=hb, stats=st,
                                     eps=blk.ln_2.eps)], B, dt)
-                smm.launch([smm.job([part(hb, mlp.fc_in.weight, (st.stats, blk.ln_2.weight, blk.ln_2.bias))],
+                smm.launch([smm.job([part(hb, mlp.fc_in.weight, (st, blk.ln_2.weight, blk.ln_2.bias))],
                                     g.shape[1], g, mlp.fc_in.bias, act)], B, dt)
                 smm.launch([smm.job([part(g, mlp.fc_out.weight)], hb.shape[1], hb, mlp.fc_out.bias, res=hb,
                                     stats=st, eps=nln.eps)], B, dt)
                 continue
             # parallel residual: [QKV | fc_in] of the same residual rows, one launch
             if kind == "neox":
-                ln2 = (st.stats, blk.ln_2.weight, blk.ln_2.bias) if not first else None
+                ln2 = (st, blk.ln_2.weight, blk.ln_2.bias) if not first else None
                 x2 = xn2 if first else hb
             else:
                 ln2, x2 = ln1, x1
@@ -750,9 +750,9 @@ class ModelRunner:
         w, b, grp = self._head_weight()
         V = w.shape[0]
         if V % 4 == 0:
-            logits = smm.mm(hb, w, b, ln=(st.stats, m.ln_f.weight, m.ln_f.bias), packed=pk(w))
+            logits = smm.mm(hb, w, b, ln=(st, m.ln_f.weight, m.ln_f.bias), packed=pk(w))
         else:  # (GPT-2's 50257 rows: the head takes the normalised rows through the plain path)
-            y = smm.ln_on_load_reference(hb, st.stats, m.ln_f.weight, m.ln_f.bias)
+            y = smm.ln_on_load_reference(hb, st.merged(hb.shape[0]), m.ln_f.weight, m.ln_f.bias)
             logits = skinny_linear(y, w, b)
         if grp is not None:
             from ..parallel.tensor_parallel import gather_last_dim

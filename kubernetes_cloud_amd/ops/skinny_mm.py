@@ -34,7 +34,7 @@ _F = ctypes.c_float
 
 class _Part(ctypes.Structure):
     _fields_ = [("x", _P), ("ldx", _LL), ("w", _P), ("ldw", _LL), ("K", _I), ("packed", _I), ("stats", _P),
-                ("gamma", _P), ("beta", _P)]
+                ("gamma", _P), ("beta", _P), ("st_nt", _I), ("st_eps", _F)]
 
 
 class _Job(ctypes.Structure):
@@ -79,15 +79,37 @@ def _abi_ok() -> bool:
     return _ABI_OK
 
 
+# consumer-side merge: the residual tails only publish per-slice (mean, M2) partials and the next
+# projection merges them in its prologue (MmPart.st_nt) -- no arrival count / last-arriver merge on the
+# producer. Same box, B=8: BLOOM rank 12.14 -> 11.92 ms, GPT-J 3.27 -> 3.21, NeoX 8.67 -> 8.71
+# (profiles/mm_stats_consumer_ab_r6.jsonl); KCA_MM_STATS_CONSUMER=0: the producer merges (last arriver)
+STATS_CONSUMER = os.environ.get("KCA_MM_STATS_CONSUMER", "1") not in ("0", "false")
+
+
 class RowStatsBuf:
     """Workspace of one row-stats tail: per-tile partials, the (mean, rstd) output, arrival counters
-    (zero-initialised, re-armed by every launch). One instance serves consecutive tails on a stream."""
+    (zero-initialised, re-armed by every launch). One instance serves consecutive tails on a stream.
+    ``nt`` > 0: the last producer left unmerged partials (``nt`` slices per row, ``eps`` for the
+    consumer's merge) instead of merged stats (STATS_CONSUMER)."""
 
     def __init__(self, M: int, N: int, device):
         self.M, self.N = M, N
         self.part = torch.empty(M * (N // 16) * 2, device=device, dtype=torch.float32)
         self.stats = torch.zeros(M, 2, device=device, dtype=torch.float32)
         self.cnt = torch.zeros(32 * 65, device=device, dtype=torch.int32)
+        self.nt, self.eps = 0, 1e-5
+
+    def merged(self, M: int | None = None) -> torch.Tensor:
+        """[M, 2] (mean, rstd) for host-side consumers: the kernel's merged stats, or the published
+        partials merged here (the consumer kernels' equal-count Chan merge) when only those exist."""
+        M = self.M if M is None else M
+        if self.nt == 0:
+            return self.stats[:M]
+        p = self.part[:M * self.nt * 2].view(M, self.nt, 2)
+        mt, qt = p[..., 0], p[..., 1]
+        mean = mt.mean(1, keepdim=True)
+        m2 = qt.sum(1, keepdim=True) + (self.N / self.nt) * ((mt - mean) ** 2).sum(1, keepdim=True)
+        return torch.cat([mean, torch.rsqrt(m2 / self.N + self.eps)], dim=1)
 
 
 def supported(x: torch.Tensor, w: torch.Tensor) -> bool:
@@ -124,7 +146,14 @@ def part(x, w, ln=None, packed=None):
         p.w, p.ldw, p.packed = packed.data_ptr(), packed.shape[1] * 16 * 128, 1
     if ln is not None:
         st, g, b = ln
-        p.stats, p.gamma, p.beta = st.data_ptr(), g.data_ptr(), _lib.ptr(b)
+        if isinstance(st, RowStatsBuf):
+            if st.nt > 0:  # unmerged partials: the kernel merges them (MmPart.st_nt)
+                p.stats, p.st_nt, p.st_eps = st.part.data_ptr(), st.nt, st.eps
+            else:
+                p.stats = st.stats.data_ptr()
+        else:
+            p.stats = st.data_ptr()
+        p.gamma, p.beta = g.data_ptr(), _lib.ptr(b)
     return p
 
 
@@ -138,7 +167,12 @@ def job(parts, N: int, y: torch.Tensor, bias=None, act: int = 0, res=None, stats
     if res is not None:
         j.res, j.ldr = res.data_ptr(), res.stride(0)
     if stats is not None:
-        j.part, j.stats_out, j.cnt, j.eps = stats.part.data_ptr(), stats.stats.data_ptr(), stats.cnt.data_ptr(), eps
+        if STATS_CONSUMER:  # publish-only tail: 16-column slices, merged by the consumer
+            j.part, j.eps = stats.part.data_ptr(), eps
+            stats.nt, stats.eps = N // 16, eps
+        else:
+            j.part, j.stats_out, j.cnt, j.eps = stats.part.data_ptr(), stats.stats.data_ptr(), stats.cnt.data_ptr(), eps
+            stats.nt = 0
     return j
 
 

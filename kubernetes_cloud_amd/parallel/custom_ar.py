@@ -223,10 +223,13 @@ class XGMIAllReduce:
                              "N % 64 == 0, N <= 16384)")
         groups = t.numel() // 64
         blocks = max(1, min(self.max_blocks, -(-groups // 32)))
+        from ..ops import skinny_mm as smm
+        pub = smm.STATS_CONSUMER  # publish-only: 64-column slices, merged by the consuming projection
         rc = self._res_statss[t.dtype](self._stage0, self._stage1, self._sig, P(self._ctl), self.rank, self.world,
                              t.data_ptr(), M, N, blocks, self.spin_limit, _lib.ptr(bias), h.data_ptr(),
-                             h_out.data_ptr(), float(eps), stats.part.data_ptr(), stats.stats.data_ptr(),
-                             stats.cnt.data_ptr(), _lib.stream())
+                             h_out.data_ptr(), float(eps), stats.part.data_ptr(),
+                             None if pub else stats.stats.data_ptr(), stats.cnt.data_ptr(), _lib.stream())
+        stats.nt, stats.eps = (N // 64 if pub else 0), float(eps)
         if rc != 0:
             raise RuntimeError(f"kca_ar_res_stats status {rc}")
         self.calls += 1

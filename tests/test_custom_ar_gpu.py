@@ -73,7 +73,7 @@ def _tails(rank, world, ar):
             ref_h = (h.float() + (sum(t.float() for t in ts) + bias.float())).bfloat16()
             errs.append(float((hb.cpu().float() - ref_h.float()).abs().max()))
             ref_st = row_stats_reference(hb.cpu(), 1e-5)
-            rel = ((st.stats.cpu() - ref_st).abs() / (ref_st.abs() + 1e-3)).max()
+            rel = ((st.merged(M).cpu() - ref_st).abs() / (ref_st.abs() + 1e-3)).max()
             errs.append(max(0.0, float(rel) - 1e-4))
     return errs
 

@@ -10,6 +10,13 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
+@pytest.fixture(autouse=True)
+def _producer_merged_stats(monkeypatch):
+    """These tests read RowStatsBuf.stats: the producer-merged (last-arriver) tails. The consumer-merged
+    default is covered by test_consumer_merged_row_stats and the engine tests."""
+    monkeypatch.setattr(sm, "STATS_CONSUMER", False)
+
+
 def _close(a, b, tol):
     a, b = a.float(), b.float()
     err = (a - b).abs().max().item()
@@ -181,3 +188,37 @@ def test_packed_weight_stream_is_bit_identical(dt, M, NK):
             y = sm.mm(hb, wn, ln=(st.stats, gam, None), packed=sm.pack_weight(wn) if pk else None)
             outs.append((hb, y, wn))
         assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("M", [2, 8, 32])
+@pytest.mark.parametrize("N", [1024, 14336])
+def test_consumer_merged_row_stats(M, N, monkeypatch):
+    """Publish-only residual tails (STATS_CONSUMER): the producer writes per-16-column (mean, M2)
+    partials and no merged stats; the next projection merges them in its prologue (MmPart.st_nt).
+    Its LN-on-load output matches the merged-stats path and the fp32 reference, and the host-side
+    merge of the partials matches the rows' statistics."""
+    dt = torch.bfloat16
+    g = torch.Generator(device=DEV).manual_seed(M + N)
+    K = 2048
+    x = torch.randn(M, K, generator=g, device=DEV).to(dt)
+    w = _w(N, K, dt, g)
+    b = (0.1 * torch.randn(N, generator=g, device=DEV)).to(dt)
+    h0 = torch.randn(M, N, generator=g, device=DEV).to(dt)
+    wn = _w(512, N, dt, g)
+    gam = (1 + 0.1 * torch.randn(N, generator=g, device=DEV)).to(dt)
+    bet = (0.1 * torch.randn(N, generator=g, device=DEV)).to(dt)
+    outs = {}
+    for cons in (False, True):
+        monkeypatch.setattr(sm, "STATS_CONSUMER", cons)
+        hb = h0.clone()
+        st = sm.RowStatsBuf(M, N, DEV)
+        sm.launch([sm.job([sm.part(x, w)], N, hb, b, res=hb, stats=st, eps=1e-5)], M, dt)
+        assert st.nt == (N // 16 if cons else 0)
+        y = sm.mm(hb, wn, ln=(st, gam, bet))
+        outs[cons] = (hb, y, st.merged(M).clone())
+    assert torch.equal(outs[False][0], outs[True][0])
+    _close(outs[True][2], sm.row_stats_reference(outs[True][0], 1e-5), 1e-4)
+    _close(outs[True][1], outs[False][1], 1e-2)
+    ref = sm.mm_reference([(sm.ln_on_load_reference(outs[True][0], sm.row_stats_reference(outs[True][0], 1e-5),
+                                                     gam, bet), wn, None)])
+    _close(outs[True][1], ref, 1.5e-2)
