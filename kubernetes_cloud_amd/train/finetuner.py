@@ -374,7 +374,12 @@ def main(argv=None):
             if step >= total_steps:
                 break
             if fault_step >= 0 and step == fault_step and rank in fault_ranks:
-                # fault injection: die hard mid-run, like a lost node
+                # fault injection: die hard mid-run, like a lost node. A checkpoint still
+                # being written by the async writer is then incomplete and a restart skips it (correct,
+                # but timing-dependent); KCA_FAULT_AFTER_CKPT=1 lets the in-flight write land first so a
+                # resume test always finds it
+                if os.environ.get("KCA_FAULT_AFTER_CKPT", "0") == "1":
+                    ckpt_writer.wait()
                 log.error(f"KCA_FAULT_STEP={fault_step}: rank {rank} exiting")
                 os._exit(17)
             if hang_step >= 0 and step == hang_step and rank in fault_ranks:

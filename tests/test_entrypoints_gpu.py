@@ -32,7 +32,9 @@ def test_finetuner_cli_checkpoint_kill_resume_final(tmp_path):
     argv = ["-m", "kubernetes_cloud_amd.train.finetuner", "--run-name", "g", "--model", model, "--dataset", data,
             "--context-size", "128", "--bs", "2", "--gradients", "2", "--output-path", str(tmp_path / "o"),
             "--logs", str(tmp_path / "l"), "--save-steps", "2", "--max-steps", "4", "--zero-stage", "0"]
-    r = _run(argv, {"KCA_FAULT_STEP": "3", "KCA_FAULT_RANKS": "0"})  # dies hard before step 3
+    # dies hard before step 3, once checkpoint-2's async write has landed (otherwise the kill can beat the
+    # writer and the restart rightly starts over: the resume assertion below would depend on timing)
+    r = _run(argv, {"KCA_FAULT_STEP": "3", "KCA_FAULT_RANKS": "0", "KCA_FAULT_AFTER_CKPT": "1"})
     assert r.returncode == 17, r.stderr[-3000:]
     rd = tmp_path / "o" / "results-g"
     assert (rd / "checkpoint-2" / "model.safetensors").exists() and not (rd / "final").exists()

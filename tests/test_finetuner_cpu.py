@@ -168,7 +168,7 @@ def test_fault_injection_and_deterministic_resume(tmp_path):
                 "--zero-stage", "0", "--lr", "1e-3", "--max-steps", "5"]
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     cmd = [sys.executable, "-m", "kubernetes_cloud_amd.train.finetuner"]
-    env = dict(os.environ, KCA_FAULT_STEP="3", PYTHONPATH=root)
+    env = dict(os.environ, KCA_FAULT_STEP="3", KCA_FAULT_AFTER_CKPT="1", PYTHONPATH=root)
     r = subprocess.run(cmd + args(tmp_path / "a"), env=env, cwd=root, capture_output=True, text=True, timeout=600)
     assert r.returncode == 17, r.stderr[-2000:]
     rd = tmp_path / "a" / "results-f"
