@@ -30,7 +30,7 @@ def run_tp_decode(model_name="bloom-176b", layers=0, batches=(1, 8, 32), prompt_
                   custom_ar=True, dtype="bf16", emulate_tp=0):
     """All ranks call this inside an initialised process group (or world 1). ``dtype`` "fp16" runs
     the model in float16 as BASELINE config 4 / DS-Inference state (the native fp16 decode step: the
-    matrix-core layer at every batch, the all-reduce tails' fp16 instantiations). ``emulate_tp`` N > 1 (one process, no process
+    same per-batch dispatch as bf16, the all-reduce tails' fp16 instantiations). ``emulate_tp`` N > 1 (one process, no process
     group): rank 0's shard of a TP=N layout with stand-in collectives (parallel/tp_emulation.py) --
     the per-rank weight stream and kernel schedule of the real run, all-reduces priced separately.
     Returns the per-batch records on rank 0, None on followers."""
